@@ -1,0 +1,95 @@
+// Device-side helpers shared by every libvq3d kernel (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/vq3d.h"
+
+namespace vq3d {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- storage types
+using bf16_t = uint16_t;  // raw bf16 bits; arithmetic always in fp32
+
+__device__ __forceinline__ float ld(const float *p) { return *p; }
+__device__ __forceinline__ float ld(const bf16_t *p) { return __uint_as_float(uint32_t(*p) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (torch's conversion); NaN stays NaN
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return bf16_t((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return bf16_t(u >> 16);
+}
+__device__ __forceinline__ void st(float *p, float v) { *p = v; }
+__device__ __forceinline__ void st(bf16_t *p, float v) { *p = f2bf(v); }
+
+// ---------------------------------------------------------------- activations
+__device__ __forceinline__ float elu(float z) { return z > 0.f ? z : (expf(z) - 1.f); }
+__device__ __forceinline__ float elu_grad(float z) { return z > 0.f ? 1.f : expf(z); }
+
+struct Prologue {
+    int kind;  // VQ3D_PRO_*
+    float a, b;
+    __device__ __forceinline__ float apply(float x) const {
+        if (kind == VQ3D_PRO_NONE) return x;
+        if (kind == VQ3D_PRO_ADD) return x + a;
+        return elu(x + a) + b;
+    }
+    __device__ __forceinline__ float deriv(float x) const {
+        return kind == VQ3D_PRO_ELU_ADD ? elu_grad(x + a) : 1.f;
+    }
+};
+
+__device__ __forceinline__ Prologue make_prologue(int kind, const float *a, const float *b) {
+    Prologue p;
+    p.kind = kind;
+    p.a = (kind != VQ3D_PRO_NONE && a) ? *a : 0.f;
+    p.b = (kind == VQ3D_PRO_ELU_ADD && b) ? *b : 0.f;
+    return p;
+}
+
+// ---------------------------------------------------------------- reductions
+template <typename F>
+__device__ __forceinline__ F wave_sum(F v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Deterministic block sum (fixed shuffle tree + fixed LDS order). All threads return the total.
+template <typename F, int NT>
+__device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    F t = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += scratch[i];
+    return t;
+}
+
+// ---------------------------------------------------------------- trilinear x2 (align_corners=False)
+// Source index pair and weight of the upper neighbour for destination index j (size n source),
+// as ATen's area_pixel_compute_source_index + upsample_trilinear3d compute it.
+__device__ __forceinline__ void up_coeff(int j, int n, int &i0, int &i1, float &l1) {
+    float src = 0.5f * (float(j) + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    i0 = int(src);
+    i1 = i0 + ((i0 < n - 1) ? 1 : 0);
+    l1 = src - float(i0);
+}
+
+}  // namespace vq3d
+
+// ---------------------------------------------------------------- error plumbing (host)
+namespace vq3d {
+void set_error(const std::string &msg);
+int fail(const std::string &msg);
+int check_launch(const char *what);
+inline hipStream_t as_stream(vq3d_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace vq3d

@@ -1,0 +1,627 @@
+// Upsample (ResizeConv3D's nn.Upsample), reconstruction loss, EvoNorm-S0, Adam(amsgrad),
+// casts, and the error plumbing of libvq3d.
+#include "common.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace vq3d {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+int fail(const std::string &msg) {
+    set_error(msg);
+    return -1;
+}
+int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(std::string(what) + ": " + hipGetErrorString(e));
+    return 0;
+}
+
+// ============================================================================ upsample x2
+// y[b, 2h', 2w', 2d', c] = trilinear(prologue(x)) ; thread per output element
+template <typename T>
+__global__ __launch_bounds__(256) void k_up_fwd(const T *__restrict__ x, int B, int C, int H, int W, int D,
+                                               int pk, const float *pa, const float *pb, T *__restrict__ y) {
+    const int64_t n = int64_t(B) * 8 * H * W * D * C;
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const Prologue pro = make_prologue(pk, pa, pb);
+    int64_t t = i;
+    const int c = int(t % C); t /= C;
+    const int od = int(t % (2 * D)); t /= 2 * D;
+    const int ow = int(t % (2 * W)); t /= 2 * W;
+    const int oh = int(t % (2 * H));
+    const int b = int(t / (2 * H));
+    int h0, h1, w0, w1, d0, d1;
+    float lh, lw, ldd;
+    up_coeff(oh, H, h0, h1, lh);
+    up_coeff(ow, W, w0, w1, lw);
+    up_coeff(od, D, d0, d1, ldd);
+    auto X = [&](int hh, int ww, int dd) {
+        return pro.apply(ld(x + (((int64_t(b) * H + hh) * W + ww) * D + dd) * C + c));
+    };
+    const float v = (1.f - lh) * ((1.f - lw) * ((1.f - ldd) * X(h0, w0, d0) + ldd * X(h0, w0, d1)) +
+                                  lw * ((1.f - ldd) * X(h0, w1, d0) + ldd * X(h0, w1, d1))) +
+                    lh * ((1.f - lw) * ((1.f - ldd) * X(h1, w0, d0) + ldd * X(h1, w0, d1)) +
+                          lw * ((1.f - ldd) * X(h1, w1, d0) + ldd * X(h1, w1, d1)));
+    st(y + i, v);
+}
+
+// list of (destination index, weight) pairs that read source index i along one axis
+__device__ __forceinline__ int up_adjoint(int i, int n, int *js, float *ws) {
+    int cnt = 0;
+    for (int j = max(0, 2 * i - 2); j <= min(2 * n - 1, 2 * i + 2); ++j) {
+        int a0, a1;
+        float l1;
+        up_coeff(j, n, a0, a1, l1);
+        float wv = 0.f;
+        if (a0 == i) wv += 1.f - l1;
+        if (a1 == i) wv += l1;
+        if (wv != 0.f) {
+            js[cnt] = j;
+            ws[cnt] = wv;
+            ++cnt;
+        }
+    }
+    return cnt;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B, int C, int H, int W, int D, int pk,
+                                               const float *pa, const T *__restrict__ aux,
+                                               const T *__restrict__ addend, T *__restrict__ gx,
+                                               float *__restrict__ spart) {
+    __shared__ float red[8];
+    const int64_t n = int64_t(B) * H * W * D * C;
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    float pre = 0.f, post = 0.f;
+    if (i < n) {
+        const Prologue pro = make_prologue(pk, pa, nullptr);
+        int64_t t = i;
+        const int c = int(t % C); t /= C;
+        const int id = int(t % D); t /= D;
+        const int iw = int(t % W); t /= W;
+        const int ih = int(t % H);
+        const int b = int(t / H);
+        int jh[5], jw[5], jd[5];
+        float wh[5], ww[5], wd[5];
+        const int nh = up_adjoint(ih, H, jh, wh), nw = up_adjoint(iw, W, jw, ww), nd = up_adjoint(id, D, jd, wd);
+        float acc = 0.f;
+        for (int a = 0; a < nh; ++a)
+            for (int bb = 0; bb < nw; ++bb) {
+                float s = 0.f;
+                for (int cc = 0; cc < nd; ++cc)
+                    s = fmaf(wd[cc],
+                             ld(gy + (((int64_t(b) * 2 * H + jh[a]) * 2 * W + jw[bb]) * 2 * D + jd[cc]) * C + c), s);
+                acc = fmaf(wh[a] * ww[bb], s, acc);
+            }
+        float v = acc;
+        pre = v;
+        if (aux && pro.kind == VQ3D_PRO_ELU_ADD) v *= pro.deriv(ld(aux + i));
+        post = v;
+        if (addend) v += ld(addend + i);
+        st(gx + i, v);
+    }
+    pre = block_sum<float, 256>(pre, red);
+    post = block_sum<float, 256>(post, red + 4);
+    if (threadIdx.x == 0) {
+        spart[2 * blockIdx.x] = pre;
+        spart[2 * blockIdx.x + 1] = post;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_pairs(const float *__restrict__ spart, int nb, float *dpre,
+                                                  float *dpost) {
+    __shared__ float red[8];
+    float p0 = 0.f, p1 = 0.f;
+    for (int j = threadIdx.x; j < nb; j += 256) {
+        p0 += spart[2 * j];
+        p1 += spart[2 * j + 1];
+    }
+    p0 = block_sum<float, 256>(p0, red);
+    p1 = block_sum<float, 256>(p1, red + 4);
+    if (threadIdx.x == 0) {
+        if (dpre) *dpre += p0;
+        if (dpost) *dpost += p1;
+    }
+}
+
+// ============================================================================ reconstruction loss
+__device__ __forceinline__ bool in_cylinder(int h, int w, int H, int W) {
+    // dist((h,w), (H/2, W/2)) <= min(H,W)/2  <=>  (2h-H)^2 + (2w-W)^2 <= min(H,W)^2 (exact)
+    const int64_t a = 2 * h - H, b = 2 * w - W, m = min(H, W);
+    return a * a + b * b <= m * m;
+}
+
+__device__ __forceinline__ float huber(float d) {
+    const float ad = fabsf(d);
+    return ad < 1.f ? 0.5f * d * d : ad - 0.5f;
+}
+__device__ __forceinline__ float huber_grad(float d) {
+    return d <= -1.f ? -1.f : (d >= 1.f ? 1.f : d);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_recon_fwd(const T *__restrict__ dec, const float *__restrict__ x,
+                                                  const int64_t *__restrict__ nvs, int B, int H, int W, int D,
+                                                  int cyl, float *__restrict__ part) {
+    __shared__ float red[4];
+    const int64_t n = int64_t(B) * H * W * D;
+    float s = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        int64_t t = i;
+        const int d = int(t % D); t /= D;
+        const int w = int(t % W); t /= W;
+        const int h = int(t % H);
+        const int b = int(t / H);
+        if (cyl && !in_cylinder(h, w, H, W)) continue;
+        const float loc = (d >= nvs[b]) ? 0.f : elu(ld(dec + i));
+        s += huber(loc - x[i]);
+    }
+    s = block_sum<float, 256>(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+struct CommitPtrs {
+    const float *p[8];
+};
+
+__global__ __launch_bounds__(256) void k_recon_fin(const float *__restrict__ part, int nb, float inv_count,
+                                                  CommitPtrs commit, int nc, float *recon, float *total) {
+    __shared__ float red[4];
+    float s = 0.f;
+    for (int j = threadIdx.x; j < nb; j += 256) s += part[j];
+    s = block_sum<float, 256>(s, red);
+    if (threadIdx.x == 0) {
+        const float r = s * inv_count;
+        if (recon) *recon = r;
+        float tot = r;
+        for (int c = 0; c < nc; ++c) tot += *commit.p[c];
+        if (total) *total = tot;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_recon_bwd(const T *__restrict__ dec, const float *__restrict__ x,
+                                                  const int64_t *__restrict__ nvs, int B, int H, int W, int D,
+                                                  int cyl, const float *__restrict__ gtot, float inv_count,
+                                                  T *__restrict__ gdec) {
+    const int64_t n = int64_t(B) * H * W * D;
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    int64_t t = i;
+    const int d = int(t % D); t /= D;
+    const int w = int(t % W); t /= W;
+    const int h = int(t % H);
+    const int b = int(t / H);
+    float g = 0.f;
+    if ((!cyl || in_cylinder(h, w, H, W)) && d < nvs[b]) {
+        const float z = ld(dec + i);
+        const float loc = elu(z);
+        g = (*gtot * inv_count) * huber_grad(loc - x[i]) * elu_grad(z);
+    }
+    st(gdec + i, g);
+}
+
+// ============================================================================ EvoNorm-S0 (B = 1)
+// stats[g] = {mean, std} with unbiased var over (C/G) x voxels; fp64 partial sums per block.
+template <typename T>
+__global__ __launch_bounds__(256) void k_evo_stats_part(const T *__restrict__ x, int C, int G, int64_t nvox,
+                                                       int64_t vox_per_blk, const float *__restrict__ mean,
+                                                       double *__restrict__ part) {
+    __shared__ double red[4];
+    const int cpg = C / G;
+    const int64_t v0 = int64_t(blockIdx.x) * vox_per_blk, v1 = min(nvox, v0 + vox_per_blk);
+    for (int g = 0; g < G; ++g) {
+        const double mu = mean ? double(mean[2 * g]) : 0.0;
+        double s = 0.0;
+        for (int64_t e = v0 * cpg + threadIdx.x; e < v1 * cpg; e += 256) {
+            const int64_t v = e / cpg;
+            const int c = g * cpg + int(e - v * cpg);
+            const double val = double(ld(x + v * C + c)) - mu;
+            s += mean ? val * val : val;
+        }
+        s = block_sum<double, 256>(s, red);
+        if (threadIdx.x == 0) part[int64_t(blockIdx.x) * G + g] = s;
+    }
+}
+
+__global__ void k_evo_stats_fin(const double *__restrict__ part, int nb, int G, double m, float *__restrict__ stats,
+                                int pass) {
+    const int g = threadIdx.x;
+    if (g >= G) return;
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += part[int64_t(b) * G + g];
+    if (pass == 0) stats[2 * g] = float(s / m);
+    else stats[2 * g + 1] = sqrtf(float(s / (m - 1.0)) + 1e-5f);
+}
+
+__device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + expf(-z)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_evo_apply(const T *__restrict__ x, int C, int G, int64_t nvox,
+                                                  const float *__restrict__ v, const float *__restrict__ gamma,
+                                                  const float *__restrict__ beta, const float *__restrict__ stats,
+                                                  T *__restrict__ y) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= nvox * C) return;
+    const int c = int(i % C);
+    const int g = c / (C / G);
+    const float xv = ld(x + i);
+    const float num = xv * sigmoidf_(xv * v[c]);
+    st(y + i, num * gamma[c] / stats[2 * g + 1] + beta[c]);
+}
+
+// per block partials: [G] sum(g * num * gamma) and per channel [C] dgamma, dbeta, dv
+template <typename T>
+__global__ __launch_bounds__(256) void k_evo_bwd_part(const T *__restrict__ x, const T *__restrict__ gy, int C, int G,
+                                                     int64_t nvox, int64_t vox_per_blk, const float *__restrict__ v,
+                                                     const float *__restrict__ gamma, const float *__restrict__ stats,
+                                                     float *__restrict__ part) {
+    __shared__ float red[4];
+    const int64_t v0 = int64_t(blockIdx.x) * vox_per_blk, v1 = min(nvox, v0 + vox_per_blk);
+    const int cpg = C / G;
+    float *out = part + int64_t(blockIdx.x) * (G + 3 * C);
+    for (int c = 0; c < C; ++c) {
+        const float sd = stats[2 * (c / cpg) + 1];
+        float sg = 0.f, sb = 0.f, sv = 0.f, ss = 0.f;
+        for (int64_t vv = v0 + threadIdx.x; vv < v1; vv += 256) {
+            const float xv = ld(x + vv * C + c), g = ld(gy + vv * C + c);
+            const float xvv = xv * v[c];
+            const float sgm = sigmoidf_(xvv);
+            const float num = xv * sgm;
+            sg += g * num / sd;
+            sb += g;
+            sv += (g * gamma[c] / sd) * (xv * xv * sgm * (1.f - sgm));
+            ss += g * num * gamma[c];
+        }
+        sg = block_sum<float, 256>(sg, red);
+        sb = block_sum<float, 256>(sb, red);
+        sv = block_sum<float, 256>(sv, red);
+        ss = block_sum<float, 256>(ss, red);
+        if (threadIdx.x == 0) {
+            out[G + 3 * c] = sg;
+            out[G + 3 * c + 1] = sb;
+            out[G + 3 * c + 2] = sv;
+            if (c % cpg == 0) out[c / cpg] = 0.f;
+            out[c / cpg] += ss;
+        }
+    }
+}
+
+__global__ void k_evo_bwd_fin(const float *__restrict__ part, int nb, int C, int G, float *__restrict__ red_out,
+                              float *dv, float *dgamma, float *dbeta) {
+    const int j = threadIdx.x;
+    const int W = G + 3 * C;
+    for (int e = j; e < W; e += blockDim.x) {
+        float s = 0.f;
+        for (int b = 0; b < nb; ++b) s += part[int64_t(b) * W + e];
+        if (e < G) red_out[e] = s;
+        else {
+            const int c = (e - G) / 3, k = (e - G) % 3;
+            if (k == 0 && dgamma) dgamma[c] += s;
+            if (k == 1 && dbeta) dbeta[c] += s;
+            if (k == 2 && dv) dv[c] += s;
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_evo_bwd_apply(const T *__restrict__ x, const T *__restrict__ gy, int C, int G,
+                                                      int64_t nvox, const float *__restrict__ v,
+                                                      const float *__restrict__ gamma, const float *__restrict__ stats,
+                                                      const float *__restrict__ gsum, T *__restrict__ gx) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= nvox * C) return;
+    const int c = int(i % C);
+    const int cpg = C / G;
+    const int g = c / cpg;
+    const float mu = stats[2 * g], sd = stats[2 * g + 1];
+    const float m = float(nvox) * cpg;
+    const float xv = ld(x + i), gv = ld(gy + i);
+    const float xvv = xv * v[c];
+    const float sgm = sigmoidf_(xvv);
+    const float dnum = gv * gamma[c] / sd;
+    // d/d sd of sum(g * num * gamma / sd) = -S / sd^2 ; d sd / d var = 1 / (2 sd)
+    const float dvar = -gsum[g] / (sd * sd) / (2.f * sd);
+    const float r = dnum * (sgm + xvv * sgm * (1.f - sgm)) + dvar * 2.f * (xv - mu) / (m - 1.f);
+    st(gx + i, r);
+}
+
+// ============================================================================ Adam (amsgrad)
+__global__ __launch_bounds__(256) void k_adam_amsgrad(float *__restrict__ p, const float *__restrict__ g,
+                                                     float *__restrict__ m, float *__restrict__ v,
+                                                     float *__restrict__ vmax, int64_t n, float beta1, float omb1,
+                                                     float beta2, float omb2, float step_size, float bc2_sqrt,
+                                                     float eps) {
+#pragma clang fp contract(off)
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        const float gi = g[i];
+        float mi = m[i];
+        mi = mi + omb1 * (gi - mi);  // torch lerp_ (weight < 0.5)
+        float vi = v[i] * beta2 + omb2 * gi * gi;
+        const float vm = fmaxf(vmax[i], vi);
+        const float denom = sqrtf(vm) / bc2_sqrt + eps;
+        p[i] = p[i] + (-step_size) * (mi / denom);
+        m[i] = mi;
+        v[i] = vi;
+        vmax[i] = vm;
+    }
+}
+
+// ============================================================================ casts
+template <typename S, typename D>
+__global__ __launch_bounds__(256) void k_cast(const S *__restrict__ s, D *__restrict__ d, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+        st(d + i, ld(s + i));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_elu_bwd_out(const T *__restrict__ g, const T *__restrict__ y,
+                                                    T *__restrict__ gz, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        const float yv = ld(y + i);
+        st(gz + i, ld(g + i) * (yv > 0.f ? 1.f : yv + 1.f));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scale(float *__restrict__ x, float a, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) x[i] *= a;
+}
+
+static unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192))); }
+
+}  // namespace vq3d
+
+using namespace vq3d;
+
+extern "C" {
+
+const char *vq3d_last_error(void) { return g_last_error.c_str(); }
+const char *vq3d_version(void) { return "vq3d 0.1 gfx950"; }
+
+int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
+                        const void *x, int32_t pro_kind, const float *pro_a, const float *pro_b, void *y,
+                        vq3d_stream_t stream) {
+    if (batch <= 0 || channels <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("upsample2x_fwd: bad sizes");
+    if (!x || !y || (pro_kind && !pro_a) || (pro_kind == VQ3D_PRO_ELU_ADD && !pro_b))
+        return fail("upsample2x_fwd: null pointer");
+    const int64_t n = int64_t(batch) * 8 * h * w * dd * channels;
+    const unsigned nb = unsigned((n + 255) / 256);
+    hipStream_t s = as_stream(stream);
+    if (dtype == VQ3D_F32)
+        k_up_fwd<float><<<nb, 256, 0, s>>>((const float *)x, batch, channels, h, w, dd, pro_kind, pro_a, pro_b,
+                                           (float *)y);
+    else
+        k_up_fwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)x, batch, channels, h, w, dd, pro_kind, pro_a, pro_b,
+                                            (bf16_t *)y);
+    return check_launch("upsample2x_fwd");
+}
+
+size_t vq3d_upsample2x_bwd_workspace_size(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd) {
+    const int64_t n = int64_t(batch) * h * w * dd * channels;
+    return size_t((n + 255) / 256) * 8 + 256;
+}
+
+int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
+                        const void *gy, int32_t pro_kind, const float *pro_a, const vq3d_dgrad_epilogue *epi,
+                        void *gx, void *workspace, vq3d_stream_t stream) {
+    if (batch <= 0 || channels <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("upsample2x_bwd: bad sizes");
+    if (!gy || !gx || !workspace) return fail("upsample2x_bwd: null pointer");
+    if (pro_kind == VQ3D_PRO_ELU_ADD && (!epi || !epi->aux || !pro_a))
+        return fail("upsample2x_bwd: ELU prologue derivative needs aux and pro_a");
+    const int64_t n = int64_t(batch) * h * w * dd * channels;
+    const unsigned nb = unsigned((n + 255) / 256);
+    hipStream_t s = as_stream(stream);
+    const void *aux = epi ? epi->aux : nullptr, *add = epi ? epi->addend : nullptr;
+    if (dtype == VQ3D_F32)
+        k_up_bwd<float><<<nb, 256, 0, s>>>((const float *)gy, batch, channels, h, w, dd, pro_kind, pro_a,
+                                           (const float *)aux, (const float *)add, (float *)gx, (float *)workspace);
+    else
+        k_up_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)gy, batch, channels, h, w, dd, pro_kind, pro_a,
+                                            (const bf16_t *)aux, (const bf16_t *)add, (bf16_t *)gx,
+                                            (float *)workspace);
+    return check_launch("upsample2x_bwd");
+}
+
+int vq3d_upsample2x_bwd_finalize(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
+                                 const void *workspace, float *dpro_pre, float *dpro_post, vq3d_stream_t stream) {
+    if (!workspace) return fail("upsample2x_bwd_finalize: null workspace");
+    const int64_t n = int64_t(batch) * h * w * dd * channels;
+    k_sum_pairs<<<1, 256, 0, as_stream(stream)>>>((const float *)workspace, int((n + 255) / 256), dpro_pre,
+                                                  dpro_post);
+    return check_launch("upsample2x_bwd_finalize");
+}
+
+int64_t vq3d_cylinder_count(int32_t h, int32_t w) {
+    int64_t c = 0;
+    const int64_t m = std::min(h, w);
+    for (int64_t i = 0; i < h; ++i)
+        for (int64_t j = 0; j < w; ++j) {
+            const int64_t a = 2 * i - h, b = 2 * j - w;
+            c += (a * a + b * b <= m * m);
+        }
+    return c;
+}
+
+size_t vq3d_recon_loss_workspace_size(int32_t, int32_t, int32_t, int32_t) { return 4096 * 4; }
+
+int vq3d_recon_loss_fwd(int32_t dtype, const void *dec, const float *x, const int64_t *nvs, int32_t batch, int32_t h,
+                        int32_t w, int32_t dd, int32_t cylinder, const float *const *commit, int32_t n_commit,
+                        float *recon, float *total, void *workspace, vq3d_stream_t stream) {
+    if (batch <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("recon_loss_fwd: bad sizes");
+    if (!dec || !x || !nvs || !workspace || (n_commit && !commit)) return fail("recon_loss_fwd: null pointer");
+    if (n_commit < 0 || n_commit > 8) return fail("recon_loss_fwd: at most 8 commitment losses");
+    CommitPtrs cp = {};
+    for (int i = 0; i < n_commit; ++i) {
+        if (!commit[i]) return fail("recon_loss_fwd: null commitment pointer");
+        cp.p[i] = commit[i];
+    }
+    const int64_t n = int64_t(batch) * h * w * dd;
+    const int nb = int(std::min<int64_t>(4096, (n + 255) / 256));
+    const int64_t cnt = int64_t(batch) * dd * (cylinder ? vq3d_cylinder_count(h, w) : int64_t(h) * w);
+    hipStream_t s = as_stream(stream);
+    float *part = (float *)workspace;
+    if (dtype == VQ3D_F32)
+        k_recon_fwd<float><<<nb, 256, 0, s>>>((const float *)dec, x, nvs, batch, h, w, dd, cylinder, part);
+    else
+        k_recon_fwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)dec, x, nvs, batch, h, w, dd, cylinder, part);
+    k_recon_fin<<<1, 256, 0, s>>>(part, nb, float(1.0 / double(cnt)), cp, n_commit, recon, total);
+    return check_launch("recon_loss_fwd");
+}
+
+int vq3d_recon_loss_bwd(int32_t dtype, const void *dec, const float *x, const int64_t *nvs, int32_t batch, int32_t h,
+                        int32_t w, int32_t dd, int32_t cylinder, const float *g_total, void *gdec,
+                        vq3d_stream_t stream) {
+    if (batch <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("recon_loss_bwd: bad sizes");
+    if (!dec || !x || !nvs || !g_total || !gdec) return fail("recon_loss_bwd: null pointer");
+    const int64_t n = int64_t(batch) * h * w * dd;
+    const int64_t cnt = int64_t(batch) * dd * (cylinder ? vq3d_cylinder_count(h, w) : int64_t(h) * w);
+    const unsigned nb = unsigned((n + 255) / 256);
+    hipStream_t s = as_stream(stream);
+    const float ic = float(1.0 / double(cnt));
+    if (dtype == VQ3D_F32)
+        k_recon_bwd<float><<<nb, 256, 0, s>>>((const float *)dec, x, nvs, batch, h, w, dd, cylinder, g_total, ic,
+                                              (float *)gdec);
+    else
+        k_recon_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)dec, x, nvs, batch, h, w, dd, cylinder, g_total, ic,
+                                               (bf16_t *)gdec);
+    return check_launch("recon_loss_bwd");
+}
+
+static int evo_groups(int c) { return std::max(c / 8, 1); }
+static int64_t evo_blocks(int64_t nvox) { return std::min<int64_t>(1024, (nvox + 255) / 256); }
+
+size_t vq3d_evonorm_workspace_size(int32_t channels, int64_t voxels) {
+    const int64_t nb = evo_blocks(voxels);
+    const int G = evo_groups(channels);
+    return size_t(nb) * G * 8 + size_t(nb) * (G + 3 * channels) * 4 + size_t(G) * 4 + 1024;
+}
+
+int vq3d_evonorm_fwd(int32_t dtype, const void *x, int32_t channels, int64_t voxels, const float *v,
+                     const float *gamma, const float *beta, void *y, float *stats, void *workspace,
+                     vq3d_stream_t stream) {
+    if (channels <= 0 || voxels <= 1) return fail("evonorm_fwd: bad sizes");
+    if (!x || !v || !gamma || !beta || !y || !stats || !workspace) return fail("evonorm_fwd: null pointer");
+    const int G = evo_groups(channels);
+    if (channels % G) return fail("evonorm_fwd: channels not divisible by groups");
+    const int64_t nb = evo_blocks(voxels);
+    const int64_t vpb = (voxels + nb - 1) / nb;
+    hipStream_t s = as_stream(stream);
+    double *part = (double *)workspace;
+    const double m = double(voxels) * (channels / G);
+    for (int pass = 0; pass < 2; ++pass) {
+        const float *mean = pass ? stats : nullptr;
+        if (dtype == VQ3D_F32)
+            k_evo_stats_part<float><<<unsigned(nb), 256, 0, s>>>((const float *)x, channels, G, voxels, vpb, mean,
+                                                                 part);
+        else
+            k_evo_stats_part<bf16_t><<<unsigned(nb), 256, 0, s>>>((const bf16_t *)x, channels, G, voxels, vpb, mean,
+                                                                  part);
+        k_evo_stats_fin<<<1, 64 * ((G + 63) / 64), 0, s>>>(part, int(nb), G, m, stats, pass);
+    }
+    const unsigned na = unsigned((voxels * channels + 255) / 256);
+    if (dtype == VQ3D_F32)
+        k_evo_apply<float><<<na, 256, 0, s>>>((const float *)x, channels, G, voxels, v, gamma, beta, stats,
+                                              (float *)y);
+    else
+        k_evo_apply<bf16_t><<<na, 256, 0, s>>>((const bf16_t *)x, channels, G, voxels, v, gamma, beta, stats,
+                                               (bf16_t *)y);
+    return check_launch("evonorm_fwd");
+}
+
+int vq3d_evonorm_bwd(int32_t dtype, const void *x, const void *gy, int32_t channels, int64_t voxels, const float *v,
+                     const float *gamma, const float *stats, void *gx, float *dv, float *dgamma, float *dbeta,
+                     void *workspace, vq3d_stream_t stream) {
+    if (channels <= 0 || voxels <= 1) return fail("evonorm_bwd: bad sizes");
+    if (!x || !gy || !v || !gamma || !stats || !gx || !workspace) return fail("evonorm_bwd: null pointer");
+    const int G = evo_groups(channels);
+    const int64_t nb = evo_blocks(voxels);
+    const int64_t vpb = (voxels + nb - 1) / nb;
+    hipStream_t s = as_stream(stream);
+    float *part = (float *)((char *)workspace + size_t(nb) * G * 8);
+    float *gsum = part + size_t(nb) * (G + 3 * channels);
+    if (dtype == VQ3D_F32)
+        k_evo_bwd_part<float><<<unsigned(nb), 256, 0, s>>>((const float *)x, (const float *)gy, channels, G, voxels,
+                                                           vpb, v, gamma, stats, part);
+    else
+        k_evo_bwd_part<bf16_t><<<unsigned(nb), 256, 0, s>>>((const bf16_t *)x, (const bf16_t *)gy, channels, G,
+                                                            voxels, vpb, v, gamma, stats, part);
+    k_evo_bwd_fin<<<1, 256, 0, s>>>(part, int(nb), channels, G, gsum, dv, dgamma, dbeta);
+    const unsigned na = unsigned((voxels * channels + 255) / 256);
+    if (dtype == VQ3D_F32)
+        k_evo_bwd_apply<float><<<na, 256, 0, s>>>((const float *)x, (const float *)gy, channels, G, voxels, v, gamma,
+                                                  stats, gsum, (float *)gx);
+    else
+        k_evo_bwd_apply<bf16_t><<<na, 256, 0, s>>>((const bf16_t *)x, (const bf16_t *)gy, channels, G, voxels, v,
+                                                   gamma, stats, gsum, (bf16_t *)gx);
+    return check_launch("evonorm_bwd");
+}
+
+int vq3d_adam_amsgrad(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr, float beta1,
+                      float beta2, float eps, int64_t step, vq3d_stream_t stream) {
+    if (n <= 0 || step <= 0) return fail("adam: bad sizes/step");
+    if (!p || !g || !m || !v || !vmax) return fail("adam: null pointer");
+    const double bc1 = 1.0 - std::pow(double(beta1), double(step));
+    const double bc2 = 1.0 - std::pow(double(beta2), double(step));
+    const float step_size = float(double(lr) / bc1);
+    const float bc2_sqrt = float(std::sqrt(bc2));
+    k_adam_amsgrad<<<grid_for(n), 256, 0, as_stream(stream)>>>(p, g, m, v, vmax, n, beta1, float(1.0 - beta1), beta2,
+                                                               float(1.0 - beta2), step_size, bc2_sqrt, eps);
+    return check_launch("adam_amsgrad");
+}
+
+int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, int64_t n, vq3d_stream_t stream) {
+    if (n < 0 || (n && (!src || !dst))) return fail("cast: bad args");
+    if (n == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    const unsigned nb = grid_for(n);
+    if (src_dtype == VQ3D_F32 && dst_dtype == VQ3D_BF16)
+        k_cast<float, bf16_t><<<nb, 256, 0, s>>>((const float *)src, (bf16_t *)dst, n);
+    else if (src_dtype == VQ3D_BF16 && dst_dtype == VQ3D_F32)
+        k_cast<bf16_t, float><<<nb, 256, 0, s>>>((const bf16_t *)src, (float *)dst, n);
+    else if (src_dtype == dst_dtype)
+        return vq3d_copy(dst, src, size_t(n) * (src_dtype == VQ3D_F32 ? 4 : 2), stream);
+    else
+        return fail("cast: bad dtype");
+    return check_launch("cast");
+}
+
+int vq3d_zero(void *p, size_t bytes, vq3d_stream_t stream) {
+    if (!bytes) return 0;
+    if (!p) return fail("zero: null pointer");
+    hipError_t e = hipMemsetAsync(p, 0, bytes, as_stream(stream));
+    return e == hipSuccess ? 0 : fail(std::string("zero: ") + hipGetErrorString(e));
+}
+
+int vq3d_copy(void *dst, const void *src, size_t bytes, vq3d_stream_t stream) {
+    if (!bytes) return 0;
+    if (!dst || !src) return fail("copy: null pointer");
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, as_stream(stream));
+    return e == hipSuccess ? 0 : fail(std::string("copy: ") + hipGetErrorString(e));
+}
+
+int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *gz, int64_t n,
+                             vq3d_stream_t stream) {
+    if (n <= 0) return 0;
+    if (!g || !y || !gz) return fail("elu_bwd_from_output: null pointer");
+    if (dtype == VQ3D_F32)
+        k_elu_bwd_out<float><<<grid_for(n), 256, 0, as_stream(stream)>>>((const float *)g, (const float *)y,
+                                                                          (float *)gz, n);
+    else
+        k_elu_bwd_out<bf16_t><<<grid_for(n), 256, 0, as_stream(stream)>>>((const bf16_t *)g, (const bf16_t *)y,
+                                                                           (bf16_t *)gz, n);
+    return check_launch("elu_bwd_from_output");
+}
+
+int vq3d_scale(float *x, float a, int64_t n, vq3d_stream_t stream) {
+    if (n <= 0) return 0;
+    if (!x) return fail("scale: null pointer");
+    k_scale<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, a, n);
+    return check_launch("scale");
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+"""ctypes binding of libvq3d.so (C-ABI declared in include/vq3d.h).
+
+The library is REQUIRED: importing an op without it, or calling it on a non-GPU tensor,
+raises.  There is no CPU / PyTorch fallback anywhere in the product path.
+"""
+import ctypes
+import os
+
+import torch
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("VQ3D_LIB", os.path.join(_PKG_ROOT, "lib", "libvq3d.so"))
+
+F32, BF16 = 0, 1
+PAD_ZEROS, PAD_CIRCULAR = 0, 1
+PRO_NONE, PRO_ADD, PRO_ELU_ADD = 0, 1, 2
+
+c_int, c_i64, c_size, c_float, c_void = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
+P = ctypes.c_void_p
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("dtype", "batch", "cin", "cin2", "cout", "in_h", "in_w", "in_d",
+                                     "out_h", "out_w", "out_d", "kernel", "stride", "pad", "pad_mode",
+                                     "pro_kind")]
+
+
+class ConvEpilogue(ctypes.Structure):
+    _fields_ = [("scale", P), ("bias", P), ("cbias", P), ("residual", P), ("residual_up2", c_int),
+                ("post_elu", c_int)]
+
+
+class DgradEpilogue(ctypes.Structure):
+    _fields_ = [("aux", P), ("addend", P)]
+
+
+_SIGS = {
+    "vq3d_conv3d_fwd": (c_int, [P, P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_bwd_workspace_size": (c_size, [P]),
+    "vq3d_conv3d_bwd_data": (c_int, [P, P, P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_bwd_finalize": (c_int, [P, P, P, P, P, P, P, P, P, P, P]),
+    "vq3d_upsample2x_fwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P]),
+    "vq3d_upsample2x_bwd_workspace_size": (c_size, [c_int] * 5),
+    "vq3d_upsample2x_bwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P, P]),
+    "vq3d_upsample2x_bwd_finalize": (c_int, [c_int] * 5 + [P, P, P, P]),
+    "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),
+    "vq3d_vq_nearest": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, c_int, P, P, P, P]),
+    "vq3d_vq_commit_loss": (c_int, [P, c_float, P, P]),
+    "vq3d_vq_bwd": (c_int, [c_int, P, c_i64, c_int, P, P, c_int, P, P, c_float, P, P]),
+    "vq3d_vq_ema_stats": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, P, P, P]),
+    "vq3d_vq_ema_update": (c_int, [P, P, P, P, P, c_int, c_int, c_float, c_float, P]),
+    "vq3d_vq_moments": (c_int, [c_int, P, c_i64, c_int, P, P, P, P]),
+    "vq3d_vq_init_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, c_float, P]),
+    "vq3d_recon_loss_workspace_size": (c_size, [c_int] * 4),
+    "vq3d_recon_loss_fwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
+    "vq3d_recon_loss_bwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    "vq3d_cylinder_count": (c_i64, [c_int, c_int]),
+    "vq3d_evonorm_workspace_size": (c_size, [c_int, c_i64]),
+    "vq3d_evonorm_fwd": (c_int, [c_int, P, c_int, c_i64, P, P, P, P, P, P, P]),
+    "vq3d_evonorm_bwd": (c_int, [c_int, P, P, c_int, c_i64, P, P, P, P, P, P, P, P, P]),
+    "vq3d_adam_amsgrad": (c_int, [P, P, P, P, P, c_i64, c_float, c_float, c_float, c_float, c_i64, P]),
+    "vq3d_cast": (c_int, [c_int, P, c_int, P, c_i64, P]),
+    "vq3d_zero": (c_int, [P, c_size, P]),
+    "vq3d_copy": (c_int, [P, P, c_size, P]),
+    "vq3d_scale": (c_int, [P, c_float, c_i64, P]),
+    "vq3d_elu_bwd_from_output": (c_int, [c_int, P, P, P, c_i64, P]),
+    "vq3d_last_error": (ctypes.c_char_p, []),
+    "vq3d_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def load():
+    """Load libvq3d.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libvq3d.so not found at {LIB_PATH}: run `make -C 3d-vq-vae-2_amd` "
+                               "(or __graft_entry__.build()); the HIP path has no fallback")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def declared_symbols():
+    return sorted(_SIGS)
+
+
+class Vq3dError(RuntimeError):
+    pass
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise Vq3dError(f"{name}: {load().vq3d_last_error().decode()}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def stream():
+    """The current torch (HIP) stream: every launch goes there (graph-capture safe)."""
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise Vq3dError("vq3d ops take GPU tensors only (no CPU path)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def dtype_code(t_or_dtype):
+    dt = t_or_dtype.dtype if isinstance(t_or_dtype, torch.Tensor) else t_or_dtype
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise Vq3dError(f"unsupported activation dtype {dt}")

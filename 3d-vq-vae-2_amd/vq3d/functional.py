@@ -1,0 +1,320 @@
+"""autograd Functions of the VQ-VAE-2 hot path, each a fixed sequence of libvq3d kernels.
+
+Parameter gradients are written by the kernels straight into `param.grad` (fp32, one flat
+buffer per model, see flat.py) with += semantics, and the Functions return None for those
+inputs: no torch accumulate kernels, no extra allocations.  Every tensor in and out is a
+GPU tensor; the activations are channels-last (ops.py).
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from . import ops
+from .ops import ConvGeom
+
+CL = torch.channels_last_3d
+
+
+def grad_buf(p):
+    """fp32 gradient buffer of parameter p (allocated zeroed if the caller set it to None)."""
+    if p is None:
+        return None
+    if p.grad is None:
+        p.grad = ops.zero_(torch.empty_like(p))
+    return p.grad
+
+
+def _cl(g):
+    if g.is_contiguous(memory_format=CL) or (g.shape[1] == 1 and g.is_contiguous()):
+        return g
+    return g.contiguous(memory_format=CL)
+
+
+def mode_geometry(mode):
+    """branch conv2 of a residual block (layers.py:124-132 / 239-247 / 28-36)."""
+    if mode == "down":
+        return 4, 2, 1, False
+    if mode in ("same", "out"):
+        return 3, 1, 1, False
+    return 3, 1, 1, True
+
+
+# ============================================================================================ PreAct block
+class PreActBlockFn(torch.autograd.Function):
+    """PreActFixupResBlock.forward (layers.py:176-195) as 4 (5 in up mode) kernels forward and
+    ~12 backward.  Circular padding (layers.py:109).  Saved for backward: x, h1, h2 (+ the
+    upsampled branch input in up mode)."""
+
+    @staticmethod
+    def forward(ctx, x, blk, *params):
+        k, s, p, up = mode_geometry(blk.mode)
+        g1 = ConvGeom(1)
+        x = ops.as_cl(x)
+        h1 = ops.conv_fwd(x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b))
+        if up:
+            tup = ops.upsample2x(h1, pro=(blk.bias2a, blk.bias2b))
+            h2 = ops.conv_fwd(tup, blk.branch_conv2.weight, ConvGeom(3, 1, 1, True))
+        else:
+            tup = None
+            h2 = ops.conv_fwd(h1, blk.branch_conv2.weight, ConvGeom(k, s, p, True), pro=(blk.bias2a, blk.bias2b))
+        if blk.skip_conv is not None:
+            gs = ConvGeom(2, 2, 0) if blk.mode == "down" else g1
+            # up mode: W (up(x + b1c)) + b1d == up(W (x + b1c) + b1d) (both linear, weights sum to 1),
+            # so the skip runs on the half grid and is upsampled inside conv3's epilogue
+            res = ops.conv_fwd(x, blk.skip_conv.weight, gs, pro=(blk.bias1c,), bias=blk.bias1d)
+        else:
+            res = x
+        out = ops.conv_fwd(h2, blk.branch_conv3.weight, g1, pro=(blk.bias3a, blk.bias3b), scale=blk.scale,
+                           bias=blk.bias4, residual=res, residual_up2=up)
+        ctx.blk = blk
+        ctx.save_for_backward(x, h1, h2, tup)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        blk = ctx.blk
+        x, h1, h2, tup = ctx.saved_tensors
+        g = _cl(g)
+        k, s, p, up = mode_geometry(blk.mode)
+        g1 = ConvGeom(1)
+        gb = grad_buf
+        # conv3 (1x1 on the output grid): g_h2 = scale * W3^T g * elu'(h2 + b3a)
+        g_h2, _ = ops.conv_bwd(g, h2, blk.branch_conv3.weight, g1, pro=(blk.bias3a, blk.bias3b),
+                               gscale=blk.scale, aux=h2, dw=gb(blk.branch_conv3.weight), dscale=gb(blk.scale),
+                               dbias=gb(blk.bias4), dpro_pre=gb(blk.bias3b), dpro_post=gb(blk.bias3a),
+                               escale=blk.scale)
+        # conv2
+        if up:
+            g_tup, _ = ops.conv_bwd(g_h2, tup, blk.branch_conv2.weight, ConvGeom(3, 1, 1, True),
+                                    dw=gb(blk.branch_conv2.weight))
+            g_h1 = ops.upsample2x_bwd(g_tup, h1.shape, pro=(blk.bias2a, blk.bias2b), aux=h1,
+                                      dpro_pre=gb(blk.bias2b), dpro_post=gb(blk.bias2a))
+        else:
+            g_h1, _ = ops.conv_bwd(g_h2, h1, blk.branch_conv2.weight, ConvGeom(k, s, p, True),
+                                   pro=(blk.bias2a, blk.bias2b), aux=h1, dw=gb(blk.branch_conv2.weight),
+                                   dpro_pre=gb(blk.bias2b), dpro_post=gb(blk.bias2a))
+        # skip path
+        if blk.skip_conv is not None:
+            gs = ConvGeom(2, 2, 0) if blk.mode == "down" else g1
+            g_s = ops.upsample2x_bwd(g, x.shape[:1] + (blk.skip_conv.weight.shape[0],) + x.shape[2:]) if up else g
+            addend, _ = ops.conv_bwd(g_s, x, blk.skip_conv.weight, gs, pro=(blk.bias1c,),
+                                     dw=gb(blk.skip_conv.weight), dbias=gb(blk.bias1d), dpro_pre=gb(blk.bias1c))
+        else:
+            addend = g
+        # conv1 (1x1 on the input grid) + residual gradient
+        g_x, _ = ops.conv_bwd(g_h1, x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), aux=x,
+                              addend=addend, dw=gb(blk.branch_conv1.weight), dpro_pre=gb(blk.bias1b),
+                              dpro_post=gb(blk.bias1a))
+        return (g_x, None) + (None,) * len(blk._fn_params)
+
+
+# ============================================================================================ generic conv
+class ConvFn(torch.autograd.Function):
+    """One nn.Conv3d call with the fused prologue / epilogue (regular + EvoNorm blocks,
+    parse_input / proj / out, layers.py:535,377,490,508).  `spec` carries the geometry and
+    the Parameter objects whose .grad the kernels accumulate into."""
+
+    @staticmethod
+    def forward(ctx, x, x2, residual, spec, *tensors):
+        y = ops.conv_fwd(x, spec.w, spec.geom, pro=spec.pro, x2=x2, scale=spec.scale, bias=spec.bias,
+                         cbias=spec.cbias, residual=residual, residual_up2=spec.residual_up2,
+                         post_elu=spec.post_elu)
+        ctx.spec = spec
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, x2, y if spec.post_elu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        spec = ctx.spec
+        x, x2, y = ctx.saved_tensors
+        g = _cl(g)
+        if spec.post_elu:
+            gz = torch.empty_like(g)
+            L.call("vq3d_elu_bwd_from_output", L.dtype_code(g), L.ptr(g), L.ptr(y), L.ptr(gz), g.numel(),
+                   L.stream())
+            g = gz
+        g_res = None
+        if ctx.has_res and ctx.needs_input_grad[2]:
+            if spec.residual_up2:
+                b, c, h, w, d = g.shape
+                g_res = ops.upsample2x_bwd(g, (b, c, h // 2, w // 2, d // 2))
+            else:
+                g_res = g
+        gb = grad_buf
+        pro_pre = pro_post = None
+        if spec.pro is not None:
+            if len(spec.pro) == 1:
+                pro_pre = gb(spec.pro_params[0])
+            else:
+                pro_pre, pro_post = gb(spec.pro_params[1]), gb(spec.pro_params[0])
+        want = ctx.needs_input_grad[0] or (x2 is not None and ctx.needs_input_grad[1])
+        gx, gx2 = ops.conv_bwd(g, x, spec.w, spec.geom, pro=spec.pro, x2=x2, gscale=spec.scale, aux=x,
+                               want_gx=want, dw=gb(spec.w), dscale=gb(spec.scale), dbias=gb(spec.bias),
+                               dcbias=gb(spec.cbias), dpro_pre=pro_pre, dpro_post=pro_post, escale=spec.scale)
+        if not want:
+            gx = gx2 = None
+        return (gx, gx2, g_res, None) + (None,) * len(spec.tensors)
+
+
+class ConvSpec:
+    __slots__ = ("w", "geom", "pro", "pro_params", "scale", "bias", "cbias", "residual_up2", "post_elu",
+                 "tensors")
+
+    def __init__(self, w, geom, pro=None, scale=None, bias=None, cbias=None, residual_up2=False, post_elu=False):
+        self.w, self.geom, self.scale, self.bias, self.cbias = w, geom, scale, bias, cbias
+        self.pro = pro
+        self.pro_params = pro
+        self.residual_up2, self.post_elu = residual_up2, post_elu
+        self.tensors = tuple(t for t in (w, scale, bias, cbias) + tuple(pro or ()) if t is not None)
+
+
+def conv(x, spec, x2=None, residual=None):
+    return ConvFn.apply(x, x2, residual, spec, *spec.tensors)
+
+
+# ============================================================================================ upsample
+class UpsampleFn(torch.autograd.Function):
+    """nn.Upsample(trilinear, x2, align_corners=False) of ResizeConv3D (layers.py:591-597)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = tuple(x.shape)
+        return ops.upsample2x(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.upsample2x_bwd(_cl(g), ctx.shape)
+
+
+# ============================================================================================ EvoNorm-S0
+class EvoNormFn(torch.autograd.Function):
+    """EvoNorm3DS0 (evonorm.py:59-76): x*sigmoid(v x)*gamma / group_std(x) + beta, batch 1."""
+
+    @staticmethod
+    def forward(ctx, x, mod, v, gamma, beta):
+        x = ops.as_cl(x)
+        b, c = x.shape[:2]
+        if b != 1:
+            # the reference's group_std reshapes its std to batch 1 (evonorm.py:24) and fails
+            raise RuntimeError("EvoNorm3DS0 supports batch size 1 only (reference semantics, evonorm.py:24)")
+        nvox = x.numel() // c
+        y = torch.empty_like(x)
+        groups = max(c // 8, 1)
+        stats = torch.empty(2 * groups, dtype=torch.float32, device=x.device)
+        ws = ops.workspace(L.query("vq3d_evonorm_workspace_size", c, nvox), x.device)
+        L.call("vq3d_evonorm_fwd", L.dtype_code(x), L.ptr(x), c, nvox, L.ptr(v), L.ptr(gamma), L.ptr(beta),
+               L.ptr(y), L.ptr(stats), L.ptr(ws), L.stream())
+        ctx.mod = mod
+        ctx.save_for_backward(x, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, stats = ctx.saved_tensors
+        mod = ctx.mod
+        g = _cl(g)
+        c = x.shape[1]
+        nvox = x.numel() // c
+        gx = torch.empty_like(x)
+        ws = ops.workspace(L.query("vq3d_evonorm_workspace_size", c, nvox), x.device)
+        L.call("vq3d_evonorm_bwd", L.dtype_code(x), L.ptr(x), L.ptr(g), c, nvox, L.ptr(mod.v), L.ptr(mod.gamma),
+               L.ptr(stats), L.ptr(gx), L.ptr(grad_buf(mod.v)), L.ptr(grad_buf(mod.gamma)),
+               L.ptr(grad_buf(mod.beta)), L.ptr(ws), L.stream())
+        return gx, None, None, None, None
+
+
+# ============================================================================================ quantizer
+class QuantizeFn(torch.autograd.Function):
+    """Quantizer.forward (layers.py:685-728): fp32 codebook search (exact torch-CPU cdist
+    arithmetic), EMA update in train mode, commitment loss, straight-through output."""
+
+    @staticmethod
+    def forward(ctx, z, q):
+        z = ops.as_cl(z)
+        b, d, h, w, dz = z.shape
+        n = b * h * w * dz
+        k = q.num_embeddings
+        dev = z.device
+        st = L.stream()
+        ws = ops.workspace(L.query("vq3d_vq_workspace_size", n, d, k), dev)
+        zc = L.dtype_code(z)
+        if q.training and q.first_pass_host:
+            mean = torch.empty(d, dtype=torch.float32, device=dev)
+            std = torch.empty(d, dtype=torch.float32, device=dev)
+            L.call("vq3d_vq_moments", zc, L.ptr(z), n, d, L.ptr(mean), L.ptr(std), L.ptr(ws), st)
+            world, n_tot = 1, float(n)
+            if q.dist_reduce is not None:
+                world = q.dist_reduce(mean, std)
+                n_tot = float(n) * world
+            L.call("vq3d_vq_init_apply", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size),
+                   L.ptr(q.first_pass), L.ptr(mean), L.ptr(std), k, d, 1.0 / world, n_tot, st)
+            q.first_pass_host = False
+        embed = q.embed
+        if q.training:
+            embed = ops.copy_(torch.empty_like(q.embed), q.embed)  # pre-update codebook for q / backward
+        idx = torch.empty((b, h, w, dz), dtype=torch.int64, device=dev)
+        zst = torch.empty_like(z)
+        sq = torch.empty((), dtype=torch.float32, device=dev)
+        L.call("vq3d_vq_nearest", zc, L.ptr(z), n, d, L.ptr(embed), k, L.ptr(idx), zc, L.ptr(zst), L.ptr(sq),
+               L.ptr(ws), st)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        L.call("vq3d_vq_commit_loss", L.ptr(sq), q.commitment_cost / float(n * d), L.ptr(loss), st)
+        if q.training:
+            counts = torch.empty(k, dtype=torch.float32, device=dev)
+            dw = torch.empty((k, d), dtype=torch.float32, device=dev)
+            L.call("vq3d_vq_ema_stats", zc, L.ptr(z), n, d, L.ptr(idx), k, L.ptr(counts), L.ptr(dw), L.ptr(ws), st)
+            if q.dist_reduce is not None:
+                q.dist_reduce(counts, dw)
+            L.call("vq3d_vq_ema_update", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size), L.ptr(counts),
+                   L.ptr(dw), k, d, q.decay, q.laplace_alpha, st)
+        ctx.coef = 2.0 * q.commitment_cost / float(n * d)
+        ctx.save_for_backward(z, embed, idx)
+        ctx.mark_non_differentiable(idx)
+        return loss, zst, idx
+
+    @staticmethod
+    def backward(ctx, g_loss, g_zst, g_idx):
+        z, embed, idx = ctx.saved_tensors
+        b, d, h, w, dz = z.shape
+        n = b * h * w * dz
+        if g_zst is None:
+            g_zst = ops.zero_(torch.empty_like(z))
+        g_zst = _cl(g_zst)
+        gz = torch.empty_like(z)
+        L.call("vq3d_vq_bwd", L.dtype_code(z), L.ptr(z), n, d, L.ptr(embed), L.ptr(idx), L.dtype_code(g_zst),
+               L.ptr(g_zst), None if g_loss is None else L.ptr(g_loss), ctx.coef, L.ptr(gz), L.stream())
+        return gz, None
+
+
+# ============================================================================================ loss
+class ReconLossFn(torch.autograd.Function):
+    """VQVAE.loc_metric with F.smooth_l1_loss (model.py:115-163): returns (total, recon) with
+    total = recon + sum(commitment losses)."""
+
+    @staticmethod
+    def forward(ctx, dec, x, nvs, cylinder, *commit):
+        dec = ops.as_cl(dec)
+        b, _, h, w, d = dec.shape
+        dev = dec.device
+        recon = torch.empty((), dtype=torch.float32, device=dev)
+        total = torch.empty((), dtype=torch.float32, device=dev)
+        ws = ops.workspace(L.query("vq3d_recon_loss_workspace_size", b, h, w, d), dev)
+        arr = (ctypes.c_void_p * 8)(*[c.data_ptr() for c in commit])
+        L.call("vq3d_recon_loss_fwd", L.dtype_code(dec), L.ptr(dec), L.ptr(x), L.ptr(nvs), b, h, w, d,
+               int(cylinder), arr, len(commit), L.ptr(recon), L.ptr(total), L.ptr(ws), L.stream())
+        ctx.cyl = int(cylinder)
+        ctx.ncommit = len(commit)
+        ctx.save_for_backward(dec, x, nvs)
+        ctx.mark_non_differentiable(recon)
+        return total, recon
+
+    @staticmethod
+    def backward(ctx, g_total, g_recon):
+        dec, x, nvs = ctx.saved_tensors
+        b, _, h, w, d = dec.shape
+        gdec = torch.empty_like(dec)
+        L.call("vq3d_recon_loss_bwd", L.dtype_code(dec), L.ptr(dec), L.ptr(x), L.ptr(nvs), b, h, w, d, ctx.cyl,
+               L.ptr(g_total), L.ptr(gdec), L.stream())
+        return (gdec, None, None, None) + (g_total,) * ctx.ncommit

@@ -1,0 +1,178 @@
+"""Tensor-level wrappers over the libvq3d C-ABI.
+
+Activations are torch tensors with the reference's logical shape (B, C, H, W, D) stored
+channels-last (torch.channels_last_3d == physical [B][H][W][D][C]), fp32 or bf16.
+Every call enqueues on the current torch stream; nothing here synchronises the host.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+CL = torch.channels_last_3d
+
+
+def new_act(b, c, h, w, d, dtype, device):
+    return torch.empty((b, c, h, w, d), dtype=dtype, device=device, memory_format=CL)
+
+
+def as_cl(x):
+    """Return x in channels-last layout (no copy when already there; C == 1 is both)."""
+    if x.is_contiguous(memory_format=CL):
+        return x
+    if x.shape[1] == 1 and x.is_contiguous():
+        return x
+    raise L.Vq3dError("vq3d activations must be channels-last (torch.channels_last_3d); "
+                      "convert once at the model boundary")
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------------------------------------ conv
+class ConvGeom:
+    """Geometry of one nn.Conv3d call (kernel, stride, pad, padding mode)."""
+    __slots__ = ("k", "s", "p", "circular")
+
+    def __init__(self, k, s=1, p=0, circular=False):
+        self.k, self.s, self.p, self.circular = int(k), int(s), int(p), bool(circular)
+
+    def out(self, n):
+        return (n + 2 * self.p - self.k) // self.s + 1
+
+    def key(self):
+        return (self.k, self.s, self.p, self.circular)
+
+
+_desc_cache = {}
+
+
+def conv_desc(dtype, b, cin, cin2, cout, h, w, d, geom, pro_kind):
+    key = (dtype, b, cin, cin2, cout, h, w, d, geom.key(), pro_kind)
+    r = _desc_cache.get(key)
+    if r is None:
+        oh, ow, od = geom.out(h), geom.out(w), geom.out(d)
+        desc = L.ConvDesc(dtype=L.dtype_code(dtype), batch=b, cin=cin, cin2=cin2, cout=cout, in_h=h, in_w=w,
+                          in_d=d, out_h=oh, out_w=ow, out_d=od, kernel=geom.k, stride=geom.s, pad=geom.p,
+                          pad_mode=L.PAD_CIRCULAR if geom.circular else L.PAD_ZEROS, pro_kind=pro_kind)
+        ws = L.query("vq3d_conv3d_bwd_workspace_size", ctypes.byref(desc))
+        if ws == 0:
+            raise L.Vq3dError(f"invalid conv descriptor: {L.load().vq3d_last_error().decode()}")
+        r = (desc, (oh, ow, od), ws)
+        _desc_cache[key] = r
+    return r
+
+
+def pro_kind_of(pro):
+    """pro = None | (a,) | (a, b): none / x + a / elu(x + a) + b (device scalar tensors)."""
+    if pro is None:
+        return L.PRO_NONE, None, None
+    if len(pro) == 1:
+        return L.PRO_ADD, pro[0], None
+    return L.PRO_ELU_ADD, pro[0], pro[1]
+
+
+def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, residual=None,
+             residual_up2=False, post_elu=False, out=None):
+    x = as_cl(x)
+    b, cin, h, wd, d = x.shape
+    cin2 = 0 if x2 is None else x2.shape[1]
+    cout = w.shape[0]
+    kind, pa, pb = pro_kind_of(pro)
+    desc, (oh, ow, od), _ = conv_desc(x.dtype, b, cin, cin2, cout, h, wd, d, geom, kind)
+    if w.shape[1] != cin + cin2 or w.shape[2] != geom.k:
+        raise L.Vq3dError(f"weight {tuple(w.shape)} does not match conv ({cin}+{cin2} -> {cout}, k={geom.k})")
+    y = out if out is not None else new_act(b, cout, oh, ow, od, x.dtype, x.device)
+    if residual is not None:
+        rs = (b, cout, oh // 2, ow // 2, od // 2) if residual_up2 else (b, cout, oh, ow, od)
+        if tuple(residual.shape) != rs or residual.dtype != x.dtype:
+            raise L.Vq3dError(f"residual {tuple(residual.shape)} does not match {rs}")
+        as_cl(residual)
+    epi = L.ConvEpilogue(scale=_p(scale), bias=_p(bias), cbias=_p(cbias), residual=_p(residual),
+                         residual_up2=int(residual_up2), post_elu=int(post_elu))
+    L.call("vq3d_conv3d_fwd", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(w), _p(pa), _p(pb),
+           ctypes.byref(epi), L.ptr(y), L.stream())
+    return y
+
+
+def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, addend=None, want_gx=True,
+             dw=None, dscale=None, dbias=None, dcbias=None, dpro_pre=None, dpro_post=None, escale=None):
+    """Backward of conv_fwd: returns (gx, gx2); parameter gradients are ACCUMULATED into the
+    given fp32 buffers (dw: weight, dscale/dbias: epilogue scalars, dcbias: conv bias,
+    dpro_pre/dpro_post: prologue scalars (+b / +a of elu(x+a)+b, or a of x+a))."""
+    x = as_cl(x)
+    b, cin, h, wd, d = x.shape
+    cin2 = 0 if x2 is None else x2.shape[1]
+    kind, pa, pb = pro_kind_of(pro)
+    desc, _, wsb = conv_desc(x.dtype, b, cin, cin2, w.shape[0], h, wd, d, geom, kind)
+    ws = workspace(wsb, x.device)
+    s = L.stream()
+    gx = gx2 = None
+    need_partials = dpro_pre is not None or dpro_post is not None
+    if want_gx or need_partials:
+        gx = new_act(b, cin, h, wd, d, x.dtype, x.device)
+        gx2 = None if x2 is None else new_act(b, cin2, h, wd, d, x.dtype, x.device)
+        epi = L.DgradEpilogue(aux=_p(aux), addend=_p(addend))
+        L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), _p(gscale), L.ptr(w), _p(pa),
+               ctypes.byref(epi), L.ptr(gx), _p(gx2), L.ptr(ws), s)
+    L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb),
+           L.ptr(ws), s)
+    L.call("vq3d_conv3d_bwd_finalize", ctypes.byref(desc), L.ptr(w), _p(escale), L.ptr(ws), _p(dw),
+           _p(dscale), _p(dbias), _p(dcbias), _p(dpro_pre), _p(dpro_post), s)
+    return gx, gx2
+
+
+# ------------------------------------------------------------------------------------------------ upsample
+def upsample2x(x, pro=None):
+    x = as_cl(x)
+    b, c, h, w, d = x.shape
+    kind, pa, pb = pro_kind_of(pro)
+    y = new_act(b, c, 2 * h, 2 * w, 2 * d, x.dtype, x.device)
+    L.call("vq3d_upsample2x_fwd", L.dtype_code(x), b, c, h, w, d, L.ptr(x), kind, _p(pa), _p(pb), L.ptr(y),
+           L.stream())
+    return y
+
+
+def upsample2x_bwd(gy, src_shape, pro=None, aux=None, addend=None, dpro_pre=None, dpro_post=None):
+    b, c, h, w, d = src_shape
+    kind, pa, _ = pro_kind_of(pro)
+    gx = new_act(b, c, h, w, d, gy.dtype, gy.device)
+    ws = workspace(L.query("vq3d_upsample2x_bwd_workspace_size", b, c, h, w, d), gy.device)
+    epi = L.DgradEpilogue(aux=_p(aux), addend=_p(addend))
+    s = L.stream()
+    L.call("vq3d_upsample2x_bwd", L.dtype_code(gy), b, c, h, w, d, L.ptr(gy), kind, _p(pa), ctypes.byref(epi),
+           L.ptr(gx), L.ptr(ws), s)
+    if dpro_pre is not None or dpro_post is not None:
+        L.call("vq3d_upsample2x_bwd_finalize", b, c, h, w, d, L.ptr(ws), _p(dpro_pre), _p(dpro_post), s)
+    return gx
+
+
+# ------------------------------------------------------------------------------------------------ misc
+def cast(x, dtype):
+    if x.dtype == dtype:
+        return x
+    y = torch.empty_like(x, dtype=dtype)
+    L.call("vq3d_cast", L.dtype_code(x), L.ptr(x), L.dtype_code(dtype), L.ptr(y), x.numel(), L.stream())
+    return y
+
+
+def zero_(t):
+    L.call("vq3d_zero", L.ptr(t), t.numel() * t.element_size(), L.stream())
+    return t
+
+
+def copy_(dst, src):
+    assert dst.numel() == src.numel() and dst.dtype == src.dtype
+    L.call("vq3d_copy", L.ptr(dst), L.ptr(src), src.numel() * src.element_size(), L.stream())
+    return dst
+
+
+def scale_(t, a):
+    L.call("vq3d_scale", L.ptr(t), float(a), t.numel(), L.stream())
+    return t

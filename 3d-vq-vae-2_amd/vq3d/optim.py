@@ -1,0 +1,72 @@
+"""torch.optim.Adam(amsgrad=True) (reference vqvae/model.py:91-93) as one fused kernel over
+the flat parameter buffer.  state_dict() uses torch Adam's per-parameter layout
+(exp_avg / exp_avg_sq / max_exp_avg_sq / step) so checkpoints interchange."""
+import torch
+
+from . import _lib as L
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=True):
+        if weight_decay != 0 or not amsgrad:
+            raise NotImplementedError("FusedAdam implements the reference's Adam(amsgrad=True, weight_decay=0)")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=True))
+        self.flat = flat
+        for g in self.param_groups:
+            for p in g["params"]:
+                if not flat.owns(p):
+                    raise ValueError("FusedAdam: every parameter must live in the model's flat buffer")
+        self.m = torch.zeros_like(flat.data)
+        self.v = torch.zeros_like(flat.data)
+        self.vmax = torch.zeros_like(flat.data)
+        self.step_count = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        f = self.flat
+        L.call("vq3d_adam_amsgrad", L.ptr(f.data), L.ptr(f.grad), L.ptr(self.m), L.ptr(self.v), L.ptr(self.vmax),
+               f.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), self.step_count, L.stream())
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    def state_dict(self):
+        sd = super().state_dict()
+        st = {}
+        idx = 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                off = self.flat.offsets[self.flat.params.index(p)]
+                n = p.numel()
+                if self.step_count:
+                    st[idx] = dict(step=torch.tensor(float(self.step_count)),
+                                   exp_avg=self.m[off:off + n].view(p.shape).clone(),
+                                   exp_avg_sq=self.v[off:off + n].view(p.shape).clone(),
+                                   max_exp_avg_sq=self.vmax[off:off + n].view(p.shape).clone())
+                idx += 1
+        sd["state"] = st
+        return sd
+
+    def load_state_dict(self, state_dict):
+        st = state_dict["state"]
+        idx = 0
+        steps = set()
+        for g in self.param_groups:
+            for p in g["params"]:
+                off = self.flat.offsets[self.flat.params.index(p)]
+                n = p.numel()
+                s = st.get(idx)
+                if s is not None:
+                    self.m[off:off + n].copy_(s["exp_avg"].reshape(-1))
+                    self.v[off:off + n].copy_(s["exp_avg_sq"].reshape(-1))
+                    self.vmax[off:off + n].copy_(s["max_exp_avg_sq"].reshape(-1))
+                    steps.add(int(float(s["step"])))
+                idx += 1
+        self.step_count = steps.pop() if steps else 0
+        for g, sg in zip(self.param_groups, state_dict["param_groups"]):
+            g["lr"] = sg["lr"]

@@ -1,0 +1,191 @@
+/*
+ * vq3d.h — C-ABI of libvq3d.so, the MI355X (gfx950) kernels behind the 3D VQ-VAE-2
+ * training step.  Plain pointers + sizes; no torch types.  The caller owns every
+ * buffer (activations, gradients, workspaces); the library never allocates device
+ * memory and never synchronises: every entry point enqueues work on `stream` and
+ * returns.  Return value 0 = success, < 0 = error (message in vq3d_last_error(),
+ * thread-local).  Entry points are stateless and re-entrant.
+ *
+ * The reference (sara-nl/3D-VQ-VAE-2) has no native code or FFI: its "operator API"
+ * is nn.Module calls into ATen.  Each entry below replaces
+ * the ATen work behind one reference call site, cited per function.
+ *
+ * Activation layout: channels-last NDHWC, i.e. the reference tensor (B, C, H, W, D)
+ * stored as [B][H][W][D][C].  Storage dtype per call (VQ3D_F32 or VQ3D_BF16);
+ * arithmetic is fp32.  Weights are fp32 in the reference layout (Cout, Cin, k, k, k).
+ */
+#ifndef VQ3D_H
+#define VQ3D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *vq3d_stream_t; /* == hipStream_t */
+
+enum { VQ3D_F32 = 0, VQ3D_BF16 = 1 };
+enum { VQ3D_PAD_ZEROS = 0, VQ3D_PAD_CIRCULAR = 1 };
+/* prologue applied to every input element as it is loaded (reference glue, layers.py:178-185) */
+enum { VQ3D_PRO_NONE = 0, VQ3D_PRO_ADD = 1 /* x + a */, VQ3D_PRO_ELU_ADD = 2 /* elu(x + a) + b */ };
+
+/* One 3-D convolution as nn.Conv3d computes it (padding_mode 'zeros' or 'circular';
+ * circular == F.pad(x, p, 'circular') then a valid conv). */
+typedef struct vq3d_conv_desc {
+    int32_t dtype;      /* activation storage: VQ3D_F32 | VQ3D_BF16 */
+    int32_t batch;
+    int32_t cin;        /* channels of input 1 */
+    int32_t cin2;       /* channels of input 2, concatenated after input 1 (torch.cat dim=1); 0 = none */
+    int32_t cout;
+    int32_t in_h, in_w, in_d;
+    int32_t out_h, out_w, out_d;
+    int32_t kernel, stride, pad, pad_mode;
+    int32_t pro_kind;   /* VQ3D_PRO_* applied to the input on load */
+} vq3d_conv_desc;
+
+/* Forward epilogue: y = post( acc*scale + bias + cbias[co] + residual ) */
+typedef struct vq3d_conv_epilogue {
+    const float *scale;     /* device scalar or NULL (PreAct `scale`, layers.py:187) */
+    const float *bias;      /* device scalar or NULL (`bias4`, `bias1d`, `bias2b`)  */
+    const float *cbias;     /* device [cout] or NULL (nn.Conv3d bias)               */
+    const void *residual;   /* NULL or activation tensor added before post-ELU       */
+    int32_t residual_up2;   /* 1: residual lives on the half-resolution grid and is
+                               trilinearly upsampled x2 on the fly (ResizeConv skip)  */
+    int32_t post_elu;       /* 1: y = elu(.) (FixupResBlock, layers.py:287-288)      */
+} vq3d_conv_epilogue;
+
+/* Backward-data epilogue on the conv INPUT grid:
+ *   v = acc;  pre += v;  v *= d/dx prologue(aux);  post += v;  v += addend;  store
+ * pre/post are summed over every element into `scalar_partials` (see finalize). */
+typedef struct vq3d_dgrad_epilogue {
+    const void *aux;        /* forward input before the prologue (needed for ELU'), or NULL */
+    const void *addend;     /* gradient added after the prologue derivative, or NULL */
+} vq3d_dgrad_epilogue;
+
+/* --- 3-D convolution (replaces nn.Conv3d / F.pad circular, layers.py:124-171,535,377,490,508) --- */
+int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w,
+                    const float *pro_a, const float *pro_b, const vq3d_conv_epilogue *epi,
+                    void *y, vq3d_stream_t stream);
+
+/* Workspace (bytes) for the backward of one conv: weight-grad partial slabs + scalar partials. */
+size_t vq3d_conv3d_bwd_workspace_size(const vq3d_conv_desc *d);
+
+/* Gradient w.r.t. the input(s).  g = dL/dy (y grid, cout channels); gscale: device scalar
+ * multiplying g (the PreAct `scale`) or NULL.  gx (and gx2 for input 2) receive the result. */
+int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
+                         const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2,
+                         void *workspace, vq3d_stream_t stream);
+
+/* Gradient w.r.t. the weight: G[co,ci,t] = sum_v g[v,co] * prologue(x)[nbr(v,t),ci], written
+ * as fp32 partial slabs into `workspace` (same workspace as bwd_data, disjoint region). */
+int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g,
+                           const float *pro_a, const float *pro_b, void *workspace,
+                           vq3d_stream_t stream);
+
+/* Reduce the partial slabs in a fixed order (deterministic) and ACCUMULATE (+=) into the
+ * fp32 gradient buffers (any may be NULL):
+ *   dw      += scale * G            (scale = *epi_scale, or 1)
+ *   dscale  += sum(W * G)           (d/d scale of the forward epilogue)
+ *   dbias   += sum(g)               (forward epilogue scalar bias)
+ *   dcbias  += sum_v g[v, co]       (nn.Conv3d bias)
+ *   dpro_pre += sum(pre), dpro_post += sum(post)   (prologue scalars: see bwd_data) */
+int vq3d_conv3d_bwd_finalize(const vq3d_conv_desc *d, const float *w, const float *epi_scale,
+                             const void *workspace, float *dw, float *dscale, float *dbias,
+                             float *dcbias, float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
+
+/* --- trilinear x2 upsample, align_corners=False (nn.Upsample in ResizeConv3D, layers.py:591-597) --- */
+int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
+                        const void *x, int32_t pro_kind, const float *pro_a, const float *pro_b, void *y,
+                        vq3d_stream_t stream);
+/* Adjoint of the upsample on the source grid, with the bwd_data epilogue (prologue
+ * derivative w.r.t. aux, addend) and pre/post scalar partials in `workspace`
+ * (vq3d_upsample2x_bwd_workspace_size bytes), reduced by vq3d_reduce_scalars. */
+size_t vq3d_upsample2x_bwd_workspace_size(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd);
+int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
+                        const void *gy, int32_t pro_kind, const float *pro_a, const vq3d_dgrad_epilogue *epi,
+                        void *gx, void *workspace, vq3d_stream_t stream);
+/* sum the pre/post partials written by vq3d_upsample2x_bwd into dpro_pre / dpro_post (+=) */
+int vq3d_upsample2x_bwd_finalize(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
+                                 const void *workspace, float *dpro_pre, float *dpro_post,
+                                 vq3d_stream_t stream);
+
+/* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
+/* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),
+ * q = E[idx], zst = fl(x + fl(q - x)) stored as zst_dtype, and the squared-error sum
+ * for the commitment loss (layers.py:716) reduced into *sqerr_out (fp32 scalar).
+ * z: n rows of d fp32-or-bf16 values (z_dtype), row order (b, h, w, d) = channels-last. */
+size_t vq3d_vq_workspace_size(int64_t n, int32_t d, int32_t k);
+int vq3d_vq_nearest(int32_t z_dtype, const void *z, int64_t n, int32_t d, const float *embed, int32_t k,
+                    int64_t *idx, int32_t zst_dtype, void *zst, float *sqerr_out, void *workspace,
+                    vq3d_stream_t stream);
+/* loss = coef * (*sqerr) ; writes a device scalar (coef = commitment_cost / numel) */
+int vq3d_vq_commit_loss(const float *sqerr, float coef, float *loss, vq3d_stream_t stream);
+/* gz = g_zst + (*g_loss) * coef * (x - q)    (coef = 2 * commitment_cost / numel) */
+int vq3d_vq_bwd(int32_t z_dtype, const void *z, int64_t n, int32_t d, const float *embed, const int64_t *idx,
+                int32_t g_dtype, const void *g_zst, const float *g_loss, float coef, void *gz,
+                vq3d_stream_t stream);
+/* counts[k] = #rows with idx == k ; dw[k, :] = sum of those rows   (deterministic) */
+int vq3d_vq_ema_stats(int32_t z_dtype, const void *z, int64_t n, int32_t d, const int64_t *idx, int32_t k,
+                      float *counts, float *dw, void *workspace, vq3d_stream_t stream);
+/* cluster_size = cs*decay + counts*(1-decay); embed_avg likewise with dw; Laplace smoothing;
+ * embed = embed_avg / smoothed  (layers.py:649-663). counts/dw already world-summed. */
+int vq3d_vq_ema_update(float *embed, float *embed_avg, float *cluster_size, const float *counts,
+                       const float *dw, int32_t k, int32_t d, float decay, float laplace_alpha,
+                       vq3d_stream_t stream);
+/* mean[d] and unbiased std[d] over the n rows (layers.py:666-667) */
+int vq3d_vq_moments(int32_t z_dtype, const void *z, int64_t n, int32_t d, float *mean, float *std,
+                    void *workspace, vq3d_stream_t stream);
+/* embed = embed*(std/world) + mean/world ; embed_avg = embed ; cluster_size += n_total/k ;
+ * *first_pass = 0   (layers.py:670-683; mean/std already world-summed) */
+int vq3d_vq_init_apply(float *embed, float *embed_avg, float *cluster_size, int64_t *first_pass,
+                       const float *mean, const float *std, int32_t k, int32_t d, float inv_world,
+                       float n_total, vq3d_stream_t stream);
+
+/* --- reconstruction loss (VQVAE.loc_metric with F.smooth_l1_loss, model.py:115-163) ---
+ * loc = elu(dec); loc[..., s >= nvs[b]] = 0; optional centre-cylinder gather
+ * (ExtractCenterCylinder, load_nrrd_dataset.py:258-300); smooth-L1 (beta 1) mean. */
+size_t vq3d_recon_loss_workspace_size(int32_t batch, int32_t h, int32_t w, int32_t dd);
+/* total = recon + sum_i *commit[i]  (commit: host array of n_commit <= 8 device scalars) */
+int vq3d_recon_loss_fwd(int32_t dtype, const void *dec, const float *x, const int64_t *nvs, int32_t batch,
+                        int32_t h, int32_t w, int32_t dd, int32_t cylinder, const float *const *commit,
+                        int32_t n_commit, float *recon, float *total, void *workspace, vq3d_stream_t stream);
+int vq3d_recon_loss_bwd(int32_t dtype, const void *dec, const float *x, const int64_t *nvs, int32_t batch,
+                        int32_t h, int32_t w, int32_t dd, int32_t cylinder, const float *g_total,
+                        void *gdec, vq3d_stream_t stream);
+/* number of (h, w) pixels inside the cylinder (host function) */
+int64_t vq3d_cylinder_count(int32_t h, int32_t w);
+
+/* --- EvoNorm-S0 (evonorm.py:8-76), batch 1 --- */
+size_t vq3d_evonorm_workspace_size(int32_t channels, int64_t voxels);
+int vq3d_evonorm_fwd(int32_t dtype, const void *x, int32_t channels, int64_t voxels, const float *v,
+                     const float *gamma, const float *beta, void *y, float *stats, void *workspace,
+                     vq3d_stream_t stream);
+int vq3d_evonorm_bwd(int32_t dtype, const void *x, const void *gy, int32_t channels, int64_t voxels,
+                     const float *v, const float *gamma, const float *stats, void *gx, float *dv,
+                     float *dgamma, float *dbeta, void *workspace, vq3d_stream_t stream);
+
+/* --- optimizer: torch.optim.Adam(amsgrad=True) over one flat fp32 buffer (model.py:91-93) --- */
+int vq3d_adam_amsgrad(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr,
+                      float beta1, float beta2, float eps, int64_t step, vq3d_stream_t stream);
+
+/* --- utilities --- */
+int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, int64_t n,
+              vq3d_stream_t stream);
+int vq3d_zero(void *p, size_t bytes, vq3d_stream_t stream);
+int vq3d_copy(void *dst, const void *src, size_t bytes, vq3d_stream_t stream);
+/* gz = g * elu'(z) recovered from the OUTPUT y = elu(z): 1 if y > 0 else y + 1 (FixupResBlock's
+ * post-activation, layers.py:287-288); n elements of dtype */
+int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *gz, int64_t n,
+                             vq3d_stream_t stream);
+/* x *= a over n fp32 values (gradient averaging after the all-reduce uses a = 1/world) */
+int vq3d_scale(float *x, float a, int64_t n, vq3d_stream_t stream);
+
+const char *vq3d_last_error(void);
+const char *vq3d_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VQ3D_H */

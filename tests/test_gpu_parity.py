@@ -1,0 +1,228 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's goldens and the CPU
+oracle.  Tolerances: codes / indices bit-exact; fp32 conv path within 2e-4 relative to the
+tensor's max magnitude (summation order differs from MKLDNN); bf16 path within the stated
+bf16 bounds."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last_3d
+
+
+def to_gpu(a, dev, dtype=torch.float32):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    if t.dim() == 5:
+        t = t.contiguous(memory_format=CL)
+    return t.to(dtype)
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+
+
+# ------------------------------------------------------------------------------------------ VQ (bit-exact)
+def test_vq_nearest_kats_bitexact(gpu):
+    from vq3d import _lib as L
+    from vq3d import ops
+    d = golden("vq_kat")
+    names = sorted({k.split("/")[0] for k in d.files})
+    for n in names:
+        z = torch.from_numpy(d[n + "/z"]).to(gpu)
+        e = torch.from_numpy(d[n + "/embed"]).to(gpu)
+        rows, dim = z.shape
+        k = e.shape[0]
+        idx = torch.empty(rows, dtype=torch.int64, device=gpu)
+        zst = torch.empty_like(z)
+        sq = torch.empty((), dtype=torch.float32, device=gpu)
+        ws = ops.workspace(L.query("vq3d_vq_workspace_size", rows, dim, k), gpu)
+        L.call("vq3d_vq_nearest", L.F32, L.ptr(z), rows, dim, L.ptr(e), k, L.ptr(idx), L.F32, L.ptr(zst),
+               L.ptr(sq), L.ptr(ws), L.stream())
+        assert np.array_equal(idx.cpu().numpy(), d[n + "/idx"]), n
+        assert np.array_equal(zst.cpu().numpy().view(np.uint32), d[n + "/zst"].view(np.uint32)), n
+        loss = 0.1 * float(sq) / z.numel()
+        assert abs(loss - float(d[n + "/loss"])) <= 1e-5 * abs(float(d[n + "/loss"])) + 1e-12, n
+
+
+def test_quantizer_train_goldens(gpu):
+    from vq3d.layers import Quantizer
+    d = golden("quantizer_train")
+    for pre in ["k128_d2", "k256_d8", "k512_d32"]:
+        k, dim = int(pre.split("_")[0][1:]), int(pre.split("_")[1][1:])
+        q = Quantizer(k, dim, 0.1).to(gpu).train()
+        with torch.no_grad():
+            q.embed.copy_(torch.from_numpy(d[pre + "/embed0"]))
+            q.embed_avg.copy_(torch.from_numpy(d[pre + "/embed_avg0"]))
+            q.cluster_size.copy_(torch.from_numpy(d[pre + "/cluster_size0"]))
+        for step in range(2):
+            s = f"{pre}/step{step}"
+            x = to_gpu(d[s + "/x"], gpu).requires_grad_(True)
+            loss, qst, idx = q(x)
+            (loss * 2.0 + (qst * to_gpu(d[s + "/gq"], gpu)).sum()).backward()
+            assert np.array_equal(idx.cpu().numpy(), d[s + "/idx"]), s
+            assert abs(float(loss.detach()) - float(d[s + "/loss"])) <= 1e-5 * abs(float(d[s + "/loss"])), s
+            # step 0 codebook is bit-identical; after one EMA update (dw summed in a different
+            # order than the reference's BLAS) the codewords agree to ~1e-6 relative
+            assert rel_err(qst.detach().cpu().numpy(), d[s + "/qst"]) < (1e-6 if step == 0 else 2e-5), s
+            assert rel_err(x.grad.cpu().numpy(), d[s + "/gx"]) < 1e-5, s
+            for b in ("embed", "embed_avg", "cluster_size"):
+                assert rel_err(getattr(q, b).cpu().numpy(), d[f"{s}/{b}"]) < 2e-5, (s, b)
+            assert int(q.first_pass) == int(d[s + "/first_pass"])
+
+
+# ------------------------------------------------------------------------------------------ single ops + blocks
+def _build(name, meta=None):
+    import vq3d
+    from vq3d import layers as VL
+    from vq3d.functional import UpsampleFn
+    if name.startswith(("preact", "regular", "evonorm_same", "evonorm_down", "evonorm_up")):
+        cin, cout, mode = int(meta[0]), int(meta[1]), ["down", "same", "up", "out"][int(meta[2])]
+        cls = {"preact": VL.PreActFixupResBlock, "regular": VL.FixupResBlock, "evonorm": VL.EvonormResBlock}
+        return cls[name.split("_")[0]](cin, cout, mode=mode)
+    table = {
+        "conv3_circ_5_3_d2": lambda: VL.Conv3d(5, 3, 3, 1, 1, bias=False, padding_mode='circular'),
+        "conv4s2_circ_3_6": lambda: VL.Conv3d(3, 6, 4, 2, 1, bias=False, padding_mode='circular'),
+        "conv2s2_4_8": lambda: VL.Conv3d(4, 8, 2, 2, 0, bias=False),
+        "conv1_bias_3_5": lambda: VL.Conv3d(3, 5, 1),
+        "resize3_circ_3_4": lambda: VL.ResizeConv3D(3, 4, 3, 1, 1, bias=False, padding_mode='circular'),
+        "resize1_4_2": lambda: VL.ResizeConv3D(4, 2, 1, 1, 0, bias=False),
+        "conv3_zero_bias_4_4": lambda: VL.Conv3d(4, 4, 3, 1, 1),
+        "conv4s2_zero_4_4": lambda: VL.Conv3d(4, 4, 4, 2, 1),
+        "evonorm_s0_16": lambda: vq3d.EvoNorm3DS0(16),
+    }
+    if name == "upsample_tri":
+        class Up(torch.nn.Module):
+            def forward(self, x):
+                return UpsampleFn.apply(x)
+        return Up()
+    return table[name]()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_blocks_and_ops(gpu, dtype):
+    from vq3d.flat import FlatParams
+    d = golden("blocks")
+    names = sorted({k.split("/")[0] for k in d.files})
+    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    tol = 2e-4 if dtype == "fp32" else 6e-2
+    failures = []
+    for name in names:
+        meta = d[name + "/meta"] if name + "/meta" in d.files else None
+        m = _build(name, meta)
+        pnames = [k[len(name) + 7:] for k in d.files if k.startswith(name + "/param/")]
+        with torch.no_grad():
+            for pn, p in m.named_parameters():
+                p.copy_(torch.from_numpy(d[f"{name}/param/{pn}"]))
+        assert set(pnames) == {pn for pn, _ in m.named_parameters()}, name
+        m = m.to(gpu)
+        if len(list(m.parameters())):
+            FlatParams(m.parameters(), gpu)
+        x = to_gpu(d[name + "/x"], gpu, tdt).requires_grad_(True)
+        y = m(x)
+        y.backward(to_gpu(d[name + "/gy"], gpu, tdt))
+        errs = {"y": rel_err(y.detach().float().cpu().numpy(), d[name + "/y"]),
+                "gx": rel_err(x.grad.float().cpu().numpy(), d[name + "/gx"])}
+        small = set()
+        for pn, p in m.named_parameters():
+            errs["grad/" + pn] = rel_err(p.grad.cpu().numpy(), d[f"{name}/grad/{pn}"])
+            if p.numel() <= 64:
+                small.add("grad/" + pn)
+        # bf16: scalar / bias gradients are sums of thousands of bf16-rounded terms with heavy
+        # cancellation, so they are held to 0.5 relative (fp32 run: 2e-4 like everything else)
+        bad = {k: v for k, v in errs.items() if not v <= (0.5 if dtype == "bf16" and k in small else tol)}
+        if bad:
+            failures.append((name, bad))
+    assert not failures, failures
+
+
+# ------------------------------------------------------------------------------------------ whole model
+MODEL_CFGS = {
+    "model_2l_dflt_32": dict(n_bottleneck_blocks=2),
+    "model_2l_blocks_32": dict(n_bottleneck_blocks=2, n_pre_quantization_blocks=1, n_post_quantization_blocks=1,
+                               n_post_upscale_blocks=1, n_post_downscale_blocks=1, num_embeddings=[64, 32]),
+    "model_3l_b2_64": dict(n_bottleneck_blocks=3, base_network_channels=2, num_embeddings=[128, 256, 512]),
+    "model_2l_regular_32": dict(n_bottleneck_blocks=2, block_type='regular', base_network_channels=2),
+    "model_2l_evonorm_32": dict(n_bottleneck_blocks=2, block_type='evonorm'),
+}
+
+
+def load_model(name, dev, dtype="fp32"):
+    import vq3d
+    d = golden(name)
+    args = vq3d.default_args(compute_dtype=dtype, **MODEL_CFGS[name])
+    m = vq3d.VQVAE(args)
+    sd = {k[5:]: torch.from_numpy(d[k].copy()) for k in d.files if k.startswith("init/")}
+    m.load_state_dict(sd)
+    m.lr = float(d["lr"])
+    m = m.to(dev)
+    return m, d
+
+
+@pytest.mark.parametrize("name", sorted(MODEL_CFGS))
+def test_model_train_step_fp32(gpu, name):
+    """fp32 path vs the reference: codes bit-exact, decoded/loss/grads/Adam state within fp tol."""
+    m, d = load_model(name, gpu, "fp32")
+    opt = m.configure_optimizers()
+    xs = tuple(int(v) for v in d["x_shape"])
+    nvs = torch.as_tensor(d["nvs"])
+    stride = int(d["dec_stride"])
+    for step in range(2):
+        if f"step{step}/loss" not in d.files:
+            break
+        x = (torch.rand(xs, generator=torch.Generator().manual_seed(1234 + step)) * 4.5 - 0.5).to(gpu)
+        m.train()
+        opt.zero_grad()
+        cap = {}
+        fwd = m.forward
+
+        def capture(data):
+            r = fwd(data)
+            cap["r"] = r
+            return r
+        m.forward = capture
+        loss = m.training_step((x, nvs), step)
+        del m.forward
+        loss.backward()
+        opt.step()
+        dec, (commit, qst, idx) = cap["r"]
+        for lvl, ix in enumerate(idx):
+            got = ix.cpu().numpy()
+            ref = d[f"step{step}/idx{lvl}"]
+            match = (got == ref).mean()
+            # exact arithmetic differs only in conv summation order; codes on near-ties may flip
+            assert match >= 0.999, (name, step, lvl, match)
+        assert abs(float(loss) - float(d[f"step{step}/loss"])) <= 2e-4 * abs(float(d[f"step{step}/loss"])), \
+            (float(loss), float(d[f"step{step}/loss"]))
+        e = rel_err(dec.detach().float().cpu().numpy()[..., ::stride, ::stride, ::stride], d[f"step{step}/dec"])
+        assert e < 5e-4, (name, step, e)
+        if f"step{step}/grad/encoder.parse_input.weight" in d.files:
+            for pn, p in m.named_parameters():
+                g = d[f"step{step}/grad/{pn}"]
+                ge = rel_err(p.grad.cpu().numpy(), g)
+                assert ge < 5e-3, (name, pn, ge)
+        for k in [k for k in d.files if k.startswith(f"step{step}/state/")]:
+            pn = k.split("/", 2)[2]
+            got = m.state_dict()[pn].cpu().numpy()
+            ref = d[k]
+            if ref.dtype.kind == "f":
+                assert np.abs(got - ref).max() <= 1e-3 * max(np.abs(ref).max(), 1.0), (name, pn)
+            else:
+                assert np.array_equal(got, ref), (name, pn)
+
+
+def test_model_bf16_step(gpu):
+    """bf16 activations: loss within 2 %, decoded within bf16 tolerance, codes mostly equal."""
+    m, d = load_model("model_2l_dflt_32", gpu, "bf16")
+    opt = m.configure_optimizers()
+    x = (torch.rand((1, 1, 32, 32, 32), generator=torch.Generator().manual_seed(1234)) * 4.5 - 0.5).to(gpu)
+    loss = m.training_step((x, torch.tensor([32])), 0)
+    loss.backward()
+    opt.step()
+    ref = float(d["step0/loss"])
+    assert abs(float(loss) - ref) <= 0.02 * ref, (float(loss), ref)
+    assert torch.isfinite(m.flat.data).all()
