@@ -8,10 +8,16 @@
 // Layout: activations channels-last [B][H][W][D][C] (fp32 or bf16 storage), fp32 math;
 // weights fp32 [Cout][Cin][k][k][k] (reference layout, read straight from the param).
 //
-// v1 engine: direct convolution on the VALU with the per-tap weight slice staged in LDS
-// and broadcast to the wave; one thread = one output voxel x COT channels.  Circular
-// padding is index arithmetic (out[o] = sum_t W[t] x[(s*o + t - p) mod H]), so no padded
-// copy is ever materialised.
+// Engines
+//   pointwise (k = 1): a workgroup owns 256 consecutive voxels = one contiguous slab of
+//     memory; input channels are staged through LDS in chunks (prologue applied once per
+//     element), weights broadcast from LDS.  Forward and backward-data share the kernel.
+//   k > 1: direct convolution, one thread = one output voxel x COT channels, all taps'
+//     weights of the channel tile staged in LDS once.  Circular padding is index
+//     arithmetic (out[o] = sum_t W[t] x[(s*o + t - p) mod H]); no padded copy exists.
+//   weight gradient: thread = (row = (tap, ci), voxel sub-stream), g staged in LDS per
+//     chunk of one output row; partial sums leave each workgroup as fp32 atomics straight
+//     into the parameter-gradient buffer (no partial slabs, no finalize pass).
 #include "common.h"
 
 #include <algorithm>
@@ -41,39 +47,188 @@ static ConvArgs make_args(const vq3d_conv_desc *d, const float *pa, const float 
     return a;
 }
 
+// wrap into [0, n) for |i| < a few n (no integer division)
+__device__ __forceinline__ int wrap(int i, int n) {
+    while (i < 0) i += n;
+    while (i >= n) i -= n;
+    return i;
+}
+
 // forward tap: output coordinate o, kernel offset t -> input coordinate, or -1 if in zero padding
 __device__ __forceinline__ int fwd_index(int o, int t, int s, int p, int n, int circ) {
-    int i = o * s + t - p;
-    if (circ) {
-        i %= n;
-        return i < 0 ? i + n : i;
-    }
+    const int i = o * s + t - p;
+    if (circ) return wrap(i, n);
     return (i < 0 || i >= n) ? -1 : i;
 }
 
 // transposed tap: input coordinate i, kernel offset t -> output coordinate o with
-// fwd_index(o, t) == i, or -1 if none (unique when it exists: see DESIGN.md §conv)
+// fwd_index(o, t) == i, or -1 if none (unique when it exists: DESIGN.md §conv)
 __device__ __forceinline__ int bwd_index(int i, int t, int s, int p, int n_in, int n_out, int circ) {
     int r = i - t + p;
-    if (circ) {
-        r %= n_in;
-        if (r < 0) r += n_in;
-    } else if (r < 0) {
-        return -1;
+    if (circ) r = wrap(r, n_in);
+    else if (r < 0) return -1;
+    if (s == 2) {
+        if (r & 1) return -1;
+        r >>= 1;
+    } else if (s != 1) {
+        if (r % s) return -1;
+        r /= s;
     }
-    if (r % s) return -1;
-    r /= s;
     return r < n_out ? r : -1;
 }
 
-// ============================================================================ forward
+__device__ __forceinline__ void atomic_add_f(float *p, float v) {
+    if (p) atomicAdd(p, v);
+}
+
+// ============================================================================ pointwise
+constexpr int kPwSeg = 256;  // voxels per workgroup
+constexpr int kPwCC = 32;    // input channels per LDS chunk
+
+// DGRAD = false: y[v, o] = epi( sum_i W[o][i] * pro(x[v, i]) )          (i over Cin + Cin2)
+// DGRAD = true : gx[v, i] = dgrad_epi( gscale * sum_o W[o][i] * g[v, o] ) (o over Cout)
+template <typename T, int COT, bool DGRAD>
+__global__ __launch_bounds__(256) void k_pw(ConvArgs a, const T *__restrict__ in, const T *__restrict__ in2,
+                                           const float *__restrict__ w, const float *__restrict__ e_scale,
+                                           const float *__restrict__ e_bias, const float *__restrict__ e_cbias,
+                                           const T *__restrict__ res, int res_up2, int post_elu,
+                                           const T *__restrict__ aux, const T *__restrict__ addend,
+                                           T *__restrict__ out, T *__restrict__ out2, float *dpre, float *dpost) {
+    __shared__ float xs[kPwSeg][kPwCC + 1];
+    __shared__ __attribute__((aligned(16))) float ws[kPwCC][COT];
+    __shared__ float red[8];
+    const int Ct = a.Cin + a.Cin2;
+    const int nin = DGRAD ? a.Cout : Ct;    // channels read
+    const int nout = DGRAD ? Ct : a.Cout;   // channels written
+    const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
+    const int64_t v0 = int64_t(blockIdx.x) * kPwSeg;
+    const int nv = int(min<int64_t>(kPwSeg, nvox - v0));
+    const int o0 = blockIdx.y * COT;
+    const Prologue pro = make_prologue(a.pro_kind, a.pro_a, DGRAD ? nullptr : a.pro_b);
+    const int tid = threadIdx.x;
+
+    float acc[COT];
+#pragma unroll
+    for (int c = 0; c < COT; ++c) acc[c] = 0.f;
+
+    for (int c0 = 0; c0 < nin; c0 += kPwCC) {
+        const int cc = min(kPwCC, nin - c0);
+        __syncthreads();
+        // cooperative, coalesced staging of the [nv][cc] sub-block (rows contiguous when cc == nin)
+        for (int e = tid; e < nv * cc; e += 256) {
+            const int vv = e / cc, c = e - vv * cc;
+            const int ch = c0 + c;
+            float val;
+            if (DGRAD) {
+                val = ld(in + (v0 + vv) * a.Cout + ch);
+            } else if (ch < a.Cin) {
+                val = pro.apply(ld(in + (v0 + vv) * a.Cin + ch));
+            } else {
+                val = pro.apply(ld(in2 + (v0 + vv) * a.Cin2 + (ch - a.Cin)));
+            }
+            xs[vv][c] = val;
+        }
+        for (int e = tid; e < cc * COT; e += 256) {
+            const int c = e / COT, j = e - c * COT;
+            const int oc = o0 + j, ic = c0 + c;
+            float wv = 0.f;
+            if (oc < nout) wv = DGRAD ? w[int64_t(ic) * Ct + oc] : w[int64_t(oc) * Ct + ic];
+            ws[c][j] = wv;
+        }
+        __syncthreads();
+        if (tid < nv) {
+            for (int c = 0; c < cc; ++c) {
+                const float xv = xs[tid][c];
+#pragma unroll
+                for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, ws[c][j], acc[j]);
+            }
+        }
+    }
+
+    const int64_t v = v0 + tid;
+    if (!DGRAD) {
+        if (tid >= nv) return;
+        const float sc = e_scale ? *e_scale : 1.f;
+        const float bi = e_bias ? *e_bias : 0.f;
+        int h0 = 0, h1 = 0, w0 = 0, w1 = 0, d0 = 0, d1 = 0, b = 0;
+        float lh = 0.f, lw = 0.f, ldd = 0.f;
+        const int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
+        if (res && res_up2) {
+            int64_t t = v;
+            const int od = int(t % a.oD); t /= a.oD;
+            const int ow = int(t % a.oW); t /= a.oW;
+            const int oh = int(t % a.oH);
+            b = int(t / a.oH);
+            up_coeff(oh, rH, h0, h1, lh);
+            up_coeff(ow, rW, w0, w1, lw);
+            up_coeff(od, rD, d0, d1, ldd);
+        }
+        T *yp = out + v * a.Cout;
+#pragma unroll
+        for (int j = 0; j < COT; ++j) {
+            const int co = o0 + j;
+            if (co >= a.Cout) break;
+            float val = acc[j];
+            if (e_scale) val = val * sc;
+            if (e_bias) val = val + bi;
+            if (e_cbias) val = val + e_cbias[co];
+            if (res) {
+                if (!res_up2) {
+                    val = val + ld(res + v * a.Cout + co);
+                } else {
+                    auto R = [&](int hh, int ww, int dd) {
+                        return ld(res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.Cout + co);
+                    };
+                    val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
+                                              lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
+                                 lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
+                                       lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1))));
+                }
+            }
+            if (post_elu) val = elu(val);
+            st(yp + co, val);
+        }
+    } else {
+        float pre = 0.f, post = 0.f;
+        if (tid < nv) {
+            const float gs = e_scale ? *e_scale : 1.f;  // gscale
+#pragma unroll
+            for (int j = 0; j < COT; ++j) {
+                const int ci = o0 + j;
+                if (ci >= Ct) break;
+                float val = acc[j];
+                if (e_scale) val = val * gs;
+                if (ci < a.Cin) {
+                    const int64_t o = v * a.Cin + ci;
+                    pre += val;
+                    if (aux && pro.kind == VQ3D_PRO_ELU_ADD) val = val * pro.deriv(ld(aux + o));
+                    post += val;
+                    if (addend) val = val + ld(addend + o);
+                    st(out + o, val);
+                } else {
+                    st(out2 + v * a.Cin2 + (ci - a.Cin), val);
+                }
+            }
+        }
+        if (dpre || dpost) {
+            pre = block_sum<float, 256>(pre, red);
+            post = block_sum<float, 256>(post, red + 4);
+            if (tid == 0) {
+                atomic_add_f(dpre, pre);
+                atomic_add_f(dpost, post);
+            }
+        }
+    }
+}
+
+// ============================================================================ forward, k > 1
 template <typename T, int COT>
 __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restrict__ x, const T *__restrict__ x2,
                                                  const float *__restrict__ w, const float *__restrict__ e_scale,
                                                  const float *__restrict__ e_bias, const float *__restrict__ e_cbias,
-                                                 const T *__restrict__ res, int res_up2, int post_elu,
+                                                 const T *__restrict__ res, int res_up2, int post_elu, int all_taps,
                                                  T *__restrict__ y) {
-    extern __shared__ __attribute__((aligned(16))) float wsh[];  // [Ct][COT]
+    extern __shared__ __attribute__((aligned(16))) float wsh[];  // [taps][Ct][COT]
     const int Ct = a.Cin + a.Cin2;
     const int K3 = a.k * a.k * a.k;
     const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
@@ -92,35 +247,52 @@ __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restric
 #pragma unroll
     for (int c = 0; c < COT; ++c) acc[c] = 0.f;
 
-    for (int tap = 0; tap < K3; ++tap) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < Ct * COT; i += 256) {
-            const int ci = i / COT, c = i - ci * COT;
+    if (all_taps) {
+        for (int i = threadIdx.x; i < K3 * Ct * COT; i += 256) {
+            const int c = i % COT, r = i / COT, ci = r % Ct, tap = r / Ct;
             const int co = co0 + c;
             wsh[i] = co < a.Cout ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
         }
         __syncthreads();
-        if (v >= nvox) continue;
-        const int kd = tap % a.k, kw = (tap / a.k) % a.k, kh = tap / (a.k * a.k);
+    }
+    int tap = 0;
+    for (int kh = 0; kh < a.k; ++kh) {
         const int ih = fwd_index(oh, kh, a.s, a.p, a.iH, a.circ);
-        const int iw = fwd_index(ow, kw, a.s, a.p, a.iW, a.circ);
-        const int id = fwd_index(od, kd, a.s, a.p, a.iD, a.circ);
-        if ((ih | iw | id) < 0) continue;
-        const int64_t pos = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id;
-        const T *xp = x + pos * a.Cin;
-        for (int ci = 0; ci < a.Cin; ++ci) {
-            const float xv = pro.apply(ld(xp + ci));
-            const float *wr = wsh + ci * COT;
+        for (int kw = 0; kw < a.k; ++kw) {
+            const int iw = fwd_index(ow, kw, a.s, a.p, a.iW, a.circ);
+            for (int kd = 0; kd < a.k; ++kd, ++tap) {
+                const float *wt = wsh;
+                if (all_taps) {
+                    wt = wsh + tap * Ct * COT;
+                } else {
+                    __syncthreads();
+                    for (int i = threadIdx.x; i < Ct * COT; i += 256) {
+                        const int ci = i / COT, c = i - ci * COT;
+                        const int co = co0 + c;
+                        wsh[i] = co < a.Cout ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
+                    }
+                    __syncthreads();
+                }
+                if (v >= nvox) continue;
+                const int id = fwd_index(od, kd, a.s, a.p, a.iD, a.circ);
+                if ((ih | iw | id) < 0) continue;
+                const int64_t pos = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id;
+                const T *xp = x + pos * a.Cin;
+                for (int ci = 0; ci < a.Cin; ++ci) {
+                    const float xv = pro.apply(ld(xp + ci));
+                    const float *wr = wt + ci * COT;
 #pragma unroll
-            for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
-        }
-        if (a.Cin2) {
-            const T *xq = x2 + pos * a.Cin2;
-            for (int ci = 0; ci < a.Cin2; ++ci) {
-                const float xv = pro.apply(ld(xq + ci));
-                const float *wr = wsh + (a.Cin + ci) * COT;
+                    for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
+                }
+                if (a.Cin2) {
+                    const T *xq = x2 + pos * a.Cin2;
+                    for (int ci = 0; ci < a.Cin2; ++ci) {
+                        const float xv = pro.apply(ld(xq + ci));
+                        const float *wr = wt + (a.Cin + ci) * COT;
 #pragma unroll
-                for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
+                        for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
+                    }
+                }
             }
         }
     }
@@ -128,10 +300,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restric
     const float sc = e_scale ? *e_scale : 1.f;
     const float bi = e_bias ? *e_bias : 0.f;
     T *yp = y + v * a.Cout;
-    // residual on the half grid, upsampled on the fly: 8-point trilinear stencil
     int h0 = 0, h1 = 0, w0 = 0, w1 = 0, d0 = 0, d1 = 0;
     float lh = 0.f, lw = 0.f, ldd = 0.f;
-    int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
+    const int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
     if (res && res_up2) {
         up_coeff(oh, rH, h0, h1, lh);
         up_coeff(ow, rW, w0, w1, lw);
@@ -152,11 +323,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restric
                 auto R = [&](int hh, int ww, int dd) {
                     return ld(res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.Cout + co);
                 };
-                const float r = (1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
-                                              lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
-                                lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
-                                      lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1)));
-                val = val + r;
+                val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
+                                          lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
+                             lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
+                                   lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1))));
             }
         }
         if (post_elu) val = elu(val);
@@ -164,15 +334,13 @@ __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restric
     }
 }
 
-// ============================================================================ backward data
-// thread = one input voxel x CIT input channels; partial sums of the epilogue scalars
-// (pre, post) per block -> spart[block][2]
+// ============================================================================ backward data, k > 1
 template <typename T, int CIT>
 __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restrict__ g, const float *__restrict__ gscale,
                                                    const float *__restrict__ w, const T *__restrict__ aux,
-                                                   const T *__restrict__ addend, T *__restrict__ gx,
-                                                   T *__restrict__ gx2, float *__restrict__ spart) {
-    extern __shared__ __attribute__((aligned(16))) float wsh[];  // [Cout][CIT]
+                                                   const T *__restrict__ addend, int all_taps, T *__restrict__ gx,
+                                                   T *__restrict__ gx2, float *dpre, float *dpost) {
+    extern __shared__ __attribute__((aligned(16))) float wsh[];  // [taps][Cout][CIT]
     __shared__ float red[8];
     const int Ct = a.Cin + a.Cin2;
     const int K3 = a.k * a.k * a.k;
@@ -192,26 +360,43 @@ __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restr
 #pragma unroll
     for (int c = 0; c < CIT; ++c) acc[c] = 0.f;
 
-    for (int tap = 0; tap < K3; ++tap) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < a.Cout * CIT; i += 256) {
-            const int co = i / CIT, c = i - co * CIT;
+    if (all_taps) {
+        for (int i = threadIdx.x; i < K3 * a.Cout * CIT; i += 256) {
+            const int c = i % CIT, r = i / CIT, co = r % a.Cout, tap = r / a.Cout;
             const int ci = ci0 + c;
             wsh[i] = ci < Ct ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
         }
         __syncthreads();
-        if (v >= nvox) continue;
-        const int kd = tap % a.k, kw = (tap / a.k) % a.k, kh = tap / (a.k * a.k);
+    }
+    int tap = 0;
+    for (int kh = 0; kh < a.k; ++kh) {
         const int oh = bwd_index(ih, kh, a.s, a.p, a.iH, a.oH, a.circ);
-        const int ow = bwd_index(iw, kw, a.s, a.p, a.iW, a.oW, a.circ);
-        const int od = bwd_index(id, kd, a.s, a.p, a.iD, a.oD, a.circ);
-        if ((oh | ow | od) < 0) continue;
-        const T *gp = g + (((int64_t(b) * a.oH + oh) * a.oW + ow) * a.oD + od) * a.Cout;
-        for (int co = 0; co < a.Cout; ++co) {
-            const float gv = ld(gp + co);
-            const float *wr = wsh + co * CIT;
+        for (int kw = 0; kw < a.k; ++kw) {
+            const int ow = bwd_index(iw, kw, a.s, a.p, a.iW, a.oW, a.circ);
+            for (int kd = 0; kd < a.k; ++kd, ++tap) {
+                const float *wt = wsh;
+                if (all_taps) {
+                    wt = wsh + tap * a.Cout * CIT;
+                } else {
+                    __syncthreads();
+                    for (int i = threadIdx.x; i < a.Cout * CIT; i += 256) {
+                        const int co = i / CIT, c = i - co * CIT;
+                        const int ci = ci0 + c;
+                        wsh[i] = ci < Ct ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
+                    }
+                    __syncthreads();
+                }
+                if (v >= nvox) continue;
+                const int od = bwd_index(id, kd, a.s, a.p, a.iD, a.oD, a.circ);
+                if ((oh | ow | od) < 0) continue;
+                const T *gp = g + (((int64_t(b) * a.oH + oh) * a.oW + ow) * a.oD + od) * a.Cout;
+                for (int co = 0; co < a.Cout; ++co) {
+                    const float gv = ld(gp + co);
+                    const float *wr = wt + co * CIT;
 #pragma unroll
-            for (int c = 0; c < CIT; ++c) acc[c] = fmaf(gv, wr[c], acc[c]);
+                    for (int c = 0; c < CIT; ++c) acc[c] = fmaf(gv, wr[c], acc[c]);
+                }
+            }
         }
     }
     float pre = 0.f, post = 0.f;
@@ -235,151 +420,120 @@ __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restr
             }
         }
     }
-    pre = block_sum<float, 256>(pre, red);
-    post = block_sum<float, 256>(post, red + 4);
-    if (threadIdx.x == 0) {
-        const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-        spart[2 * blk] = pre;
-        spart[2 * blk + 1] = post;
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            atomic_add_f(dpre, pre);
+            atomic_add_f(dpost, post);
+        }
     }
 }
 
 // ============================================================================ backward weight
-// Grid: x = voxel chunks, y = row tiles (row = tap * Ct + ci), z = co tiles of COT.
-// Thread = (row, voxel sub-stream vs); g for a chunk of voxels is staged in LDS and
-// broadcast.  Output: wpart[bx][co][ci][tap] (fp32 partial slab of chunk bx), gpart[bx][co].
+// Grid: x = voxel chunks, y = row tiles (row = tap * Ct + ci, R rows per workgroup),
+// z = co tiles of COT.  Thread = (row, voxel sub-stream vs), VS = 256 / R sub-streams.
+// Each chunk is a run of consecutive output voxels inside one D-row, so the voxel
+// coordinates advance without divisions.
 constexpr int kWgChunk = 64;
 
 template <typename T, int COT>
 __global__ __launch_bounds__(256) void k_conv_wgrad(ConvArgs a, const T *__restrict__ x, const T *__restrict__ x2,
-                                                   const T *__restrict__ g, int64_t vox_per_blk, int rows_per_wg,
-                                                   float *__restrict__ wpart, float *__restrict__ gpart) {
-    __shared__ float gsh[kWgChunk][COT];
+                                                   const T *__restrict__ g, int64_t rows_per_blk, int R,
+                                                   const float *__restrict__ w, const float *__restrict__ escale,
+                                                   float *dw, float *dscale, float *dbias, float *dcbias) {
+    __shared__ __attribute__((aligned(16))) float gsh[kWgChunk][COT];
     __shared__ float racc[256][COT + 1];
+    __shared__ float red[8];
     const int Ct = a.Cin + a.Cin2;
     const int K3 = a.k * a.k * a.k;
     const int Kt = Ct * K3;
-    const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
-    const int R = rows_per_wg, VS = 256 / rows_per_wg;
-    const int rl = threadIdx.x % R, vs = threadIdx.x / R;
+    const int VS = 256 / R;
+    const int tid = threadIdx.x;
+    const int rl = tid % R, vs = tid / R;
     const int row = blockIdx.y * R + rl;
     const int co0 = blockIdx.z * COT;
     const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
-    const bool active = row < Kt;
+    const bool active = vs < VS && row < Kt;
     const int tap = active ? row / Ct : 0, ci = active ? row - (row / Ct) * Ct : 0;
     const int kd = tap % a.k, kw = (tap / a.k) % a.k, kh = tap / (a.k * a.k);
     const bool second = ci >= a.Cin;
     const T *src = second ? x2 : x;
     const int srcC = second ? a.Cin2 : a.Cin;
     const int sci = second ? ci - a.Cin : ci;
+    const bool pointwise = a.k == 1 && a.s == 1 && a.p == 0;
 
     float acc[COT];
 #pragma unroll
     for (int c = 0; c < COT; ++c) acc[c] = 0.f;
-    float gsum = 0.f;  // thread c < COT of (blockIdx.y == 0) sums g[., co0 + c]
+    float gsum = 0.f;  // threads tid < COT of row tile 0 sum g[., co0 + tid]
 
-    const int64_t v_begin = int64_t(blockIdx.x) * vox_per_blk;
-    const int64_t v_end = min(nvox, v_begin + vox_per_blk);
-    for (int64_t v0 = v_begin; v0 < v_end; v0 += kWgChunk) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < kWgChunk * COT; i += 256) {
-            const int vv = i / COT, c = i - vv * COT;
-            const int64_t vg = v0 + vv;
-            gsh[vv][c] = (vg < v_end && co0 + c < a.Cout) ? ld(g + vg * a.Cout + co0 + c) : 0.f;
-        }
-        __syncthreads();
-        if (blockIdx.y == 0 && threadIdx.x < COT) {
-            for (int vv = 0; vv < kWgChunk; ++vv) gsum += gsh[vv][threadIdx.x];
-        }
-        if (!active) continue;
-        const int nv = int(min<int64_t>(kWgChunk, v_end - v0));
-        for (int vv = vs; vv < nv; vv += VS) {
-            int64_t t = v0 + vv;
-            const int od = int(t % a.oD); t /= a.oD;
-            const int ow = int(t % a.oW); t /= a.oW;
-            const int oh = int(t % a.oH);
-            const int b = int(t / a.oH);
-            const int ih = fwd_index(oh, kh, a.s, a.p, a.iH, a.circ);
-            const int iw = fwd_index(ow, kw, a.s, a.p, a.iW, a.circ);
-            const int id = fwd_index(od, kd, a.s, a.p, a.iD, a.circ);
-            if ((ih | iw | id) < 0) continue;
-            const float xv =
-                pro.apply(ld(src + (((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id) * srcC + sci));
+    const int64_t nrows = int64_t(a.B) * a.oH * a.oW;  // output D-rows
+    const int64_t r_begin = int64_t(blockIdx.x) * rows_per_blk;
+    const int64_t r_end = min(nrows, r_begin + rows_per_blk);
+    for (int64_t orow = r_begin; orow < r_end; ++orow) {
+        const int ow = int(orow % a.oW);
+        const int oh = int((orow / a.oW) % a.oH);
+        const int b = int(orow / (int64_t(a.oW) * a.oH));
+        const int ih = pointwise ? oh : fwd_index(oh, kh, a.s, a.p, a.iH, a.circ);
+        const int iw = pointwise ? ow : fwd_index(ow, kw, a.s, a.p, a.iW, a.circ);
+        const bool row_ok = (ih | iw) >= 0;
+        const T *srow = src + ((int64_t(b) * a.iH + (ih < 0 ? 0 : ih)) * a.iW + (iw < 0 ? 0 : iw)) * a.iD * srcC;
+        const int64_t gbase = orow * a.oD;
+        for (int d0 = 0; d0 < a.oD; d0 += kWgChunk) {
+            const int nv = min(kWgChunk, a.oD - d0);
+            __syncthreads();
+            for (int i = tid; i < kWgChunk * COT; i += 256) {
+                const int vv = i / COT, c = i - vv * COT;
+                gsh[vv][c] = (vv < nv && co0 + c < a.Cout) ? ld(g + (gbase + d0 + vv) * a.Cout + co0 + c) : 0.f;
+            }
+            __syncthreads();
+            if (blockIdx.y == 0 && tid < COT) {
+                for (int vv = 0; vv < nv; ++vv) gsum += gsh[vv][tid];
+            }
+            if (!active || !row_ok) continue;
+            for (int vv = vs; vv < nv; vv += VS) {
+                const int od = d0 + vv;
+                const int id = pointwise ? od : fwd_index(od, kd, a.s, a.p, a.iD, a.circ);
+                if (id < 0) continue;
+                const float xv = pro.apply(ld(srow + int64_t(id) * srcC + sci));
 #pragma unroll
-            for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, gsh[vv][c], acc[c]);
+                for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, gsh[vv][c], acc[c]);
+            }
         }
     }
-    // fixed-order reduction over the VS voxel sub-streams
+    // fixed-order reduction over the VS voxel sub-streams, then one atomic per entry
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < COT; ++c) racc[threadIdx.x][c] = acc[c];
+    for (int c = 0; c < COT; ++c) racc[tid][c] = acc[c];
     __syncthreads();
-    if (vs == 0 && active) {
+    const float sc = escale ? *escale : 1.f;
+    float wg = 0.f;
+    if (vs == 0 && row < Kt) {
         const int ncot = min(COT, a.Cout - co0);
         for (int c = 0; c < ncot; ++c) {
             float s = 0.f;
             for (int j = 0; j < VS; ++j) s += racc[j * R + rl][c];
-            wpart[(int64_t(blockIdx.x) * a.Cout + co0 + c) * Kt + int64_t(ci) * K3 + tap] = s;  // reference [co][ci][tap]
+            const int64_t e = (int64_t(co0 + c) * Ct + ci) * K3 + tap;  // reference [co][ci][tap]
+            if (dw) atomicAdd(dw + e, escale ? s * sc : s);
+            if (dscale) wg = fmaf(w[e], s, wg);
         }
-    }
-    if (blockIdx.y == 0 && threadIdx.x < COT && co0 + threadIdx.x < a.Cout)
-        gpart[int64_t(blockIdx.x) * a.Cout + co0 + threadIdx.x] = gsum;
-}
-
-// ============================================================================ finalize
-// one workgroup per 256 weight entries (or a single workgroup when dscale is requested)
-__global__ __launch_bounds__(256) void k_conv_finalize(int64_t E, int nbw, const float *__restrict__ wpart,
-                                                      const float *__restrict__ w, const float *__restrict__ escale,
-                                                      float *__restrict__ dw, float *__restrict__ dscale,
-                                                      int Cout, const float *__restrict__ gpart,
-                                                      float *__restrict__ dbias, float *__restrict__ dcbias,
-                                                      int nbd, const float *__restrict__ spart,
-                                                      float *__restrict__ dpre, float *__restrict__ dpost) {
-    __shared__ float red[8];
-    const float sc = escale ? *escale : 1.f;
-    float wg = 0.f;
-    const int64_t stride = int64_t(gridDim.x) * 256;
-    for (int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x; e < E; e += stride) {
-        float s = 0.f;
-        for (int j = 0; j < nbw; ++j) s += wpart[int64_t(j) * E + e];
-        if (dw) dw[e] += escale ? s * sc : s;
-        if (dscale) wg = fmaf(w[e], s, wg);
     }
     if (dscale) {
         wg = block_sum<float, 256>(wg, red);
-        if (threadIdx.x == 0) *dscale += wg;
+        if (tid == 0) atomicAdd(dscale, wg);
     }
-    if (blockIdx.x != 0) return;
-    // per-channel bias and the scalar epilogue bias (sum of g), fixed order
-    float tot = 0.f;
-    for (int co = threadIdx.x; co < Cout; co += 256) {
-        float s = 0.f;
-        for (int j = 0; j < nbw; ++j) s += gpart[int64_t(j) * Cout + co];
-        if (dcbias) dcbias[co] += s;
-        tot += s;
-    }
-    if (dbias) {
-        tot = block_sum<float, 256>(tot, red);
-        if (threadIdx.x == 0) *dbias += tot;
-    }
-    if (dpre || dpost) {
-        float p0 = 0.f, p1 = 0.f;
-        for (int j = threadIdx.x; j < nbd; j += 256) {
-            p0 += spart[2 * j];
-            p1 += spart[2 * j + 1];
-        }
-        p0 = block_sum<float, 256>(p0, red);
-        p1 = block_sum<float, 256>(p1, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) *dpre += p0;
-            if (dpost) *dpost += p1;
+    if (blockIdx.y == 0) {
+        if (dcbias && tid < COT && co0 + tid < a.Cout) atomicAdd(dcbias + co0 + tid, gsum);
+        if (dbias) {
+            const float t = block_sum<float, 256>(tid < COT && co0 + tid < a.Cout ? gsum : 0.f, red + 4);
+            if (tid == 0) atomicAdd(dbias, t);
         }
     }
 }
 
 // ============================================================================ host side
 static int pick_tile(int c) {
-    // tiles of at most 16 channels, sized to waste as little as possible
     const int ntiles = (c + 15) / 16;
     const int per = (c + ntiles - 1) / ntiles;
     static const int opts[] = {1, 2, 4, 8, 12, 16};
@@ -388,42 +542,7 @@ static int pick_tile(int c) {
     return 16;
 }
 
-struct BwdPlan {
-    int64_t nvox_out, nvox_in, E;
-    int Kt, rows_per_wg, ytiles, cot, ztiles, nbw, nbd, cit;
-    int64_t vox_per_blk;
-    size_t off_wpart, off_gpart, off_spart, bytes;
-};
-
-static BwdPlan plan_bwd(const vq3d_conv_desc *d) {
-    BwdPlan p;
-    const int Ct = d->cin + d->cin2;
-    const int K3 = d->kernel * d->kernel * d->kernel;
-    p.nvox_out = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
-    p.nvox_in = int64_t(d->batch) * d->in_h * d->in_w * d->in_d;
-    p.Kt = Ct * K3;
-    p.E = int64_t(d->cout) * p.Kt;
-    int vsplit = 1;
-    while (vsplit * 2 * p.Kt <= 256 && vsplit < 256) vsplit *= 2;
-    p.rows_per_wg = 256 / vsplit;
-    p.ytiles = (p.Kt + p.rows_per_wg - 1) / p.rows_per_wg;
-    p.cot = pick_tile(d->cout);
-    p.ztiles = (d->cout + p.cot - 1) / p.cot;
-    const int64_t tiles = int64_t(p.ytiles) * p.ztiles;
-    int64_t nbw = std::max<int64_t>(1, 1024 / tiles);
-    nbw = std::min<int64_t>(nbw, (p.nvox_out + kWgChunk - 1) / kWgChunk);
-    p.vox_per_blk = (p.nvox_out + nbw - 1) / nbw;
-    p.vox_per_blk = (p.vox_per_blk + kWgChunk - 1) / kWgChunk * kWgChunk;
-    p.nbw = int((p.nvox_out + p.vox_per_blk - 1) / p.vox_per_blk);
-    p.cit = pick_tile(Ct);
-    p.nbd = int(((p.nvox_in + 255) / 256) * ((Ct + p.cit - 1) / p.cit));
-    p.off_wpart = 0;
-    p.off_gpart = p.off_wpart + size_t(p.nbw) * p.E * 4;
-    p.off_spart = p.off_gpart + size_t(p.nbw) * d->cout * 4;
-    p.bytes = p.off_spart + size_t(p.nbd) * 2 * 4;
-    p.bytes = (p.bytes + 255) / 256 * 256;
-    return p;
-}
+static bool is_pointwise(const vq3d_conv_desc *d) { return d->kernel == 1 && d->stride == 1 && d->pad == 0; }
 
 static int validate(const vq3d_conv_desc *d) {
     if (!d) return fail("conv: null descriptor");
@@ -443,8 +562,12 @@ static int validate(const vq3d_conv_desc *d) {
     if (d->pro_kind < 0 || d->pro_kind > 2) return fail("conv: bad prologue");
     if ((int64_t(d->cin) + d->cin2) * 16 * 4 > 64 * 1024) return fail("conv: too many input channels");
     if (int64_t(d->cout) * 16 * 4 > 64 * 1024) return fail("conv: too many output channels");
+    if (int64_t(d->batch) * d->in_h * d->in_w * d->in_d * (d->cin + d->cin2) > (int64_t(1) << 40))
+        return fail("conv: tensor too large");
     return 0;
 }
+
+constexpr size_t kAllTapsLds = 48 * 1024;
 
 template <typename T>
 static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w, const float *pa,
@@ -452,18 +575,32 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
     ConvArgs a = make_args(d, pa, pb);
     const int cot = pick_tile(d->cout);
     const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
-    dim3 grid(unsigned((nvox + 255) / 256), unsigned((d->cout + cot - 1) / cot));
-    const size_t lds = size_t(d->cin + d->cin2) * cot * 4;
     const float *es = epi ? epi->scale : nullptr;
     const float *eb = epi ? epi->bias : nullptr;
     const float *ec = epi ? epi->cbias : nullptr;
     const T *res = epi ? static_cast<const T *>(epi->residual) : nullptr;
     const int rup = epi ? epi->residual_up2 : 0, pe = epi ? epi->post_elu : 0;
     if (res && rup && ((d->out_h | d->out_w | d->out_d) & 1)) return fail("conv: residual_up2 needs even output");
-#define L(C)                                                                                              \
-    case C:                                                                                               \
-        k_conv_fwd<T, C><<<grid, 256, lds, s>>>(a, (const T *)x, (const T *)x2, w, es, eb, ec, res, rup, pe, \
-                                                (T *)y);                                                  \
+    if (is_pointwise(d)) {
+        dim3 grid(unsigned((nvox + kPwSeg - 1) / kPwSeg), unsigned((d->cout + cot - 1) / cot));
+#define L(C)                                                                                                   \
+    case C:                                                                                                    \
+        k_pw<T, C, false><<<grid, 256, 0, s>>>(a, (const T *)x, (const T *)x2, w, es, eb, ec, res, rup, pe,      \
+                                               nullptr, nullptr, (T *)y, nullptr, nullptr, nullptr);          \
+        break;
+        switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
+#undef L
+        return check_launch("conv3d_fwd(pointwise)");
+    }
+    const int Ct = d->cin + d->cin2, K3 = d->kernel * d->kernel * d->kernel;
+    const size_t all = size_t(K3) * Ct * cot * 4;
+    const int all_taps = all <= kAllTapsLds;
+    const size_t lds = all_taps ? all : size_t(Ct) * cot * 4;
+    dim3 grid(unsigned((nvox + 255) / 256), unsigned((d->cout + cot - 1) / cot));
+#define L(C)                                                                                                   \
+    case C:                                                                                                    \
+        k_conv_fwd<T, C><<<grid, 256, lds, s>>>(a, (const T *)x, (const T *)x2, w, es, eb, ec, res, rup, pe,     \
+                                                all_taps, (T *)y);                                             \
         break;
     switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
@@ -472,40 +609,68 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
 
 template <typename T>
 static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
-                        const float *pa, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2, void *ws,
-                        hipStream_t s) {
+                        const float *pa, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2, float *dpre,
+                        float *dpost, hipStream_t s) {
     ConvArgs a = make_args(d, pa, nullptr);
-    BwdPlan p = plan_bwd(d);
     const int Ct = d->cin + d->cin2;
-    dim3 grid(unsigned((p.nvox_in + 255) / 256), unsigned((Ct + p.cit - 1) / p.cit));
-    const size_t lds = size_t(d->cout) * p.cit * 4;
-    float *spart = reinterpret_cast<float *>(static_cast<char *>(ws) + p.off_spart);
+    const int cit = pick_tile(Ct);
+    const int64_t nvox = int64_t(d->batch) * d->in_h * d->in_w * d->in_d;
     const T *aux = epi ? static_cast<const T *>(epi->aux) : nullptr;
     const T *add = epi ? static_cast<const T *>(epi->addend) : nullptr;
-#define L(C)                                                                                            \
-    case C:                                                                                             \
-        k_conv_dgrad<T, C><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, aux, add, (T *)gx, (T *)gx2, \
-                                                  spart);                                               \
+    if (is_pointwise(d)) {
+        dim3 grid(unsigned((nvox + kPwSeg - 1) / kPwSeg), unsigned((Ct + cit - 1) / cit));
+#define L(C)                                                                                                  \
+    case C:                                                                                                   \
+        k_pw<T, C, true><<<grid, 256, 0, s>>>(a, (const T *)g, nullptr, w, gscale, nullptr, nullptr, nullptr, 0, \
+                                              0, aux, add, (T *)gx, (T *)gx2, dpre, dpost);                   \
         break;
-    switch (p.cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
+        switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
+#undef L
+        return check_launch("conv3d_bwd_data(pointwise)");
+    }
+    const int K3 = d->kernel * d->kernel * d->kernel;
+    const size_t all = size_t(K3) * d->cout * cit * 4;
+    const int all_taps = all <= kAllTapsLds;
+    const size_t lds = all_taps ? all : size_t(d->cout) * cit * 4;
+    dim3 grid(unsigned((nvox + 255) / 256), unsigned((Ct + cit - 1) / cit));
+#define L(C)                                                                                                  \
+    case C:                                                                                                   \
+        k_conv_dgrad<T, C><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, aux, add, all_taps, (T *)gx,     \
+                                                  (T *)gx2, dpre, dpost);                                     \
+        break;
+    switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
     return check_launch("conv3d_bwd_data");
 }
 
 template <typename T>
 static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pa,
-                        const float *pb, void *ws, hipStream_t s) {
+                        const float *pb, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
+                        float *dcbias, hipStream_t s) {
     ConvArgs a = make_args(d, pa, pb);
-    BwdPlan p = plan_bwd(d);
-    dim3 grid(unsigned(p.nbw), unsigned(p.ytiles), unsigned(p.ztiles));
-    float *wpart = reinterpret_cast<float *>(static_cast<char *>(ws) + p.off_wpart);
-    float *gpart = reinterpret_cast<float *>(static_cast<char *>(ws) + p.off_gpart);
+    const int Ct = d->cin + d->cin2;
+    const int K3 = d->kernel * d->kernel * d->kernel;
+    const int Kt = Ct * K3;
+    // rows per workgroup: all rows when they fit (voxel sub-streams fill the rest), else 256
+    const int R = Kt >= 256 ? 256 : (Kt > 128 ? Kt : std::max(1, Kt));
+    const int ytiles = (Kt + R - 1) / R;
+    const int cot = pick_tile(d->cout);
+    const int ztiles = (d->cout + cot - 1) / cot;
+    const int64_t nrows = int64_t(d->batch) * d->out_h * d->out_w;
+    const int64_t tiles = int64_t(ytiles) * ztiles;
+    // enough workgroups to fill the chip, each with >= ~64 output voxels of work
+    int64_t nbx = std::max<int64_t>(1, 2048 / tiles);
+    const int64_t min_rows = std::max<int64_t>(1, 64 / std::max(1, d->out_d));
+    nbx = std::min<int64_t>(nbx, (nrows + min_rows - 1) / min_rows);
+    const int64_t rows_per_blk = (nrows + nbx - 1) / nbx;
+    nbx = (nrows + rows_per_blk - 1) / rows_per_blk;
+    dim3 grid((unsigned)nbx, (unsigned)ytiles, (unsigned)ztiles);
 #define L(C)                                                                                                   \
     case C:                                                                                                    \
-        k_conv_wgrad<T, C><<<grid, 256, 0, s>>>(a, (const T *)x, (const T *)x2, (const T *)g, p.vox_per_blk,     \
-                                                p.rows_per_wg, wpart, gpart);                                  \
+        k_conv_wgrad<T, C><<<grid, 256, 0, s>>>(a, (const T *)x, (const T *)x2, (const T *)g, rows_per_blk, R,  \
+                                                w, escale, dw, dscale, dbias, dcbias);                         \
         break;
-    switch (p.cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
+    switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
     return check_launch("conv3d_bwd_weight");
 }
@@ -526,48 +691,31 @@ int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, cons
                                 : launch_fwd<bf16_t>(d, x, x2, w, pro_a, pro_b, epi, y, as_stream(stream));
 }
 
-size_t vq3d_conv3d_bwd_workspace_size(const vq3d_conv_desc *d) {
-    if (validate(d)) return 0;
-    return plan_bwd(d).bytes;
-}
-
 int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
-                         const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2, void *workspace,
-                         vq3d_stream_t stream) {
+                         const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2, float *dpro_pre,
+                         float *dpro_post, vq3d_stream_t stream) {
     if (int r = validate(d)) return r;
-    if (!g || !w || !gx || !workspace || (d->cin2 && !gx2)) return fail("conv3d_bwd_data: null pointer");
+    if (!g || !w || !gx || (d->cin2 && !gx2)) return fail("conv3d_bwd_data: null pointer");
     if (d->pro_kind != VQ3D_PRO_NONE && !pro_a) return fail("conv3d_bwd_data: prologue needs pro_a");
     if (d->pro_kind == VQ3D_PRO_ELU_ADD && (!epi || !epi->aux))
         return fail("conv3d_bwd_data: ELU prologue derivative needs epi->aux");
-    return d->dtype == VQ3D_F32
-               ? launch_dgrad<float>(d, g, gscale, w, pro_a, epi, gx, gx2, workspace, as_stream(stream))
-               : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, workspace, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    return d->dtype == VQ3D_F32 ? launch_dgrad<float>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s)
+                                : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s);
 }
 
-int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g,
-                           const float *pro_a, const float *pro_b, void *workspace, vq3d_stream_t stream) {
+int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
+                           const float *pro_b, const float *w, const float *epi_scale, float *dw, float *dscale,
+                           float *dbias, float *dcbias, vq3d_stream_t stream) {
     if (int r = validate(d)) return r;
-    if (!x || !g || !workspace || (d->cin2 && !x2)) return fail("conv3d_bwd_weight: null pointer");
+    if (!x || !g || (d->cin2 && !x2)) return fail("conv3d_bwd_weight: null pointer");
     if (d->pro_kind != VQ3D_PRO_NONE && !pro_a) return fail("conv3d_bwd_weight: prologue needs pro_a");
     if (d->pro_kind == VQ3D_PRO_ELU_ADD && !pro_b) return fail("conv3d_bwd_weight: ELU prologue needs pro_b");
-    return d->dtype == VQ3D_F32 ? launch_wgrad<float>(d, x, x2, g, pro_a, pro_b, workspace, as_stream(stream))
-                                : launch_wgrad<bf16_t>(d, x, x2, g, pro_a, pro_b, workspace, as_stream(stream));
-}
-
-int vq3d_conv3d_bwd_finalize(const vq3d_conv_desc *d, const float *w, const float *epi_scale, const void *workspace,
-                             float *dw, float *dscale, float *dbias, float *dcbias, float *dpro_pre,
-                             float *dpro_post, vq3d_stream_t stream) {
-    if (int r = validate(d)) return r;
-    if (!workspace || (dscale && (!w || !epi_scale))) return fail("conv3d_bwd_finalize: null pointer");
-    BwdPlan p = plan_bwd(d);
-    const char *ws = static_cast<const char *>(workspace);
-    unsigned nb = dscale ? 1u : unsigned(std::min<int64_t>((p.E + 255) / 256, 4096));
-    if (nb == 0) nb = 1;
-    k_conv_finalize<<<nb, 256, 0, as_stream(stream)>>>(
-        p.E, p.nbw, reinterpret_cast<const float *>(ws + p.off_wpart), w, epi_scale, dw, dscale, d->cout,
-        reinterpret_cast<const float *>(ws + p.off_gpart), dbias, dcbias, p.nbd,
-        reinterpret_cast<const float *>(ws + p.off_spart), dpro_pre, dpro_post);
-    return check_launch("conv3d_bwd_finalize");
+    if (dscale && (!w || !epi_scale)) return fail("conv3d_bwd_weight: dscale needs w and epi_scale");
+    hipStream_t s = as_stream(stream);
+    return d->dtype == VQ3D_F32
+               ? launch_wgrad<float>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias, dcbias, s)
+               : launch_wgrad<bf16_t>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias, dcbias, s);
 }
 
 }  // extern "C"

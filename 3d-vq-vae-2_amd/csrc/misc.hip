@@ -72,8 +72,8 @@ __device__ __forceinline__ int up_adjoint(int i, int n, int *js, float *ws) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B, int C, int H, int W, int D, int pk,
                                                const float *pa, const T *__restrict__ aux,
-                                               const T *__restrict__ addend, T *__restrict__ gx,
-                                               float *__restrict__ spart) {
+                                               const T *__restrict__ addend, T *__restrict__ gx, float *dpre,
+                                               float *dpost) {
     __shared__ float red[8];
     const int64_t n = int64_t(B) * H * W * D * C;
     const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -105,27 +105,13 @@ __global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B,
         if (addend) v += ld(addend + i);
         st(gx + i, v);
     }
-    pre = block_sum<float, 256>(pre, red);
-    post = block_sum<float, 256>(post, red + 4);
-    if (threadIdx.x == 0) {
-        spart[2 * blockIdx.x] = pre;
-        spart[2 * blockIdx.x + 1] = post;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_sum_pairs(const float *__restrict__ spart, int nb, float *dpre,
-                                                  float *dpost) {
-    __shared__ float red[8];
-    float p0 = 0.f, p1 = 0.f;
-    for (int j = threadIdx.x; j < nb; j += 256) {
-        p0 += spart[2 * j];
-        p1 += spart[2 * j + 1];
-    }
-    p0 = block_sum<float, 256>(p0, red);
-    p1 = block_sum<float, 256>(p1, red + 4);
-    if (threadIdx.x == 0) {
-        if (dpre) *dpre += p0;
-        if (dpost) *dpost += p1;
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
+        }
     }
 }
 
@@ -401,16 +387,11 @@ int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     return check_launch("upsample2x_fwd");
 }
 
-size_t vq3d_upsample2x_bwd_workspace_size(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd) {
-    const int64_t n = int64_t(batch) * h * w * dd * channels;
-    return size_t((n + 255) / 256) * 8 + 256;
-}
-
 int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
                         const void *gy, int32_t pro_kind, const float *pro_a, const vq3d_dgrad_epilogue *epi,
-                        void *gx, void *workspace, vq3d_stream_t stream) {
+                        void *gx, float *dpro_pre, float *dpro_post, vq3d_stream_t stream) {
     if (batch <= 0 || channels <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("upsample2x_bwd: bad sizes");
-    if (!gy || !gx || !workspace) return fail("upsample2x_bwd: null pointer");
+    if (!gy || !gx) return fail("upsample2x_bwd: null pointer");
     if (pro_kind == VQ3D_PRO_ELU_ADD && (!epi || !epi->aux || !pro_a))
         return fail("upsample2x_bwd: ELU prologue derivative needs aux and pro_a");
     const int64_t n = int64_t(batch) * h * w * dd * channels;
@@ -419,21 +400,12 @@ int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     const void *aux = epi ? epi->aux : nullptr, *add = epi ? epi->addend : nullptr;
     if (dtype == VQ3D_F32)
         k_up_bwd<float><<<nb, 256, 0, s>>>((const float *)gy, batch, channels, h, w, dd, pro_kind, pro_a,
-                                           (const float *)aux, (const float *)add, (float *)gx, (float *)workspace);
+                                           (const float *)aux, (const float *)add, (float *)gx, dpro_pre, dpro_post);
     else
         k_up_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)gy, batch, channels, h, w, dd, pro_kind, pro_a,
-                                            (const bf16_t *)aux, (const bf16_t *)add, (bf16_t *)gx,
-                                            (float *)workspace);
+                                            (const bf16_t *)aux, (const bf16_t *)add, (bf16_t *)gx, dpro_pre,
+                                            dpro_post);
     return check_launch("upsample2x_bwd");
-}
-
-int vq3d_upsample2x_bwd_finalize(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
-                                 const void *workspace, float *dpro_pre, float *dpro_post, vq3d_stream_t stream) {
-    if (!workspace) return fail("upsample2x_bwd_finalize: null workspace");
-    const int64_t n = int64_t(batch) * h * w * dd * channels;
-    k_sum_pairs<<<1, 256, 0, as_stream(stream)>>>((const float *)workspace, int((n + 255) / 256), dpro_pre,
-                                                  dpro_post);
-    return check_launch("upsample2x_bwd_finalize");
 }
 
 int64_t vq3d_cylinder_count(int32_t h, int32_t w) {

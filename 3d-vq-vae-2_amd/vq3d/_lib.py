@@ -36,14 +36,10 @@ class DgradEpilogue(ctypes.Structure):
 
 _SIGS = {
     "vq3d_conv3d_fwd": (c_int, [P, P, P, P, P, P, P, P, P]),
-    "vq3d_conv3d_bwd_workspace_size": (c_size, [P]),
-    "vq3d_conv3d_bwd_data": (c_int, [P, P, P, P, P, P, P, P, P, P]),
-    "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P]),
-    "vq3d_conv3d_bwd_finalize": (c_int, [P, P, P, P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_bwd_data": (c_int, [P, P, P, P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "vq3d_upsample2x_fwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P]),
-    "vq3d_upsample2x_bwd_workspace_size": (c_size, [c_int] * 5),
-    "vq3d_upsample2x_bwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P, P]),
-    "vq3d_upsample2x_bwd_finalize": (c_int, [c_int] * 5 + [P, P, P, P]),
+    "vq3d_upsample2x_bwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),
     "vq3d_vq_nearest": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, c_int, P, P, P, P]),
     "vq3d_vq_commit_loss": (c_int, [P, c_float, P, P]),

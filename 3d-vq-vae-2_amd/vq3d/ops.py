@@ -61,10 +61,7 @@ def conv_desc(dtype, b, cin, cin2, cout, h, w, d, geom, pro_kind):
         desc = L.ConvDesc(dtype=L.dtype_code(dtype), batch=b, cin=cin, cin2=cin2, cout=cout, in_h=h, in_w=w,
                           in_d=d, out_h=oh, out_w=ow, out_d=od, kernel=geom.k, stride=geom.s, pad=geom.p,
                           pad_mode=L.PAD_CIRCULAR if geom.circular else L.PAD_ZEROS, pro_kind=pro_kind)
-        ws = L.query("vq3d_conv3d_bwd_workspace_size", ctypes.byref(desc))
-        if ws == 0:
-            raise L.Vq3dError(f"invalid conv descriptor: {L.load().vq3d_last_error().decode()}")
-        r = (desc, (oh, ow, od), ws)
+        r = (desc, (oh, ow, od))
         _desc_cache[key] = r
     return r
 
@@ -85,7 +82,7 @@ def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, r
     cin2 = 0 if x2 is None else x2.shape[1]
     cout = w.shape[0]
     kind, pa, pb = pro_kind_of(pro)
-    desc, (oh, ow, od), _ = conv_desc(x.dtype, b, cin, cin2, cout, h, wd, d, geom, kind)
+    desc, (oh, ow, od) = conv_desc(x.dtype, b, cin, cin2, cout, h, wd, d, geom, kind)
     if w.shape[1] != cin + cin2 or w.shape[2] != geom.k:
         raise L.Vq3dError(f"weight {tuple(w.shape)} does not match conv ({cin}+{cin2} -> {cout}, k={geom.k})")
     y = out if out is not None else new_act(b, cout, oh, ow, od, x.dtype, x.device)
@@ -103,28 +100,24 @@ def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, r
 
 def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, addend=None, want_gx=True,
              dw=None, dscale=None, dbias=None, dcbias=None, dpro_pre=None, dpro_post=None, escale=None):
-    """Backward of conv_fwd: returns (gx, gx2); parameter gradients are ACCUMULATED into the
-    given fp32 buffers (dw: weight, dscale/dbias: epilogue scalars, dcbias: conv bias,
-    dpro_pre/dpro_post: prologue scalars (+b / +a of elu(x+a)+b, or a of x+a))."""
+    """Backward of conv_fwd: returns (gx, gx2); parameter gradients are ACCUMULATED (fp32
+    atomics) into the given buffers (dw: weight, dscale/dbias: epilogue scalars, dcbias: conv
+    bias, dpro_pre/dpro_post: prologue scalars (+b / +a of elu(x+a)+b, or a of x+a))."""
     x = as_cl(x)
     b, cin, h, wd, d = x.shape
     cin2 = 0 if x2 is None else x2.shape[1]
     kind, pa, pb = pro_kind_of(pro)
-    desc, _, wsb = conv_desc(x.dtype, b, cin, cin2, w.shape[0], h, wd, d, geom, kind)
-    ws = workspace(wsb, x.device)
+    desc, _ = conv_desc(x.dtype, b, cin, cin2, w.shape[0], h, wd, d, geom, kind)
     s = L.stream()
     gx = gx2 = None
-    need_partials = dpro_pre is not None or dpro_post is not None
-    if want_gx or need_partials:
+    if want_gx or dpro_pre is not None or dpro_post is not None:
         gx = new_act(b, cin, h, wd, d, x.dtype, x.device)
         gx2 = None if x2 is None else new_act(b, cin2, h, wd, d, x.dtype, x.device)
         epi = L.DgradEpilogue(aux=_p(aux), addend=_p(addend))
         L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), _p(gscale), L.ptr(w), _p(pa),
-               ctypes.byref(epi), L.ptr(gx), _p(gx2), L.ptr(ws), s)
-    L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb),
-           L.ptr(ws), s)
-    L.call("vq3d_conv3d_bwd_finalize", ctypes.byref(desc), L.ptr(w), _p(escale), L.ptr(ws), _p(dw),
-           _p(dscale), _p(dbias), _p(dcbias), _p(dpro_pre), _p(dpro_post), s)
+               ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), s)
+    L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb), L.ptr(w),
+           _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), s)
     return gx, gx2
 
 
@@ -143,13 +136,9 @@ def upsample2x_bwd(gy, src_shape, pro=None, aux=None, addend=None, dpro_pre=None
     b, c, h, w, d = src_shape
     kind, pa, _ = pro_kind_of(pro)
     gx = new_act(b, c, h, w, d, gy.dtype, gy.device)
-    ws = workspace(L.query("vq3d_upsample2x_bwd_workspace_size", b, c, h, w, d), gy.device)
     epi = L.DgradEpilogue(aux=_p(aux), addend=_p(addend))
-    s = L.stream()
     L.call("vq3d_upsample2x_bwd", L.dtype_code(gy), b, c, h, w, d, L.ptr(gy), kind, _p(pa), ctypes.byref(epi),
-           L.ptr(gx), L.ptr(ws), s)
-    if dpro_pre is not None or dpro_post is not None:
-        L.call("vq3d_upsample2x_bwd_finalize", b, c, h, w, d, L.ptr(ws), _p(dpro_pre), _p(dpro_post), s)
+           L.ptr(gx), _p(dpro_pre), _p(dpro_post), L.stream())
     return gx
 
 

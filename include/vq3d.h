@@ -58,7 +58,7 @@ typedef struct vq3d_conv_epilogue {
 
 /* Backward-data epilogue on the conv INPUT grid:
  *   v = acc;  pre += v;  v *= d/dx prologue(aux);  post += v;  v += addend;  store
- * pre/post are summed over every element into `scalar_partials` (see finalize). */
+ * pre / post are summed over every element (see vq3d_conv3d_bwd_data). */
 typedef struct vq3d_dgrad_epilogue {
     const void *aux;        /* forward input before the prologue (needed for ELU'), or NULL */
     const void *addend;     /* gradient added after the prologue derivative, or NULL */
@@ -69,47 +69,36 @@ int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, cons
                     const float *pro_a, const float *pro_b, const vq3d_conv_epilogue *epi,
                     void *y, vq3d_stream_t stream);
 
-/* Workspace (bytes) for the backward of one conv: weight-grad partial slabs + scalar partials. */
-size_t vq3d_conv3d_bwd_workspace_size(const vq3d_conv_desc *d);
-
 /* Gradient w.r.t. the input(s).  g = dL/dy (y grid, cout channels); gscale: device scalar
- * multiplying g (the PreAct `scale`) or NULL.  gx (and gx2 for input 2) receive the result. */
+ * multiplying g (the PreAct `scale`) or NULL.  gx (and gx2 for input 2) receive the result,
+ * with the dgrad epilogue applied.  The prologue-scalar gradients are ACCUMULATED (fp32
+ * atomics, one per workgroup) into dpro_pre (+= sum of v before the prologue derivative:
+ * d/db of elu(x+a)+b, or d/da of x+a) and dpro_post (+= sum after it: d/da of elu(x+a)+b);
+ * either may be NULL. */
 int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
                          const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2,
-                         void *workspace, vq3d_stream_t stream);
+                         float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
 
-/* Gradient w.r.t. the weight: G[co,ci,t] = sum_v g[v,co] * prologue(x)[nbr(v,t),ci], written
- * as fp32 partial slabs into `workspace` (same workspace as bwd_data, disjoint region). */
+/* Gradient w.r.t. the weight and the forward-epilogue parameters, ACCUMULATED (+=) with fp32
+ * atomics into the fp32 gradient buffers (any may be NULL):
+ *   dw     += scale * G,  G[co,ci,t] = sum_v g[v,co] * prologue(x)[nbr(v,t),ci]
+ *   dscale += sum(W * G)     (epilogue `scale`; needs w and epi_scale)
+ *   dbias  += sum(g)         (epilogue scalar bias)
+ *   dcbias += sum_v g[v,co]  (nn.Conv3d bias)
+ * Atomic accumulation makes the last bits order-dependent (like cuDNN's wgrad). */
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g,
-                           const float *pro_a, const float *pro_b, void *workspace,
-                           vq3d_stream_t stream);
-
-/* Reduce the partial slabs in a fixed order (deterministic) and ACCUMULATE (+=) into the
- * fp32 gradient buffers (any may be NULL):
- *   dw      += scale * G            (scale = *epi_scale, or 1)
- *   dscale  += sum(W * G)           (d/d scale of the forward epilogue)
- *   dbias   += sum(g)               (forward epilogue scalar bias)
- *   dcbias  += sum_v g[v, co]       (nn.Conv3d bias)
- *   dpro_pre += sum(pre), dpro_post += sum(post)   (prologue scalars: see bwd_data) */
-int vq3d_conv3d_bwd_finalize(const vq3d_conv_desc *d, const float *w, const float *epi_scale,
-                             const void *workspace, float *dw, float *dscale, float *dbias,
-                             float *dcbias, float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
+                           const float *pro_a, const float *pro_b, const float *w, const float *epi_scale,
+                           float *dw, float *dscale, float *dbias, float *dcbias, vq3d_stream_t stream);
 
 /* --- trilinear x2 upsample, align_corners=False (nn.Upsample in ResizeConv3D, layers.py:591-597) --- */
 int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
                         const void *x, int32_t pro_kind, const float *pro_a, const float *pro_b, void *y,
                         vq3d_stream_t stream);
 /* Adjoint of the upsample on the source grid, with the bwd_data epilogue (prologue
- * derivative w.r.t. aux, addend) and pre/post scalar partials in `workspace`
- * (vq3d_upsample2x_bwd_workspace_size bytes), reduced by vq3d_reduce_scalars. */
-size_t vq3d_upsample2x_bwd_workspace_size(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd);
+ * derivative w.r.t. aux, addend) and the same dpro_pre / dpro_post accumulation. */
 int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
                         const void *gy, int32_t pro_kind, const float *pro_a, const vq3d_dgrad_epilogue *epi,
-                        void *gx, void *workspace, vq3d_stream_t stream);
-/* sum the pre/post partials written by vq3d_upsample2x_bwd into dpro_pre / dpro_post (+=) */
-int vq3d_upsample2x_bwd_finalize(int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
-                                 const void *workspace, float *dpro_pre, float *dpro_post,
-                                 vq3d_stream_t stream);
+                        void *gx, float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
 
 /* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
 /* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),

@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol():
     from vq3d import _lib as L
     lib = L.load()
     syms = header_symbols()
-    assert len(syms) >= 30
+    assert len(syms) >= 25
     for s in syms:
         assert hasattr(lib, s), s
     # the python binding declares exactly the header's entry points
@@ -37,13 +37,12 @@ def test_library_exports_every_header_symbol():
 def test_conv_descriptor_validation_and_workspace():
     from vq3d import _lib as L
     from vq3d import ops
-    desc, out, ws = ops.conv_desc(torch.float32, 1, 9, 0, 9, 128, 128, 32, ops.ConvGeom(3, 1, 1, True), 2)
-    assert out == (128, 128, 32) and ws > 0
-    desc, out, ws = ops.conv_desc(torch.bfloat16, 1, 4, 0, 4, 512, 512, 128, ops.ConvGeom(4, 2, 1, True), 2)
+    desc, out = ops.conv_desc(torch.float32, 1, 9, 0, 9, 128, 128, 32, ops.ConvGeom(3, 1, 1, True), 2)
+    assert out == (128, 128, 32)
+    desc, out = ops.conv_desc(torch.bfloat16, 1, 4, 0, 4, 512, 512, 128, ops.ConvGeom(4, 2, 1, True), 2)
     assert out == (256, 256, 64)
     bad = L.ConvDesc(dtype=0, batch=1, cin=4, cin2=0, cout=4, in_h=8, in_w=8, in_d=8, out_h=9, out_w=8, out_d=8,
                      kernel=3, stride=1, pad=1, pad_mode=1, pro_kind=0)
-    assert L.query("vq3d_conv3d_bwd_workspace_size", ctypes.byref(bad)) == 0
     rc = L.load().vq3d_conv3d_fwd(ctypes.byref(bad), None, None, None, None, None, None, None, None)
     assert rc < 0 and b"output size" in L.load().vq3d_last_error()
     # a null pointer is refused before any launch
