@@ -43,6 +43,25 @@ struct Prologue {
     }
 };
 
+// derivative of the activation in front of a conv, applied in backward-data epilogues
+// (vq3d_dgrad_epilogue): mode 1 from the pre-prologue input (elu'(aux + a)); mode 2 from an
+// activated tensor t = elu(z) + b: elu'(z) = t - b > 0 ? 1 : t - b + 1.
+struct ActDeriv {
+    int mode;
+    float p;
+    __device__ __forceinline__ float operator()(float aux) const {
+        if (mode == 1) return elu_grad(aux + p);
+        const float z1 = aux - p;
+        return z1 > 0.f ? 1.f : z1 + 1.f;
+    }
+};
+
+__device__ __forceinline__ float epi_act(int act, float v, float a, float b) {
+    if (act == VQ3D_ACT_ELU) return elu(v);
+    if (act == VQ3D_ACT_ELU_AFFINE) return elu(v + a) + b;
+    return v;
+}
+
 __device__ __forceinline__ Prologue make_prologue(int kind, const float *a, const float *b) {
     Prologue p;
     p.kind = kind;

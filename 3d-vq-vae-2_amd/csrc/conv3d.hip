@@ -81,19 +81,117 @@ __device__ __forceinline__ void atomic_add_f(float *p, float v) {
     if (p) atomicAdd(p, v);
 }
 
+// forward epilogue (vq3d_conv_epilogue), by value
+template <typename T>
+struct FwdEpi {
+    const float *scale, *bias, *cbias;
+    const T *res;
+    int res_up2, act;
+    const float *act_a, *act_b;
+};
+
+// backward-data epilogue (vq3d_dgrad_epilogue) resolved on the host: mode 0 none,
+// 1 elu'(aux + *p) (pre-prologue input), 2 from activated aux with offset *p
+template <typename T>
+struct BwdEpi {
+    const T *aux;
+    int mode;
+    const float *p;
+    const T *addend;
+};
+
+template <typename T>
+__device__ __forceinline__ ActDeriv make_deriv(const BwdEpi<T> &e) {
+    ActDeriv d;
+    d.mode = e.aux ? e.mode : 0;
+    d.p = (d.mode && e.p) ? *e.p : 0.f;
+    return d;
+}
+
+// y[v, co] for one voxel's accumulators (shared by the pointwise and the k > 1 forward)
+template <typename T, int COT>
+__device__ __forceinline__ void fwd_epilogue(const ConvArgs &a, const FwdEpi<T> &e, const float (&acc)[COT],
+                                             int64_t v, int co0, T *__restrict__ y) {
+    const float sc = e.scale ? *e.scale : 1.f;
+    const float bi = e.bias ? *e.bias : 0.f;
+    const float aa = e.act_a ? *e.act_a : 0.f, ab = e.act_b ? *e.act_b : 0.f;
+    int h0 = 0, h1 = 0, w0 = 0, w1 = 0, d0 = 0, d1 = 0, b = 0;
+    float lh = 0.f, lw = 0.f, ldd = 0.f;
+    const int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
+    if (e.res && e.res_up2) {
+        int64_t t = v;
+        const int od = int(t % a.oD); t /= a.oD;
+        const int ow = int(t % a.oW); t /= a.oW;
+        const int oh = int(t % a.oH);
+        b = int(t / a.oH);
+        up_coeff(oh, rH, h0, h1, lh);
+        up_coeff(ow, rW, w0, w1, lw);
+        up_coeff(od, rD, d0, d1, ldd);
+    }
+    T *yp = y + v * a.Cout;
+#pragma unroll
+    for (int c = 0; c < COT; ++c) {
+        const int co = co0 + c;
+        if (co >= a.Cout) break;
+        float val = acc[c];
+        if (e.scale) val = val * sc;
+        if (e.bias) val = val + bi;
+        if (e.cbias) val = val + e.cbias[co];
+        if (e.res) {
+            if (!e.res_up2) {
+                val = val + ld(e.res + v * a.Cout + co);
+            } else {
+                auto R = [&](int hh, int ww, int dd) {
+                    return ld(e.res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.Cout + co);
+                };
+                val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
+                                          lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
+                             lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
+                                   lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1))));
+            }
+        }
+        st(yp + co, epi_act(e.act, val, aa, ab));
+    }
+}
+
+// gx[v, ci] for one voxel's accumulators; returns the (pre, post) contributions
+template <typename T, int CIT>
+__device__ __forceinline__ void bwd_epilogue(const ConvArgs &a, const BwdEpi<T> &e, const ActDeriv &dv, float gs,
+                                             bool has_gs, const float (&acc)[CIT], int64_t v, int ci0,
+                                             T *__restrict__ gx, T *__restrict__ gx2, float &pre, float &post) {
+    const int Ct = a.Cin + a.Cin2;
+#pragma unroll
+    for (int c = 0; c < CIT; ++c) {
+        const int ci = ci0 + c;
+        if (ci >= Ct) break;
+        float val = acc[c];
+        if (has_gs) val = val * gs;
+        if (ci < a.Cin) {
+            const int64_t o = v * a.Cin + ci;
+            pre += val;
+            if (dv.mode) val = val * dv(ld(e.aux + o));
+            post += val;
+            if (e.addend) val = val + ld(e.addend + o);
+            st(gx + o, val);
+        } else {
+            st(gx2 + v * a.Cin2 + (ci - a.Cin), val);
+        }
+    }
+}
+
 // ============================================================================ pointwise
-constexpr int kPwSeg = 256;  // voxels per workgroup
+constexpr int kPwSeg = 256;  // voxels per segment
 constexpr int kPwCC = 32;    // input channels per LDS chunk
+constexpr int kMaxBlocksX = 2048;  // grid-stride cap (bounds the per-block scalar atomics)
 
 // DGRAD = false: y[v, o] = epi( sum_i W[o][i] * pro(x[v, i]) )          (i over Cin + Cin2)
-// DGRAD = true : gx[v, i] = dgrad_epi( gscale * sum_o W[o][i] * g[v, o] ) (o over Cout)
+// DGRAD = true : gx[v, i] = bwd_epi( gscale * sum_o W[o][i] * g[v, o] ) (o over Cout)
+// Workgroups stride over 256-voxel segments; each segment is one contiguous slab.
 template <typename T, int COT, bool DGRAD>
 __global__ __launch_bounds__(256) void k_pw(ConvArgs a, const T *__restrict__ in, const T *__restrict__ in2,
-                                           const float *__restrict__ w, const float *__restrict__ e_scale,
-                                           const float *__restrict__ e_bias, const float *__restrict__ e_cbias,
-                                           const T *__restrict__ res, int res_up2, int post_elu,
-                                           const T *__restrict__ aux, const T *__restrict__ addend,
-                                           T *__restrict__ out, T *__restrict__ out2, float *dpre, float *dpost) {
+                                           const float *__restrict__ w, FwdEpi<T> fe, BwdEpi<T> be,
+                                           const float *__restrict__ gscale, T *__restrict__ out,
+                                           T *__restrict__ out2, float *dpre, float *dpost) {
     __shared__ float xs[kPwSeg][kPwCC + 1];
     __shared__ __attribute__((aligned(16))) float ws[kPwCC][COT];
     __shared__ float red[8];
@@ -101,151 +199,76 @@ __global__ __launch_bounds__(256) void k_pw(ConvArgs a, const T *__restrict__ in
     const int nin = DGRAD ? a.Cout : Ct;    // channels read
     const int nout = DGRAD ? Ct : a.Cout;   // channels written
     const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
-    const int64_t v0 = int64_t(blockIdx.x) * kPwSeg;
-    const int nv = int(min<int64_t>(kPwSeg, nvox - v0));
+    const int64_t nseg = (nvox + kPwSeg - 1) / kPwSeg;
     const int o0 = blockIdx.y * COT;
-    const Prologue pro = make_prologue(a.pro_kind, a.pro_a, DGRAD ? nullptr : a.pro_b);
+    const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
+    const ActDeriv dv = make_deriv(be);
+    const float gs = gscale ? *gscale : 1.f;
     const int tid = threadIdx.x;
+    float pre = 0.f, post = 0.f;
 
-    float acc[COT];
+    for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int64_t v0 = seg * kPwSeg;
+        const int nv = int(min<int64_t>(kPwSeg, nvox - v0));
+        float acc[COT];
 #pragma unroll
-    for (int c = 0; c < COT; ++c) acc[c] = 0.f;
-
-    for (int c0 = 0; c0 < nin; c0 += kPwCC) {
-        const int cc = min(kPwCC, nin - c0);
-        __syncthreads();
-        // cooperative, coalesced staging of the [nv][cc] sub-block (rows contiguous when cc == nin)
-        for (int e = tid; e < nv * cc; e += 256) {
-            const int vv = e / cc, c = e - vv * cc;
-            const int ch = c0 + c;
-            float val;
-            if (DGRAD) {
-                val = ld(in + (v0 + vv) * a.Cout + ch);
-            } else if (ch < a.Cin) {
-                val = pro.apply(ld(in + (v0 + vv) * a.Cin + ch));
-            } else {
-                val = pro.apply(ld(in2 + (v0 + vv) * a.Cin2 + (ch - a.Cin)));
+        for (int c = 0; c < COT; ++c) acc[c] = 0.f;
+        for (int c0 = 0; c0 < nin; c0 += kPwCC) {
+            const int cc = min(kPwCC, nin - c0);
+            __syncthreads();
+            // cooperative, coalesced staging of the [nv][cc] sub-block (prologue once per element)
+            for (int e = tid; e < nv * cc; e += 256) {
+                const int vv = e / cc, c = e - vv * cc;
+                const int ch = c0 + c;
+                float val;
+                if (DGRAD) val = ld(in + (v0 + vv) * a.Cout + ch);
+                else if (ch < a.Cin) val = pro.apply(ld(in + (v0 + vv) * a.Cin + ch));
+                else val = pro.apply(ld(in2 + (v0 + vv) * a.Cin2 + (ch - a.Cin)));
+                xs[vv][c] = val;
             }
-            xs[vv][c] = val;
+            for (int e = tid; e < cc * COT; e += 256) {
+                const int c = e / COT, j = e - c * COT;
+                const int oc = o0 + j, ic = c0 + c;
+                float wv = 0.f;
+                if (oc < nout) wv = DGRAD ? w[int64_t(ic) * Ct + oc] : w[int64_t(oc) * Ct + ic];
+                ws[c][j] = wv;
+            }
+            __syncthreads();
+            if (tid < nv) {
+                for (int c = 0; c < cc; ++c) {
+                    const float xv = xs[tid][c];
+#pragma unroll
+                    for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, ws[c][j], acc[j]);
+                }
+            }
         }
-        for (int e = tid; e < cc * COT; e += 256) {
-            const int c = e / COT, j = e - c * COT;
-            const int oc = o0 + j, ic = c0 + c;
-            float wv = 0.f;
-            if (oc < nout) wv = DGRAD ? w[int64_t(ic) * Ct + oc] : w[int64_t(oc) * Ct + ic];
-            ws[c][j] = wv;
-        }
-        __syncthreads();
         if (tid < nv) {
-            for (int c = 0; c < cc; ++c) {
-                const float xv = xs[tid][c];
-#pragma unroll
-                for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, ws[c][j], acc[j]);
-            }
+            if (!DGRAD) fwd_epilogue<T, COT>(a, fe, acc, v0 + tid, o0, out);
+            else bwd_epilogue<T, COT>(a, be, dv, gs, gscale != nullptr, acc, v0 + tid, o0, out, out2, pre, post);
         }
     }
-
-    const int64_t v = v0 + tid;
-    if (!DGRAD) {
-        if (tid >= nv) return;
-        const float sc = e_scale ? *e_scale : 1.f;
-        const float bi = e_bias ? *e_bias : 0.f;
-        int h0 = 0, h1 = 0, w0 = 0, w1 = 0, d0 = 0, d1 = 0, b = 0;
-        float lh = 0.f, lw = 0.f, ldd = 0.f;
-        const int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
-        if (res && res_up2) {
-            int64_t t = v;
-            const int od = int(t % a.oD); t /= a.oD;
-            const int ow = int(t % a.oW); t /= a.oW;
-            const int oh = int(t % a.oH);
-            b = int(t / a.oH);
-            up_coeff(oh, rH, h0, h1, lh);
-            up_coeff(ow, rW, w0, w1, lw);
-            up_coeff(od, rD, d0, d1, ldd);
-        }
-        T *yp = out + v * a.Cout;
-#pragma unroll
-        for (int j = 0; j < COT; ++j) {
-            const int co = o0 + j;
-            if (co >= a.Cout) break;
-            float val = acc[j];
-            if (e_scale) val = val * sc;
-            if (e_bias) val = val + bi;
-            if (e_cbias) val = val + e_cbias[co];
-            if (res) {
-                if (!res_up2) {
-                    val = val + ld(res + v * a.Cout + co);
-                } else {
-                    auto R = [&](int hh, int ww, int dd) {
-                        return ld(res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.Cout + co);
-                    };
-                    val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
-                                              lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
-                                 lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
-                                       lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1))));
-                }
-            }
-            if (post_elu) val = elu(val);
-            st(yp + co, val);
-        }
-    } else {
-        float pre = 0.f, post = 0.f;
-        if (tid < nv) {
-            const float gs = e_scale ? *e_scale : 1.f;  // gscale
-#pragma unroll
-            for (int j = 0; j < COT; ++j) {
-                const int ci = o0 + j;
-                if (ci >= Ct) break;
-                float val = acc[j];
-                if (e_scale) val = val * gs;
-                if (ci < a.Cin) {
-                    const int64_t o = v * a.Cin + ci;
-                    pre += val;
-                    if (aux && pro.kind == VQ3D_PRO_ELU_ADD) val = val * pro.deriv(ld(aux + o));
-                    post += val;
-                    if (addend) val = val + ld(addend + o);
-                    st(out + o, val);
-                } else {
-                    st(out2 + v * a.Cin2 + (ci - a.Cin), val);
-                }
-            }
-        }
-        if (dpre || dpost) {
-            pre = block_sum<float, 256>(pre, red);
-            post = block_sum<float, 256>(post, red + 4);
-            if (tid == 0) {
-                atomic_add_f(dpre, pre);
-                atomic_add_f(dpost, post);
-            }
+    if (DGRAD && (dpre || dpost)) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (tid == 0) {
+            atomic_add_f(dpre, pre);
+            atomic_add_f(dpost, post);
         }
     }
 }
 
 // ============================================================================ forward, k > 1
+// thread = one output voxel x COT channels (grid-stride over voxel blocks of 256)
 template <typename T, int COT>
 __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restrict__ x, const T *__restrict__ x2,
-                                                 const float *__restrict__ w, const float *__restrict__ e_scale,
-                                                 const float *__restrict__ e_bias, const float *__restrict__ e_cbias,
-                                                 const T *__restrict__ res, int res_up2, int post_elu, int all_taps,
+                                                 const float *__restrict__ w, FwdEpi<T> fe, int all_taps,
                                                  T *__restrict__ y) {
     extern __shared__ __attribute__((aligned(16))) float wsh[];  // [taps][Ct][COT]
     const int Ct = a.Cin + a.Cin2;
     const int K3 = a.k * a.k * a.k;
     const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
-    const int64_t v = int64_t(blockIdx.x) * 256 + threadIdx.x;
     const int co0 = blockIdx.y * COT;
     const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
-
-    int od = 0, ow = 0, oh = 0, b = 0;
-    if (v < nvox) {
-        int64_t t = v;
-        od = int(t % a.oD); t /= a.oD;
-        ow = int(t % a.oW); t /= a.oW;
-        oh = int(t % a.oH); b = int(t / a.oH);
-    }
-    float acc[COT];
-#pragma unroll
-    for (int c = 0; c < COT; ++c) acc[c] = 0.f;
 
     if (all_taps) {
         for (int i = threadIdx.x; i < K3 * Ct * COT; i += 256) {
@@ -255,110 +278,78 @@ __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restric
         }
         __syncthreads();
     }
-    int tap = 0;
-    for (int kh = 0; kh < a.k; ++kh) {
-        const int ih = fwd_index(oh, kh, a.s, a.p, a.iH, a.circ);
-        for (int kw = 0; kw < a.k; ++kw) {
-            const int iw = fwd_index(ow, kw, a.s, a.p, a.iW, a.circ);
-            for (int kd = 0; kd < a.k; ++kd, ++tap) {
-                const float *wt = wsh;
-                if (all_taps) {
-                    wt = wsh + tap * Ct * COT;
-                } else {
-                    __syncthreads();
-                    for (int i = threadIdx.x; i < Ct * COT; i += 256) {
-                        const int ci = i / COT, c = i - ci * COT;
-                        const int co = co0 + c;
-                        wsh[i] = co < a.Cout ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
-                    }
-                    __syncthreads();
-                }
-                if (v >= nvox) continue;
-                const int id = fwd_index(od, kd, a.s, a.p, a.iD, a.circ);
-                if ((ih | iw | id) < 0) continue;
-                const int64_t pos = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id;
-                const T *xp = x + pos * a.Cin;
-                for (int ci = 0; ci < a.Cin; ++ci) {
-                    const float xv = pro.apply(ld(xp + ci));
-                    const float *wr = wt + ci * COT;
+    for (int64_t vb = int64_t(blockIdx.x) * 256; vb < nvox; vb += int64_t(gridDim.x) * 256) {
+        const int64_t v = vb + threadIdx.x;
+        int od = 0, ow = 0, oh = 0, b = 0;
+        if (v < nvox) {
+            int64_t t = v;
+            od = int(t % a.oD); t /= a.oD;
+            ow = int(t % a.oW); t /= a.oW;
+            oh = int(t % a.oH); b = int(t / a.oH);
+        }
+        float acc[COT];
 #pragma unroll
-                    for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
-                }
-                if (a.Cin2) {
-                    const T *xq = x2 + pos * a.Cin2;
-                    for (int ci = 0; ci < a.Cin2; ++ci) {
-                        const float xv = pro.apply(ld(xq + ci));
-                        const float *wr = wt + (a.Cin + ci) * COT;
+        for (int c = 0; c < COT; ++c) acc[c] = 0.f;
+        int tap = 0;
+        for (int kh = 0; kh < a.k; ++kh) {
+            const int ih = fwd_index(oh, kh, a.s, a.p, a.iH, a.circ);
+            for (int kw = 0; kw < a.k; ++kw) {
+                const int iw = fwd_index(ow, kw, a.s, a.p, a.iW, a.circ);
+                for (int kd = 0; kd < a.k; ++kd, ++tap) {
+                    const float *wt = wsh;
+                    if (all_taps) {
+                        wt = wsh + tap * Ct * COT;
+                    } else {
+                        __syncthreads();
+                        for (int i = threadIdx.x; i < Ct * COT; i += 256) {
+                            const int ci = i / COT, c = i - ci * COT;
+                            const int co = co0 + c;
+                            wsh[i] = co < a.Cout ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
+                        }
+                        __syncthreads();
+                    }
+                    if (v >= nvox) continue;
+                    const int id = fwd_index(od, kd, a.s, a.p, a.iD, a.circ);
+                    if ((ih | iw | id) < 0) continue;
+                    const int64_t pos = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id;
+                    const T *xp = x + pos * a.Cin;
+                    for (int ci = 0; ci < a.Cin; ++ci) {
+                        const float xv = pro.apply(ld(xp + ci));
+                        const float *wr = wt + ci * COT;
 #pragma unroll
                         for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
                     }
+                    if (a.Cin2) {
+                        const T *xq = x2 + pos * a.Cin2;
+                        for (int ci = 0; ci < a.Cin2; ++ci) {
+                            const float xv = pro.apply(ld(xq + ci));
+                            const float *wr = wt + (a.Cin + ci) * COT;
+#pragma unroll
+                            for (int c = 0; c < COT; ++c) acc[c] = fmaf(xv, wr[c], acc[c]);
+                        }
+                    }
                 }
             }
         }
-    }
-    if (v >= nvox) return;
-    const float sc = e_scale ? *e_scale : 1.f;
-    const float bi = e_bias ? *e_bias : 0.f;
-    T *yp = y + v * a.Cout;
-    int h0 = 0, h1 = 0, w0 = 0, w1 = 0, d0 = 0, d1 = 0;
-    float lh = 0.f, lw = 0.f, ldd = 0.f;
-    const int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
-    if (res && res_up2) {
-        up_coeff(oh, rH, h0, h1, lh);
-        up_coeff(ow, rW, w0, w1, lw);
-        up_coeff(od, rD, d0, d1, ldd);
-    }
-#pragma unroll
-    for (int c = 0; c < COT; ++c) {
-        const int co = co0 + c;
-        if (co >= a.Cout) break;
-        float val = acc[c];
-        if (e_scale) val = val * sc;
-        if (e_bias) val = val + bi;
-        if (e_cbias) val = val + e_cbias[co];
-        if (res) {
-            if (!res_up2) {
-                val = val + ld(res + v * a.Cout + co);
-            } else {
-                auto R = [&](int hh, int ww, int dd) {
-                    return ld(res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.Cout + co);
-                };
-                val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
-                                          lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
-                             lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
-                                   lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1))));
-            }
-        }
-        if (post_elu) val = elu(val);
-        st(yp + co, val);
+        if (v < nvox) fwd_epilogue<T, COT>(a, fe, acc, v, co0, y);
     }
 }
 
 // ============================================================================ backward data, k > 1
 template <typename T, int CIT>
 __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restrict__ g, const float *__restrict__ gscale,
-                                                   const float *__restrict__ w, const T *__restrict__ aux,
-                                                   const T *__restrict__ addend, int all_taps, T *__restrict__ gx,
-                                                   T *__restrict__ gx2, float *dpre, float *dpost) {
+                                                   const float *__restrict__ w, BwdEpi<T> be, int all_taps,
+                                                   T *__restrict__ gx, T *__restrict__ gx2, float *dpre,
+                                                   float *dpost) {
     extern __shared__ __attribute__((aligned(16))) float wsh[];  // [taps][Cout][CIT]
     __shared__ float red[8];
     const int Ct = a.Cin + a.Cin2;
     const int K3 = a.k * a.k * a.k;
     const int64_t nvox = int64_t(a.B) * a.iH * a.iW * a.iD;
-    const int64_t v = int64_t(blockIdx.x) * 256 + threadIdx.x;
     const int ci0 = blockIdx.y * CIT;
-    const Prologue pro = make_prologue(a.pro_kind, a.pro_a, nullptr);
-
-    int id = 0, iw = 0, ih = 0, b = 0;
-    if (v < nvox) {
-        int64_t t = v;
-        id = int(t % a.iD); t /= a.iD;
-        iw = int(t % a.iW); t /= a.iW;
-        ih = int(t % a.iH); b = int(t / a.iH);
-    }
-    float acc[CIT];
-#pragma unroll
-    for (int c = 0; c < CIT; ++c) acc[c] = 0.f;
+    const ActDeriv dv = make_deriv(be);
+    const float gs = gscale ? *gscale : 1.f;
+    float pre = 0.f, post = 0.f;
 
     if (all_taps) {
         for (int i = threadIdx.x; i < K3 * a.Cout * CIT; i += 256) {
@@ -368,57 +359,50 @@ __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restr
         }
         __syncthreads();
     }
-    int tap = 0;
-    for (int kh = 0; kh < a.k; ++kh) {
-        const int oh = bwd_index(ih, kh, a.s, a.p, a.iH, a.oH, a.circ);
-        for (int kw = 0; kw < a.k; ++kw) {
-            const int ow = bwd_index(iw, kw, a.s, a.p, a.iW, a.oW, a.circ);
-            for (int kd = 0; kd < a.k; ++kd, ++tap) {
-                const float *wt = wsh;
-                if (all_taps) {
-                    wt = wsh + tap * a.Cout * CIT;
-                } else {
-                    __syncthreads();
-                    for (int i = threadIdx.x; i < a.Cout * CIT; i += 256) {
-                        const int co = i / CIT, c = i - co * CIT;
-                        const int ci = ci0 + c;
-                        wsh[i] = ci < Ct ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
+    for (int64_t vb = int64_t(blockIdx.x) * 256; vb < nvox; vb += int64_t(gridDim.x) * 256) {
+        const int64_t v = vb + threadIdx.x;
+        int id = 0, iw = 0, ih = 0, b = 0;
+        if (v < nvox) {
+            int64_t t = v;
+            id = int(t % a.iD); t /= a.iD;
+            iw = int(t % a.iW); t /= a.iW;
+            ih = int(t % a.iH); b = int(t / a.iH);
+        }
+        float acc[CIT];
+#pragma unroll
+        for (int c = 0; c < CIT; ++c) acc[c] = 0.f;
+        int tap = 0;
+        for (int kh = 0; kh < a.k; ++kh) {
+            const int oh = bwd_index(ih, kh, a.s, a.p, a.iH, a.oH, a.circ);
+            for (int kw = 0; kw < a.k; ++kw) {
+                const int ow = bwd_index(iw, kw, a.s, a.p, a.iW, a.oW, a.circ);
+                for (int kd = 0; kd < a.k; ++kd, ++tap) {
+                    const float *wt = wsh;
+                    if (all_taps) {
+                        wt = wsh + tap * a.Cout * CIT;
+                    } else {
+                        __syncthreads();
+                        for (int i = threadIdx.x; i < a.Cout * CIT; i += 256) {
+                            const int co = i / CIT, c = i - co * CIT;
+                            const int ci = ci0 + c;
+                            wsh[i] = ci < Ct ? w[(int64_t(co) * Ct + ci) * K3 + tap] : 0.f;
+                        }
+                        __syncthreads();
                     }
-                    __syncthreads();
-                }
-                if (v >= nvox) continue;
-                const int od = bwd_index(id, kd, a.s, a.p, a.iD, a.oD, a.circ);
-                if ((oh | ow | od) < 0) continue;
-                const T *gp = g + (((int64_t(b) * a.oH + oh) * a.oW + ow) * a.oD + od) * a.Cout;
-                for (int co = 0; co < a.Cout; ++co) {
-                    const float gv = ld(gp + co);
-                    const float *wr = wt + co * CIT;
+                    if (v >= nvox) continue;
+                    const int od = bwd_index(id, kd, a.s, a.p, a.iD, a.oD, a.circ);
+                    if ((oh | ow | od) < 0) continue;
+                    const T *gp = g + (((int64_t(b) * a.oH + oh) * a.oW + ow) * a.oD + od) * a.Cout;
+                    for (int co = 0; co < a.Cout; ++co) {
+                        const float gv = ld(gp + co);
+                        const float *wr = wt + co * CIT;
 #pragma unroll
-                    for (int c = 0; c < CIT; ++c) acc[c] = fmaf(gv, wr[c], acc[c]);
+                        for (int c = 0; c < CIT; ++c) acc[c] = fmaf(gv, wr[c], acc[c]);
+                    }
                 }
             }
         }
-    }
-    float pre = 0.f, post = 0.f;
-    if (v < nvox) {
-        const float gs = gscale ? *gscale : 1.f;
-#pragma unroll
-        for (int c = 0; c < CIT; ++c) {
-            const int ci = ci0 + c;
-            if (ci >= Ct) break;
-            float val = acc[c];
-            if (gscale) val = val * gs;
-            if (ci < a.Cin) {
-                const int64_t o = v * a.Cin + ci;
-                pre += val;
-                if (aux && pro.kind == VQ3D_PRO_ELU_ADD) val = val * pro.deriv(ld(aux + o));
-                post += val;
-                if (addend) val = val + ld(addend + o);
-                st(gx + o, val);
-            } else {
-                st(gx2 + v * a.Cin2 + (ci - a.Cin), val);
-            }
-        }
+        if (v < nvox) bwd_epilogue<T, CIT>(a, be, dv, gs, gscale != nullptr, acc, v, ci0, gx, gx2, pre, post);
     }
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
@@ -533,13 +517,26 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(ConvArgs a, const T *__restr
 }
 
 // ============================================================================ host side
+static const int kTiles[] = {1, 2, 4, 8, 12, 16};
+
 static int pick_tile(int c) {
     const int ntiles = (c + 15) / 16;
     const int per = (c + ntiles - 1) / ntiles;
-    static const int opts[] = {1, 2, 4, 8, 12, 16};
-    for (int o : opts)
+    for (int o : kTiles)
         if (o >= per) return o;
     return 16;
+}
+
+// shrink the channel tile while the grid would leave the chip idle (tiny top-level grids)
+static int pick_tile_for(int c, int64_t work_items, int64_t target = 65536) {
+    int t = pick_tile(c);
+    while (t > 1 && work_items * ((c + t - 1) / t) < target) {
+        int smaller = 1;
+        for (int o : kTiles)
+            if (o < t) smaller = o;
+        t = smaller;
+    }
+    return t;
 }
 
 static bool is_pointwise(const vq3d_conv_desc *d) { return d->kernel == 1 && d->stride == 1 && d->pad == 0; }
@@ -569,38 +566,73 @@ static int validate(const vq3d_conv_desc *d) {
 
 constexpr size_t kAllTapsLds = 48 * 1024;
 
+static unsigned blocks_x(int64_t units) { return unsigned(std::max<int64_t>(1, std::min<int64_t>(units, kMaxBlocksX))); }
+
+template <typename T>
+static FwdEpi<T> make_fwd_epi(const vq3d_conv_epilogue *epi) {
+    FwdEpi<T> e = {};
+    if (epi) {
+        e.scale = epi->scale;
+        e.bias = epi->bias;
+        e.cbias = epi->cbias;
+        e.res = static_cast<const T *>(epi->residual);
+        e.res_up2 = epi->residual_up2;
+        e.act = epi->act;
+        e.act_a = epi->act_a;
+        e.act_b = epi->act_b;
+    }
+    return e;
+}
+
+template <typename T>
+static BwdEpi<T> make_bwd_epi(const vq3d_dgrad_epilogue *epi, int pro_kind, const float *pro_a) {
+    BwdEpi<T> e = {};
+    if (epi) {
+        e.aux = static_cast<const T *>(epi->aux);
+        e.addend = static_cast<const T *>(epi->addend);
+        if (epi->aux_kind == 1) {
+            e.mode = 2;
+            e.p = epi->aux_b;
+        } else if (pro_kind == VQ3D_PRO_ELU_ADD) {
+            e.mode = 1;
+            e.p = pro_a;
+        }
+        if (!e.aux) e.mode = 0;
+    }
+    return e;
+}
+
 template <typename T>
 static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w, const float *pa,
                       const float *pb, const vq3d_conv_epilogue *epi, void *y, hipStream_t s) {
     ConvArgs a = make_args(d, pa, pb);
-    const int cot = pick_tile(d->cout);
     const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
-    const float *es = epi ? epi->scale : nullptr;
-    const float *eb = epi ? epi->bias : nullptr;
-    const float *ec = epi ? epi->cbias : nullptr;
-    const T *res = epi ? static_cast<const T *>(epi->residual) : nullptr;
-    const int rup = epi ? epi->residual_up2 : 0, pe = epi ? epi->post_elu : 0;
-    if (res && rup && ((d->out_h | d->out_w | d->out_d) & 1)) return fail("conv: residual_up2 needs even output");
+    FwdEpi<T> fe = make_fwd_epi<T>(epi);
+    if (fe.res && fe.res_up2 && ((d->out_h | d->out_w | d->out_d) & 1))
+        return fail("conv: residual_up2 needs even output");
+    if (fe.act == VQ3D_ACT_ELU_AFFINE && (!fe.act_a || !fe.act_b)) return fail("conv: ELU_AFFINE needs act_a/b");
     if (is_pointwise(d)) {
-        dim3 grid(unsigned((nvox + kPwSeg - 1) / kPwSeg), unsigned((d->cout + cot - 1) / cot));
-#define L(C)                                                                                                   \
-    case C:                                                                                                    \
-        k_pw<T, C, false><<<grid, 256, 0, s>>>(a, (const T *)x, (const T *)x2, w, es, eb, ec, res, rup, pe,      \
-                                               nullptr, nullptr, (T *)y, nullptr, nullptr, nullptr);          \
+        const int cot = pick_tile_for(d->cout, nvox);
+        dim3 grid(blocks_x((nvox + kPwSeg - 1) / kPwSeg), unsigned((d->cout + cot - 1) / cot));
+        BwdEpi<T> be = {};
+#define L(C)                                                                                                  \
+    case C:                                                                                                   \
+        k_pw<T, C, false><<<grid, 256, 0, s>>>(a, (const T *)x, (const T *)x2, w, fe, be, nullptr, (T *)y,    \
+                                               nullptr, nullptr, nullptr);                                    \
         break;
         switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
         return check_launch("conv3d_fwd(pointwise)");
     }
+    const int cot = pick_tile_for(d->cout, nvox);
     const int Ct = d->cin + d->cin2, K3 = d->kernel * d->kernel * d->kernel;
     const size_t all = size_t(K3) * Ct * cot * 4;
     const int all_taps = all <= kAllTapsLds;
     const size_t lds = all_taps ? all : size_t(Ct) * cot * 4;
-    dim3 grid(unsigned((nvox + 255) / 256), unsigned((d->cout + cot - 1) / cot));
+    dim3 grid(blocks_x((nvox + 255) / 256), unsigned((d->cout + cot - 1) / cot));
 #define L(C)                                                                                                   \
     case C:                                                                                                    \
-        k_conv_fwd<T, C><<<grid, 256, lds, s>>>(a, (const T *)x, (const T *)x2, w, es, eb, ec, res, rup, pe,     \
-                                                all_taps, (T *)y);                                             \
+        k_conv_fwd<T, C><<<grid, 256, lds, s>>>(a, (const T *)x, (const T *)x2, w, fe, all_taps, (T *)y);      \
         break;
     switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
@@ -613,16 +645,16 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
                         float *dpost, hipStream_t s) {
     ConvArgs a = make_args(d, pa, nullptr);
     const int Ct = d->cin + d->cin2;
-    const int cit = pick_tile(Ct);
     const int64_t nvox = int64_t(d->batch) * d->in_h * d->in_w * d->in_d;
-    const T *aux = epi ? static_cast<const T *>(epi->aux) : nullptr;
-    const T *add = epi ? static_cast<const T *>(epi->addend) : nullptr;
+    const int cit = pick_tile_for(Ct, nvox);
+    BwdEpi<T> be = make_bwd_epi<T>(epi, d->pro_kind, pa);
     if (is_pointwise(d)) {
-        dim3 grid(unsigned((nvox + kPwSeg - 1) / kPwSeg), unsigned((Ct + cit - 1) / cit));
+        FwdEpi<T> fe = {};
+        dim3 grid(blocks_x((nvox + kPwSeg - 1) / kPwSeg), unsigned((Ct + cit - 1) / cit));
 #define L(C)                                                                                                  \
     case C:                                                                                                   \
-        k_pw<T, C, true><<<grid, 256, 0, s>>>(a, (const T *)g, nullptr, w, gscale, nullptr, nullptr, nullptr, 0, \
-                                              0, aux, add, (T *)gx, (T *)gx2, dpre, dpost);                   \
+        k_pw<T, C, true><<<grid, 256, 0, s>>>(a, (const T *)g, nullptr, w, fe, be, gscale, (T *)gx, (T *)gx2,  \
+                                              dpre, dpost);                                                   \
         break;
         switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
@@ -632,11 +664,11 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
     const size_t all = size_t(K3) * d->cout * cit * 4;
     const int all_taps = all <= kAllTapsLds;
     const size_t lds = all_taps ? all : size_t(d->cout) * cit * 4;
-    dim3 grid(unsigned((nvox + 255) / 256), unsigned((Ct + cit - 1) / cit));
+    dim3 grid(blocks_x((nvox + 255) / 256), unsigned((Ct + cit - 1) / cit));
 #define L(C)                                                                                                  \
     case C:                                                                                                   \
-        k_conv_dgrad<T, C><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, aux, add, all_taps, (T *)gx,     \
-                                                  (T *)gx2, dpre, dpost);                                     \
+        k_conv_dgrad<T, C><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, be, all_taps, (T *)gx, (T *)gx2,  \
+                                                  dpre, dpost);                                               \
         break;
     switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
@@ -654,14 +686,21 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     // rows per workgroup: all rows when they fit (voxel sub-streams fill the rest), else 256
     const int R = Kt >= 256 ? 256 : (Kt > 128 ? Kt : std::max(1, Kt));
     const int ytiles = (Kt + R - 1) / R;
-    const int cot = pick_tile(d->cout);
-    const int ztiles = (d->cout + cot - 1) / cot;
     const int64_t nrows = int64_t(d->batch) * d->out_h * d->out_w;
-    const int64_t tiles = int64_t(ytiles) * ztiles;
-    // enough workgroups to fill the chip, each with >= ~64 output voxels of work
-    int64_t nbx = std::max<int64_t>(1, 2048 / tiles);
     const int64_t min_rows = std::max<int64_t>(1, 64 / std::max(1, d->out_d));
-    nbx = std::min<int64_t>(nbx, (nrows + min_rows - 1) / min_rows);
+    const int64_t max_nbx = (nrows + min_rows - 1) / min_rows;
+    // channel tile: shrink it while there are too few workgroups to fill the chip
+    int cot = pick_tile(d->cout);
+    while (cot > 1 && int64_t(ytiles) * ((d->cout + cot - 1) / cot) * std::min<int64_t>(max_nbx, 2048) < 512) {
+        int smaller = 1;
+        for (int o : kTiles)
+            if (o < cot) smaller = o;
+        cot = smaller;
+    }
+    const int ztiles = (d->cout + cot - 1) / cot;
+    const int64_t tiles = int64_t(ytiles) * ztiles;
+    int64_t nbx = std::max<int64_t>(1, 2048 / tiles);
+    nbx = std::min<int64_t>(nbx, max_nbx);
     const int64_t rows_per_blk = (nrows + nbx - 1) / nbx;
     nbx = (nrows + rows_per_blk - 1) / rows_per_blk;
     dim3 grid((unsigned)nbx, (unsigned)ytiles, (unsigned)ztiles);
@@ -697,8 +736,8 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
     if (int r = validate(d)) return r;
     if (!g || !w || !gx || (d->cin2 && !gx2)) return fail("conv3d_bwd_data: null pointer");
     if (d->pro_kind != VQ3D_PRO_NONE && !pro_a) return fail("conv3d_bwd_data: prologue needs pro_a");
-    if (d->pro_kind == VQ3D_PRO_ELU_ADD && (!epi || !epi->aux))
-        return fail("conv3d_bwd_data: ELU prologue derivative needs epi->aux");
+    if (epi && epi->aux_kind == 1 && epi->aux && !epi->aux_b)
+        return fail("conv3d_bwd_data: aux_kind 1 needs aux_b");
     hipStream_t s = as_stream(stream);
     return d->dtype == VQ3D_F32 ? launch_dgrad<float>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s)
                                 : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s);

@@ -20,6 +20,8 @@ int check_launch(const char *what) {
     return 0;
 }
 
+static unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048))); }
+
 // ============================================================================ upsample x2
 // y[b, 2h', 2w', 2d', c] = trilinear(prologue(x)) ; thread per output element
 template <typename T>
@@ -70,16 +72,17 @@ __device__ __forceinline__ int up_adjoint(int i, int n, int *js, float *ws) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B, int C, int H, int W, int D, int pk,
-                                               const float *pa, const T *__restrict__ aux,
+__global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B, int C, int H, int W, int D,
+                                               int dmode, const float *dparam, const T *__restrict__ aux,
                                                const T *__restrict__ addend, T *__restrict__ gx, float *dpre,
                                                float *dpost) {
     __shared__ float red[8];
     const int64_t n = int64_t(B) * H * W * D * C;
-    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    ActDeriv dv;
+    dv.mode = aux ? dmode : 0;
+    dv.p = (dv.mode && dparam) ? *dparam : 0.f;
     float pre = 0.f, post = 0.f;
-    if (i < n) {
-        const Prologue pro = make_prologue(pk, pa, nullptr);
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
         int64_t t = i;
         const int c = int(t % C); t /= C;
         const int id = int(t % D); t /= D;
@@ -99,9 +102,9 @@ __global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B,
                 acc = fmaf(wh[a] * ww[bb], s, acc);
             }
         float v = acc;
-        pre = v;
-        if (aux && pro.kind == VQ3D_PRO_ELU_ADD) v *= pro.deriv(ld(aux + i));
-        post = v;
+        pre += v;
+        if (dv.mode) v *= dv(ld(aux + i));
+        post += v;
         if (addend) v += ld(addend + i);
         st(gx + i, v);
     }
@@ -358,7 +361,6 @@ __global__ __launch_bounds__(256) void k_scale(float *__restrict__ x, float a, i
     for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) x[i] *= a;
 }
 
-static unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192))); }
 
 }  // namespace vq3d
 
@@ -392,17 +394,25 @@ int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         void *gx, float *dpro_pre, float *dpro_post, vq3d_stream_t stream) {
     if (batch <= 0 || channels <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("upsample2x_bwd: bad sizes");
     if (!gy || !gx) return fail("upsample2x_bwd: null pointer");
-    if (pro_kind == VQ3D_PRO_ELU_ADD && (!epi || !epi->aux || !pro_a))
-        return fail("upsample2x_bwd: ELU prologue derivative needs aux and pro_a");
-    const int64_t n = int64_t(batch) * h * w * dd * channels;
-    const unsigned nb = unsigned((n + 255) / 256);
-    hipStream_t s = as_stream(stream);
     const void *aux = epi ? epi->aux : nullptr, *add = epi ? epi->addend : nullptr;
+    int dmode = 0;
+    const float *dparam = nullptr;
+    if (aux && epi->aux_kind == 1) {
+        dmode = 2;
+        dparam = epi->aux_b;
+    } else if (aux && pro_kind == VQ3D_PRO_ELU_ADD) {
+        dmode = 1;
+        dparam = pro_a;
+    }
+    if (dmode && !dparam) return fail("upsample2x_bwd: derivative needs its scalar (pro_a or aux_b)");
+    const int64_t n = int64_t(batch) * h * w * dd * channels;
+    const unsigned nb = grid_for(n);
+    hipStream_t s = as_stream(stream);
     if (dtype == VQ3D_F32)
-        k_up_bwd<float><<<nb, 256, 0, s>>>((const float *)gy, batch, channels, h, w, dd, pro_kind, pro_a,
+        k_up_bwd<float><<<nb, 256, 0, s>>>((const float *)gy, batch, channels, h, w, dd, dmode, dparam,
                                            (const float *)aux, (const float *)add, (float *)gx, dpro_pre, dpro_post);
     else
-        k_up_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)gy, batch, channels, h, w, dd, pro_kind, pro_a,
+        k_up_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)gy, batch, channels, h, w, dd, dmode, dparam,
                                             (const bf16_t *)aux, (const bf16_t *)add, (bf16_t *)gx, dpro_pre,
                                             dpro_post);
     return check_launch("upsample2x_bwd");

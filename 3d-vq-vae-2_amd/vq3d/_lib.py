@@ -25,13 +25,16 @@ class ConvDesc(ctypes.Structure):
                                      "pro_kind")]
 
 
+ACT_NONE, ACT_ELU, ACT_ELU_AFFINE = 0, 1, 2
+
+
 class ConvEpilogue(ctypes.Structure):
     _fields_ = [("scale", P), ("bias", P), ("cbias", P), ("residual", P), ("residual_up2", c_int),
-                ("post_elu", c_int)]
+                ("act", c_int), ("act_a", P), ("act_b", P)]
 
 
 class DgradEpilogue(ctypes.Structure):
-    _fields_ = [("aux", P), ("addend", P)]
+    _fields_ = [("aux", P), ("aux_kind", c_int), ("aux_b", P), ("addend", P)]
 
 
 _SIGS = {

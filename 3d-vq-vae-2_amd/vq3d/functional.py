@@ -42,22 +42,29 @@ def mode_geometry(mode):
 
 # ============================================================================================ PreAct block
 class PreActBlockFn(torch.autograd.Function):
-    """PreActFixupResBlock.forward (layers.py:176-195) as 4 (5 in up mode) kernels forward and
-    ~12 backward.  Circular padding (layers.py:109).  Saved for backward: x, h1, h2 (+ the
-    upsampled branch input in up mode)."""
+    """PreActFixupResBlock.forward (layers.py:176-195), circular padding (layers.py:109).
+
+    Each conv's epilogue writes the NEXT conv's activated input, so no kernel recomputes an
+    ELU for a k^3 gather:
+        t2  = elu(conv1(elu(x + b1a) + b1b) + b2a) + b2b      (1x1, prologue + ELU_AFFINE epilogue)
+        t3  = elu(conv2(t2 | up(t2)) + b3a) + b3b            (k^3 circular, ELU_AFFINE epilogue)
+        s   = skip(x + b1c) + b1d                              (if present; half grid in up mode)
+        out = conv3(t3) * scale + b4 + (s | up(s) | x)        (1x1)
+    Backward recovers elu'(z) from the saved activated tensors (t - b > 0 ? 1 : t - b + 1).
+    Saved: x, t2, t3 (+ up(t2) in up mode)."""
 
     @staticmethod
     def forward(ctx, x, blk, *params):
         k, s, p, up = mode_geometry(blk.mode)
         g1 = ConvGeom(1)
         x = ops.as_cl(x)
-        h1 = ops.conv_fwd(x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b))
+        t2 = ops.conv_fwd(x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), act=(blk.bias2a, blk.bias2b))
         if up:
-            tup = ops.upsample2x(h1, pro=(blk.bias2a, blk.bias2b))
-            h2 = ops.conv_fwd(tup, blk.branch_conv2.weight, ConvGeom(3, 1, 1, True))
+            tup = ops.upsample2x(t2)
+            t3 = ops.conv_fwd(tup, blk.branch_conv2.weight, ConvGeom(3, 1, 1, True), act=(blk.bias3a, blk.bias3b))
         else:
             tup = None
-            h2 = ops.conv_fwd(h1, blk.branch_conv2.weight, ConvGeom(k, s, p, True), pro=(blk.bias2a, blk.bias2b))
+            t3 = ops.conv_fwd(t2, blk.branch_conv2.weight, ConvGeom(k, s, p, True), act=(blk.bias3a, blk.bias3b))
         if blk.skip_conv is not None:
             gs = ConvGeom(2, 2, 0) if blk.mode == "down" else g1
             # up mode: W (up(x + b1c)) + b1d == up(W (x + b1c) + b1d) (both linear, weights sum to 1),
@@ -65,35 +72,34 @@ class PreActBlockFn(torch.autograd.Function):
             res = ops.conv_fwd(x, blk.skip_conv.weight, gs, pro=(blk.bias1c,), bias=blk.bias1d)
         else:
             res = x
-        out = ops.conv_fwd(h2, blk.branch_conv3.weight, g1, pro=(blk.bias3a, blk.bias3b), scale=blk.scale,
-                           bias=blk.bias4, residual=res, residual_up2=up)
+        out = ops.conv_fwd(t3, blk.branch_conv3.weight, g1, scale=blk.scale, bias=blk.bias4, residual=res,
+                           residual_up2=up)
         ctx.blk = blk
-        ctx.save_for_backward(x, h1, h2, tup)
+        ctx.save_for_backward(x, t2, t3, tup)
         return out
 
     @staticmethod
     def backward(ctx, g):
         blk = ctx.blk
-        x, h1, h2, tup = ctx.saved_tensors
+        x, t2, t3, tup = ctx.saved_tensors
         g = _cl(g)
         k, s, p, up = mode_geometry(blk.mode)
         g1 = ConvGeom(1)
         gb = grad_buf
-        # conv3 (1x1 on the output grid): g_h2 = scale * W3^T g * elu'(h2 + b3a)
-        g_h2, _ = ops.conv_bwd(g, h2, blk.branch_conv3.weight, g1, pro=(blk.bias3a, blk.bias3b),
-                               gscale=blk.scale, aux=h2, dw=gb(blk.branch_conv3.weight), dscale=gb(blk.scale),
-                               dbias=gb(blk.bias4), dpro_pre=gb(blk.bias3b), dpro_post=gb(blk.bias3a),
-                               escale=blk.scale)
+        # conv3 (1x1): g_h2 = scale * W3^T g * elu'(h2 + b3a), elu' from t3
+        g_h2, _ = ops.conv_bwd(g, t3, blk.branch_conv3.weight, g1, gscale=blk.scale, aux=t3, aux_b=blk.bias3b,
+                               dw=gb(blk.branch_conv3.weight), dscale=gb(blk.scale), dbias=gb(blk.bias4),
+                               dpro_pre=gb(blk.bias3b), dpro_post=gb(blk.bias3a), escale=blk.scale)
         # conv2
         if up:
             g_tup, _ = ops.conv_bwd(g_h2, tup, blk.branch_conv2.weight, ConvGeom(3, 1, 1, True),
                                     dw=gb(blk.branch_conv2.weight))
-            g_h1 = ops.upsample2x_bwd(g_tup, h1.shape, pro=(blk.bias2a, blk.bias2b), aux=h1,
-                                      dpro_pre=gb(blk.bias2b), dpro_post=gb(blk.bias2a))
+            g_h1 = ops.upsample2x_bwd(g_tup, t2.shape, aux=t2, aux_b=blk.bias2b, dpro_pre=gb(blk.bias2b),
+                                      dpro_post=gb(blk.bias2a))
         else:
-            g_h1, _ = ops.conv_bwd(g_h2, h1, blk.branch_conv2.weight, ConvGeom(k, s, p, True),
-                                   pro=(blk.bias2a, blk.bias2b), aux=h1, dw=gb(blk.branch_conv2.weight),
-                                   dpro_pre=gb(blk.bias2b), dpro_post=gb(blk.bias2a))
+            g_h1, _ = ops.conv_bwd(g_h2, t2, blk.branch_conv2.weight, ConvGeom(k, s, p, True), aux=t2,
+                                   aux_b=blk.bias2b, dw=gb(blk.branch_conv2.weight), dpro_pre=gb(blk.bias2b),
+                                   dpro_post=gb(blk.bias2a))
         # skip path
         if blk.skip_conv is not None:
             gs = ConvGeom(2, 2, 0) if blk.mode == "down" else g1
@@ -102,7 +108,7 @@ class PreActBlockFn(torch.autograd.Function):
                                      dw=gb(blk.skip_conv.weight), dbias=gb(blk.bias1d), dpro_pre=gb(blk.bias1c))
         else:
             addend = g
-        # conv1 (1x1 on the input grid) + residual gradient
+        # conv1 (1x1 on the input grid) + residual gradient; elu'(x + b1a) from x
         g_x, _ = ops.conv_bwd(g_h1, x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), aux=x,
                               addend=addend, dw=gb(blk.branch_conv1.weight), dpro_pre=gb(blk.bias1b),
                               dpro_post=gb(blk.bias1a))
@@ -119,7 +125,7 @@ class ConvFn(torch.autograd.Function):
     def forward(ctx, x, x2, residual, spec, *tensors):
         y = ops.conv_fwd(x, spec.w, spec.geom, pro=spec.pro, x2=x2, scale=spec.scale, bias=spec.bias,
                          cbias=spec.cbias, residual=residual, residual_up2=spec.residual_up2,
-                         post_elu=spec.post_elu)
+                         act="elu" if spec.post_elu else None)
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, x2, y if spec.post_elu else None)

@@ -75,8 +75,17 @@ def pro_kind_of(pro):
     return L.PRO_ELU_ADD, pro[0], pro[1]
 
 
+def _act(act):
+    """act = None | 'elu' | (a, b) -> (kind, a, b): none / elu(v) / elu(v + a) + b."""
+    if act is None:
+        return L.ACT_NONE, None, None
+    if act == "elu":
+        return L.ACT_ELU, None, None
+    return L.ACT_ELU_AFFINE, act[0], act[1]
+
+
 def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, residual=None,
-             residual_up2=False, post_elu=False, out=None):
+             residual_up2=False, act=None, out=None):
     x = as_cl(x)
     b, cin, h, wd, d = x.shape
     cin2 = 0 if x2 is None else x2.shape[1]
@@ -91,14 +100,21 @@ def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, r
         if tuple(residual.shape) != rs or residual.dtype != x.dtype:
             raise L.Vq3dError(f"residual {tuple(residual.shape)} does not match {rs}")
         as_cl(residual)
+    ak, aa, ab = _act(act)
     epi = L.ConvEpilogue(scale=_p(scale), bias=_p(bias), cbias=_p(cbias), residual=_p(residual),
-                         residual_up2=int(residual_up2), post_elu=int(post_elu))
+                         residual_up2=int(residual_up2), act=ak, act_a=_p(aa), act_b=_p(ab))
     L.call("vq3d_conv3d_fwd", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(w), _p(pa), _p(pb),
            ctypes.byref(epi), L.ptr(y), L.stream())
     return y
 
 
-def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, addend=None, want_gx=True,
+def _depi(aux, aux_b, addend):
+    """dgrad epilogue: aux with aux_b=None -> derivative of the conv's own prologue (aux = its
+    input before the prologue); with aux_b -> aux is an activated tensor elu(z) + aux_b."""
+    return L.DgradEpilogue(aux=_p(aux), aux_kind=0 if aux_b is None else 1, aux_b=_p(aux_b), addend=_p(addend))
+
+
+def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None, addend=None, want_gx=True,
              dw=None, dscale=None, dbias=None, dcbias=None, dpro_pre=None, dpro_post=None, escale=None):
     """Backward of conv_fwd: returns (gx, gx2); parameter gradients are ACCUMULATED (fp32
     atomics) into the given buffers (dw: weight, dscale/dbias: epilogue scalars, dcbias: conv
@@ -113,7 +129,7 @@ def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, addend=Non
     if want_gx or dpro_pre is not None or dpro_post is not None:
         gx = new_act(b, cin, h, wd, d, x.dtype, x.device)
         gx2 = None if x2 is None else new_act(b, cin2, h, wd, d, x.dtype, x.device)
-        epi = L.DgradEpilogue(aux=_p(aux), addend=_p(addend))
+        epi = _depi(aux, aux_b, addend)
         L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), _p(gscale), L.ptr(w), _p(pa),
                ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), s)
     L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb), L.ptr(w),
@@ -132,11 +148,11 @@ def upsample2x(x, pro=None):
     return y
 
 
-def upsample2x_bwd(gy, src_shape, pro=None, aux=None, addend=None, dpro_pre=None, dpro_post=None):
+def upsample2x_bwd(gy, src_shape, pro=None, aux=None, aux_b=None, addend=None, dpro_pre=None, dpro_post=None):
     b, c, h, w, d = src_shape
     kind, pa, _ = pro_kind_of(pro)
     gx = new_act(b, c, h, w, d, gy.dtype, gy.device)
-    epi = L.DgradEpilogue(aux=_p(aux), addend=_p(addend))
+    epi = _depi(aux, aux_b, addend)
     L.call("vq3d_upsample2x_bwd", L.dtype_code(gy), b, c, h, w, d, L.ptr(gy), kind, _p(pa), ctypes.byref(epi),
            L.ptr(gx), _p(dpro_pre), _p(dpro_post), L.stream())
     return gx

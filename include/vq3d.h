@@ -45,23 +45,33 @@ typedef struct vq3d_conv_desc {
     int32_t pro_kind;   /* VQ3D_PRO_* applied to the input on load */
 } vq3d_conv_desc;
 
-/* Forward epilogue: y = post( acc*scale + bias + cbias[co] + residual ) */
+/* Forward epilogue: y = act( acc*scale + bias + cbias[co] + residual ) */
+enum { VQ3D_ACT_NONE = 0, VQ3D_ACT_ELU = 1 /* elu(v) */, VQ3D_ACT_ELU_AFFINE = 2 /* elu(v + a) + b */ };
 typedef struct vq3d_conv_epilogue {
     const float *scale;     /* device scalar or NULL (PreAct `scale`, layers.py:187) */
     const float *bias;      /* device scalar or NULL (`bias4`, `bias1d`, `bias2b`)  */
     const float *cbias;     /* device [cout] or NULL (nn.Conv3d bias)               */
-    const void *residual;   /* NULL or activation tensor added before post-ELU       */
+    const void *residual;   /* NULL or activation tensor added before the activation */
     int32_t residual_up2;   /* 1: residual lives on the half-resolution grid and is
                                trilinearly upsampled x2 on the fly (ResizeConv skip)  */
-    int32_t post_elu;       /* 1: y = elu(.) (FixupResBlock, layers.py:287-288)      */
+    int32_t act;            /* VQ3D_ACT_*: ELU = FixupResBlock's post-activation
+                               (layers.py:287-288); ELU_AFFINE = the NEXT PreAct conv's
+                               "elu(x + a) + b" input glue fused here (layers.py:181-185) */
+    const float *act_a, *act_b;  /* device scalars for VQ3D_ACT_ELU_AFFINE */
 } vq3d_conv_epilogue;
 
 /* Backward-data epilogue on the conv INPUT grid:
- *   v = acc;  pre += v;  v *= d/dx prologue(aux);  post += v;  v += addend;  store
+ *   v = acc;  pre += v;  v *= elu'(z);  post += v;  v += addend;  store
+ * with elu'(z) from `aux`:
+ *   aux_kind 0: aux = the conv input before its prologue elu(x + a) + b: z = aux + pro_a
+ *   aux_kind 1: aux = an activated tensor t = elu(z) + b (b = *aux_b), as written by an
+ *               ELU_AFFINE epilogue: elu'(z) = (t - b > 0) ? 1 : t - b + 1
  * pre / post are summed over every element (see vq3d_conv3d_bwd_data). */
 typedef struct vq3d_dgrad_epilogue {
-    const void *aux;        /* forward input before the prologue (needed for ELU'), or NULL */
-    const void *addend;     /* gradient added after the prologue derivative, or NULL */
+    const void *aux;        /* NULL: no derivative */
+    int32_t aux_kind;
+    const float *aux_b;
+    const void *addend;     /* gradient added after the derivative, or NULL */
 } vq3d_dgrad_epilogue;
 
 /* --- 3-D convolution (replaces nn.Conv3d / F.pad circular, layers.py:124-171,535,377,490,508) --- */
