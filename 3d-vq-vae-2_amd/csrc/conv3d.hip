@@ -415,7 +415,8 @@ __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restr
 }
 
 // ============================================================================ backward weight
-// Grid: x = voxel chunks, y = row tiles (row = tap * Ct + ci, R rows per workgroup),
+// Grid: x = voxel chunks, y = row tiles (row = ci * K3 + tap: the reference weight order, so a
+// workgroup's atomics hit consecutive addresses; R rows per workgroup),
 // z = co tiles of COT.  Thread = (row, voxel sub-stream vs), VS = 256 / R sub-streams.
 // Each chunk is a run of consecutive output voxels inside one D-row, so the voxel
 // coordinates advance without divisions.
@@ -439,7 +440,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(ConvArgs a, const T *__restr
     const int co0 = blockIdx.z * COT;
     const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
     const bool active = vs < VS && row < Kt;
-    const int tap = active ? row / Ct : 0, ci = active ? row - (row / Ct) * Ct : 0;
+    const int ci = active ? row / K3 : 0, tap = active ? row - (row / K3) * K3 : 0;
     const int kd = tap % a.k, kw = (tap / a.k) % a.k, kh = tap / (a.k * a.k);
     const bool second = ci >= a.Cin;
     const T *src = second ? x2 : x;
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(ConvArgs a, const T *__restr
         for (int c = 0; c < ncot; ++c) {
             float s = 0.f;
             for (int j = 0; j < VS; ++j) s += racc[j * R + rl][c];
-            const int64_t e = (int64_t(co0 + c) * Ct + ci) * K3 + tap;  // reference [co][ci][tap]
+            const int64_t e = int64_t(co0 + c) * Kt + row;  // reference [co][ci][tap]: lanes contiguous
             if (dw) atomicAdd(dw + e, escale ? s * sc : s);
             if (dscale) wg = fmaf(w[e], s, wg);
         }
@@ -699,7 +700,7 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     }
     const int ztiles = (d->cout + cot - 1) / cot;
     const int64_t tiles = int64_t(ytiles) * ztiles;
-    int64_t nbx = std::max<int64_t>(1, 2048 / tiles);
+    int64_t nbx = std::max<int64_t>(1, 1024 / tiles);  // x tiles: bounds the atomic traffic (nbx * E)
     nbx = std::min<int64_t>(nbx, max_nbx);
     const int64_t rows_per_blk = (nrows + nbx - 1) / nbx;
     nbx = (nrows + rows_per_blk - 1) / rows_per_blk;

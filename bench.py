@@ -46,6 +46,80 @@ def parse():
     return p.parse_args()
 
 
+# ---------------------------------------------------------------------------------------------- roofline
+# Dominant kernel of the path = the 3x3x3 circular conv 9->9 at 128x128x32 (decoder bottom
+# level, 51 launches per step in the 3-layer published model: the largest conv-FLOP share,
+# SURVEY.md App. A).  Algorithmic bytes per launch = bf16 input + bf16 output + fp32 weights.
+DOM = dict(cin=9, cout=9, grid=(128, 128, 32), k=3)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_dominant.json")
+
+
+def dominant_kernel_roofline(dtype, dev, iters=50):
+    import torch
+
+    from vq3d import ops
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    h, w, d = DOM["grid"]
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = (torch.randn((1, DOM["cin"], h, w, d), device=dev, generator=g) * 0.5).to(tdt).contiguous(
+        memory_format=torch.channels_last_3d)
+    wt = torch.randn((DOM["cout"], DOM["cin"], 3, 3, 3), device=dev, generator=g) * 0.1
+    geom = ops.ConvGeom(3, 1, 1, True)
+    for _ in range(3):
+        ops.conv_fwd(x, wt, geom)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        ops.conv_fwd(x, wt, geom)
+    e1.record(st)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    esz = x.element_size()
+    nvox = h * w * d
+    algo = nvox * (DOM["cin"] + DOM["cout"]) * esz + wt.numel() * 4
+    flops = 2.0 * nvox * DOM["cout"] * DOM["cin"] * 27
+    achieved = algo / t / 1e9
+    traffic = None
+    if os.path.exists(PMC_FILE):
+        try:
+            traffic = json.load(open(PMC_FILE)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "vq3d conv3d fwd 3x3x3 circular 9->9 @128x128x32 bf16",
+            "avg_launch_us": t * 1e6, "algorithmic_bytes": algo, "tflops": flops / t / 1e12}
+
+
+# ---------------------------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(mkw, size, sample=(256, 256, 64)):
+    """The CPU oracle (oracle/vqvae_cpu.py, fp32 torch-CPU restatement of the reference step)
+    timed on this host: one full training step of the same model on a smaller volume with
+    `frac` of the voxels, scaled to volumes/s of the full 512x512x128 volume."""
+    import torch
+
+    from oracle import vqvae_cpu as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    import vq3d
+    cfg = O.Config(**{k: v for k, v in mkw.items()})
+    torch.manual_seed(0)
+    ref = vq3d.VQVAE(vq3d.default_args(**mkw))
+    sd = {k: v.detach().clone() for k, v in ref.state_dict().items()}
+    x = torch.rand((1, 1) + tuple(sample), generator=torch.Generator().manual_seed(1234)) * 4.5 - 0.5
+    st = {}
+    O.train_step(cfg, sd, st, x, [sample[2]], 1e-4)  # warm-up (first-pass codebook init)
+    t0 = time.perf_counter()
+    O.train_step(cfg, sd, st, x, [sample[2]], 1e-4)
+    dt = time.perf_counter() - t0
+    frac = (sample[0] * sample[1] * sample[2]) / float(size[0] * size[1] * size[2])
+    return {"value": frac / dt, "unit": "volumes/s", "cores": threads, "kind": "port",
+            "sample": f"one oracle train step (fp32, same model) on a {sample[0]}x{sample[1]}x{sample[2]} "
+                      f"volume = {frac:.4g} of the 512x512x128 voxels, {dt:.2f} s, scaled by voxel count"}
+
+
 def main():
     a = parse()
     import torch
@@ -105,7 +179,7 @@ def main():
         elapsed = float(t)
     if a.profile_steps and rank == 0:
         print("per-step s:", [round(v, 4) for v in per], file=sys.stderr)
-    final_loss = float(loss)
+    final_loss = float(loss.detach())
     vols = world * batch * a.steps
     res = {
         "metric": "volumes/sec (enc+VQ+dec fwd+bwd) at 512x512x128",
@@ -123,6 +197,10 @@ def main():
         "config": {"workload": f"vqvae_{a.config}_train_step", "volume": list(size), "batch_per_gpu": batch,
                    "global_batch": batch * world, "parallelism": f"dp{world}", "final_loss": final_loss},
     }
+    if rank == 0 and not a.no_roofline:
+        res["roofline"] = dominant_kernel_roofline(a.dtype, dev)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(mkw, size)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
