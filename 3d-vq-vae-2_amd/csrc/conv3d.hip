@@ -21,6 +21,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 namespace vq3d {
 
@@ -178,6 +180,10 @@ __device__ __forceinline__ void bwd_epilogue(const ConvArgs &a, const BwdEpi<T> 
         }
     }
 }
+
+}  // namespace vq3d
+#include "conv_mfma.inc"
+namespace vq3d {
 
 // ============================================================================ pointwise
 constexpr int kPwSeg = 256;  // voxels per segment
@@ -625,6 +631,21 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
 #undef L
         return check_launch("conv3d_fwd(pointwise)");
     }
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        if (!mfma_disabled()) {
+            MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
+                                d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR);
+            if (m.ok) {
+                m.a.pro_kind = d->pro_kind;
+                m.a.pro_a = pa;
+                m.a.pro_b = pb;
+                m.a.wCt = d->cin + d->cin2;
+                BwdEpi<T> be = {};
+                return launch_mfma<false>(m, (const T *)x, (const T *)x2, w, fe, be, 0, nullptr, (T *)y, nullptr,
+                                          nullptr, nullptr, s);
+            }
+        }
+    }
     const int cot = pick_tile_for(d->cout, nvox);
     const int Ct = d->cin + d->cin2, K3 = d->kernel * d->kernel * d->kernel;
     const size_t all = size_t(K3) * Ct * cot * 4;
@@ -660,6 +681,21 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
         switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
         return check_launch("conv3d_bwd_data(pointwise)");
+    }
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        // stride-1 backward-data == forward conv of g with the flipped, transposed kernel
+        if (!mfma_disabled() && d->stride == 1) {
+            const int pp = d->kernel - 1 - d->pad;
+            MPlan m = plan_mfma(d->batch, d->cout, 0, Ct, d->out_h, d->out_w, d->out_d, d->in_h, d->in_w, d->in_d,
+                                d->kernel, 1, pp, d->pad_mode == VQ3D_PAD_CIRCULAR);
+            if (m.ok && pp >= 0) {
+                m.a.pro_kind = VQ3D_PRO_NONE;
+                m.a.wCt = Ct;
+                FwdEpi<T> fe = {};
+                return launch_mfma<true>(m, (const T *)g, nullptr, w, fe, be, d->cin, gscale, (T *)gx, (T *)gx2,
+                                         dpre, dpost, s);
+            }
+        }
     }
     const int K3 = d->kernel * d->kernel * d->kernel;
     const size_t all = size_t(K3) * d->cout * cit * 4;

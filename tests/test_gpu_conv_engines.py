@@ -1,0 +1,86 @@
+"""GPU: the bf16 MFMA implicit-GEMM conv engine against the fp32 VALU engine on the same
+bf16-representable inputs, over the geometries / channel counts the model uses (including
+tiny, odd and wrap-heavy grids).  Tolerance: 1.5e-2 of the output's max magnitude (bf16
+weights and outputs in the MFMA path, fp32 in the reference engine)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last_3d
+
+CASES = [
+    # (cin, cout, (h, w, d), k, s, p, circular)
+    (9, 9, (16, 16, 8), 3, 1, 1, True),
+    (4, 4, (8, 8, 32), 3, 1, 1, True),
+    (1, 1, (8, 8, 8), 3, 1, 1, True),
+    (2, 2, (6, 5, 3), 3, 1, 1, True),
+    (16, 16, (8, 8, 2), 3, 1, 1, True),
+    (36, 36, (8, 8, 4), 3, 1, 1, True),
+    (72, 72, (4, 4, 2), 3, 1, 1, True),
+    (128, 64, (4, 4, 2), 3, 1, 1, True),
+    (18, 9, (4, 4, 4), 3, 1, 1, False),
+    (4, 4, (8, 8, 8), 4, 2, 1, True),
+    (8, 8, (4, 4, 2), 4, 2, 1, True),
+    (16, 16, (8, 8, 4), 4, 2, 1, False),
+    (4, 8, (8, 8, 8), 2, 2, 0, False),
+    (3, 5, (3, 3, 3), 3, 1, 1, True),
+    (1, 4, (2, 2, 1), 3, 1, 1, True),
+]
+
+
+def rnd(shape, dev, g, scale=1.0):
+    return (torch.randn(shape, device=dev, generator=g) * scale).to(torch.bfloat16).float()
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_mfma_forward_and_dgrad_match_valu(gpu, case):
+    from vq3d import ops
+    cin, cout, (h, w, d), k, s, p, circ = case
+    g = torch.Generator(device=gpu).manual_seed(hash(case) % 1000)
+    geom = ops.ConvGeom(k, s, p, circ)
+    x = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((cout, cin, k, k, k), gpu, g, 0.3)
+    a = rnd((1,), gpu, g, 0.1)
+    b = rnd((1,), gpu, g, 0.1)
+    ref = ops.conv_fwd(x, wt, geom, pro=(a, b), act=(b, a))
+    out = ops.conv_fwd(x.to(torch.bfloat16), wt, geom, pro=(a, b), act=(b, a))
+    assert rel(out.float(), ref) < 1.5e-2, ("fwd", case, rel(out.float(), ref))
+    if s != 1:
+        return
+    oh, ow, od = geom.out(h), geom.out(w), geom.out(d)
+    gy = rnd((2, cout, oh, ow, od), gpu, g).contiguous(memory_format=CL)
+    add = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    dpre_r = torch.zeros(1, device=gpu)
+    dpost_r = torch.zeros(1, device=gpu)
+    dpre = torch.zeros(1, device=gpu)
+    dpost = torch.zeros(1, device=gpu)
+    gscale = rnd((1,), gpu, g)
+    gr, _ = ops.conv_bwd(gy, x, wt, geom, pro=(a, b), gscale=gscale, aux=x, addend=add, dpro_pre=dpre_r,
+                         dpro_post=dpost_r)
+    gm, _ = ops.conv_bwd(gy.to(torch.bfloat16), x.to(torch.bfloat16), wt, geom, pro=(a, b), gscale=gscale,
+                         aux=x.to(torch.bfloat16), addend=add.to(torch.bfloat16), dpro_pre=dpre, dpro_post=dpost)
+    assert rel(gm.float(), gr) < 1.5e-2, ("dgrad", case, rel(gm.float(), gr))
+    assert abs(float(dpre) - float(dpre_r)) <= 2e-2 * float(gr.abs().sum()) / gr.numel() * gr.numel() ** 0.5 + 1e-3
+
+
+def test_mfma_dual_input_and_residual(gpu):
+    from vq3d import ops
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x1 = rnd((1, 8, 8, 8, 4), gpu, g).contiguous(memory_format=CL)
+    x2 = rnd((1, 2, 8, 8, 4), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((6, 10, 3, 3, 3), gpu, g, 0.3)
+    res = rnd((1, 6, 4, 4, 2), gpu, g).contiguous(memory_format=CL)
+    sc = rnd((1,), gpu, g)
+    bi = rnd((1,), gpu, g)
+    geom = ops.ConvGeom(3, 1, 1, True)
+    ref = ops.conv_fwd(x1, wt, geom, x2=x2, scale=sc, bias=bi, residual=res, residual_up2=True)
+    out = ops.conv_fwd(x1.bfloat16(), wt, geom, x2=x2.bfloat16(), scale=sc, bias=bi, residual=res.bfloat16(),
+                       residual_up2=True)
+    assert rel(out.float(), ref) < 1.5e-2
