@@ -16,13 +16,21 @@ using bf16_t = uint16_t;  // raw bf16 bits; arithmetic always in fp32
 __device__ __forceinline__ float ld(const float *p) { return *p; }
 __device__ __forceinline__ float ld(const bf16_t *p) { return __uint_as_float(uint32_t(*p) << 16); }
 
-// round-to-nearest-even f32 -> bf16 (torch's conversion); NaN stays NaN
-__device__ __forceinline__ bf16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return bf16_t((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return bf16_t(u >> 16);
-}
+// round-to-nearest-even f32 -> bf16 (torch's conversion; NaN stays NaN): the hardware
+// v_cvt_pk_bf16_f32 on gfx950
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, static_cast<__bf16>(f)); }
+
+// n / d for 0 <= n < 2^31 without an integer divide (Granlund-Montgomery, host-built)
+struct FastDiv {
+    uint32_t m, s, d;
+    __host__ __device__ FastDiv() : m(0), s(0), d(1) {}
+    __host__ explicit FastDiv(uint32_t dd) : d(dd) {
+        s = 0;
+        while ((1u << s) < dd) ++s;
+        m = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << s) - dd)) / dd + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> s; }
+};
 __device__ __forceinline__ void st(float *p, float v) { *p = v; }
 __device__ __forceinline__ void st(bf16_t *p, float v) { *p = f2bf(v); }
 
