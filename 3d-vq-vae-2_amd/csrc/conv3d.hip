@@ -720,6 +720,20 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     const int Ct = d->cin + d->cin2;
     const int K3 = d->kernel * d->kernel * d->kernel;
     const int Kt = Ct * K3;
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        if (!mfma_disabled() && !is_pointwise(d)) {
+            MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
+                                d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true);
+            if (m.ok) {
+                m.a.pro_kind = d->pro_kind;
+                m.a.pro_a = pa;
+                m.a.pro_b = pb;
+                m.a.wCt = Ct;
+                return launch_wgrad_tiled(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
+                                          dbias, dcbias, s);
+            }
+        }
+    }
     // rows per workgroup: all rows when they fit (voxel sub-streams fill the rest), else 256
     const int R = Kt >= 256 ? 256 : (Kt > 128 ? Kt : std::max(1, Kt));
     const int ytiles = (Kt + R - 1) / R;

@@ -84,3 +84,33 @@ def test_mfma_dual_input_and_residual(gpu):
     out = ops.conv_fwd(x1.bfloat16(), wt, geom, x2=x2.bfloat16(), scale=sc, bias=bi, residual=res.bfloat16(),
                        residual_up2=True)
     assert rel(out.float(), ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_tiled_wgrad_matches_valu(gpu, case):
+    """bf16 LDS-tiled weight gradient (+ epilogue scalar / conv-bias gradients) vs the fp32 engine."""
+    from vq3d import ops
+    cin, cout, (h, w, d), k, s, p, circ = case
+    g = torch.Generator(device=gpu).manual_seed(1 + hash(case) % 1000)
+    geom = ops.ConvGeom(k, s, p, circ)
+    x = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((cout, cin, k, k, k), gpu, g, 0.3)
+    a = rnd((1,), gpu, g, 0.1)
+    b = rnd((1,), gpu, g, 0.1)
+    sc = rnd((1,), gpu, g)
+    oh, ow, od = geom.out(h), geom.out(w), geom.out(d)
+    gy = rnd((2, cout, oh, ow, od), gpu, g).contiguous(memory_format=CL)
+    outs = []
+    for dt in (torch.float32, torch.bfloat16):
+        dw = torch.zeros_like(wt)
+        dscale = torch.zeros(1, device=gpu)
+        dbias = torch.zeros(1, device=gpu)
+        dcb = torch.zeros(cout, device=gpu)
+        ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, pro=(a, b), want_gx=False, dw=dw, dscale=dscale, dbias=dbias,
+                     dcbias=dcb, escale=sc)
+        outs.append((dw, dscale, dbias, dcb))
+    (rw, rs, rb, rc), (mw, ms, mb, mc) = outs
+    assert rel(mw, rw) < 1.5e-2, ("dw", case, rel(mw, rw))
+    assert rel(mc, rc) < 1.5e-2, ("dcbias", case)
+    assert abs(float(mb) - float(rb)) <= 1e-2 * float(rc.abs().sum()) + 1e-3
+    assert abs(float(ms) - float(rs)) <= 2e-2 * (float((wt * rw).abs().sum()) / max(abs(float(sc)), 1e-3)) + 1e-3
