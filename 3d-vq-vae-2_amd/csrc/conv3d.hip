@@ -21,6 +21,9 @@
 #include "common.h"
 
 #include <algorithm>
+#include <map>
+#include <utility>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -113,7 +116,7 @@ __device__ __forceinline__ ActDeriv make_deriv(const BwdEpi<T> &e) {
 // y[v, co] for one voxel's accumulators (shared by the pointwise and the k > 1 forward)
 template <typename T, int COT>
 __device__ __forceinline__ void fwd_epilogue(const ConvArgs &a, const FwdEpi<T> &e, const float (&acc)[COT],
-                                             int64_t v, int co0, T *__restrict__ y) {
+                                             int64_t v, int co0, T *__restrict__ yp) {
     const float sc = e.scale ? *e.scale : 1.f;
     const float bi = e.bias ? *e.bias : 0.f;
     const float aa = e.act_a ? *e.act_a : 0.f, ab = e.act_b ? *e.act_b : 0.f;
@@ -130,7 +133,6 @@ __device__ __forceinline__ void fwd_epilogue(const ConvArgs &a, const FwdEpi<T> 
         up_coeff(ow, rW, w0, w1, lw);
         up_coeff(od, rD, d0, d1, ldd);
     }
-    T *yp = y + v * a.Cout;
 #pragma unroll
     for (int c = 0; c < COT; ++c) {
         const int co = co0 + c;
@@ -160,7 +162,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvArgs &a, const FwdEpi<T> 
 template <typename T, int CIT>
 __device__ __forceinline__ void bwd_epilogue(const ConvArgs &a, const BwdEpi<T> &e, const ActDeriv &dv, float gs,
                                              bool has_gs, const float (&acc)[CIT], int64_t v, int ci0,
-                                             T *__restrict__ gx, T *__restrict__ gx2, float &pre, float &post) {
+                                             T *__restrict__ gxr, T *__restrict__ gx2r, float &pre, float &post) {
     const int Ct = a.Cin + a.Cin2;
 #pragma unroll
     for (int c = 0; c < CIT; ++c) {
@@ -174,9 +176,9 @@ __device__ __forceinline__ void bwd_epilogue(const ConvArgs &a, const BwdEpi<T> 
             if (dv.mode) val = val * dv(ld(e.aux + o));
             post += val;
             if (e.addend) val = val + ld(e.addend + o);
-            st(gx + o, val);
+            st(gxr + ci, val);
         } else {
-            st(gx2 + v * a.Cin2 + (ci - a.Cin), val);
+            st(gx2r + (ci - a.Cin), val);
         }
     }
 }
@@ -186,71 +188,104 @@ __device__ __forceinline__ void bwd_epilogue(const ConvArgs &a, const BwdEpi<T> 
 namespace vq3d {
 
 // ============================================================================ pointwise
-constexpr int kPwSeg = 256;  // voxels per segment
-constexpr int kPwCC = 32;    // input channels per LDS chunk
+constexpr int kPwSeg = 256;        // voxels per segment (one thread each)
 constexpr int kMaxBlocksX = 2048;  // grid-stride cap (bounds the per-block scalar atomics)
+
+// contiguous global <-> LDS copy by the workgroup, 16-byte vectors when `vec` (both ends aligned)
+template <typename T>
+__device__ __forceinline__ void slab_copy(T *__restrict__ dst, const T *__restrict__ src, int n, bool vec) {
+    constexpr int E = 16 / sizeof(T);
+    int i0 = 0;
+    if (vec) {
+        const int nv = n / E;
+        for (int i = threadIdx.x; i < nv; i += 256)
+            reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+        i0 = nv * E;
+    }
+    for (int i = i0 + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+}
 
 // DGRAD = false: y[v, o] = epi( sum_i W[o][i] * pro(x[v, i]) )          (i over Cin + Cin2)
 // DGRAD = true : gx[v, i] = bwd_epi( gscale * sum_o W[o][i] * g[v, o] ) (o over Cout)
-// Workgroups stride over 256-voxel segments; each segment is one contiguous slab.
+// A segment of (up to) 256 voxels is one contiguous slab per tensor: it is staged into LDS with 16-byte
+// loads, each thread computes one voxel (weights of the COT-channel tile broadcast from LDS,
+// loaded once per workgroup), and when the tile holds every output channel (`slab`), results
+// leave through an LDS slab with 16-byte stores.
 template <typename T, int COT, bool DGRAD>
 __global__ __launch_bounds__(256) void k_pw(ConvArgs a, const T *__restrict__ in, const T *__restrict__ in2,
                                            const float *__restrict__ w, FwdEpi<T> fe, BwdEpi<T> be,
                                            const float *__restrict__ gscale, T *__restrict__ out,
-                                           T *__restrict__ out2, float *dpre, float *dpost) {
-    __shared__ float xs[kPwSeg][kPwCC + 1];
-    __shared__ __attribute__((aligned(16))) float ws[kPwCC][COT];
+                                           T *__restrict__ out2, float *dpre, float *dpost, int slab, int vec,
+                                           int seg_len) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float red[8];
     const int Ct = a.Cin + a.Cin2;
-    const int nin = DGRAD ? a.Cout : Ct;    // channels read
-    const int nout = DGRAD ? Ct : a.Cout;   // channels written
+    const int nA = DGRAD ? a.Cout : a.Cin;  // input slabs: A [256][nA] (+ B [256][nB] forward dual input)
+    const int nB = DGRAD ? 0 : a.Cin2;
+    const int nin = nA + nB;
+    const int oA = DGRAD ? a.Cin : a.Cout;  // output slabs (slab mode): A [256][oA] (+ B [256][oB])
+    const int oB = DGRAD ? a.Cin2 : 0;
     const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
-    const int64_t nseg = (nvox + kPwSeg - 1) / kPwSeg;
+    const int64_t nseg = (nvox + seg_len - 1) / seg_len;
     const int o0 = blockIdx.y * COT;
+    float *ws = reinterpret_cast<float *>(smem);  // [nin][COT]
+    T *sA = reinterpret_cast<T *>(smem + ((size_t(nin) * COT * 4 + 15) & ~size_t(15)));
+    T *sB = sA + seg_len * nA;
+    T *rA = sB + seg_len * nB;
+    T *rB = rA + seg_len * oA;
     const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
     const ActDeriv dv = make_deriv(be);
     const float gs = gscale ? *gscale : 1.f;
     const int tid = threadIdx.x;
     float pre = 0.f, post = 0.f;
 
+    for (int e = tid; e < nin * COT; e += 256) {
+        const int c = e / COT, j = e - c * COT;
+        const int oc = o0 + j;
+        float wv = 0.f;
+        if (DGRAD) wv = oc < Ct ? w[int64_t(c) * Ct + oc] : 0.f;
+        else wv = oc < a.Cout ? w[int64_t(oc) * Ct + c] : 0.f;
+        ws[e] = wv;
+    }
     for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        const int64_t v0 = seg * kPwSeg;
-        const int nv = int(min<int64_t>(kPwSeg, nvox - v0));
-        float acc[COT];
+        const int64_t v0 = seg * seg_len;
+        const int nv = int(min<int64_t>(seg_len, nvox - v0));
+        __syncthreads();
+        slab_copy(sA, in + v0 * nA, nv * nA, vec);
+        if (nB) slab_copy(sB, in2 + v0 * nB, nv * nB, vec);
+        __syncthreads();
+        if (tid < nv) {
+            float acc[COT];
 #pragma unroll
-        for (int c = 0; c < COT; ++c) acc[c] = 0.f;
-        for (int c0 = 0; c0 < nin; c0 += kPwCC) {
-            const int cc = min(kPwCC, nin - c0);
-            __syncthreads();
-            // cooperative, coalesced staging of the [nv][cc] sub-block (prologue once per element)
-            for (int e = tid; e < nv * cc; e += 256) {
-                const int vv = e / cc, c = e - vv * cc;
-                const int ch = c0 + c;
-                float val;
-                if (DGRAD) val = ld(in + (v0 + vv) * a.Cout + ch);
-                else if (ch < a.Cin) val = pro.apply(ld(in + (v0 + vv) * a.Cin + ch));
-                else val = pro.apply(ld(in2 + (v0 + vv) * a.Cin2 + (ch - a.Cin)));
-                xs[vv][c] = val;
-            }
-            for (int e = tid; e < cc * COT; e += 256) {
-                const int c = e / COT, j = e - c * COT;
-                const int oc = o0 + j, ic = c0 + c;
-                float wv = 0.f;
-                if (oc < nout) wv = DGRAD ? w[int64_t(ic) * Ct + oc] : w[int64_t(oc) * Ct + ic];
-                ws[c][j] = wv;
-            }
-            __syncthreads();
-            if (tid < nv) {
-                for (int c = 0; c < cc; ++c) {
-                    const float xv = xs[tid][c];
+            for (int j = 0; j < COT; ++j) acc[j] = 0.f;
+            const T *xr = sA + tid * nA;
+            for (int c = 0; c < nA; ++c) {
+                float xv = ld(xr + c);
+                if (!DGRAD) xv = pro.apply(xv);
+                const float *wr = ws + c * COT;
 #pragma unroll
-                    for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, ws[c][j], acc[j]);
-                }
+                for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, wr[j], acc[j]);
+            }
+            const T *xr2 = sB + tid * nB;
+            for (int c = 0; c < nB; ++c) {
+                const float xv = pro.apply(ld(xr2 + c));
+                const float *wr = ws + (nA + c) * COT;
+#pragma unroll
+                for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, wr[j], acc[j]);
+            }
+            const int64_t v = v0 + tid;
+            if (!DGRAD) {
+                fwd_epilogue<T, COT>(a, fe, acc, v, o0, slab ? rA + tid * oA : out + v * a.Cout);
+            } else {
+                T *ra = slab ? rA + tid * oA : out + v * a.Cin;
+                T *rb = slab ? rB + tid * oB : (out2 ? out2 + v * a.Cin2 : nullptr);
+                bwd_epilogue<T, COT>(a, be, dv, gs, gscale != nullptr, acc, v, o0, ra, rb, pre, post);
             }
         }
-        if (tid < nv) {
-            if (!DGRAD) fwd_epilogue<T, COT>(a, fe, acc, v0 + tid, o0, out);
-            else bwd_epilogue<T, COT>(a, be, dv, gs, gscale != nullptr, acc, v0 + tid, o0, out, out2, pre, post);
+        if (slab) {
+            __syncthreads();
+            slab_copy(out + v0 * oA, rA, nv * oA, vec);
+            if (oB) slab_copy(out2 + v0 * oB, rB, nv * oB, vec);
         }
     }
     if (DGRAD && (dpre || dpost)) {
@@ -337,7 +372,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(ConvArgs a, const T *__restric
                 }
             }
         }
-        if (v < nvox) fwd_epilogue<T, COT>(a, fe, acc, v, co0, y);
+        if (v < nvox) fwd_epilogue<T, COT>(a, fe, acc, v, co0, y + v * a.Cout);
     }
 }
 
@@ -408,7 +443,9 @@ __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restr
                 }
             }
         }
-        if (v < nvox) bwd_epilogue<T, CIT>(a, be, dv, gs, gscale != nullptr, acc, v, ci0, gx, gx2, pre, post);
+        if (v < nvox)
+            bwd_epilogue<T, CIT>(a, be, dv, gs, gscale != nullptr, acc, v, ci0, gx + v * a.Cin,
+                                 gx2 ? gx2 + v * a.Cin2 : nullptr, pre, post);
     }
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
@@ -609,6 +646,38 @@ static BwdEpi<T> make_bwd_epi(const vq3d_dgrad_epilogue *epi, int pro_kind, cons
     return e;
 }
 
+static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <typename T, bool DGRAD>
+static int launch_pw(const vq3d_conv_desc *d, const ConvArgs &a, const void *in, const void *in2, const float *w,
+                     const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale, void *out, void *out2,
+                     float *dpre, float *dpost, hipStream_t s) {
+    const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    const int Ct = d->cin + d->cin2;
+    const int nout = DGRAD ? Ct : d->cout;
+    const int nA = DGRAD ? d->cout : d->cin, nB = DGRAD ? 0 : d->cin2;
+    const int cot = nout <= 1 ? 1 : nout <= 2 ? 2 : nout <= 4 ? 4 : nout <= 8 ? 8 : nout <= 12 ? 12 : 16;
+    const int ychunks = (nout + cot - 1) / cot;
+    const int slab = ychunks == 1 ? 1 : 0;
+    const int vec = al16(in) && (!in2 || al16(in2)) && al16(out) && (!out2 || al16(out2));
+    const size_t ws = (size_t(nA + nB) * cot * 4 + 15) & ~size_t(15);
+    // segment of `seg` voxels (one per thread; shorter when the slabs would not fit 64 KB of LDS)
+    int seg = kPwSeg;
+    auto lds_of = [&](int sl) { return ws + size_t(sl) * (nA + nB + (slab ? nout : 0)) * sizeof(T); };
+    while (seg > 16 && lds_of(seg) > 64 * 1024) seg /= 2;
+    const size_t lds = lds_of(seg);
+    if (lds > 64 * 1024) return fail("conv: pointwise channel count too large");
+    dim3 grid(blocks_x((nvox + seg - 1) / seg), unsigned(ychunks));
+#define L(C)                                                                                                  \
+    case C:                                                                                                   \
+        k_pw<T, C, DGRAD><<<grid, 256, lds, s>>>(a, (const T *)in, (const T *)in2, w, fe, be, gscale, (T *)out, \
+                                                 (T *)out2, dpre, dpost, slab, vec, seg);                     \
+        break;
+    switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
+#undef L
+    return check_launch(DGRAD ? "conv3d_bwd_data(pointwise)" : "conv3d_fwd(pointwise)");
+}
+
 template <typename T>
 static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w, const float *pa,
                       const float *pb, const vq3d_conv_epilogue *epi, void *y, hipStream_t s) {
@@ -619,17 +688,8 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
         return fail("conv: residual_up2 needs even output");
     if (fe.act == VQ3D_ACT_ELU_AFFINE && (!fe.act_a || !fe.act_b)) return fail("conv: ELU_AFFINE needs act_a/b");
     if (is_pointwise(d)) {
-        const int cot = pick_tile_for(d->cout, nvox);
-        dim3 grid(blocks_x((nvox + kPwSeg - 1) / kPwSeg), unsigned((d->cout + cot - 1) / cot));
         BwdEpi<T> be = {};
-#define L(C)                                                                                                  \
-    case C:                                                                                                   \
-        k_pw<T, C, false><<<grid, 256, 0, s>>>(a, (const T *)x, (const T *)x2, w, fe, be, nullptr, (T *)y,    \
-                                               nullptr, nullptr, nullptr);                                    \
-        break;
-        switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
-#undef L
-        return check_launch("conv3d_fwd(pointwise)");
+        return launch_pw<T, false>(d, a, x, x2, w, fe, be, nullptr, y, nullptr, nullptr, nullptr, s);
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
         if (!mfma_disabled()) {
@@ -672,15 +732,7 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
     BwdEpi<T> be = make_bwd_epi<T>(epi, d->pro_kind, pa);
     if (is_pointwise(d)) {
         FwdEpi<T> fe = {};
-        dim3 grid(blocks_x((nvox + kPwSeg - 1) / kPwSeg), unsigned((Ct + cit - 1) / cit));
-#define L(C)                                                                                                  \
-    case C:                                                                                                   \
-        k_pw<T, C, true><<<grid, 256, 0, s>>>(a, (const T *)g, nullptr, w, fe, be, gscale, (T *)gx, (T *)gx2,  \
-                                              dpre, dpost);                                                   \
-        break;
-        switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
-#undef L
-        return check_launch("conv3d_bwd_data(pointwise)");
+        return launch_pw<T, true>(d, a, g, nullptr, w, fe, be, gscale, gx, gx2, dpre, dpost, s);
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
         // stride-1 backward-data == forward conv of g with the flipped, transposed kernel
@@ -729,6 +781,9 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
                 m.a.pro_a = pa;
                 m.a.pro_b = pb;
                 m.a.wCt = Ct;
+                if (d->cout <= 64)  // MFMA engine holds up to 4 tiles of 16 output channels
+                    return launch_wgrad_mfma(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
+                                             dbias, dcbias, s);
                 return launch_wgrad_tiled(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
                                           dbias, dcbias, s);
             }

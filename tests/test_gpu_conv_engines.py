@@ -27,6 +27,9 @@ CASES = [
     (4, 8, (8, 8, 8), 2, 2, 0, False),
     (3, 5, (3, 3, 3), 3, 1, 1, True),
     (1, 4, (2, 2, 1), 3, 1, 1, True),
+    (18, 9, (8, 8, 8), 1, 1, 0, False),
+    (9, 2, (8, 8, 5), 1, 1, 0, False),
+    (64, 128, (4, 4, 2), 1, 1, 0, False),
 ]
 
 
@@ -88,7 +91,7 @@ def test_mfma_dual_input_and_residual(gpu):
 
 @pytest.mark.parametrize("case", CASES)
 def test_tiled_wgrad_matches_valu(gpu, case):
-    """bf16 LDS-tiled weight gradient (+ epilogue scalar / conv-bias gradients) vs the fp32 engine."""
+    """bf16 MFMA / LDS-tiled weight gradient (+ epilogue scalar / conv-bias gradients) vs the fp32 engine."""
     from vq3d import ops
     cin, cout, (h, w, d), k, s, p, circ = case
     g = torch.Generator(device=gpu).manual_seed(1 + hash(case) % 1000)
