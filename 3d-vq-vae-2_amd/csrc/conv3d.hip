@@ -19,6 +19,7 @@
 //     chunk of one output row; partial sums leave each workgroup as fp32 atomics straight
 //     into the parameter-gradient buffer (no partial slabs, no finalize pass).
 #include "common.h"
+#include "engines.h"
 
 #include <algorithm>
 #include <map>
@@ -767,13 +768,15 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
 template <typename T>
 static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pa,
                         const float *pb, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
-                        float *dcbias, hipStream_t s) {
+                        float *dcbias, void *ws, size_t ws_bytes, hipStream_t s) {
     ConvArgs a = make_args(d, pa, pb);
     const int Ct = d->cin + d->cin2;
     const int K3 = d->kernel * d->kernel * d->kernel;
     const int Kt = Ct * K3;
+    if (is_pointwise(d))
+        return launch_pw_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
     if constexpr (std::is_same<T, bf16_t>::value) {
-        if (!mfma_disabled() && !is_pointwise(d)) {
+        if (!mfma_disabled()) {
             MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
                                 d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true);
             if (m.ok) {
@@ -849,18 +852,25 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
                                 : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s);
 }
 
+size_t vq3d_conv3d_bwd_weight_workspace_size(const vq3d_conv_desc *d) {
+    if (validate(d)) return 0;
+    return is_pointwise(d) ? pw_wgrad_workspace(d) : 0;
+}
+
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
                            const float *pro_b, const float *w, const float *epi_scale, float *dw, float *dscale,
-                           float *dbias, float *dcbias, vq3d_stream_t stream) {
+                           float *dbias, float *dcbias, void *workspace, size_t workspace_bytes,
+                           vq3d_stream_t stream) {
     if (int r = validate(d)) return r;
     if (!x || !g || (d->cin2 && !x2)) return fail("conv3d_bwd_weight: null pointer");
     if (d->pro_kind != VQ3D_PRO_NONE && !pro_a) return fail("conv3d_bwd_weight: prologue needs pro_a");
     if (d->pro_kind == VQ3D_PRO_ELU_ADD && !pro_b) return fail("conv3d_bwd_weight: ELU prologue needs pro_b");
     if (dscale && (!w || !epi_scale)) return fail("conv3d_bwd_weight: dscale needs w and epi_scale");
     hipStream_t s = as_stream(stream);
-    return d->dtype == VQ3D_F32
-               ? launch_wgrad<float>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias, dcbias, s)
-               : launch_wgrad<bf16_t>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias, dcbias, s);
+    return d->dtype == VQ3D_F32 ? launch_wgrad<float>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias,
+                                                      dcbias, workspace, workspace_bytes, s)
+                                : launch_wgrad<bf16_t>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias,
+                                                       dcbias, workspace, workspace_bytes, s);
 }
 
 }  // extern "C"

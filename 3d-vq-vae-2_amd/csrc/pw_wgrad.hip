@@ -1,0 +1,394 @@
+// 1x1x1 convolution weight gradient (nn.Conv3d kernel_size=1 at the block convs 1 / 3 and
+// the skip / proj / parse_input / out convs: vqvae/layers.py:134-171, 377, 490, 508, 535).
+//
+//   G[co][ci] = sum_v g[v][co] * pro(x)[v][ci]        (x channels then x2 channels: torch.cat)
+//
+// is a GEMM whose reduction runs over the voxels.  Channels-last slabs of `seg` consecutive
+// voxels are contiguous for both x and g, so each workgroup streams them through LDS with
+// 16-byte loads (all of a segment's loads in flight before the first is unpacked; the
+// prologue elu(x + a) + b applied once per element) and every thread accumulates a 4x4
+// (ci, co) tile over its voxel sub-stream.  A constant-1 column appended to x yields
+// sum_v g[v][co] (conv-bias / scalar-bias gradients) from the same loop.
+//
+// Reduction is deterministic and atomic-free on the data: sub-streams are summed in a fixed
+// order through LDS, each workgroup writes its partial G to the caller's workspace, and a
+// second kernel sums the partials in workgroup order and adds them to the fp32 gradients
+// (thousands of same-address atomics serialise at the L2 and were the bottleneck).
+#include "engines.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+constexpr int TI = 4, TO = 4;  // thread tile: input x output channels
+constexpr int kMaxBlocks = 2048;
+
+struct PwwArgs {
+    int64_t nvox;
+    int Ca, Cb, N;
+    int Xp, Gp;   // LDS row strides (floats) of the x and g slabs
+    int ones;     // column of the constant-1 entry in the x slab (Ct)
+    int ne;       // partial entries per workgroup: N x (Ct + 1)
+    int seg;      // voxels per segment
+    int nti;      // ci tiles
+    int tpb;      // tiles per workgroup
+    int S;        // voxel sub-streams per workgroup
+    int vec;      // every slab base 16-B aligned
+    FastDiv fa, fb, fn;
+};
+
+// Load a segment's slab (U x 16 B per thread in flight), then unpack:
+// dst[v * P + off + c] = f(src[v * C + c]) for v < nv.
+template <typename T, bool PRO, int U>
+__device__ __forceinline__ void stage(float *__restrict__ dst, int P, int off, const T *__restrict__ src, int nv,
+                                      int C, const FastDiv &fd, const Prologue &pro, bool vec) {
+    constexpr int E = 16 / sizeof(T);
+    const int n = nv * C;
+    const int nq = vec ? n / E : 0;
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    for (int q0 = threadIdx.x; q0 < nq; q0 += U * 256) {
+        uint4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q0 + u * 256 < nq) r[u] = s4[q0 + u * 256];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = q0 + u * 256;
+            if (q >= nq) break;
+            const T *el = reinterpret_cast<const T *>(&r[u]);
+            int v = int(fd.div(uint32_t(q * E))), c = q * E - v * C;
+#pragma unroll
+            for (int j = 0; j < E; ++j) {
+                const float val = ld(el + j);
+                dst[v * P + off + c] = PRO ? pro.apply(val) : val;
+                if (++c == C) {
+                    c = 0;
+                    ++v;
+                }
+            }
+        }
+    }
+    for (int e = nq * E + threadIdx.x; e < n; e += 256) {
+        const int v = int(fd.div(uint32_t(e))), c = e - v * C;
+        const float val = ld(src + e);
+        dst[v * P + off + c] = PRO ? pro.apply(val) : val;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pw_wgrad(PwwArgs a, const T *__restrict__ x, const T *__restrict__ x2,
+                                                 const T *__restrict__ g, int pro_kind, const float *pro_a,
+                                                 const float *pro_b, float *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *xs = sm;                     // [seg][Xp]
+    float *gs = sm + a.seg * a.Xp;      // [seg][Gp]
+    const int tid = threadIdx.x;
+    const int Ct = a.Ca + a.Cb;
+    const Prologue pro = make_prologue(pro_kind, pro_a, pro_b);
+    const int tl = tid % a.tpb, sub = tid / a.tpb;
+    const int tile = blockIdx.y * a.tpb + tl;
+    const int ntiles = a.nti * (a.Gp / TO);
+    const bool active = sub < a.S && tile < ntiles;
+    const int ci0 = (tile % a.nti) * TI, co0 = (tile / a.nti) * TO;
+
+    // columns the staging never writes: zero padding and the constant-1 column
+    for (int e = tid; e < a.seg * a.Xp; e += 256) {
+        const int c = e % a.Xp;
+        if (c >= Ct) xs[e] = c == a.ones ? 1.f : 0.f;
+    }
+    for (int e = tid; e < a.seg * a.Gp; e += 256)
+        if (e % a.Gp >= a.N) gs[e] = 0.f;
+
+    float acc[TI][TO];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TO; ++j) acc[i][j] = 0.f;
+
+    const int64_t nseg = (a.nvox + a.seg - 1) / a.seg;
+    for (int64_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const int64_t v0 = sg * a.seg;
+        const int nv = int(min<int64_t>(a.seg, a.nvox - v0));
+        __syncthreads();
+        if (pro.kind == VQ3D_PRO_NONE) {
+            stage<T, false, 4>(xs, a.Xp, 0, x + v0 * a.Ca, nv, a.Ca, a.fa, pro, a.vec);
+            if (a.Cb) stage<T, false, 2>(xs, a.Xp, a.Ca, x2 + v0 * a.Cb, nv, a.Cb, a.fb, pro, a.vec);
+        } else {
+            stage<T, true, 4>(xs, a.Xp, 0, x + v0 * a.Ca, nv, a.Ca, a.fa, pro, a.vec);
+            if (a.Cb) stage<T, true, 2>(xs, a.Xp, a.Ca, x2 + v0 * a.Cb, nv, a.Cb, a.fb, pro, a.vec);
+        }
+        stage<T, false, 4>(gs, a.Gp, 0, g + v0 * a.N, nv, a.N, a.fn, pro, a.vec);
+        __syncthreads();
+        if (active) {
+            for (int v = sub; v < nv; v += a.S) {
+                const float4 xv = *reinterpret_cast<const float4 *>(xs + v * a.Xp + ci0);
+                const float4 gv = *reinterpret_cast<const float4 *>(gs + v * a.Gp + co0);
+                const float xa[4] = {xv.x, xv.y, xv.z, xv.w}, ga[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TO; ++j) acc[i][j] = fmaf(xa[i], ga[j], acc[i][j]);
+            }
+        }
+    }
+    // fixed-order reduction of the sub-streams (one thread per tile entry), partial -> workspace
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < TI * TO; ++q) sm[q * 256 + tid] = acc[q / TO][q % TO];
+    __syncthreads();
+    const int nblk = gridDim.x;
+    for (int idx = tid; idx < a.tpb * TI * TO; idx += 256) {
+        const int q = idx / a.tpb, t = idx - q * a.tpb;
+        const int tt = blockIdx.y * a.tpb + t;
+        if (tt >= ntiles) continue;
+        const int ci = (tt % a.nti) * TI + q / TO, co = (tt / a.nti) * TO + q % TO;
+        if (co >= a.N || ci > Ct) continue;
+        float sum = 0.f;
+        for (int j = 0; j < a.S; ++j) sum += sm[q * 256 + j * a.tpb + t];
+        part[int64_t(co * (Ct + 1) + ci) * nblk + blockIdx.x] = sum;
+    }
+}
+
+// Few-channel convs (x: CX, g: CG channels, both in {1, 2, 4, 8}, one input): each thread
+// streams whole voxel rows straight from HBM (one vector load per row, 4 voxels in flight) and
+// keeps every (ci, co) product plus the bias column in registers; wave shuffles + one LDS
+// pass reduce the workgroup, which writes its partials like k_pw_wgrad.
+template <typename T, int C>
+__device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[C]) {
+    if constexpr (sizeof(T) == 2) {
+        if constexpr (C == 1) {
+            o[0] = ld(p);
+        } else if constexpr (C == 2) {
+            const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
+            o[0] = __uint_as_float(u << 16);
+            o[1] = __uint_as_float(u & 0xffff0000u);
+        } else if constexpr (C == 4) {
+            const uint2 u = *reinterpret_cast<const uint2 *>(p);
+            const uint32_t w[2] = {u.x, u.y};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                o[2 * j] = __uint_as_float(w[j] << 16);
+                o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+            }
+        } else {
+            const uint4 u = *reinterpret_cast<const uint4 *>(p);
+            const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[2 * j] = __uint_as_float(w[j] << 16);
+                o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < C; ++j) o[j] = p[j];
+    }
+}
+
+template <typename T, int CX, int CG>
+__global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__restrict__ x,
+                                                     const T *__restrict__ g, int pro_kind, const float *pro_a,
+                                                     const float *pro_b, float *__restrict__ part) {
+    constexpr int NE = CG * (CX + 1);
+    __shared__ float wred[4][NE];
+    const Prologue pro = make_prologue(pro_kind, pro_a, pro_b);
+    float acc[CG][CX + 1];
+#pragma unroll
+    for (int j = 0; j < CG; ++j)
+#pragma unroll
+        for (int i = 0; i <= CX; ++i) acc[j][i] = 0.f;
+    const int64_t stride = int64_t(gridDim.x) * 256;
+    for (int64_t v0 = int64_t(blockIdx.x) * 256 + threadIdx.x; v0 < nvox; v0 += 4 * stride) {
+        float xr[4][CX], gr[4][CG];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t v = v0 + u * stride;
+            if (v < nvox) {
+                load_row<T, CX>(x + v * CX, xr[u]);
+                load_row<T, CG>(g + v * CG, gr[u]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < CX; ++i) xr[u][i] = 0.f;
+#pragma unroll
+                for (int j = 0; j < CG; ++j) gr[u][j] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int i = 0; i < CX; ++i) xr[u][i] = pro.apply(xr[u][i]);
+#pragma unroll
+            for (int j = 0; j < CG; ++j) {
+#pragma unroll
+                for (int i = 0; i < CX; ++i) acc[j][i] = fmaf(xr[u][i], gr[u][j], acc[j][i]);
+                acc[j][CX] += gr[u][j];
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < CG; ++j)
+#pragma unroll
+        for (int i = 0; i <= CX; ++i) {
+            const float t = wave_sum(acc[j][i]);
+            if (lane == 0) wred[wv][j * (CX + 1) + i] = t;
+        }
+    __syncthreads();
+    if (threadIdx.x < NE) {
+        const int e = threadIdx.x;
+        part[int64_t(e) * gridDim.x + blockIdx.x] = (wred[0][e] + wred[1][e]) + (wred[2][e] + wred[3][e]);
+    }
+}
+
+// G = sum over the workgroup partials (part[entry][blk], fixed-order shuffle tree per entry);
+// dw += escale * G, dscale += sum W*G, dcbias[co] += G[co][Ct], dbias += sum_co G[co][Ct].
+// LANES lanes of a wave share one entry: each sums a strided slice of the partials (8 loads in
+// flight), then the lanes combine with a fixed xor-shuffle tree.
+template <int LANES>
+__global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict__ part, int nblk, int ne, int Ct,
+                                                        const float *__restrict__ w, const float *__restrict__ escale,
+                                                        float *dw, float *dscale, float *dbias, float *dcbias) {
+    __shared__ float red[8];
+    const int lane = threadIdx.x % LANES;
+    const int e = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
+    float sum = 0.f;
+    if (e < ne) {
+        const float *p = part + int64_t(e) * nblk;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int b0 = lane; b0 < nblk; b0 += 8 * LANES) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u * LANES < nblk) acc[u] += p[b0 + u * LANES];
+        }
+        sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+#pragma unroll
+    for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    float wg = 0.f, bs = 0.f;
+    if (e < ne && lane == 0) {
+        const int co = e / (Ct + 1), ci = e - co * (Ct + 1);
+        if (ci < Ct) {
+            const int64_t o = int64_t(co) * Ct + ci;
+            if (dw) dw[o] += escale ? sum * *escale : sum;
+            if (dscale) wg = w[o] * sum;
+        } else {
+            if (dcbias) dcbias[co] += sum;
+            bs = sum;
+        }
+    }
+    if (dscale) {
+        wg = block_sum<float, 256>(wg, red);
+        if (threadIdx.x == 0) atomicAdd(dscale, wg);
+    }
+    if (dbias) {
+        bs = block_sum<float, 256>(bs, red + 4);
+        if (threadIdx.x == 0) atomicAdd(dbias, bs);
+    }
+}
+
+int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+bool reg_path(const vq3d_conv_desc *d) {
+    auto p2 = [](int c) { return c == 1 || c == 2 || c == 4 || c == 8; };
+    return d->cin2 == 0 && p2(d->cin) && p2(d->cout) && d->cout * (d->cin + 1) <= 40;
+}
+
+PwwArgs plan(const vq3d_conv_desc *d, int &ytiles, int &nbx, size_t &lds) {
+    PwwArgs a = {};
+    a.nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    a.Ca = d->cin;
+    a.Cb = d->cin2;
+    a.N = d->cout;
+    const int Ct = a.Ca + a.Cb;
+    a.ones = Ct;
+    a.ne = a.N * (Ct + 1);
+    a.Xp = round_up(Ct + 1, TI);
+    a.Gp = round_up(a.N, TO);
+    a.nti = a.Xp / TI;
+    const int ntiles = a.nti * (a.Gp / TO);
+    a.tpb = std::min(ntiles, 64);
+    a.S = 256 / a.tpb;
+    ytiles = (ntiles + a.tpb - 1) / a.tpb;
+    // segment: ~16 KB of fp32 slabs (several workgroups per CU hide the load latency)
+    const int row_bytes = (a.Xp + a.Gp) * 4;
+    a.seg = 1024;
+    while (a.seg > 16 && size_t(a.seg) * row_bytes > 16 * 1024) a.seg /= 2;
+    a.fa = FastDiv(uint32_t(std::max(1, a.Ca)));
+    a.fb = FastDiv(uint32_t(std::max(1, a.Cb)));
+    a.fn = FastDiv(uint32_t(a.N));
+    lds = std::max(size_t(a.seg) * row_bytes, size_t(256) * TI * TO * 4);
+    const int64_t nseg = (a.nvox + a.seg - 1) / a.seg;
+    nbx = int(std::max<int64_t>(1, std::min<int64_t>(nseg, std::max(1, kMaxBlocks / ytiles))));
+    if (reg_path(d)) {  // 4 x 256 voxels per workgroup-iteration
+        ytiles = 1;
+        nbx = int(std::max<int64_t>(1, std::min<int64_t>((a.nvox + 1023) / 1024, kMaxBlocks)));
+    }
+    return a;
+}
+
+}  // namespace
+
+size_t pw_wgrad_workspace(const vq3d_conv_desc *d) {
+    int ytiles, nbx;
+    size_t lds;
+    const PwwArgs a = plan(d, ytiles, nbx, lds);
+    return size_t(nbx) * a.ne * 4;
+}
+
+int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
+                    const float *pro_b, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
+                    float *dcbias, void *workspace, size_t ws_bytes, hipStream_t s) {
+    int ytiles, nbx;
+    size_t lds;
+    PwwArgs a = plan(d, ytiles, nbx, lds);
+    if (!workspace || ws_bytes < size_t(nbx) * a.ne * 4) return fail("conv3d_bwd_weight: workspace too small");
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    a.vec = al(x) && al(g) && (!x2 || al(x2));
+    float *part = static_cast<float *>(workspace);
+    const dim3 grid{unsigned(nbx), unsigned(ytiles), 1u};
+    if (reg_path(d) && a.vec) {
+        const int key = d->cin * 16 + d->cout;
+        const bool bf = d->dtype == VQ3D_BF16;
+#define REG(CX, CG)                                                                                            \
+    case CX * 16 + CG:                                                                                         \
+        if (bf)                                                                                                \
+            k_pw_wgrad_reg<bf16_t, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,  \
+                                                               d->pro_kind, pro_a, pro_b, part);              \
+        else                                                                                                   \
+            k_pw_wgrad_reg<float, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,     \
+                                                              d->pro_kind, pro_a, pro_b, part);               \
+        break;
+        switch (key) {
+            REG(1, 1) REG(1, 2) REG(1, 4) REG(1, 8) REG(2, 1) REG(2, 2) REG(2, 4) REG(2, 8)
+            REG(4, 1) REG(4, 2) REG(4, 4) REG(4, 8) REG(8, 1) REG(8, 2) REG(8, 4)
+        default: return fail("conv3d_bwd_weight: no register-path kernel");
+        }
+#undef REG
+    } else if (d->dtype == VQ3D_BF16)
+        k_pw_wgrad<bf16_t><<<grid, 256, lds, s>>>(a, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g,
+                                                   d->pro_kind, pro_a, pro_b, part);
+    else
+        k_pw_wgrad<float><<<grid, 256, lds, s>>>(a, (const float *)x, (const float *)x2, (const float *)g,
+                                                  d->pro_kind, pro_a, pro_b, part);
+    const int Ct = a.Ca + a.Cb;
+    int lanes = 1;
+    while (lanes < 64 && lanes * 32 < nbx) lanes *= 2;
+#define RED(L)                                                                                                 \
+    k_pw_wgrad_reduce<L><<<(a.ne + 256 / L - 1) / (256 / L), 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw,    \
+                                                                          dscale, dbias, dcbias)
+    switch (lanes) {
+    case 1: RED(1); break;
+    case 2: RED(2); break;
+    case 4: RED(4); break;
+    case 8: RED(8); break;
+    case 16: RED(16); break;
+    case 32: RED(32); break;
+    default: RED(64); break;
+    }
+#undef RED
+    return check_launch("conv3d_bwd_weight(pointwise)");
+}
+
+}  // namespace vq3d

@@ -40,7 +40,8 @@ class DgradEpilogue(ctypes.Structure):
 _SIGS = {
     "vq3d_conv3d_fwd": (c_int, [P, P, P, P, P, P, P, P, P]),
     "vq3d_conv3d_bwd_data": (c_int, [P, P, P, P, P, P, P, P, P, P, P]),
-    "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, c_size, P]),
+    "vq3d_conv3d_bwd_weight_workspace_size": (c_size, [P]),
     "vq3d_upsample2x_fwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P]),
     "vq3d_upsample2x_bwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),

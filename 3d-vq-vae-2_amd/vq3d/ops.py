@@ -108,6 +108,17 @@ def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, r
     return y
 
 
+_ws_cache = {}
+
+
+def wgrad_workspace_bytes(desc):
+    key = bytes(desc)
+    r = _ws_cache.get(key)
+    if r is None:
+        r = _ws_cache[key] = int(L.query("vq3d_conv3d_bwd_weight_workspace_size", ctypes.byref(desc)))
+    return r
+
+
 def _depi(aux, aux_b, addend):
     """dgrad epilogue: aux with aux_b=None -> derivative of the conv's own prologue (aux = its
     input before the prologue); with aux_b -> aux is an activated tensor elu(z) + aux_b."""
@@ -132,8 +143,10 @@ def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None
         epi = _depi(aux, aux_b, addend)
         L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), _p(gscale), L.ptr(w), _p(pa),
                ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), s)
+    wsb = wgrad_workspace_bytes(desc)
+    ws = workspace(wsb, x.device) if wsb else None
     L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb), L.ptr(w),
-           _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), s)
+           _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), _p(ws), wsb, s)
     return gx, gx2
 
 

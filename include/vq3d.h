@@ -89,16 +89,21 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
                          const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2,
                          float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
 
-/* Gradient w.r.t. the weight and the forward-epilogue parameters, ACCUMULATED (+=) with fp32
- * atomics into the fp32 gradient buffers (any may be NULL):
+/* Gradient w.r.t. the weight and the forward-epilogue parameters, ACCUMULATED (+=) into the
+ * fp32 gradient buffers (any may be NULL):
  *   dw     += scale * G,  G[co,ci,t] = sum_v g[v,co] * prologue(x)[nbr(v,t),ci]
  *   dscale += sum(W * G)     (epilogue `scale`; needs w and epi_scale)
  *   dbias  += sum(g)         (epilogue scalar bias)
  *   dcbias += sum_v g[v,co]  (nn.Conv3d bias)
- * Atomic accumulation makes the last bits order-dependent (like cuDNN's wgrad). */
+ * `workspace` (vq3d_conv3d_bwd_weight_workspace_size(d) bytes, caller-owned, contents
+ * scratch) holds per-workgroup partials that a second kernel sums in a fixed order
+ * (1x1x1 convs: deterministic); k > 1 engines accumulate with fp32 atomics, so their last
+ * bits are order-dependent like cuDNN's wgrad. */
+size_t vq3d_conv3d_bwd_weight_workspace_size(const vq3d_conv_desc *d);
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g,
                            const float *pro_a, const float *pro_b, const float *w, const float *epi_scale,
-                           float *dw, float *dscale, float *dbias, float *dcbias, vq3d_stream_t stream);
+                           float *dw, float *dscale, float *dbias, float *dcbias, void *workspace,
+                           size_t workspace_bytes, vq3d_stream_t stream);
 
 /* --- trilinear x2 upsample, align_corners=False (nn.Upsample in ResizeConv3D, layers.py:591-597) --- */
 int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,

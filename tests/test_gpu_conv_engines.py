@@ -117,3 +117,45 @@ def test_tiled_wgrad_matches_valu(gpu, case):
     assert rel(mc, rc) < 1.5e-2, ("dcbias", case)
     assert abs(float(mb) - float(rb)) <= 1e-2 * float(rc.abs().sum()) + 1e-3
     assert abs(float(ms) - float(rs)) <= 2e-2 * (float((wt * rw).abs().sum()) / max(abs(float(sc)), 1e-3)) + 1e-3
+
+
+PW_CASES = [
+    # (cin, cin2, cout, (h, w, d))
+    (9, 0, 18, (16, 16, 8)),
+    (18, 0, 9, (8, 8, 8)),
+    (4, 0, 2, (32, 16, 64)),
+    (2, 0, 4, (8, 8, 8)),
+    (1, 0, 2, (5, 7, 3)),
+    (16, 2, 18, (8, 8, 4)),
+    (64, 8, 72, (4, 4, 2)),
+    (256, 0, 32, (4, 4, 2)),
+    (72, 0, 36, (8, 8, 8)),
+]
+
+
+@pytest.mark.parametrize("case", PW_CASES)
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pointwise_wgrad_vs_torch(gpu, case, dt):
+    """1x1x1 weight / conv-bias / scalar gradients vs a plain torch fp32 einsum of the same
+    (bf16-representable) inputs, with the ELU-affine prologue and a concatenated second input."""
+    from vq3d import ops
+    cin, cin2, cout, (h, w, d) = case
+    g = torch.Generator(device=gpu).manual_seed(7 + cin * 31 + cout)
+    x = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    x2 = rnd((2, cin2, h, w, d), gpu, g).contiguous(memory_format=CL) if cin2 else None
+    wt = rnd((cout, cin + cin2, 1, 1, 1), gpu, g, 0.3)
+    a, b, sc = rnd((1,), gpu, g, 0.1), rnd((1,), gpu, g, 0.1), rnd((1,), gpu, g)
+    gy = rnd((2, cout, h, w, d), gpu, g).contiguous(memory_format=CL)
+    xs = x if x2 is None else torch.cat([x, x2], 1)
+    xp = torch.nn.functional.elu(xs.float() + a) + b
+    G = torch.einsum("bchwd,bohwd->oc", xp.double(), gy.double())
+    dw = torch.zeros_like(wt)
+    dscale, dbias, dcb = torch.zeros(1, device=gpu), torch.zeros(1, device=gpu), torch.zeros(cout, device=gpu)
+    ops.conv_bwd(gy.to(dt), x.to(dt), wt, ops.ConvGeom(1), pro=(a, b), x2=None if x2 is None else x2.to(dt),
+                 want_gx=False, dw=dw, dscale=dscale, dbias=dbias, dcbias=dcb, escale=sc)
+    tol = 1e-4 if dt == torch.float32 else 1.5e-2
+    assert rel(dw.view(cout, -1), (G * sc.double()).float()) < tol
+    assert rel(dcb, gy.double().sum((0, 2, 3, 4)).float()) < tol
+    assert abs(float(dbias) - float(gy.double().sum())) <= tol * float(gy.abs().sum()) + 1e-4
+    ref_s = float((wt.view(cout, -1).double() * G).sum())
+    assert abs(float(dscale) - ref_s) <= tol * float((wt.view(cout, -1).double() * G).abs().sum()) + 1e-4

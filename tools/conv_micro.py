@@ -47,8 +47,10 @@ def main():
 
     def _wgrad_only():
         desc, _ = ops.conv_desc(x.dtype, 1, cin, 0, cout, h, w, d, geom, 0)
+        wsb = ops.wgrad_workspace_bytes(desc)
+        ws = ops.workspace(wsb, x.device) if wsb else None
         L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), None, L.ptr(g), None, None, L.ptr(wt), None,
-               L.ptr(dw), None, None, None, L.stream())
+               L.ptr(dw), None, None, None, None if ws is None else L.ptr(ws), wsb, L.stream())
 
     for _ in range(3):
         run()
