@@ -87,25 +87,6 @@ __device__ __forceinline__ void atomic_add_f(float *p, float v) {
     if (p) atomicAdd(p, v);
 }
 
-// forward epilogue (vq3d_conv_epilogue), by value
-template <typename T>
-struct FwdEpi {
-    const float *scale, *bias, *cbias;
-    const T *res;
-    int res_up2, act;
-    const float *act_a, *act_b;
-};
-
-// backward-data epilogue (vq3d_dgrad_epilogue) resolved on the host: mode 0 none,
-// 1 elu'(aux + *p) (pre-prologue input), 2 from activated aux with offset *p
-template <typename T>
-struct BwdEpi {
-    const T *aux;
-    int mode;
-    const float *p;
-    const T *addend;
-};
-
 template <typename T>
 __device__ __forceinline__ ActDeriv make_deriv(const BwdEpi<T> &e) {
     ActDeriv d;
@@ -681,7 +662,8 @@ static int launch_pw(const vq3d_conv_desc *d, const ConvArgs &a, const void *in,
 
 template <typename T>
 static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w, const float *pa,
-                      const float *pb, const vq3d_conv_epilogue *epi, void *y, hipStream_t s) {
+                      const float *pb, const vq3d_conv_epilogue *epi, void *y, void *ws, size_t ws_bytes,
+                      hipStream_t s) {
     ConvArgs a = make_args(d, pa, pb);
     const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
     FwdEpi<T> fe = make_fwd_epi<T>(epi);
@@ -693,6 +675,11 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
         return launch_pw<T, false>(d, a, x, x2, w, fe, be, nullptr, y, nullptr, nullptr, nullptr, s);
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
+        if (lines_applicable(d, false)) {
+            BwdEpi<T> be = {};
+            return launch_lines(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws,
+                                ws_bytes, s);
+        }
         if (!mfma_disabled()) {
             MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
                                 d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR);
@@ -725,7 +712,7 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
 template <typename T>
 static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
                         const float *pa, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2, float *dpre,
-                        float *dpost, hipStream_t s) {
+                        float *dpost, void *ws, size_t ws_bytes, hipStream_t s) {
     ConvArgs a = make_args(d, pa, nullptr);
     const int Ct = d->cin + d->cin2;
     const int64_t nvox = int64_t(d->batch) * d->in_h * d->in_w * d->in_d;
@@ -737,6 +724,11 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
         // stride-1 backward-data == forward conv of g with the flipped, transposed kernel
+        if (lines_applicable(d, true)) {
+            FwdEpi<T> fe = {};
+            return launch_lines(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws,
+                                ws_bytes, s);
+        }
         if (!mfma_disabled() && d->stride == 1) {
             const int pp = d->kernel - 1 - d->pad;
             MPlan m = plan_mfma(d->batch, d->cout, 0, Ct, d->out_h, d->out_w, d->out_d, d->in_h, d->in_w, d->in_d,
@@ -830,30 +822,38 @@ using namespace vq3d;
 extern "C" {
 
 int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w, const float *pro_a,
-                    const float *pro_b, const vq3d_conv_epilogue *epi, void *y, vq3d_stream_t stream) {
+                    const float *pro_b, const vq3d_conv_epilogue *epi, void *y, void *workspace,
+                    size_t workspace_bytes, vq3d_stream_t stream) {
     if (int r = validate(d)) return r;
     if (!x || !w || !y || (d->cin2 && !x2)) return fail("conv3d_fwd: null pointer");
     if (d->pro_kind != VQ3D_PRO_NONE && !pro_a) return fail("conv3d_fwd: prologue needs pro_a");
     if (d->pro_kind == VQ3D_PRO_ELU_ADD && !pro_b) return fail("conv3d_fwd: ELU prologue needs pro_b");
-    return d->dtype == VQ3D_F32 ? launch_fwd<float>(d, x, x2, w, pro_a, pro_b, epi, y, as_stream(stream))
-                                : launch_fwd<bf16_t>(d, x, x2, w, pro_a, pro_b, epi, y, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    return d->dtype == VQ3D_F32
+               ? launch_fwd<float>(d, x, x2, w, pro_a, pro_b, epi, y, workspace, workspace_bytes, s)
+               : launch_fwd<bf16_t>(d, x, x2, w, pro_a, pro_b, epi, y, workspace, workspace_bytes, s);
 }
 
 int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
                          const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2, float *dpro_pre,
-                         float *dpro_post, vq3d_stream_t stream) {
+                         float *dpro_post, void *workspace, size_t workspace_bytes, vq3d_stream_t stream) {
     if (int r = validate(d)) return r;
     if (!g || !w || !gx || (d->cin2 && !gx2)) return fail("conv3d_bwd_data: null pointer");
     if (d->pro_kind != VQ3D_PRO_NONE && !pro_a) return fail("conv3d_bwd_data: prologue needs pro_a");
     if (epi && epi->aux_kind == 1 && epi->aux && !epi->aux_b)
         return fail("conv3d_bwd_data: aux_kind 1 needs aux_b");
     hipStream_t s = as_stream(stream);
-    return d->dtype == VQ3D_F32 ? launch_dgrad<float>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s)
-                                : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, s);
+    return d->dtype == VQ3D_F32
+               ? launch_dgrad<float>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, workspace,
+                                     workspace_bytes, s)
+               : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, workspace,
+                                      workspace_bytes, s);
 }
 
-size_t vq3d_conv3d_bwd_weight_workspace_size(const vq3d_conv_desc *d) {
+size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
     if (validate(d)) return 0;
+    if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
+    if (pass == VQ3D_PASS_BWD_DATA) return lines_workspace(d, true);
     return is_pointwise(d) ? pw_wgrad_workspace(d) : 0;
 }
 

@@ -5,6 +5,26 @@
 
 namespace vq3d {
 
+// forward epilogue (vq3d_conv_epilogue), by value
+template <typename T>
+struct FwdEpi {
+    const float *scale, *bias, *cbias;
+    const T *res;
+    int res_up2, act;
+    const float *act_a, *act_b;
+};
+
+// backward-data epilogue (vq3d_dgrad_epilogue) resolved on the host: mode 0 none,
+// 1 elu'(aux + *p) (pre-prologue input), 2 from activated aux with offset *p
+template <typename T>
+struct BwdEpi {
+    const T *aux;
+    int mode;
+    const float *p;
+    const T *addend;
+};
+
+
 // 1x1x1 weight gradient (and the epilogue-parameter gradients of that conv), ACCUMULATED:
 //   G[co][ci] = sum_v g[v][co] * pro(x|x2)[v][ci]
 //   dw += escale * G ; dscale += sum W*G ; dbias += sum g ; dcbias[co] += sum_v g[v][co]
@@ -14,5 +34,13 @@ size_t pw_wgrad_workspace(const vq3d_conv_desc *d);
 int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
                     const float *pro_b, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
                     float *dcbias, void *workspace, size_t ws_bytes, hipStream_t s);
+
+// k^3 conv on the MFMA "lines" engine (conv_lines.hip): forward, or (dgrad) stride-1 backward-data.
+// lines_applicable: bf16 and a geometry the engine plans; lines_workspace: packed-weight bytes.
+bool lines_applicable(const vq3d_conv_desc *d, bool dgrad);
+size_t lines_workspace(const vq3d_conv_desc *d, bool dgrad);
+int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void *x2, const float *w, const float *pa,
+                 const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
+                 void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
 }  // namespace vq3d

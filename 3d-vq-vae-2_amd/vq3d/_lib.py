@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("VQ3D_LIB", os.path.join(_PKG_ROOT, "lib", "libvq3d.so
 F32, BF16 = 0, 1
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
 PRO_NONE, PRO_ADD, PRO_ELU_ADD = 0, 1, 2
+PASS_FWD, PASS_BWD_DATA, PASS_BWD_WEIGHT = 0, 1, 2
 
 c_int, c_i64, c_size, c_float, c_void = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
 P = ctypes.c_void_p
@@ -38,10 +39,10 @@ class DgradEpilogue(ctypes.Structure):
 
 
 _SIGS = {
-    "vq3d_conv3d_fwd": (c_int, [P, P, P, P, P, P, P, P, P]),
-    "vq3d_conv3d_bwd_data": (c_int, [P, P, P, P, P, P, P, P, P, P, P]),
+    "vq3d_conv3d_workspace_size": (c_size, [P, c_int]),
+    "vq3d_conv3d_fwd": (c_int, [P, P, P, P, P, P, P, P, P, c_size, P]),
+    "vq3d_conv3d_bwd_data": (c_int, [P, P, P, P, P, P, P, P, P, P, P, c_size, P]),
     "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, c_size, P]),
-    "vq3d_conv3d_bwd_weight_workspace_size": (c_size, [P]),
     "vq3d_upsample2x_fwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P]),
     "vq3d_upsample2x_bwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),

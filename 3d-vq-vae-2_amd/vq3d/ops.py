@@ -103,20 +103,27 @@ def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, r
     ak, aa, ab = _act(act)
     epi = L.ConvEpilogue(scale=_p(scale), bias=_p(bias), cbias=_p(cbias), residual=_p(residual),
                          residual_up2=int(residual_up2), act=ak, act_a=_p(aa), act_b=_p(ab))
+    ws, wsb = _ws(desc, L.PASS_FWD, x.device)
     L.call("vq3d_conv3d_fwd", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(w), _p(pa), _p(pb),
-           ctypes.byref(epi), L.ptr(y), L.stream())
+           ctypes.byref(epi), L.ptr(y), _p(ws), wsb, L.stream())
     return y
 
 
 _ws_cache = {}
 
 
-def wgrad_workspace_bytes(desc):
-    key = bytes(desc)
+def conv_workspace_bytes(desc, pass_):
+    """Scratch bytes one conv launch needs (vq3d_conv3d_workspace_size), cached per descriptor."""
+    key = (bytes(desc), pass_)
     r = _ws_cache.get(key)
     if r is None:
-        r = _ws_cache[key] = int(L.query("vq3d_conv3d_bwd_weight_workspace_size", ctypes.byref(desc)))
+        r = _ws_cache[key] = int(L.query("vq3d_conv3d_workspace_size", ctypes.byref(desc), pass_))
     return r
+
+
+def _ws(desc, pass_, device):
+    n = conv_workspace_bytes(desc, pass_)
+    return (workspace(n, device), n) if n else (None, 0)
 
 
 def _depi(aux, aux_b, addend):
@@ -141,10 +148,10 @@ def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None
         gx = new_act(b, cin, h, wd, d, x.dtype, x.device)
         gx2 = None if x2 is None else new_act(b, cin2, h, wd, d, x.dtype, x.device)
         epi = _depi(aux, aux_b, addend)
+        ws, wsb = _ws(desc, L.PASS_BWD_DATA, x.device)
         L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), _p(gscale), L.ptr(w), _p(pa),
-               ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), s)
-    wsb = wgrad_workspace_bytes(desc)
-    ws = workspace(wsb, x.device) if wsb else None
+               ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), _p(ws), wsb, s)
+    ws, wsb = _ws(desc, L.PASS_BWD_WEIGHT, x.device)
     L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb), L.ptr(w),
            _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), _p(ws), wsb, s)
     return gx, gx2

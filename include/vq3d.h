@@ -74,10 +74,17 @@ typedef struct vq3d_dgrad_epilogue {
     const void *addend;     /* gradient added after the derivative, or NULL */
 } vq3d_dgrad_epilogue;
 
-/* --- 3-D convolution (replaces nn.Conv3d / F.pad circular, layers.py:124-171,535,377,490,508) --- */
+/* --- 3-D convolution (replaces nn.Conv3d / F.pad circular, layers.py:124-171,535,377,490,508) ---
+ * Every conv entry point takes a caller-owned scratch `workspace` of at least
+ * vq3d_conv3d_workspace_size(d, pass) bytes (may be 0 -> NULL allowed): packed bf16 weight
+ * fragments for the k^3 MFMA engine, per-workgroup partials for the weight gradient.  Its
+ * contents are scratch; it must stay allocated until the launches on `stream` complete. */
+enum { VQ3D_PASS_FWD = 0, VQ3D_PASS_BWD_DATA = 1, VQ3D_PASS_BWD_WEIGHT = 2 };
+size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass);
+
 int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w,
                     const float *pro_a, const float *pro_b, const vq3d_conv_epilogue *epi,
-                    void *y, vq3d_stream_t stream);
+                    void *y, void *workspace, size_t workspace_bytes, vq3d_stream_t stream);
 
 /* Gradient w.r.t. the input(s).  g = dL/dy (y grid, cout channels); gscale: device scalar
  * multiplying g (the PreAct `scale`) or NULL.  gx (and gx2 for input 2) receive the result,
@@ -87,7 +94,8 @@ int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, cons
  * either may be NULL. */
 int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
                          const float *pro_a, const vq3d_dgrad_epilogue *epi, void *gx, void *gx2,
-                         float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
+                         float *dpro_pre, float *dpro_post, void *workspace, size_t workspace_bytes,
+                         vq3d_stream_t stream);
 
 /* Gradient w.r.t. the weight and the forward-epilogue parameters, ACCUMULATED (+=) into the
  * fp32 gradient buffers (any may be NULL):
@@ -95,11 +103,9 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
  *   dscale += sum(W * G)     (epilogue `scale`; needs w and epi_scale)
  *   dbias  += sum(g)         (epilogue scalar bias)
  *   dcbias += sum_v g[v,co]  (nn.Conv3d bias)
- * `workspace` (vq3d_conv3d_bwd_weight_workspace_size(d) bytes, caller-owned, contents
- * scratch) holds per-workgroup partials that a second kernel sums in a fixed order
+ * The workspace holds per-workgroup partials that a second kernel sums in a fixed order
  * (1x1x1 convs: deterministic); k > 1 engines accumulate with fp32 atomics, so their last
  * bits are order-dependent like cuDNN's wgrad. */
-size_t vq3d_conv3d_bwd_weight_workspace_size(const vq3d_conv_desc *d);
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g,
                            const float *pro_a, const float *pro_b, const float *w, const float *epi_scale,
                            float *dw, float *dscale, float *dbias, float *dcbias, void *workspace,

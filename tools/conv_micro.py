@@ -2,7 +2,8 @@
 """Micro-benchmark one conv launch (forward or backward-data / weight) of the vq3d library.
 
     python3 tools/conv_micro.py CIN COUT H W D K S P CIRC [fwd|dgrad|wgrad] [bf16|fp32] [iters]
-Prints the average launch time (HIP events on the launch stream) and algorithmic GB/s."""
+Prints the average launch time (HIP events around a graph replay of `iters` launches) and
+algorithmic GB/s."""
 import os
 import sys
 
@@ -42,23 +43,32 @@ def main():
         desc, _ = ops.conv_desc(x.dtype, 1, cin, 0, cout, h, w, d, geom, 0)
         gx = torch.empty_like(x)
         epi = L.DgradEpilogue()
+        ws, wsb = ops._ws(desc, L.PASS_BWD_DATA, x.device)
         L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), None, L.ptr(wt), None, ctypes.byref(epi),
-               L.ptr(gx), None, None, None, L.stream())
+               L.ptr(gx), None, None, None, None if ws is None else L.ptr(ws), wsb, L.stream())
 
     def _wgrad_only():
         desc, _ = ops.conv_desc(x.dtype, 1, cin, 0, cout, h, w, d, geom, 0)
-        wsb = ops.wgrad_workspace_bytes(desc)
-        ws = ops.workspace(wsb, x.device) if wsb else None
+        ws, wsb = ops._ws(desc, L.PASS_BWD_WEIGHT, x.device)
         L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), None, L.ptr(g), None, None, L.ptr(wt), None,
                L.ptr(dw), None, None, None, None if ws is None else L.ptr(ws), wsb, L.stream())
 
     for _ in range(3):
         run()
+    # capture the launches in a HIP graph so host-side (Python / ctypes) overhead is not timed
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            for _ in range(iters):
+                run()
+    graph.replay()
+    torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(iters):
-        run()
+    graph.replay()
     e1.record(st)
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters

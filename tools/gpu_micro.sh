@@ -1,0 +1,9 @@
+# micro timings of the main conv shapes (fwd / dgrad / wgrad), bf16
+set -o pipefail
+mkdir -p gpurun_out
+: > gpurun_out/micro.log
+for m in fwd dgrad wgrad; do
+for a in "9 9 128 128 32 3 1 1 1" "2 2 512 512 128 3 1 1 1" "1 1 128 128 32 3 1 1 1" "36 36 32 32 8 3 1 1 1" "16 16 8 8 2 3 1 1 1" "4 4 256 256 64 3 1 1 1" "4 4 512 512 128 4 2 1 1"; do
+  timeout -k 10 120 python tools/conv_micro.py $a $m bf16 20 >> gpurun_out/micro.log 2>&1 || exit 1
+done; done
+cat gpurun_out/micro.log
