@@ -628,6 +628,15 @@ static BwdEpi<T> make_bwd_epi(const vq3d_dgrad_epilogue *epi, int pro_kind, cons
     return e;
 }
 
+// VQ3D_LEGACY_PW=1 selects the LDS-slab pointwise kernel (k_pw) instead of pw_conv.hip
+static bool legacy_pw() {
+    static const bool on = [] {
+        const char *e = std::getenv("VQ3D_LEGACY_PW");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 template <typename T, bool DGRAD>
@@ -672,6 +681,7 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
     if (fe.act == VQ3D_ACT_ELU_AFFINE && (!fe.act_a || !fe.act_b)) return fail("conv: ELU_AFFINE needs act_a/b");
     if (is_pointwise(d)) {
         BwdEpi<T> be = {};
+        if (!legacy_pw()) return launch_pw1<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes, s);
         return launch_pw<T, false>(d, a, x, x2, w, fe, be, nullptr, y, nullptr, nullptr, nullptr, s);
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
@@ -720,6 +730,7 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
     BwdEpi<T> be = make_bwd_epi<T>(epi, d->pro_kind, pa);
     if (is_pointwise(d)) {
         FwdEpi<T> fe = {};
+        if (!legacy_pw()) return launch_pw1<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes, s);
         return launch_pw<T, true>(d, a, g, nullptr, w, fe, be, gscale, gx, gx2, dpre, dpost, s);
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
@@ -853,7 +864,7 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
 size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
     if (validate(d)) return 0;
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
-    if (pass == VQ3D_PASS_BWD_DATA) return lines_workspace(d, true);
+    if (pass == VQ3D_PASS_BWD_DATA) return is_pointwise(d) ? pw_dgrad_workspace(d) : lines_workspace(d, true);
     return is_pointwise(d) ? pw_wgrad_workspace(d) : 0;
 }
 

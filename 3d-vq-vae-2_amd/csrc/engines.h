@@ -12,6 +12,7 @@ struct FwdEpi {
     const T *res;
     int res_up2, act;
     const float *act_a, *act_b;
+    int oH, oW, oD;  // output grid (filled by engines that need voxel coordinates)
 };
 
 // backward-data epilogue (vq3d_dgrad_epilogue) resolved on the host: mode 0 none,
@@ -42,5 +43,14 @@ size_t lines_workspace(const vq3d_conv_desc *d, bool dgrad);
 int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void *x2, const float *w, const float *pa,
                  const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
                  void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
+
+// 1x1x1 conv forward / backward-data (pw_conv.hip), both storage dtypes
+// (dgrad with prologue-scalar partials on big grids: per-workgroup partials in `ws`,
+// pw_dgrad_workspace(d) bytes, summed in order by a second kernel)
+size_t pw_dgrad_workspace(const vq3d_conv_desc *d);
+template <typename T>
+int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w, const float *pa,
+               const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale, void *out,
+               void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
 }  // namespace vq3d

@@ -325,8 +325,15 @@ __global__ __launch_bounds__(256) void k_adam_amsgrad(float *__restrict__ p, con
                                                      float *__restrict__ m, float *__restrict__ v,
                                                      float *__restrict__ vmax, int64_t n, float beta1, float omb1,
                                                      float beta2, float omb2, float step_size, float bc2_sqrt,
-                                                     float eps) {
+                                                     float eps, const int64_t *__restrict__ step_dev, float lr) {
 #pragma clang fp contract(off)
+    if (step_dev) {  // bias corrections of step *step_dev + 1, as the host path computes them (double)
+        const double st = double(*step_dev + 1);
+        const double bc1 = 1.0 - pow(double(beta1), st);
+        const double bc2 = 1.0 - pow(double(beta2), st);
+        step_size = float(double(lr) / bc1);
+        bc2_sqrt = float(sqrt(bc2));
+    }
     for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
         const float gi = g[i];
         float mi = m[i];
@@ -340,6 +347,8 @@ __global__ __launch_bounds__(256) void k_adam_amsgrad(float *__restrict__ p, con
         vmax[i] = vm;
     }
 }
+
+__global__ void k_step_inc(int64_t *step) { *step += 1; }
 
 // ============================================================================ casts
 template <typename S, typename D>
@@ -552,8 +561,20 @@ int vq3d_adam_amsgrad(float *p, const float *g, float *m, float *v, float *vmax,
     const float step_size = float(double(lr) / bc1);
     const float bc2_sqrt = float(std::sqrt(bc2));
     k_adam_amsgrad<<<grid_for(n), 256, 0, as_stream(stream)>>>(p, g, m, v, vmax, n, beta1, float(1.0 - beta1), beta2,
-                                                               float(1.0 - beta2), step_size, bc2_sqrt, eps);
+                                                               float(1.0 - beta2), step_size, bc2_sqrt, eps,
+                                                               nullptr, lr);
     return check_launch("adam_amsgrad");
+}
+
+int vq3d_adam_amsgrad_dev(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr,
+                          float beta1, float beta2, float eps, int64_t *step, vq3d_stream_t stream) {
+    if (n <= 0 || !step) return fail("adam: bad sizes/step");
+    if (!p || !g || !m || !v || !vmax) return fail("adam: null pointer");
+    hipStream_t s = as_stream(stream);
+    k_adam_amsgrad<<<grid_for(n), 256, 0, s>>>(p, g, m, v, vmax, n, beta1, float(1.0 - beta1), beta2,
+                                              float(1.0 - beta2), 0.f, 1.f, eps, step, lr);
+    k_step_inc<<<1, 1, 0, s>>>(step);
+    return check_launch("adam_amsgrad_dev");
 }
 
 int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, int64_t n, vq3d_stream_t stream) {

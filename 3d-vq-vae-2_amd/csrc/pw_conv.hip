@@ -1,0 +1,490 @@
+// 1x1x1 convolution forward and backward-data (nn.Conv3d kernel_size=1: PreAct branch_conv1 /
+// branch_conv3 / skip_conv, proj, parse_input, out -- vqvae/layers.py:134-171, 377, 490, 508,
+// 535) with the block glue fused: prologue elu(x + a) + b on the input, scale / bias / conv-bias
+// / residual / ELU epilogue on the output (layers.py:176-195), or for backward-data the
+// activation derivative, the residual-gradient addend and the prologue-scalar partial sums.
+//
+// At these channel counts (1..256 in, 1..128 out) the op streams voxel rows and is bound by
+// memory, never by arithmetic.  Rows are 2..512 bytes and rarely 16-B aligned, and a per-lane
+// row access (lanes 18..144 bytes apart) costs far more than its bytes, so EVERY per-voxel
+// operand -- input(s), activation-derivative source, addend, residual, and the output -- moves
+// between HBM and LDS as a contiguous slab of SEG voxels with 16-byte coalesced accesses.  One
+// thread owns one voxel of the segment: it reads its rows from LDS, runs the channel GEMV in fp32
+// against weights broadcast from LDS (16 output channels at a time), applies the epilogue and
+// writes its output row back to the LDS out slab.
+#include "engines.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+constexpr int SEG = 256;  // threads per workgroup (= max voxels per segment)
+
+struct PwArgs {
+    int64_t nvox;
+    int Ca, Cb;      // input channels (x then x2); dgrad: Ca = conv Cout (g), Cb = 0
+    int Cin;         // Ca + Cb
+    int CinP;        // weight row stride in LDS (multiple of 8)
+    int N;           // output channels (fwd: Cout; dgrad: conv Cin + Cin2)
+    int N1, N2;      // outputs to tensor 1 / 2 (dgrad: cin_split / Cin2; fwd: N / 0)
+    int pro_kind;
+    const float *pro_a, *pro_b;
+    int vec;         // every slab base 16-B aligned
+    int segv, tpv;   // voxels per segment, threads per voxel (segv * tpv == 256)
+    // LDS slab offsets (elements of T) after the weights
+    int o_x, o_x2, o_aux, o_add, o_res, o_out, o_out2;
+};
+
+// contiguous global <-> LDS copy of n elements, 16-byte units when `vec`
+template <typename T>
+__device__ __forceinline__ void copy_in(T *__restrict__ dst, const T *__restrict__ src, int n, bool vec) {
+    constexpr int E = 16 / sizeof(T);
+    int i0 = 0;
+    if (vec) {
+        const int nq = n / E;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (int q = threadIdx.x; q < nq; q += SEG) d4[q] = s4[q];
+        i0 = nq * E;
+    }
+    for (int i = i0 + threadIdx.x; i < n; i += SEG) dst[i] = src[i];
+}
+
+template <typename T>
+__device__ __forceinline__ void copy_out(T *__restrict__ dst, const T *__restrict__ src, int n, bool vec) {
+    copy_in<T>(dst, src, n, vec);
+}
+
+template <typename T, int COT, bool DGRAD>
+__global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in, const T *__restrict__ in2,
+                                            const float *__restrict__ w, FwdEpi<T> fe, BwdEpi<T> be,
+                                            const float *__restrict__ gscale, T *__restrict__ out,
+                                            T *__restrict__ out2, float *dpre, float *dpost, float *part) {
+    extern __shared__ __attribute__((aligned(16))) float ws[];  // [N pad COT][CinP] then slabs
+    __shared__ float red[8];
+    const int tid = threadIdx.x;
+    const int NP = (a.N + COT - 1) / COT * COT;
+    const int Ct = DGRAD ? a.N : a.Cin;  // the weight's 2nd dim (conv input channels)
+    for (int e = tid; e < NP * a.CinP; e += SEG) {
+        const int o = e / a.CinP, c = e - o * a.CinP;
+        float val = 0.f;
+        if (o < a.N && c < a.Cin) val = DGRAD ? w[int64_t(c) * Ct + o] : w[int64_t(o) * Ct + c];
+        ws[e] = val;
+    }
+    T *sl = reinterpret_cast<T *>(ws + NP * a.CinP);
+    T *sx = sl + a.o_x, *sx2 = sl + a.o_x2, *saux = sl + a.o_aux, *sadd = sl + a.o_add, *sres = sl + a.o_res;
+    T *sout = sl + a.o_out, *sout2 = sl + a.o_out2;
+    const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
+    const float gs = gscale ? *gscale : 1.f;
+    const float sc = fe.scale ? *fe.scale : 1.f, bias = fe.bias ? *fe.bias : 0.f;
+    const float aa = fe.act_a ? *fe.act_a : 0.f, ab = fe.act_b ? *fe.act_b : 0.f;
+    ActDeriv dv;
+    dv.mode = (DGRAD && be.aux) ? be.mode : 0;
+    dv.p = (dv.mode && be.p) ? *be.p : 0.f;
+    const bool res_slab = !DGRAD && fe.res && !fe.res_up2;
+    float pre = 0.f, post = 0.f;
+    const int64_t nseg = (a.nvox + a.segv - 1) / a.segv;
+    const int vt = tid / a.tpv, part_o = tid - vt * a.tpv;  // this thread's voxel and output-tile phase
+
+    for (int64_t sg = blockIdx.x; sg < nseg; sg += gridDim.x) {
+        const int64_t v0 = sg * a.segv;
+        const int nv = int(min<int64_t>(a.segv, a.nvox - v0));
+        __syncthreads();
+        copy_in<T>(sx, in + v0 * a.Ca, nv * a.Ca, a.vec);
+        if (a.Cb) copy_in<T>(sx2, in2 + v0 * a.Cb, nv * a.Cb, a.vec);
+        if (DGRAD && dv.mode) copy_in<T>(saux, be.aux + v0 * a.N1, nv * a.N1, a.vec);
+        if (DGRAD && be.addend) copy_in<T>(sadd, be.addend + v0 * a.N1, nv * a.N1, a.vec);
+        if (res_slab) copy_in<T>(sres, fe.res + v0 * a.N, nv * a.N, a.vec);
+        __syncthreads();
+        if (vt < nv) {
+            const int tid = vt;  // slab row of this thread's voxel
+            const int64_t v = v0 + vt;
+            const T *xr = sx + tid * a.Ca;
+            const T *xr2 = sx2 + tid * a.Cb;
+            int h0 = 0, h1 = 0, w0i = 0, w1i = 0, d0 = 0, d1 = 0, b = 0;
+            float lh = 0.f, lw = 0.f, ldd = 0.f;
+            if (!DGRAD && fe.res && fe.res_up2) {
+                int64_t t = v;
+                const int od = int(t % fe.oD); t /= fe.oD;
+                const int ow = int(t % fe.oW); t /= fe.oW;
+                const int oh = int(t % fe.oH);
+                b = int(t / fe.oH);
+                up_coeff(oh, fe.oH / 2, h0, h1, lh);
+                up_coeff(ow, fe.oW / 2, w0i, w1i, lw);
+                up_coeff(od, fe.oD / 2, d0, d1, ldd);
+            }
+            for (int o0 = part_o * COT; o0 < a.N; o0 += a.tpv * COT) {
+                float acc[COT];
+#pragma unroll
+                for (int j = 0; j < COT; ++j) acc[j] = 0.f;
+                for (int c0 = 0; c0 < a.Cin; c0 += 8) {
+                    float xv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int c = c0 + j;
+                        float val = c < a.Ca ? ld(xr + c) : (c < a.Cin ? ld(xr2 + (c - a.Ca)) : 0.f);
+                        if (!DGRAD && pro.kind != VQ3D_PRO_NONE && c < a.Cin) val = pro.apply(val);
+                        xv[j] = val;
+                    }
+#pragma unroll
+                    for (int j = 0; j < COT; ++j) {
+                        const float4 w0 = *reinterpret_cast<const float4 *>(ws + (o0 + j) * a.CinP + c0);
+                        const float4 w1 = *reinterpret_cast<const float4 *>(ws + (o0 + j) * a.CinP + c0 + 4);
+                        float s = acc[j];
+                        s = fmaf(xv[0], w0.x, s);
+                        s = fmaf(xv[1], w0.y, s);
+                        s = fmaf(xv[2], w0.z, s);
+                        s = fmaf(xv[3], w0.w, s);
+                        s = fmaf(xv[4], w1.x, s);
+                        s = fmaf(xv[5], w1.y, s);
+                        s = fmaf(xv[6], w1.z, s);
+                        s = fmaf(xv[7], w1.w, s);
+                        acc[j] = s;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < COT; ++j) {
+                    const int o = o0 + j;
+                    if (o >= a.N) break;
+                    float val = acc[j];
+                    if (!DGRAD) {
+                        if (fe.scale) val = val * sc;
+                        if (fe.bias) val = val + bias;
+                        if (fe.cbias) val = val + fe.cbias[o];
+                        if (res_slab) {
+                            val = val + ld(sres + tid * a.N + o);
+                        } else if (fe.res) {
+                            const int rH = fe.oH / 2, rW = fe.oW / 2, rD = fe.oD / 2;
+                            auto R = [&](int hh, int ww, int dd) {
+                                return ld(fe.res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.N + o);
+                            };
+                            val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0i, d0) + ldd * R(h0, w0i, d1)) +
+                                                      lw * ((1.f - ldd) * R(h0, w1i, d0) + ldd * R(h0, w1i, d1))) +
+                                         lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0i, d0) + ldd * R(h1, w0i, d1)) +
+                                               lw * ((1.f - ldd) * R(h1, w1i, d0) + ldd * R(h1, w1i, d1))));
+                        }
+                        st(sout + tid * a.N + o, epi_act(fe.act, val, aa, ab));
+                    } else {
+                        if (gscale) val = val * gs;
+                        if (o < a.N1) {
+                            const int e = tid * a.N1 + o;
+                            pre += val;
+                            if (dv.mode) val = val * dv(ld(saux + e));
+                            post += val;
+                            if (be.addend) val = val + ld(sadd + e);
+                            st(sout + e, val);
+                        } else {
+                            st(sout2 + tid * a.N2 + (o - a.N1), val);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        copy_out<T>(out + v0 * a.N1, sout, nv * a.N1, a.vec);
+        if (a.N2) copy_out<T>(out2 + v0 * a.N2, sout2, nv * a.N2, a.vec);
+    }
+    if (DGRAD && (dpre || dpost)) {
+        pre = block_sum<float, SEG>(pre, red);
+        post = block_sum<float, SEG>(post, red + 4);
+        if (tid == 0) {
+            if (part) {  // per-workgroup partials, summed in order by k_sum_partials
+                part[blockIdx.x] = pre;
+                part[gridDim.x + blockIdx.x] = post;
+            } else {
+                if (dpre) atomicAdd(dpre, pre);
+                if (dpost) atomicAdd(dpost, post);
+            }
+        }
+    }
+}
+
+// *dpre += sum(part[0..n)), *dpost += sum(part[n..2n)) in a fixed order (one workgroup)
+__global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ part, int n, float *dpre,
+                                                     float *dpost) {
+    __shared__ float red[8];
+    float s0 = 0.f, s1 = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        s0 += part[i];
+        s1 += part[n + i];
+    }
+    s0 = block_sum<float, 256>(s0, red);
+    s1 = block_sum<float, 256>(s1, red + 4);
+    if (threadIdx.x == 0) {
+        if (dpre) *dpre += s0;
+        if (dpost) *dpost += s1;
+    }
+}
+
+// Few-channel rows (Cin, N in {1, 2, 4, 8}, one input, no upsampled residual): each row is one
+// naturally aligned 2..16-byte vector, so lanes read and write consecutive rows as one contiguous
+// span -- no LDS staging; 4 voxels per thread in flight.
+template <typename T, int C>
+__device__ __forceinline__ void row_ld(const T *__restrict__ p, float (&o)[C]) {
+    if constexpr (sizeof(T) == 2) {
+        if constexpr (C == 1) {
+            o[0] = ld(p);
+        } else if constexpr (C == 2) {
+            const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
+            o[0] = __uint_as_float(u << 16);
+            o[1] = __uint_as_float(u & 0xffff0000u);
+        } else if constexpr (C == 4) {
+            const uint2 u = *reinterpret_cast<const uint2 *>(p);
+            const uint32_t q[2] = {u.x, u.y};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                o[2 * j] = __uint_as_float(q[j] << 16);
+                o[2 * j + 1] = __uint_as_float(q[j] & 0xffff0000u);
+            }
+        } else {
+            const uint4 u = *reinterpret_cast<const uint4 *>(p);
+            const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[2 * j] = __uint_as_float(q[j] << 16);
+                o[2 * j + 1] = __uint_as_float(q[j] & 0xffff0000u);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < C; ++j) o[j] = p[j];
+    }
+}
+
+template <typename T, int C>
+__device__ __forceinline__ void row_st(T *__restrict__ p, const float (&v)[C]) {
+    if constexpr (sizeof(T) == 2) {
+        if constexpr (C == 1) {
+            st(p, v[0]);
+        } else {
+            uint32_t q[C / 2];
+#pragma unroll
+            for (int j = 0; j < C / 2; ++j) q[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+            if constexpr (C == 2) *reinterpret_cast<uint32_t *>(p) = q[0];
+            else if constexpr (C == 4) *reinterpret_cast<uint2 *>(p) = uint2{q[0], q[1]};
+            else *reinterpret_cast<uint4 *>(p) = uint4{q[0], q[1], q[2], q[3]};
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < C; ++j) p[j] = v[j];
+    }
+}
+
+template <typename T, int CI, int CO, bool DGRAD>
+__global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restrict__ in, const float *__restrict__ w,
+                                                int pro_kind, const float *pro_a, const float *pro_b,
+                                                FwdEpi<T> fe, BwdEpi<T> be, const float *__restrict__ gscale,
+                                                T *__restrict__ out, float *dpre, float *dpost, float *part) {
+    __shared__ float wsh[CO * CI];
+    __shared__ float red[8];
+    const int Ct = DGRAD ? CO : CI;
+    for (int e = threadIdx.x; e < CO * CI; e += 256) {
+        const int o = e / CI, c = e - o * CI;
+        wsh[e] = DGRAD ? w[c * Ct + o] : w[o * Ct + c];
+    }
+    __syncthreads();
+    float wr[CO][CI];
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+#pragma unroll
+        for (int c = 0; c < CI; ++c) wr[o][c] = wsh[o * CI + c];
+    const Prologue pro = make_prologue(pro_kind, pro_a, pro_b);
+    const float gs = gscale ? *gscale : 1.f;
+    const float sc = fe.scale ? *fe.scale : 1.f, bias = fe.bias ? *fe.bias : 0.f;
+    const float aa = fe.act_a ? *fe.act_a : 0.f, ab = fe.act_b ? *fe.act_b : 0.f;
+    ActDeriv dv;
+    dv.mode = (DGRAD && be.aux) ? be.mode : 0;
+    dv.p = (dv.mode && be.p) ? *be.p : 0.f;
+    float pre = 0.f, post = 0.f;
+    const int64_t stride = int64_t(gridDim.x) * 256;
+    for (int64_t vb = int64_t(blockIdx.x) * 256 + threadIdx.x; vb < nvox; vb += 4 * stride) {
+        float xr[4][CI], er[4][CO], dr[4][CO];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t v = vb + u * stride;
+            if (v < nvox) {
+                row_ld<T, CI>(in + v * CI, xr[u]);
+                if (!DGRAD && fe.res) row_ld<T, CO>(fe.res + v * CO, er[u]);
+                if (DGRAD && dv.mode) row_ld<T, CO>(be.aux + v * CO, er[u]);
+                if (DGRAD && be.addend) row_ld<T, CO>(be.addend + v * CO, dr[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t v = vb + u * stride;
+            if (v >= nvox) break;
+            float y[CO];
+#pragma unroll
+            for (int o = 0; o < CO; ++o) {
+                float s = 0.f;
+#pragma unroll
+                for (int c = 0; c < CI; ++c) s = fmaf(DGRAD ? xr[u][c] : pro.apply(xr[u][c]), wr[o][c], s);
+                if (!DGRAD) {
+                    if (fe.scale) s = s * sc;
+                    if (fe.bias) s = s + bias;
+                    if (fe.cbias) s = s + fe.cbias[o];
+                    if (fe.res) s = s + er[u][o];
+                    s = epi_act(fe.act, s, aa, ab);
+                } else {
+                    if (gscale) s = s * gs;
+                    pre += s;
+                    if (dv.mode) s = s * dv(er[u][o]);
+                    post += s;
+                    if (be.addend) s = s + dr[u][o];
+                }
+                y[o] = s;
+            }
+            row_st<T, CO>(out + v * CO, y);
+        }
+    }
+    if (DGRAD && (dpre || dpost)) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (part) {
+                part[blockIdx.x] = pre;
+                part[gridDim.x + blockIdx.x] = post;
+            } else {
+                if (dpre) atomicAdd(dpre, pre);
+                if (dpost) atomicAdd(dpost, post);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+namespace {
+
+constexpr int kMaxPwBlocks = 2048;
+
+bool rows_path(const vq3d_conv_desc *d, bool dgrad, const void *res_up2_flag) {
+    auto p2 = [](int c) { return c == 1 || c == 2 || c == 4 || c == 8; };
+    const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
+    return d->cin2 == 0 && p2(ci) && p2(co) && !res_up2_flag;
+}
+
+}  // namespace
+
+size_t pw_dgrad_workspace(const vq3d_conv_desc *) { return size_t(2) * kMaxPwBlocks * sizeof(float); }
+
+template <typename T>
+int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w, const float *pa,
+               const float *pb, const FwdEpi<T> &fe_in, const BwdEpi<T> &be, const float *gscale, void *out,
+               void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s) {
+    const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    FwdEpi<T> fe = fe_in;
+    fe.oH = d->out_h;
+    fe.oW = d->out_w;
+    fe.oD = d->out_d;
+    auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const bool want_part = dgrad && (dpre || dpost);
+    // ---- few-channel rows: no LDS staging
+    if (rows_path(d, dgrad, fe.res_up2 ? fe.res : nullptr) && al(in) && al(out) && al(fe.res) && al(be.aux) && al(be.addend)) {
+        const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
+        const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 1023) / 1024, kMaxPwBlocks)));
+        float *part = (want_part && nbx > 32 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
+        const int key = ci * 16 + co;
+        const int pk = dgrad ? VQ3D_PRO_NONE : d->pro_kind;
+#define R(CI, CO)                                                                                              \
+    case CI * 16 + CO:                                                                                         \
+        if (dgrad)                                                                                             \
+            k_pw_rows<T, CI, CO, true><<<nbx, 256, 0, s>>>(nvox, (const T *)in, w, pk, pa, pb, fe, be, gscale, \
+                                                           (T *)out, dpre, dpost, part);                       \
+        else                                                                                                   \
+            k_pw_rows<T, CI, CO, false><<<nbx, 256, 0, s>>>(nvox, (const T *)in, w, pk, pa, pb, fe, be,       \
+                                                            nullptr, (T *)out, nullptr, nullptr, nullptr);     \
+        break;
+        switch (key) {
+            R(1, 1) R(1, 2) R(1, 4) R(1, 8) R(2, 1) R(2, 2) R(2, 4) R(2, 8)
+            R(4, 1) R(4, 2) R(4, 4) R(4, 8) R(8, 1) R(8, 2) R(8, 4) R(8, 8)
+        default: return fail("conv(pointwise): no row kernel");
+        }
+#undef R
+        if (part) k_sum_partials<<<1, 256, 0, s>>>(part, int(nbx), dpre, dpost);
+        return check_launch(dgrad ? "conv3d_bwd_data(pointwise rows)" : "conv3d_fwd(pointwise rows)");
+    }
+    // ---- LDS slabs
+    PwArgs a = {};
+    a.nvox = nvox;
+    const int Ct = d->cin + d->cin2;
+    if (!dgrad) {
+        a.Ca = d->cin;
+        a.Cb = d->cin2;
+        a.N = d->cout;
+        a.N1 = a.N;
+        a.N2 = 0;
+        a.pro_kind = d->pro_kind;
+        a.pro_a = pa;
+        a.pro_b = pb;
+    } else {
+        a.Ca = d->cout;
+        a.Cb = 0;
+        a.N = Ct;
+        a.N1 = d->cin;
+        a.N2 = d->cin2;
+        a.pro_kind = VQ3D_PRO_NONE;
+    }
+    a.Cin = a.Ca + a.Cb;
+    a.CinP = (a.Cin + 7) / 8 * 8;
+    const int cot = a.N <= 1 ? 1 : a.N <= 2 ? 2 : a.N <= 4 ? 4 : a.N <= 8 ? 8 : a.N <= 12 ? 12 : 16;
+    const int NP = (a.N + cot - 1) / cot * cot;
+    // voxels per segment: 256 (one thread each) unless the grid would leave CUs idle; then
+    // fewer voxels with several threads splitting each voxel's output tiles
+    const int ntiles = NP / cot;
+    a.segv = 256;
+    while (a.segv > 32 && (nvox + a.segv - 1) / a.segv < 512 && 256 / (a.segv / 2) <= ntiles) a.segv /= 2;
+    auto r8 = [](int v) { return (v + 7) / 8 * 8; };
+    const bool aux = dgrad && be.aux && be.mode;
+    size_t lds = 0;
+    while (true) {  // shrink the segment until the slabs fit
+        a.tpv = 256 / a.segv;
+        const int S = a.segv;
+        int off = 0;
+        a.o_x = off; off += r8(S * a.Ca);
+        a.o_x2 = off; off += r8(S * a.Cb);
+        a.o_aux = off; off += aux ? r8(S * a.N1) : 0;
+        a.o_add = off; off += (dgrad && be.addend) ? r8(S * a.N1) : 0;
+        a.o_res = off; off += (!dgrad && fe.res && !fe.res_up2) ? r8(S * a.N) : 0;
+        a.o_out = off; off += r8(S * a.N1);
+        a.o_out2 = off; off += r8(S * a.N2);
+        lds = size_t(NP) * a.CinP * 4 + size_t(off) * sizeof(T);
+        if (lds <= 96 * 1024 || a.segv <= 8) break;
+        a.segv /= 2;
+    }
+    if (lds > 150 * 1024) return fail("conv(pointwise): too many channels for the LDS slabs");
+    a.vec = al(in) && al(in2) && al(out) && al(out2) && al(be.aux) && al(be.addend) && al(fe.res);
+    const int64_t nseg = (a.nvox + a.segv - 1) / a.segv;
+    const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, kMaxPwBlocks)));
+    float *part = (want_part && nbx > 32 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
+#define L(C)                                                                                                    \
+    case C: {                                                                                                   \
+        auto kern = dgrad ? k_pw2<T, C, true> : k_pw2<T, C, false>;                                             \
+        static bool attr = false;                                                                               \
+        if (!attr) {                                                                                            \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pw2<T, C, true>),                        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                  \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pw2<T, C, false>),                       \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                  \
+            (void)hipGetLastError();                                                                            \
+            attr = true;                                                                                        \
+        }                                                                                                       \
+        kern<<<nbx, SEG, lds, s>>>(a, (const T *)in, (const T *)in2, w, fe, be, gscale, (T *)out, (T *)out2,    \
+                                   dpre, dpost, part);                                                          \
+    } break;
+    switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
+#undef L
+    if (part) k_sum_partials<<<1, 256, 0, s>>>(part, int(nbx), dpre, dpost);
+    return check_launch(dgrad ? "conv3d_bwd_data(pointwise)" : "conv3d_fwd(pointwise)");
+}
+
+template int launch_pw1<float>(const vq3d_conv_desc *, bool, const void *, const void *, const float *, const float *,
+                               const float *, const FwdEpi<float> &, const BwdEpi<float> &, const float *, void *,
+                               void *, float *, float *, void *, size_t, hipStream_t);
+template int launch_pw1<bf16_t>(const vq3d_conv_desc *, bool, const void *, const void *, const float *,
+                                const float *, const float *, const FwdEpi<bf16_t> &, const BwdEpi<bf16_t> &,
+                                const float *, void *, void *, float *, float *, void *, size_t, hipStream_t);
+
+}  // namespace vq3d

@@ -151,6 +151,8 @@ def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None
         ws, wsb = _ws(desc, L.PASS_BWD_DATA, x.device)
         L.call("vq3d_conv3d_bwd_data", ctypes.byref(desc), L.ptr(g), _p(gscale), L.ptr(w), _p(pa),
                ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), _p(ws), wsb, s)
+    if dw is None and dscale is None and dbias is None and dcbias is None:
+        return gx, gx2
     ws, wsb = _ws(desc, L.PASS_BWD_WEIGHT, x.device)
     L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb), L.ptr(w),
            _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), _p(ws), wsb, s)

@@ -19,17 +19,23 @@ class FusedAdam(torch.optim.Optimizer):
         self.m = torch.zeros_like(flat.data)
         self.v = torch.zeros_like(flat.data)
         self.vmax = torch.zeros_like(flat.data)
-        self.step_count = 0
+        # completed steps, on the device: the kernel derives the bias corrections from it and
+        # increments it, so a captured HIP graph of the whole step replays correctly
+        self.step_t = torch.zeros((), dtype=torch.int64, device=flat.data.device)
+
+    @property
+    def step_count(self):
+        return int(self.step_t.item())
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        self.step_count += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         f = self.flat
-        L.call("vq3d_adam_amsgrad", L.ptr(f.data), L.ptr(f.grad), L.ptr(self.m), L.ptr(self.v), L.ptr(self.vmax),
-               f.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), self.step_count, L.stream())
+        L.call("vq3d_adam_amsgrad_dev", L.ptr(f.data), L.ptr(f.grad), L.ptr(self.m), L.ptr(self.v),
+               L.ptr(self.vmax), f.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), L.ptr(self.step_t),
+               L.stream())
         return loss
 
     def zero_grad(self, set_to_none: bool = False):
@@ -38,13 +44,14 @@ class FusedAdam(torch.optim.Optimizer):
     def state_dict(self):
         sd = super().state_dict()
         st = {}
+        step_count = self.step_count
         idx = 0
         for g in self.param_groups:
             for p in g["params"]:
                 off = self.flat.offsets[self.flat.params.index(p)]
                 n = p.numel()
-                if self.step_count:
-                    st[idx] = dict(step=torch.tensor(float(self.step_count)),
+                if step_count:
+                    st[idx] = dict(step=torch.tensor(float(step_count)),
                                    exp_avg=self.m[off:off + n].view(p.shape).clone(),
                                    exp_avg_sq=self.v[off:off + n].view(p.shape).clone(),
                                    max_exp_avg_sq=self.vmax[off:off + n].view(p.shape).clone())
@@ -67,6 +74,6 @@ class FusedAdam(torch.optim.Optimizer):
                     self.vmax[off:off + n].copy_(s["max_exp_avg_sq"].reshape(-1))
                     steps.add(int(float(s["step"])))
                 idx += 1
-        self.step_count = steps.pop() if steps else 0
+        self.step_t.fill_(steps.pop() if steps else 0)
         for g, sg in zip(self.param_groups, state_dict["param_groups"]):
             g["lr"] = sg["lr"]

@@ -179,6 +179,11 @@ int vq3d_evonorm_bwd(int32_t dtype, const void *x, const void *gy, int32_t chann
 /* --- optimizer: torch.optim.Adam(amsgrad=True) over one flat fp32 buffer (model.py:91-93) --- */
 int vq3d_adam_amsgrad(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr,
                       float beta1, float beta2, float eps, int64_t step, vq3d_stream_t stream);
+/* Same update with the step count on the device: uses *step + 1 for the bias corrections, then
+ * increments *step -- no host value baked into the launch, so a captured HIP graph of the
+ * training step replays correctly. */
+int vq3d_adam_amsgrad_dev(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr,
+                          float beta1, float beta2, float eps, int64_t *step, vq3d_stream_t stream);
 
 /* --- utilities --- */
 int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, int64_t n,
