@@ -779,6 +779,8 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     if (is_pointwise(d))
         return launch_pw_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
     if constexpr (std::is_same<T, bf16_t>::value) {
+        if (lines_wgrad_applicable(d))
+            return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, s);
         if (!mfma_disabled()) {
             MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
                                 d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true);

@@ -44,6 +44,12 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
                  const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
                  void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
+// k^3 weight gradient on the lines layout (conv_lines_wgrad.hip), bf16, cout <= 64
+bool lines_wgrad_applicable(const vq3d_conv_desc *d);
+int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
+                       const float *pro_b, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
+                       float *dcbias, hipStream_t s);
+
 // 1x1x1 conv forward / backward-data (pw_conv.hip), both storage dtypes
 // (dgrad with prologue-scalar partials on big grids: per-workgroup partials in `ws`,
 // pw_dgrad_workspace(d) bytes, summed in order by a second kernel)
