@@ -753,6 +753,7 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
             }
         }
     }
+    if (dgrad_s2_applicable(d)) return launch_dgrad_s2<T>(d, g, gscale, w, be, gx, gx2, dpre, dpost, s);
     const int K3 = d->kernel * d->kernel * d->kernel;
     const size_t all = size_t(K3) * d->cout * cit * 4;
     const int all_taps = all <= kAllTapsLds;

@@ -1,0 +1,238 @@
+// Backward-data of the stride-2 convolutions (PreAct down blocks: branch_conv2 4x4x4 stride 2
+// circular, skip_conv 2x2x2 stride 2 -- vqvae/layers.py:124-126, 164-171).
+//
+// gx[i] = sum over taps t with 2o + t - p == i (mod n) of W[t]^T g[o].  Per dimension only the
+// taps whose parity matches i + p contribute (k / 2 of them, each with a unique o), so a thread
+// owning one input voxel visits (k/2)^3 taps instead of k^3, reading each contributing g row
+// once; the weights of all taps sit in LDS.  The backward-data epilogue (activation derivative
+// from aux, addend, prologue-scalar partial sums, split into gx / gx2) is fused.  VALU fp32: the
+// stride-2 layers carry few channels on large grids (4..16 at 512^2..128^2) or few voxels.
+#include "engines.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+struct S2Args {
+    int B, Cin1, Cin2, Cin, Cout;
+    int iH, iW, iD, oH, oW, oD;
+    int k, p, circ;
+    FastDiv fD, fW, fH;  // 32-bit voxel index decomposition (no 64-bit divides in the loop)
+};
+
+// the <= 2 (o, t) pairs of one dimension for input coordinate i (k in {2, 4}, stride 2)
+__device__ __forceinline__ int taps_s2(int i, int k, int p, int n_in, int n_out, int circ, int (&o)[2], int (&t)[2]) {
+    int cnt = 0;
+    const int t0 = (i + p) & 1;  // taps with (i + p - t) even
+    for (int tt = t0; tt < k; tt += 2) {
+        int r = i + p - tt;
+        if (circ) {
+            r = r < 0 ? r + n_in : (r >= n_in ? r - n_in : r);
+        } else if (r < 0) {
+            continue;
+        }
+        r >>= 1;
+        if (r >= n_out) continue;
+        o[cnt] = r;
+        t[cnt] = tt;
+        ++cnt;
+    }
+    return cnt;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[N]) {
+    if constexpr (sizeof(T) == 2 && (N % 8) == 0) {
+#pragma unroll
+        for (int q = 0; q < N / 8; ++q) {
+            const uint4 u = reinterpret_cast<const uint4 *>(p)[q];
+            const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[8 * q + 2 * j] = __uint_as_float(w4[j] << 16);
+                o[8 * q + 2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+            }
+        }
+    } else if constexpr (sizeof(T) == 2 && N == 4) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(p);
+        o[0] = __uint_as_float(u.x << 16);
+        o[1] = __uint_as_float(u.x & 0xffff0000u);
+        o[2] = __uint_as_float(u.y << 16);
+        o[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) o[j] = ld(p + j);
+    }
+}
+
+// CO: g channels (conv Cout) when a compile-time row is used (0: runtime loop)
+template <typename T, int COT, int CO>
+__global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict__ g, const float *__restrict__ gscale,
+                                                 const float *__restrict__ w, BwdEpi<T> be, T *__restrict__ gx,
+                                                 T *__restrict__ gx2, float *dpre, float *dpost) {
+    extern __shared__ __attribute__((aligned(16))) float wsh[];  // [tap][Cout][COT]
+    __shared__ float red[8];
+    const int K3 = a.k * a.k * a.k;
+    const int c0 = blockIdx.y * COT;
+    for (int e = threadIdx.x; e < K3 * a.Cout * COT; e += 256) {
+        const int c = e % COT, r = e / COT, co = r % a.Cout, tap = r / a.Cout;
+        const int ci = c0 + c;
+        wsh[e] = ci < a.Cin ? w[(int64_t(co) * a.Cin + ci) * K3 + tap] : 0.f;
+    }
+    __syncthreads();
+    ActDeriv dv;
+    dv.mode = be.aux ? be.mode : 0;
+    dv.p = (dv.mode && be.p) ? *be.p : 0.f;
+    const float gs = gscale ? *gscale : 1.f;
+    float pre = 0.f, post = 0.f;
+    const int64_t nvox = int64_t(a.B) * a.iH * a.iW * a.iD;
+    for (int64_t v = int64_t(blockIdx.x) * 256 + threadIdx.x; v < nvox; v += int64_t(gridDim.x) * 256) {
+        uint32_t q = uint32_t(v);
+        uint32_t q2 = a.fD.div(q);
+        const int id = int(q - q2 * uint32_t(a.iD));
+        q = a.fW.div(q2);
+        const int iw = int(q2 - q * uint32_t(a.iW));
+        q2 = a.fH.div(q);
+        const int ih = int(q - q2 * uint32_t(a.iH));
+        const int b = int(q2);
+        int oh[2], th[2], ow[2], tw[2], od[2], td[2];
+        const int nh = taps_s2(ih, a.k, a.p, a.iH, a.oH, a.circ, oh, th);
+        const int nw = taps_s2(iw, a.k, a.p, a.iW, a.oW, a.circ, ow, tw);
+        const int nd = taps_s2(id, a.k, a.p, a.iD, a.oD, a.circ, od, td);
+        float acc[COT];
+#pragma unroll
+        for (int c = 0; c < COT; ++c) acc[c] = 0.f;
+        if constexpr (CO > 0) {
+            // all contributing g rows loaded first (up to 8 x CO values in flight)
+            float gr[8][CO];
+            int wt[8];
+            int cnt = 0;
+#pragma unroll
+            for (int xh = 0; xh < 2; ++xh)
+#pragma unroll
+                for (int xw = 0; xw < 2; ++xw)
+#pragma unroll
+                    for (int xd = 0; xd < 2; ++xd) {
+                        const int j = (xh * 2 + xw) * 2 + xd;
+                        const bool live = xh < nh && xw < nw && xd < nd;
+                        if (live) {
+                            load_row<T, CO>(g + (((int64_t(b) * a.oH + oh[xh]) * a.oW + ow[xw]) * a.oD + od[xd]) * CO,
+                                            gr[j]);
+                            wt[j] = ((th[xh] * a.k + tw[xw]) * a.k + td[xd]) * CO * COT;
+                        } else {
+                            wt[j] = -1;
+                        }
+                    }
+            (void)cnt;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (wt[j] < 0) continue;
+                const float *wr = wsh + wt[j];
+#pragma unroll
+                for (int co = 0; co < CO; ++co)
+#pragma unroll
+                    for (int c = 0; c < COT; ++c) acc[c] = fmaf(gr[j][co], wr[co * COT + c], acc[c]);
+            }
+        } else {
+            for (int xh = 0; xh < nh; ++xh)
+                for (int xw = 0; xw < nw; ++xw)
+                    for (int xd = 0; xd < nd; ++xd) {
+                        const T *grp = g + (((int64_t(b) * a.oH + oh[xh]) * a.oW + ow[xw]) * a.oD + od[xd]) * a.Cout;
+                        const float *wr = wsh + ((th[xh] * a.k + tw[xw]) * a.k + td[xd]) * a.Cout * COT;
+                        for (int co = 0; co < a.Cout; ++co) {
+                            const float gv = ld(grp + co);
+#pragma unroll
+                            for (int c = 0; c < COT; ++c) acc[c] = fmaf(gv, wr[co * COT + c], acc[c]);
+                        }
+                    }
+        }
+#pragma unroll
+        for (int c = 0; c < COT; ++c) {
+            const int ci = c0 + c;
+            if (ci >= a.Cin) break;
+            float val = acc[c];
+            if (gscale) val = val * gs;
+            if (ci < a.Cin1) {
+                const int64_t o = v * a.Cin1 + ci;
+                pre += val;
+                if (dv.mode) val = val * dv(ld(be.aux + o));
+                post += val;
+                if (be.addend) val = val + ld(be.addend + o);
+                st(gx + o, val);
+            } else {
+                st(gx2 + v * a.Cin2 + (ci - a.Cin1), val);
+            }
+        }
+    }
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
+        }
+    }
+}
+
+}  // namespace
+
+bool dgrad_s2_applicable(const vq3d_conv_desc *d) {
+    return d->stride == 2 && (d->kernel == 2 || d->kernel == 4) && d->in_h % 2 == 0 && d->in_w % 2 == 0 &&
+           d->in_d % 2 == 0;
+}
+
+template <typename T>
+int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
+                    const BwdEpi<T> &be, void *gx, void *gx2, float *dpre, float *dpost, hipStream_t s) {
+    S2Args a;
+    a.B = d->batch;
+    a.Cin1 = d->cin;
+    a.Cin2 = d->cin2;
+    a.Cin = d->cin + d->cin2;
+    a.Cout = d->cout;
+    a.iH = d->in_h; a.iW = d->in_w; a.iD = d->in_d;
+    a.oH = d->out_h; a.oW = d->out_w; a.oD = d->out_d;
+    a.k = d->kernel;
+    a.p = d->pad;
+    a.circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
+    a.fD = FastDiv(uint32_t(a.iD));
+    a.fW = FastDiv(uint32_t(a.iW));
+    a.fH = FastDiv(uint32_t(a.iH));
+    if (int64_t(a.B) * a.iH * a.iW * a.iD >= (int64_t(1) << 31)) return fail("conv3d_bwd_data(s2): grid too large");
+    const int K3 = a.k * a.k * a.k;
+    int cot = a.Cin <= 1 ? 1 : a.Cin <= 2 ? 2 : a.Cin <= 4 ? 4 : a.Cin <= 8 ? 8 : 16;
+    while (cot > 1 && size_t(K3) * a.Cout * cot * 4 > 64 * 1024) cot /= 2;
+    const size_t lds = size_t(K3) * a.Cout * cot * 4;
+    if (lds > 64 * 1024) return fail("conv3d_bwd_data(s2): too many channels");
+    const int64_t nvox = int64_t(a.B) * a.iH * a.iW * a.iD;
+    const int ych = (a.Cin + cot - 1) / cot;
+    const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 255) / 256, 4096 / ych + 1)));
+    const dim3 grid{nbx, unsigned(ych), 1u};
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    const int co_t = (al(g) && (a.Cout == 4 || a.Cout == 8 || a.Cout == 16)) ? a.Cout : 0;
+#define L(C, CO)                                                                                              \
+    case C:                                                                                                   \
+        k_dgrad_s2<T, C, CO><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, be, (T *)gx, (T *)gx2, dpre,  \
+                                                    dpost);                                                   \
+        break;
+#define LS(CO)                                                                                                \
+    switch (cot) { L(1, CO) L(2, CO) L(4, CO) L(8, CO) L(16, CO) }
+    switch (co_t) {
+    case 4: LS(4) break;
+    case 8: LS(8) break;
+    case 16: LS(16) break;
+    default: LS(0) break;
+    }
+#undef LS
+#undef L
+    return check_launch("conv3d_bwd_data(s2)");
+}
+
+template int launch_dgrad_s2<float>(const vq3d_conv_desc *, const void *, const float *, const float *,
+                                    const BwdEpi<float> &, void *, void *, float *, float *, hipStream_t);
+template int launch_dgrad_s2<bf16_t>(const vq3d_conv_desc *, const void *, const float *, const float *,
+                                     const BwdEpi<bf16_t> &, void *, void *, float *, float *, hipStream_t);
+
+}  // namespace vq3d

@@ -50,6 +50,19 @@ int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, c
                        const float *pro_b, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
                        float *dcbias, hipStream_t s);
 
+// stride-2 (k = 2 or 4) backward-data visiting only the parity-matching taps (conv_s2.hip)
+bool dgrad_s2_applicable(const vq3d_conv_desc *d);
+template <typename T>
+int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w, const BwdEpi<T> &be,
+                    void *gx, void *gx2, float *dpre, float *dpost, hipStream_t s);
+
+// trilinear x2 upsample forward / adjoint (upsample.hip)
+int launch_up2_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd, const void *x,
+                   int32_t pro_kind, const float *pro_a, const float *pro_b, void *y, hipStream_t s);
+int launch_up2_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd, const void *gy,
+                   int dmode, const float *dparam, const void *aux, const void *add, void *gx, float *dpre,
+                   float *dpost, hipStream_t s);
+
 // 1x1x1 conv forward / backward-data (pw_conv.hip), both storage dtypes
 // (dgrad with prologue-scalar partials on big grids: per-workgroup partials in `ws`,
 // pw_dgrad_workspace(d) bytes, summed in order by a second kernel)

@@ -1,6 +1,7 @@
 // Upsample (ResizeConv3D's nn.Upsample), reconstruction loss, EvoNorm-S0, Adam(amsgrad),
 // casts, and the error plumbing of libvq3d.
 #include "common.h"
+#include "engines.h"
 
 #include <algorithm>
 #include <cmath>
@@ -386,16 +387,7 @@ int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     if (batch <= 0 || channels <= 0 || h <= 0 || w <= 0 || dd <= 0) return fail("upsample2x_fwd: bad sizes");
     if (!x || !y || (pro_kind && !pro_a) || (pro_kind == VQ3D_PRO_ELU_ADD && !pro_b))
         return fail("upsample2x_fwd: null pointer");
-    const int64_t n = int64_t(batch) * 8 * h * w * dd * channels;
-    const unsigned nb = unsigned((n + 255) / 256);
-    hipStream_t s = as_stream(stream);
-    if (dtype == VQ3D_F32)
-        k_up_fwd<float><<<nb, 256, 0, s>>>((const float *)x, batch, channels, h, w, dd, pro_kind, pro_a, pro_b,
-                                           (float *)y);
-    else
-        k_up_fwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)x, batch, channels, h, w, dd, pro_kind, pro_a, pro_b,
-                                            (bf16_t *)y);
-    return check_launch("upsample2x_fwd");
+    return launch_up2_fwd(dtype, batch, channels, h, w, dd, x, pro_kind, pro_a, pro_b, y, as_stream(stream));
 }
 
 int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
@@ -414,17 +406,8 @@ int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
         dparam = pro_a;
     }
     if (dmode && !dparam) return fail("upsample2x_bwd: derivative needs its scalar (pro_a or aux_b)");
-    const int64_t n = int64_t(batch) * h * w * dd * channels;
-    const unsigned nb = grid_for(n);
-    hipStream_t s = as_stream(stream);
-    if (dtype == VQ3D_F32)
-        k_up_bwd<float><<<nb, 256, 0, s>>>((const float *)gy, batch, channels, h, w, dd, dmode, dparam,
-                                           (const float *)aux, (const float *)add, (float *)gx, dpro_pre, dpro_post);
-    else
-        k_up_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)gy, batch, channels, h, w, dd, dmode, dparam,
-                                            (const bf16_t *)aux, (const bf16_t *)add, (bf16_t *)gx, dpro_pre,
-                                            dpro_post);
-    return check_launch("upsample2x_bwd");
+    return launch_up2_bwd(dtype, batch, channels, h, w, dd, gy, dmode, dparam, aux, add, gx, dpro_pre, dpro_post,
+                          as_stream(stream));
 }
 
 int64_t vq3d_cylinder_count(int32_t h, int32_t w) {

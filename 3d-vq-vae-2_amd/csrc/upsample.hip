@@ -1,0 +1,251 @@
+// Trilinear x2 upsampling, align_corners=False (nn.Upsample inside ResizeConv3D,
+// vqvae/layers.py:591-597), forward and adjoint, on channels-last tensors.
+//
+// Along one axis the destination j reads source floor(j/2 - 1/4) and its upper neighbour with
+// weights (0.75, 0.25) or (0.25, 0.75), clamped at the edges (ATen's area_pixel source index).
+// Hence source i receives from exactly the four destinations 2i-1 .. 2i+2 with weights
+// 0.25, 0.75, 0.75, 0.25 -- the first 0.75 becomes 1 at i = 0 (j = 0 clamps onto it) and the
+// second at i = n-1 -- which the adjoint applies in closed form, separably.  A thread owns one
+// voxel and CV consecutive channels (8- or 16-byte rows), decomposes its index with 32-bit
+// multiplicative division, and the backward fuses the activation derivative, the addend and the
+// prologue-scalar partial sums of its consumer conv.
+#include "common.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+template <typename T, int CV>
+__device__ __forceinline__ void ldv(const T *__restrict__ p, float (&o)[CV]) {
+    if constexpr (sizeof(T) == 2 && CV == 4) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(p);
+        o[0] = __uint_as_float(u.x << 16);
+        o[1] = __uint_as_float(u.x & 0xffff0000u);
+        o[2] = __uint_as_float(u.y << 16);
+        o[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else if constexpr (sizeof(T) == 2 && CV == 8) {
+        const uint4 u = *reinterpret_cast<const uint4 *>(p);
+        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o[2 * j] = __uint_as_float(w4[j] << 16);
+            o[2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < CV; ++j) o[j] = ld(p + j);
+    }
+}
+
+template <typename T, int CV>
+__device__ __forceinline__ void stv(T *__restrict__ p, const float (&v)[CV]) {
+    if constexpr (sizeof(T) == 2 && CV == 4) {
+        *reinterpret_cast<uint2 *>(p) = uint2{uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
+                                              uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
+    } else if constexpr (sizeof(T) == 2 && CV == 8) {
+        uint32_t q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+        *reinterpret_cast<uint4 *>(p) = uint4{q[0], q[1], q[2], q[3]};
+    } else {
+#pragma unroll
+        for (int j = 0; j < CV; ++j) st(p + j, v[j]);
+    }
+}
+
+struct UArgs {
+    int B, C, H, W, D;  // source grid (destination is 2H x 2W x 2D)
+    int nchunk;         // C / CV
+    FastDiv fch, f1, f2, f3;
+};
+
+// decompose e = (((b * n3 + i3) * n2 + i2) * n1 + i1) * nchunk + ch
+__device__ __forceinline__ void split(const UArgs &a, uint32_t e, int n1, int n2, int n3, int &ch, int &i1, int &i2,
+                                      int &i3, int &b) {
+    uint32_t q = a.fch.div(e);
+    ch = int(e - q * uint32_t(a.nchunk));
+    uint32_t r = a.f1.div(q);
+    i1 = int(q - r * uint32_t(n1));
+    q = a.f2.div(r);
+    i2 = int(r - q * uint32_t(n2));
+    r = a.f3.div(q);
+    i3 = int(q - r * uint32_t(n3));
+    b = int(r);
+}
+
+// destination j -> (source i0, i1, weight of i1)
+__device__ __forceinline__ void src_of(int j, int n, int &i0, int &i1, float &l1) { up_coeff(j, n, i0, i1, l1); }
+
+template <typename T, int CV>
+__global__ __launch_bounds__(256) void k_up2_fwd(UArgs a, const T *__restrict__ x, int pk, const float *pa,
+                                                const float *pb, T *__restrict__ y) {
+    const Prologue pro = make_prologue(pk, pa, pb);
+    const uint32_t n = uint32_t(a.B) * 8u * a.H * a.W * a.D * a.nchunk;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
+        int ch, od, ow, oh, b;
+        split(a, e, 2 * a.D, 2 * a.W, 2 * a.H, ch, od, ow, oh, b);
+        int h0, h1, w0, w1, d0, d1;
+        float lh, lw, ldd;
+        src_of(oh, a.H, h0, h1, lh);
+        src_of(ow, a.W, w0, w1, lw);
+        src_of(od, a.D, d0, d1, ldd);
+        float v[8][CV];
+        const int hs[2] = {h0, h1}, wsx[2] = {w0, w1}, ds[2] = {d0, d1};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            ldv<T, CV>(x + (((int64_t(b) * a.H + hs[q >> 2]) * a.W + wsx[(q >> 1) & 1]) * a.D + ds[q & 1]) * a.C +
+                           ch * CV,
+                       v[q]);
+        float out[CV];
+#pragma unroll
+        for (int c = 0; c < CV; ++c) {
+            float X[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) X[q] = pro.apply(v[q][c]);
+            out[c] = (1.f - lh) * ((1.f - lw) * ((1.f - ldd) * X[0] + ldd * X[1]) + lw * ((1.f - ldd) * X[2] + ldd * X[3])) +
+                     lh * ((1.f - lw) * ((1.f - ldd) * X[4] + ldd * X[5]) + lw * ((1.f - ldd) * X[6] + ldd * X[7]));
+        }
+        const int64_t vo = ((int64_t(b) * 2 * a.H + oh) * 2 * a.W + ow) * 2 * a.D + od;
+        stv<T, CV>(y + vo * a.C + ch * CV, out);
+    }
+}
+
+// the four destinations of source i along an axis of source length n, with their weights
+__device__ __forceinline__ void adj4(int i, int n, int (&j)[4], float (&wt)[4]) {
+    j[0] = 2 * i - 1;
+    wt[0] = i >= 1 ? 0.25f : 0.f;
+    j[1] = 2 * i;
+    wt[1] = i == 0 ? 1.f : 0.75f;
+    j[2] = 2 * i + 1;
+    wt[2] = i == n - 1 ? 1.f : 0.75f;
+    j[3] = 2 * i + 2;
+    wt[3] = i <= n - 2 ? 0.25f : 0.f;
+    if (j[0] < 0) j[0] = 0;          // weight 0: any valid index
+    if (j[3] > 2 * n - 1) j[3] = 2 * n - 1;
+}
+
+template <typename T, int CV>
+__global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ gy, int dmode, const float *dparam,
+                                                const T *__restrict__ aux, const T *__restrict__ addend,
+                                                T *__restrict__ gx, float *dpre, float *dpost) {
+    __shared__ float red[8];
+    ActDeriv dv;
+    dv.mode = aux ? dmode : 0;
+    dv.p = (dv.mode && dparam) ? *dparam : 0.f;
+    float pre = 0.f, post = 0.f;
+    const uint32_t n = uint32_t(a.B) * a.H * a.W * a.D * a.nchunk;
+    const int D2 = 2 * a.D, W2 = 2 * a.W, H2 = 2 * a.H;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
+        int ch, id, iw, ih, b;
+        split(a, e, a.D, a.W, a.H, ch, id, iw, ih, b);
+        int jh[4], jw[4], jd[4];
+        float wh[4], ww[4], wd[4];
+        adj4(ih, a.H, jh, wh);
+        adj4(iw, a.W, jw, ww);
+        adj4(id, a.D, jd, wd);
+        float acc[CV];
+#pragma unroll
+        for (int c = 0; c < CV; ++c) acc[c] = 0.f;
+#pragma unroll
+        for (int x0 = 0; x0 < 4; ++x0)
+#pragma unroll
+            for (int x1 = 0; x1 < 4; ++x1) {
+                const float whw = wh[x0] * ww[x1];
+                const int64_t rowb = ((int64_t(b) * H2 + jh[x0]) * W2 + jw[x1]) * D2;
+                float r[4][CV];
+#pragma unroll
+                for (int x2 = 0; x2 < 4; ++x2) ldv<T, CV>(gy + (rowb + jd[x2]) * a.C + ch * CV, r[x2]);
+#pragma unroll
+                for (int c = 0; c < CV; ++c) {
+                    const float sd = wd[0] * r[0][c] + wd[1] * r[1][c] + wd[2] * r[2][c] + wd[3] * r[3][c];
+                    acc[c] = fmaf(whw, sd, acc[c]);
+                }
+            }
+        const int64_t o = (((int64_t(b) * a.H + ih) * a.W + iw) * a.D + id) * a.C + ch * CV;
+        float xa[CV], ad[CV];
+        if (dv.mode) ldv<T, CV>(aux + o, xa);
+        if (addend) ldv<T, CV>(addend + o, ad);
+#pragma unroll
+        for (int c = 0; c < CV; ++c) {
+            float v = acc[c];
+            pre += v;
+            if (dv.mode) v *= dv(xa[c]);
+            post += v;
+            if (addend) v += ad[c];
+            acc[c] = v;
+        }
+        stv<T, CV>(gx + o, acc);
+    }
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
+        }
+    }
+}
+
+UArgs make_args(int B, int C, int H, int W, int D, int cv, bool fwd) {
+    UArgs a;
+    a.B = B; a.C = C; a.H = H; a.W = W; a.D = D;
+    a.nchunk = C / cv;
+    a.fch = FastDiv(uint32_t(a.nchunk));
+    const int m = fwd ? 2 : 1;
+    a.f1 = FastDiv(uint32_t(m * D));
+    a.f2 = FastDiv(uint32_t(m * W));
+    a.f3 = FastDiv(uint32_t(m * H));
+    return a;
+}
+
+int pick_cv(int dtype, int C, const void *p0, const void *p1, const void *p2, const void *p3) {
+    auto al = [](const void *p, int b) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % b) == 0; };
+    if (dtype != VQ3D_BF16) return 1;
+    if (C % 8 == 0 && al(p0, 16) && al(p1, 16) && al(p2, 16) && al(p3, 16)) return 8;
+    if (C % 4 == 0 && al(p0, 8) && al(p1, 8) && al(p2, 8) && al(p3, 8)) return 4;
+    return 1;
+}
+
+}  // namespace
+
+int launch_up2_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd, const void *x,
+                   int32_t pro_kind, const float *pro_a, const float *pro_b, void *y, hipStream_t s) {
+    if (int64_t(batch) * 8 * h * w * dd * channels >= (int64_t(1) << 31)) return fail("upsample2x: tensor too large");
+    const int cv = pick_cv(dtype, channels, x, y, nullptr, nullptr);
+    const UArgs a = make_args(batch, channels, h, w, dd, cv, true);
+    const int64_t n = int64_t(batch) * 8 * h * w * dd * a.nchunk;
+    const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)));
+    if (dtype == VQ3D_F32)
+        k_up2_fwd<float, 1><<<nb, 256, 0, s>>>(a, (const float *)x, pro_kind, pro_a, pro_b, (float *)y);
+    else if (cv == 8)
+        k_up2_fwd<bf16_t, 8><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, pro_kind, pro_a, pro_b, (bf16_t *)y);
+    else if (cv == 4)
+        k_up2_fwd<bf16_t, 4><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, pro_kind, pro_a, pro_b, (bf16_t *)y);
+    else
+        k_up2_fwd<bf16_t, 1><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, pro_kind, pro_a, pro_b, (bf16_t *)y);
+    return check_launch("upsample2x_fwd");
+}
+
+int launch_up2_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd, const void *gy,
+                   int dmode, const float *dparam, const void *aux, const void *add, void *gx, float *dpre,
+                   float *dpost, hipStream_t s) {
+    if (int64_t(batch) * 8 * h * w * dd * channels >= (int64_t(1) << 31)) return fail("upsample2x: tensor too large");
+    const int cv = pick_cv(dtype, channels, gy, gx, aux, add);
+    const UArgs a = make_args(batch, channels, h, w, dd, cv, false);
+    const int64_t n = int64_t(batch) * h * w * dd * a.nchunk;
+    // grid-stride; bounded so the per-workgroup partial-sum atomics stay few
+    const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)));
+#define UB(T, CV)                                                                                             \
+    k_up2_bwd<T, CV><<<nb, 256, 0, s>>>(a, (const T *)gy, dmode, dparam, (const T *)aux, (const T *)add, (T *)gx, \
+                                        dpre, dpost)
+    if (dtype == VQ3D_F32) UB(float, 1);
+    else if (cv == 8) UB(bf16_t, 8);
+    else if (cv == 4) UB(bf16_t, 4);
+    else UB(bf16_t, 1);
+#undef UB
+    return check_launch("upsample2x_bwd");
+}
+
+}  // namespace vq3d
