@@ -385,7 +385,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     if (rows_path(d, dgrad, fe.res_up2 ? fe.res : nullptr) && al(in) && al(out) && al(fe.res) && al(be.aux) && al(be.addend)) {
         const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
         const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 1023) / 1024, kMaxPwBlocks)));
-        float *part = (want_part && nbx > 32 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
+        float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
         const int key = ci * 16 + co;
         const int pk = dgrad ? VQ3D_PRO_NONE : d->pro_kind;
 #define R(CI, CO)                                                                                              \
@@ -458,7 +458,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     a.vec = al(in) && al(in2) && al(out) && al(out2) && al(be.aux) && al(be.addend) && al(fe.res);
     const int64_t nseg = (a.nvox + a.segv - 1) / a.segv;
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, kMaxPwBlocks)));
-    float *part = (want_part && nbx > 32 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
+    float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
 #define L(C)                                                                                                    \
     case C: {                                                                                                   \
         auto kern = dgrad ? k_pw2<T, C, true> : k_pw2<T, C, false>;                                             \
