@@ -129,47 +129,53 @@ struct MT {
     static constexpr int value = NT <= 2 ? 8 : 4;  // M tiles per wave (accumulators MT * NT * 4 VGPRs)
 };
 
-// pack this workgroup's weight image into LDS: item (c, nn) = 8 bf16 of chunk c for column
-// gi*NTOT + nn; chunk c = ((kh*k + kw)*nch + j) holds window elements e = 8j + t = (kd, ci).
+// one item of the weight image: 8 bf16 of chunk c for column gi*ntot + nn; chunk
+// c = ((kh*k + kw)*nch + j) holds window elements e = 8j + t = (kd, ci)
 template <bool DGRAD>
-__device__ __forceinline__ void pack_weights(const LArgs &a, const float *__restrict__ w, int wCt, int gi, int ntot,
-                                             uint4 *wl) {
+__device__ __forceinline__ uint4 pack_item(const LArgs &a, const float *__restrict__ w, int wCt, int gi, int ntot,
+                                           int it) {
     const int K3 = a.k * a.k * a.k;
-    const int items = a.nks * 4 * ntot;
-    for (int it = threadIdx.x; it < items; it += 256) {
-        const int c = it / ntot, nn = it - c * ntot;
-        const int n = gi * ntot + nn;
-        const int t2 = c / a.nch, j = c - t2 * a.nch;
-        const bool live = c < a.NCH && n < a.N;
-        int e = 8 * j;
-        int kd = int(a.fC.div(uint32_t(e))), ci = e - kd * a.C;
-        uint32_t pk[4];
+    const int c = it / ntot, nn = it - c * ntot;
+    const int n = gi * ntot + nn;
+    const int t2 = c / a.nch, j = c - t2 * a.nch;
+    const bool live = c < a.NCH && n < a.N;
+    int e = 8 * j;
+    int kd = int(a.fC.div(uint32_t(e))), ci = e - kd * a.C;
+    uint32_t pk[4];
 #pragma unroll
-        for (int t = 0; t < 8; t += 2) {
-            float v2[2];
+    for (int t = 0; t < 8; t += 2) {
+        float v2[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                float val = 0.f;
-                if (live && kd < a.k) {
-                    const int tap = t2 * a.k + kd;  // t2 = kh * k + kw
-                    val = DGRAD ? w[(int64_t(ci) * wCt + n) * K3 + (K3 - 1 - tap)]
-                                : w[(int64_t(n) * wCt + ci) * K3 + tap];
-                }
-                v2[h] = val;
-                if (++ci == a.C) {
-                    ci = 0;
-                    ++kd;
-                }
+        for (int h = 0; h < 2; ++h) {
+            float val = 0.f;
+            if (live && kd < a.k) {
+                const int tap = t2 * a.k + kd;  // t2 = kh * k + kw
+                val = DGRAD ? w[(int64_t(ci) * wCt + n) * K3 + (K3 - 1 - tap)] : w[(int64_t(n) * wCt + ci) * K3 + tap];
             }
-            pk[t / 2] = pack2(v2[0], v2[1]);
+            v2[h] = val;
+            if (++ci == a.C) {
+                ci = 0;
+                ++kd;
+            }
         }
-        wl[it] = uint4{pk[0], pk[1], pk[2], pk[3]};
+        pk[t / 2] = pack2(v2[0], v2[1]);
     }
+    return uint4{pk[0], pk[1], pk[2], pk[3]};
+}
+
+// the whole image [group][chunk][ntot] into global memory (caller workspace), once per call
+template <bool DGRAD>
+__global__ __launch_bounds__(256) void k_lines_pack(LArgs a, const float *__restrict__ w, int wCt, int ntot,
+                                                    uint4 *__restrict__ out) {
+    const int items = a.nks * 4 * ntot;
+    const int it = blockIdx.x * 256 + threadIdx.x;
+    if (it < items) out[int64_t(blockIdx.y) * items + it] = pack_item<DGRAD>(a, w, wCt, blockIdx.y, ntot, it);
 }
 
 template <int NT, int ALN, bool DGRAD>
-__global__ __launch_bounds__(256) void k_lines(LArgs a, const bf16_t *__restrict__ x, const bf16_t *__restrict__ x2,
-                                              const float *__restrict__ w, int wCt, FwdEpi<bf16_t> fe,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 || NT == 3) ? 4 : 2))) void k_lines(LArgs a, const bf16_t *__restrict__ x, const bf16_t *__restrict__ x2,
+                                              const float *__restrict__ w, int wCt, const uint4 *__restrict__ wpk,
+                                              FwdEpi<bf16_t> fe,
                                               BwdEpi<bf16_t> be, const float *__restrict__ gscale,
                                               bf16_t *__restrict__ y, bf16_t *__restrict__ y2, float *dpre,
                                               float *dpost) {
@@ -191,7 +197,15 @@ __global__ __launch_bounds__(256) void k_lines(LArgs a, const bf16_t *__restrict
     const int nw = min(NTOT, a.N - gi * NTOT);  // output columns of this group
 
     // ---- once per workgroup: weight image of this N group + chunk offset table
-    pack_weights<DGRAD>(a, w, wCt, gi, NTOT, wl);
+    {
+        const int items = a.nks * 4 * NTOT;
+        if (wpk) {  // pre-packed image: 16-byte copies
+            const uint4 *src = wpk + int64_t(gi) * items;
+            for (int it = tid; it < items; it += 256) wl[it] = src[it];
+        } else {
+            for (int it = tid; it < items; it += 256) wl[it] = pack_item<DGRAD>(a, w, wCt, gi, NTOT, it);
+        }
+    }
     for (int c = tid; c < a.nks * 4; c += 256) {
         int off = 0;  // padding chunks: zero weights, any valid window
         if (c < a.NCH) {
@@ -672,7 +686,8 @@ unsigned resident_blocks(K kernel, size_t lds, unsigned units) {
 }
 
 template <bool DGRAD>
-void launch(const Plan &P, const bf16_t *x, const bf16_t *x2, const float *w, int wCt, const FwdEpi<bf16_t> &fe,
+void launch(const Plan &P, const bf16_t *x, const bf16_t *x2, const float *w, int wCt, const uint4 *wpk,
+            const FwdEpi<bf16_t> &fe,
             const BwdEpi<bf16_t> &be, const float *gscale, bf16_t *y, bf16_t *y2, float *dpre, float *dpost,
             hipStream_t s) {
 #define K(NT, ALN)                                                                                            \
@@ -687,7 +702,7 @@ void launch(const Plan &P, const bf16_t *x, const bf16_t *x2, const float *w, in
         }                                                                                                     \
         const unsigned nb = resident_blocks(kern, P.lds, unsigned(P.a.nbricks));                              \
         const dim3 grid{nb, unsigned(P.a.ntg), 1u};                                                           \
-        kern<<<grid, 256, P.lds, s>>>(P.a, x, x2, w, wCt, fe, be, gscale, y, y2, dpre, dpost);                \
+        kern<<<grid, 256, P.lds, s>>>(P.a, x, x2, w, wCt, wpk, fe, be, gscale, y, y2, dpre, dpost);           \
     }
 #define ALNS(NT)                                                                                              \
     switch (P.aln) {                                                                                          \
@@ -708,13 +723,19 @@ void launch(const Plan &P, const bf16_t *x, const bf16_t *x2, const float *w, in
 
 }  // namespace
 
-size_t lines_workspace(const vq3d_conv_desc *, bool) { return 0; }  // weights are packed in-kernel
+static size_t ws_of(const Plan &P) { return size_t(P.a.ntg) * P.a.nks * 4 * P.a.ntn * 16; }
+
+// packed B-fragment image of every N group (k_lines_pack), filled per call
+size_t lines_workspace(const vq3d_conv_desc *d, bool dgrad) {
+    const Plan P = plan_for(d, dgrad);
+    return P.ok ? ws_of(P) : 0;
+}
 
 bool lines_applicable(const vq3d_conv_desc *d, bool dgrad) { return plan_for(d, dgrad).ok; }
 
 int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void *x2, const float *w, const float *pa,
                  const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
-                 void *y2, float *dpre, float *dpost, void *, size_t, hipStream_t s) {
+                 void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s) {
     Plan P = plan_for(d, dgrad);
     if (!P.ok) return fail("conv(lines): geometry not supported");
     P.a.pro_kind = dgrad ? VQ3D_PRO_NONE : d->pro_kind;
@@ -734,10 +755,19 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
     }();
     P.a.dbg = dbg;
     const int wCt = d->cin + d->cin2;
+    // pre-pack the weights once per call when the caller gave room (else each workgroup packs)
+    const uint4 *wpk = nullptr;
+    if (ws && ws_bytes >= ws_of(P)) {
+        const int items = P.a.nks * 4 * P.a.ntn;
+        const dim3 pg{unsigned((items + 255) / 256), unsigned(P.a.ntg), 1u};
+        if (dgrad) k_lines_pack<true><<<pg, 256, 0, s>>>(P.a, w, wCt, P.a.ntn, static_cast<uint4 *>(ws));
+        else k_lines_pack<false><<<pg, 256, 0, s>>>(P.a, w, wCt, P.a.ntn, static_cast<uint4 *>(ws));
+        wpk = static_cast<const uint4 *>(ws);
+    }
     if (dgrad)
-        launch<true>(P, (const bf16_t *)x, nullptr, w, wCt, fe, be, gscale, (bf16_t *)y, (bf16_t *)y2, dpre, dpost, s);
+        launch<true>(P, (const bf16_t *)x, nullptr, w, wCt, wpk, fe, be, gscale, (bf16_t *)y, (bf16_t *)y2, dpre, dpost, s);
     else
-        launch<false>(P, (const bf16_t *)x, (const bf16_t *)x2, w, wCt, fe, be, nullptr, (bf16_t *)y, nullptr,
+        launch<false>(P, (const bf16_t *)x, (const bf16_t *)x2, w, wCt, wpk, fe, be, nullptr, (bf16_t *)y, nullptr,
                       nullptr, nullptr, s);
     return check_launch(dgrad ? "conv3d_bwd_data(lines)" : "conv3d_fwd(lines)");
 }

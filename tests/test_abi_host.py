@@ -50,15 +50,16 @@ def test_conv_descriptor_validation_and_workspace():
                       kernel=3, stride=1, pad=1, pad_mode=1, pro_kind=0)
     rc = L.load().vq3d_conv3d_fwd(ctypes.byref(good), None, None, None, None, None, None, None, None, 0, None)
     assert rc < 0 and b"null" in L.load().vq3d_last_error()
-    # workspace sizes (host-only planning): the 1x1 weight gradient keeps per-workgroup partials;
-    # the k^3 MFMA engine packs its weights in-kernel (no scratch)
+    # workspace sizes (host-only planning): the 1x1 weight gradient keeps per-workgroup partials,
+    # the k^3 MFMA engine its packed bf16 weight fragments
     d3 = L.ConvDesc(dtype=1, batch=1, cin=9, cin2=0, cout=9, in_h=128, in_w=128, in_d=32, out_h=128, out_w=128,
                     out_d=32, kernel=3, stride=1, pad=1, pad_mode=1, pro_kind=2)
-    assert L.query("vq3d_conv3d_workspace_size", ctypes.byref(d3), L.PASS_FWD) == 0
+    assert L.query("vq3d_conv3d_workspace_size", ctypes.byref(d3), L.PASS_FWD) > 0
+    assert L.query("vq3d_conv3d_workspace_size", ctypes.byref(d3), L.PASS_BWD_DATA) > 0
     d1 = L.ConvDesc(dtype=1, batch=1, cin=18, cin2=0, cout=9, in_h=128, in_w=128, in_d=32, out_h=128, out_w=128,
                     out_d=32, kernel=1, stride=1, pad=0, pad_mode=0, pro_kind=2)
     assert L.query("vq3d_conv3d_workspace_size", ctypes.byref(d1), L.PASS_BWD_WEIGHT) >= 9 * 19 * 4
-    d3.dtype = 0
+    d3.dtype = 0  # fp32 k^3 runs on the VALU engine: no scratch
     assert L.query("vq3d_conv3d_workspace_size", ctypes.byref(d3), L.PASS_FWD) == 0
 
 
