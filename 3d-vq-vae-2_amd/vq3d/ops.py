@@ -153,10 +153,53 @@ def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None
                ctypes.byref(epi), L.ptr(gx), _p(gx2), _p(dpro_pre), _p(dpro_post), _p(ws), wsb, s)
     if dw is None and dscale is None and dbias is None and dcbias is None:
         return gx, gx2
+    if _concurrent:
+        # the weight gradient only reads x and g: run it on the side stream, overlapped with the
+        # backward-data chain on the main stream (joined before the optimizer, join_side())
+        main = torch.cuda.current_stream()
+        side = _side_stream(x.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            ws, wsb = _ws(desc, L.PASS_BWD_WEIGHT, x.device)
+            L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb),
+                   L.ptr(w), _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), _p(ws), wsb, L.stream())
+        for t in (x, x2, g):
+            if t is not None:
+                t.record_stream(side)
+        return gx, gx2
     ws, wsb = _ws(desc, L.PASS_BWD_WEIGHT, x.device)
     L.call("vq3d_conv3d_bwd_weight", ctypes.byref(desc), L.ptr(x), _p(x2), L.ptr(g), _p(pa), _p(pb), L.ptr(w),
            _p(escale), _p(dw), _p(dscale), _p(dbias), _p(dcbias), _p(ws), wsb, s)
     return gx, gx2
+
+
+# ------------------------------------------------------------------------------------------------ streams
+_concurrent = False
+_side = {}
+
+
+def set_concurrent_wgrad(enabled=True):
+    """Run every conv weight gradient on a per-device side stream, overlapped with the
+    backward-data chain (the two only share read-only inputs and write disjoint gradient
+    entries).  join_side() must precede any read of the gradients (the optimizer and the
+    gradient all-reduce call it)."""
+    global _concurrent
+    _concurrent = bool(enabled)
+
+
+def _side_stream(device):
+    s = _side.get(device.index)
+    if s is None:
+        s = _side[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
+def join_side():
+    """Current stream waits for all weight-gradient work issued on the side streams."""
+    if _side:
+        cur = torch.cuda.current_stream()
+        for s in _side.values():
+            cur.wait_stream(s)
 
 
 # ------------------------------------------------------------------------------------------------ upsample

@@ -4,6 +4,7 @@ the flat parameter buffer.  state_dict() uses torch Adam's per-parameter layout
 import torch
 
 from . import _lib as L
+from . import ops
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -30,6 +31,7 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        ops.join_side()  # weight gradients issued on the side stream are complete
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         f = self.flat

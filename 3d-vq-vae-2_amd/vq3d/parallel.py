@@ -54,6 +54,8 @@ class GradientAllReduce:
     def __call__(self):
         if self.world == 1:
             return
+        from . import ops
+        ops.join_side()
         if self.backend == "nccl":
             dist.all_reduce(self.flat.grad, op=dist.ReduceOp.AVG, group=self.group)
         else:  # gloo (CPU test transport): SUM then divide

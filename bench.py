@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="print per-step times to stderr")
+    p.add_argument("--serial-wgrad", action="store_true",
+                   help="run weight gradients on the main stream (default: side stream, overlapped)")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
     return p.parse_args()
@@ -138,6 +140,8 @@ def main():
     if a.size:
         size = tuple(a.size)
     torch.manual_seed(0)
+    from vq3d import ops
+    ops.set_concurrent_wgrad(not a.serial_wgrad)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
     model.train()

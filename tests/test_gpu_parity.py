@@ -226,3 +226,51 @@ def test_model_bf16_step(gpu):
     ref = float(d["step0/loss"])
     assert abs(float(loss) - ref) <= 0.02 * ref, (float(loss), ref)
     assert torch.isfinite(m.flat.data).all()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_concurrent_wgrad_and_graph_replay_match_serial(gpu, graph):
+    """Weight gradients on the side stream (and the whole step captured / replayed as a HIP
+    graph) give the same gradients and updated weights as the serial eager step: only the
+    fp32-atomic summation order may differ."""
+    from vq3d import ops
+
+    def run(concurrent, use_graph):
+        ops.set_concurrent_wgrad(concurrent)
+        try:
+            m, _ = load_model("model_2l_blocks_32", gpu, "bf16")
+            opt = m.configure_optimizers()
+            x = (torch.rand((1, 1, 32, 32, 32), generator=torch.Generator().manual_seed(4)) * 4.5 - 0.5).to(gpu)
+            nvs = torch.tensor([32], device=gpu)
+
+            def step():
+                opt.zero_grad()
+                loss = m.training_step((x, nvs), 0)
+                loss.backward()
+                opt.step()
+                return loss
+
+            step()  # first pass (codebook init) eagerly
+            if use_graph:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    step()
+                torch.cuda.current_stream().wait_stream(side)
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    step()
+                gr.replay()
+            else:
+                step()
+                step()
+            torch.cuda.synchronize()
+            return m.flat.grad.clone(), m.flat.data.clone()
+        finally:
+            ops.set_concurrent_wgrad(False)
+
+    g0, w0 = run(False, False)
+    g1, w1 = run(True, graph)
+    scale = g0.abs().max()
+    assert float((g1 - g0).abs().max()) <= 2e-2 * float(scale), float((g1 - g0).abs().max() / scale)
+    assert float((w1 - w0).abs().max()) <= 1e-3 * float(w0.abs().max())
