@@ -757,7 +757,8 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
     const int wCt = d->cin + d->cin2;
     // pre-pack the weights once per call when the caller gave room (else each workgroup packs)
     const uint4 *wpk = nullptr;
-    if (ws && ws_bytes >= ws_of(P)) {
+    const int items_per_wg = P.a.nks * 4 * P.a.ntn;
+    if (items_per_wg > 2048 && ws && ws_bytes >= ws_of(P)) {  // small images are packed in-kernel
         const int items = P.a.nks * 4 * P.a.ntn;
         const dim3 pg{unsigned((items + 255) / 256), unsigned(P.a.ntg), 1u};
         if (dgrad) k_lines_pack<true><<<pg, 256, 0, s>>>(P.a, w, wCt, P.a.ntn, static_cast<uint4 *>(ws));

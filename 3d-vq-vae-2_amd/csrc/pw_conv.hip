@@ -429,7 +429,8 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     }
     a.Cin = a.Ca + a.Cb;
     a.CinP = (a.Cin + 7) / 8 * 8;
-    const int cot = a.N <= 1 ? 1 : a.N <= 2 ? 2 : a.N <= 4 ? 4 : a.N <= 8 ? 8 : a.N <= 12 ? 12 : 16;
+    int cot = a.N <= 1 ? 1 : a.N <= 2 ? 2 : a.N <= 4 ? 4 : a.N <= 8 ? 8 : a.N <= 12 ? 12 : 16;
+    if (nvox <= 8192 && cot > 4) cot = 4;  // tiny grids: split each voxel's outputs over more threads
     const int NP = (a.N + cot - 1) / cot * cot;
     // voxels per segment: 256 (one thread each) unless the grid would leave CUs idle; then
     // fewer voxels with several threads splitting each voxel's output tiles

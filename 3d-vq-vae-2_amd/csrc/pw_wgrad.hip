@@ -77,11 +77,43 @@ __device__ __forceinline__ void stage(float *__restrict__ dst, int P, int off, c
     }
 }
 
+// Final accumulation of one gradient entry e = co * (Ct + 1) + ci into the fp32 gradients
+// (atomics: the reduce kernel owns an entry exclusively, direct-mode workgroups are few);
+// the scale / scalar-bias contributions go to wg / bs for a block reduction.
+struct WgOut {
+    const float *w, *escale;
+    float *dw, *dscale, *dbias, *dcbias;
+};
+
+__device__ __forceinline__ void finish_entry(const WgOut &o, int e, int Ct, float sum, float &wg, float &bs) {
+    const int co = e / (Ct + 1), ci = e - co * (Ct + 1);
+    if (ci < Ct) {
+        const int64_t idx = int64_t(co) * Ct + ci;
+        if (o.dw) atomicAdd(o.dw + idx, o.escale ? sum * *o.escale : sum);
+        if (o.dscale) wg = fmaf(o.w[idx], sum, wg);
+    } else {
+        if (o.dcbias) atomicAdd(o.dcbias + co, sum);
+        bs += sum;
+    }
+}
+
+__device__ __forceinline__ void finish_block(const WgOut &o, float wg, float bs, float *red) {
+    if (o.dscale) {
+        wg = block_sum<float, 256>(wg, red);
+        if (threadIdx.x == 0) atomicAdd(o.dscale, wg);
+    }
+    if (o.dbias) {
+        bs = block_sum<float, 256>(bs, red + 4);
+        if (threadIdx.x == 0) atomicAdd(o.dbias, bs);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_pw_wgrad(PwwArgs a, const T *__restrict__ x, const T *__restrict__ x2,
                                                  const T *__restrict__ g, int pro_kind, const float *pro_a,
-                                                 const float *pro_b, float *__restrict__ part) {
+                                                 const float *pro_b, float *__restrict__ part, WgOut out) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
+    __shared__ float red[8];
     float *xs = sm;                     // [seg][Xp]
     float *gs = sm + a.seg * a.Xp;      // [seg][Gp]
     const int tid = threadIdx.x;
@@ -139,6 +171,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad(PwwArgs a, const T *__restrict
     for (int q = 0; q < TI * TO; ++q) sm[q * 256 + tid] = acc[q / TO][q % TO];
     __syncthreads();
     const int nblk = gridDim.x;
+    float wg = 0.f, bs = 0.f;
     for (int idx = tid; idx < a.tpb * TI * TO; idx += 256) {
         const int q = idx / a.tpb, t = idx - q * a.tpb;
         const int tt = blockIdx.y * a.tpb + t;
@@ -147,8 +180,10 @@ __global__ __launch_bounds__(256) void k_pw_wgrad(PwwArgs a, const T *__restrict
         if (co >= a.N || ci > Ct) continue;
         float sum = 0.f;
         for (int j = 0; j < a.S; ++j) sum += sm[q * 256 + j * a.tpb + t];
-        part[int64_t(co * (Ct + 1) + ci) * nblk + blockIdx.x] = sum;
+        if (part) part[int64_t(co * (Ct + 1) + ci) * nblk + blockIdx.x] = sum;
+        else finish_entry(out, co * (Ct + 1) + ci, Ct, sum, wg, bs);
     }
+    if (!part) finish_block(out, wg, bs, red);
 }
 
 // Few-channel convs (x: CX, g: CG channels, both in {1, 2, 4, 8}, one input): each thread
@@ -190,9 +225,10 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[C])
 template <typename T, int CX, int CG>
 __global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__restrict__ x,
                                                      const T *__restrict__ g, int pro_kind, const float *pro_a,
-                                                     const float *pro_b, float *__restrict__ part) {
+                                                     const float *pro_b, float *__restrict__ part, WgOut out) {
     constexpr int NE = CG * (CX + 1);
     __shared__ float wred[4][NE];
+    __shared__ float red[8];
     const Prologue pro = make_prologue(pro_kind, pro_a, pro_b);
     float acc[CG][CX + 1];
 #pragma unroll
@@ -236,10 +272,14 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__r
             if (lane == 0) wred[wv][j * (CX + 1) + i] = t;
         }
     __syncthreads();
+    float wg = 0.f, bs = 0.f;
     if (threadIdx.x < NE) {
         const int e = threadIdx.x;
-        part[int64_t(e) * gridDim.x + blockIdx.x] = (wred[0][e] + wred[1][e]) + (wred[2][e] + wred[3][e]);
+        const float sum = (wred[0][e] + wred[1][e]) + (wred[2][e] + wred[3][e]);
+        if (part) part[int64_t(e) * gridDim.x + blockIdx.x] = sum;
+        else finish_entry(out, e, CX, sum, wg, bs);
     }
+    if (!part) finish_block(out, wg, bs, red);
 }
 
 // G = sum over the workgroup partials (part[entry][blk], fixed-order shuffle tree per entry);
@@ -346,7 +386,10 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     if (!workspace || ws_bytes < size_t(nbx) * a.ne * 4) return fail("conv3d_bwd_weight: workspace too small");
     auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     a.vec = al(x) && al(g) && (!x2 || al(x2));
-    float *part = static_cast<float *>(workspace);
+    // few workgroups: each adds its partial straight into the gradients (no reduce launch)
+    const bool direct = nbx <= 16;
+    float *part = direct ? nullptr : static_cast<float *>(workspace);
+    const WgOut out{w, escale, dw, dscale, dbias, dcbias};
     const dim3 grid{unsigned(nbx), unsigned(ytiles), 1u};
     if (reg_path(d) && a.vec) {
         const int key = d->cin * 16 + d->cout;
@@ -355,10 +398,10 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     case CX * 16 + CG:                                                                                         \
         if (bf)                                                                                                \
             k_pw_wgrad_reg<bf16_t, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,  \
-                                                               d->pro_kind, pro_a, pro_b, part);              \
+                                                               d->pro_kind, pro_a, pro_b, part, out);         \
         else                                                                                                   \
             k_pw_wgrad_reg<float, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,     \
-                                                              d->pro_kind, pro_a, pro_b, part);               \
+                                                              d->pro_kind, pro_a, pro_b, part, out);          \
         break;
         switch (key) {
             REG(1, 1) REG(1, 2) REG(1, 4) REG(1, 8) REG(2, 1) REG(2, 2) REG(2, 4) REG(2, 8)
@@ -368,10 +411,11 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
 #undef REG
     } else if (d->dtype == VQ3D_BF16)
         k_pw_wgrad<bf16_t><<<grid, 256, lds, s>>>(a, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g,
-                                                   d->pro_kind, pro_a, pro_b, part);
+                                                   d->pro_kind, pro_a, pro_b, part, out);
     else
         k_pw_wgrad<float><<<grid, 256, lds, s>>>(a, (const float *)x, (const float *)x2, (const float *)g,
-                                                  d->pro_kind, pro_a, pro_b, part);
+                                                  d->pro_kind, pro_a, pro_b, part, out);
+    if (direct) return check_launch("conv3d_bwd_weight(pointwise)");
     const int Ct = a.Ca + a.Cb;
     int lanes = 1;
     while (lanes < 64 && lanes * 32 < nbx) lanes *= 2;
