@@ -19,6 +19,7 @@
 //     chunk of one output row; partial sums leave each workgroup as fp32 atomics straight
 //     into the parameter-gradient buffer (no partial slabs, no finalize pass).
 #include "common.h"
+#include "conv_epi.h"
 #include "engines.h"
 
 #include <algorithm>
@@ -28,144 +29,6 @@
 #include <cstdlib>
 #include <type_traits>
 
-namespace vq3d {
-
-struct ConvArgs {
-    int B, Cin, Cin2, Cout;
-    int iH, iW, iD, oH, oW, oD;
-    int k, s, p, circ;
-    int pro_kind;
-    const float *pro_a, *pro_b;
-};
-
-static ConvArgs make_args(const vq3d_conv_desc *d, const float *pa, const float *pb) {
-    ConvArgs a;
-    a.B = d->batch;
-    a.Cin = d->cin;
-    a.Cin2 = d->cin2;
-    a.Cout = d->cout;
-    a.iH = d->in_h; a.iW = d->in_w; a.iD = d->in_d;
-    a.oH = d->out_h; a.oW = d->out_w; a.oD = d->out_d;
-    a.k = d->kernel; a.s = d->stride; a.p = d->pad; a.circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
-    a.pro_kind = d->pro_kind;
-    a.pro_a = pa;
-    a.pro_b = pb;
-    return a;
-}
-
-// wrap into [0, n) for |i| < a few n (no integer division)
-__device__ __forceinline__ int wrap(int i, int n) {
-    while (i < 0) i += n;
-    while (i >= n) i -= n;
-    return i;
-}
-
-// forward tap: output coordinate o, kernel offset t -> input coordinate, or -1 if in zero padding
-__device__ __forceinline__ int fwd_index(int o, int t, int s, int p, int n, int circ) {
-    const int i = o * s + t - p;
-    if (circ) return wrap(i, n);
-    return (i < 0 || i >= n) ? -1 : i;
-}
-
-// transposed tap: input coordinate i, kernel offset t -> output coordinate o with
-// fwd_index(o, t) == i, or -1 if none (unique when it exists: DESIGN.md §conv)
-__device__ __forceinline__ int bwd_index(int i, int t, int s, int p, int n_in, int n_out, int circ) {
-    int r = i - t + p;
-    if (circ) r = wrap(r, n_in);
-    else if (r < 0) return -1;
-    if (s == 2) {
-        if (r & 1) return -1;
-        r >>= 1;
-    } else if (s != 1) {
-        if (r % s) return -1;
-        r /= s;
-    }
-    return r < n_out ? r : -1;
-}
-
-__device__ __forceinline__ void atomic_add_f(float *p, float v) {
-    if (p) atomicAdd(p, v);
-}
-
-template <typename T>
-__device__ __forceinline__ ActDeriv make_deriv(const BwdEpi<T> &e) {
-    ActDeriv d;
-    d.mode = e.aux ? e.mode : 0;
-    d.p = (d.mode && e.p) ? *e.p : 0.f;
-    return d;
-}
-
-// y[v, co] for one voxel's accumulators (shared by the pointwise and the k > 1 forward)
-template <typename T, int COT>
-__device__ __forceinline__ void fwd_epilogue(const ConvArgs &a, const FwdEpi<T> &e, const float (&acc)[COT],
-                                             int64_t v, int co0, T *__restrict__ yp) {
-    const float sc = e.scale ? *e.scale : 1.f;
-    const float bi = e.bias ? *e.bias : 0.f;
-    const float aa = e.act_a ? *e.act_a : 0.f, ab = e.act_b ? *e.act_b : 0.f;
-    int h0 = 0, h1 = 0, w0 = 0, w1 = 0, d0 = 0, d1 = 0, b = 0;
-    float lh = 0.f, lw = 0.f, ldd = 0.f;
-    const int rH = a.oH / 2, rW = a.oW / 2, rD = a.oD / 2;
-    if (e.res && e.res_up2) {
-        int64_t t = v;
-        const int od = int(t % a.oD); t /= a.oD;
-        const int ow = int(t % a.oW); t /= a.oW;
-        const int oh = int(t % a.oH);
-        b = int(t / a.oH);
-        up_coeff(oh, rH, h0, h1, lh);
-        up_coeff(ow, rW, w0, w1, lw);
-        up_coeff(od, rD, d0, d1, ldd);
-    }
-#pragma unroll
-    for (int c = 0; c < COT; ++c) {
-        const int co = co0 + c;
-        if (co >= a.Cout) break;
-        float val = acc[c];
-        if (e.scale) val = val * sc;
-        if (e.bias) val = val + bi;
-        if (e.cbias) val = val + e.cbias[co];
-        if (e.res) {
-            if (!e.res_up2) {
-                val = val + ld(e.res + v * a.Cout + co);
-            } else {
-                auto R = [&](int hh, int ww, int dd) {
-                    return ld(e.res + (((int64_t(b) * rH + hh) * rW + ww) * rD + dd) * a.Cout + co);
-                };
-                val = val + ((1.f - lh) * ((1.f - lw) * ((1.f - ldd) * R(h0, w0, d0) + ldd * R(h0, w0, d1)) +
-                                          lw * ((1.f - ldd) * R(h0, w1, d0) + ldd * R(h0, w1, d1))) +
-                             lh * ((1.f - lw) * ((1.f - ldd) * R(h1, w0, d0) + ldd * R(h1, w0, d1)) +
-                                   lw * ((1.f - ldd) * R(h1, w1, d0) + ldd * R(h1, w1, d1))));
-            }
-        }
-        st(yp + co, epi_act(e.act, val, aa, ab));
-    }
-}
-
-// gx[v, ci] for one voxel's accumulators; returns the (pre, post) contributions
-template <typename T, int CIT>
-__device__ __forceinline__ void bwd_epilogue(const ConvArgs &a, const BwdEpi<T> &e, const ActDeriv &dv, float gs,
-                                             bool has_gs, const float (&acc)[CIT], int64_t v, int ci0,
-                                             T *__restrict__ gxr, T *__restrict__ gx2r, float &pre, float &post) {
-    const int Ct = a.Cin + a.Cin2;
-#pragma unroll
-    for (int c = 0; c < CIT; ++c) {
-        const int ci = ci0 + c;
-        if (ci >= Ct) break;
-        float val = acc[c];
-        if (has_gs) val = val * gs;
-        if (ci < a.Cin) {
-            const int64_t o = v * a.Cin + ci;
-            pre += val;
-            if (dv.mode) val = val * dv(ld(e.aux + o));
-            post += val;
-            if (e.addend) val = val + ld(e.addend + o);
-            st(gxr + ci, val);
-        } else {
-            st(gx2r + (ci - a.Cin), val);
-        }
-    }
-}
-
-}  // namespace vq3d
 #include "conv_mfma.inc"
 namespace vq3d {
 
@@ -669,6 +532,16 @@ static int launch_pw(const vq3d_conv_desc *d, const ConvArgs &a, const void *in,
     return check_launch(DGRAD ? "conv3d_bwd_data(pointwise)" : "conv3d_fwd(pointwise)");
 }
 
+// small grids with many channels: reduction split over workgroups (conv_small.hip);
+// VQ3D_NO_SMALL=1 disables it (A/B measurements)
+static bool use_small(const vq3d_conv_desc *d, bool dgrad) {
+    static const bool off = [] {
+        const char *e = std::getenv("VQ3D_NO_SMALL");
+        return e && e[0] == '1';
+    }();
+    return !off && small_applicable(d, dgrad);
+}
+
 template <typename T>
 static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, const float *w, const float *pa,
                       const float *pb, const vq3d_conv_epilogue *epi, void *y, void *ws, size_t ws_bytes,
@@ -683,6 +556,11 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
         BwdEpi<T> be = {};
         if (!legacy_pw()) return launch_pw1<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes, s);
         return launch_pw<T, false>(d, a, x, x2, w, fe, be, nullptr, y, nullptr, nullptr, nullptr, s);
+    }
+    if (use_small(d, false)) {
+        BwdEpi<T> be = {};
+        return launch_small<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes,
+                               s);
     }
     if constexpr (std::is_same<T, bf16_t>::value) {
         if (lines_applicable(d, false)) {
@@ -733,6 +611,11 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
         if (!legacy_pw()) return launch_pw1<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes, s);
         return launch_pw<T, true>(d, a, g, nullptr, w, fe, be, gscale, gx, gx2, dpre, dpost, s);
     }
+    if (use_small(d, true)) {
+        FwdEpi<T> fe = {};
+        return launch_small<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes,
+                               s);
+    }
     if constexpr (std::is_same<T, bf16_t>::value) {
         // stride-1 backward-data == forward conv of g with the flipped, transposed kernel
         if (lines_applicable(d, true)) {
@@ -769,6 +652,18 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
     return check_launch("conv3d_bwd_data");
 }
 
+// k^3 weight gradient engine choice (bf16): the lines engine for wide inputs (>= 32 channels:
+// 36 -> 36 at 32x32x8 runs 4.7x faster than the direct MFMA engine) or where the direct engine
+// does not apply; the direct engine for the few-channel large grids, where it is measured
+// faster (9 -> 9 at 128^2 x 32 on par, 4 -> 4 at 256^2 x 64 1.9x).
+static bool use_lines_wgrad(const vq3d_conv_desc *d) {
+    if (d->dtype != VQ3D_BF16 || !lines_wgrad_applicable(d)) return false;
+    if (d->cin + d->cin2 >= 32 || mfma_disabled()) return true;
+    return !plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
+                      d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)
+                .ok;
+}
+
 template <typename T>
 static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pa,
                         const float *pb, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
@@ -780,8 +675,8 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     if (is_pointwise(d))
         return launch_pw_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
     if constexpr (std::is_same<T, bf16_t>::value) {
-        if (lines_wgrad_applicable(d))
-            return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, s);
+        if (use_lines_wgrad(d))
+            return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
         if (!mfma_disabled()) {
             MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
                                 d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true);
@@ -866,9 +761,12 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
 
 size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
     if (validate(d)) return 0;
+    if (pass != VQ3D_PASS_BWD_WEIGHT && !is_pointwise(d) && use_small(d, pass == VQ3D_PASS_BWD_DATA))
+        return small_workspace(d, pass == VQ3D_PASS_BWD_DATA);
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
     if (pass == VQ3D_PASS_BWD_DATA) return is_pointwise(d) ? pw_dgrad_workspace(d) : lines_workspace(d, true);
-    return is_pointwise(d) ? pw_wgrad_workspace(d) : 0;
+    if (is_pointwise(d)) return pw_wgrad_workspace(d);
+    return use_lines_wgrad(d) ? lines_wgrad_workspace(d) : 0;
 }
 
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,

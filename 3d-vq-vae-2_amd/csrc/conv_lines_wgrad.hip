@@ -48,7 +48,10 @@ struct WArgs {
     int nbh, nbw, nbd, nbricks;
     int wCt;                   // weight's 2nd dim
     int gvec;                  // g runs of bd*N elements are 16-B aligned multiples of 8
-    FastDiv fC, fhw, fN;
+    int mc;                    // 8-element chunks per line run (C % 4 != 0 staging)
+    int nent;                  // partial entries per workgroup: N * C * k^3 weights + N g sums
+    int64_t xtotal;            // elements of x
+    FastDiv fC, fhw, fN, fCr, fmc;
 };
 
 __device__ __forceinline__ s16x4 tr_read(const bf16_t *p) {
@@ -68,8 +71,7 @@ __device__ __forceinline__ int wrapw(int i, int n) {
 template <int NTM, int NPW>
 __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__restrict__ x,
                                                     const bf16_t *__restrict__ x2, const bf16_t *__restrict__ g,
-                                                    const float *__restrict__ w, const float *__restrict__ escale,
-                                                    float *dw, float *dscale, float *dbias, float *dcbias) {
+                                                    float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float red[8];
     const int nlines = a.hh * a.hw;
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
     const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
     const bool raw = pro.kind == VQ3D_PRO_NONE;
     const int tile0 = blockIdx.y * 4 * NPW;
-    const bool do_bias = blockIdx.y == 0 && (dbias || dcbias);
+    const bool do_bias = blockIdx.y == 0;
 
     // this lane's B column offset (element) per owned tile: (kh, kw) line delta + column chunk
     int coff[NPW];
@@ -109,55 +111,115 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
         const int ih0 = oh0 * a.s - a.p, iw0 = ow0 * a.s - a.p, id0 = od0 * a.s - a.p;
         __syncthreads();
         // ---- lines: element (pos, c) at line*LS + pad0 + pos*CS + c; padding channels and
-        // the slack are zero.  Unit = one position's CS channels.
-        {
-            const int64_t bbase = int64_t(b) * a.iH * a.iW * a.iD;
-            const int total = nlines * a.LP;
-            for (int u = tid; u < total; u += 256) {
-                const int ln = u / a.LP, pos = u - ln * a.LP;
-                const int lh_ = int(a.fhw.div(uint32_t(ln))), lw_ = ln - lh_ * a.hw;
-                int ih = ih0 + lh_, iw = iw0 + lw_, id = id0 + pos;
-                bool ok;
-                if (a.circ) {
-                    ih = wrapw(ih, a.iH);
-                    iw = wrapw(iw, a.iW);
-                    id = wrapw(id, a.iD);
-                    ok = true;
-                } else {
-                    ok = unsigned(ih) < unsigned(a.iH) && unsigned(iw) < unsigned(a.iW) && unsigned(id) < unsigned(a.iD);
-                }
-                const int64_t vox = bbase + (int64_t(ih) * a.iW + iw) * a.iD + id;
-                bf16_t *dst = lines + ln * a.LS + a.pad0 + pos * a.CS;
-                if (ok && a.Cb == 0 && (a.C & 3) == 0) {
-                    const uint2 *src = reinterpret_cast<const uint2 *>(x + vox * a.C);
-                    for (int c4 = 0; c4 < a.C / 4; ++c4) {
-                        uint2 qv = src[c4];
-                        if (!raw) {
-                            auto f = [&](uint32_t uu) {
-                                const float lo = pro.apply(__uint_as_float(uu << 16));
-                                const float hi = pro.apply(__uint_as_float(uu & 0xffff0000u));
-                                return uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
-                            };
-                            qv = uint2{f(qv.x), f(qv.y)};
-                        }
-                        reinterpret_cast<uint2 *>(dst)[c4] = qv;
+        // the slack are zero.
+        if (a.Cb == 0 && (a.C & 3) != 0) {
+            // C not a multiple of 4 (1, 2, 9 channels): a line's in-grid positions are one
+            // contiguous run of x, read with 16-byte loads and scattered to the CS-padded slots
+            for (int e = tid; e < nlines * a.LS / 8; e += 256) reinterpret_cast<uint4 *>(lines)[e] = uint4{0, 0, 0, 0};
+            __syncthreads();
+            const int pa = max(0, -id0), pb = min(a.LP, a.iD - id0);
+            if (pb > pa) {
+                for (int u = tid; u < nlines * a.mc; u += 256) {
+                    const int ln = int(a.fmc.div(uint32_t(u))), ch = u - ln * a.mc;
+                    const int lh_ = int(a.fhw.div(uint32_t(ln))), lw_ = ln - lh_ * a.hw;
+                    int ih = ih0 + lh_, iw = iw0 + lw_;
+                    if (a.circ) {
+                        ih = wrapw(ih, a.iH);
+                        iw = wrapw(iw, a.iW);
+                    } else if (unsigned(ih) >= unsigned(a.iH) || unsigned(iw) >= unsigned(a.iW)) {
+                        continue;
                     }
-                } else {
-                    for (int c = 0; c < a.CS; ++c) {
-                        bf16_t v = 0;
-                        if (ok && c < a.C) {
-                            const bf16_t *src = c < a.Ca ? x + vox * a.Ca + c : x2 + vox * a.Cb + (c - a.Ca);
-                            v = raw ? *src : f2bf(pro.apply(ld(src)));
+                    const int64_t lbase = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD * a.C;
+                    const int64_t E0 = lbase + int64_t(pa + id0) * a.C, E1 = lbase + int64_t(pb + id0) * a.C;
+                    const int64_t cs = (E0 & ~int64_t(7)) + int64_t(ch) * 8;
+                    if (cs >= E1) continue;
+                    bf16_t el[8];
+                    if (cs + 8 <= a.xtotal) {
+                        const uint4 qv = *reinterpret_cast<const uint4 *>(x + cs);
+                        const bf16_t *q8 = reinterpret_cast<const bf16_t *>(&qv);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) el[j] = q8[j];
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) el[j] = cs + j < a.xtotal ? x[cs + j] : bf16_t(0);
+                    }
+                    const int j0 = cs < E0 ? int(E0 - cs) : 0;
+                    const int rel = int(cs + j0 - lbase);
+                    int idd = int(a.fCr.div(uint32_t(rel))), c = rel - idd * a.C;
+                    bf16_t *dst = lines + ln * a.LS + a.pad0 + (idd - id0) * a.CS;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (j < j0 || cs + j >= E1) continue;
+                        dst[c] = raw ? el[j] : f2bf(pro.apply(__uint_as_float(uint32_t(el[j]) << 16)));
+                        if (++c == a.C) {
+                            c = 0;
+                            dst += a.CS;
                         }
-                        dst[c] = v;
                     }
                 }
             }
-            const int tail0 = a.pad0 + a.LP * a.CS;
-            const int z = a.LS - tail0 + a.pad0;
-            for (int e = tid; e < nlines * z; e += 256) {
-                const int ln = e / z, r = e - ln * z;
-                lines[ln * a.LS + (r < a.pad0 ? r : tail0 + r - a.pad0)] = 0;
+            const int nw = pb > pa ? pa + (a.LP - pb) : a.LP;
+            if (a.circ && nw > 0) {  // positions outside [pa, pb) wrap around D (zero padding: zeros)
+                for (int u = tid; u < nlines * nw * a.C; u += 256) {
+                    const int lk = int(a.fCr.div(uint32_t(u))), r = u - lk * a.C;  // r = channel
+                    const int ln = lk / nw, k = lk - ln * nw;
+                    const int pos = pb > pa ? (k < pa ? k : pb + (k - pa)) : k;
+                    const int lh_ = int(a.fhw.div(uint32_t(ln))), lw_ = ln - lh_ * a.hw;
+                    const int ih = wrapw(ih0 + lh_, a.iH), iw = wrapw(iw0 + lw_, a.iW), id = wrapw(id0 + pos, a.iD);
+                    const bf16_t v = x[(((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id) * a.C + r];
+                    lines[ln * a.LS + a.pad0 + pos * a.CS + r] = raw ? v : f2bf(pro.apply(ld(&v)));
+                }
+            }
+        } else {
+            {
+                const int64_t bbase = int64_t(b) * a.iH * a.iW * a.iD;
+                const int total = nlines * a.LP;
+                for (int u = tid; u < total; u += 256) {
+                    const int ln = u / a.LP, pos = u - ln * a.LP;
+                    const int lh_ = int(a.fhw.div(uint32_t(ln))), lw_ = ln - lh_ * a.hw;
+                    int ih = ih0 + lh_, iw = iw0 + lw_, id = id0 + pos;
+                    bool ok;
+                    if (a.circ) {
+                        ih = wrapw(ih, a.iH);
+                        iw = wrapw(iw, a.iW);
+                        id = wrapw(id, a.iD);
+                        ok = true;
+                    } else {
+                        ok = unsigned(ih) < unsigned(a.iH) && unsigned(iw) < unsigned(a.iW) && unsigned(id) < unsigned(a.iD);
+                    }
+                    const int64_t vox = bbase + (int64_t(ih) * a.iW + iw) * a.iD + id;
+                    bf16_t *dst = lines + ln * a.LS + a.pad0 + pos * a.CS;
+                    if (ok && a.Cb == 0 && (a.C & 3) == 0) {
+                        const uint2 *src = reinterpret_cast<const uint2 *>(x + vox * a.C);
+                        for (int c4 = 0; c4 < a.C / 4; ++c4) {
+                            uint2 qv = src[c4];
+                            if (!raw) {
+                                auto f = [&](uint32_t uu) {
+                                    const float lo = pro.apply(__uint_as_float(uu << 16));
+                                    const float hi = pro.apply(__uint_as_float(uu & 0xffff0000u));
+                                    return uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+                                };
+                                qv = uint2{f(qv.x), f(qv.y)};
+                            }
+                            reinterpret_cast<uint2 *>(dst)[c4] = qv;
+                        }
+                    } else {
+                        for (int c = 0; c < a.CS; ++c) {
+                            bf16_t v = 0;
+                            if (ok && c < a.C) {
+                                const bf16_t *src = c < a.Ca ? x + vox * a.Ca + c : x2 + vox * a.Cb + (c - a.Ca);
+                                v = raw ? *src : f2bf(pro.apply(ld(src)));
+                            }
+                            dst[c] = v;
+                        }
+                    }
+                }
+                const int tail0 = a.pad0 + a.LP * a.CS;
+                const int z = a.LS - tail0 + a.pad0;
+                for (int e = tid; e < nlines * z; e += 256) {
+                    const int ln = e / z, r = e - ln * z;
+                    lines[ln * a.LS + (r < a.pad0 ? r : tail0 + r - a.pad0)] = 0;
+                }
             }
         }
         // ---- g tile [nvp][GS]: the brick's g is bh*bw contiguous runs of bd*N elements: 16-byte
@@ -219,10 +281,11 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
             }
         }
     }
-    // ---- D[co][col]: lane column li -> window column, rows 4*grp + i -> co
-    const float sc = escale ? *escale : 1.f;
+    // ---- this workgroup's partial G -> part[blk][entry], entry = (co * C + c) * K3 + tap (the
+    // reference weight order), then the N per-channel g sums (conv bias); every entry of a row
+    // is written by exactly one column group
+    float *pw = part + int64_t(blockIdx.x) * a.nent;
     const int K3 = a.k * a.k * a.k;
-    float wg = 0.f;
 #pragma unroll
     for (int t = 0; t < NPW; ++t) {
         const int tt = tile0 + wave + 4 * t;
@@ -237,23 +300,52 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int co = m * 16 + grp * 4 + i;
-                if (co >= a.N) continue;
-                const int64_t o = (int64_t(co) * a.wCt + c) * K3 + tap;
-                const float v = acc[m][t][i];
-                if (dw) atomicAdd(dw + o, escale ? v * sc : v);
-                if (dscale) wg = fmaf(w[o], v, wg);
+                if (co < a.N) pw[(co * a.C + c) * K3 + tap] = acc[m][t][i];
             }
+    }
+    if (do_bias && tid < a.N) pw[a.N * a.C * K3 + tid] = gsum;
+}
+
+// dw[e] += escale * sum_blk part[blk][e] ; dscale += sum W * G ; dcbias / dbias from the g sums.
+// LANES lanes share an entry (strided slices, 8 loads in flight, fixed xor-shuffle tree):
+// deterministic.
+template <int LANES>
+__global__ __launch_bounds__(256) void k_lines_wgrad_reduce(const float *__restrict__ part, int nblk, int nw, int ne,
+                                                           const float *__restrict__ w,
+                                                           const float *__restrict__ escale, float *dw, float *dscale,
+                                                           float *dbias, float *dcbias) {
+    __shared__ float red[8];
+    const int lane = threadIdx.x % LANES;
+    const int e = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
+    float sum = 0.f;
+    if (e < ne) {
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int b0 = lane; b0 < nblk; b0 += 8 * LANES) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u * LANES < nblk) acc[u] += part[int64_t(b0 + u * LANES) * ne + e];
+        }
+        sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
+#pragma unroll
+    for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    float wg = 0.f, bs = 0.f;
+    if (e < ne && lane == 0) {
+        if (e < nw) {
+            if (dw) dw[e] += escale ? sum * *escale : sum;
+            if (dscale) wg = w[e] * sum;
+        } else {
+            if (dcbias) dcbias[e - nw] += sum;
+            bs = sum;
+        }
     }
     if (dscale) {
         wg = block_sum<float, 256>(wg, red);
-        if (tid == 0) atomicAdd(dscale, wg);
+        if (threadIdx.x == 0) atomicAdd(dscale, wg);
     }
-    if (do_bias) {
-        if (dcbias && tid < a.N) atomicAdd(dcbias + tid, gsum);
-        if (dbias) {
-            const float tb = block_sum<float, 256>(tid < a.N ? gsum : 0.f, red + 4);
-            if (tid == 0) atomicAdd(dbias, tb);
-        }
+    if (dbias) {
+        bs = block_sum<float, 256>(bs, red + 4);
+        if (threadIdx.x == 0) atomicAdd(dbias, bs);
     }
 }
 
@@ -280,7 +372,7 @@ struct WPlan {
 WPlan plan_w(const vq3d_conv_desc *d) {
     WPlan P = {};
     WArgs &a = P.a;
-    if (d->dtype != VQ3D_BF16 || d->kernel < 2 || d->cout > 64 || (d->cin + d->cin2) % 4) return P;
+    if (d->dtype != VQ3D_BF16 || d->kernel < 2 || d->cout > 64 || (d->cin2 && (d->cin + d->cin2) % 4)) return P;
     a.B = d->batch; a.Ca = d->cin; a.Cb = d->cin2; a.C = a.Ca + a.Cb; a.N = d->cout;
     a.CS = (a.C + 3) / 4 * 4;
     a.iH = d->in_h; a.iW = d->in_w; a.iD = d->in_d; a.oH = d->out_h; a.oW = d->out_w; a.oD = d->out_d;
@@ -327,29 +419,42 @@ WPlan plan_w(const vq3d_conv_desc *d) {
     a.fC = FastDiv(uint32_t(a.CS));
     a.fhw = FastDiv(uint32_t(a.hw));
     a.fN = FastDiv(uint32_t(a.N));
+    a.fCr = FastDiv(uint32_t(a.C));
+    a.mc = (a.LP * a.C + 7) / 8 + 1;
+    a.fmc = FastDiv(uint32_t(a.mc));
+    a.xtotal = int64_t(a.B) * a.iH * a.iW * a.iD * a.C;
     a.gvec = (a.bd * a.N) % 8 == 0 && (int64_t(a.oD) * a.N) % 8 == 0;
     P.lds = lds_of();
-    // Every workgroup adds a partial of the whole (column-group slice of the) weight gradient,
-    // so few voxels per workgroup means many atomics per voxel: give each workgroup >= 2
-    // bricks (<= 64 adders per entry) and find parallelism in the column tiles instead
-    // (fewer column tiles per wave -> more column groups).
-    P.nbx = std::max(1, std::min(64, (a.nbricks + 1) / 2));
+    // Column tiles: as few column groups as the accumulator budget allows (each group
+    // re-stages the bricks).  Bricks: ~1024 workgroups in all, each writing one partial G that
+    // a fixed-order reduction sums (no atomics, deterministic).
     const int cands[] = {1, 2, 4, 7, 14};
     P.npw = 1;
     for (int c : cands) {
         if (c > cap) break;
         P.npw = c;
-        const int groups = (a.ntiles + 4 * c - 1) / (4 * c);
-        if (int64_t(groups) * P.nbx <= 512) break;
+        if (4 * c >= a.ntiles) break;
     }
     P.ygroups = (a.ntiles + 4 * P.npw - 1) / (4 * P.npw);
-    if (a.nbricks > 16 * P.nbx) return P;  // big grids: the brick-serial loop would be latency bound
+    a.nent = a.N * a.C * a.k * a.k * a.k + a.N;
+    int64_t nbx = std::max<int64_t>(1, std::min<int64_t>(a.nbricks, 1024 / P.ygroups));
+    while (nbx > 1 && nbx * a.nent * 4 > (int64_t(64) << 20)) nbx /= 2;
+    P.nbx = int(nbx);
     P.ok = true;
     if (std::getenv("VQ3D_VERBOSE"))
         std::fprintf(stderr, "[vq3d] lines wgrad C%d(CS%d)->N%d k%d s%d: brick %dx%dx%d ntm %d npw %d groups %d nbx %d lds %zu\n",
                      a.C, a.CS, a.N, a.k, a.s, a.bh, a.bw, a.bd, P.ntm, P.npw, P.ygroups, P.nbx, P.lds);
     return P;
 }
+
+}  // namespace
+
+size_t lines_wgrad_workspace(const vq3d_conv_desc *d) {
+    const WPlan P = plan_w(d);
+    return P.ok ? size_t(P.nbx) * P.a.nent * 4 : 0;
+}
+
+namespace {
 
 bool wdisabled() {
     static const bool off = [] {
@@ -365,9 +470,11 @@ bool lines_wgrad_applicable(const vq3d_conv_desc *d) { return !wdisabled() && pl
 
 int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pa,
                        const float *pb, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
-                       float *dcbias, hipStream_t s) {
+                       float *dcbias, void *ws, size_t ws_bytes, hipStream_t s) {
     WPlan P = plan_w(d);
     if (!P.ok) return fail("conv3d_bwd_weight(lines): geometry not supported");
+    if (!ws || ws_bytes < size_t(P.nbx) * P.a.nent * 4) return fail("conv3d_bwd_weight(lines): workspace too small");
+    float *part = static_cast<float *>(ws);
     P.a.pro_kind = d->pro_kind;
     P.a.pro_a = pa;
     P.a.pro_b = pb;
@@ -382,8 +489,7 @@ int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, c
             (void)hipGetLastError();
             attr = true;
         }
-        kern<<<grid, 256, P.lds, s>>>(P.a, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g, w, escale, dw,
-                                      dscale, dbias, dcbias);
+        kern<<<grid, 256, P.lds, s>>>(P.a, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g, part);
     };
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
@@ -410,6 +516,22 @@ int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, c
     case 3: by_npw(I3{}); break;
     default: by_npw(I4{}); break;
     }
+    const int nw = P.a.nent - P.a.N;
+    int lanes = 1;
+    while (lanes < 64 && lanes * 32 < P.nbx) lanes *= 2;
+#define RED(L)                                                                                                 \
+    k_lines_wgrad_reduce<L><<<(P.a.nent + 256 / L - 1) / (256 / L), 256, 0, s>>>(part, P.nbx, nw, P.a.nent, w,  \
+                                                                                 escale, dw, dscale, dbias, dcbias)
+    switch (lanes) {
+    case 1: RED(1); break;
+    case 2: RED(2); break;
+    case 4: RED(4); break;
+    case 8: RED(8); break;
+    case 16: RED(16); break;
+    case 32: RED(32); break;
+    default: RED(64); break;
+    }
+#undef RED
     return check_launch("conv3d_bwd_weight(lines)");
 }
 

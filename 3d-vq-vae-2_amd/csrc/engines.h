@@ -44,11 +44,13 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
                  const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
                  void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
-// k^3 weight gradient on the lines layout (conv_lines_wgrad.hip), bf16, cout <= 64
+// k^3 weight gradient on the lines layout (conv_lines_wgrad.hip), bf16, cout <= 64: per-workgroup
+// partial G in the workspace (lines_wgrad_workspace bytes), summed in a fixed order
 bool lines_wgrad_applicable(const vq3d_conv_desc *d);
+size_t lines_wgrad_workspace(const vq3d_conv_desc *d);
 int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
                        const float *pro_b, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
-                       float *dcbias, hipStream_t s);
+                       float *dcbias, void *ws, size_t ws_bytes, hipStream_t s);
 
 // stride-2 (k = 2 or 4) backward-data visiting only the parity-matching taps (conv_s2.hip)
 bool dgrad_s2_applicable(const vq3d_conv_desc *d);
@@ -71,5 +73,15 @@ template <typename T>
 int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w, const float *pa,
                const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale, void *out,
                void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
+
+// k > 1 forward / backward-data on small grids (<= 512 voxels) with >= 32 reduction channels:
+// reduction channels split over workgroups, partials [split][voxel][out] in the workspace
+// (small_workspace bytes), summed in a fixed order by an epilogue kernel (conv_small.hip)
+bool small_applicable(const vq3d_conv_desc *d, bool dgrad);
+size_t small_workspace(const vq3d_conv_desc *d, bool dgrad);
+template <typename T>
+int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w,
+                 const float *pa, const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale,
+                 void *out, void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
 }  // namespace vq3d

@@ -34,6 +34,15 @@ class ConvEpilogue(ctypes.Structure):
                 ("act", c_int), ("act_a", P), ("act_b", P)]
 
 
+class PreactParams(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("bias1a", "bias1b", "bias2a", "bias2b", "bias3a", "bias3b", "scale", "bias4")]
+
+
+class PreactGrads(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("dw1", "dw2", "dw3", "dbias1a", "dbias1b", "dbias2a", "dbias2b", "dbias3a",
+                                 "dbias3b", "dscale", "dbias4")]
+
+
 class DgradEpilogue(ctypes.Structure):
     _fields_ = [("aux", P), ("aux_kind", c_int), ("aux_b", P), ("addend", P)]
 
@@ -45,6 +54,9 @@ _SIGS = {
     "vq3d_conv3d_bwd_weight": (c_int, [P, P, P, P, P, P, P, P, P, P, P, P, P, c_size, P]),
     "vq3d_upsample2x_fwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P]),
     "vq3d_upsample2x_bwd": (c_int, [c_int] * 6 + [P, c_int, P, P, P, P, P, P]),
+    "vq3d_preact_tiny_supported": (c_int, [c_int] * 6),
+    "vq3d_preact_tiny_fwd": (c_int, [c_int] * 7 + [P, P, P, P, P, P, P]),
+    "vq3d_preact_tiny_bwd": (c_int, [c_int] * 7 + [P, P, P, P, P, P, P, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),
     "vq3d_vq_nearest": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, c_int, P, P, P, P]),
     "vq3d_vq_commit_loss": (c_int, [P, c_float, P, P]),

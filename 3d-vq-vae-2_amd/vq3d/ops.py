@@ -5,6 +5,7 @@ channels-last (torch.channels_last_3d == physical [B][H][W][D][C]), fp32 or bf16
 Every call enqueues on the current torch stream; nothing here synchronises the host.
 """
 import ctypes
+import os
 
 import torch
 
@@ -220,6 +221,53 @@ def upsample2x_bwd(gy, src_shape, pro=None, aux=None, aux_b=None, addend=None, d
     epi = _depi(aux, aux_b, addend)
     L.call("vq3d_upsample2x_bwd", L.dtype_code(gy), b, c, h, w, d, L.ptr(gy), kind, _p(pa), ctypes.byref(epi),
            L.ptr(gx), _p(dpro_pre), _p(dpro_post), L.stream())
+    return gx
+
+
+# ------------------------------------------------------------------------------------------------ tiny PreAct block
+_tiny = [os.environ.get("VQ3D_NO_TINY", "0") != "1"]
+
+
+def set_tiny_blocks(enabled):
+    """Route eligible PreAct blocks on tiny grids through the one-workgroup block kernels."""
+    _tiny[0] = bool(enabled)
+
+
+def tiny_blocks_enabled():
+    return _tiny[0]
+
+
+def preact_tiny_supported(x_shape, branch):
+    b, c, h, w, d = x_shape
+    return bool(L.query("vq3d_preact_tiny_supported", b, c, branch, h, w, d))
+
+
+def _preact_params(blk):
+    return L.PreactParams(*[_p(getattr(blk, n)) for n in ("bias1a", "bias1b", "bias2a", "bias2b", "bias3a",
+                                                            "bias3b", "scale", "bias4")])
+
+
+def preact_tiny_fwd(x, blk):
+    """Whole PreActFixupResBlock ('same', no skip) in one kernel on a tiny grid (vq3d.h)."""
+    x = as_cl(x)
+    b, c, h, w, d = x.shape
+    w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    out = torch.empty_like(x, memory_format=CL)
+    prm = _preact_params(blk)
+    L.call("vq3d_preact_tiny_fwd", L.dtype_code(x), b, c, w1.shape[0], h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2),
+           L.ptr(w3), ctypes.byref(prm), L.ptr(out), L.stream())
+    return out
+
+
+def preact_tiny_bwd(g, x, blk, grads):
+    """gx of preact_tiny_fwd; grads: dict name -> fp32 buffer (+=), names as in L.PreactGrads."""
+    b, c, h, w, d = x.shape
+    w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    gx = torch.empty_like(x, memory_format=CL)
+    prm = _preact_params(blk)
+    gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
+    L.call("vq3d_preact_tiny_bwd", L.dtype_code(x), b, c, w1.shape[0], h, w, d, L.ptr(x), L.ptr(g), L.ptr(w1),
+           L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(gx), L.stream())
     return gx
 
 

@@ -30,6 +30,12 @@ CASES = [
     (18, 9, (8, 8, 8), 1, 1, 0, False),
     (9, 2, (8, 8, 5), 1, 1, 0, False),
     (64, 128, (4, 4, 2), 1, 1, 0, False),
+    # channel counts that are not multiples of 4 (lines weight gradient, vector-run staging)
+    (9, 9, (16, 16, 32), 3, 1, 1, True),
+    (1, 1, (16, 8, 32), 3, 1, 1, True),
+    (2, 2, (8, 8, 40), 3, 1, 1, True),
+    (9, 9, (8, 8, 8), 3, 1, 1, False),
+    (3, 6, (6, 6, 8), 4, 2, 1, True),
 ]
 
 
