@@ -12,9 +12,11 @@
 // thread owns one voxel of the segment: it reads its rows from LDS, runs the channel GEMV in fp32
 // against weights broadcast from LDS (16 output channels at a time), applies the epilogue and
 // writes its output row back to the LDS out slab.
+#include "conv_epi.h"
 #include "engines.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace vq3d {
 
@@ -360,6 +362,138 @@ namespace {
 
 constexpr int kMaxPwBlocks = 2048;
 
+
+// Mid-size grids (a few thousand voxels, tens of channels: the 32x32x8 / 16x16x4 levels): the
+// slab kernel's per-workgroup staging is pure latency there.  Here a thread owns one voxel and
+// OPT consecutive output channels; every wave of a workgroup shares the same output group
+// (blockIdx.y), so the weights are wave-uniform and come through the scalar cache (SGPR
+// operands, no LDS); input rows are read per lane with 8/16-byte loads.
+template <typename T, int N>
+__device__ __forceinline__ void load_run(const T *__restrict__ p, int vw, float (&o)[N]) {
+    if constexpr (sizeof(T) == 2) {
+        if (vw == 8) {
+#pragma unroll
+            for (int q = 0; q < N / 8; ++q) {
+                const uint4 u = reinterpret_cast<const uint4 *>(p)[q];
+                const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[8 * q + 2 * j] = __uint_as_float(w4[j] << 16);
+                    o[8 * q + 2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+                }
+            }
+            return;
+        }
+        if (vw == 4) {
+#pragma unroll
+            for (int q = 0; q < N / 4; ++q) {
+                const uint2 u = reinterpret_cast<const uint2 *>(p)[q];
+                o[4 * q] = __uint_as_float(u.x << 16);
+                o[4 * q + 1] = __uint_as_float(u.x & 0xffff0000u);
+                o[4 * q + 2] = __uint_as_float(u.y << 16);
+                o[4 * q + 3] = __uint_as_float(u.y & 0xffff0000u);
+            }
+            return;
+        }
+    } else {
+        if (vw >= 4) {
+#pragma unroll
+            for (int q = 0; q < N / 4; ++q) {
+                const float4 f = reinterpret_cast<const float4 *>(p)[q];
+                o[4 * q] = f.x;
+                o[4 * q + 1] = f.y;
+                o[4 * q + 2] = f.z;
+                o[4 * q + 3] = f.w;
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) o[j] = ld(p + j);
+}
+
+struct SgArgs {
+    int64_t nvox;
+    int Ca, Cb, Ct, N;  // row channels (x | x2, or g), weight 2nd dim, output channels
+    int vwa, vwb;       // row vector width of in / in2 (8, 4 or 1 elements)
+};
+
+template <typename T, bool DG, int OPT>
+__device__ __forceinline__ void sg_row(const SgArgs &s, const T *__restrict__ row, int n, int cbase, int vw,
+                                       const Prologue &pro, const float *__restrict__ w, int o0, float (&acc)[OPT]) {
+    // W(o, k): forward w[o * Ct + k], backward-data w[k * Ct + o]; o clamped in range (the
+    // surplus accumulators of the last output group are never stored)
+    int oc[OPT];
+#pragma unroll
+    for (int j = 0; j < OPT; ++j) oc[j] = min(o0 + j, s.N - 1);
+    int c = 0;
+    for (; c + 8 <= n; c += 8) {
+        float xv[8];
+        load_run<T, 8>(row + c, vw, xv);
+        if (!DG && pro.kind != VQ3D_PRO_NONE) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) xv[q] = pro.apply(xv[q]);
+        }
+#pragma unroll
+        for (int j = 0; j < OPT; ++j)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int k = cbase + c + q;
+                const float wv = DG ? w[int64_t(k) * s.Ct + oc[j]] : w[int64_t(oc[j]) * s.Ct + k];
+                acc[j] = fmaf(xv[q], wv, acc[j]);
+            }
+    }
+    for (; c < n; ++c) {
+        float xv = ld(row + c);
+        if (!DG) xv = pro.apply(xv);
+        const int k = cbase + c;
+#pragma unroll
+        for (int j = 0; j < OPT; ++j) {
+            const float wv = DG ? w[int64_t(k) * s.Ct + oc[j]] : w[int64_t(oc[j]) * s.Ct + k];
+            acc[j] = fmaf(xv, wv, acc[j]);
+        }
+    }
+}
+
+template <typename T, bool DG, int OPT>
+__global__ __launch_bounds__(256) void k_pw_sg(SgArgs s, ConvArgs ca, const T *__restrict__ in,
+                                              const T *__restrict__ in2, const float *__restrict__ w, FwdEpi<T> fe,
+                                              BwdEpi<T> be, const float *__restrict__ gscale, T *__restrict__ out,
+                                              T *__restrict__ out2, float *dpre, float *dpost, float *part) {
+    __shared__ float red[8];
+    const int o0 = blockIdx.y * OPT;
+    const Prologue pro = make_prologue(DG ? VQ3D_PRO_NONE : ca.pro_kind, ca.pro_a, ca.pro_b);
+    const ActDeriv dv = make_deriv(be);
+    const float gs = gscale ? *gscale : 1.f;
+    float pre = 0.f, post = 0.f;
+    for (int64_t v = int64_t(blockIdx.x) * 256 + threadIdx.x; v < s.nvox; v += int64_t(gridDim.x) * 256) {
+        float acc[OPT];
+#pragma unroll
+        for (int j = 0; j < OPT; ++j) acc[j] = 0.f;
+        sg_row<T, DG, OPT>(s, in + v * s.Ca, s.Ca, 0, s.vwa, pro, w, o0, acc);
+        if (!DG && s.Cb) sg_row<T, DG, OPT>(s, in2 + v * s.Cb, s.Cb, s.Ca, s.vwb, pro, w, o0, acc);
+        if (!DG)
+            fwd_epilogue<T, OPT>(ca, fe, acc, v, o0, out + v * ca.Cout);
+        else
+            bwd_epilogue<T, OPT>(ca, be, dv, gs, gscale != nullptr, acc, v, o0, out + v * ca.Cin,
+                                 out2 ? out2 + v * ca.Cin2 : nullptr, pre, post);
+    }
+    if (DG && (dpre || dpost)) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            const int nb = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+            if (part) {
+                part[bid] = pre;
+                part[nb + bid] = post;
+            } else {
+                if (dpre) atomicAdd(dpre, pre);
+                if (dpost) atomicAdd(dpost, post);
+            }
+        }
+    }
+}
+
 bool rows_path(const vq3d_conv_desc *d, bool dgrad, const void *res_up2_flag) {
     auto p2 = [](int c) { return c == 1 || c == 2 || c == 4 || c == 8; };
     const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
@@ -367,6 +501,69 @@ bool rows_path(const vq3d_conv_desc *d, bool dgrad, const void *res_up2_flag) {
 }
 
 }  // namespace
+
+
+// scalar-weight kernel choice: VQ3D_PW_SG=0 never, =1 always, unset: grids up to 64K voxels
+static int sg_mode() {
+    static const int m = [] {
+        const char *e = std::getenv("VQ3D_PW_SG");
+        return e ? (e[0] == '1' ? 1 : 0) : 2;
+    }();
+    return m;
+}
+
+template <typename T>
+static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w,
+                 const float *pa, const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale,
+                 void *out, void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t st) {
+    const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    SgArgs s;
+    s.nvox = nvox;
+    s.Ca = dgrad ? d->cout : d->cin;
+    s.Cb = dgrad ? 0 : d->cin2;
+    s.Ct = d->cin + d->cin2;
+    s.N = dgrad ? s.Ct : d->cout;
+    auto vw = [](const void *p, int ch) {
+        const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+        const int esz = int(sizeof(T));
+        if (ch % 8 == 0 && (u & 15) == 0 && (ch * esz) % 16 == 0) return 8;
+        if (ch % 4 == 0 && (u & 7) == 0 && (ch * esz) % 8 == 0) return 4;
+        return 1;
+    };
+    s.vwa = vw(in, s.Ca);
+    s.vwb = s.Cb ? vw(in2, s.Cb) : 1;
+    ConvArgs ca = make_args(d, pa, pb);
+    // outputs per thread: enough (voxel, group) threads to fill the chip; an ELU prologue is
+    // recomputed by every group, so it gets twice the outputs per thread
+    const int64_t want = (!dgrad && d->pro_kind == VQ3D_PRO_ELU_ADD) ? 65536 : 131072;
+    int opt = 16;
+    while (opt > 1 && (opt / 2 >= s.N || nvox * ((s.N + opt - 1) / opt) < want)) opt /= 2;
+    const int ny = (s.N + opt - 1) / opt;
+    const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 255) / 256, kMaxPwBlocks / ny)));
+    const dim3 grid{nbx, unsigned(ny), 1u};
+    const bool want_part = dgrad && (dpre || dpost);
+    const int nb = int(nbx) * ny;
+    float *part = (want_part && nb > 1024 && ws && ws_bytes >= size_t(2) * nb * 4) ? static_cast<float *>(ws) : nullptr;
+#define SG(O)                                                                                                    \
+    case O:                                                                                                      \
+        if (dgrad)                                                                                               \
+            k_pw_sg<T, true, O><<<grid, 256, 0, st>>>(s, ca, (const T *)in, nullptr, w, fe, be, gscale, (T *)out, \
+                                                      (T *)out2, dpre, dpost, part);                             \
+        else                                                                                                     \
+            k_pw_sg<T, false, O><<<grid, 256, 0, st>>>(s, ca, (const T *)in, (const T *)in2, w, fe, be, nullptr,  \
+                                                       (T *)out, nullptr, nullptr, nullptr, nullptr);            \
+        break;
+    switch (opt) {
+        SG(1)
+        SG(2)
+        SG(4)
+        SG(8)
+        SG(16)
+    }
+#undef SG
+    if (part) k_sum_partials<<<1, 256, 0, st>>>(part, nb, dpre, dpost);
+    return check_launch(dgrad ? "conv3d_bwd_data(pointwise sg)" : "conv3d_fwd(pointwise sg)");
+}
 
 size_t pw_dgrad_workspace(const vq3d_conv_desc *) { return size_t(2) * kMaxPwBlocks * sizeof(float); }
 
@@ -381,6 +578,9 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     fe.oD = d->out_d;
     auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool want_part = dgrad && (dpre || dpost);
+    // ---- mid-size grids: scalar-cache weights, one thread per (voxel, output group)
+    if (sg_mode() == 1 || (sg_mode() == 2 && nvox <= 65536))
+        return launch_pw_sg<T>(d, dgrad, in, in2, w, pa, pb, fe, be, gscale, out, out2, dpre, dpost, ws, ws_bytes, s);
     // ---- few-channel rows: no LDS staging
     if (rows_path(d, dgrad, fe.res_up2 ? fe.res : nullptr) && al(in) && al(out) && al(fe.res) && al(be.aux) && al(be.addend)) {
         const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
