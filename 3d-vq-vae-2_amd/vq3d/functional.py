@@ -61,10 +61,11 @@ class PreActBlockFn(torch.autograd.Function):
         ctx.tiny = (blk.skip_conv is None and not up and k == 3 and s == 1 and ops.tiny_blocks_enabled()
                     and ops.preact_tiny_supported(x.shape, blk.branch_conv1.weight.shape[0]))
         if ctx.tiny:
-            # whole block in one workgroup (tiny_block.hip); the backward recomputes t2 / t3 from x
+            # whole block in one launch (tiny_block.hip); t2 / t3 saved in fp32
+            out, saved = ops.preact_tiny_fwd(x, blk)
             ctx.blk = blk
-            ctx.save_for_backward(x)
-            return ops.preact_tiny_fwd(x, blk)
+            ctx.save_for_backward(x, saved)
+            return out
         t2 = ops.conv_fwd(x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), act=(blk.bias2a, blk.bias2b))
         if up:
             tup = ops.upsample2x(t2)
@@ -90,12 +91,12 @@ class PreActBlockFn(torch.autograd.Function):
         blk = ctx.blk
         g = _cl(g)
         if ctx.tiny:
-            (x,) = ctx.saved_tensors
+            x, saved = ctx.saved_tensors
             gb = grad_buf
             names = {"dw1": blk.branch_conv1.weight, "dw2": blk.branch_conv2.weight, "dw3": blk.branch_conv3.weight,
                      "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
-            g_x = ops.preact_tiny_bwd(g, x, blk, {n: gb(t) for n, t in names.items()})
+            g_x = ops.preact_tiny_bwd(g, x, saved, blk, {n: gb(t) for n, t in names.items()})
             return (g_x, None) + (None,) * len(blk._fn_params)
         x, t2, t3, tup = ctx.saved_tensors
         k, s, p, up = mode_geometry(blk.mode)

@@ -253,21 +253,28 @@ def preact_tiny_fwd(x, blk):
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     out = torch.empty_like(x, memory_format=CL)
+    nb = w1.shape[0]
+    saved = torch.empty(L.query("vq3d_preact_tiny_saved_floats", b, nb, h, w, d), dtype=torch.float32,
+                        device=x.device)
     prm = _preact_params(blk)
-    L.call("vq3d_preact_tiny_fwd", L.dtype_code(x), b, c, w1.shape[0], h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2),
-           L.ptr(w3), ctypes.byref(prm), L.ptr(out), L.stream())
-    return out
+    L.call("vq3d_preact_tiny_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2),
+           L.ptr(w3), ctypes.byref(prm), L.ptr(out), L.ptr(saved), L.stream())
+    return out, saved
 
 
-def preact_tiny_bwd(g, x, blk, grads):
+def preact_tiny_bwd(g, x, saved, blk, grads):
     """gx of preact_tiny_fwd; grads: dict name -> fp32 buffer (+=), names as in L.PreactGrads."""
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    nb = w1.shape[0]
     gx = torch.empty_like(x, memory_format=CL)
+    ws = torch.empty(L.query("vq3d_preact_tiny_workspace_floats", b, nb, h, w, d), dtype=torch.float32,
+                     device=x.device)
     prm = _preact_params(blk)
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
-    L.call("vq3d_preact_tiny_bwd", L.dtype_code(x), b, c, w1.shape[0], h, w, d, L.ptr(x), L.ptr(g), L.ptr(w1),
-           L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(gx), L.stream())
+    L.call("vq3d_preact_tiny_bwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(g), L.ptr(w1),
+           L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(saved), L.ptr(ws), L.ptr(gx),
+           L.stream())
     return gx
 
 

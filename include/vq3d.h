@@ -122,14 +122,14 @@ int vq3d_upsample2x_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         void *gx, float *dpro_pre, float *dpro_post, vq3d_stream_t stream);
 
 /* --- one whole PreActFixupResBlock, mode 'same', no skip conv (layers.py:102-216), on a tiny
- * grid in ONE workgroup: the 100 top-level blocks of the published model run on 8x8x2 voxels,
- * where per-conv launches are pure fixed cost.  Limits: batch*h*w*d <= 256, channels <= 32,
+ * grid with all operands in LDS: the 100 top-level blocks of the published model run on 8x8x2 voxels,
+ * where per-conv launches are pure fixed cost (forward: one launch; backward: two).  Limits: batch*h*w*d <= 256, channels <= 32,
  * branch <= 16, both multiples of 4 (vq3d_preact_tiny_supported).  Weights are the fp32
  * nn.Conv3d tensors: w1 [branch][channels], w2 [branch][branch][3][3][3], w3 [channels][branch].
  *   out = scale * W3 t3 + bias4 + x,  t3 = elu(W2 (*) t2 + bias3a) + bias3b (3x3x3 circular),
  *   t2 = elu(W1 (elu(x + bias1a) + bias1b) + bias2a) + bias2b
- * The backward recomputes t2 / t3 from x, writes gx and accumulates (+=) every parameter
- * gradient (NULL pointers skipped). */
+ * The forward saves t2 / t3 (fp32) for the backward, which writes gx and accumulates (+=)
+ * every parameter gradient (NULL pointers skipped). */
 typedef struct vq3d_preact_params {
     const float *bias1a, *bias1b, *bias2a, *bias2b, *bias3a, *bias3b, *scale, *bias4;
 } vq3d_preact_params;
@@ -138,13 +138,16 @@ typedef struct vq3d_preact_grads {
     float *dbias1a, *dbias1b, *dbias2a, *dbias2b, *dbias3a, *dbias3b, *dscale, *dbias4;
 } vq3d_preact_grads;
 int vq3d_preact_tiny_supported(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd);
+/* fp32 sizes of the forward's saved intermediates (t2, t3) and of the backward workspace */
+size_t vq3d_preact_tiny_saved_floats(int32_t batch, int32_t branch, int32_t h, int32_t w, int32_t dd);
+size_t vq3d_preact_tiny_workspace_floats(int32_t batch, int32_t branch, int32_t h, int32_t w, int32_t dd);
 int vq3d_preact_tiny_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                          int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
-                         const vq3d_preact_params *p, void *out, vq3d_stream_t stream);
+                         const vq3d_preact_params *p, void *out, float *saved, vq3d_stream_t stream);
 int vq3d_preact_tiny_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                          int32_t dd, const void *x, const void *g, const float *w1, const float *w2,
-                         const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *gx,
-                         vq3d_stream_t stream);
+                         const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                         const float *saved, float *workspace, void *gx, vq3d_stream_t stream);
 
 /* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
 /* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),
