@@ -658,6 +658,11 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
 // faster (9 -> 9 at 128^2 x 32 on par, 4 -> 4 at 256^2 x 64 1.9x).
 static bool use_lines_wgrad(const vq3d_conv_desc *d) {
     if (d->dtype != VQ3D_BF16 || !lines_wgrad_applicable(d)) return false;
+    static const int force = [] {
+        const char *e = std::getenv("VQ3D_LINES_WGRAD");
+        return e ? (e[0] == '1' ? 1 : 0) : 2;
+    }();
+    if (force != 2) return force == 1;
     if (d->cin + d->cin2 >= 32 || mfma_disabled()) return true;
     return !plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
                       d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)

@@ -49,7 +49,7 @@ struct WArgs {
     int wCt;                   // weight's 2nd dim
     int gvec;                  // g runs of bd*N elements are 16-B aligned multiples of 8
     int mc;                    // 8-element chunks per line run (C % 4 != 0 staging)
-    int nent;                  // partial entries per workgroup: N * C * k^3 weights + N g sums
+    int nent;                  // partial slots per workgroup: ntiles * NTM * 256 fragments + N g sums
     int64_t xtotal;            // elements of x
     FastDiv fC, fhw, fN, fCr, fmc;
 };
@@ -281,61 +281,64 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
             }
         }
     }
-    // ---- this workgroup's partial G -> part[blk][entry], entry = (co * C + c) * K3 + tap (the
-    // reference weight order), then the N per-channel g sums (conv bias); every entry of a row
-    // is written by exactly one column group
+    // ---- this workgroup's partial G in MFMA fragment order (coalesced 16-byte stores):
+    // part[blk][((tile * NTM + m) * 64 + lane) * 4 + i], then the N per-channel g sums; the
+    // reduction maps each slot back to its weight entry
     float *pw = part + int64_t(blockIdx.x) * a.nent;
-    const int K3 = a.k * a.k * a.k;
 #pragma unroll
     for (int t = 0; t < NPW; ++t) {
         const int tt = tile0 + wave + 4 * t;
         if (tt >= a.ntiles) continue;
-        const int t2 = tt / a.ctile, jt = tt - t2 * a.ctile;
-        const int e = 16 * jt + li;  // window element (kd, c) with channel stride CS
-        const int kd = int(a.fC.div(uint32_t(e))), c = e - kd * a.CS;
-        if (kd >= a.k || c >= a.C) continue;
-        const int tap = t2 * a.k + kd;
 #pragma unroll
         for (int m = 0; m < NTM; ++m)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int co = m * 16 + grp * 4 + i;
-                if (co < a.N) pw[(co * a.C + c) * K3 + tap] = acc[m][t][i];
-            }
+            *reinterpret_cast<f32x4 *>(pw + ((tt * NTM + m) * 64 + lane) * 4) = acc[m][t];
     }
-    if (do_bias && tid < a.N) pw[a.N * a.C * K3 + tid] = gsum;
+    if (do_bias && tid < a.N) pw[a.ntiles * NTM * 256 + tid] = gsum;
 }
 
-// dw[e] += escale * sum_blk part[blk][e] ; dscale += sum W * G ; dcbias / dbias from the g sums.
-// LANES lanes share an entry (strided slices, 8 loads in flight, fixed xor-shuffle tree):
-// deterministic.
+// Sum the workgroup partials of every fragment slot (LANES lanes per slot, strided slices, 8
+// loads in flight, fixed xor-shuffle tree: deterministic), map the slot to its weight entry
+// (co, c, tap) and apply: dw += escale * G, dscale += sum W * G; the trailing N slots are
+// the conv-bias / scalar-bias sums.
 template <int LANES>
-__global__ __launch_bounds__(256) void k_lines_wgrad_reduce(const float *__restrict__ part, int nblk, int nw, int ne,
-                                                           const float *__restrict__ w,
-                                                           const float *__restrict__ escale, float *dw, float *dscale,
-                                                           float *dbias, float *dcbias) {
+__global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, const float *__restrict__ part,
+                                                           int nblk, const float *__restrict__ w,
+                                                           const float *__restrict__ escale, float *dw,
+                                                           float *dscale, float *dbias, float *dcbias) {
     __shared__ float red[8];
     const int lane = threadIdx.x % LANES;
-    const int e = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
+    const int f = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
+    const int ne = a.nent;
     float sum = 0.f;
-    if (e < ne) {
+    if (f < ne) {
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int b0 = lane; b0 < nblk; b0 += 8 * LANES) {
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (b0 + u * LANES < nblk) acc[u] += part[int64_t(b0 + u * LANES) * ne + e];
+                if (b0 + u * LANES < nblk) acc[u] += part[int64_t(b0 + u * LANES) * ne + f];
         }
         sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
 #pragma unroll
     for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     float wg = 0.f, bs = 0.f;
-    if (e < ne && lane == 0) {
-        if (e < nw) {
-            if (dw) dw[e] += escale ? sum * *escale : sum;
-            if (dscale) wg = w[e] * sum;
+    const int nfr = a.ntiles * ntm * 256;
+    if (f < ne && lane == 0) {
+        if (f < nfr) {
+            const int i = f & 3, ln = (f >> 2) & 63, q = f >> 8;  // q = tile * NTM + m
+            const int tt = q / ntm, m = q - tt * ntm;
+            const int co = m * 16 + (ln >> 4) * 4 + i;
+            const int t2 = tt / a.ctile, jt = tt - t2 * a.ctile;
+            const int e = 16 * jt + (ln & 15);
+            const int kd = e / a.CS, c = e - kd * a.CS;
+            if (co < a.N && kd < a.k && c < a.C) {
+                const int K3 = a.k * a.k * a.k;
+                const int64_t o = (int64_t(co) * a.wCt + c) * K3 + t2 * a.k + kd;
+                if (dw) dw[o] += escale ? sum * *escale : sum;
+                if (dscale) wg = w[o] * sum;
+            }
         } else {
-            if (dcbias) dcbias[e - nw] += sum;
+            if (dcbias) dcbias[f - nfr] += sum;
             bs = sum;
         }
     }
@@ -436,9 +439,9 @@ WPlan plan_w(const vq3d_conv_desc *d) {
         if (4 * c >= a.ntiles) break;
     }
     P.ygroups = (a.ntiles + 4 * P.npw - 1) / (4 * P.npw);
-    a.nent = a.N * a.C * a.k * a.k * a.k + a.N;
+    a.nent = a.ntiles * P.ntm * 256 + a.N;
     int64_t nbx = std::max<int64_t>(1, std::min<int64_t>(a.nbricks, 1024 / P.ygroups));
-    while (nbx > 1 && nbx * a.nent * 4 > (int64_t(64) << 20)) nbx /= 2;
+    while (nbx > 1 && nbx * a.nent * 4 > (int64_t(16) << 20)) nbx /= 2;
     P.nbx = int(nbx);
     P.ok = true;
     if (std::getenv("VQ3D_VERBOSE"))
@@ -516,11 +519,10 @@ int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, c
     case 3: by_npw(I3{}); break;
     default: by_npw(I4{}); break;
     }
-    const int nw = P.a.nent - P.a.N;
     int lanes = 1;
     while (lanes < 64 && lanes * 32 < P.nbx) lanes *= 2;
 #define RED(L)                                                                                                 \
-    k_lines_wgrad_reduce<L><<<(P.a.nent + 256 / L - 1) / (256 / L), 256, 0, s>>>(part, P.nbx, nw, P.a.nent, w,  \
+    k_lines_wgrad_reduce<L><<<(P.a.nent + 256 / L - 1) / (256 / L), 256, 0, s>>>(P.a, P.ntm, part, P.nbx, w,    \
                                                                                  escale, dw, dscale, dbias, dcbias)
     switch (lanes) {
     case 1: RED(1); break;
