@@ -758,7 +758,12 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
     // pre-pack the weights once per call when the caller gave room (else each workgroup packs)
     const uint4 *wpk = nullptr;
     const int items_per_wg = P.a.nks * 4 * P.a.ntn;
-    if (items_per_wg > 2048 && ws && ws_bytes >= ws_of(P)) {  // small images are packed in-kernel
+    static const int prepack = [] {  // VQ3D_LINES_PREPACK=1 / 0: always / never pre-pack (A/B runs)
+        const char *e = std::getenv("VQ3D_LINES_PREPACK");
+        return e ? (e[0] == '1' ? 1 : 0) : 2;
+    }();
+    const bool want_pack = prepack == 2 ? items_per_wg > 2048 : prepack == 1;
+    if (want_pack && ws && ws_bytes >= ws_of(P)) {  // small images are packed in-kernel
         const int items = P.a.nks * 4 * P.a.ntn;
         const dim3 pg{unsigned((items + 255) / 256), unsigned(P.a.ntg), 1u};
         if (dgrad) k_lines_pack<true><<<pg, 256, 0, s>>>(P.a, w, wCt, P.a.ntn, static_cast<uint4 *>(ws));

@@ -658,7 +658,11 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     if (lds > 150 * 1024) return fail("conv(pointwise): too many channels for the LDS slabs");
     a.vec = al(in) && al(in2) && al(out) && al(out2) && al(be.aux) && al(be.addend) && al(fe.res);
     const int64_t nseg = (a.nvox + a.segv - 1) / a.segv;
-    const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, kMaxPwBlocks)));
+    static const int slab_cap = [] {  // VQ3D_PW_SLAB_BLOCKS: workgroup cap of the slab kernel (A/B runs)
+        const char *e = std::getenv("VQ3D_PW_SLAB_BLOCKS");
+        return e ? std::max(1, std::min(kMaxPwBlocks, std::atoi(e))) : 1024;  // measured: 1024 >= 2048 > 512
+    }();
+    const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, slab_cap)));
     float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
 #define L(C)                                                                                                    \
     case C: {                                                                                                   \

@@ -72,11 +72,21 @@ def dominant_kernel_roofline(dtype, dev, iters=50):
     geom = ops.ConvGeom(3, 1, 1, True)
     for _ in range(3):
         ops.conv_fwd(x, wt, geom)
+    torch.cuda.synchronize()
+    # the `iters` launches captured in a HIP graph, so the events time back-to-back kernels on
+    # the replay stream (no host launch gaps)
+    side = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            for _ in range(iters):
+                ops.conv_fwd(x, wt, geom)
+    graph.replay()
+    torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(iters):
-        ops.conv_fwd(x, wt, geom)
+    graph.replay()
     e1.record(st)
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters

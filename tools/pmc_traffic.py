@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_conv_fwd"
+KERNEL = "k_lines"
 
 
 def per_dispatch(d, counter):
