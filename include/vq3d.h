@@ -104,8 +104,9 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
  *   dbias  += sum(g)         (epilogue scalar bias)
  *   dcbias += sum_v g[v,co]  (nn.Conv3d bias)
  * The workspace holds per-workgroup partials that a second kernel sums in a fixed order
- * (1x1x1 convs: deterministic); k > 1 engines accumulate with fp32 atomics, so their last
- * bits are order-dependent like cuDNN's wgrad. */
+ * (1x1x1 convs and the lines k^3 engine: deterministic); the direct k^3 engine used for
+ * few-channel large grids accumulates with fp32 atomics, so its last bits are
+ * order-dependent like cuDNN's wgrad. */
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g,
                            const float *pro_a, const float *pro_b, const float *w, const float *epi_scale,
                            float *dw, float *dscale, float *dbias, float *dcbias, void *workspace,

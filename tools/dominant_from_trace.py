@@ -7,6 +7,7 @@
 """
 import csv
 import json
+import re
 import sys
 
 
@@ -19,7 +20,8 @@ def main():
     grid = (rows[-1]["Grid_Size_X"], rows[-1]["LDS_Block_Size"])
     sel = [r for r in rows if (r["Grid_Size_X"], r["LDS_Block_Size"]) == grid][-n:]
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in sel]
-    print(json.dumps({"kernel": sel[-1]["Kernel_Name"].split("(")[0], "launches": len(d),
+    m = re.search(r"k_lines<[^>]*>", sel[-1]["Kernel_Name"])
+    print(json.dumps({"kernel": m.group(0) if m else sel[-1]["Kernel_Name"][:80], "launches": len(d),
                       "avg_us": sum(d) / len(d), "min_us": min(d), "max_us": max(d)}))
 
 
