@@ -59,6 +59,43 @@ __device__ __forceinline__ void copy_out(T *__restrict__ dst, const T *__restric
     copy_in<T>(dst, src, n, vec);
 }
 
+// copy_in with the input prologue applied once per element on the way into LDS (the staged
+// slab then holds the conv's actual operand, as the k^3 engines stage theirs)
+template <typename T>
+__device__ __forceinline__ void copy_in_pro(T *__restrict__ dst, const T *__restrict__ src, int n, bool vec,
+                                            const Prologue &pro) {
+    if (pro.kind == VQ3D_PRO_NONE) {
+        copy_in<T>(dst, src, n, vec);
+        return;
+    }
+    constexpr int E = 16 / sizeof(T);
+    int i0 = 0;
+    if (vec) {
+        const int nq = n / E;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (int q = threadIdx.x; q < nq; q += SEG) {
+            uint4 u = s4[q];
+            if constexpr (sizeof(T) == 2) {
+                uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float lo = pro.apply(__uint_as_float(w4[j] << 16));
+                    const float hi = pro.apply(__uint_as_float(w4[j] & 0xffff0000u));
+                    w4[j] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+                }
+                u = uint4{w4[0], w4[1], w4[2], w4[3]};
+            } else {
+                u = uint4{__float_as_uint(pro.apply(__uint_as_float(u.x))), __float_as_uint(pro.apply(__uint_as_float(u.y))),
+                          __float_as_uint(pro.apply(__uint_as_float(u.z))), __float_as_uint(pro.apply(__uint_as_float(u.w)))};
+            }
+            d4[q] = u;
+        }
+        i0 = nq * E;
+    }
+    for (int i = i0 + threadIdx.x; i < n; i += SEG) st(dst + i, pro.apply(ld(src + i)));
+}
+
 template <typename T, int COT, bool DGRAD>
 __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in, const T *__restrict__ in2,
                                             const float *__restrict__ w, FwdEpi<T> fe, BwdEpi<T> be,
@@ -94,8 +131,8 @@ __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in,
         const int64_t v0 = sg * a.segv;
         const int nv = int(min<int64_t>(a.segv, a.nvox - v0));
         __syncthreads();
-        copy_in<T>(sx, in + v0 * a.Ca, nv * a.Ca, a.vec);
-        if (a.Cb) copy_in<T>(sx2, in2 + v0 * a.Cb, nv * a.Cb, a.vec);
+        copy_in_pro<T>(sx, in + v0 * a.Ca, nv * a.Ca, a.vec, pro);
+        if (a.Cb) copy_in_pro<T>(sx2, in2 + v0 * a.Cb, nv * a.Cb, a.vec, pro);
         if (DGRAD && dv.mode) copy_in<T>(saux, be.aux + v0 * a.N1, nv * a.N1, a.vec);
         if (DGRAD && be.addend) copy_in<T>(sadd, be.addend + v0 * a.N1, nv * a.N1, a.vec);
         if (res_slab) copy_in<T>(sres, fe.res + v0 * a.N, nv * a.N, a.vec);
@@ -121,15 +158,13 @@ __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in,
                 float acc[COT];
 #pragma unroll
                 for (int j = 0; j < COT; ++j) acc[j] = 0.f;
-                for (int c0 = 0; c0 < a.Cin; c0 += 8) {
+                // full 8-channel chunks of one input (prologue already applied in the slab),
+                // then the remaining channels one at a time
+                const int full_a = a.Cb ? 0 : (a.Cin & ~7);
+                for (int c0 = 0; c0 < full_a; c0 += 8) {
                     float xv[8];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int c = c0 + j;
-                        float val = c < a.Ca ? ld(xr + c) : (c < a.Cin ? ld(xr2 + (c - a.Ca)) : 0.f);
-                        if (!DGRAD && pro.kind != VQ3D_PRO_NONE && c < a.Cin) val = pro.apply(val);
-                        xv[j] = val;
-                    }
+                    for (int j = 0; j < 8; ++j) xv[j] = ld(xr + c0 + j);
 #pragma unroll
                     for (int j = 0; j < COT; ++j) {
                         const float4 w0 = *reinterpret_cast<const float4 *>(ws + (o0 + j) * a.CinP + c0);
@@ -145,6 +180,11 @@ __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in,
                         s = fmaf(xv[7], w1.w, s);
                         acc[j] = s;
                     }
+                }
+                for (int c = full_a; c < a.Cin; ++c) {
+                    const float xv = c < a.Ca ? ld(xr + c) : ld(xr2 + (c - a.Ca));
+#pragma unroll
+                    for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, ws[(o0 + j) * a.CinP + c], acc[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < COT; ++j) {
