@@ -539,7 +539,14 @@ static bool use_small(const vq3d_conv_desc *d, bool dgrad) {
         const char *e = std::getenv("VQ3D_NO_SMALL");
         return e && e[0] == '1';
     }();
-    return !off && small_applicable(d, dgrad);
+    if (off || !small_applicable(d, dgrad)) return false;
+    // measured: 9-20x faster than the lines / VALU engines at 128 voxels (8x8x2, 128 channels);
+    // from 1024 voxels on only where the lines engine cannot take the shape
+    const int64_t nv = dgrad ? int64_t(d->batch) * d->in_h * d->in_w * d->in_d
+                             : int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    if (nv <= 512) return true;
+    if (dgrad && dgrad_s2_applicable(d)) return false;  // parity-tap engine measured 2x faster there
+    return !lines_applicable(d, dgrad);
 }
 
 template <typename T>
@@ -669,6 +676,16 @@ static bool use_lines_wgrad(const vq3d_conv_desc *d) {
                 .ok;
 }
 
+// 1x1x1 weight gradient on the lines MFMA engine (k = 1) instead of the VALU slab kernel:
+// VQ3D_PW_LINES_WGRAD=1 (A/B runs)
+static bool use_lines_pw_wgrad(const vq3d_conv_desc *d) {
+    static const int mode = [] {
+        const char *e = std::getenv("VQ3D_PW_LINES_WGRAD");
+        return e ? (e[0] == '1' ? 1 : 0) : 0;
+    }();
+    return mode == 1 && lines_wgrad_applicable(d);
+}
+
 template <typename T>
 static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pa,
                         const float *pb, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
@@ -677,8 +694,11 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     const int Ct = d->cin + d->cin2;
     const int K3 = d->kernel * d->kernel * d->kernel;
     const int Kt = Ct * K3;
-    if (is_pointwise(d))
+    if (is_pointwise(d)) {
+        if (use_lines_pw_wgrad(d))
+            return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
         return launch_pw_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
+    }
     if constexpr (std::is_same<T, bf16_t>::value) {
         if (use_lines_wgrad(d))
             return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
@@ -770,7 +790,7 @@ size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
         return small_workspace(d, pass == VQ3D_PASS_BWD_DATA);
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
     if (pass == VQ3D_PASS_BWD_DATA) return is_pointwise(d) ? pw_dgrad_workspace(d) : lines_workspace(d, true);
-    if (is_pointwise(d)) return pw_wgrad_workspace(d);
+    if (is_pointwise(d)) return use_lines_pw_wgrad(d) ? lines_wgrad_workspace(d) : pw_wgrad_workspace(d);
     return use_lines_wgrad(d) ? lines_wgrad_workspace(d) : 0;
 }
 

@@ -375,7 +375,7 @@ struct WPlan {
 WPlan plan_w(const vq3d_conv_desc *d) {
     WPlan P = {};
     WArgs &a = P.a;
-    if (d->dtype != VQ3D_BF16 || d->kernel < 2 || d->cout > 64 || (d->cin2 && (d->cin + d->cin2) % 4)) return P;
+    if (d->dtype != VQ3D_BF16 || d->kernel < 1 || d->cout > 64 || (d->cin2 && (d->cin + d->cin2) % 4)) return P;
     a.B = d->batch; a.Ca = d->cin; a.Cb = d->cin2; a.C = a.Ca + a.Cb; a.N = d->cout;
     a.CS = (a.C + 3) / 4 * 4;
     a.iH = d->in_h; a.iW = d->in_w; a.iD = d->in_d; a.oH = d->out_h; a.oW = d->out_w; a.oD = d->out_d;

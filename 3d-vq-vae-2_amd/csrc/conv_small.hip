@@ -239,9 +239,7 @@ bool small_applicable(const vq3d_conv_desc *d, bool dgrad) {
                              : int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
     const int rt = dgrad ? d->cout : d->cin + d->cin2;
     const int ot = dgrad ? d->cin + d->cin2 : d->cout;
-    // measured: wins 9-20x at 128 voxels (8x8x2, 128 channels); the lines / stride-2 engines are
-    // faster from 1024 voxels (16x16x4) on
-    if (nv > 512 || rt < 32 || ot < 16) return false;
+    if (nv > 4096 || rt < 32 || ot < 16) return false;
     return size_t(d->kernel) * d->kernel * d->kernel * 4 * OT * 4 <= kSmallLds;
 }
 

@@ -74,7 +74,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
                const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale, void *out,
                void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
-// k > 1 forward / backward-data on small grids (<= 512 voxels) with >= 32 reduction channels:
+// k > 1 forward / backward-data on small grids (<= 4096 voxels) with >= 32 reduction channels:
 // reduction channels split over workgroups, partials [split][voxel][out] in the workspace
 // (small_workspace bytes), summed in a fixed order by an epilogue kernel (conv_small.hip)
 bool small_applicable(const vq3d_conv_desc *d, bool dgrad);
