@@ -564,6 +564,10 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
         if (!legacy_pw()) return launch_pw1<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes, s);
         return launch_pw<T, false>(d, a, x, x2, w, fe, be, nullptr, y, nullptr, nullptr, nullptr, s);
     }
+    if (tc_applicable(d) && !(fe.res && fe.res_up2)) {
+        BwdEpi<T> be = {};
+        return launch_tc<T>(d, false, x, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, ws, ws_bytes, s);
+    }
     if (use_small(d, false)) {
         BwdEpi<T> be = {};
         return launch_small<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes,
@@ -617,6 +621,10 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
         FwdEpi<T> fe = {};
         if (!legacy_pw()) return launch_pw1<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes, s);
         return launch_pw<T, true>(d, a, g, nullptr, w, fe, be, gscale, gx, gx2, dpre, dpost, s);
+    }
+    if (tc_applicable(d)) {
+        FwdEpi<T> fe = {};
+        return launch_tc<T>(d, true, g, w, pa, nullptr, fe, be, gscale, gx, dpre, dpost, ws, ws_bytes, s);
     }
     if (use_small(d, true)) {
         FwdEpi<T> fe = {};
@@ -699,6 +707,8 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
             return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
         return launch_pw_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
     }
+    if (tc_applicable(d))
+        return launch_tc_wgrad<T>(d, x, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
     if constexpr (std::is_same<T, bf16_t>::value) {
         if (use_lines_wgrad(d))
             return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
@@ -786,6 +796,7 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
 
 size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
     if (validate(d)) return 0;
+    if (tc_applicable(d)) return tc_workspace(d, pass);
     if (pass != VQ3D_PASS_BWD_WEIGHT && !is_pointwise(d) && use_small(d, pass == VQ3D_PASS_BWD_DATA))
         return small_workspace(d, pass == VQ3D_PASS_BWD_DATA);
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);

@@ -84,4 +84,18 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
                  const float *pa, const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale,
                  void *out, void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
+// 3x3x3 stride-1 convs with 1 / 2 / 4 channels in and out on grids of 8 x 8 x 32 bricks
+// (conv_tc.hip): VALU direct conv over a staged halo; weight gradient with per-workgroup
+// partials (tc_workspace bytes per pass) and a fixed-order reduction
+bool tc_applicable(const vq3d_conv_desc *d);
+size_t tc_workspace(const vq3d_conv_desc *d, int pass);
+template <typename T>
+int launch_tc(const vq3d_conv_desc *d, bool dgrad, const void *in, const float *w, const float *pa, const float *pb,
+              const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale, void *out, float *dpre, float *dpost,
+              void *ws, size_t ws_bytes, hipStream_t s);
+template <typename T>
+int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const float *pa, const float *pb,
+                    const float *w, const float *escale, float *dw, float *dscale, float *dbias, float *dcbias,
+                    void *ws, size_t ws_bytes, hipStream_t s);
+
 }  // namespace vq3d
