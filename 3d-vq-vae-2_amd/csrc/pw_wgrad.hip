@@ -17,6 +17,7 @@
 #include "engines.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace vq3d {
 
@@ -207,7 +208,7 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[C])
                 o[2 * j] = __uint_as_float(w[j] << 16);
                 o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
             }
-        } else {
+        } else if constexpr (C == 8) {
             const uint4 u = *reinterpret_cast<const uint4 *>(p);
             const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -215,6 +216,17 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[C])
                 o[2 * j] = __uint_as_float(w[j] << 16);
                 o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
             }
+        } else if constexpr (C % 2 == 0) {  // rows 4-byte aligned
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+#pragma unroll
+            for (int j = 0; j < C / 2; ++j) {
+                const uint32_t u = q[j];
+                o[2 * j] = __uint_as_float(u << 16);
+                o[2 * j + 1] = __uint_as_float(u & 0xffff0000u);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < C; ++j) o[j] = ld(p + j);
         }
     } else {
 #pragma unroll
@@ -222,7 +234,7 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[C])
     }
 }
 
-template <typename T, int CX, int CG>
+template <typename T, int CX, int CG, int U = 4>
 __global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__restrict__ x,
                                                      const T *__restrict__ g, int pro_kind, const float *pro_a,
                                                      const float *pro_b, float *__restrict__ part, WgOut out) {
@@ -236,10 +248,10 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__r
 #pragma unroll
         for (int i = 0; i <= CX; ++i) acc[j][i] = 0.f;
     const int64_t stride = int64_t(gridDim.x) * 256;
-    for (int64_t v0 = int64_t(blockIdx.x) * 256 + threadIdx.x; v0 < nvox; v0 += 4 * stride) {
-        float xr[4][CX], gr[4][CG];
+    for (int64_t v0 = int64_t(blockIdx.x) * 256 + threadIdx.x; v0 < nvox; v0 += U * stride) {
+        float xr[U][CX], gr[U][CG];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t v = v0 + u * stride;
             if (v < nvox) {
                 load_row<T, CX>(x + v * CX, xr[u]);
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__r
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
             for (int i = 0; i < CX; ++i) xr[u][i] = pro.apply(xr[u][i]);
 #pragma unroll
@@ -330,8 +342,20 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
+// the 9 <-> 18 channel convs of the 128^2 x 32 level on the register path (one voxel per
+// thread-iteration, 180 accumulators): VQ3D_PWW_WIDE=1 only -- measured 1.25x slower than the
+// slab kernel (52 vs 42 us at 128^2 x 32)
+bool wide_reg(const vq3d_conv_desc *d) {
+    return d->cin2 == 0 && ((d->cin == 9 && d->cout == 18) || (d->cin == 18 && d->cout == 9));
+}
+
 bool reg_path(const vq3d_conv_desc *d) {
+    static const bool wide = [] {
+        const char *e = std::getenv("VQ3D_PWW_WIDE");
+        return e && e[0] == '1';
+    }();
     auto p2 = [](int c) { return c == 1 || c == 2 || c == 4 || c == 8; };
+    if (wide && wide_reg(d)) return true;
     return d->cin2 == 0 && p2(d->cin) && p2(d->cout) && d->cout * (d->cin + 1) <= 40;
 }
 
@@ -361,7 +385,14 @@ PwwArgs plan(const vq3d_conv_desc *d, int &ytiles, int &nbx, size_t &lds) {
     lds = std::max(size_t(a.seg) * row_bytes, size_t(256) * TI * TO * 4);
     const int64_t nseg = (a.nvox + a.seg - 1) / a.seg;
     nbx = int(std::max<int64_t>(1, std::min<int64_t>(nseg, std::max(1, kMaxBlocks / ytiles))));
-    if (reg_path(d)) {  // 4 x 256 voxels per workgroup-iteration
+    // mid-size grids: few workgroups striding over the segments, so the partials go straight
+    // into the gradients (direct mode) instead of through a second reduction launch
+    static const int mid_cap = [] {
+        const char *e = std::getenv("VQ3D_PWW_MID_NBX");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    if (mid_cap > 0 && a.nvox <= 65536) nbx = std::min(nbx, mid_cap);
+    if (reg_path(d)) {  // 4 x 256 voxels per workgroup-iteration (wide rows: ~4 voxels per thread)
         ytiles = 1;
         nbx = int(std::max<int64_t>(1, std::min<int64_t>((a.nvox + 1023) / 1024, kMaxBlocks)));
     }
@@ -404,6 +435,22 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
                                                               d->pro_kind, pro_a, pro_b, part, out);          \
         break;
         switch (key) {
+            case 9 * 16 + 18:  // 162 / 297: no power-of-two pair maps to these keys
+                if (bf)
+                    k_pw_wgrad_reg<bf16_t, 9, 18, 1><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,
+                                                                         d->pro_kind, pro_a, pro_b, part, out);
+                else
+                    k_pw_wgrad_reg<float, 9, 18, 1><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,
+                                                                        d->pro_kind, pro_a, pro_b, part, out);
+                break;
+            case 18 * 16 + 9:
+                if (bf)
+                    k_pw_wgrad_reg<bf16_t, 18, 9, 1><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,
+                                                                         d->pro_kind, pro_a, pro_b, part, out);
+                else
+                    k_pw_wgrad_reg<float, 18, 9, 1><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,
+                                                                        d->pro_kind, pro_a, pro_b, part, out);
+                break;
             REG(1, 1) REG(1, 2) REG(1, 4) REG(1, 8) REG(2, 1) REG(2, 2) REG(2, 4) REG(2, 8)
             REG(4, 1) REG(4, 2) REG(4, 4) REG(4, 8) REG(8, 1) REG(8, 2) REG(8, 4)
         default: return fail("conv3d_bwd_weight: no register-path kernel");
