@@ -84,6 +84,71 @@ __global__ __launch_bounds__(kVqThreads) void k_vq_nearest(const TZ *__restrict_
     if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
 }
 
+// Few rows (the small top-level grids): the codebook is split into chunks over blockIdx.y so the
+// search fills the chip.  Each (row, chunk) keeps the first strict minimum of its codes; the
+// finish kernel scans the chunks in increasing code order with the same strict `<`, which
+// reproduces the sequential first-index argmin exactly.
+template <typename TZ, int DM>
+__global__ __launch_bounds__(kVqThreads) void k_vq_nearest_part(const TZ *__restrict__ z, int64_t n, int d,
+                                                               const float *__restrict__ embed, int k, int ck,
+                                                               float *__restrict__ pbest, int *__restrict__ pidx) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) float esh[];
+    const int c0 = blockIdx.y * ck, nc = min(ck, k - c0);
+    for (int i = threadIdx.x; i < nc * d; i += kVqThreads) esh[i] = embed[int64_t(c0) * d + i];
+    __syncthreads();
+    const int64_t r = int64_t(blockIdx.x) * kVqThreads + threadIdx.x;
+    if (r >= n) return;
+    float x[DM];
+#pragma unroll
+    for (int i = 0; i < DM; ++i) x[i] = i < d ? ld(z + r * d + i) : 0.f;
+    float best = __builtin_inff();
+    int bi = c0;
+    for (int c = 0; c < nc; ++c) {
+        const float dv = exact_dist<DM>(x, esh + c * d, d);
+        if (dv < best) {
+            best = dv;
+            bi = c0 + c;
+        }
+    }
+    pbest[int64_t(blockIdx.y) * n + r] = best;
+    pidx[int64_t(blockIdx.y) * n + r] = bi;
+}
+
+template <typename TZ, typename TQ>
+__global__ __launch_bounds__(kVqThreads) void k_vq_nearest_finish(const TZ *__restrict__ z, int64_t n, int d,
+                                                                 const float *__restrict__ embed, int nchunk,
+                                                                 const float *__restrict__ pbest,
+                                                                 const int *__restrict__ pidx,
+                                                                 int64_t *__restrict__ idx, TQ *__restrict__ zst,
+                                                                 float *__restrict__ sqpart) {
+#pragma clang fp contract(off)
+    __shared__ float red[4];
+    const int64_t r = int64_t(blockIdx.x) * kVqThreads + threadIdx.x;
+    float sq = 0.f;
+    if (r < n) {
+        float best = __builtin_inff();
+        int bi = 0;
+        for (int j = 0; j < nchunk; ++j) {
+            const float v = pbest[int64_t(j) * n + r];
+            if (v < best) {
+                best = v;
+                bi = pidx[int64_t(j) * n + r];
+            }
+        }
+        idx[r] = bi;
+        const float *q = embed + int64_t(bi) * d;
+        for (int i = 0; i < d; ++i) {
+            const float xv = ld(z + r * d + i);
+            const float diff = q[i] - xv;
+            st(zst + r * d + i, xv + diff);
+            sq = __builtin_fmaf(diff, diff, sq);
+        }
+    }
+    sq = block_sum<float, kVqThreads>(sq, red);
+    if (threadIdx.x == 0) sqpart[blockIdx.x] = sq;
+}
+
 // generic-D fallback (D > 64): row read from memory for every codeword
 template <typename TZ, typename TQ>
 __global__ __launch_bounds__(kVqThreads) void k_vq_nearest_wide(const TZ *__restrict__ z, int64_t n, int d,
@@ -204,20 +269,33 @@ __global__ __launch_bounds__(256) void k_vq_ema_stats(const TZ *__restrict__ z, 
     }
 }
 
+// counts / dw = sum of the per-block partials in block order: LANES lanes per entry sum
+// strided slices (8 loads in flight), then a fixed xor-shuffle tree (deterministic)
+template <int LANES>
 __global__ __launch_bounds__(256) void k_vq_stats_reduce(int nb, int k, int d, const float *__restrict__ cpart,
                                                         const float *__restrict__ dpart, float *__restrict__ counts,
                                                         float *__restrict__ dw) {
-    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
     const int64_t kd = int64_t(k) * d;
-    if (e < kd) {
-        float s = 0.f;
-        for (int j = 0; j < nb; ++j) s += dpart[int64_t(j) * kd + e];
-        dw[e] = s;
+    const int64_t f = int64_t(blockIdx.x) * (256 / LANES) + threadIdx.x / LANES;  // [0, kd) dw, [kd, kd + k) counts
+    const int lane = threadIdx.x % LANES;
+    float s = 0.f;
+    const bool isd = f < kd;
+    if (f < kd + k) {
+        const float *src = isd ? dpart + f : cpart + (f - kd);
+        const int64_t stride = isd ? kd : k;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int b0 = lane; b0 < nb; b0 += 8 * LANES) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u * LANES < nb) acc[u] += src[int64_t(b0 + u * LANES) * stride];
+        }
+        s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
-    if (e < k) {
-        float s = 0.f;
-        for (int j = 0; j < nb; ++j) s += cpart[int64_t(j) * k + e];
-        counts[e] = s;
+#pragma unroll
+    for (int o = LANES / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0 && f < kd + k) {
+        if (isd) dw[f] = s;
+        else counts[f - kd] = s;
     }
 }
 
@@ -294,7 +372,8 @@ __global__ __launch_bounds__(256) void k_vq_init_apply(float *__restrict__ embed
 // ---------------------------------------------------------------- host
 struct VqPlan {
     int64_t nb_near, nb_stats;
-    size_t off_sq, off_c, off_d, off_mom, bytes;
+    int nchunk, ck;  // codebook chunks of the split search (1: single pass)
+    size_t off_sq, off_c, off_d, off_mom, off_pb, off_pi, bytes;
 };
 
 static VqPlan plan_vq(int64_t n, int d, int k) {
@@ -305,7 +384,17 @@ static VqPlan plan_vq(int64_t n, int d, int k) {
     p.off_c = (size_t(p.nb_near) * 4 + 255) / 256 * 256;
     p.off_d = p.off_c + (size_t(p.nb_stats) * k * 4 + 255) / 256 * 256;
     p.off_mom = p.off_d + (size_t(p.nb_stats) * k * d * 4 + 255) / 256 * 256;
-    p.bytes = p.off_mom + size_t(1024) * d * 8 + 256;
+    // split the codebook when the rows alone leave the chip idle (< 128 row blocks)
+    p.nchunk = 1;
+    p.ck = k;
+    if (p.nb_near < 128 && d <= 64) {
+        int nc = int(std::min<int64_t>(std::max<int64_t>(1, 512 / p.nb_near), std::max(1, k / 8)));
+        p.ck = (k + nc - 1) / nc;
+        p.nchunk = (k + p.ck - 1) / p.ck;
+    }
+    p.off_pb = p.off_mom + (size_t(1024) * d * 8 + 255) / 256 * 256;
+    p.off_pi = p.off_pb + (size_t(p.nchunk) * n * 4 + 255) / 256 * 256;
+    p.bytes = p.off_pi + size_t(p.nchunk) * n * 4 + 256;
     return p;
 }
 
@@ -352,6 +441,33 @@ int vq3d_vq_nearest(int32_t z_dtype, const void *z, int64_t n, int32_t d, const 
     VqPlan p = plan_vq(n, d, k);
     float *sqpart = reinterpret_cast<float *>(static_cast<char *>(workspace) + p.off_sq);
     const bool zf = z_dtype == VQ3D_F32, qf = zst_dtype == VQ3D_F32;
+    if (p.nchunk > 1) {
+        float *pb = reinterpret_cast<float *>(static_cast<char *>(workspace) + p.off_pb);
+        int *pi = reinterpret_cast<int *>(static_cast<char *>(workspace) + p.off_pi);
+        const dim3 g1{unsigned(p.nb_near), unsigned(p.nchunk), 1u};
+        const size_t lds = size_t(p.ck) * d * 4;
+        auto part = [&](auto tz) {
+            using TZ = decltype(tz);
+            const TZ *zz = static_cast<const TZ *>(z);
+            if (d <= 8) k_vq_nearest_part<TZ, 8><<<g1, kVqThreads, lds, s>>>(zz, n, d, embed, k, p.ck, pb, pi);
+            else if (d <= 16) k_vq_nearest_part<TZ, 16><<<g1, kVqThreads, lds, s>>>(zz, n, d, embed, k, p.ck, pb, pi);
+            else if (d <= 32) k_vq_nearest_part<TZ, 32><<<g1, kVqThreads, lds, s>>>(zz, n, d, embed, k, p.ck, pb, pi);
+            else k_vq_nearest_part<TZ, 64><<<g1, kVqThreads, lds, s>>>(zz, n, d, embed, k, p.ck, pb, pi);
+        };
+        const unsigned nb = unsigned(p.nb_near);
+        if (zf) {
+            part(float{});
+            if (qf) k_vq_nearest_finish<float, float><<<nb, kVqThreads, 0, s>>>((const float *)z, n, d, embed, p.nchunk, pb, pi, idx, (float *)zst, sqpart);
+            else k_vq_nearest_finish<float, bf16_t><<<nb, kVqThreads, 0, s>>>((const float *)z, n, d, embed, p.nchunk, pb, pi, idx, (bf16_t *)zst, sqpart);
+        } else {
+            part(bf16_t{});
+            if (qf) k_vq_nearest_finish<bf16_t, float><<<nb, kVqThreads, 0, s>>>((const bf16_t *)z, n, d, embed, p.nchunk, pb, pi, idx, (float *)zst, sqpart);
+            else k_vq_nearest_finish<bf16_t, bf16_t><<<nb, kVqThreads, 0, s>>>((const bf16_t *)z, n, d, embed, p.nchunk, pb, pi, idx, (bf16_t *)zst, sqpart);
+        }
+        if (int r = check_launch("vq_nearest(split)")) return r;
+        k_sum_partials<<<1, 256, 0, s>>>(sqpart, int(p.nb_near), sqerr_out, 0.f, nullptr);
+        return check_launch("vq_nearest(sum)");
+    }
     if (zf && qf) launch_nearest<float, float>(z, n, d, embed, k, idx, zst, sqpart, s);
     else if (zf) launch_nearest<float, bf16_t>(z, n, d, embed, k, idx, zst, sqpart, s);
     else if (qf) launch_nearest<bf16_t, float>(z, n, d, embed, k, idx, zst, sqpart, s);
@@ -405,8 +521,22 @@ int vq3d_vq_ema_stats(int32_t z_dtype, const void *z, int64_t n, int32_t d, cons
     else
         k_vq_ema_stats<bf16_t><<<unsigned(p.nb_stats), 256, lds, s>>>((const bf16_t *)z, n, d, idx, k, cpart, dpart);
     if (int r = check_launch("vq_ema_stats")) return r;
-    const int64_t kd = std::max<int64_t>(int64_t(k) * d, k);
-    k_vq_stats_reduce<<<unsigned((kd + 255) / 256), 256, 0, s>>>(int(p.nb_stats), k, d, cpart, dpart, counts, dw);
+    const int64_t ne = int64_t(k) * d + k;
+    int lanes = 1;
+    while (lanes < 64 && lanes * 16 < p.nb_stats) lanes *= 2;
+#define RED(L)                                                                                                 \
+    k_vq_stats_reduce<L><<<unsigned((ne + 256 / L - 1) / (256 / L)), 256, 0, s>>>(int(p.nb_stats), k, d, cpart, \
+                                                                                  dpart, counts, dw)
+    switch (lanes) {
+    case 1: RED(1); break;
+    case 2: RED(2); break;
+    case 4: RED(4); break;
+    case 8: RED(8); break;
+    case 16: RED(16); break;
+    case 32: RED(32); break;
+    default: RED(64); break;
+    }
+#undef RED
     return check_launch("vq_ema_stats(reduce)");
 }
 
