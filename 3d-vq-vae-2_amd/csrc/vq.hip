@@ -228,74 +228,55 @@ __global__ __launch_bounds__(256) void k_vq_bwd(const TZ *__restrict__ z, int64_
 }
 
 // ---------------------------------------------------------------- EMA statistics
-// block = kStatRows rows staged in LDS; thread owns codes c = tid, tid + 256, ... and scans
-// the rows in order -> per-block partials cpart[blk][k], dpart[blk][k][d]
+// Workgroup (row chunk of kStatRows rows, tile of 256 (code, column) entries); entry
+// e = c * (d + 1) + j: j < d sums z[r][j] over the chunk's rows with idx[r] == c, j == d counts
+// them.  Every thread walks the chunk's rows in order (the row's code is wave-uniform, its z
+// row is read by consecutive lanes), so partials are deterministic; part[chunk][k * (d + 1)].
 constexpr int kStatRows = 256;
 
 template <typename TZ>
 __global__ __launch_bounds__(256) void k_vq_ema_stats(const TZ *__restrict__ z, int64_t n, int d,
                                                      const int64_t *__restrict__ idx, int k,
-                                                     float *__restrict__ cpart, float *__restrict__ dpart) {
-    extern __shared__ __attribute__((aligned(16))) float zsh[];  // [kStatRows][d]
-    __shared__ int ish[kStatRows];
+                                                     float *__restrict__ part) {
     const int64_t r0 = int64_t(blockIdx.x) * kStatRows;
     const int nr = int(min<int64_t>(kStatRows, n - r0));
-    for (int i = threadIdx.x; i < nr; i += 256) ish[i] = int(idx[r0 + i]);
-    for (int i = threadIdx.x; i < nr * d; i += 256) zsh[i] = ld(z + r0 * d + i);
-    __syncthreads();
-    for (int c = threadIdx.x; c < k; c += 256) {
-        float cnt = 0.f;
-        float *out = dpart + (int64_t(blockIdx.x) * k + c) * d;
-        // accumulate the d sums in registers for small d, in chunks of 32 otherwise
-        for (int j0 = 0; j0 < d; j0 += 32) {
-            float acc[32];
-#pragma unroll
-            for (int j = 0; j < 32; ++j) acc[j] = 0.f;
-            float cc = 0.f;
-            for (int rr = 0; rr < nr; ++rr) {
-                if (ish[rr] == c) {
-                    cc += 1.f;
-#pragma unroll
-                    for (int j = 0; j < 32; ++j)
-                        if (j0 + j < d) acc[j] += zsh[rr * d + j0 + j];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 32; ++j)
-                if (j0 + j < d) out[j0 + j] = acc[j];
-            cnt = cc;
+    const int ne = k * (d + 1);
+    const int e = blockIdx.y * 256 + threadIdx.x;
+    const int c = e / (d + 1), j = e - c * (d + 1);
+    float acc = 0.f;
+    if (e < ne) {
+        for (int rr = 0; rr < nr; ++rr) {
+            const int64_t r = r0 + rr;
+            if (int(idx[r]) == c) acc += j < d ? ld(z + r * d + j) : 1.f;
         }
-        cpart[int64_t(blockIdx.x) * k + c] = cnt;
+        part[int64_t(blockIdx.x) * ne + e] = acc;
     }
 }
 
 // counts / dw = sum of the per-block partials in block order: LANES lanes per entry sum
 // strided slices (8 loads in flight), then a fixed xor-shuffle tree (deterministic)
 template <int LANES>
-__global__ __launch_bounds__(256) void k_vq_stats_reduce(int nb, int k, int d, const float *__restrict__ cpart,
-                                                        const float *__restrict__ dpart, float *__restrict__ counts,
-                                                        float *__restrict__ dw) {
-    const int64_t kd = int64_t(k) * d;
-    const int64_t f = int64_t(blockIdx.x) * (256 / LANES) + threadIdx.x / LANES;  // [0, kd) dw, [kd, kd + k) counts
+__global__ __launch_bounds__(256) void k_vq_stats_reduce(int nb, int k, int d, const float *__restrict__ part,
+                                                        float *__restrict__ counts, float *__restrict__ dw) {
+    const int64_t ne = int64_t(k) * (d + 1);
+    const int64_t f = int64_t(blockIdx.x) * (256 / LANES) + threadIdx.x / LANES;
     const int lane = threadIdx.x % LANES;
     float s = 0.f;
-    const bool isd = f < kd;
-    if (f < kd + k) {
-        const float *src = isd ? dpart + f : cpart + (f - kd);
-        const int64_t stride = isd ? kd : k;
+    if (f < ne) {
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int b0 = lane; b0 < nb; b0 += 8 * LANES) {
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (b0 + u * LANES < nb) acc[u] += src[int64_t(b0 + u * LANES) * stride];
+                if (b0 + u * LANES < nb) acc[u] += part[int64_t(b0 + u * LANES) * ne + f];
         }
         s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
 #pragma unroll
     for (int o = LANES / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0 && f < kd + k) {
-        if (isd) dw[f] = s;
-        else counts[f - kd] = s;
+    if (lane == 0 && f < ne) {
+        const int c = int(f / (d + 1)), j = int(f - int64_t(c) * (d + 1));
+        if (j < d) dw[int64_t(c) * d + j] = s;
+        else counts[c] = s;
     }
 }
 
@@ -510,23 +491,21 @@ int vq3d_vq_ema_stats(int32_t z_dtype, const void *z, int64_t n, int32_t d, cons
                       float *counts, float *dw, void *workspace, vq3d_stream_t stream) {
     if (n <= 0 || d <= 0 || k <= 0) return fail("vq_ema_stats: bad sizes");
     if (!z || !idx || !counts || !dw || !workspace) return fail("vq_ema_stats: null pointer");
-    if (size_t(kStatRows) * d * 4 > 64 * 1024) return fail("vq_ema_stats: embedding dim too large");
     hipStream_t s = as_stream(stream);
     VqPlan p = plan_vq(n, d, k);
-    float *cpart = reinterpret_cast<float *>(static_cast<char *>(workspace) + p.off_c);
-    float *dpart = reinterpret_cast<float *>(static_cast<char *>(workspace) + p.off_d);
-    const size_t lds = size_t(kStatRows) * d * 4;
+    float *part = reinterpret_cast<float *>(static_cast<char *>(workspace) + p.off_c);  // off_c..off_mom
+    const int64_t ne = int64_t(k) * (d + 1);
+    const dim3 grid{unsigned(p.nb_stats), unsigned((ne + 255) / 256), 1u};
     if (z_dtype == VQ3D_F32)
-        k_vq_ema_stats<float><<<unsigned(p.nb_stats), 256, lds, s>>>((const float *)z, n, d, idx, k, cpart, dpart);
+        k_vq_ema_stats<float><<<grid, 256, 0, s>>>((const float *)z, n, d, idx, k, part);
     else
-        k_vq_ema_stats<bf16_t><<<unsigned(p.nb_stats), 256, lds, s>>>((const bf16_t *)z, n, d, idx, k, cpart, dpart);
+        k_vq_ema_stats<bf16_t><<<grid, 256, 0, s>>>((const bf16_t *)z, n, d, idx, k, part);
     if (int r = check_launch("vq_ema_stats")) return r;
-    const int64_t ne = int64_t(k) * d + k;
     int lanes = 1;
     while (lanes < 64 && lanes * 16 < p.nb_stats) lanes *= 2;
 #define RED(L)                                                                                                 \
-    k_vq_stats_reduce<L><<<unsigned((ne + 256 / L - 1) / (256 / L)), 256, 0, s>>>(int(p.nb_stats), k, d, cpart, \
-                                                                                  dpart, counts, dw)
+    k_vq_stats_reduce<L><<<unsigned((ne + 256 / L - 1) / (256 / L)), 256, 0, s>>>(int(p.nb_stats), k, d, part,  \
+                                                                                  counts, dw)
     switch (lanes) {
     case 1: RED(1); break;
     case 2: RED(2); break;
