@@ -245,7 +245,21 @@ __global__ __launch_bounds__(256) void k_vq_ema_stats(const TZ *__restrict__ z, 
     const int c = e / (d + 1), j = e - c * (d + 1);
     float acc = 0.f;
     if (e < ne) {
-        for (int rr = 0; rr < nr; ++rr) {
+        int rr = 0;
+        for (; rr + 8 <= nr; rr += 8) {  // 8 rows' loads in flight, summed in row order
+            int ci[8];
+            float zv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t r = r0 + rr + u;
+                ci[u] = int(idx[r]);
+                zv[u] = j < d ? ld(z + r * d + j) : 1.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (ci[u] == c) acc += zv[u];
+        }
+        for (; rr < nr; ++rr) {
             const int64_t r = r0 + rr;
             if (int(idx[r]) == c) acc += j < d ? ld(z + r * d + j) : 1.f;
         }
