@@ -107,6 +107,33 @@ def dominant_kernel_roofline(dtype, dev, iters=50):
             "avg_launch_us": t * 1e6, "algorithmic_bytes": algo, "tflops": flops / t / 1e12}
 
 
+def dist_graph_probe(dev, rank, world):
+    """Capture + replay one RCCL all-reduce in a HIP graph; True when every rank got the right
+    value (agreed through an eager all-reduce of the per-rank verdicts)."""
+    import torch
+    import torch.distributed as dist
+    ok = 1.0
+    try:
+        t = torch.full((256,), float(rank + 1), device=dev)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                dist.all_reduce(t)
+        torch.cuda.synchronize()
+        t.fill_(float(rank + 1))
+        g.replay()
+        torch.cuda.synchronize()
+        ok = 1.0 if abs(float(t[0]) - world * (world + 1) / 2) < 1e-3 else 0.0
+    except Exception as e:  # capture unsupported: fall back to eager launches
+        print(f"[bench] rank {rank}: graph capture of all_reduce failed ({e}); eager", file=sys.stderr)
+        ok = 0.0
+    v = torch.tensor([ok], device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    return float(v) > 0.5
+
+
 # ---------------------------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(mkw, size, sample=(256, 256, 64)):
     """The CPU oracle (oracle/vqvae_cpu.py, fp32 torch-CPU restatement of the reference step)
@@ -173,13 +200,18 @@ def main():
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
-    # Single-GPU default: capture one whole training step (forward, loss, backward, Adam; ~4k
+    # Capture one whole training step (forward, loss, backward, gradient all-reduce, Adam; ~3.7k
     # kernel launches) as a HIP graph after the eager warm-up (the Quantizer's first-pass init
     # happened there) and replay it per step: no Python / launch overhead on the timed path.
     # Every replay runs the full step on the resident input; Adam's step count lives on the
-    # device.  N > 1 keeps eager launches (the RCCL collectives stay outside graphs).
+    # device.  N > 1: the RCCL collectives (EMA statistics in forward, gradient all-reduce) are
+    # captured too, after a probe capture of one all-reduce succeeded on every rank; otherwise
+    # (or with VQ3D_BENCH_DIST_GRAPH=0) the ranks run eagerly.
     graph = None
-    if not a.eager and world == 1 and a.warmup >= 2:
+    use_graph = not a.eager and a.warmup >= 2
+    if use_graph and world > 1:
+        use_graph = os.environ.get("VQ3D_BENCH_DIST_GRAPH", "1") != "0" and dist_graph_probe(dev, rank, world)
+    if use_graph:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
