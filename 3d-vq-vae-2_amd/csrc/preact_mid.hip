@@ -1,0 +1,242 @@
+// Forward of a whole PreActFixupResBlock (vqvae/layers.py:176-195, mode 'same', no skip conv)
+// in ONE launch for the 18-channel / branch-9 blocks of the published model's 128x128x32 level
+// (50 per step).  Unfused, the block forward is three launches that each stream activations
+// through HBM (1x1 conv, 3x3x3 conv, 1x1 conv + residual); here a workgroup owns a 16 x 16 x 8
+// brick and 768 threads (one D-run of 8 voxels x 3 channel groups):
+//
+//   A. t2 = elu(W1 (elu(x + b1a) + b1b) + b2a) + b2b on the brick's 18 x 18 x 10 halo
+//      (circular wrap), straight from the x rows, bf16 in LDS (rows padded to 16 channels)
+//   B. t3 = elu(W2 (*) t2 + b3a) + b3b: a thread owns a D-run of 8 voxels and 3 output channels,
+//      so one halo line read (10 positions) feeds 3 taps x 8 voxels; W2 broadcast from LDS; the
+//      line stride is an odd number of dwords (adjacent D-runs hit different banks)
+//   C. out = scale * W3 t3 + b4 + x for the D-run's 8 voxels, 6 output channels per thread
+//
+// t2 (brick rows) and t3 go to HBM as bf16 for the backward, which is unchanged.  Rounding
+// points are the unfused path's (t2 and t3 rounded to bf16 before the next conv), fp32
+// accumulation; all three weight tensors are broadcast from LDS (fp32, rows padded to 48 B).
+#include "engines.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+constexpr int C = 18, BR = 9;                 // block channels, branch channels
+constexpr int BH = 16, BW = 16, BD = 8;       // brick
+constexpr int HH = BH + 2, HW = BW + 2, HD = BD + 2, HP = HH * HW * HD;
+constexpr int RS = 16;                        // t2 position row in LDS (bf16, 32 B)
+constexpr int LSD = HD * RS + 2;              // t2 line stride (bf16): 81 dwords, odd -> no bank aliasing
+constexpr int WS = 12;                        // weight row stride in LDS (fp32, 48 B)
+constexpr int NR = BH * BW;                   // D-runs per brick (8 voxels each)
+constexpr int NG = 3;                         // thread groups: 3 output channels each in phase B
+constexpr int NTP = NR * NG;                  // 768 threads
+
+struct MidArgs {
+    int B, H, W, D;
+    int nbh, nbw, nbd, nbricks;
+};
+
+__device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+
+__global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t *__restrict__ x,
+                                                       const float *__restrict__ w1, const float *__restrict__ w2,
+                                                       const float *__restrict__ w3, vq3d_preact_params p,
+                                                       bf16_t *__restrict__ out, bf16_t *__restrict__ t2o,
+                                                       bf16_t *__restrict__ t3o) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *w2s = reinterpret_cast<float *>(smem);                      // [tap][c][WS] (o < 9)
+    float *w1s = w2s + 27 * BR * WS;                                   // [c][WS]      (o < 9)
+    float *w3s = w1s + C * WS;                                         // [co][WS]     (o < 9)
+    bf16_t *t2h = reinterpret_cast<bf16_t *>(w3s + C * WS);            // [HH * HW lines][LSD]
+    bf16_t *t3s = t2h + HH * HW * LSD + 8;                             // [NR][BD * BR]
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 27 * BR * WS; i += NTP) {
+        const int o = i % WS, r = i / WS, c = r % BR, tap = r / BR;
+        w2s[i] = o < BR ? w2[(o * BR + c) * 27 + tap] : 0.f;
+    }
+    for (int i = tid; i < C * WS; i += NTP) {
+        const int o = i % WS, c = i / WS;
+        w1s[i] = o < BR ? w1[o * C + c] : 0.f;  // W1 [BR][C] -> [c][o]
+        w3s[i] = o < BR ? w3[c * BR + o] : 0.f;  // W3 [C][BR] -> [co][o]
+    }
+    const float b1a = *p.bias1a, b1b = *p.bias1b, b2a = *p.bias2a, b2b = *p.bias2b;
+    const float b3a = *p.bias3a, b3b = *p.bias3b, sc = *p.scale, b4 = *p.bias4;
+    const int run = tid % NR, grp = tid / NR;  // D-run (lh, lw) and channel group (wave-uniform)
+    const int lh = run / BW, lw = run % BW;
+
+    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
+        int bi = brick;
+        const int bzd = bi % a.nbd;
+        bi /= a.nbd;
+        const int bzw = bi % a.nbw;
+        bi /= a.nbw;
+        const int bzh = bi % a.nbh;
+        const int b = bi / a.nbh;
+        const int oh0 = bzh * BH, ow0 = bzw * BW, od0 = bzd * BD;
+        __syncthreads();
+        // ---- A. t2 on the halo
+        for (int q = tid; q < HP; q += NTP) {
+            asm volatile("" ::: "memory");  // keep the W1 rows as per-iteration LDS reads (no hoisting)
+            const int dd = q % HD, line = q / HD, ww = line % HW, hh = line / HW;
+            const int gh = wrapm(oh0 - 1 + hh, a.H), gw = wrapm(ow0 - 1 + ww, a.W), gd = wrapm(od0 - 1 + dd, a.D);
+            const uint32_t *s32 =
+                reinterpret_cast<const uint32_t *>(x + (((int64_t(b) * a.H + gh) * a.W + gw) * a.D + gd) * C);
+            float u[C];
+#pragma unroll
+            for (int j = 0; j < C / 2; ++j) {
+                const uint32_t v = s32[j];
+                u[2 * j] = elu(__uint_as_float(v << 16) + b1a) + b1b;
+                u[2 * j + 1] = elu(__uint_as_float(v & 0xffff0000u) + b1a) + b1b;
+            }
+            float a9[WS];
+#pragma unroll
+            for (int o = 0; o < WS; ++o) a9[o] = 0.f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float4 *wr = reinterpret_cast<const float4 *>(w1s + c * WS);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float4 wq = wr[k];
+                    a9[4 * k] = fmaf(u[c], wq.x, a9[4 * k]);
+                    a9[4 * k + 1] = fmaf(u[c], wq.y, a9[4 * k + 1]);
+                    a9[4 * k + 2] = fmaf(u[c], wq.z, a9[4 * k + 2]);
+                    a9[4 * k + 3] = fmaf(u[c], wq.w, a9[4 * k + 3]);
+                }
+            }
+            uint32_t *dst = reinterpret_cast<uint32_t *>(t2h + line * LSD + dd * RS);
+#pragma unroll
+            for (int o = 0; o < RS; o += 2) {
+                const float lo = o < BR ? elu(a9[o] + b2a) + b2b : 0.f;
+                const float hi = o + 1 < BR ? elu(a9[o + 1] + b2a) + b2b : 0.f;
+                dst[o / 2] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+            }
+        }
+        __syncthreads();
+        // ---- B. t3 channels grp*3 .. grp*3+2 for the thread's D-run (lh, lw, 0..7)
+        float acc[BD][NG];
+#pragma unroll
+        for (int v = 0; v < BD; ++v)
+#pragma unroll
+            for (int o = 0; o < NG; ++o) acc[v][o] = 0.f;
+        for (int kh = 0; kh < 3; ++kh)
+            for (int kw = 0; kw < 3; ++kw) {
+                const bf16_t *ln = t2h + ((lh + kh) * HW + lw + kw) * LSD;
+                for (int c = 0; c < BR; ++c) {
+                    float tc[HD];  // channel c of the line's 10 positions
+#pragma unroll
+                    for (int q = 0; q < HD; ++q) tc[q] = ld(ln + q * RS + c);
+#pragma unroll
+                    for (int kd = 0; kd < 3; ++kd) {
+                        const float *wr = w2s + (((kh * 3 + kw) * 3 + kd) * BR + c) * WS + grp * NG;
+                        const float wv[NG] = {wr[0], wr[1], wr[2]};
+#pragma unroll
+                        for (int v = 0; v < BD; ++v)
+#pragma unroll
+                            for (int o = 0; o < NG; ++o) acc[v][o] = fmaf(tc[v + kd], wv[o], acc[v][o]);
+                    }
+                }
+            }
+#pragma unroll
+        for (int v = 0; v < BD; ++v)
+#pragma unroll
+            for (int o = 0; o < NG; ++o)
+                t3s[run * BD * BR + v * BR + grp * NG + o] = bf16_t(f2bf(elu(acc[v][o] + b3a) + b3b));
+        __syncthreads();
+        const int64_t vox0 = ((int64_t(b) * a.H + oh0 + lh) * a.W + ow0 + lw) * a.D + od0;
+        if (grp == 0) {  // t3 and the brick's t2 rows of this D-run to HBM (72 contiguous bf16 each)
+            const uint16_t *t3r = reinterpret_cast<const uint16_t *>(t3s + run * BD * BR);
+            const uint16_t *own = reinterpret_cast<const uint16_t *>(t2h + ((lh + 1) * HW + lw + 1) * LSD);
+            uint32_t *d3 = reinterpret_cast<uint32_t *>(t3o + vox0 * BR);
+            uint32_t *d2 = reinterpret_cast<uint32_t *>(t2o + vox0 * BR);
+#pragma unroll
+            for (int i = 0; i < BD * BR; i += 2) {
+                d3[i / 2] = uint32_t(t3r[i]) | (uint32_t(t3r[i + 1]) << 16);
+                const uint16_t lo = own[(1 + i / BR) * RS + i % BR];
+                const uint16_t hi = own[(1 + (i + 1) / BR) * RS + (i + 1) % BR];
+                d2[i / 2] = uint32_t(lo) | (uint32_t(hi) << 16);
+            }
+        }
+        // ---- C. out channels grp*6 .. grp*6+5 = scale * W3 t3 + b4 + x over the D-run
+        {
+            const bf16_t *t3r = t3s + run * BD * BR;
+            constexpr int CG = C / NG;  // 6 output channels per group
+            for (int v = 0; v < BD; ++v) {
+                asm volatile("" ::: "memory");  // W3 rows re-read from LDS per voxel (no hoisting)
+                float t3v[BR];
+#pragma unroll
+                for (int o = 0; o < BR; ++o) t3v[o] = ld(t3r + v * BR + o);
+                const int64_t e0 = (vox0 + v) * C + grp * CG;
+                const uint32_t *xr = reinterpret_cast<const uint32_t *>(x + e0);
+                uint32_t *orow = reinterpret_cast<uint32_t *>(out + e0);
+#pragma unroll
+                for (int k = 0; k < CG / 2; ++k) {
+                    const uint32_t xq = xr[k];
+                    float r2[2];
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int co = grp * CG + 2 * k + s2;
+                        const float4 *wr = reinterpret_cast<const float4 *>(w3s + co * WS);
+                        const float4 wa = wr[0], wb = wr[1];
+                        const float wc = w3s[co * WS + 8];
+                        const float wv[BR] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w, wc};
+                        float accv = 0.f;
+#pragma unroll
+                        for (int o = 0; o < BR; ++o) accv = fmaf(t3v[o], wv[o], accv);
+                        const float xv = s2 ? __uint_as_float(xq & 0xffff0000u) : __uint_as_float(xq << 16);
+                        r2[s2] = accv * sc + b4 + xv;
+                    }
+                    orow[k] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
+                }
+            }
+        }
+    }
+}
+
+size_t lds_mid() {
+    return (size_t(27) * BR * WS + 2 * size_t(C) * WS) * 4 + (size_t(HH) * HW * LSD + 8 + size_t(NR) * BD * BR) * 2;
+}
+
+}  // namespace
+
+}  // namespace vq3d
+
+using namespace vq3d;
+
+extern "C" {
+
+int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                              int32_t dd) {
+    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h % BH == 0 && w % BW == 0 &&
+           dd % BD == 0 && h > 0 && w > 0 && dd > 0;
+}
+
+int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                        int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
+                        const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
+    if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
+        return fail("preact_mid_fwd: shape outside the fused mid-level block kernel");
+    if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_mid_fwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    MidArgs a;
+    a.B = batch;
+    a.H = h;
+    a.W = w;
+    a.D = dd;
+    a.nbh = h / BH;
+    a.nbw = w / BW;
+    a.nbd = dd / BD;
+    a.nbricks = batch * a.nbh * a.nbw * a.nbd;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - 256));
+        (void)hipGetLastError();
+        attr = true;
+    }
+    k_preact_mid_fwd<<<unsigned(a.nbricks), NTP, lds_mid(), s>>>(a, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out,
+                                                                (bf16_t *)t2, (bf16_t *)t3);
+    return check_launch("preact_mid_fwd");
+}
+
+}  // extern "C"

@@ -66,6 +66,14 @@ class PreActBlockFn(torch.autograd.Function):
             ctx.blk = blk
             ctx.save_for_backward(x, saved)
             return out
+        if (blk.skip_conv is None and not up and k == 3 and s == 1
+                and ops.preact_mid_supported(x, blk.branch_conv1.weight.shape[0])):
+            # 18-channel level: fused forward (preact_mid.hip) writing t2 / t3 like the unfused
+            # convs, so the backward below is unchanged
+            out, t2, t3 = ops.preact_mid_fwd(x, blk)
+            ctx.blk = blk
+            ctx.save_for_backward(x, t2, t3, None)
+            return out
         t2 = ops.conv_fwd(x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), act=(blk.bias2a, blk.bias2b))
         if up:
             tup = ops.upsample2x(t2)

@@ -278,6 +278,34 @@ def preact_tiny_bwd(g, x, saved, blk, grads):
     return gx
 
 
+_mid = [os.environ.get("VQ3D_NO_MID", "0") != "1"]
+
+
+def set_mid_blocks(enabled):
+    """Route eligible bf16 PreAct blocks of the 18-channel level through the fused forward."""
+    _mid[0] = bool(enabled)
+
+
+def preact_mid_supported(x, branch):
+    b, c, h, w, d = x.shape
+    return _mid[0] and bool(L.query("vq3d_preact_mid_supported", L.dtype_code(x), b, c, branch, h, w, d))
+
+
+def preact_mid_fwd(x, blk):
+    """Fused PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last)."""
+    x = as_cl(x)
+    b, c, h, w, d = x.shape
+    w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    nb = w1.shape[0]
+    out = torch.empty_like(x, memory_format=CL)
+    t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    t3 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    prm = _preact_params(blk)
+    L.call("vq3d_preact_mid_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3),
+           ctypes.byref(prm), L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+    return out, t2, t3
+
+
 # ------------------------------------------------------------------------------------------------ misc
 def cast(x, dtype):
     if x.dtype == dtype:

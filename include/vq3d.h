@@ -150,6 +150,17 @@ int vq3d_preact_tiny_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t
                          const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                          const float *saved, float *workspace, void *gx, vq3d_stream_t stream);
 
+/* Forward of one whole PreActFixupResBlock (mode 'same', no skip conv) in one launch on the
+ * 18-channel / branch-9 level (bf16, h % 16 == w % 16 == 0, d % 8 == 0): writes out and the
+ * block's intermediates t2 = elu(W1 u1 + bias2a) + bias2b and t3 = elu(W2 (*) t2 + bias3a) + bias3b
+ * ([B][H][W][D][branch] bf16, as the unfused convs' epilogues write them), so the backward is
+ * the unfused one. */
+int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                              int32_t dd);
+int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                        int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
+                        const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream);
+
 /* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
 /* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),
  * q = E[idx], zst = fl(x + fl(q - x)) stored as zst_dtype, and the squared-error sum

@@ -1,0 +1,89 @@
+"""Fused PreAct block forward of the 18-channel level (csrc/preact_mid.hip) against the per-conv
+engine path of the same block (bf16) and a float64 torch CPU restatement of the block
+(vqvae/layers.py:176-195): output, the saved intermediates t2 / t3 (checked through the
+backward, which reads them) and every gradient.  Tolerance 3e-2 of each tensor's max
+magnitude (bf16 activations; the fused kernel keeps the 3x3x3 weights in fp32 where the MFMA
+engine rounds them to bf16)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last_3d
+SHAPES = [(1, 18, 16, 16, 8), (1, 18, 32, 16, 16), (2, 18, 16, 32, 8)]
+
+
+def _block(seed):
+    from vq3d import layers as VL
+    torch.manual_seed(seed)
+    blk = VL.PreActFixupResBlock(18, 18, mode="same")
+    rng = np.random.default_rng(seed)
+    with torch.no_grad():
+        for n, p in blk.named_parameters():
+            if p.numel() == 1:
+                p.fill_(float(rng.normal(0, 0.3)))
+            else:
+                p.normal_(0, 0.3)
+        blk.scale.fill_(0.8)
+    return blk
+
+
+def _ref(blk, x, gy):
+    P = {n: p.detach().double().cpu().clone().requires_grad_(True) for n, p in blk.named_parameters()}
+    x = x.detach().double().cpu().clone().requires_grad_(True)
+    h = F.elu(x + P["bias1a"])
+    h = F.conv3d(h + P["bias1b"], P["branch_conv1.weight"])
+    h = F.elu(h + P["bias2a"])
+    h = F.conv3d(F.pad(h + P["bias2b"], (1,) * 6, mode="circular"), P["branch_conv2.weight"])
+    h = F.elu(h + P["bias3a"])
+    h = F.conv3d(h + P["bias3b"], P["branch_conv3.weight"])
+    out = h * P["scale"] + P["bias4"] + x
+    out.backward(gy.detach().double().cpu())
+    return out.detach(), x.grad, {n: p.grad for n, p in P.items()}
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
+
+
+def _run(blk, x, gy, dev, mid):
+    from vq3d import ops
+    from vq3d.flat import FlatParams
+    ops.set_mid_blocks(mid)
+    try:
+        m = blk.to(dev)
+        for p in m.parameters():
+            p.grad = None
+        FlatParams(m.parameters(), dev)
+        xg = x.to(dev).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        y = m(xg)
+        y.backward(gy.to(dev).to(torch.bfloat16).contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+        return y.detach().float().cpu(), xg.grad.float().cpu(), {n: p.grad.cpu().clone()
+                                                                  for n, p in m.named_parameters()}
+    finally:
+        ops.set_mid_blocks(True)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_fused_mid_block_forward(gpu, shape):
+    from vq3d import ops
+    blk = _block(seed=shape[2] + shape[4])
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(shape, generator=g).bfloat16().float()
+    gy = torch.randn(shape, generator=g).bfloat16().float()
+    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    assert ops.preact_mid_supported(xg, 9)
+    ry, rgx, rgp = _ref(blk, x, gy)
+    y1, gx1, gp1 = _run(blk, x, gy, gpu, mid=True)
+    y0, gx0, gp0 = _run(blk, x, gy, gpu, mid=False)
+    errs = {"y": rel(y1, ry), "gx": rel(gx1, rgx), "y_vs_engines": rel(y1, y0), "gx_vs_engines": rel(gx1, gx0)}
+    for n in rgp:
+        errs["grad/" + n] = rel(gp1[n], rgp[n])
+    tol = 3e-2
+    small = {"grad/" + n for n, p in blk.named_parameters() if p.numel() == 1}
+    bad = {k: v for k, v in errs.items() if not v <= (0.5 if k in small else tol)}
+    assert not bad, bad
