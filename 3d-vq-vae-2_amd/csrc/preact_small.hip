@@ -1,0 +1,564 @@
+// A whole PreActFixupResBlock (vqvae/layers.py:176-195, mode 'same', no skip conv) with few
+// channels, forward in ONE launch and backward in TWO, for the published model's narrow blocks:
+// (block channels C, branch B) = (2, 1) at 128x128x32 (50 encoder pre-quantize blocks), (8, 4) at
+// 32x32x8 (50) and 256x256x64 (post-up), (4, 2) at 512x512x128 (post-up).  Unfused, one block is
+// ~20 launches (three convs fwd, three dgrads, three wgrads + reductions) whose few-channel
+// operands never fill a wave; here every thread owns whole voxels and all channels:
+//
+//   u1  = elu(x + b1a) + b1b          t2 = elu(W1 u1 + b2a) + b2b            (1x1, C -> B)
+//   t3  = elu(W2 (*) t2 + b3a) + b3b  (3x3x3 circular, B -> B)
+//   out = scale * (W3 t3) + b4 + x                                           (1x1, B -> C)
+//
+// forward: a workgroup owns a brick of voxels; phase A computes t2 on the brick's circular halo
+//   (one halo position per thread iteration, x read straight from HBM) into LDS, phase B the
+//   voxel's t3 (27 taps from LDS, weights broadcast from LDS) and, from registers, out.
+//   t2 / t3 are written (bf16) for the backward.  Rounding points are the unfused path's:
+//   t2 and t3 rounded to bf16 before the next conv, fp32 accumulation.
+// backward: per brick, gz3 = scale W3^T g * elu'(t3) on the halo (bf16, as the unfused conv3
+//   dgrad writes it), then per voxel dL/dt2 = W2^T (*) gz3 (transposed taps), gz1 = dL/dt2 *
+//   elu'(t2) (bf16), gx = g + (W1^T gz1) elu'(x + b1a); the brick's weight-gradient partials
+//   (W3: sum g t3, W2: sum gz3 t2(shifted), W1: sum gz1 u1) and the eight scalar-gradient
+//   partials go to the workspace [entry][brick]; a second launch sums every entry over the
+//   bricks in a fixed order (deterministic, one adder per gradient entry).
+#include "engines.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+constexpr int NT = 256;           // threads per workgroup (both kernels)
+constexpr int kNScal = 8;         // scalar partials: b4, scale, b3b, b3a, b2b, b2a, b1b, b1a
+constexpr size_t kLdsTarget = 80 * 1024;
+
+struct SArgs {
+    int B, H, W, D;
+    int bh, bw, bd, lbw, lbd;  // brick (powers of two)
+    int hw, hd, hp;            // halo W / D extents, halo positions
+    int nvb;                   // voxels per brick
+    int nbh, nbw, nbd, nbricks;
+};
+
+constexpr int n_entries(int C, int BR) { return C * BR + 27 * BR * BR + BR * C; }
+
+__device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+__device__ __forceinline__ float rbf(float v) { return __uint_as_float(uint32_t(f2bf(v)) << 16); }
+__device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
+    const float z1 = t - b;
+    return z1 > 0.f ? 1.f : z1 + 1.f;
+}
+
+// N consecutive bf16 (N in 1, 2, 4, 8; the address is N * 2-byte aligned) <-> fp32 registers
+template <int N>
+__device__ __forceinline__ void ldv(const bf16_t *__restrict__ p, float (&o)[N]) {
+    if constexpr (N == 1) {
+        o[0] = ld(p);
+    } else if constexpr (N == 2) {
+        const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
+        o[0] = __uint_as_float(u << 16);
+        o[1] = __uint_as_float(u & 0xffff0000u);
+    } else if constexpr (N == 4) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(p);
+        const uint32_t w[2] = {u.x, u.y};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            o[2 * i] = __uint_as_float(w[i] << 16);
+            o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+        }
+    } else {
+        static_assert(N == 8, "channel count");
+        const uint4 u = *reinterpret_cast<const uint4 *>(p);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = __uint_as_float(w[i] << 16);
+            o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void stv(bf16_t *__restrict__ p, const float (&v)[N]) {
+    if constexpr (N == 1) {
+        *p = f2bf(v[0]);
+    } else {
+        uint32_t w[N / 2];
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+        if constexpr (N == 2) *reinterpret_cast<uint32_t *>(p) = w[0];
+        else if constexpr (N == 4) *reinterpret_cast<uint2 *>(p) = uint2{w[0], w[1]};
+        else *reinterpret_cast<uint4 *>(p) = uint4{w[0], w[1], w[2], w[3]};
+    }
+}
+
+struct Brick {
+    int b, oh0, ow0, od0;
+};
+
+__device__ __forceinline__ Brick brick_of(const SArgs &a, int brick) {
+    Brick k;
+    int bi = brick;
+    const int bzd = bi % a.nbd;
+    bi /= a.nbd;
+    const int bzw = bi % a.nbw;
+    bi /= a.nbw;
+    const int bzh = bi % a.nbh;
+    k.b = bi / a.nbh;
+    k.oh0 = bzh * a.bh;
+    k.ow0 = bzw * a.bw;
+    k.od0 = bzd * a.bd;
+    return k;
+}
+
+// halo position of brick voxel v, and the global voxel index of halo position q
+__device__ __forceinline__ int halo_pos(const SArgs &a, int v) {
+    const int ld_ = v & (a.bd - 1), lw = (v >> a.lbd) & (a.bw - 1), lh = v >> (a.lbd + a.lbw);
+    return ((lh + 1) * a.hw + lw + 1) * a.hd + ld_ + 1;
+}
+__device__ __forceinline__ int64_t brick_vox(const SArgs &a, const Brick &k, int v) {
+    const int ld_ = v & (a.bd - 1), lw = (v >> a.lbd) & (a.bw - 1), lh = v >> (a.lbd + a.lbw);
+    return ((int64_t(k.b) * a.H + k.oh0 + lh) * a.W + k.ow0 + lw) * a.D + k.od0 + ld_;
+}
+// (global voxel, interior brick voxel or -1) of halo position q (circular wrap)
+__device__ __forceinline__ int64_t halo_vox(const SArgs &a, const Brick &k, int q, int &vi) {
+    const int dd = q % a.hd, r = q / a.hd, ww = r % a.hw, hh = r / a.hw;
+    const int gh = wrapm(k.oh0 - 1 + hh, a.H), gw = wrapm(k.ow0 - 1 + ww, a.W), gd = wrapm(k.od0 - 1 + dd, a.D);
+    vi = (hh >= 1 && hh <= a.bh && ww >= 1 && ww <= a.bw && dd >= 1 && dd <= a.bd)
+             ? ((hh - 1) * a.bw + ww - 1) * a.bd + dd - 1
+             : -1;
+    return ((int64_t(k.b) * a.H + gh) * a.W + gw) * a.D + gd;
+}
+// halo offset of tap (kh, kw, kd), tap = (kh * 3 + kw) * 3 + kd (nn.Conv3d weight order)
+__device__ __forceinline__ int tap_off(const SArgs &a, int tap) {
+    const int kd = tap % 3, kw = (tap / 3) % 3, kh = tap / 9;
+    return ((kh - 1) * a.hw + kw - 1) * a.hd + kd - 1;
+}
+
+struct Scal {
+    float b1a, b1b, b2a, b2b, b3a, b3b, sc, b4;
+};
+__device__ __forceinline__ Scal load_scal(const vq3d_preact_params &p) {
+    return Scal{*p.bias1a, *p.bias1b, *p.bias2a, *p.bias2b, *p.bias3a, *p.bias3b, *p.scale, *p.bias4};
+}
+
+// ------------------------------------------------------------------------------------ forward
+template <int C, int BR, int UA = (C <= 4 ? 8 : 4)>
+__global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restrict__ x, const float *__restrict__ w1,
+                                                 const float *__restrict__ w2, const float *__restrict__ w3,
+                                                 vq3d_preact_params p, bf16_t *__restrict__ out,
+                                                 bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *w2s = sm;                  // [tap][c][o]
+    float *t2h = w2s + 27 * BR * BR;  // [halo position][BR]
+    __shared__ float w1s[BR * C], w3s[C * BR];  // W1 [o][c], W3 [co][o] (torch order)
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 27 * BR * BR; i += NT) {
+        const int tap = i % 27, r = i / 27, c = r % BR, o = r / BR;
+        w2s[(tap * BR + c) * BR + o] = w2[i];
+    }
+    for (int i = tid; i < BR * C; i += NT) {
+        w1s[i] = w1[i];
+        w3s[i] = w3[i];
+    }
+    const Scal s = load_scal(p);
+    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
+        const Brick k = brick_of(a, brick);
+        __syncthreads();
+        // A. t2 on the halo (UA positions' x loads in flight per thread before any compute)
+        for (int q0 = tid; q0 < a.hp; q0 += UA * NT) {
+            int vi[UA];
+            int64_t vox[UA];
+            float xv[UA][C];
+#pragma unroll
+            for (int u = 0; u < UA; ++u) {
+                const int q = q0 + u * NT;
+                vox[u] = halo_vox(a, k, q < a.hp ? q : q0, vi[u]);
+                ldv<C>(x + vox[u] * C, xv[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < UA; ++u) {
+                const int q = q0 + u * NT;
+                if (q >= a.hp) break;
+#pragma unroll
+                for (int c = 0; c < C; ++c) xv[u][c] = elu(xv[u][c] + s.b1a) + s.b1b;
+                float t[BR];
+#pragma unroll
+                for (int o = 0; o < BR; ++o) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], xv[u][c], acc);
+                    t[o] = rbf(elu(acc + s.b2a) + s.b2b);
+                    t2h[q * BR + o] = t[o];
+                }
+                if (vi[u] >= 0) stv<BR>(t2o + vox[u] * BR, t);
+            }
+        }
+        __syncthreads();
+        // B. t3 and out of the brick's voxels, one voxel per thread
+        for (int v = tid; v < a.nvb; v += NT) {
+            const int pos = halo_pos(a, v);
+            const int64_t vox = brick_vox(a, k, v);
+            float xv[C], ov[C];
+            ldv<C>(x + vox * C, xv);  // in flight during the taps
+            float acc[BR];
+#pragma unroll
+            for (int o = 0; o < BR; ++o) acc[o] = 0.f;
+#pragma unroll 1
+            for (int tap = 0; tap < 27; ++tap) {
+                const float *tr = t2h + (pos + tap_off(a, tap)) * BR;
+                const float *wr = w2s + tap * BR * BR;
+#pragma unroll
+                for (int c = 0; c < BR; ++c) {
+                    const float tv = tr[c];
+#pragma unroll
+                    for (int o = 0; o < BR; ++o) acc[o] = fmaf(tv, wr[c * BR + o], acc[o]);
+                }
+            }
+            float t3v[BR];
+#pragma unroll
+            for (int o = 0; o < BR; ++o) t3v[o] = rbf(elu(acc[o] + s.b3a) + s.b3b);
+            stv<BR>(t3o + vox * BR, t3v);
+#pragma unroll
+            for (int co = 0; co < C; ++co) {
+                float r = 0.f;
+#pragma unroll
+                for (int o = 0; o < BR; ++o) r = fmaf(w3s[co * BR + o], t3v[o], r);
+                ov[co] = r * s.sc + s.b4 + xv[co];
+            }
+            stv<C>(out + vox * C, ov);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------ backward
+template <int C, int BR, int UB = (C <= 4 ? 4 : 2)>
+__global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restrict__ g, const bf16_t *__restrict__ x,
+                                                 const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
+                                                 const float *__restrict__ w1, const float *__restrict__ w2,
+                                                 const float *__restrict__ w3, vq3d_preact_params p,
+                                                 float *__restrict__ part, bf16_t *__restrict__ gx) {
+    constexpr int E1 = C * BR, E2 = 27 * BR * BR, E = n_entries(C, BR);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *w2t = sm;                      // [tap][o][c]
+    float *gzh = w2t + 27 * BR * BR;      // [halo position][BR]  gz3 (bf16 values)
+    float *t2h = gzh + a.hp * BR;         // [halo position][BR]
+    float *gs = t2h + a.hp * BR;          // [brick voxel][C]   g
+    float *t3s = gs + a.nvb * C;          // [brick voxel][BR]  t3
+    float *gz1 = t3s + a.nvb * BR;        // [brick voxel][BR]  gz1 (bf16 values)
+    float *u1 = gz1 + a.nvb * BR;         // [brick voxel][C]   elu(x + b1a) + b1b
+    float *scr = u1 + a.nvb * C;          // [NT] sub-stream scratch
+    __shared__ float w1s[BR * C], w3s[C * BR];
+    __shared__ float red[NT / 64];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 27 * BR * BR; i += NT) {
+        const int tap = i % 27, r = i / 27, c = r % BR, o = r / BR;
+        w2t[(tap * BR + o) * BR + c] = w2[i];
+    }
+    for (int i = tid; i < BR * C; i += NT) {
+        w1s[i] = w1[i];
+        w3s[i] = w3[i];
+    }
+    const Scal s = load_scal(p);
+    const Brick k = brick_of(a, blockIdx.x);
+    float sp[kNScal];
+#pragma unroll
+    for (int j = 0; j < kNScal; ++j) sp[j] = 0.f;
+    __syncthreads();
+    // 1. gz3 and t2 on the halo; g and t3 of the interior
+    for (int q0 = tid; q0 < a.hp; q0 += UB * NT) {
+      int vis[UB];
+      float gvs[UB][C], t3vs[UB][BR], t2vs[UB][BR];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {  // UB positions' loads in flight before any compute
+        const int q = q0 + u * NT;
+        const int64_t vox = halo_vox(a, k, q < a.hp ? q : q0, vis[u]);
+        ldv<C>(g + vox * C, gvs[u]);
+        ldv<BR>(t3 + vox * BR, t3vs[u]);
+        ldv<BR>(t2 + vox * BR, t2vs[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int q = q0 + u * NT;
+        if (q >= a.hp) break;
+        const int vi = vis[u];
+        const float(&gv)[C] = gvs[u];
+        const float(&t3v)[BR] = t3vs[u];
+        const float(&t2v)[BR] = t2vs[u];
+#pragma unroll
+        for (int o = 0; o < BR; ++o) {
+            float h = 0.f;
+#pragma unroll
+            for (int co = 0; co < C; ++co) h = fmaf(w3s[co * BR + o], gv[co], h);
+            h *= s.sc;
+            const float z = h * elu_d_act(t3v[o], s.b3b);
+            gzh[q * BR + o] = rbf(z);
+            t2h[q * BR + o] = t2v[o];
+            if (vi >= 0) {
+                sp[2] += h;
+                sp[3] += z;
+                t3s[vi * BR + o] = t3v[o];
+            }
+        }
+        if (vi >= 0) {
+#pragma unroll
+            for (int co = 0; co < C; ++co) {
+                gs[vi * C + co] = gv[co];
+                sp[0] += gv[co];
+            }
+        }
+      }
+    }
+    __syncthreads();
+    // 2. per voxel: dL/dt2 = W2^T (*) gz3, gz1, gx
+    for (int v = tid; v < a.nvb; v += NT) {
+        const int pos = halo_pos(a, v);
+        const int64_t vox = brick_vox(a, k, v);
+        float xv[C], gxv[C];
+        ldv<C>(x + vox * C, xv);  // in flight during the taps
+        float dt[BR];
+#pragma unroll
+        for (int c = 0; c < BR; ++c) dt[c] = 0.f;
+#pragma unroll 1
+        for (int tap = 0; tap < 27; ++tap) {
+            const float *zr = gzh + (pos - tap_off(a, tap)) * BR;
+            const float *wr = w2t + tap * BR * BR;
+#pragma unroll
+            for (int o = 0; o < BR; ++o) {
+                const float zv = zr[o];
+#pragma unroll
+                for (int c = 0; c < BR; ++c) dt[c] = fmaf(zv, wr[o * BR + c], dt[c]);
+            }
+        }
+        float z1[BR];
+#pragma unroll
+        for (int c = 0; c < BR; ++c) {
+            const float z = dt[c] * elu_d_act(t2h[pos * BR + c], s.b2b);
+            sp[4] += dt[c];
+            sp[5] += z;
+            z1[c] = rbf(z);
+            gz1[v * BR + c] = z1[c];
+        }
+#pragma unroll
+        for (int ci = 0; ci < C; ++ci) {
+            float r = 0.f;
+#pragma unroll
+            for (int o = 0; o < BR; ++o) r = fmaf(w1s[o * C + ci], z1[o], r);
+            sp[6] += r;
+            const float e = r * elu_grad(xv[ci] + s.b1a);
+            sp[7] += e;
+            gxv[ci] = gs[v * C + ci] + e;
+            u1[v * C + ci] = elu(xv[ci] + s.b1a) + s.b1b;
+        }
+        stv<C>(gx + vox * C, gxv);
+    }
+    __syncthreads();
+    // 3. weight-gradient partials of the brick: entry sums over its voxels in S sub-streams
+    auto entry_sum = [&](int e, int sub, int S) {
+        float acc = 0.f;
+        if (e < E1) {
+            const int co = e / BR, o = e - co * BR;
+            for (int v = sub; v < a.nvb; v += S) acc = fmaf(gs[v * C + co], t3s[v * BR + o], acc);
+        } else if (e < E1 + E2) {
+            const int r = e - E1, tap = r / (BR * BR), o = (r / BR) % BR, c = r % BR;
+            const int off = tap_off(a, tap);
+            for (int v = sub; v < a.nvb; v += S) {
+                const int pos = halo_pos(a, v);
+                acc = fmaf(gzh[pos * BR + o], t2h[(pos + off) * BR + c], acc);
+            }
+        } else {
+            const int r = e - E1 - E2, o = r / C, c = r - o * C;
+            for (int v = sub; v < a.nvb; v += S) acc = fmaf(gz1[v * BR + o], u1[v * C + c], acc);
+        }
+        return acc;
+    };
+    const int nb = gridDim.x;
+    float psc = 0.f;  // dscale partial: sum W3 o (sum_v g t3)
+    if (E >= NT) {
+        for (int e = tid; e < E; e += NT) {
+            const float t = entry_sum(e, 0, 1);
+            part[int64_t(e) * nb + blockIdx.x] = t;
+            if (e < E1) psc = fmaf(w3s[e], t, psc);
+        }
+    } else {
+        const int S = NT / E, sub = tid / E, e = tid - sub * E;
+        scr[tid] = sub < S ? entry_sum(e, sub, S) : 0.f;
+        __syncthreads();
+        if (tid < E) {
+            float t = 0.f;
+            for (int j = 0; j < S; ++j) t += scr[j * E + tid];
+            part[int64_t(tid) * nb + blockIdx.x] = t;
+            if (tid < E1) psc = fmaf(w3s[tid], t, psc);
+        }
+    }
+    sp[1] = psc;
+#pragma unroll
+    for (int j = 0; j < kNScal; ++j) {
+        const float t = block_sum<float, NT>(sp[j], red);
+        if (tid == 0) part[int64_t(E + j) * nb + blockIdx.x] = t;
+    }
+}
+
+// sum of one gradient entry's per-brick partials (fixed order), added to its gradient
+template <int C, int BR>
+__global__ __launch_bounds__(NT) void k_small_bwd_reduce(const float *__restrict__ part, int nb,
+                                                        const float *__restrict__ scale, vq3d_preact_grads gr) {
+    constexpr int E1 = C * BR, E2 = 27 * BR * BR, E = n_entries(C, BR);
+    __shared__ float red[NT / 64];
+    const int e = blockIdx.x;
+    const float *pp = part + int64_t(e) * nb;
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < nb; i += NT) acc += pp[i];
+    const float t = block_sum<float, NT>(acc, red);
+    if (threadIdx.x != 0) return;
+    float *dst = nullptr;
+    float v = t;
+    if (e < E1) {
+        dst = gr.dw3 ? gr.dw3 + e : nullptr;  // W3 [co][o]
+        v = t * *scale;
+    } else if (e < E1 + E2) {
+        const int r = e - E1, tap = r / (BR * BR), o = (r / BR) % BR, c = r % BR;
+        dst = gr.dw2 ? gr.dw2 + (o * BR + c) * 27 + tap : nullptr;
+    } else if (e < E) {
+        dst = gr.dw1 ? gr.dw1 + (e - E1 - E2) : nullptr;  // W1 [o][c]
+    } else {
+        float *const sl[kNScal] = {gr.dbias4, gr.dscale, gr.dbias3b, gr.dbias3a,
+                                   gr.dbias2b, gr.dbias2a, gr.dbias1b, gr.dbias1a};
+        dst = sl[e - E];
+    }
+    if (dst) *dst += v;
+}
+
+// ------------------------------------------------------------------------------------ planning
+size_t lds_fwd(const SArgs &a, int BR) { return (size_t(27) * BR * BR + size_t(a.hp) * BR) * 4; }
+size_t lds_bwd(const SArgs &a, int C, int BR) {
+    return (size_t(27) * BR * BR + 2 * size_t(a.hp) * BR + size_t(a.nvb) * (2 * C + 2 * BR) + NT) * 4;
+}
+
+int ilog2(int v) {
+    int r = 0;
+    while ((1 << r) < v) ++r;
+    return r;
+}
+
+bool shape_ok(int C, int BR) { return (C == 2 && BR == 1) || (C == 4 && BR == 2) || (C == 8 && BR == 4); }
+
+// Brick: up to 8 x 8 x 16 voxels (powers of two dividing the grid), halved while the backward's
+// LDS exceeds ~80 KB (two workgroups per CU) or while there are fewer than 256 bricks.
+bool plan(int batch, int C, int BR, int h, int w, int d, SArgs &a) {
+    if (!shape_ok(C, BR) || batch < 1 || h < 1 || w < 1 || d < 1) return false;
+    auto pow2 = [](int v) { return (v & (v - 1)) == 0; };
+    if (!pow2(h) || !pow2(w) || !pow2(d)) return false;
+    a.B = batch;
+    a.H = h;
+    a.W = w;
+    a.D = d;
+    auto set = [&](int bh, int bw, int bd) {
+        a.bh = bh;
+        a.bw = bw;
+        a.bd = bd;
+        a.lbw = ilog2(bw);
+        a.lbd = ilog2(bd);
+        a.hw = bw + 2;
+        a.hd = bd + 2;
+        a.hp = (bh + 2) * a.hw * a.hd;
+        a.nvb = bh * bw * bd;
+        a.nbh = h / bh;
+        a.nbw = w / bw;
+        a.nbd = d / bd;
+        a.nbricks = batch * a.nbh * a.nbw * a.nbd;
+    };
+    set(std::min(h, 8), std::min(w, 8), std::min(d, 16));
+    while (lds_bwd(a, C, BR) > kLdsTarget || (a.nbricks < 256 && a.nvb > 64)) {
+        if (a.bd >= a.bh && a.bd >= a.bw && a.bd > 1) set(a.bh, a.bw, a.bd / 2);
+        else if (a.bh >= a.bw && a.bh > 1) set(a.bh / 2, a.bw, a.bd);
+        else if (a.bw > 1) set(a.bh, a.bw / 2, a.bd);
+        else return false;
+    }
+    return true;
+}
+
+template <typename K>
+void allow_lds(K kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(160 * 1024 - 1024));
+    (void)hipGetLastError();
+}
+
+}  // namespace
+
+}  // namespace vq3d
+
+using namespace vq3d;
+
+extern "C" {
+
+int vq3d_preact_small_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                                int32_t dd) {
+    SArgs a;
+    return dtype == VQ3D_BF16 && plan(batch, channels, branch, h, w, dd, a) ? 1 : 0;
+}
+
+size_t vq3d_preact_small_workspace_bytes(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                                         int32_t dd) {
+    SArgs a;
+    if (!plan(batch, channels, branch, h, w, dd, a)) return 0;
+    return size_t(a.nbricks) * (n_entries(channels, branch) + kNScal) * 4;
+}
+
+int vq3d_preact_small_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                          int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
+                          const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
+    SArgs a;
+    if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
+        return fail("preact_small_fwd: shape outside the fused few-channel block kernels");
+    if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_small_fwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    const size_t lds = lds_fwd(a, branch);
+#define F(C_, B_)                                                                                              \
+    if (channels == C_ && branch == B_) {                                                                      \
+        static bool attr = false;                                                                              \
+        if (!attr) {                                                                                           \
+            allow_lds(k_small_fwd<C_, B_>);                                                                    \
+            attr = true;                                                                                       \
+        }                                                                                                      \
+        k_small_fwd<C_, B_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const bf16_t *)x, w1, w2, w3, *p,           \
+                                                                (bf16_t *)out, (bf16_t *)t2, (bf16_t *)t3);    \
+    }
+    F(2, 1) else F(4, 2) else F(8, 4)
+#undef F
+    return check_launch("preact_small_fwd");
+}
+
+int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                          int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
+                          const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                          void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream) {
+    SArgs a;
+    if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
+        return fail("preact_small_bwd: shape outside the fused few-channel block kernels");
+    if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx)
+        return fail("preact_small_bwd: null pointer");
+    const int ne = n_entries(channels, branch) + kNScal;
+    if (!workspace || ws_bytes < size_t(a.nbricks) * ne * 4) return fail("preact_small_bwd: workspace too small");
+    hipStream_t s = as_stream(stream);
+    const size_t lds = lds_bwd(a, channels, branch);
+    float *part = static_cast<float *>(workspace);
+#define Bk(C_, B_)                                                                                             \
+    if (channels == C_ && branch == B_) {                                                                      \
+        static bool attr = false;                                                                              \
+        if (!attr) {                                                                                           \
+            allow_lds(k_small_bwd<C_, B_>);                                                                    \
+            attr = true;                                                                                       \
+        }                                                                                                      \
+        k_small_bwd<C_, B_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const bf16_t *)g, (const bf16_t *)x,        \
+                                                                (const bf16_t *)t2, (const bf16_t *)t3, w1, w2, \
+                                                                w3, *p, part, (bf16_t *)gx);                   \
+        k_small_bwd_reduce<C_, B_><<<unsigned(ne), NT, 0, s>>>(part, a.nbricks, p->scale, *gr);                 \
+    }
+    Bk(2, 1) else Bk(4, 2) else Bk(8, 4)
+#undef Bk
+    return check_launch("preact_small_bwd");
+}
+
+}  // extern "C"

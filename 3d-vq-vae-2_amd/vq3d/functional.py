@@ -66,6 +66,16 @@ class PreActBlockFn(torch.autograd.Function):
             ctx.blk = blk
             ctx.save_for_backward(x, saved)
             return out
+        ctx.small = False
+        if (blk.skip_conv is None and not up and k == 3 and s == 1
+                and ops.preact_small_supported(x, blk.branch_conv1.weight.shape[0])):
+            # few-channel blocks: fused forward (preact_small.hip); t2 / t3 saved in bf16 as the
+            # unfused convs write them, so either backward applies
+            out, t2, t3 = ops.preact_small_fwd(x, blk)
+            ctx.blk = blk
+            ctx.small = ops.small_backward_fused(x)
+            ctx.save_for_backward(x, t2, t3, None)
+            return out
         if (blk.skip_conv is None and not up and k == 3 and s == 1
                 and ops.preact_mid_supported(x, blk.branch_conv1.weight.shape[0])):
             # 18-channel level: fused forward (preact_mid.hip) writing t2 / t3 like the unfused
@@ -107,6 +117,12 @@ class PreActBlockFn(torch.autograd.Function):
             g_x = ops.preact_tiny_bwd(g, x, saved, blk, {n: gb(t) for n, t in names.items()})
             return (g_x, None) + (None,) * len(blk._fn_params)
         x, t2, t3, tup = ctx.saved_tensors
+        if ctx.small:
+            names = {"dw1": blk.branch_conv1.weight, "dw2": blk.branch_conv2.weight, "dw3": blk.branch_conv3.weight,
+                     "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
+                     "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
+            g_x = ops.preact_small_bwd(g, x, t2, t3, blk, {n: grad_buf(t) for n, t in names.items()})
+            return (g_x, None) + (None,) * len(blk._fn_params)
         k, s, p, up = mode_geometry(blk.mode)
         g1 = ConvGeom(1)
         gb = grad_buf

@@ -306,6 +306,64 @@ def preact_mid_fwd(x, blk):
     return out, t2, t3
 
 
+_small = [os.environ.get("VQ3D_NO_SMALL", "0") != "1", os.environ.get("VQ3D_SMALL_BWD", "1") != "0"]
+
+
+def set_small_blocks(enabled, fused_backward=True):
+    """Route eligible bf16 few-channel PreAct blocks ((C, branch) = (2, 1), (4, 2), (8, 4))
+    through the fused block kernels (preact_small.hip); fused_backward=False keeps the fused
+    forward but runs the per-conv backward from its saved t2 / t3."""
+    _small[0] = bool(enabled)
+    _small[1] = bool(fused_backward)
+
+
+# fused backward up to this many voxels (measured, bench 3L pub: 23.6 vs ~100 us per (8, 4) block
+# at 32x32x8, 51 vs ~80 us per (2, 1) block at 128x128x32); beyond it the per-brick weight-gradient
+# partials are LDS-bound (6.2 ms per (4, 2) block at 512x512x128) and the per-conv backward wins
+_SMALL_BWD_MAX_VOX = 1 << 19
+
+
+def small_backward_fused(x):
+    b, _, h, w, d = x.shape
+    return _small[1] and b * h * w * d <= _SMALL_BWD_MAX_VOX
+
+
+def preact_small_supported(x, branch):
+    b, c, h, w, d = x.shape
+    return _small[0] and bool(L.query("vq3d_preact_small_supported", L.dtype_code(x), b, c, branch, h, w, d))
+
+
+def preact_small_fwd(x, blk):
+    """Fused few-channel PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last)."""
+    x = as_cl(x)
+    b, c, h, w, d = x.shape
+    w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    nb = w1.shape[0]
+    out = torch.empty_like(x, memory_format=CL)
+    t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    t3 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    prm = _preact_params(blk)
+    L.call("vq3d_preact_small_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2),
+           L.ptr(w3), ctypes.byref(prm), L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+    return out, t2, t3
+
+
+def preact_small_bwd(g, x, t2, t3, blk, grads):
+    """gx of preact_small_fwd; grads: dict name -> fp32 buffer (+=), names as in L.PreactGrads."""
+    b, c, h, w, d = x.shape
+    w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    nb = w1.shape[0]
+    gx = torch.empty_like(x, memory_format=CL)
+    nbytes = L.query("vq3d_preact_small_workspace_bytes", b, c, nb, h, w, d)
+    ws = workspace(nbytes, x.device)
+    prm = _preact_params(blk)
+    gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
+    L.call("vq3d_preact_small_bwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2),
+           L.ptr(t3), L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws),
+           ctypes.c_size_t(ws.numel()), L.ptr(gx), L.stream())
+    return gx
+
+
 # ------------------------------------------------------------------------------------------------ misc
 def cast(x, dtype):
     if x.dtype == dtype:

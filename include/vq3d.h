@@ -161,6 +161,25 @@ int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                         const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream);
 
+/* Whole PreActFixupResBlock (mode 'same', no skip conv) on few channels: (channels, branch) in
+ * {(2, 1), (4, 2), (8, 4)}, bf16, power-of-two grid.  Forward in one launch writes out, t2 and t3
+ * ([B][H][W][D][branch] bf16, as the unfused convs' epilogues write them); backward in two
+ * launches writes gx and accumulates (+=) every parameter gradient of *gr (NULL skipped),
+ * deterministically, through a caller-owned workspace of vq3d_preact_small_workspace_bytes.
+ * Replaces, for these blocks, the per-conv calls of layers.py:176-195 (fwd) and their autograd
+ * backward. */
+int vq3d_preact_small_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                                int32_t dd);
+size_t vq3d_preact_small_workspace_bytes(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                                         int32_t dd);
+int vq3d_preact_small_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                          int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
+                          const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream);
+int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                          int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
+                          const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                          void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream);
+
 /* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
 /* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),
  * q = E[idx], zst = fl(x + fl(q - x)) stored as zst_dtype, and the squared-error sum

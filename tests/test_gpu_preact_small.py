@@ -1,0 +1,100 @@
+"""Fused few-channel PreAct blocks (csrc/preact_small.hip; (C, branch) = (2, 1), (4, 2), (8, 4))
+against a float64 torch CPU restatement of the block (vqvae/layers.py:176-195) and against the
+per-conv engine path of the same block (bf16): output, input gradient and every parameter
+gradient.  The fused forward with the per-conv backward (which reads the saved t2 / t3) is
+checked too, and the fused backward's gradients must be bitwise reproducible (fixed-order
+reduction).  Tolerance 3e-2 of each tensor's max magnitude (bf16 activations); 0.5 for the
+scalar bias / scale gradients, which are sums over every voxel with heavy cancellation."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last_3d
+SHAPES = [(1, 2, 16, 16, 32), (1, 2, 128, 128, 32), (1, 4, 32, 16, 16), (1, 8, 32, 32, 8), (2, 8, 8, 16, 8),
+          (1, 4, 4, 8, 2)]
+
+
+def _block(c, seed):
+    from vq3d import layers as VL
+    torch.manual_seed(seed)
+    blk = VL.PreActFixupResBlock(c, c, mode="same")
+    rng = np.random.default_rng(seed)
+    with torch.no_grad():
+        for n, p in blk.named_parameters():
+            if p.numel() == 1:
+                p.fill_(float(rng.normal(0, 0.3)))
+            else:
+                p.normal_(0, 0.3)
+        blk.scale.fill_(0.8)
+    return blk
+
+
+def _ref(blk, x, gy):
+    P = {n: p.detach().double().cpu().clone().requires_grad_(True) for n, p in blk.named_parameters()}
+    x = x.detach().double().cpu().clone().requires_grad_(True)
+    h = F.elu(x + P["bias1a"])
+    h = F.conv3d(h + P["bias1b"], P["branch_conv1.weight"])
+    h = F.elu(h + P["bias2a"])
+    h = F.conv3d(F.pad(h + P["bias2b"], (1,) * 6, mode="circular"), P["branch_conv2.weight"])
+    h = F.elu(h + P["bias3a"])
+    h = F.conv3d(h + P["bias3b"], P["branch_conv3.weight"])
+    out = h * P["scale"] + P["bias4"] + x
+    out.backward(gy.detach().double().cpu())
+    return out.detach(), x.grad, {n: p.grad for n, p in P.items()}
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
+
+
+def _run(blk, x, gy, dev, small, fused_bwd=True):
+    from vq3d import ops
+    from vq3d.flat import FlatParams
+    ops.set_small_blocks(small, fused_bwd)
+    try:
+        m = blk.to(dev)
+        for p in m.parameters():
+            p.grad = None
+        FlatParams(m.parameters(), dev)
+        xg = x.to(dev).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        y = m(xg)
+        y.backward(gy.to(dev).to(torch.bfloat16).contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+        return y.detach().float().cpu(), xg.grad.float().cpu(), {n: p.grad.cpu().clone()
+                                                                  for n, p in m.named_parameters()}
+    finally:
+        ops.set_small_blocks(True, True)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_fused_small_block(gpu, shape):
+    from vq3d import ops
+    c = shape[1]
+    blk = _block(c, seed=shape[2] + shape[4] + c)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(shape, generator=g).bfloat16().float()
+    gy = torch.randn(shape, generator=g).bfloat16().float()
+    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    assert ops.preact_small_supported(xg, max(c // 2, 1))
+    ry, rgx, rgp = _ref(blk, x, gy)
+    y1, gx1, gp1 = _run(blk, x, gy, gpu, small=True)
+    y2, gx2, gp2 = _run(blk, x, gy, gpu, small=True)
+    yh, gxh, gph = _run(blk, x, gy, gpu, small=True, fused_bwd=False)
+    y0, gx0, gp0 = _run(blk, x, gy, gpu, small=False)
+    errs = {"y": rel(y1, ry), "gx": rel(gx1, rgx), "y_vs_engines": rel(y1, y0), "gx_vs_engines": rel(gx1, gx0),
+            "gx_half_fused": rel(gxh, rgx)}
+    for n in rgp:
+        errs["grad/" + n] = rel(gp1[n], rgp[n])
+        errs["grad_half_fused/" + n] = rel(gph[n], rgp[n])
+    tol = 3e-2
+    small = {p + n for n, q in blk.named_parameters() if q.numel() == 1 for p in ("grad/", "grad_half_fused/")}
+    bad = {k: v for k, v in errs.items() if not v <= (0.5 if k in small else tol)}
+    assert not bad, bad
+    # deterministic: the same inputs give bitwise the same output and gradients
+    assert torch.equal(y1, y2) and torch.equal(gx1, gx2)
+    for n in gp1:
+        assert torch.equal(gp1[n], gp2[n]), n
