@@ -41,6 +41,7 @@ struct SArgs {
 };
 
 constexpr int n_entries(int C, int BR) { return C * BR + 27 * BR * BR + BR * C; }
+constexpr int s2_of(int BR) { return BR >= 4 ? 14 : 28; }  // W2-gradient sub-streams (9 each)
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 __device__ __forceinline__ float rbf(float v) { return __uint_as_float(uint32_t(f2bf(v)) << 16); }
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restr
 }
 
 // ------------------------------------------------------------------------------------ backward
-template <int C, int BR, int UB = (C <= 4 ? 4 : 2)>
+template <int C, int BR, int UB = (C <= 4 ? 4 : 2), int S2 = s2_of(BR)>
 __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restrict__ g, const bf16_t *__restrict__ x,
                                                  const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
                                                  const float *__restrict__ w1, const float *__restrict__ w2,
@@ -245,11 +246,9 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
     float *t2h = gzh + a.hp * BR;         // [halo position][BR]
     float *gs = t2h + a.hp * BR;          // [brick voxel][C]   g
     float *t3s = gs + a.nvb * C;          // [brick voxel][BR]  t3
-    float *gz1 = t3s + a.nvb * BR;        // [brick voxel][BR]  gz1 (bf16 values)
-    float *u1 = gz1 + a.nvb * BR;         // [brick voxel][C]   elu(x + b1a) + b1b
-    float *scr = u1 + a.nvb * C;          // [NT] sub-stream scratch
-    __shared__ float w1s[BR * C], w3s[C * BR];
-    __shared__ float red[NT / 64];
+    float *scr = t3s + a.nvb * BR;        // [S2][E2] W2 sub-stream sums
+    __shared__ float w1s[BR * C], w3s[C * BR], g3s[C * BR];
+    __shared__ float red2[4 * (2 * C * BR + kNScal)];
     const int tid = threadIdx.x;
     for (int i = tid; i < 27 * BR * BR; i += NT) {
         const int tap = i % 27, r = i / 27, c = r % BR, o = r / BR;
@@ -310,7 +309,12 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
       }
     }
     __syncthreads();
-    // 2. per voxel: dL/dt2 = W2^T (*) gz3, gz1, gx
+    // 2. per voxel: dL/dt2 = W2^T (*) gz3, gz1, gx; W3 and W1 weight-gradient sums in registers
+    float acc1[C][BR], acc3[BR][C];
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+#pragma unroll
+        for (int j = 0; j < BR; ++j) acc1[i][j] = acc3[j][i] = 0.f;
     for (int v = tid; v < a.nvb; v += NT) {
         const int pos = halo_pos(a, v);
         const int64_t vox = brick_vox(a, k, v);
@@ -330,14 +334,14 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
                 for (int c = 0; c < BR; ++c) dt[c] = fmaf(zv, wr[o * BR + c], dt[c]);
             }
         }
-        float z1[BR];
+        float z1[BR], t3v[BR];
 #pragma unroll
         for (int c = 0; c < BR; ++c) {
             const float z = dt[c] * elu_d_act(t2h[pos * BR + c], s.b2b);
             sp[4] += dt[c];
             sp[5] += z;
             z1[c] = rbf(z);
-            gz1[v * BR + c] = z1[c];
+            t3v[c] = t3s[v * BR + c];
         }
 #pragma unroll
         for (int ci = 0; ci < C; ++ci) {
@@ -347,55 +351,103 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
             sp[6] += r;
             const float e = r * elu_grad(xv[ci] + s.b1a);
             sp[7] += e;
-            gxv[ci] = gs[v * C + ci] + e;
-            u1[v * C + ci] = elu(xv[ci] + s.b1a) + s.b1b;
+            const float gv = gs[v * C + ci];
+            gxv[ci] = gv + e;
+            const float u = elu(xv[ci] + s.b1a) + s.b1b;
+#pragma unroll
+            for (int o = 0; o < BR; ++o) {
+                acc1[ci][o] = fmaf(gv, t3v[o], acc1[ci][o]);
+                acc3[o][ci] = fmaf(z1[o], u, acc3[o][ci]);
+            }
         }
         stv<C>(gx + vox * C, gxv);
     }
-    __syncthreads();
-    // 3. weight-gradient partials of the brick: entry sums over its voxels in S sub-streams
-    auto entry_sum = [&](int e, int sub, int S) {
-        float acc = 0.f;
-        if (e < E1) {
-            const int co = e / BR, o = e - co * BR;
-            for (int v = sub; v < a.nvb; v += S) acc = fmaf(gs[v * C + co], t3s[v * BR + o], acc);
-        } else if (e < E1 + E2) {
-            const int r = e - E1, tap = r / (BR * BR), o = (r / BR) % BR, c = r % BR;
-            const int off = tap_off(a, tap);
-            for (int v = sub; v < a.nvb; v += S) {
-                const int pos = halo_pos(a, v);
-                acc = fmaf(gzh[pos * BR + o], t2h[(pos + off) * BR + c], acc);
-            }
-        } else {
-            const int r = e - E1 - E2, o = r / C, c = r - o * C;
-            for (int v = sub; v < a.nvb; v += S) acc = fmaf(gz1[v * BR + o], u1[v * C + c], acc);
-        }
-        return acc;
-    };
     const int nb = gridDim.x;
-    float psc = 0.f;  // dscale partial: sum W3 o (sum_v g t3)
-    if (E >= NT) {
-        for (int e = tid; e < E; e += NT) {
-            const float t = entry_sum(e, 0, 1);
-            part[int64_t(e) * nb + blockIdx.x] = t;
-            if (e < E1) psc = fmaf(w3s[e], t, psc);
+    // 3. W2 weight-gradient partial: thread (g9 = (kh, kw), sub) runs over D-lines of the brick,
+    //    3 kd taps x BR x BR sums in registers; the S2 sub-streams summed in a fixed order
+    {
+        float acc2[3][BR][BR];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int o = 0; o < BR; ++o)
+#pragma unroll
+                for (int c = 0; c < BR; ++c) acc2[i][o][c] = 0.f;
+        const int g9 = tid % 9, sub = tid / 9;
+        if (sub < S2) {
+            const int kh = g9 / 3, kw = g9 - kh * 3;
+            const int nr = a.bh * a.bw;
+            for (int r = sub; r < nr; r += S2) {
+                const int lh = r / a.bw, lw = r - lh * a.bw;
+                const int base = ((lh + 1) * a.hw + lw + 1) * a.hd + 1;         // voxel j = 0
+                const int tb = base + ((kh - 1) * a.hw + kw - 1) * a.hd - 1;    // its kd = 0 tap
+                for (int j = 0; j < a.bd; ++j) {
+                    float gz[BR];
+#pragma unroll
+                    for (int o = 0; o < BR; ++o) gz[o] = gzh[(base + j) * BR + o];
+#pragma unroll
+                    for (int kd = 0; kd < 3; ++kd) {
+                        float tv[BR];
+#pragma unroll
+                        for (int c = 0; c < BR; ++c) tv[c] = t2h[(tb + j + kd) * BR + c];
+#pragma unroll
+                        for (int o = 0; o < BR; ++o)
+#pragma unroll
+                            for (int c = 0; c < BR; ++c) acc2[kd][o][c] = fmaf(gz[o], tv[c], acc2[kd][o][c]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+                for (int o = 0; o < BR; ++o)
+#pragma unroll
+                    for (int c = 0; c < BR; ++c) scr[sub * E2 + ((g9 * 3 + kd) * BR + o) * BR + c] = acc2[kd][o][c];
         }
-    } else {
-        const int S = NT / E, sub = tid / E, e = tid - sub * E;
-        scr[tid] = sub < S ? entry_sum(e, sub, S) : 0.f;
         __syncthreads();
-        if (tid < E) {
+        for (int e = tid; e < E2; e += NT) {
             float t = 0.f;
-            for (int j = 0; j < S; ++j) t += scr[j * E + tid];
-            part[int64_t(tid) * nb + blockIdx.x] = t;
-            if (tid < E1) psc = fmaf(w3s[tid], t, psc);
+            for (int j = 0; j < S2; ++j) t += scr[j * E2 + e];
+            part[int64_t(E1 + e) * nb + blockIdx.x] = t;
         }
     }
-    sp[1] = psc;
+    // 4. W3 / W1 sums and the scalar partials: wave trees, then the 4 waves in order
+    constexpr int NR2 = 2 * C * BR + kNScal;
+    {
+        float vals[NR2];
 #pragma unroll
-    for (int j = 0; j < kNScal; ++j) {
-        const float t = block_sum<float, NT>(sp[j], red);
-        if (tid == 0) part[int64_t(E + j) * nb + blockIdx.x] = t;
+        for (int i = 0; i < C; ++i)
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                vals[i * BR + j] = acc1[i][j];
+                vals[E1 + j * C + i] = acc3[j][i];
+            }
+#pragma unroll
+        for (int j = 0; j < kNScal; ++j) vals[2 * E1 + j] = sp[j];
+        const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+        for (int n = 0; n < NR2; ++n) {
+            const float t = wave_sum(vals[n]);
+            if (lane == 0) red2[wv * NR2 + n] = t;
+        }
+    }
+    __syncthreads();
+    for (int n = tid; n < NR2; n += NT) {
+        const float t = red2[n] + red2[NR2 + n] + red2[2 * NR2 + n] + red2[3 * NR2 + n];
+        if (n < E1) {
+            part[int64_t(n) * nb + blockIdx.x] = t;
+            g3s[n] = t;
+        } else if (n < 2 * E1) {
+            part[int64_t(E1 + E2 + n - E1) * nb + blockIdx.x] = t;
+        } else if (n != 2 * E1 + 1) {
+            part[int64_t(E + n - 2 * E1) * nb + blockIdx.x] = t;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {  // dscale partial: sum W3 o (sum_v g t3)
+        float psc = 0.f;
+        for (int n = 0; n < E1; ++n) psc = fmaf(w3s[n], g3s[n], psc);
+        part[int64_t(E + 1) * nb + blockIdx.x] = psc;
     }
 }
 
@@ -432,7 +484,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd_reduce(const float *__restrict
 // ------------------------------------------------------------------------------------ planning
 size_t lds_fwd(const SArgs &a, int BR) { return (size_t(27) * BR * BR + size_t(a.hp) * BR) * 4; }
 size_t lds_bwd(const SArgs &a, int C, int BR) {
-    return (size_t(27) * BR * BR + 2 * size_t(a.hp) * BR + size_t(a.nvb) * (2 * C + 2 * BR) + NT) * 4;
+    return (size_t(27) * BR * BR * (1 + s2_of(BR)) + 2 * size_t(a.hp) * BR + size_t(a.nvb) * (C + BR)) * 4;
 }
 
 int ilog2(int v) {

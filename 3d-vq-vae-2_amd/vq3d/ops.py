@@ -320,7 +320,7 @@ def set_small_blocks(enabled, fused_backward=True):
 # fused backward up to this many voxels (measured, bench 3L pub: 23.6 vs ~100 us per (8, 4) block
 # at 32x32x8, 51 vs ~80 us per (2, 1) block at 128x128x32); beyond it the per-brick weight-gradient
 # partials are LDS-bound (6.2 ms per (4, 2) block at 512x512x128) and the per-conv backward wins
-_SMALL_BWD_MAX_VOX = 1 << 19
+_SMALL_BWD_MAX_VOX = int(os.environ.get("VQ3D_SMALL_BWD_MAX_VOX", 1 << 19))
 
 
 def small_backward_fused(x):
