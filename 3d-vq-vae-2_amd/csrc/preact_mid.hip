@@ -9,10 +9,13 @@
 //   B. t3 = elu(W2 (*) t2 + b3a) + b3b: a thread owns a D-run of 8 voxels and 3 output channels,
 //      so one halo line read (10 positions) feeds 3 taps x 8 voxels; W2 broadcast from LDS; the
 //      line stride is an odd number of dwords (adjacent D-runs hit different banks)
-//   C. out = scale * W3 t3 + b4 + x for the D-run's 8 voxels, 6 output channels per thread
+//   C. out = scale * W3 t3 + b4 + x for the D-run's 8 voxels, 6 output channels per thread, on
+//      the brick's x rows staged in LDS (over the dead t2 halo) and updated in place
 //
-// t2 (brick rows) and t3 go to HBM as bf16 for the backward, which is unchanged.  Rounding
-// points are the unfused path's (t2 and t3 rounded to bf16 before the next conv), fp32
+// t2 (brick rows) and t3 go to HBM as bf16 for the backward, which is unchanged.  Every HBM
+// access of the brick's rows (x in, out / t2 / t3 out) is a 16-B chunk per thread with
+// consecutive threads on consecutive chunks: whole cache lines per wave, no partial-line writes.
+// Rounding points are the unfused path's (t2 and t3 rounded to bf16 before the next conv), fp32
 // accumulation; all three weight tensors are broadcast from LDS (fp32, rows padded to 48 B).
 #include "engines.h"
 
@@ -31,6 +34,9 @@ constexpr int WS = 12;                        // weight row stride in LDS (fp32,
 constexpr int NR = BH * BW;                   // D-runs per brick (8 voxels each)
 constexpr int NG = 3;                         // thread groups: 3 output channels each in phase B
 constexpr int NTP = NR * NG;                  // 768 threads
+static_assert(HH * HW * LSD * 2 % 16 == 0 && (27 * BR * WS + 2 * C * WS) * 4 % 16 == 0,
+              "t2h and the t3 tile 16-B aligned (16-B row chunks)");
+static_assert(NR * BD * C <= HH * HW * LSD, "x / out rows of the brick fit over the t2 halo");
 
 struct MidArgs {
     int B, H, W, D;
@@ -143,21 +149,37 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
             for (int o = 0; o < NG; ++o)
                 t3s[run * BD * BR + v * BR + grp * NG + o] = bf16_t(f2bf(elu(acc[v][o] + b3a) + b3b));
         __syncthreads();
-        const int64_t vox0 = ((int64_t(b) * a.H + oh0 + lh) * a.W + ow0 + lw) * a.D + od0;
-        if (grp == 0) {  // t3 and the brick's t2 rows of this D-run to HBM (72 contiguous bf16 each)
-            const uint16_t *t3r = reinterpret_cast<const uint16_t *>(t3s + run * BD * BR);
-            const uint16_t *own = reinterpret_cast<const uint16_t *>(t2h + ((lh + 1) * HW + lw + 1) * LSD);
-            uint32_t *d3 = reinterpret_cast<uint32_t *>(t3o + vox0 * BR);
-            uint32_t *d2 = reinterpret_cast<uint32_t *>(t2o + vox0 * BR);
+        // t3 and the brick's t2 rows to HBM in 16-B chunks, consecutive threads on consecutive
+        // chunks of a D-run's 144 contiguous bytes (whole cache lines per wave store)
+        auto run_vox = [&](int r) {
+            return ((int64_t(b) * a.H + oh0 + r / BW) * a.W + ow0 + r % BW) * a.D + od0;
+        };
+        constexpr int CH2 = BD * BR / 8;  // 9 chunks per D-run
+        for (int j = tid; j < NR * CH2; j += NTP) {
+            const int r = j / CH2, part = j - r * CH2;
+            const int64_t v0 = run_vox(r);
+            *reinterpret_cast<uint4 *>(t3o + v0 * BR + part * 8) =
+                *reinterpret_cast<const uint4 *>(t3s + r * BD * BR + part * 8);
+            const uint16_t *own = reinterpret_cast<const uint16_t *>(t2h + ((r / BW + 1) * HW + r % BW + 1) * LSD);
+            uint32_t w4[4];
 #pragma unroll
-            for (int i = 0; i < BD * BR; i += 2) {
-                d3[i / 2] = uint32_t(t3r[i]) | (uint32_t(t3r[i + 1]) << 16);
-                const uint16_t lo = own[(1 + i / BR) * RS + i % BR];
-                const uint16_t hi = own[(1 + (i + 1) / BR) * RS + (i + 1) % BR];
-                d2[i / 2] = uint32_t(lo) | (uint32_t(hi) << 16);
+            for (int i = 0; i < 4; ++i) {
+                const int e0 = part * 8 + 2 * i, e1 = e0 + 1;
+                w4[i] = uint32_t(own[(1 + e0 / BR) * RS + e0 % BR]) | (uint32_t(own[(1 + e1 / BR) * RS + e1 % BR]) << 16);
             }
+            *reinterpret_cast<uint4 *>(t2o + v0 * BR + part * 8) = uint4{w4[0], w4[1], w4[2], w4[3]};
         }
-        // ---- C. out channels grp*6 .. grp*6+5 = scale * W3 t3 + b4 + x over the D-run
+        __syncthreads();  // t2h is reused below for the brick's x / out rows
+        // ---- C. x rows into LDS (16-B chunks), out = scale * W3 t3 + b4 + x in place (thread:
+        //      D-run x 6 output channels), out rows back to HBM in 16-B chunks
+        bf16_t *obuf = t2h;               // [D-run][BD * C]
+        constexpr int CH1 = BD * C / 8;  // 18 chunks per D-run
+        for (int j = tid; j < NR * CH1; j += NTP) {
+            const int r = j / CH1, part = j - r * CH1;
+            *reinterpret_cast<uint4 *>(obuf + r * BD * C + part * 8) =
+                *reinterpret_cast<const uint4 *>(x + run_vox(r) * C + part * 8);
+        }
+        __syncthreads();
         {
             const bf16_t *t3r = t3s + run * BD * BR;
             constexpr int CG = C / NG;  // 6 output channels per group
@@ -166,9 +188,7 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
                 float t3v[BR];
 #pragma unroll
                 for (int o = 0; o < BR; ++o) t3v[o] = ld(t3r + v * BR + o);
-                const int64_t e0 = (vox0 + v) * C + grp * CG;
-                const uint32_t *xr = reinterpret_cast<const uint32_t *>(x + e0);
-                uint32_t *orow = reinterpret_cast<uint32_t *>(out + e0);
+                uint32_t *xr = reinterpret_cast<uint32_t *>(obuf + run * BD * C + v * C + grp * CG);
 #pragma unroll
                 for (int k = 0; k < CG / 2; ++k) {
                     const uint32_t xq = xr[k];
@@ -186,9 +206,15 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
                         const float xv = s2 ? __uint_as_float(xq & 0xffff0000u) : __uint_as_float(xq << 16);
                         r2[s2] = accv * sc + b4 + xv;
                     }
-                    orow[k] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
+                    xr[k] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
                 }
             }
+        }
+        __syncthreads();
+        for (int j = tid; j < NR * CH1; j += NTP) {
+            const int r = j / CH1, part = j - r * CH1;
+            *reinterpret_cast<uint4 *>(out + run_vox(r) * C + part * 8) =
+                *reinterpret_cast<const uint4 *>(obuf + r * BD * C + part * 8);
         }
     }
 }

@@ -51,27 +51,46 @@ def parse():
 
 
 # ---------------------------------------------------------------------------------------------- roofline
-# Dominant kernel of the path = the 3x3x3 circular conv 9->9 at 128x128x32 (decoder bottom
-# level, 51 launches per step in the 3-layer published model: the largest conv-FLOP share,
-# SURVEY.md App. A).  Algorithmic bytes per launch = bf16 input + bf16 output + fp32 weights.
-DOM = dict(cin=9, cout=9, grid=(128, 128, 32), k=3)
+# Dominant kernel of the path = the one with the largest share of the step's kernel time in the
+# rocprofv3 kernel trace of this bench (profiles/r01_step_breakdown_v9.txt): the fused forward of
+# the 18-channel PreActFixupResBlock at 128x128x32 (preact_mid.hip, 50 launches per step, decoder
+# bottom level).  Algorithmic bytes per launch = bf16 x (18 ch) read + out (18 ch), t2 (9 ch),
+# t3 (9 ch) written + the three fp32 weight tensors.
+DOM = dict(channels=18, branch=9, grid=(128, 128, 32))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_dominant.json")
+DOM_NAME = "vq3d preact_mid_fwd: fused PreActFixupResBlock 18ch/branch 9 @128x128x32 bf16"
+
+
+def dominant_setup(dev, seed=7):
+    """(launch(), algorithmic bytes, flops) of one dominant-kernel launch on resident inputs."""
+    import torch
+
+    from vq3d import layers as VL
+    from vq3d import ops
+    torch.manual_seed(seed)
+    blk = VL.PreActFixupResBlock(DOM["channels"], DOM["channels"], mode="same").to(dev)
+    h, w, d = DOM["grid"]
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = (torch.randn((1, DOM["channels"], h, w, d), device=dev, generator=g) * 0.5).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last_3d)
+    assert ops.preact_mid_supported(x, DOM["branch"])
+
+    def launch():
+        return ops.preact_mid_fwd(x, blk)
+    nvox = h * w * d
+    c, b = DOM["channels"], DOM["branch"]
+    wbytes = sum(p.numel() for p in (blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight)) * 4
+    algo = nvox * (2 * c + 2 * b) * 2 + wbytes
+    flops = 2.0 * nvox * (c * b + b * b * 27 + b * c)
+    return launch, algo, flops
 
 
 def dominant_kernel_roofline(dtype, dev, iters=50):
     import torch
-
-    from vq3d import ops
-    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
-    h, w, d = DOM["grid"]
-    g = torch.Generator(device=dev).manual_seed(7)
-    x = (torch.randn((1, DOM["cin"], h, w, d), device=dev, generator=g) * 0.5).to(tdt).contiguous(
-        memory_format=torch.channels_last_3d)
-    wt = torch.randn((DOM["cout"], DOM["cin"], 3, 3, 3), device=dev, generator=g) * 0.1
-    geom = ops.ConvGeom(3, 1, 1, True)
+    launch, algo, flops = dominant_setup(dev)
     for _ in range(3):
-        ops.conv_fwd(x, wt, geom)
+        launch()
     torch.cuda.synchronize()
     # the `iters` launches captured in a HIP graph, so the events time back-to-back kernels on
     # the replay stream (no host launch gaps)
@@ -80,7 +99,7 @@ def dominant_kernel_roofline(dtype, dev, iters=50):
     with torch.cuda.stream(side):
         with torch.cuda.graph(graph, stream=side):
             for _ in range(iters):
-                ops.conv_fwd(x, wt, geom)
+                launch()
     graph.replay()
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
@@ -90,20 +109,17 @@ def dominant_kernel_roofline(dtype, dev, iters=50):
     e1.record(st)
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters
-    esz = x.element_size()
-    nvox = h * w * d
-    algo = nvox * (DOM["cin"] + DOM["cout"]) * esz + wt.numel() * 4
-    flops = 2.0 * nvox * DOM["cout"] * DOM["cin"] * 27
     achieved = algo / t / 1e9
     traffic = None
     if os.path.exists(PMC_FILE):
         try:
-            traffic = json.load(open(PMC_FILE)).get("hbm_bytes_per_launch")
+            pmc = json.load(open(PMC_FILE))
+            if pmc.get("kernel") == DOM_NAME:
+                traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "vq3d conv3d fwd 3x3x3 circular 9->9 @128x128x32 bf16",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": DOM_NAME,
             "avg_launch_us": t * 1e6, "algorithmic_bytes": algo, "tflops": flops / t / 1e12}
 
 

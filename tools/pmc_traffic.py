@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch HBM bytes of the dominant conv kernel from two rocprofv3 --pmc passes
+"""Per-launch HBM bytes of the dominant kernel (bench.DOM_NAME) from two rocprofv3 --pmc passes
 (FETCH_SIZE, WRITE_SIZE; kilobytes per dispatch).  Correction per MI355X_MICROARCH.md
 §HBM: FETCH_SIZE reads exactly 1/2 of a wide coalesced streaming read on gfx950, so the
 read side is doubled; WRITE_SIZE is taken as is.  Prints JSON."""
@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_lines"
+KERNEL = "k_preact_mid_fwd"
 
 
 def per_dispatch(d, counter):
@@ -26,7 +26,7 @@ def main():
     w = per_dispatch(sys.argv[2], "WRITE_SIZE")
     fetch = sum(f) / len(f) * 1024.0
     write = sum(w) / len(w) * 1024.0
-    out = {"kernel": "vq3d conv3d fwd 3x3x3 circular 9->9 @128x128x32 bf16", "dispatches": [len(f), len(w)],
+    out = {"kernel": "vq3d preact_mid_fwd: fused PreActFixupResBlock 18ch/branch 9 @128x128x32 bf16", "dispatches": [len(f), len(w)],
            "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2.0 * fetch + write,
            "note": "FETCH_SIZE doubled (gfx950 counts 64 B per 128 B request, MI355X_MICROARCH.md §HBM); "
