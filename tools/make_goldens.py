@@ -405,9 +405,44 @@ def gen_ema_dist():
     save("ema_dist2", **out)
 
 
+# ----------------------------------------------------------------------------------------
+# G. Encode-only extraction (extract_embeddings.py:16-23): eval mode, no_grad, batch 1,
+#    codes per level bottom -> top, from a model whose codebooks went through one EMA step
+# ----------------------------------------------------------------------------------------
+
+def gen_encode(name, args, x_shape, n_samples=2):
+    """State after one reference train step (first pass + EMA done), then model.eval() and
+    `*_, idx = zip(*model.encode(x))` for n_samples volumes x_i = rand(seed 5000 + i) * 4.5 - 0.5."""
+    torch.manual_seed(0)
+    m = VQVAE(args)
+    perturb_(m, seed=1)
+    opt = m.configure_optimizers()
+    g = torch.Generator().manual_seed(1234)
+    x = torch.rand(x_shape, generator=g) * 4.5 - 0.5
+    m.train()
+    loss = m.training_step((x, torch.tensor([x_shape[-1]] * x_shape[0])), 0)
+    loss.backward()
+    opt.step()
+    out = {"x_shape": np.array((1,) + tuple(x_shape[1:])), "n_samples": np.int64(n_samples)}
+    for pn, p in m.state_dict().items():
+        out[f"state/{pn}"] = t2n(p).copy()
+    m.eval()
+    with torch.no_grad():
+        for i in range(n_samples):
+            gi = torch.Generator().manual_seed(5000 + i)
+            xi = torch.rand((1,) + tuple(x_shape[1:]), generator=gi) * 4.5 - 0.5
+            losses, qsts, idxs = zip(*m.encode(xi))
+            for lvl, (c, q, ix) in enumerate(zip(losses, qsts, idxs)):
+                out[f"sample{i}/idx{lvl}"] = t2n(ix).astype(np.int16)
+                out[f"sample{i}/commit{lvl}"] = np.float32(float(c))
+                if lvl == 0:
+                    out[f"sample{i}/qst{lvl}"] = t2n(q)
+    save(name, **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["vq", "qtrain", "blocks", "loss", "ema", "models"]
+    which = sys.argv[1:] or ["vq", "qtrain", "blocks", "loss", "ema", "models", "encode"]
     if "ema" in which:
         gen_ema_dist()
     if "vq" in which:
@@ -435,6 +470,12 @@ def main():
                   (1, 1, 32, 32, 16), [16], steps=1, keep_state=False)
         gen_model("model_2l_evonorm_32", model_args(block_type='evonorm'), (1, 1, 32, 32, 16), [16],
                   steps=1, keep_state=False)
+    if "encode" in which:
+        gen_encode("encode_2l_blocks_32", model_args(n_pre_quantization_blocks=1, n_post_quantization_blocks=1,
+                                                     n_post_upscale_blocks=1, n_post_downscale_blocks=1,
+                                                     num_embeddings=[64, 32]), (1, 1, 32, 32, 32))
+        gen_encode("encode_3l_b2_64", model_args(n_bottleneck_blocks=3, base_network_channels=2,
+                                                 num_embeddings=[128, 256, 512]), (2, 1, 64, 64, 64))
 
 
 if __name__ == "__main__":
