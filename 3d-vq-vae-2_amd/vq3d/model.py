@@ -64,6 +64,13 @@ class VQVAE(nn.Module):
     def save_hyperparameters(self, args):
         self.hparams = {"args": args}
 
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location=None, strict=True, **overrides):
+        """LightningModule.load_from_checkpoint (used by extract_embeddings.py:45,
+        decode_embeddings.py:23) over a PL 1.2-layout .ckpt; see vq3d/checkpoint.py."""
+        from .checkpoint import load_from_checkpoint
+        return load_from_checkpoint(cls, checkpoint_path, map_location=map_location, strict=strict, **overrides)
+
     def log(self, name, value, **kwargs):
         self.logged[name] = value.detach() if torch.is_tensor(value) else value
 

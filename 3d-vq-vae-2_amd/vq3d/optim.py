@@ -47,10 +47,11 @@ class FusedAdam(torch.optim.Optimizer):
         sd = super().state_dict()
         st = {}
         step_count = self.step_count
+        offs = {id(q): off for q, off in zip(self.flat.params, self.flat.offsets)}
         idx = 0
         for g in self.param_groups:
             for p in g["params"]:
-                off = self.flat.offsets[self.flat.params.index(p)]
+                off = offs[id(p)]
                 n = p.numel()
                 if step_count:
                     st[idx] = dict(step=torch.tensor(float(step_count)),
@@ -63,11 +64,12 @@ class FusedAdam(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         st = state_dict["state"]
+        offs = {id(q): off for q, off in zip(self.flat.params, self.flat.offsets)}
         idx = 0
         steps = set()
         for g in self.param_groups:
             for p in g["params"]:
-                off = self.flat.offsets[self.flat.params.index(p)]
+                off = offs[id(p)]
                 n = p.numel()
                 s = st.get(idx)
                 if s is not None:
