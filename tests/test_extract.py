@@ -145,3 +145,53 @@ def test_gpu_extract_bf16_codes(gpu):
         for lvl, ix in enumerate(idxs):
             match = (ix.cpu().numpy() == d[f"sample{i}/idx{lvl}"]).mean()
             assert match >= 0.9, (i, lvl, match)
+
+
+# ------------------------------------------------------------------------- decode path (§8(f) row 3)
+def test_nrrd_roundtrip(tmp_path):
+    from vq3d.decode import read_nrrd, write_nrrd
+    rng = np.random.default_rng(1)
+    for dt in (np.int64, np.int16, np.float32):
+        a = (rng.standard_normal((5, 4, 3)) * 1000).astype(dt)
+        p = str(tmp_path / f"v_{np.dtype(dt).name}.nrrd")
+        write_nrrd(p, a)
+        b, hdr = read_nrrd(p)
+        assert b.dtype == a.dtype and np.array_equal(a, b)
+        assert hdr["sizes"] == "5 4 3" and hdr["spacings"].split() == ["0.976", "0.976", "3.0"]
+
+
+@pytest.mark.parametrize("name", sorted(ENC_CFGS))
+def test_oracle_decode_codes_vs_reference(name):
+    """Oracle decode of the reference's codes: HU volume (rint(elu(dec) * 1000 - 1000)) within
+    1 HU of the reference (fp32 summation order; rint boundaries)."""
+    torch.set_num_threads(4)
+    d = golden(name)
+    cfg = O.Config(**ENC_CFGS[name])
+    sd = {k[6:]: torch.from_numpy(d[k].copy()) for k in d.files if k.startswith("state/")}
+    for i in range(int(d["n_samples"])):
+        qs = [sd[f"encoder.quantize.{lvl}.embed"][torch.from_numpy(d[f"sample{i}/idx{lvl}"].astype(np.int64))]
+              .permute(0, 4, 1, 2, 3) for lvl in range(cfg.n_bottleneck_blocks)]
+        with torch.no_grad():
+            hu = np.rint(torch.nn.functional.elu(O.decode(cfg, sd, qs)).squeeze().numpy() * 1000 - 1000)
+        assert np.abs(hu - d[f"sample{i}/hu"]).max() <= 1, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(ENC_CFGS))
+def test_gpu_decode_codes_vs_reference(gpu, name, tmp_path):
+    """HIP decode of the reference's codes (fp32): HU within 1 + 5e-4 of the volume's max |HU|;
+    written to NRRD and read back unchanged."""
+    from vq3d.decode import decode_codes, read_nrrd, write_nrrd
+    m, d = _load(name, gpu, "fp32")
+    for i in range(int(d["n_samples"])):
+        codes = [d[f"sample{i}/idx{lvl}"].astype(np.int64) for lvl in range(m.n_bottleneck_blocks)]
+        hu = decode_codes(m, codes).cpu().numpy()
+        ref = d[f"sample{i}/hu"]
+        assert hu.shape == ref.shape and hu.dtype == np.int64
+        assert np.abs(hu - ref).max() <= 1 + 5e-4 * np.abs(ref).max(), (name, i, np.abs(hu - ref).max())
+        p = str(tmp_path / f"s{i}.nrrd")
+        write_nrrd(p, hu)
+        back, _ = read_nrrd(p)
+        assert np.array_equal(back, hu)
+    with pytest.raises(IndexError):
+        decode_codes(m, [np.full_like(codes[0], 10 ** 6)] + codes[1:])

@@ -437,6 +437,11 @@ def gen_encode(name, args, x_shape, n_samples=2):
                 out[f"sample{i}/commit{lvl}"] = np.float32(float(c))
                 if lvl == 0:
                     out[f"sample{i}/qst{lvl}"] = t2n(q)
+            # decode_embeddings.py:35-45 (without autocast: CPU fp32): codes -> embed_code ->
+            # decode -> elu -> HU = rint(x * 1000 - 1000)
+            embs = [qz.embed_code(ix).permute(0, 4, 1, 2, 3) for ix, qz in zip(idxs, m.encoder.quantize)]
+            res = F.elu(m.decode(embs)).squeeze().numpy() * 1000 - 1000
+            out[f"sample{i}/hu"] = np.rint(res).astype(np.int32)
     save(name, **out)
 
 
