@@ -20,42 +20,56 @@
 #include "engines.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace vq3d {
 
 namespace {
 
 constexpr int C = 18, BR = 9;                 // block channels, branch channels
-constexpr int BH = 16, BW = 16, BD = 8;       // brick
-constexpr int HH = BH + 2, HW = BW + 2, HD = BD + 2, HP = HH * HW * HD;
-constexpr int RS = 16;                        // t2 position row in LDS (bf16, 32 B)
-constexpr int LSD = HD * RS + 2;              // t2 line stride (bf16): 81 dwords, odd -> no bank aliasing
+constexpr int BD = 8, HD = BD + 2;            // brick depth (one D-run of 8 voxels per thread)
 constexpr int WS = 12;                        // weight row stride in LDS (fp32, 48 B)
-constexpr int NR = BH * BW;                   // D-runs per brick (8 voxels each)
 constexpr int NG = 3;                         // thread groups: 3 output channels each in phase B
-constexpr int NTP = NR * NG;                  // 768 threads
-static_assert(HH * HW * LSD * 2 % 16 == 0 && (27 * BR * WS + 2 * C * WS) * 4 % 16 == 0,
-              "t2h and the t3 tile 16-B aligned (16-B row chunks)");
-static_assert(NR * BD * C <= HH * HW * LSD, "x / out rows of the brick fit over the t2 halo");
+
+// Brick geometry (BH x BW x 8 voxels) and the t2 position row RS (bf16, >= 9): the 16 x 16
+// brick with 16-wide rows needs 155 KB of LDS (one workgroup per CU, phases serialised on
+// every CU); 8 x 16 with 10-wide rows fits two workgroups per CU (68 KB each).
+template <int BH_, int BW_, int RS_>
+struct Geo {
+    static constexpr int BH = BH_, BW = BW_, RS = RS_;
+    static constexpr int HH = BH + 2, HW = BW + 2, HP = HH * HW * HD;
+    static constexpr int LSD = HD * RS + 2;   // t2 line stride (bf16): odd number of dwords -> no bank aliasing
+    static constexpr int NR = BH * BW;        // D-runs per brick
+    static constexpr int NTP = NR * NG;       // threads
+    static constexpr int T2H = (HH * HW * LSD > NR * BD * C ? HH * HW * LSD : NR * BD * C + 0);  // t2 halo / x rows
+    static constexpr int T2HA = (T2H + 7) / 8 * 8;
+    static_assert(LSD / 2 % 2 == 1 && RS % 2 == 0 && RS >= BR, "odd dword line stride, paired rows");
+    static_assert((27 * BR * WS + 2 * C * WS) * 4 % 16 == 0, "t2h 16-B aligned");
+    static size_t lds() { return (size_t(27) * BR * WS + 2 * size_t(C) * WS) * 4 + (size_t(T2HA) + 8 + size_t(NR) * BD * BR) * 2; }
+};
 
 struct MidArgs {
     int B, H, W, D;
     int nbh, nbw, nbd, nbricks;
+    int dbg;  // timing experiments only (VQ3D_PM_DBG): bit 0 skips phase A, 1 phase B, 2 phase C's math
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
-__global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t *__restrict__ x,
+template <class G>
+__global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t *__restrict__ x,
                                                        const float *__restrict__ w1, const float *__restrict__ w2,
                                                        const float *__restrict__ w3, vq3d_preact_params p,
                                                        bf16_t *__restrict__ out, bf16_t *__restrict__ t2o,
                                                        bf16_t *__restrict__ t3o) {
+    constexpr int BH = G::BH, BW = G::BW, RS = G::RS, HW = G::HW, HP = G::HP, LSD = G::LSD, NR = G::NR,
+                  NTP = G::NTP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *w2s = reinterpret_cast<float *>(smem);                      // [tap][c][WS] (o < 9)
     float *w1s = w2s + 27 * BR * WS;                                   // [c][WS]      (o < 9)
     float *w3s = w1s + C * WS;                                         // [co][WS]     (o < 9)
     bf16_t *t2h = reinterpret_cast<bf16_t *>(w3s + C * WS);            // [HH * HW lines][LSD]
-    bf16_t *t3s = t2h + HH * HW * LSD + 8;                             // [NR][BD * BR]
+    bf16_t *t3s = t2h + G::T2HA + 8;                             // [NR][BD * BR]
     const int tid = threadIdx.x;
     for (int i = tid; i < 27 * BR * WS; i += NTP) {
         const int o = i % WS, r = i / WS, c = r % BR, tap = r / BR;
@@ -82,7 +96,7 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
         const int oh0 = bzh * BH, ow0 = bzw * BW, od0 = bzd * BD;
         __syncthreads();
         // ---- A. t2 on the halo
-        for (int q = tid; q < HP; q += NTP) {
+        for (int q = (a.dbg & 1) ? HP : tid; q < HP; q += NTP) {
             asm volatile("" ::: "memory");  // keep the W1 rows as per-iteration LDS reads (no hoisting)
             const int dd = q % HD, line = q / HD, ww = line % HW, hh = line / HW;
             const int gh = wrapm(oh0 - 1 + hh, a.H), gw = wrapm(ow0 - 1 + ww, a.W), gd = wrapm(od0 - 1 + dd, a.D);
@@ -125,21 +139,43 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
         for (int v = 0; v < BD; ++v)
 #pragma unroll
             for (int o = 0; o < NG; ++o) acc[v][o] = 0.f;
-        for (int kh = 0; kh < 3; ++kh)
+        // t2 channels read four at a time (two dwords per position: 30 LDS reads per (kh, kw)
+        // instead of 90); W2 is wave-uniform (the channel group is per wave) and read through the
+        // scalar cache straight from the fp32 weights, so phase B's LDS traffic is t2 only
+        const int grpu = __builtin_amdgcn_readfirstlane(grp);
+        const float *__restrict__ w2g = w2 + grpu * NG * BR * 27;  // o = grpu * 3 + j: + j * BR * 27
+        for (int kh = (a.dbg & 2) ? 3 : 0; kh < 3; ++kh)
             for (int kw = 0; kw < 3; ++kw) {
                 const bf16_t *ln = t2h + ((lh + kh) * HW + lw + kw) * LSD;
-                for (int c = 0; c < BR; ++c) {
-                    float tc[HD];  // channel c of the line's 10 positions
+                const int tap0 = (kh * 3 + kw) * 3;
 #pragma unroll
-                    for (int q = 0; q < HD; ++q) tc[q] = ld(ln + q * RS + c);
+                for (int cg = 0; cg < (BR + 3) / 4; ++cg) {
+                    uint32_t raw[HD][2];
 #pragma unroll
-                    for (int kd = 0; kd < 3; ++kd) {
-                        const float *wr = w2s + (((kh * 3 + kw) * 3 + kd) * BR + c) * WS + grp * NG;
-                        const float wv[NG] = {wr[0], wr[1], wr[2]};
+                    for (int q = 0; q < HD; ++q) {
+                        const uint32_t *p32 = reinterpret_cast<const uint32_t *>(ln + q * RS + 4 * cg);
+                        raw[q][0] = p32[0];
+                        raw[q][1] = 4 * cg + 2 < BR ? p32[1] : 0u;
+                    }
 #pragma unroll
-                        for (int v = 0; v < BD; ++v)
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const int c = 4 * cg + cc;
+                        if (c >= BR) break;
+                        float tc[HD];  // channel c of the line's 10 positions
 #pragma unroll
-                            for (int o = 0; o < NG; ++o) acc[v][o] = fmaf(tc[v + kd], wv[o], acc[v][o]);
+                        for (int q = 0; q < HD; ++q) {
+                            const uint32_t u = raw[q][cc >> 1];
+                            tc[q] = __uint_as_float((cc & 1) ? (u & 0xffff0000u) : (u << 16));
+                        }
+#pragma unroll
+                        for (int kd = 0; kd < 3; ++kd) {
+                            const float *wr = w2g + c * 27 + tap0 + kd;
+                            const float wv[NG] = {wr[0], wr[BR * 27], wr[2 * BR * 27]};
+#pragma unroll
+                            for (int v = 0; v < BD; ++v)
+#pragma unroll
+                                for (int o = 0; o < NG; ++o) acc[v][o] = fmaf(tc[v + kd], wv[o], acc[v][o]);
+                        }
                     }
                 }
             }
@@ -183,7 +219,7 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
         {
             const bf16_t *t3r = t3s + run * BD * BR;
             constexpr int CG = C / NG;  // 6 output channels per group
-            for (int v = 0; v < BD; ++v) {
+            for (int v = (a.dbg & 4) ? BD : 0; v < BD; ++v) {
                 asm volatile("" ::: "memory");  // W3 rows re-read from LDS per voxel (no hoisting)
                 float t3v[BR];
 #pragma unroll
@@ -219,8 +255,34 @@ __global__ __launch_bounds__(NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t 
     }
 }
 
-size_t lds_mid() {
-    return (size_t(27) * BR * WS + 2 * size_t(C) * WS) * 4 + (size_t(HH) * HW * LSD + 8 + size_t(NR) * BD * BR) * 2;
+using GeoWide = Geo<16, 16, 16>;  // 256 bricks at 128 x 128 x 32
+using GeoHalf = Geo<8, 16, 10>;   // 512 bricks, two workgroups per CU
+
+// VQ3D_PM_BRICK=8 selects the 8 x 16 brick (A/B switch; measured slower); default 16 x 16
+bool use_wide() {
+    static const int v = [] {
+        const char *e = std::getenv("VQ3D_PM_BRICK");
+        return e ? std::atoi(e) : 16;
+    }();
+    return v == 16;
+}
+
+template <class G>
+void launch_mid(const MidArgs &a0, hipStream_t s, const bf16_t *x, const float *w1, const float *w2, const float *w3,
+                const vq3d_preact_params &p, bf16_t *out, bf16_t *t2, bf16_t *t3) {
+    MidArgs a = a0;
+    a.nbh = a.H / G::BH;
+    a.nbw = a.W / G::BW;
+    a.nbd = a.D / BD;
+    a.nbricks = a.B * a.nbh * a.nbw * a.nbd;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd<G>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - 256));
+        (void)hipGetLastError();
+        attr = true;
+    }
+    k_preact_mid_fwd<G><<<unsigned(a.nbricks), G::NTP, G::lds(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
 }
 
 }  // namespace
@@ -233,7 +295,7 @@ extern "C" {
 
 int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                               int32_t dd) {
-    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h % BH == 0 && w % BW == 0 &&
+    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h % 16 == 0 && w % 16 == 0 &&
            dd % BD == 0 && h > 0 && w > 0 && dd > 0;
 }
 
@@ -245,23 +307,19 @@ int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_mid_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     MidArgs a;
+    static const int dbg = [] {
+        const char *e = std::getenv("VQ3D_PM_DBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    a.dbg = dbg;
     a.B = batch;
     a.H = h;
     a.W = w;
     a.D = dd;
-    a.nbh = h / BH;
-    a.nbw = w / BW;
-    a.nbd = dd / BD;
-    a.nbricks = batch * a.nbh * a.nbw * a.nbd;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - 256));
-        (void)hipGetLastError();
-        attr = true;
-    }
-    k_preact_mid_fwd<<<unsigned(a.nbricks), NTP, lds_mid(), s>>>(a, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out,
-                                                                (bf16_t *)t2, (bf16_t *)t3);
+    if (use_wide())
+        launch_mid<GeoWide>(a, s, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out, (bf16_t *)t2, (bf16_t *)t3);
+    else
+        launch_mid<GeoHalf>(a, s, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out, (bf16_t *)t2, (bf16_t *)t3);
     return check_launch("preact_mid_fwd");
 }
 
