@@ -30,6 +30,7 @@ constexpr int C = 18, BR = 9;                 // block channels, branch channels
 constexpr int BD = 8, HD = BD + 2;            // brick depth (one D-run of 8 voxels per thread)
 constexpr int WS = 12;                        // weight row stride in LDS (fp32, 48 B)
 constexpr int NG = 3;                         // thread groups: 3 output channels each in phase B
+constexpr int W2R = 27 * 9 * 12 > 14 * 64 * 8 / 2 ? 27 * 9 * 12 : 14 * 64 * 8 / 2;  // W2 region (floats)
 
 // Brick geometry (BH x BW x 8 voxels) and the t2 position row RS (bf16, >= 9): the 16 x 16
 // brick with 16-wide rows needs 155 KB of LDS (one workgroup per CU, phases serialised on
@@ -44,9 +45,13 @@ struct Geo {
     static constexpr int T2H = (HH * HW * LSD > NR * BD * C ? HH * HW * LSD : NR * BD * C + 0);  // t2 halo / x rows
     static constexpr int T2HA = (T2H + 7) / 8 * 8;
     static_assert(LSD / 2 % 2 == 1 && RS % 2 == 0 && RS >= BR, "odd dword line stride, paired rows");
-    static_assert((27 * BR * WS + 2 * C * WS) * 4 % 16 == 0, "t2h 16-B aligned");
-    static size_t lds() { return (size_t(27) * BR * WS + 2 * size_t(C) * WS) * 4 + (size_t(T2HA) + 8 + size_t(NR) * BD * BR) * 2; }
+    static_assert((W2R + 2 * C * WS) * 4 % 16 == 0, "t2h 16-B aligned");
+    static size_t lds() { return (size_t(W2R) + 2 * size_t(C) * WS) * 4 + (size_t(T2HA) + 8 + size_t(NR) * BD * BR) * 2; }
 };
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int NPAIR = 14;  // MFMA k-steps of phase B: 27 taps in pairs x 16 (padded) channels
 
 struct MidArgs {
     int B, H, W, D;
@@ -56,7 +61,7 @@ struct MidArgs {
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
-template <class G>
+template <class G, bool MFB>
 __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t *__restrict__ x,
                                                        const float *__restrict__ w1, const float *__restrict__ w2,
                                                        const float *__restrict__ w3, vq3d_preact_params p,
@@ -66,14 +71,25 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
                   NTP = G::NTP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *w2s = reinterpret_cast<float *>(smem);                      // [tap][c][WS] (o < 9)
-    float *w1s = w2s + 27 * BR * WS;                                   // [c][WS]      (o < 9)
+    float *w1s = w2s + W2R;                                            // [c][WS]      (o < 9)
     float *w3s = w1s + C * WS;                                         // [co][WS]     (o < 9)
     bf16_t *t2h = reinterpret_cast<bf16_t *>(w3s + C * WS);            // [HH * HW lines][LSD]
     bf16_t *t3s = t2h + G::T2HA + 8;                             // [NR][BD * BR]
     const int tid = threadIdx.x;
-    for (int i = tid; i < 27 * BR * WS; i += NTP) {
-        const int o = i % WS, r = i / WS, c = r % BR, tap = r / BR;
-        w2s[i] = o < BR ? w2[(o * BR + c) * 27 + tap] : 0.f;
+    if constexpr (MFB) {
+        // phase-B MFMA B fragments, bf16: [pair][lane][8], lane l holds B[k = 8 (l >> 4) + j][n = l & 15]
+        // with k = 16 * (tap - 2 pair) + c (c < 16 padded, tap < 27), n = output channel (< 9)
+        bf16_t *wf = reinterpret_cast<bf16_t *>(w2s);
+        for (int i = tid; i < NPAIR * 64 * 8; i += NTP) {
+            const int j = i & 7, l = (i >> 3) & 63, pr = i >> 9;
+            const int k = 8 * (l >> 4) + j, n = l & 15, c = k & 15, tap = 2 * pr + (k >> 4);
+            wf[i] = bf16_t(f2bf(n < BR && c < BR && tap < 27 ? w2[(n * BR + c) * 27 + tap] : 0.f));
+        }
+    } else {
+        for (int i = tid; i < 27 * BR * WS; i += NTP) {
+            const int o = i % WS, r = i / WS, c = r % BR, tap = r / BR;
+            w2s[i] = o < BR ? w2[(o * BR + c) * 27 + tap] : 0.f;
+        }
     }
     for (int i = tid; i < C * WS; i += NTP) {
         const int o = i % WS, c = i / WS;
@@ -133,57 +149,100 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
             }
         }
         __syncthreads();
-        // ---- B. t3 channels grp*3 .. grp*3+2 for the thread's D-run (lh, lw, 0..7)
-        float acc[BD][NG];
+        static_assert(!MFB || G::RS == 16, "MFMA phase B reads 8-channel halves of 16-wide rows");
+        if constexpr (MFB) {
+        // ---- B (matrix cores). t3 = W2 (*) t2 as 16-voxel x 16-channel tiles (two D-runs of 8
+        //      voxels; 9 of 16 output columns valid), K = 27 taps x 16 channels in 14 steps of
+        //      v_mfma_f32_16x16x32_bf16; lane l reads its A row (voxel l & 15) straight from the
+        //      t2 halo lines: 8 channels of one tap, 16 B in two dword pairs (lines are 4-B aligned)
+            const int lane = tid & 63, wave = tid >> 6;
+            const int ri = lane & 15, kb = lane >> 4, ts = kb >> 1, ch = (kb & 1) * 8;
+            const bf16_t *wf = reinterpret_cast<const bf16_t *>(w2s);
+            constexpr int NW = NTP / 64;
+            for (int t = (a.dbg & 2) ? NR / 2 : wave; t < NR / 2; t += NW) {
+                const int run_i = 2 * t + (ri >> 3), d_i = ri & 7;
+                const bf16_t *abase = t2h + ((run_i / BW) * HW + run_i % BW) * LSD + d_i * RS + ch;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int v = 0; v < BD; ++v)
-#pragma unroll
-            for (int o = 0; o < NG; ++o) acc[v][o] = 0.f;
-        // t2 channels read four at a time (two dwords per position: 30 LDS reads per (kh, kw)
-        // instead of 90); W2 is wave-uniform (the channel group is per wave) and read through the
-        // scalar cache straight from the fp32 weights, so phase B's LDS traffic is t2 only
-        const int grpu = __builtin_amdgcn_readfirstlane(grp);
-        const float *__restrict__ w2g = w2 + grpu * NG * BR * 27;  // o = grpu * 3 + j: + j * BR * 27
-        for (int kh = (a.dbg & 2) ? 3 : 0; kh < 3; ++kh)
-            for (int kw = 0; kw < 3; ++kw) {
-                const bf16_t *ln = t2h + ((lh + kh) * HW + lw + kw) * LSD;
-                const int tap0 = (kh * 3 + kw) * 3;
-#pragma unroll
-                for (int cg = 0; cg < (BR + 3) / 4; ++cg) {
-                    uint32_t raw[HD][2];
-#pragma unroll
-                    for (int q = 0; q < HD; ++q) {
-                        const uint32_t *p32 = reinterpret_cast<const uint32_t *>(ln + q * RS + 4 * cg);
-                        raw[q][0] = p32[0];
-                        raw[q][1] = 4 * cg + 2 < BR ? p32[1] : 0u;
+                for (int pr = 0; pr < NPAIR; ++pr) {
+                    constexpr auto toff = [](int tap) { return ((tap / 9) * HW + (tap / 3) % 3) * LSD + (tap % 3) * RS; };
+                    const int ta = 2 * pr, tb = 2 * pr + 1;
+                    const bool valid = ts == 0 || tb < 27;
+                    const uint32_t *ap = reinterpret_cast<const uint32_t *>(abase + (ts ? toff(tb < 27 ? tb : ta) : toff(ta)));
+                    uint32_t au[4] = {0u, 0u, 0u, 0u};
+                    if (valid) {
+                        au[0] = ap[0];
+                        au[1] = ap[1];
+                        au[2] = ap[2];
+                        au[3] = ap[3];
                     }
+                    bf16x8 af;
+                    __builtin_memcpy(&af, au, 16);
+                    const bf16x8 bfr = *reinterpret_cast<const bf16x8 *>(wf + (pr * 64 + lane) * 8);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc, 0, 0, 0);
+                }
+                const int o = lane & 15;
+                if (o < BR) {
 #pragma unroll
-                    for (int cc = 0; cc < 4; ++cc) {
-                        const int c = 4 * cg + cc;
-                        if (c >= BR) break;
-                        float tc[HD];  // channel c of the line's 10 positions
-#pragma unroll
-                        for (int q = 0; q < HD; ++q) {
-                            const uint32_t u = raw[q][cc >> 1];
-                            tc[q] = __uint_as_float((cc & 1) ? (u & 0xffff0000u) : (u << 16));
-                        }
-#pragma unroll
-                        for (int kd = 0; kd < 3; ++kd) {
-                            const float *wr = w2g + c * 27 + tap0 + kd;
-                            const float wv[NG] = {wr[0], wr[BR * 27], wr[2 * BR * 27]};
-#pragma unroll
-                            for (int v = 0; v < BD; ++v)
-#pragma unroll
-                                for (int o = 0; o < NG; ++o) acc[v][o] = fmaf(tc[v + kd], wv[o], acc[v][o]);
-                        }
+                    for (int j = 0; j < 4; ++j) {
+                        const int row = kb * 4 + j, r = 2 * t + (row >> 3), v = row & 7;
+                        t3s[r * BD * BR + v * BR + o] = bf16_t(f2bf(elu(acc[j] + b3a) + b3b));
                     }
                 }
             }
-#pragma unroll
-        for (int v = 0; v < BD; ++v)
-#pragma unroll
-            for (int o = 0; o < NG; ++o)
-                t3s[run * BD * BR + v * BR + grp * NG + o] = bf16_t(f2bf(elu(acc[v][o] + b3a) + b3b));
+        } else {
+            // ---- B. t3 channels grp*3 .. grp*3+2 for the thread's D-run (lh, lw, 0..7)
+            float acc[BD][NG];
+    #pragma unroll
+            for (int v = 0; v < BD; ++v)
+    #pragma unroll
+                for (int o = 0; o < NG; ++o) acc[v][o] = 0.f;
+            // t2 channels read four at a time (two dwords per position: 30 LDS reads per (kh, kw)
+            // instead of 90); W2 is wave-uniform (the channel group is per wave) and read through the
+            // scalar cache straight from the fp32 weights, so phase B's LDS traffic is t2 only
+            const int grpu = __builtin_amdgcn_readfirstlane(grp);
+            const float *__restrict__ w2g = w2 + grpu * NG * BR * 27;  // o = grpu * 3 + j: + j * BR * 27
+            for (int kh = (a.dbg & 2) ? 3 : 0; kh < 3; ++kh)
+                for (int kw = 0; kw < 3; ++kw) {
+                    const bf16_t *ln = t2h + ((lh + kh) * HW + lw + kw) * LSD;
+                    const int tap0 = (kh * 3 + kw) * 3;
+    #pragma unroll
+                    for (int cg = 0; cg < (BR + 3) / 4; ++cg) {
+                        uint32_t raw[HD][2];
+    #pragma unroll
+                        for (int q = 0; q < HD; ++q) {
+                            const uint32_t *p32 = reinterpret_cast<const uint32_t *>(ln + q * RS + 4 * cg);
+                            raw[q][0] = p32[0];
+                            raw[q][1] = 4 * cg + 2 < BR ? p32[1] : 0u;
+                        }
+    #pragma unroll
+                        for (int cc = 0; cc < 4; ++cc) {
+                            const int c = 4 * cg + cc;
+                            if (c >= BR) break;
+                            float tc[HD];  // channel c of the line's 10 positions
+    #pragma unroll
+                            for (int q = 0; q < HD; ++q) {
+                                const uint32_t u = raw[q][cc >> 1];
+                                tc[q] = __uint_as_float((cc & 1) ? (u & 0xffff0000u) : (u << 16));
+                            }
+    #pragma unroll
+                            for (int kd = 0; kd < 3; ++kd) {
+                                const float *wr = w2g + c * 27 + tap0 + kd;
+                                const float wv[NG] = {wr[0], wr[BR * 27], wr[2 * BR * 27]};
+    #pragma unroll
+                                for (int v = 0; v < BD; ++v)
+    #pragma unroll
+                                    for (int o = 0; o < NG; ++o) acc[v][o] = fmaf(tc[v + kd], wv[o], acc[v][o]);
+                            }
+                        }
+                    }
+                }
+    #pragma unroll
+            for (int v = 0; v < BD; ++v)
+    #pragma unroll
+                for (int o = 0; o < NG; ++o)
+                    t3s[run * BD * BR + v * BR + grp * NG + o] = bf16_t(f2bf(elu(acc[v][o] + b3a) + b3b));
+        }
         __syncthreads();
         // t3 and the brick's t2 rows to HBM in 16-B chunks, consecutive threads on consecutive
         // chunks of a D-run's 144 contiguous bytes (whole cache lines per wave store)
@@ -267,7 +326,7 @@ bool use_wide() {
     return v == 16;
 }
 
-template <class G>
+template <class G, bool MFB>
 void launch_mid(const MidArgs &a0, hipStream_t s, const bf16_t *x, const float *w1, const float *w2, const float *w3,
                 const vq3d_preact_params &p, bf16_t *out, bf16_t *t2, bf16_t *t3) {
     MidArgs a = a0;
@@ -277,12 +336,12 @@ void launch_mid(const MidArgs &a0, hipStream_t s, const bf16_t *x, const float *
     a.nbricks = a.B * a.nbh * a.nbw * a.nbd;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd<G>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd<G, MFB>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - 256));
         (void)hipGetLastError();
         attr = true;
     }
-    k_preact_mid_fwd<G><<<unsigned(a.nbricks), G::NTP, G::lds(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
+    k_preact_mid_fwd<G, MFB><<<unsigned(a.nbricks), G::NTP, G::lds(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
 }
 
 }  // namespace
@@ -316,10 +375,18 @@ int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     a.H = h;
     a.W = w;
     a.D = dd;
-    if (use_wide())
-        launch_mid<GeoWide>(a, s, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out, (bf16_t *)t2, (bf16_t *)t3);
-    else
-        launch_mid<GeoHalf>(a, s, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out, (bf16_t *)t2, (bf16_t *)t3);
+    static const bool mfb = [] {
+        const char *e = std::getenv("VQ3D_PM_MFMA");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    const bf16_t *xb = (const bf16_t *)x;
+    bf16_t *ob = (bf16_t *)out, *t2b = (bf16_t *)t2, *t3b = (bf16_t *)t3;
+    if (use_wide()) {
+        if (mfb) launch_mid<GeoWide, true>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);
+        else launch_mid<GeoWide, false>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);
+    } else {
+        launch_mid<GeoHalf, false>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);  // 10-wide rows: VALU phase B only
+    }
     return check_launch("preact_mid_fwd");
 }
 
