@@ -159,35 +159,48 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
             const int ri = lane & 15, kb = lane >> 4, ts = kb >> 1, ch = (kb & 1) * 8;
             const bf16_t *wf = reinterpret_cast<const bf16_t *>(w2s);
             constexpr int NW = NTP / 64;
-            for (int t = (a.dbg & 2) ? NR / 2 : wave; t < NR / 2; t += NW) {
-                const int run_i = 2 * t + (ri >> 3), d_i = ri & 7;
-                const bf16_t *abase = t2h + ((run_i / BW) * HW + run_i % BW) * LSD + d_i * RS + ch;
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            // two tiles per iteration share each B fragment read and overlap their dependent
+            // MFMA chains
+            static_assert(NR % 4 == 0, "tile pairs");
+            for (int tp = (a.dbg & 2) ? NR / 4 : wave; tp < NR / 4; tp += NW) {
+                const bf16_t *abase[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int run_i = 2 * (2 * tp + h) + (ri >> 3), d_i = ri & 7;
+                    abase[h] = t2h + ((run_i / BW) * HW + run_i % BW) * LSD + d_i * RS + ch;
+                }
+                f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
                 for (int pr = 0; pr < NPAIR; ++pr) {
                     constexpr auto toff = [](int tap) { return ((tap / 9) * HW + (tap / 3) % 3) * LSD + (tap % 3) * RS; };
                     const int ta = 2 * pr, tb = 2 * pr + 1;
                     const bool valid = ts == 0 || tb < 27;
-                    const uint32_t *ap = reinterpret_cast<const uint32_t *>(abase + (ts ? toff(tb < 27 ? tb : ta) : toff(ta)));
-                    uint32_t au[4] = {0u, 0u, 0u, 0u};
-                    if (valid) {
-                        au[0] = ap[0];
-                        au[1] = ap[1];
-                        au[2] = ap[2];
-                        au[3] = ap[3];
-                    }
-                    bf16x8 af;
-                    __builtin_memcpy(&af, au, 16);
+                    const int off = ts ? toff(tb < 27 ? tb : ta) : toff(ta);
                     const bf16x8 bfr = *reinterpret_cast<const bf16x8 *>(wf + (pr * 64 + lane) * 8);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc, 0, 0, 0);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t *ap = reinterpret_cast<const uint32_t *>(abase[h] + off);
+                        uint32_t au[4] = {0u, 0u, 0u, 0u};
+                        if (valid) {
+                            au[0] = ap[0];
+                            au[1] = ap[1];
+                            au[2] = ap[2];
+                            au[3] = ap[3];
+                        }
+                        bf16x8 af;
+                        __builtin_memcpy(&af, au, 16);
+                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[h], 0, 0, 0);
+                    }
                 }
                 const int o = lane & 15;
                 if (o < BR) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int row = kb * 4 + j, r = 2 * t + (row >> 3), v = row & 7;
-                        t3s[r * BD * BR + v * BR + o] = bf16_t(f2bf(elu(acc[j] + b3a) + b3b));
-                    }
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int row = kb * 4 + j, r = 2 * (2 * tp + h) + (row >> 3), v = row & 7;
+                            t3s[r * BD * BR + v * BR + o] = bf16_t(f2bf(elu(acc[h][j] + b3a) + b3b));
+                        }
                 }
             }
         } else {
