@@ -316,8 +316,19 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
         }
         sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
+    if constexpr (LANES > 64) {  // one entry per workgroup: waves, then the 4 wave sums in order
+        __shared__ float wsum[LANES / 64];
 #pragma unroll
-    for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = sum;
+        __syncthreads();
+        sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < LANES / 64; ++i) sum += wsum[i];
+    } else {
+#pragma unroll
+        for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    }
     float wg = 0.f, bs = 0.f;
     if (e < ne && lane == 0) {
         const int co = e / (Ct + 1), ci = e - co * (Ct + 1);
@@ -466,6 +477,7 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     const int Ct = a.Ca + a.Cb;
     int lanes = 1;
     while (lanes < 64 && lanes * 32 < nbx) lanes *= 2;
+    if (lanes == 64 && nbx > 1024) lanes = 256;  // a workgroup per entry: one round of 8 loads per thread
 #define RED(L)                                                                                                 \
     k_pw_wgrad_reduce<L><<<(a.ne + 256 / L - 1) / (256 / L), 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw,    \
                                                                           dscale, dbias, dcbias)
@@ -476,7 +488,8 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     case 8: RED(8); break;
     case 16: RED(16); break;
     case 32: RED(32); break;
-    default: RED(64); break;
+    case 64: RED(64); break;
+    default: RED(256); break;
     }
 #undef RED
     return check_launch("conv3d_bwd_weight(pointwise)");
