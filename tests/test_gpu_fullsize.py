@@ -1,0 +1,83 @@
+"""The headline configuration itself (BASELINE.json configs[2] per GPU: 3-layer published model,
+512 x 512 x 128, bf16) through size-independent properties, since the oracle cannot run a
+whole step at this size in seconds:
+
+* codebook search bit-exact at full size: every level's codes equal the C oracle's nearest
+  codeword (oracle/vq_nearest.c, pinned by the reference's KATs) for the very z the HIP encoder
+  produced (524,288 / 8,192 / 128 rows), and the commitment losses agree;
+* one training step (forward, loss, backward, Adam) leaves a finite loss, finite gradients
+  and finite parameters, and codes inside [0, K) with the reference's shapes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import vq_oracle
+
+pytestmark = pytest.mark.gpu
+
+PUB = dict(n_bottleneck_blocks=3, n_pre_quantization_blocks=50, n_post_quantization_blocks=50,
+           n_post_upscale_blocks=3, n_post_downscale_blocks=2, num_embeddings=[128, 256, 512])
+SHAPES = [(1, 128, 128, 32), (1, 32, 32, 8), (1, 8, 8, 2)]
+
+
+def _model(dev):
+    import vq3d
+    torch.manual_seed(0)
+    return vq3d.VQVAE(vq3d.default_args(compute_dtype="bf16", **PUB)).to(dev)
+
+
+def test_fullsize_codes_bitexact_vs_oracle(gpu):
+    from vq3d.extract import extract_samples
+    from vq3d.utils import synthetic_volume
+    m = _model(gpu)
+    zs = {}
+    hooks = [q.register_forward_pre_hook(lambda mod, inp, i=i: zs.__setitem__(i, inp[0].detach()))
+             for i, q in enumerate(m.encoder.quantize)]
+    losses = {}
+    m.eval()
+    x = synthetic_volume((1, 1, 512, 512, 128), 0).to(gpu)
+    with torch.no_grad():
+        for lvl, (c, _, _) in enumerate(m.encode(x)):
+            losses[lvl] = float(c)
+    idxs = next(extract_samples(m, [x]))
+    for h in hooks:
+        h.remove()
+    for lvl, q in enumerate(m.encoder.quantize):
+        ix = idxs[lvl]
+        assert tuple(ix.shape) == SHAPES[lvl] and ix.dtype == torch.int64
+        z = zs[lvl].float().permute(0, 2, 3, 4, 1).reshape(-1, q.embedding_dim).cpu().numpy()
+        ref_idx, _, sq = vq_oracle.nearest(z, q.embed.cpu().numpy())
+        assert np.array_equal(ix.reshape(-1).cpu().numpy(), ref_idx), lvl
+        ref_loss = q.commitment_cost * sq / z.size
+        assert abs(losses[lvl] - ref_loss) <= 1e-4 * abs(ref_loss) + 1e-12, (lvl, losses[lvl], ref_loss)
+
+
+def test_fullsize_train_step_finite(gpu):
+    from vq3d.utils import synthetic_volume
+    m = _model(gpu)
+    opt = m.configure_optimizers()
+    x = synthetic_volume((1, 1, 512, 512, 128), 0).to(gpu)
+    nvs = torch.tensor([128], device=gpu)
+    m.train()
+    cap = {}
+    fwd = m.forward
+
+    def capture(data):
+        cap["r"] = fwd(data)
+        return cap["r"]
+    m.forward = capture
+    loss = m.training_step((x, nvs), 0)
+    del m.forward
+    loss.backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(loss))
+    assert torch.isfinite(m.flat.grad).all() and float(m.flat.grad.abs().max()) > 0
+    assert torch.isfinite(m.flat.data).all()
+    _, (_, _, idxs) = cap["r"]
+    for lvl, (ix, k) in enumerate(zip(idxs, PUB["num_embeddings"])):
+        assert tuple(ix.shape) == SHAPES[lvl]
+        assert int(ix.min()) >= 0 and int(ix.max()) < k
+    for q in m.encoder.quantize:  # first pass done: codebook initialised from the data statistics
+        assert int(q.first_pass) == 0 and torch.isfinite(q.embed).all()
