@@ -33,115 +33,7 @@
 namespace vq3d {
 
 // ============================================================================ pointwise
-constexpr int kPwSeg = 256;        // voxels per segment (one thread each)
 constexpr int kMaxBlocksX = 2048;  // grid-stride cap (bounds the per-block scalar atomics)
-
-// contiguous global <-> LDS copy by the workgroup, 16-byte vectors when `vec` (both ends aligned)
-template <typename T>
-__device__ __forceinline__ void slab_copy(T *__restrict__ dst, const T *__restrict__ src, int n, bool vec) {
-    constexpr int E = 16 / sizeof(T);
-    int i0 = 0;
-    if (vec) {
-        const int nv = n / E;
-        for (int i = threadIdx.x; i < nv; i += 256)
-            reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
-        i0 = nv * E;
-    }
-    for (int i = i0 + threadIdx.x; i < n; i += 256) dst[i] = src[i];
-}
-
-// DGRAD = false: y[v, o] = epi( sum_i W[o][i] * pro(x[v, i]) )          (i over Cin + Cin2)
-// DGRAD = true : gx[v, i] = bwd_epi( gscale * sum_o W[o][i] * g[v, o] ) (o over Cout)
-// A segment of (up to) 256 voxels is one contiguous slab per tensor: it is staged into LDS with 16-byte
-// loads, each thread computes one voxel (weights of the COT-channel tile broadcast from LDS,
-// loaded once per workgroup), and when the tile holds every output channel (`slab`), results
-// leave through an LDS slab with 16-byte stores.
-template <typename T, int COT, bool DGRAD>
-__global__ __launch_bounds__(256) void k_pw(ConvArgs a, const T *__restrict__ in, const T *__restrict__ in2,
-                                           const float *__restrict__ w, FwdEpi<T> fe, BwdEpi<T> be,
-                                           const float *__restrict__ gscale, T *__restrict__ out,
-                                           T *__restrict__ out2, float *dpre, float *dpost, int slab, int vec,
-                                           int seg_len) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float red[8];
-    const int Ct = a.Cin + a.Cin2;
-    const int nA = DGRAD ? a.Cout : a.Cin;  // input slabs: A [256][nA] (+ B [256][nB] forward dual input)
-    const int nB = DGRAD ? 0 : a.Cin2;
-    const int nin = nA + nB;
-    const int oA = DGRAD ? a.Cin : a.Cout;  // output slabs (slab mode): A [256][oA] (+ B [256][oB])
-    const int oB = DGRAD ? a.Cin2 : 0;
-    const int64_t nvox = int64_t(a.B) * a.oH * a.oW * a.oD;
-    const int64_t nseg = (nvox + seg_len - 1) / seg_len;
-    const int o0 = blockIdx.y * COT;
-    float *ws = reinterpret_cast<float *>(smem);  // [nin][COT]
-    T *sA = reinterpret_cast<T *>(smem + ((size_t(nin) * COT * 4 + 15) & ~size_t(15)));
-    T *sB = sA + seg_len * nA;
-    T *rA = sB + seg_len * nB;
-    T *rB = rA + seg_len * oA;
-    const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
-    const ActDeriv dv = make_deriv(be);
-    const float gs = gscale ? *gscale : 1.f;
-    const int tid = threadIdx.x;
-    float pre = 0.f, post = 0.f;
-
-    for (int e = tid; e < nin * COT; e += 256) {
-        const int c = e / COT, j = e - c * COT;
-        const int oc = o0 + j;
-        float wv = 0.f;
-        if (DGRAD) wv = oc < Ct ? w[int64_t(c) * Ct + oc] : 0.f;
-        else wv = oc < a.Cout ? w[int64_t(oc) * Ct + c] : 0.f;
-        ws[e] = wv;
-    }
-    for (int64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        const int64_t v0 = seg * seg_len;
-        const int nv = int(min<int64_t>(seg_len, nvox - v0));
-        __syncthreads();
-        slab_copy(sA, in + v0 * nA, nv * nA, vec);
-        if (nB) slab_copy(sB, in2 + v0 * nB, nv * nB, vec);
-        __syncthreads();
-        if (tid < nv) {
-            float acc[COT];
-#pragma unroll
-            for (int j = 0; j < COT; ++j) acc[j] = 0.f;
-            const T *xr = sA + tid * nA;
-            for (int c = 0; c < nA; ++c) {
-                float xv = ld(xr + c);
-                if (!DGRAD) xv = pro.apply(xv);
-                const float *wr = ws + c * COT;
-#pragma unroll
-                for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, wr[j], acc[j]);
-            }
-            const T *xr2 = sB + tid * nB;
-            for (int c = 0; c < nB; ++c) {
-                const float xv = pro.apply(ld(xr2 + c));
-                const float *wr = ws + (nA + c) * COT;
-#pragma unroll
-                for (int j = 0; j < COT; ++j) acc[j] = fmaf(xv, wr[j], acc[j]);
-            }
-            const int64_t v = v0 + tid;
-            if (!DGRAD) {
-                fwd_epilogue<T, COT>(a, fe, acc, v, o0, slab ? rA + tid * oA : out + v * a.Cout);
-            } else {
-                T *ra = slab ? rA + tid * oA : out + v * a.Cin;
-                T *rb = slab ? rB + tid * oB : (out2 ? out2 + v * a.Cin2 : nullptr);
-                bwd_epilogue<T, COT>(a, be, dv, gs, gscale != nullptr, acc, v, o0, ra, rb, pre, post);
-            }
-        }
-        if (slab) {
-            __syncthreads();
-            slab_copy(out + v0 * oA, rA, nv * oA, vec);
-            if (oB) slab_copy(out2 + v0 * oB, rB, nv * oB, vec);
-        }
-    }
-    if (DGRAD && (dpre || dpost)) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
-        if (tid == 0) {
-            atomic_add_f(dpre, pre);
-            atomic_add_f(dpost, post);
-        }
-    }
-}
 
 // ============================================================================ forward, k > 1
 // thread = one output voxel x COT channels (grid-stride over voxel blocks of 256)
@@ -491,55 +383,11 @@ static BwdEpi<T> make_bwd_epi(const vq3d_dgrad_epilogue *epi, int pro_kind, cons
     return e;
 }
 
-// VQ3D_LEGACY_PW=1 selects the LDS-slab pointwise kernel (k_pw) instead of pw_conv.hip
-static bool legacy_pw() {
-    static const bool on = [] {
-        const char *e = std::getenv("VQ3D_LEGACY_PW");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <typename T, bool DGRAD>
-static int launch_pw(const vq3d_conv_desc *d, const ConvArgs &a, const void *in, const void *in2, const float *w,
-                     const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale, void *out, void *out2,
-                     float *dpre, float *dpost, hipStream_t s) {
-    const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
-    const int Ct = d->cin + d->cin2;
-    const int nout = DGRAD ? Ct : d->cout;
-    const int nA = DGRAD ? d->cout : d->cin, nB = DGRAD ? 0 : d->cin2;
-    const int cot = nout <= 1 ? 1 : nout <= 2 ? 2 : nout <= 4 ? 4 : nout <= 8 ? 8 : nout <= 12 ? 12 : 16;
-    const int ychunks = (nout + cot - 1) / cot;
-    const int slab = ychunks == 1 ? 1 : 0;
-    const int vec = al16(in) && (!in2 || al16(in2)) && al16(out) && (!out2 || al16(out2));
-    const size_t ws = (size_t(nA + nB) * cot * 4 + 15) & ~size_t(15);
-    // segment of `seg` voxels (one per thread; shorter when the slabs would not fit 64 KB of LDS)
-    int seg = kPwSeg;
-    auto lds_of = [&](int sl) { return ws + size_t(sl) * (nA + nB + (slab ? nout : 0)) * sizeof(T); };
-    while (seg > 16 && lds_of(seg) > 64 * 1024) seg /= 2;
-    const size_t lds = lds_of(seg);
-    if (lds > 64 * 1024) return fail("conv: pointwise channel count too large");
-    dim3 grid(blocks_x((nvox + seg - 1) / seg), unsigned(ychunks));
-#define L(C)                                                                                                  \
-    case C:                                                                                                   \
-        k_pw<T, C, DGRAD><<<grid, 256, lds, s>>>(a, (const T *)in, (const T *)in2, w, fe, be, gscale, (T *)out, \
-                                                 (T *)out2, dpre, dpost, slab, vec, seg);                     \
-        break;
-    switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
-#undef L
-    return check_launch(DGRAD ? "conv3d_bwd_data(pointwise)" : "conv3d_fwd(pointwise)");
-}
-
-// small grids with many channels: reduction split over workgroups (conv_small.hip);
-// VQ3D_NO_SMALL=1 disables it (A/B measurements)
+// small grids with many channels: reduction split over workgroups (conv_small.hip)
 static bool use_small(const vq3d_conv_desc *d, bool dgrad) {
-    static const bool off = [] {
-        const char *e = std::getenv("VQ3D_NO_SMALL");
-        return e && e[0] == '1';
-    }();
-    if (off || !small_applicable(d, dgrad)) return false;
+    if (!small_applicable(d, dgrad)) return false;
     // measured: 9-20x faster than the lines / VALU engines at 128 voxels (8x8x2, 128 channels);
     // from 1024 voxels on only where the lines engine cannot take the shape
     const int64_t nv = dgrad ? int64_t(d->batch) * d->in_h * d->in_w * d->in_d
@@ -561,8 +409,8 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
     if (fe.act == VQ3D_ACT_ELU_AFFINE && (!fe.act_a || !fe.act_b)) return fail("conv: ELU_AFFINE needs act_a/b");
     if (is_pointwise(d)) {
         BwdEpi<T> be = {};
-        if (!legacy_pw()) return launch_pw1<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes, s);
-        return launch_pw<T, false>(d, a, x, x2, w, fe, be, nullptr, y, nullptr, nullptr, nullptr, s);
+        return launch_pw1<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes,
+                             s);
     }
     if (tc_applicable(d) && !(fe.res && fe.res_up2)) {
         BwdEpi<T> be = {};
@@ -579,7 +427,7 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
             return launch_lines(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws,
                                 ws_bytes, s);
         }
-        if (!mfma_disabled()) {
+        {
             MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
                                 d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR);
             if (m.ok) {
@@ -619,8 +467,8 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
     BwdEpi<T> be = make_bwd_epi<T>(epi, d->pro_kind, pa);
     if (is_pointwise(d)) {
         FwdEpi<T> fe = {};
-        if (!legacy_pw()) return launch_pw1<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes, s);
-        return launch_pw<T, true>(d, a, g, nullptr, w, fe, be, gscale, gx, gx2, dpre, dpost, s);
+        return launch_pw1<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes,
+                             s);
     }
     if (tc_applicable(d)) {
         FwdEpi<T> fe = {};
@@ -638,7 +486,7 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
             return launch_lines(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws,
                                 ws_bytes, s);
         }
-        if (!mfma_disabled() && d->stride == 1) {
+        if (d->stride == 1) {
             const int pp = d->kernel - 1 - d->pad;
             MPlan m = plan_mfma(d->batch, d->cout, 0, Ct, d->out_h, d->out_w, d->out_d, d->in_h, d->in_w, d->in_d,
                                 d->kernel, 1, pp, d->pad_mode == VQ3D_PAD_CIRCULAR);
@@ -673,25 +521,10 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
 // faster (9 -> 9 at 128^2 x 32 on par, 4 -> 4 at 256^2 x 64 1.9x).
 static bool use_lines_wgrad(const vq3d_conv_desc *d) {
     if (d->dtype != VQ3D_BF16 || !lines_wgrad_applicable(d)) return false;
-    static const int force = [] {
-        const char *e = std::getenv("VQ3D_LINES_WGRAD");
-        return e ? (e[0] == '1' ? 1 : 0) : 2;
-    }();
-    if (force != 2) return force == 1;
-    if (d->cin + d->cin2 >= 32 || mfma_disabled()) return true;
+    if (d->cin + d->cin2 >= 32) return true;
     return !plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
                       d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)
                 .ok;
-}
-
-// 1x1x1 weight gradient on the lines MFMA engine (k = 1) instead of the VALU slab kernel:
-// VQ3D_PW_LINES_WGRAD=1 (A/B runs)
-static bool use_lines_pw_wgrad(const vq3d_conv_desc *d) {
-    static const int mode = [] {
-        const char *e = std::getenv("VQ3D_PW_LINES_WGRAD");
-        return e ? (e[0] == '1' ? 1 : 0) : 0;
-    }();
-    return mode == 1 && lines_wgrad_applicable(d);
 }
 
 template <typename T>
@@ -703,8 +536,6 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     const int K3 = d->kernel * d->kernel * d->kernel;
     const int Kt = Ct * K3;
     if (is_pointwise(d)) {
-        if (use_lines_pw_wgrad(d))
-            return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
         return launch_pw_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
     }
     if (tc_applicable(d))
@@ -712,7 +543,7 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     if constexpr (std::is_same<T, bf16_t>::value) {
         if (use_lines_wgrad(d))
             return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
-        if (!mfma_disabled()) {
+        {
             MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
                                 d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true);
             if (m.ok) {
@@ -801,7 +632,7 @@ size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
         return small_workspace(d, pass == VQ3D_PASS_BWD_DATA);
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
     if (pass == VQ3D_PASS_BWD_DATA) return is_pointwise(d) ? pw_dgrad_workspace(d) : lines_workspace(d, true);
-    if (is_pointwise(d)) return use_lines_pw_wgrad(d) ? lines_wgrad_workspace(d) : pw_wgrad_workspace(d);
+    if (is_pointwise(d)) return pw_wgrad_workspace(d);
     return use_lines_wgrad(d) ? lines_wgrad_workspace(d) : 0;
 }
 

@@ -56,7 +56,6 @@ struct LArgs {
     int vec_out;               // 16-B epilogue path allowed (one N group, bd*N % 8 == 0, no y2 / res_up2)
     int region_lines;          // bytes of the lines region (weights follow)
     int cin_split;             // dgrad: output channels < cin_split go to y, the rest to y2
-    int dbg;                   // profiling only (VQ3D_LINES_DBG): 1 skip staging, 2 skip MFMA, 4 skip stores
 };
 
 __device__ __forceinline__ int wrapc(int i, int n) {
@@ -248,7 +247,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
         // are contiguous and 16-B aligned in HBM and land 16-B aligned in LDS (pad0), copied in
         // units of mvec elements; the p + (k - 1 - p) edge positions (wrap / zero padding) go
         // element-group wise.  Otherwise every position takes the generic unit path.
-        if (!(a.dbg & 1)) {
+        {
             const int64_t bbase = int64_t(b) * a.iH * a.iW * a.iD;
             auto line_src = [&](int li, int id, bool &ok) -> int64_t {
                 const int lh_ = int(a.fhw.div(uint32_t(li))), lw_ = li - lh_ * a.hw;
@@ -324,7 +323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
         for (int m = 0; m < MTW; ++m)
 #pragma unroll
             for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int ks = 0; ks < ((a.dbg & 2) ? 0 : a.nks); ++ks) {
+        for (int ks = 0; ks < a.nks; ++ks) {
             const int c = ks * 4 + kq;
             const int off = ctab[c];
             bf16x8 bfr[NT];
@@ -357,7 +356,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
             }
         }
         __syncthreads();
-        if (a.dbg & 4) continue;
 
         // ---- epilogue over the tile.  Vector path: the brick is inside the grid, the group
         // holds every output channel, so the tile [v][N] is bh*bw contiguous runs of bd*N
@@ -638,16 +636,8 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
     return P;
 }
 
-bool disabled() {
-    static const bool off = [] {
-        const char *e = std::getenv("VQ3D_DISABLE_LINES");
-        return e && e[0] == '1';
-    }();
-    return off;
-}
-
 Plan plan_for(const vq3d_conv_desc *d, bool dgrad) {
-    if (d->dtype != VQ3D_BF16 || disabled() || d->kernel < 2) return Plan{};
+    if (d->dtype != VQ3D_BF16 || d->kernel < 2) return Plan{};
     const int circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
     if (!dgrad)
         return plan(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
@@ -749,20 +739,11 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
     } else {
         P.a.vec_out = P.a.vec_out && !fe.res_up2 && al(y) && (!fe.res || al(fe.res));
     }
-    static const int dbg = [] {
-        const char *e = std::getenv("VQ3D_LINES_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
-    P.a.dbg = dbg;
     const int wCt = d->cin + d->cin2;
     // pre-pack the weights once per call when the caller gave room (else each workgroup packs)
     const uint4 *wpk = nullptr;
     const int items_per_wg = P.a.nks * 4 * P.a.ntn;
-    static const int prepack = [] {  // VQ3D_LINES_PREPACK=1 / 0: always / never pre-pack (A/B runs)
-        const char *e = std::getenv("VQ3D_LINES_PREPACK");
-        return e ? (e[0] == '1' ? 1 : 0) : 2;
-    }();
-    const bool want_pack = prepack == 2 ? items_per_wg > 2048 : prepack == 1;
+    const bool want_pack = items_per_wg > 2048;
     if (want_pack && ws && ws_bytes >= ws_of(P)) {  // small images are packed in-kernel
         const int items = P.a.nks * 4 * P.a.ntn;
         const dim3 pg{unsigned((items + 255) / 256), unsigned(P.a.ntg), 1u};

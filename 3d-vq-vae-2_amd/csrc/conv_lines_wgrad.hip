@@ -73,7 +73,6 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                                                     const bf16_t *__restrict__ x2, const bf16_t *__restrict__ g,
                                                     float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ float red[8];
     const int nlines = a.hh * a.hw;
     bf16_t *lines = reinterpret_cast<bf16_t *>(smem);                             // [nlines][LS]
     bf16_t *gt = lines + ((nlines * a.LS + 7) / 8) * 8;                           // [nvp][GS]
@@ -459,17 +458,10 @@ size_t lines_wgrad_workspace(const vq3d_conv_desc *d) {
 
 namespace {
 
-bool wdisabled() {
-    static const bool off = [] {
-        const char *e = std::getenv("VQ3D_DISABLE_LINES_WGRAD");
-        return e && e[0] == '1';
-    }();
-    return off;
-}
 
 }  // namespace
 
-bool lines_wgrad_applicable(const vq3d_conv_desc *d) { return !wdisabled() && plan_w(d).ok; }
+bool lines_wgrad_applicable(const vq3d_conv_desc *d) { return plan_w(d).ok; }
 
 int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pa,
                        const float *pb, const float *w, const float *escale, float *dw, float *dscale, float *dbias,

@@ -428,11 +428,6 @@ unsigned grid_tc(const TcArgs &a) { return unsigned(std::min(a.nbricks, kTcBlock
 }  // namespace
 
 bool tc_applicable(const vq3d_conv_desc *d) {
-    static const bool off = [] {
-        const char *e = std::getenv("VQ3D_NO_TC");
-        return e && e[0] == '1';
-    }();
-    if (off) return false;
     // measured: 1 -> 1 3x faster, 2 -> 2 1.2-2x faster than the MFMA engines; 4 -> 4 is slower
     // (27 x 16 wave-uniform weights per voxel group), so it stays on the MFMA engines
     return d->kernel == 3 && d->stride == 1 && d->pad == 1 && d->cin2 == 0 && pow124(d->cin) && pow124(d->cout) &&

@@ -56,12 +56,11 @@ constexpr int NPAIR = 14;  // MFMA k-steps of phase B: 27 taps in pairs x 16 (pa
 struct MidArgs {
     int B, H, W, D;
     int nbh, nbw, nbd, nbricks;
-    int dbg;  // timing experiments only (VQ3D_PM_DBG): bit 0 skips phase A, 1 phase B, 2 phase C's math
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
-template <class G, bool MFB>
+template <class G>
 __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t *__restrict__ x,
                                                        const float *__restrict__ w1, const float *__restrict__ w2,
                                                        const float *__restrict__ w3, vq3d_preact_params p,
@@ -76,7 +75,7 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
     bf16_t *t2h = reinterpret_cast<bf16_t *>(w3s + C * WS);            // [HH * HW lines][LSD]
     bf16_t *t3s = t2h + G::T2HA + 8;                             // [NR][BD * BR]
     const int tid = threadIdx.x;
-    if constexpr (MFB) {
+    {
         // phase-B MFMA B fragments, bf16: [pair][lane][8], lane l holds B[k = 8 (l >> 4) + j][n = l & 15]
         // with k = 16 * (tap - 2 pair) + c (c < 16 padded, tap < 27), n = output channel (< 9)
         bf16_t *wf = reinterpret_cast<bf16_t *>(w2s);
@@ -84,11 +83,6 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
             const int j = i & 7, l = (i >> 3) & 63, pr = i >> 9;
             const int k = 8 * (l >> 4) + j, n = l & 15, c = k & 15, tap = 2 * pr + (k >> 4);
             wf[i] = bf16_t(f2bf(n < BR && c < BR && tap < 27 ? w2[(n * BR + c) * 27 + tap] : 0.f));
-        }
-    } else {
-        for (int i = tid; i < 27 * BR * WS; i += NTP) {
-            const int o = i % WS, r = i / WS, c = r % BR, tap = r / BR;
-            w2s[i] = o < BR ? w2[(o * BR + c) * 27 + tap] : 0.f;
         }
     }
     for (int i = tid; i < C * WS; i += NTP) {
@@ -99,7 +93,7 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
     const float b1a = *p.bias1a, b1b = *p.bias1b, b2a = *p.bias2a, b2b = *p.bias2b;
     const float b3a = *p.bias3a, b3b = *p.bias3b, sc = *p.scale, b4 = *p.bias4;
     const int run = tid % NR, grp = tid / NR;  // D-run (lh, lw) and channel group (wave-uniform)
-    const int lh = run / BW, lw = run % BW;
+
 
     for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
         int bi = brick;
@@ -112,7 +106,7 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
         const int oh0 = bzh * BH, ow0 = bzw * BW, od0 = bzd * BD;
         __syncthreads();
         // ---- A. t2 on the halo
-        for (int q = (a.dbg & 1) ? HP : tid; q < HP; q += NTP) {
+        for (int q = tid; q < HP; q += NTP) {
             asm volatile("" ::: "memory");  // keep the W1 rows as per-iteration LDS reads (no hoisting)
             const int dd = q % HD, line = q / HD, ww = line % HW, hh = line / HW;
             const int gh = wrapm(oh0 - 1 + hh, a.H), gw = wrapm(ow0 - 1 + ww, a.W), gd = wrapm(od0 - 1 + dd, a.D);
@@ -149,8 +143,8 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
             }
         }
         __syncthreads();
-        static_assert(!MFB || G::RS == 16, "MFMA phase B reads 8-channel halves of 16-wide rows");
-        if constexpr (MFB) {
+        static_assert(G::RS == 16, "MFMA phase B reads 8-channel halves of 16-wide rows");
+        {
         // ---- B (matrix cores). t3 = W2 (*) t2 as 16-voxel x 16-channel tiles (two D-runs of 8
         //      voxels; 9 of 16 output columns valid), K = 27 taps x 16 channels in 14 steps of
         //      v_mfma_f32_16x16x32_bf16; lane l reads its A row (voxel l & 15) straight from the
@@ -162,7 +156,7 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
             // two tiles per iteration share each B fragment read and overlap their dependent
             // MFMA chains
             static_assert(NR % 4 == 0, "tile pairs");
-            for (int tp = (a.dbg & 2) ? NR / 4 : wave; tp < NR / 4; tp += NW) {
+            for (int tp = wave; tp < NR / 4; tp += NW) {
                 const bf16_t *abase[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -203,58 +197,6 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
                         }
                 }
             }
-        } else {
-            // ---- B. t3 channels grp*3 .. grp*3+2 for the thread's D-run (lh, lw, 0..7)
-            float acc[BD][NG];
-    #pragma unroll
-            for (int v = 0; v < BD; ++v)
-    #pragma unroll
-                for (int o = 0; o < NG; ++o) acc[v][o] = 0.f;
-            // t2 channels read four at a time (two dwords per position: 30 LDS reads per (kh, kw)
-            // instead of 90); W2 is wave-uniform (the channel group is per wave) and read through the
-            // scalar cache straight from the fp32 weights, so phase B's LDS traffic is t2 only
-            const int grpu = __builtin_amdgcn_readfirstlane(grp);
-            const float *__restrict__ w2g = w2 + grpu * NG * BR * 27;  // o = grpu * 3 + j: + j * BR * 27
-            for (int kh = (a.dbg & 2) ? 3 : 0; kh < 3; ++kh)
-                for (int kw = 0; kw < 3; ++kw) {
-                    const bf16_t *ln = t2h + ((lh + kh) * HW + lw + kw) * LSD;
-                    const int tap0 = (kh * 3 + kw) * 3;
-    #pragma unroll
-                    for (int cg = 0; cg < (BR + 3) / 4; ++cg) {
-                        uint32_t raw[HD][2];
-    #pragma unroll
-                        for (int q = 0; q < HD; ++q) {
-                            const uint32_t *p32 = reinterpret_cast<const uint32_t *>(ln + q * RS + 4 * cg);
-                            raw[q][0] = p32[0];
-                            raw[q][1] = 4 * cg + 2 < BR ? p32[1] : 0u;
-                        }
-    #pragma unroll
-                        for (int cc = 0; cc < 4; ++cc) {
-                            const int c = 4 * cg + cc;
-                            if (c >= BR) break;
-                            float tc[HD];  // channel c of the line's 10 positions
-    #pragma unroll
-                            for (int q = 0; q < HD; ++q) {
-                                const uint32_t u = raw[q][cc >> 1];
-                                tc[q] = __uint_as_float((cc & 1) ? (u & 0xffff0000u) : (u << 16));
-                            }
-    #pragma unroll
-                            for (int kd = 0; kd < 3; ++kd) {
-                                const float *wr = w2g + c * 27 + tap0 + kd;
-                                const float wv[NG] = {wr[0], wr[BR * 27], wr[2 * BR * 27]};
-    #pragma unroll
-                                for (int v = 0; v < BD; ++v)
-    #pragma unroll
-                                    for (int o = 0; o < NG; ++o) acc[v][o] = fmaf(tc[v + kd], wv[o], acc[v][o]);
-                            }
-                        }
-                    }
-                }
-    #pragma unroll
-            for (int v = 0; v < BD; ++v)
-    #pragma unroll
-                for (int o = 0; o < NG; ++o)
-                    t3s[run * BD * BR + v * BR + grp * NG + o] = bf16_t(f2bf(elu(acc[v][o] + b3a) + b3b));
         }
         __syncthreads();
         // t3 and the brick's t2 rows to HBM in 16-B chunks, consecutive threads on consecutive
@@ -291,7 +233,7 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
         {
             const bf16_t *t3r = t3s + run * BD * BR;
             constexpr int CG = C / NG;  // 6 output channels per group
-            for (int v = (a.dbg & 4) ? BD : 0; v < BD; ++v) {
+            for (int v = 0; v < BD; ++v) {
                 asm volatile("" ::: "memory");  // W3 rows re-read from LDS per voxel (no hoisting)
                 float t3v[BR];
 #pragma unroll
@@ -328,18 +270,7 @@ __global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16
 }
 
 using GeoWide = Geo<16, 16, 16>;  // 256 bricks at 128 x 128 x 32
-using GeoHalf = Geo<8, 16, 10>;   // 512 bricks, two workgroups per CU
-
-// VQ3D_PM_BRICK=8 selects the 8 x 16 brick (A/B switch; measured slower); default 16 x 16
-bool use_wide() {
-    static const int v = [] {
-        const char *e = std::getenv("VQ3D_PM_BRICK");
-        return e ? std::atoi(e) : 16;
-    }();
-    return v == 16;
-}
-
-template <class G, bool MFB>
+template <class G>
 void launch_mid(const MidArgs &a0, hipStream_t s, const bf16_t *x, const float *w1, const float *w2, const float *w3,
                 const vq3d_preact_params &p, bf16_t *out, bf16_t *t2, bf16_t *t3) {
     MidArgs a = a0;
@@ -349,12 +280,12 @@ void launch_mid(const MidArgs &a0, hipStream_t s, const bf16_t *x, const float *
     a.nbricks = a.B * a.nbh * a.nbw * a.nbd;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd<G, MFB>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd<G>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - 256));
         (void)hipGetLastError();
         attr = true;
     }
-    k_preact_mid_fwd<G, MFB><<<unsigned(a.nbricks), G::NTP, G::lds(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
+    k_preact_mid_fwd<G><<<unsigned(a.nbricks), G::NTP, G::lds(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
 }
 
 }  // namespace
@@ -379,27 +310,13 @@ int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_mid_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     MidArgs a;
-    static const int dbg = [] {
-        const char *e = std::getenv("VQ3D_PM_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
-    a.dbg = dbg;
     a.B = batch;
     a.H = h;
     a.W = w;
     a.D = dd;
-    static const bool mfb = [] {
-        const char *e = std::getenv("VQ3D_PM_MFMA");
-        return e ? std::atoi(e) != 0 : true;
-    }();
     const bf16_t *xb = (const bf16_t *)x;
     bf16_t *ob = (bf16_t *)out, *t2b = (bf16_t *)t2, *t3b = (bf16_t *)t3;
-    if (use_wide()) {
-        if (mfb) launch_mid<GeoWide, true>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);
-        else launch_mid<GeoWide, false>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);
-    } else {
-        launch_mid<GeoHalf, false>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);  // 10-wide rows: VALU phase B only
-    }
+    launch_mid<GeoWide>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);
     return check_launch("preact_mid_fwd");
 }
 

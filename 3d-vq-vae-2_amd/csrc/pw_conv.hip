@@ -543,15 +543,6 @@ bool rows_path(const vq3d_conv_desc *d, bool dgrad, const void *res_up2_flag) {
 }  // namespace
 
 
-// scalar-weight kernel choice: VQ3D_PW_SG=0 never, =1 always, unset: grids up to 64K voxels
-static int sg_mode() {
-    static const int m = [] {
-        const char *e = std::getenv("VQ3D_PW_SG");
-        return e ? (e[0] == '1' ? 1 : 0) : 2;
-    }();
-    return m;
-}
-
 template <typename T>
 static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w,
                  const float *pa, const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale,
@@ -619,7 +610,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool want_part = dgrad && (dpre || dpost);
     // ---- mid-size grids: scalar-cache weights, one thread per (voxel, output group)
-    if (sg_mode() == 1 || (sg_mode() == 2 && nvox <= 65536))
+    if (nvox <= 65536)
         return launch_pw_sg<T>(d, dgrad, in, in2, w, pa, pb, fe, be, gscale, out, out2, dpre, dpost, ws, ws_bytes, s);
     // ---- few-channel rows: no LDS staging
     if (rows_path(d, dgrad, fe.res_up2 ? fe.res : nullptr) && al(in) && al(out) && al(fe.res) && al(be.aux) && al(be.addend)) {
@@ -698,10 +689,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     if (lds > 150 * 1024) return fail("conv(pointwise): too many channels for the LDS slabs");
     a.vec = al(in) && al(in2) && al(out) && al(out2) && al(be.aux) && al(be.addend) && al(fe.res);
     const int64_t nseg = (a.nvox + a.segv - 1) / a.segv;
-    static const int slab_cap = [] {  // VQ3D_PW_SLAB_BLOCKS: workgroup cap of the slab kernel (A/B runs)
-        const char *e = std::getenv("VQ3D_PW_SLAB_BLOCKS");
-        return e ? std::max(1, std::min(kMaxPwBlocks, std::atoi(e))) : 1024;  // measured: 1024 >= 2048 > 512
-    }();
+    const int slab_cap = std::min(kMaxPwBlocks, 1024);  // measured: 1024 >= 2048 > 512 workgroups
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, slab_cap)));
     float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
 #define L(C)                                                                                                    \

@@ -353,20 +353,8 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
-// the 9 <-> 18 channel convs of the 128^2 x 32 level on the register path (one voxel per
-// thread-iteration, 180 accumulators): VQ3D_PWW_WIDE=1 only -- measured 1.25x slower than the
-// slab kernel (52 vs 42 us at 128^2 x 32)
-bool wide_reg(const vq3d_conv_desc *d) {
-    return d->cin2 == 0 && ((d->cin == 9 && d->cout == 18) || (d->cin == 18 && d->cout == 9));
-}
-
 bool reg_path(const vq3d_conv_desc *d) {
-    static const bool wide = [] {
-        const char *e = std::getenv("VQ3D_PWW_WIDE");
-        return e && e[0] == '1';
-    }();
     auto p2 = [](int c) { return c == 1 || c == 2 || c == 4 || c == 8; };
-    if (wide && wide_reg(d)) return true;
     return d->cin2 == 0 && p2(d->cin) && p2(d->cout) && d->cout * (d->cin + 1) <= 40;
 }
 
@@ -398,11 +386,6 @@ PwwArgs plan(const vq3d_conv_desc *d, int &ytiles, int &nbx, size_t &lds) {
     nbx = int(std::max<int64_t>(1, std::min<int64_t>(nseg, std::max(1, kMaxBlocks / ytiles))));
     // mid-size grids: few workgroups striding over the segments, so the partials go straight
     // into the gradients (direct mode) instead of through a second reduction launch
-    static const int mid_cap = [] {
-        const char *e = std::getenv("VQ3D_PWW_MID_NBX");
-        return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    if (mid_cap > 0 && a.nvox <= 65536) nbx = std::min(nbx, mid_cap);
     if (reg_path(d)) {  // 4 x 256 voxels per workgroup-iteration (wide rows: ~4 voxels per thread)
         ytiles = 1;
         nbx = int(std::max<int64_t>(1, std::min<int64_t>((a.nvox + 1023) / 1024, kMaxBlocks)));
@@ -446,22 +429,6 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
                                                               d->pro_kind, pro_a, pro_b, part, out);          \
         break;
         switch (key) {
-            case 9 * 16 + 18:  // 162 / 297: no power-of-two pair maps to these keys
-                if (bf)
-                    k_pw_wgrad_reg<bf16_t, 9, 18, 1><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,
-                                                                         d->pro_kind, pro_a, pro_b, part, out);
-                else
-                    k_pw_wgrad_reg<float, 9, 18, 1><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,
-                                                                        d->pro_kind, pro_a, pro_b, part, out);
-                break;
-            case 18 * 16 + 9:
-                if (bf)
-                    k_pw_wgrad_reg<bf16_t, 18, 9, 1><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,
-                                                                         d->pro_kind, pro_a, pro_b, part, out);
-                else
-                    k_pw_wgrad_reg<float, 18, 9, 1><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,
-                                                                        d->pro_kind, pro_a, pro_b, part, out);
-                break;
             REG(1, 1) REG(1, 2) REG(1, 4) REG(1, 8) REG(2, 1) REG(2, 2) REG(2, 4) REG(2, 8)
             REG(4, 1) REG(4, 2) REG(4, 4) REG(4, 8) REG(8, 1) REG(8, 2) REG(8, 4)
         default: return fail("conv3d_bwd_weight: no register-path kernel");

@@ -16,9 +16,11 @@ PL collects the init arguments by name and `load_from_checkpoint` calls `cls(**h
 checkpoint written here loads in the reference and vice versa.
 
 Loading never unpickles arbitrary objects: `torch.load(weights_only=True)` with an allowlist
-of `argparse.Namespace` and inert stand-ins for the PL callback classes whose *types* key the
+of `argparse.Namespace`, the `pathlib` path classes (train.py:22 stores `dataset_path` as a
+Path) and inert stand-ins for the PL callback classes whose *types* key the
 `callbacks` entry of a Trainer checkpoint.
 """
+import pathlib
 from argparse import Namespace
 
 import torch
@@ -33,7 +35,10 @@ def _stub(qualname):
     return type(qualname.rsplit(".", 1)[1], (), {"__module__": qualname.rsplit(".", 1)[0]})
 
 
-_SAFE = [Namespace] + [(_stub(q), q) for q in _PL_CALLBACKS]
+# the reference's train.py parses `dataset_path` with type=Path (train.py:22), so every Namespace it
+# saves holds a pathlib object
+_PATHS = [pathlib.PosixPath, pathlib.PurePosixPath, pathlib.WindowsPath, pathlib.PureWindowsPath]
+_SAFE = [Namespace] + _PATHS + [(_stub(q), q) for q in _PL_CALLBACKS]
 
 
 def save_checkpoint(path, model, optimizer=None, epoch: int = 0, global_step: int = 0, callbacks=None):

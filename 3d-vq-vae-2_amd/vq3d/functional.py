@@ -12,6 +12,7 @@ import torch
 from . import _lib as L
 from . import ops
 from .ops import ConvGeom
+from .parallel import grads_ready, sum_allreduce
 
 CL = torch.channels_last_3d
 
@@ -115,6 +116,7 @@ class PreActBlockFn(torch.autograd.Function):
                      "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
             g_x = ops.preact_tiny_bwd(g, x, saved, blk, {n: gb(t) for n, t in names.items()})
+            grads_ready(blk._fn_params)
             return (g_x, None) + (None,) * len(blk._fn_params)
         x, t2, t3, tup = ctx.saved_tensors
         if ctx.small:
@@ -122,6 +124,7 @@ class PreActBlockFn(torch.autograd.Function):
                      "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
             g_x = ops.preact_small_bwd(g, x, t2, t3, blk, {n: grad_buf(t) for n, t in names.items()})
+            grads_ready(blk._fn_params)
             return (g_x, None) + (None,) * len(blk._fn_params)
         k, s, p, up = mode_geometry(blk.mode)
         g1 = ConvGeom(1)
@@ -152,6 +155,7 @@ class PreActBlockFn(torch.autograd.Function):
         g_x, _ = ops.conv_bwd(g_h1, x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), aux=x,
                               addend=addend, dw=gb(blk.branch_conv1.weight), dpro_pre=gb(blk.bias1b),
                               dpro_post=gb(blk.bias1a))
+        grads_ready(blk._fn_params)
         return (g_x, None) + (None,) * len(blk._fn_params)
 
 
@@ -201,6 +205,7 @@ class ConvFn(torch.autograd.Function):
                                dcbias=gb(spec.cbias), dpro_pre=pro_pre, dpro_post=pro_post, escale=spec.scale)
         if not want:
             gx = gx2 = None
+        grads_ready(spec.tensors)
         return (gx, gx2, g_res, None) + (None,) * len(spec.tensors)
 
 
@@ -268,6 +273,7 @@ class EvoNormFn(torch.autograd.Function):
         L.call("vq3d_evonorm_bwd", L.dtype_code(x), L.ptr(x), L.ptr(g), c, nvox, L.ptr(mod.v), L.ptr(mod.gamma),
                L.ptr(stats), L.ptr(gx), L.ptr(grad_buf(mod.v)), L.ptr(grad_buf(mod.gamma)),
                L.ptr(grad_buf(mod.beta)), L.ptr(ws), L.stream())
+        grads_ready((mod.v, mod.gamma, mod.beta))
         return gx, None, None, None, None
 
 
@@ -287,13 +293,13 @@ class QuantizeFn(torch.autograd.Function):
         ws = ops.workspace(L.query("vq3d_vq_workspace_size", n, d, k), dev)
         zc = L.dtype_code(z)
         if q.training and q.first_pass_host:
-            mean = torch.empty(d, dtype=torch.float32, device=dev)
-            std = torch.empty(d, dtype=torch.float32, device=dev)
+            # _init_ema (layers.py:665-683): mean / unbiased std of this rank's rows, summed over
+            # the ranks in one all-reduce (C3) and divided by the world size in the init kernel
+            ms = torch.empty(2 * d, dtype=torch.float32, device=dev)
+            mean, std = ms[:d], ms[d:]
             L.call("vq3d_vq_moments", zc, L.ptr(z), n, d, L.ptr(mean), L.ptr(std), L.ptr(ws), st)
-            world, n_tot = 1, float(n)
-            if q.dist_reduce is not None:
-                world = q.dist_reduce(mean, std)
-                n_tot = float(n) * world
+            world = sum_allreduce(ms)
+            n_tot = float(n) * world
             L.call("vq3d_vq_init_apply", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size),
                    L.ptr(q.first_pass), L.ptr(mean), L.ptr(std), k, d, 1.0 / world, n_tot, st)
             q.first_pass_host = False
@@ -308,13 +314,16 @@ class QuantizeFn(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=dev)
         L.call("vq3d_vq_commit_loss", L.ptr(sq), q.commitment_cost / float(n * d), L.ptr(loss), st)
         if q.training:
-            counts = torch.empty(k, dtype=torch.float32, device=dev)
-            dw = torch.empty((k, d), dtype=torch.float32, device=dev)
+            # _update_ema (layers.py:636-663).  Inside Encoder2 the statistics land in the
+            # encoder's fused buffer and the update waits for its single all-reduce (the updated
+            # codebook is first read by the NEXT step: q and backward use the copy above)
+            slot = q.ema_slot
+            stats = torch.empty(k * (d + 1), dtype=torch.float32, device=dev) if slot is None else slot
+            counts, dw = stats[:k], stats[k:]
             L.call("vq3d_vq_ema_stats", zc, L.ptr(z), n, d, L.ptr(idx), k, L.ptr(counts), L.ptr(dw), L.ptr(ws), st)
-            if q.dist_reduce is not None:
-                q.dist_reduce(counts, dw)
-            L.call("vq3d_vq_ema_update", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size), L.ptr(counts),
-                   L.ptr(dw), k, d, q.decay, q.laplace_alpha, st)
+            if slot is None:
+                sum_allreduce(stats)
+                ema_update(q, stats)
         ctx.coef = 2.0 * q.commitment_cost / float(n * d)
         ctx.save_for_backward(z, embed, idx)
         ctx.mark_non_differentiable(idx)
@@ -334,6 +343,14 @@ class QuantizeFn(torch.autograd.Function):
         return gz, None
 
 
+def ema_update(q, stats):
+    """EMA decay + Laplace smoothing of one Quantizer from its (all-reduced) statistics
+    [counts (K) | dw (K x D)] (layers.py:649-663)."""
+    k, d = q.num_embeddings, q.embedding_dim
+    L.call("vq3d_vq_ema_update", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size), L.ptr(stats[:k]),
+           L.ptr(stats[k:]), k, d, q.decay, q.laplace_alpha, L.stream())
+
+
 # ============================================================================================ loss
 class ReconLossFn(torch.autograd.Function):
     """VQVAE.loc_metric with F.smooth_l1_loss (model.py:115-163): returns (total, recon) with
@@ -342,7 +359,12 @@ class ReconLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, dec, x, nvs, cylinder, *commit):
         dec = ops.as_cl(dec)
-        b, _, h, w, d = dec.shape
+        b, c, h, w, d = dec.shape
+        if c != 1:
+            # the loss kernels index (B, H, W, D) volumes; the published runs use one input channel
+            raise NotImplementedError(f"recon loss kernels take --input-channels 1 (got {c} channels)")
+        if tuple(x.shape) != tuple(dec.shape) or not x.is_contiguous():
+            raise ValueError(f"target volume {tuple(x.shape)} must be a contiguous {tuple(dec.shape)} tensor")
         dev = dec.device
         recon = torch.empty((), dtype=torch.float32, device=dev)
         total = torch.empty((), dtype=torch.float32, device=dev)

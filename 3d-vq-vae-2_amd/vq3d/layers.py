@@ -16,6 +16,7 @@ from . import _lib as L
 from . import functional as Fn
 from .evonorm import EvoNorm3DS0
 from .ops import ConvGeom
+from .parallel import sum_allreduce
 
 
 # ============================================================================================ conv containers
@@ -309,12 +310,38 @@ class Encoder2(nn.Module):
             downsampled.append(down)
         aux = None
         quantizations = []
-        for down, pre_quantize, pre_quantize_cond, quantize in reversed(
-                list(zip(downsampled, self.pre_quantize, self.pre_quantize_cond, self.quantize))):
-            quantization = quantize(pre_quantize(pre_quantize_cond(down, aux)))
-            quantizations.append(quantization)
-            _, aux, *_ = quantization
+        stats = self._ema_slots(data.device) if self.training else None
+        try:
+            for down, pre_quantize, pre_quantize_cond, quantize in reversed(
+                    list(zip(downsampled, self.pre_quantize, self.pre_quantize_cond, self.quantize))):
+                quantization = quantize(pre_quantize(pre_quantize_cond(down, aux)))
+                quantizations.append(quantization)
+                _, aux, *_ = quantization
+        finally:
+            for q in self.quantize:
+                q.ema_slot = None
+        if stats is not None:
+            # the reference all-reduces counts and dw inside each level's forward (C1 / C2,
+            # layers.py:645-647: six latency-bound calls on the critical path); every level's
+            # codes are final before any EMA update matters (the updated codebooks are first
+            # read by the next step), so one SUM all-reduce of all levels' statistics follows
+            sum_allreduce(stats)
+            off = 0
+            for q in self.quantize:
+                n = q.num_embeddings * (q.embedding_dim + 1)
+                if q.training:
+                    Fn.ema_update(q, stats[off:off + n])
+                off += n
         return reversed(quantizations)
+
+    def _ema_slots(self, device):
+        sizes = [q.num_embeddings * (q.embedding_dim + 1) for q in self.quantize]
+        stats = torch.empty(sum(sizes), dtype=torch.float32, device=device)
+        off = 0
+        for q, n in zip(self.quantize, sizes):
+            q.ema_slot = stats[off:off + n] if q.training else None
+            off += n
+        return stats
 
 
 class Decoder(nn.Module):
@@ -363,6 +390,9 @@ class Quantizer(nn.Module):
         self.register_buffer("cluster_size", torch.zeros(num_embeddings))
         self.register_buffer("first_pass", torch.as_tensor(1))
         self.first_pass_host = True
+        # fp32 [counts (K) | dw (K x D)] slice of the encoder's fused EMA-statistics buffer while
+        # Encoder2.forward runs (None: a standalone forward reduces and updates by itself)
+        self.ema_slot = None
         self.commitment_cost = commitment_cost
         self.decay = decay
         self.laplace_alpha = laplace_alpha
@@ -374,19 +404,6 @@ class Quantizer(nn.Module):
         fp = state_dict.get(prefix + "first_pass")
         if fp is not None:
             self.first_pass_host = bool(int(fp))
-
-    @property
-    def dist_reduce(self):
-        """SUM all-reduce of the EMA statistics across data-parallel ranks (layers.py:645-647,
-        670-676), over RCCL when the default process group is initialised; returns world size."""
-        if not (torch.distributed.is_available() and torch.distributed.is_initialized()):
-            return None
-
-        def reduce(*tensors):
-            for t in tensors:
-                torch.distributed.all_reduce(t)
-            return torch.distributed.get_world_size()
-        return reduce
 
     def embed_code(self, embed_idx):
         """F.embedding(idx, embed) (layers.py:633-634)."""

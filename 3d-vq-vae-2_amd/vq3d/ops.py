@@ -5,7 +5,6 @@ channels-last (torch.channels_last_3d == physical [B][H][W][D][C]), fp32 or bf16
 Every call enqueues on the current torch stream; nothing here synchronises the host.
 """
 import ctypes
-import os
 
 import torch
 
@@ -195,6 +194,10 @@ def _side_stream(device):
     return s
 
 
+def side_streams():
+    return list(_side.values())
+
+
 def join_side():
     """Current stream waits for all weight-gradient work issued on the side streams."""
     if _side:
@@ -225,7 +228,7 @@ def upsample2x_bwd(gy, src_shape, pro=None, aux=None, aux_b=None, addend=None, d
 
 
 # ------------------------------------------------------------------------------------------------ tiny PreAct block
-_tiny = [os.environ.get("VQ3D_NO_TINY", "0") != "1"]
+_tiny = [True]
 
 
 def set_tiny_blocks(enabled):
@@ -278,7 +281,7 @@ def preact_tiny_bwd(g, x, saved, blk, grads):
     return gx
 
 
-_mid = [os.environ.get("VQ3D_NO_MID", "0") != "1"]
+_mid = [True]
 
 
 def set_mid_blocks(enabled):
@@ -306,7 +309,7 @@ def preact_mid_fwd(x, blk):
     return out, t2, t3
 
 
-_small = [os.environ.get("VQ3D_NO_SMALL", "0") != "1", os.environ.get("VQ3D_SMALL_BWD", "1") != "0"]
+_small = [True, True]
 
 
 def set_small_blocks(enabled, fused_backward=True):
@@ -320,7 +323,7 @@ def set_small_blocks(enabled, fused_backward=True):
 # fused backward up to this many voxels (measured, bench 3L pub: 23.6 vs ~100 us per (8, 4) block
 # at 32x32x8, 51 vs ~80 us per (2, 1) block at 128x128x32); beyond it the per-brick weight-gradient
 # partials are LDS-bound (6.2 ms per (4, 2) block at 512x512x128) and the per-conv backward wins
-_SMALL_BWD_MAX_VOX = int(os.environ.get("VQ3D_SMALL_BWD_MAX_VOX", 1 << 19))
+_SMALL_BWD_MAX_VOX = 1 << 19
 
 
 def small_backward_fused(x):

@@ -1,15 +1,25 @@
 """Data parallelism: one process per GPU, whole volumes sharded across ranks (the reference's
 PL 'ddp' accelerator, vqvae/train.py:26-27), RCCL over xGMI via torch.distributed 'nccl'.
 
-Per step the only data-path exchange is the gradient all-reduce of the flat fp32 gradient
-buffer (flat.py); the Quantizer's EMA statistics are all-reduced inside its forward exactly
-where the reference does (layers.py:645-647, 670-676).  Replicas start identical (rank 0
-broadcasts parameters and buffers once), so no per-step buffer broadcast is needed.
+Per step the data-path exchanges are:
+  * the gradient average of the flat fp32 gradient buffer (flat.py), cut into buckets of
+    contiguous parameters in reverse registration order (the order backward finishes them).
+    Every autograd Function of the path reports its parameters once their gradient kernels are
+    enqueued (`grads_ready`); when a bucket's last parameter is in, its all-reduce is issued
+    on a communication stream that waits for the main and the weight-gradient side stream, so
+    the RCCL ring runs while backward continues (what PL DDP's bucketing gives the reference,
+    train.py:27).  `GradientAllReduce.__call__` issues what is left and joins before Adam.
+  * the Quantizers' EMA statistics: ONE fused SUM all-reduce per forward (layers.Encoder2,
+    reference layers.py:645-647 does two per level), plus the first-step mean/std (C3).
+Replicas start identical (rank 0 broadcasts parameters and buffers once), so the reference's
+per-forward buffer broadcast (DDP broadcast_buffers) is not needed.
 """
 import os
 
 import torch
 import torch.distributed as dist
+
+_active = [None]  # the GradientAllReduce whose buckets the autograd Functions report to
 
 
 def init_from_env(backend=None):
@@ -37,27 +47,133 @@ def shard_indices(step, rank, world, per_rank=1):
     return list(range(base, base + per_rank))
 
 
-class GradientAllReduce:
-    """Average the model's flat gradient across ranks (one RCCL all-reduce; gloo in CPU tests)."""
+def world_size(group=None):
+    return dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
 
-    def __init__(self, model, group=None):
+
+def sum_allreduce(t, group=None):
+    """In-place SUM all-reduce over the data-parallel ranks (no-op at world 1); returns world."""
+    w = world_size(group)
+    if w > 1:
+        dist.all_reduce(t, group=group)
+    return w
+
+
+def grads_ready(params):
+    """Called by the autograd Functions once the gradient kernels of `params` are enqueued."""
+    r = _active[0]
+    if r is not None:
+        r.ready(params)
+
+
+class GradientAllReduce:
+    """Average the model's flat gradient across ranks in buckets overlapped with backward (one
+    RCCL all-reduce per bucket; gloo SUM + divide in CPU tests).
+
+    bucket_bytes: target bucket size.  A bucket is a contiguous slice of the flat gradient (the
+    parameters are laid out in registration order, backward finishes them roughly in reverse)."""
+
+    def __init__(self, model, group=None, bucket_bytes=8 << 20, overlap=True):
         self.flat = model.flat
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = world_size(group)
+        self.works = []
         if self.world > 1:
             self.backend = dist.get_backend(group)
             # identical replicas: parameters and buffers from rank 0 (what DDP does at wrap time)
             dist.broadcast(self.flat.data, 0, group=group)
             for b in model.buffers():
                 dist.broadcast(b, 0, group=group)
+            # host mirrors of broadcast buffers follow rank 0 (Quantizer.first_pass_host gates a
+            # collective, so every rank must agree on it)
+            for m in model.modules():
+                if hasattr(m, "first_pass_host"):
+                    m.first_pass_host = bool(int(m.first_pass))
+        self._build_buckets(bucket_bytes)
+        self.overlap = overlap and self.world > 1
+        self._comm = None
+        if self.overlap:
+            _active[0] = self
+        self._reset()
+
+    def _build_buckets(self, bucket_bytes):
+        f = self.flat
+        order = sorted(range(len(f.params)), key=lambda i: -f.offsets[i])  # reverse registration
+        self.buckets = []  # (lo, hi, [param ids])
+        cur, lo, hi = [], None, None
+        for i in order:
+            p, off = f.params[i], f.offsets[i]
+            end = off + p.numel()
+            if not cur:
+                hi = f.numel if not self.buckets else self.buckets[-1][0]
+            cur.append(id(p))
+            lo = off
+            if (hi - lo) * 4 >= bucket_bytes:
+                self.buckets.append((lo, hi, cur))
+                cur = []
+        if cur:
+            self.buckets.append((0, hi, cur))
+        elif self.buckets:
+            lo0, hi0, ids0 = self.buckets[-1]
+            self.buckets[-1] = (0, hi0, ids0)
+        self.bucket_of = {pid: bi for bi, (_, _, ids) in enumerate(self.buckets) for pid in ids}
+
+    def _reset(self):
+        self.pending = [set(ids) for _, _, ids in self.buckets]
+        self.issued = [False] * len(self.buckets)
+        self.works = []
+
+    def _stream(self):
+        if self._comm is None and self.flat.data.is_cuda:
+            self._comm = torch.cuda.Stream(device=self.flat.data.device)
+        return self._comm
+
+    def _issue(self, bi):
+        lo, hi, _ = self.buckets[bi]
+        view = self.flat.grad[lo:hi]
+        self.issued[bi] = True
+        if not view.is_cuda:
+            self.works.append((dist.all_reduce(view, group=self.group, async_op=True), view))
+            return
+        from . import ops
+        comm = self._stream()
+        comm.wait_stream(torch.cuda.current_stream())
+        for s in ops.side_streams():
+            comm.wait_stream(s)
+        with torch.cuda.stream(comm):
+            op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
+            self.works.append((dist.all_reduce(view, op=op, group=self.group, async_op=True), view))
+
+    def ready(self, params):
+        for p in params:
+            if p is None:
+                continue
+            bi = self.bucket_of.get(id(p))
+            if bi is None or self.issued[bi]:
+                continue
+            s = self.pending[bi]
+            s.discard(id(p))
+            if not s:
+                self._issue(bi)
 
     def __call__(self):
+        """Issue the buckets still pending, then make the current stream wait for every
+        all-reduce (the optimizer follows on it)."""
         if self.world == 1:
             return
         from . import ops
         ops.join_side()
-        if self.backend == "nccl":
-            dist.all_reduce(self.flat.grad, op=dist.ReduceOp.AVG, group=self.group)
-        else:  # gloo (CPU test transport): SUM then divide
-            dist.all_reduce(self.flat.grad, group=self.group)
-            self.flat.grad.div_(self.world)
+        for bi in range(len(self.buckets)):
+            if not self.issued[bi]:
+                self._issue(bi)
+        for work, view in self.works:
+            work.wait()
+            if self.backend != "nccl":
+                view.div_(self.world)
+        if self._comm is not None:
+            torch.cuda.current_stream().wait_stream(self._comm)
+        self._reset()
+
+    def close(self):
+        if _active[0] is self:
+            _active[0] = None

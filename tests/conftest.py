@@ -8,6 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "3d-vq-vae-2_amd"))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+PKG = os.path.join(ROOT, "3d-vq-vae-2_amd")
 
 
 def pytest_configure(config):

@@ -60,6 +60,9 @@ def test_loads_reference_state_dict_and_pl_callbacks(tmp_path):
                              n_post_upscale_blocks=1, n_post_downscale_blocks=1, num_embeddings=[64, 32])
     del args.compute_dtype  # the reference's args have no such field
     args.gpus, args.precision, args.max_epochs = 1, 16, 1000  # Trainer.add_argparse_args fields
+    from pathlib import Path
+    args.dataset_path = Path("/data")  # train.py:22 parses it with type=Path
+    args.num_workers, args.rescale_input = 5, None  # train.py:20-21
     mc = next(c for c, q in (x for x in _SAFE if isinstance(x, tuple)) if q.endswith("ModelCheckpoint"))
     ck = {"epoch": 0, "global_step": 1, "pytorch-lightning_version": PL_VERSION, "state_dict": sd,
           "callbacks": {mc: {"monitor": "val_recon_loss", "best_model_score": torch.tensor(0.5)}},
@@ -87,6 +90,7 @@ def test_loads_reference_state_dict_and_pl_callbacks(tmp_path):
     for k, v in m.state_dict().items():
         assert torch.equal(v, sd[k]), k
     assert m.compute_dtype == torch.bfloat16
+    assert m.hparams["args"].dataset_path == Path("/data")
     q = m.encoder.quantize[0]
     assert not q.first_pass_host and int(q.first_pass) == 0
 

@@ -58,20 +58,28 @@ def test_distributed_ema_matches_reference_two_ranks():
     assert all(bool(torch.load(out + f".{r}")) for r in range(2))
 
 
-class _FakeFlat:
-    def __init__(self, n, seed):
-        g = torch.Generator().manual_seed(seed)
-        self.data = torch.randn(n, generator=g)
-        self.grad = torch.randn(n, generator=g)
+class _FakeQuantizer(torch.nn.Module):
+    """Carries the first_pass buffer + host mirror (vq3d.layers.Quantizer) whose agreement
+    across ranks GradientAllReduce must establish."""
 
-
-class _FakeModel:
     def __init__(self, rank):
-        self.flat = _FakeFlat(1000, 10 + rank)
-        self._buf = torch.full((4,), float(rank))
+        super().__init__()
+        self.register_buffer("first_pass", torch.as_tensor(1 - rank))
+        self.first_pass_host = bool(1 - rank)
 
-    def buffers(self):
-        return [self._buf]
+
+class _FakeModel(torch.nn.Module):
+    """Parameters in one flat buffer (vq3d.flat.FlatParams on the CPU) + a Quantizer-like buffer."""
+
+    def __init__(self, rank):
+        super().__init__()
+        from vq3d.flat import FlatParams
+        g = torch.Generator().manual_seed(10 + rank)
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(n, generator=g)) for n in (300, 1000, 7, 64, 2000)])
+        self.q = _FakeQuantizer(rank)
+        self.flat = FlatParams(self.ps, "cpu")
+        for p in self.ps:
+            p.grad.copy_(torch.randn(p.shape, generator=g))
 
 
 def _allreduce_worker(rank, world, port, out):
@@ -79,13 +87,32 @@ def _allreduce_worker(rank, world, port, out):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "3d-vq-vae-2_amd"))
     from vq3d import parallel
     _init(rank, world, port)
-    m = _FakeModel(rank)
-    grads = [_FakeFlat(1000, 10 + r).grad for r in range(world)]
-    ar = parallel.GradientAllReduce(m)
+    models = [_FakeModel(r) for r in range(world)]
+    m = models[rank]
+    expect = sum(mm.flat.grad for mm in models) / world
+    # 2 KB buckets: several buckets over the 3,371 parameters (+ alignment padding)
+    ar = parallel.GradientAllReduce(m, bucket_bytes=2048)
+    ok = len(ar.buckets) >= 3
+    # buckets tile the flat buffer, highest offsets first
+    ok &= ar.buckets[0][1] == m.flat.numel and ar.buckets[-1][0] == 0
+    ok &= all(a[0] == b[1] for a, b in zip(ar.buckets, ar.buckets[1:]))
+    # backward reports parameters in reverse order: buckets go out as they complete
+    ps = list(m.ps)
+    parallel.grads_ready(ps[4:])
+    ok &= ar.issued[0] and not all(ar.issued)
+    parallel.grads_ready(ps[:4])
+    ok &= all(ar.issued)
     ar()
-    ok = torch.allclose(m.flat.grad, sum(grads) / world, atol=1e-6)
-    ok &= torch.equal(m.flat.data, _FakeFlat(1000, 10).data)  # rank 0's replica everywhere
-    ok &= torch.equal(m._buf, torch.zeros(4))
+    ok &= torch.allclose(m.flat.grad, expect, atol=1e-6)
+    ok &= torch.equal(m.flat.data, models[0].flat.data)  # rank 0's replica everywhere
+    ok &= int(m.q.first_pass) == 1 and m.q.first_pass_host  # buffer and host mirror follow rank 0
+    # a second step: the bucket state was reset; unreported buckets are issued by __call__
+    for p in m.ps:
+        p.grad.fill_(float(rank + 1))
+    parallel.grads_ready(ps[4:])
+    ar()
+    ok &= torch.allclose(m.flat.grad[m.flat.offsets[0]:m.flat.offsets[0] + 300], torch.full((300,), 1.5))
+    ar.close()
     shards = [parallel.shard_indices(s, rank, world, 2) for s in range(3)]
     torch.save({"ok": torch.tensor(bool(ok)), "shards": shards}, out + f".{rank}")
     dist.destroy_process_group()
