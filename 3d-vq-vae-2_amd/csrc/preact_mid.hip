@@ -1,291 +1,833 @@
-// Forward of a whole PreActFixupResBlock (vqvae/layers.py:176-195, mode 'same', no skip conv)
-// in ONE launch for the 18-channel / branch-9 blocks of the published model's 128x128x32 level
-// (50 per step).  Unfused, the block forward is three launches that each stream activations
-// through HBM (1x1 conv, 3x3x3 conv, 1x1 conv + residual); here a workgroup owns a 16 x 16 x 8
-// brick and 768 threads (one D-run of 8 voxels x 3 channel groups):
+// The 18-channel / branch-9 PreActFixupResBlock (vqvae/layers.py:176-195, mode 'same', no skip
+// conv) of the published model's 128x128x32 level (50 decoder post-quantize blocks), forward in
+// TWO launches and backward in THREE, all on resident bf16 channels-last tensors:
 //
-//   A. t2 = elu(W1 (elu(x + b1a) + b1b) + b2a) + b2b on the brick's 18 x 18 x 10 halo
-//      (circular wrap), straight from the x rows, bf16 in LDS (rows padded to 16 channels)
-//   B. t3 = elu(W2 (*) t2 + b3a) + b3b: a thread owns a D-run of 8 voxels and 3 output channels,
-//      so one halo line read (10 positions) feeds 3 taps x 8 voxels; W2 broadcast from LDS; the
-//      line stride is an odd number of dwords (adjacent D-runs hit different banks)
-//   C. out = scale * W3 t3 + b4 + x for the D-run's 8 voxels, 6 output channels per thread, on
-//      the brick's x rows staged in LDS (over the dead t2 halo) and updated in place
+//   u1  = elu(x + b1a) + b1b      t2 = elu(W1 u1 + b2a) + b2b        (1x1, 18 -> 9)
+//   t3  = elu(W2 (*) t2 + b3a) + b3b                                   (3x3x3 circular, 9 -> 9)
+//   out = scale * (W3 t3) + b4 + x                                     (1x1, 9 -> 18)
 //
-// t2 (brick rows) and t3 go to HBM as bf16 for the backward, which is unchanged.  Every HBM
-// access of the brick's rows (x in, out / t2 / t3 out) is a 16-B chunk per thread with
-// consecutive threads on consecutive chunks: whole cache lines per wave, no partial-line writes.
-// Rounding points are the unfused path's (t2 and t3 rounded to bf16 before the next conv), fp32
-// accumulation; all three weight tensors are broadcast from LDS (fp32, rows padded to 48 B).
+// forward  k_pm_t2   : t2 from x, a streaming pointwise kernel (t2 is saved for the backward
+//                      anyway, so computing it once beats recomputing it on every tile halo)
+//          k_pm_fwd  : per tile, t2 on the tile's circular halo in LDS -> t3 on the matrix cores
+//                      -> out = scale W3 t3 + b4 + x on the matrix cores; t3 / out leave in 16-B
+//                      chunks.
+// backward k_pm_bwd1 : gz3 = bf16(scale W3^T g * elu'(t3)) (pointwise) + the W3 / scale / b4 / b3
+//                      partials
+//          k_pm_bwd2 : per tile, gz3 and t2 on the halo in LDS -> gt2 = W2^T (*) gz3 (flipped
+//                      taps, matrix cores) -> gz1 = bf16(gt2 * elu'(t2)) -> gx = g + (W1^T gz1)
+//                      * elu'(x + b1a); the W2 gradient (matrix cores, voxels as the reduction
+//                      axis) and the W1 / b2 / b1 partials
+//          k_pm_reduce: every gradient entry summed over the workgroups in a fixed order and
+//                      added into the gradient buffers (deterministic, one adder per entry).
+// Rounding points are the unfused per-conv path's (t2, t3, gz3, gz1, gx, out rounded to bf16,
+// fp32 accumulation), except that the W1 gradient reads u1 rounded to bf16 (the matrix-core
+// operand).
+//
+// The k^3 convs use a "windowed" reduction order: for a voxel and a tap row (kh, kw) the three
+// kd taps x 9 channels are 27 CONSECUTIVE elements of the halo D-line (channels-last, pitch 9),
+// so one v_mfma_f32_16x16x32_bf16 k-step covers a whole tap row: 9 k-steps per 16 voxels
+// instead of 14 with channel padding.  The five trailing elements of each window belong to the
+// next position and meet zero weights.
 #include "engines.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace vq3d {
 
 namespace {
 
-constexpr int C = 18, BR = 9;                 // block channels, branch channels
-constexpr int BD = 8, HD = BD + 2;            // brick depth (one D-run of 8 voxels per thread)
-constexpr int WS = 12;                        // weight row stride in LDS (fp32, 48 B)
-constexpr int NG = 3;                         // thread groups: 3 output channels each in phase B
-constexpr int W2R = 27 * 9 * 12 > 14 * 64 * 8 / 2 ? 27 * 9 * 12 : 14 * 64 * 8 / 2;  // W2 region (floats)
-
-// Brick geometry (BH x BW x 8 voxels) and the t2 position row RS (bf16, >= 9): the 16 x 16
-// brick with 16-wide rows needs 155 KB of LDS (one workgroup per CU, phases serialised on
-// every CU); 8 x 16 with 10-wide rows fits two workgroups per CU (68 KB each).
-template <int BH_, int BW_, int RS_>
-struct Geo {
-    static constexpr int BH = BH_, BW = BW_, RS = RS_;
-    static constexpr int HH = BH + 2, HW = BW + 2, HP = HH * HW * HD;
-    static constexpr int LSD = HD * RS + 2;   // t2 line stride (bf16): odd number of dwords -> no bank aliasing
-    static constexpr int NR = BH * BW;        // D-runs per brick
-    static constexpr int NTP = NR * NG;       // threads
-    static constexpr int T2H = (HH * HW * LSD > NR * BD * C ? HH * HW * LSD : NR * BD * C + 0);  // t2 halo / x rows
-    static constexpr int T2HA = (T2H + 7) / 8 * 8;
-    static_assert(LSD / 2 % 2 == 1 && RS % 2 == 0 && RS >= BR, "odd dword line stride, paired rows");
-    static_assert((W2R + 2 * C * WS) * 4 % 16 == 0, "t2h 16-B aligned");
-    static size_t lds() { return (size_t(W2R) + 2 * size_t(C) * WS) * 4 + (size_t(T2HA) + 8 + size_t(NR) * BD * BR) * 2; }
-};
-
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int NPAIR = 14;  // MFMA k-steps of phase B: 27 taps in pairs x 16 (padded) channels
 
-struct MidArgs {
+constexpr int C = 18, BR = 9, TD = 8;  // block channels, branch channels, tile depth (one D-run)
+constexpr int NT = 256;                // threads per workgroup (every kernel)
+constexpr int LSP = 104;               // halo line pitch (elements): [7 pad][pos -1][pos 0..7][pos 8][pad]
+constexpr int LOFF = 7;                // element of halo position -1 (position p at LOFF + 9 (p + 1))
+constexpr int LINT = 16;               // element of position 0: the interior run is 16-B aligned
+constexpr int LEND = LINT + 9 * 9;     // first element after position 8 (97): zero padding
+constexpr int SPAD = 40;               // zero tail of the pitch-9 / pitch-18 tile buffers
+
+// partial-gradient entries
+constexpr int NE1 = C * BR + 4;                    // K1: G3 [co][o], b4, b3b, b3a, scale
+constexpr int NW2 = BR * BR * 27;                  // W2 gradient [co][ci][tap]
+constexpr int NE2 = NW2 + BR * C + 4;              // K2: W2, W1 [o][c], b2b, b2a, b1b, b1a
+
+struct PmArgs {
     int B, H, W, D;
-    int nbh, nbw, nbd, nbricks;
+    int nth, ntw, ntd, ntiles;
+};
+
+template <int TH, int TW>
+struct Tile {
+    static constexpr int LH = TH + 2, LW = TW + 2, NL = LH * LW;
+    static constexpr int NRUN = TH * TW, TV = NRUN * TD, NMT = TV / 16;
+    static constexpr int LINES = NL * LSP;                      // elements of one halo image
+    static constexpr int S9 = (TV * BR + SPAD + 7) / 8 * 8;      // pitch-9 tile buffer
+    static constexpr int S18 = (TV * C + SPAD + 7) / 8 * 8;      // pitch-18 tile buffer
+    static_assert(TV % 64 == 0 && NRUN % 4 == 0, "tile");
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+__device__ __forceinline__ float bf(uint32_t u16) { return __uint_as_float(u16 << 16); }
+__device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
+    const float z1 = t - b;
+    return z1 > 0.f ? 1.f : z1 + 1.f;
+}
 
-template <class G>
-__global__ __launch_bounds__(G::NTP) void k_preact_mid_fwd(MidArgs a, const bf16_t *__restrict__ x,
-                                                       const float *__restrict__ w1, const float *__restrict__ w2,
-                                                       const float *__restrict__ w3, vq3d_preact_params p,
-                                                       bf16_t *__restrict__ out, bf16_t *__restrict__ t2o,
-                                                       bf16_t *__restrict__ t3o) {
-    constexpr int BH = G::BH, BW = G::BW, RS = G::RS, HW = G::HW, HP = G::HP, LSD = G::LSD, NR = G::NR,
-                  NTP = G::NTP;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float *w2s = reinterpret_cast<float *>(smem);                      // [tap][c][WS] (o < 9)
-    float *w1s = w2s + W2R;                                            // [c][WS]      (o < 9)
-    float *w3s = w1s + C * WS;                                         // [co][WS]     (o < 9)
-    bf16_t *t2h = reinterpret_cast<bf16_t *>(w3s + C * WS);            // [HH * HW lines][LSD]
-    bf16_t *t3s = t2h + G::T2HA + 8;                             // [NR][BD * BR]
-    const int tid = threadIdx.x;
-    {
-        // phase-B MFMA B fragments, bf16: [pair][lane][8], lane l holds B[k = 8 (l >> 4) + j][n = l & 15]
-        // with k = 16 * (tap - 2 pair) + c (c < 16 padded, tap < 27), n = output channel (< 9)
-        bf16_t *wf = reinterpret_cast<bf16_t *>(w2s);
-        for (int i = tid; i < NPAIR * 64 * 8; i += NTP) {
-            const int j = i & 7, l = (i >> 3) & 63, pr = i >> 9;
-            const int k = 8 * (l >> 4) + j, n = l & 15, c = k & 15, tap = 2 * pr + (k >> 4);
-            wf[i] = bf16_t(f2bf(n < BR && c < BR && tap < 27 ? w2[(n * BR + c) * 27 + tap] : 0.f));
+// 8 consecutive bf16 from LDS at element offset `off` (any parity; base 16-B aligned): five
+// dwords + v_alignbyte when odd
+__device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(base + (off & ~1));
+    const uint32_t sh = uint32_t(off & 1) * 2u;
+    const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3], u4 = q[4];
+    const uint4 r = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
+                     __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// 8 bf16 at element offsets off + j * stride (j = 0..7) from LDS; zeros when !ok
+__device__ __forceinline__ bf16x8 gather8(const bf16_t *base, int off, int stride, bool ok) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (ok) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            w[j] = uint32_t(base[off + 2 * j * stride]) | (uint32_t(base[off + (2 * j + 1) * stride]) << 16);
+    }
+    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// copy n fp32 weights to LDS (coalesced; the fragments are then built from LDS instead of from
+// scattered global loads)
+__device__ __forceinline__ void stage_w(float *dst, const float *__restrict__ src, int n) {
+    for (int i = threadIdx.x; i < n; i += NT) dst[i] = src[i];
+}
+
+// W2 B fragments (from the LDS copy), one per tap row kk = kh * 3 + kw: B[k = e][n] with
+// e = kd * 9 + c (e < 27).
+// Forward: n = co, c = ci, tap kk * 3 + kd.  Backward-data (transposed, flipped): n = ci,
+// c = co, tap 26 - (kk * 3 + kd).
+template <bool DGRAD>
+__device__ __forceinline__ bf16x8 w2_frag(const float *w2, int kk, int lane) {
+    const int n = lane & 15, kb = lane >> 4;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int e = 8 * kb + j, kd = e / 9, c = e - 9 * kd;
+        float x = 0.f;
+        if (n < BR && e < 27) {
+            const int tap = kk * 3 + kd;
+            x = DGRAD ? w2[(c * BR + n) * 27 + 26 - tap] : w2[(n * BR + c) * 27 + tap];
+        }
+        v[j] = x;
+    }
+    return pack8(v);
+}
+
+struct Scal {
+    float b1a, b1b, b2a, b2b, b3a, b3b, sc, b4;
+};
+__device__ __forceinline__ Scal load_scal(const vq3d_preact_params &p) {
+    return Scal{*p.bias1a, *p.bias1b, *p.bias2a, *p.bias2b, *p.bias3a, *p.bias3b, *p.scale, *p.bias4};
+}
+
+struct Org {
+    int b, h0, w0, d0;
+};
+__device__ __forceinline__ Org tile_org(const PmArgs &a, int t, int TH, int TW) {
+    Org o;
+    o.d0 = (t % a.ntd) * TD;
+    t /= a.ntd;
+    o.w0 = (t % a.ntw) * TW;
+    t /= a.ntw;
+    o.h0 = (t % a.nth) * TH;
+    o.b = t / a.nth;
+    return o;
+}
+// global voxel index of D-run r (0 .. TH*TW-1) of the tile
+template <int TW>
+__device__ __forceinline__ int64_t run_vox(const PmArgs &a, const Org &o, int r) {
+    return ((int64_t(o.b) * a.H + o.h0 + r / TW) * a.W + o.w0 + r % TW) * a.D + o.d0;
+}
+
+// Stage the (TH+2) x (TW+2) halo D-lines of a 9-channel tensor around the tile (circular wrap):
+// per line the 8 interior positions (144 contiguous, 16-B aligned bytes) as 9 16-B chunks and
+// the two edge positions as 9 bf16 each.  load() issues every global load into registers,
+// store() writes them to LDS, so several tensors' loads are in flight together.
+template <int TH, int TW>
+struct LinesLd {
+    using T = Tile<TH, TW>;
+    static constexpr int NI = T::NL * 9, PI = (NI + NT - 1) / NT;
+    static constexpr int NEG = T::NL * 2 * BR, PE = (NEG + NT - 1) / NT;
+    uint4 vi[PI];
+    uint32_t ve[PE];
+    // every load is unconditional (indices past the end are clamped): a branch around a load
+    // makes hipcc wait for it on the spot
+    __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < PI; ++u) {
+            const int i = min(tid + u * NT, NI - 1);
+            const int line = i / 9, part = i - 9 * line, lh = line / T::LW, lw = line - lh * T::LW;
+            const int gh = wrapm(o.h0 - 1 + lh, a.H), gw = wrapm(o.w0 - 1 + lw, a.W);
+            const int64_t v0 = ((int64_t(o.b) * a.H + gh) * a.W + gw) * a.D + o.d0;
+            vi[u] = reinterpret_cast<const uint4 *>(src + v0 * BR)[part];
+        }
+#pragma unroll
+        for (int u = 0; u < PE; ++u) {
+            const int i = min(tid + u * NT, NEG - 1);
+            const int pos = i / BR, c = i - BR * pos, line = pos >> 1, side = pos & 1;
+            const int lh = line / T::LW, lw = line - lh * T::LW;
+            const int gh = wrapm(o.h0 - 1 + lh, a.H), gw = wrapm(o.w0 - 1 + lw, a.W);
+            const int gd = side ? wrapm(o.d0 + TD, a.D) : wrapm(o.d0 - 1, a.D);
+            ve[u] = src[(((int64_t(o.b) * a.H + gh) * a.W + gw) * a.D + gd) * BR + c];
         }
     }
-    for (int i = tid; i < C * WS; i += NTP) {
-        const int o = i % WS, c = i / WS;
-        w1s[i] = o < BR ? w1[o * C + c] : 0.f;  // W1 [BR][C] -> [c][o]
-        w3s[i] = o < BR ? w3[c * BR + o] : 0.f;  // W3 [C][BR] -> [co][o]
+    __device__ __forceinline__ void store(bf16_t *lines) const {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < PI; ++u) {
+            const int i = tid + u * NT;
+            if (i < NI) {
+                const int line = i / 9, part = i - 9 * line;
+                reinterpret_cast<uint4 *>(lines + line * LSP + LINT)[part] = vi[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PE; ++u) {
+            const int i = tid + u * NT;
+            if (i < NEG) {
+                const int pos = i / BR, c = i - BR * pos, line = pos >> 1, side = pos & 1;
+                lines[line * LSP + (side ? LINT + 9 * TD : LOFF) + c] = bf16_t(ve[u]);
+            }
+        }
     }
-    const float b1a = *p.bias1a, b1b = *p.bias1b, b2a = *p.bias2a, b2b = *p.bias2b;
-    const float b3a = *p.bias3a, b3b = *p.bias3b, sc = *p.scale, b4 = *p.bias4;
-    const int run = tid % NR, grp = tid / NR;  // D-run (lh, lw) and channel group (wave-uniform)
+};
 
+// A tile of a channels-last tensor with CH channels (CH * 8 * 2 bytes per D-run, 16-B chunks)
+// into LDS [voxel][CH]
+template <int TH, int TW, int CH>
+struct TileLd {
+    using T = Tile<TH, TW>;
+    static constexpr int PR = CH * TD / 8, N = T::NRUN * PR, P = (N + NT - 1) / NT;
+    uint4 v[P];
+    __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            const int i = min(tid + u * NT, N - 1);
+            const int r = i / PR, part = i - PR * r;
+            v[u] = reinterpret_cast<const uint4 *>(src + run_vox<TW>(a, o, r) * CH)[part];
+        }
+    }
+    __device__ __forceinline__ void store(bf16_t *dst) const {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            const int i = tid + u * NT;
+            if (i < N) reinterpret_cast<uint4 *>(dst)[i] = v[u];
+        }
+    }
+};
 
-    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
-        int bi = brick;
-        const int bzd = bi % a.nbd;
-        bi /= a.nbd;
-        const int bzw = bi % a.nbw;
-        bi /= a.nbw;
-        const int bzh = bi % a.nbh;
-        const int b = bi / a.nbh;
-        const int oh0 = bzh * BH, ow0 = bzw * BW, od0 = bzd * BD;
-        __syncthreads();
-        // ---- A. t2 on the halo
-        for (int q = tid; q < HP; q += NTP) {
-            asm volatile("" ::: "memory");  // keep the W1 rows as per-iteration LDS reads (no hoisting)
-            const int dd = q % HD, line = q / HD, ww = line % HW, hh = line / HW;
-            const int gh = wrapm(oh0 - 1 + hh, a.H), gw = wrapm(ow0 - 1 + ww, a.W), gd = wrapm(od0 - 1 + dd, a.D);
-            const uint32_t *s32 =
-                reinterpret_cast<const uint32_t *>(x + (((int64_t(b) * a.H + gh) * a.W + gw) * a.D + gd) * C);
-            float u[C];
-#pragma unroll
-            for (int j = 0; j < C / 2; ++j) {
-                const uint32_t v = s32[j];
-                u[2 * j] = elu(__uint_as_float(v << 16) + b1a) + b1b;
-                u[2 * j + 1] = elu(__uint_as_float(v & 0xffff0000u) + b1a) + b1b;
-            }
-            float a9[WS];
-#pragma unroll
-            for (int o = 0; o < WS; ++o) a9[o] = 0.f;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const float4 *wr = reinterpret_cast<const float4 *>(w1s + c * WS);
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float4 wq = wr[k];
-                    a9[4 * k] = fmaf(u[c], wq.x, a9[4 * k]);
-                    a9[4 * k + 1] = fmaf(u[c], wq.y, a9[4 * k + 1]);
-                    a9[4 * k + 2] = fmaf(u[c], wq.z, a9[4 * k + 2]);
-                    a9[4 * k + 3] = fmaf(u[c], wq.w, a9[4 * k + 3]);
-                }
-            }
-            uint32_t *dst = reinterpret_cast<uint32_t *>(t2h + line * LSD + dd * RS);
-#pragma unroll
-            for (int o = 0; o < RS; o += 2) {
-                const float lo = o < BR ? elu(a9[o] + b2a) + b2b : 0.f;
-                const float hi = o + 1 < BR ? elu(a9[o + 1] + b2a) + b2b : 0.f;
-                dst[o / 2] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
-            }
-        }
-        __syncthreads();
-        static_assert(G::RS == 16, "MFMA phase B reads 8-channel halves of 16-wide rows");
-        {
-        // ---- B (matrix cores). t3 = W2 (*) t2 as 16-voxel x 16-channel tiles (two D-runs of 8
-        //      voxels; 9 of 16 output columns valid), K = 27 taps x 16 channels in 14 steps of
-        //      v_mfma_f32_16x16x32_bf16; lane l reads its A row (voxel l & 15) straight from the
-        //      t2 halo lines: 8 channels of one tap, 16 B in two dword pairs (lines are 4-B aligned)
-            const int lane = tid & 63, wave = tid >> 6;
-            const int ri = lane & 15, kb = lane >> 4, ts = kb >> 1, ch = (kb & 1) * 8;
-            const bf16_t *wf = reinterpret_cast<const bf16_t *>(w2s);
-            constexpr int NW = NTP / 64;
-            // two tiles per iteration share each B fragment read and overlap their dependent
-            // MFMA chains
-            static_assert(NR % 4 == 0, "tile pairs");
-            for (int tp = wave; tp < NR / 4; tp += NW) {
-                const bf16_t *abase[2];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int run_i = 2 * (2 * tp + h) + (ri >> 3), d_i = ri & 7;
-                    abase[h] = t2h + ((run_i / BW) * HW + run_i % BW) * LSD + d_i * RS + ch;
-                }
-                f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-                for (int pr = 0; pr < NPAIR; ++pr) {
-                    constexpr auto toff = [](int tap) { return ((tap / 9) * HW + (tap / 3) % 3) * LSD + (tap % 3) * RS; };
-                    const int ta = 2 * pr, tb = 2 * pr + 1;
-                    const bool valid = ts == 0 || tb < 27;
-                    const int off = ts ? toff(tb < 27 ? tb : ta) : toff(ta);
-                    const bf16x8 bfr = *reinterpret_cast<const bf16x8 *>(wf + (pr * 64 + lane) * 8);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t *ap = reinterpret_cast<const uint32_t *>(abase[h] + off);
-                        uint32_t au[4] = {0u, 0u, 0u, 0u};
-                        if (valid) {
-                            au[0] = ap[0];
-                            au[1] = ap[1];
-                            au[2] = ap[2];
-                            au[3] = ap[3];
-                        }
-                        bf16x8 af;
-                        __builtin_memcpy(&af, au, 16);
-                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[h], 0, 0, 0);
-                    }
-                }
-                const int o = lane & 15;
-                if (o < BR) {
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int row = kb * 4 + j, r = 2 * (2 * tp + h) + (row >> 3), v = row & 7;
-                            t3s[r * BD * BR + v * BR + o] = bf16_t(f2bf(elu(acc[h][j] + b3a) + b3b));
-                        }
-                }
-            }
-        }
-        __syncthreads();
-        // t3 and the brick's t2 rows to HBM in 16-B chunks, consecutive threads on consecutive
-        // chunks of a D-run's 144 contiguous bytes (whole cache lines per wave store)
-        auto run_vox = [&](int r) {
-            return ((int64_t(b) * a.H + oh0 + r / BW) * a.W + ow0 + r % BW) * a.D + od0;
-        };
-        constexpr int CH2 = BD * BR / 8;  // 9 chunks per D-run
-        for (int j = tid; j < NR * CH2; j += NTP) {
-            const int r = j / CH2, part = j - r * CH2;
-            const int64_t v0 = run_vox(r);
-            *reinterpret_cast<uint4 *>(t3o + v0 * BR + part * 8) =
-                *reinterpret_cast<const uint4 *>(t3s + r * BD * BR + part * 8);
-            const uint16_t *own = reinterpret_cast<const uint16_t *>(t2h + ((r / BW + 1) * HW + r % BW + 1) * LSD);
-            uint32_t w4[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int e0 = part * 8 + 2 * i, e1 = e0 + 1;
-                w4[i] = uint32_t(own[(1 + e0 / BR) * RS + e0 % BR]) | (uint32_t(own[(1 + e1 / BR) * RS + e1 % BR]) << 16);
-            }
-            *reinterpret_cast<uint4 *>(t2o + v0 * BR + part * 8) = uint4{w4[0], w4[1], w4[2], w4[3]};
-        }
-        __syncthreads();  // t2h is reused below for the brick's x / out rows
-        // ---- C. x rows into LDS (16-B chunks), out = scale * W3 t3 + b4 + x in place (thread:
-        //      D-run x 6 output channels), out rows back to HBM in 16-B chunks
-        bf16_t *obuf = t2h;               // [D-run][BD * C]
-        constexpr int CH1 = BD * C / 8;  // 18 chunks per D-run
-        for (int j = tid; j < NR * CH1; j += NTP) {
-            const int r = j / CH1, part = j - r * CH1;
-            *reinterpret_cast<uint4 *>(obuf + r * BD * C + part * 8) =
-                *reinterpret_cast<const uint4 *>(x + run_vox(r) * C + part * 8);
-        }
-        __syncthreads();
-        {
-            const bf16_t *t3r = t3s + run * BD * BR;
-            constexpr int CG = C / NG;  // 6 output channels per group
-            for (int v = 0; v < BD; ++v) {
-                asm volatile("" ::: "memory");  // W3 rows re-read from LDS per voxel (no hoisting)
-                float t3v[BR];
-#pragma unroll
-                for (int o = 0; o < BR; ++o) t3v[o] = ld(t3r + v * BR + o);
-                uint32_t *xr = reinterpret_cast<uint32_t *>(obuf + run * BD * C + v * C + grp * CG);
-#pragma unroll
-                for (int k = 0; k < CG / 2; ++k) {
-                    const uint32_t xq = xr[k];
-                    float r2[2];
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        const int co = grp * CG + 2 * k + s2;
-                        const float4 *wr = reinterpret_cast<const float4 *>(w3s + co * WS);
-                        const float4 wa = wr[0], wb = wr[1];
-                        const float wc = w3s[co * WS + 8];
-                        const float wv[BR] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w, wc};
-                        float accv = 0.f;
-#pragma unroll
-                        for (int o = 0; o < BR; ++o) accv = fmaf(t3v[o], wv[o], accv);
-                        const float xv = s2 ? __uint_as_float(xq & 0xffff0000u) : __uint_as_float(xq << 16);
-                        r2[s2] = accv * sc + b4 + xv;
-                    }
-                    xr[k] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
-                }
-            }
-        }
-        __syncthreads();
-        for (int j = tid; j < NR * CH1; j += NTP) {
-            const int r = j / CH1, part = j - r * CH1;
-            *reinterpret_cast<uint4 *>(out + run_vox(r) * C + part * 8) =
-                *reinterpret_cast<const uint4 *>(obuf + r * BD * C + part * 8);
-        }
+template <int TH, int TW, int CH>
+__device__ __forceinline__ void store_tile(const PmArgs &a, const Org &o, const bf16_t *src, bf16_t *__restrict__ dst) {
+    using T = Tile<TH, TW>;
+    constexpr int PR = CH * TD / 8, N = T::NRUN * PR;
+    for (int i = threadIdx.x; i < N; i += NT) {
+        const int r = i / PR, part = i - PR * r;
+        reinterpret_cast<uint4 *>(dst + run_vox<TW>(a, o, r) * CH)[part] = reinterpret_cast<const uint4 *>(src)[i];
     }
 }
 
-using GeoWide = Geo<16, 16, 16>;  // 256 bricks at 128 x 128 x 32
-template <class G>
-void launch_mid(const MidArgs &a0, hipStream_t s, const bf16_t *x, const float *w1, const float *w2, const float *w3,
-                const vq3d_preact_params &p, bf16_t *out, bf16_t *t2, bf16_t *t3) {
-    MidArgs a = a0;
-    a.nbh = a.H / G::BH;
-    a.nbw = a.W / G::BW;
-    a.nbd = a.D / BD;
-    a.nbricks = a.B * a.nbh * a.nbw * a.nbd;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_preact_mid_fwd<G>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024 - 256));
-        (void)hipGetLastError();
-        attr = true;
+// zero the never-staged tails of the halo lines and of the tile buffers (read by the windows /
+// fragments that run past the valid data and meet zero weights: they must be finite)
+template <int TH, int TW>
+__device__ __forceinline__ void zero_pads(bf16_t *lines, int nimg, bf16_t *const *tails, const int *tail_at,
+                                          int ntails) {
+    using T = Tile<TH, TW>;
+    for (int i = threadIdx.x; i < nimg * T::NL * (LSP - LEND); i += NT) {
+        const int l = i / (LSP - LEND), e = i - l * (LSP - LEND);
+        lines[l * LSP + LEND + e] = 0;
     }
-    k_preact_mid_fwd<G><<<unsigned(a.nbricks), G::NTP, G::lds(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
+    for (int t = 0; t < ntails; ++t)
+        for (int i = threadIdx.x; i < SPAD; i += NT) tails[t][tail_at[t] + i] = 0;
+}
+
+// ============================================================================================ forward
+// t2 = elu(W1 (elu(x + b1a) + b1b) + b2a) + b2b, 256 voxels per workgroup iteration (the next
+// block's x in flight during the current one)
+__global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__restrict__ x,
+                                              const float *__restrict__ w1, vq3d_preact_params p,
+                                              bf16_t *__restrict__ t2o) {
+    __shared__ float w1s[BR * C];
+    __shared__ __attribute__((aligned(16))) bf16_t xs[NT * C];
+    __shared__ __attribute__((aligned(16))) bf16_t ts[NT * BR];
+    constexpr int N = NT * C / 8, P = (N + NT - 1) / NT;
+    const int tid = threadIdx.x;
+    stage_w(w1s, w1, BR * C);
+    const Scal s = load_scal(p);
+    const int64_t nblk = nvox / NT;
+    uint4 v[P];
+    auto load = [&](int64_t blk) {
+#pragma unroll
+        for (int u = 0; u < P; ++u) v[u] = reinterpret_cast<const uint4 *>(x + blk * NT * C)[min(tid + u * NT, N - 1)];
+    };
+    if (blockIdx.x < nblk) load(blockIdx.x);
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int64_t v0 = blk * NT;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < P; ++u)
+            if (tid + u * NT < N) reinterpret_cast<uint4 *>(xs)[tid + u * NT] = v[u];
+        if (blk + gridDim.x < nblk) load(blk + gridDim.x);
+        __syncthreads();
+        float uu[C];
+        const uint32_t *xr = reinterpret_cast<const uint32_t *>(xs + tid * C);
+#pragma unroll
+        for (int j = 0; j < C / 2; ++j) {
+            const uint32_t q = xr[j];
+            uu[2 * j] = elu(bf(q & 0xffffu) + s.b1a) + s.b1b;
+            uu[2 * j + 1] = elu(bf(q >> 16) + s.b1a) + s.b1b;
+        }
+#pragma unroll
+        for (int o = 0; o < BR; ++o) {
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], uu[c], acc);
+            ts[tid * BR + o] = f2bf(elu(acc + s.b2a) + s.b2b);
+        }
+        __syncthreads();
+        constexpr int NO = NT * BR / 8;
+        for (int i = tid; i < NO; i += NT)
+            reinterpret_cast<uint4 *>(t2o + v0 * BR)[i] = reinterpret_cast<const uint4 *>(ts)[i];
+    }
+}
+
+// t3 and out of a TH x TW x 8 tile from t2 on its halo and x
+template <int TH, int TW>
+__global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restrict__ t2, const bf16_t *__restrict__ x,
+                                               const float *__restrict__ w2, const float *__restrict__ w3,
+                                               vq3d_preact_params p, bf16_t *__restrict__ t3o,
+                                               bf16_t *__restrict__ out) {
+    using T = Tile<TH, TW>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t *t2l = reinterpret_cast<bf16_t *>(smem);  // halo lines [NL][LSP]
+    bf16_t *t3s = t2l + T::LINES;                     // [TV][9]
+    bf16_t *xs = t3s + T::S9;                         // [TV][18]: x, then out in place
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row = lane & 15, kb = lane >> 4;
+    bf16x8 bw2[9], bw3[2];
+    {
+        float *w2s = reinterpret_cast<float *>(smem), *w3s = w2s + NW2;  // scratch over the halo image
+        static_assert(T::LINES * 2 >= (NW2 + C * BR) * 4, "weights fit the halo image");
+        stage_w(w2s, w2, NW2);
+        stage_w(w3s, w3, C * BR);
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) bw2[kk] = w2_frag<false>(w2s, kk, lane);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {  // W3 as B[k = o][n = co]
+            float v[8];
+            const int co = 16 * nt + row;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = 8 * kb + j;
+                v[j] = (o < BR && co < C) ? w3s[co * BR + o] : 0.f;
+            }
+            bw3[nt] = pack8(v);
+        }
+        __syncthreads();
+    }
+    {
+        bf16_t *tails[2] = {t3s, xs};
+        const int at[2] = {T::TV * BR, T::TV * C};
+        zero_pads<TH, TW>(t2l, 1, tails, at, 2);
+    }
+    const Scal s = load_scal(p);
+    // the next tile's loads are in flight while the current tile computes
+    LinesLd<TH, TW> lt;
+    TileLd<TH, TW, C> lx;
+    if (blockIdx.x < a.ntiles) {
+        const Org o0 = tile_org(a, blockIdx.x, TH, TW);
+        lt.load(a, o0, t2);
+        lx.load(a, o0, x);
+    }
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        const Org o = tile_org(a, tile, TH, TW);
+        __syncthreads();
+        lt.store(t2l);
+        lx.store(xs);
+        if (tile + int(gridDim.x) < a.ntiles) {
+            const Org on = tile_org(a, tile + gridDim.x, TH, TW);
+            lt.load(a, on, t2);
+            lx.load(a, on, x);
+        }
+        __syncthreads();
+        // t3 = elu(W2 (*) t2 + b3a) + b3b: 16-voxel x 9-channel tiles, 9 windowed k-steps
+        for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+            const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
+            const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 9; ++kk)
+                acc = mfma(read8(t2l, base + ((kk / 3) * T::LW + kk % 3) * LSP), bw2[kk], acc);
+            if (row < BR) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    t3s[(mt * 16 + 4 * kb + j) * BR + row] = f2bf(elu(acc[j] + s.b3a) + s.b3b);
+            }
+        }
+        __syncthreads();
+        // out = scale * W3 t3 + b4 + x (in place over x)
+        for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+            const bf16x8 af = read8(t3s, (mt * 16 + row) * BR + 8 * kb);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const f32x4 acc = mfma(af, bw3[nt], f32x4{0.f, 0.f, 0.f, 0.f});
+                const int co = 16 * nt + row;
+                if (co < C) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int xi = (mt * 16 + 4 * kb + j) * C + co;
+                        xs[xi] = f2bf(acc[j] * s.sc + s.b4 + bf(xs[xi]));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        store_tile<TH, TW, BR>(a, o, t3s, t3o);
+        store_tile<TH, TW, C>(a, o, xs, out);
+    }
+}
+
+// ============================================================================================ backward
+// K1: gz3 = bf16(scale * W3^T g * elu'(t3 - b3b)); G3 = sum g (x) t3 (matrix cores, voxels as
+// the reduction axis), sums of g (b4), of scale W3^T g (b3b), of gz3 (b3a) and of g . (W3 t3)
+// (scale).  Blocks of 256 voxels; the next block's loads are in flight during the current one.
+__global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__restrict__ g,
+                                                const bf16_t *__restrict__ t3, const float *__restrict__ w3,
+                                                vq3d_preact_params p, bf16_t *__restrict__ gz3o,
+                                                float *__restrict__ part) {
+    __shared__ float w3s[C * BR];
+    __shared__ __attribute__((aligned(16))) bf16_t gs[NT * C + SPAD];
+    __shared__ __attribute__((aligned(16))) bf16_t ts[NT * BR + SPAD];
+    __shared__ __attribute__((aligned(16))) bf16_t zs[NT * BR];
+    __shared__ float red[4 * 2 * 64 * 4];
+    constexpr int NG = NT * C / 8, NTT = NT * BR / 8, PG = (NG + NT - 1) / NT, PT = (NTT + NT - 1) / NT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    stage_w(w3s, w3, C * BR);
+    for (int i = tid; i < SPAD; i += NT) {
+        gs[NT * C + i] = 0;
+        ts[NT * BR + i] = 0;
+    }
+    const Scal s = load_scal(p);
+    float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int64_t nblk = nvox / NT;
+    uint4 vg[PG], vt[PT];
+    auto load = [&](int64_t blk) {
+        const int64_t v0 = blk * NT;
+#pragma unroll
+        for (int u = 0; u < PG; ++u) vg[u] = reinterpret_cast<const uint4 *>(g + v0 * C)[min(tid + u * NT, NG - 1)];
+#pragma unroll
+        for (int u = 0; u < PT; ++u) vt[u] = reinterpret_cast<const uint4 *>(t3 + v0 * BR)[min(tid + u * NT, NTT - 1)];
+    };
+    if (blockIdx.x < nblk) load(blockIdx.x);
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const int64_t v0 = blk * NT;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PG; ++u)
+            if (tid + u * NT < NG) reinterpret_cast<uint4 *>(gs)[tid + u * NT] = vg[u];
+#pragma unroll
+        for (int u = 0; u < PT; ++u)
+            if (tid + u * NT < NTT) reinterpret_cast<uint4 *>(ts)[tid + u * NT] = vt[u];
+        if (blk + gridDim.x < nblk) load(blk + gridDim.x);
+        __syncthreads();
+        {
+            float gv[C], tv[BR];
+            const uint32_t *gr = reinterpret_cast<const uint32_t *>(gs + tid * C);
+#pragma unroll
+            for (int j = 0; j < C / 2; ++j) {
+                const uint32_t q = gr[j];
+                gv[2 * j] = bf(q & 0xffffu);
+                gv[2 * j + 1] = bf(q >> 16);
+                s4 += gv[2 * j] + gv[2 * j + 1];
+            }
+#pragma unroll
+            for (int o = 0; o < BR; ++o) tv[o] = bf(ts[tid * BR + o]);
+#pragma unroll
+            for (int o = 0; o < BR; ++o) {
+                float a3 = 0.f;
+#pragma unroll
+                for (int co = 0; co < C; ++co) a3 = fmaf(w3s[co * BR + o], gv[co], a3);
+                const float gt3 = a3 * s.sc;
+                const float z = gt3 * elu_d_act(tv[o], s.b3b);
+                s3b += gt3;
+                s3a += z;
+                ssc = fmaf(a3, tv[o], ssc);  // sum_co g[co] (W3 t3)[co] == sum_o t3[o] (W3^T g)[o]
+                zs[tid * BR + o] = f2bf(z);
+            }
+        }
+        // G3[o][co] += sum_v t3[v][o] g[v][co]: wave w takes voxels 64 w .. 64 w + 63 (2 k-steps)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int vb = wave * 64 + ks * 32 + 8 * kb;
+            const bf16x8 af = gather8(ts, vb * BR + row, BR, row < BR);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int co = 16 * nt + row;
+                acc[nt] = mfma(af, gather8(gs, vb * C + co, C, co < C), acc[nt]);
+            }
+        }
+        __syncthreads();
+        constexpr int NO = NT * BR / 8;
+        for (int i = tid; i < NO; i += NT)
+            reinterpret_cast<uint4 *>(gz3o + v0 * BR)[i] = reinterpret_cast<const uint4 *>(zs)[i];
+    }
+    // workgroup partials: the 4 waves' accumulators summed in a fixed order
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[((wave * 2 + nt) * 64 + lane) * 4 + j] = acc[nt][j];
+    __syncthreads();
+    float *dst = part + int64_t(blockIdx.x) * NE1;
+    for (int e = tid; e < 2 * 64 * 4; e += NT) {
+        const int nt = e / 256, l = (e / 4) % 64, j = e % 4;
+        const int o = 4 * (l >> 4) + j, co = 16 * nt + (l & 15);
+        if (o < BR && co < C) {
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) t += red[((w * 2 + nt) * 64 + l) * 4 + j];
+            dst[co * BR + o] = t;
+        }
+    }
+    __syncthreads();
+    const float t4 = block_sum<float, NT>(s4, red);
+    const float t3b = block_sum<float, NT>(s3b, red + 8);
+    const float t3a = block_sum<float, NT>(s3a, red + 16);
+    const float tsc = block_sum<float, NT>(ssc, red + 24);
+    if (tid == 0) {
+        dst[C * BR] = t4;
+        dst[C * BR + 1] = t3b;
+        dst[C * BR + 2] = t3a;
+        dst[C * BR + 3] = tsc;
+    }
+}
+
+// K2: per TH x TW x 8 tile (see the file comment)
+template <int TH, int TW>
+__global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restrict__ gz3, const bf16_t *__restrict__ t2,
+                                                const bf16_t *__restrict__ x, const bf16_t *__restrict__ g,
+                                                const float *__restrict__ w1, const float *__restrict__ w2,
+                                                vq3d_preact_params p, bf16_t *__restrict__ gx,
+                                                float *__restrict__ part) {
+    using T = Tile<TH, TW>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t *zl = reinterpret_cast<bf16_t *>(smem);  // gz3 halo lines
+    bf16_t *tl = zl + T::LINES;                       // t2 halo lines
+    bf16_t *z1s = tl + T::LINES;                      // gz1 [TV][9]
+    bf16_t *xs = z1s + T::S9;                         // x [TV][18], then u1 in place
+    bf16_t *gs = xs + T::S18;                         // g [TV][18], then gx in place
+    float *w1s = reinterpret_cast<float *>(gs + T::S18);  // W1 [o][c]
+    float *red = reinterpret_cast<float *>(smem);         // after the tiles: [4][2][64][4] cross-wave sums
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int row = lane & 15, kb = lane >> 4;
+    bf16x8 bw2[9];
+    {
+        float *w2s = reinterpret_cast<float *>(smem);  // scratch over the halo images
+        stage_w(w2s, w2, NW2);
+        stage_w(w1s, w1, BR * C);
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) bw2[kk] = w2_frag<true>(w2s, kk, lane);
+        __syncthreads();
+    }
+    {
+        bf16_t *tails[3] = {z1s, xs, gs};
+        const int at[3] = {T::TV * BR, T::TV * C, T::TV * C};
+        zero_pads<TH, TW>(zl, 2, tails, at, 3);
+    }
+    const Scal s = load_scal(p);
+    // W2 gradient accumulators: wave w owns tap rows kk = w, w + 4, w + 8 (< 9), 2 column tiles
+    // of the 27-element window each; W1 gradient: 2 column tiles (18 channels)
+    f32x4 aw2[3][2], aw1[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) aw2[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    aw1[0] = aw1[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
+    // the next tile's halo loads are in flight while the current tile computes (x / g of the
+    // current tile are loaded at the top: prefetching them too costs the second wave per SIMD)
+    LinesLd<TH, TW> lz, lt;
+    if (blockIdx.x < a.ntiles) {
+        const Org o0 = tile_org(a, blockIdx.x, TH, TW);
+        lz.load(a, o0, gz3);
+        lt.load(a, o0, t2);
+    }
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        const Org o = tile_org(a, tile, TH, TW);
+        __syncthreads();
+        {
+            TileLd<TH, TW, C> lx, lg;
+            lx.load(a, o, x);
+            lg.load(a, o, g);
+            lz.store(zl);
+            lt.store(tl);
+            if (tile + int(gridDim.x) < a.ntiles) {
+                const Org on = tile_org(a, tile + gridDim.x, TH, TW);
+                lz.load(a, on, gz3);
+                lt.load(a, on, t2);
+            }
+            lx.store(xs);
+            lg.store(gs);
+        }
+        __syncthreads();
+        // gt2 = W2^T (*) gz3 (flipped taps) -> gz1 = bf16(gt2 * elu'(t2 - b2b))
+        for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+            const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
+            const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 9; ++kk)
+                acc = mfma(read8(zl, base + ((kk / 3) * T::LW + kk % 3) * LSP), bw2[kk], acc);
+            if (row < BR) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int v = mt * 16 + 4 * kb + j, rr = v >> 3, dd = v & 7;
+                    const float t2v = bf(tl[((rr / TW + 1) * T::LW + rr % TW + 1) * LSP + LINT + 9 * dd + row]);
+                    const float z1 = acc[j] * elu_d_act(t2v, s.b2b);
+                    s2b += acc[j];
+                    s2a += z1;
+                    z1s[v * BR + row] = f2bf(z1);
+                }
+            }
+        }
+        // W2 gradient: dW2[co][kk][e] += sum_v gz3[v][co] * t2window(kk)[v][e], k-steps of 32
+        // voxels = 4 D-runs
+#pragma unroll 1
+        for (int ks = 0; ks < T::TV / 32; ++ks) {
+            const int r = ks * 4 + kb;
+            const int lbase = ((r / TW) * T::LW + r % TW) * LSP;
+            const bf16x8 af = gather8(zl, lbase + (T::LW + 1) * LSP + LINT + row, BR, row < BR);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                asm volatile("" ::: "memory");  // one tap row's gathers in flight at a time (registers)
+                const int kk = wave + 4 * i;
+                if (kk < 9) {
+                    const int off = lbase + ((kk / 3) * T::LW + kk % 3) * LSP + LOFF;
+#pragma unroll
+                    for (int n = 0; n < 2; ++n) {
+                        const int e = 16 * n + row;
+                        aw2[i][n] = mfma(af, gather8(tl, off + e, BR, e < 27), aw2[i][n]);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // gx = g + (W1^T gz1) * elu'(x + b1a); u1 = elu(x + b1a) + b1b in place over x
+        for (int v = tid; v < T::TV; v += NT) {
+            float z1[BR];
+#pragma unroll
+            for (int oo = 0; oo < BR; ++oo) z1[oo] = bf(z1s[v * BR + oo]);
+            uint32_t *xr = reinterpret_cast<uint32_t *>(xs + v * C);
+            uint32_t *gr = reinterpret_cast<uint32_t *>(gs + v * C);
+#pragma unroll 1
+            for (int j = 0; j < C / 2; ++j) {
+                const uint32_t xq = xr[j], gq = gr[j];
+                float r2[2], u2[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int c = 2 * j + h;
+                    float gt1 = 0.f;
+#pragma unroll
+                    for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1s[oo * C + c], z1[oo], gt1);
+                    const float zx = bf(h ? (xq >> 16) : (xq & 0xffffu)) + s.b1a;
+                    const float ez = zx > 0.f ? 1.f : expf(zx);
+                    s1b += gt1;
+                    s1a += gt1 * ez;
+                    r2[h] = bf(h ? (gq >> 16) : (gq & 0xffffu)) + gt1 * ez;
+                    u2[h] = (zx > 0.f ? zx : ez - 1.f) + s.b1b;
+                }
+                gr[j] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
+                xr[j] = uint32_t(f2bf(u2[0])) | (uint32_t(f2bf(u2[1])) << 16);
+            }
+        }
+        __syncthreads();
+        // W1 gradient: dW1[o][c] += sum_v gz1[v][o] u1[v][c]; wave w takes k-steps w, w + 4, ...
+        for (int ks = wave; ks < T::TV / 32; ks += NT / 64) {
+            const int vb = ks * 32 + 8 * kb;
+            const bf16x8 af = gather8(z1s, vb * BR + row, BR, row < BR);
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const int c = 16 * n + row;
+                aw1[n] = mfma(af, gather8(xs, vb * C + c, C, c < C), aw1[n]);
+            }
+        }
+        store_tile<TH, TW, C>(a, o, gs, gx);
+    }
+    // workgroup partials [entry]: W2 in nn.Conv3d order [co][ci][tap], W1 [o][c], then scalars
+    static_assert(2 * T::LINES * 2 >= 4 * 2 * 64 * 4 * 4, "cross-wave sums fit the halo images");
+    float *dst = part + int64_t(blockIdx.x) * NE2;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int kk = wave + 4 * i;
+        if (kk < 9) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const int e = 16 * n + row;
+                if (e < 27) {
+                    const int kd = e / 9, ci = e - 9 * kd;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int co = 4 * kb + j;
+                        if (co < BR) dst[(co * BR + ci) * 27 + kk * 3 + kd] = aw2[i][n][j];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[((wave * 2 + n) * 64 + lane) * 4 + j] = aw1[n][j];
+    __syncthreads();
+    for (int e = tid; e < 2 * 64 * 4; e += NT) {
+        const int n = e / 256, l = (e / 4) % 64, j = e % 4;
+        const int oo = 4 * (l >> 4) + j, c = 16 * n + (l & 15);
+        if (oo < BR && c < C) {
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) t += red[((w * 2 + n) * 64 + l) * 4 + j];
+            dst[NW2 + oo * C + c] = t;
+        }
+    }
+    __syncthreads();
+    const float t2b = block_sum<float, NT>(s2b, red);
+    const float t2a = block_sum<float, NT>(s2a, red + 8);
+    const float t1b = block_sum<float, NT>(s1b, red + 16);
+    const float t1a = block_sum<float, NT>(s1a, red + 24);
+    if (tid == 0) {
+        dst[NW2 + BR * C] = t2b;
+        dst[NW2 + BR * C + 1] = t2a;
+        dst[NW2 + BR * C + 2] = t1b;
+        dst[NW2 + BR * C + 3] = t1a;
+    }
+}
+
+// K3: every gradient entry summed over the workgroup partials in a fixed order and added into
+// its gradient buffer.  A workgroup owns 32 consecutive entries of one partial array: 8 row
+// groups x 32 entries, so each row read is one 128-B segment, then the 8 group sums in order.
+struct RedOut {
+    float *dw1, *dw2, *dw3, *db1a, *db1b, *db2a, *db2b, *db3a, *db3b, *dscale, *db4;
+    const float *scale;
+};
+
+constexpr int NB1 = (NE1 + 31) / 32, NB2 = (NE2 + 31) / 32;
+
+__global__ __launch_bounds__(NT) void k_pm_reduce(const float *__restrict__ p1, int n1, const float *__restrict__ p2,
+                                                  int n2, RedOut o) {
+    __shared__ float sm[8][32];
+    const int el = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    const bool first = blockIdx.x < NB1;
+    const int e = (first ? blockIdx.x : blockIdx.x - NB1) * 32 + el;
+    const float *P = first ? p1 : p2;
+    const int n = first ? n1 : n2, ne = first ? NE1 : NE2;
+    float t = 0.f;
+    if (e < ne)
+        for (int r = rg; r < n; r += 8) t += P[int64_t(r) * ne + e];
+    sm[rg][el] = t;
+    __syncthreads();
+    if (rg != 0 || e >= ne) return;
+    t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += sm[i][el];
+    if (first) {
+        if (e < C * BR) o.dw3[e] += *o.scale * t;
+        else if (e == C * BR) *o.db4 += t;
+        else if (e == C * BR + 1) *o.db3b += t;
+        else if (e == C * BR + 2) *o.db3a += t;
+        else *o.dscale += t;
+    } else {
+        if (e < NW2) o.dw2[e] += t;
+        else if (e < NW2 + BR * C) o.dw1[e - NW2] += t;
+        else if (e == NW2 + BR * C) *o.db2b += t;
+        else if (e == NW2 + BR * C + 1) *o.db2a += t;
+        else if (e == NW2 + BR * C + 2) *o.db1b += t;
+        else *o.db1a += t;
+    }
+}
+
+// ============================================================================================ host
+constexpr int FTH = 4, FTW = 8;  // forward tile 4 x 8 x 8 (256 voxels)
+constexpr int BTH = 4, BTW = 8;  // backward tile
+
+template <int TH, int TW>
+size_t fwd_lds() {
+    using T = Tile<TH, TW>;
+    return size_t(T::LINES + T::S9 + T::S18) * 2;
+}
+template <int TH, int TW>
+size_t bwd_lds() {
+    using T = Tile<TH, TW>;
+    return size_t(2 * T::LINES + T::S9 + 2 * T::S18) * 2 + size_t(BR * C) * 4;
+}
+
+int n_cu() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    }
+    return n;
+}
+
+template <class K>
+int resident(K kern, size_t lds) {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, NT, lds) != hipSuccess || per < 1) per = 1;
+    (void)hipGetLastError();
+    return per;
+}
+
+constexpr int kBwd1Blocks = 512;  // K1 workgroups (partial rows)
+
+PmArgs make_args(int B, int H, int W, int D, int TH, int TW) {
+    PmArgs a;
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    a.D = D;
+    a.nth = H / TH;
+    a.ntw = W / TW;
+    a.ntd = D / TD;
+    a.ntiles = B * a.nth * a.ntw * a.ntd;
+    return a;
+}
+
+int bwd2_blocks(const PmArgs &a) {
+    static int per = 0;
+    if (!per) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_bwd2<BTH, BTW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(bwd_lds<BTH, BTW>()));
+        per = resident(k_pm_bwd2<BTH, BTW>, bwd_lds<BTH, BTW>());
+    }
+    return std::max(1, std::min(a.ntiles, per * n_cu()));
 }
 
 }  // namespace
@@ -298,26 +840,69 @@ extern "C" {
 
 int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                               int32_t dd) {
-    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h % 16 == 0 && w % 16 == 0 &&
-           dd % BD == 0 && h > 0 && w > 0 && dd > 0;
+    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h >= 8 && w >= 8 && dd >= TD &&
+           h % 8 == 0 && w % 8 == 0 && dd % TD == 0 && int64_t(batch) * h * w * dd % NT == 0;
 }
 
 int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                         int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                         const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
     if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
-        return fail("preact_mid_fwd: shape outside the fused mid-level block kernel");
+        return fail("preact_mid_fwd: shape outside the fused mid-level block kernels");
     if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_mid_fwd: null pointer");
     hipStream_t s = as_stream(stream);
-    MidArgs a;
-    a.B = batch;
-    a.H = h;
-    a.W = w;
-    a.D = dd;
-    const bf16_t *xb = (const bf16_t *)x;
-    bf16_t *ob = (bf16_t *)out, *t2b = (bf16_t *)t2, *t3b = (bf16_t *)t3;
-    launch_mid<GeoWide>(a, s, xb, w1, w2, w3, *p, ob, t2b, t3b);
+    const int64_t nvox = int64_t(batch) * h * w * dd;
+    const unsigned g1 = unsigned(std::min<int64_t>(nvox / NT, 1024));
+    k_pm_t2<<<g1, NT, 0, s>>>(nvox, (const bf16_t *)x, w1, *p, (bf16_t *)t2);
+    const PmArgs a = make_args(batch, h, w, dd, FTH, FTW);
+    static int per = 0;
+    if (!per) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_fwd<FTH, FTW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(fwd_lds<FTH, FTW>()));
+        per = resident(k_pm_fwd<FTH, FTW>, fwd_lds<FTH, FTW>());
+    }
+    const unsigned g2 = unsigned(std::max(1, std::min(a.ntiles, per * n_cu())));
+    k_pm_fwd<FTH, FTW><<<g2, NT, fwd_lds<FTH, FTW>(), s>>>(a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, *p,
+                                                           (bf16_t *)t3, (bf16_t *)out);
     return check_launch("preact_mid_fwd");
+}
+
+size_t vq3d_preact_mid_workspace_bytes(int32_t batch, int32_t h, int32_t w, int32_t dd) {
+    const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
+    const size_t n2 = size_t(bwd2_blocks(a));
+    return (size_t(kBwd1Blocks) * NE1 + n2 * NE2) * 4 + size_t(batch) * h * w * dd * BR * 2 + 256;
+}
+
+int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                        int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
+                        const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                        void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
+    if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
+        return fail("preact_mid_bwd: shape outside the fused mid-level block kernels");
+    if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx || !workspace)
+        return fail("preact_mid_bwd: null pointer");
+    const vq3d_preact_grads &G = *gr;
+    if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||
+        !G.dbias3b || !G.dscale || !G.dbias4)
+        return fail("preact_mid_bwd: every gradient buffer is required");
+    if (workspace_bytes < vq3d_preact_mid_workspace_bytes(batch, h, w, dd))
+        return fail("preact_mid_bwd: workspace too small");
+    hipStream_t s = as_stream(stream);
+    const int64_t nvox = int64_t(batch) * h * w * dd;
+    const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
+    const int n2 = bwd2_blocks(a);
+    const int n1 = int(std::min<int64_t>(kBwd1Blocks, nvox / NT));
+    float *p1 = static_cast<float *>(workspace);
+    float *p2 = p1 + size_t(kBwd1Blocks) * NE1;
+    bf16_t *gz3 = reinterpret_cast<bf16_t *>(
+        (reinterpret_cast<uintptr_t>(p2 + size_t(n2) * NE2) + 255) & ~uintptr_t(255));
+    k_pm_bwd1<<<n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, gz3, p1);
+    k_pm_bwd2<BTH, BTW><<<n2, NT, bwd_lds<BTH, BTW>(), s>>>(a, gz3, (const bf16_t *)t2, (const bf16_t *)x,
+                                                             (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, p2);
+    RedOut o{G.dw1, G.dw2, G.dw3, G.dbias1a, G.dbias1b, G.dbias2a, G.dbias2b, G.dbias3a, G.dbias3b,
+             G.dscale, G.dbias4, p->scale};
+    k_pm_reduce<<<NB1 + NB2, NT, 0, s>>>(p1, n1, p2, n2, o);
+    return check_launch("preact_mid_bwd");
 }
 
 }  // extern "C"

@@ -79,10 +79,11 @@ class PreActBlockFn(torch.autograd.Function):
             return out
         if (blk.skip_conv is None and not up and k == 3 and s == 1
                 and ops.preact_mid_supported(x, blk.branch_conv1.weight.shape[0])):
-            # 18-channel level: fused forward (preact_mid.hip) writing t2 / t3 like the unfused
-            # convs, so the backward below is unchanged
+            # 18-channel level: fused forward (2 launches) and backward (3 launches),
+            # preact_mid.hip
             out, t2, t3 = ops.preact_mid_fwd(x, blk)
             ctx.blk = blk
+            ctx.mid = True
             ctx.save_for_backward(x, t2, t3, None)
             return out
         t2 = ops.conv_fwd(x, blk.branch_conv1.weight, g1, pro=(blk.bias1a, blk.bias1b), act=(blk.bias2a, blk.bias2b))
@@ -119,11 +120,12 @@ class PreActBlockFn(torch.autograd.Function):
             grads_ready(blk._fn_params)
             return (g_x, None) + (None,) * len(blk._fn_params)
         x, t2, t3, tup = ctx.saved_tensors
-        if ctx.small:
+        if ctx.small or getattr(ctx, "mid", False):
             names = {"dw1": blk.branch_conv1.weight, "dw2": blk.branch_conv2.weight, "dw3": blk.branch_conv3.weight,
                      "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
-            g_x = ops.preact_small_bwd(g, x, t2, t3, blk, {n: grad_buf(t) for n, t in names.items()})
+            bwd = ops.preact_small_bwd if ctx.small else ops.preact_mid_bwd
+            g_x = bwd(g, x, t2, t3, blk, {n: grad_buf(t) for n, t in names.items()})
             grads_ready(blk._fn_params)
             return (g_x, None) + (None,) * len(blk._fn_params)
         k, s, p, up = mode_geometry(blk.mode)

@@ -309,6 +309,22 @@ def preact_mid_fwd(x, blk):
     return out, t2, t3
 
 
+def preact_mid_bwd(g, x, t2, t3, blk, grads):
+    """gx of preact_mid_fwd; grads: dict name -> fp32 buffer (+=, all required), names as in
+    L.PreactGrads."""
+    b, c, h, w, d = x.shape
+    w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    nb = w1.shape[0]
+    gx = torch.empty_like(x, memory_format=CL)
+    ws = workspace(L.query("vq3d_preact_mid_workspace_bytes", b, h, w, d), x.device)
+    prm = _preact_params(blk)
+    gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
+    L.call("vq3d_preact_mid_bwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
+           L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws),
+           ctypes.c_size_t(ws.numel()), L.ptr(gx), L.stream())
+    return gx
+
+
 _small = [True, True]
 
 

@@ -150,16 +150,25 @@ int vq3d_preact_tiny_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t
                          const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                          const float *saved, float *workspace, void *gx, vq3d_stream_t stream);
 
-/* Forward of one whole PreActFixupResBlock (mode 'same', no skip conv) in one launch on the
- * 18-channel / branch-9 level (bf16, h % 16 == w % 16 == 0, d % 8 == 0): writes out and the
- * block's intermediates t2 = elu(W1 u1 + bias2a) + bias2b and t3 = elu(W2 (*) t2 + bias3a) + bias3b
- * ([B][H][W][D][branch] bf16, as the unfused convs' epilogues write them), so the backward is
- * the unfused one. */
+/* One whole PreActFixupResBlock (mode 'same', no skip conv) on the 18-channel / branch-9 level
+ * (bf16, h % 8 == w % 8 == 0, d % 8 == 0, batch*h*w*d % 256 == 0; the 50 decoder
+ * post-quantize blocks of the published model at 128x128x32).  Replaces the per-conv calls of
+ * layers.py:176-195 and their autograd backward for these blocks.
+ * Forward (two launches): writes out and the intermediates t2 = elu(W1 u1 + bias2a) + bias2b and
+ * t3 = elu(W2 (*) t2 + bias3a) + bias3b ([B][H][W][D][branch] bf16).
+ * Backward (three launches): writes gx and accumulates (+=) every parameter gradient of *gr (all
+ * required), deterministically (fixed-order workgroup partials), through a caller-owned
+ * workspace of vq3d_preact_mid_workspace_bytes. */
 int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                               int32_t dd);
 int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                         int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                         const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream);
+size_t vq3d_preact_mid_workspace_bytes(int32_t batch, int32_t h, int32_t w, int32_t dd);
+int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                        int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
+                        const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                        void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream);
 
 /* Whole PreActFixupResBlock (mode 'same', no skip conv) on few channels: (channels, branch) in
  * {(2, 1), (4, 2), (8, 4)}, bf16, power-of-two grid.  Forward in one launch writes out, t2 and t3

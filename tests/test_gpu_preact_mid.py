@@ -1,9 +1,16 @@
-"""Fused PreAct block forward of the 18-channel level (csrc/preact_mid.hip) against the per-conv
-engine path of the same block (bf16) and a float64 torch CPU restatement of the block
-(vqvae/layers.py:176-195): output, the saved intermediates t2 / t3 (checked through the
-backward, which reads them) and every gradient.  Tolerance 3e-2 of each tensor's max
-magnitude (bf16 activations; the fused kernel keeps the 3x3x3 weights in fp32 where the MFMA
-engine rounds them to bf16)."""
+"""Fused PreAct block of the 18-channel level (csrc/preact_mid.hip: forward 2 launches, backward
+3) against float64 torch-CPU restatements of vqvae/layers.py:176-195 and against the per-conv
+engine path of the same block:
+
+* strict: a float64 restatement that rounds to bf16 exactly where the kernels do (t2, t3, out;
+  gz3, gz1, gx; the matrix-core weights W2 / W3 and the W1-gradient operand u1) -- what remains
+  is fp32-vs-float64 summation order.  Tolerances: every tensor within 1e-2 of its max
+  magnitude, every scalar-parameter gradient within 2e-2 relative.
+* loose: the plain float64 block (no rounding), 3e-2 of the max for output / gx / weight grads
+  (bf16 activations).
+Shapes include the production one (1 x 18 x 128 x 128 x 32, the published model's decoder
+bottom level) and grids whose circular wrap lands inside the first / last tile.
+"""
 import numpy as np
 import pytest
 import torch
@@ -12,7 +19,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last_3d
-SHAPES = [(1, 18, 16, 16, 8), (1, 18, 32, 16, 16), (2, 18, 16, 32, 8)]
+SHAPES = [(1, 18, 8, 8, 8), (2, 18, 16, 8, 16), (1, 18, 32, 16, 16), (1, 18, 128, 128, 32)]
 
 
 def _block(seed):
@@ -30,17 +37,64 @@ def _block(seed):
     return blk
 
 
-def _ref(blk, x, gy):
-    P = {n: p.detach().double().cpu().clone().requires_grad_(True) for n, p in blk.named_parameters()}
-    x = x.detach().double().cpu().clone().requires_grad_(True)
+def rb(t):
+    """round float64 -> bf16 -> float64 (round-to-nearest-even, torch's conversion)"""
+    return t.float().bfloat16().double()
+
+
+def pad(t):
+    return F.pad(t, (1,) * 6, mode="circular")
+
+
+def _ref_strict(P, x, g):
+    """float64 block fwd + bwd with the kernels' bf16 rounding points."""
+    sc, b1a, b1b, b2a, b2b, b3a, b3b, b4 = (float(P[k]) for k in
+                                             ("scale", "bias1a", "bias1b", "bias2a", "bias2b", "bias3a", "bias3b", "bias4"))
+    w1, w2, w3 = P["branch_conv1.weight"], P["branch_conv2.weight"], P["branch_conv3.weight"]
+    w2r, w3r = rb(w2), rb(w3)
+    u1 = F.elu(x + b1a) + b1b
+    t2 = rb(F.elu(F.conv3d(u1, w1) + b2a) + b2b)
+    t2v = t2.clone().requires_grad_(True)
+    w2v = w2.clone().requires_grad_(True)
+    h2 = F.conv3d(pad(t2v), w2v)
+    t3 = rb(F.elu(F.conv3d(pad(t2), w2r) + b3a) + b3b)
+    o3 = F.conv3d(t3, w3r)
+    out = rb(o3 * sc + b4 + x)
+    # backward
+    G3 = torch.einsum("bchwd,bohwd->co", g, t3)
+    gt3 = sc * F.conv3d(g, w3.permute(1, 0, 2, 3, 4))
+    d3 = torch.where(t3 - b3b > 0, torch.ones_like(t3), t3 - b3b + 1)
+    z3 = gt3 * d3
+    gz3 = rb(z3)
+    gt2 = torch.autograd.grad(F.conv3d(pad(t2v), w2r), t2v, gz3)[0]
+    dw2 = torch.autograd.grad(h2, w2v, gz3)[0]
+    d2 = torch.where(t2 - b2b > 0, torch.ones_like(t2), t2 - b2b + 1)
+    z1 = gt2 * d2
+    gz1 = rb(z1)
+    gt1 = F.conv3d(gz1, w1.permute(1, 0, 2, 3, 4))
+    e1 = torch.where(x + b1a > 0, torch.ones_like(x), torch.exp(x + b1a))
+    gx = rb(g + gt1 * e1)
+    grads = {
+        "branch_conv3.weight": (sc * G3)[..., None, None, None], "scale": (w3[..., 0, 0, 0] * G3).sum().reshape(1),
+        "bias4": g.sum().reshape(1), "bias3b": gt3.sum().reshape(1), "bias3a": z3.sum().reshape(1),
+        "branch_conv2.weight": dw2, "bias2b": gt2.sum().reshape(1), "bias2a": z1.sum().reshape(1),
+        "branch_conv1.weight": torch.einsum("bohwd,bchwd->oc", gz1, rb(u1))[..., None, None, None],
+        "bias1b": gt1.sum().reshape(1), "bias1a": (gt1 * e1).sum().reshape(1),
+    }
+    return out, gx, grads
+
+
+def _ref_loose(P, x, g):
+    P = {n: p.clone().requires_grad_(True) for n, p in P.items()}
+    x = x.clone().requires_grad_(True)
     h = F.elu(x + P["bias1a"])
     h = F.conv3d(h + P["bias1b"], P["branch_conv1.weight"])
     h = F.elu(h + P["bias2a"])
-    h = F.conv3d(F.pad(h + P["bias2b"], (1,) * 6, mode="circular"), P["branch_conv2.weight"])
+    h = F.conv3d(pad(h + P["bias2b"]), P["branch_conv2.weight"])
     h = F.elu(h + P["bias3a"])
     h = F.conv3d(h + P["bias3b"], P["branch_conv3.weight"])
     out = h * P["scale"] + P["bias4"] + x
-    out.backward(gy.detach().double().cpu())
+    out.backward(g)
     return out.detach(), x.grad, {n: p.grad for n, p in P.items()}
 
 
@@ -69,21 +123,45 @@ def _run(blk, x, gy, dev, mid):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_fused_mid_block_forward(gpu, shape):
+def test_fused_mid_block(gpu, shape):
     from vq3d import ops
     blk = _block(seed=shape[2] + shape[4])
     g = torch.Generator().manual_seed(11)
-    x = torch.randn(shape, generator=g).bfloat16().float()
-    gy = torch.randn(shape, generator=g).bfloat16().float()
+    x = torch.randn(shape, generator=g).bfloat16().double()
+    gy = torch.randn(shape, generator=g).bfloat16().double()
     xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
     assert ops.preact_mid_supported(xg, 9)
-    ry, rgx, rgp = _ref(blk, x, gy)
+    P = {n: p.detach().double().clone() for n, p in blk.named_parameters()}
+    sy, sgx, sgp = _ref_strict(P, x, gy)
     y1, gx1, gp1 = _run(blk, x, gy, gpu, mid=True)
-    y0, gx0, gp0 = _run(blk, x, gy, gpu, mid=False)
-    errs = {"y": rel(y1, ry), "gx": rel(gx1, rgx), "y_vs_engines": rel(y1, y0), "gx_vs_engines": rel(gx1, gx0)}
-    for n in rgp:
-        errs["grad/" + n] = rel(gp1[n], rgp[n])
-    tol = 3e-2
-    small = {"grad/" + n for n, p in blk.named_parameters() if p.numel() == 1}
-    bad = {k: v for k, v in errs.items() if not v <= (0.5 if k in small else tol)}
+    errs = {"y": rel(y1, sy), "gx": rel(gx1, sgx)}
+    for n in sgp:
+        errs["grad/" + n] = rel(gp1[n], sgp[n].reshape(gp1[n].shape))
+    scal = {"grad/" + n for n, p in blk.named_parameters() if p.numel() == 1}
+    bad = {k: v for k, v in errs.items() if not v <= (2e-2 if k in scal else 1e-2)}
+    print(shape, "strict", {k: f"{v:.2e}" for k, v in errs.items()})
     assert not bad, bad
+    if shape[2] * shape[3] * shape[4] <= 16 * 16 * 16:
+        ly, lgx, lgp = _ref_loose(P, x, gy)
+        y0, gx0, gp0 = _run(blk, x, gy, gpu, mid=False)
+        loose = {"y": rel(y1, ly), "gx": rel(gx1, lgx), "y_vs_engines": rel(y1, y0), "gx_vs_engines": rel(gx1, gx0)}
+        for n in lgp:
+            if n not in {k[5:] for k in scal}:
+                loose["grad/" + n] = rel(gp1[n], lgp[n])
+                loose["grad_vs_engines/" + n] = rel(gp1[n], gp0[n])
+        bad = {k: v for k, v in loose.items() if not v <= 3e-2}
+        assert not bad, bad
+
+
+def test_fused_mid_block_deterministic(gpu):
+    """Two backward passes give bit-identical gradients (fixed-order partial reductions)."""
+    blk = _block(seed=3)
+    g = torch.Generator().manual_seed(5)
+    shape = (1, 18, 32, 32, 16)
+    x = torch.randn(shape, generator=g).bfloat16().double()
+    gy = torch.randn(shape, generator=g).bfloat16().double()
+    a = _run(blk, x, gy, gpu, mid=True)
+    b = _run(blk, x, gy, gpu, mid=True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n
