@@ -265,52 +265,54 @@ __device__ __forceinline__ void zero_pads(bf16_t *lines, int nimg, bf16_t *const
 }
 
 // ============================================================================================ forward
-// t2 = elu(W1 (elu(x + b1a) + b1b) + b2a) + b2b, 256 voxels per workgroup iteration (the next
-// block's x in flight during the current one)
+// t2 = elu(W1 (elu(x + b1a) + b1b) + b2a) + b2b.  A thread owns a PAIR of voxels: 72 bytes of x
+// (9 8-byte loads, all issued before any math) in, 36 bytes of t2 (9 dword stores) out; no LDS
+// staging, no barriers.  W1 is broadcast from LDS.
 __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__restrict__ x,
                                               const float *__restrict__ w1, vq3d_preact_params p,
                                               bf16_t *__restrict__ t2o) {
     __shared__ float w1s[BR * C];
-    __shared__ __attribute__((aligned(16))) bf16_t xs[NT * C];
-    __shared__ __attribute__((aligned(16))) bf16_t ts[NT * BR];
-    constexpr int N = NT * C / 8, P = (N + NT - 1) / NT;
-    const int tid = threadIdx.x;
     stage_w(w1s, w1, BR * C);
+    __syncthreads();
     const Scal s = load_scal(p);
-    const int64_t nblk = nvox / NT;
-    uint4 v[P];
-    auto load = [&](int64_t blk) {
+    const int64_t npair = nvox / 2;
+    for (int64_t q = int64_t(blockIdx.x) * NT + threadIdx.x; q < npair; q += int64_t(gridDim.x) * NT) {
+        uint2 v[C / 2];
+        const uint2 *src = reinterpret_cast<const uint2 *>(x + q * 2 * C);
 #pragma unroll
-        for (int u = 0; u < P; ++u) v[u] = reinterpret_cast<const uint4 *>(x + blk * NT * C)[min(tid + u * NT, N - 1)];
-    };
-    if (blockIdx.x < nblk) load(blockIdx.x);
-    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const int64_t v0 = blk * NT;
-        __syncthreads();
+        for (int j = 0; j < C / 2; ++j) v[j] = src[j];
+        uint32_t outw[BR];
 #pragma unroll
-        for (int u = 0; u < P; ++u)
-            if (tid + u * NT < N) reinterpret_cast<uint4 *>(xs)[tid + u * NT] = v[u];
-        if (blk + gridDim.x < nblk) load(blk + gridDim.x);
-        __syncthreads();
-        float uu[C];
-        const uint32_t *xr = reinterpret_cast<const uint32_t *>(xs + tid * C);
+        for (int h = 0; h < 2; ++h) {
+            asm volatile("" ::: "memory");  // W1 re-read from LDS per voxel (not held in 162 registers)
+            float uu[C];
 #pragma unroll
-        for (int j = 0; j < C / 2; ++j) {
-            const uint32_t q = xr[j];
-            uu[2 * j] = elu(bf(q & 0xffffu) + s.b1a) + s.b1b;
-            uu[2 * j + 1] = elu(bf(q >> 16) + s.b1a) + s.b1b;
+            for (int c = 0; c < C; ++c) {
+                const int e = h * C + c;  // element of the 36 bf16 of the pair
+                const uint2 w = v[e / 4];
+                const uint32_t d = (e & 2) ? w.y : w.x;
+                uu[c] = elu(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b;
+            }
+            float t2v[BR];
+#pragma unroll
+            for (int o = 0; o < BR; ++o) {
+                asm volatile("" ::: "memory");  // one W1 row (18 floats) in registers at a time
+                float acc = 0.f;
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], uu[c], acc);
+                t2v[o] = elu(acc + s.b2a) + s.b2b;
+            }
+#pragma unroll
+            for (int o = 0; o < BR; ++o) {
+                const uint32_t hb = f2bf(t2v[o]);
+                const int e = h * BR + o;  // element of the 18 bf16 of the pair's t2
+                if (e & 1) outw[e / 2] |= hb << 16;
+                else outw[e / 2] = hb;
+            }
         }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(t2o + q * 2 * BR);
 #pragma unroll
-        for (int o = 0; o < BR; ++o) {
-            float acc = 0.f;
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], uu[c], acc);
-            ts[tid * BR + o] = f2bf(elu(acc + s.b2a) + s.b2b);
-        }
-        __syncthreads();
-        constexpr int NO = NT * BR / 8;
-        for (int i = tid; i < NO; i += NT)
-            reinterpret_cast<uint4 *>(t2o + v0 * BR)[i] = reinterpret_cast<const uint4 *>(ts)[i];
+        for (int j = 0; j < BR; ++j) dst[j] = outw[j];
     }
 }
 
@@ -847,13 +849,21 @@ int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, in
 int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                         int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                         const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
+    return vq3d_preact_mid_fwd_stages(3, dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, p, out, t2, t3,
+                                      stream);
+}
+
+int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                               int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
+                               const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,
+                               vq3d_stream_t stream) {
     if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
         return fail("preact_mid_fwd: shape outside the fused mid-level block kernels");
     if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_mid_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     const int64_t nvox = int64_t(batch) * h * w * dd;
-    const unsigned g1 = unsigned(std::min<int64_t>(nvox / NT, 1024));
-    k_pm_t2<<<g1, NT, 0, s>>>(nvox, (const bf16_t *)x, w1, *p, (bf16_t *)t2);
+    const unsigned g1 = unsigned(std::max<int64_t>(1, std::min<int64_t>(nvox / 2 / NT, 2048)));
+    if (stages & 1) k_pm_t2<<<g1, NT, 0, s>>>(nvox, (const bf16_t *)x, w1, *p, (bf16_t *)t2);
     const PmArgs a = make_args(batch, h, w, dd, FTH, FTW);
     static int per = 0;
     if (!per) {
@@ -862,7 +872,8 @@ int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
         per = resident(k_pm_fwd<FTH, FTW>, fwd_lds<FTH, FTW>());
     }
     const unsigned g2 = unsigned(std::max(1, std::min(a.ntiles, per * n_cu())));
-    k_pm_fwd<FTH, FTW><<<g2, NT, fwd_lds<FTH, FTW>(), s>>>(a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, *p,
+    if (stages & 2)
+        k_pm_fwd<FTH, FTW><<<g2, NT, fwd_lds<FTH, FTW>(), s>>>(a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, *p,
                                                            (bf16_t *)t3, (bf16_t *)out);
     return check_launch("preact_mid_fwd");
 }
@@ -877,6 +888,15 @@ int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                         const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                         void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
+    return vq3d_preact_mid_bwd_stages(7, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, p, gr,
+                                      workspace, workspace_bytes, gx, stream);
+}
+
+int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                               int32_t h, int32_t w, int32_t dd, const void *g, const void *x, const void *t2,
+                               const void *t3, const float *w1, const float *w2, const float *w3,
+                               const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
+                               size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
     if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
         return fail("preact_mid_bwd: shape outside the fused mid-level block kernels");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx || !workspace)
@@ -896,12 +916,13 @@ int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
     float *p2 = p1 + size_t(kBwd1Blocks) * NE1;
     bf16_t *gz3 = reinterpret_cast<bf16_t *>(
         (reinterpret_cast<uintptr_t>(p2 + size_t(n2) * NE2) + 255) & ~uintptr_t(255));
-    k_pm_bwd1<<<n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, gz3, p1);
-    k_pm_bwd2<BTH, BTW><<<n2, NT, bwd_lds<BTH, BTW>(), s>>>(a, gz3, (const bf16_t *)t2, (const bf16_t *)x,
+    if (stages & 1) k_pm_bwd1<<<n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, gz3, p1);
+    if (stages & 2)
+        k_pm_bwd2<BTH, BTW><<<n2, NT, bwd_lds<BTH, BTW>(), s>>>(a, gz3, (const bf16_t *)t2, (const bf16_t *)x,
                                                              (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, p2);
     RedOut o{G.dw1, G.dw2, G.dw3, G.dbias1a, G.dbias1b, G.dbias2a, G.dbias2b, G.dbias3a, G.dbias3b,
              G.dscale, G.dbias4, p->scale};
-    k_pm_reduce<<<NB1 + NB2, NT, 0, s>>>(p1, n1, p2, n2, o);
+    if (stages & 4) k_pm_reduce<<<NB1 + NB2, NT, 0, s>>>(p1, n1, p2, n2, o);
     return check_launch("preact_mid_bwd");
 }
 

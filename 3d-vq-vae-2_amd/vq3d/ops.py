@@ -294,34 +294,50 @@ def preact_mid_supported(x, branch):
     return _mid[0] and bool(L.query("vq3d_preact_mid_supported", L.dtype_code(x), b, c, branch, h, w, d))
 
 
-def preact_mid_fwd(x, blk):
-    """Fused PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last)."""
+def preact_mid_fwd(x, blk, stages=None, bufs=None):
+    """Fused PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last).
+    stages / bufs: measurement only (vq3d_preact_mid_fwd_stages, preallocated outputs)."""
     x = as_cl(x)
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     nb = w1.shape[0]
-    out = torch.empty_like(x, memory_format=CL)
-    t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
-    t3 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    if bufs is None:
+        out = torch.empty_like(x, memory_format=CL)
+        t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
+        t3 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    else:
+        out, t2, t3 = bufs
     prm = _preact_params(blk)
-    L.call("vq3d_preact_mid_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3),
-           ctypes.byref(prm), L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+    args = (L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm),
+            L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+    if stages is None:
+        L.call("vq3d_preact_mid_fwd", *args)
+    else:
+        L.call("vq3d_preact_mid_fwd_stages", int(stages), *args)
     return out, t2, t3
 
 
-def preact_mid_bwd(g, x, t2, t3, blk, grads):
+def preact_mid_bwd(g, x, t2, t3, blk, grads, stages=None, bufs=None):
     """gx of preact_mid_fwd; grads: dict name -> fp32 buffer (+=, all required), names as in
-    L.PreactGrads."""
+    L.PreactGrads.  stages / bufs: measurement only (vq3d_preact_mid_bwd_stages, preallocated
+    gx and workspace)."""
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     nb = w1.shape[0]
-    gx = torch.empty_like(x, memory_format=CL)
-    ws = workspace(L.query("vq3d_preact_mid_workspace_bytes", b, h, w, d), x.device)
+    if bufs is None:
+        gx = torch.empty_like(x, memory_format=CL)
+        ws = workspace(L.query("vq3d_preact_mid_workspace_bytes", b, h, w, d), x.device)
+    else:
+        gx, ws = bufs
     prm = _preact_params(blk)
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
-    L.call("vq3d_preact_mid_bwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
-           L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws),
-           ctypes.c_size_t(ws.numel()), L.ptr(gx), L.stream())
+    args = (L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(w1), L.ptr(w2),
+            L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx),
+            L.stream())
+    if stages is None:
+        L.call("vq3d_preact_mid_bwd", *args)
+    else:
+        L.call("vq3d_preact_mid_bwd_stages", int(stages), *args)
     return gx
 
 

@@ -169,6 +169,18 @@ int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                         const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                         void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream);
+/* Measurement entries (bench.py's roofline probe, tools/block_micro.py): the same calls, launching
+ * only the kernels selected by `stages` (forward: bit 0 t2, bit 1 tile kernel; backward: bit 0
+ * pointwise gz3 kernel, bit 1 tile kernel, bit 2 reduction).  The product path uses the calls above. */
+int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                               int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
+                               const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,
+                               vq3d_stream_t stream);
+int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                               int32_t h, int32_t w, int32_t dd, const void *g, const void *x, const void *t2,
+                               const void *t3, const float *w1, const float *w2, const float *w3,
+                               const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
+                               size_t workspace_bytes, void *gx, vq3d_stream_t stream);
 
 /* Whole PreActFixupResBlock (mode 'same', no skip conv) on few channels: (channels, branch) in
  * {(2, 1), (4, 2), (8, 4)}, bf16, power-of-two grid.  Forward in one launch writes out, t2 and t3

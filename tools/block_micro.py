@@ -68,6 +68,15 @@ def main():
         kind = "small"
     else:
         raise SystemExit("no fused block kernel for this shape")
+    # calibration: torch copies of the block's input (18.9 MB at 128^2 x 32 x 18) and of a 4x
+    # larger buffer
+    big = torch.empty(x.numel() * 4, dtype=torch.bfloat16, device=dev)
+    big_dst = torch.empty_like(big)
+    xc = torch.empty_like(x)
+    tc = timed(lambda: xc.copy_(x), iters)
+    tcb = timed(lambda: big_dst.copy_(big), iters)
+    print(f"copy {x.numel() * 2 / 1e6:.1f} MB: {tc:7.1f} us ({2 * x.numel() * 2 / tc / 1e3:7.1f} GB/s r+w); "
+          f"copy {big.numel() * 2 / 1e6:.1f} MB: {tcb:7.1f} us ({2 * big.numel() * 2 / tcb / 1e3:7.1f} GB/s r+w)")
     tf = timed(fwd, iters)
     tb = timed(bwd, iters)
     nv = h * w * d
