@@ -1,0 +1,208 @@
+"""Training entry mirroring the reference's vqvae/train.py:14-59 on the vq3d path.
+
+    python -m vq3d.train DATASET [--batch-size 1] [model flags of VQVAE.add_model_specific_args]
+                         [--max_epochs N] [--max_steps N] [--default_root_dir DIR]
+                         [--resume_from_checkpoint last.ckpt]
+    python -m torch.distributed.run --nproc-per-node 8 -m vq3d.train DATASET ...   (one rank per GPU)
+
+What the reference gets from PyTorch-Lightning 1.2.10 (Trainer.from_argparse_args +
+ModelCheckpoint), restated here without that dependency:
+  * argument composition: Trainer flags (the subset the reference's jobs set), then
+    VQVAE.add_model_specific_args, then the script's own --rescale-input / --batch-size /
+    dataset_path, with the reference's set_defaults (train.py:25-40);
+  * seed_everything(42) (train.py:50): Python, numpy and torch RNGs;
+  * CTDataModule(path, batch_size, num_workers=5, rescale_input) (train.py:52);
+  * 'ddp': one process per GPU, DistributedSampler sharding, the bucketed RCCL gradient average
+    of vq3d.parallel (overlapped with backward) and the Quantizers' fused EMA all-reduce;
+  * validation every val_check_interval of an epoch (val_recon_loss_mean, eval mode);
+  * ModelCheckpoint(save_top_k=1, save_last=True, monitor='val_recon_loss_mean') (train.py:56):
+    last.ckpt after every validation, the best one as epoch=E-step=S.ckpt (PL 1.2 layout,
+    vq3d.checkpoint);
+  * --resume_from_checkpoint restores weights, codebooks, Adam state, epoch and global step;
+    last.ckpt is also written when training stops (max_steps / max_epochs).
+precision=16 is recorded (the path computes in bf16 activations per --compute-dtype).
+"""
+import os
+import random
+from argparse import ArgumentParser, Namespace
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from . import parallel
+from .checkpoint import load_checkpoint, save_checkpoint
+from .data import CTDataModule
+from .model import VQVAE
+
+
+def add_trainer_args(parser):
+    """The Trainer flags the reference's jobs use (pl.Trainer.add_argparse_args, train.py:17)."""
+    parser.add_argument("--gpus", type=str, default=None)
+    parser.add_argument("--accelerator", type=str, default=None)
+    parser.add_argument("--benchmark", type=bool, default=False)
+    parser.add_argument("--num_sanity_val_steps", type=int, default=2)
+    parser.add_argument("--precision", type=int, default=32)
+    parser.add_argument("--log_every_n_steps", type=int, default=50)
+    parser.add_argument("--val_check_interval", type=float, default=1.0)
+    parser.add_argument("--flush_logs_every_n_steps", type=int, default=100)
+    parser.add_argument("--weights_summary", type=str, default="top")
+    parser.add_argument("--max_epochs", type=int, default=1000)
+    parser.add_argument("--max_steps", type=int, default=None)
+    parser.add_argument("--default_root_dir", type=str, default=os.getcwd())
+    parser.add_argument("--resume_from_checkpoint", type=str, default=None)
+    parser.add_argument("--num_nodes", type=int, default=1)
+    return parser
+
+
+def build_parser():
+    parser = ArgumentParser()
+    parser = add_trainer_args(parser)
+    parser = VQVAE.add_model_specific_args(parser)
+    parser.add_argument('--rescale-input', type=int, nargs='+')
+    parser.add_argument("--batch-size", type=int)
+    parser.add_argument("dataset_path", type=Path)
+    parser.set_defaults(gpus="-1", accelerator='ddp', benchmark=True, num_sanity_val_steps=0, precision=16,
+                        log_every_n_steps=50, val_check_interval=0.5, flush_logs_every_n_steps=100,
+                        weights_summary='full', max_epochs=int(1e5))
+    return parser
+
+
+def parse_arguments(argv=None):
+    args = build_parser().parse_args(argv)
+    if isinstance(args.num_embeddings, int):
+        args.num_embeddings = [args.num_embeddings]
+    return args
+
+
+def seed_everything(seed=42):
+    """pl.trainer.seed_everything (train.py:50)."""
+    os.environ["PL_GLOBAL_SEED"] = str(seed)
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed_all(seed)
+    return seed
+
+
+class Checkpointer:
+    """ModelCheckpoint(save_top_k=1, save_last=True, monitor='val_recon_loss_mean')."""
+
+    def __init__(self, dirpath, monitor="val_recon_loss_mean"):
+        self.dirpath = Path(dirpath)
+        self.monitor = monitor
+        self.best_score = None
+        self.best_path = None
+
+    def state(self):
+        return {"monitor": self.monitor, "best_model_score": self.best_score, "best_model_path": self.best_path,
+                "dirpath": str(self.dirpath)}
+
+    def __call__(self, model, opt, epoch, step, score):
+        self.dirpath.mkdir(parents=True, exist_ok=True)
+        if score is not None and (self.best_score is None or score < self.best_score):
+            old = self.best_path
+            self.best_score = float(score)
+            self.best_path = str(self.dirpath / f"epoch={epoch}-step={step}.ckpt")
+            save_checkpoint(self.best_path, model, opt, epoch=epoch, global_step=step, callbacks={"ModelCheckpoint":
+                                                                                                  self.state()})
+            if old and old != self.best_path and os.path.exists(old):
+                os.remove(old)
+        save_checkpoint(str(self.dirpath / "last.ckpt"), model, opt, epoch=epoch, global_step=step,
+                        callbacks={"ModelCheckpoint": self.state()})
+
+
+def _to_device(batch, dev):
+    x, nvs = batch
+    return x.to(dev, non_blocking=True).float(), torch.as_tensor(nvs).to(dev)
+
+
+def validate(model, loader, dev):
+    model.eval()
+    tot, n = 0.0, 0
+    with torch.no_grad():
+        for batch in loader:
+            x, nvs = _to_device(batch, dev)
+            model.validation_step((x, nvs), n)
+            tot += float(model.logged["val_recon_loss_mean"])
+            n += 1
+    model.train()
+    if torch.distributed.is_initialized():
+        t = torch.tensor([tot, float(n)], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t)
+        tot, n = float(t[0]), int(t[1])
+    return tot / n if n else None
+
+
+def main(args: Namespace, datamodule=None):
+    """train.py:47-59."""
+    rank, world, _, dev = parallel.init_from_env()
+    if dev.type != "cuda":
+        raise RuntimeError("vq3d.train runs the HIP path: a GPU is required")
+    seed_everything(42)
+    if datamodule is None:
+        datamodule = CTDataModule(path=args.dataset_path, batch_size=args.batch_size, num_workers=5,
+                                  rescale_input=args.rescale_input)
+    datamodule.setup()
+    model = VQVAE(args).to(dev)
+    model.train()
+    opt = model.configure_optimizers()
+    reducer = parallel.GradientAllReduce(model)
+    ckpt = Checkpointer(Path(args.default_root_dir) / "checkpoints")
+    epoch0, step = 0, 0
+    if args.resume_from_checkpoint:
+        ck = load_checkpoint(args.resume_from_checkpoint)
+        model.load_state_dict(ck["state_dict"])
+        if ck.get("optimizer_states"):
+            opt.load_state_dict(ck["optimizer_states"][0])
+        epoch0, step = int(ck["epoch"]) + 1, int(ck["global_step"])
+        st = ck.get("callbacks", {}).get("ModelCheckpoint") or {}
+        ckpt.best_score, ckpt.best_path = st.get("best_model_score"), st.get("best_model_path")
+        if world > 1:  # every rank resumed from the same file; re-sync host mirrors anyway
+            reducer = parallel.GradientAllReduce(model)
+    train_ds, val_ds = datamodule.train_dataset, datamodule.val_dataset
+    sampler = (torch.utils.data.distributed.DistributedSampler(train_ds, world, rank, shuffle=True, seed=42,
+                                                               drop_last=True) if world > 1 else None)
+    loader = torch.utils.data.DataLoader(train_ds, batch_size=datamodule.batch_size, shuffle=sampler is None,
+                                         sampler=sampler, num_workers=datamodule.num_workers, pin_memory=True,
+                                         drop_last=True)
+    vsampler = (torch.utils.data.distributed.DistributedSampler(val_ds, world, rank, shuffle=False)
+                if world > 1 else None)
+    vloader = torch.utils.data.DataLoader(val_ds, batch_size=datamodule.batch_size, shuffle=False, sampler=vsampler,
+                                          num_workers=datamodule.num_workers, pin_memory=True, drop_last=True)
+    n_batches = len(loader)
+    val_every = max(1, int(n_batches * args.val_check_interval)) if args.val_check_interval <= 1 else \
+        int(args.val_check_interval)
+    history = []
+    epoch = epoch0
+    for epoch in range(epoch0, args.max_epochs):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        for i, batch in enumerate(loader):
+            x, nvs = _to_device(batch, dev)
+            opt.zero_grad()
+            loss = model.training_step((x, nvs), i)
+            loss.backward()
+            reducer()
+            opt.step()
+            step += 1
+            if step % args.log_every_n_steps == 0 or step == 1:
+                history.append((step, float(loss.detach())))
+                if rank == 0:
+                    print(f"epoch {epoch} step {step} loss {history[-1][1]:.6f}", flush=True)
+            if (i + 1) % val_every == 0 or (i + 1) == n_batches:
+                score = validate(model, vloader, dev) if len(val_ds) else None
+                if rank == 0:
+                    ckpt(model, opt, epoch, step, score)
+            if args.max_steps is not None and step >= args.max_steps:
+                break
+        if args.max_steps is not None and step >= args.max_steps:
+            break
+    if rank == 0:  # training ended (max_steps / max_epochs): last.ckpt holds the final state
+        ckpt(model, opt, epoch, step, None)
+    reducer.close()
+    return model, opt, history, ckpt
+
+
+if __name__ == '__main__':
+    main(parse_arguments())

@@ -81,3 +81,50 @@ def test_fullsize_train_step_finite(gpu):
         assert int(ix.min()) >= 0 and int(ix.max()) < k
     for q in m.encoder.quantize:  # first pass done: codebook initialised from the data statistics
         assert int(q.first_pass) == 0 and torch.isfinite(q.embed).all()
+
+
+# ---------------------------------------------------------------------------------------- cfg2
+# BASELINE.json configs[1]: the 2-layer published model (150 pre-q / 150 post-q / 5 post-up /
+# 5 post-down, K = 128 / 256; slurm-jobs/train_vqvae_3d_downscaled.job) on 256 x 256 x 128
+# volumes, batch 2, bf16.
+PUB2 = dict(n_bottleneck_blocks=2, n_pre_quantization_blocks=150, n_post_quantization_blocks=150,
+            n_post_upscale_blocks=5, n_post_downscale_blocks=5, num_embeddings=[128, 256])
+SHAPES2 = [(2, 64, 64, 32), (2, 16, 16, 8)]
+
+
+def test_cfg2_train_step_and_codes_bitexact(gpu):
+    """One batch-2 training step (finite loss / grads / params, in-range codes), then the eval
+    encode of the same batch: every level's codes equal the C oracle's nearest codeword for
+    the z the HIP encoder produced (bit-exact), commitment losses within 1e-4."""
+    import vq3d
+    from vq3d.utils import synthetic_volume
+    torch.manual_seed(0)
+    m = vq3d.VQVAE(vq3d.default_args(compute_dtype="bf16", **PUB2)).to(gpu)
+    opt = m.configure_optimizers()
+    x = torch.cat([synthetic_volume((1, 1, 256, 256, 128), i) for i in range(2)]).to(gpu)
+    nvs = torch.tensor([128, 128], device=gpu)
+    m.train()
+    opt.zero_grad()
+    loss = m.training_step((x, nvs), 0)
+    loss.backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(loss))
+    assert torch.isfinite(m.flat.grad).all() and float(m.flat.grad.abs().max()) > 0
+    assert torch.isfinite(m.flat.data).all()
+    zs = {}
+    hooks = [q.register_forward_pre_hook(lambda mod, inp, i=i: zs.__setitem__(i, inp[0].detach()))
+             for i, q in enumerate(m.encoder.quantize)]
+    m.eval()
+    with torch.no_grad():
+        res = list(m.encode(x))
+    for h in hooks:
+        h.remove()
+    for lvl, (q, (c, _, ix)) in enumerate(zip(m.encoder.quantize, res)):
+        assert tuple(ix.shape) == SHAPES2[lvl] and ix.dtype == torch.int64
+        assert int(ix.min()) >= 0 and int(ix.max()) < PUB2["num_embeddings"][lvl]
+        z = zs[lvl].float().permute(0, 2, 3, 4, 1).reshape(-1, q.embedding_dim).cpu().numpy()
+        ref_idx, _, sq = vq_oracle.nearest(z, q.embed.cpu().numpy())
+        assert np.array_equal(ix.reshape(-1).cpu().numpy(), ref_idx), lvl
+        ref_loss = q.commitment_cost * sq / z.size
+        assert abs(float(c) - ref_loss) <= 1e-4 * abs(ref_loss) + 1e-12, (lvl, float(c), ref_loss)
