@@ -32,6 +32,13 @@
 
 #include <algorithm>
 
+// Timing experiments only (tools builds: make -C 3d-vq-vae-2_amd exp EXP=N): bit 0 skips the
+// forward tile kernel's k^3 phase, 1 its 1x1 phase, 2 its stores, 3 its staging.  The product
+// library is built with PM_EXP = 0.
+#ifndef PM_EXP
+#define PM_EXP 0
+#endif
+
 namespace vq3d {
 
 namespace {
@@ -368,16 +375,18 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const Org o = tile_org(a, tile, TH, TW);
         __syncthreads();
-        lt.store(t2l);
-        lx.store(xs);
-        if (tile + int(gridDim.x) < a.ntiles) {
-            const Org on = tile_org(a, tile + gridDim.x, TH, TW);
-            lt.load(a, on, t2);
-            lx.load(a, on, x);
+        if constexpr (!(PM_EXP & 8)) {
+            lt.store(t2l);
+            lx.store(xs);
+            if (tile + int(gridDim.x) < a.ntiles) {
+                const Org on = tile_org(a, tile + gridDim.x, TH, TW);
+                lt.load(a, on, t2);
+                lx.load(a, on, x);
+            }
         }
         __syncthreads();
         // t3 = elu(W2 (*) t2 + b3a) + b3b: 16-voxel x 9-channel tiles, 9 windowed k-steps
-        for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+        for (int mt = (PM_EXP & 1) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
             const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
             const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -392,7 +401,7 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
         }
         __syncthreads();
         // out = scale * W3 t3 + b4 + x (in place over x)
-        for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+        for (int mt = (PM_EXP & 2) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
             const bf16x8 af = read8(t3s, (mt * 16 + row) * BR + 8 * kb);
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
@@ -408,8 +417,10 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
             }
         }
         __syncthreads();
-        store_tile<TH, TW, BR>(a, o, t3s, t3o);
-        store_tile<TH, TW, C>(a, o, xs, out);
+        if constexpr (!(PM_EXP & 4)) {
+            store_tile<TH, TW, BR>(a, o, t3s, t3o);
+            store_tile<TH, TW, C>(a, o, xs, out);
+        }
     }
 }
 

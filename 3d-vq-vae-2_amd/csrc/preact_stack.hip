@@ -1,0 +1,853 @@
+// A STACK of consecutive PreActFixupResBlocks (vqvae/layers.py:102-216, mode 'same', no skip
+// conv, identical channels) on a tiny grid, forward in ONE launch and backward in ONE launch:
+// the 50 top-level pre-quantize blocks of the encoder and the 50 post-quantize blocks of the
+// decoder of the published 3-layer model (8 x 8 x 2 = 128 voxels, 32 channels, branch 16).
+// Per block, unfused, that level costs a forward and a two-launch backward whose grids hold a
+// handful of workgroups; chained, one workgroup (1,024 threads) keeps the whole residual stream
+// in LDS and walks the blocks:
+//
+//   u1  = elu(x + b1a) + b1b        t2 = elu(W1 u1 + b2a) + b2b          (1x1, C -> B)
+//   t3  = elu(W2 (*) t2 + b3a) + b3b                                      (3x3x3 circular, B -> B)
+//   x  <- scale * (W3 t3) + b4 + x                                        (1x1, B -> C)
+//
+// The residual stream stays fp32 between the blocks of the stack (the reference's blocks return
+// fp32 under fp16 autocast: `out * self.scale` promotes); input and output are the caller's
+// storage dtype.  The forward saves every block's input x and its t2 / t3 (fp32) to `saved`;
+// the backward walks the blocks in reverse from them, writes gx and accumulates (+=) every
+// parameter gradient of every block.  One workgroup owns all of it, so each gradient entry has
+// exactly one adder and the scalar sums are fixed-order: deterministic.  Each block's weights
+// are staged into LDS while the previous block computes (register prefetch).
+#include "engines.h"
+
+#include <algorithm>
+
+namespace vq3d {
+
+namespace {
+
+constexpr int NT = 1024;                   // one workgroup, 16 waves
+constexpr int MAXV = 256, MAXC = 32, MAXB = 16;
+constexpr int NPRM = 11;                   // per block: w1, w2, w3, b1a, b1b, b2a, b2b, b3a, b3b, scale, b4
+constexpr int WMAX = MAXB * MAXC * 2 + MAXB * MAXB * 27;
+
+struct SkArgs {
+    int nv, C, B, H, W, D;  // voxels (batch folded in), channels, branch, grid
+    int nblk;
+    int PC, PB;             // LDS row pitches (odd: lanes on consecutive voxels hit distinct banks)
+};
+
+__device__ __forceinline__ int nbr(const SkArgs &a, int v, int tap, int sgn) {
+    const int kd = tap % 3, kw = (tap / 3) % 3, kh = tap / 9;
+    int d = v % a.D, t = v / a.D;
+    int w = t % a.W;
+    t /= a.W;
+    int h = t % a.H;
+    const int b = t / a.H;
+    h += sgn * (kh - 1);
+    w += sgn * (kw - 1);
+    d += sgn * (kd - 1);
+    h = h < 0 ? h + a.H : (h >= a.H ? h - a.H : h);
+    w = w < 0 ? w + a.W : (w >= a.W ? w - a.W : w);
+    d = d < 0 ? d + a.D : (d >= a.D ? d - a.D : d);
+    return ((b * a.H + h) * a.W + w) * a.D + d;
+}
+
+__device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
+    const float z1 = t - b;
+    return z1 > 0.f ? 1.f : z1 + 1.f;
+}
+
+struct Scal {
+    float b1a, b1b, b2a, b2b, b3a, b3b, sc, b4;
+};
+__device__ __forceinline__ Scal scal_of(const float *const *t) {
+    return Scal{*t[3], *t[4], *t[5], *t[6], *t[7], *t[8], *t[9], *t[10]};
+}
+
+// LDS weight image of one block: w1s [C][B] (o fastest), w3s [B][C] (co fastest), w2s
+// [tap][ci][co] (co fastest); `n` = total floats.  Prefetched into registers (<= 8 per thread)
+// from the nn.Conv3d tensors, then stored.
+struct WLd {
+    float v[(WMAX + NT - 1) / NT];
+    __device__ __forceinline__ void load(const SkArgs &a, const float *const *t) {
+        const int nB1 = a.B * a.C, nB2 = a.B * a.B * 27;
+#pragma unroll
+        for (int u = 0; u < (WMAX + NT - 1) / NT; ++u) {
+            const int i = threadIdx.x + u * NT;
+            float x = 0.f;
+            if (i < nB1) x = t[0][i];                       // W1 [o][c]
+            else if (i < 2 * nB1) x = t[2][i - nB1];        // W3 [co][o]
+            else if (i < 2 * nB1 + nB2) x = t[1][i - 2 * nB1];  // W2 [co][ci][tap]
+            v[u] = x;
+        }
+    }
+    __device__ __forceinline__ void store(const SkArgs &a, float *w1s, float *w3s, float *w2s) const {
+        const int nB1 = a.B * a.C, nB2 = a.B * a.B * 27;
+#pragma unroll
+        for (int u = 0; u < (WMAX + NT - 1) / NT; ++u) {
+            const int i = threadIdx.x + u * NT;
+            if (i < nB1) {
+                const int o = i / a.C, c = i - o * a.C;
+                w1s[c * a.B + o] = v[u];
+            } else if (i < 2 * nB1) {
+                const int j = i - nB1, co = j / a.B, o = j - co * a.B;
+                w3s[o * a.C + co] = v[u];
+            } else if (i < 2 * nB1 + nB2) {
+                const int j = i - 2 * nB1, tap = j % 27, r = j / 27, ci = r % a.B, co = r / a.B;
+                w2s[(tap * a.B + ci) * a.B + co] = v[u];
+            }
+        }
+    }
+};
+
+struct Lds {
+    float *xs, *us, *t2s, *t3s, *gs, *z3s, *z1s, *w1s, *w3s, *w2s, *red;
+    short *nb;
+};
+
+__device__ __forceinline__ Lds carve(const SkArgs &a, char *smem, bool bwd) {
+    Lds l;
+    float *p = reinterpret_cast<float *>(smem);
+    auto take = [&](int n) {
+        float *r = p;
+        p += (n + 3) & ~3;
+        return r;
+    };
+    l.w2s = take(a.B * a.B * 27);
+    l.w1s = take(a.B * a.C);
+    l.w3s = take(a.B * a.C);
+    l.xs = take(a.nv * a.PC);
+    l.us = take(a.nv * a.PC);
+    l.t2s = take(a.nv * a.PB);
+    l.t3s = take(a.nv * a.PB);
+    l.red = take(16 * 8);
+    l.gs = l.z3s = l.z1s = nullptr;
+    if (bwd) {
+        l.gs = take(a.nv * a.PC);
+        l.z3s = take(a.nv * a.PB);
+        l.z1s = take(a.nv * a.PB);
+    }
+    l.nb = reinterpret_cast<short *>(p);
+    return l;
+}
+
+size_t lds_bytes(const SkArgs &a, bool bwd) {
+    auto r4 = [](int n) { return size_t((n + 3) & ~3); };
+    size_t f = r4(a.B * a.B * 27) + 2 * r4(a.B * a.C) + 2 * r4(a.nv * a.PC) + 2 * r4(a.nv * a.PB) + 16 * 8;
+    if (bwd) f += r4(a.nv * a.PC) + 2 * r4(a.nv * a.PB);
+    return f * 4 + size_t(a.nv) * 27 * 2;
+}
+
+// fixed-order sums of 8 per-thread partials over the workgroup (all threads get them)
+__device__ __forceinline__ void sum8(float (&s)[8], float *red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = wave_sum(s[k]);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[wid * 8 + k] = s[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        float t = 0.f;
+        for (int w = 0; w < NT / 64; ++w) t += red[w * 8 + k];
+        s[k] = t;
+    }
+}
+
+// t3[v][o] (4 outputs from o0) = W2 (*) src over the neighbours of v; sgn -1: transposed taps
+// over [tap][ci][co] with the roles of ci / co swapped (backward-data)
+template <bool DGRAD>
+__device__ __forceinline__ void conv4(const SkArgs &a, const Lds &l, const float *src, int v, int o0, float (&acc)[4]) {
+    acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
+    for (int tap = 0; tap < 27; ++tap) {
+        const float *nrow = src + int(l.nb[v * 27 + (DGRAD ? 26 - tap : tap)]) * a.PB;
+        const float *wt = l.w2s + tap * a.B * a.B;
+        for (int c = 0; c < a.B; ++c) {
+            const float u = nrow[c];
+            if (!DGRAD) {
+                const float4 w = *reinterpret_cast<const float4 *>(wt + c * a.B + o0);  // [ci = c][co = o0..]
+                acc[0] = fmaf(u, w.x, acc[0]);
+                acc[1] = fmaf(u, w.y, acc[1]);
+                acc[2] = fmaf(u, w.z, acc[2]);
+                acc[3] = fmaf(u, w.w, acc[3]);
+            } else {  // gt2[v][ci = o0 + j] += W2[co = c][ci][tap] gz3[nbr(v, -tap)][c]
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = fmaf(u, wt[(o0 + j) * a.B + c], acc[j]);
+            }
+        }
+    }
+}
+
+// ============================================================================================ forward
+template <typename T>
+__global__ __launch_bounds__(NT) void k_stack_fwd(SkArgs a, const T *__restrict__ x, const float *const *tab,
+                                                  T *__restrict__ out, float *__restrict__ saved) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Lds l = carve(a, smem, false);
+    const int tid = threadIdx.x;
+    const int nvc = a.nv * a.C, nvb = a.nv * a.B, nog = a.B / 4;
+    const size_t stride = size_t(a.nv) * (a.C + 2 * a.B);
+    for (int i = tid; i < a.nv * 27; i += NT) l.nb[i] = short(nbr(a, i / 27, i % 27, 1));
+    for (int i = tid; i < nvc; i += NT) l.xs[(i / a.C) * a.PC + i % a.C] = ld(x + i);
+    WLd wl;
+    wl.load(a, tab);
+    for (int blk = 0; blk < a.nblk; ++blk) {
+        const float *const *t = tab + blk * NPRM;
+        const Scal s = scal_of(t);
+        float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
+        __syncthreads();  // previous block's readers of the weight image / xs are done
+        wl.store(a, l.w1s, l.w3s, l.w2s);
+        if (blk + 1 < a.nblk) wl.load(a, tab + (blk + 1) * NPRM);
+        for (int i = tid; i < nvc; i += NT) {
+            const int v = i / a.C, c = i - v * a.C;
+            const float xv = l.xs[v * a.PC + c];
+            sx[i] = xv;
+            l.us[v * a.PC + c] = elu(xv + s.b1a) + s.b1b;
+        }
+        __syncthreads();
+        // t2 (items: voxel x 4 outputs)
+        for (int i = tid; i < a.nv * nog; i += NT) {
+            const int v = i % a.nv, o0 = (i / a.nv) * 4;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < a.C; ++c) {
+                const float u = l.us[v * a.PC + c];
+                const float4 w = *reinterpret_cast<const float4 *>(l.w1s + c * a.B + o0);
+                acc[0] = fmaf(u, w.x, acc[0]);
+                acc[1] = fmaf(u, w.y, acc[1]);
+                acc[2] = fmaf(u, w.z, acc[2]);
+                acc[3] = fmaf(u, w.w, acc[3]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float tv = elu(acc[j] + s.b2a) + s.b2b;
+                l.t2s[v * a.PB + o0 + j] = tv;
+                st2[v * a.B + o0 + j] = tv;
+            }
+        }
+        __syncthreads();
+        // t3
+        for (int i = tid; i < a.nv * nog; i += NT) {
+            const int v = i % a.nv, o0 = (i / a.nv) * 4;
+            float acc[4];
+            conv4<false>(a, l, l.t2s, v, o0, acc);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float tv = elu(acc[j] + s.b3a) + s.b3b;
+                l.t3s[v * a.PB + o0 + j] = tv;
+                st3[v * a.B + o0 + j] = tv;
+            }
+        }
+        __syncthreads();
+        // x <- scale * W3 t3 + b4 + x (items: voxel x 4 channels)
+        for (int i = tid; i < a.nv * (a.C / 4); i += NT) {
+            const int v = i % a.nv, c0 = (i / a.nv) * 4;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int o = 0; o < a.B; ++o) {
+                const float u = l.t3s[v * a.PB + o];
+                const float4 w = *reinterpret_cast<const float4 *>(l.w3s + o * a.C + c0);
+                acc[0] = fmaf(u, w.x, acc[0]);
+                acc[1] = fmaf(u, w.y, acc[1]);
+                acc[2] = fmaf(u, w.z, acc[2]);
+                acc[3] = fmaf(u, w.w, acc[3]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) l.xs[v * a.PC + c0 + j] += acc[j] * s.sc + s.b4;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nvc; i += NT) st(out + i, l.xs[(i / a.C) * a.PC + i % a.C]);
+}
+
+// ============================================================================================ backward
+template <typename T>
+__global__ __launch_bounds__(NT) void k_stack_bwd(SkArgs a, const T *__restrict__ g, const float *const *tab,
+                                                  float *const *gtab, const float *__restrict__ saved,
+                                                  T *__restrict__ gx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Lds l = carve(a, smem, true);
+    const int tid = threadIdx.x;
+    const int nvc = a.nv * a.C, nvb = a.nv * a.B, nog = a.B / 4, ncg = a.C / 4;
+    const size_t stride = size_t(a.nv) * (a.C + 2 * a.B);
+    for (int i = tid; i < a.nv * 27; i += NT) l.nb[i] = short(nbr(a, i / 27, i % 27, 1));
+    for (int i = tid; i < nvc; i += NT) l.gs[(i / a.C) * a.PC + i % a.C] = ld(g + i);
+    WLd wl;
+    wl.load(a, tab + (a.nblk - 1) * NPRM);
+    for (int blk = a.nblk - 1; blk >= 0; --blk) {
+        const float *const *t = tab + blk * NPRM;
+        float *const *gt = gtab + blk * NPRM;
+        const Scal s = scal_of(t);
+        const float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
+        __syncthreads();
+        wl.store(a, l.w1s, l.w3s, l.w2s);
+        if (blk > 0) wl.load(a, tab + (blk - 1) * NPRM);
+        // saved block input -> u1 (us) and elu'(x + b1a) (xs); t2, t3
+        for (int i = tid; i < nvc; i += NT) {
+            const int v = i / a.C, c = i - v * a.C;
+            const float z = sx[i] + s.b1a;
+            const float e = z > 0.f ? 1.f : expf(z);
+            l.us[v * a.PC + c] = (z > 0.f ? z : e - 1.f) + s.b1b;
+            l.xs[v * a.PC + c] = e;
+        }
+        for (int i = tid; i < nvb; i += NT) {
+            const int v = i / a.B, o = i - v * a.B;
+            l.t2s[v * a.PB + o] = st2[i];
+            l.t3s[v * a.PB + o] = st3[i];
+        }
+        __syncthreads();
+        // scalar partials: 0 b4, 1 scale, 2 b3b, 3 b3a, 4 b2b, 5 b2a, 6 b1b, 7 b1a
+        float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        // gz3 = scale W3^T g * elu'(t3 - b3b)
+        for (int i = tid; i < a.nv * nog; i += NT) {
+            const int v = i % a.nv, o0 = (i / a.nv) * 4;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < a.C; ++c) {
+                const float gv = l.gs[v * a.PC + c];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = fmaf(gv, l.w3s[(o0 + j) * a.C + c], acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float g3 = acc[j] * s.sc;
+                const float z = g3 * elu_d_act(l.t3s[v * a.PB + o0 + j], s.b3b);
+                ps[2] += g3;
+                ps[3] += z;
+                l.z3s[v * a.PB + o0 + j] = z;
+            }
+        }
+        // W3 gradient (entries co x o), dscale = sum W3 . G3, db4 = sum g
+        for (int e = tid; e < a.C * a.B; e += NT) {
+            const int co = e / a.B, o = e - co * a.B;
+            float acc = 0.f, gsum = 0.f;
+            for (int v = 0; v < a.nv; ++v) {
+                const float gv = l.gs[v * a.PC + co];
+                acc = fmaf(gv, l.t3s[v * a.PB + o], acc);
+                if (o == 0) gsum += gv;
+            }
+            gt[2][e] += s.sc * acc;
+            ps[1] = fmaf(l.w3s[o * a.C + co], acc, ps[1]);
+            ps[0] += gsum;
+        }
+        __syncthreads();
+        // gt2 = W2^T (*) gz3 -> gz1 = gt2 * elu'(t2 - b2b)
+        for (int i = tid; i < a.nv * nog; i += NT) {
+            const int v = i % a.nv, o0 = (i / a.nv) * 4;
+            float acc[4];
+            conv4<true>(a, l, l.z3s, v, o0, acc);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float z = acc[j] * elu_d_act(l.t2s[v * a.PB + o0 + j], s.b2b);
+                ps[4] += acc[j];
+                ps[5] += z;
+                l.z1s[v * a.PB + o0 + j] = z;
+            }
+        }
+        // W2 gradient: items (tap, ci group, co group) x 16 entries, sum over voxels
+        for (int i = tid; i < 27 * nog * nog; i += NT) {
+            const int tap = i % 27, r = i / 27, cig = r % nog, cog = r / nog;
+            float acc[4][4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[p][q] = 0.f;
+            for (int v = 0; v < a.nv; ++v) {
+                const float *zr = l.z3s + v * a.PB + cog * 4;
+                const float *tr = l.t2s + int(l.nb[v * 27 + tap]) * a.PB + cig * 4;
+                float zz[4], tt[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    zz[q] = zr[q];
+                    tt[q] = tr[q];
+                }
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[p][q] = fmaf(zz[p], tt[q], acc[p][q]);
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    gt[1][((cog * 4 + p) * a.B + cig * 4 + q) * 27 + tap] += acc[p][q];
+        }
+        __syncthreads();
+        // gx = g + (W1^T gz1) * elu'(x + b1a) (in place over g); W1 gradient
+        for (int i = tid; i < a.nv * ncg; i += NT) {
+            const int v = i % a.nv, c0 = (i / a.nv) * 4;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int o = 0; o < a.B; ++o) {
+                const float z = l.z1s[v * a.PB + o];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = fmaf(z, l.w1s[(c0 + j) * a.B + o], acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float e = l.xs[v * a.PC + c0 + j];
+                ps[6] += acc[j];
+                ps[7] += acc[j] * e;
+                l.gs[v * a.PC + c0 + j] += acc[j] * e;
+            }
+        }
+        for (int e = tid; e < a.B * a.C; e += NT) {
+            const int o = e / a.C, c = e - o * a.C;
+            float acc = 0.f;
+            for (int v = 0; v < a.nv; ++v) acc = fmaf(l.z1s[v * a.PB + o], l.us[v * a.PC + c], acc);
+            gt[0][e] += acc;
+        }
+        sum8(ps, l.red);
+        if (tid == 0) {
+            *gt[10] += ps[0];
+            *gt[9] += ps[1];
+            *gt[8] += ps[2];
+            *gt[7] += ps[3];
+            *gt[6] += ps[4];
+            *gt[5] += ps[5];
+            *gt[4] += ps[6];
+            *gt[3] += ps[7];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nvc; i += NT) st(gx + i, l.gs[(i / a.C) * a.PC + i % a.C]);
+}
+
+// ============================================================================================ matrix cores
+// bf16 storage with (C, B) = (32, 16) (the published top level): every contraction of the
+// block on v_mfma_f32_16x16x32_bf16 (t2, t3, the block output, and in the backward gz3, the
+// transposed conv, gx and the three weight gradients with the voxels as the reduction axis).
+// Rounding points are the unfused bf16 path's (u1, t2, t3, gz3, gz1 rounded to bf16 as matrix
+// operands, fp32 accumulation); the residual stream and the gradient stream stay fp32.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int MC = 32, MB = 16;            // channels, branch
+constexpr int PF = 36, PU = 40, PT = 24;   // row pitches: fp32 streams, u1 (bf16), branch tensors (bf16)
+constexpr int MAXVM = 128;
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+__device__ __forceinline__ bf16x8 rd8(const bf16_t *p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(p)); }
+__device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, uint4{0u, 0u, 0u, 0u}); }
+// 8 bf16 at p[j * stride] (LDS)
+__device__ __forceinline__ bf16x8 gat8(const bf16_t *p, int stride) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(p[2 * j * stride]) | (uint32_t(p[(2 * j + 1) * stride]) << 16);
+    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+// 8 fp32 at p[j * stride] (LDS), rounded to bf16
+__device__ __forceinline__ bf16x8 gat8f(const float *p, int stride) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[j * stride];
+    return pack8(v);
+}
+// 8 consecutive fp32 (16-B aligned), rounded to bf16
+__device__ __forceinline__ bf16x8 rd8f(const float *p) {
+    const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    return pack8(v);
+}
+
+struct Mk {
+    float *xs, *gs, *part, *w;   // fp32: residual / gradient stream, conv partials [2][nv][16], weights
+    bf16_t *u1, *t2, *t3, *z3, *z1;
+    short *nb;
+    float *red;
+};
+
+// weight image (fp32): w1 [o][c] at 0, w3 [co][o] at 512, w2 [co][ci][tap] at 1024 (torch order)
+constexpr int W1O = 0, W3O = MB * MC, W2O = 2 * MB * MC, WN = W2O + MB * MB * 27;
+
+__device__ __forceinline__ Mk carve_m(int nv, char *smem) {
+    Mk m;
+    float *p = reinterpret_cast<float *>(smem);
+    m.w = p;
+    p += WN;
+    m.xs = p;
+    p += nv * PF;
+    m.gs = p;
+    p += nv * PF;
+    m.part = p;
+    p += 2 * nv * MB;
+    m.red = p;
+    p += 16 * 8;
+    bf16_t *q = reinterpret_cast<bf16_t *>(p);
+    m.u1 = q;
+    q += nv * PU;
+    m.t2 = q;
+    q += nv * PT + 32;
+    m.t3 = q;
+    q += nv * PT + 32;
+    m.z3 = q;
+    q += nv * PT + 32;
+    m.z1 = q;
+    q += nv * PT + 32;
+    m.nb = reinterpret_cast<short *>(q);
+    return m;
+}
+size_t lds_m(int nv) {
+    return size_t(WN + 2 * nv * PF + 2 * nv * MB + 16 * 8) * 4 + size_t(nv * PU + 4 * (nv * PT + 32)) * 2 +
+           size_t(nv) * 27 * 2;
+}
+
+struct WReg {  // register prefetch of one block's weights (fp32, torch order)
+    float v[(WN + NT - 1) / NT];
+    __device__ __forceinline__ void load(const float *const *t) {
+#pragma unroll
+        for (int u = 0; u < (WN + NT - 1) / NT; ++u) {
+            const int i = min(int(threadIdx.x) + u * NT, WN - 1);
+            v[u] = i < W3O ? t[0][i] : (i < W2O ? t[2][i - W3O] : t[1][i - W2O]);
+        }
+    }
+    __device__ __forceinline__ void store(float *w) const {
+#pragma unroll
+        for (int u = 0; u < (WN + NT - 1) / NT; ++u) {
+            const int i = threadIdx.x + u * NT;
+            if (i < WN) w[i] = v[u];
+        }
+    }
+};
+
+// conv2 (t3 from t2) or its transpose (gt2 from gz3): M-tile mt, k-steps of tap pairs
+// [ks0, ks0 + 7); B[k][n] built from the fp32 image: forward n = co, k = (tap, ci); transposed
+// n = ci, k = (tap, co) with the flipped tap
+template <bool T>
+__device__ __forceinline__ f32x4 conv_half(const Mk &m, const bf16_t *src, int mt, int ks0, int lane) {
+    const int row = lane & 15, kb = lane >> 4, v = mt * 16 + row;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ks = ks0; ks < ks0 + 7; ++ks) {
+        const int tap = 2 * ks + (kb >> 1), c0 = 8 * (kb & 1);
+        const bf16x8 af = tap < 27 ? rd8(src + int(m.nb[v * 27 + (T ? 26 - tap : tap)]) * PT + c0) : zero8();
+        float wv[8];
+        const int n = row;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = c0 + j;  // contraction channel
+            wv[j] = tap < 27 ? (T ? m.w[W2O + (c * MB + n) * 27 + tap] : m.w[W2O + (n * MB + c) * 27 + tap]) : 0.f;
+        }
+        acc = mfma(af, pack8(wv), acc);
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__restrict__ x, const float *const *tab,
+                                                   bf16_t *__restrict__ out, float *__restrict__ saved) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Mk m = carve_m(a.nv, smem);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int nv = a.nv, nmt = nv / 16, nvc = nv * MC, nvb = nv * MB;
+    const size_t stride = size_t(nv) * (MC + 2 * MB);
+    for (int i = tid; i < nv * 27; i += NT) m.nb[i] = short(nbr(a, i / 27, i % 27, 1));
+    for (int i = tid; i < nvc; i += NT) m.xs[(i / MC) * PF + i % MC] = ld(x + i);
+    for (int i = tid; i < 32; i += NT) m.t3[nv * PT + i] = 0;  // zero tail / row pads read by the fragments
+    for (int i = tid; i < nv * (PT - MB); i += NT) m.t3[(i / (PT - MB)) * PT + MB + i % (PT - MB)] = 0;
+    WReg wr;
+    wr.load(tab);
+    for (int blk = 0; blk < a.nblk; ++blk) {
+        const Scal s = scal_of(tab + blk * NPRM);
+        float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
+        __syncthreads();
+        wr.store(m.w);
+        if (blk + 1 < a.nblk) wr.load(tab + (blk + 1) * NPRM);
+        for (int i = tid; i < nvc; i += NT) {
+            const int v = i / MC, c = i - v * MC;
+            const float xv = m.xs[v * PF + c];
+            sx[i] = xv;
+            m.u1[v * PU + c] = f2bf(elu(xv + s.b1a) + s.b1b);
+        }
+        __syncthreads();
+        // t2: M-tile per wave, K = 32 channels, N = 16
+        if (wave < nmt) {
+            float wv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wv[j] = m.w[W1O + row * MC + 8 * kb + j];
+            const f32x4 acc = mfma(rd8(m.u1 + (wave * 16 + row) * PU + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int v = wave * 16 + 4 * kb + j;
+                const bf16_t tv = f2bf(elu(acc[j] + s.b2a) + s.b2b);
+                m.t2[v * PT + row] = tv;
+                st2[v * MB + row] = ld(&tv);
+            }
+        }
+        __syncthreads();
+        // t3: (M-tile, half of the 14 tap-pair k-steps) per wave, partials summed in LDS
+        if (wave < 2 * nmt) {
+            const int mt = wave % nmt, half = wave / nmt;
+            const f32x4 acc = conv_half<false>(m, m.t2, mt, 7 * half, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m.part[(half * nv + mt * 16 + 4 * kb + j) * MB + row] = acc[j];
+        }
+        __syncthreads();
+        for (int i = tid; i < nvb; i += NT) {
+            const int v = i / MB, o = i - v * MB;
+            const bf16_t tv = f2bf(elu(m.part[i] + m.part[nvb + i] + s.b3a) + s.b3b);
+            m.t3[v * PT + o] = tv;
+            st3[i] = ld(&tv);
+        }
+        __syncthreads();
+        // x += scale * W3 t3 + b4: M-tile x 2 N-tiles per wave, K = 16 (+ zero half)
+        if (wave < 2 * nmt) {
+            const int mt = wave % nmt, nt = wave / nmt;
+            float wv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = 8 * kb + j;
+                wv[j] = o < MB ? m.w[W3O + (16 * nt + row) * MB + o] : 0.f;
+            }
+            const f32x4 acc = mfma(rd8(m.t3 + (mt * 16 + row) * PT + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m.xs[(mt * 16 + 4 * kb + j) * PF + 16 * nt + row] += acc[j] * s.sc + s.b4;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nvc; i += NT) out[i] = f2bf(m.xs[(i / MC) * PF + i % MC]);
+}
+
+__global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__restrict__ g, const float *const *tab,
+                                                   float *const *gtab, const float *__restrict__ saved,
+                                                   bf16_t *__restrict__ gx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const Mk m = carve_m(a.nv, smem);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int nv = a.nv, nmt = nv / 16, nks = nv / 32, nvc = nv * MC, nvb = nv * MB;
+    const size_t stride = size_t(nv) * (MC + 2 * MB);
+    for (int i = tid; i < nv * 27; i += NT) m.nb[i] = short(nbr(a, i / 27, i % 27, 1));
+    for (int i = tid; i < nvc; i += NT) m.gs[(i / MC) * PF + i % MC] = ld(g + i);
+    for (int i = tid; i < nv * (PT - MB); i += NT) {  // zero row pads / tail read by the gx fragments
+        const int v = i / (PT - MB), e = MB + i % (PT - MB);
+        m.z1[v * PT + e] = 0;
+    }
+    for (int i = tid; i < 32; i += NT) m.z1[nv * PT + i] = 0;
+    WReg wr;
+    wr.load(tab + (a.nblk - 1) * NPRM);
+    for (int blk = a.nblk - 1; blk >= 0; --blk) {
+        const Scal s = scal_of(tab + blk * NPRM);
+        float *const *gt = gtab + blk * NPRM;
+        const float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
+        __syncthreads();
+        wr.store(m.w);
+        if (blk > 0) wr.load(tab + (blk - 1) * NPRM);
+        for (int i = tid; i < nvc; i += NT) {
+            const int v = i / MC, c = i - v * MC;
+            const float z = sx[i] + s.b1a;
+            const float e = z > 0.f ? 1.f : expf(z);
+            m.u1[v * PU + c] = f2bf((z > 0.f ? z : e - 1.f) + s.b1b);
+            m.xs[v * PF + c] = e;
+        }
+        for (int i = tid; i < nvb; i += NT) {
+            const int v = i / MB, o = i - v * MB;
+            m.t2[v * PT + o] = f2bf(st2[i]);
+            m.t3[v * PT + o] = f2bf(st3[i]);
+        }
+        __syncthreads();
+        float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // b4, scale, b3b, b3a, b2b, b2a, b1b, b1a
+        if (wave < nmt) {
+            // gz3 = scale W3^T g * elu'(t3 - b3b): K = 32 channels of g, N = 16
+            float wv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wv[j] = m.w[W3O + (8 * kb + j) * MB + row];
+            const f32x4 acc = mfma(rd8f(m.gs + (wave * 16 + row) * PF + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int v = wave * 16 + 4 * kb + j;
+                const float g3 = acc[j] * s.sc;
+                const float z = g3 * elu_d_act(ld(&m.t3[v * PT + row]), s.b3b);
+                ps[2] += g3;
+                ps[3] += z;
+                m.z3[v * PT + row] = f2bf(z);
+            }
+        } else if (wave < nmt + 2) {
+            // W3 gradient: M = co tile (wave - nmt), N = o, K = voxels; dscale = sum W3 . G3
+            const int ct = wave - nmt;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int ks = 0; ks < nks; ++ks) {
+                const int v0 = ks * 32 + 8 * kb;
+                acc = mfma(gat8f(m.gs + v0 * PF + 16 * ct + row, PF), gat8(m.t3 + v0 * PT + row, PT), acc);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = 16 * ct + 4 * kb + j;
+                gt[2][co * MB + row] += s.sc * acc[j];
+                ps[1] = fmaf(m.w[W3O + co * MB + row], acc[j], ps[1]);
+            }
+        }
+        for (int i = tid; i < nvc; i += NT) ps[0] += m.gs[(i / MC) * PF + i % MC];
+        __syncthreads();
+        // gt2 = W2^T (*) gz3 (M-tile x half of the k-steps per wave); W2 gradient per tap
+        if (wave < 2 * nmt) {
+            const int mt = wave % nmt, half = wave / nmt;
+            const f32x4 acc = conv_half<true>(m, m.z3, mt, 7 * half, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m.part[(half * nv + mt * 16 + 4 * kb + j) * MB + row] = acc[j];
+        }
+        for (int tap = wave; tap < 27; tap += NT / 64) {  // M = co, N = ci, K = voxels
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int ks = 0; ks < nks; ++ks) {
+                const int v0 = ks * 32 + 8 * kb;
+                uint32_t w[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int va = v0 + 2 * j, vb = va + 1;
+                    w[j] = uint32_t(m.t2[int(m.nb[va * 27 + tap]) * PT + row]) |
+                           (uint32_t(m.t2[int(m.nb[vb * 27 + tap]) * PT + row]) << 16);
+                }
+                acc = mfma(gat8(m.z3 + v0 * PT + row, PT), __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]}),
+                           acc);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gt[1][((4 * kb + j) * MB + row) * 27 + tap] += acc[j];
+        }
+        __syncthreads();
+        for (int i = tid; i < nvb; i += NT) {
+            const int v = i / MB, o = i - v * MB;
+            const float g2 = m.part[i] + m.part[nvb + i];
+            const float z = g2 * elu_d_act(ld(&m.t2[v * PT + o]), s.b2b);
+            ps[4] += g2;
+            ps[5] += z;
+            m.z1[v * PT + o] = f2bf(z);
+        }
+        __syncthreads();
+        if (wave < 2 * nmt) {
+            // gx = g + (W1^T gz1) * elu'(x + b1a): M-tile x 2 N-tiles (channels), K = 16 (+ zero half)
+            const int mt = wave % nmt, nt = wave / nmt;
+            float wv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = 8 * kb + j;
+                wv[j] = o < MB ? m.w[W1O + o * MC + 16 * nt + row] : 0.f;
+            }
+            const f32x4 acc = mfma(rd8(m.z1 + (mt * 16 + row) * PT + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int i = (mt * 16 + 4 * kb + j) * PF + 16 * nt + row;
+                const float e = m.xs[i];
+                ps[6] += acc[j];
+                ps[7] += acc[j] * e;
+                m.gs[i] += acc[j] * e;
+            }
+        }
+        if (wave < 2) {
+            // W1 gradient: M = o, N = channel tile (wave), K = voxels
+            const int nt = wave;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int ks = 0; ks < nks; ++ks) {
+                const int v0 = ks * 32 + 8 * kb;
+                acc = mfma(gat8(m.z1 + v0 * PT + row, PT), gat8(m.u1 + v0 * PU + 16 * nt + row, PU), acc);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gt[0][(4 * kb + j) * MC + 16 * nt + row] += acc[j];
+        }
+        sum8(ps, m.red);
+        if (tid == 0) {
+            *gt[10] += ps[0];
+            *gt[9] += ps[1];
+            *gt[8] += ps[2];
+            *gt[7] += ps[3];
+            *gt[6] += ps[4];
+            *gt[5] += ps[5];
+            *gt[4] += ps[6];
+            *gt[3] += ps[7];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nvc; i += NT) gx[i] = f2bf(m.gs[(i / MC) * PF + i % MC]);
+}
+
+bool mfma_ok(const SkArgs &a) { return a.C == MC && a.B == MB && a.nv % 32 == 0 && a.nv <= MAXVM; }
+
+int check(int32_t nblk, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+          SkArgs &a) {
+    a.nv = batch * h * w * dd;
+    a.C = channels;
+    a.B = branch;
+    a.H = h;
+    a.W = w;
+    a.D = dd;
+    a.nblk = nblk;
+    a.PC = channels + 1;
+    a.PB = branch + 1;
+    if (nblk < 1 || batch < 1 || h < 1 || w < 1 || dd < 1) return 1;
+    if (a.nv > MAXV || channels > MAXC || branch > MAXB || channels % 4 || branch % 4) return 1;
+    if (lds_bytes(a, true) > 160 * 1024) return 1;
+    return 0;
+}
+
+}  // namespace
+
+}  // namespace vq3d
+
+using namespace vq3d;
+
+extern "C" {
+
+int vq3d_preact_stack_supported(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd) {
+    SkArgs a;
+    return check(2, batch, channels, branch, h, w, dd, a) == 0 ? 1 : 0;
+}
+
+size_t vq3d_preact_stack_saved_floats(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                                      int32_t w, int32_t dd) {
+    return size_t(nblocks) * batch * h * w * dd * (channels + 2 * branch);
+}
+
+int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                          int32_t w, int32_t dd, const void *x, const float *const *params, void *out, float *saved,
+                          vq3d_stream_t stream) {
+    SkArgs a;
+    if (check(nblocks, batch, channels, branch, h, w, dd, a)) return fail("preact_stack_fwd: unsupported shape");
+    if (!x || !params || !out || !saved) return fail("preact_stack_fwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    const size_t lds = lds_bytes(a, false);
+    if (dtype == VQ3D_BF16 && mfma_ok(a)) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(160 * 1024));
+        k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)x, params, (bf16_t *)out, saved);
+    } else if (dtype == VQ3D_BF16) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<bf16_t>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+        k_stack_fwd<bf16_t><<<1, NT, lds, s>>>(a, (const bf16_t *)x, params, (bf16_t *)out, saved);
+    } else if (dtype == VQ3D_F32) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<float>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+        k_stack_fwd<float><<<1, NT, lds, s>>>(a, (const float *)x, params, (float *)out, saved);
+    } else {
+        return fail("preact_stack_fwd: dtype");
+    }
+    return check_launch("preact_stack_fwd");
+}
+
+int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                          int32_t w, int32_t dd, const void *g, const float *const *params, float *const *grads,
+                          const float *saved, void *gx, vq3d_stream_t stream) {
+    SkArgs a;
+    if (check(nblocks, batch, channels, branch, h, w, dd, a)) return fail("preact_stack_bwd: unsupported shape");
+    if (!g || !params || !grads || !saved || !gx) return fail("preact_stack_bwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    const size_t lds = lds_bytes(a, true);
+    if (dtype == VQ3D_BF16 && mfma_ok(a)) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(160 * 1024));
+        k_stackm_bwd<<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx);
+    } else if (dtype == VQ3D_BF16) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<bf16_t>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+        k_stack_bwd<bf16_t><<<1, NT, lds, s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx);
+    } else if (dtype == VQ3D_F32) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<float>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+        k_stack_bwd<float><<<1, NT, lds, s>>>(a, (const float *)g, params, grads, saved, (float *)gx);
+    } else {
+        return fail("preact_stack_bwd: dtype");
+    }
+    return check_launch("preact_stack_bwd");
+}
+
+}  // extern "C"

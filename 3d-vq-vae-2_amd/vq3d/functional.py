@@ -161,6 +161,76 @@ class PreActBlockFn(torch.autograd.Function):
         return (g_x, None) + (None,) * len(blk._fn_params)
 
 
+# ============================================================================================ block stack
+_PRM = ("branch_conv1", "branch_conv2", "branch_conv3", "bias1a", "bias1b", "bias2a", "bias2b", "bias3a", "bias3b",
+        "scale", "bias4")
+
+
+def _prm_tensor(blk, n):
+    return getattr(blk, n).weight if n.startswith("branch_conv") else getattr(blk, n)
+
+
+class StackPlan:
+    """Device tables of the parameter / gradient pointers of a run of blocks ([block][11], the
+    order of vq3d_preact_stack_fwd), rebuilt when the parameters move (flat.py re-views)."""
+
+    def __init__(self, blocks):
+        self.blocks = list(blocks)
+        self.params = [_prm_tensor(b, n) for b in self.blocks for n in _PRM]
+        self.key = None
+
+    def tables(self, dev):
+        for p in self.params:
+            grad_buf(p)
+        key = tuple(p.data_ptr() for p in self.params) + tuple(p.grad.data_ptr() for p in self.params)
+        if key != self.key:
+            n = len(self.params)
+            self.ptab = torch.tensor([p.data_ptr() for p in self.params], dtype=torch.int64).to(dev)
+            self.gtab = torch.tensor([p.grad.data_ptr() for p in self.params], dtype=torch.int64).to(dev)
+            assert self.ptab.numel() == n
+            self.key = key
+        return self.ptab, self.gtab
+
+
+class PreActStackFn(torch.autograd.Function):
+    """A run of identical PreActFixupResBlocks ('same', no skip) on a tiny grid: forward and
+    backward in one launch each (preact_stack.hip), the residual stream fp32 inside the run."""
+
+    @staticmethod
+    def forward(ctx, x, plan, *params):
+        x = ops.as_cl(x)
+        b, c, h, w, d = x.shape
+        nb = plan.blocks[0].branch_conv1.weight.shape[0]
+        nblk = len(plan.blocks)
+        ptab, _ = plan.tables(x.device)
+        saved = torch.empty(L.query("vq3d_preact_stack_saved_floats", nblk, b, c, nb, h, w, d), dtype=torch.float32,
+                            device=x.device)
+        out = torch.empty_like(x, memory_format=ops.CL)
+        L.call("vq3d_preact_stack_fwd", L.dtype_code(x), nblk, b, c, nb, h, w, d, L.ptr(x), L.ptr(ptab), L.ptr(out),
+               L.ptr(saved), L.stream())
+        ctx.plan = plan
+        ctx.save_for_backward(saved)
+        ctx.shape = (b, c, nb, h, w, d)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (saved,) = ctx.saved_tensors
+        plan = ctx.plan
+        b, c, nb, h, w, d = ctx.shape
+        g = _cl(g)
+        ptab, gtab = plan.tables(g.device)
+        gx = torch.empty_like(g, memory_format=ops.CL)
+        L.call("vq3d_preact_stack_bwd", L.dtype_code(g), len(plan.blocks), b, c, nb, h, w, d, L.ptr(g), L.ptr(ptab),
+               L.ptr(gtab), L.ptr(saved), L.ptr(gx), L.stream())
+        grads_ready(plan.params)
+        return (gx, None) + (None,) * len(plan.params)
+
+
+def stack_eligible(blk):
+    return (type(blk).__name__ == "PreActFixupResBlock" and blk.skip_conv is None and blk.mode in ("same", "out"))
+
+
 # ============================================================================================ generic conv
 class ConvFn(torch.autograd.Function):
     """One nn.Conv3d call with the fused prologue / epilogue (regular + EvoNorm blocks,

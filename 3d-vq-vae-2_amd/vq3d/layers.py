@@ -220,6 +220,44 @@ class EvonormResBlock(nn.Module):
 
 
 # ============================================================================================ stacks
+class BlockStack(nn.Sequential):
+    """nn.Sequential (same children, same state_dict keys) whose forward runs every maximal run of
+    >= 2 identical PreActFixupResBlocks ('same', no skip) on a tiny grid as ONE fused stack
+    (Fn.PreActStackFn: one launch forward, one backward); everything else runs module by module."""
+
+    def forward(self, x):
+        mods = list(self)
+        i = 0
+        while i < len(mods):
+            j = i
+            if Fn.stack_eligible(mods[i]):
+                c, nb = mods[i].in_channels, mods[i].branch_conv1.weight.shape[0]
+                while (j + 1 < len(mods) and Fn.stack_eligible(mods[j + 1]) and mods[j + 1].in_channels == c
+                       and mods[j + 1].branch_conv1.weight.shape[0] == nb):
+                    j += 1
+            if j > i and self._stack_ok(x, mods[i]):
+                run = tuple(mods[i:j + 1])
+                plan = self._plans.get((i, j)) if hasattr(self, "_plans") else None
+                if plan is None or plan.blocks != list(run):
+                    if not hasattr(self, "_plans"):
+                        self._plans = {}
+                    plan = self._plans[(i, j)] = Fn.StackPlan(run)
+                x = Fn.PreActStackFn.apply(x, plan, *plan.params)
+                i = j + 1
+            else:
+                x = mods[i](x)
+                i += 1
+        return x
+
+    @staticmethod
+    def _stack_ok(x, blk):
+        if not (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)):
+            return False
+        b, c, h, w, d = x.shape
+        return c == blk.in_channels and bool(L.query("vq3d_preact_stack_supported", b, c,
+                                                      blk.branch_conv1.weight.shape[0], h, w, d))
+
+
 class DownBlock(nn.Module):
     """layers.py:306-324."""
 
@@ -292,7 +330,7 @@ class Encoder2(nn.Module):
             self.pre_quantize_cond.append(PreQuantizationConditioning(
                 in_channels=after_channels + (embedding_dim if i != n_enc - 1 else 0), out_channels=embedding_dim,
                 n_up=n_down_per_enc, resblock=resblock, n_post_upscale_blocks=n_post_upscale_blocks))
-            self.pre_quantize.append(nn.Sequential(
+            self.pre_quantize.append(BlockStack(
                 *(resblock(embedding_dim, embedding_dim, mode='same') for _ in range(n_pre_q_blocks))))
             self.quantize.append(Quantizer(num_embeddings=num_embeddings[i], embedding_dim=embedding_dim,
                                            commitment_cost=0.1))
@@ -360,7 +398,7 @@ class Decoder(nn.Module):
             in_channels = embedding_dim + (before_channels if i != n_enc - 1 else 0)
             if i != n_enc - 1:
                 self.proj.append(Conv3d(in_channels, in_channels, kernel_size=1))
-            self.up.append(nn.Sequential(
+            self.up.append(BlockStack(
                 *(resblock(in_channels, in_channels, mode='same') for _ in range(n_post_q_blocks)),
                 UpBlock(in_channels=in_channels, out_channels=after_channels, n_up=n_up_per_enc, mode='decoder',
                         resblock=resblock, n_post_upscale_blocks=n_post_upscale_blocks),

@@ -1,0 +1,174 @@
+"""Fused stack of PreActFixupResBlocks on tiny grids (csrc/preact_stack.hip: the whole run forward
+in one launch, backward in one) against a float64 chain of the oracle's block restatement
+(oracle/vqvae_cpu.preact_block, pinned to vqvae/layers.py:176-195 by the block goldens):
+output, input gradient and every parameter gradient of every block.
+
+Tolerances: fp32 storage (VALU kernels, fp32 throughout) 1e-4 of each tensor's max magnitude;
+bf16 storage: (C, B) = (32, 16) runs the matrix-core kernels (u1 / t2 / t3 / gz3 / gz1 and the
+weights rounded to bf16 as matrix operands, residual and gradient streams fp32) and is checked
+against a float64 chain that rounds at exactly those points (what remains is fp32 vs float64
+summation order and the bf16 ties it flips, measured <= 1.2 %): 2e-2 for output, gx and every
+weight tensor, each block's 8 scalar-parameter gradients as one vector within 5e-2 relative
+L2; other shapes run the fp32 VALU kernels between bf16 input and output and are checked
+against the plain float64 chain with the same tolerances."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import vqvae_cpu as O
+
+pytestmark = pytest.mark.gpu
+CL = torch.channels_last_3d
+CASES = [  # (batch, C, branch, H, W, D, blocks): the published top level (8x8x2, 32 ch) and wraps
+    (1, 32, 16, 8, 8, 2, 6), (2, 32, 16, 4, 4, 2, 3), (1, 32, 16, 4, 4, 1, 3), (1, 8, 4, 4, 8, 4, 4)]
+
+
+def _stack(c, nbr, n, seed):
+    from vq3d import layers as VL
+    torch.manual_seed(seed)
+    blocks = [VL.PreActFixupResBlock(c, c, mode="same") for _ in range(n)]
+    rng = np.random.default_rng(seed)
+    with torch.no_grad():
+        for blk in blocks:
+            assert blk.branch_conv1.weight.shape[0] == nbr
+            for _, p in blk.named_parameters():
+                if p.numel() == 1:
+                    p.fill_(float(rng.normal(0, 0.3)))
+                else:
+                    p.normal_(0, 0.2)
+            blk.scale.fill_(0.5 + 0.5 * float(rng.random()))
+    return VL.BlockStack(*blocks)
+
+
+def _ref(stack, x, g):
+    sd = {k: v.detach().double().clone().requires_grad_(True) for k, v in stack.state_dict().items()}
+    xr = x.detach().double().clone().requires_grad_(True)
+    c = x.shape[1]
+    out = xr
+    for i in range(len(stack)):
+        out = O.preact_block(sd, f"{i}.", out, c, c, "same")
+    out.backward(g.double())
+    return out.detach(), xr.grad, {k: v.grad for k, v in sd.items()}
+
+
+def rb(t):
+    return t.float().bfloat16().double()
+
+
+def _pad(t):
+    return torch.nn.functional.pad(t, (1,) * 6, mode="circular")
+
+
+def _ref_strict(stack, x, g):
+    """float64 chain with the matrix-core kernels' bf16 rounding points (u1, t2, t3, the weights
+    as matrix operands, gz3, gz1, g as an operand); residual / gradient streams unrounded."""
+    import torch.nn.functional as F
+    P = [{k: v.detach().double() for k, v in blk.state_dict().items()} for blk in stack]
+    xs, saved = x.clone(), []
+    for p in P:
+        sc, b1a, b1b, b2a, b2b, b3a, b3b, b4 = (float(p[k]) for k in
+                                                 ("scale", "bias1a", "bias1b", "bias2a", "bias2b", "bias3a", "bias3b", "bias4"))
+        u1 = rb(F.elu(xs + b1a) + b1b)
+        t2 = rb(F.elu(F.conv3d(u1, rb(p["branch_conv1.weight"])) + b2a) + b2b)
+        t3 = rb(F.elu(F.conv3d(_pad(t2), rb(p["branch_conv2.weight"])) + b3a) + b3b)
+        saved.append((xs, u1, t2, t3))
+        xs = xs + sc * F.conv3d(t3, rb(p["branch_conv3.weight"])) + b4
+    out = rb(xs)
+    grads = [None] * len(P)
+    gs = g.clone()
+    for i in reversed(range(len(P))):
+        p = P[i]
+        sc, b1a, b1b, b2a, b2b, b3a, b3b, b4 = (float(p[k]) for k in
+                                                 ("scale", "bias1a", "bias1b", "bias2a", "bias2b", "bias3a", "bias3b", "bias4"))
+        xi, u1, t2, t3 = saved[i]
+        w1, w2, w3 = p["branch_conv1.weight"], p["branch_conv2.weight"], p["branch_conv3.weight"]
+        gr = rb(gs)
+        G3 = torch.einsum("bchwd,bohwd->co", gr, t3)
+        gt3 = sc * F.conv3d(gr, rb(w3).permute(1, 0, 2, 3, 4))
+        z3 = gt3 * torch.where(t3 - b3b > 0, torch.ones_like(t3), t3 - b3b + 1)
+        z3r = rb(z3)
+        t2v = t2.clone().requires_grad_(True)
+        w2v = w2.clone().requires_grad_(True)
+        gt2 = torch.autograd.grad(F.conv3d(_pad(t2v), rb(w2)), t2v, z3r)[0]
+        dw2 = torch.autograd.grad(F.conv3d(_pad(t2), w2v), w2v, z3r)[0]
+        z1 = gt2 * torch.where(t2 - b2b > 0, torch.ones_like(t2), t2 - b2b + 1)
+        z1r = rb(z1)
+        gt1 = F.conv3d(z1r, rb(w1).permute(1, 0, 2, 3, 4))
+        e1 = torch.where(xi + b1a > 0, torch.ones_like(xi), torch.exp(xi + b1a))
+        grads[i] = {
+            "branch_conv3.weight": (sc * G3)[..., None, None, None], "scale": (w3[..., 0, 0, 0] * G3).sum(),
+            "bias4": gs.sum(), "bias3b": gt3.sum(), "bias3a": z3.sum(), "branch_conv2.weight": dw2,
+            "bias2b": gt2.sum(), "bias2a": z1.sum(),
+            "branch_conv1.weight": torch.einsum("bohwd,bchwd->oc", z1r, u1)[..., None, None, None],
+            "bias1b": gt1.sum(), "bias1a": (gt1 * e1).sum()}
+        gs = gs + gt1 * e1
+    return out, rb(gs), {f"{i}.{k}": v for i, gi in enumerate(grads) for k, v in gi.items()}
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES)
+def test_stack_matches_float64_chain(gpu, case, dtype):
+    from vq3d import functional as Fn
+    from vq3d.flat import FlatParams
+    b, c, nbr, h, w, d, n = case
+    dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    stack = _stack(c, nbr, n, seed=h * 10 + d)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn((b, c, h, w, d), generator=gen).to(dt).double()
+    gy = torch.randn((b, c, h, w, d), generator=gen).to(dt).double()
+    ry, rgx, rgp = _ref(stack, x, gy) if dtype == "fp32" or c != 32 else _ref_strict(stack, x, gy)
+    m = stack.to(gpu)
+    FlatParams(m.parameters(), gpu)
+    calls = []
+    orig = Fn.PreActStackFn.apply
+    Fn.PreActStackFn.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        xg = x.to(gpu).to(dt).contiguous(memory_format=CL).requires_grad_(True)
+        y = m(xg)
+        y.backward(gy.to(gpu).to(dt).contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+    finally:
+        Fn.PreActStackFn.apply = orig
+    assert calls == [1]  # the whole run went through the fused stack
+    tol = 1e-4 if dtype == "fp32" else 2e-2
+    errs = {"y": rel(y.float(), ry), "gx": rel(xg.grad.float(), rgx)}
+    scal = {}
+    for k, p in m.state_dict(keep_vars=True).items():
+        if p.numel() > 1 or dtype == "fp32":
+            errs["grad/" + k] = rel(p.grad, rgp[k].reshape(p.shape))
+        else:  # bf16: a block's 8 scalar gradients as one vector (single sums nearly cancel)
+            rgp[k] = rgp[k].reshape(p.shape)
+            blk = k.split(".")[0]
+            scal.setdefault(blk, ([], []))
+            scal[blk][0].append(p.grad.double().cpu().reshape(-1))
+            scal[blk][1].append(rgp[k].double().reshape(-1))
+    for blk, (gs, rs) in scal.items():
+        gv, rv = torch.cat(gs), torch.cat(rs)
+        errs[f"scalars/{blk}"] = float((gv - rv).norm() / rv.norm())
+    print(case, dtype, {k: f"{v:.2e}" for k, v in errs.items() if v > tol / 10})
+    bad = {k: v for k, v in errs.items() if not v <= (5e-2 if k.startswith("scalars/") else tol)}
+    assert not bad, (case, dtype, bad)
+
+
+def test_stack_deterministic(gpu):
+    from vq3d.flat import FlatParams
+    stack = _stack(32, 16, 4, seed=9).to(gpu)
+    FlatParams(stack.parameters(), gpu)
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn((1, 32, 8, 8, 2), generator=gen).to(gpu).contiguous(memory_format=CL)
+    gy = torch.randn((1, 32, 8, 8, 2), generator=gen).to(gpu).contiguous(memory_format=CL)
+    res = []
+    for _ in range(2):
+        for p in stack.parameters():
+            p.grad.zero_()
+        xg = x.clone().requires_grad_(True)
+        stack(xg).backward(gy)
+        torch.cuda.synchronize()
+        res.append([xg.grad.clone()] + [p.grad.clone() for p in stack.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

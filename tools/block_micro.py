@@ -77,6 +77,15 @@ def main():
     tcb = timed(lambda: big_dst.copy_(big), iters)
     print(f"copy {x.numel() * 2 / 1e6:.1f} MB: {tc:7.1f} us ({2 * x.numel() * 2 / tc / 1e3:7.1f} GB/s r+w); "
           f"copy {big.numel() * 2 / 1e6:.1f} MB: {tcb:7.1f} us ({2 * big.numel() * 2 / tcb / 1e3:7.1f} GB/s r+w)")
+    if kind == "mid":  # per kernel (vq3d_preact_mid_*_stages), preallocated outputs
+        bufs = (out, t2, t3)
+        gx = torch.empty_like(x)
+        ws = ops.workspace(ops.L.query("vq3d_preact_mid_workspace_bytes", 1, h, w, d), dev)
+        ops.preact_mid_bwd(g, x, t2, t3, blk, grads, bufs=(gx, ws))
+        per = {f"fwd{k}": timed(lambda k=k: ops.preact_mid_fwd(x, blk, stages=k, bufs=bufs), iters) for k in (1, 2)}
+        per.update({f"bwd{k}": timed(lambda k=k: ops.preact_mid_bwd(g, x, t2, t3, blk, grads, stages=k,
+                                                                      bufs=(gx, ws)), iters) for k in (1, 2, 4)})
+        print("per kernel us:", {k: round(v, 1) for k, v in per.items()})
     tf = timed(fwd, iters)
     tb = timed(bwd, iters)
     nv = h * w * d
