@@ -182,6 +182,26 @@ int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
                                const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                size_t workspace_bytes, void *gx, vq3d_stream_t stream);
 
+/* A RUN of nblocks identical PreActFixupResBlocks (mode 'same', no skip conv) on a tiny grid
+ * (batch*h*w*d <= 256, channels <= 32, branch <= 16, both multiples of 4): forward in ONE launch,
+ * backward in ONE launch, one workgroup walking the blocks with the residual stream in LDS (fp32).
+ * Replaces, for the published model's 50 + 50 top-level blocks (8x8x2, 32 channels), the
+ * per-block calls of layers.py:176-195 and their autograd backward.  bf16 with (32, 16) runs on the
+ * matrix cores, everything else on fp32 VALU.
+ * params: device array [nblocks][11] of device pointers, per block {w1, w2, w3, bias1a, bias1b,
+ * bias2a, bias2b, bias3a, bias3b, scale, bias4}; grads: the same layout for the fp32 gradient
+ * buffers, all accumulated (+=), deterministically.  saved: vq3d_preact_stack_saved_floats fp32
+ * written by the forward (each block's input, t2, t3) and read by the backward. */
+int vq3d_preact_stack_supported(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd);
+size_t vq3d_preact_stack_saved_floats(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                                      int32_t w, int32_t dd);
+int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                          int32_t w, int32_t dd, const void *x, const float *const *params, void *out, float *saved,
+                          vq3d_stream_t stream);
+int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                          int32_t w, int32_t dd, const void *g, const float *const *params, float *const *grads,
+                          const float *saved, void *gx, vq3d_stream_t stream);
+
 /* Whole PreActFixupResBlock (mode 'same', no skip conv) on few channels: (channels, branch) in
  * {(2, 1), (4, 2), (8, 4)}, bf16, power-of-two grid.  Forward in one launch writes out, t2 and t3
  * ([B][H][W][D][branch] bf16, as the unfused convs' epilogues write them); backward in two
