@@ -1,17 +1,32 @@
 #!/usr/bin/env python3
 """Throughput of the 3D VQ-VAE-2 training step (enc + VQ + dec, fwd + bwd + Adam) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3l_pub]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3l_pub] [--eager] [--encode-only]
 
 N > 1 runs under torch.distributed.run, one process per GPU (RCCL); each rank trains on its
 own synthetic 512x512x128 volume (weak scaling: batch 1 per GPU, BASELINE.json configs[2]).
 Rank 0 prints ONE JSON line.  Default workload = the BASELINE metric's configuration:
 3-layer VQ-VAE with the reference's published block counts (50 pre-q / 50 post-q / 3 post-up /
 2 post-down, K = 128/256/512, slurm-jobs/train_vqvae_3d.job:76-86), bf16 activations.
+--config 2l_pub is BASELINE configs[1] (256x256x128, batch 2); --encode-only is configs[3]
+(eval encode + codebook search per volume, the extract_embeddings.py path).
+
+The line carries:
+  roofline       the dominant kernel of the step -- the top kernel of the step's own rocprofv3
+                 kernel-time ranking (profiles/r02_step_top.json, tools/step_profile.py) that has
+                 a probe below -- launched alone on resident inputs and timed with HIP events on
+                 its stream; achieved = algorithmic bytes / average launch time; traffic = PMC HBM
+                 bytes per launch (profiles/r02_pmc_<kernel>.json) when collected
+  roofline_top   the same for the top probe-able kernels of the ranking
+  step_conv_roofline_frac  the per-layer conv roofline of the whole step (SURVEY.md 8(d):
+                 5.55 ms per 3L-pub volume) / the measured step time
+  cpu_baseline   the CPU oracle (oracle/vqvae_cpu.py) on this host: warm-up + median of 2 steps
+                 on a bounded sample volume, scaled by voxel count
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -20,26 +35,32 @@ sys.path.insert(0, os.path.join(ROOT, "3d-vq-vae-2_amd"))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (model kwargs, volume (H, W, D), batch per GPU)
+    # name: (model kwargs, volume (H, W, D), batch per GPU, conv-roofline ms per volume)
     "3l_pub": (dict(n_bottleneck_blocks=3, n_pre_quantization_blocks=50, n_post_quantization_blocks=50,
                     n_post_upscale_blocks=3, n_post_downscale_blocks=2, num_embeddings=[128, 256, 512]),
-               (512, 512, 128), 1),
-    "3l_dflt": (dict(n_bottleneck_blocks=3, num_embeddings=[256]), (512, 512, 128), 1),
+               (512, 512, 128), 1, 5.55),
+    "3l_dflt": (dict(n_bottleneck_blocks=3, num_embeddings=[256]), (512, 512, 128), 1, 1.97),
     "2l_pub": (dict(n_bottleneck_blocks=2, n_pre_quantization_blocks=150, n_post_quantization_blocks=150,
                     n_post_upscale_blocks=5, n_post_downscale_blocks=5, num_embeddings=[128, 256]),
-               (256, 256, 128), 2),
-    "2l_dflt": (dict(n_bottleneck_blocks=2, num_embeddings=[256]), (256, 256, 128), 2),
+               (256, 256, 128), 2, 2.52),
+    "2l_dflt": (dict(n_bottleneck_blocks=2, num_embeddings=[256]), (256, 256, 128), 2, 0.49),
 }
+ENC_ROOF_MS = {"3l_pub": 0.42, "3l_dflt": 0.27}  # encoder-only fwd roofline per volume
+ENC_BYTES = {"3l_pub": 3.39e9, "3l_dflt": 2.19e9}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_PEAK_TFS = 2500.0  # dense bf16
+STEP_TOP = os.path.join(ROOT, "profiles", "r02_step_top.json")
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="3l_pub", choices=sorted(CONFIGS))
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--size", type=int, nargs=3, default=None, help="override the volume H W D")
+    p.add_argument("--encode-only", action="store_true", help="eval encode + codebook search (configs[3])")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="print per-step times to stderr")
@@ -47,53 +68,134 @@ def parse():
                    help="run weight gradients on the main stream (default: side stream, overlapped)")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
+    p.add_argument("--no-dist-graph", action="store_true", help="N > 1: never capture the collectives")
     return p.parse_args()
 
 
-# ---------------------------------------------------------------------------------------------- roofline
-# Dominant kernel of the path = the one with the largest share of the step's kernel time in the
-# rocprofv3 kernel trace of this bench (profiles/r01_step_breakdown_v9.txt): the fused forward of
-# the 18-channel PreActFixupResBlock at 128x128x32 (preact_mid.hip, 50 launches per step, decoder
-# bottom level).  Algorithmic bytes per launch = bf16 x (18 ch) read + out (18 ch), t2 (9 ch),
-# t3 (9 ch) written + the three fp32 weight tensors.
-DOM = dict(channels=18, branch=9, grid=(128, 128, 32))
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_dominant.json")
-DOM_NAME = "vq3d preact_mid_fwd: fused PreActFixupResBlock 18ch/branch 9 @128x128x32 bf16"
-
-
-def dominant_setup(dev, seed=7):
-    """(launch(), algorithmic bytes, flops) of one dominant-kernel launch on resident inputs."""
+# ---------------------------------------------------------------------------------------------- kernel probes
+def _mid_block(dev, seed=7):
     import torch
 
     from vq3d import layers as VL
-    from vq3d import ops
+    from vq3d.flat import FlatParams
     torch.manual_seed(seed)
-    blk = VL.PreActFixupResBlock(DOM["channels"], DOM["channels"], mode="same").to(dev)
-    h, w, d = DOM["grid"]
+    blk = VL.PreActFixupResBlock(18, 18, mode="same").to(dev)
+    FlatParams(blk.parameters(), dev)
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.normal_(0, 0.2)
     g = torch.Generator(device=dev).manual_seed(seed)
-    x = (torch.randn((1, DOM["channels"], h, w, d), device=dev, generator=g) * 0.5).to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last_3d)
-    assert ops.preact_mid_supported(x, DOM["branch"])
-
-    def launch():
-        return ops.preact_mid_fwd(x, blk)
-    nvox = h * w * d
-    c, b = DOM["channels"], DOM["branch"]
-    wbytes = sum(p.numel() for p in (blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight)) * 4
-    algo = nvox * (2 * c + 2 * b) * 2 + wbytes
-    flops = 2.0 * nvox * (c * b + b * b * 27 + b * c)
-    return launch, algo, flops
+    shape = (1, 18, 128, 128, 32)
+    x = (torch.randn(shape, device=dev, generator=g) * 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last_3d)
+    gy = (torch.randn(shape, device=dev, generator=g) * 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last_3d)
+    return blk, x, gy
 
 
-def dominant_kernel_roofline(dtype, dev, iters=50):
+def probe_mid(dev, kind):
+    """Kernels of the fused 18-channel / branch-9 block at 128x128x32 (the decoder's 50 bottom-level
+    post-quantize blocks), launched alone through vq3d_preact_mid_*_stages."""
     import torch
-    launch, algo, flops = dominant_setup(dev)
+
+    from vq3d import _lib as L
+    from vq3d import ops
+    blk, x, gy = _mid_block(dev)
+    nv = 128 * 128 * 32
+    out, t2, t3 = ops.preact_mid_fwd(x, blk)
+    grads = {n: p.grad for n, p in (("dw1", blk.branch_conv1.weight), ("dw2", blk.branch_conv2.weight),
+                                    ("dw3", blk.branch_conv3.weight), ("dbias1a", blk.bias1a),
+                                    ("dbias1b", blk.bias1b), ("dbias2a", blk.bias2a), ("dbias2b", blk.bias2b),
+                                    ("dbias3a", blk.bias3a), ("dbias3b", blk.bias3b), ("dscale", blk.scale),
+                                    ("dbias4", blk.bias4))}
+    gx = torch.empty_like(x)
+    ws = ops.workspace(L.query("vq3d_preact_mid_workspace_bytes", 1, 128, 128, 32), dev)
+    ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, bufs=(gx, ws))
+    wb = (18 * 9 * 2 + 9 * 9 * 27) * 4
+    fl_pw, fl_k3 = 2.0 * nv * 18 * 9, 2.0 * nv * 9 * 9 * 27
+    if kind == "k_pm_fwd":  # t3 and out from t2 (halo) and x: reads t2 9 + x 18, writes t3 9 + out 18
+        return (lambda: ops.preact_mid_fwd(x, blk, stages=2, bufs=(out, t2, t3)), nv * 54 * 2 + wb, fl_k3 + fl_pw,
+                "k_pm_fwd: fused 18-ch block t3 + out (3x3x3 9->9 + 1x1 9->18 + residual) @128x128x32 bf16")
+    if kind == "k_pm_t2":
+        return (lambda: ops.preact_mid_fwd(x, blk, stages=1, bufs=(out, t2, t3)), nv * 27 * 2 + wb, fl_pw,
+                "k_pm_t2: fused 18-ch block t2 (1x1 18->9 + elu) @128x128x32 bf16")
+    if kind == "k_pm_bwd2":  # reads gz3 9 + t2 9 + x 18 + g 18, writes gx 18
+        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=2, bufs=(gx, ws)), nv * 72 * 2 + wb,
+                2 * fl_k3 + 2 * fl_pw,
+                "k_pm_bwd2: fused 18-ch block backward tile (dgrad 3x3x3 + W2 grad + 1x1 dgrad + W1 grad) @128x128x32")
+    if kind == "k_pm_bwd1":  # reads g 18 + t3 9, writes gz3 9
+        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=1, bufs=(gx, ws)), nv * 36 * 2 + wb,
+                2 * fl_pw, "k_pm_bwd1: fused 18-ch block backward pointwise (gz3 + W3 grad) @128x128x32")
+    raise KeyError(kind)
+
+
+def probe_stack(dev, kind):
+    """The fused run of 50 top-level blocks (8x8x2, 32 channels, branch 16, bf16) through
+    vq3d_preact_stack_fwd / _bwd (one launch each)."""
+    import torch
+
+    from vq3d import _lib as L
+    from vq3d import layers as VL
+    from vq3d.flat import FlatParams
+    from vq3d.functional import StackPlan
+    torch.manual_seed(3)
+    nblk, c, nb, shp = 50, 32, 16, (8, 8, 2)
+    stack = VL.BlockStack(*[VL.PreActFixupResBlock(c, c, mode="same") for _ in range(nblk)]).to(dev)
+    FlatParams(stack.parameters(), dev)
+    with torch.no_grad():
+        for p in stack.parameters():
+            p.normal_(0, 0.05)
+    cl = torch.channels_last_3d
+    x = torch.randn((1, c) + shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    gy = torch.randn((1, c) + shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    out, gx = torch.empty_like(x), torch.empty_like(x)
+    plan = StackPlan(list(stack))
+    ptab, gtab = plan.tables(dev)
+    dims = (L.dtype_code(x), nblk, 1, c, nb) + shp
+    saved = torch.empty(L.query("vq3d_preact_stack_saved_floats", *dims[1:]), dtype=torch.float32, device=dev)
+
+    def fwd():
+        L.call("vq3d_preact_stack_fwd", *dims, L.ptr(x), L.ptr(ptab), L.ptr(out), L.ptr(saved), L.stream())
+
+    def bwd():
+        L.call("vq3d_preact_stack_bwd", *dims, L.ptr(gy), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
+               L.stream())
+    fwd()
+    nv = 128
+    wbytes = nblk * (c * nb * 2 + nb * nb * 27 + 8) * 4
+    # the residual stream and saved branch tensors stay in the kernel's LDS / L2; HBM sees the
+    # weights, the saved-tensor round trip (fp32) and the bf16 input / output
+    sv = saved.numel() * 4
+    flops = nblk * 2.0 * nv * (c * nb * 2 + nb * nb * 27)
+    if kind == "k_stackm_fwd":
+        return fwd, wbytes + sv + 2 * nv * c * 2, flops, \
+            "k_stackm_fwd: 50 fused top-level blocks (8x8x2, 32 ch) forward, one launch"
+    if kind == "k_stackm_bwd":
+        return bwd, 2 * wbytes + sv + 2 * nv * c * 2, 2 * flops, \
+            "k_stackm_bwd: 50 fused top-level blocks (8x8x2, 32 ch) backward, one launch"
+    raise KeyError(kind)
+
+
+PROBES = {
+    "k_pm_bwd2": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
+    "k_stackm_bwd": probe_stack, "k_stackm_fwd": probe_stack,
+}
+
+
+def probe_for(name):
+    for k in PROBES:
+        if k + "<" in name or name.endswith(k) or (k + " ") in name or k == name.split("::")[-1].split("<")[0]:
+            return k
+    return None
+
+
+def timed_launch(dev, launch, iters=20):
+    """Average launch time: `iters` back-to-back launches captured in a HIP graph, HIP events
+    on the replay stream (no host gaps)."""
+    import torch
     for _ in range(3):
         launch()
     torch.cuda.synchronize()
-    # the `iters` launches captured in a HIP graph, so the events time back-to-back kernels on
-    # the replay stream (no host launch gaps)
     side = torch.cuda.Stream()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.stream(side):
@@ -108,42 +210,88 @@ def dominant_kernel_roofline(dtype, dev, iters=50):
     graph.replay()
     e1.record(st)
     e1.synchronize()
-    t = e0.elapsed_time(e1) / 1e3 / iters
+    return e0.elapsed_time(e1) / 1e3 / iters
+
+
+def roofline_of(dev, kind, step_entry=None):
+    launch, algo, flops, desc = PROBES[kind](dev, kind)
+    t = timed_launch(dev, launch)
     achieved = algo / t / 1e9
     traffic = None
-    if os.path.exists(PMC_FILE):
+    pmc = os.path.join(ROOT, "profiles", f"r02_pmc_{kind}.json")
+    if os.path.exists(pmc):
         try:
-            pmc = json.load(open(PMC_FILE))
-            if pmc.get("kernel") == DOM_NAME:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             traffic = None
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": DOM_NAME,
-            "avg_launch_us": t * 1e6, "algorithmic_bytes": algo, "tflops": flops / t / 1e12}
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": traffic, "kernel": desc, "avg_launch_us": t * 1e6, "algorithmic_bytes": algo,
+         "tflops": flops / t / 1e12, "mfma_frac_of_peak": flops / t / 1e12 / MFMA_PEAK_TFS}
+    if step_entry:
+        r["step_share"] = {"launches_per_step": step_entry["launches"], "us_per_step": step_entry["total_us"],
+                           "trace_avg_us": step_entry["avg_us"]}
+    return r
 
 
+def rooflines(dev, top=5):
+    """(dominant, top list) from the committed step ranking; kernels without a probe are
+    listed by name with their step share only."""
+    ranking = []
+    if os.path.exists(STEP_TOP):
+        ranking = json.load(open(STEP_TOP)).get("by_name", [])
+    out, skipped = [], []
+    for e in ranking:
+        k = probe_for(e["kernel"])
+        if k is None:
+            if len(out) < top:
+                skipped.append({"kernel": e["kernel"], "us_per_step": e["total_us"], "launches": e["launches"]})
+            continue
+        if any(r.get("probe") == k for r in out):
+            continue
+        r = roofline_of(dev, k, e)
+        r["probe"] = k
+        out.append(r)
+        if len(out) >= top:
+            break
+    if not out:
+        r = roofline_of(dev, "k_pm_bwd2")
+        r["probe"] = "k_pm_bwd2"
+        out.append(r)
+    return out[0], out, skipped
+
+
+# ---------------------------------------------------------------------------------------------- distributed
 def dist_graph_probe(dev, rank, world):
-    """Capture + replay one RCCL all-reduce in a HIP graph; True when every rank got the right
-    value (agreed through an eager all-reduce of the per-rank verdicts)."""
+    """Capture + replay the step's collective pattern in a HIP graph: a bucket all-reduce issued
+    asynchronously on a side communication stream and joined back (vq3d.parallel), plus a plain
+    all-reduce (the fused EMA statistics); True when every rank got the right values."""
     import torch
     import torch.distributed as dist
     ok = 1.0
     try:
         t = torch.full((256,), float(rank + 1), device=dev)
+        u = torch.full((64,), float(rank + 1), device=dev)
         side = torch.cuda.Stream()
+        comm = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
             with torch.cuda.graph(g, stream=side):
-                dist.all_reduce(t)
+                dist.all_reduce(u)
+                comm.wait_stream(side)
+                with torch.cuda.stream(comm):
+                    w = dist.all_reduce(t, op=dist.ReduceOp.AVG, async_op=True)
+                w.wait()
+                side.wait_stream(comm)
         torch.cuda.synchronize()
         t.fill_(float(rank + 1))
+        u.fill_(float(rank + 1))
         g.replay()
         torch.cuda.synchronize()
-        ok = 1.0 if abs(float(t[0]) - world * (world + 1) / 2) < 1e-3 else 0.0
+        ok = 1.0 if (abs(float(t[0]) - (world + 1) / 2) < 1e-3 and abs(float(u[0]) - world * (world + 1) / 2) < 1e-3) \
+            else 0.0
     except Exception as e:  # capture unsupported: fall back to eager launches
-        print(f"[bench] rank {rank}: graph capture of all_reduce failed ({e}); eager", file=sys.stderr)
+        print(f"[bench] rank {rank}: graph capture of the collectives failed ({e}); eager", file=sys.stderr)
         ok = 0.0
     v = torch.tensor([ok], device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MIN)
@@ -151,10 +299,10 @@ def dist_graph_probe(dev, rank, world):
 
 
 # ---------------------------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(mkw, size, sample=(256, 256, 64)):
-    """The CPU oracle (oracle/vqvae_cpu.py, fp32 torch-CPU restatement of the reference step)
-    timed on this host: one full training step of the same model on a smaller volume with
-    `frac` of the voxels, scaled to volumes/s of the full 512x512x128 volume."""
+def cpu_baseline(mkw, size, encode_only=False, sample=(256, 256, 64), reps=2):
+    """The CPU oracle (oracle/vqvae_cpu.py, fp32 torch-CPU restatement of the reference step) on
+    this host: one warm-up, then the median of `reps` steps of the same model on a sample volume
+    with `frac` of the voxels, scaled to volumes/s of the full volume."""
     import torch
 
     from oracle import vqvae_cpu as O
@@ -167,14 +315,46 @@ def cpu_baseline(mkw, size, sample=(256, 256, 64)):
     sd = {k: v.detach().clone() for k, v in ref.state_dict().items()}
     x = torch.rand((1, 1) + tuple(sample), generator=torch.Generator().manual_seed(1234)) * 4.5 - 0.5
     st = {}
-    O.train_step(cfg, sd, st, x, [sample[2]], 1e-4)  # warm-up (first-pass codebook init)
-    t0 = time.perf_counter()
-    O.train_step(cfg, sd, st, x, [sample[2]], 1e-4)
-    dt = time.perf_counter() - t0
+    if encode_only:
+        def once():
+            with torch.no_grad():
+                O.encode(cfg, sd, x, train=False)
+        for k in [k for k in sd if k.endswith("first_pass")]:
+            sd[k].zero_()
+    else:
+        def once():
+            O.train_step(cfg, sd, st, x, [sample[2]], 1e-4)
+    once()  # warm-up (first-pass codebook init)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        once()
+        ts.append(time.perf_counter() - t0)
+    dt = statistics.median(ts)
     frac = (sample[0] * sample[1] * sample[2]) / float(size[0] * size[1] * size[2])
+    what = "eval encode" if encode_only else "train step"
     return {"value": frac / dt, "unit": "volumes/s", "cores": threads, "kind": "port",
-            "sample": f"one oracle train step (fp32, same model) on a {sample[0]}x{sample[1]}x{sample[2]} "
-                      f"volume = {frac:.4g} of the 512x512x128 voxels, {dt:.2f} s, scaled by voxel count"}
+            "sample": f"oracle {what} (fp32 torch-CPU, same model) on a {sample[0]}x{sample[1]}x{sample[2]} volume "
+                      f"= {frac:.4g} of the {size[0]}x{size[1]}x{size[2]} voxels: warm-up + median of {reps} "
+                      f"({', '.join(f'{t:.2f}' for t in ts)} s), scaled by voxel count"}
+
+
+# ---------------------------------------------------------------------------------------------- main
+def capture(step, warmup):
+    """Capture one call of step() as a HIP graph (after an allocator warm-up on the capture
+    stream); returns (graph, static result)."""
+    import torch
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step(warmup)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        res = step(warmup + 1)
+    torch.cuda.synchronize()
+    return graph, res
 
 
 def main():
@@ -183,65 +363,68 @@ def main():
     import torch.distributed as dist
 
     import vq3d
-    from vq3d import parallel
+    from vq3d import ops, parallel
     from vq3d.utils import synthetic_volume
 
     rank, world, local, dev = parallel.init_from_env()
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    mkw, size, batch = CONFIGS[a.config]
+    mkw, size, batch, roof_ms = CONFIGS[a.config]
     if a.size:
         size = tuple(a.size)
     torch.manual_seed(0)
-    from vq3d import ops
     ops.set_concurrent_wgrad(not a.serial_wgrad)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
-    model.train()
-    opt = model.configure_optimizers()
-    allreduce = parallel.GradientAllReduce(model)
+    if a.encode_only:
+        batch = 1
     # this rank's synthetic volumes, resident in HBM before timing
     idx = parallel.shard_indices(0, rank, world, batch)
     x = torch.cat([synthetic_volume((1, 1) + size, i) for i in idx]).to(dev)
     nvs = torch.full((batch,), size[2], dtype=torch.int64, device=dev)
+    allreduce = None
+    if a.encode_only:
+        from vq3d.extract import extract_samples
+        model.eval()
+        for q in model.encoder.quantize:  # a trained checkpoint's codebooks (no first-pass init in eval)
+            q.first_pass.zero_()
+            q.first_pass_host = False
 
-    def step(i):
-        opt.zero_grad()
-        loss = model.training_step((x, nvs), i)
-        loss.backward()
-        allreduce()
-        opt.step()
-        return loss
+        def step(i):
+            with torch.no_grad():
+                return next(extract_samples(model, [x]))[0]
+    else:
+        model.train()
+        opt = model.configure_optimizers()
+        allreduce = parallel.GradientAllReduce(model)
+
+        def step(i):
+            opt.zero_grad()
+            loss = model.training_step((x, nvs), i)
+            loss.backward()
+            allreduce()
+            opt.step()
+            return loss
 
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
-    # Capture one whole training step (forward, loss, backward, gradient all-reduce, Adam; ~3.7k
-    # kernel launches) as a HIP graph after the eager warm-up (the Quantizer's first-pass init
-    # happened there) and replay it per step: no Python / launch overhead on the timed path.
-    # Every replay runs the full step on the resident input; Adam's step count lives on the
-    # device.  N > 1: the RCCL collectives (EMA statistics in forward, gradient all-reduce) are
-    # captured too, after a probe capture of one all-reduce succeeded on every rank; otherwise
-    # (or with VQ3D_BENCH_DIST_GRAPH=0) the ranks run eagerly.
+    # Capture one whole step (training: forward, loss, backward, gradient all-reduce, Adam) as a
+    # HIP graph after the eager warm-up (the Quantizer's first-pass init happened there) and
+    # replay it per step: no Python / launch overhead on the timed path; every replay runs the
+    # full step on the resident input; Adam's step count lives on the device.  N > 1: the RCCL
+    # collectives are captured too once a probe capture of the same pattern replayed correctly on
+    # every rank; otherwise the ranks run eagerly.
     graph = None
     use_graph = not a.eager and a.warmup >= 2
     if use_graph and world > 1:
-        use_graph = os.environ.get("VQ3D_BENCH_DIST_GRAPH", "1") != "0" and dist_graph_probe(dev, rank, world)
+        use_graph = not a.no_dist_graph and dist_graph_probe(dev, rank, world)
     if use_graph:
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            step(a.warmup)  # allocator warm-up on the capture stream (one more untimed step)
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            loss_static = step(a.warmup + 1)
-        torch.cuda.synchronize()
+        graph, static = capture(step, a.warmup)
 
         def step(i):  # noqa: F811
             graph.replay()
-            return loss_static
+            return static
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -249,7 +432,7 @@ def main():
     per = []
     for i in range(a.steps):
         ts = time.perf_counter()
-        loss = step(a.warmup + i)
+        res = step(a.warmup + i)
         if a.profile_steps:
             torch.cuda.synchronize()
             per.append(time.perf_counter() - ts)
@@ -264,31 +447,54 @@ def main():
         elapsed = float(t)
     if a.profile_steps and rank == 0:
         print("per-step s:", [round(v, 4) for v in per], file=sys.stderr)
-    final_loss = float(loss.detach())
     vols = world * batch * a.steps
-    res = {
-        "metric": "volumes/sec (enc+VQ+dec fwd+bwd) at 512x512x128",
+    ms = 1000.0 * elapsed / a.steps
+    if a.encode_only:
+        metric = f"volumes/sec (encode+VQ, eval, codes extraction) at {size[0]}x{size[1]}x{size[2]}"
+        workload = f"vqvae_{a.config}_encode_extract"
+    else:
+        metric = f"volumes/sec (enc+VQ+dec fwd+bwd) at {size[0]}x{size[1]}x{size[2]}"
+        workload = f"vqvae_{a.config}_train_step"
+    res_line = {
+        "metric": metric,
         "value": vols / elapsed,
         "unit": "volumes/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": 1000.0 * elapsed / a.steps,
+        "ms_per_step": ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": a.dtype,
         "data": "synthetic (torch.rand*4.5-0.5 volumes, reference init weights, seed 0)",
         "launch": "hip_graph" if graph is not None else "eager",
-        "config": {"workload": f"vqvae_{a.config}_train_step", "volume": list(size), "batch_per_gpu": batch,
-                   "global_batch": batch * world, "parallelism": f"dp{world}", "final_loss": final_loss},
+        "config": {"workload": workload, "volume": list(size), "batch_per_gpu": batch, "global_batch": batch * world,
+                   "parallelism": f"dp{world}" if not a.encode_only else f"replicas{world}"},
     }
+    if not a.encode_only:
+        res_line["config"]["final_loss"] = float(res.detach())
+        res_line["step_conv_roofline_frac"] = roof_ms * batch / ms
+        res_line["step_conv_roofline"] = {"ms_per_volume": roof_ms, "source": "SURVEY.md 8(d) per-layer conv "
+                                          "roofline (bf16 bytes per layer / 8 TB/s, FLOPs / 2.5 PF)"}
+    elif a.config in ENC_ROOF_MS:
+        res_line["step_conv_roofline_frac"] = ENC_ROOF_MS[a.config] / ms
+        res_line["encoder_traffic_frac"] = ENC_BYTES[a.config] / (ms / 1e3) / 1e9 / HBM_PEAK_GBS
     if rank == 0 and not a.no_roofline:
-        res["roofline"] = dominant_kernel_roofline(a.dtype, dev)
+        dom, top, unprobed = rooflines(dev)
+        res_line["roofline"] = dom
+        res_line["roofline_top"] = [{k: r[k] for k in ("probe", "frac", "achieved", "avg_launch_us", "tflops",
+                                                       "mfma_frac_of_peak", "traffic") if k in r} |
+                                    ({"us_per_step": r["step_share"]["us_per_step"]} if "step_share" in r else {})
+                                    for r in top]
+        if unprobed:
+            res_line["unprobed_above_dominant"] = unprobed
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(mkw, size)
+        res_line["cpu_baseline"] = cpu_baseline(mkw, size, encode_only=a.encode_only)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res_line), flush=True)
+    if allreduce is not None:
+        allreduce.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""Launch the dominant kernel (bench.py DOM: fused 18-channel PreAct block forward @128x128x32,
-bf16) N times with the Infinity Cache flushed in between, for rocprofv3 PMC passes:
+"""Launch one of bench.py's kernel probes (default: the dominant one of profiles/r02_step_top.json)
+N times with the Infinity Cache flushed in between, for rocprofv3 PMC passes (one counter
+block per run, MI355X_MICROARCH.md §HBM):
 
   rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_f -o run --output-format csv -- \
-      python3 tools/dominant_kernel.py
+      python3 tools/dominant_kernel.py k_pm_bwd2
   rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_w -o run --output-format csv -- \
-      python3 tools/dominant_kernel.py
-  python3 tools/pmc_traffic.py gpurun_out/pmc_f gpurun_out/pmc_w > profiles/pmc_dominant.json
+      python3 tools/dominant_kernel.py k_pm_bwd2
+  python3 tools/pmc_traffic.py k_pm_bwd2 gpurun_out/pmc_f gpurun_out/pmc_w > profiles/r02_pmc_k_pm_bwd2.json
 """
+import json
 import os
 import sys
 
@@ -20,14 +22,29 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
-def main(n=int(sys.argv[1]) if len(sys.argv) > 1 else 10):
+def dominant():
+    for e in json.load(open(bench.STEP_TOP))["by_name"]:
+        k = bench.probe_for(e["kernel"])
+        if k:
+            return k
+    return "k_pm_bwd2"
+
+
+def main():
+    kind = sys.argv[1] if len(sys.argv) > 1 else dominant()
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     dev = torch.device("cuda:0")
-    launch, _, _ = bench.dominant_setup(dev)
-    flush = torch.empty(300 * 2 ** 20 // 4, device=dev)  # evicts the inputs from the Infinity Cache
+    launch = bench.PROBES[kind](dev, kind)[0]
+    # a 300 MB READ sweep between launches evicts the inputs from L2 and the Infinity Cache without
+    # leaving dirty lines whose write-back would be counted in the next launch's WRITE_SIZE
+    flush = torch.ones(300 * 2 ** 20 // 4, device=dev)
+    sink = torch.empty((), device=dev)
+    torch.cuda.synchronize()
     for _ in range(n):
-        flush.zero_()
+        torch.sum(flush, dim=0, out=sink)
         launch()
     torch.cuda.synchronize()
+    print(kind)
 
 
 if __name__ == "__main__":

@@ -32,7 +32,7 @@ def fake_call(name, *args):
 
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "3l_pub"
-    mkw, size, batch = bench.CONFIGS[cfg]
+    mkw, size, batch = bench.CONFIGS[cfg][:3]
     if len(sys.argv) > 4:
         size = tuple(int(v) for v in sys.argv[2:5])
     L.call = fake_call

@@ -1,36 +1,43 @@
 #!/usr/bin/env python3
-"""Per-launch HBM bytes of the dominant kernel (bench.DOM_NAME) from two rocprofv3 --pmc passes
-(FETCH_SIZE, WRITE_SIZE; kilobytes per dispatch).  Correction per MI355X_MICROARCH.md
-§HBM: FETCH_SIZE reads exactly 1/2 of a wide coalesced streaming read on gfx950, so the
-read side is doubled; WRITE_SIZE is taken as is.  Prints JSON."""
+"""Per-launch HBM bytes of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE;
+kilobytes per dispatch) of tools/dominant_kernel.py.
+
+    python3 tools/pmc_traffic.py KERNEL FETCH_DIR WRITE_DIR > profiles/r02_pmc_KERNEL.json
+
+Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 64 B per 128 B request of a wide
+coalesced streaming read on gfx950, so the read side is doubled; WRITE_SIZE is taken as is.
+The first dispatch of each pass (cold instruction cache / first touch) is dropped."""
 import csv
 import glob
 import json
 import os
 import sys
 
-KERNEL = "k_preact_mid_fwd"
 
-
-def per_dispatch(d, counter):
+def per_dispatch(d, kernel, counter):
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     vals = {}
     for r in csv.DictReader(open(path)):
-        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return list(vals.values())
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            k = int(r["Dispatch_Id"])
+            vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+    v = [vals[k] for k in sorted(vals)]
+    return v[1:] if len(v) > 1 else v
 
 
 def main():
-    f = per_dispatch(sys.argv[1], "FETCH_SIZE")
-    w = per_dispatch(sys.argv[2], "WRITE_SIZE")
+    kernel, fdir, wdir = sys.argv[1:4]
+    f = per_dispatch(fdir, kernel, "FETCH_SIZE")
+    w = per_dispatch(wdir, kernel, "WRITE_SIZE")
+    if not f or not w:
+        sys.exit(f"no {kernel} dispatches in the counter files")
     fetch = sum(f) / len(f) * 1024.0
     write = sum(w) / len(w) * 1024.0
-    out = {"kernel": "vq3d preact_mid_fwd: fused PreActFixupResBlock 18ch/branch 9 @128x128x32 bf16", "dispatches": [len(f), len(w)],
+    out = {"kernel": kernel, "dispatches": [len(f), len(w)],
            "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2.0 * fetch + write,
            "note": "FETCH_SIZE doubled (gfx950 counts 64 B per 128 B request, MI355X_MICROARCH.md §HBM); "
-                   "Infinity-Cache flushed with a 300 MB write between launches"}
+                   "L2 / Infinity Cache swept by a 300 MB read between launches (tools/dominant_kernel.py)"}
     print(json.dumps(out, indent=1))
 
 
