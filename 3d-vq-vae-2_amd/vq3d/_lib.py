@@ -69,6 +69,13 @@ _SIGS = {
     "vq3d_preact_stack_saved_floats": (c_size, [c_int] * 7),
     "vq3d_preact_stack_fwd": (c_int, [c_int] * 8 + [P] * 5),
     "vq3d_preact_stack_bwd": (c_int, [c_int] * 8 + [P] * 6),
+    "vq3d_preact_wide_supported": (c_int, [c_int] * 6),
+    "vq3d_preact_wide_image_bytes": (c_size, [c_int] * 2),
+    "vq3d_preact_wide_pack": (c_int, [c_int] * 3 + [P] * 3),
+    "vq3d_preact_wide_fwd": (c_int, [c_int] * 6 + [P] * 7),
+    "vq3d_preact_wide_workspace_bytes": (c_size, [c_int] * 4),
+    "vq3d_preact_wide_bwd_data": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P, P]),
+    "vq3d_preact_wide_bwd_weight": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P]),
     "vq3d_preact_small_supported": (c_int, [c_int] * 7),
     "vq3d_preact_small_workspace_bytes": (c_size, [c_int] * 6),
     "vq3d_preact_small_fwd": (c_int, [c_int] * 7 + [P] * 9),

@@ -227,6 +227,53 @@ class PreActStackFn(torch.autograd.Function):
         return (gx, None) + (None,) * len(plan.params)
 
 
+class PreActWideFn(torch.autograd.Function):
+    """A run of 72-channel / branch-36 PreActFixupResBlocks (preact_wide.hip): the weights of the
+    whole run packed once (one launch), then one fused launch per block forward and two-plus-two
+    per block backward (data path on the current stream, weight gradients on the side stream);
+    the residual and gradient streams fp32 inside the run."""
+
+    @staticmethod
+    def forward(ctx, x, plan, *params):
+        x = ops.as_cl(x)
+        b, c, h, w, d = x.shape
+        nb = plan.blocks[0].branch_conv1.weight.shape[0]
+        ptab, _ = plan.tables(x.device)
+        img, per = ops.preact_wide_pack(ptab, len(plan.blocks), c, nb, x.device)
+        base = img.data_ptr()
+        xs = ops.cast(x, torch.float32)
+        saved = []
+        for i, blk in enumerate(plan.blocks):
+            out, t2, t3 = ops.preact_wide_fwd(xs, base + i * per, blk)
+            saved += [xs, t2, t3]
+            xs = out
+        ctx.plan, ctx.per, ctx.in_dtype = plan, per, x.dtype
+        ctx.save_for_backward(img, *saved)
+        return ops.cast(xs, x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        img, *saved = ctx.saved_tensors
+        plan = ctx.plan
+        base = img.data_ptr()
+        gs = ops.cast(_cl(g), torch.float32)
+        for i in reversed(range(len(plan.blocks))):
+            blk = plan.blocks[i]
+            xs, t2, t3 = saved[3 * i: 3 * i + 3]
+            names = {"dw1": blk.branch_conv1.weight, "dw2": blk.branch_conv2.weight, "dw3": blk.branch_conv3.weight,
+                     "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
+                     "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
+            gs = ops.preact_wide_bwd(gs, xs, t2, t3, base + i * ctx.per, blk,
+                                     {n: grad_buf(t) for n, t in names.items()})
+        grads_ready(plan.params)
+        return (ops.cast(gs, ctx.in_dtype), None) + (None,) * len(plan.params)
+
+
+def wide_eligible(x, blk):
+    return (stack_eligible(blk) and x.is_cuda and x.dim() == 5 and x.shape[1] == blk.in_channels
+            and ops.preact_wide_supported(x, blk.branch_conv1.weight.shape[0]))
+
+
 def stack_eligible(blk):
     return (type(blk).__name__ == "PreActFixupResBlock" and blk.skip_conv is None and blk.mode in ("same", "out"))
 

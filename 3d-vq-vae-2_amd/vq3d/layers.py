@@ -222,8 +222,9 @@ class EvonormResBlock(nn.Module):
 # ============================================================================================ stacks
 class BlockStack(nn.Sequential):
     """nn.Sequential (same children, same state_dict keys) whose forward runs every maximal run of
-    >= 2 identical PreActFixupResBlocks ('same', no skip) on a tiny grid as ONE fused stack
-    (Fn.PreActStackFn: one launch forward, one backward); everything else runs module by module."""
+    identical PreActFixupResBlocks ('same', no skip) fused: >= 2 blocks on a tiny grid as ONE stack
+    (Fn.PreActStackFn: one launch forward, one backward), a run of 72-channel / branch-36 blocks
+    through Fn.PreActWideFn (preact_wide.hip); everything else runs module by module."""
 
     def forward(self, x):
         mods = list(self)
@@ -235,14 +236,20 @@ class BlockStack(nn.Sequential):
                 while (j + 1 < len(mods) and Fn.stack_eligible(mods[j + 1]) and mods[j + 1].in_channels == c
                        and mods[j + 1].branch_conv1.weight.shape[0] == nb):
                     j += 1
-            if j > i and self._stack_ok(x, mods[i]):
+            fn = None
+            if Fn.stack_eligible(mods[i]):
+                if j > i and self._stack_ok(x, mods[i]):
+                    fn = Fn.PreActStackFn
+                elif Fn.wide_eligible(x, mods[i]):
+                    fn = Fn.PreActWideFn
+            if fn is not None:
                 run = tuple(mods[i:j + 1])
                 plan = self._plans.get((i, j)) if hasattr(self, "_plans") else None
                 if plan is None or plan.blocks != list(run):
                     if not hasattr(self, "_plans"):
                         self._plans = {}
                     plan = self._plans[(i, j)] = Fn.StackPlan(run)
-                x = Fn.PreActStackFn.apply(x, plan, *plan.params)
+                x = fn.apply(x, plan, *plan.params)
                 i = j + 1
             else:
                 x = mods[i](x)

@@ -399,6 +399,69 @@ def preact_small_bwd(g, x, t2, t3, blk, grads):
     return gx
 
 
+# ------------------------------------------------------------------------------------------------ wide blocks
+_wide = [True]
+
+
+def set_wide_blocks(enabled):
+    """Route runs of bf16 72-channel / branch-36 PreAct blocks through preact_wide.hip."""
+    _wide[0] = bool(enabled)
+
+
+def preact_wide_supported(x, branch):
+    b, c, h, w, d = x.shape
+    return (_wide[0] and x.dtype == torch.bfloat16
+            and bool(L.query("vq3d_preact_wide_supported", b, c, branch, h, w, d)))
+
+
+def preact_wide_pack(ptab, nblocks, c, nb, device):
+    """Packed bf16 fragment images of a run's weights (one per block, consecutive)."""
+    per = int(L.query("vq3d_preact_wide_image_bytes", c, nb))
+    img = torch.empty(nblocks * per, dtype=torch.uint8, device=device)
+    L.call("vq3d_preact_wide_pack", nblocks, c, nb, L.ptr(ptab), L.ptr(img), L.stream())
+    return img, per
+
+
+def preact_wide_fwd(x32, img_ptr, blk):
+    """One block on the fp32 residual stream: returns out (fp32), t2, t3 (bf16), channels-last."""
+    b, c, h, w, d = x32.shape
+    nb = blk.branch_conv1.weight.shape[0]
+    out = torch.empty_like(x32, memory_format=CL)
+    t2 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device)
+    t3 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device)
+    prm = _preact_params(blk)
+    L.call("vq3d_preact_wide_fwd", b, c, nb, h, w, d, L.ptr(x32), ctypes.c_void_p(img_ptr), ctypes.byref(prm),
+           L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+    return out, t2, t3
+
+
+def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads):
+    """gx (fp32) of preact_wide_fwd; the parameter gradients (grads: name -> fp32 buffer, +=) on
+    the side stream when concurrent weight gradients are on."""
+    b, c, h, w, d = x32.shape
+    nb = blk.branch_conv1.weight.shape[0]
+    gx = torch.empty_like(x32, memory_format=CL)
+    nws = int(L.query("vq3d_preact_wide_workspace_bytes", b, h, w, d))
+    ws = torch.empty(nws, dtype=torch.uint8, device=x32.device)
+    prm = _preact_params(blk)
+    L.call("vq3d_preact_wide_bwd_data", b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
+           ctypes.c_void_p(img_ptr), ctypes.byref(prm), L.ptr(ws), ctypes.c_size_t(nws), L.ptr(gx), L.stream())
+    gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
+    args = (b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3), ctypes.byref(prm), ctypes.byref(gr),
+            L.ptr(ws), ctypes.c_size_t(nws))
+    if _concurrent:
+        main = torch.cuda.current_stream()
+        side = _side_stream(x32.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            L.call("vq3d_preact_wide_bwd_weight", *args, L.stream())
+        for t in (g32, x32, t2, t3, ws):
+            t.record_stream(side)
+    else:
+        L.call("vq3d_preact_wide_bwd_weight", *args, L.stream())
+    return gx
+
+
 # ------------------------------------------------------------------------------------------------ misc
 def cast(x, dtype):
     if x.dtype == dtype:

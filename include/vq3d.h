@@ -202,6 +202,32 @@ int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
                           int32_t w, int32_t dd, const void *g, const float *const *params, float *const *grads,
                           const float *saved, void *gx, vq3d_stream_t stream);
 
+/* The 72-channel / branch-36 PreActFixupResBlock (mode 'same', no skip conv) of the published
+ * model's decoder level 1 (50 blocks at 32x32x8, layers.py:176-195, Decoder.up layers.py:395-405):
+ * h % 2 == 0, w % 4 == 0, dd % 8 == 0, batch*h*w*dd % 512 == 0.  The residual stream (x, out, g,
+ * gx) is fp32 [B][H][W][D][72]; t2 / t3 are saved bf16 [B][H][W][D][36]; weights are read from a
+ * packed bf16 fragment image (vq3d_preact_wide_pack, per RUN of blocks, params as for
+ * vq3d_preact_stack_fwd; each block's image is vq3d_preact_wide_image_bytes long).
+ * Forward: one launch.  Backward: bwd_data (one launch: gx, plus gz3 / gz1 / scalar partials in
+ * the workspace) then bwd_weight (two launches reading the workspace: every parameter gradient,
+ * accumulated (+=) deterministically); bwd_weight may run on another stream after bwd_data. */
+int vq3d_preact_wide_supported(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd);
+size_t vq3d_preact_wide_image_bytes(int32_t channels, int32_t branch);
+int vq3d_preact_wide_pack(int32_t nblocks, int32_t channels, int32_t branch, const float *const *params, void *image,
+                          vq3d_stream_t stream);
+int vq3d_preact_wide_fwd(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+                         const float *x, const void *image, const vq3d_preact_params *p, float *out, void *t2,
+                         void *t3, vq3d_stream_t stream);
+size_t vq3d_preact_wide_workspace_bytes(int32_t batch, int32_t h, int32_t w, int32_t dd);
+int vq3d_preact_wide_bwd_data(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+                              const float *g, const float *x, const void *t2, const void *t3, const void *image,
+                              const vq3d_preact_params *p, void *workspace, size_t workspace_bytes, float *gx,
+                              vq3d_stream_t stream);
+int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+                                const float *g, const float *x, const void *t2, const void *t3,
+                                const vq3d_preact_params *p, const vq3d_preact_grads *gr, const void *workspace,
+                                size_t workspace_bytes, vq3d_stream_t stream);
+
 /* Whole PreActFixupResBlock (mode 'same', no skip conv) on few channels: (channels, branch) in
  * {(2, 1), (4, 2), (8, 4)}, bf16, power-of-two grid.  Forward in one launch writes out, t2 and t3
  * ([B][H][W][D][branch] bf16, as the unfused convs' epilogues write them); backward in two
