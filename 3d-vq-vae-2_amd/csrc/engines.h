@@ -98,4 +98,13 @@ int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const
                     const float *w, const float *escale, float *dw, float *dscale, float *dbias, float *dcbias,
                     void *ws, size_t ws_bytes, hipStream_t s);
 
+// few-channel blocks on the big grids (preact_col.hip), behind vq3d_preact_small_*
+bool col_supported(int batch, int C, int BR, int h, int w, int d);
+size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d);
+int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1, const float *w2,
+            const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3, hipStream_t s);
+int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
+            const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
+            const vq3d_preact_grads &gr, void *workspace, void *gx, hipStream_t s);
+
 }  // namespace vq3d

@@ -1,0 +1,685 @@
+// Few-channel PreActFixupResBlocks (vqvae/layers.py:176-195, mode 'same', no skip conv) on the
+// big grids: (block channels C, branch B) = (4, 2) at 512x512x128 (decoder post-upscale blocks),
+// (2, 1) at 128x128x32 (50 encoder pre-quantize blocks), (8, 4) at 256x256x64; any grid with
+// H % 8 == W % 8 == 0 and D % 32 == 0.  Forward in ONE launch, backward in TWO (fused kernel +
+// fixed-order reduction), for the vq3d_preact_small_* entry points (preact_small.hip keeps its
+// brick kernels for the small grids).
+//
+//   u1  = elu(x + b1a) + b1b      t2 = elu(W1 u1 + b2a) + b2b        (1x1, C -> B)
+//   t3  = elu(W2 (*) t2 + b3a) + b3b                                   (3x3x3 circular, B -> B)
+//   out = scale * (W3 t3) + b4 + x                                     (1x1, B -> C)
+//
+// A workgroup owns an 8 x 8 x 32 brick (2048 voxels, 256 threads).  The 1x1 convs and the
+// activations run on the VALU, one voxel per work item, weights wave-uniform; the 3x3x3 conv and
+// its backward run on the matrix cores (v_mfma_f32_16x16x32_bf16) with a "row-windowed" K: for a
+// voxel and a tap row (kh, kw) the 3 kd taps x B channels are 3B consecutive bf16 of the halo line
+// (position-major [line][pos][B]), padded to 8 (B <= 2) or 16 (B = 4) K entries whose extra
+// weights are zero, so one k-step covers 4 (or 2) tap rows of 16 voxels.  Only B of the 16 MFMA
+// columns are real: the k^3 conv is still ~2x cheaper on the matrix cores than on the VALU.
+//
+//   forward  A: t2 on the brick's circular halo (10 x 10 lines x 34 positions) into LDS, the
+//               interior also to HBM (saved for the backward)
+//            B: raw W2 (*) t2 per 16-voxel m-tile (matrix cores) into LDS
+//            C: per thread 8 consecutive voxels: t3, out (16-byte stores)
+//   backward A: gz3 = bf16(scale W3^T g * elu'(t3)) on the halo; the interior's scalar sums and
+//               the W3 gradient (sum t3 (x) g) in registers; t2 on the halo channel-major
+//            B: gt2 = W2^T (*) gz3 (flipped taps) per m-tile, and the W2 gradient
+//               sum_v gz3[v][co] t2[v + tap][ci] with voxels as the MFMA reduction axis
+//            C: per thread 8 voxels: gz1 = bf16(gt2 * elu'(t2)), gx = g + (W1^T gz1) * elu'(x + b1a),
+//               the W1 gradient (sum gz1 (x) u1) and the b2 / b1 sums
+//            per-brick partial rows [entry][brick], summed in a fixed order by k_col_reduce.
+// Rounding points are the unfused path's: t2, t3, gz3, gz1, gx, out rounded to bf16, fp32
+// accumulation; the W1 gradient reads u1 rounded to bf16 (the unfused wgrad's operand).
+#include "engines.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace vq3d {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BH = 8, BW = 8, BD = 32, DV = 8;  // brick; voxels per thread along D
+constexpr int HL = BH + 2, WL = BW + 2, PL = BD + 2, NLN = HL * WL, HVX = NLN * PL;
+constexpr int NV = BH * BW * BD, NMT = NV / 16;  // 2048 voxels, 128 m-tiles
+constexpr int NT = 256;
+constexpr int TP = 40;        // channel-major halo line pitch (positions 0..33, zero pad)
+constexpr int ZP = NV + 16;   // channel-major interior pitch
+constexpr int PADE = 32;      // zero tail of the position-major halo buffers
+constexpr int NSC = 8;        // scalar partials: b4, b3b, b3a, scale, b2b, b2a, b1b, b1a
+
+template <int BR>
+struct K3 {
+    static constexpr int EPR = 3 * BR <= 8 ? 8 : 16;  // K entries per tap row
+    static constexpr int RPK = 32 / EPR;              // tap rows per k-step
+    static constexpr int KS = (9 + RPK - 1) / RPK;    // k-steps
+    static constexpr int NTN = (27 * BR + 15) / 16;   // W2-gradient column tiles
+};
+template <int C, int BR>
+constexpr int n_entries() {
+    return BR * C + 27 * BR * BR + BR * C + NSC;  // G3 [o][c], W2 [co][r][kd][ci], W1 [o][c], scalars
+}
+
+struct CArgs {
+    int B, H, W, D;
+    int nbh, nbw, nbd, nbricks;
+};
+
+__device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+__device__ __forceinline__ float bf(uint32_t u16) { return __uint_as_float(u16 << 16); }
+__device__ __forceinline__ float rbf(float v) { return bf(f2bf(v)); }
+__device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : __expf(z) - 1.f; }
+__device__ __forceinline__ float elu_d_act(float t, float b) {
+    const float z1 = t - b;
+    return z1 > 0.f ? 1.f : z1 + 1.f;
+}
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// 8 consecutive bf16 from LDS at any element offset of a 4-byte aligned base
+__device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(base + (off & ~1));
+    const uint32_t sh = uint32_t(off & 1) * 2u;
+    const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3], u4 = q[4];
+    const uint4 r = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
+                     __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
+    return __builtin_bit_cast(bf16x8, r);
+}
+// 8 bf16 at an even element offset (4-byte aligned)
+__device__ __forceinline__ bf16x8 read8e(const bf16_t *p) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+    return __builtin_bit_cast(bf16x8, uint4{q[0], q[1], q[2], q[3]});
+}
+__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+
+// N bf16 <-> fp32 (N = 1, 2, 4, 8: one 2/4/8/16-byte access)
+template <int N>
+struct Vec {
+    using U = typename std::conditional<N == 1, uint16_t,
+              typename std::conditional<N == 2, uint32_t, typename std::conditional<N == 4, uint2, uint4>::type>::type>::type;
+};
+template <int N>
+__device__ __forceinline__ void unpack(const typename Vec<N>::U &u, float (&o)[N]) {
+    if constexpr (N == 1) {
+        o[0] = bf(u);
+    } else if constexpr (N == 2) {
+        o[0] = __uint_as_float(u << 16);
+        o[1] = __uint_as_float(u & 0xffff0000u);
+    } else if constexpr (N == 4) {
+        o[0] = __uint_as_float(u.x << 16);
+        o[1] = __uint_as_float(u.x & 0xffff0000u);
+        o[2] = __uint_as_float(u.y << 16);
+        o[3] = __uint_as_float(u.y & 0xffff0000u);
+    } else {
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = __uint_as_float(w[i] << 16);
+            o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+        }
+    }
+}
+template <int N>
+__device__ __forceinline__ typename Vec<N>::U packv(const float (&v)[N]) {
+    if constexpr (N == 1) {
+        return f2bf(v[0]);
+    } else {
+        uint32_t w[(N + 1) / 2];
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+        if constexpr (N == 2) return w[0];
+        else if constexpr (N == 4) return uint2{w[0], w[1]};
+        else return uint4{w[0], w[1], w[2], w[3]};
+    }
+}
+// n bf16 (n * 2 bytes, a multiple of 16) between global memory and registers as uint4
+template <int NB>
+__device__ __forceinline__ void ld16s(const bf16_t *__restrict__ p, uint4 (&o)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) o[i] = reinterpret_cast<const uint4 *>(p)[i];
+}
+
+struct Scal {
+    float b1a, b1b, b2a, b2b, b3a, b3b, sc, b4;
+};
+__device__ __forceinline__ Scal load_scal(const vq3d_preact_params &p) {
+    return Scal{*p.bias1a, *p.bias1b, *p.bias2a, *p.bias2b, *p.bias3a, *p.bias3b, *p.scale, *p.bias4};
+}
+
+struct Org {
+    int b, h0, w0, d0;
+};
+__device__ __forceinline__ Org brick_org(const CArgs &a, int t) {
+    Org o;
+    o.d0 = (t % a.nbd) * BD;
+    t /= a.nbd;
+    o.w0 = (t % a.nbw) * BW;
+    t /= a.nbw;
+    o.h0 = (t % a.nbh) * BH;
+    o.b = t / a.nbh;
+    return o;
+}
+// per halo line: global voxel index of (line, d = d0) (H / W wrapped)
+__device__ __forceinline__ void line_table(const CArgs &a, const Org &o, int *lbase) {
+    const int t = threadIdx.x;
+    if (t < NLN) {
+        const int lh = t / WL, lw = t - lh * WL;
+        lbase[t] = ((o.b * a.H + wrapm(o.h0 - 1 + lh, a.H)) * a.W + wrapm(o.w0 - 1 + lw, a.W)) * a.D + o.d0;
+    }
+}
+// global voxel of halo item q (line, pos), pos 0 = position -1 (D wrapped)
+__device__ __forceinline__ int halo_voxel(const CArgs &a, const Org &o, const int *lbase, int q, int &line, int &pos) {
+    line = q / PL;
+    pos = q - line * PL;
+    const int d = o.d0 - 1 + pos;
+    return lbase[line] - o.d0 + (d < 0 ? d + a.D : (d >= a.D ? d - a.D : d));
+}
+__device__ __forceinline__ bool interior(int line, int pos) {
+    const int lh = line / WL, lw = line - lh * WL;
+    return lh >= 1 && lh <= BH && lw >= 1 && lw <= BW && pos >= 1 && pos <= BD;
+}
+
+// B fragment of k-step s of the row-windowed W2 (DGRAD: transposed, flipped taps)
+template <int BR, bool DGRAD>
+__device__ __forceinline__ bf16x8 w2_frag(const float *__restrict__ w2, int s, int lane) {
+    using K = K3<BR>;
+    const int n = lane & 15, kb = lane >> 4;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * kb + j, r = s * K::RPK + k / K::EPR, e = k % K::EPR, kd = e / BR, c = e - kd * BR;
+        float x = 0.f;
+        if (r < 9 && e < 3 * BR && n < BR) {
+            const int tap = r * 3 + kd;
+            x = DGRAD ? w2[(c * BR + n) * 27 + 26 - tap] : w2[(n * BR + c) * 27 + tap];
+        }
+        v[j] = x;
+    }
+    return pack8(v);
+}
+
+// A fragment: 8 K entries of tap-row window (s, kb) for interior voxel v (line li = v >> 5,
+// d = v & 31) from the position-major halo buffer [line][pos][BR]
+template <int BR>
+__device__ __forceinline__ bf16x8 win_frag(const bf16_t *h, int v, int s, int kb) {
+    using K = K3<BR>;
+    const int r = min(s * K::RPK + (8 * kb) / K::EPR, 8), e0 = (8 * kb) % K::EPR;
+    const int li = v >> 5, d = v & 31, kh = r / 3, kw = r - 3 * kh;
+    const int hl = ((li >> 3) + kh) * WL + (li & 7) + kw;
+    const int off = (hl * PL + d) * BR + e0;
+    if constexpr (BR == 1) return read8(h, off);
+    else return read8e(h + off);
+}
+
+// ============================================================================================ forward
+template <int C, int BR>
+__global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restrict__ x, const float *__restrict__ w1,
+                                                const float *__restrict__ w2, const float *__restrict__ w3,
+                                                vq3d_preact_params p, bf16_t *__restrict__ out,
+                                                bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
+    using K = K3<BR>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t *t2h = reinterpret_cast<bf16_t *>(smem);            // [HVX][BR] + PADE
+    float *accs = reinterpret_cast<float *>(t2h + HVX * BR + PADE);  // [NV][BR] raw W2 (*) t2
+    int *lbase = reinterpret_cast<int *>(accs + NV * BR);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
+    const Org o = brick_org(a, blockIdx.x);
+    const Scal s = load_scal(p);
+    bf16x8 fw[K::KS];
+#pragma unroll
+    for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, false>(w2, k, lane);
+    line_table(a, o, lbase);
+    for (int i = tid; i < PADE; i += NT) t2h[HVX * BR + i] = 0;
+    __syncthreads();
+    // A. t2 on the halo, every x load issued first
+    {
+        constexpr int P = (HVX + NT - 1) / NT;
+        typename Vec<C>::U xv[P];
+        int vox[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            int line, pos;
+            vox[u] = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
+            xv[u] = *reinterpret_cast<const typename Vec<C>::U *>(x + int64_t(vox[u]) * C);
+        }
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            const int q = tid + u * NT;
+            if (q < HVX) {
+                float xf[C], t[BR];
+                unpack<C>(xv[u], xf);
+#pragma unroll
+                for (int c = 0; c < C; ++c) xf[c] = elu_f(xf[c] + s.b1a) + s.b1b;
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc = fmaf(w1[oo * C + c], xf[c], acc);
+                    t[oo] = elu_f(acc + s.b2a) + s.b2b;
+                }
+                const typename Vec<BR>::U tp = packv<BR>(t);
+                *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = tp;
+                const int line = q / PL, pos = q - line * PL;
+                if (t2o && interior(line, pos)) *reinterpret_cast<typename Vec<BR>::U *>(t2o + int64_t(vox[u]) * BR) = tp;
+            }
+        }
+    }
+    __syncthreads();
+    // this thread's 8 voxels (phase C): brick line ln, D-group dg; x in flight during phase B
+    const int ln = tid >> 2, dg = tid & 3;
+    const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
+    constexpr int NXB = DV * C * 2 / 16;  // 16-byte pieces of the 8 voxels' x
+    uint4 xr[NXB];
+    ld16s<NXB>(x + vox0 * C, xr);
+    // B. raw W2 (*) t2 per m-tile
+    for (int mt = wave; mt < NMT; mt += NT / 64) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, 16 * mt + row, k, kb), fw[k], acc);
+        if (row < BR) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) accs[(16 * mt + 4 * kb + j) * BR + row] = acc[j];
+        }
+    }
+    __syncthreads();
+    // C. t3 and out of the thread's 8 voxels
+    const int v0 = ln * BD + dg * DV;
+    float t3v[DV][BR];
+#pragma unroll
+    for (int i = 0; i < DV; ++i)
+#pragma unroll
+        for (int oo = 0; oo < BR; ++oo) t3v[i][oo] = rbf(elu_f(accs[(v0 + i) * BR + oo] + s.b3a) + s.b3b);
+    {
+        constexpr int NTB = DV * BR * 2 / 16;  // B >= 1: 8 voxels x B bf16 = 16 B x B
+        static_assert(NTB >= 1, "t3 store");
+        uint32_t w[DV * BR / 2];
+#pragma unroll
+        for (int i = 0; i < DV * BR / 2; ++i) {
+            const int e0 = 2 * i, e1 = 2 * i + 1;
+            w[i] = uint32_t(f2bf(t3v[e0 / BR][e0 % BR])) | (uint32_t(f2bf(t3v[e1 / BR][e1 % BR])) << 16);
+        }
+        if (t3o) {  // NULL: eval forward, nothing saved
+#pragma unroll
+            for (int i = 0; i < NTB; ++i)
+                reinterpret_cast<uint4 *>(t3o + vox0 * BR)[i] = uint4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+        }
+    }
+    float xf[DV * C];
+#pragma unroll
+    for (int i = 0; i < NXB; ++i) {
+        const uint32_t ww[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            xf[8 * i + 2 * k] = __uint_as_float(ww[k] << 16);
+            xf[8 * i + 2 * k + 1] = __uint_as_float(ww[k] & 0xffff0000u);
+        }
+    }
+    uint4 orr[NXB];
+#pragma unroll
+    for (int i = 0; i < NXB; ++i) {
+        float ov[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = 8 * i + k, vv = e / C, c = e - vv * C;
+            float r = 0.f;
+#pragma unroll
+            for (int oo = 0; oo < BR; ++oo) r = fmaf(w3[c * BR + oo], t3v[vv][oo], r);
+            ov[k] = r * s.sc + s.b4 + xf[e];
+        }
+        orr[i] = __builtin_bit_cast(uint4, pack8(ov));
+    }
+#pragma unroll
+    for (int i = 0; i < NXB; ++i) reinterpret_cast<uint4 *>(out + vox0 * C)[i] = orr[i];
+}
+
+// ============================================================================================ backward
+template <int C, int BR>
+__global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restrict__ g, const bf16_t *__restrict__ x,
+                                                const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
+                                                const float *__restrict__ w1, const float *__restrict__ w2,
+                                                const float *__restrict__ w3, vq3d_preact_params p,
+                                                float *__restrict__ part, bf16_t *__restrict__ gx) {
+    using K = K3<BR>;
+    constexpr int NE = n_entries<C, BR>();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t *z3h = reinterpret_cast<bf16_t *>(smem);  // gz3 on the halo [HVX][BR] + PADE
+    bf16_t *t2T = z3h + HVX * BR + PADE;             // t2 on the halo, channel-major [BR][NLN][TP]
+    bf16_t *z3T = t2T + BR * NLN * TP;                // gz3 of the brick, channel-major [BR][ZP]
+    float *accs = reinterpret_cast<float *>(z3T + BR * ZP);  // [NV][BR] raw W2^T (*) gz3
+    int *lbase = reinterpret_cast<int *>(accs + NV * BR);
+    float *red = reinterpret_cast<float *>(lbase + NLN);  // [4 waves][NE]
+    float *wred = reinterpret_cast<float *>(smem);        // after phase C: [4][NTN][64][4] over z3h / t2T
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
+    const Org o = brick_org(a, blockIdx.x);
+    const Scal s = load_scal(p);
+    bf16x8 fw[K::KS];
+#pragma unroll
+    for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, true>(w2, k, lane);
+    line_table(a, o, lbase);
+    for (int i = tid; i < PADE; i += NT) z3h[HVX * BR + i] = 0;
+    for (int i = tid; i < BR * NLN * (TP - PL) / 2; i += NT) {  // zero the channel-major line tails
+        const int l = i / ((TP - PL) / 2), e = i - l * ((TP - PL) / 2);
+        reinterpret_cast<uint32_t *>(t2T + l * TP + PL)[e] = 0u;
+    }
+    __syncthreads();
+    // A. gz3 on the halo; t2 on the halo (channel-major); interior sums and G3 = sum t3 (x) g
+    float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f, g3[BR][C];
+#pragma unroll
+    for (int oo = 0; oo < BR; ++oo)
+#pragma unroll
+        for (int c = 0; c < C; ++c) g3[oo][c] = 0.f;
+    {
+        constexpr int P = (HVX + NT - 1) / NT;
+        typename Vec<C>::U gv[P];
+        typename Vec<BR>::U tv3[P], tv2[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            int line, pos;
+            const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
+            gv[u] = *reinterpret_cast<const typename Vec<C>::U *>(g + int64_t(vx) * C);
+            tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
+            tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
+        }
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            const int q = tid + u * NT;
+            if (q < HVX) {
+                const int line = q / PL, pos = q - line * PL;
+                const bool in = interior(line, pos);
+                float gf[C], t3f[BR], t2f[BR], z[BR];
+                unpack<C>(gv[u], gf);
+                unpack<BR>(tv3[u], t3f);
+                unpack<BR>(tv2[u], t2f);
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc = fmaf(w3[c * BR + oo], gf[c], acc);
+                    const float gt3 = s.sc * acc;
+                    z[oo] = gt3 * elu_d_act(t3f[oo], s.b3b);
+                    if (in) {
+                        s3b += gt3;
+                        s3a += z[oo];
+                        ssc = fmaf(acc, t3f[oo], ssc);
+#pragma unroll
+                        for (int c = 0; c < C; ++c) g3[oo][c] = fmaf(t3f[oo], gf[c], g3[oo][c]);
+                    }
+                    t2T[(oo * NLN + line) * TP + pos] = f2bf(t2f[oo]);
+                }
+                const typename Vec<BR>::U zp = packv<BR>(z);
+                *reinterpret_cast<typename Vec<BR>::U *>(z3h + q * BR) = zp;
+                if (in) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) s4 += gf[c];
+                    const int lh = line / WL, lw = line - lh * WL;
+                    const int v = ((lh - 1) * BW + lw - 1) * BD + pos - 1;
+#pragma unroll
+                    for (int oo = 0; oo < BR; ++oo) z3T[oo * ZP + v] = f2bf(z[oo]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // the thread's 8 voxels (phase C): g and x in flight during phase B
+    const int ln = tid >> 2, dg = tid & 3;
+    const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
+    constexpr int NXB = DV * C * 2 / 16;
+    uint4 xr[NXB], gr[NXB];
+    ld16s<NXB>(x + vox0 * C, xr);
+    ld16s<NXB>(g + vox0 * C, gr);
+    // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
+    for (int mt = wave; mt < NMT; mt += NT / 64) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, 16 * mt + row, k, kb), fw[k], acc);
+        if (row < BR) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) accs[(16 * mt + 4 * kb + j) * BR + row] = acc[j];
+        }
+    }
+    // B2. W2 gradient: D[co][col] += sum_v gz3[v][co] * t2win[v][col], col = r * 3B + kd * B + ci;
+    // wave w takes the brick lines 16 w .. 16 w + 15 (one 32-voxel k-step each)
+    f32x4 aw[K::NTN];
+    int toff[K::NTN];
+#pragma unroll
+    for (int n = 0; n < K::NTN; ++n) {
+        aw[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int col = min(16 * n + row, 27 * BR - 1), r = col / (3 * BR), e = col - r * 3 * BR, kd = e / BR,
+                  ci = e - kd * BR, kh = r / 3, kw = r - 3 * kh;
+        toff[n] = (ci * NLN + kh * WL + kw) * TP + kd + 8 * kb;  // + line offset of the k-step
+    }
+    for (int ks = 16 * wave; ks < 16 * wave + 16; ++ks) {
+        // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
+        const bf16x8 af = *reinterpret_cast<const bf16x8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
+        const int lo = ((ks >> 3) * WL + (ks & 7)) * TP;
+#pragma unroll
+        for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
+    }
+    __syncthreads();
+    // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 8 voxels
+    const int v0 = ln * BD + dg * DV;
+    float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f, dw1[BR][C];
+#pragma unroll
+    for (int oo = 0; oo < BR; ++oo)
+#pragma unroll
+        for (int c = 0; c < C; ++c) dw1[oo][c] = 0.f;
+    float xf[DV * C], gf[DV * C], gxo[DV * C];
+#pragma unroll
+    for (int i = 0; i < NXB; ++i) {
+        const uint32_t wx[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w}, wg[4] = {gr[i].x, gr[i].y, gr[i].z, gr[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            xf[8 * i + 2 * k] = __uint_as_float(wx[k] << 16);
+            xf[8 * i + 2 * k + 1] = __uint_as_float(wx[k] & 0xffff0000u);
+            gf[8 * i + 2 * k] = __uint_as_float(wg[k] << 16);
+            gf[8 * i + 2 * k + 1] = __uint_as_float(wg[k] & 0xffff0000u);
+        }
+    }
+    const int hl0 = ((ln >> 3) + 1) * WL + (ln & 7) + 1;
+#pragma unroll
+    for (int i = 0; i < DV; ++i) {
+        float z1[BR];
+#pragma unroll
+        for (int oo = 0; oo < BR; ++oo) {
+            const float gt2 = accs[(v0 + i) * BR + oo];
+            const float t2v = bf(t2T[(oo * NLN + hl0) * TP + dg * DV + i + 1]);
+            const float zz = gt2 * elu_d_act(t2v, s.b2b);
+            s2b += gt2;
+            s2a += zz;
+            z1[oo] = rbf(zz);
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            float gt1 = 0.f;
+#pragma unroll
+            for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
+            const float zx = xf[i * C + c] + s.b1a;
+            const float e1 = zx > 0.f ? 1.f : __expf(zx);
+            const float u1 = rbf((zx > 0.f ? zx : e1 - 1.f) + s.b1b);
+            s1b += gt1;
+            s1a = fmaf(gt1, e1, s1a);
+            gxo[i * C + c] = gf[i * C + c] + gt1 * e1;
+#pragma unroll
+            for (int oo = 0; oo < BR; ++oo) dw1[oo][c] = fmaf(z1[oo], u1, dw1[oo][c]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NXB; ++i) {
+        float ov[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ov[k] = gxo[8 * i + k];
+        reinterpret_cast<uint4 *>(gx + vox0 * C)[i] = __builtin_bit_cast(uint4, pack8(ov));
+    }
+    // partial row of this brick: per-wave shuffle sums, then the 4 waves in order
+    float vals[NE];
+    {
+        int e = 0;
+#pragma unroll
+        for (int oo = 0; oo < BR; ++oo)
+#pragma unroll
+            for (int c = 0; c < C; ++c) vals[e++] = g3[oo][c];
+        e += 27 * BR * BR;  // W2: from the MFMA accumulators below
+#pragma unroll
+        for (int oo = 0; oo < BR; ++oo)
+#pragma unroll
+            for (int c = 0; c < C; ++c) vals[e++] = dw1[oo][c];
+        const float sc8[NSC] = {s4, s3b, s3a, ssc, s2b, s2a, s1b, s1a};
+#pragma unroll
+        for (int k = 0; k < NSC; ++k) vals[e++] = sc8[k];
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        if (e >= BR * C && e < BR * C + 27 * BR * BR) continue;
+        const float t = wave_sum(vals[e]);
+        if (lane == 0) red[wave * NE + e] = t;
+    }
+    __syncthreads();  // every wave is past phase C (t2T) before the W2 sums go over it
+    // W2 accumulators: D rows 4 kb + j = co, columns 16 n + row = col
+#pragma unroll
+    for (int n = 0; n < K::NTN; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wred[((wave * K::NTN + n) * 64 + lane) * 4 + j] = aw[n][j];
+    __syncthreads();
+    for (int e = tid; e < NE; e += NT) {
+        float t = 0.f;
+        if (e >= BR * C && e < BR * C + 27 * BR * BR) {
+            const int r2 = e - BR * C, co = r2 / (27 * BR), col = r2 - co * 27 * BR;
+            const int n = col >> 4, l = 16 * (co >> 2) + (col & 15), j = co & 3;
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) t += wred[((w * K::NTN + n) * 64 + l) * 4 + j];
+        } else {
+#pragma unroll
+            for (int w = 0; w < NT / 64; ++w) t += red[w * NE + e];
+        }
+        part[int64_t(e) * gridDim.x + blockIdx.x] = t;
+    }
+}
+
+// every entry summed over the bricks in a fixed order, added into its gradient buffer
+template <int C, int BR>
+__global__ __launch_bounds__(256) void k_col_reduce(const float *__restrict__ part, int nb, const float *__restrict__ scale,
+                                                    vq3d_preact_grads gr) {
+    constexpr int E1 = BR * C, E2 = 27 * BR * BR, E3 = BR * C;
+    __shared__ float sm[4];
+    const int e = blockIdx.x;
+    const float *pp = part + int64_t(e) * nb;
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < nb; i += 256) acc += pp[i];
+    const float t = block_sum<float, 256>(acc, sm);
+    if (threadIdx.x != 0) return;
+    if (e < E1) {  // G3 [o][c] -> dW3 [c][o] * scale
+        const int oo = e / C, c = e - oo * C;
+        gr.dw3[c * BR + oo] += *scale * t;
+    } else if (e < E1 + E2) {  // [co][r][kd][ci] -> dW2 [co][ci][r * 3 + kd]
+        const int r2 = e - E1, co = r2 / (27 * BR), col = r2 - co * 27 * BR, r = col / (3 * BR),
+                  el = col - r * 3 * BR, kd = el / BR, ci = el - kd * BR;
+        gr.dw2[(co * BR + ci) * 27 + r * 3 + kd] += t;
+    } else if (e < E1 + E2 + E3) {
+        gr.dw1[e - E1 - E2] += t;  // [o][c]
+    } else {
+        float *const sl[NSC] = {gr.dbias4, gr.dbias3b, gr.dbias3a, gr.dscale, gr.dbias2b, gr.dbias2a, gr.dbias1b, gr.dbias1a};
+        *sl[e - E1 - E2 - E3] += t;
+    }
+}
+
+template <int C, int BR>
+constexpr size_t fwd_lds() {
+    return size_t(HVX * BR + PADE) * 2 + size_t(NV * BR) * 4 + NLN * 4;
+}
+template <int C, int BR>
+constexpr size_t bwd_lds() {
+    return size_t(HVX * BR + PADE + BR * NLN * TP + BR * ZP) * 2 + size_t(NV * BR) * 4 + NLN * 4 +
+           size_t(4 * n_entries<C, BR>()) * 4;
+}
+
+CArgs make_args(int B, int H, int W, int D) {
+    CArgs a;
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    a.D = D;
+    a.nbh = H / BH;
+    a.nbw = W / BW;
+    a.nbd = D / BD;
+    a.nbricks = B * a.nbh * a.nbw * a.nbd;
+    return a;
+}
+
+template <class Kern>
+void allow(Kern k, size_t lds) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    (void)hipGetLastError();
+}
+
+template <int C, int BR>
+void launch_fwd(const CArgs &a, const bf16_t *x, const float *w1, const float *w2, const float *w3,
+                const vq3d_preact_params &p, bf16_t *out, bf16_t *t2, bf16_t *t3, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        allow(k_col_fwd<C, BR>, fwd_lds<C, BR>());
+        attr = true;
+    }
+    k_col_fwd<C, BR><<<a.nbricks, NT, fwd_lds<C, BR>(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
+}
+template <int C, int BR>
+void launch_bwd(const CArgs &a, const bf16_t *g, const bf16_t *x, const bf16_t *t2, const bf16_t *t3, const float *w1,
+                const float *w2, const float *w3, const vq3d_preact_params &p, const vq3d_preact_grads &gr, float *part,
+                bf16_t *gx, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        allow(k_col_bwd<C, BR>, bwd_lds<C, BR>());
+        attr = true;
+    }
+    k_col_bwd<C, BR><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, g, x, t2, t3, w1, w2, w3, p, part, gx);
+    k_col_reduce<C, BR><<<n_entries<C, BR>(), 256, 0, s>>>(part, a.nbricks, p.scale, gr);
+}
+
+}  // namespace
+
+bool col_supported(int batch, int C, int BR, int h, int w, int d) {
+    const bool shape = (C == 2 && BR == 1) || (C == 4 && BR == 2) || (C == 8 && BR == 4);
+    return shape && batch >= 1 && h >= BH && w >= BW && d >= BD && h % BH == 0 && w % BW == 0 && d % BD == 0 &&
+           int64_t(batch) * h * w * d * C < (int64_t(1) << 31);
+}
+
+size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d) {
+    if (!col_supported(batch, C, BR, h, w, d)) return 0;
+    const CArgs a = make_args(batch, h, w, d);
+    const int ne = C == 2 ? n_entries<2, 1>() : C == 4 ? n_entries<4, 2>() : n_entries<8, 4>();
+    return size_t(a.nbricks) * ne * 4;
+}
+
+int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1, const float *w2,
+            const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3, hipStream_t s) {
+    const CArgs a = make_args(batch, h, w, d);
+    auto X = static_cast<const bf16_t *>(x);
+    auto O = static_cast<bf16_t *>(out), T2 = static_cast<bf16_t *>(t2), T3 = static_cast<bf16_t *>(t3);
+    if (C == 2) launch_fwd<2, 1>(a, X, w1, w2, w3, p, O, T2, T3, s);
+    else if (C == 4) launch_fwd<4, 2>(a, X, w1, w2, w3, p, O, T2, T3, s);
+    else launch_fwd<8, 4>(a, X, w1, w2, w3, p, O, T2, T3, s);
+    return check_launch("preact_small_fwd (column kernels)");
+}
+
+int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
+            const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
+            const vq3d_preact_grads &gr, void *workspace, void *gx, hipStream_t s) {
+    const CArgs a = make_args(batch, h, w, d);
+    auto G = static_cast<const bf16_t *>(g), X = static_cast<const bf16_t *>(x);
+    auto T2 = static_cast<const bf16_t *>(t2), T3 = static_cast<const bf16_t *>(t3);
+    auto GX = static_cast<bf16_t *>(gx);
+    float *part = static_cast<float *>(workspace);
+    if (C == 2) launch_bwd<2, 1>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, s);
+    else if (C == 4) launch_bwd<4, 2>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, s);
+    else launch_bwd<8, 4>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, s);
+    return check_launch("preact_small_bwd (column kernels)");
+}
+
+}  // namespace vq3d

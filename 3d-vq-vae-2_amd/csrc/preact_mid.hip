@@ -418,7 +418,7 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
         }
         __syncthreads();
         if constexpr (!(PM_EXP & 4)) {
-            store_tile<TH, TW, BR>(a, o, t3s, t3o);
+            if (t3o) store_tile<TH, TW, BR>(a, o, t3s, t3o);
             store_tile<TH, TW, C>(a, o, xs, out);
         }
     }
@@ -870,7 +870,7 @@ int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
                                vq3d_stream_t stream) {
     if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
         return fail("preact_mid_fwd: shape outside the fused mid-level block kernels");
-    if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_mid_fwd: null pointer");
+    if (!x || !w1 || !w2 || !w3 || !p || !out || !t2) return fail("preact_mid_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     const int64_t nvox = int64_t(batch) * h * w * dd;
     const unsigned g1 = unsigned(std::max<int64_t>(1, std::min<int64_t>(nvox / 2 / NT, 2048)));

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restr
                     t[o] = rbf(elu(acc + s.b2a) + s.b2b);
                     t2h[q * BR + o] = t[o];
                 }
-                if (vi[u] >= 0) stv<BR>(t2o + vox[u] * BR, t);
+                if (vi[u] >= 0 && t2o) stv<BR>(t2o + vox[u] * BR, t);
             }
         }
         __syncthreads();
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restr
             float t3v[BR];
 #pragma unroll
             for (int o = 0; o < BR; ++o) t3v[o] = rbf(elu(acc[o] + s.b3a) + s.b3b);
-            stv<BR>(t3o + vox * BR, t3v);
+            if (t3o) stv<BR>(t3o + vox * BR, t3v);
 #pragma unroll
             for (int co = 0; co < C; ++co) {
                 float r = 0.f;
@@ -548,11 +548,21 @@ extern "C" {
 int vq3d_preact_small_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                                 int32_t dd) {
     SArgs a;
-    return dtype == VQ3D_BF16 && plan(batch, channels, branch, h, w, dd, a) ? 1 : 0;
+    return dtype == VQ3D_BF16 && (col_supported(batch, channels, branch, h, w, dd) ||
+                                  plan(batch, channels, branch, h, w, dd, a))
+               ? 1
+               : 0;
+}
+
+int vq3d_preact_small_plan(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd) {
+    SArgs a;
+    if (col_supported(batch, channels, branch, h, w, dd)) return 2;
+    return plan(batch, channels, branch, h, w, dd, a) ? 1 : 0;
 }
 
 size_t vq3d_preact_small_workspace_bytes(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                                          int32_t dd) {
+    if (col_supported(batch, channels, branch, h, w, dd)) return col_workspace_bytes(batch, channels, branch, h, w, dd);
     SArgs a;
     if (!plan(batch, channels, branch, h, w, dd, a)) return 0;
     return size_t(a.nbricks) * (n_entries(channels, branch) + kNScal) * 4;
@@ -562,9 +572,11 @@ int vq3d_preact_small_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_
                           int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                           const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
     SArgs a;
+    if (!x || !w1 || !w2 || !w3 || !p || !out) return fail("preact_small_fwd: null pointer");
+    if (dtype == VQ3D_BF16 && col_supported(batch, channels, branch, h, w, dd))
+        return col_fwd(batch, channels, branch, h, w, dd, x, w1, w2, w3, *p, out, t2, t3, as_stream(stream));
     if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
         return fail("preact_small_fwd: shape outside the fused few-channel block kernels");
-    if (!x || !w1 || !w2 || !w3 || !p || !out || !t2 || !t3) return fail("preact_small_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     const size_t lds = lds_fwd(a, branch);
 #define F(C_, B_)                                                                                              \
@@ -587,10 +599,20 @@ int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_
                           const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                           void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream) {
     SArgs a;
-    if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
-        return fail("preact_small_bwd: shape outside the fused few-channel block kernels");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx)
         return fail("preact_small_bwd: null pointer");
+    if (dtype == VQ3D_BF16 && col_supported(batch, channels, branch, h, w, dd)) {
+        const vq3d_preact_grads &G = *gr;
+        if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||
+            !G.dbias3b || !G.dscale || !G.dbias4)
+            return fail("preact_small_bwd: every gradient buffer is required");
+        if (!workspace || ws_bytes < col_workspace_bytes(batch, channels, branch, h, w, dd))
+            return fail("preact_small_bwd: workspace too small");
+        return col_bwd(batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, *p, G, workspace, gx,
+                       as_stream(stream));
+    }
+    if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
+        return fail("preact_small_bwd: shape outside the fused few-channel block kernels");
     const int ne = n_entries(channels, branch) + kNScal;
     if (!workspace || ws_bytes < size_t(a.nbricks) * ne * 4) return fail("preact_small_bwd: workspace too small");
     hipStream_t s = as_stream(stream);

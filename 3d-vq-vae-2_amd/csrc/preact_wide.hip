@@ -329,7 +329,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         }
     }
     __syncthreads();
-    if constexpr (!(WIDE_EXP & 8)) tile_to_global<true>(runv, t2h, t2o);
+    if (!(WIDE_EXP & 8) && t2o) tile_to_global<true>(runv, t2h, t2o);
     // x of this lane's output entries, in flight during the 3x3x3 phase: m-tiles 2 hf + mm,
     // channel tiles nt + 3 q; voxel 16 m + 4 kb + j = run 2 m + (kb >> 1), d = 4 (kb & 1) + j
     int vb[2];
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
                 t3s[(16 * (2 * hf + mm) + 4 * kb + j) * BR + ob] = f2bf(elu_f(acc3[mm][j] + s.b3a) + s.b3b);
     }
     __syncthreads();
-    if constexpr (!(WIDE_EXP & 8)) tile_to_global<false>(runv, t3s, t3o);
+    if (!(WIDE_EXP & 8) && t3o) tile_to_global<false>(runv, t3s, t3o);
     // out = x + scale * W3 t3 + b4
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -898,7 +898,7 @@ int vq3d_preact_wide_fwd(int32_t batch, int32_t channels, int32_t branch, int32_
                          vq3d_stream_t stream) {
     if (!vq3d_preact_wide_supported(batch, channels, branch, h, w, dd))
         return fail("preact_wide_fwd: shape outside the fused wide-block kernels");
-    if (!x || !image || !p || !out || !t2 || !t3) return fail("preact_wide_fwd: null pointer");
+    if (!x || !image || !p || !out) return fail("preact_wide_fwd: null pointer");
     if (static_cast<const void *>(x) == static_cast<const void *>(out)) return fail("preact_wide_fwd: out aliases x");
     set_lds_limits();
     const WArgs a = make_args(batch, h, w, dd);

@@ -78,6 +78,7 @@ _SIGS = {
     "vq3d_preact_wide_bwd_weight": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P]),
     "vq3d_preact_small_supported": (c_int, [c_int] * 7),
     "vq3d_preact_small_workspace_bytes": (c_size, [c_int] * 6),
+    "vq3d_preact_small_plan": (c_int, [c_int] * 6),
     "vq3d_preact_small_fwd": (c_int, [c_int] * 7 + [P] * 9),
     "vq3d_preact_small_bwd": (c_int, [c_int] * 7 + [P] * 10 + [c_size, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),

@@ -68,11 +68,14 @@ class PreActBlockFn(torch.autograd.Function):
             ctx.save_for_backward(x, saved)
             return out
         ctx.small = False
+        # no backward follows (eval / no_grad: the encode-only extraction path): the fused
+        # kernels skip writing the saved intermediates
+        save = any(ctx.needs_input_grad)
         if (blk.skip_conv is None and not up and k == 3 and s == 1
                 and ops.preact_small_supported(x, blk.branch_conv1.weight.shape[0])):
-            # few-channel blocks: fused forward (preact_small.hip); t2 / t3 saved in bf16 as the
-            # unfused convs write them, so either backward applies
-            out, t2, t3 = ops.preact_small_fwd(x, blk)
+            # few-channel blocks: fused forward (preact_small.hip / preact_col.hip); t2 / t3 saved
+            # in bf16 as the unfused convs write them, so either backward applies
+            out, t2, t3 = ops.preact_small_fwd(x, blk, save=save)
             ctx.blk = blk
             ctx.small = ops.small_backward_fused(x)
             ctx.save_for_backward(x, t2, t3, None)
@@ -81,7 +84,7 @@ class PreActBlockFn(torch.autograd.Function):
                 and ops.preact_mid_supported(x, blk.branch_conv1.weight.shape[0])):
             # 18-channel level: fused forward (2 launches) and backward (3 launches),
             # preact_mid.hip
-            out, t2, t3 = ops.preact_mid_fwd(x, blk)
+            out, t2, t3 = ops.preact_mid_fwd(x, blk, save=save)
             ctx.blk = blk
             ctx.mid = True
             ctx.save_for_backward(x, t2, t3, None)
@@ -242,10 +245,12 @@ class PreActWideFn(torch.autograd.Function):
         img, per = ops.preact_wide_pack(ptab, len(plan.blocks), c, nb, x.device)
         base = img.data_ptr()
         xs = ops.cast(x, torch.float32)
+        save = any(ctx.needs_input_grad)
         saved = []
         for i, blk in enumerate(plan.blocks):
-            out, t2, t3 = ops.preact_wide_fwd(xs, base + i * per, blk)
-            saved += [xs, t2, t3]
+            out, t2, t3 = ops.preact_wide_fwd(xs, base + i * per, blk, save=save)
+            if save:
+                saved += [xs, t2, t3]
             xs = out
         ctx.plan, ctx.per, ctx.in_dtype = plan, per, x.dtype
         ctx.save_for_backward(img, *saved)

@@ -294,9 +294,10 @@ def preact_mid_supported(x, branch):
     return _mid[0] and bool(L.query("vq3d_preact_mid_supported", L.dtype_code(x), b, c, branch, h, w, d))
 
 
-def preact_mid_fwd(x, blk, stages=None, bufs=None):
-    """Fused PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last).
-    stages / bufs: measurement only (vq3d_preact_mid_fwd_stages, preallocated outputs)."""
+def preact_mid_fwd(x, blk, stages=None, bufs=None, save=True):
+    """Fused PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last); save=False
+    (no backward follows): t3 is not written (None).  stages / bufs: measurement only
+    (vq3d_preact_mid_fwd_stages, preallocated outputs)."""
     x = as_cl(x)
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
@@ -304,12 +305,12 @@ def preact_mid_fwd(x, blk, stages=None, bufs=None):
     if bufs is None:
         out = torch.empty_like(x, memory_format=CL)
         t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
-        t3 = new_act(b, nb, h, w, d, x.dtype, x.device)
+        t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
     else:
         out, t2, t3 = bufs
     prm = _preact_params(blk)
     args = (L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm),
-            L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+            L.ptr(out), L.ptr(t2), _p(t3), L.stream())
     if stages is None:
         L.call("vq3d_preact_mid_fwd", *args)
     else:
@@ -352,15 +353,19 @@ def set_small_blocks(enabled, fused_backward=True):
     _small[1] = bool(fused_backward)
 
 
-# fused backward up to this many voxels (measured, bench 3L pub: 23.6 vs ~100 us per (8, 4) block
-# at 32x32x8, 51 vs ~80 us per (2, 1) block at 128x128x32); beyond it the per-brick weight-gradient
-# partials are LDS-bound (6.2 ms per (4, 2) block at 512x512x128) and the per-conv backward wins
+# the brick kernels' fused backward up to this many voxels (measured, bench 3L pub: 23.6 vs ~100
+# us per (8, 4) block at 32x32x8); beyond it their per-brick weight-gradient partials are
+# LDS-bound and, where the column kernels (preact_col.hip, D % 32 == 0) do not apply, the
+# per-conv backward wins
 _SMALL_BWD_MAX_VOX = 1 << 19
 
 
 def small_backward_fused(x):
-    b, _, h, w, d = x.shape
-    return _small[1] and b * h * w * d <= _SMALL_BWD_MAX_VOX
+    b, c, h, w, d = x.shape
+    if not _small[1]:
+        return False
+    nb = c // 2
+    return int(L.query("vq3d_preact_small_plan", b, c, nb, h, w, d)) == 2 or b * h * w * d <= _SMALL_BWD_MAX_VOX
 
 
 def preact_small_supported(x, branch):
@@ -368,18 +373,19 @@ def preact_small_supported(x, branch):
     return _small[0] and bool(L.query("vq3d_preact_small_supported", L.dtype_code(x), b, c, branch, h, w, d))
 
 
-def preact_small_fwd(x, blk):
-    """Fused few-channel PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last)."""
+def preact_small_fwd(x, blk, save=True):
+    """Fused few-channel PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last);
+    save=False (no backward follows): t2 / t3 are not written (None)."""
     x = as_cl(x)
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     nb = w1.shape[0]
     out = torch.empty_like(x, memory_format=CL)
-    t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
-    t3 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    t2 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
+    t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
     prm = _preact_params(blk)
     L.call("vq3d_preact_small_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2),
-           L.ptr(w3), ctypes.byref(prm), L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+           L.ptr(w3), ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream())
     return out, t2, t3
 
 
@@ -422,16 +428,17 @@ def preact_wide_pack(ptab, nblocks, c, nb, device):
     return img, per
 
 
-def preact_wide_fwd(x32, img_ptr, blk):
-    """One block on the fp32 residual stream: returns out (fp32), t2, t3 (bf16), channels-last."""
+def preact_wide_fwd(x32, img_ptr, blk, save=True):
+    """One block on the fp32 residual stream: returns out (fp32), t2, t3 (bf16), channels-last;
+    save=False (no backward follows): t2 / t3 are not written (None)."""
     b, c, h, w, d = x32.shape
     nb = blk.branch_conv1.weight.shape[0]
     out = torch.empty_like(x32, memory_format=CL)
-    t2 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device)
-    t3 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device)
+    t2 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device) if save else None
+    t3 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device) if save else None
     prm = _preact_params(blk)
     L.call("vq3d_preact_wide_fwd", b, c, nb, h, w, d, L.ptr(x32), ctypes.c_void_p(img_ptr), ctypes.byref(prm),
-           L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
+           L.ptr(out), _p(t2), _p(t3), L.stream())
     return out, t2, t3
 
 

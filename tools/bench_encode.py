@@ -70,7 +70,7 @@ def main():
     from vq3d.utils import synthetic_volume
 
     rank, world, local, dev = parallel.init_from_env()
-    mkw, size, _ = bench.CONFIGS[a.config]
+    mkw, size, _ = bench.CONFIGS[a.config][:3]
     torch.manual_seed(0)
     model = vq3d.VQVAE(vq3d.default_args(compute_dtype=a.dtype, **mkw)).to(dev)
     for q in (m for m in model.modules() if isinstance(m, vq3d.Quantizer)):

@@ -38,7 +38,7 @@ def main():
     p.add_argument("--top", type=int, default=60)
     a = p.parse_args()
     import vq3d
-    mkw, size, batch = bench.CONFIGS[a.config]
+    mkw, size, batch = bench.CONFIGS[a.config][:3]
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     model = vq3d.VQVAE(vq3d.default_args(compute_dtype="bf16", **mkw)).to(dev)

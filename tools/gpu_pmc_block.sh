@@ -12,5 +12,5 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_
 done
 rm -rf gpurun_out/tr_$tag
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/tr_$tag -o run --output-format csv -- python3 tools/block_micro.py "$@" > gpurun_out/tr_$tag.log 2>&1 || exit 1
-python3 tools/pmc_kernels.py "gpurun_out/pmc_${tag}_*" k_pm
-grep -h "k_pm\|k_small" gpurun_out/tr_$tag/*kernel_stats.csv | cut -d, -f1-8
+python3 tools/pmc_kernels.py "gpurun_out/pmc_${tag}_*" ${FILT:-k_}
+cut -d, -f1-8 gpurun_out/tr_$tag/*kernel_stats.csv | head -30
