@@ -1,15 +1,16 @@
 // Few-channel PreActFixupResBlocks (vqvae/layers.py:176-195, mode 'same', no skip conv) on the
 // big grids: (block channels C, branch B) = (4, 2) at 512x512x128 (decoder post-upscale blocks),
 // (2, 1) at 128x128x32 (50 encoder pre-quantize blocks), (8, 4) at 256x256x64; any grid with
-// H % 8 == W % 8 == 0 and D % 32 == 0.  Forward in ONE launch, backward in TWO (fused kernel +
-// fixed-order reduction), for the vq3d_preact_small_* entry points (preact_small.hip keeps its
+// H % 8 == W % 8 == 0 and D % 16 == 0.  Forward in ONE launch, backward in THREE (fused kernel +
+// two-stage fixed-order reduction), for the vq3d_preact_small_* entry points (preact_small.hip keeps its
 // brick kernels for the small grids).
 //
 //   u1  = elu(x + b1a) + b1b      t2 = elu(W1 u1 + b2a) + b2b        (1x1, C -> B)
 //   t3  = elu(W2 (*) t2 + b3a) + b3b                                   (3x3x3 circular, B -> B)
 //   out = scale * (W3 t3) + b4 + x                                     (1x1, B -> C)
 //
-// A workgroup owns an 8 x 8 x 32 brick (2048 voxels, 256 threads).  The 1x1 convs and the
+// A workgroup owns an 8 x 8 x 16 brick (1024 voxels, 256 threads, 4 voxels each along D: small
+// enough LDS for 4-5 workgroups per CU).  The 1x1 convs and the
 // activations run on the VALU, one voxel per work item, weights wave-uniform; the 3x3x3 conv and
 // its backward run on the matrix cores (v_mfma_f32_16x16x32_bf16) with a "row-windowed" K: for a
 // voxel and a tap row (kh, kw) the 3 kd taps x B channels are 3B consecutive bf16 of the halo line
@@ -17,23 +18,29 @@
 // weights are zero, so one k-step covers 4 (or 2) tap rows of 16 voxels.  Only B of the 16 MFMA
 // columns are real: the k^3 conv is still ~2x cheaper on the matrix cores than on the VALU.
 //
-//   forward  A: t2 on the brick's circular halo (10 x 10 lines x 34 positions) into LDS, the
-//               interior also to HBM (saved for the backward)
+//   forward  A: t2 on the brick's circular halo (10 x 10 lines x 18 positions) into LDS
 //            B: raw W2 (*) t2 per 16-voxel m-tile (matrix cores) into LDS
-//            C: per thread 8 consecutive voxels: t3, out (16-byte stores)
+//            C: per thread 4 consecutive voxels: t2 / t3 (saved for the backward), out
 //   backward A: gz3 = bf16(scale W3^T g * elu'(t3)) on the halo; the interior's scalar sums and
 //               the W3 gradient (sum t3 (x) g) in registers; t2 on the halo channel-major
 //            B: gt2 = W2^T (*) gz3 (flipped taps) per m-tile, and the W2 gradient
 //               sum_v gz3[v][co] t2[v + tap][ci] with voxels as the MFMA reduction axis
-//            C: per thread 8 voxels: gz1 = bf16(gt2 * elu'(t2)), gx = g + (W1^T gz1) * elu'(x + b1a),
+//            C: per thread 4 voxels: gz1 = bf16(gt2 * elu'(t2)), gx = g + (W1^T gz1) * elu'(x + b1a),
 //               the W1 gradient (sum gz1 (x) u1) and the b2 / b1 sums
-//            per-brick partial rows [entry][brick], summed in a fixed order by k_col_reduce.
+//            per-brick partial rows [brick][entry], summed in a fixed order by k_col_reduce1 / 2.
 // Rounding points are the unfused path's: t2, t3, gz3, gz1, gx, out rounded to bf16, fp32
 // accumulation; the W1 gradient reads u1 rounded to bf16 (the unfused wgrad's operand).
 #include "engines.h"
 
 #include <algorithm>
 #include <type_traits>
+
+// Timing experiments only (make exp EXP=N EXPSRC=preact_col EXPDEF=COL_EXP): bit 0 skips the halo
+// loads, 1 the halo math, 2 the k^3 MFMA phase, 3 the W2-gradient MFMAs, 4 the per-voxel epilogue.
+// The product library is built with COL_EXP = 0.
+#ifndef COL_EXP
+#define COL_EXP 0
+#endif
 
 namespace vq3d {
 
@@ -42,14 +49,19 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BH = 8, BW = 8, BD = 32, DV = 8;  // brick; voxels per thread along D
+constexpr int BH = 8, BW = 8, BD = 16, DV = 4;  // brick; voxels per thread along D
 constexpr int HL = BH + 2, WL = BW + 2, PL = BD + 2, NLN = HL * WL, HVX = NLN * PL;
-constexpr int NV = BH * BW * BD, NMT = NV / 16;  // 2048 voxels, 128 m-tiles
+constexpr int NV = BH * BW * BD, NMT = NV / 16;  // 1024 voxels, 64 m-tiles (one per brick line)
 constexpr int NT = 256;
-constexpr int TP = 40;        // channel-major halo line pitch (positions 0..33, zero pad)
+static_assert(BD == 16 && NT / (BD / DV) == BH * BW, "m-tile = brick line; thread = (line, D-group)");
+constexpr int TP = 24;        // channel-major halo line pitch (positions 0..17, zero pad)
 constexpr int ZP = NV + 16;   // channel-major interior pitch
 constexpr int PADE = 32;      // zero tail of the position-major halo buffers
 constexpr int NSC = 8;        // scalar partials: b4, b3b, b3a, scale, b2b, b2a, b1b, b1a
+// raw k^3 sums [voxel][B] fp32 with one pad float per brick line (16 voxels), so the per-thread
+// epilogue reads of 16 lines do not share a bank
+__host__ __device__ constexpr int acc_at(int v, int BR_) { return v * BR_ + v / BD; }
+constexpr int acc_floats(int BR_) { return NV * BR_ + NV / BD; }
 
 template <int BR>
 struct K3 {
@@ -98,6 +110,19 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
     return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+}
+
+// NW dwords (2, 4 or 8) to global memory as 8- / 16-byte stores
+template <int NW>
+__device__ __forceinline__ void store_words(bf16_t *__restrict__ p, const uint32_t (&w)[NW]) {
+    if constexpr (NW == 2) {
+        *reinterpret_cast<uint2 *>(p) = uint2{w[0], w[1]};
+    } else {
+        static_assert(NW % 4 == 0, "store width");
+#pragma unroll
+        for (int i = 0; i < NW / 4; ++i)
+            reinterpret_cast<uint4 *>(p)[i] = uint4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+    }
 }
 
 // N bf16 <-> fp32 (N = 1, 2, 4, 8: one 2/4/8/16-byte access)
@@ -206,15 +231,23 @@ __device__ __forceinline__ bf16x8 w2_frag(const float *__restrict__ w2, int s, i
     return pack8(v);
 }
 
-// A fragment: 8 K entries of tap-row window (s, kb) for interior voxel v (line li = v >> 5,
-// d = v & 31) from the position-major halo buffer [line][pos][BR]
+// A fragments of the row-windowed k^3 operand from the position-major halo buffer [line][pos][BR]:
+// the lane's part of the element offset, per k-step (m-tile independent), and the m-tile's
+// wave-uniform base.  Interior voxel v = 16 mt + row: brick line mt, d = row.
 template <int BR>
-__device__ __forceinline__ bf16x8 win_frag(const bf16_t *h, int v, int s, int kb) {
+__device__ __forceinline__ void win_offsets(int row, int kb, int (&off)[K3<BR>::KS]) {
     using K = K3<BR>;
-    const int r = min(s * K::RPK + (8 * kb) / K::EPR, 8), e0 = (8 * kb) % K::EPR;
-    const int li = v >> 5, d = v & 31, kh = r / 3, kw = r - 3 * kh;
-    const int hl = ((li >> 3) + kh) * WL + (li & 7) + kw;
-    const int off = (hl * PL + d) * BR + e0;
+#pragma unroll
+    for (int s = 0; s < K::KS; ++s) {
+        const int r = min(s * K::RPK + (8 * kb) / K::EPR, 8), e0 = (8 * kb) % K::EPR, kh = r / 3, kw = r - 3 * kh;
+        off[s] = ((kh * WL + kw) * PL + row) * BR + e0;
+    }
+}
+__device__ __forceinline__ int win_base(int mt, int BR) {  // m-tile mt = brick line mt
+    return ((mt >> 3) * WL + (mt & 7)) * PL * BR;
+}
+template <int BR>
+__device__ __forceinline__ bf16x8 win_frag(const bf16_t *h, int off) {
     if constexpr (BR == 1) return read8(h, off);
     else return read8e(h + off);
 }
@@ -229,7 +262,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t *t2h = reinterpret_cast<bf16_t *>(smem);            // [HVX][BR] + PADE
     float *accs = reinterpret_cast<float *>(t2h + HVX * BR + PADE);  // [NV][BR] raw W2 (*) t2
-    int *lbase = reinterpret_cast<int *>(accs + NV * BR);
+    int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
     const Org o = brick_org(a, blockIdx.x);
     const Scal s = load_scal(p);
@@ -243,17 +276,16 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
     {
         constexpr int P = (HVX + NT - 1) / NT;
         typename Vec<C>::U xv[P];
-        int vox[P];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             int line, pos;
-            vox[u] = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
-            xv[u] = *reinterpret_cast<const typename Vec<C>::U *>(x + int64_t(vox[u]) * C);
+            const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
+            xv[u] = (COL_EXP & 1) ? typename Vec<C>::U{} : *reinterpret_cast<const typename Vec<C>::U *>(x + int64_t(vx) * C);
         }
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             const int q = tid + u * NT;
-            if (q < HVX) {
+            if (!(COL_EXP & 2) && q < HVX) {
                 float xf[C], t[BR];
                 unpack<C>(xv[u], xf);
 #pragma unroll
@@ -265,52 +297,60 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
                     for (int c = 0; c < C; ++c) acc = fmaf(w1[oo * C + c], xf[c], acc);
                     t[oo] = elu_f(acc + s.b2a) + s.b2b;
                 }
-                const typename Vec<BR>::U tp = packv<BR>(t);
-                *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = tp;
-                const int line = q / PL, pos = q - line * PL;
-                if (t2o && interior(line, pos)) *reinterpret_cast<typename Vec<BR>::U *>(t2o + int64_t(vox[u]) * BR) = tp;
+                *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = packv<BR>(t);
             }
         }
     }
     __syncthreads();
-    // this thread's 8 voxels (phase C): brick line ln, D-group dg; x in flight during phase B
-    const int ln = tid >> 2, dg = tid & 3;
+    // this thread's 4 voxels (phase C): brick line ln, D-group dg; x in flight during phase B
+    const int ln = tid / (BD / DV), dg = tid % (BD / DV);
     const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
     constexpr int NXB = DV * C * 2 / 16;  // 16-byte pieces of the 8 voxels' x
     uint4 xr[NXB];
     ld16s<NXB>(x + vox0 * C, xr);
     // B. raw W2 (*) t2 per m-tile
-    for (int mt = wave; mt < NMT; mt += NT / 64) {
+    int woff[K::KS];
+    win_offsets<BR>(row, kb, woff);
+#pragma unroll 4
+    for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int wb = win_base(mt, BR);
 #pragma unroll
-        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, 16 * mt + row, k, kb), fw[k], acc);
+        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, wb + woff[k]), fw[k], acc);
         if (row < BR) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) accs[(16 * mt + 4 * kb + j) * BR + row] = acc[j];
+            for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
         }
     }
     __syncthreads();
-    // C. t3 and out of the thread's 8 voxels
+    // C. t3 and out of the thread's 4 voxels (and their t2, saved for the backward)
+    if constexpr ((COL_EXP & 16) != 0) return;
     const int v0 = ln * BD + dg * DV;
+    if (t2o) {
+        const bf16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
+        uint32_t w[DV * BR / 2];
+        if constexpr (BR == 1) {  // 4 positions at an odd element offset
+            const uint4 u4 = __builtin_bit_cast(uint4, read8(t2h, int(src - t2h)));
+            w[0] = u4.x, w[1] = u4.y;
+        } else {
+#pragma unroll
+            for (int i = 0; i < DV * BR / 2; ++i) w[i] = reinterpret_cast<const uint32_t *>(src)[i];
+        }
+        store_words<DV * BR / 2>(t2o + vox0 * BR, w);
+    }
     float t3v[DV][BR];
 #pragma unroll
     for (int i = 0; i < DV; ++i)
 #pragma unroll
-        for (int oo = 0; oo < BR; ++oo) t3v[i][oo] = rbf(elu_f(accs[(v0 + i) * BR + oo] + s.b3a) + s.b3b);
+        for (int oo = 0; oo < BR; ++oo) t3v[i][oo] = rbf(elu_f(accs[acc_at(v0 + i, BR) + oo] + s.b3a) + s.b3b);
     {
-        constexpr int NTB = DV * BR * 2 / 16;  // B >= 1: 8 voxels x B bf16 = 16 B x B
-        static_assert(NTB >= 1, "t3 store");
         uint32_t w[DV * BR / 2];
 #pragma unroll
         for (int i = 0; i < DV * BR / 2; ++i) {
             const int e0 = 2 * i, e1 = 2 * i + 1;
             w[i] = uint32_t(f2bf(t3v[e0 / BR][e0 % BR])) | (uint32_t(f2bf(t3v[e1 / BR][e1 % BR])) << 16);
         }
-        if (t3o) {  // NULL: eval forward, nothing saved
-#pragma unroll
-            for (int i = 0; i < NTB; ++i)
-                reinterpret_cast<uint4 *>(t3o + vox0 * BR)[i] = uint4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-        }
+        if (t3o) store_words<DV * BR / 2>(t3o + vox0 * BR, w);  // NULL: eval forward, nothing saved
     }
     float xf[DV * C];
 #pragma unroll
@@ -354,9 +394,10 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
     bf16_t *t2T = z3h + HVX * BR + PADE;             // t2 on the halo, channel-major [BR][NLN][TP]
     bf16_t *z3T = t2T + BR * NLN * TP;                // gz3 of the brick, channel-major [BR][ZP]
     float *accs = reinterpret_cast<float *>(z3T + BR * ZP);  // [NV][BR] raw W2^T (*) gz3
-    int *lbase = reinterpret_cast<int *>(accs + NV * BR);
+    int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     float *red = reinterpret_cast<float *>(lbase + NLN);  // [4 waves][NE]
     float *wred = reinterpret_cast<float *>(smem);        // after phase C: [4][NTN][64][4] over z3h / t2T
+    static_assert(size_t(HVX * BR + PADE + BR * NLN * TP) * 2 >= size_t(4 * K::NTN * 256) * 4, "W2 sums fit z3h + t2T");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
     const Org o = brick_org(a, blockIdx.x);
     const Scal s = load_scal(p);
@@ -376,22 +417,30 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
     for (int oo = 0; oo < BR; ++oo)
 #pragma unroll
         for (int c = 0; c < C; ++c) g3[oo][c] = 0.f;
-    {
-        constexpr int P = (HVX + NT - 1) / NT;
+    // two batches of halo items: every load of a batch issued before its math (registers)
+    constexpr int PH = ((HVX + NT - 1) / NT + 1) / 2;
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+        constexpr int P = PH;
         typename Vec<C>::U gv[P];
         typename Vec<BR>::U tv3[P], tv2[P];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             int line, pos;
-            const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
-            gv[u] = *reinterpret_cast<const typename Vec<C>::U *>(g + int64_t(vx) * C);
-            tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
-            tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
+            const int vx = halo_voxel(a, o, lbase, min(tid + (half * PH + u) * NT, HVX - 1), line, pos);
+            if constexpr (!(COL_EXP & 1)) {
+                gv[u] = *reinterpret_cast<const typename Vec<C>::U *>(g + int64_t(vx) * C);
+                tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
+                tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
+            } else {
+                gv[u] = typename Vec<C>::U{};
+                tv3[u] = tv2[u] = typename Vec<BR>::U{};
+            }
         }
 #pragma unroll
         for (int u = 0; u < P; ++u) {
-            const int q = tid + u * NT;
-            if (q < HVX) {
+            const int q = tid + (half * PH + u) * NT;
+            if (!(COL_EXP & 2) && q < HVX) {
                 const int line = q / PL, pos = q - line * PL;
                 const bool in = interior(line, pos);
                 float gf[C], t3f[BR], t2f[BR], z[BR];
@@ -428,25 +477,27 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
         }
     }
     __syncthreads();
-    // the thread's 8 voxels (phase C): g and x in flight during phase B
-    const int ln = tid >> 2, dg = tid & 3;
+    // the thread's 4 voxels (phase C): g and x in flight during phase B
+    const int ln = tid / (BD / DV), dg = tid % (BD / DV);
     const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
     constexpr int NXB = DV * C * 2 / 16;
-    uint4 xr[NXB], gr[NXB];
-    ld16s<NXB>(x + vox0 * C, xr);
-    ld16s<NXB>(g + vox0 * C, gr);
     // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
-    for (int mt = wave; mt < NMT; mt += NT / 64) {
+    int woff[K::KS];
+    win_offsets<BR>(row, kb, woff);
+#pragma unroll 2
+    for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int wb = win_base(mt, BR);
 #pragma unroll
-        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, 16 * mt + row, k, kb), fw[k], acc);
+        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, wb + woff[k]), fw[k], acc);
         if (row < BR) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) accs[(16 * mt + 4 * kb + j) * BR + row] = acc[j];
+            for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
         }
     }
     // B2. W2 gradient: D[co][col] += sum_v gz3[v][co] * t2win[v][col], col = r * 3B + kd * B + ci;
-    // wave w takes the brick lines 16 w .. 16 w + 15 (one 32-voxel k-step each)
+    // wave w takes the 32-voxel k-steps 8 w .. 8 w + 7 (two brick lines each; lane kb: line
+    // 2 ks + kb / 2, d = 8 (kb & 1) + j)
     f32x4 aw[K::NTN];
     int toff[K::NTN];
 #pragma unroll
@@ -454,92 +505,94 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
         aw[n] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int col = min(16 * n + row, 27 * BR - 1), r = col / (3 * BR), e = col - r * 3 * BR, kd = e / BR,
                   ci = e - kd * BR, kh = r / 3, kw = r - 3 * kh;
-        toff[n] = (ci * NLN + kh * WL + kw) * TP + kd + 8 * kb;  // + line offset of the k-step
+        toff[n] = (ci * NLN + kh * WL + kw) * TP + kd + 8 * (kb & 1);  // + line offset of the k-step
     }
-    for (int ks = 16 * wave; ks < 16 * wave + 16; ++ks) {
+#pragma unroll 2
+    for (int ks = 8 * wave; ks < ((COL_EXP & 8) ? 0 : 8 * wave + 8); ++ks) {
         // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
         const bf16x8 af = *reinterpret_cast<const bf16x8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
-        const int lo = ((ks >> 3) * WL + (ks & 7)) * TP;
+        const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
 #pragma unroll
         for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
     }
     __syncthreads();
-    // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 8 voxels
+    // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 4 voxels
+    if constexpr ((COL_EXP & 16) != 0) return;
     const int v0 = ln * BD + dg * DV;
     float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f, dw1[BR][C];
 #pragma unroll
     for (int oo = 0; oo < BR; ++oo)
 #pragma unroll
         for (int c = 0; c < C; ++c) dw1[oo][c] = 0.f;
-    float xf[DV * C], gf[DV * C], gxo[DV * C];
-#pragma unroll
-    for (int i = 0; i < NXB; ++i) {
-        const uint32_t wx[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w}, wg[4] = {gr[i].x, gr[i].y, gr[i].z, gr[i].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            xf[8 * i + 2 * k] = __uint_as_float(wx[k] << 16);
-            xf[8 * i + 2 * k + 1] = __uint_as_float(wx[k] & 0xffff0000u);
-            gf[8 * i + 2 * k] = __uint_as_float(wg[k] << 16);
-            gf[8 * i + 2 * k + 1] = __uint_as_float(wg[k] & 0xffff0000u);
-        }
-    }
+    // 16-byte pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
+    // flight during the current one's math (one piece of registers at a time: occupancy)
+    constexpr int PV = 8 / C;
+    auto elem = [](const uint4 &q, int e) {  // element e (0..7) of a piece
+        const int wsel = e >> 1;
+        const uint32_t wv = wsel == 0 ? q.x : wsel == 1 ? q.y : wsel == 2 ? q.z : q.w;
+        return (e & 1) ? __uint_as_float(wv & 0xffff0000u) : __uint_as_float(wv << 16);
+    };
     const int hl0 = ((ln >> 3) + 1) * WL + (ln & 7) + 1;
-#pragma unroll
-    for (int i = 0; i < DV; ++i) {
-        float z1[BR];
-#pragma unroll
-        for (int oo = 0; oo < BR; ++oo) {
-            const float gt2 = accs[(v0 + i) * BR + oo];
-            const float t2v = bf(t2T[(oo * NLN + hl0) * TP + dg * DV + i + 1]);
-            const float zz = gt2 * elu_d_act(t2v, s.b2b);
-            s2b += gt2;
-            s2a += zz;
-            z1[oo] = rbf(zz);
+    const uint4 *xp = reinterpret_cast<const uint4 *>(x + vox0 * C), *gp = reinterpret_cast<const uint4 *>(g + vox0 * C);
+    uint4 xq = xp[0], gq = gp[0];
+#pragma unroll 1
+    for (int pc = 0; pc < NXB; ++pc) {
+        uint4 xn = xq, gn = gq;
+        if (pc + 1 < NXB) {
+            xn = xp[pc + 1];
+            gn = gp[pc + 1];
         }
+        uint32_t ow[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            float gt1 = 0.f;
+        for (int vi = 0; vi < PV; ++vi) {
+            const int i = pc * PV + vi;
+            float z1[BR];
 #pragma unroll
-            for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
-            const float zx = xf[i * C + c] + s.b1a;
-            const float e1 = zx > 0.f ? 1.f : __expf(zx);
-            const float u1 = rbf((zx > 0.f ? zx : e1 - 1.f) + s.b1b);
-            s1b += gt1;
-            s1a = fmaf(gt1, e1, s1a);
-            gxo[i * C + c] = gf[i * C + c] + gt1 * e1;
+            for (int oo = 0; oo < BR; ++oo) {
+                const float gt2 = accs[acc_at(v0 + i, BR) + oo];
+                const float t2v = bf(t2T[(oo * NLN + hl0) * TP + dg * DV + i + 1]);
+                const float zz = gt2 * elu_d_act(t2v, s.b2b);
+                s2b += gt2;
+                s2a += zz;
+                z1[oo] = rbf(zz);
+            }
 #pragma unroll
-            for (int oo = 0; oo < BR; ++oo) dw1[oo][c] = fmaf(z1[oo], u1, dw1[oo][c]);
+            for (int c = 0; c < C; ++c) {
+                float gt1 = 0.f;
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
+                const int e = vi * C + c;
+                const float zx = elem(xq, e) + s.b1a;
+                const float e1 = zx > 0.f ? 1.f : __expf(zx);
+                const float u1 = rbf((zx > 0.f ? zx : e1 - 1.f) + s.b1b);
+                s1b += gt1;
+                s1a = fmaf(gt1, e1, s1a);
+                const uint32_t hb = f2bf(elem(gq, e) + gt1 * e1);
+                ow[e >> 1] |= (e & 1) ? (hb << 16) : hb;
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) dw1[oo][c] = fmaf(z1[oo], u1, dw1[oo][c]);
+            }
         }
-    }
-#pragma unroll
-    for (int i = 0; i < NXB; ++i) {
-        float ov[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) ov[k] = gxo[8 * i + k];
-        reinterpret_cast<uint4 *>(gx + vox0 * C)[i] = __builtin_bit_cast(uint4, pack8(ov));
+        reinterpret_cast<uint4 *>(gx + vox0 * C)[pc] = uint4{ow[0], ow[1], ow[2], ow[3]};
+        xq = xn;
+        gq = gn;
     }
     // partial row of this brick: per-wave shuffle sums, then the 4 waves in order
-    float vals[NE];
     {
-        int e = 0;
+        auto put = [&](int e, float v) {
+            const float t = wave_sum(v);
+            if (lane == 0) red[wave * NE + e] = t;
+        };
 #pragma unroll
         for (int oo = 0; oo < BR; ++oo)
 #pragma unroll
-            for (int c = 0; c < C; ++c) vals[e++] = g3[oo][c];
-        e += 27 * BR * BR;  // W2: from the MFMA accumulators below
-#pragma unroll
-        for (int oo = 0; oo < BR; ++oo)
-#pragma unroll
-            for (int c = 0; c < C; ++c) vals[e++] = dw1[oo][c];
+            for (int c = 0; c < C; ++c) {
+                put(oo * C + c, g3[oo][c]);
+                put(BR * C + 27 * BR * BR + oo * C + c, dw1[oo][c]);
+            }
         const float sc8[NSC] = {s4, s3b, s3a, ssc, s2b, s2a, s1b, s1a};
 #pragma unroll
-        for (int k = 0; k < NSC; ++k) vals[e++] = sc8[k];
-    }
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        if (e >= BR * C && e < BR * C + 27 * BR * BR) continue;
-        const float t = wave_sum(vals[e]);
-        if (lane == 0) red[wave * NE + e] = t;
+        for (int k = 0; k < NSC; ++k) put(2 * BR * C + 27 * BR * BR + k, sc8[k]);
     }
     __syncthreads();  // every wave is past phase C (t2T) before the W2 sums go over it
     // W2 accumulators: D rows 4 kb + j = co, columns 16 n + row = col
@@ -559,22 +612,34 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
 #pragma unroll
             for (int w = 0; w < NT / 64; ++w) t += red[w * NE + e];
         }
-        part[int64_t(e) * gridDim.x + blockIdx.x] = t;
+        part[int64_t(blockIdx.x) * NE + e] = t;  // the brick's row: one contiguous write
     }
 }
 
-// every entry summed over the bricks in a fixed order, added into its gradient buffer
+// Fixed-order sum of the brick rows [brick][NE]: stage 1, workgroup r sums bricks
+// [r * RCH, (r + 1) * RCH) per entry (threads over entries: coalesced rows) into part2[r][e];
+// stage 2 sums the stage-1 rows per entry in order and adds into the gradient buffers.
+constexpr int RCH = 128;
 template <int C, int BR>
-__global__ __launch_bounds__(256) void k_col_reduce(const float *__restrict__ part, int nb, const float *__restrict__ scale,
-                                                    vq3d_preact_grads gr) {
-    constexpr int E1 = BR * C, E2 = 27 * BR * BR, E3 = BR * C;
-    __shared__ float sm[4];
-    const int e = blockIdx.x;
-    const float *pp = part + int64_t(e) * nb;
-    float acc = 0.f;
-    for (int i = threadIdx.x; i < nb; i += 256) acc += pp[i];
-    const float t = block_sum<float, 256>(acc, sm);
-    if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void k_col_reduce1(const float *__restrict__ part, int nb, float *__restrict__ part2) {
+    constexpr int NE = n_entries<C, BR>();
+    const int b0 = blockIdx.x * RCH, b1 = min(nb, b0 + RCH);
+    for (int e = threadIdx.x; e < NE; e += 256) {
+        float t = 0.f;
+#pragma unroll 8
+        for (int b = b0; b < b1; ++b) t += part[int64_t(b) * NE + e];
+        part2[int64_t(blockIdx.x) * NE + e] = t;
+    }
+}
+template <int C, int BR>
+__global__ __launch_bounds__(256) void k_col_reduce2(const float *__restrict__ part2, int nr, const float *__restrict__ scale,
+                                                     vq3d_preact_grads gr) {
+    constexpr int E1 = BR * C, E2 = 27 * BR * BR, E3 = BR * C, NE = n_entries<C, BR>();
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= NE) return;
+    float t = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < nr; ++r) t += part2[int64_t(r) * NE + e];
     if (e < E1) {  // G3 [o][c] -> dW3 [c][o] * scale
         const int oo = e / C, c = e - oo * C;
         gr.dw3[c * BR + oo] += *scale * t;
@@ -592,11 +657,11 @@ __global__ __launch_bounds__(256) void k_col_reduce(const float *__restrict__ pa
 
 template <int C, int BR>
 constexpr size_t fwd_lds() {
-    return size_t(HVX * BR + PADE) * 2 + size_t(NV * BR) * 4 + NLN * 4;
+    return size_t(HVX * BR + PADE) * 2 + size_t(acc_floats(BR)) * 4 + NLN * 4;
 }
 template <int C, int BR>
 constexpr size_t bwd_lds() {
-    return size_t(HVX * BR + PADE + BR * NLN * TP + BR * ZP) * 2 + size_t(NV * BR) * 4 + NLN * 4 +
+    return size_t(HVX * BR + PADE + BR * NLN * TP + BR * ZP) * 2 + size_t(acc_floats(BR)) * 4 + NLN * 4 +
            size_t(4 * n_entries<C, BR>()) * 4;
 }
 
@@ -639,7 +704,10 @@ void launch_bwd(const CArgs &a, const bf16_t *g, const bf16_t *x, const bf16_t *
         attr = true;
     }
     k_col_bwd<C, BR><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, g, x, t2, t3, w1, w2, w3, p, part, gx);
-    k_col_reduce<C, BR><<<n_entries<C, BR>(), 256, 0, s>>>(part, a.nbricks, p.scale, gr);
+    const int nr = (a.nbricks + RCH - 1) / RCH;
+    float *part2 = part + size_t(a.nbricks) * n_entries<C, BR>();
+    k_col_reduce1<C, BR><<<nr, 256, 0, s>>>(part, a.nbricks, part2);
+    k_col_reduce2<C, BR><<<(n_entries<C, BR>() + 255) / 256, 256, 0, s>>>(part2, nr, p.scale, gr);
 }
 
 }  // namespace
@@ -654,7 +722,7 @@ size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d) {
     if (!col_supported(batch, C, BR, h, w, d)) return 0;
     const CArgs a = make_args(batch, h, w, d);
     const int ne = C == 2 ? n_entries<2, 1>() : C == 4 ? n_entries<4, 2>() : n_entries<8, 4>();
-    return size_t(a.nbricks) * ne * 4;
+    return (size_t(a.nbricks) + (a.nbricks + RCH - 1) / RCH) * ne * 4;
 }
 
 int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1, const float *w2,

@@ -355,7 +355,7 @@ def set_small_blocks(enabled, fused_backward=True):
 
 # the brick kernels' fused backward up to this many voxels (measured, bench 3L pub: 23.6 vs ~100
 # us per (8, 4) block at 32x32x8); beyond it their per-brick weight-gradient partials are
-# LDS-bound and, where the column kernels (preact_col.hip, D % 32 == 0) do not apply, the
+# LDS-bound and, where the column kernels (preact_col.hip, D % 16 == 0) do not apply, the
 # per-conv backward wins
 _SMALL_BWD_MAX_VOX = 1 << 19
 
@@ -365,7 +365,9 @@ def small_backward_fused(x):
     if not _small[1]:
         return False
     nb = c // 2
-    return int(L.query("vq3d_preact_small_plan", b, c, nb, h, w, d)) == 2 or b * h * w * d <= _SMALL_BWD_MAX_VOX
+    if int(L.query("vq3d_preact_small_plan", b, c, nb, h, w, d)) == 2:  # column kernels
+        return True
+    return b * h * w * d <= _SMALL_BWD_MAX_VOX
 
 
 def preact_small_supported(x, branch):

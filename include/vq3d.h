@@ -238,7 +238,7 @@ int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch,
 int vq3d_preact_small_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                                 int32_t dd);
 /* 0: unsupported; 1: brick kernels (small grids); 2: column kernels (H % 8 == W % 8 == 0,
- * D % 32 == 0: one-launch forward, fused backward + fixed-order reduction, preact_col.hip) */
+ * D % 16 == 0: one-launch forward, fused backward + fixed-order reduction, preact_col.hip) */
 int vq3d_preact_small_plan(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd);
 size_t vq3d_preact_small_workspace_bytes(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                                          int32_t dd);
