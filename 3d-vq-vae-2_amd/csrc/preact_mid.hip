@@ -11,12 +11,15 @@
 //          k_pm_fwd  : per tile, t2 on the tile's circular halo in LDS -> t3 on the matrix cores
 //                      -> out = scale W3 t3 + b4 + x on the matrix cores; t3 / out leave in 16-B
 //                      chunks.
-// backward k_pm_bwd1 : gz3 = bf16(scale W3^T g * elu'(t3)) (pointwise) + the W3 / scale / b4 / b3
+// backward k_pm_bwd1 : gz3 = bf16(scale W3^T g * elu'(t3)) (pointwise) + the scale / b4 / b3
 //                      partials
 //          k_pm_bwd2 : per tile, gz3 and t2 on the halo in LDS -> gt2 = W2^T (*) gz3 (flipped
 //                      taps, matrix cores) -> gz1 = bf16(gt2 * elu'(t2)) -> gx = g + (W1^T gz1)
-//                      * elu'(x + b1a); the W2 gradient (matrix cores, voxels as the reduction
-//                      axis) and the W1 / b2 / b1 partials
+//                      * elu'(x + b1a); gz1 to the workspace and the b2 / b1 partials
+//          k_pm_w2grad, k_pm_w13grad: the W2 and the W1 / W3 gradient partials (matrix cores,
+//                      voxels as the reduction axis, channel-major LDS copies); they only read,
+//                      so the caller may run them on a second stream next to the next block's
+//                      backward
 //          k_pm_reduce: every gradient entry summed over the workgroups in a fixed order and
 //                      added into the gradient buffers (deterministic, one adder per entry).
 // Rounding points are the unfused per-conv path's (t2, t3, gz3, gz1, gx, out rounded to bf16,
@@ -54,10 +57,15 @@ constexpr int LINT = 16;               // element of position 0: the interior ru
 constexpr int LEND = LINT + 9 * 9;     // first element after position 8 (97): zero padding
 constexpr int SPAD = 40;               // zero tail of the pitch-9 / pitch-18 tile buffers
 
-// partial-gradient entries
-constexpr int NE1 = C * BR + 4;                    // K1: G3 [co][o], b4, b3b, b3a, scale
-constexpr int NW2 = BR * BR * 27;                  // W2 gradient [co][ci][tap]
-constexpr int NE2 = NW2 + BR * C + 4;              // K2: W2, W1 [o][c], b2b, b2a, b1b, b1a
+// scalar partials per workgroup: K1 b4, b3b, b3a, scale; K2 b2b, b2a, b1b, b1a
+constexpr int NE1 = 4, NE2 = 4;
+constexpr int NW2 = BR * BR * 27;  // W2 gradient [co][ci][tap]
+// weight-gradient kernels: W2 over 512-voxel chunks (k_pm_w2grad), W1 / G3 over 128-voxel pieces
+// (k_pm_w13grad)
+constexpr int CHV = 512, ZP = CHV + 16;
+constexpr int SUBV = 128, SP = SUBV + 8;
+constexpr int NER = BR * 3 * BR;  // W2 entries of one tap row: co x (kd, ci)
+constexpr int NEB = 2 * BR * C;   // W1 [o][c] then G3 [o][co]
 
 struct PmArgs {
     int B, H, W, D;
@@ -425,28 +433,23 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
 }
 
 // ============================================================================================ backward
-// K1: gz3 = bf16(scale * W3^T g * elu'(t3 - b3b)); G3 = sum g (x) t3 (matrix cores, voxels as
-// the reduction axis), sums of g (b4), of scale W3^T g (b3b), of gz3 (b3a) and of g . (W3 t3)
-// (scale).  Blocks of 256 voxels; the next block's loads are in flight during the current one.
+// K1: gz3 = bf16(scale * W3^T g * elu'(t3 - b3b)) and the sums of g (b4), of scale W3^T g (b3b),
+// of gz3 (b3a) and of g . (W3 t3) (scale).  Blocks of 256 voxels; the next block's loads are in
+// flight during the current one.  (The W3 gradient, sum t3 (x) g, is k_pm_w13grad's.)
 __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__restrict__ g,
                                                 const bf16_t *__restrict__ t3, const float *__restrict__ w3,
                                                 vq3d_preact_params p, bf16_t *__restrict__ gz3o,
                                                 float *__restrict__ part) {
     __shared__ float w3s[C * BR];
-    __shared__ __attribute__((aligned(16))) bf16_t gs[NT * C + SPAD];
-    __shared__ __attribute__((aligned(16))) bf16_t ts[NT * BR + SPAD];
+    __shared__ __attribute__((aligned(16))) bf16_t gs[NT * C];
+    __shared__ __attribute__((aligned(16))) bf16_t ts[NT * BR];
     __shared__ __attribute__((aligned(16))) bf16_t zs[NT * BR];
-    __shared__ float red[4 * 2 * 64 * 4];
+    __shared__ float red[32];
     constexpr int NG = NT * C / 8, NTT = NT * BR / 8, PG = (NG + NT - 1) / NT, PT = (NTT + NT - 1) / NT;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int tid = threadIdx.x;
     stage_w(w3s, w3, C * BR);
-    for (int i = tid; i < SPAD; i += NT) {
-        gs[NT * C + i] = 0;
-        ts[NT * BR + i] = 0;
-    }
     const Scal s = load_scal(p);
     float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f;
-    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int64_t nblk = nvox / NT;
     uint4 vg[PG], vt[PT];
     auto load = [&](int64_t blk) {
@@ -493,69 +496,41 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
                 zs[tid * BR + o] = f2bf(z);
             }
         }
-        // G3[o][co] += sum_v t3[v][o] g[v][co]: wave w takes voxels 64 w .. 64 w + 63 (2 k-steps)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int vb = wave * 64 + ks * 32 + 8 * kb;
-            const bf16x8 af = gather8(ts, vb * BR + row, BR, row < BR);
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                const int co = 16 * nt + row;
-                acc[nt] = mfma(af, gather8(gs, vb * C + co, C, co < C), acc[nt]);
-            }
-        }
         __syncthreads();
         constexpr int NO = NT * BR / 8;
         for (int i = tid; i < NO; i += NT)
             reinterpret_cast<uint4 *>(gz3o + v0 * BR)[i] = reinterpret_cast<const uint4 *>(zs)[i];
     }
-    // workgroup partials: the 4 waves' accumulators summed in a fixed order
-    __syncthreads();
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[((wave * 2 + nt) * 64 + lane) * 4 + j] = acc[nt][j];
-    __syncthreads();
     float *dst = part + int64_t(blockIdx.x) * NE1;
-    for (int e = tid; e < 2 * 64 * 4; e += NT) {
-        const int nt = e / 256, l = (e / 4) % 64, j = e % 4;
-        const int o = 4 * (l >> 4) + j, co = 16 * nt + (l & 15);
-        if (o < BR && co < C) {
-            float t = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) t += red[((w * 2 + nt) * 64 + l) * 4 + j];
-            dst[co * BR + o] = t;
-        }
-    }
-    __syncthreads();
     const float t4 = block_sum<float, NT>(s4, red);
     const float t3b = block_sum<float, NT>(s3b, red + 8);
     const float t3a = block_sum<float, NT>(s3a, red + 16);
     const float tsc = block_sum<float, NT>(ssc, red + 24);
     if (tid == 0) {
-        dst[C * BR] = t4;
-        dst[C * BR + 1] = t3b;
-        dst[C * BR + 2] = t3a;
-        dst[C * BR + 3] = tsc;
+        dst[0] = t4;
+        dst[1] = t3b;
+        dst[2] = t3a;
+        dst[3] = tsc;
     }
 }
 
-// K2: per TH x TW x 8 tile (see the file comment)
+// K2: per TH x TW x 8 tile: gt2 = W2^T (*) gz3 (flipped taps) -> gz1 = bf16(gt2 * elu'(t2)) ->
+// gx = g + (W1^T gz1) * elu'(x + b1a); gz1 to the workspace (k_pm_w13grad) and the b2 / b1 sums
 template <int TH, int TW>
 __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restrict__ gz3, const bf16_t *__restrict__ t2,
                                                 const bf16_t *__restrict__ x, const bf16_t *__restrict__ g,
                                                 const float *__restrict__ w1, const float *__restrict__ w2,
                                                 vq3d_preact_params p, bf16_t *__restrict__ gx,
-                                                float *__restrict__ part) {
+                                                bf16_t *__restrict__ gz1o, float *__restrict__ part) {
     using T = Tile<TH, TW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t *zl = reinterpret_cast<bf16_t *>(smem);  // gz3 halo lines
     bf16_t *tl = zl + T::LINES;                       // t2 halo lines
     bf16_t *z1s = tl + T::LINES;                      // gz1 [TV][9]
-    bf16_t *xs = z1s + T::S9;                         // x [TV][18], then u1 in place
+    bf16_t *xs = z1s + T::S9;                         // x [TV][18]
     bf16_t *gs = xs + T::S18;                         // g [TV][18], then gx in place
     float *w1s = reinterpret_cast<float *>(gs + T::S18);  // W1 [o][c]
-    float *red = reinterpret_cast<float *>(smem);         // after the tiles: [4][2][64][4] cross-wave sums
+    float *red = w1s + BR * C;                            // [32] block sums
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int row = lane & 15, kb = lane >> 4;
     bf16x8 bw2[9];
@@ -574,17 +549,8 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
         zero_pads<TH, TW>(zl, 2, tails, at, 3);
     }
     const Scal s = load_scal(p);
-    // W2 gradient accumulators: wave w owns tap rows kk = w, w + 4, w + 8 (< 9), 2 column tiles
-    // of the 27-element window each; W1 gradient: 2 column tiles (18 channels)
-    f32x4 aw2[3][2], aw1[2];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) aw2[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    aw1[0] = aw1[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
-    // the next tile's halo loads are in flight while the current tile computes (x / g of the
-    // current tile are loaded at the top: prefetching them too costs the second wave per SIMD)
+    // the next tile's halo loads are in flight while the current tile computes
     LinesLd<TH, TW> lz, lt;
     if (blockIdx.x < a.ntiles) {
         const Org o0 = tile_org(a, blockIdx.x, TH, TW);
@@ -609,7 +575,6 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             lg.store(gs);
         }
         __syncthreads();
-        // gt2 = W2^T (*) gz3 (flipped taps) -> gz1 = bf16(gt2 * elu'(t2 - b2b))
         for (int mt = wave; mt < T::NMT; mt += NT / 64) {
             const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
             const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
@@ -629,39 +594,18 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
                 }
             }
         }
-        // W2 gradient: dW2[co][kk][e] += sum_v gz3[v][co] * t2window(kk)[v][e], k-steps of 32
-        // voxels = 4 D-runs
-#pragma unroll 1
-        for (int ks = 0; ks < T::TV / 32; ++ks) {
-            const int r = ks * 4 + kb;
-            const int lbase = ((r / TW) * T::LW + r % TW) * LSP;
-            const bf16x8 af = gather8(zl, lbase + (T::LW + 1) * LSP + LINT + row, BR, row < BR);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                asm volatile("" ::: "memory");  // one tap row's gathers in flight at a time (registers)
-                const int kk = wave + 4 * i;
-                if (kk < 9) {
-                    const int off = lbase + ((kk / 3) * T::LW + kk % 3) * LSP + LOFF;
-#pragma unroll
-                    for (int n = 0; n < 2; ++n) {
-                        const int e = 16 * n + row;
-                        aw2[i][n] = mfma(af, gather8(tl, off + e, BR, e < 27), aw2[i][n]);
-                    }
-                }
-            }
-        }
         __syncthreads();
-        // gx = g + (W1^T gz1) * elu'(x + b1a); u1 = elu(x + b1a) + b1b in place over x
+        // gx = g + (W1^T gz1) * elu'(x + b1a)
         for (int v = tid; v < T::TV; v += NT) {
             float z1[BR];
 #pragma unroll
             for (int oo = 0; oo < BR; ++oo) z1[oo] = bf(z1s[v * BR + oo]);
-            uint32_t *xr = reinterpret_cast<uint32_t *>(xs + v * C);
+            const uint32_t *xr = reinterpret_cast<const uint32_t *>(xs + v * C);
             uint32_t *gr = reinterpret_cast<uint32_t *>(gs + v * C);
 #pragma unroll 1
             for (int j = 0; j < C / 2; ++j) {
                 const uint32_t xq = xr[j], gq = gr[j];
-                float r2[2], u2[2];
+                float r2[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int c = 2 * j + h;
@@ -673,115 +617,299 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
                     s1b += gt1;
                     s1a += gt1 * ez;
                     r2[h] = bf(h ? (gq >> 16) : (gq & 0xffffu)) + gt1 * ez;
-                    u2[h] = (zx > 0.f ? zx : ez - 1.f) + s.b1b;
                 }
                 gr[j] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
-                xr[j] = uint32_t(f2bf(u2[0])) | (uint32_t(f2bf(u2[1])) << 16);
             }
         }
         __syncthreads();
-        // W1 gradient: dW1[o][c] += sum_v gz1[v][o] u1[v][c]; wave w takes k-steps w, w + 4, ...
-        for (int ks = wave; ks < T::TV / 32; ks += NT / 64) {
-            const int vb = ks * 32 + 8 * kb;
-            const bf16x8 af = gather8(z1s, vb * BR + row, BR, row < BR);
-#pragma unroll
-            for (int n = 0; n < 2; ++n) {
-                const int c = 16 * n + row;
-                aw1[n] = mfma(af, gather8(xs, vb * C + c, C, c < C), aw1[n]);
-            }
-        }
         store_tile<TH, TW, C>(a, o, gs, gx);
+        store_tile<TH, TW, BR>(a, o, z1s, gz1o);
     }
-    // workgroup partials [entry]: W2 in nn.Conv3d order [co][ci][tap], W1 [o][c], then scalars
-    static_assert(2 * T::LINES * 2 >= 4 * 2 * 64 * 4 * 4, "cross-wave sums fit the halo images");
     float *dst = part + int64_t(blockIdx.x) * NE2;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int kk = wave + 4 * i;
-        if (kk < 9) {
-#pragma unroll
-            for (int n = 0; n < 2; ++n) {
-                const int e = 16 * n + row;
-                if (e < 27) {
-                    const int kd = e / 9, ci = e - 9 * kd;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int co = 4 * kb + j;
-                        if (co < BR) dst[(co * BR + ci) * 27 + kk * 3 + kd] = aw2[i][n][j];
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[((wave * 2 + n) * 64 + lane) * 4 + j] = aw1[n][j];
-    __syncthreads();
-    for (int e = tid; e < 2 * 64 * 4; e += NT) {
-        const int n = e / 256, l = (e / 4) % 64, j = e % 4;
-        const int oo = 4 * (l >> 4) + j, c = 16 * n + (l & 15);
-        if (oo < BR && c < C) {
-            float t = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) t += red[((w * 2 + n) * 64 + l) * 4 + j];
-            dst[NW2 + oo * C + c] = t;
-        }
-    }
-    __syncthreads();
     const float t2b = block_sum<float, NT>(s2b, red);
     const float t2a = block_sum<float, NT>(s2a, red + 8);
     const float t1b = block_sum<float, NT>(s1b, red + 16);
     const float t1a = block_sum<float, NT>(s1a, red + 24);
     if (tid == 0) {
-        dst[NW2 + BR * C] = t2b;
-        dst[NW2 + BR * C + 1] = t2a;
-        dst[NW2 + BR * C + 2] = t1b;
-        dst[NW2 + BR * C + 3] = t1a;
+        dst[0] = t2b;
+        dst[1] = t2a;
+        dst[2] = t1b;
+        dst[3] = t1a;
     }
 }
 
-// K3: every gradient entry summed over the workgroup partials in a fixed order and added into
-// its gradient buffer.  A workgroup owns 32 consecutive entries of one partial array: 8 row
-// groups x 32 entries, so each row read is one 128-B segment, then the 8 group sums in order.
+// K3 (the weight gradients; may run on another stream after K1 / K2): voxels are the MFMA
+// reduction axis, so both operands are staged channel-major in LDS -- 16-B global loads whose 8
+// elements are scattered to their channel rows as they are written (no LDS gathers after).
+//
+// k_pm_w2grad: dW2[co][kk][kd, ci] += sum_v gz3[v][co] t2[v + tap][ci].  A chunk is a TH x TW
+// tile of whole D-lines (512 voxels); the workgroup stages gz3 over the tile and t2 over its
+// circular (TH + 2) x (TW + 2) halo (positions -1 .. D of each line), and wave kk (9 waves) owns
+// tap row kk = (kh, kw): its 2 accumulators (co x the 27 (kd, ci) window entries) sum over the
+// workgroup's npc chunks, the next chunk's loads in flight during the current one's MFMAs.
+// Chunks of one workgroup are consecutive and each XCD takes a contiguous eighth of them (the
+// halo re-reads hit that XCD's L2).
+constexpr int NT9 = 9 * 64;
+template <int D>
+struct W2c {
+    static constexpr int NL = CHV / D;  // lines per chunk
+    static constexpr int TH = NL >= 64 ? 8 : NL >= 16 ? 4 : NL >= 4 ? 2 : 1, TW = NL / TH;
+    static constexpr int LW = TW + 2, HL = (TH + 2) * LW;  // halo lines
+    static constexpr int RPD = D + 2;                       // positions -1 .. D
+    static constexpr int CSTR = HL * RPD + 8;               // per channel (read8 reads one dword past)
+    static constexpr int QL = D * BR / 8;                   // 16-B pieces of one 9-channel line
+    static constexpr int ZQ = NL * QL, TQ = HL * QL;
+    static constexpr int PZ = (ZQ + NT9 - 1) / NT9, PT = (TQ + NT9 - 1) / NT9;
+    static constexpr size_t LDS = size_t(16 * ZP + BR * CSTR) * 2;
+    static_assert(NL * D == CHV && TH * TW == NL, "chunk");
+};
+
+__device__ __forceinline__ void scatter9(bf16_t *dst, int pitch, int e0, uint4 q, int base) {
+    // the 8 elements e0 .. e0 + 7 of a 9-channel voxel-major run to dst[c * pitch + base + pos]
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int e = e0 + j, pos = e / BR, c = e - pos * BR;
+        dst[c * pitch + base + pos] = bf16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const bf16_t *__restrict__ gz3,
+                                                   const bf16_t *__restrict__ t2, float *__restrict__ p2a) {
+    using K = W2c<D>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    bf16_t *zT = reinterpret_cast<bf16_t *>(smem);  // gz3 [16][ZP] channel-major (rows >= 9 never read into results)
+    bf16_t *tT = zT + 16 * ZP;                      // t2 [9][HL][RPD] (+ tail)
+    const int tid = threadIdx.x, lane = tid & 63, kk = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int kh = kk / 3, kw = kk - 3 * kh;
+    const int nth = a.H / K::TH, ntw = a.W / K::TW;
+    // workgroup -> chunk range (XCD-aware when the grid is a multiple of 8)
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int slot = (nwg & 7) ? bid : (bid & 7) * (nwg >> 3) + (bid >> 3);
+    const int c0 = slot * npc;
+    for (int i = tid; i < BR * 8; i += NT9) tT[(i >> 3) * K::CSTR + K::HL * K::RPD + (i & 7)] = 0;
+    int toff[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const int e = min(16 * n + row, 26), kd = e / BR, ci = e - kd * BR;
+        toff[n] = ci * K::CSTR + kd;
+    }
+    uint4 vz[K::PZ], vt[K::PT];
+    auto load = [&](int c) {
+        const int tw_i = c % ntw, r = c / ntw, th_i = r % nth, b = r / nth;
+        const int h0 = th_i * K::TH, w0 = tw_i * K::TW;
+#pragma unroll
+        for (int u = 0; u < K::PZ; ++u) {
+            const int i = min(tid + u * NT9, K::ZQ - 1), l = i / K::QL, part = i - l * K::QL;
+            const int64_t lv = ((int64_t(b) * a.H + h0 + l / K::TW) * a.W + w0 + l % K::TW) * D;
+            vz[u] = reinterpret_cast<const uint4 *>(gz3 + lv * BR)[part];
+        }
+#pragma unroll
+        for (int u = 0; u < K::PT; ++u) {
+            const int i = min(tid + u * NT9, K::TQ - 1), hl = i / K::QL, part = i - hl * K::QL;
+            const int lh = hl / K::LW, lw = hl - lh * K::LW;
+            const int64_t lv = ((int64_t(b) * a.H + wrapm(h0 - 1 + lh, a.H)) * a.W + wrapm(w0 - 1 + lw, a.W)) * D;
+            vt[u] = reinterpret_cast<const uint4 *>(t2 + lv * BR)[part];
+        }
+    };
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int cend = min(c0 + npc, nchunk);
+    if (c0 < cend) load(c0);
+#pragma unroll 1
+    for (int c = c0; c < cend; ++c) {
+        __syncthreads();  // the previous chunk's fragments are read
+#pragma unroll
+        for (int u = 0; u < K::PZ; ++u) {
+            const int i = tid + u * NT9;
+            if (i < K::ZQ) {
+                const int l = i / K::QL, part = i - l * K::QL;
+                scatter9(zT, ZP, part * 8, vz[u], l * D);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < K::PT; ++u) {
+            const int i = tid + u * NT9;
+            if (i < K::TQ) {
+                const int hl = i / K::QL, part = i - hl * K::QL;
+                const uint32_t w[4] = {vt[u].x, vt[u].y, vt[u].z, vt[u].w};
+                bf16_t *ln = tT + hl * K::RPD;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int e = part * 8 + j, pos = e / BR, ci = e - pos * BR;
+                    const bf16_t v = bf16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                    ln[ci * K::CSTR + pos + 1] = v;
+                    if (pos == 0) ln[ci * K::CSTR + D + 1] = v;  // position D wraps to 0
+                    if (pos == D - 1) ln[ci * K::CSTR] = v;      // position -1 wraps to D - 1
+                }
+            }
+        }
+        __syncthreads();
+        if (c + 1 < cend) load(c + 1);
+#pragma unroll 4
+        for (int ks = 0; ks < CHV / 32; ++ks) {
+            const int v = 32 * ks + 8 * kb, l = v / D, d0 = v - l * D;
+            const int hl = (l / K::TW + kh) * K::LW + l % K::TW + kw;
+            const bf16x8 af = *reinterpret_cast<const bf16x8 *>(zT + row * ZP + v);
+            const int off = hl * K::RPD + d0;
+#pragma unroll
+            for (int n = 0; n < 2; ++n) acc[n] = mfma(af, read8(tT, toff[n] + off), acc[n]);
+        }
+    }
+    float *dst = p2a + (int64_t(bid) * 9 + kk) * NER;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = 4 * kb + j, col = 16 * n + row;
+            if (co < BR && col < 27) dst[co * 27 + col] = acc[n][j];
+        }
+}
+
+// k_pm_w13grad: W1 (sum gz1 (x) u1, u1 = bf16(elu(x + b1a) + b1b)) and G3 (sum t3 (x) g) over npb
+// pieces of SUBV voxels per workgroup (the next piece's loads in flight); wave w: (W1 | G3,
+// 16-column tile)
+__global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const bf16_t *__restrict__ gz1,
+                                                   const bf16_t *__restrict__ t3, const bf16_t *__restrict__ x,
+                                                   const bf16_t *__restrict__ g, vq3d_preact_params p,
+                                                   float *__restrict__ p2b) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int ch = blockIdx.x;
+    const Scal s = load_scal(p);
+    bf16_t *z1T = reinterpret_cast<bf16_t *>(smem);  // [16][SP] gz1
+    bf16_t *t3T = z1T + 16 * SP;                     // [16][SP] t3
+    bf16_t *u1T = t3T + 16 * SP;                     // [32][SP] u1
+    bf16_t *gT = u1T + 32 * SP;                      // [32][SP] g
+    const int isG3 = wave >> 1, nt = wave & 1;
+    const bf16_t *aT = isG3 ? t3T : z1T, *bT = isG3 ? gT : u1T;
+    // per piece: gz1 / t3 SUBV * 9 / 8 16-B pieces each, x / g SUBV * 18 / 8 each
+    constexpr int N9 = SUBV * BR / 8, N18 = SUBV * C / 8, NQ = 2 * N9 + 2 * N18, PQ = (NQ + NT - 1) / NT;
+    uint4 vq[PQ];
+    auto load = [&](int64_t v0) {
+#pragma unroll
+        for (int u = 0; u < PQ; ++u) {
+            const int i = min(tid + u * NT, NQ - 1);
+            const uint4 *src;
+            int k;
+            if (i < N9) src = reinterpret_cast<const uint4 *>(gz1 + v0 * BR), k = i;
+            else if (i < 2 * N9) src = reinterpret_cast<const uint4 *>(t3 + v0 * BR), k = i - N9;
+            else if (i < 2 * N9 + N18) src = reinterpret_cast<const uint4 *>(x + v0 * C), k = i - 2 * N9;
+            else src = reinterpret_cast<const uint4 *>(g + v0 * C), k = i - 2 * N9 - N18;
+            vq[u] = src[k];
+        }
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    load(int64_t(ch) * npb * SUBV);
+#pragma unroll 1
+    for (int pc = 0; pc < npb; ++pc) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PQ; ++u) {
+            const int i = tid + u * NT;
+            if (i < NQ) {
+                const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
+                if (i < 2 * N9) {
+                    bf16_t *dT = i < N9 ? z1T : t3T;
+                    const int e0 = (i < N9 ? i : i - N9) * 8;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int e = e0 + j, v = e / BR, c = e - v * BR;
+                        dT[c * SP + v] = bf16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                    }
+                } else {
+                    const bool isx = i < 2 * N9 + N18;
+                    bf16_t *dT = isx ? u1T : gT;
+                    const int e0 = (isx ? i - 2 * N9 : i - 2 * N9 - N18) * 8;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int e = e0 + j, v = e / C, c = e - v * C;
+                        uint32_t h = (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
+                        if (isx) h = f2bf(elu(bf(h) + s.b1a) + s.b1b);
+                        dT[c * SP + v] = bf16_t(h);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (pc + 1 < npb) load((int64_t(ch) * npb + pc + 1) * SUBV);
+#pragma unroll
+        for (int ks = 0; ks < SUBV / 32; ++ks) {
+            const int ko = 32 * ks + 8 * kb;
+            acc = mfma(*reinterpret_cast<const bf16x8 *>(aT + row * SP + ko),
+                       *reinterpret_cast<const bf16x8 *>(bT + (16 * nt + row) * SP + ko), acc);
+        }
+    }
+    float *dst = p2b + int64_t(ch) * NEB + isG3 * BR * C;
+    const int c = 16 * nt + row;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int oo = 4 * kb + j;
+        if (oo < BR && c < C) dst[oo * C + c] = acc[j];
+    }
+}
+
+// K4: every gradient entry summed over its partial rows in a fixed order and added into its
+// gradient buffer.  A workgroup owns 32 consecutive entries of one partial array: 8 row groups
+// x 32 entries (each row read one 128-B segment), then the 8 group sums in order.
 struct RedOut {
     float *dw1, *dw2, *dw3, *db1a, *db1b, *db2a, *db2b, *db3a, *db3b, *dscale, *db4;
     const float *scale;
 };
 
-constexpr int NB1 = (NE1 + 31) / 32, NB2 = (NE2 + 31) / 32;
+constexpr int NBA = (9 * NER + 31) / 32, NBB = (NEB + 31) / 32;
 
 __global__ __launch_bounds__(NT) void k_pm_reduce(const float *__restrict__ p1, int n1, const float *__restrict__ p2,
-                                                  int n2, RedOut o) {
+                                                  int n2, const float *__restrict__ p2a, int nwa,
+                                                  const float *__restrict__ p2b, int nchb, RedOut o) {
     __shared__ float sm[8][32];
     const int el = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    const bool first = blockIdx.x < NB1;
-    const int e = (first ? blockIdx.x : blockIdx.x - NB1) * 32 + el;
-    const float *P = first ? p1 : p2;
-    const int n = first ? n1 : n2, ne = first ? NE1 : NE2;
+    const int blk = blockIdx.x;
+    // blocks [0, NBA): W2 entries (kk, co, kd, ci) over the k_pm_w2grad workgroups; [NBA, NBA +
+    // NBB): W1 / G3; the last: the 8 scalars over the K1 / K2 workgroups
+    int e, n, stride;
+    const float *P;
+    if (blk < NBA) {
+        e = blk * 32 + el;
+        P = p2a + min(e, 9 * NER - 1);
+        n = e < 9 * NER ? nwa : 0;
+        stride = 9 * NER;
+    } else if (blk < NBA + NBB) {
+        e = (blk - NBA) * 32 + el;
+        P = p2b + min(e, NEB - 1);
+        n = e < NEB ? nchb : 0;
+        stride = NEB;
+    } else {
+        e = el;
+        const bool first = el < NE1;
+        P = first ? p1 + el : p2 + (el - NE1);
+        n = el < NE1 + NE2 ? (first ? n1 : n2) : 0;
+        stride = first ? NE1 : NE2;
+    }
     float t = 0.f;
-    if (e < ne)
-        for (int r = rg; r < n; r += 8) t += P[int64_t(r) * ne + e];
+#pragma unroll 4
+    for (int r = rg; r < n; r += 8) t += P[int64_t(r) * stride];
     sm[rg][el] = t;
     __syncthreads();
-    if (rg != 0 || e >= ne) return;
+    if (rg != 0 || n == 0) return;
     t = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) t += sm[i][el];
-    if (first) {
-        if (e < C * BR) o.dw3[e] += *o.scale * t;
-        else if (e == C * BR) *o.db4 += t;
-        else if (e == C * BR + 1) *o.db3b += t;
-        else if (e == C * BR + 2) *o.db3a += t;
-        else *o.dscale += t;
+    if (blk < NBA) {
+        const int kk = e / NER, r = e - kk * NER, co = r / (3 * BR), col = r - co * 3 * BR, kd = col / BR,
+                  ci = col - kd * BR;
+        o.dw2[(co * BR + ci) * 27 + kk * 3 + kd] += t;
+    } else if (blk < NBA + NBB) {
+        if (e < BR * C) {
+            o.dw1[e] += t;  // [o][c]
+        } else {
+            const int r = e - BR * C, oo = r / C, co = r - oo * C;
+            o.dw3[co * BR + oo] += *o.scale * t;  // G3 [o][co] -> W3 [co][o]
+        }
     } else {
-        if (e < NW2) o.dw2[e] += t;
-        else if (e < NW2 + BR * C) o.dw1[e - NW2] += t;
-        else if (e == NW2 + BR * C) *o.db2b += t;
-        else if (e == NW2 + BR * C + 1) *o.db2a += t;
-        else if (e == NW2 + BR * C + 2) *o.db1b += t;
-        else *o.db1a += t;
+        float *const sl[NE1 + NE2] = {o.db4, o.db3b, o.db3a, o.dscale, o.db2b, o.db2a, o.db1b, o.db1a};
+        *sl[e] += t;
     }
 }
 
@@ -843,6 +971,68 @@ int bwd2_blocks(const PmArgs &a) {
     return std::max(1, std::min(a.ntiles, per * n_cu()));
 }
 
+// k_pm_w13grad LDS: z1T, t3T [16][SP] + u1T, gT [32][SP]
+constexpr size_t w13_lds() { return size_t(96 * SP) * 2; }
+
+template <int D>
+void launch_w2(const PmArgs &a, int nwa, int npc, const bf16_t *gz3, const bf16_t *t2, float *p2a, hipStream_t s) {
+    static bool init = false;
+    if (!init) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad<D>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<D>::LDS));
+        init = true;
+    }
+    k_pm_w2grad<D><<<nwa, NT9, W2c<D>::LDS, s>>>(a, int(int64_t(a.B) * a.H * a.W * a.D / CHV), npc, gz3, t2, p2a);
+}
+
+// backward workspace: K1 / K2 scalar partial rows, the W2 partials [nwa][9][NER], the W1 / G3
+// partials [nchb][NEB], then gz3 and gz1 (bf16 [nvox][9] each, 256-B aligned)
+struct MidWs {
+    float *p1, *p2, *p2a, *p2b;
+    bf16_t *gz3, *gz1;
+    int n1, n2, nwa, nchb, npc, npb;
+    size_t bytes;
+};
+constexpr int kW2Chunks = 2;  // 512-voxel chunks per k_pm_w2grad workgroup (when they divide)
+constexpr int kW13Pieces = 4;  // SUBV-voxel pieces per k_pm_w13grad workgroup (when they divide)
+
+MidWs mid_ws(int B, int H, int W, int D, void *base) {
+    MidWs m;
+    const int64_t nvox = int64_t(B) * H * W * D;  // a multiple of 512 (H, W, D % 8 == 0)
+    const PmArgs a = make_args(B, H, W, D, BTH, BTW);
+    m.n2 = bwd2_blocks(a);
+    m.n1 = int(std::min<int64_t>(kBwd1Blocks, nvox / NT));
+    m.npc = kW2Chunks;
+    while ((nvox / CHV) % m.npc) m.npc >>= 1;
+    m.npb = kW13Pieces;
+    while ((nvox / SUBV) % m.npb) m.npb >>= 1;
+    m.nwa = int(nvox / (int64_t(m.npc) * CHV));
+    m.nchb = int(nvox / (int64_t(m.npb) * SUBV));
+    auto al = [](size_t n) { return (n + 255) & ~size_t(255); };
+    size_t off = 0;
+    const size_t o1 = off;
+    off = al(off + size_t(m.n1) * NE1 * 4);
+    const size_t o2 = off;
+    off = al(off + size_t(m.n2) * NE2 * 4);
+    const size_t oa = off;
+    off = al(off + size_t(9) * m.nwa * NER * 4);
+    const size_t ob = off;
+    off = al(off + size_t(m.nchb) * NEB * 4);
+    const size_t oz3 = off;
+    off = al(off + size_t(nvox) * BR * 2);
+    const size_t oz1 = off;
+    off = al(off + size_t(nvox) * BR * 2);
+    m.bytes = off;
+    char *c = static_cast<char *>(base);
+    m.p1 = reinterpret_cast<float *>(c + o1);
+    m.p2 = reinterpret_cast<float *>(c + o2);
+    m.p2a = reinterpret_cast<float *>(c + oa);
+    m.p2b = reinterpret_cast<float *>(c + ob);
+    m.gz3 = reinterpret_cast<bf16_t *>(c + oz3);
+    m.gz1 = reinterpret_cast<bf16_t *>(c + oz1);
+    return m;
+}
+
 }  // namespace
 
 }  // namespace vq3d
@@ -853,8 +1043,9 @@ extern "C" {
 
 int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                               int32_t dd) {
-    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h >= 8 && w >= 8 && dd >= TD &&
-           h % 8 == 0 && w % 8 == 0 && dd % TD == 0 && int64_t(batch) * h * w * dd % NT == 0;
+    // D a power of two in [8, 128]: the weight-gradient chunks are tiles of whole D-lines
+    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h >= 8 && w >= 8 && h % 8 == 0 &&
+           w % 8 == 0 && dd >= TD && dd <= 128 && (dd & (dd - 1)) == 0;
 }
 
 int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
@@ -890,16 +1081,14 @@ int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
 }
 
 size_t vq3d_preact_mid_workspace_bytes(int32_t batch, int32_t h, int32_t w, int32_t dd) {
-    const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
-    const size_t n2 = size_t(bwd2_blocks(a));
-    return (size_t(kBwd1Blocks) * NE1 + n2 * NE2) * 4 + size_t(batch) * h * w * dd * BR * 2 + 256;
+    return mid_ws(batch, h, w, dd, nullptr).bytes;
 }
 
 int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                         int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                         const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                         void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
-    return vq3d_preact_mid_bwd_stages(7, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, p, gr,
+    return vq3d_preact_mid_bwd_stages(31, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, p, gr,
                                       workspace, workspace_bytes, gx, stream);
 }
 
@@ -910,30 +1099,41 @@ int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
                                size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
     if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
         return fail("preact_mid_bwd: shape outside the fused mid-level block kernels");
-    if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx || !workspace)
+    if (stages < 1 || stages > 31) return fail("preact_mid_bwd: stages must be a mask of 1 | 2 | 4 | 8 | 16");
+    if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !workspace)
         return fail("preact_mid_bwd: null pointer");
+    if ((stages & 2) && !gx) return fail("preact_mid_bwd: gx is required by the data stage");
     const vq3d_preact_grads &G = *gr;
     if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||
         !G.dbias3b || !G.dscale || !G.dbias4)
         return fail("preact_mid_bwd: every gradient buffer is required");
-    if (workspace_bytes < vq3d_preact_mid_workspace_bytes(batch, h, w, dd))
-        return fail("preact_mid_bwd: workspace too small");
+    const MidWs m = mid_ws(batch, h, w, dd, workspace);
+    if (workspace_bytes < m.bytes) return fail("preact_mid_bwd: workspace too small");
     hipStream_t s = as_stream(stream);
     const int64_t nvox = int64_t(batch) * h * w * dd;
     const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
-    const int n2 = bwd2_blocks(a);
-    const int n1 = int(std::min<int64_t>(kBwd1Blocks, nvox / NT));
-    float *p1 = static_cast<float *>(workspace);
-    float *p2 = p1 + size_t(kBwd1Blocks) * NE1;
-    bf16_t *gz3 = reinterpret_cast<bf16_t *>(
-        (reinterpret_cast<uintptr_t>(p2 + size_t(n2) * NE2) + 255) & ~uintptr_t(255));
-    if (stages & 1) k_pm_bwd1<<<n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, gz3, p1);
+    if (stages & 1) k_pm_bwd1<<<m.n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, m.gz3, m.p1);
     if (stages & 2)
-        k_pm_bwd2<BTH, BTW><<<n2, NT, bwd_lds<BTH, BTW>(), s>>>(a, gz3, (const bf16_t *)t2, (const bf16_t *)x,
-                                                             (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, p2);
+        k_pm_bwd2<BTH, BTW><<<m.n2, NT, bwd_lds<BTH, BTW>(), s>>>(a, m.gz3, (const bf16_t *)t2, (const bf16_t *)x,
+                                                               (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, m.gz1,
+                                                               m.p2);
+    if (stages & 4) {
+        const bf16_t *t2b = static_cast<const bf16_t *>(t2);
+        switch (dd) {
+            case 8: launch_w2<8>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
+            case 16: launch_w2<16>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
+            case 32: launch_w2<32>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
+            case 64: launch_w2<64>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
+            default: launch_w2<128>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
+        }
+    }
+    if (stages & 8) {
+        k_pm_w13grad<<<m.nchb, NT, w13_lds(), s>>>(m.npb, m.gz1, (const bf16_t *)t3, (const bf16_t *)x,
+                                                   (const bf16_t *)g, *p, m.p2b);
+    }
     RedOut o{G.dw1, G.dw2, G.dw3, G.dbias1a, G.dbias1b, G.dbias2a, G.dbias2b, G.dbias3a, G.dbias3b,
              G.dscale, G.dbias4, p->scale};
-    if (stages & 4) k_pm_reduce<<<NB1 + NB2, NT, 0, s>>>(p1, n1, p2, n2, o);
+    if (stages & 16) k_pm_reduce<<<NBA + NBB + 1, NT, 0, s>>>(m.p1, m.n1, m.p2, m.n2, m.p2a, m.nwa, m.p2b, m.nchb, o);
     return check_launch("preact_mid_bwd");
 }
 

@@ -333,12 +333,22 @@ def preact_mid_bwd(g, x, t2, t3, blk, grads, stages=None, bufs=None):
     prm = _preact_params(blk)
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
     args = (L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(w1), L.ptr(w2),
-            L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx),
-            L.stream())
-    if stages is None:
-        L.call("vq3d_preact_mid_bwd", *args)
+            L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx))
+    if stages is not None:
+        L.call("vq3d_preact_mid_bwd_stages", int(stages), *args, L.stream())
+    elif _concurrent:
+        # data stages (gz3, gx; gz1 to the workspace) on the main stream, the weight gradient and
+        # the fixed-order reduction on the side stream (they read g / x / t2 / t3 / workspace only)
+        L.call("vq3d_preact_mid_bwd_stages", 3, *args, L.stream())
+        main = torch.cuda.current_stream()
+        side = _side_stream(x.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            L.call("vq3d_preact_mid_bwd_stages", 28, *args, L.stream())
+        for t in (g, x, t2, t3, ws):
+            t.record_stream(side)
     else:
-        L.call("vq3d_preact_mid_bwd_stages", int(stages), *args)
+        L.call("vq3d_preact_mid_bwd", *args, L.stream())
     return gx
 
 

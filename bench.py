@@ -119,10 +119,16 @@ def probe_mid(dev, kind):
     if kind == "k_pm_t2":
         return (lambda: ops.preact_mid_fwd(x, blk, stages=1, bufs=(out, t2, t3)), nv * 27 * 2 + wb, fl_pw,
                 "k_pm_t2: fused 18-ch block t2 (1x1 18->9 + elu) @128x128x32 bf16")
-    if kind == "k_pm_bwd2":  # reads gz3 9 + t2 9 + x 18 + g 18, writes gx 18
-        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=2, bufs=(gx, ws)), nv * 72 * 2 + wb,
-                2 * fl_k3 + 2 * fl_pw,
-                "k_pm_bwd2: fused 18-ch block backward tile (dgrad 3x3x3 + W2 grad + 1x1 dgrad + W1 grad) @128x128x32")
+    if kind == "k_pm_bwd2":  # reads gz3 9 + t2 9 + x 18 + g 18, writes gx 18 + gz1 9
+        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=2, bufs=(gx, ws)), nv * 81 * 2 + wb,
+                fl_k3 + fl_pw,
+                "k_pm_bwd2: fused 18-ch block backward data tile (dgrad 3x3x3 + 1x1 dgrad) @128x128x32")
+    if kind == "k_pm_w2grad":  # reads gz3 9 + t2 9 (halo re-reads are L2 traffic), writes partials
+        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=4, bufs=(gx, ws)), nv * 18 * 2 + wb,
+                fl_k3, "k_pm_w2grad: fused 18-ch block 3x3x3 9->9 weight gradient @128x128x32")
+    if kind == "k_pm_w13grad":  # reads gz1 9 + t3 9 + x 18 + g 18
+        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=8, bufs=(gx, ws)), nv * 54 * 2 + wb,
+                2 * fl_pw, "k_pm_w13grad: fused 18-ch block 1x1 weight gradients (W1, W3) @128x128x32")
     if kind == "k_pm_bwd1":  # reads g 18 + t3 9, writes gz3 9
         return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=1, bufs=(gx, ws)), nv * 36 * 2 + wb,
                 2 * fl_pw, "k_pm_bwd1: fused 18-ch block backward pointwise (gz3 + W3 grad) @128x128x32")
@@ -177,7 +183,7 @@ def probe_stack(dev, kind):
 
 
 PROBES = {
-    "k_pm_bwd2": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
+    "k_pm_bwd2": probe_mid, "k_pm_w2grad": probe_mid, "k_pm_w13grad": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
     "k_stackm_bwd": probe_stack, "k_stackm_fwd": probe_stack,
 }
 

@@ -156,7 +156,7 @@ int vq3d_preact_tiny_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t
  * layers.py:176-195 and their autograd backward for these blocks.
  * Forward (two launches): writes out and the intermediates t2 = elu(W1 u1 + bias2a) + bias2b and
  * t3 = elu(W2 (*) t2 + bias3a) + bias3b ([B][H][W][D][branch] bf16).
- * Backward (three launches): writes gx and accumulates (+=) every parameter gradient of *gr (all
+ * Backward (four launches): writes gx and accumulates (+=) every parameter gradient of *gr (all
  * required), deterministically (fixed-order workgroup partials), through a caller-owned
  * workspace of vq3d_preact_mid_workspace_bytes. */
 int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
@@ -169,9 +169,12 @@ int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                         const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                         void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream);
-/* Measurement entries (bench.py's roofline probe, tools/block_micro.py): the same calls, launching
- * only the kernels selected by `stages` (forward: bit 0 t2, bit 1 tile kernel; backward: bit 0
- * pointwise gz3 kernel, bit 1 tile kernel, bit 2 reduction).  The product path uses the calls above. */
+/* Staged entries: the same calls, launching only the kernels selected by `stages` (forward: bit 0
+ * t2, bit 1 tile kernel; backward: bit 0 pointwise gz3 kernel, bit 1 data tile kernel (gx), bit 2
+ * W2-gradient kernel, bit 3 W1 / W3-gradient kernel, bit 4 reduction).  Backward stages 4 | 8 | 16 read only g / x / t2 / t3 and
+ * the workspace that stages 1 | 2 wrote, so a caller may issue them on a second stream ordered
+ * after the first (the product's concurrent weight-gradient mode does); bench.py's roofline
+ * probe and tools/block_micro.py time single stages. */
 int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
                                int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
                                const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,

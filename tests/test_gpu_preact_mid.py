@@ -165,3 +165,23 @@ def test_fused_mid_block_deterministic(gpu):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     for n in a[2]:
         assert torch.equal(a[2][n], b[2][n]), n
+
+
+@pytest.mark.parametrize("shape", [(2, 18, 16, 8, 16), (1, 18, 128, 128, 32)])
+def test_fused_mid_block_side_stream(gpu, shape):
+    """Weight-gradient stages on the side stream (the product's concurrent mode) give the same
+    bits as the single-stream backward."""
+    from vq3d import ops
+    blk = _block(seed=9)
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(shape, generator=g).bfloat16().double()
+    gy = torch.randn(shape, generator=g).bfloat16().double()
+    a = _run(blk, x, gy, gpu, mid=True)
+    ops.set_concurrent_wgrad(True)
+    try:
+        b = _run(blk, x, gy, gpu, mid=True)
+    finally:
+        ops.set_concurrent_wgrad(False)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n

@@ -84,7 +84,7 @@ def main():
         ops.preact_mid_bwd(g, x, t2, t3, blk, grads, bufs=(gx, ws))
         per = {f"fwd{k}": timed(lambda k=k: ops.preact_mid_fwd(x, blk, stages=k, bufs=bufs), iters) for k in (1, 2)}
         per.update({f"bwd{k}": timed(lambda k=k: ops.preact_mid_bwd(g, x, t2, t3, blk, grads, stages=k,
-                                                                      bufs=(gx, ws)), iters) for k in (1, 2, 4)})
+                                                                      bufs=(gx, ws)), iters) for k in (1, 2, 4, 8, 16)})
         print("per kernel us:", {k: round(v, 1) for k, v in per.items()})
     tf = timed(fwd, iters)
     tb = timed(bwd, iters)
