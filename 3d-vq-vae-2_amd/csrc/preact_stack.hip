@@ -457,6 +457,7 @@ __device__ __forceinline__ bf16x8 rd8f(const float *p) {
 
 struct Mk {
     float *xs, *gs, *part, *w;   // fp32: residual / gradient stream, conv partials [2][nv][16], weights
+    bf16_t *fr;                  // the block's weights as packed bf16 MFMA B fragments (FR_* below)
     bf16_t *u1, *t2, *t3, *z3, *z1;
     short *nb;
     float *red;
@@ -464,6 +465,44 @@ struct Mk {
 
 // weight image (fp32): w1 [o][c] at 0, w3 [co][o] at 512, w2 [co][ci][tap] at 1024 (torch order)
 constexpr int W1O = 0, W3O = MB * MC, W2O = 2 * MB * MC, WN = W2O + MB * MB * 27;
+
+// Packed B-fragment images (bf16, [k-step / n-tile][lane = kb * 16 + n][8]; one 16-B LDS read per
+// lane, no strided fp32 gathers -- those were bank-conflict bound).  Forward: FA = W1 (t2:
+// k = c, n = o), FB = W2 (14 tap-pair k-steps: k = (tap, ci), n = co), FC = W3 (2 n-tiles: k = o
+// (+ zero half), n = co).  Backward: FA = W3 (gz3: k = co, n = o), FB = W2 transposed (k = (tap,
+// co), n = ci), FC = W1 (gx, 2 n-tiles: k = o (+ zero half), n = c).  Slots past tap 26 and the
+// zero k-halves are cleared once per kernel.
+constexpr int FRT = 512, FR_A = 0, FR_B = FRT, FR_C = 15 * FRT, FR_N = 17 * FRT;
+__device__ __forceinline__ int frpos(int ktile, int kb, int n, int j) { return ktile * FRT + ((kb * 16 + n) << 3) + j; }
+
+// weight element (torch-order image index i, value v) -> its fragment slots
+template <bool BWD>
+__device__ __forceinline__ void frag_store(bf16_t *fr, int i, float v) {
+    const bf16_t b = f2bf(v);
+    if (i < W3O) {  // W1 [o][c]
+        const int o = i / MC, c = i - o * MC;
+        if (!BWD) fr[FR_A + frpos(0, c >> 3, o, c & 7)] = b;
+        else fr[FR_C + frpos(c >> 4, o >> 3, c & 15, o & 7)] = b;
+    } else if (i < W2O) {  // W3 [co][o]
+        const int e = i - W3O, co = e / MB, o = e - co * MB;
+        if (!BWD) fr[FR_C + frpos(co >> 4, o >> 3, co & 15, o & 7)] = b;
+        else fr[FR_A + frpos(0, co >> 3, o, co & 7)] = b;
+    } else {  // W2 [co][ci][tap]
+        const int e = i - W2O, tap = e % 27, r = e / 27, ci = r % MB, co = r / MB;
+        const int kc = BWD ? co : ci, n = BWD ? ci : co;
+        fr[FR_B + frpos(tap >> 1, 2 * (tap & 1) + (kc >> 3), n, kc & 7)] = b;
+    }
+}
+__device__ __forceinline__ void frag_zero(bf16_t *fr) {
+    // tap 27 (k-step 13, kb 2 / 3) and the k-halves o >= 16 of the two FC tiles (kb 2 / 3)
+    for (int i = threadIdx.x; i < 3 * 32 * 8; i += NT) {
+        const int t = i / 256, r = i - t * 256, lane = 32 + (r >> 3), j = r & 7;
+        fr[(t == 0 ? FR_B + 13 * FRT : FR_C + (t - 1) * FRT) + lane * 8 + j] = 0;
+    }
+}
+__device__ __forceinline__ bf16x8 frag(const bf16_t *fr, int ktile, int lane) {
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(fr + ktile * FRT + lane * 8));
+}
 
 __device__ __forceinline__ Mk carve_m(int nv, char *smem) {
     Mk m;
@@ -479,6 +518,8 @@ __device__ __forceinline__ Mk carve_m(int nv, char *smem) {
     m.red = p;
     p += 16 * 8;
     bf16_t *q = reinterpret_cast<bf16_t *>(p);
+    m.fr = q;
+    q += FR_N;
     m.u1 = q;
     q += nv * PU;
     m.t2 = q;
@@ -493,27 +534,55 @@ __device__ __forceinline__ Mk carve_m(int nv, char *smem) {
     return m;
 }
 size_t lds_m(int nv) {
-    return size_t(WN + 2 * nv * PF + 2 * nv * MB + 16 * 8) * 4 + size_t(nv * PU + 4 * (nv * PT + 32)) * 2 +
+    return size_t(WN + 2 * nv * PF + 2 * nv * MB + 16 * 8) * 4 + size_t(FR_N + nv * PU + 4 * (nv * PT + 32)) * 2 +
            size_t(nv) * 27 * 2;
 }
 
 struct WReg {  // register prefetch of one block's weights (fp32, torch order)
     float v[(WN + NT - 1) / NT];
-    __device__ __forceinline__ void load(const float *const *t) {
+    __device__ __forceinline__ void load(const float *w1, const float *w2, const float *w3) {
 #pragma unroll
         for (int u = 0; u < (WN + NT - 1) / NT; ++u) {
             const int i = min(int(threadIdx.x) + u * NT, WN - 1);
-            v[u] = i < W3O ? t[0][i] : (i < W2O ? t[2][i - W3O] : t[1][i - W2O]);
+            v[u] = i < W3O ? w1[i] : (i < W2O ? w3[i - W3O] : w2[i - W2O]);
         }
     }
-    __device__ __forceinline__ void store(float *w) const {
+    template <bool BWD>
+    __device__ __forceinline__ void store(float *w, bf16_t *fr) const {
 #pragma unroll
         for (int u = 0; u < (WN + NT - 1) / NT; ++u) {
             const int i = threadIdx.x + u * NT;
-            if (i < WN) w[i] = v[u];
+            if (i < WN) {
+                w[i] = v[u];
+                frag_store<BWD>(fr, i, v[u]);
+            }
         }
     }
 };
+
+// A block's parameter-table row, lane-distributed in VECTOR registers: lane k (< NPRM) holds
+// the row's k-th pointer, and after deref() lanes 3 .. 10 hold the scalar values.  Rows are
+// fetched one block ahead, so the waits ride vmcnt a whole block after the issue (scalar loads
+// would share lgkmcnt with every LDS access and stall at the next LDS wait).
+__device__ __forceinline__ const float *row_ptr(const float *const *tab, int j, int lane) {
+    return tab[j * NPRM + min(lane, NPRM - 1)];
+}
+__device__ __forceinline__ float *row_ptr(float *const *tab, int j, int lane) {
+    return tab[j * NPRM + min(lane, NPRM - 1)];
+}
+template <typename P>
+__device__ __forceinline__ P *bcast_ptr(P *p, int k) {
+    const uint64_t u = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(u), k), hi = __builtin_amdgcn_readlane(uint32_t(u >> 32), k);
+    return reinterpret_cast<P *>((uint64_t(hi) << 32) | lo);
+}
+__device__ __forceinline__ float bcastf(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+__device__ __forceinline__ Scal scal_lanes(float v) {
+    return Scal{bcastf(v, 3), bcastf(v, 4), bcastf(v, 5), bcastf(v, 6),
+                bcastf(v, 7), bcastf(v, 8), bcastf(v, 9), bcastf(v, 10)};
+}
 
 // conv2 (t3 from t2) or its transpose (gt2 from gz3): M-tile mt, k-steps of tap pairs
 // [ks0, ks0 + 7); B[k][n] built from the fp32 image: forward n = co, k = (tap, ci); transposed
@@ -522,17 +591,11 @@ template <bool T>
 __device__ __forceinline__ f32x4 conv_half(const Mk &m, const bf16_t *src, int mt, int ks0, int lane) {
     const int row = lane & 15, kb = lane >> 4, v = mt * 16 + row;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
     for (int ks = ks0; ks < ks0 + 7; ++ks) {
         const int tap = 2 * ks + (kb >> 1), c0 = 8 * (kb & 1);
         const bf16x8 af = tap < 27 ? rd8(src + int(m.nb[v * 27 + (T ? 26 - tap : tap)]) * PT + c0) : zero8();
-        float wv[8];
-        const int n = row;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int c = c0 + j;  // contraction channel
-            wv[j] = tap < 27 ? (T ? m.w[W2O + (c * MB + n) * 27 + tap] : m.w[W2O + (n * MB + c) * 27 + tap]) : 0.f;
-        }
-        acc = mfma(af, pack8(wv), acc);
+        acc = mfma(af, frag(m.fr + FR_B, ks, lane), acc);
     }
     return acc;
 }
@@ -547,15 +610,24 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
     for (int i = tid; i < nv * 27; i += NT) m.nb[i] = short(nbr(a, i / 27, i % 27, 1));
     for (int i = tid; i < nvc; i += NT) m.xs[(i / MC) * PF + i % MC] = ld(x + i);
     for (int i = tid; i < 32; i += NT) m.t3[nv * PT + i] = 0;  // zero tail / row pads read by the fragments
+    frag_zero(m.fr);
     for (int i = tid; i < nv * (PT - MB); i += NT) m.t3[(i / (PT - MB)) * PT + MB + i % (PT - MB)] = 0;
     WReg wr;
-    wr.load(tab);
+    const float *pc = row_ptr(tab, 0, lane);
+    float vc = *pc;
+    wr.load(bcast_ptr(pc, 0), bcast_ptr(pc, 1), bcast_ptr(pc, 2));
+    const float *pn = row_ptr(tab, min(1, a.nblk - 1), lane);
     for (int blk = 0; blk < a.nblk; ++blk) {
-        const Scal s = scal_of(tab + blk * NPRM);
+        const Scal s = scal_lanes(vc);
         float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
         __syncthreads();
-        wr.store(m.w);
-        if (blk + 1 < a.nblk) wr.load(tab + (blk + 1) * NPRM);
+        wr.store<false>(m.w, m.fr);
+        // the next block's weights and scalars, and the row after it
+        if (blk + 1 < a.nblk) {
+            wr.load(bcast_ptr(pn, 0), bcast_ptr(pn, 1), bcast_ptr(pn, 2));
+            vc = *pn;
+            pn = row_ptr(tab, min(blk + 2, a.nblk - 1), lane);
+        }
         for (int i = tid; i < nvc; i += NT) {
             const int v = i / MC, c = i - v * MC;
             const float xv = m.xs[v * PF + c];
@@ -565,10 +637,8 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
         __syncthreads();
         // t2: M-tile per wave, K = 32 channels, N = 16
         if (wave < nmt) {
-            float wv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) wv[j] = m.w[W1O + row * MC + 8 * kb + j];
-            const f32x4 acc = mfma(rd8(m.u1 + (wave * 16 + row) * PU + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 acc = mfma(rd8(m.u1 + (wave * 16 + row) * PU + 8 * kb), frag(m.fr + FR_A, 0, lane),
+                                   f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int v = wave * 16 + 4 * kb + j;
@@ -596,13 +666,8 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
         // x += scale * W3 t3 + b4: M-tile x 2 N-tiles per wave, K = 16 (+ zero half)
         if (wave < 2 * nmt) {
             const int mt = wave % nmt, nt = wave / nmt;
-            float wv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int o = 8 * kb + j;
-                wv[j] = o < MB ? m.w[W3O + (16 * nt + row) * MB + o] : 0.f;
-            }
-            const f32x4 acc = mfma(rd8(m.t3 + (mt * 16 + row) * PT + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 acc = mfma(rd8(m.t3 + (mt * 16 + row) * PT + 8 * kb), frag(m.fr + FR_C, nt, lane),
+                                   f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
             for (int j = 0; j < 4; ++j) m.xs[(mt * 16 + 4 * kb + j) * PF + 16 * nt + row] += acc[j] * s.sc + s.b4;
         }
@@ -616,9 +681,10 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                                                    bf16_t *__restrict__ gx) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Mk m = carve_m(a.nv, smem);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int tid0 = threadIdx.x;
     const int nv = a.nv, nmt = nv / 16, nks = nv / 32, nvc = nv * MC, nvb = nv * MB;
     const size_t stride = size_t(nv) * (MC + 2 * MB);
+    const int tid = tid0, lane = tid0 & 63;
     for (int i = tid; i < nv * 27; i += NT) m.nb[i] = short(nbr(a, i / 27, i % 27, 1));
     for (int i = tid; i < nvc; i += NT) m.gs[(i / MC) * PF + i % MC] = ld(g + i);
     for (int i = tid; i < nv * (PT - MB); i += NT) {  // zero row pads / tail read by the gx fragments
@@ -626,35 +692,81 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
         m.z1[v * PT + e] = 0;
     }
     for (int i = tid; i < 32; i += NT) m.z1[nv * PT + i] = 0;
+    frag_zero(m.fr);
+    // prefetched one block ahead (the walk is in reverse): weights, scalars, gradient pointers,
+    // the saved x / t2 / t3; the current block's old gradient values at its top
+    constexpr int SX = MAXVM * MC / NT, SB = MAXVM * MB / NT;
     WReg wr;
-    wr.load(tab + (a.nblk - 1) * NPRM);
-    for (int blk = a.nblk - 1; blk >= 0; --blk) {
-        const Scal s = scal_of(tab + blk * NPRM);
-        float *const *gt = gtab + blk * NPRM;
-        const float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
-        __syncthreads();
-        wr.store(m.w);
-        if (blk > 0) wr.load(tab + (blk - 1) * NPRM);
-        for (int i = tid; i < nvc; i += NT) {
-            const int v = i / MC, c = i - v * MC;
-            const float z = sx[i] + s.b1a;
-            const float e = z > 0.f ? 1.f : expf(z);
-            m.u1[v * PU + c] = f2bf((z > 0.f ? z : e - 1.f) + s.b1b);
-            m.xs[v * PF + c] = e;
+    const int last = a.nblk - 1;
+    const float *pc = row_ptr(tab, last, lane);
+    float vc = *pc;
+    wr.load(bcast_ptr(pc, 0), bcast_ptr(pc, 1), bcast_ptr(pc, 2));
+    const float *pn = row_ptr(tab, max(last - 1, 0), lane);
+    float *gc = row_ptr(gtab, last, lane);
+    float svx[SX], sv2[SB], sv3[SB];
+    auto load_saved = [&](int b) {
+        const float *sx = saved + b * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
+#pragma unroll
+        for (int u = 0; u < SX; ++u) svx[u] = sx[min(tid + u * NT, nvc - 1)];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            sv2[u] = st2[min(tid + u * NT, nvb - 1)];
+            sv3[u] = st3[min(tid + u * NT, nvb - 1)];
         }
-        for (int i = tid; i < nvb; i += NT) {
-            const int v = i / MB, o = i - v * MB;
-            m.t2[v * PT + o] = f2bf(st2[i]);
-            m.t3[v * PT + o] = f2bf(st3[i]);
+    };
+    load_saved(last);
+    for (int blk = last; blk >= 0; --blk) {
+        // the thread / lane indices are re-derived from an opaque copy each block, so the
+        // compiler recomputes the per-phase LDS addresses instead of hoisting ~60 loop-invariant
+        // ones out of the block loop and spilling them
+        int tl = tid0;
+        asm volatile("" : "+v"(tl));
+        const int tid = tl, lane = tl & 63, wave = __builtin_amdgcn_readfirstlane(tl >> 6), row = lane & 15,
+                  kb = lane >> 4;
+        const Scal s = scal_lanes(vc);
+        // this block's gradient pointers (fetched a block ago) and their old values: W3 entries of
+        // waves nmt, nmt + 1, W2 entries of taps wave / wave + 16, W1 entries of waves 0, 1, the
+        // scalars on lanes 3 .. 10 of wave 0 (every load unconditional, clamped indices)
+        float *gw1 = bcast_ptr(gc, 0), *gw2 = bcast_ptr(gc, 1), *gw3 = bcast_ptr(gc, 2);
+        float o3[4], o2[2][4], o1[4];
+        const int ct = min(max(wave - nmt, 0), 1), nt1 = min(wave, 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o3[j] = gw3[(16 * ct + 4 * kb + j) * MB + row];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) o2[q][j] = gw2[((4 * kb + j) * MB + row) * 27 + min(wave + 16 * q, 26)];
+        }
+        const float osc = *gc;
+        float *const gsc = gc;  // lanes 3 .. 10: this block's scalar-gradient pointers
+        if (blk > 0) gc = row_ptr(gtab, blk - 1, lane);
+        __syncthreads();
+        wr.store<true>(m.w, m.fr);
+#pragma unroll
+        for (int u = 0; u < SX; ++u) {
+            const int i = tid + u * NT;
+            if (i < nvc) {
+                const int v = i / MC, c = i - v * MC;
+                const float z = svx[u] + s.b1a;
+                const float e = z > 0.f ? 1.f : expf(z);
+                m.u1[v * PU + c] = f2bf((z > 0.f ? z : e - 1.f) + s.b1b);
+                m.xs[v * PF + c] = e;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int i = tid + u * NT;
+            if (i < nvb) {
+                const int v = i / MB, o = i - v * MB;
+                m.t2[v * PT + o] = f2bf(sv2[u]);
+                m.t3[v * PT + o] = f2bf(sv3[u]);
+            }
         }
         __syncthreads();
         float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // b4, scale, b3b, b3a, b2b, b2a, b1b, b1a
         if (wave < nmt) {
             // gz3 = scale W3^T g * elu'(t3 - b3b): K = 32 channels of g, N = 16
-            float wv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) wv[j] = m.w[W3O + (8 * kb + j) * MB + row];
-            const f32x4 acc = mfma(rd8f(m.gs + (wave * 16 + row) * PF + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 acc = mfma(rd8f(m.gs + (wave * 16 + row) * PF + 8 * kb), frag(m.fr + FR_A, 0, lane),
+                                   f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int v = wave * 16 + 4 * kb + j;
@@ -675,7 +787,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int co = 16 * ct + 4 * kb + j;
-                gt[2][co * MB + row] += s.sc * acc[j];
+                gw3[co * MB + row] = o3[j] + s.sc * acc[j];
                 ps[1] = fmaf(m.w[W3O + co * MB + row], acc[j], ps[1]);
             }
         }
@@ -688,8 +800,12 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
 #pragma unroll
             for (int j = 0; j < 4; ++j) m.part[(half * nv + mt * 16 + 4 * kb + j) * MB + row] = acc[j];
         }
-        for (int tap = wave; tap < 27; tap += NT / 64) {  // M = co, N = ci, K = voxels
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // M = co, N = ci, K = voxels: taps wave, wave + 16
+            const int tap = wave + 16 * q;
+            if (tap >= 27) continue;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
             for (int ks = 0; ks < nks; ++ks) {
                 const int v0 = ks * 32 + 8 * kb;
                 uint32_t w[4];
@@ -703,9 +819,19 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                            acc);
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) gt[1][((4 * kb + j) * MB + row) * 27 + tap] += acc[j];
+            for (int j = 0; j < 4; ++j) gw2[((4 * kb + j) * MB + row) * 27 + tap] = o2[q][j] + acc[j];
         }
         __syncthreads();
+        // the next block's weights / scalars / saved tensors and this block's old W1 gradient
+        // (issued here, after the register-heavy k^3 phases)
+        if (blk > 0) {
+            wr.load(bcast_ptr(pn, 0), bcast_ptr(pn, 1), bcast_ptr(pn, 2));
+            vc = *pn;
+            pn = row_ptr(tab, max(blk - 2, 0), lane);
+            load_saved(blk - 1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o1[j] = gw1[(4 * kb + j) * MC + 16 * nt1 + row];
         for (int i = tid; i < nvb; i += NT) {
             const int v = i / MB, o = i - v * MB;
             const float g2 = m.part[i] + m.part[nvb + i];
@@ -718,13 +844,8 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
         if (wave < 2 * nmt) {
             // gx = g + (W1^T gz1) * elu'(x + b1a): M-tile x 2 N-tiles (channels), K = 16 (+ zero half)
             const int mt = wave % nmt, nt = wave / nmt;
-            float wv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int o = 8 * kb + j;
-                wv[j] = o < MB ? m.w[W1O + o * MC + 16 * nt + row] : 0.f;
-            }
-            const f32x4 acc = mfma(rd8(m.z1 + (mt * 16 + row) * PT + 8 * kb), pack8(wv), f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 acc = mfma(rd8(m.z1 + (mt * 16 + row) * PT + 8 * kb), frag(m.fr + FR_C, nt, lane),
+                                   f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int i = (mt * 16 + 4 * kb + j) * PF + 16 * nt + row;
@@ -743,18 +864,14 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 acc = mfma(gat8(m.z1 + v0 * PT + row, PT), gat8(m.u1 + v0 * PU + 16 * nt + row, PU), acc);
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) gt[0][(4 * kb + j) * MC + 16 * nt + row] += acc[j];
+            for (int j = 0; j < 4; ++j) gw1[(4 * kb + j) * MC + 16 * nt + row] = o1[j] + acc[j];
         }
         sum8(ps, m.red);
-        if (tid == 0) {
-            *gt[10] += ps[0];
-            *gt[9] += ps[1];
-            *gt[8] += ps[2];
-            *gt[7] += ps[3];
-            *gt[6] += ps[4];
-            *gt[5] += ps[5];
-            *gt[4] += ps[6];
-            *gt[3] += ps[7];
+        if (wave == 0 && lane >= 3 && lane < NPRM) {  // table slot k gets ps[10 - k]
+            float add = ps[0];
+#pragma unroll
+            for (int k = 3; k < NPRM - 1; ++k) add = lane == k ? ps[10 - k] : add;
+            *gsc = osc + add;
         }
     }
     __syncthreads();
