@@ -18,6 +18,10 @@ class LightningModule(nn.Module):
     def log_dict(self, *args, **kwargs):
         pass
 
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
 
 class LightningDataModule:
     pass

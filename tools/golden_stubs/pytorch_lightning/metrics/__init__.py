@@ -1,0 +1,20 @@
+"""Arithmetic-free stand-ins for pytorch_lightning.metrics classes the reference's
+pixel_model/pixelsnail.py constructs (validation-only; never called by the fixtures)."""
+from torch import nn
+
+
+class _Metric(nn.Module):
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("validation metrics are unavailable offline")
+
+
+class Accuracy(_Metric):
+    pass
+
+
+class Precision(_Metric):
+    pass
+
+
+class Recall(_Metric):
+    pass
