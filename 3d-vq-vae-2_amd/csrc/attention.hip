@@ -1,0 +1,339 @@
+// Dense causal attention of the PixelSNAIL prior (pixel_model/layers.py:613-647,
+// pixel_model/pixelsnail.py:295-298): for every (problem = stack x batch, head)
+//
+//   out[i] = sum_{j <= i} softmax_j(scale * q_i . k_j) v_j        (i, j over the n code positions)
+//
+// without ever forming the n x n logits (the reference materialises them, with the tril mask,
+// per block: 3 x 8 x 8192^2 fp32 at the published mid level).  Head dims are tiny (model-dim
+// 256 / bottleneck 4 / 8 heads = 8), so the contraction is per-thread VALU work: a thread owns
+// one query row (fwd, dQ) or one key row (dK / dV) with its q / k / v / dO rows in registers;
+// the opposite side streams through LDS in 256-row tiles that every lane reads as broadcasts.
+// Causality bounds the tile loops (query tile t meets key tiles 0 .. t), the diagonal tile masks
+// per lane.  The online softmax runs in base 2 on chunks of 8 scores (one rescale per chunk);
+// the forward saves the per-row log-sum-exp (base 2) for the backward, which recomputes the
+// probabilities (flash-attention style, fp32 arithmetic throughout, bf16 or fp32 storage).
+//
+// Layout: q, k [P][n][nh * dk], v, out [P][n][nh * dv] -- channels-last rows with head-major
+// channels (head h owns channels h * d .. h * d + d - 1, the reference's reshape(..., nh, d, n)).
+#include "engines.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace vq3d {
+
+namespace {
+
+constexpr int NT = 256;  // threads per workgroup = rows per tile
+constexpr int CH = 8;    // scores per online-softmax chunk
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AttnArgs {
+    int P, n, nh, dk, dv;
+    float c2;  // scale * log2(e)
+};
+
+template <typename T, int DM>
+__device__ __forceinline__ void load_row(const T *__restrict__ src, int64_t base, int d, bool ok, float (&r)[DM]) {
+#pragma unroll
+    for (int c = 0; c < DM; ++c) r[c] = (ok && c < d) ? ld(src + base + c) : 0.f;
+}
+
+template <typename T, int DM>
+__device__ __forceinline__ void store_row(T *__restrict__ dst, int64_t base, int d, const float (&r)[DM]) {
+#pragma unroll
+    for (int c = 0; c < DM; ++c)
+        if (c < d) st(dst + base + c, r[c]);
+}
+
+// rows [r0, r0 + NT) of a [P][n][nh * d] tensor's head h into LDS [NT][DM] fp32 (zero past n / d)
+template <typename T, int DM>
+__device__ __forceinline__ void stage(float *dst, const T *__restrict__ src, const AttnArgs &a, int p, int h, int d,
+                                      int r0) {
+    const int r = r0 + int(threadIdx.x);
+    float v[DM];
+    load_row<T, DM>(src, (int64_t(p) * a.n + min(r, a.n - 1)) * (a.nh * d) + h * d, d, r < a.n, v);
+#pragma unroll
+    for (int c = 0; c < DM; c += 4)
+        *reinterpret_cast<float4 *>(dst + threadIdx.x * DM + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+}
+
+template <int DM>
+__device__ __forceinline__ float dot(const float (&a)[DM], const float *b) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < DM; c += 4) {
+        const float4 q = *reinterpret_cast<const float4 *>(b + c);
+        s = fmaf(a[c], q.x, s);
+        s = fmaf(a[c + 1], q.y, s);
+        s = fmaf(a[c + 2], q.z, s);
+        s = fmaf(a[c + 3], q.w, s);
+    }
+    return s;
+}
+
+template <int DM>
+__device__ __forceinline__ void axpy(float (&y)[DM], float a, const float *x) {
+#pragma unroll
+    for (int c = 0; c < DM; c += 4) {
+        const float4 q = *reinterpret_cast<const float4 *>(x + c);
+        y[c] = fmaf(a, q.x, y[c]);
+        y[c + 1] = fmaf(a, q.y, y[c + 1]);
+        y[c + 2] = fmaf(a, q.z, y[c + 2]);
+        y[c + 3] = fmaf(a, q.w, y[c + 3]);
+    }
+}
+
+// grid: (query tiles, P * nh), heaviest (last) query tiles first
+template <typename T, int DM>
+__global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict__ q, const T *__restrict__ k,
+                                                 const T *__restrict__ v, T *__restrict__ out,
+                                                 float *__restrict__ lse) {
+    __shared__ __attribute__((aligned(16))) float ks[NT * DM], vs[NT * DM];
+    const int nqt = (a.n + NT - 1) / NT, qt = nqt - 1 - int(blockIdx.x);
+    const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
+    const int i = qt * NT + int(threadIdx.x);
+    float qr[DM], o[DM];
+    load_row<T, DM>(q, (int64_t(p) * a.n + min(i, a.n - 1)) * (a.nh * a.dk) + h * a.dk, a.dk, i < a.n, qr);
+#pragma unroll
+    for (int c = 0; c < DM; ++c) {
+        qr[c] *= a.c2;
+        o[c] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int kt = 0; kt <= qt; ++kt) {
+        __syncthreads();
+        stage<T, DM>(ks, k, a, p, h, a.dk, kt * NT);
+        stage<T, DM>(vs, v, a, p, h, a.dv, kt * NT);
+        __syncthreads();
+        const int jmax = kt < qt ? NT : min(NT, i - kt * NT + 1);  // keys j <= i of this tile
+        const int jend = kt < qt ? NT : NT;                          // uniform trip count
+#pragma unroll 1
+        for (int j0 = 0; j0 < jend; j0 += CH) {
+            float s[CH], cm = m;
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                s[u] = j0 + u < jmax ? dot<DM>(qr, ks + (j0 + u) * DM) : -INFINITY;
+                cm = fmaxf(cm, s[u]);
+            }
+            const float alpha = exp2f(m - cm);  // m = -inf on the first chunk: 0
+            l *= alpha;
+#pragma unroll
+            for (int c = 0; c < DM; ++c) o[c] *= alpha;
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const float pr = exp2f(s[u] - cm);
+                l += pr;
+                axpy<DM>(o, pr, vs + (j0 + u) * DM);
+            }
+            m = cm;
+        }
+    }
+    if (i < a.n) {
+        const float inv = 1.f / l;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) o[c] *= inv;
+        store_row<T, DM>(out, (int64_t(p) * a.n + i) * (a.nh * a.dv) + h * a.dv, a.dv, o);
+        lse[(int64_t(p) * a.nh + h) * a.n + i] = m + log2f(l);
+    }
+}
+
+// backward, query side: delta_i = dO_i . O_i (to the workspace) and dQ_i = scale sum_j ds_ij k_j,
+// ds_ij = p_ij (dO_i . v_j - delta_i)
+template <typename T, int DM>
+__global__ __launch_bounds__(NT) void k_attn_bwd_q(AttnArgs a, float scale, const T *__restrict__ q,
+                                                   const T *__restrict__ k, const T *__restrict__ v,
+                                                   const T *__restrict__ out, const T *__restrict__ gout,
+                                                   const float *__restrict__ lse, float *__restrict__ delta,
+                                                   T *__restrict__ gq) {
+    __shared__ __attribute__((aligned(16))) float ks[NT * DM], vs[NT * DM];
+    const int nqt = (a.n + NT - 1) / NT, qt = nqt - 1 - int(blockIdx.x);
+    const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
+    const int i = qt * NT + int(threadIdx.x);
+    const bool ok = i < a.n;
+    const int ic = min(i, a.n - 1);
+    float qr[DM], go[DM], orow[DM], dq[DM];
+    load_row<T, DM>(q, (int64_t(p) * a.n + ic) * (a.nh * a.dk) + h * a.dk, a.dk, ok, qr);
+    load_row<T, DM>(gout, (int64_t(p) * a.n + ic) * (a.nh * a.dv) + h * a.dv, a.dv, ok, go);
+    load_row<T, DM>(out, (int64_t(p) * a.n + ic) * (a.nh * a.dv) + h * a.dv, a.dv, ok, orow);
+    float dl = 0.f;
+#pragma unroll
+    for (int c = 0; c < DM; ++c) {
+        dl = fmaf(go[c], orow[c], dl);
+        qr[c] *= a.c2;
+        dq[c] = 0.f;
+    }
+    const int64_t row = (int64_t(p) * a.nh + h) * a.n + ic;
+    const float lz = ok ? lse[row] : 0.f;
+    if (ok) delta[row] = dl;
+    for (int kt = 0; kt <= qt; ++kt) {
+        __syncthreads();
+        stage<T, DM>(ks, k, a, p, h, a.dk, kt * NT);
+        stage<T, DM>(vs, v, a, p, h, a.dv, kt * NT);
+        __syncthreads();
+        const int jmax = kt < qt ? NT : min(NT, i - kt * NT + 1);
+#pragma unroll 4
+        for (int j = 0; j < NT; ++j) {
+            if (j < jmax) {
+                const float pr = exp2f(dot<DM>(qr, ks + j * DM) - lz);
+                const float ds = pr * (dot<DM>(go, vs + j * DM) - dl);
+                axpy<DM>(dq, ds, ks + j * DM);
+            }
+        }
+    }
+    if (ok) {
+#pragma unroll
+        for (int c = 0; c < DM; ++c) dq[c] *= scale;
+        store_row<T, DM>(gq, (int64_t(p) * a.n + i) * (a.nh * a.dk) + h * a.dk, a.dk, dq);
+    }
+}
+
+// backward, key side: dV_j = sum_{i >= j} p_ij dO_i, dK_j = scale sum_{i >= j} ds_ij q_i
+template <typename T, int DM>
+__global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, const T *__restrict__ q,
+                                                    const T *__restrict__ k, const T *__restrict__ v,
+                                                    const T *__restrict__ gout, const float *__restrict__ lse,
+                                                    const float *__restrict__ delta, T *__restrict__ gk,
+                                                    T *__restrict__ gv) {
+    __shared__ __attribute__((aligned(16))) float qs[NT * DM], gs[NT * DM];
+    __shared__ float ls[NT], dls[NT];
+    const int nkt = (a.n + NT - 1) / NT, kt = int(blockIdx.x);  // the lightest tiles last
+    const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
+    const int j = kt * NT + int(threadIdx.x);
+    const bool ok = j < a.n;
+    const int jc = min(j, a.n - 1);
+    float kr[DM], vr[DM], dk[DM], dv[DM];
+    load_row<T, DM>(k, (int64_t(p) * a.n + jc) * (a.nh * a.dk) + h * a.dk, a.dk, ok, kr);
+    load_row<T, DM>(v, (int64_t(p) * a.n + jc) * (a.nh * a.dv) + h * a.dv, a.dv, ok, vr);
+#pragma unroll
+    for (int c = 0; c < DM; ++c) {
+        kr[c] *= a.c2;
+        dk[c] = dv[c] = 0.f;
+    }
+    const int64_t rb = (int64_t(p) * a.nh + h) * a.n;
+    for (int qt = kt; qt < nkt; ++qt) {
+        __syncthreads();
+        stage<T, DM>(qs, q, a, p, h, a.dk, qt * NT);
+        stage<T, DM>(gs, gout, a, p, h, a.dv, qt * NT);
+        {
+            const int r = qt * NT + int(threadIdx.x);
+            ls[threadIdx.x] = r < a.n ? lse[rb + r] : 0.f;
+            dls[threadIdx.x] = r < a.n ? delta[rb + r] : 0.f;
+        }
+        __syncthreads();
+        const int i0 = qt > kt ? 0 : int(threadIdx.x);           // queries i >= j of this tile
+        const int iend = min(NT, a.n - qt * NT);
+#pragma unroll 4
+        for (int ii = 0; ii < NT; ++ii) {
+            if (ii >= i0 && ii < iend) {
+                const float pr = exp2f(dot<DM>(kr, qs + ii * DM) - ls[ii]);
+                axpy<DM>(dv, pr, gs + ii * DM);
+                const float ds = pr * (dot<DM>(vr, gs + ii * DM) - dls[ii]);
+                axpy<DM>(dk, ds, qs + ii * DM);
+            }
+        }
+    }
+    if (ok) {
+#pragma unroll
+        for (int c = 0; c < DM; ++c) dk[c] *= scale;
+        store_row<T, DM>(gk, (int64_t(p) * a.n + j) * (a.nh * a.dk) + h * a.dk, a.dk, dk);
+        store_row<T, DM>(gv, (int64_t(p) * a.n + j) * (a.nh * a.dv) + h * a.dv, a.dv, dv);
+    }
+}
+
+int dmax_of(int dk, int dv) {
+    const int d = std::max(dk, dv);
+    return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 0;
+}
+
+template <typename T, int DM>
+void launch_fwd(const AttnArgs &a, const void *q, const void *k, const void *v, void *out, float *lse,
+                hipStream_t s) {
+    const dim3 grid((a.n + NT - 1) / NT, a.P * a.nh);
+    k_attn_fwd<T, DM><<<grid, NT, 0, s>>>(a, (const T *)q, (const T *)k, (const T *)v, (T *)out, lse);
+}
+
+template <typename T, int DM>
+void launch_bwd(const AttnArgs &a, float scale, const void *q, const void *k, const void *v, const void *out,
+                const void *gout, const float *lse, float *delta, void *gq, void *gk, void *gv, hipStream_t s) {
+    const dim3 grid((a.n + NT - 1) / NT, a.P * a.nh);
+    k_attn_bwd_q<T, DM><<<grid, NT, 0, s>>>(a, scale, (const T *)q, (const T *)k, (const T *)v, (const T *)out,
+                                            (const T *)gout, lse, delta, (T *)gq);
+    k_attn_bwd_kv<T, DM><<<grid, NT, 0, s>>>(a, scale, (const T *)q, (const T *)k, (const T *)v, (const T *)gout,
+                                             lse, delta, (T *)gk, (T *)gv);
+}
+
+int check_args(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, AttnArgs &a,
+               float scale) {
+    if (dtype != VQ3D_BF16 && dtype != VQ3D_F32) return 1;
+    if (nprob < 1 || n < 1 || nh < 1 || dk < 1 || dv < 1 || !dmax_of(dk, dv)) return 1;
+    if (int64_t(nprob) * nh > 65535) return 1;
+    a.P = nprob;
+    a.n = n;
+    a.nh = nh;
+    a.dk = dk;
+    a.dv = dv;
+    a.c2 = scale * LOG2E;
+    return 0;
+}
+
+}  // namespace
+
+}  // namespace vq3d
+
+using namespace vq3d;
+
+extern "C" {
+
+int vq3d_causal_attn_supported(int32_t nh, int32_t dk, int32_t dv) {
+    return nh >= 1 && dk >= 1 && dv >= 1 && dmax_of(dk, dv) ? 1 : 0;
+}
+
+size_t vq3d_causal_attn_workspace_bytes(int32_t nprob, int32_t n, int32_t nh) {
+    return size_t(nprob) * nh * n * sizeof(float);
+}
+
+int vq3d_causal_attn_fwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                         const void *q, const void *k, const void *v, void *out, float *lse, vq3d_stream_t stream) {
+    AttnArgs a;
+    if (check_args(dtype, nprob, n, nh, dk, dv, a, scale)) return fail("causal_attn_fwd: unsupported shape / dtype");
+    if (!q || !k || !v || !out || !lse) return fail("causal_attn_fwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    const int dm = dmax_of(dk, dv);
+    if (dtype == VQ3D_BF16) {
+        if (dm == 4) launch_fwd<bf16_t, 4>(a, q, k, v, out, lse, s);
+        else if (dm == 8) launch_fwd<bf16_t, 8>(a, q, k, v, out, lse, s);
+        else launch_fwd<bf16_t, 16>(a, q, k, v, out, lse, s);
+    } else {
+        if (dm == 4) launch_fwd<float, 4>(a, q, k, v, out, lse, s);
+        else if (dm == 8) launch_fwd<float, 8>(a, q, k, v, out, lse, s);
+        else launch_fwd<float, 16>(a, q, k, v, out, lse, s);
+    }
+    return check_launch("causal_attn_fwd");
+}
+
+int vq3d_causal_attn_bwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                         const void *q, const void *k, const void *v, const void *out, const void *gout,
+                         const float *lse, void *workspace, size_t workspace_bytes, void *gq, void *gk, void *gv,
+                         vq3d_stream_t stream) {
+    AttnArgs a;
+    if (check_args(dtype, nprob, n, nh, dk, dv, a, scale)) return fail("causal_attn_bwd: unsupported shape / dtype");
+    if (!q || !k || !v || !out || !gout || !lse || !workspace || !gq || !gk || !gv)
+        return fail("causal_attn_bwd: null pointer");
+    if (workspace_bytes < vq3d_causal_attn_workspace_bytes(nprob, n, nh)) return fail("causal_attn_bwd: workspace too small");
+    hipStream_t s = as_stream(stream);
+    float *delta = static_cast<float *>(workspace);
+    const int dm = dmax_of(dk, dv);
+    if (dtype == VQ3D_BF16) {
+        if (dm == 4) launch_bwd<bf16_t, 4>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+        else if (dm == 8) launch_bwd<bf16_t, 8>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+        else launch_bwd<bf16_t, 16>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+    } else {
+        if (dm == 4) launch_bwd<float, 4>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+        else if (dm == 8) launch_bwd<float, 8>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+        else launch_bwd<float, 16>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+    }
+    return check_launch("causal_attn_bwd");
+}
+
+}  // extern "C"

@@ -102,6 +102,10 @@ _SIGS = {
     "vq3d_zero": (c_int, [P, c_size, P]),
     "vq3d_copy": (c_int, [P, P, c_size, P]),
     "vq3d_scale": (c_int, [P, c_float, c_i64, P]),
+    "vq3d_causal_attn_supported": (c_int, [c_int] * 3),
+    "vq3d_causal_attn_workspace_bytes": (c_size, [c_int] * 3),
+    "vq3d_causal_attn_fwd": (c_int, [c_int] * 6 + [c_float] + [P] * 6),
+    "vq3d_causal_attn_bwd": (c_int, [c_int] * 6 + [c_float] + [P] * 7 + [c_size] + [P] * 4),
     "vq3d_elu_bwd_from_output": (c_int, [c_int, P, P, P, c_i64, P]),
     "vq3d_last_error": (ctypes.c_char_p, []),
     "vq3d_version": (ctypes.c_char_p, []),

@@ -1,0 +1,449 @@
+"""PixelSNAIL prior over VQ-VAE codes (reference pixel_model/pixelsnail.py + pixel_model/layers.py),
+module API and state_dict of the reference, GPU path through libvq3d:
+
+* every causal 3-stack conv (CausalConv3dAdd, layers.py:122-222) runs on the hand-written conv
+  engines (conv3d.hip): the (k-1, k, k) depth, (1, k-1, k) height and (1, 1, k//2 [+1]) width
+  kernels are embedded in a zero-padded k^3 kernel whose dead taps are exactly zero, so the
+  causal front padding becomes the engines' symmetric zero padding (k = 3; k = 1 is a pointwise
+  conv); mask 'A' shifts its (pre-activated) input by one position first.  The PreAct
+  pre-activations elu(x + a) + b run as the convs' fused prologue where no padding intervenes;
+* the dense causal attention (CausalAttention, layers.py:613-647) is attention.hip: no n x n
+  logits, fp32 online softmax, recomputing backward;
+* elementwise glue (shifts, residual adds, ELU of the attention aux input, Dropout3d, the
+  cross-entropy) is plain torch on the same stream.
+
+A stack is the reference's (3, b, c, d, h, w) tensor (depth-, height-, width-wise streams); inside
+the model it travels as a list of three channels-last (b, c, d, h, w) tensors.  Dropout: the
+causal Dropout3d runs per stream as in the reference; attention dropout > 0 in training is not
+implemented (the published run uses 0.0, train_pixelsnail_mid_downscaled.job:84).
+"""
+import math
+from argparse import ArgumentParser, Namespace
+from functools import partial
+from operator import attrgetter
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib as L
+from . import ops
+from .ops import ConvGeom
+
+CL = torch.channels_last_3d
+
+
+def cl(t):
+    return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+
+
+def _zeros_like(t):
+    return ops.zero_(torch.empty_like(t))
+
+
+# ============================================================================================ conv
+class CausalConvFn(torch.autograd.Function):
+    """y = conv(prologue(x), w) + cbias on the libvq3d engines; w is the (embedded) k^3 weight.
+    Gradients of w / cbias / the prologue scalars come back as tensors (torch autograd maps them
+    onto the reference-shaped parameters through the embedding)."""
+
+    @staticmethod
+    def forward(ctx, x, w, cbias, pa, pb, k):
+        geom = ConvGeom(k, 1, k // 2, False)
+        pro = None if pa is None else (pa, pb)
+        y = ops.conv_fwd(x, w, geom, pro=pro, cbias=cbias)
+        ctx.geom, ctx.pro = geom, pro
+        ctx.has_bias = cbias is not None
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = cl(g)
+        dw = _zeros_like(w)
+        dcb = torch.zeros(w.shape[0], dtype=torch.float32, device=w.device) if ctx.has_bias else None
+        da = db = None
+        if ctx.pro is not None:
+            da, db = _zeros_like(ctx.pro[0]), _zeros_like(ctx.pro[1])
+        gx, _ = ops.conv_bwd(g, x, w, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
+                             dcbias=dcb, dpro_pre=db, dpro_post=da)
+        return gx, dw, dcb, da, db, None
+
+
+def _embed(depth_w, height_w, width_w, k):
+    """the three causal kernels inside k^3 kernels (k = 3): taps the reference never reads are 0.
+    depth (k-1, k, k) at kd = 0 .. k-2 (front pad k-2 = offsets -1, 0); height (1, k-1, k) at
+    kd = 1, kh = 0 .. k-2; width (1, 1, wk) at kd = kh = 1, kw = 0 .. wk-1."""
+    if k == 1:
+        return depth_w, height_w, width_w
+    wk = width_w.shape[-1]
+    ed = F.pad(depth_w, (0, 0, 0, 0, 0, 1))
+    eh = F.pad(height_w, (0, 0, 0, 1, 1, 1))
+    ew = F.pad(width_w, (0, 3 - wk, 1, 1, 1, 1))
+    return ed, eh, ew
+
+
+def _shift(t, axis):
+    """front-pad spatial axis (0 = d, 1 = h, 2 = w) by one and drop the last slice (the mask 'A'
+    shifts, layers.py:13-100)"""
+    pad = [0, 0, 0, 0, 0, 0]
+    pad[2 * (2 - axis)] = 1
+    t = F.pad(t, tuple(pad))
+    sl = [slice(None)] * 5
+    sl[2 + axis] = slice(0, -1)
+    return cl(t[tuple(sl)])
+
+
+class CausalConv3dAdd(nn.Module):
+    """layers.py:122-222 (parameters: depth_conv / height_conv / width_conv nn.Conv3d)."""
+
+    def __init__(self, mask: str = "B", **conv_kwargs):
+        super().__init__()
+        assert "padding" not in conv_kwargs
+        assert mask in ("A", "B")
+        self.mask = mask
+        kernel_size = conv_kwargs.pop("kernel_size")
+        assert kernel_size > 0 and kernel_size % 2 == 1, "even kernel sizes are not supported"
+        if conv_kwargs.get("groups", 1) != 1:
+            raise NotImplementedError("grouped causal convs (concat_activation) are not implemented")
+        self.kernel_size = kernel_size
+        depth_size = max(kernel_size - 1, 1)
+        height_size = max(kernel_size - 1, 1)
+        width_size = max(kernel_size // 2 + (1 if mask == "B" else 0), 1)
+        self.depth_conv = nn.Conv3d(kernel_size=(depth_size, kernel_size, kernel_size), **conv_kwargs)
+        self.height_conv = nn.Conv3d(kernel_size=(1, height_size, kernel_size), **conv_kwargs)
+        self.width_conv = nn.Conv3d(kernel_size=(1, 1, width_size), **conv_kwargs)
+
+    def run(self, stack, pro=None):
+        """stack: list of 3 channels-last tensors; pro = (a, b): every input goes through
+        elu(x + a) + b first (fused as the conv prologue unless mask 'A' has to shift it)."""
+        k = self.kernel_size
+        if k not in (1, 3):
+            raise NotImplementedError("causal conv kernel sizes 1 and 3 (the reference's default) are supported")
+        ws = _embed(self.depth_conv.weight, self.height_conv.weight, self.width_conv.weight, k)
+        bs = (self.depth_conv.bias, self.height_conv.bias, self.width_conv.bias)
+        out = []
+        for i, (x, w, b) in enumerate(zip(stack, ws, bs)):
+            pa = pb = None
+            if self.mask == "A":
+                if pro is not None:
+                    x = F.elu(x + pro[0]) + pro[1]
+                x = _shift(x, i)
+            elif pro is not None:
+                pa, pb = pro
+            out.append(CausalConvFn.apply(cl(x), w, b, pa, pb, k))
+        return out
+
+    def forward(self, stack):
+        return torch.stack(self.run(to_list(stack)))
+
+
+def to_list(stack):
+    if isinstance(stack, (list, tuple)):
+        return [cl(s) for s in stack]
+    return [cl(stack[i]) for i in range(3)]
+
+
+class ExpandRFConv(nn.Module):
+    """layers.py:225-248"""
+
+    def __init__(self, in_channels):
+        super().__init__()
+        self.depth_conv = nn.Conv3d(in_channels=in_channels, out_channels=in_channels * 2, kernel_size=1)
+        self.height_conv = nn.Conv3d(in_channels=in_channels, out_channels=in_channels, kernel_size=1)
+
+    def run(self, stack):
+        d, h, w = stack
+        dc = CausalConvFn.apply(d, self.depth_conv.weight, self.depth_conv.bias, None, None, 1)
+        dch, dcw = torch.chunk(dc, 2, dim=1)
+        hc = CausalConvFn.apply(h, self.height_conv.weight, self.height_conv.bias, None, None, 1)
+        return [d, cl(h + dch), cl(w + hc + dcw)]
+
+    def forward(self, stack):
+        return torch.stack(self.run(to_list(stack)))
+
+
+def _dropout3d(stack, mod):
+    if mod is None or not mod.training or mod.p == 0:
+        return stack
+    return [cl(F.dropout3d(s, mod.p, True)) for s in stack]
+
+
+class PreActFixupCausalResBlock(nn.Module):
+    """layers.py:338-497"""
+
+    def __init__(self, in_channels, out_channels, kernel_size, mask="B", condition_dim=0, condition_kernel_size=1,
+                 activation=nn.ELU, dropout_prob=0.5, bottleneck_divisor=4, concat_activation=False, aux=False,
+                 *args, **kwargs):
+        super().__init__()
+        if concat_activation:
+            raise NotImplementedError("concat_activation is not implemented")
+        self.bias1a, self.bias1b, self.bias2a, self.bias2b, self.bias3a, self.bias3b, self.bias4 = (
+            nn.Parameter(torch.zeros(1)) for _ in range(7))
+        self.scale = nn.Parameter(torch.ones(1))
+        groups = 1
+        branch_channels = max(max(in_channels, out_channels) // bottleneck_divisor, groups)
+        self.branch_conv1 = CausalConv3dAdd(in_channels=in_channels * groups, out_channels=branch_channels,
+                                            kernel_size=1, mask=mask, bias=False, groups=groups)
+        self.branch_conv2 = CausalConv3dAdd(in_channels=branch_channels * groups, out_channels=branch_channels,
+                                            kernel_size=kernel_size, mask="B", bias=False, groups=groups)
+        self.branch_conv3 = CausalConv3dAdd(in_channels=branch_channels * groups, out_channels=out_channels,
+                                            kernel_size=1, mask="B", bias=False, groups=groups)
+        self.expand_rf = ExpandRFConv(branch_channels * groups)
+        self.skip_conv = CausalConv3dAdd(in_channels=in_channels, out_channels=out_channels, kernel_size=1,
+                                         mask=mask, bias=True) if (in_channels != out_channels or mask == "A") else None
+        self.condition = nn.Conv3d(in_channels=condition_dim, out_channels=branch_channels,
+                                   kernel_size=condition_kernel_size, padding=condition_kernel_size // 2,
+                                   bias=True) if condition_dim > 0 else None
+        self.aux = CausalConv3dAdd(in_channels=branch_channels, out_channels=branch_channels, kernel_size=1,
+                                   bias=True) if aux else None
+        self.activation = activation()
+        self.dropout = nn.Dropout3d(dropout_prob) if dropout_prob > 0 else None
+
+    def run(self, stack, aux=None):
+        out = self.branch_conv1.run(stack, pro=(self.bias1a, self.bias1b))
+        out = self.expand_rf.run(out)
+        if aux is not None:
+            assert self.aux is not None
+            a = self.aux.run([cl(F.elu(t)) for t in aux])
+            out = [cl(o + t) for o, t in zip(out, a)]
+        out = self.branch_conv2.run(out, pro=(self.bias2a, self.bias2b))
+        out = _dropout3d(out, self.dropout)
+        out = self.branch_conv3.run(out, pro=(self.bias3a, self.bias3b))
+        skip = stack if self.skip_conv is None else self.skip_conv.run(stack)
+        return [cl(o * self.scale + self.bias4 + s) for o, s in zip(out, skip)]
+
+    def forward(self, stack, aux=None, condition=None, condition_cache=None):
+        if condition is not None or condition_cache is not None:
+            raise NotImplementedError("conditioning (use_conditioning) is not implemented")
+        return torch.stack(self.run(to_list(stack), None if aux is None else to_list(aux)))
+
+    @torch.no_grad()
+    def initialize_weights(self, num_layers):
+        """layers.py:469-497 (same init calls in the same order)"""
+        getter = attrgetter("depth_conv.weight", "height_conv.weight", "width_conv.weight")
+        for weight in getter(self.branch_conv1):
+            torch.nn.init.normal_(weight, mean=0,
+                                  std=np.sqrt(2 / (weight.shape[0] * np.prod(weight.shape[2:]))) * num_layers ** (-0.5))
+        for weight in getter(self.branch_conv2):
+            torch.nn.init.kaiming_normal_(weight)
+        for weight in getter(self.branch_conv3):
+            torch.nn.init.constant_(weight, val=0)
+        if self.skip_conv is not None:
+            for weight in getter(self.skip_conv):
+                torch.nn.init.xavier_normal_(weight)
+            for bias in attrgetter("depth_conv.bias", "height_conv.bias", "width_conv.bias")(self.skip_conv):
+                torch.nn.init.constant_(tensor=bias, val=0)
+
+
+# ============================================================================================ attention
+class CausalAttentionFn(torch.autograd.Function):
+    """One stream's causal attention (attention.hip): q, k [b][n][nh * dk], v [b][n][nh * dv]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, nh):
+        b, ck = q.shape[:2]
+        n = math.prod(q.shape[2:])
+        cv = v.shape[1]
+        dk, dv = ck // nh, cv // nh
+        scale = float(dk) ** -0.5
+        q, k, v = (t.contiguous(memory_format=CL) for t in (q, k, v))
+        out = torch.empty_like(v, memory_format=CL)
+        lse = torch.empty((b, nh, n), dtype=torch.float32, device=q.device)
+        L.call("vq3d_causal_attn_fwd", L.dtype_code(q), b, n, nh, dk, dv, scale, L.ptr(q), L.ptr(k), L.ptr(v),
+               L.ptr(out), L.ptr(lse), L.stream())
+        ctx.dims = (b, n, nh, dk, dv, scale)
+        ctx.save_for_backward(q, k, v, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k, v, out, lse = ctx.saved_tensors
+        b, n, nh, dk, dv, scale = ctx.dims
+        g = cl(g)
+        gq, gk, gv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        nws = int(L.query("vq3d_causal_attn_workspace_bytes", b, n, nh))
+        ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=q.device)
+        L.call("vq3d_causal_attn_bwd", L.dtype_code(q), b, n, nh, dk, dv, scale, L.ptr(q), L.ptr(k), L.ptr(v),
+               L.ptr(out), L.ptr(g), L.ptr(lse), L.ptr(ws), ctypes_size(nws), L.ptr(gq), L.ptr(gk), L.ptr(gv),
+               L.stream())
+        return gq, gk, gv, None
+
+
+def ctypes_size(n):
+    import ctypes
+    return ctypes.c_size_t(int(n))
+
+
+class CausalAttention(nn.Module):
+    """layers.py:613-647.  Parameter names as the reference's forward: the caller
+    (CausalAttentionPixelBlock, layers.py:694) passes its projected queries as `keys` and its keys
+    as `queries`, and the logits are `queries`^T `keys` -- reproduced exactly."""
+
+    def __init__(self, dropout_prob=0.5, num_heads=8):
+        super().__init__()
+        self.num_heads = num_heads
+        self.dropout = nn.Dropout(dropout_prob)
+
+    def run(self, keys, queries, values):
+        if self.dropout.training and self.dropout.p > 0:
+            raise NotImplementedError("attention dropout > 0 in training is not implemented "
+                                      "(the published prior uses --attention-dropout-prob 0.0)")
+        nh = self.num_heads
+        assert values[0].shape[1] % nh == 0 and keys[0].shape[1] % nh == 0
+        return [CausalAttentionFn.apply(cl(q), cl(k), cl(v), nh) for q, k, v in zip(queries, keys, values)]
+
+    def forward(self, keys, queries, values, attn_mask=None):
+        return torch.stack(self.run(to_list(keys), to_list(queries), to_list(values)))
+
+
+class CausalAttentionPixelBlock(nn.Module):
+    """layers.py:650-703 (attn_mask: the kernels implement the tril mask the reference generates)."""
+
+    def __init__(self, in_channels, bottleneck_divisor, num_layers, causal_conv, num_heads=8,
+                 attention_dropout_prob=0.5):
+        super().__init__()
+        branch_channels = in_channels // bottleneck_divisor
+        self.key_value_proj = CausalConv3dAdd(in_channels=(in_channels * 2 + 3), out_channels=(branch_channels * 2),
+                                              kernel_size=1)
+        self.query_proj = CausalConv3dAdd(in_channels=(in_channels + 3), out_channels=branch_channels, kernel_size=1)
+        self.causal_layers = nn.ModuleList([causal_conv() for _ in range(num_layers)])
+        self.causal_attention = CausalAttention(dropout_prob=attention_dropout_prob, num_heads=num_heads)
+        self.out_proj = causal_conv(aux=True)
+
+    def run(self, stack, bg):
+        out = stack
+        for layer in self.causal_layers:
+            out = layer.run(out)
+        kv = self.key_value_proj.run([cl(torch.cat([s, o, g], dim=1)) for s, o, g in zip(stack, out, bg)])
+        keys, values = zip(*(torch.chunk(t, 2, dim=1) for t in kv))
+        queries = self.query_proj.run([cl(torch.cat([o, g], dim=1)) for o, g in zip(out, bg)])
+        att = self.causal_attention.run(list(queries), list(keys), list(values))
+        return self.out_proj.run(out, aux=att)
+
+    def forward(self, stack, background, attn_mask=None, condition=None, condition_cache=None):
+        if condition is not None or condition_cache is not None:
+            raise NotImplementedError("conditioning (use_conditioning) is not implemented")
+        return torch.stack(self.run(to_list(stack), to_list(background)))
+
+
+# ============================================================================================ model
+def background_list(b, dims, dtype, device):
+    """_generate_background (pixelsnail.py:283-293) per stream: the (d, h, w) linspace grids."""
+    d, h, w = dims
+    g = torch.cat([
+        torch.linspace(-1, 1, d, device=device).view(1, 1, -1, 1, 1).expand(b, 1, d, h, w),
+        torch.linspace(-1, 1, h, device=device).view(1, 1, 1, -1, 1).expand(b, 1, d, h, w),
+        torch.linspace(-1, 1, w, device=device).view(1, 1, 1, 1, -1).expand(b, 1, d, h, w),
+    ], dim=1).to(dtype)
+    g = cl(g)
+    return [g, g, g]
+
+
+class PixelSNAIL(nn.Module):
+    """pixel_model/pixelsnail.py:27-320 (module tree, argument parsing, init and loss of the
+    reference; conditioning and mixup are not implemented -- the published mid-level run disables
+    conditioning; mixup is a data-side blend, train_helpers.py:20-51)."""
+
+    def __init__(self, args, compute_dtype="bf16"):
+        super().__init__()
+        self._parse_input_args(args)
+        self.compute_dtype = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self.parse_input = nn.Conv3d(in_channels=self.input_dim, out_channels=self.model_dim, kernel_size=1)
+        condition_dim = self.model_dim if self.use_conditioning else 0
+        self.embed_condition = nn.Conv3d(in_channels=self.condition_dim, out_channels=condition_dim,
+                                         kernel_size=1) if self.use_conditioning else None
+        causal_conv = partial(PreActFixupCausalResBlock, in_channels=self.model_dim, out_channels=self.model_dim,
+                              kernel_size=self.kernel_size, dropout_prob=self.causal_dropout_prob,
+                              condition_dim=condition_dim, condition_kernel_size=1,
+                              bottleneck_divisor=self.bottleneck_divisor)
+        self.to_causal = causal_conv(mask="A")
+        self.layers = nn.ModuleList([
+            CausalAttentionPixelBlock(in_channels=self.model_dim, bottleneck_divisor=self.bottleneck_divisor,
+                                      causal_conv=partial(causal_conv, mask="B"),
+                                      num_layers=self.num_layers_per_block,
+                                      attention_dropout_prob=self.attention_dropout_prob)
+            for _ in range(self.num_blocks)])
+        self.parse_output = nn.Conv3d(in_channels=self.model_dim, out_channels=self.input_dim, kernel_size=1)
+        num_layers = self.num_blocks * self.num_layers_per_block + 1
+        self.apply(lambda layer: layer.initialize_weights(num_layers=num_layers)
+                   if isinstance(layer, PreActFixupCausalResBlock) else None)
+
+    def _parse_input_args(self, args: Namespace):
+        args.use_gated_block = False
+        self.input_dim, self.condition_dim = args.num_embeddings
+        if not args.use_conditioning:
+            self.condition_dim = 0
+        for name in ("model_dim", "kernel_size", "num_layers_per_block", "num_blocks", "causal_dropout_prob",
+                     "attention_dropout_prob", "bottleneck_divisor", "use_conditioning", "mixup_alpha"):
+            setattr(self, name, getattr(args, name))
+        if self.use_conditioning:
+            raise NotImplementedError("conditioning (use_conditioning) is not implemented")
+        if args.metric != "cross_entropy":
+            raise ValueError
+        self.lr = args.lr
+
+    @classmethod
+    def add_model_specific_args(cls, parent_parser):
+        """pixelsnail.py:193-217"""
+        from .utils import booltype
+        parser = ArgumentParser(parents=[parent_parser], add_help=False)
+        parser.add_argument("--model-dim", default=32, type=int)
+        parser.add_argument("--kernel-size", default=3, type=int)
+        parser.add_argument("--num-layers-per-block", default=5, type=int)
+        parser.add_argument("--num-blocks", default=5, type=int)
+        parser.add_argument("--causal-dropout-prob", default=0.5, type=float)
+        parser.add_argument("--attention-dropout-prob", default=0.5, type=float, help="Set to 0 to disable dropout.")
+        parser.add_argument("--bottleneck-divisor", default=4, type=int, help="Set to 1 to disable bottlenecking")
+        parser.add_argument("--use-conditioning", default=False, type=booltype)
+        parser.add_argument("--mixup-alpha", default=0, type=float)
+        parser.add_argument("--use-mixup-batch-hack", default=False, type=booltype)
+        parser.add_argument("--metric", choices=["cross_entropy"])
+        parser.add_argument("--lr", default=1e-5, type=float)
+        return parser
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.parameters(), lr=self.lr, amsgrad=True)
+
+    def logits(self, onehot):
+        """forward (pixelsnail.py:301-320) of a one-hot (b, K, d, h, w) input; fp32 logits."""
+        b = onehot.shape[0]
+        dims = tuple(onehot.shape[2:])
+        x = cl(onehot.to(self.compute_dtype))
+        x = CausalConvFn.apply(x, self.parse_input.weight, self.parse_input.bias, None, None, 1)
+        stack = self.to_causal.run([x, x, x])
+        bg = background_list(b, dims, self.compute_dtype, x.device)
+        for layer in self.layers:
+            stack = layer.run(stack, bg)
+        s = cl(stack[0] + stack[1] + stack[2])
+        return CausalConvFn.apply(s, self.parse_output.weight, self.parse_output.bias, None, None, 1).float()
+
+    def forward(self, data, background=None, attn_mask=None, condition=None, condition_cache=None):
+        if condition is not None or condition_cache is not None:
+            raise NotImplementedError("conditioning (use_conditioning) is not implemented")
+        return self.logits(data)
+
+    def cross_entropy(self, batch, batch_idx=0, metrics=None, mode="train"):
+        """pixelsnail.py:112-161 without conditioning / mixup: mean cross-entropy of the logits
+        over every code position, plus the log dict's bits_per_dim."""
+        data = batch[0]
+        codes = data.squeeze(1)
+        onehot = F.one_hot(codes, num_classes=self.input_dim).permute(0, 4, 1, 2, 3)
+        logits = self.logits(onehot)
+        loss = F.cross_entropy(logits, codes, reduction="none").mean()
+        return loss, {"bits_per_dim": loss.detach() / np.log(2)}
+
+    def training_step(self, batch, batch_idx):
+        return self.cross_entropy(batch, batch_idx, mode="train")[0]
+
+
+def default_args(**kw):
+    """the reference's argparse defaults (pixelsnail.py:197-216) as a Namespace."""
+    a = Namespace(num_embeddings=[512, 0], model_dim=32, kernel_size=3, num_layers_per_block=5, num_blocks=5,
+                  causal_dropout_prob=0.5, attention_dropout_prob=0.5, bottleneck_divisor=4, use_conditioning=False,
+                  mixup_alpha=0.0, use_mixup_batch_hack=False, metric="cross_entropy", lr=1e-5)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a

@@ -329,6 +329,24 @@ int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *
 /* x *= a over n fp32 values (gradient averaging after the all-reduce uses a = 1/world) */
 int vq3d_scale(float *x, float a, int64_t n, vq3d_stream_t stream);
 
+/* --- PixelSNAIL prior: dense causal attention (pixel_model/layers.py:613-647) ---
+ * For each of nprob problems (stack x batch) and nh heads: out[i] = sum_{j <= i} softmax_j(scale *
+ * q_i . k_j) v_j over n positions, without the n x n logits.  q, k: [nprob][n][nh * dk], v, out:
+ * [nprob][n][nh * dv] (rows channels-last, head h owns channels h*d .. h*d + d - 1), dtype bf16 or
+ * fp32, fp32 arithmetic; head dims up to 16.  The forward saves lse [nprob][nh][n] (fp32, base-2
+ * log-sum-exp of the scaled scores); the backward recomputes the probabilities from it and writes
+ * gq, gk, gv (same layouts as q, k, v) through a workspace of vq3d_causal_attn_workspace_bytes.
+ * The reference's CausalAttentionPixelBlock binds its projected queries to the parameter named
+ * `keys` and vice versa (layers.py:694 vs 619); callers pass q = that block's keys projection. */
+int vq3d_causal_attn_supported(int32_t nh, int32_t dk, int32_t dv);
+size_t vq3d_causal_attn_workspace_bytes(int32_t nprob, int32_t n, int32_t nh);
+int vq3d_causal_attn_fwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                         const void *q, const void *k, const void *v, void *out, float *lse, vq3d_stream_t stream);
+int vq3d_causal_attn_bwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                         const void *q, const void *k, const void *v, const void *out, const void *gout,
+                         const float *lse, void *workspace, size_t workspace_bytes, void *gq, void *gk, void *gv,
+                         vq3d_stream_t stream);
+
 const char *vq3d_last_error(void);
 const char *vq3d_version(void);
 

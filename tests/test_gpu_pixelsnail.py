@@ -1,0 +1,150 @@
+"""PixelSNAIL prior on the GPU (vq3d.pixelsnail: causal convs on the libvq3d conv engines,
+attention.hip) against the reference's own outputs (tests/golden/psnail_*.npz) and, at the
+published mid-level size, against a torch fp32 restatement of the attention.
+
+Tolerances: fp32 path 1e-4 of each tensor's max (summation order only); bf16 path 3e-2 of the
+max (bf16 activations, fp32 accumulation); the attention kernel in bf16 storage 2e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+G = "tests/golden/"
+CL = torch.channels_last_3d
+
+
+def P_of(d, pre="p/"):
+    return {k[len(pre):]: torch.tensor(d[k]) for k in d.files if k.startswith(pre)}
+
+
+def rel(a, b):
+    a = np.asarray(a.detach().float().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+
+
+def load_params(mod, P, dev):
+    sd = {k: v for k, v in P.items()}
+    mod.load_state_dict(sd, strict=True)
+    return mod.to(dev)
+
+
+def stack_in(x, dev, dtype=torch.float32):
+    """(3, b, c, d, h, w) -> list of 3 channels-last GPU tensors requiring grad"""
+    return [torch.tensor(x[i]).to(dev, dtype).contiguous(memory_format=CL).requires_grad_(True) for i in range(3)]
+
+
+@pytest.mark.parametrize("name,nh", [("psnail_attn_h2", 2), ("psnail_attn_h8", 8)])
+def test_attention_golden(gpu, name, nh):
+    from vq3d import pixelsnail as PS
+    d = np.load(G + name + ".npz")
+    att = PS.CausalAttention(dropout_prob=0.0, num_heads=nh).to(gpu)
+    keys, queries, values = stack_in(d["q"], gpu), stack_in(d["k"], gpu), stack_in(d["v"], gpu)
+    # the golden was made with the reference's binding: its `keys` parameter got d["q"]
+    y = att.run(keys, queries, values)
+    assert rel(torch.stack(y), d["y"]) < 1e-5
+    torch.autograd.backward(y, [torch.tensor(d["gy"][i]).to(gpu).contiguous(memory_format=CL) for i in range(3)])
+    assert rel(torch.stack([t.grad for t in keys]), d["gq"]) < 1e-4
+    assert rel(torch.stack([t.grad for t in queries]), d["gk"]) < 1e-4
+    assert rel(torch.stack([t.grad for t in values]), d["gv"]) < 1e-4
+
+
+def _attn_ref(q, k, v, nh):
+    """torch fp32 restatement (GPU), one stream: q, k (b, ck, n), v (b, cv, n)"""
+    b, ck, n = q.shape
+    cv = v.shape[1]
+    fq = q.reshape(b, nh, ck // nh, n) * (ck // nh) ** -0.5
+    fk = k.reshape(b, nh, ck // nh, n)
+    fv = v.reshape(b, nh, cv // nh, n)
+    logits = torch.matmul(fq.transpose(2, 3), fk)
+    mask = torch.tril(torch.ones((n, n), dtype=torch.bool, device=q.device))
+    w = torch.softmax(logits.masked_fill(~mask, float("-inf")), -1)
+    return torch.matmul(w, fv.transpose(2, 3)).transpose(2, 3).reshape(b, cv, n)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+def test_attention_mid_level_size(gpu, dtype, tol):
+    """the published mid level: 32 x 32 x 8 = 8,192 positions, 64 channels = 8 heads x 8"""
+    from vq3d import pixelsnail as PS
+    g = torch.Generator(device=gpu).manual_seed(0)
+    dims, c, nh = (32, 32, 8), 64, 8
+    q, k, v = (torch.randn((1, c) + dims, device=gpu, generator=g).to(dtype).contiguous(memory_format=CL)
+               .requires_grad_(True) for _ in range(3))
+    y = PS.CausalAttentionFn.apply(q, k, v, nh)
+    gy = torch.randn(y.shape, device=gpu, generator=g).to(dtype)
+    y.backward(gy)
+    qf, kf, vf = (t.detach().float().reshape(1, c, -1).requires_grad_(True) for t in (q, k, v))
+    yr = _attn_ref(qf, kf, vf, nh)
+    yr.backward(gy.float().reshape(1, c, -1))
+    assert rel(y.reshape(1, c, -1), yr.detach().cpu().numpy()) < tol
+    for t, r in ((q, qf), (k, kf), (v, vf)):
+        assert rel(t.grad.reshape(1, c, -1), r.grad.cpu().numpy()) < 2 * tol
+
+
+@pytest.mark.parametrize("name,mask,k,bias", [("psnail_conv_b3", "B", 3, False), ("psnail_conv_a1", "A", 1, True),
+                                              ("psnail_conv_b1", "B", 1, True)])
+def test_causal_conv_golden(gpu, name, mask, k, bias):
+    from vq3d import pixelsnail as PS
+    d = np.load(G + name + ".npz")
+    cin, cout = d["x"].shape[2], d["y"].shape[2]
+    m = load_params(PS.CausalConv3dAdd(mask=mask, in_channels=cin, out_channels=cout, kernel_size=k, bias=bias),
+                    P_of(d), gpu)
+    xs = stack_in(d["x"], gpu)
+    y = m.run(xs)
+    assert rel(torch.stack(y), d["y"]) < 1e-5
+    torch.autograd.backward(y, [torch.tensor(d["gy"][i]).to(gpu).contiguous(memory_format=CL) for i in range(3)])
+    assert rel(torch.stack([t.grad for t in xs]), d["gx"]) < 1e-4
+    for n, p in m.named_parameters():
+        assert rel(p.grad, d["g/" + n]) < 1e-4, n
+
+
+@pytest.mark.parametrize("name,mask,aux", [("psnail_block_a", "A", False), ("psnail_block_b_aux", "B", True)])
+def test_causal_block_golden(gpu, name, mask, aux):
+    from vq3d import pixelsnail as PS
+    d = np.load(G + name + ".npz")
+    c = d["x"].shape[2]
+    m = load_params(PS.PreActFixupCausalResBlock(c, c, 3, mask=mask, dropout_prob=0.0, bottleneck_divisor=4, aux=aux),
+                    P_of(d), gpu)
+    xs = stack_in(d["x"], gpu)
+    a = stack_in(d["aux"], gpu) if aux else None
+    y = m.run(xs, a)
+    assert rel(torch.stack(y), d["y"]) < 1e-5
+    torch.autograd.backward(y, [torch.tensor(d["gy"][i]).to(gpu).contiguous(memory_format=CL) for i in range(3)])
+    assert rel(torch.stack([t.grad for t in xs]), d["gx"]) < 1e-4
+    if aux:
+        assert rel(torch.stack([t.grad for t in a]), d["gaux"]) < 1e-4
+    scale = max(np.abs(d["g/" + n]).max() for n, _ in m.named_parameters())
+    for n, p in m.named_parameters():
+        err = np.abs(p.grad.detach().cpu().numpy() - d["g/" + n]).max()
+        assert err <= max(1e-4 * np.abs(d["g/" + n]).max(), 1e-5 * scale), n
+
+
+@pytest.mark.parametrize("dtype,tol,gtol", [("fp32", 1e-4, 1e-3), ("bf16", 3e-2, 8e-2)])
+def test_pixelsnail_model_golden(gpu, dtype, tol, gtol):
+    """whole prior: logits, loss and every parameter gradient of a training step (dropout 0)"""
+    from vq3d import pixelsnail as PS
+    d = np.load(G + "psnail_model_32.npz")
+    ne, md, nl, nb, bd = (int(c) for c in d["cfg"])
+    args = PS.default_args(num_embeddings=[ne, 0], model_dim=md, num_layers_per_block=nl, num_blocks=nb,
+                           bottleneck_divisor=bd, causal_dropout_prob=0.0, attention_dropout_prob=0.0, lr=1e-3)
+    m = load_params(PS.PixelSNAIL(args, compute_dtype=dtype), P_of(d), gpu)
+    m.train()
+    data = torch.tensor(d["data"]).to(gpu)
+    loss, _ = m.cross_entropy([data])
+    loss.backward()
+    with torch.no_grad():
+        onehot = torch.nn.functional.one_hot(data.squeeze(1), ne).permute(0, 4, 1, 2, 3)
+        logits = m.logits(onehot)
+    print(dtype, "loss", float(loss), float(d["loss"]), "logits rel", rel(logits, d["logits"]))
+    assert rel(logits, d["logits"]) < tol
+    assert abs(float(loss) - float(d["loss"])) < tol * abs(float(d["loss"]))
+    scale = max(np.abs(d["g/" + n]).max() for n, _ in m.named_parameters())
+    worst = 0.0
+    for n, p in m.named_parameters():
+        ref = d["g/" + n]
+        err = np.abs(p.grad.detach().cpu().numpy() - ref).max() / max(np.abs(ref).max(), 1e-3 * scale)
+        worst = max(worst, err)
+        assert err <= gtol, n
+    print(dtype, "worst gradient error (of max(|ref|, 1e-3 scale))", worst)

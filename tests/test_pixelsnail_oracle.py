@@ -74,3 +74,19 @@ def test_pixelsnail_loss_and_grads():
     for n in P:  # the key-role projection biases have exactly-zero true gradients (softmax shift)
         err = np.abs(P[n].grad.numpy() - d["g/" + n]).max()
         assert err <= max(1e-4 * np.abs(d["g/" + n]).max(), 1e-6 * scale), n
+
+
+def test_product_module_tree_and_seeded_init():
+    """vq3d.pixelsnail.PixelSNAIL builds the reference's module tree (state_dict keys / shapes)
+    and, seeded, bit-identical initial parameters (construction order + initialize_weights)."""
+    from vq3d import pixelsnail as PS
+    d = np.load(G + "psnail_init_64.npz")
+    torch.manual_seed(3)
+    m = PS.PixelSNAIL(PS.default_args(model_dim=64, num_blocks=2, num_layers_per_block=2, num_embeddings=[16, 0],
+                                      causal_dropout_prob=0.0, attention_dropout_prob=0.0), compute_dtype="fp32")
+    ref = {k[2:]: d[k] for k in d.files}
+    mine = dict(m.named_parameters())
+    assert sorted(mine) == sorted(ref)
+    for n, p in mine.items():
+        assert tuple(p.shape) == ref[n].shape, n
+        assert np.array_equal(p.detach().numpy(), ref[n]), n
