@@ -7,11 +7,13 @@
 // per block: 3 x 8 x 8192^2 fp32 at the published mid level).  Head dims are tiny (model-dim
 // 256 / bottleneck 4 / 8 heads = 8), so the contraction is per-thread VALU work: a thread owns
 // one query row (fwd, dQ) or one key row (dK / dV) with its q / k / v / dO rows in registers;
-// the opposite side streams through LDS in 256-row tiles that every lane reads as broadcasts.
+// the opposite side streams through LDS in 64-row tiles that every lane reads as broadcasts.
 // Causality bounds the tile loops (query tile t meets key tiles 0 .. t), the diagonal tile masks
 // per lane.  The online softmax runs in base 2 on chunks of 8 scores (one rescale per chunk);
 // the forward saves the per-row log-sum-exp (base 2) for the backward, which recomputes the
 // probabilities (flash-attention style, fp32 arithmetic throughout, bf16 or fp32 storage).
+// A workgroup owns 64 rows; its 4 waves split every staged 64-row tile of the other side four
+// ways (4 waves per SIMD at the mid level's 8,192 positions x 8 heads) and merge at the end.
 //
 // Layout: q, k [P][n][nh * dk], v, out [P][n][nh * dv] -- channels-last rows with head-major
 // channels (head h owns channels h * d .. h * d + d - 1, the reference's reshape(..., nh, d, n)).
@@ -24,8 +26,11 @@ namespace vq3d {
 
 namespace {
 
-constexpr int NT = 256;  // threads per workgroup = rows per tile
-constexpr int CH = 8;    // scores per online-softmax chunk
+constexpr int QR = 64;          // rows (queries, or keys in the dK / dV kernel) per workgroup
+constexpr int NW = 4;           // waves per workgroup: each takes a quarter of every staged tile
+constexpr int NT = QR * NW;     // 256 threads
+constexpr int SUB = QR / NW;    // 16 staged rows per wave
+constexpr int CH = 8;           // scores per online-softmax chunk
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct AttnArgs {
@@ -46,16 +51,19 @@ __device__ __forceinline__ void store_row(T *__restrict__ dst, int64_t base, int
         if (c < d) st(dst + base + c, r[c]);
 }
 
-// rows [r0, r0 + NT) of a [P][n][nh * d] tensor's head h into LDS [NT][DM] fp32 (zero past n / d)
+// rows [r0, r0 + QR) of a [P][n][nh * d] tensor's head h into LDS [QR][DM] fp32 (zero past n / d),
+// by the QR threads [t0, t0 + QR)
 template <typename T, int DM>
 __device__ __forceinline__ void stage(float *dst, const T *__restrict__ src, const AttnArgs &a, int p, int h, int d,
-                                      int r0) {
-    const int r = r0 + int(threadIdx.x);
+                                      int r0, int t0) {
+    const int t = int(threadIdx.x) - t0;
+    if (t < 0 || t >= QR) return;
+    const int r = r0 + t;
     float v[DM];
     load_row<T, DM>(src, (int64_t(p) * a.n + min(r, a.n - 1)) * (a.nh * d) + h * d, d, r < a.n, v);
 #pragma unroll
     for (int c = 0; c < DM; c += 4)
-        *reinterpret_cast<float4 *>(dst + threadIdx.x * DM + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+        *reinterpret_cast<float4 *>(dst + t * DM + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
 }
 
 template <int DM>
@@ -84,15 +92,19 @@ __device__ __forceinline__ void axpy(float (&y)[DM], float a, const float *x) {
     }
 }
 
-// grid: (query tiles, P * nh), heaviest (last) query tiles first
+// Forward.  Workgroup = QR query rows of one (problem, head); lane r of every wave owns query row
+// r, wave w the keys w * SUB .. w * SUB + SUB - 1 of each staged QR-key tile (online softmax per
+// wave), the 4 partial (m, l, o) merged at the end.  grid (query tiles, P * nh), heaviest first.
 template <typename T, int DM>
 __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict__ q, const T *__restrict__ k,
                                                  const T *__restrict__ v, T *__restrict__ out,
                                                  float *__restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) float ks[NT * DM], vs[NT * DM];
-    const int nqt = (a.n + NT - 1) / NT, qt = nqt - 1 - int(blockIdx.x);
+    __shared__ __attribute__((aligned(16))) float ks[QR * DM], vs[QR * DM];
+    __shared__ __attribute__((aligned(16))) float pm[NW][QR], pl[NW][QR], po[NW][QR][DM];
+    const int nqt = (a.n + QR - 1) / QR, qt = nqt - 1 - int(blockIdx.x);
     const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
-    const int i = qt * NT + int(threadIdx.x);
+    const int r = int(threadIdx.x) & (QR - 1), w = int(threadIdx.x) / QR;
+    const int i = qt * QR + r;
     float qr[DM], o[DM];
     load_row<T, DM>(q, (int64_t(p) * a.n + min(i, a.n - 1)) * (a.nh * a.dk) + h * a.dk, a.dk, i < a.n, qr);
 #pragma unroll
@@ -103,20 +115,21 @@ __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict
     float m = -INFINITY, l = 0.f;
     for (int kt = 0; kt <= qt; ++kt) {
         __syncthreads();
-        stage<T, DM>(ks, k, a, p, h, a.dk, kt * NT);
-        stage<T, DM>(vs, v, a, p, h, a.dv, kt * NT);
+        stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
+        stage<T, DM>(vs, v, a, p, h, a.dv, kt * QR, QR);
         __syncthreads();
-        const int jmax = kt < qt ? NT : min(NT, i - kt * NT + 1);  // keys j <= i of this tile
-        const int jend = kt < qt ? NT : NT;                          // uniform trip count
-#pragma unroll 1
-        for (int j0 = 0; j0 < jend; j0 += CH) {
+        const int jlim = kt < qt ? QR : r + 1;  // local keys j <= i
+#pragma unroll
+        for (int c0 = 0; c0 < SUB; c0 += CH) {
+            const int j0 = w * SUB + c0;
+            if (j0 >= jlim) break;
             float s[CH], cm = m;
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
-                s[u] = j0 + u < jmax ? dot<DM>(qr, ks + (j0 + u) * DM) : -INFINITY;
+                s[u] = j0 + u < jlim ? dot<DM>(qr, ks + (j0 + u) * DM) : -INFINITY;
                 cm = fmaxf(cm, s[u]);
             }
-            const float alpha = exp2f(m - cm);  // m = -inf on the first chunk: 0
+            const float alpha = exp2f(m - cm);  // m = -inf before the wave's first key: 0
             l *= alpha;
 #pragma unroll
             for (int c = 0; c < DM; ++c) o[c] *= alpha;
@@ -129,27 +142,49 @@ __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict
             m = cm;
         }
     }
-    if (i < a.n) {
-        const float inv = 1.f / l;
+    // merge the 4 waves' partial softmaxes (a wave that met no key has m = -inf, l = 0)
+    pm[w][r] = m;
+    pl[w][r] = l;
 #pragma unroll
-        for (int c = 0; c < DM; ++c) o[c] *= inv;
-        store_row<T, DM>(out, (int64_t(p) * a.n + i) * (a.nh * a.dv) + h * a.dv, a.dv, o);
-        lse[(int64_t(p) * a.nh + h) * a.n + i] = m + log2f(l);
+    for (int c = 0; c < DM; ++c) po[w][r][c] = o[c];
+    __syncthreads();
+    if (w == 0 && i < a.n) {
+        float M = pm[0][r];
+#pragma unroll
+        for (int x = 1; x < NW; ++x) M = fmaxf(M, pm[x][r]);
+        float Lt = 0.f, O[DM];
+#pragma unroll
+        for (int c = 0; c < DM; ++c) O[c] = 0.f;
+#pragma unroll
+        for (int x = 0; x < NW; ++x) {
+            const float f = pm[x][r] == -INFINITY ? 0.f : exp2f(pm[x][r] - M);
+            Lt = fmaf(pl[x][r], f, Lt);
+#pragma unroll
+            for (int c = 0; c < DM; ++c) O[c] = fmaf(po[x][r][c], f, O[c]);
+        }
+        const float inv = 1.f / Lt;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) O[c] *= inv;
+        store_row<T, DM>(out, (int64_t(p) * a.n + i) * (a.nh * a.dv) + h * a.dv, a.dv, O);
+        lse[(int64_t(p) * a.nh + h) * a.n + i] = M + log2f(Lt);
     }
 }
 
 // backward, query side: delta_i = dO_i . O_i (to the workspace) and dQ_i = scale sum_j ds_ij k_j,
-// ds_ij = p_ij (dO_i . v_j - delta_i)
+// ds_ij = p_ij (dO_i . v_j - delta_i); the waves split the keys as in the forward, the partial dQ
+// summed at the end in wave order
 template <typename T, int DM>
 __global__ __launch_bounds__(NT) void k_attn_bwd_q(AttnArgs a, float scale, const T *__restrict__ q,
                                                    const T *__restrict__ k, const T *__restrict__ v,
                                                    const T *__restrict__ out, const T *__restrict__ gout,
                                                    const float *__restrict__ lse, float *__restrict__ delta,
                                                    T *__restrict__ gq) {
-    __shared__ __attribute__((aligned(16))) float ks[NT * DM], vs[NT * DM];
-    const int nqt = (a.n + NT - 1) / NT, qt = nqt - 1 - int(blockIdx.x);
+    __shared__ __attribute__((aligned(16))) float ks[QR * DM], vs[QR * DM];
+    __shared__ __attribute__((aligned(16))) float pq[NW][QR][DM];
+    const int nqt = (a.n + QR - 1) / QR, qt = nqt - 1 - int(blockIdx.x);
     const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
-    const int i = qt * NT + int(threadIdx.x);
+    const int r = int(threadIdx.x) & (QR - 1), w = int(threadIdx.x) / QR;
+    const int i = qt * QR + r;
     const bool ok = i < a.n;
     const int ic = min(i, a.n - 1);
     float qr[DM], go[DM], orow[DM], dq[DM];
@@ -165,41 +200,48 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_q(AttnArgs a, float scale, cons
     }
     const int64_t row = (int64_t(p) * a.nh + h) * a.n + ic;
     const float lz = ok ? lse[row] : 0.f;
-    if (ok) delta[row] = dl;
+    if (ok && w == 0) delta[row] = dl;
     for (int kt = 0; kt <= qt; ++kt) {
         __syncthreads();
-        stage<T, DM>(ks, k, a, p, h, a.dk, kt * NT);
-        stage<T, DM>(vs, v, a, p, h, a.dv, kt * NT);
+        stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
+        stage<T, DM>(vs, v, a, p, h, a.dv, kt * QR, QR);
         __syncthreads();
-        const int jmax = kt < qt ? NT : min(NT, i - kt * NT + 1);
+        const int jlim = kt < qt ? QR : r + 1;
 #pragma unroll 4
-        for (int j = 0; j < NT; ++j) {
-            if (j < jmax) {
+        for (int u = 0; u < SUB; ++u) {
+            const int j = w * SUB + u;
+            if (j < jlim) {
                 const float pr = exp2f(dot<DM>(qr, ks + j * DM) - lz);
                 const float ds = pr * (dot<DM>(go, vs + j * DM) - dl);
                 axpy<DM>(dq, ds, ks + j * DM);
             }
         }
     }
-    if (ok) {
 #pragma unroll
-        for (int c = 0; c < DM; ++c) dq[c] *= scale;
+    for (int c = 0; c < DM; ++c) pq[w][r][c] = dq[c];
+    __syncthreads();
+    if (w == 0 && ok) {
+#pragma unroll
+        for (int c = 0; c < DM; ++c) dq[c] = scale * (((pq[0][r][c] + pq[1][r][c]) + pq[2][r][c]) + pq[3][r][c]);
         store_row<T, DM>(gq, (int64_t(p) * a.n + i) * (a.nh * a.dk) + h * a.dk, a.dk, dq);
     }
 }
 
-// backward, key side: dV_j = sum_{i >= j} p_ij dO_i, dK_j = scale sum_{i >= j} ds_ij q_i
+// backward, key side: dV_j = sum_{i >= j} p_ij dO_i, dK_j = scale sum_{i >= j} ds_ij q_i.
+// Workgroup = QR key rows; wave w takes the queries w * SUB .. of each staged query tile.
 template <typename T, int DM>
 __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, const T *__restrict__ q,
                                                     const T *__restrict__ k, const T *__restrict__ v,
                                                     const T *__restrict__ gout, const float *__restrict__ lse,
                                                     const float *__restrict__ delta, T *__restrict__ gk,
                                                     T *__restrict__ gv) {
-    __shared__ __attribute__((aligned(16))) float qs[NT * DM], gs[NT * DM];
-    __shared__ float ls[NT], dls[NT];
-    const int nkt = (a.n + NT - 1) / NT, kt = int(blockIdx.x);  // the lightest tiles last
+    __shared__ __attribute__((aligned(16))) float qs[QR * DM], gs[QR * DM];
+    __shared__ float ls[QR], dls[QR];
+    __shared__ __attribute__((aligned(16))) float pk[NW][QR][DM], pv[NW][QR][DM];
+    const int nt = (a.n + QR - 1) / QR, kt = int(blockIdx.x);  // key tile 0 meets every query tile: first
     const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
-    const int j = kt * NT + int(threadIdx.x);
+    const int r = int(threadIdx.x) & (QR - 1), w = int(threadIdx.x) / QR;
+    const int j = kt * QR + r;
     const bool ok = j < a.n;
     const int jc = min(j, a.n - 1);
     float kr[DM], vr[DM], dk[DM], dv[DM];
@@ -211,20 +253,21 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
         dk[c] = dv[c] = 0.f;
     }
     const int64_t rb = (int64_t(p) * a.nh + h) * a.n;
-    for (int qt = kt; qt < nkt; ++qt) {
+    for (int qt = kt; qt < nt; ++qt) {
         __syncthreads();
-        stage<T, DM>(qs, q, a, p, h, a.dk, qt * NT);
-        stage<T, DM>(gs, gout, a, p, h, a.dv, qt * NT);
-        {
-            const int r = qt * NT + int(threadIdx.x);
-            ls[threadIdx.x] = r < a.n ? lse[rb + r] : 0.f;
-            dls[threadIdx.x] = r < a.n ? delta[rb + r] : 0.f;
+        stage<T, DM>(qs, q, a, p, h, a.dk, qt * QR, 0);
+        stage<T, DM>(gs, gout, a, p, h, a.dv, qt * QR, QR);
+        if (threadIdx.x >= 2 * QR && threadIdx.x < 3 * QR) {
+            const int t = int(threadIdx.x) - 2 * QR, rr = qt * QR + t;
+            ls[t] = rr < a.n ? lse[rb + rr] : 0.f;
+            dls[t] = rr < a.n ? delta[rb + rr] : 0.f;
         }
         __syncthreads();
-        const int i0 = qt > kt ? 0 : int(threadIdx.x);           // queries i >= j of this tile
-        const int iend = min(NT, a.n - qt * NT);
+        const int i0 = qt > kt ? 0 : r;  // local queries i >= j
+        const int iend = min(QR, a.n - qt * QR);
 #pragma unroll 4
-        for (int ii = 0; ii < NT; ++ii) {
+        for (int u = 0; u < SUB; ++u) {
+            const int ii = w * SUB + u;
             if (ii >= i0 && ii < iend) {
                 const float pr = exp2f(dot<DM>(kr, qs + ii * DM) - ls[ii]);
                 axpy<DM>(dv, pr, gs + ii * DM);
@@ -233,9 +276,18 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
             }
         }
     }
-    if (ok) {
 #pragma unroll
-        for (int c = 0; c < DM; ++c) dk[c] *= scale;
+    for (int c = 0; c < DM; ++c) {
+        pk[w][r][c] = dk[c];
+        pv[w][r][c] = dv[c];
+    }
+    __syncthreads();
+    if (w == 0 && ok) {
+#pragma unroll
+        for (int c = 0; c < DM; ++c) {
+            dk[c] = scale * (((pk[0][r][c] + pk[1][r][c]) + pk[2][r][c]) + pk[3][r][c]);
+            dv[c] = ((pv[0][r][c] + pv[1][r][c]) + pv[2][r][c]) + pv[3][r][c];
+        }
         store_row<T, DM>(gk, (int64_t(p) * a.n + j) * (a.nh * a.dk) + h * a.dk, a.dk, dk);
         store_row<T, DM>(gv, (int64_t(p) * a.n + j) * (a.nh * a.dv) + h * a.dv, a.dv, dv);
     }
@@ -249,14 +301,14 @@ int dmax_of(int dk, int dv) {
 template <typename T, int DM>
 void launch_fwd(const AttnArgs &a, const void *q, const void *k, const void *v, void *out, float *lse,
                 hipStream_t s) {
-    const dim3 grid((a.n + NT - 1) / NT, a.P * a.nh);
+    const dim3 grid((a.n + QR - 1) / QR, a.P * a.nh);
     k_attn_fwd<T, DM><<<grid, NT, 0, s>>>(a, (const T *)q, (const T *)k, (const T *)v, (T *)out, lse);
 }
 
 template <typename T, int DM>
 void launch_bwd(const AttnArgs &a, float scale, const void *q, const void *k, const void *v, const void *out,
                 const void *gout, const float *lse, float *delta, void *gq, void *gk, void *gv, hipStream_t s) {
-    const dim3 grid((a.n + NT - 1) / NT, a.P * a.nh);
+    const dim3 grid((a.n + QR - 1) / QR, a.P * a.nh);
     k_attn_bwd_q<T, DM><<<grid, NT, 0, s>>>(a, scale, (const T *)q, (const T *)k, (const T *)v, (const T *)out,
                                             (const T *)gout, lse, delta, (T *)gq);
     k_attn_bwd_kv<T, DM><<<grid, NT, 0, s>>>(a, scale, (const T *)q, (const T *)k, (const T *)v, (const T *)gout,

@@ -428,9 +428,13 @@ class PixelSNAIL(nn.Module):
     def cross_entropy(self, batch, batch_idx=0, metrics=None, mode="train"):
         """pixelsnail.py:112-161 without conditioning / mixup: mean cross-entropy of the logits
         over every code position, plus the log dict's bits_per_dim."""
-        data = batch[0]
-        codes = data.squeeze(1)
+        codes = batch[0].squeeze(1)
         onehot = F.one_hot(codes, num_classes=self.input_dim).permute(0, 4, 1, 2, 3)
+        return self.cross_entropy_onehot(onehot, codes)
+
+    def cross_entropy_onehot(self, onehot, codes):
+        """the loss from a prepared one-hot input (F.one_hot validates its input on the host, which
+        a captured HIP graph cannot do)"""
         logits = self.logits(onehot)
         loss = F.cross_entropy(logits, codes, reduction="none").mean()
         return loss, {"bits_per_dim": loss.detach() / np.log(2)}

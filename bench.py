@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--size", type=int, nargs=3, default=None, help="override the volume H W D")
     p.add_argument("--encode-only", action="store_true", help="eval encode + codebook search (configs[3])")
+    p.add_argument("--prior", action="store_true",
+                   help="PixelSNAIL mid-level prior training step (configs[4]) instead of the VQ-VAE step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="print per-step times to stderr")
@@ -366,8 +368,134 @@ def capture(step, warmup):
     return graph, res
 
 
+# PixelSNAIL mid-level prior (BASELINE configs[4]; slurm-jobs/train_pixelsnail_mid_downscaled.job:76-90):
+# codes of the 3-layer published model's middle level at 512^2 x 128 (32 x 32 x 8, K = 256),
+# model-dim 256, 8 blocks x 5 layers, causal dropout 0.2, attention dropout 0, batch 1
+PRIOR = dict(dims=(32, 32, 8), num_embeddings=[256, 0], model_dim=256, num_blocks=8, num_layers_per_block=5,
+             causal_dropout_prob=0.2, attention_dropout_prob=0.0, bottleneck_divisor=4, lr=5e-5)
+
+
+def prior_cpu_baseline(sample=(8, 8, 8), reps=2):
+    """oracle/pixelsnail_cpu.py: forward + backward of the same prior (dropout 0) on a bounded
+    sample of positions, scaled linearly by position count (the attention's n^2 term makes the
+    real CPU cost at 8,192 positions higher: the scaled number flatters the CPU)."""
+    import torch
+
+    from oracle import pixelsnail_cpu as O
+    from vq3d import pixelsnail as PS
+    torch.set_num_threads(os.cpu_count() or 1)
+    kw = {k: v for k, v in PRIOR.items() if k != "dims"}
+    torch.manual_seed(0)
+    m = PS.PixelSNAIL(PS.default_args(**kw), compute_dtype="fp32")
+    P = {n: p.detach().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    data = torch.randint(0, kw["num_embeddings"][0], (1, 1) + sample)
+    ts = []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        loss, _ = O.loss(P, data, kw["num_embeddings"][0], kw["num_blocks"], kw["num_layers_per_block"])
+        loss.backward()
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts[1:])
+    scale = (PRIOR["dims"][0] * PRIOR["dims"][1] * PRIOR["dims"][2]) / (sample[0] * sample[1] * sample[2])
+    return {"value": 1.0 / (t * scale), "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle fwd+bwd (no optimizer) of the same prior on {sample[0]}x{sample[1]}x{sample[2]} codes, "
+                      f"median of {reps} after a warm-up ({t:.2f} s), scaled x{scale:.0f} by position count"}
+
+
+def prior_main(a):
+    import torch
+
+    from vq3d import pixelsnail as PS
+    from vq3d.flat import FlatParams
+    from vq3d.optim import FusedAdam
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    kw = {k: v for k, v in PRIOR.items() if k != "dims"}
+    dims = PRIOR["dims"]
+    model = PS.PixelSNAIL(PS.default_args(**kw), compute_dtype=a.dtype).to(dev)
+    flat = FlatParams(model.parameters(), dev)
+    opt = FusedAdam(model.parameters(), flat, lr=kw["lr"], amsgrad=True)
+    model.train()
+    g = torch.Generator().manual_seed(1)
+    data = torch.randint(0, kw["num_embeddings"][0], (1, 1) + dims, generator=g).to(dev)
+    codes = data.squeeze(1)
+    onehot = torch.nn.functional.one_hot(codes, kw["num_embeddings"][0]).permute(0, 4, 1, 2, 3).contiguous()
+
+    def step(i):
+        opt.zero_grad()
+        loss, _ = model.cross_entropy_onehot(onehot, codes)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    print("[bench] prior warm-up done", file=sys.stderr, flush=True)
+    graph = None
+    if not a.eager and a.warmup >= 2:
+        graph, static = capture(step, a.warmup)
+        print("[bench] prior step captured", file=sys.stderr, flush=True)
+
+        def step(i):  # noqa: F811
+            graph.replay()
+            return static
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        res = step(a.warmup + i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = 1000.0 * elapsed / a.steps
+    # the attention kernels alone (forward + backward of one stream at the step's shape), HIP
+    # events on the launching stream: flops = causal pairs x (fwd 2 (dk + dv) + bwd 2 (2 dk + 2 dv))
+    n, c, nh = dims[0] * dims[1] * dims[2], kw["model_dim"] // kw["bottleneck_divisor"], 8
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    q, k, v = (torch.randn((1, c) + dims, device=dev).to(dtype).contiguous(memory_format=torch.channels_last_3d)
+               .requires_grad_(True) for _ in range(3))
+    gy = torch.randn((1, c) + dims, device=dev).to(dtype).contiguous(memory_format=torch.channels_last_3d)
+    for _ in range(3):
+        PS.CausalAttentionFn.apply(q, k, v, nh).backward(gy)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    reps = 10
+    e0.record(st)
+    for _ in range(reps):
+        y = PS.CausalAttentionFn.apply(q, k, v, nh)
+    e1.record(st)
+    for _ in range(reps):
+        y.backward(gy, retain_graph=True)
+    e2.record(st)
+    e2.synchronize()
+    tf, tb = e0.elapsed_time(e1) / reps, e1.elapsed_time(e2) / reps
+    d = c // nh
+    pairs = nh * n * (n + 1) / 2
+    res_line = {
+        "metric": f"samples/sec (PixelSNAIL prior train step) on {dims[0]}x{dims[1]}x{dims[2]} codes",
+        "value": 1000.0 / ms, "unit": "samples/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+        "data": "synthetic codes (uniform over K = 256), reference init weights, seed 0",
+        "launch": "hip_graph" if graph is not None else "eager",
+        "config": {"workload": "pixelsnail_mid_prior_train_step", "codes": list(dims), "num_embeddings": 256,
+                   "model_dim": kw["model_dim"], "blocks_x_layers": [kw["num_blocks"], kw["num_layers_per_block"]],
+                   "batch_per_gpu": 1, "global_batch": 1, "parallelism": "dp1", "final_loss": float(res.detach()),
+                   "mixup": "off (data-side blend, not part of the step's kernels)"},
+        "attention_kernel": {"positions": n, "heads": nh, "head_dim": d, "fwd_ms": tf, "bwd_ms": tb,
+                             "fwd_tflops": pairs * 4 * d / (tf * 1e-3) / 1e12,
+                             "bwd_tflops": pairs * 8 * d / (tb * 1e-3) / 1e12,
+                             "note": "fp32 VALU online softmax; per stream and block (24 per step)"},
+    }
+    if not a.no_cpu_baseline:
+        print("[bench] prior CPU baseline", file=sys.stderr, flush=True)
+        res_line["cpu_baseline"] = prior_cpu_baseline()
+    print(json.dumps(res_line), flush=True)
+
+
 def main():
     a = parse()
+    if a.prior:
+        return prior_main(a)
     import torch
     import torch.distributed as dist
 
