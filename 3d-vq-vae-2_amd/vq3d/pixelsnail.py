@@ -42,6 +42,16 @@ def _zeros_like(t):
     return ops.zero_(torch.empty_like(t))
 
 
+# the conv operand dtype of the model being run (PixelSNAIL.logits sets it): the residual streams
+# stay fp32 between blocks as under the reference's fp16 autocast (`out * self.scale` with the
+# fp32 parameter promotes, layers.py:463-465); every conv reads its operand in this dtype
+_compute = [torch.float32]
+
+
+def _operand(x):
+    return cl(x if x.dtype == _compute[0] else x.to(_compute[0]))
+
+
 # ============================================================================================ conv
 class CausalConvFn(torch.autograd.Function):
     """y = conv(prologue(x), w) + cbias on the libvq3d engines; w is the (embedded) k^3 weight.
@@ -130,10 +140,10 @@ class CausalConv3dAdd(nn.Module):
             if self.mask == "A":
                 if pro is not None:
                     x = F.elu(x + pro[0]) + pro[1]
-                x = _shift(x, i)
+                x = _shift(_operand(x), i)
             elif pro is not None:
                 pa, pb = pro
-            out.append(CausalConvFn.apply(cl(x), w, b, pa, pb, k))
+            out.append(CausalConvFn.apply(_operand(x), w, b, pa, pb, k))
         return out
 
     def forward(self, stack):
@@ -156,9 +166,9 @@ class ExpandRFConv(nn.Module):
 
     def run(self, stack):
         d, h, w = stack
-        dc = CausalConvFn.apply(d, self.depth_conv.weight, self.depth_conv.bias, None, None, 1)
+        dc = CausalConvFn.apply(_operand(d), self.depth_conv.weight, self.depth_conv.bias, None, None, 1)
         dch, dcw = torch.chunk(dc, 2, dim=1)
-        hc = CausalConvFn.apply(h, self.height_conv.weight, self.height_conv.bias, None, None, 1)
+        hc = CausalConvFn.apply(_operand(h), self.height_conv.weight, self.height_conv.bias, None, None, 1)
         return [d, cl(h + dch), cl(w + hc + dcw)]
 
     def forward(self, stack):
@@ -213,6 +223,7 @@ class PreActFixupCausalResBlock(nn.Module):
         out = _dropout3d(out, self.dropout)
         out = self.branch_conv3.run(out, pro=(self.bias3a, self.bias3b))
         skip = stack if self.skip_conv is None else self.skip_conv.run(stack)
+        # out * scale + bias4 + skip: fp32 (the 1-element fp32 parameters promote, as in the reference)
         return [cl(o * self.scale + self.bias4 + s) for o, s in zip(out, skip)]
 
     def forward(self, stack, aux=None, condition=None, condition_cache=None):
@@ -411,13 +422,14 @@ class PixelSNAIL(nn.Module):
         """forward (pixelsnail.py:301-320) of a one-hot (b, K, d, h, w) input; fp32 logits."""
         b = onehot.shape[0]
         dims = tuple(onehot.shape[2:])
+        _compute[0] = self.compute_dtype
         x = cl(onehot.to(self.compute_dtype))
         x = CausalConvFn.apply(x, self.parse_input.weight, self.parse_input.bias, None, None, 1)
         stack = self.to_causal.run([x, x, x])
         bg = background_list(b, dims, self.compute_dtype, x.device)
         for layer in self.layers:
             stack = layer.run(stack, bg)
-        s = cl(stack[0] + stack[1] + stack[2])
+        s = _operand(stack[0] + stack[1] + stack[2])
         return CausalConvFn.apply(s, self.parse_output.weight, self.parse_output.bias, None, None, 1).float()
 
     def forward(self, data, background=None, attn_mask=None, condition=None, condition_cache=None):
