@@ -1,12 +1,14 @@
 """PixelSNAIL prior over VQ-VAE codes (reference pixel_model/pixelsnail.py + pixel_model/layers.py),
 module API and state_dict of the reference, GPU path through libvq3d:
 
-* every causal 3-stack conv (CausalConv3dAdd, layers.py:122-222) runs on the hand-written conv
-  engines (conv3d.hip): the (k-1, k, k) depth, (1, k-1, k) height and (1, 1, k//2 [+1]) width
-  kernels are embedded in a zero-padded k^3 kernel whose dead taps are exactly zero, so the
-  causal front padding becomes the engines' symmetric zero padding (k = 3; k = 1 is a pointwise
-  conv); mask 'A' shifts its (pre-activated) input by one position first.  The PreAct
-  pre-activations elu(x + a) + b run as the convs' fused prologue where no padding intervenes;
+* the masked k = 3 causal 3-stack convs (CausalConv3dAdd, layers.py:122-222) run on the
+  hand-written conv engines (conv3d.hip): the (k-1, k, k) depth, (1, k-1, k) height and
+  (1, 1, k//2 + 1) width kernels are embedded in a zero-padded k^3 kernel whose dead taps are
+  exactly zero, so the causal front padding becomes the engines' symmetric zero padding; the
+  PreAct pre-activation elu(x + a) + b runs as the conv's fused prologue;
+* the 1x1x1 convs (branch 1 / 3, expand_rf, the attention projections, skip / aux, parse_input /
+  parse_output) are plain GEMMs over the voxel rows of the channels-last tensors: hipBLASLt via
+  torch.nn.functional.linear (mask 'A' shifts its pre-activated input by one position first);
 * the dense causal attention (CausalAttention, layers.py:613-647) is attention.hip: no n x n
   logits, fp32 online softmax, recomputing backward;
 * elementwise glue (shifts, residual adds, ELU of the attention aux input, Dropout3d, the
@@ -82,6 +84,44 @@ class CausalConvFn(torch.autograd.Function):
         return gx, dw, dcb, da, db, None
 
 
+class PointwiseFn(torch.autograd.Function):
+    """1x1x1 conv of a channels-last (b, c, d, h, w) tensor as GEMMs over its voxel rows
+    (hipBLASLt, fp32 accumulation).  The weight gradient sum_v g[v] (x) x[v] has the voxels as
+    its K dimension and only co x ci outputs: it runs as a batched GEMM over 256-voxel slices
+    (split K, enough workgroups to fill the chip) plus one sum over the slices."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xv = x.permute(0, 2, 3, 4, 1).reshape(-1, x.shape[1])
+        w2 = w.reshape(w.shape[0], -1)
+        y = F.linear(xv, w2.to(x.dtype), None if b is None else b.to(x.dtype))
+        ctx.save_for_backward(xv, w2)
+        ctx.shape = (x.shape[0],) + tuple(x.shape[2:])
+        ctx.has_b = b is not None
+        ctx.wshape = w.shape
+        return y.reshape(ctx.shape + (w.shape[0],)).permute(0, 4, 1, 2, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        xv, w2 = ctx.saved_tensors
+        co = w2.shape[0]
+        gv = g.permute(0, 2, 3, 4, 1).reshape(-1, co)
+        if not gv.is_contiguous():
+            gv = gv.contiguous()
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = (gv @ w2.to(gv.dtype)).reshape(ctx.shape + (w2.shape[1],)).permute(0, 4, 1, 2, 3)
+        n = gv.shape[0]
+        sk = 256 if n % 256 == 0 and n >= 4096 else n
+        gw = torch.bmm(gv.reshape(-1, sk, co).transpose(1, 2).float(), xv.reshape(-1, sk, xv.shape[1]).float()).sum(0)
+        gb = gv.float().sum(0) if ctx.has_b else None
+        return gx, gw.reshape(ctx.wshape), gb
+
+
+def pointwise(x, w, b):
+    return PointwiseFn.apply(x, w, b)
+
+
 def _embed(depth_w, height_w, width_w, k):
     """the three causal kernels inside k^3 kernels (k = 3): taps the reference never reads are 0.
     depth (k-1, k, k) at kd = 0 .. k-2 (front pad k-2 = offsets -1, 0); height (1, k-1, k) at
@@ -136,6 +176,14 @@ class CausalConv3dAdd(nn.Module):
         bs = (self.depth_conv.bias, self.height_conv.bias, self.width_conv.bias)
         out = []
         for i, (x, w, b) in enumerate(zip(stack, ws, bs)):
+            if k == 1:  # a plain GEMM over the voxels (hipBLASLt): pre-activation + shift as glue
+                if pro is not None:
+                    x = F.elu(x + pro[0]) + pro[1]
+                x = _operand(x)
+                if self.mask == "A":
+                    x = _shift(x, i)
+                out.append(pointwise(x, w, b))
+                continue
             pa = pb = None
             if self.mask == "A":
                 if pro is not None:
@@ -166,9 +214,9 @@ class ExpandRFConv(nn.Module):
 
     def run(self, stack):
         d, h, w = stack
-        dc = CausalConvFn.apply(_operand(d), self.depth_conv.weight, self.depth_conv.bias, None, None, 1)
+        dc = pointwise(_operand(d), self.depth_conv.weight, self.depth_conv.bias)
         dch, dcw = torch.chunk(dc, 2, dim=1)
-        hc = CausalConvFn.apply(_operand(h), self.height_conv.weight, self.height_conv.bias, None, None, 1)
+        hc = pointwise(_operand(h), self.height_conv.weight, self.height_conv.bias)
         return [d, cl(h + dch), cl(w + hc + dcw)]
 
     def forward(self, stack):
@@ -424,13 +472,13 @@ class PixelSNAIL(nn.Module):
         dims = tuple(onehot.shape[2:])
         _compute[0] = self.compute_dtype
         x = cl(onehot.to(self.compute_dtype))
-        x = CausalConvFn.apply(x, self.parse_input.weight, self.parse_input.bias, None, None, 1)
+        x = cl(pointwise(x, self.parse_input.weight, self.parse_input.bias))
         stack = self.to_causal.run([x, x, x])
         bg = background_list(b, dims, self.compute_dtype, x.device)
         for layer in self.layers:
             stack = layer.run(stack, bg)
         s = _operand(stack[0] + stack[1] + stack[2])
-        return CausalConvFn.apply(s, self.parse_output.weight, self.parse_output.bias, None, None, 1).float()
+        return pointwise(s, self.parse_output.weight, self.parse_output.bias).float()
 
     def forward(self, data, background=None, attn_mask=None, condition=None, condition_cache=None):
         if condition is not None or condition_cache is not None:
