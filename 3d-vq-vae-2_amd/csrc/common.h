@@ -78,6 +78,27 @@ __device__ __forceinline__ Prologue make_prologue(int kind, const float *a, cons
     return p;
 }
 
+// ---------------------------------------------------------------- XCD-aware tile schedules
+// The dispatcher places workgroup b on XCD b % 8 and every XCD has its own L2.  With a grid that
+// is a multiple of 8, a persistent kernel gives each XCD a contiguous eighth of the tiles, and
+// the XCD's workgroups walk that range side by side: the halo re-reads of neighbouring tiles and
+// the cache lines their partial D-runs share are served by one L2 instead of eight.
+struct TileSched {
+    int t, end, step;
+};
+__device__ __forceinline__ TileSched xcd_sched(int ntiles) {
+    const int G = gridDim.x, b = blockIdx.x;
+    if ((G & 7) || ntiles < G) return TileSched{b, ntiles, G};
+    const int per = (ntiles + 7) >> 3, start = (b & 7) * per;
+    return TileSched{start + (b >> 3), min(ntiles, start + per), G >> 3};
+}
+// one tile per workgroup (non-persistent grids): consecutive tiles on one XCD
+__device__ __forceinline__ int xcd_tile(int ntiles) {
+    const int G = gridDim.x, b = blockIdx.x;
+    if ((G & 7) || G != ntiles) return b;
+    return (b & 7) * (G >> 3) + (b >> 3);
+}
+
 // ---------------------------------------------------------------- reductions
 template <typename F>
 __device__ __forceinline__ F wave_sum(F v) {

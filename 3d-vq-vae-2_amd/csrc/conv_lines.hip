@@ -233,7 +233,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
     float pre = 0.f, post = 0.f;
     const bool raw = pro.kind == VQ3D_PRO_NONE;
 
-    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
+    const TileSched bsc = xcd_sched(a.nbricks);
+    for (int brick = bsc.t; brick < bsc.end; brick += bsc.step) {
         int bi = brick;
         const int bzd = bi % a.nbd; bi /= a.nbd;
         const int bzw = bi % a.nbw; bi /= a.nbw;

@@ -190,7 +190,8 @@ __global__ __launch_bounds__(NTC) void k_tc(TcArgs a, const T *__restrict__ in, 
 #pragma unroll
     for (int o = 0; o < CO; ++o) cb[o] = (!DG && fe.cbias) ? fe.cbias[o] : 0.f;
     float pre = 0.f, post = 0.f;
-    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
+    const TileSched bsc = xcd_sched(a.nbricks);
+    for (int brick = bsc.t; brick < bsc.end; brick += bsc.step) {
         int b, oh0, ow0, od0;
         brick_of(a, brick, b, oh0, ow0, od0);
         __syncthreads();
@@ -304,7 +305,8 @@ __global__ __launch_bounds__(NTC) void k_tc_wgrad(TcArgs a, const T *__restrict_
     float acc[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) acc[e] = 0.f;
-    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
+    const TileSched bsc = xcd_sched(a.nbricks);
+    for (int brick = bsc.t; brick < bsc.end; brick += bsc.step) {
         int b, oh0, ow0, od0;
         brick_of(a, brick, b, oh0, ow0, od0);
         __syncthreads();

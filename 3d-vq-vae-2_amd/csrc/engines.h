@@ -105,6 +105,6 @@ int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const 
             const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3, hipStream_t s);
 int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
             const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
-            const vq3d_preact_grads &gr, void *workspace, void *gx, hipStream_t s);
+            const vq3d_preact_grads &gr, void *workspace, void *gx, int stages, hipStream_t s);
 
 }  // namespace vq3d

@@ -78,6 +78,7 @@ constexpr int n_entries() {
 struct CArgs {
     int B, H, W, D;
     int nbh, nbw, nbd, nbricks;
+    int xcd;  // XCD-contiguous brick order (measured: faster up to 4096 bricks, slower at 32768)
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
     float *accs = reinterpret_cast<float *>(t2h + HVX * BR + PADE);  // [NV][BR] raw W2 (*) t2
     int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
-    const Org o = brick_org(a, blockIdx.x);
+    const Org o = brick_org(a, a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x));
     const Scal s = load_scal(p);
     bf16x8 fw[K::KS];
 #pragma unroll
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
     float *wred = reinterpret_cast<float *>(smem);        // after phase C: [4][NTN][64][4] over z3h / t2T
     static_assert(size_t(HVX * BR + PADE + BR * NLN * TP) * 2 >= size_t(4 * K::NTN * 256) * 4, "W2 sums fit z3h + t2T");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
-    const Org o = brick_org(a, blockIdx.x);
+    const Org o = brick_org(a, a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x));
     const Scal s = load_scal(p);
     bf16x8 fw[K::KS];
 #pragma unroll
@@ -675,6 +676,7 @@ CArgs make_args(int B, int H, int W, int D) {
     a.nbw = W / BW;
     a.nbd = D / BD;
     a.nbricks = B * a.nbh * a.nbw * a.nbd;
+    a.xcd = a.nbricks <= 4096;
     return a;
 }
 
@@ -697,17 +699,19 @@ void launch_fwd(const CArgs &a, const bf16_t *x, const float *w1, const float *w
 template <int C, int BR>
 void launch_bwd(const CArgs &a, const bf16_t *g, const bf16_t *x, const bf16_t *t2, const bf16_t *t3, const float *w1,
                 const float *w2, const float *w3, const vq3d_preact_params &p, const vq3d_preact_grads &gr, float *part,
-                bf16_t *gx, hipStream_t s) {
+                bf16_t *gx, int stages, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         allow(k_col_bwd<C, BR>, bwd_lds<C, BR>());
         attr = true;
     }
-    k_col_bwd<C, BR><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, g, x, t2, t3, w1, w2, w3, p, part, gx);
+    if (stages & 1) k_col_bwd<C, BR><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, g, x, t2, t3, w1, w2, w3, p, part, gx);
     const int nr = (a.nbricks + RCH - 1) / RCH;
     float *part2 = part + size_t(a.nbricks) * n_entries<C, BR>();
-    k_col_reduce1<C, BR><<<nr, 256, 0, s>>>(part, a.nbricks, part2);
-    k_col_reduce2<C, BR><<<(n_entries<C, BR>() + 255) / 256, 256, 0, s>>>(part2, nr, p.scale, gr);
+    if (stages & 2) {
+        k_col_reduce1<C, BR><<<nr, 256, 0, s>>>(part, a.nbricks, part2);
+        k_col_reduce2<C, BR><<<(n_entries<C, BR>() + 255) / 256, 256, 0, s>>>(part2, nr, p.scale, gr);
+    }
 }
 
 }  // namespace
@@ -738,15 +742,15 @@ int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const 
 
 int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
             const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
-            const vq3d_preact_grads &gr, void *workspace, void *gx, hipStream_t s) {
+            const vq3d_preact_grads &gr, void *workspace, void *gx, int stages, hipStream_t s) {
     const CArgs a = make_args(batch, h, w, d);
     auto G = static_cast<const bf16_t *>(g), X = static_cast<const bf16_t *>(x);
     auto T2 = static_cast<const bf16_t *>(t2), T3 = static_cast<const bf16_t *>(t3);
     auto GX = static_cast<bf16_t *>(gx);
     float *part = static_cast<float *>(workspace);
-    if (C == 2) launch_bwd<2, 1>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, s);
-    else if (C == 4) launch_bwd<4, 2>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, s);
-    else launch_bwd<8, 4>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, s);
+    if (C == 2) launch_bwd<2, 1>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, stages, s);
+    else if (C == 4) launch_bwd<4, 2>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, stages, s);
+    else launch_bwd<8, 4>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, stages, s);
     return check_launch("preact_small_bwd (column kernels)");
 }
 

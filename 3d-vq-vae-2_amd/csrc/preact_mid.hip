@@ -375,19 +375,20 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
     // the next tile's loads are in flight while the current tile computes
     LinesLd<TH, TW> lt;
     TileLd<TH, TW, C> lx;
-    if (blockIdx.x < a.ntiles) {
-        const Org o0 = tile_org(a, blockIdx.x, TH, TW);
+    const TileSched sc = xcd_sched(a.ntiles);
+    if (sc.t < sc.end) {
+        const Org o0 = tile_org(a, sc.t, TH, TW);
         lt.load(a, o0, t2);
         lx.load(a, o0, x);
     }
-    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    for (int tile = sc.t; tile < sc.end; tile += sc.step) {
         const Org o = tile_org(a, tile, TH, TW);
         __syncthreads();
         if constexpr (!(PM_EXP & 8)) {
             lt.store(t2l);
             lx.store(xs);
-            if (tile + int(gridDim.x) < a.ntiles) {
-                const Org on = tile_org(a, tile + gridDim.x, TH, TW);
+            if (tile + sc.step < sc.end) {
+                const Org on = tile_org(a, tile + sc.step, TH, TW);
                 lt.load(a, on, t2);
                 lx.load(a, on, x);
             }
@@ -552,12 +553,13 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
     float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
     // the next tile's halo loads are in flight while the current tile computes
     LinesLd<TH, TW> lz, lt;
-    if (blockIdx.x < a.ntiles) {
-        const Org o0 = tile_org(a, blockIdx.x, TH, TW);
+    const TileSched sc = xcd_sched(a.ntiles);
+    if (sc.t < sc.end) {
+        const Org o0 = tile_org(a, sc.t, TH, TW);
         lz.load(a, o0, gz3);
         lt.load(a, o0, t2);
     }
-    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    for (int tile = sc.t; tile < sc.end; tile += sc.step) {
         const Org o = tile_org(a, tile, TH, TW);
         __syncthreads();
         {
@@ -566,8 +568,8 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             lg.load(a, o, g);
             lz.store(zl);
             lt.store(tl);
-            if (tile + int(gridDim.x) < a.ntiles) {
-                const Org on = tile_org(a, tile + gridDim.x, TH, TW);
+            if (tile + sc.step < sc.end) {
+                const Org on = tile_org(a, tile + sc.step, TH, TW);
                 lz.load(a, on, gz3);
                 lt.load(a, on, t2);
             }

@@ -598,7 +598,17 @@ int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_
                           int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                           const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                           void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream) {
+    return vq3d_preact_small_bwd_stages(3, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, p, gr,
+                                        workspace, ws_bytes, gx, stream);
+}
+
+int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                                 int32_t h, int32_t w, int32_t dd, const void *g, const void *x, const void *t2,
+                                 const void *t3, const float *w1, const float *w2, const float *w3,
+                                 const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
+                                 size_t ws_bytes, void *gx, vq3d_stream_t stream) {
     SArgs a;
+    if (stages < 1 || stages > 3) return fail("preact_small_bwd: stages must be a mask of 1 | 2");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx)
         return fail("preact_small_bwd: null pointer");
     if (dtype == VQ3D_BF16 && col_supported(batch, channels, branch, h, w, dd)) {
@@ -608,7 +618,7 @@ int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_
             return fail("preact_small_bwd: every gradient buffer is required");
         if (!workspace || ws_bytes < col_workspace_bytes(batch, channels, branch, h, w, dd))
             return fail("preact_small_bwd: workspace too small");
-        return col_bwd(batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, *p, G, workspace, gx,
+        return col_bwd(batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, *p, G, workspace, gx, stages,
                        as_stream(stream));
     }
     if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
@@ -625,10 +635,11 @@ int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_
             allow_lds(k_small_bwd<C_, B_>);                                                                    \
             attr = true;                                                                                       \
         }                                                                                                      \
-        k_small_bwd<C_, B_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const bf16_t *)g, (const bf16_t *)x,        \
-                                                                (const bf16_t *)t2, (const bf16_t *)t3, w1, w2, \
-                                                                w3, *p, part, (bf16_t *)gx);                   \
-        k_small_bwd_reduce<C_, B_><<<unsigned(ne), NT, 0, s>>>(part, a.nbricks, p->scale, *gr);                 \
+        if (stages & 1)                                                                                        \
+            k_small_bwd<C_, B_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const bf16_t *)g, (const bf16_t *)x,    \
+                                                                    (const bf16_t *)t2, (const bf16_t *)t3, w1, \
+                                                                    w2, w3, *p, part, (bf16_t *)gx);           \
+        if (stages & 2) k_small_bwd_reduce<C_, B_><<<unsigned(ne), NT, 0, s>>>(part, a.nbricks, p->scale, *gr); \
     }
     Bk(2, 1) else Bk(4, 2) else Bk(8, 4)
 #undef Bk

@@ -187,6 +187,32 @@ def set_concurrent_wgrad(enabled=True):
     _concurrent = bool(enabled)
 
 
+_side_reduce = False
+
+
+def set_side_reduce(enabled=True):
+    """Issue the fused blocks' fixed-order partial-sum reductions (small / column / mid block
+    backward) on the side stream: they only read their own workspace and add into gradient
+    entries no other kernel touches, and they occupy a handful of CUs for a few microseconds
+    each, so on the main stream they are pure latency between the data kernels.  join_side()
+    must precede any read of the gradients (the optimizer and the all-reduce call it)."""
+    global _side_reduce
+    _side_reduce = bool(enabled)
+
+
+def _on_side(device, fn, *keep):
+    """Run fn() on the device's side stream after the work already queued on the current one;
+    `keep` tensors stay allocated until the side stream is done with them."""
+    main = torch.cuda.current_stream()
+    side = _side_stream(device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        fn()
+    for t in keep:
+        if t is not None:
+            t.record_stream(side)
+
+
 def _side_stream(device):
     s = _side.get(device.index)
     if s is None:
@@ -336,6 +362,10 @@ def preact_mid_bwd(g, x, t2, t3, blk, grads, stages=None, bufs=None):
             L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx))
     if stages is not None:
         L.call("vq3d_preact_mid_bwd_stages", int(stages), *args, L.stream())
+    elif _side_reduce and not _concurrent:
+        # everything but the fixed-order reduction on the main stream
+        L.call("vq3d_preact_mid_bwd_stages", 15, *args, L.stream())
+        _on_side(x.device, lambda: L.call("vq3d_preact_mid_bwd_stages", 16, *args, L.stream()), ws)
     elif _concurrent:
         # data stages (gz3, gx; gz1 to the workspace) on the main stream, the weight gradient and
         # the fixed-order reduction on the side stream (they read g / x / t2 / t3 / workspace only)
@@ -411,9 +441,13 @@ def preact_small_bwd(g, x, t2, t3, blk, grads):
     ws = workspace(nbytes, x.device)
     prm = _preact_params(blk)
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
-    L.call("vq3d_preact_small_bwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2),
-           L.ptr(t3), L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws),
-           ctypes.c_size_t(ws.numel()), L.ptr(gx), L.stream())
+    args = (L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(w1), L.ptr(w2),
+            L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx))
+    if _side_reduce:
+        L.call("vq3d_preact_small_bwd_stages", 1, *args, L.stream())
+        _on_side(x.device, lambda: L.call("vq3d_preact_small_bwd_stages", 2, *args, L.stream()), ws)
+    else:
+        L.call("vq3d_preact_small_bwd", *args, L.stream())
     return gx
 
 

@@ -252,6 +252,14 @@ int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_
                           int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                           const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                           void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream);
+/* the same in stages: 1 = the fused data / partial-sum kernel (gx, per-brick partial rows in the
+ * workspace), 2 = the fixed-order reduction of the partial rows into the gradient buffers.  Stage 2
+ * only reads the workspace, so a caller may issue it on a second stream (after stage 1). */
+int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                                 int32_t h, int32_t w, int32_t dd, const void *g, const void *x, const void *t2,
+                                 const void *t3, const float *w1, const float *w2, const float *w3,
+                                 const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
+                                 size_t ws_bytes, void *gx, vq3d_stream_t stream);
 
 /* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
 /* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),
