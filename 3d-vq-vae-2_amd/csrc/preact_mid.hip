@@ -331,18 +331,45 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
     }
 }
 
-// t3 and out of a TH x TW x 8 tile from t2 on its halo and x
-template <int TH, int TW>
+// The next block's t2 (k_pm_t2's arithmetic, bit for bit) of the tile's voxels from its bf16 out
+// in LDS: the chained forward of a run of blocks writes it here instead of a k_pm_t2 launch
+// re-reading out from HBM.
+__device__ __forceinline__ void next_t2(const bf16_t *xs, const float *w1n, const Scal &sn, bf16_t *dst, int nv) {
+    for (int v = threadIdx.x; v < nv; v += NT) {
+        const uint32_t *xr = reinterpret_cast<const uint32_t *>(xs + v * C);
+        float uu[C];
+#pragma unroll
+        for (int j = 0; j < C / 2; ++j) {
+            const uint32_t q = xr[j];
+            uu[2 * j] = elu(bf(q & 0xffffu) + sn.b1a) + sn.b1b;
+            uu[2 * j + 1] = elu(bf(q >> 16) + sn.b1a) + sn.b1b;
+        }
+#pragma unroll
+        for (int o = 0; o < BR; ++o) {
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc = fmaf(w1n[o * C + c], uu[c], acc);
+            dst[v * BR + o] = f2bf(elu(acc + sn.b2a) + sn.b2b);
+        }
+    }
+}
+
+// t3 and out of a TH x TW x 8 tile from t2 on its halo and x; CHAIN: also the next block's t2
+template <int TH, int TW, bool CHAIN>
 __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restrict__ t2, const bf16_t *__restrict__ x,
                                                const float *__restrict__ w2, const float *__restrict__ w3,
                                                vq3d_preact_params p, bf16_t *__restrict__ t3o,
-                                               bf16_t *__restrict__ out) {
+                                               bf16_t *__restrict__ out, const float *__restrict__ w1n,
+                                               vq3d_preact_params pn, bf16_t *__restrict__ t2n) {
     using T = Tile<TH, TW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *t2l = reinterpret_cast<bf16_t *>(smem);  // halo lines [NL][LSP]
+    bf16_t *t2l = reinterpret_cast<bf16_t *>(smem);  // halo lines [NL][LSP]; CHAIN: then next t2 [TV][9]
     bf16_t *t3s = t2l + T::LINES;                     // [TV][9]
     bf16_t *xs = t3s + T::S9;                         // [TV][18]: x, then out in place
+    float *w1ns = reinterpret_cast<float *>(xs + T::S18);  // CHAIN: next block's W1 [o][c]
+    static_assert(T::LINES >= T::TV * BR, "next t2 fits the halo image");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if constexpr (CHAIN) stage_w(w1ns, w1n, BR * C);
     const int row = lane & 15, kb = lane >> 4;
     bf16x8 bw2[9], bw3[2];
     {
@@ -372,6 +399,8 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
         zero_pads<TH, TW>(t2l, 1, tails, at, 2);
     }
     const Scal s = load_scal(p);
+    Scal sn{};
+    if constexpr (CHAIN) sn = load_scal(pn);
     // the next tile's loads are in flight while the current tile computes
     LinesLd<TH, TW> lt;
     TileLd<TH, TW, C> lx;
@@ -426,9 +455,14 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
             }
         }
         __syncthreads();
+        if constexpr (CHAIN) next_t2(xs, w1ns, sn, t2l, T::TV);
         if constexpr (!(PM_EXP & 4)) {
             if (t3o) store_tile<TH, TW, BR>(a, o, t3s, t3o);
             store_tile<TH, TW, C>(a, o, xs, out);
+        }
+        if constexpr (CHAIN) {
+            __syncthreads();
+            store_tile<TH, TW, BR>(a, o, t2l, t2n);
         }
     }
 }
@@ -517,23 +551,33 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
 
 // K2: per TH x TW x 8 tile: gt2 = W2^T (*) gz3 (flipped taps) -> gz1 = bf16(gt2 * elu'(t2)) ->
 // gx = g + (W1^T gz1) * elu'(x + b1a); gz1 to the workspace (k_pm_w13grad) and the b2 / b1 sums
-template <int TH, int TW>
+// CHAIN (the chained backward of a run of blocks): the PREVIOUS block's K1 -- its gz3 and its four
+// scalar partials, k_pm_bwd1's arithmetic -- from this tile's gx while it is still in LDS (gx is
+// that block's g) and the previous block's t3, instead of a k_pm_bwd1 launch re-reading gx.
+template <int TH, int TW, bool CHAIN>
 __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restrict__ gz3, const bf16_t *__restrict__ t2,
                                                 const bf16_t *__restrict__ x, const bf16_t *__restrict__ g,
                                                 const float *__restrict__ w1, const float *__restrict__ w2,
                                                 vq3d_preact_params p, bf16_t *__restrict__ gx,
-                                                bf16_t *__restrict__ gz1o, float *__restrict__ part) {
+                                                bf16_t *__restrict__ gz1o, float *__restrict__ part,
+                                                const bf16_t *__restrict__ t3p, const float *__restrict__ w3p,
+                                                vq3d_preact_params pp, bf16_t *__restrict__ gz3p,
+                                                float *__restrict__ part1p) {
     using T = Tile<TH, TW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *zl = reinterpret_cast<bf16_t *>(smem);  // gz3 halo lines
+    bf16_t *zl = reinterpret_cast<bf16_t *>(smem);  // gz3 halo lines; CHAIN: then the previous gz3 [TV][9]
     bf16_t *tl = zl + T::LINES;                       // t2 halo lines
     bf16_t *z1s = tl + T::LINES;                      // gz1 [TV][9]
     bf16_t *xs = z1s + T::S9;                         // x [TV][18]
     bf16_t *gs = xs + T::S18;                         // g [TV][18], then gx in place
     float *w1s = reinterpret_cast<float *>(gs + T::S18);  // W1 [o][c]
     float *red = w1s + BR * C;                            // [32] block sums
+    float *w3ps = red + 32;                               // CHAIN: previous W3 [co][o]
+    bf16_t *t3ps = reinterpret_cast<bf16_t *>(w3ps + C * BR);  // CHAIN: previous t3 [TV][9]
+    static_assert(T::LINES >= T::TV * BR, "previous gz3 fits the halo image");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int row = lane & 15, kb = lane >> 4;
+    if constexpr (CHAIN) stage_w(w3ps, w3p, C * BR);
     bf16x8 bw2[9];
     {
         float *w2s = reinterpret_cast<float *>(smem);  // scratch over the halo images
@@ -551,6 +595,9 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
     }
     const Scal s = load_scal(p);
     float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
+    Scal sp{};
+    if constexpr (CHAIN) sp = load_scal(pp);
+    float q4 = 0.f, q3b = 0.f, q3a = 0.f, qsc = 0.f;  // CHAIN: the previous block's K1 sums
     // the next tile's halo loads are in flight while the current tile computes
     LinesLd<TH, TW> lz, lt;
     const TileSched sc = xcd_sched(a.ntiles);
@@ -564,8 +611,10 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
         __syncthreads();
         {
             TileLd<TH, TW, C> lx, lg;
+            TileLd<TH, TW, BR> l3;
             lx.load(a, o, x);
             lg.load(a, o, g);
+            if constexpr (CHAIN) l3.load(a, o, t3p);
             lz.store(zl);
             lt.store(tl);
             if (tile + sc.step < sc.end) {
@@ -575,6 +624,7 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             }
             lx.store(xs);
             lg.store(gs);
+            if constexpr (CHAIN) l3.store(t3ps);
         }
         __syncthreads();
         for (int mt = wave; mt < T::NMT; mt += NT / 64) {
@@ -624,8 +674,53 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             }
         }
         __syncthreads();
+        if constexpr (CHAIN) {
+            // previous block: gz3 = bf16(scale W3^T gx * elu'(t3)) into the free halo image
+            for (int v = tid; v < T::TV; v += NT) {
+                float gv[C], tv[BR];
+                const uint32_t *gr = reinterpret_cast<const uint32_t *>(gs + v * C);
+#pragma unroll
+                for (int j = 0; j < C / 2; ++j) {
+                    const uint32_t q = gr[j];
+                    gv[2 * j] = bf(q & 0xffffu);
+                    gv[2 * j + 1] = bf(q >> 16);
+                    q4 += gv[2 * j] + gv[2 * j + 1];
+                }
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) tv[oo] = bf(t3ps[v * BR + oo]);
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) {
+                    float a3 = 0.f;
+#pragma unroll
+                    for (int co = 0; co < C; ++co) a3 = fmaf(w3ps[co * BR + oo], gv[co], a3);
+                    const float gt3 = a3 * sp.sc;
+                    const float z = gt3 * elu_d_act(tv[oo], sp.b3b);
+                    q3b += gt3;
+                    q3a += z;
+                    qsc = fmaf(a3, tv[oo], qsc);
+                    zl[v * BR + oo] = f2bf(z);
+                }
+            }
+        }
         store_tile<TH, TW, C>(a, o, gs, gx);
         store_tile<TH, TW, BR>(a, o, z1s, gz1o);
+        if constexpr (CHAIN) {
+            __syncthreads();
+            store_tile<TH, TW, BR>(a, o, zl, gz3p);
+        }
+    }
+    if constexpr (CHAIN) {
+        float *dp = part1p + int64_t(blockIdx.x) * NE1;
+        const float t4 = block_sum<float, NT>(q4, red);
+        const float t3b = block_sum<float, NT>(q3b, red + 8);
+        const float t3a = block_sum<float, NT>(q3a, red + 16);
+        const float tsc = block_sum<float, NT>(qsc, red + 24);
+        if (tid == 0) {
+            dp[0] = t4;
+            dp[1] = t3b;
+            dp[2] = t3a;
+            dp[3] = tsc;
+        }
     }
     float *dst = part + int64_t(blockIdx.x) * NE2;
     const float t2b = block_sum<float, NT>(s2b, red);
@@ -919,15 +1014,16 @@ __global__ __launch_bounds__(NT) void k_pm_reduce(const float *__restrict__ p1, 
 constexpr int FTH = 4, FTW = 8;  // forward tile 4 x 8 x 8 (256 voxels)
 constexpr int BTH = 4, BTW = 8;  // backward tile
 
-template <int TH, int TW>
+template <int TH, int TW, bool CHAIN>
 size_t fwd_lds() {
     using T = Tile<TH, TW>;
-    return size_t(T::LINES + T::S9 + T::S18) * 2;
+    return size_t(T::LINES + T::S9 + T::S18) * 2 + (CHAIN ? size_t(BR * C) * 4 : 0);
 }
-template <int TH, int TW>
+template <int TH, int TW, bool CHAIN>
 size_t bwd_lds() {
     using T = Tile<TH, TW>;
-    return size_t(2 * T::LINES + T::S9 + 2 * T::S18) * 2 + size_t(BR * C) * 4;
+    return size_t(2 * T::LINES + T::S9 + 2 * T::S18) * 2 + size_t(BR * C + 32) * 4 +
+           (CHAIN ? size_t(C * BR) * 4 + size_t(T::S9) * 2 : 0);
 }
 
 int n_cu() {
@@ -948,8 +1044,6 @@ int resident(K kern, size_t lds) {
     return per;
 }
 
-constexpr int kBwd1Blocks = 512;  // K1 workgroups (partial rows)
-
 PmArgs make_args(int B, int H, int W, int D, int TH, int TW) {
     PmArgs a;
     a.B = B;
@@ -963,13 +1057,20 @@ PmArgs make_args(int B, int H, int W, int D, int TH, int TW) {
     return a;
 }
 
+// resident workgroups per CU of a tile kernel (dynamic LDS opted in once)
+template <class K>
+int per_cu(K kern, size_t lds) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(lds));
+    return resident(kern, lds);
+}
+// K2 grid: both variants must give the same count (the chained variant writes the previous
+// block's K1 partial rows, whose count the reduction assumes to be the K2 grid)
 int bwd2_blocks(const PmArgs &a) {
     static int per = 0;
-    if (!per) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_bwd2<BTH, BTW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(bwd_lds<BTH, BTW>()));
-        per = resident(k_pm_bwd2<BTH, BTW>, bwd_lds<BTH, BTW>());
-    }
+    if (!per)
+        per = std::min(per_cu(k_pm_bwd2<BTH, BTW, false>, bwd_lds<BTH, BTW, false>()),
+                       per_cu(k_pm_bwd2<BTH, BTW, true>, bwd_lds<BTH, BTW, true>()));
     return std::max(1, std::min(a.ntiles, per * n_cu()));
 }
 
@@ -985,6 +1086,24 @@ void launch_w2(const PmArgs &a, int nwa, int npc, const bf16_t *gz3, const bf16_
         init = true;
     }
     k_pm_w2grad<D><<<nwa, NT9, W2c<D>::LDS, s>>>(a, int(int64_t(a.B) * a.H * a.W * a.D / CHV), npc, gz3, t2, p2a);
+}
+
+void launch_fwd(int batch, int h, int w, int dd, const void *x, const float *w2, const float *w3,
+                const vq3d_preact_params &p, void *out, const void *t2, void *t3, const float *w1n,
+                const vq3d_preact_params *pn, void *t2n, hipStream_t s) {
+    const PmArgs a = make_args(batch, h, w, dd, FTH, FTW);
+    static int per = 0;
+    if (!per)
+        per = std::min(per_cu(k_pm_fwd<FTH, FTW, false>, fwd_lds<FTH, FTW, false>()),
+                       per_cu(k_pm_fwd<FTH, FTW, true>, fwd_lds<FTH, FTW, true>()));
+    const unsigned g2 = unsigned(std::max(1, std::min(a.ntiles, per * n_cu())));
+    if (w1n)
+        k_pm_fwd<FTH, FTW, true><<<g2, NT, fwd_lds<FTH, FTW, true>(), s>>>(
+            a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, p, (bf16_t *)t3, (bf16_t *)out, w1n, *pn,
+            (bf16_t *)t2n);
+    else
+        k_pm_fwd<FTH, FTW, false><<<g2, NT, fwd_lds<FTH, FTW, false>(), s>>>(
+            a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, p, (bf16_t *)t3, (bf16_t *)out, nullptr, p, nullptr);
 }
 
 // backward workspace: K1 / K2 scalar partial rows, the W2 partials [nwa][9][NER], the W1 / G3
@@ -1003,7 +1122,7 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
     const int64_t nvox = int64_t(B) * H * W * D;  // a multiple of 512 (H, W, D % 8 == 0)
     const PmArgs a = make_args(B, H, W, D, BTH, BTW);
     m.n2 = bwd2_blocks(a);
-    m.n1 = int(std::min<int64_t>(kBwd1Blocks, nvox / NT));
+    m.n1 = m.n2;  // K1 rows: k_pm_bwd1's grid, or the next block's chained K2 grid
     m.npc = kW2Chunks;
     while ((nvox / CHV) % m.npc) m.npc >>= 1;
     m.npb = kW13Pieces;
@@ -1068,18 +1187,21 @@ int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
     const int64_t nvox = int64_t(batch) * h * w * dd;
     const unsigned g1 = unsigned(std::max<int64_t>(1, std::min<int64_t>(nvox / 2 / NT, 2048)));
     if (stages & 1) k_pm_t2<<<g1, NT, 0, s>>>(nvox, (const bf16_t *)x, w1, *p, (bf16_t *)t2);
-    const PmArgs a = make_args(batch, h, w, dd, FTH, FTW);
-    static int per = 0;
-    if (!per) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_fwd<FTH, FTW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(fwd_lds<FTH, FTW>()));
-        per = resident(k_pm_fwd<FTH, FTW>, fwd_lds<FTH, FTW>());
-    }
-    const unsigned g2 = unsigned(std::max(1, std::min(a.ntiles, per * n_cu())));
-    if (stages & 2)
-        k_pm_fwd<FTH, FTW><<<g2, NT, fwd_lds<FTH, FTW>(), s>>>(a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, *p,
-                                                           (bf16_t *)t3, (bf16_t *)out);
+    if (stages & 2) launch_fwd(batch, h, w, dd, x, w2, w3, *p, out, t2, t3, nullptr, nullptr, nullptr, s);
     return check_launch("preact_mid_fwd");
+}
+
+int vq3d_preact_mid_fwd_chain(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                              int32_t dd, const void *x, const float *w2, const float *w3,
+                              const vq3d_preact_params *p, const void *t2, void *out, void *t3,
+                              const float *next_w1, const vq3d_preact_params *next_p, void *next_t2,
+                              vq3d_stream_t stream) {
+    if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
+        return fail("preact_mid_fwd_chain: shape outside the fused mid-level block kernels");
+    if (!x || !w2 || !w3 || !p || !out || !t2) return fail("preact_mid_fwd_chain: null pointer");
+    if (next_w1 && (!next_p || !next_t2)) return fail("preact_mid_fwd_chain: next_w1 needs next_p and next_t2");
+    launch_fwd(batch, h, w, dd, x, w2, w3, *p, out, t2, t3, next_w1, next_p, next_t2, as_stream(stream));
+    return check_launch("preact_mid_fwd_chain");
 }
 
 size_t vq3d_preact_mid_workspace_bytes(int32_t batch, int32_t h, int32_t w, int32_t dd) {
@@ -1099,26 +1221,51 @@ int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
                                const void *t3, const float *w1, const float *w2, const float *w3,
                                const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
+    return vq3d_preact_mid_bwd_chain(stages, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, p,
+                                     gr, workspace, workspace_bytes, gx, nullptr, nullptr, nullptr, nullptr, 0,
+                                     stream);
+}
+
+int vq3d_preact_mid_bwd_chain(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                              int32_t h, int32_t w, int32_t dd, const void *g, const void *x, const void *t2,
+                              const void *t3, const float *w1, const float *w2, const float *w3,
+                              const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
+                              size_t workspace_bytes, void *gx, const void *prev_t3, const float *prev_w3,
+                              const vq3d_preact_params *prev_p, void *prev_workspace, size_t prev_workspace_bytes,
+                              vq3d_stream_t stream) {
     if (!vq3d_preact_mid_supported(dtype, batch, channels, branch, h, w, dd))
         return fail("preact_mid_bwd: shape outside the fused mid-level block kernels");
     if (stages < 1 || stages > 31) return fail("preact_mid_bwd: stages must be a mask of 1 | 2 | 4 | 8 | 16");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !workspace)
         return fail("preact_mid_bwd: null pointer");
     if ((stages & 2) && !gx) return fail("preact_mid_bwd: gx is required by the data stage");
+    const bool chain = prev_t3 != nullptr;
+    if (chain && (!prev_w3 || !prev_p || !prev_workspace))
+        return fail("preact_mid_bwd_chain: prev_t3 needs prev_w3, prev_p and prev_workspace");
+    if (chain && !(stages & 2)) return fail("preact_mid_bwd_chain: the chained K1 rides the data stage (2)");
     const vq3d_preact_grads &G = *gr;
     if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||
         !G.dbias3b || !G.dscale || !G.dbias4)
         return fail("preact_mid_bwd: every gradient buffer is required");
     const MidWs m = mid_ws(batch, h, w, dd, workspace);
     if (workspace_bytes < m.bytes) return fail("preact_mid_bwd: workspace too small");
+    MidWs mp{};
+    if (chain) {
+        mp = mid_ws(batch, h, w, dd, prev_workspace);
+        if (prev_workspace_bytes < mp.bytes) return fail("preact_mid_bwd_chain: previous workspace too small");
+    }
     hipStream_t s = as_stream(stream);
     const int64_t nvox = int64_t(batch) * h * w * dd;
     const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
     if (stages & 1) k_pm_bwd1<<<m.n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, m.gz3, m.p1);
-    if (stages & 2)
-        k_pm_bwd2<BTH, BTW><<<m.n2, NT, bwd_lds<BTH, BTW>(), s>>>(a, m.gz3, (const bf16_t *)t2, (const bf16_t *)x,
-                                                               (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, m.gz1,
-                                                               m.p2);
+    if ((stages & 2) && chain)
+        k_pm_bwd2<BTH, BTW, true><<<m.n2, NT, bwd_lds<BTH, BTW, true>(), s>>>(
+            a, m.gz3, (const bf16_t *)t2, (const bf16_t *)x, (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, m.gz1, m.p2,
+            (const bf16_t *)prev_t3, prev_w3, *prev_p, mp.gz3, mp.p1);
+    else if (stages & 2)
+        k_pm_bwd2<BTH, BTW, false><<<m.n2, NT, bwd_lds<BTH, BTW, false>(), s>>>(
+            a, m.gz3, (const bf16_t *)t2, (const bf16_t *)x, (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, m.gz1, m.p2,
+            nullptr, nullptr, *p, nullptr, nullptr);
     if (stages & 4) {
         const bf16_t *t2b = static_cast<const bf16_t *>(t2);
         switch (dd) {

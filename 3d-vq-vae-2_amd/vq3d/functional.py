@@ -274,6 +274,47 @@ class PreActWideFn(torch.autograd.Function):
         return (ops.cast(gs, ctx.in_dtype), None) + (None,) * len(plan.params)
 
 
+class PreActMidRunFn(torch.autograd.Function):
+    """A run of 18-channel / branch-9 PreActFixupResBlocks (preact_mid.hip), chained: each block's
+    tile kernel also writes the next block's t2 (forward) / the previous block's gz3 (backward)
+    from the tile it holds in LDS, so a run of n blocks costs n + 1 forward and 4n + 1 backward
+    launches instead of 2n and 5n, and the out / gx round trips through the pointwise kernels are
+    gone.  Numerics are the per-block path's (bit-identical t2 / gz3; only the scalar partial-sum
+    grouping of the fused stage differs)."""
+
+    @staticmethod
+    def forward(ctx, x, plan, *params):
+        save = any(ctx.needs_input_grad)
+        out, saved = ops.preact_mid_run_fwd(x, plan.blocks, save=save)
+        ctx.plan = plan
+        if save:
+            ctx.save_for_backward(*[t for trio in saved for t in trio])
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        plan = ctx.plan
+        flat = ctx.saved_tensors
+        saved = [flat[3 * i: 3 * i + 3] for i in range(len(plan.blocks))]
+
+        def grads_of(blk):
+            return {"dw1": grad_buf(blk.branch_conv1.weight), "dw2": grad_buf(blk.branch_conv2.weight),
+                    "dw3": grad_buf(blk.branch_conv3.weight), "dbias1a": grad_buf(blk.bias1a),
+                    "dbias1b": grad_buf(blk.bias1b), "dbias2a": grad_buf(blk.bias2a), "dbias2b": grad_buf(blk.bias2b),
+                    "dbias3a": grad_buf(blk.bias3a), "dbias3b": grad_buf(blk.bias3b), "dscale": grad_buf(blk.scale),
+                    "dbias4": grad_buf(blk.bias4)}
+
+        gx = ops.preact_mid_run_bwd(g, plan.blocks, saved, grads_of,
+                                    on_block_done=lambda blk: grads_ready(blk._fn_params))
+        return (gx, None) + (None,) * len(plan.params)
+
+
+def mid_run_eligible(x, blk):
+    k, s, _, up = mode_geometry(blk.mode)
+    return (stack_eligible(blk) and k == 3 and s == 1 and not up and x.is_cuda and x.dim() == 5
+            and x.shape[1] == blk.in_channels and ops.preact_mid_supported(x, blk.branch_conv1.weight.shape[0]))
+
+
 def wide_eligible(x, blk):
     return (stack_eligible(blk) and x.is_cuda and x.dim() == 5 and x.shape[1] == blk.in_channels
             and ops.preact_wide_supported(x, blk.branch_conv1.weight.shape[0]))

@@ -224,7 +224,8 @@ class BlockStack(nn.Sequential):
     """nn.Sequential (same children, same state_dict keys) whose forward runs every maximal run of
     identical PreActFixupResBlocks ('same', no skip) fused: >= 2 blocks on a tiny grid as ONE stack
     (Fn.PreActStackFn: one launch forward, one backward), a run of 72-channel / branch-36 blocks
-    through Fn.PreActWideFn (preact_wide.hip); everything else runs module by module."""
+    through Fn.PreActWideFn (preact_wide.hip), a run of 18-channel / branch-9 blocks chained through
+    Fn.PreActMidRunFn (preact_mid.hip); everything else runs module by module."""
 
     def forward(self, x):
         mods = list(self)
@@ -242,6 +243,8 @@ class BlockStack(nn.Sequential):
                     fn = Fn.PreActStackFn
                 elif Fn.wide_eligible(x, mods[i]):
                     fn = Fn.PreActWideFn
+                elif j > i and Fn.mid_run_eligible(x, mods[i]):
+                    fn = Fn.PreActMidRunFn
             if fn is not None:
                 run = tuple(mods[i:j + 1])
                 plan = self._plans.get((i, j)) if hasattr(self, "_plans") else None

@@ -187,32 +187,6 @@ def set_concurrent_wgrad(enabled=True):
     _concurrent = bool(enabled)
 
 
-_side_reduce = False
-
-
-def set_side_reduce(enabled=True):
-    """Issue the fused blocks' fixed-order partial-sum reductions (small / column / mid block
-    backward) on the side stream: they only read their own workspace and add into gradient
-    entries no other kernel touches, and they occupy a handful of CUs for a few microseconds
-    each, so on the main stream they are pure latency between the data kernels.  join_side()
-    must precede any read of the gradients (the optimizer and the all-reduce call it)."""
-    global _side_reduce
-    _side_reduce = bool(enabled)
-
-
-def _on_side(device, fn, *keep):
-    """Run fn() on the device's side stream after the work already queued on the current one;
-    `keep` tensors stay allocated until the side stream is done with them."""
-    main = torch.cuda.current_stream()
-    side = _side_stream(device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        fn()
-    for t in keep:
-        if t is not None:
-            t.record_stream(side)
-
-
 def _side_stream(device):
     s = _side.get(device.index)
     if s is None:
@@ -362,10 +336,6 @@ def preact_mid_bwd(g, x, t2, t3, blk, grads, stages=None, bufs=None):
             L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx))
     if stages is not None:
         L.call("vq3d_preact_mid_bwd_stages", int(stages), *args, L.stream())
-    elif _side_reduce and not _concurrent:
-        # everything but the fixed-order reduction on the main stream
-        L.call("vq3d_preact_mid_bwd_stages", 15, *args, L.stream())
-        _on_side(x.device, lambda: L.call("vq3d_preact_mid_bwd_stages", 16, *args, L.stream()), ws)
     elif _concurrent:
         # data stages (gz3, gx; gz1 to the workspace) on the main stream, the weight gradient and
         # the fixed-order reduction on the side stream (they read g / x / t2 / t3 / workspace only)
@@ -380,6 +350,97 @@ def preact_mid_bwd(g, x, t2, t3, blk, grads, stages=None, bufs=None):
     else:
         L.call("vq3d_preact_mid_bwd", *args, L.stream())
     return gx
+
+
+def preact_mid_run_fwd(x, blocks, save=True):
+    """A RUN of fused mid-level blocks, chained (vq3d_preact_mid_fwd_chain): the first block's t2
+    stage, then one tile launch per block that also writes the next block's t2 from its out while
+    the tile is in LDS.  Returns out and, per block, (x_i, t2_i, t3_i) (t3_i None when save=False:
+    no backward follows)."""
+    x = as_cl(x)
+    b, c, h, w, d = x.shape
+    nb = blocks[0].branch_conv1.weight.shape[0]
+    dc = L.dtype_code(x)
+    b0 = blocks[0]
+    t2 = new_act(b, nb, h, w, d, x.dtype, x.device)
+    out = torch.empty_like(x, memory_format=CL)
+    prm = _preact_params(b0)
+    L.call("vq3d_preact_mid_fwd_stages", 1, dc, b, c, nb, h, w, d, L.ptr(x), L.ptr(b0.branch_conv1.weight),
+           L.ptr(b0.branch_conv2.weight), L.ptr(b0.branch_conv3.weight), ctypes.byref(prm), L.ptr(out), L.ptr(t2),
+           None, L.stream())
+    saved = []
+    for i, blk in enumerate(blocks):
+        nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+        if i:
+            out = torch.empty_like(x, memory_format=CL)
+        t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
+        t2n = new_act(b, nb, h, w, d, x.dtype, x.device) if nxt is not None else None
+        prm = _preact_params(blk)
+        prmn = _preact_params(nxt) if nxt is not None else None
+        L.call("vq3d_preact_mid_fwd_chain", dc, b, c, nb, h, w, d, L.ptr(x), L.ptr(blk.branch_conv2.weight),
+               L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), L.ptr(t2), L.ptr(out), _p(t3),
+               None if nxt is None else L.ptr(nxt.branch_conv1.weight),
+               None if prmn is None else ctypes.byref(prmn), _p(t2n), L.stream())
+        if save:
+            saved.append((x, t2, t3))
+        x, t2 = out, t2n
+    return x, saved
+
+
+def preact_mid_run_bwd(g, blocks, saved, grads_of, on_block_done=None):
+    """Backward of preact_mid_run_fwd (vq3d_preact_mid_bwd_chain): per block, in reverse, the data
+    tile kernel also computes the PREVIOUS block's pointwise gz3 stage from its gx; the weight
+    gradients and the fixed-order reduction follow per block (on the side stream in concurrent
+    weight-gradient mode).  grads_of(blk): dict name -> fp32 gradient buffer (+=).  Returns gx of
+    the run's input."""
+    g = g if g.is_contiguous(memory_format=CL) else g.contiguous(memory_format=CL)
+    b, c, h, w, d = g.shape
+    nb = blocks[0].branch_conv1.weight.shape[0]
+    dc = L.dtype_code(g)
+    nws = int(L.query("vq3d_preact_mid_workspace_bytes", b, h, w, d))
+    ws = workspace(nws, g.device)
+    for i in reversed(range(len(blocks))):
+        blk = blocks[i]
+        x, t2, t3 = saved[i]
+        gx = torch.empty_like(x, memory_format=CL)
+        prm = _preact_params(blk)
+        gr = L.PreactGrads(*[_p(grads_of(blk).get(n)) for n, _ in L.PreactGrads._fields_])
+        if i:
+            prev = blocks[i - 1]
+            wsp = workspace(nws, g.device)
+            prmp = _preact_params(prev)
+            chain = (L.ptr(saved[i - 1][2]), L.ptr(prev.branch_conv3.weight), ctypes.byref(prmp), L.ptr(wsp),
+                     ctypes.c_size_t(nws))
+        else:
+            wsp = None
+            chain = (None, None, None, None, ctypes.c_size_t(0))
+        first = 1 if i == len(blocks) - 1 else 0
+        args = (dc, b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(blk.branch_conv1.weight),
+                L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), ctypes.byref(gr),
+                L.ptr(ws), ctypes.c_size_t(nws), L.ptr(gx))
+        if _concurrent:
+            L.call("vq3d_preact_mid_bwd_chain", first | 2, *args, *chain, L.stream())
+            _on_side(g.device, lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 28, *a, L.stream()),
+                     g, x, t2, t3, ws)
+        else:
+            L.call("vq3d_preact_mid_bwd_chain", first | 30, *args, *chain, L.stream())
+        if on_block_done is not None:
+            on_block_done(blk)
+        g, ws = gx, wsp
+    return g
+
+
+def _on_side(device, fn, *keep):
+    """Run fn() on the device's side stream after the work already queued on the current one;
+    `keep` tensors stay allocated until the side stream is done with them."""
+    main = torch.cuda.current_stream()
+    side = _side_stream(device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        fn()
+    for t in keep:
+        if t is not None:
+            t.record_stream(side)
 
 
 _small = [True, True]
@@ -443,11 +504,7 @@ def preact_small_bwd(g, x, t2, t3, blk, grads):
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
     args = (L.dtype_code(x), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(w1), L.ptr(w2),
             L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx))
-    if _side_reduce:
-        L.call("vq3d_preact_small_bwd_stages", 1, *args, L.stream())
-        _on_side(x.device, lambda: L.call("vq3d_preact_small_bwd_stages", 2, *args, L.stream()), ws)
-    else:
-        L.call("vq3d_preact_small_bwd", *args, L.stream())
+    L.call("vq3d_preact_small_bwd", *args, L.stream())
     return gx
 
 

@@ -71,8 +71,6 @@ def parse():
     p.add_argument("--concurrent-wgrad", action="store_true",
                    help="run weight gradients on a side stream, overlapped with backward-data (measured "
                         "0.3 ms/step slower than serial on the 3L-pub step now that the big blocks are fused)")
-    p.add_argument("--serial-reduce", action="store_true",
-                   help="keep the fused blocks' partial-sum reductions on the main stream (default: side stream)")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
     p.add_argument("--no-dist-graph", action="store_true", help="N > 1: never capture the collectives")
@@ -513,7 +511,6 @@ def main():
         size = tuple(a.size)
     torch.manual_seed(0)
     ops.set_concurrent_wgrad(a.concurrent_wgrad and not a.serial_wgrad)
-    ops.set_side_reduce(not a.serial_reduce)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
     if a.encode_only:

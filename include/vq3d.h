@@ -184,6 +184,26 @@ int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
                                const void *t3, const float *w1, const float *w2, const float *w3,
                                const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                size_t workspace_bytes, void *gx, vq3d_stream_t stream);
+/* Chained entries for a RUN of these blocks (block i's out is block i+1's x), each fusing the
+ * neighbouring block's pointwise stage into its tile kernel's epilogue, while the tile is in LDS:
+ *  - fwd_chain: the tile kernel only (t2 is an INPUT: stage 1 of the first block, or the previous
+ *    block's chained forward); with next_w1 != NULL it also writes the next block's t2 (next_w1,
+ *    next_p: that block's W1 and scalars) -- bit-identical to that block's own stage 1.
+ *  - bwd_chain: vq3d_preact_mid_bwd_stages; with prev_t3 != NULL the data stage (2, required) also
+ *    computes the PREVIOUS block's stage 1 (its gz3 and scalar partials, from this block's gx = its
+ *    g, prev_t3 / prev_w3 / prev_p) into prev_workspace, whose own call then omits stage 1. */
+int vq3d_preact_mid_fwd_chain(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                              int32_t dd, const void *x, const float *w2, const float *w3,
+                              const vq3d_preact_params *p, const void *t2, void *out, void *t3,
+                              const float *next_w1, const vq3d_preact_params *next_p, void *next_t2,
+                              vq3d_stream_t stream);
+int vq3d_preact_mid_bwd_chain(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                              int32_t h, int32_t w, int32_t dd, const void *g, const void *x, const void *t2,
+                              const void *t3, const float *w1, const float *w2, const float *w3,
+                              const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
+                              size_t workspace_bytes, void *gx, const void *prev_t3, const float *prev_w3,
+                              const vq3d_preact_params *prev_p, void *prev_workspace, size_t prev_workspace_bytes,
+                              vq3d_stream_t stream);
 
 /* A RUN of nblocks identical PreActFixupResBlocks (mode 'same', no skip conv) on a tiny grid
  * (batch*h*w*d <= 256, channels <= 32, branch <= 16, both multiples of 4): forward in ONE launch,

@@ -185,3 +185,52 @@ def test_fused_mid_block_side_stream(gpu, shape):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     for n in a[2]:
         assert torch.equal(a[2][n], b[2][n]), n
+
+
+def _run_chain(blocks, x, gy, gpu, chained, concurrent=False):
+    """A run of blocks through layers.BlockStack (chained: Fn.PreActMidRunFn) or block by block
+    (Fn.PreActBlockFn); returns out, gx and every parameter gradient, all as float64 on the CPU."""
+    from vq3d import functional as Fn, ops
+    from vq3d import layers as VL
+    stack = VL.BlockStack(*[b for b in blocks]).to(gpu)
+    for p in stack.parameters():
+        p.grad = None
+    xd = x.to(gpu).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
+    ops.set_concurrent_wgrad(concurrent)
+    try:
+        if chained:
+            out = stack(xd)
+        else:
+            out = xd
+            for b in stack:
+                out = Fn.PreActBlockFn.apply(out, b, *b._fn_params)
+        out.backward(gy.to(gpu).bfloat16().contiguous(memory_format=CL))
+        ops.join_side()
+    finally:
+        ops.set_concurrent_wgrad(False)
+    torch.cuda.synchronize()
+    grads = {n: p.grad.double().cpu().clone() for n, p in stack.named_parameters()}
+    return out.double().cpu(), xd.grad.double().cpu(), grads
+
+
+@pytest.mark.parametrize("shape,nblk,concurrent", [((2, 18, 16, 8, 16), 4, False), ((1, 18, 32, 16, 16), 3, True),
+                                                   ((1, 18, 128, 128, 32), 3, False)])
+def test_mid_run_chain_matches_per_block(gpu, shape, nblk, concurrent):
+    """The chained run (next block's t2 in the forward tile epilogue, previous block's gz3 in the
+    backward tile epilogue) against the same blocks run one by one: out, gx and every weight
+    gradient bit-identical (same roundings, same orders); the four scalars whose partial sums the
+    chained stage groups differently (bias4, bias3b, bias3a, scale) within 1e-5 relative."""
+    blocks = [_block(seed=20 + i) for i in range(nblk)]
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(shape, generator=g).bfloat16().double()
+    gy = torch.randn(shape, generator=g).bfloat16().double()
+    a = _run_chain(blocks, x, gy, gpu, chained=False)
+    b = _run_chain(blocks, x, gy, gpu, chained=True, concurrent=concurrent)
+    assert torch.equal(a[0], b[0]), float((a[0] - b[0]).abs().max())
+    assert torch.equal(a[1], b[1]), float((a[1] - b[1]).abs().max())
+    regrouped = ("bias4", "bias3b", "bias3a", "scale")
+    for n in a[2]:
+        if n.split(".")[-1] in regrouped:
+            assert float((a[2][n] - b[2][n]).abs().max()) <= 1e-5 * max(1.0, float(a[2][n].abs().max())), n
+        else:
+            assert torch.equal(a[2][n], b[2][n]), (n, float((a[2][n] - b[2][n]).abs().max()))
