@@ -346,6 +346,7 @@ __device__ __forceinline__ void next_t2(const bf16_t *xs, const float *w1n, cons
         }
 #pragma unroll
         for (int o = 0; o < BR; ++o) {
+            asm volatile("" ::: "memory");  // one W1 row in registers at a time (not all 162 hoisted)
             float acc = 0.f;
 #pragma unroll
             for (int c = 0; c < C; ++c) acc = fmaf(w1n[o * C + c], uu[c], acc);
@@ -690,6 +691,7 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
                 for (int oo = 0; oo < BR; ++oo) tv[oo] = bf(t3ps[v * BR + oo]);
 #pragma unroll
                 for (int oo = 0; oo < BR; ++oo) {
+                    asm volatile("" ::: "memory");  // one W3 column in registers at a time
                     float a3 = 0.f;
 #pragma unroll
                     for (int co = 0; co < C; ++co) a3 = fmaf(w3ps[co * BR + oo], gv[co], a3);
