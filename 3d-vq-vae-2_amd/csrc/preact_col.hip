@@ -622,7 +622,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
 // stage 2 sums the stage-1 rows per entry in order and adds into the gradient buffers.
 constexpr int RCH = 128;
 template <int C, int BR>
-__global__ __launch_bounds__(256) void k_col_reduce1(const float *__restrict__ part, int nb, float *__restrict__ part2) {
+__device__ __forceinline__ void col_reduce1(const float *__restrict__ part, int nb, float *__restrict__ part2) {
     constexpr int NE = n_entries<C, BR>();
     const int b0 = blockIdx.x * RCH, b1 = min(nb, b0 + RCH);
     for (int e = threadIdx.x; e < NE; e += 256) {
@@ -633,8 +633,34 @@ __global__ __launch_bounds__(256) void k_col_reduce1(const float *__restrict__ p
     }
 }
 template <int C, int BR>
+__global__ __launch_bounds__(256) void k_col_reduce1(const float *__restrict__ part, int nb, float *__restrict__ part2) {
+    col_reduce1<C, BR>(part, nb, part2);
+}
+template <int C, int BR>
+__device__ __forceinline__ void col_reduce2(const float *__restrict__ part2, int nr, const float *__restrict__ scale,
+                                            const vq3d_preact_grads &gr);
+template <int C, int BR>
 __global__ __launch_bounds__(256) void k_col_reduce2(const float *__restrict__ part2, int nr, const float *__restrict__ scale,
                                                      vq3d_preact_grads gr) {
+    col_reduce2<C, BR>(part2, nr, scale, gr);
+}
+// both stages for a whole run of blocks (blockIdx.y = block; its workspace at y * stride floats,
+// its gradient / scale pointers from the run's [block][11] device tables)
+template <int C, int BR>
+__global__ __launch_bounds__(256) void k_col_reduce1_run(float *__restrict__ ws, size_t stride, int nb) {
+    float *part = ws + blockIdx.y * stride;
+    col_reduce1<C, BR>(part, nb, part + size_t(nb) * n_entries<C, BR>());
+}
+template <int C, int BR>
+__global__ __launch_bounds__(256) void k_col_reduce2_run(const float *__restrict__ ws, size_t stride, int nb, int nr,
+                                                         float *const *gtab, const float *const *ptab) {
+    float *const *g = gtab + blockIdx.y * 11;
+    const vq3d_preact_grads gr{g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10]};
+    col_reduce2<C, BR>(ws + blockIdx.y * stride + size_t(nb) * n_entries<C, BR>(), nr, ptab[blockIdx.y * 11 + 9], gr);
+}
+template <int C, int BR>
+__device__ __forceinline__ void col_reduce2(const float *__restrict__ part2, int nr, const float *__restrict__ scale,
+                                            const vq3d_preact_grads &gr) {
     constexpr int E1 = BR * C, E2 = 27 * BR * BR, E3 = BR * C, NE = n_entries<C, BR>();
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (e >= NE) return;
@@ -715,6 +741,26 @@ void launch_bwd(const CArgs &a, const bf16_t *g, const bf16_t *x, const bf16_t *
 }
 
 }  // namespace
+
+template <int C, int BR>
+void launch_reduce_run(const CArgs &a, int nblocks, float *ws, size_t stride_f, float *const *gtab,
+                       const float *const *ptab, hipStream_t s) {
+    const int nr = (a.nbricks + RCH - 1) / RCH;
+    k_col_reduce1_run<C, BR><<<dim3(nr, nblocks), 256, 0, s>>>(ws, stride_f, a.nbricks);
+    k_col_reduce2_run<C, BR><<<dim3((n_entries<C, BR>() + 255) / 256, nblocks), 256, 0, s>>>(ws, stride_f, a.nbricks,
+                                                                                        nr, gtab, ptab);
+}
+
+int col_reduce_run(int nblocks, int batch, int C, int BR, int h, int w, int d, void *workspaces, size_t stride,
+                   float *const *gtab, const float *const *ptab, hipStream_t s) {
+    const CArgs a = make_args(batch, h, w, d);
+    float *ws = static_cast<float *>(workspaces);
+    const size_t sf = stride / 4;
+    if (C == 2) launch_reduce_run<2, 1>(a, nblocks, ws, sf, gtab, ptab, s);
+    else if (C == 4) launch_reduce_run<4, 2>(a, nblocks, ws, sf, gtab, ptab, s);
+    else launch_reduce_run<8, 4>(a, nblocks, ws, sf, gtab, ptab, s);
+    return check_launch("preact_small_reduce_run (column kernels)");
+}
 
 bool col_supported(int batch, int C, int BR, int h, int w, int d) {
     const bool shape = (C == 2 && BR == 1) || (C == 4 && BR == 2) || (C == 8 && BR == 4);

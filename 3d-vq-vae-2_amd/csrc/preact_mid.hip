@@ -959,9 +959,9 @@ struct RedOut {
 
 constexpr int NBA = (9 * NER + 31) / 32, NBB = (NEB + 31) / 32;
 
-__global__ __launch_bounds__(NT) void k_pm_reduce(const float *__restrict__ p1, int n1, const float *__restrict__ p2,
-                                                  int n2, const float *__restrict__ p2a, int nwa,
-                                                  const float *__restrict__ p2b, int nchb, RedOut o) {
+__device__ __forceinline__ void pm_reduce(const float *__restrict__ p1, int n1, const float *__restrict__ p2, int n2,
+                                          const float *__restrict__ p2a, int nwa, const float *__restrict__ p2b,
+                                          int nchb, const RedOut &o) {
     __shared__ float sm[8][32];
     const int el = threadIdx.x & 31, rg = threadIdx.x >> 5;
     const int blk = blockIdx.x;
@@ -1010,6 +1010,26 @@ __global__ __launch_bounds__(NT) void k_pm_reduce(const float *__restrict__ p1, 
         float *const sl[NE1 + NE2] = {o.db4, o.db3b, o.db3a, o.dscale, o.db2b, o.db2a, o.db1b, o.db1a};
         *sl[e] += t;
     }
+}
+
+__global__ __launch_bounds__(NT) void k_pm_reduce(const float *__restrict__ p1, int n1, const float *__restrict__ p2,
+                                                  int n2, const float *__restrict__ p2a, int nwa,
+                                                  const float *__restrict__ p2b, int nchb, RedOut o) {
+    pm_reduce(p1, n1, p2, n2, p2a, nwa, p2b, nchb, o);
+}
+
+// K4 of a whole run of blocks in one launch (blockIdx.y = block): block y's workspace at
+// base + y * stride (same layout for every block), its gradient / scale pointers from the run's
+// device tables [block][11] (w1, w2, w3, bias1a, bias1b, bias2a, bias2b, bias3a, bias3b, scale,
+// bias4).  Entry for entry the same fixed-order sums as k_pm_reduce.
+__global__ __launch_bounds__(NT) void k_pm_reduce_run(const char *__restrict__ base, size_t stride, int64_t o1,
+                                                      int n1, int64_t o2, int n2, int64_t oa, int nwa, int64_t ob,
+                                                      int nchb, float *const *gtab, const float *const *ptab) {
+    const char *ws = base + size_t(blockIdx.y) * stride;
+    float *const *g = gtab + blockIdx.y * 11;
+    const RedOut o{g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], ptab[blockIdx.y * 11 + 9]};
+    pm_reduce(reinterpret_cast<const float *>(ws + o1), n1, reinterpret_cast<const float *>(ws + o2), n2,
+              reinterpret_cast<const float *>(ws + oa), nwa, reinterpret_cast<const float *>(ws + ob), nchb, o);
 }
 
 // ============================================================================================ host
@@ -1216,6 +1236,23 @@ int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
                         void *workspace, size_t workspace_bytes, void *gx, vq3d_stream_t stream) {
     return vq3d_preact_mid_bwd_stages(31, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, p, gr,
                                       workspace, workspace_bytes, gx, stream);
+}
+
+int vq3d_preact_mid_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                               const void *workspaces, size_t workspace_stride, float *const *grads,
+                               const float *const *params, vq3d_stream_t stream) {
+    if (!vq3d_preact_mid_supported(VQ3D_BF16, batch, C, BR, h, w, dd))
+        return fail("preact_mid_reduce_run: shape outside the fused mid-level block kernels");
+    if (nblocks < 1 || nblocks > 65535 || !workspaces || !grads || !params)
+        return fail("preact_mid_reduce_run: bad arguments");
+    char *const b0 = static_cast<char *>(const_cast<void *>(workspaces));
+    const MidWs m = mid_ws(batch, h, w, dd, b0);
+    if (workspace_stride < m.bytes || workspace_stride % 256)
+        return fail("preact_mid_reduce_run: workspace stride below vq3d_preact_mid_workspace_bytes or unaligned");
+    auto off = [&](const void *p) { return int64_t(static_cast<const char *>(p) - b0); };
+    k_pm_reduce_run<<<dim3(NBA + NBB + 1, unsigned(nblocks)), NT, 0, as_stream(stream)>>>(
+        b0, workspace_stride, off(m.p1), m.n1, off(m.p2), m.n2, off(m.p2a), m.nwa, off(m.p2b), m.nchb, grads, params);
+    return check_launch("preact_mid_reduce_run");
 }
 
 int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,

@@ -453,8 +453,8 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
 
 // sum of one gradient entry's per-brick partials (fixed order), added to its gradient
 template <int C, int BR>
-__global__ __launch_bounds__(NT) void k_small_bwd_reduce(const float *__restrict__ part, int nb,
-                                                        const float *__restrict__ scale, vq3d_preact_grads gr) {
+__device__ __forceinline__ void small_bwd_reduce(const float *__restrict__ part, int nb, const float *__restrict__ scale,
+                                                 const vq3d_preact_grads &gr) {
     constexpr int E1 = C * BR, E2 = 27 * BR * BR, E = n_entries(C, BR);
     __shared__ float red[NT / 64];
     const int e = blockIdx.x;
@@ -479,6 +479,20 @@ __global__ __launch_bounds__(NT) void k_small_bwd_reduce(const float *__restrict
         dst = sl[e - E];
     }
     if (dst) *dst += v;
+}
+template <int C, int BR>
+__global__ __launch_bounds__(NT) void k_small_bwd_reduce(const float *__restrict__ part, int nb,
+                                                        const float *__restrict__ scale, vq3d_preact_grads gr) {
+    small_bwd_reduce<C, BR>(part, nb, scale, gr);
+}
+// a whole run of blocks (blockIdx.y = block; workspace at y * stride floats, pointers from the
+// run's [block][11] device tables)
+template <int C, int BR>
+__global__ __launch_bounds__(NT) void k_small_bwd_reduce_run(const float *__restrict__ ws, size_t stride, int nb,
+                                                            float *const *gtab, const float *const *ptab) {
+    float *const *g = gtab + blockIdx.y * 11;
+    const vq3d_preact_grads gr{g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10]};
+    small_bwd_reduce<C, BR>(ws + blockIdx.y * stride, nb, ptab[blockIdx.y * 11 + 9], gr);
 }
 
 // ------------------------------------------------------------------------------------ planning
@@ -644,6 +658,31 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
     Bk(2, 1) else Bk(4, 2) else Bk(8, 4)
 #undef Bk
     return check_launch("preact_small_bwd");
+}
+
+int vq3d_preact_small_reduce_run(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                                 int32_t w, int32_t dd, const void *workspaces, size_t workspace_stride,
+                                 float *const *grads, const float *const *params, vq3d_stream_t stream) {
+    if (nblocks < 1 || nblocks > 65535 || !workspaces || !grads || !params)
+        return fail("preact_small_reduce_run: bad arguments");
+    const size_t need = vq3d_preact_small_workspace_bytes(batch, channels, branch, h, w, dd);
+    if (!need || workspace_stride < need || workspace_stride % 256)
+        return fail("preact_small_reduce_run: shape unsupported, or stride below the workspace size / unaligned");
+    void *ws = const_cast<void *>(workspaces);
+    hipStream_t s = as_stream(stream);
+    if (col_supported(batch, channels, branch, h, w, dd))
+        return col_reduce_run(nblocks, batch, channels, branch, h, w, dd, ws, workspace_stride, grads, params, s);
+    SArgs a;
+    if (!plan(batch, channels, branch, h, w, dd, a)) return fail("preact_small_reduce_run: unsupported shape");
+    const int ne = n_entries(channels, branch) + kNScal;
+    const float *wsf = static_cast<const float *>(ws);
+#define Rk(C_, B_)                                                                                             \
+    if (channels == C_ && branch == B_)                                                                        \
+        k_small_bwd_reduce_run<C_, B_><<<dim3(unsigned(ne), unsigned(nblocks)), NT, 0, s>>>(                    \
+            wsf, workspace_stride / 4, a.nbricks, grads, params);
+    Rk(2, 1) else Rk(4, 2) else Rk(8, 4)
+#undef Rk
+    return check_launch("preact_small_reduce_run");
 }
 
 }  // extern "C"

@@ -67,6 +67,7 @@ _SIGS = {
     "vq3d_preact_mid_bwd_stages": (c_int, [c_int] * 8 + [P] * 10 + [c_size, P, P]),
     "vq3d_preact_mid_fwd_chain": (c_int, [c_int] * 7 + [P] * 11),
     "vq3d_preact_mid_bwd_chain": (c_int, [c_int] * 8 + [P] * 10 + [c_size, P] + [P] * 4 + [c_size, P]),
+    "vq3d_preact_mid_reduce_run": (c_int, [c_int] * 5 + [P, c_size, P, P, P]),
     "vq3d_preact_stack_supported": (c_int, [c_int] * 6),
     "vq3d_preact_stack_saved_floats": (c_size, [c_int] * 7),
     "vq3d_preact_stack_fwd": (c_int, [c_int] * 8 + [P] * 5),
@@ -84,6 +85,7 @@ _SIGS = {
     "vq3d_preact_small_fwd": (c_int, [c_int] * 7 + [P] * 9),
     "vq3d_preact_small_bwd": (c_int, [c_int] * 7 + [P] * 10 + [c_size, P, P]),
     "vq3d_preact_small_bwd_stages": (c_int, [c_int] * 8 + [P] * 10 + [c_size, P, P]),
+    "vq3d_preact_small_reduce_run": (c_int, [c_int] * 7 + [P, c_size, P, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),
     "vq3d_vq_nearest": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, c_int, P, P, P, P]),
     "vq3d_vq_commit_loss": (c_int, [P, c_float, P, P]),

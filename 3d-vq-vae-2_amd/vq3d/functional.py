@@ -182,11 +182,16 @@ class StackPlan:
         self.params = [_prm_tensor(b, n) for b in self.blocks for n in _PRM]
         self.key = None
 
+    def grad_ptrs(self, i):
+        """gradient buffer addresses of block i (in the table order), after tables()"""
+        return self.gptrs[i * len(_PRM): (i + 1) * len(_PRM)]
+
     def tables(self, dev):
         for p in self.params:
             grad_buf(p)
         key = tuple(p.data_ptr() for p in self.params) + tuple(p.grad.data_ptr() for p in self.params)
         if key != self.key:
+            self.gptrs = [p.grad.data_ptr() for p in self.params]
             n = len(self.params)
             self.ptab = torch.tensor([p.data_ptr() for p in self.params], dtype=torch.int64).to(dev)
             self.gtab = torch.tensor([p.grad.data_ptr() for p in self.params], dtype=torch.int64).to(dev)
@@ -277,9 +282,9 @@ class PreActWideFn(torch.autograd.Function):
 class PreActMidRunFn(torch.autograd.Function):
     """A run of 18-channel / branch-9 PreActFixupResBlocks (preact_mid.hip), chained: each block's
     tile kernel also writes the next block's t2 (forward) / the previous block's gz3 (backward)
-    from the tile it holds in LDS, so a run of n blocks costs n + 1 forward and 4n + 1 backward
-    launches instead of 2n and 5n, and the out / gx round trips through the pointwise kernels are
-    gone.  Numerics are the per-block path's (bit-identical t2 / gz3; only the scalar partial-sum
+    from the tile it holds in LDS, and the fixed-order gradient reductions of all blocks run as one
+    launch, so a run of n blocks costs n + 1 forward and 3n + 2 backward launches instead of 2n and
+    5n, and the out / gx round trips through the pointwise kernels are gone.  Numerics are the per-block path's (bit-identical t2 / gz3; only the scalar partial-sum
     grouping of the fused stage differs)."""
 
     @staticmethod
@@ -297,16 +302,44 @@ class PreActMidRunFn(torch.autograd.Function):
         flat = ctx.saved_tensors
         saved = [flat[3 * i: 3 * i + 3] for i in range(len(plan.blocks))]
 
-        def grads_of(blk):
-            return {"dw1": grad_buf(blk.branch_conv1.weight), "dw2": grad_buf(blk.branch_conv2.weight),
-                    "dw3": grad_buf(blk.branch_conv3.weight), "dbias1a": grad_buf(blk.bias1a),
-                    "dbias1b": grad_buf(blk.bias1b), "dbias2a": grad_buf(blk.bias2a), "dbias2b": grad_buf(blk.bias2b),
-                    "dbias3a": grad_buf(blk.bias3a), "dbias3b": grad_buf(blk.bias3b), "dscale": grad_buf(blk.scale),
-                    "dbias4": grad_buf(blk.bias4)}
-
-        gx = ops.preact_mid_run_bwd(g, plan.blocks, saved, grads_of,
-                                    on_block_done=lambda blk: grads_ready(blk._fn_params))
+        gx = ops.preact_mid_run_bwd(g, plan, saved, on_done=lambda: grads_ready(plan.params))
         return (gx, None) + (None,) * len(plan.params)
+
+
+class PreActSmallRunFn(torch.autograd.Function):
+    """A run of few-channel PreActFixupResBlocks ((C, branch) = (2, 1), (4, 2), (8, 4); preact_small.hip /
+    preact_col.hip): the fused forward per block, the fused backward per block into slices of one
+    run workspace, and the fixed-order gradient reductions of all blocks as one launch pair at the
+    end (instead of one or two small launches per block).  Numerics are the per-block path's."""
+
+    @staticmethod
+    def forward(ctx, x, plan, *params):
+        save = any(ctx.needs_input_grad)
+        saved = []
+        for blk in plan.blocks:
+            out, t2, t3 = ops.preact_small_fwd(x, blk, save=save)
+            if save:
+                saved += [x, t2, t3]
+            x = out
+        ctx.plan = plan
+        if save:
+            ctx.save_for_backward(*saved)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        plan = ctx.plan
+        flat = ctx.saved_tensors
+        saved = [flat[3 * i: 3 * i + 3] for i in range(len(plan.blocks))]
+        gx = ops.preact_small_run_bwd(g, plan, saved, on_done=lambda: grads_ready(plan.params))
+        return (gx, None) + (None,) * len(plan.params)
+
+
+def small_run_eligible(x, blk):
+    k, s, _, up = mode_geometry(blk.mode)
+    return (stack_eligible(blk) and k == 3 and s == 1 and not up and x.is_cuda and x.dim() == 5
+            and x.shape[1] == blk.in_channels and ops.preact_small_supported(x, blk.branch_conv1.weight.shape[0])
+            and ops.small_backward_fused(x))
 
 
 def mid_run_eligible(x, blk):

@@ -225,7 +225,8 @@ class BlockStack(nn.Sequential):
     identical PreActFixupResBlocks ('same', no skip) fused: >= 2 blocks on a tiny grid as ONE stack
     (Fn.PreActStackFn: one launch forward, one backward), a run of 72-channel / branch-36 blocks
     through Fn.PreActWideFn (preact_wide.hip), a run of 18-channel / branch-9 blocks chained through
-    Fn.PreActMidRunFn (preact_mid.hip); everything else runs module by module."""
+    Fn.PreActMidRunFn (preact_mid.hip), a run of few-channel blocks through Fn.PreActSmallRunFn
+    (one reduction for the whole run); everything else runs module by module."""
 
     def forward(self, x):
         mods = list(self)
@@ -245,6 +246,8 @@ class BlockStack(nn.Sequential):
                     fn = Fn.PreActWideFn
                 elif j > i and Fn.mid_run_eligible(x, mods[i]):
                     fn = Fn.PreActMidRunFn
+                elif j > i and Fn.small_run_eligible(x, mods[i]):
+                    fn = Fn.PreActSmallRunFn
             if fn is not None:
                 run = tuple(mods[i:j + 1])
                 plan = self._plans.get((i, j)) if hasattr(self, "_plans") else None

@@ -387,46 +387,54 @@ def preact_mid_run_fwd(x, blocks, save=True):
     return x, saved
 
 
-def preact_mid_run_bwd(g, blocks, saved, grads_of, on_block_done=None):
+def preact_mid_run_bwd(g, plan, saved, on_done=None):
     """Backward of preact_mid_run_fwd (vq3d_preact_mid_bwd_chain): per block, in reverse, the data
-    tile kernel also computes the PREVIOUS block's pointwise gz3 stage from its gx; the weight
-    gradients and the fixed-order reduction follow per block (on the side stream in concurrent
-    weight-gradient mode).  grads_of(blk): dict name -> fp32 gradient buffer (+=).  Returns gx of
-    the run's input."""
+    tile kernel also computes the PREVIOUS block's pointwise gz3 stage from its gx, and the weight
+    gradient kernels follow (on the side stream in concurrent weight-gradient mode); every block's
+    workspace is a slice of one run buffer, so the fixed-order reductions of all blocks run as ONE
+    launch at the end (vq3d_preact_mid_reduce_run, plan's device tables).  Returns gx of the run's
+    input; on_done() runs once the reduction is enqueued."""
+    blocks = plan.blocks
     g = g if g.is_contiguous(memory_format=CL) else g.contiguous(memory_format=CL)
     b, c, h, w, d = g.shape
     nb = blocks[0].branch_conv1.weight.shape[0]
     dc = L.dtype_code(g)
     nws = int(L.query("vq3d_preact_mid_workspace_bytes", b, h, w, d))
-    ws = workspace(nws, g.device)
+    stride = (nws + 255) // 256 * 256
+    run_ws = workspace(stride * len(blocks), g.device)
+    base = run_ws.data_ptr()
+    ptab, gtab = plan.tables(g.device)
     for i in reversed(range(len(blocks))):
         blk = blocks[i]
         x, t2, t3 = saved[i]
         gx = torch.empty_like(x, memory_format=CL)
         prm = _preact_params(blk)
-        gr = L.PreactGrads(*[_p(grads_of(blk).get(n)) for n, _ in L.PreactGrads._fields_])
+        gr = L.PreactGrads(*[ctypes.c_void_p(int(gp)) for gp in plan.grad_ptrs(i)])
         if i:
             prev = blocks[i - 1]
-            wsp = workspace(nws, g.device)
             prmp = _preact_params(prev)
-            chain = (L.ptr(saved[i - 1][2]), L.ptr(prev.branch_conv3.weight), ctypes.byref(prmp), L.ptr(wsp),
-                     ctypes.c_size_t(nws))
+            chain = (L.ptr(saved[i - 1][2]), L.ptr(prev.branch_conv3.weight), ctypes.byref(prmp),
+                     ctypes.c_void_p(base + (i - 1) * stride), ctypes.c_size_t(nws))
         else:
-            wsp = None
             chain = (None, None, None, None, ctypes.c_size_t(0))
         first = 1 if i == len(blocks) - 1 else 0
         args = (dc, b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(blk.branch_conv1.weight),
                 L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), ctypes.byref(gr),
-                L.ptr(ws), ctypes.c_size_t(nws), L.ptr(gx))
+                ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws), L.ptr(gx))
         if _concurrent:
             L.call("vq3d_preact_mid_bwd_chain", first | 2, *args, *chain, L.stream())
-            _on_side(g.device, lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 28, *a, L.stream()),
-                     g, x, t2, t3, ws)
+            _on_side(g.device, lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 12, *a, L.stream()),
+                     g, x, t2, t3)
         else:
-            L.call("vq3d_preact_mid_bwd_chain", first | 30, *args, *chain, L.stream())
-        if on_block_done is not None:
-            on_block_done(blk)
-        g, ws = gx, wsp
+            L.call("vq3d_preact_mid_bwd_chain", first | 14, *args, *chain, L.stream())
+        g = gx
+    red = (len(blocks), b, h, w, d, ctypes.c_void_p(base), ctypes.c_size_t(stride), L.ptr(gtab), L.ptr(ptab))
+    if _concurrent:
+        _on_side(g.device, lambda: L.call("vq3d_preact_mid_reduce_run", *red, L.stream()), run_ws, ptab, gtab)
+    else:
+        L.call("vq3d_preact_mid_reduce_run", *red, L.stream())
+    if on_done is not None:
+        on_done()
     return g
 
 
@@ -506,6 +514,39 @@ def preact_small_bwd(g, x, t2, t3, blk, grads):
             L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(ws.numel()), L.ptr(gx))
     L.call("vq3d_preact_small_bwd", *args, L.stream())
     return gx
+
+
+def preact_small_run_bwd(g, plan, saved, on_done=None):
+    """Backward of a run of fused few-channel blocks (the forward is per block, preact_small_fwd):
+    per block, in reverse, the fused data / partial-sum kernel (vq3d_preact_small_bwd_stages 1) into
+    its slice of one run workspace, then the fixed-order reductions of every block as one launch
+    pair (vq3d_preact_small_reduce_run, plan's device tables).  Returns gx of the run's input."""
+    blocks = plan.blocks
+    g = g if g.is_contiguous(memory_format=CL) else g.contiguous(memory_format=CL)
+    b, c, h, w, d = g.shape
+    nb = blocks[0].branch_conv1.weight.shape[0]
+    dc = L.dtype_code(g)
+    nws = int(L.query("vq3d_preact_small_workspace_bytes", b, c, nb, h, w, d))
+    stride = (nws + 255) // 256 * 256
+    run_ws = workspace(stride * len(blocks), g.device)
+    base = run_ws.data_ptr()
+    ptab, gtab = plan.tables(g.device)
+    for i in reversed(range(len(blocks))):
+        blk = blocks[i]
+        x, t2, t3 = saved[i]
+        gx = torch.empty_like(x, memory_format=CL)
+        prm = _preact_params(blk)
+        gr = L.PreactGrads(*[ctypes.c_void_p(int(gp)) for gp in plan.grad_ptrs(i)])
+        L.call("vq3d_preact_small_bwd_stages", 1, dc, b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
+               L.ptr(blk.branch_conv1.weight), L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight),
+               ctypes.byref(prm), ctypes.byref(gr), ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws),
+               L.ptr(gx), L.stream())
+        g = gx
+    L.call("vq3d_preact_small_reduce_run", len(blocks), b, c, nb, h, w, d, ctypes.c_void_p(base),
+           ctypes.c_size_t(stride), L.ptr(gtab), L.ptr(ptab), L.stream())
+    if on_done is not None:
+        on_done()
+    return g
 
 
 # ------------------------------------------------------------------------------------------------ wide blocks

@@ -118,16 +118,37 @@ def probe_mid(dev, kind):
     ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, bufs=(gx, ws))
     wb = (18 * 9 * 2 + 9 * 9 * 27) * 4
     fl_pw, fl_k3 = 2.0 * nv * 18 * 9, 2.0 * nv * 9 * 9 * 27
-    if kind == "k_pm_fwd":  # t3 and out from t2 (halo) and x: reads t2 9 + x 18, writes t3 9 + out 18
-        return (lambda: ops.preact_mid_fwd(x, blk, stages=2, bufs=(out, t2, t3)), nv * 54 * 2 + wb, fl_k3 + fl_pw,
-                "k_pm_fwd: fused 18-ch block t3 + out (3x3x3 9->9 + 1x1 9->18 + residual) @128x128x32 bf16")
+    # the step runs 49 of a run's 50 blocks through the CHAINED tile kernels (vq3d.h *_chain): the
+    # probes launch those, with the same block standing in as its own neighbour
+    import ctypes
+    dc, w1, w2, w3 = L.dtype_code(x), blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
+    prm = ops._preact_params(blk)
+    t2n = torch.empty_like(t2)
+    nws = L.query("vq3d_preact_mid_workspace_bytes", 1, 128, 128, 32)
+    wsp = ops.workspace(nws, dev)
+    gr = L.PreactGrads(*[ops._p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
+
+    def fwd_chain():
+        L.call("vq3d_preact_mid_fwd_chain", dc, 1, 18, 9, 128, 128, 32, L.ptr(x), L.ptr(w2), L.ptr(w3),
+               ctypes.byref(prm), L.ptr(t2), L.ptr(out), L.ptr(t3), L.ptr(w1), ctypes.byref(prm), L.ptr(t2n),
+               L.stream())
+
+    def bwd_chain():
+        L.call("vq3d_preact_mid_bwd_chain", 2, dc, 1, 18, 9, 128, 128, 32, L.ptr(gy), L.ptr(x), L.ptr(t2),
+               L.ptr(t3), L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws),
+               ctypes.c_size_t(nws), L.ptr(gx), L.ptr(t3), L.ptr(w3), ctypes.byref(prm), L.ptr(wsp),
+               ctypes.c_size_t(nws), L.stream())
+    if kind == "k_pm_fwd":  # reads t2 9 (halo) + x 18, writes t3 9 + out 18 + the next block's t2 9
+        return (fwd_chain, nv * 63 * 2 + wb, fl_k3 + 2 * fl_pw,
+                "k_pm_fwd (chained): fused 18-ch block t3 + out (3x3x3 9->9 + 1x1 9->18 + residual) + next "
+                "block's t2 (1x1 18->9) @128x128x32 bf16")
     if kind == "k_pm_t2":
         return (lambda: ops.preact_mid_fwd(x, blk, stages=1, bufs=(out, t2, t3)), nv * 27 * 2 + wb, fl_pw,
                 "k_pm_t2: fused 18-ch block t2 (1x1 18->9 + elu) @128x128x32 bf16")
-    if kind == "k_pm_bwd2":  # reads gz3 9 + t2 9 + x 18 + g 18, writes gx 18 + gz1 9
-        return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=2, bufs=(gx, ws)), nv * 81 * 2 + wb,
-                fl_k3 + fl_pw,
-                "k_pm_bwd2: fused 18-ch block backward data tile (dgrad 3x3x3 + 1x1 dgrad) @128x128x32")
+    if kind == "k_pm_bwd2":  # reads gz3 9 + t2 9 + x 18 + g 18 + prev t3 9, writes gx 18 + gz1 9 + prev gz3 9
+        return (bwd_chain, nv * 99 * 2 + wb, fl_k3 + 2 * fl_pw,
+                "k_pm_bwd2 (chained): fused 18-ch block backward data tile (dgrad 3x3x3 + 1x1 dgrad) + previous "
+                "block's gz3 (1x1 18->9 dgrad) @128x128x32")
     if kind == "k_pm_w2grad":  # reads gz3 9 + t2 9 (halo re-reads are L2 traffic), writes partials
         return (lambda: ops.preact_mid_bwd(gy, x, t2, t3, blk, grads, stages=4, bufs=(gx, ws)), nv * 18 * 2 + wb,
                 fl_k3, "k_pm_w2grad: fused 18-ch block 3x3x3 9->9 weight gradient @128x128x32")

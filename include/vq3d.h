@@ -204,6 +204,14 @@ int vq3d_preact_mid_bwd_chain(int32_t stages, int32_t dtype, int32_t batch, int3
                               size_t workspace_bytes, void *gx, const void *prev_t3, const float *prev_w3,
                               const vq3d_preact_params *prev_p, void *prev_workspace, size_t prev_workspace_bytes,
                               vq3d_stream_t stream);
+/* Stage 16 (the fixed-order reduction) of a whole run in ONE launch: block i's workspace at
+ * workspaces + i * workspace_stride (stride >= vq3d_preact_mid_workspace_bytes, a multiple of 256),
+ * grads / params: device arrays [nblocks][11] of device pointers in the order of
+ * vq3d_preact_stack_fwd's table (w1, w2, w3, bias1a, bias1b, bias2a, bias2b, bias3a, bias3b, scale,
+ * bias4) -- gradient buffers (+=) and parameters (scale is read).  Same sums as per-block stage 16. */
+int vq3d_preact_mid_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                               const void *workspaces, size_t workspace_stride, float *const *grads,
+                               const float *const *params, vq3d_stream_t stream);
 
 /* A RUN of nblocks identical PreActFixupResBlocks (mode 'same', no skip conv) on a tiny grid
  * (batch*h*w*d <= 256, channels <= 32, branch <= 16, both multiples of 4): forward in ONE launch,
@@ -280,6 +288,12 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
                                  const void *t3, const float *w1, const float *w2, const float *w3,
                                  const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                  size_t ws_bytes, void *gx, vq3d_stream_t stream);
+/* Stage 2 of a whole RUN of these blocks in one launch pair: block i's workspace at
+ * workspaces + i * workspace_stride (stride >= vq3d_preact_small_workspace_bytes, a multiple of
+ * 256), grads / params as for vq3d_preact_mid_reduce_run ([nblocks][11] device pointer tables). */
+int vq3d_preact_small_reduce_run(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                                 int32_t w, int32_t dd, const void *workspaces, size_t workspace_stride,
+                                 float *const *grads, const float *const *params, vq3d_stream_t stream);
 
 /* --- codebook (Quantizer.forward / _update_ema / _init_ema, layers.py:636-728) --- */
 /* Nearest codeword with torch-CPU cdist arithmetic (bit-exact),
