@@ -163,3 +163,39 @@ def test_col_block_fullsize_sampled(gpu):
         got = y.float().double().cpu()[0, :, hh, ww, dd]
         worst = max(worst, float((got - o).abs().max() / max(float(o.abs().max()), 1e-6)))
     assert worst <= 1e-2, worst
+
+
+@pytest.mark.parametrize("shape,nblk", [((1, 2, 128, 128, 32), 3), ((1, 4, 16, 8, 64), 2), ((1, 8, 32, 32, 8), 3)])
+def test_small_run_matches_per_block(gpu, shape, nblk):
+    """A run of few-channel blocks through layers.BlockStack (Fn.PreActSmallRunFn: per-block fused
+    kernels into slices of one run workspace, one reduction launch pair for the whole run; the
+    (8, 4) 32x32x8 case takes the brick kernels' reduction) against the blocks run one by one:
+    out, gx and every parameter gradient bit-identical (same kernels, same fixed-order sums)."""
+    from vq3d import functional as Fn
+    from vq3d import layers as VL
+    c = shape[1]
+    blocks = [_block(c, seed=40 + i) for i in range(nblk)]
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(shape, generator=g).bfloat16()
+    gy = torch.randn(shape, generator=g).bfloat16()
+    res = []
+    for chained in (False, True):
+        stack = VL.BlockStack(*blocks).to(gpu)
+        for p in stack.parameters():
+            p.grad = None
+        xd = x.to(gpu).contiguous(memory_format=CL).requires_grad_(True)
+        if chained:
+            assert Fn.small_run_eligible(xd, blocks[0])
+            out = stack(xd)
+        else:
+            out = xd
+            for b in stack:
+                out = Fn.PreActBlockFn.apply(out, b, *b._fn_params)
+        out.backward(gy.to(gpu).contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+        res.append((out.float().cpu(), xd.grad.float().cpu(),
+                    {n: p.grad.cpu().clone() for n, p in stack.named_parameters()}))
+    a, b = res
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), (n, float((a[2][n] - b[2][n]).abs().max()))
