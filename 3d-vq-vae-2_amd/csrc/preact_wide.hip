@@ -774,9 +774,9 @@ struct RedOut {
 // Every gradient entry: its partial rows summed in a fixed order, added into the gradient
 // buffer.  The last workgroup sums the scalar partials of every tile.
 constexpr int RNT = 256;
-__global__ __launch_bounds__(RNT) void k_wide_reduce(int nch, int nchb, int ntiles, const float *__restrict__ p2a,
-                                                     const float *__restrict__ p2b, const float *__restrict__ p1,
-                                                     RedOut o) {
+__device__ __forceinline__ void wide_reduce(int nch, int nchb, int ntiles, const float *__restrict__ p2a,
+                                            const float *__restrict__ p2b, const float *__restrict__ p1,
+                                            const RedOut &o) {
     constexpr int EA = 9 * NE2, EB = NEB;
     if (int(blockIdx.x) == int(gridDim.x) - 1) {
         __shared__ float sm[RNT];
@@ -815,6 +815,22 @@ __global__ __launch_bounds__(RNT) void k_wide_reduce(int nch, int nchb, int ntil
             o.dw3[co * BR + oo] += *o.scale * t;
         }
     }
+}
+__global__ __launch_bounds__(RNT) void k_wide_reduce(int nch, int nchb, int ntiles, const float *__restrict__ p2a,
+                                                     const float *__restrict__ p2b, const float *__restrict__ p1,
+                                                     RedOut o) {
+    wide_reduce(nch, nchb, ntiles, p2a, p2b, p1, o);
+}
+// a whole run of blocks (blockIdx.y = block; its workspace at base + y * stride, pointers from the
+// run's [block][11] device tables)
+__global__ __launch_bounds__(RNT) void k_wide_reduce_run(int nch, int nchb, int ntiles, const char *__restrict__ base,
+                                                         size_t stride, int64_t oa, int64_t ob, int64_t o1,
+                                                         float *const *gtab, const float *const *ptab) {
+    const char *ws = base + size_t(blockIdx.y) * stride;
+    float *const *g = gtab + blockIdx.y * 11;
+    const RedOut o{g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], ptab[blockIdx.y * 11 + 9]};
+    wide_reduce(nch, nchb, ntiles, reinterpret_cast<const float *>(ws + oa), reinterpret_cast<const float *>(ws + ob),
+                reinterpret_cast<const float *>(ws + o1), o);
 }
 
 // ============================================================================================ host
@@ -935,6 +951,34 @@ int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch,
                                 const float *g, const float *x, const void *t2, const void *t3,
                                 const vq3d_preact_params *p, const vq3d_preact_grads *gr, const void *workspace,
                                 size_t workspace_bytes, vq3d_stream_t stream) {
+    return vq3d_preact_wide_bwd_weight_stages(3, batch, channels, branch, h, w, dd, g, x, t2, t3, p, gr, workspace,
+                                              workspace_bytes, stream);
+}
+
+int vq3d_preact_wide_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                                const void *workspaces, size_t workspace_stride, float *const *grads,
+                                const float *const *params, vq3d_stream_t stream) {
+    if (!vq3d_preact_wide_supported(batch, C, BR, h, w, dd))
+        return fail("preact_wide_reduce_run: shape outside the fused wide-block kernels");
+    if (nblocks < 1 || nblocks > 65535 || !workspaces || !grads || !params)
+        return fail("preact_wide_reduce_run: bad arguments");
+    const WsLayout l = ws_layout(batch, h, w, dd);
+    if (workspace_stride < l.total || workspace_stride % 256)
+        return fail("preact_wide_reduce_run: stride below the workspace size or unaligned");
+    const WArgs a = make_args(batch, h, w, dd);
+    const int nch = int(int64_t(batch) * h * w * dd / CHV), nchb = int(int64_t(batch) * h * w * dd / SUBV);
+    const int ne = 9 * NE2 + NEB;
+    k_wide_reduce_run<<<dim3((ne + RNT - 1) / RNT + 1, unsigned(nblocks)), RNT, 0, as_stream(stream)>>>(
+        nch, nchb, a.ntiles, static_cast<const char *>(workspaces), workspace_stride, int64_t(l.p2a), int64_t(l.p2b),
+        int64_t(l.p1), grads, params);
+    return check_launch("preact_wide_reduce_run");
+}
+
+int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                                       int32_t w, int32_t dd, const float *g, const float *x, const void *t2,
+                                       const void *t3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                                       const void *workspace, size_t workspace_bytes, vq3d_stream_t stream) {
+    if (stages < 1 || stages > 3) return fail("preact_wide_bwd_weight: stages must be a mask of 1 | 2");
     if (!vq3d_preact_wide_supported(batch, channels, branch, h, w, dd))
         return fail("preact_wide_bwd_weight: shape outside the fused wide-block kernels");
     if (!g || !x || !t2 || !t3 || !p || !gr || !workspace) return fail("preact_wide_bwd_weight: null pointer");
@@ -951,10 +995,12 @@ int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch,
     hipStream_t s = as_stream(stream);
     float *p2a = reinterpret_cast<float *>(const_cast<char *>(ws) + l.p2a);
     float *p2b = reinterpret_cast<float *>(const_cast<char *>(ws) + l.p2b);
-    k_wide_wgrad<<<9 * nch + nchb, NT, kWgLds, s>>>(a, nch, g, x, static_cast<const bf16_t *>(t2),
-                                               static_cast<const bf16_t *>(t3),
-                                               reinterpret_cast<const bf16_t *>(ws + l.gz3),
-                                               reinterpret_cast<const bf16_t *>(ws + l.gz1), *p, p2a, p2b);
+    if (stages & 1)
+        k_wide_wgrad<<<9 * nch + nchb, NT, kWgLds, s>>>(a, nch, g, x, static_cast<const bf16_t *>(t2),
+                                                   static_cast<const bf16_t *>(t3),
+                                                   reinterpret_cast<const bf16_t *>(ws + l.gz3),
+                                                   reinterpret_cast<const bf16_t *>(ws + l.gz1), *p, p2a, p2b);
+    if (!(stages & 2)) return check_launch("preact_wide_bwd_weight");
     RedOut o{G.dw1, G.dw2, G.dw3, G.dbias1a, G.dbias1b, G.dbias2a, G.dbias2b, G.dbias3a, G.dbias3b,
              G.dscale, G.dbias4, p->scale};
     const int ne = 9 * NE2 + NEB;

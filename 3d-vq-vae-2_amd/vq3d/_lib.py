@@ -79,6 +79,8 @@ _SIGS = {
     "vq3d_preact_wide_workspace_bytes": (c_size, [c_int] * 4),
     "vq3d_preact_wide_bwd_data": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P, P]),
     "vq3d_preact_wide_bwd_weight": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P]),
+    "vq3d_preact_wide_bwd_weight_stages": (c_int, [c_int] * 7 + [P] * 7 + [c_size, P]),
+    "vq3d_preact_wide_reduce_run": (c_int, [c_int] * 5 + [P, c_size, P, P, P]),
     "vq3d_preact_small_supported": (c_int, [c_int] * 7),
     "vq3d_preact_small_workspace_bytes": (c_size, [c_int] * 6),
     "vq3d_preact_small_plan": (c_int, [c_int] * 6),

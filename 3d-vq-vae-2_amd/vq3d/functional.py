@@ -237,8 +237,9 @@ class PreActStackFn(torch.autograd.Function):
 
 class PreActWideFn(torch.autograd.Function):
     """A run of 72-channel / branch-36 PreActFixupResBlocks (preact_wide.hip): the weights of the
-    whole run packed once (one launch), then one fused launch per block forward and two-plus-two
-    per block backward (data path on the current stream, weight gradients on the side stream);
+    whole run packed once (one launch), then one fused launch per block forward and two per block
+    backward (data path, weight-gradient partials into a slice of one run workspace) plus one
+    fixed-order reduction launch for the whole run;
     the residual and gradient streams fp32 inside the run."""
 
     @staticmethod
@@ -267,6 +268,7 @@ class PreActWideFn(torch.autograd.Function):
         plan = ctx.plan
         base = img.data_ptr()
         gs = ops.cast(_cl(g), torch.float32)
+        run_ws, wbase, stride = ops.preact_wide_run_workspace(plan, gs.shape, gs.device)
         for i in reversed(range(len(plan.blocks))):
             blk = plan.blocks[i]
             xs, t2, t3 = saved[3 * i: 3 * i + 3]
@@ -274,7 +276,9 @@ class PreActWideFn(torch.autograd.Function):
                      "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
             gs = ops.preact_wide_bwd(gs, xs, t2, t3, base + i * ctx.per, blk,
-                                     {n: grad_buf(t) for n, t in names.items()})
+                                     {n: grad_buf(t) for n, t in names.items()}, ws_ptr=wbase + i * stride,
+                                     reduce=False)
+        ops.preact_wide_reduce_run(plan, gs.shape, run_ws, stride)
         grads_ready(plan.params)
         return (ops.cast(gs, ctx.in_dtype), None) + (None,) * len(plan.params)
 

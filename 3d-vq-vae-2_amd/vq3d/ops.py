@@ -586,31 +586,52 @@ def preact_wide_fwd(x32, img_ptr, blk, save=True):
     return out, t2, t3
 
 
-def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads):
+def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads, ws_ptr=None, reduce=True):
     """gx (fp32) of preact_wide_fwd; the parameter gradients (grads: name -> fp32 buffer, +=) on
-    the side stream when concurrent weight gradients are on."""
+    the side stream when concurrent weight gradients are on.  ws_ptr: the block's slice of a run
+    workspace (else one is allocated); reduce=False leaves the fixed-order reduction to the
+    caller's vq3d_preact_wide_reduce_run."""
     b, c, h, w, d = x32.shape
     nb = blk.branch_conv1.weight.shape[0]
     gx = torch.empty_like(x32, memory_format=CL)
     nws = int(L.query("vq3d_preact_wide_workspace_bytes", b, h, w, d))
-    ws = torch.empty(nws, dtype=torch.uint8, device=x32.device)
+    ws = None
+    if ws_ptr is None:
+        ws = torch.empty(nws, dtype=torch.uint8, device=x32.device)
+        ws_ptr = ws.data_ptr()
+    wsp = ctypes.c_void_p(ws_ptr)
     prm = _preact_params(blk)
     L.call("vq3d_preact_wide_bwd_data", b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
-           ctypes.c_void_p(img_ptr), ctypes.byref(prm), L.ptr(ws), ctypes.c_size_t(nws), L.ptr(gx), L.stream())
+           ctypes.c_void_p(img_ptr), ctypes.byref(prm), wsp, ctypes.c_size_t(nws), L.ptr(gx), L.stream())
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
-    args = (b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3), ctypes.byref(prm), ctypes.byref(gr),
-            L.ptr(ws), ctypes.c_size_t(nws))
+    args = (1 | (2 if reduce else 0), b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
+            ctypes.byref(prm), ctypes.byref(gr), wsp, ctypes.c_size_t(nws))
     if _concurrent:
-        main = torch.cuda.current_stream()
-        side = _side_stream(x32.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            L.call("vq3d_preact_wide_bwd_weight", *args, L.stream())
-        for t in (g32, x32, t2, t3, ws):
-            t.record_stream(side)
+        _on_side(x32.device, lambda: L.call("vq3d_preact_wide_bwd_weight_stages", *args, L.stream()),
+                 g32, x32, t2, t3, ws)
     else:
-        L.call("vq3d_preact_wide_bwd_weight", *args, L.stream())
+        L.call("vq3d_preact_wide_bwd_weight_stages", *args, L.stream())
     return gx
+
+
+def preact_wide_run_workspace(plan, shape, device):
+    """One workspace for a run of wide blocks: (buffer, base address, per-block stride)."""
+    b, c, h, w, d = shape
+    nws = int(L.query("vq3d_preact_wide_workspace_bytes", b, h, w, d))
+    stride = (nws + 255) // 256 * 256
+    buf = workspace(stride * len(plan.blocks), device)
+    return buf, buf.data_ptr(), stride
+
+
+def preact_wide_reduce_run(plan, shape, run_ws, stride):
+    """The fixed-order gradient reductions of every block of a wide run, one launch."""
+    b, c, h, w, d = shape
+    ptab, gtab = plan.tables(run_ws.device)
+    args = (len(plan.blocks), b, h, w, d, L.ptr(run_ws), ctypes.c_size_t(stride), L.ptr(gtab), L.ptr(ptab))
+    if _concurrent:
+        _on_side(run_ws.device, lambda: L.call("vq3d_preact_wide_reduce_run", *args, L.stream()), run_ws, ptab, gtab)
+    else:
+        L.call("vq3d_preact_wide_reduce_run", *args, L.stream())
 
 
 # ------------------------------------------------------------------------------------------------ misc

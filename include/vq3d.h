@@ -258,6 +258,17 @@ int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch,
                                 const float *g, const float *x, const void *t2, const void *t3,
                                 const vq3d_preact_params *p, const vq3d_preact_grads *gr, const void *workspace,
                                 size_t workspace_bytes, vq3d_stream_t stream);
+/* bwd_weight in stages: 1 = the weight-gradient partial kernel, 2 = the fixed-order reduction;
+ * reduce_run = stage 2 of a whole RUN in one launch (block i's workspace at workspaces + i *
+ * workspace_stride, stride >= vq3d_preact_wide_workspace_bytes and a multiple of 256; grads /
+ * params as for vq3d_preact_mid_reduce_run). */
+int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+                                       int32_t w, int32_t dd, const float *g, const float *x, const void *t2,
+                                       const void *t3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                                       const void *workspace, size_t workspace_bytes, vq3d_stream_t stream);
+int vq3d_preact_wide_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                                const void *workspaces, size_t workspace_stride, float *const *grads,
+                                const float *const *params, vq3d_stream_t stream);
 
 /* Whole PreActFixupResBlock (mode 'same', no skip conv) on few channels: (channels, branch) in
  * {(2, 1), (4, 2), (8, 4)}, bf16, power-of-two grid.  Forward in one launch writes out, t2 and t3
