@@ -106,6 +106,23 @@ __device__ __forceinline__ F wave_sum(F v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// fp32 wave sum on the DPP network (no LDS traffic, unlike the ds_bpermute behind __shfl_xor):
+// pairs and quads by quad_perm, rows by rotation, then row_bcast:15 / row_bcast:31 carry the row
+// totals into lane 63, whose value every lane receives.  A fixed order: deterministic.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false));
+}
+template <>
+__device__ __forceinline__ float wave_sum<float>(float v) {
+    v += dpp_mov<0xb1>(v);        // quad_perm [1, 0, 3, 2]
+    v += dpp_mov<0x4e>(v);        // quad_perm [2, 3, 0, 1]
+    v += dpp_mov<0x124>(v);       // row_ror:4
+    v += dpp_mov<0x128>(v);       // row_ror:8
+    v += dpp_mov<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+    v += dpp_mov<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 
 // Deterministic block sum (fixed shuffle tree + fixed LDS order). All threads return the total.
 template <typename F, int NT>

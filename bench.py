@@ -208,14 +208,58 @@ def probe_stack(dev, kind):
     raise KeyError(kind)
 
 
+def probe_col(dev, kind):
+    """The few-channel column block kernels (preact_col.hip) at their production shapes: (4, 2) at
+    512x512x128 (decoder post-upscale blocks), (8, 4) at 256x256x64, (2, 1) at 128x128x32."""
+    import torch
+
+    from vq3d import _lib as L
+    from vq3d import layers as VL
+    from vq3d import ops
+    from vq3d.flat import FlatParams
+    c = {"4_2": 4, "8_4": 8, "2_1": 2}[kind.split("<")[-1]] if "<" in kind else 4
+    shp = {4: (512, 512, 128), 8: (256, 256, 64), 2: (128, 128, 32)}[c]
+    torch.manual_seed(5)
+    blk = VL.PreActFixupResBlock(c, c, mode="same").to(dev)
+    FlatParams(blk.parameters(), dev)
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.normal_(0, 0.2)
+    cl = torch.channels_last_3d
+    x = torch.randn((1, c) + shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    gy = torch.randn((1, c) + shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    out, t2, t3 = ops.preact_small_fwd(x, blk)
+    grads = {n: p.grad for n, p in (("dw1", blk.branch_conv1.weight), ("dw2", blk.branch_conv2.weight),
+                                    ("dw3", blk.branch_conv3.weight), ("dbias1a", blk.bias1a),
+                                    ("dbias1b", blk.bias1b), ("dbias2a", blk.bias2a), ("dbias2b", blk.bias2b),
+                                    ("dbias3a", blk.bias3a), ("dbias3b", blk.bias3b), ("dscale", blk.scale),
+                                    ("dbias4", blk.bias4))}
+    nv = shp[0] * shp[1] * shp[2]
+    nb = c // 2
+    fl = 2.0 * nv * (c * nb * 2 + nb * nb * 27)
+    if kind.startswith("k_col_fwd"):  # reads x c, writes out c + t2 nb + t3 nb
+        return (lambda: ops.preact_small_fwd(x, blk), nv * (2 * c + 2 * nb) * 2, fl,
+                f"k_col_fwd<{c},{nb}>: fused few-channel block forward @{shp[0]}x{shp[1]}x{shp[2]}")
+    # reads g c + x c + t2 nb + t3 nb, writes gx c (+ per-brick partial rows)
+    return (lambda: ops.preact_small_bwd(gy, x, t2, t3, blk, grads), nv * (3 * c + 2 * nb) * 2, 2 * fl,
+            f"k_col_bwd<{c},{nb}>: fused few-channel block backward + reduction @{shp[0]}x{shp[1]}x{shp[2]}")
+
+
 PROBES = {
+    "k_col_bwd<4_2": probe_col, "k_col_fwd<4_2": probe_col, "k_col_bwd<8_4": probe_col, "k_col_fwd<8_4": probe_col,
+    "k_col_bwd<2_1": probe_col, "k_col_fwd<2_1": probe_col,
     "k_pm_bwd2": probe_mid, "k_pm_w2grad": probe_mid, "k_pm_w13grad": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
     "k_stackm_bwd": probe_stack, "k_stackm_fwd": probe_stack,
 }
 
 
 def probe_for(name):
+    n = name.replace(", ", "_")
     for k in PROBES:
+        if "<" in k:  # shape-keyed probes: k_col_bwd<4_2 matches "k_col_bwd<4, 2>"
+            if k + ">" in n:
+                return k
+            continue
         if k + "<" in name or name.endswith(k) or (k + " ") in name or k == name.split("::")[-1].split("<")[0]:
             return k
     return None
