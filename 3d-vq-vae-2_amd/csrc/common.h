@@ -124,6 +124,24 @@ __device__ __forceinline__ float wave_sum<float>(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// fp32 sum over aligned groups of LANES lanes (a power of two <= 64), every lane of a group
+// receiving its group's total: DPP within rows (quad_perm, half-mirror, mirror), one
+// ds_bpermute step across rows for 32, the broadcast wave sum for 64.
+template <int LANES>
+__device__ __forceinline__ float group_sum(float v) {
+    static_assert(LANES >= 1 && LANES <= 64 && (LANES & (LANES - 1)) == 0, "group width");
+    if constexpr (LANES == 64) {
+        return wave_sum(v);
+    } else {
+        if constexpr (LANES >= 2) v += dpp_mov<0xb1>(v);   // quad_perm [1, 0, 3, 2]
+        if constexpr (LANES >= 4) v += dpp_mov<0x4e>(v);   // quad_perm [2, 3, 0, 1]
+        if constexpr (LANES >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror: the other quad
+        if constexpr (LANES >= 16) v += dpp_mov<0x140>(v); // row_mirror: the other half-row
+        if constexpr (LANES >= 32) v += __shfl_xor(v, 16, 64);
+        return v;
+    }
+}
+
 // Deterministic block sum (fixed shuffle tree + fixed LDS order). All threads return the total.
 template <typename F, int NT>
 __device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {

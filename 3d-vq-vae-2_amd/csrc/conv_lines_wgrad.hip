@@ -318,8 +318,7 @@ __global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, co
         }
         sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
-#pragma unroll
-    for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    sum = group_sum<LANES>(sum);
     float wg = 0.f, bs = 0.f;
     const int nfr = a.ntiles * ntm * 256;
     if (f < ne && lane == 0) {

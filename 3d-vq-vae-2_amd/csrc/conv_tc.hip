@@ -343,8 +343,7 @@ __global__ __launch_bounds__(NTC) void k_tc_wgrad(TcArgs a, const T *__restrict_
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
         float s = acc[e];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        s = wave_sum(s);
         if (lane == 0) wred[wave][e] = s;
     }
     __syncthreads();
@@ -371,8 +370,7 @@ __global__ __launch_bounds__(256) void k_tc_wgrad_reduce(const float *__restrict
         }
         sum = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
-#pragma unroll
-    for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    sum = group_sum<LANES>(sum);
     float wg = 0.f, bs = 0.f;
     if (f < NPL * NE && lane == 0) {
         const int plane = f / NE, e = f - plane * NE;

@@ -318,16 +318,14 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
     }
     if constexpr (LANES > 64) {  // one entry per workgroup: waves, then the 4 wave sums in order
         __shared__ float wsum[LANES / 64];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        sum = wave_sum(sum);
         if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = sum;
         __syncthreads();
         sum = 0.f;
 #pragma unroll
         for (int i = 0; i < LANES / 64; ++i) sum += wsum[i];
     } else {
-#pragma unroll
-        for (int o = LANES / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        sum = group_sum<LANES>(sum);
     }
     float wg = 0.f, bs = 0.f;
     if (e < ne && lane == 0) {

@@ -285,8 +285,7 @@ __global__ __launch_bounds__(256) void k_vq_stats_reduce(int nb, int k, int d, c
         }
         s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     }
-#pragma unroll
-    for (int o = LANES / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = group_sum<LANES>(s);
     if (lane == 0 && f < ne) {
         const int c = int(f / (d + 1)), j = int(f - int64_t(c) * (d + 1));
         if (j < d) dw[int64_t(c) * d + j] = s;
