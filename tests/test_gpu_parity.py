@@ -128,13 +128,25 @@ def test_blocks_and_ops(gpu, dtype):
         errs = {"y": rel_err(y.detach().float().cpu().numpy(), d[name + "/y"]),
                 "gx": rel_err(x.grad.float().cpu().numpy(), d[name + "/gx"])}
         small = set()
+        sv_got, sv_ref = [], []
         for pn, p in m.named_parameters():
             errs["grad/" + pn] = rel_err(p.grad.cpu().numpy(), d[f"{name}/grad/{pn}"])
             if p.numel() <= 64:
                 small.add("grad/" + pn)
-        # bf16: scalar / bias gradients are sums of thousands of bf16-rounded terms with heavy
-        # cancellation, so they are held to 0.5 relative (fp32 run: 2e-4 like everything else)
-        bad = {k: v for k, v in errs.items() if not v <= (0.5 if dtype == "bf16" and k in small else tol)}
+                sv_got.append(p.grad.double().cpu().numpy().ravel())
+                sv_ref.append(np.asarray(d[f"{name}/grad/{pn}"], dtype=np.float64).ravel())
+        if dtype == "bf16" and sv_got:
+            # bf16: a single scalar / bias gradient is a sum of thousands of bf16-rounded terms with
+            # heavy cancellation (no meaningful relative error alone), so the block's small-parameter
+            # gradients are held as ONE vector: relative L2 against the fp32 golden <= 2e-2 (measured
+            # <= 4.3e-3 over every block type / mode of the goldens)
+            g_, r_ = np.concatenate(sv_got), np.concatenate(sv_ref)
+            errs["small_grads_vector"] = float(np.linalg.norm(g_ - r_) / max(np.linalg.norm(r_), 1e-30))
+            print(f"{name}: bf16 small-parameter gradient vector rel L2 {errs['small_grads_vector']:.3e}")
+            for k in small:
+                errs.pop(k)
+        limit = {"small_grads_vector": 2e-2}
+        bad = {k: v for k, v in errs.items() if not v <= limit.get(k, tol)}
         if bad:
             failures.append((name, bad))
     assert not failures, failures
