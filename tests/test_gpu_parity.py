@@ -177,7 +177,8 @@ def load_model(name, dev, dtype="fp32"):
 
 @pytest.mark.parametrize("name", sorted(MODEL_CFGS))
 def test_model_train_step_fp32(gpu, name):
-    """fp32 path vs the reference: codes bit-exact, decoded/loss/grads/Adam state within fp tol."""
+    """fp32 path vs the reference: codes bit-exact (every level, both steps), decoded / loss / grads /
+    Adam state within fp tolerance."""
     m, d = load_model(name, gpu, "fp32")
     opt = m.configure_optimizers()
     xs = tuple(int(v) for v in d["x_shape"])
@@ -206,8 +207,10 @@ def test_model_train_step_fp32(gpu, name):
             got = ix.cpu().numpy()
             ref = d[f"step{step}/idx{lvl}"]
             match = (got == ref).mean()
-            # exact arithmetic differs only in conv summation order; codes on near-ties may flip
-            assert match >= 0.999, (name, step, lvl, match)
+            print(f"{name} step {step} level {lvl}: code match {match:.6f} ({got.size} codes)")
+            # bit-exact against the reference's codes on every golden model (measured: all 1.0);
+            # only the conv summation order differs, which no golden case turns into a flip
+            assert np.array_equal(got, ref), (name, step, lvl, match)
         assert abs(float(loss) - float(d[f"step{step}/loss"])) <= 2e-4 * abs(float(d[f"step{step}/loss"])), \
             (float(loss), float(d[f"step{step}/loss"]))
         e = rel_err(dec.detach().float().cpu().numpy()[..., ::stride, ::stride, ::stride], d[f"step{step}/dec"])
