@@ -314,6 +314,26 @@ __device__ __forceinline__ void row_st(T *__restrict__ p, const float (&v)[C]) {
     }
 }
 
+// bf16 storage: the activations' exp on the hardware v_exp_f32 (__expf; the result is rounded to
+// bf16 anyway, as the fused block kernels do); fp32 storage keeps the accurate expf
+template <typename T>
+__device__ __forceinline__ float elu_st(float z) {
+    if constexpr (sizeof(T) == 2) return z > 0.f ? z : __expf(z) - 1.f;
+    else return elu(z);
+}
+template <typename T>
+__device__ __forceinline__ float pro_fast(const Prologue &p, float x) {
+    if (p.kind == VQ3D_PRO_NONE) return x;
+    if (p.kind == VQ3D_PRO_ADD) return x + p.a;
+    return elu_st<T>(x + p.a) + p.b;
+}
+template <typename T>
+__device__ __forceinline__ float epi_act_fast(int act, float v, float a, float b) {
+    if (act == VQ3D_ACT_ELU) return elu_st<T>(v);
+    if (act == VQ3D_ACT_ELU_AFFINE) return elu_st<T>(v + a) + b;
+    return v;
+}
+
 template <typename T, int CI, int CO, bool DGRAD>
 __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restrict__ in, const float *__restrict__ w,
                                                 int pro_kind, const float *pro_a, const float *pro_b,
@@ -348,7 +368,36 @@ __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restri
             const int64_t v = vb + u * stride;
             if (v < nvox) {
                 row_ld<T, CI>(in + v * CI, xr[u]);
-                if (!DGRAD && fe.res) row_ld<T, CO>(fe.res + v * CO, er[u]);
+                if (!DGRAD && fe.res && fe.res_up2) {
+                    // the half-grid residual upsampled x2 (trilinear, align_corners=False) on the
+                    // fly: 8 neighbour rows of CO channels, the k_pw2 / k_up2_fwd weights and order
+                    int t = int(v);
+                    const int od = t % fe.oD;
+                    t /= fe.oD;
+                    const int ow = t % fe.oW;
+                    t /= fe.oW;
+                    const int oh = t % fe.oH, b = t / fe.oH;
+                    const int rH = fe.oH / 2, rW = fe.oW / 2, rD = fe.oD / 2;
+                    int h0, h1, w0, w1, d0, d1;
+                    float lh, lw, ld_;
+                    up_coeff(oh, rH, h0, h1, lh);
+                    up_coeff(ow, rW, w0, w1, lw);
+                    up_coeff(od, rD, d0, d1, ld_);
+                    float R[8][CO];
+                    const int hs[2] = {h0, h1}, wsx[2] = {w0, w1}, dsx[2] = {d0, d1};
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        row_ld<T, CO>(fe.res + ((int64_t(b * rH + hs[q >> 2]) * rW + wsx[(q >> 1) & 1]) * rD +
+                                                dsx[q & 1]) * CO, R[q]);
+#pragma unroll
+                    for (int o = 0; o < CO; ++o)
+                        er[u][o] = (1.f - lh) * ((1.f - lw) * ((1.f - ld_) * R[0][o] + ld_ * R[1][o]) +
+                                                 lw * ((1.f - ld_) * R[2][o] + ld_ * R[3][o])) +
+                                   lh * ((1.f - lw) * ((1.f - ld_) * R[4][o] + ld_ * R[5][o]) +
+                                         lw * ((1.f - ld_) * R[6][o] + ld_ * R[7][o]));
+                } else if (!DGRAD && fe.res) {
+                    row_ld<T, CO>(fe.res + v * CO, er[u]);
+                }
                 if (DGRAD && dv.mode) row_ld<T, CO>(be.aux + v * CO, er[u]);
                 if (DGRAD && be.addend) row_ld<T, CO>(be.addend + v * CO, dr[u]);
             }
@@ -357,18 +406,20 @@ __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restri
         for (int u = 0; u < 4; ++u) {
             const int64_t v = vb + u * stride;
             if (v >= nvox) break;
-            float y[CO];
+            float y[CO], xin[CI];
+#pragma unroll
+            for (int c = 0; c < CI; ++c) xin[c] = DGRAD ? xr[u][c] : pro_fast<T>(pro, xr[u][c]);
 #pragma unroll
             for (int o = 0; o < CO; ++o) {
                 float s = 0.f;
 #pragma unroll
-                for (int c = 0; c < CI; ++c) s = fmaf(DGRAD ? xr[u][c] : pro.apply(xr[u][c]), wr[o][c], s);
+                for (int c = 0; c < CI; ++c) s = fmaf(xin[c], wr[o][c], s);
                 if (!DGRAD) {
                     if (fe.scale) s = s * sc;
                     if (fe.bias) s = s + bias;
                     if (fe.cbias) s = s + fe.cbias[o];
                     if (fe.res) s = s + er[u][o];
-                    s = epi_act(fe.act, s, aa, ab);
+                    s = epi_act_fast<T>(fe.act, s, aa, ab);
                 } else {
                     if (gscale) s = s * gs;
                     pre += s;
@@ -537,7 +588,8 @@ __global__ __launch_bounds__(256) void k_pw_sg(SgArgs s, ConvArgs ca, const T *_
 bool rows_path(const vq3d_conv_desc *d, bool dgrad, const void *res_up2_flag) {
     auto p2 = [](int c) { return c == 1 || c == 2 || c == 4 || c == 8; };
     const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
-    return d->cin2 == 0 && p2(ci) && p2(co) && !res_up2_flag;
+    // the half-grid residual (ResizeConv skip) is upsampled inside the forward row kernel
+    return d->cin2 == 0 && p2(ci) && p2(co) && !(res_up2_flag && dgrad);
 }
 
 }  // namespace

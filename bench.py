@@ -245,7 +245,52 @@ def probe_col(dev, kind):
             f"k_col_bwd<{c},{nb}>: fused few-channel block backward + reduction @{shp[0]}x{shp[1]}x{shp[2]}")
 
 
+def probe_wgrad(dev, kind):
+    """The generic k^3 weight-gradient engine (conv_mfma.inc k_wgrad_mfma) on the unfused
+    (16, 8)-block branch conv of the 128x128x32 level: 8 -> 8, 3x3x3 circular, bf16."""
+    import torch
+
+    from vq3d import ops
+    cl = torch.channels_last_3d
+    shp = (1, 8, 128, 128, 32)
+    x = torch.randn(shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    g = torch.randn(shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = torch.randn((8, 8, 3, 3, 3), device=dev)
+    dw = torch.zeros_like(w)
+    nv = 128 * 128 * 32
+    geom = ops.ConvGeom(3, 1, 1, True)
+    return (lambda: ops.conv_bwd(g, x, w, geom, want_gx=False, dw=dw), nv * 16 * 2, 2.0 * nv * 27 * 64,
+            "k_wgrad_mfma<8,1,4>: 3x3x3 8->8 circular weight gradient @128x128x32 bf16")
+
+
+def probe_pw(dev, kind):
+    """Full-resolution 1x1x1 convs of the published model's first down / last up block (512x512x128,
+    bf16): k_pw_rows 4 -> 4 with the PreAct prologue elu(x + a) + b and the next conv's ELU_AFFINE
+    epilogue (down block conv1), k_pw2 4 -> 4 with scale / bias and the half-grid skip upsampled
+    on the fly as residual (up block conv3)."""
+    import torch
+
+    from vq3d import ops
+    cl = torch.channels_last_3d
+    shp = (1, 4, 512, 512, 128)
+    x = torch.randn(shp, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = torch.randn((4, 4, 1, 1, 1), device=dev) * 0.3
+    sc = [torch.full((1,), v, device=dev) for v in (0.1, 0.2, 0.3, 0.4)]
+    y = torch.empty_like(x)
+    nv = 512 * 512 * 128
+    g1 = ops.ConvGeom(1)
+    if kind.startswith("k_pw_rows"):
+        return (lambda: ops.conv_fwd(x, w, g1, pro=(sc[0], sc[1]), act=(sc[2], sc[3]), out=y), nv * 8 * 2,
+                2.0 * nv * 16, "k_pw_rows<4,4>: 1x1 4->4 + prologue + ELU_AFFINE epilogue @512x512x128")
+    res = torch.randn((1, 4, 256, 256, 64), device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    return (lambda: ops.conv_fwd(x, w, g1, scale=sc[0], bias=sc[1], residual=res, residual_up2=True, out=y),
+            nv * 8 * 2 + nv // 8 * 4 * 2, 2.0 * nv * 16,
+            "k_pw2<4>: 1x1 4->4 + scale / bias + upsampled half-grid residual @512x512x128")
+
+
 PROBES = {
+    "k_pw_rows<4_4": probe_pw, "k_pw2<4": probe_pw,
+    "k_wgrad_mfma<8_1_4": probe_wgrad,
     "k_col_bwd<4_2": probe_col, "k_col_fwd<4_2": probe_col, "k_col_bwd<8_4": probe_col, "k_col_fwd<8_4": probe_col,
     "k_col_bwd<2_1": probe_col, "k_col_fwd<2_1": probe_col,
     "k_pm_bwd2": probe_mid, "k_pm_w2grad": probe_mid, "k_pm_w13grad": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
