@@ -20,6 +20,7 @@ struct S2Args {
     int iH, iW, iD, oH, oW, oD;
     int k, p, circ;
     FastDiv fD, fW, fH;  // 32-bit voxel index decomposition (no 64-bit divides in the loop)
+    int rows;            // one input of exactly COT channels, 16-B aligned rows: vector epilogue
 };
 
 // the <= 2 (o, t) pairs of one dimension for input coordinate i (k in {2, 4}, stride 2)
@@ -148,6 +149,29 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict_
                         }
                     }
         }
+        if constexpr (sizeof(T) == 2 && (COT == 4 || COT == 8)) {
+            if (a.rows) {  // all Cin (== COT) channels of one input: whole-row loads / stores
+                float aux[COT], add[COT], o[COT];
+                if (dv.mode) load_row<T, COT>(be.aux + v * COT, aux);
+                if (be.addend) load_row<T, COT>(be.addend + v * COT, add);
+#pragma unroll
+                for (int c = 0; c < COT; ++c) {
+                    float val = acc[c];
+                    if (gscale) val = val * gs;
+                    pre += val;
+                    if (dv.mode) val = val * dv(aux[c]);
+                    post += val;
+                    if (be.addend) val = val + add[c];
+                    o[c] = val;
+                }
+                uint32_t qv[COT / 2];
+#pragma unroll
+                for (int j = 0; j < COT / 2; ++j) qv[j] = uint32_t(f2bf(o[2 * j])) | (uint32_t(f2bf(o[2 * j + 1])) << 16);
+                if constexpr (COT == 4) *reinterpret_cast<uint2 *>(gx + v * COT) = uint2{qv[0], qv[1]};
+                else *reinterpret_cast<uint4 *>(gx + v * COT) = uint4{qv[0], qv[1], qv[2], qv[3]};
+                continue;
+            }
+        }
 #pragma unroll
         for (int c = 0; c < COT; ++c) {
             const int ci = c0 + c;
@@ -211,6 +235,8 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 255) / 256, 4096 / ych + 1)));
     const dim3 grid{nbx, unsigned(ych), 1u};
     auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    a.rows = (ych == 1 && a.Cin2 == 0 && a.Cin == cot && (cot == 4 || cot == 8) && al(gx) &&
+              (!be.aux || al(be.aux)) && (!be.addend || al(be.addend))) ? 1 : 0;
     const int co_t = (al(g) && (a.Cout == 4 || a.Cout == 8 || a.Cout == 16)) ? a.Cout : 0;
 #define L(C, CO)                                                                                              \
     case C:                                                                                                   \

@@ -288,7 +288,27 @@ def probe_pw(dev, kind):
             "k_pw2<4>: 1x1 4->4 + scale / bias + upsampled half-grid residual @512x512x128")
 
 
+def probe_s2(dev, kind):
+    """Stride-2 backward-data (conv_s2.hip) of the first down block's branch conv2: 4x4x4 stride 2
+    circular 4 -> 4, g on 256x256x64, gx on 512x512x128 with the activated-aux derivative."""
+    import torch
+
+    from vq3d import ops
+    cl = torch.channels_last_3d
+    x = torch.randn((1, 4, 512, 512, 128), device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    g = torch.randn((1, 4, 256, 256, 64), device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = torch.randn((4, 4, 4, 4, 4), device=dev) * 0.2
+    b = torch.full((1,), 0.1, device=dev)
+    dpre, dpost = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+    nv = 512 * 512 * 128
+    geom = ops.ConvGeom(4, 2, 1, True)
+    return (lambda: ops.conv_bwd(g, x, w, geom, aux=x, aux_b=b, dpro_pre=dpre, dpro_post=dpost),
+            nv * 4 * 2 * 2 + nv // 8 * 4 * 2, 2.0 * nv * 8 * 16,
+            "k_dgrad_s2<4,4>: 4x4x4 stride-2 4->4 backward-data + activated-aux derivative @512x512x128")
+
+
 PROBES = {
+    "k_dgrad_s2<4_4": probe_s2,
     "k_pw_rows<4_4": probe_pw, "k_pw2<4": probe_pw,
     "k_wgrad_mfma<8_1_4": probe_wgrad,
     "k_col_bwd<4_2": probe_col, "k_col_fwd<4_2": probe_col, "k_col_bwd<8_4": probe_col, "k_col_fwd<8_4": probe_col,
