@@ -20,7 +20,7 @@ The line carries:
   roofline_top   the same for the top probe-able kernels of the ranking
   step_conv_roofline_frac  the per-layer conv roofline of the whole step (SURVEY.md 8(d):
                  5.55 ms per 3L-pub volume) / the measured step time
-  cpu_baseline   the CPU oracle (oracle/vqvae_cpu.py) on this host: warm-up + median of 2 steps
+  cpu_baseline   the CPU oracle (oracle/vqvae_cpu.py) on this host: warm-up + median of 3 steps
                  on a bounded sample volume, scaled by voxel count
 """
 import argparse
@@ -440,7 +440,7 @@ def dist_graph_probe(dev, rank, world):
 
 
 # ---------------------------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(mkw, size, encode_only=False, sample=(256, 256, 64), reps=2):
+def cpu_baseline(mkw, size, encode_only=False, sample=(256, 256, 64), reps=3):
     """The CPU oracle (oracle/vqvae_cpu.py, fp32 torch-CPU restatement of the reference step) on
     this host: one warm-up, then the median of `reps` steps of the same model on a sample volume
     with `frac` of the voxels, scaled to volumes/s of the full volume."""
