@@ -106,6 +106,10 @@ int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const 
 int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
             const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
             const vq3d_preact_grads &gr, void *workspace, void *gx, int stages, hipStream_t s);
+bool mid_w2grad_ok(const vq3d_conv_desc *d);
+size_t mid_w2grad_ws(const vq3d_conv_desc *d);
+int mid_w2grad(const vq3d_conv_desc *d, const void *x, const void *g, float *dw, void *ws, size_t ws_bytes,
+               hipStream_t s);
 int col_reduce_run(int nblocks, int batch, int C, int BR, int h, int w, int d, void *workspaces, size_t stride,
                    float *const *gtab, const float *const *ptab, hipStream_t s);
 

@@ -1178,6 +1178,55 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
 
 }  // namespace
 
+// The W2-gradient kernel as the weight gradient of a plain 9 -> 9 3x3x3 circular conv (the up
+// blocks' branch conv2 on the upsampled t2 at 256^2 x 64): dW[co][ci][tap] = sum_v g[v][co]
+// x[v + tap][ci] is exactly k_pm_w2grad's gz3 (x) t2 window sum; its partials are summed by the
+// W2 section of k_pm_reduce (fixed order, deterministic) straight into dw.
+bool mid_w2grad_ok(const vq3d_conv_desc *d) {
+    return d->dtype == VQ3D_BF16 && d->cin == BR && d->cin2 == 0 && d->cout == BR && d->kernel == 3 &&
+           d->stride == 1 && d->pad == 1 && d->pad_mode == VQ3D_PAD_CIRCULAR && d->pro_kind == VQ3D_PRO_NONE &&
+           d->in_h == d->out_h && d->in_w == d->out_w && d->in_d == d->out_d &&
+           vq3d_preact_mid_supported(VQ3D_BF16, d->batch, C, BR, d->in_h, d->in_w, d->in_d);
+}
+
+namespace {
+struct W2Plan {
+    int nchunk, npc, nwa;
+    size_t bytes;
+};
+W2Plan w2_plan(const vq3d_conv_desc *d) {
+    W2Plan p;
+    p.nchunk = int(int64_t(d->batch) * d->in_h * d->in_w * d->in_d / CHV);
+    p.npc = kW2Chunks;
+    while (p.nchunk % p.npc) p.npc >>= 1;
+    p.nwa = p.nchunk / p.npc;
+    p.bytes = size_t(9) * p.nwa * NER * 4;
+    return p;
+}
+}  // namespace
+
+size_t mid_w2grad_ws(const vq3d_conv_desc *d) { return mid_w2grad_ok(d) ? w2_plan(d).bytes : 0; }
+
+int mid_w2grad(const vq3d_conv_desc *d, const void *x, const void *g, float *dw, void *ws, size_t ws_bytes,
+               hipStream_t s) {
+    const W2Plan p = w2_plan(d);
+    if (!mid_w2grad_ok(d) || !dw || !ws || ws_bytes < p.bytes) return fail("conv3d_bwd_weight(9->9 windowed): bad call");
+    const PmArgs a = make_args(d->batch, d->in_h, d->in_w, d->in_d, BTH, BTW);
+    float *p2a = static_cast<float *>(ws);
+    const bf16_t *gz = static_cast<const bf16_t *>(g), *xt = static_cast<const bf16_t *>(x);
+    switch (d->in_d) {
+        case 8: launch_w2<8>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
+        case 16: launch_w2<16>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
+        case 32: launch_w2<32>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
+        case 64: launch_w2<64>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
+        default: launch_w2<128>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
+    }
+    RedOut o{};
+    o.dw2 = dw;
+    k_pm_reduce<<<NBA, NT, 0, s>>>(nullptr, 0, nullptr, 0, p2a, p.nwa, nullptr, 0, o);  // W2 blocks only
+    return check_launch("conv3d_bwd_weight(9->9 windowed)");
+}
+
 }  // namespace vq3d
 
 using namespace vq3d;
