@@ -307,7 +307,25 @@ def probe_s2(dev, kind):
             "k_dgrad_s2<4,4>: 4x4x4 stride-2 4->4 backward-data + activated-aux derivative @512x512x128")
 
 
+def probe_wgrad_s2(dev, kind):
+    """The generic k^3 weight-gradient engine on a down block's branch conv2: 4x4x4 stride 2
+    circular 9 -> 9 from 256x256x64 to 128x128x32, bf16."""
+    import torch
+
+    from vq3d import ops
+    cl = torch.channels_last_3d
+    x = torch.randn((1, 9, 256, 256, 64), device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    g = torch.randn((1, 9, 128, 128, 32), device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = torch.randn((9, 9, 4, 4, 4), device=dev)
+    dw = torch.zeros_like(w)
+    nv = 128 * 128 * 32
+    geom = ops.ConvGeom(4, 2, 1, True)
+    return (lambda: ops.conv_bwd(g, x, w, geom, want_gx=False, dw=dw), (nv * 8 + nv) * 9 * 2, 2.0 * nv * 64 * 81,
+            "k_wgrad_mfma<16,1,14>: 4x4x4 stride-2 9->9 circular weight gradient 256^2x64 -> 128^2x32 bf16")
+
+
 PROBES = {
+    "k_wgrad_mfma<16_1_14": probe_wgrad_s2,
     "k_dgrad_s2<4_4": probe_s2,
     "k_pw_rows<4_4": probe_pw, "k_pw2<4": probe_pw,
     "k_wgrad_mfma<8_1_4": probe_wgrad,
