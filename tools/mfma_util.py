@@ -32,8 +32,10 @@ _V256 = 256 * 256 * 64
 _V32 = 32 * 32 * 8
 SHAPES = [
     # (kernel regex, shape, useful flops, algorithmic bytes)
-    (r"k_pm_fwd", "18-ch block fwd: 3x3x3 9->9 + 1x1 9->18 @128^2x32", 2 * _V128 * (2187 + 162), _V128 * 54 * 2),
-    (r"k_pm_bwd2", "18-ch block dgrad: 3x3x3 9->9 + 1x1 9->18 @128^2x32", 2 * _V128 * (2187 + 162), _V128 * 81 * 2),
+    (r"k_pm_fwd", "18-ch block fwd (chained): 3x3x3 9->9 + 1x1 9->18 + next 1x1 18->9 @128^2x32",
+     2 * _V128 * (2187 + 162 + 162), _V128 * 63 * 2),
+    (r"k_pm_bwd2", "18-ch block dgrad (chained): 3x3x3 9->9 + 1x1 9->18 + previous 1x1 18->9 @128^2x32",
+     2 * _V128 * (2187 + 162 + 162), _V128 * 99 * 2),
     (r"k_pm_w2grad", "18-ch block wgrad: 3x3x3 9->9 @128^2x32", 2 * _V128 * 2187, _V128 * 18 * 2),
     (r"k_wide_fwd", "72-ch block fwd: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184), _V32 * (144 * 4 + 72 * 2)),
     (r"k_wide_bwd_data", "72-ch block dgrad: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
