@@ -10,6 +10,7 @@
 #include "engines.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace vq3d {
 
@@ -65,6 +66,22 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[N])
     } else {
 #pragma unroll
         for (int j = 0; j < N; ++j) o[j] = ld(p + j);
+    }
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_row(T *__restrict__ p, const float (&v)[N]) {
+    if constexpr (sizeof(T) == 2 && (N % 8) == 0) {
+#pragma unroll
+        for (int q = 0; q < N / 8; ++q) {
+            uint32_t u[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) u[j] = uint32_t(f2bf(v[8 * q + 2 * j])) | (uint32_t(f2bf(v[8 * q + 2 * j + 1])) << 16);
+            reinterpret_cast<uint4 *>(p)[q] = uint4{u[0], u[1], u[2], u[3]};
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) st(p + j, v[j]);
     }
 }
 
@@ -200,6 +217,102 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict_
     }
 }
 
+// Parity-class form (one input of CI = 4 / 8 channels, Cout CO = 4 / 8, circular, pad k / 2 - 1,
+// every extent even): blockIdx.y = the (h, w) parity class (a, b) of the input voxels, a thread
+// owns the D-pair i = (2 oh + a, 2 ow + b, 2 od + {0, 1}) -- one 8 / 16-byte run of gx.  Every tap
+// index is then the same for all lanes (the weights come through the scalar cache, no LDS
+// broadcast), and the pair shares its h / w rows of g: (k/2)^2 x (k/2 + 1) rows for 2 voxels.
+template <typename T, int CI, int CO, int K>
+__global__ __launch_bounds__(256) void k_dgrad_s2_pair(S2Args a, const T *__restrict__ g,
+                                                      const float *__restrict__ gscale, const float *__restrict__ w,
+                                                      BwdEpi<T> be, T *__restrict__ gx, float *dpre, float *dpost) {
+    constexpr int P = K / 2 - 1, NT_ = K / 2, K3 = K * K * K;
+    __shared__ float red[8];
+    ActDeriv dv;
+    dv.mode = be.aux ? be.mode : 0;
+    dv.p = (dv.mode && be.p) ? *be.p : 0.f;
+    const float gs = gscale ? *gscale : 1.f;
+    const int pa = int(blockIdx.y) >> 1, pb = int(blockIdx.y) & 1;
+    float pre = 0.f, post = 0.f;
+    const int64_t npair = int64_t(a.B) * a.oH * a.oW * a.oD;
+    for (int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x; e < npair; e += int64_t(gridDim.x) * 256) {
+        uint32_t q = uint32_t(e);
+        uint32_t q2 = a.fD.div(q);
+        const int od = int(q - q2 * uint32_t(a.oD));
+        q = a.fW.div(q2);
+        const int ow = int(q2 - q * uint32_t(a.oW));
+        q2 = a.fH.div(q);
+        const int oh = int(q - q2 * uint32_t(a.oH));
+        const int b = int(q2);
+        const int ih = 2 * oh + pa, iw = 2 * ow + pb;
+        // per dimension: tap t meets g row (i + P - t) / 2 (circular); h / w taps: parity-fixed
+        int rh[NT_], rw[NT_];
+#pragma unroll
+        for (int x = 0; x < NT_; ++x) {
+            const int th = ((pa + P) & 1) + 2 * x, tw = ((pb + P) & 1) + 2 * x;
+            int r = ih + P - th;
+            r = r < 0 ? r + a.iH : (r >= a.iH ? r - a.iH : r);
+            rh[x] = r >> 1;
+            r = iw + P - tw;
+            r = r < 0 ? r + a.iW : (r >= a.iW ? r - a.iW : r);
+            rw[x] = r >> 1;
+        }
+        float acc[2][CI];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int c = 0; c < CI; ++c) acc[v][c] = 0.f;
+#pragma unroll
+        for (int x = 0; x < NT_; ++x)
+#pragma unroll
+            for (int y = 0; y < NT_; ++y) {
+                const int th = ((pa + P) & 1) + 2 * x, tw = ((pb + P) & 1) + 2 * y;
+                const int64_t rowb = (int64_t(b) * a.oH + rh[x]) * a.oW + rw[y];
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+#pragma unroll
+                    for (int z = 0; z < NT_; ++z) {
+                        const int td = ((v + P) & 1) + 2 * z;
+                        int r = 2 * od + v + P - td;
+                        r = r < 0 ? r + a.iD : (r >= a.iD ? r - a.iD : r);
+                        float gr[CO];
+                        load_row<T, CO>(g + (rowb * a.oD + (r >> 1)) * CO, gr);
+                        const int tap = (th * K + tw) * K + td;
+#pragma unroll
+                        for (int co = 0; co < CO; ++co)
+#pragma unroll
+                            for (int c = 0; c < CI; ++c)
+                                acc[v][c] = fmaf(gr[co], w[(co * CI + c) * K3 + tap], acc[v][c]);
+                    }
+            }
+        const int64_t vox = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + 2 * od;  // first of the pair
+        float aux[2 * CI], add[2 * CI], o[2 * CI];
+        if (dv.mode) load_row<T, 2 * CI>(be.aux + vox * CI, aux);
+        if (be.addend) load_row<T, 2 * CI>(be.addend + vox * CI, add);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int c = 0; c < CI; ++c) {
+                float val = acc[v][c];
+                if (gscale) val = val * gs;
+                pre += val;
+                if (dv.mode) val = val * dv(aux[v * CI + c]);
+                post += val;
+                if (be.addend) val = val + add[v * CI + c];
+                o[v * CI + c] = val;
+            }
+        store_row<T, 2 * CI>(gx + vox * CI, o);
+    }
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
+        }
+    }
+}
+
 }  // namespace
 
 bool dgrad_s2_applicable(const vq3d_conv_desc *d) {
@@ -225,6 +338,27 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
     a.fW = FastDiv(uint32_t(a.iW));
     a.fH = FastDiv(uint32_t(a.iH));
     if (int64_t(a.B) * a.iH * a.iW * a.iD >= (int64_t(1) << 31)) return fail("conv3d_bwd_data(s2): grid too large");
+    {
+        auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+        if (std::is_same<T, bf16_t>::value && a.circ && a.Cin2 == 0 && (a.Cin == 4 || a.Cin == 8) &&
+            (a.Cout == 4 || a.Cout == 8) && a.p == a.k / 2 - 1 && a.iH == 2 * a.oH && a.iW == 2 * a.oW &&
+            a.iD == 2 * a.oD && al16(g) && al16(gx) && (!be.aux || al16(be.aux)) && (!be.addend || al16(be.addend))) {
+            S2Args c = a;
+            c.fD = FastDiv(uint32_t(a.oD));
+            c.fW = FastDiv(uint32_t(a.oW));
+            c.fH = FastDiv(uint32_t(a.oH));
+            const int64_t npair = int64_t(a.B) * a.oH * a.oW * a.oD;
+            const dim3 pg(unsigned(std::max<int64_t>(1, std::min<int64_t>((npair + 255) / 256, 2048))), 4u, 1u);
+#define PK(CI_, CO_, K_)                                                                                      \
+            if (a.Cin == CI_ && a.Cout == CO_ && a.k == K_) {                                                  \
+                k_dgrad_s2_pair<T, CI_, CO_, K_><<<pg, 256, 0, s>>>(c, (const T *)g, gscale, w, be, (T *)gx,     \
+                                                                   dpre, dpost);                               \
+                return check_launch("conv3d_bwd_data(s2 pairs)");                                              \
+            }
+            PK(4, 4, 4) PK(4, 8, 4) PK(8, 4, 4) PK(8, 8, 4) PK(4, 4, 2) PK(4, 8, 2) PK(8, 4, 2) PK(8, 8, 2)
+#undef PK
+        }
+    }
     const int K3 = a.k * a.k * a.k;
     int cot = a.Cin <= 1 ? 1 : a.Cin <= 2 ? 2 : a.Cin <= 4 ? 4 : a.Cin <= 8 ? 8 : 16;
     while (cot > 1 && size_t(K3) * a.Cout * cot * 4 > 64 * 1024) cot /= 2;
