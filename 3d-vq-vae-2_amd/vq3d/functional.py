@@ -214,8 +214,8 @@ class PreActStackFn(torch.autograd.Function):
         saved = torch.empty(L.query("vq3d_preact_stack_saved_floats", nblk, b, c, nb, h, w, d), dtype=torch.float32,
                             device=x.device)
         out = torch.empty_like(x, memory_format=ops.CL)
-        L.call("vq3d_preact_stack_fwd", L.dtype_code(x), nblk, b, c, nb, h, w, d, L.ptr(x), L.ptr(ptab), L.ptr(out),
-               L.ptr(saved), L.stream())
+        ops._timed("k_stackm_fwd", lambda: L.call("vq3d_preact_stack_fwd", L.dtype_code(x), nblk, b, c, nb, h, w, d,
+                                                  L.ptr(x), L.ptr(ptab), L.ptr(out), L.ptr(saved), L.stream()))
         ctx.plan = plan
         ctx.save_for_backward(saved)
         ctx.shape = (b, c, nb, h, w, d)
@@ -229,8 +229,9 @@ class PreActStackFn(torch.autograd.Function):
         g = _cl(g)
         ptab, gtab = plan.tables(g.device)
         gx = torch.empty_like(g, memory_format=ops.CL)
-        L.call("vq3d_preact_stack_bwd", L.dtype_code(g), len(plan.blocks), b, c, nb, h, w, d, L.ptr(g), L.ptr(ptab),
-               L.ptr(gtab), L.ptr(saved), L.ptr(gx), L.stream())
+        ops._timed("k_stackm_bwd", lambda: L.call("vq3d_preact_stack_bwd", L.dtype_code(g), len(plan.blocks), b, c, nb,
+                                                  h, w, d, L.ptr(g), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
+                                                  L.stream()))
         grads_ready(plan.params)
         return (gx, None) + (None,) * len(plan.params)
 

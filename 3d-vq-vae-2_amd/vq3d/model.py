@@ -15,6 +15,7 @@ import torch
 from torch import nn
 
 from . import functional as Fn
+from . import parallel
 from .flat import FlatParams
 from .layers import Decoder, Encoder2, EvonormResBlock, FixupResBlock, PreActFixupResBlock
 from .optim import FusedAdam
@@ -99,6 +100,8 @@ class VQVAE(nn.Module):
 
     # ------------------------------------------------------------------ model
     def forward(self, data):
+        if torch.is_grad_enabled():
+            parallel.step_begin()
         commitment_loss, quantizations, encoding_idx = zip(*self.encode(data))
         decoded = self.decode(quantizations)
         return decoded, (commitment_loss, quantizations, encoding_idx)

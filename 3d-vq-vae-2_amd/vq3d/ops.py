@@ -173,6 +173,72 @@ def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None
     return gx, gx2
 
 
+# ------------------------------------------------------------------------------------------------ kernel timing
+_ktimer = [None]
+
+
+class KernelTimer:
+    """HIP-event timing of ONE engine kernel's launches inside a real (eager) training step.
+
+    While active (``with KernelTimer("k_pm_bwd2") as t: step()``), the run-level wrappers below issue
+    the selected kernel as a launch of its own (the multi-kernel entry points are split into their
+    stages, which is numerically identical) and bracket each launch with HIP events on the stream it
+    is launched on.  ``avg_us()`` is then the kernel's average duration with the step's real data
+    and neighbours -- what bench.py reports as the dominant kernel's live launch time.  Kinds:
+    k_pm_fwd, k_pm_bwd2, k_pm_w2grad, k_pm_w13grad (chained 18-channel runs), k_col_fwd<C_B>,
+    k_col_bwd<C_B> (few-channel column blocks, e.g. "k_col_bwd<4_2"), k_stackm_fwd, k_stackm_bwd."""
+
+    def __init__(self, kind):
+        self.kind = kind
+        self.events = []
+
+    def __enter__(self):
+        _ktimer[0] = self
+        return self
+
+    def __exit__(self, *exc):
+        _ktimer[0] = None
+        return False
+
+    def wants(self, kind):
+        return kind == self.kind
+
+    def run(self, fn):
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        fn()
+        e1.record(st)
+        self.events.append((e0, e1))
+
+    def avg_us(self):
+        if not self.events:
+            return None
+        self.events[-1][1].synchronize()
+        return 1e3 * sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
+
+
+def _timed(kind, fn):
+    """fn() bracketed by HIP events when the active KernelTimer selects `kind`."""
+    t = _ktimer[0]
+    if t is not None and t.wants(kind() if callable(kind) else kind):
+        t.run(fn)
+    else:
+        fn()
+
+
+def _small_kind(which, b, c, nb, h, w, d):
+    """timer kind of a few-channel block launch: the column kernels (plan 2) or the brick kernels"""
+    col = int(L.query("vq3d_preact_small_plan", b, c, nb, h, w, d)) == 2
+    return f"k_{'col' if col else 'small'}_{which}<{c}_{nb}"
+
+
+def timing(kind):
+    """True when a KernelTimer for `kind` is active (the caller then issues that kernel alone)."""
+    t = _ktimer[0]
+    return t is not None and t.wants(kind)
+
+
 # ------------------------------------------------------------------------------------------------ streams
 _concurrent = False
 _side = {}
@@ -377,10 +443,12 @@ def preact_mid_run_fwd(x, blocks, save=True):
         t2n = new_act(b, nb, h, w, d, x.dtype, x.device) if nxt is not None else None
         prm = _preact_params(blk)
         prmn = _preact_params(nxt) if nxt is not None else None
-        L.call("vq3d_preact_mid_fwd_chain", dc, b, c, nb, h, w, d, L.ptr(x), L.ptr(blk.branch_conv2.weight),
-               L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), L.ptr(t2), L.ptr(out), _p(t3),
-               None if nxt is None else L.ptr(nxt.branch_conv1.weight),
-               None if prmn is None else ctypes.byref(prmn), _p(t2n), L.stream())
+        fargs = (dc, b, c, nb, h, w, d, L.ptr(x), L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight),
+                 ctypes.byref(prm), L.ptr(t2), L.ptr(out), _p(t3),
+                 None if nxt is None else L.ptr(nxt.branch_conv1.weight),
+                 None if prmn is None else ctypes.byref(prmn), _p(t2n), L.stream())
+        # k_pm_fwd<..., true> (the chained tile kernel) is the launch of every block but the last
+        _timed("k_pm_fwd" if nxt is not None else "", lambda a=fargs: L.call("vq3d_preact_mid_fwd_chain", *a))
         if save:
             saved.append((x, t2, t3))
         x, t2 = out, t2n
@@ -425,6 +493,13 @@ def preact_mid_run_bwd(g, plan, saved, on_done=None):
             L.call("vq3d_preact_mid_bwd_chain", first | 2, *args, *chain, L.stream())
             _on_side(g.device, lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 12, *a, L.stream()),
                      g, x, t2, t3)
+        elif timing("k_pm_bwd2") or timing("k_pm_w2grad") or timing("k_pm_w13grad"):
+            # the same stages as one launch each (k_pm_bwd2<..., true> = the chained data tile of
+            # every block but the first / last, whose calls also carry the pointwise stage)
+            _timed("k_pm_bwd2" if (i and not first) else "",
+                   lambda a=args, ch=chain: L.call("vq3d_preact_mid_bwd_chain", first | 2, *a, *ch, L.stream()))
+            _timed("k_pm_w2grad", lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 4, *a, L.stream()))
+            _timed("k_pm_w13grad", lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 8, *a, L.stream()))
         else:
             L.call("vq3d_preact_mid_bwd_chain", first | 14, *args, *chain, L.stream())
         g = gx
@@ -495,8 +570,9 @@ def preact_small_fwd(x, blk, save=True):
     t2 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
     t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
     prm = _preact_params(blk)
-    L.call("vq3d_preact_small_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2),
-           L.ptr(w3), ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream())
+    _timed(lambda: _small_kind("fwd", b, c, nb, h, w, d), lambda: L.call(
+        "vq3d_preact_small_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3),
+        ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream()))
     return out, t2, t3
 
 
@@ -537,10 +613,10 @@ def preact_small_run_bwd(g, plan, saved, on_done=None):
         gx = torch.empty_like(x, memory_format=CL)
         prm = _preact_params(blk)
         gr = L.PreactGrads(*[ctypes.c_void_p(int(gp)) for gp in plan.grad_ptrs(i)])
-        L.call("vq3d_preact_small_bwd_stages", 1, dc, b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
-               L.ptr(blk.branch_conv1.weight), L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight),
-               ctypes.byref(prm), ctypes.byref(gr), ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws),
-               L.ptr(gx), L.stream())
+        sargs = (dc, b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(blk.branch_conv1.weight),
+                 L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), ctypes.byref(gr),
+                 ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws), L.ptr(gx), L.stream())
+        _timed(lambda: _small_kind("bwd", b, c, nb, h, w, d), lambda a=sargs: L.call("vq3d_preact_small_bwd_stages", 1, *a))
         g = gx
     L.call("vq3d_preact_small_reduce_run", len(blocks), b, c, nb, h, w, d, ctypes.c_void_p(base),
            ctypes.c_size_t(stride), L.ptr(gtab), L.ptr(ptab), L.stream())

@@ -66,6 +66,16 @@ def grads_ready(params):
         r.ready(params)
 
 
+def step_begin():
+    """Called at the start of every gradient-recording forward (VQVAE.forward): a reducer whose
+    previous backward was not followed by its __call__ (an exception, a skipped step, a second
+    backward) drains those collectives and starts the new step from fresh bucket state, so a
+    stale `issued` flag can never make this step skip its gradient average."""
+    r = _active[0]
+    if r is not None:
+        r.begin_step()
+
+
 class GradientAllReduce:
     """Average the model's flat gradient across ranks in buckets overlapped with backward (one
     RCCL all-reduce per bucket; gloo SUM + divide in CPU tests).
@@ -93,6 +103,8 @@ class GradientAllReduce:
         self.overlap = overlap and self.world > 1
         self._comm = None
         if self.overlap:
+            if _active[0] is not None and _active[0] is not self:
+                _active[0].close()  # one reducer reports per process: the newest replaces the old
             _active[0] = self
         self._reset()
 
@@ -117,6 +129,12 @@ class GradientAllReduce:
             lo0, hi0, ids0 = self.buckets[-1]
             self.buckets[-1] = (0, hi0, ids0)
         self.bucket_of = {pid: bi for bi, (_, _, ids) in enumerate(self.buckets) for pid in ids}
+
+    def begin_step(self):
+        if any(self.issued) or self.works:
+            for work, _ in self.works:
+                work.wait()
+            self._reset()
 
     def _reset(self):
         self.pending = [set(ids) for _, _, ids in self.buckets]
@@ -175,5 +193,9 @@ class GradientAllReduce:
         self._reset()
 
     def close(self):
+        """Detach from the autograd Functions (drains any issued collectives first)."""
+        for work, _ in self.works:
+            work.wait()
+        self.works = []
         if _active[0] is self:
             _active[0] = None

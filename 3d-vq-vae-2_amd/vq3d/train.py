@@ -18,7 +18,9 @@ ModelCheckpoint), restated here without that dependency:
   * ModelCheckpoint(save_top_k=1, save_last=True, monitor='val_recon_loss_mean') (train.py:56):
     last.ckpt after every validation, the best one as epoch=E-step=S.ckpt (PL 1.2 layout,
     vq3d.checkpoint);
-  * --resume_from_checkpoint restores weights, codebooks, Adam state, epoch and global step;
+  * --resume_from_checkpoint restores weights, codebooks, Adam state, epoch and global step with
+    PL 1.2.10's counter convention (pl_checkpoint_counters / resume_counters), so a checkpoint
+    written by the reference resumes here at the epoch PL would resume it at, and vice versa;
     last.ckpt is also written when training stops (max_steps / max_epochs).
 precision=16 is recorded (the path computes in bf16 activations per --compute-dtype).
 """
@@ -85,8 +87,28 @@ def seed_everything(seed=42):
     return seed
 
 
+def pl_checkpoint_counters(epoch, pl_global_step, max_steps=None):
+    """(epoch, global_step) as PL 1.2.10's CheckpointConnector.dump_checkpoint writes them while the
+    trainer is at `epoch` with its global_step counter at `pl_global_step` (the 0-based index of the
+    batch being finished: PL increments its counter only after the batch's validation /
+    checkpoint callbacks): global_step + 1, and epoch + 1 unless max_steps was reached.  On
+    restore PL sets current_epoch = ckpt['epoch'] and global_step = ckpt['global_step']
+    (resume_counters), so a checkpoint written mid-epoch resumes at the next epoch boundary."""
+    reached = max_steps is not None and max_steps <= pl_global_step
+    return (int(epoch) if reached else int(epoch) + 1), int(pl_global_step) + 1
+
+
+def resume_counters(ck):
+    """(first epoch, global step) a run resumed from checkpoint dict `ck` continues with (PL 1.2.10
+    restore_training_state): the saved values as they are."""
+    return int(ck["epoch"]), int(ck["global_step"])
+
+
 class Checkpointer:
-    """ModelCheckpoint(save_top_k=1, save_last=True, monitor='val_recon_loss_mean')."""
+    """ModelCheckpoint(save_top_k=1, save_last=True, monitor='val_recon_loss_mean'): the best
+    checkpoint as epoch=E-step=S.ckpt with PL's counters at save time (E = current epoch, S = the
+    trainer's global_step before its increment), last.ckpt always; the counters inside follow
+    pl_checkpoint_counters."""
 
     def __init__(self, dirpath, monitor="val_recon_loss_mean"):
         self.dirpath = Path(dirpath)
@@ -98,17 +120,18 @@ class Checkpointer:
         return {"monitor": self.monitor, "best_model_score": self.best_score, "best_model_path": self.best_path,
                 "dirpath": str(self.dirpath)}
 
-    def __call__(self, model, opt, epoch, step, score):
+    def __call__(self, model, opt, epoch, pl_global_step, score, max_steps=None):
         self.dirpath.mkdir(parents=True, exist_ok=True)
+        ep, gs = pl_checkpoint_counters(epoch, pl_global_step, max_steps)
         if score is not None and (self.best_score is None or score < self.best_score):
             old = self.best_path
             self.best_score = float(score)
-            self.best_path = str(self.dirpath / f"epoch={epoch}-step={step}.ckpt")
-            save_checkpoint(self.best_path, model, opt, epoch=epoch, global_step=step, callbacks={"ModelCheckpoint":
-                                                                                                  self.state()})
+            self.best_path = str(self.dirpath / f"epoch={epoch}-step={pl_global_step}.ckpt")
+            save_checkpoint(self.best_path, model, opt, epoch=ep, global_step=gs, callbacks={"ModelCheckpoint":
+                                                                                            self.state()})
             if old and old != self.best_path and os.path.exists(old):
                 os.remove(old)
-        save_checkpoint(str(self.dirpath / "last.ckpt"), model, opt, epoch=epoch, global_step=step,
+        save_checkpoint(str(self.dirpath / "last.ckpt"), model, opt, epoch=ep, global_step=gs,
                         callbacks={"ModelCheckpoint": self.state()})
 
 
@@ -147,7 +170,6 @@ def main(args: Namespace, datamodule=None):
     model = VQVAE(args).to(dev)
     model.train()
     opt = model.configure_optimizers()
-    reducer = parallel.GradientAllReduce(model)
     ckpt = Checkpointer(Path(args.default_root_dir) / "checkpoints")
     epoch0, step = 0, 0
     if args.resume_from_checkpoint:
@@ -155,11 +177,18 @@ def main(args: Namespace, datamodule=None):
         model.load_state_dict(ck["state_dict"])
         if ck.get("optimizer_states"):
             opt.load_state_dict(ck["optimizer_states"][0])
-        epoch0, step = int(ck["epoch"]) + 1, int(ck["global_step"])
+        epoch0, step = resume_counters(ck)
         st = ck.get("callbacks", {}).get("ModelCheckpoint") or {}
         ckpt.best_score, ckpt.best_path = st.get("best_model_score"), st.get("best_model_path")
-        if world > 1:  # every rank resumed from the same file; re-sync host mirrors anyway
-            reducer = parallel.GradientAllReduce(model)
+    # built after any resume, so the replicas start from the restored (identical) state
+    reducer = parallel.GradientAllReduce(model)
+    try:
+        return _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, step)
+    finally:
+        reducer.close()
+
+
+def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, step):
     train_ds, val_ds = datamodule.train_dataset, datamodule.val_dataset
     sampler = (torch.utils.data.distributed.DistributedSampler(train_ds, world, rank, shuffle=True, seed=42,
                                                                drop_last=True) if world > 1 else None)
@@ -192,15 +221,14 @@ def main(args: Namespace, datamodule=None):
                     print(f"epoch {epoch} step {step} loss {history[-1][1]:.6f}", flush=True)
             if (i + 1) % val_every == 0 or (i + 1) == n_batches:
                 score = validate(model, vloader, dev) if len(val_ds) else None
-                if rank == 0:
-                    ckpt(model, opt, epoch, step, score)
+                if rank == 0:  # PL's global_step is still this batch's 0-based index here
+                    ckpt(model, opt, epoch, step - 1, score, args.max_steps)
             if args.max_steps is not None and step >= args.max_steps:
                 break
         if args.max_steps is not None and step >= args.max_steps:
             break
-    if rank == 0:  # training ended (max_steps / max_epochs): last.ckpt holds the final state
-        ckpt(model, opt, epoch, step, None)
-    reducer.close()
+    if rank == 0 and step > 0:  # training ended (max_steps / max_epochs): last.ckpt holds the final state
+        ckpt(model, opt, epoch, step - 1, None, args.max_steps)
     return model, opt, history, ckpt
 
 

@@ -49,7 +49,9 @@ ENC_ROOF_MS = {"3l_pub": 0.42, "3l_dflt": 0.27}  # encoder-only 
 ENC_BYTES = {"3l_pub": 3.39e9, "3l_dflt": 2.19e9}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0  # dense bf16
-STEP_TOP = os.path.join(ROOT, "profiles", "r02_step_top.json")
+STEP_TOP = os.path.join(ROOT, "profiles", "r03_step_top.json")
+if not os.path.exists(STEP_TOP):
+    STEP_TOP = os.path.join(ROOT, "profiles", "r02_step_top.json")
 
 
 def parse():
@@ -372,51 +374,75 @@ def timed_launch(dev, launch, iters=20):
     return e0.elapsed_time(e1) / 1e3 / iters
 
 
-def roofline_of(dev, kind, step_entry=None):
+def roofline_of(dev, kind, step_entry=None, live_us=None):
+    """Roofline of one engine kernel.  Its launch time is taken, in order of preference, from
+    (1) `live_us`: HIP events around each of its launches inside a real training step of this run
+        (vq3d.ops.KernelTimer, on the stream the kernel is launched on),
+    (2) the committed rocprofv3 step trace (profiles/r03_step_top.json) average,
+    (3) the isolated probe (the kernel alone on resident inputs of its production shape, 20 launches
+        captured in a HIP graph).
+    The other two are reported beside it (trace_avg_us, avg_launch_us_isolated / frac_isolated)
+    so the three can be checked against each other."""
     launch, algo, flops, desc = PROBES[kind](dev, kind)
-    t = timed_launch(dev, launch)
+    t_iso = timed_launch(dev, launch)
+    t_trace = step_entry["avg_us"] * 1e-6 if step_entry else None
+    if live_us:
+        t, src = live_us * 1e-6, "live: HIP events around each launch inside an eager training step of this run"
+    elif t_trace:
+        t, src = t_trace, f"rocprofv3 step trace average ({os.path.relpath(STEP_TOP, ROOT)})"
+    else:
+        t, src = t_iso, "isolated probe (HIP-graph replay of 20 launches)"
     achieved = algo / t / 1e9
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"r02_pmc_{kind}.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    for rnd in ("r03", "r02"):
+        pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{kind}.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+            break
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-         "traffic": traffic, "kernel": desc, "avg_launch_us": t * 1e6, "algorithmic_bytes": algo,
-         "tflops": flops / t / 1e12, "mfma_frac_of_peak": flops / t / 1e12 / MFMA_PEAK_TFS}
+         "traffic": traffic, "kernel": desc, "avg_launch_us": t * 1e6, "time_source": src,
+         "algorithmic_bytes": algo, "tflops": flops / t / 1e12, "mfma_frac_of_peak": flops / t / 1e12 / MFMA_PEAK_TFS,
+         "avg_launch_us_isolated": t_iso * 1e6, "frac_isolated": algo / t_iso / 1e9 / HBM_PEAK_GBS}
+    if t_trace:
+        r["trace_avg_us"] = t_trace * 1e6
+        r["frac_trace"] = algo / t_trace / 1e9 / HBM_PEAK_GBS
+    if live_us:
+        r["live_avg_us"] = live_us
     if step_entry:
         r["step_share"] = {"launches_per_step": step_entry["launches"], "us_per_step": step_entry["total_us"],
                            "trace_avg_us": step_entry["avg_us"]}
     return r
 
 
-def rooflines(dev, top=5):
-    """(dominant, top list) from the committed step ranking; kernels without a probe are
-    listed by name with their step share only."""
+def rooflines(dev, live=None, top=5):
+    """(dominant, top list, unprobed) from the committed step ranking (by total us per step).
+    The dominant kernel is the first ranked kernel with a probe; `unprobed` lists the kernels ranked
+    ABOVE it (more us per step) that have no probe.  live(kind) -> in-step average launch us."""
     ranking = []
     if os.path.exists(STEP_TOP):
         ranking = json.load(open(STEP_TOP)).get("by_name", [])
-    out, skipped = [], []
+    out, unprobed = [], []
     for e in ranking:
         k = probe_for(e["kernel"])
         if k is None:
-            if len(out) < top:
-                skipped.append({"kernel": e["kernel"], "us_per_step": e["total_us"], "launches": e["launches"]})
+            if not out:
+                unprobed.append({"kernel": e["kernel"], "us_per_step": e["total_us"], "launches": e["launches"]})
             continue
         if any(r.get("probe") == k for r in out):
             continue
-        r = roofline_of(dev, k, e)
+        r = roofline_of(dev, k, e, live(k) if (live is not None and not out) else None)
         r["probe"] = k
         out.append(r)
         if len(out) >= top:
             break
     if not out:
-        r = roofline_of(dev, "k_pm_bwd2")
+        r = roofline_of(dev, "k_pm_bwd2", None, live("k_pm_bwd2") if live is not None else None)
         r["probe"] = "k_pm_bwd2"
         out.append(r)
-    return out[0], out, skipped
+    return out[0], out, unprobed
 
 
 # ---------------------------------------------------------------------------------------------- distributed
@@ -457,6 +483,20 @@ def dist_graph_probe(dev, rank, world):
     return float(v) > 0.5
 
 
+def host_cores():
+    """CPU cores this process may actually use: the affinity mask (what `nproc` prints), capped by
+    the cgroup CPU quota when one is set (a GPU box grants a share of a larger machine; nproc
+    there counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 # ---------------------------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(mkw, size, encode_only=False, sample=(256, 256, 64), reps=3):
     """The CPU oracle (oracle/vqvae_cpu.py, fp32 torch-CPU restatement of the reference step) on
@@ -465,7 +505,8 @@ def cpu_baseline(mkw, size, encode_only=False, sample=(256, 256, 64), reps=3):
     import torch
 
     from oracle import vqvae_cpu as O
-    threads = min(16, os.cpu_count() or 1)
+    # the CPU restatement on all of the host's cores (nproc)
+    threads = host_cores()
     torch.set_num_threads(threads)
     import vq3d
     cfg = O.Config(**{k: v for k, v in mkw.items()})
@@ -531,7 +572,7 @@ def prior_cpu_baseline(sample=(8, 8, 8), reps=2):
 
     from oracle import pixelsnail_cpu as O
     from vq3d import pixelsnail as PS
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(host_cores())
     kw = {k: v for k, v in PRIOR.items() if k != "dims"}
     torch.manual_seed(0)
     m = PS.PixelSNAIL(PS.default_args(**kw), compute_dtype="fp32")
@@ -700,6 +741,7 @@ def main():
     # full step on the resident input; Adam's step count lives on the device.  N > 1: the RCCL
     # collectives are captured too once a probe capture of the same pattern replayed correctly on
     # every rank; otherwise the ranks run eagerly.
+    eager_step = step
     graph = None
     use_graph = not a.eager and a.warmup >= 2
     if use_graph and world > 1:
@@ -766,10 +808,19 @@ def main():
         res_line["step_conv_roofline_frac"] = ENC_ROOF_MS[a.config] / ms
         res_line["encoder_traffic_frac"] = ENC_BYTES[a.config] / (ms / 1e3) / 1e9 / HBM_PEAK_GBS
     if rank == 0 and not a.no_roofline:
-        dom, top, unprobed = rooflines(dev)
+        def live(kind):
+            """the kernel's average launch time inside one more (eager, untimed) step of this run"""
+            if a.encode_only or world > 1:
+                return None
+            with ops.KernelTimer(kind) as kt:
+                eager_step(a.warmup + a.steps)
+            torch.cuda.synchronize()
+            return kt.avg_us()
+        dom, top, unprobed = rooflines(dev, live)
         res_line["roofline"] = dom
-        res_line["roofline_top"] = [{k: r[k] for k in ("probe", "frac", "achieved", "avg_launch_us", "tflops",
-                                                       "mfma_frac_of_peak", "traffic") if k in r} |
+        res_line["roofline_top"] = [{k: r[k] for k in ("probe", "frac", "achieved", "avg_launch_us", "time_source",
+                                                       "frac_isolated", "tflops", "mfma_frac_of_peak", "traffic")
+                                     if k in r} |
                                     ({"us_per_step": r["step_share"]["us_per_step"]} if "step_share" in r else {})
                                     for r in top]
         if unprobed:

@@ -112,6 +112,21 @@ def _allreduce_worker(rank, world, port, out):
     parallel.grads_ready(ps[4:])
     ar()
     ok &= torch.allclose(m.flat.grad[m.flat.offsets[0]:m.flat.offsets[0] + 300], torch.full((300,), 1.5))
+    # an abandoned step (backward reported everything, the reducer was never called): the next
+    # forward's step_begin drains it, so the new step's buckets are all issued and averaged
+    parallel.grads_ready(ps)
+    ok &= all(ar.issued)
+    parallel.step_begin()
+    ok &= not any(ar.issued) and not ar.works
+    for p in m.ps:
+        p.grad.fill_(float(2 * rank + 1))
+    parallel.grads_ready(ps[4:])
+    ar()
+    ok &= all(torch.allclose(p.grad, torch.full_like(p.grad, 2.0)) for p in m.ps)  # (1 + 3) / 2
+    # a replacement reducer (e.g. after a resume) closes the old one: only the new one reports
+    ar2 = parallel.GradientAllReduce(m, bucket_bytes=2048)
+    ok &= parallel._active[0] is ar2
+    ar2.close()
     ar.close()
     shards = [parallel.shard_indices(s, rank, world, 2) for s in range(3)]
     torch.save({"ok": torch.tensor(bool(ok)), "shards": shards}, out + f".{rank}")

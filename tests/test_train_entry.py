@@ -46,8 +46,29 @@ def test_checkpointer_keeps_best_and_last(tmp_path):
     files = sorted(p.name for p in tmp_path.iterdir())
     assert files == ["epoch=1-step=30.ckpt", "last.ckpt"]
     last = load_checkpoint(str(tmp_path / "last.ckpt"))
-    assert last["global_step"] == 30 and last["epoch"] == 1
+    # PL 1.2.10 dump_checkpoint: global_step + 1, epoch + 1 (max_steps not reached)
+    assert last["global_step"] == 31 and last["epoch"] == 2
     assert last["callbacks"]["ModelCheckpoint"]["best_model_score"] == 0.3
+    ck(m, None, 1, 40, None, max_steps=40)   # max_steps reached: the epoch is not advanced
+    last = load_checkpoint(str(tmp_path / "last.ckpt"))
+    assert last["global_step"] == 41 and last["epoch"] == 1
+
+
+def test_pl_counter_convention_round_trip():
+    """A checkpoint the reference's PL 1.2.10 Trainer wrote mid-epoch 5 at global_step 99 holds
+    epoch 6 / global_step 100 and resumes at epoch 6, step 100 -- here as in PL -- and a
+    checkpoint written here resumes in PL at the same place."""
+    from argparse import Namespace
+
+    from vq3d import train
+    ep, gs = train.pl_checkpoint_counters(5, 99)
+    assert (ep, gs) == (6, 100)
+    pl_dict = {"epoch": 6, "global_step": 100, "pytorch-lightning_version": "1.2.10", "state_dict": {},
+               "callbacks": {}, "optimizer_states": [], "lr_schedulers": [], "hparams_name": "kwargs",
+               "hyper_parameters": {"args": Namespace()}}
+    assert train.resume_counters(pl_dict) == (6, 100)
+    assert train.pl_checkpoint_counters(3, 7, max_steps=7) == (3, 8)
+    assert train.pl_checkpoint_counters(3, 6, max_steps=7) == (4, 7)
 
 
 class _SmallCT:
@@ -79,7 +100,8 @@ def test_train_two_steps_then_resume(gpu, tmp_path):
     assert [s for s, _ in hist] == [1, 2] and all(np.isfinite(v) for _, v in hist)
     last = root / "checkpoints" / "last.ckpt"
     saved = load_checkpoint(str(last))
-    assert saved["global_step"] == 2 and saved["epoch"] == 0
+    # PL 1.2.10 counters: global_step = steps done, epoch advanced (resume starts the next epoch)
+    assert saved["global_step"] == 2 and saved["epoch"] == 1
     assert ck.best_path and os.path.exists(ck.best_path)
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     for k, v in saved["state_dict"].items():
@@ -92,4 +114,4 @@ def test_train_two_steps_then_resume(gpu, tmp_path):
     r_st = load_checkpoint(str(last))["optimizer_states"][0]["state"]
     assert opt2.step_count == 3, (opt2.step_count, {float(v["step"]) for v in r_st.values()})
     resumed = load_checkpoint(str(last))
-    assert resumed["global_step"] == 3 and resumed["epoch"] == 1
+    assert resumed["global_step"] == 3 and resumed["epoch"] == 2

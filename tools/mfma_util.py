@@ -31,31 +31,36 @@ _V512 = 512 * 512 * 128
 _V256 = 256 * 256 * 64
 _V32 = 32 * 32 * 8
 SHAPES = [
-    # (kernel regex, shape, useful flops, algorithmic bytes)
-    (r"k_pm_fwd", "18-ch block fwd (chained): 3x3x3 9->9 + 1x1 9->18 + next 1x1 18->9 @128^2x32",
+    # (kernel regex, production grid (threads, as rocprofv3 reports Grid_Size), shape, useful flops,
+    # algorithmic bytes).  A kernel is attributed to a shape only at that shape's production grid: the
+    # same template also runs on other grids (e.g. k_col_bwd<4, 2> on a 64^2 x 16 level) whose useful
+    # work is different, and those rows get no shape columns.
+    (r"k_pm_fwd", 196608, "18-ch block fwd (chained): 3x3x3 9->9 + 1x1 9->18 + next 1x1 18->9 @128^2x32",
      2 * _V128 * (2187 + 162 + 162), _V128 * 63 * 2),
-    (r"k_pm_bwd2", "18-ch block dgrad (chained): 3x3x3 9->9 + 1x1 9->18 + previous 1x1 18->9 @128^2x32",
+    (r"k_pm_bwd2", 131072, "18-ch block dgrad (chained): 3x3x3 9->9 + 1x1 9->18 + previous 1x1 18->9 @128^2x32",
      2 * _V128 * (2187 + 162 + 162), _V128 * 99 * 2),
-    (r"k_pm_w2grad", "18-ch block wgrad: 3x3x3 9->9 @128^2x32", 2 * _V128 * 2187, _V128 * 18 * 2),
-    (r"k_wide_fwd", "72-ch block fwd: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184), _V32 * (144 * 4 + 72 * 2)),
-    (r"k_wide_bwd_data", "72-ch block dgrad: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
-     _V32 * (216 * 4 + 72 * 2)),
-    (r"k_wide_wgrad", "72-ch block wgrad: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
+    (r"k_pm_w2grad<32>", 294912, "18-ch block wgrad: 3x3x3 9->9 @128^2x32", 2 * _V128 * 2187, _V128 * 18 * 2),
+    (r"k_pm_w2grad<64>", 2359296, "up-block conv2 wgrad: 3x3x3 9->9 @256^2x64", 2 * _V256 * 2187, _V256 * 18 * 2),
+    (r"k_wide_fwd", 49152, "72-ch block fwd: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
      _V32 * (144 * 4 + 72 * 2)),
-    (r"k_col_fwd<4, 2>", "4-ch block fwd: 3x3x3 2->2 @512^2x128", 2 * _V512 * (108 + 16), _V512 * 12 * 2),
-    (r"k_col_bwd<4, 2>", "4-ch block bwd: 3x3x3 2->2 dgrad + wgrad @512^2x128", 4 * _V512 * (108 + 16),
+    (r"k_wide_bwd_data", 49152, "72-ch block dgrad: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
+     _V32 * (216 * 4 + 72 * 2)),
+    (r"k_wide_wgrad", 79872, "72-ch block wgrad: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
+     _V32 * (144 * 4 + 72 * 2)),
+    (r"k_col_fwd<4, 2>", 8388608, "4-ch block fwd: 3x3x3 2->2 @512^2x128", 2 * _V512 * (108 + 16), _V512 * 12 * 2),
+    (r"k_col_bwd<4, 2>", 8388608, "4-ch block bwd: 3x3x3 2->2 dgrad + wgrad @512^2x128", 4 * _V512 * (108 + 16),
      _V512 * 16 * 2),
-    (r"k_col_fwd<8, 4>", "8-ch block fwd: 3x3x3 4->4 @256^2x64", 2 * _V256 * (432 + 64), _V256 * 24 * 2),
-    (r"k_col_bwd<8, 4>", "8-ch block bwd: 3x3x3 4->4 dgrad + wgrad @256^2x64", 4 * _V256 * (432 + 64),
+    (r"k_col_fwd<8, 4>", 1048576, "8-ch block fwd: 3x3x3 4->4 @256^2x64", 2 * _V256 * (432 + 64), _V256 * 24 * 2),
+    (r"k_col_bwd<8, 4>", 1048576, "8-ch block bwd: 3x3x3 4->4 dgrad + wgrad @256^2x64", 4 * _V256 * (432 + 64),
      _V256 * 32 * 2),
-    (r"k_col_fwd<2, 1>", "2-ch block fwd: 3x3x3 1->1 @128^2x32", 2 * _V128 * (27 + 4), _V128 * 6 * 2),
-    (r"k_col_bwd<2, 1>", "2-ch block bwd: 3x3x3 1->1 @128^2x32", 4 * _V128 * (27 + 4), _V128 * 8 * 2),
+    (r"k_col_fwd<2, 1>", 131072, "2-ch block fwd: 3x3x3 1->1 @128^2x32", 2 * _V128 * (27 + 4), _V128 * 6 * 2),
+    (r"k_col_bwd<2, 1>", 131072, "2-ch block bwd: 3x3x3 1->1 @128^2x32", 4 * _V128 * (27 + 4), _V128 * 8 * 2),
 ]
 
 
-def shape_of(name):
-    for pat, desc, fl, by in SHAPES:
-        if re.search(pat, name):
+def shape_of(name, grid):
+    for pat, g, desc, fl, by in SHAPES:
+        if re.search(pat, name) and grid == g:
             return desc, fl, by
     return None
 
@@ -95,12 +100,16 @@ def main():
         flops = mops * 512
         tf = flops / (us * 1e-6) / 1e12
         util = busy / (grbm / 8 * 1024) if grbm else 0.0
-        sh = shape_of(name)
+        sh = shape_of(name, grid)
         ceil = useful_tf = None
         if sh:
             ai = sh[1] / sh[2]
             ceil = min(1.0, ai * HBM_TBS * 1e12 / (PEAK_TF * 1e12))
             useful_tf = sh[1] / (us * 1e-6) / 1e12
+            # the matrix cores cannot do less work than the shape's useful FLOPs: a shape whose
+            # useful work exceeds what the kernel issued is a wrong attribution, so fail loudly
+            if sh[1] > flops * 1.0001:
+                raise SystemExit(f"{name} [{grid}]: useful {sh[1]:.3e} FLOPs > issued {flops:.3e}: wrong shape")
         rows.append((n * us, name, grid, n, us, flops, tf, util, sh, ceil, useful_tf))
     rows.sort(reverse=True)
     out = ["| kernel [grid] | launches | avg us (profiled) | shape | MFMA GFLOP/launch (MOPS x 512) | "
