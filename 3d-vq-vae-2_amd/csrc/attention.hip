@@ -36,7 +36,40 @@ constexpr float LOG2E = 1.4426950408889634f;
 struct AttnArgs {
     int P, n, nh, dk, dv;
     float c2;  // scale * log2(e)
+    // training-mode logit transform of the reference (layers.py:633-637): dropout(logits) -- kept
+    // logits scaled by 1 / (1 - p), dropped ones 0 -- then logits == 0 -> -1e3.  train = 0: none.
+    int train;
+    uint32_t drop_below;      // a (problem, head, i, j) hash below this drops the logit (p * 2^32)
+    float keep_scale;         // 1 / (1 - p)
+    const uint64_t *seed;     // device seed of this forward (the backward reads the same value)
 };
+
+constexpr float ZERO_LOGIT2 = -1000.f * LOG2E;  // the reference's -1e3 logit, in log2 units
+
+// counter-based hash of one logit's coordinates (lowbias32 mixing of a 64-bit seed, the
+// problem / head and the two positions): the same value in the forward and both backward kernels
+__device__ __forceinline__ uint32_t logit_hash(uint64_t seed, int ph, int i, int j) {
+    uint32_t x = uint32_t(seed) ^ (uint32_t(seed >> 32) * 0x9E3779B1u) ^ (uint32_t(ph) * 0xC2B2AE3Du) ^
+                 (uint32_t(i) * 0x85EBCA77u) ^ (uint32_t(j) * 0x27D4EB2Fu);
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+// the training-mode transform of a raw (scaled, log2-unit) score s of logit (i, j); live = the
+// logit keeps its gradient (kept by dropout and not replaced), with factor keep_scale
+__device__ __forceinline__ float train_logit(const AttnArgs &a, uint64_t seed, int ph, int i, int j, float s,
+                                             bool &live) {
+    if (a.drop_below && logit_hash(seed, ph, i, j) < a.drop_below) {
+        live = false;
+        return ZERO_LOGIT2;
+    }
+    s *= a.keep_scale;
+    live = s != 0.f;
+    return live ? s : ZERO_LOGIT2;
+}
 
 template <typename T, int DM>
 __device__ __forceinline__ void load_row(const T *__restrict__ src, int64_t base, int d, bool ok, float (&r)[DM]) {
@@ -113,6 +146,7 @@ __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict
         o[c] = 0.f;
     }
     float m = -INFINITY, l = 0.f;
+    const uint64_t seed = a.drop_below ? *a.seed : 0;
     for (int kt = 0; kt <= qt; ++kt) {
         __syncthreads();
         stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
@@ -127,6 +161,10 @@ __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 s[u] = j0 + u < jlim ? dot<DM>(qr, ks + (j0 + u) * DM) : -INFINITY;
+                if (a.train && j0 + u < jlim) {
+                    bool live;
+                    s[u] = train_logit(a, seed, int(blockIdx.y), i, kt * QR + j0 + u, s[u], live);
+                }
                 cm = fmaxf(cm, s[u]);
             }
             const float alpha = exp2f(m - cm);  // m = -inf before the wave's first key: 0
@@ -201,6 +239,7 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_q(AttnArgs a, float scale, cons
     const int64_t row = (int64_t(p) * a.nh + h) * a.n + ic;
     const float lz = ok ? lse[row] : 0.f;
     if (ok && w == 0) delta[row] = dl;
+    const uint64_t seed = a.drop_below ? *a.seed : 0;
     for (int kt = 0; kt <= qt; ++kt) {
         __syncthreads();
         stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
@@ -211,8 +250,14 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_q(AttnArgs a, float scale, cons
         for (int u = 0; u < SUB; ++u) {
             const int j = w * SUB + u;
             if (j < jlim) {
-                const float pr = exp2f(dot<DM>(qr, ks + j * DM) - lz);
-                const float ds = pr * (dot<DM>(go, vs + j * DM) - dl);
+                float sc = dot<DM>(qr, ks + j * DM), gf = 1.f;
+                if (a.train) {
+                    bool live;
+                    sc = train_logit(a, seed, int(blockIdx.y), i, kt * QR + j, sc, live);
+                    gf = live ? a.keep_scale : 0.f;
+                }
+                const float pr = exp2f(sc - lz);
+                const float ds = gf * pr * (dot<DM>(go, vs + j * DM) - dl);
                 axpy<DM>(dq, ds, ks + j * DM);
             }
         }
@@ -253,6 +298,7 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
         dk[c] = dv[c] = 0.f;
     }
     const int64_t rb = (int64_t(p) * a.nh + h) * a.n;
+    const uint64_t seed = a.drop_below ? *a.seed : 0;
     for (int qt = kt; qt < nt; ++qt) {
         __syncthreads();
         stage<T, DM>(qs, q, a, p, h, a.dk, qt * QR, 0);
@@ -269,9 +315,15 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
         for (int u = 0; u < SUB; ++u) {
             const int ii = w * SUB + u;
             if (ii >= i0 && ii < iend) {
-                const float pr = exp2f(dot<DM>(kr, qs + ii * DM) - ls[ii]);
+                float sc = dot<DM>(kr, qs + ii * DM), gf = 1.f;
+                if (a.train) {
+                    bool live;
+                    sc = train_logit(a, seed, int(blockIdx.y), qt * QR + ii, j, sc, live);
+                    gf = live ? a.keep_scale : 0.f;
+                }
+                const float pr = exp2f(sc - ls[ii]);
                 axpy<DM>(dv, pr, gs + ii * DM);
-                const float ds = pr * (dot<DM>(vr, gs + ii * DM) - dls[ii]);
+                const float ds = gf * pr * (dot<DM>(vr, gs + ii * DM) - dls[ii]);
                 axpy<DM>(dk, ds, qs + ii * DM);
             }
         }
@@ -316,7 +368,7 @@ void launch_bwd(const AttnArgs &a, float scale, const void *q, const void *k, co
 }
 
 int check_args(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, AttnArgs &a,
-               float scale) {
+               float scale, const vq3d_attn_train *train) {
     if (dtype != VQ3D_BF16 && dtype != VQ3D_F32) return 1;
     if (nprob < 1 || n < 1 || nh < 1 || dk < 1 || dv < 1 || !dmax_of(dk, dv)) return 1;
     if (int64_t(nprob) * nh > 65535) return 1;
@@ -326,6 +378,19 @@ int check_args(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, 
     a.dk = dk;
     a.dv = dv;
     a.c2 = scale * LOG2E;
+    a.train = 0;
+    a.drop_below = 0;
+    a.keep_scale = 1.f;
+    a.seed = nullptr;
+    if (train) {
+        const double p = train->dropout_p;
+        if (!(p >= 0.0 && p < 1.0)) return 1;
+        if (p > 0.0 && !train->seed) return 1;
+        a.train = 1;
+        a.drop_below = uint32_t(std::min(4294967295.0, p * 4294967296.0));
+        a.keep_scale = float(1.0 / (1.0 - p));
+        a.seed = train->seed;
+    }
     return 0;
 }
 
@@ -347,8 +412,15 @@ size_t vq3d_causal_attn_workspace_bytes(int32_t nprob, int32_t n, int32_t nh) {
 
 int vq3d_causal_attn_fwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
                          const void *q, const void *k, const void *v, void *out, float *lse, vq3d_stream_t stream) {
+    return vq3d_causal_attn_fwd_ex(dtype, nprob, n, nh, dk, dv, scale, q, k, v, nullptr, out, lse, stream);
+}
+
+int vq3d_causal_attn_fwd_ex(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                            const void *q, const void *k, const void *v, const vq3d_attn_train *train, void *out,
+                            float *lse, vq3d_stream_t stream) {
     AttnArgs a;
-    if (check_args(dtype, nprob, n, nh, dk, dv, a, scale)) return fail("causal_attn_fwd: unsupported shape / dtype");
+    if (check_args(dtype, nprob, n, nh, dk, dv, a, scale, train))
+        return fail("causal_attn_fwd: unsupported shape / dtype / dropout (p in [0, 1), a seed when p > 0)");
     if (!q || !k || !v || !out || !lse) return fail("causal_attn_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     const int dm = dmax_of(dk, dv);
@@ -368,8 +440,17 @@ int vq3d_causal_attn_bwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, in
                          const void *q, const void *k, const void *v, const void *out, const void *gout,
                          const float *lse, void *workspace, size_t workspace_bytes, void *gq, void *gk, void *gv,
                          vq3d_stream_t stream) {
+    return vq3d_causal_attn_bwd_ex(dtype, nprob, n, nh, dk, dv, scale, q, k, v, nullptr, out, gout, lse, workspace,
+                                   workspace_bytes, gq, gk, gv, stream);
+}
+
+int vq3d_causal_attn_bwd_ex(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                            const void *q, const void *k, const void *v, const vq3d_attn_train *train,
+                            const void *out, const void *gout, const float *lse, void *workspace,
+                            size_t workspace_bytes, void *gq, void *gk, void *gv, vq3d_stream_t stream) {
     AttnArgs a;
-    if (check_args(dtype, nprob, n, nh, dk, dv, a, scale)) return fail("causal_attn_bwd: unsupported shape / dtype");
+    if (check_args(dtype, nprob, n, nh, dk, dv, a, scale, train))
+        return fail("causal_attn_bwd: unsupported shape / dtype / dropout (p in [0, 1), a seed when p > 0)");
     if (!q || !k || !v || !out || !gout || !lse || !workspace || !gq || !gk || !gv)
         return fail("causal_attn_bwd: null pointer");
     if (workspace_bytes < vq3d_causal_attn_workspace_bytes(nprob, n, nh)) return fail("causal_attn_bwd: workspace too small");

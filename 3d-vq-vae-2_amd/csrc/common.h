@@ -34,6 +34,83 @@ struct FastDiv {
 __device__ __forceinline__ void st(float *p, float v) { *p = v; }
 __device__ __forceinline__ void st(bf16_t *p, float v) { *p = f2bf(v); }
 
+// ---------------------------------------------------------------- N-element vector moves
+// N consecutive elements of storage type T (bf16 or fp32) as raw 32-bit words, so a kernel can
+// issue a whole voxel's (or a run of voxels') loads before it converts anything.  N * sizeof(T)
+// is 2, 4, 8 or a multiple of 16 bytes and the address is aligned to min(that, 16).
+template <typename T, int N>
+struct Raw {
+    static constexpr int B = N * int(sizeof(T));
+    static constexpr int W = (B + 3) / 4;
+    uint32_t w[W];
+};
+template <typename T, int N>
+__device__ __forceinline__ Raw<T, N> ldraw(const T *__restrict__ p) {
+    Raw<T, N> r;
+    constexpr int B = Raw<T, N>::B;
+    if constexpr (B == 2) {
+        r.w[0] = *reinterpret_cast<const uint16_t *>(p);
+    } else if constexpr (B == 4) {
+        r.w[0] = *reinterpret_cast<const uint32_t *>(p);
+    } else if constexpr (B == 8) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(p);
+        r.w[0] = u.x;
+        r.w[1] = u.y;
+    } else {
+        static_assert(B % 16 == 0, "vector width");
+#pragma unroll
+        for (int i = 0; i < B / 16; ++i) {
+            const uint4 u = reinterpret_cast<const uint4 *>(p)[i];
+            r.w[4 * i] = u.x;
+            r.w[4 * i + 1] = u.y;
+            r.w[4 * i + 2] = u.z;
+            r.w[4 * i + 3] = u.w;
+        }
+    }
+    return r;
+}
+template <typename T, int N>
+__device__ __forceinline__ void unraw(const Raw<T, N> &r, float (&o)[N]) {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) o[i] = __uint_as_float(r.w[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) o[i] = (i & 1) ? __uint_as_float(r.w[i / 2] & 0xffff0000u) : __uint_as_float(r.w[i / 2] << 16);
+    }
+}
+template <typename T, int N>
+__device__ __forceinline__ void ldvec(const T *__restrict__ p, float (&o)[N]) {
+    unraw<T, N>(ldraw<T, N>(p), o);
+}
+// N values rounded to T (bf16: round-to-nearest-even) as 2 / 4 / 8 / 16n-byte stores
+template <typename T, int N>
+__device__ __forceinline__ void stvec(T *__restrict__ p, const float (&v)[N]) {
+    Raw<T, N> r;
+    constexpr int B = Raw<T, N>::B;
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) r.w[i] = __float_as_uint(v[i]);
+    } else if constexpr (N == 1) {
+        r.w[0] = f2bf(v[0]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) r.w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+    }
+    if constexpr (B == 2) {
+        *reinterpret_cast<uint16_t *>(p) = uint16_t(r.w[0]);
+    } else if constexpr (B == 4) {
+        *reinterpret_cast<uint32_t *>(p) = r.w[0];
+    } else if constexpr (B == 8) {
+        *reinterpret_cast<uint2 *>(p) = uint2{r.w[0], r.w[1]};
+    } else {
+        static_assert(B % 16 == 0, "vector width");
+#pragma unroll
+        for (int i = 0; i < B / 16; ++i)
+            reinterpret_cast<uint4 *>(p)[i] = uint4{r.w[4 * i], r.w[4 * i + 1], r.w[4 * i + 2], r.w[4 * i + 3]};
+    }
+}
+
 // ---------------------------------------------------------------- activations
 __device__ __forceinline__ float elu(float z) { return z > 0.f ? z : (expf(z) - 1.f); }
 __device__ __forceinline__ float elu_grad(float z) { return z > 0.f ? 1.f : expf(z); }

@@ -101,11 +101,14 @@ int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const
 // few-channel blocks on the big grids (preact_col.hip), behind vq3d_preact_small_*
 bool col_supported(int batch, int C, int BR, int h, int w, int d);
 size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d);
-int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1, const float *w2,
-            const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3, hipStream_t s);
-int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
-            const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
-            const vq3d_preact_grads &gr, void *workspace, void *gx, int stages, hipStream_t s);
+// xdt / odt: storage (VQ3D_BF16 | VQ3D_F32) of the residual stream in (x, gx) and out (out, g)
+int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1,
+            const float *w2, const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3,
+            hipStream_t s);
+int col_bwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *g, const void *x,
+            const void *t2, const void *t3, const float *w1, const float *w2, const float *w3,
+            const vq3d_preact_params &p, const vq3d_preact_grads &gr, void *workspace, void *gx, int stages,
+            hipStream_t s);
 bool mid_w2grad_ok(const vq3d_conv_desc *d);
 size_t mid_w2grad_ws(const vq3d_conv_desc *d);
 int mid_w2grad(const vq3d_conv_desc *d, const void *x, const void *g, float *dw, void *ws, size_t ws_bytes,

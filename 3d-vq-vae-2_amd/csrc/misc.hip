@@ -134,6 +134,72 @@ __device__ __forceinline__ float huber_grad(float d) {
     return d <= -1.f ? -1.f : (d >= 1.f ? 1.f : d);
 }
 
+// ---------------------------------------------------------------- Encoder2.parse_input
+// Conv3d(1 -> C, k = 1, bias) on the fp32 input volume (layers.py:535): y[v][c] = w[c] x[v] + b[c],
+// written in bf16 (the next conv's operand).  The volume is read in fp32, never rounded: under the
+// reference's fp16 autocast this conv reads it with 11 mantissa bits, a bf16 copy would have 8.
+// A thread owns 4 consecutive voxels (one 16-byte load, 4 C bf16 of output).
+template <int C>
+__global__ __launch_bounds__(256) void k_pin_fwd(const float *__restrict__ x, int64_t n4, const float *__restrict__ w,
+                                                const float *__restrict__ b, bf16_t *__restrict__ y) {
+    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float4 xv = reinterpret_cast<const float4 *>(x)[i];
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    float o[4 * C];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int c = 0; c < C; ++c) o[v * C + c] = fmaf(w[c], xs[v], b[c]);
+    stvec<bf16_t, 4 * C>(y + i * 4 * C, o);
+}
+// weight / bias gradient partials per workgroup: [block][2 C] = (sum g x, sum g) per channel
+template <int C>
+__global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, const bf16_t *__restrict__ g, int64_t n4,
+                                                  float *__restrict__ part) {
+    __shared__ float red[4];
+    float sw[C], sb[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) sw[c] = sb[c] = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
+        const float4 xv = reinterpret_cast<const float4 *>(x)[i];
+        const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+        float gv[4 * C];
+        ldvec<bf16_t, 4 * C>(g + i * 4 * C, gv);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                sw[c] = fmaf(gv[v * C + c], xs[v], sw[c]);
+                sb[c] += gv[v * C + c];
+            }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const float a = block_sum<float, 256>(sw[c], red);
+        const float bb = block_sum<float, 256>(sb[c], red);
+        if (threadIdx.x == 0) {
+            part[int64_t(blockIdx.x) * 2 * C + c] = a;
+            part[int64_t(blockIdx.x) * 2 * C + C + c] = bb;
+        }
+    }
+}
+// fixed-order sum of the partials, accumulated into dw / db
+template <int C>
+__global__ __launch_bounds__(64) void k_pin_wgrad_fin(const float *__restrict__ part, int nb, float *__restrict__ dw,
+                                                     float *__restrict__ db) {
+    const int e = threadIdx.x;
+    if (e >= 2 * C) return;
+    float t = 0.f;
+    for (int j = 0; j < nb; ++j) t += part[int64_t(j) * 2 * C + e];
+    if (e < C) {
+        if (dw) dw[e] += t;
+    } else if (db) {
+        db[e - C] += t;
+    }
+}
+static int pin_blocks(int64_t voxels) { return int(std::min<int64_t>(2048, (voxels / 4 + 255) / 256)); }
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_recon_fwd(const T *__restrict__ dec, const float *__restrict__ x,
                                                   const int64_t *__restrict__ nvs, int B, int H, int W, int D,
@@ -419,6 +485,49 @@ int64_t vq3d_cylinder_count(int32_t h, int32_t w) {
             c += (a * a + b * b <= m * m);
         }
     return c;
+}
+
+int vq3d_parse_input_fwd(int64_t voxels, int32_t channels, const float *x, const float *w, const float *b, void *y,
+                         vq3d_stream_t stream) {
+    if (voxels <= 0 || voxels % 4 || !(channels == 2 || channels == 4 || channels == 8))
+        return fail("parse_input_fwd: voxels % 4 == 0 and channels in {2, 4, 8}");
+    if (!x || !w || !b || !y) return fail("parse_input_fwd: null pointer");
+    const int64_t n4 = voxels / 4;
+    const unsigned nb = unsigned((n4 + 255) / 256);
+    hipStream_t s = as_stream(stream);
+    bf16_t *Y = static_cast<bf16_t *>(y);
+    if (channels == 2) k_pin_fwd<2><<<nb, 256, 0, s>>>(x, n4, w, b, Y);
+    else if (channels == 4) k_pin_fwd<4><<<nb, 256, 0, s>>>(x, n4, w, b, Y);
+    else k_pin_fwd<8><<<nb, 256, 0, s>>>(x, n4, w, b, Y);
+    return check_launch("parse_input_fwd");
+}
+
+size_t vq3d_parse_input_workspace_bytes(int64_t voxels, int32_t channels) {
+    return size_t(pin_blocks(voxels)) * 2 * size_t(channels > 0 ? channels : 1) * 4;
+}
+
+int vq3d_parse_input_bwd(int64_t voxels, int32_t channels, const float *x, const void *g, float *dw, float *db,
+                         void *workspace, size_t ws_bytes, vq3d_stream_t stream) {
+    if (voxels <= 0 || voxels % 4 || !(channels == 2 || channels == 4 || channels == 8))
+        return fail("parse_input_bwd: voxels % 4 == 0 and channels in {2, 4, 8}");
+    if (!x || !g || !workspace) return fail("parse_input_bwd: null pointer");
+    if (ws_bytes < vq3d_parse_input_workspace_bytes(voxels, channels)) return fail("parse_input_bwd: workspace too small");
+    const int nb = pin_blocks(voxels);
+    const int64_t n4 = voxels / 4;
+    hipStream_t s = as_stream(stream);
+    const bf16_t *G = static_cast<const bf16_t *>(g);
+    float *part = static_cast<float *>(workspace);
+    if (channels == 2) {
+        k_pin_wgrad<2><<<nb, 256, 0, s>>>(x, G, n4, part);
+        k_pin_wgrad_fin<2><<<1, 64, 0, s>>>(part, nb, dw, db);
+    } else if (channels == 4) {
+        k_pin_wgrad<4><<<nb, 256, 0, s>>>(x, G, n4, part);
+        k_pin_wgrad_fin<4><<<1, 64, 0, s>>>(part, nb, dw, db);
+    } else {
+        k_pin_wgrad<8><<<nb, 256, 0, s>>>(x, G, n4, part);
+        k_pin_wgrad_fin<8><<<1, 64, 0, s>>>(part, nb, dw, db);
+    }
+    return check_launch("parse_input_bwd");
 }
 
 size_t vq3d_recon_loss_workspace_size(int32_t, int32_t, int32_t, int32_t) { return 4096 * 4; }

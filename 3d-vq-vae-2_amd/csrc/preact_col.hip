@@ -28,8 +28,10 @@
 //            C: per thread 4 voxels: gz1 = bf16(gt2 * elu'(t2)), gx = g + (W1^T gz1) * elu'(x + b1a),
 //               the W1 gradient (sum gz1 (x) u1) and the b2 / b1 sums
 //            per-brick partial rows [brick][entry], summed in a fixed order by k_col_reduce1 / 2.
-// Rounding points are the unfused path's: t2, t3, gz3, gz1, gx, out rounded to bf16, fp32
-// accumulation; the W1 gradient reads u1 rounded to bf16 (the unfused wgrad's operand).
+// Rounding points are the unfused path's: t2, t3, gz3, gz1 rounded to bf16 (the conv operands), fp32
+// accumulation; the W1 gradient reads u1 rounded to bf16 (the unfused wgrad's operand).  The
+// residual stream x / out (and g / gx) is stored bf16 or fp32 per tensor (template TX / TO): a run
+// of blocks keeps it fp32 between its blocks, as the reference's autocast blocks return fp32.
 #include "engines.h"
 
 #include <algorithm>
@@ -166,13 +168,6 @@ __device__ __forceinline__ typename Vec<N>::U packv(const float (&v)[N]) {
         else return uint4{w[0], w[1], w[2], w[3]};
     }
 }
-// n bf16 (n * 2 bytes, a multiple of 16) between global memory and registers as uint4
-template <int NB>
-__device__ __forceinline__ void ld16s(const bf16_t *__restrict__ p, uint4 (&o)[NB]) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) o[i] = reinterpret_cast<const uint4 *>(p)[i];
-}
-
 struct Scal {
     float b1a, b1b, b2a, b2b, b3a, b3b, sc, b4;
 };
@@ -254,10 +249,12 @@ __device__ __forceinline__ bf16x8 win_frag(const bf16_t *h, int off) {
 }
 
 // ============================================================================================ forward
-template <int C, int BR>
-__global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restrict__ x, const float *__restrict__ w1,
+// TX / TO: storage of the residual stream in / out (bf16 or fp32; a run of blocks carries it in
+// fp32 between its blocks like the reference's autocast blocks, layers.py:187-193)
+template <int C, int BR, typename TX, typename TO>
+__global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ x, const float *__restrict__ w1,
                                                 const float *__restrict__ w2, const float *__restrict__ w3,
-                                                vq3d_preact_params p, bf16_t *__restrict__ out,
+                                                vq3d_preact_params p, TO *__restrict__ out,
                                                 bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
     using K = K3<BR>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -276,19 +273,19 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
     // A. t2 on the halo, every x load issued first
     {
         constexpr int P = (HVX + NT - 1) / NT;
-        typename Vec<C>::U xv[P];
+        Raw<TX, C> xv[P];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             int line, pos;
             const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
-            xv[u] = (COL_EXP & 1) ? typename Vec<C>::U{} : *reinterpret_cast<const typename Vec<C>::U *>(x + int64_t(vx) * C);
+            xv[u] = (COL_EXP & 1) ? Raw<TX, C>{} : ldraw<TX, C>(x + int64_t(vx) * C);
         }
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             const int q = tid + u * NT;
             if (!(COL_EXP & 2) && q < HVX) {
                 float xf[C], t[BR];
-                unpack<C>(xv[u], xf);
+                unraw<TX, C>(xv[u], xf);
 #pragma unroll
                 for (int c = 0; c < C; ++c) xf[c] = elu_f(xf[c] + s.b1a) + s.b1b;
 #pragma unroll
@@ -306,9 +303,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
     // this thread's 4 voxels (phase C): brick line ln, D-group dg; x in flight during phase B
     const int ln = tid / (BD / DV), dg = tid % (BD / DV);
     const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
-    constexpr int NXB = DV * C * 2 / 16;  // 16-byte pieces of the 8 voxels' x
-    uint4 xr[NXB];
-    ld16s<NXB>(x + vox0 * C, xr);
+    const Raw<TX, DV * C> xr = ldraw<TX, DV * C>(x + vox0 * C);
     // B. raw W2 (*) t2 per m-tile
     int woff[K::KS];
     win_offsets<BR>(row, kb, woff);
@@ -354,40 +349,26 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const bf16_t *__restric
         if (t3o) store_words<DV * BR / 2>(t3o + vox0 * BR, w);  // NULL: eval forward, nothing saved
     }
     float xf[DV * C];
+    unraw<TX, DV * C>(xr, xf);
 #pragma unroll
-    for (int i = 0; i < NXB; ++i) {
-        const uint32_t ww[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+    for (int e = 0; e < DV * C; ++e) {
+        const int vv = e / C, c = e - vv * C;
+        float r = 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            xf[8 * i + 2 * k] = __uint_as_float(ww[k] << 16);
-            xf[8 * i + 2 * k + 1] = __uint_as_float(ww[k] & 0xffff0000u);
-        }
+        for (int oo = 0; oo < BR; ++oo) r = fmaf(w3[c * BR + oo], t3v[vv][oo], r);
+        xf[e] = r * s.sc + s.b4 + xf[e];
     }
-    uint4 orr[NXB];
-#pragma unroll
-    for (int i = 0; i < NXB; ++i) {
-        float ov[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int e = 8 * i + k, vv = e / C, c = e - vv * C;
-            float r = 0.f;
-#pragma unroll
-            for (int oo = 0; oo < BR; ++oo) r = fmaf(w3[c * BR + oo], t3v[vv][oo], r);
-            ov[k] = r * s.sc + s.b4 + xf[e];
-        }
-        orr[i] = __builtin_bit_cast(uint4, pack8(ov));
-    }
-#pragma unroll
-    for (int i = 0; i < NXB; ++i) reinterpret_cast<uint4 *>(out + vox0 * C)[i] = orr[i];
+    stvec<TO, DV * C>(out + vox0 * C, xf);
 }
 
 // ============================================================================================ backward
-template <int C, int BR>
-__global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restrict__ g, const bf16_t *__restrict__ x,
+// g has the storage of the forward's out (TO), x and gx that of its input (TX)
+template <int C, int BR, typename TX, typename TO>
+__global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ g, const TX *__restrict__ x,
                                                 const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
                                                 const float *__restrict__ w1, const float *__restrict__ w2,
                                                 const float *__restrict__ w3, vq3d_preact_params p,
-                                                float *__restrict__ part, bf16_t *__restrict__ gx) {
+                                                float *__restrict__ part, TX *__restrict__ gx) {
     using K = K3<BR>;
     constexpr int NE = n_entries<C, BR>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -423,18 +404,18 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
 #pragma unroll 1
     for (int half = 0; half < 2; ++half) {
         constexpr int P = PH;
-        typename Vec<C>::U gv[P];
+        Raw<TO, C> gv[P];
         typename Vec<BR>::U tv3[P], tv2[P];
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             int line, pos;
             const int vx = halo_voxel(a, o, lbase, min(tid + (half * PH + u) * NT, HVX - 1), line, pos);
             if constexpr (!(COL_EXP & 1)) {
-                gv[u] = *reinterpret_cast<const typename Vec<C>::U *>(g + int64_t(vx) * C);
+                gv[u] = ldraw<TO, C>(g + int64_t(vx) * C);
                 tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
                 tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
             } else {
-                gv[u] = typename Vec<C>::U{};
+                gv[u] = Raw<TO, C>{};
                 tv3[u] = tv2[u] = typename Vec<BR>::U{};
             }
         }
@@ -445,7 +426,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
                 const int line = q / PL, pos = q - line * PL;
                 const bool in = interior(line, pos);
                 float gf[C], t3f[BR], t2f[BR], z[BR];
-                unpack<C>(gv[u], gf);
+                unraw<TO, C>(gv[u], gf);
                 unpack<BR>(tv3[u], t3f);
                 unpack<BR>(tv2[u], t2f);
 #pragma unroll
@@ -481,7 +462,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
     // the thread's 4 voxels (phase C): g and x in flight during phase B
     const int ln = tid / (BD / DV), dg = tid % (BD / DV);
     const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
-    constexpr int NXB = DV * C * 2 / 16;
+    constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
     // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
     int woff[K::KS];
     win_offsets<BR>(row, kb, woff);
@@ -525,25 +506,25 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
     for (int oo = 0; oo < BR; ++oo)
 #pragma unroll
         for (int c = 0; c < C; ++c) dw1[oo][c] = 0.f;
-    // 16-byte pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
+    // 8-element pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
     // flight during the current one's math (one piece of registers at a time: occupancy)
     constexpr int PV = 8 / C;
-    auto elem = [](const uint4 &q, int e) {  // element e (0..7) of a piece
-        const int wsel = e >> 1;
-        const uint32_t wv = wsel == 0 ? q.x : wsel == 1 ? q.y : wsel == 2 ? q.z : q.w;
-        return (e & 1) ? __uint_as_float(wv & 0xffff0000u) : __uint_as_float(wv << 16);
-    };
     const int hl0 = ((ln >> 3) + 1) * WL + (ln & 7) + 1;
-    const uint4 *xp = reinterpret_cast<const uint4 *>(x + vox0 * C), *gp = reinterpret_cast<const uint4 *>(g + vox0 * C);
-    uint4 xq = xp[0], gq = gp[0];
+    const TX *xp = x + vox0 * C;
+    const TO *gp = g + vox0 * C;
+    Raw<TX, 8> xq = ldraw<TX, 8>(xp);
+    Raw<TO, 8> gq = ldraw<TO, 8>(gp);
 #pragma unroll 1
     for (int pc = 0; pc < NXB; ++pc) {
-        uint4 xn = xq, gn = gq;
+        Raw<TX, 8> xn = xq;
+        Raw<TO, 8> gn = gq;
         if (pc + 1 < NXB) {
-            xn = xp[pc + 1];
-            gn = gp[pc + 1];
+            xn = ldraw<TX, 8>(xp + 8 * (pc + 1));
+            gn = ldraw<TO, 8>(gp + 8 * (pc + 1));
         }
-        uint32_t ow[4] = {0u, 0u, 0u, 0u};
+        float xe[8], ge[8], ov[8];
+        unraw<TX, 8>(xq, xe);
+        unraw<TO, 8>(gq, ge);
 #pragma unroll
         for (int vi = 0; vi < PV; ++vi) {
             const int i = pc * PV + vi;
@@ -563,18 +544,17 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const bf16_t *__restric
 #pragma unroll
                 for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
                 const int e = vi * C + c;
-                const float zx = elem(xq, e) + s.b1a;
+                const float zx = xe[e] + s.b1a;
                 const float e1 = zx > 0.f ? 1.f : __expf(zx);
                 const float u1 = rbf((zx > 0.f ? zx : e1 - 1.f) + s.b1b);
                 s1b += gt1;
                 s1a = fmaf(gt1, e1, s1a);
-                const uint32_t hb = f2bf(elem(gq, e) + gt1 * e1);
-                ow[e >> 1] |= (e & 1) ? (hb << 16) : hb;
+                ov[e] = ge[e] + gt1 * e1;
 #pragma unroll
                 for (int oo = 0; oo < BR; ++oo) dw1[oo][c] = fmaf(z1[oo], u1, dw1[oo][c]);
             }
         }
-        reinterpret_cast<uint4 *>(gx + vox0 * C)[pc] = uint4{ow[0], ow[1], ow[2], ow[3]};
+        stvec<TX, 8>(gx + vox0 * C + 8 * pc, ov);
         xq = xn;
         gq = gn;
     }
@@ -712,32 +692,56 @@ void allow(Kern k, size_t lds) {
     (void)hipGetLastError();
 }
 
-template <int C, int BR>
-void launch_fwd(const CArgs &a, const bf16_t *x, const float *w1, const float *w2, const float *w3,
-                const vq3d_preact_params &p, bf16_t *out, bf16_t *t2, bf16_t *t3, hipStream_t s) {
+template <int C, int BR, typename TX, typename TO>
+void launch_fwd(const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
+                const vq3d_preact_params &p, void *out, bf16_t *t2, bf16_t *t3, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        allow(k_col_fwd<C, BR>, fwd_lds<C, BR>());
+        allow(k_col_fwd<C, BR, TX, TO>, fwd_lds<C, BR>());
         attr = true;
     }
-    k_col_fwd<C, BR><<<a.nbricks, NT, fwd_lds<C, BR>(), s>>>(a, x, w1, w2, w3, p, out, t2, t3);
+    k_col_fwd<C, BR, TX, TO><<<a.nbricks, NT, fwd_lds<C, BR>(), s>>>(a, static_cast<const TX *>(x), w1, w2, w3, p,
+                                                                     static_cast<TO *>(out), t2, t3);
 }
-template <int C, int BR>
-void launch_bwd(const CArgs &a, const bf16_t *g, const bf16_t *x, const bf16_t *t2, const bf16_t *t3, const float *w1,
+template <int C, int BR, typename TX, typename TO>
+void launch_bwd(const CArgs &a, const void *g, const void *x, const bf16_t *t2, const bf16_t *t3, const float *w1,
                 const float *w2, const float *w3, const vq3d_preact_params &p, const vq3d_preact_grads &gr, float *part,
-                bf16_t *gx, int stages, hipStream_t s) {
+                void *gx, int stages, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        allow(k_col_bwd<C, BR>, bwd_lds<C, BR>());
+        allow(k_col_bwd<C, BR, TX, TO>, bwd_lds<C, BR>());
         attr = true;
     }
-    if (stages & 1) k_col_bwd<C, BR><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, g, x, t2, t3, w1, w2, w3, p, part, gx);
+    if (stages & 1)
+        k_col_bwd<C, BR, TX, TO><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, static_cast<const TO *>(g),
+                                                                         static_cast<const TX *>(x), t2, t3, w1, w2, w3,
+                                                                         p, part, static_cast<TX *>(gx));
     const int nr = (a.nbricks + RCH - 1) / RCH;
     float *part2 = part + size_t(a.nbricks) * n_entries<C, BR>();
     if (stages & 2) {
         k_col_reduce1<C, BR><<<nr, 256, 0, s>>>(part, a.nbricks, part2);
         k_col_reduce2<C, BR><<<(n_entries<C, BR>() + 255) / 256, 256, 0, s>>>(part2, nr, p.scale, gr);
     }
+}
+
+// the (x, out) storage pair: VQ3D_BF16 / VQ3D_F32 each
+template <int C, int BR>
+void fwd_io(int xdt, int odt, const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
+            const vq3d_preact_params &p, void *out, bf16_t *t2, bf16_t *t3, hipStream_t s) {
+    if (xdt == VQ3D_BF16 && odt == VQ3D_BF16) launch_fwd<C, BR, bf16_t, bf16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
+    else if (xdt == VQ3D_BF16) launch_fwd<C, BR, bf16_t, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
+    else if (odt == VQ3D_BF16) launch_fwd<C, BR, float, bf16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
+    else launch_fwd<C, BR, float, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
+}
+template <int C, int BR>
+void bwd_io(int xdt, int odt, const CArgs &a, const void *g, const void *x, const bf16_t *t2, const bf16_t *t3,
+            const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p, const vq3d_preact_grads &gr,
+            float *part, void *gx, int stages, hipStream_t s) {
+    if (xdt == VQ3D_BF16 && odt == VQ3D_BF16)
+        launch_bwd<C, BR, bf16_t, bf16_t>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else if (xdt == VQ3D_BF16) launch_bwd<C, BR, bf16_t, float>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else if (odt == VQ3D_BF16) launch_bwd<C, BR, float, bf16_t>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else launch_bwd<C, BR, float, float>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
 }
 
 }  // namespace
@@ -775,28 +779,27 @@ size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d) {
     return (size_t(a.nbricks) + (a.nbricks + RCH - 1) / RCH) * ne * 4;
 }
 
-int col_fwd(int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1, const float *w2,
-            const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3, hipStream_t s) {
+int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1,
+            const float *w2, const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3,
+            hipStream_t s) {
     const CArgs a = make_args(batch, h, w, d);
-    auto X = static_cast<const bf16_t *>(x);
-    auto O = static_cast<bf16_t *>(out), T2 = static_cast<bf16_t *>(t2), T3 = static_cast<bf16_t *>(t3);
-    if (C == 2) launch_fwd<2, 1>(a, X, w1, w2, w3, p, O, T2, T3, s);
-    else if (C == 4) launch_fwd<4, 2>(a, X, w1, w2, w3, p, O, T2, T3, s);
-    else launch_fwd<8, 4>(a, X, w1, w2, w3, p, O, T2, T3, s);
+    auto T2 = static_cast<bf16_t *>(t2), T3 = static_cast<bf16_t *>(t3);
+    if (C == 2) fwd_io<2, 1>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
+    else if (C == 4) fwd_io<4, 2>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
+    else fwd_io<8, 4>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
     return check_launch("preact_small_fwd (column kernels)");
 }
 
-int col_bwd(int batch, int C, int BR, int h, int w, int d, const void *g, const void *x, const void *t2, const void *t3,
-            const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p,
-            const vq3d_preact_grads &gr, void *workspace, void *gx, int stages, hipStream_t s) {
+int col_bwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *g, const void *x,
+            const void *t2, const void *t3, const float *w1, const float *w2, const float *w3,
+            const vq3d_preact_params &p, const vq3d_preact_grads &gr, void *workspace, void *gx, int stages,
+            hipStream_t s) {
     const CArgs a = make_args(batch, h, w, d);
-    auto G = static_cast<const bf16_t *>(g), X = static_cast<const bf16_t *>(x);
     auto T2 = static_cast<const bf16_t *>(t2), T3 = static_cast<const bf16_t *>(t3);
-    auto GX = static_cast<bf16_t *>(gx);
     float *part = static_cast<float *>(workspace);
-    if (C == 2) launch_bwd<2, 1>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, stages, s);
-    else if (C == 4) launch_bwd<4, 2>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, stages, s);
-    else launch_bwd<8, 4>(a, G, X, T2, T3, w1, w2, w3, p, gr, part, GX, stages, s);
+    if (C == 2) bwd_io<2, 1>(xdt, odt, a, g, x, T2, T3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else if (C == 4) bwd_io<4, 2>(xdt, odt, a, g, x, T2, T3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else bwd_io<8, 4>(xdt, odt, a, g, x, T2, T3, w1, w2, w3, p, gr, part, gx, stages, s);
     return check_launch("preact_small_bwd (column kernels)");
 }
 

@@ -144,10 +144,11 @@ __device__ __forceinline__ Scal load_scal(const vq3d_preact_params &p) {
 }
 
 // ------------------------------------------------------------------------------------ forward
-template <int C, int BR, int UA = (C <= 4 ? 8 : 4)>
-__global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restrict__ x, const float *__restrict__ w1,
+// TX / TO: storage of the residual stream in / out (bf16 or fp32, as preact_col.hip)
+template <int C, int BR, typename TX, typename TO, int UA = (C <= 4 ? 8 : 4)>
+__global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict__ x, const float *__restrict__ w1,
                                                  const float *__restrict__ w2, const float *__restrict__ w3,
-                                                 vq3d_preact_params p, bf16_t *__restrict__ out,
+                                                 vq3d_preact_params p, TO *__restrict__ out,
                                                  bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *w2s = sm;                  // [tap][c][o]
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restr
             for (int u = 0; u < UA; ++u) {
                 const int q = q0 + u * NT;
                 vox[u] = halo_vox(a, k, q < a.hp ? q : q0, vi[u]);
-                ldv<C>(x + vox[u] * C, xv[u]);
+                ldvec<TX, C>(x + vox[u] * C, xv[u]);
             }
 #pragma unroll
             for (int u = 0; u < UA; ++u) {
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restr
             const int pos = halo_pos(a, v);
             const int64_t vox = brick_vox(a, k, v);
             float xv[C], ov[C];
-            ldv<C>(x + vox * C, xv);  // in flight during the taps
+            ldvec<TX, C>(x + vox * C, xv);  // in flight during the taps
             float acc[BR];
 #pragma unroll
             for (int o = 0; o < BR; ++o) acc[o] = 0.f;
@@ -227,18 +228,19 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const bf16_t *__restr
                 for (int o = 0; o < BR; ++o) r = fmaf(w3s[co * BR + o], t3v[o], r);
                 ov[co] = r * s.sc + s.b4 + xv[co];
             }
-            stv<C>(out + vox * C, ov);
+            stvec<TO, C>(out + vox * C, ov);
         }
     }
 }
 
 // ------------------------------------------------------------------------------------ backward
-template <int C, int BR, int UB = (C <= 4 ? 4 : 2), int S2 = s2_of(BR)>
-__global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restrict__ g, const bf16_t *__restrict__ x,
+// g has the forward out's storage (TO), x and gx the input's (TX)
+template <int C, int BR, typename TX, typename TO, int UB = (C <= 4 ? 4 : 2), int S2 = s2_of(BR)>
+__global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict__ g, const TX *__restrict__ x,
                                                  const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
                                                  const float *__restrict__ w1, const float *__restrict__ w2,
                                                  const float *__restrict__ w3, vq3d_preact_params p,
-                                                 float *__restrict__ part, bf16_t *__restrict__ gx) {
+                                                 float *__restrict__ part, TX *__restrict__ gx) {
     constexpr int E1 = C * BR, E2 = 27 * BR * BR, E = n_entries(C, BR);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *w2t = sm;                      // [tap][o][c]
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
       for (int u = 0; u < UB; ++u) {  // UB positions' loads in flight before any compute
         const int q = q0 + u * NT;
         const int64_t vox = halo_vox(a, k, q < a.hp ? q : q0, vis[u]);
-        ldv<C>(g + vox * C, gvs[u]);
+        ldvec<TO, C>(g + vox * C, gvs[u]);
         ldv<BR>(t3 + vox * BR, t3vs[u]);
         ldv<BR>(t2 + vox * BR, t2vs[u]);
       }
@@ -319,7 +321,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
         const int pos = halo_pos(a, v);
         const int64_t vox = brick_vox(a, k, v);
         float xv[C], gxv[C];
-        ldv<C>(x + vox * C, xv);  // in flight during the taps
+        ldvec<TX, C>(x + vox * C, xv);  // in flight during the taps
         float dt[BR];
 #pragma unroll
         for (int c = 0; c < BR; ++c) dt[c] = 0.f;
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const bf16_t *__restr
                 acc3[o][ci] = fmaf(z1[o], u, acc3[o][ci]);
             }
         }
-        stv<C>(gx + vox * C, gxv);
+        stvec<TX, C>(gx + vox * C, gxv);
     }
     const int nb = gridDim.x;
     // 3. W2 weight-gradient partial: thread (g9 = (kh, kw), sub) runs over D-lines of the brick,
@@ -585,26 +587,51 @@ size_t vq3d_preact_small_workspace_bytes(int32_t batch, int32_t channels, int32_
 int vq3d_preact_small_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                           int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                           const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
+    if (dtype != VQ3D_BF16) return fail("preact_small_fwd: the fused few-channel kernels take bf16 operands");
+    return vq3d_preact_small_fwd_io(dtype, dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, p, out, t2, t3,
+                                    stream);
+}
+
+namespace {
+bool io_ok(int32_t xdt, int32_t odt) {
+    return (xdt == VQ3D_BF16 || xdt == VQ3D_F32) && (odt == VQ3D_BF16 || odt == VQ3D_F32);
+}
+}  // namespace
+
+int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels, int32_t branch,
+                             int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
+                             const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,
+                             vq3d_stream_t stream) {
     SArgs a;
     if (!x || !w1 || !w2 || !w3 || !p || !out) return fail("preact_small_fwd: null pointer");
-    if (dtype == VQ3D_BF16 && col_supported(batch, channels, branch, h, w, dd))
-        return col_fwd(batch, channels, branch, h, w, dd, x, w1, w2, w3, *p, out, t2, t3, as_stream(stream));
-    if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_fwd: stream storage must be VQ3D_BF16 or VQ3D_F32");
+    if (col_supported(batch, channels, branch, h, w, dd))
+        return col_fwd(x_dtype, out_dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, *p, out, t2, t3,
+                       as_stream(stream));
+    if (!plan(batch, channels, branch, h, w, dd, a))
         return fail("preact_small_fwd: shape outside the fused few-channel block kernels");
     hipStream_t s = as_stream(stream);
     const size_t lds = lds_fwd(a, branch);
-#define F(C_, B_)                                                                                              \
-    if (channels == C_ && branch == B_) {                                                                      \
+#define F2(C_, B_, TX_, TO_)                                                                                   \
+    {                                                                                                          \
         static bool attr = false;                                                                              \
         if (!attr) {                                                                                           \
-            allow_lds(k_small_fwd<C_, B_>);                                                                    \
+            allow_lds(k_small_fwd<C_, B_, TX_, TO_>);                                                          \
             attr = true;                                                                                       \
         }                                                                                                      \
-        k_small_fwd<C_, B_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const bf16_t *)x, w1, w2, w3, *p,           \
-                                                                (bf16_t *)out, (bf16_t *)t2, (bf16_t *)t3);    \
+        k_small_fwd<C_, B_, TX_, TO_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const TX_ *)x, w1, w2, w3, *p,  \
+                                                                          (TO_ *)out, (bf16_t *)t2, (bf16_t *)t3); \
+    }
+#define F(C_, B_)                                                                                              \
+    if (channels == C_ && branch == B_) {                                                                      \
+        if (x_dtype == VQ3D_BF16 && out_dtype == VQ3D_BF16) F2(C_, B_, bf16_t, bf16_t)                         \
+        else if (x_dtype == VQ3D_BF16) F2(C_, B_, bf16_t, float)                                               \
+        else if (out_dtype == VQ3D_BF16) F2(C_, B_, float, bf16_t)                                             \
+        else F2(C_, B_, float, float)                                                                          \
     }
     F(2, 1) else F(4, 2) else F(8, 4)
 #undef F
+#undef F2
     return check_launch("preact_small_fwd");
 }
 
@@ -621,42 +648,61 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
                                  const void *t3, const float *w1, const float *w2, const float *w3,
                                  const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                  size_t ws_bytes, void *gx, vq3d_stream_t stream) {
+    if (dtype != VQ3D_BF16) return fail("preact_small_bwd: the fused few-channel kernels take bf16 operands");
+    return vq3d_preact_small_bwd_stages_io(stages, dtype, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1,
+                                           w2, w3, p, gr, workspace, ws_bytes, gx, stream);
+}
+
+int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out_dtype, int32_t batch,
+                                    int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd, const void *g,
+                                    const void *x, const void *t2, const void *t3, const float *w1, const float *w2,
+                                    const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                                    void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream) {
     SArgs a;
     if (stages < 1 || stages > 3) return fail("preact_small_bwd: stages must be a mask of 1 | 2");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx)
         return fail("preact_small_bwd: null pointer");
-    if (dtype == VQ3D_BF16 && col_supported(batch, channels, branch, h, w, dd)) {
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_bwd: stream storage must be VQ3D_BF16 or VQ3D_F32");
+    if (col_supported(batch, channels, branch, h, w, dd)) {
         const vq3d_preact_grads &G = *gr;
         if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||
             !G.dbias3b || !G.dscale || !G.dbias4)
             return fail("preact_small_bwd: every gradient buffer is required");
         if (!workspace || ws_bytes < col_workspace_bytes(batch, channels, branch, h, w, dd))
             return fail("preact_small_bwd: workspace too small");
-        return col_bwd(batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, *p, G, workspace, gx, stages,
-                       as_stream(stream));
+        return col_bwd(x_dtype, out_dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1, w2, w3, *p, G,
+                       workspace, gx, stages, as_stream(stream));
     }
-    if (dtype != VQ3D_BF16 || !plan(batch, channels, branch, h, w, dd, a))
+    if (!plan(batch, channels, branch, h, w, dd, a))
         return fail("preact_small_bwd: shape outside the fused few-channel block kernels");
     const int ne = n_entries(channels, branch) + kNScal;
     if (!workspace || ws_bytes < size_t(a.nbricks) * ne * 4) return fail("preact_small_bwd: workspace too small");
     hipStream_t s = as_stream(stream);
     const size_t lds = lds_bwd(a, channels, branch);
     float *part = static_cast<float *>(workspace);
-#define Bk(C_, B_)                                                                                             \
-    if (channels == C_ && branch == B_) {                                                                      \
+#define B2(C_, B_, TX_, TO_)                                                                                   \
+    {                                                                                                          \
         static bool attr = false;                                                                              \
         if (!attr) {                                                                                           \
-            allow_lds(k_small_bwd<C_, B_>);                                                                    \
+            allow_lds(k_small_bwd<C_, B_, TX_, TO_>);                                                          \
             attr = true;                                                                                       \
         }                                                                                                      \
         if (stages & 1)                                                                                        \
-            k_small_bwd<C_, B_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const bf16_t *)g, (const bf16_t *)x,    \
-                                                                    (const bf16_t *)t2, (const bf16_t *)t3, w1, \
-                                                                    w2, w3, *p, part, (bf16_t *)gx);           \
+            k_small_bwd<C_, B_, TX_, TO_><<<unsigned(a.nbricks), NT, lds, s>>>(                                \
+                a, (const TO_ *)g, (const TX_ *)x, (const bf16_t *)t2, (const bf16_t *)t3, w1, w2, w3, *p, part,  \
+                (TX_ *)gx);                                                                                    \
+    }
+#define Bk(C_, B_)                                                                                             \
+    if (channels == C_ && branch == B_) {                                                                      \
+        if (x_dtype == VQ3D_BF16 && out_dtype == VQ3D_BF16) B2(C_, B_, bf16_t, bf16_t)                         \
+        else if (x_dtype == VQ3D_BF16) B2(C_, B_, bf16_t, float)                                               \
+        else if (out_dtype == VQ3D_BF16) B2(C_, B_, float, bf16_t)                                             \
+        else B2(C_, B_, float, float)                                                                          \
         if (stages & 2) k_small_bwd_reduce<C_, B_><<<unsigned(ne), NT, 0, s>>>(part, a.nbricks, p->scale, *gr); \
     }
     Bk(2, 1) else Bk(4, 2) else Bk(8, 4)
 #undef Bk
+#undef B2
     return check_launch("preact_small_bwd");
 }
 

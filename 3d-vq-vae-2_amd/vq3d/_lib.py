@@ -43,6 +43,10 @@ class PreactGrads(ctypes.Structure):
                                  "dbias3b", "dscale", "dbias4")]
 
 
+class AttnTrain(ctypes.Structure):
+    _fields_ = [("dropout_p", ctypes.c_double), ("seed", P)]
+
+
 class DgradEpilogue(ctypes.Structure):
     _fields_ = [("aux", P), ("aux_kind", c_int), ("aux_b", P), ("addend", P)]
 
@@ -88,6 +92,8 @@ _SIGS = {
     "vq3d_preact_small_bwd": (c_int, [c_int] * 7 + [P] * 10 + [c_size, P, P]),
     "vq3d_preact_small_bwd_stages": (c_int, [c_int] * 8 + [P] * 10 + [c_size, P, P]),
     "vq3d_preact_small_reduce_run": (c_int, [c_int] * 7 + [P, c_size, P, P, P]),
+    "vq3d_preact_small_fwd_io": (c_int, [c_int] * 8 + [P] * 9),
+    "vq3d_preact_small_bwd_stages_io": (c_int, [c_int] * 9 + [P] * 10 + [c_size, P, P]),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),
     "vq3d_vq_nearest": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, c_int, P, P, P, P]),
     "vq3d_vq_commit_loss": (c_int, [P, c_float, P, P]),
@@ -96,6 +102,9 @@ _SIGS = {
     "vq3d_vq_ema_update": (c_int, [P, P, P, P, P, c_int, c_int, c_float, c_float, P]),
     "vq3d_vq_moments": (c_int, [c_int, P, c_i64, c_int, P, P, P, P]),
     "vq3d_vq_init_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, c_float, P]),
+    "vq3d_parse_input_fwd": (c_int, [c_i64, c_int, P, P, P, P, P]),
+    "vq3d_parse_input_workspace_bytes": (c_size, [c_i64, c_int]),
+    "vq3d_parse_input_bwd": (c_int, [c_i64, c_int, P, P, P, P, P, c_size, P]),
     "vq3d_recon_loss_workspace_size": (c_size, [c_int] * 4),
     "vq3d_recon_loss_fwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "vq3d_recon_loss_bwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
@@ -113,6 +122,8 @@ _SIGS = {
     "vq3d_causal_attn_workspace_bytes": (c_size, [c_int] * 3),
     "vq3d_causal_attn_fwd": (c_int, [c_int] * 6 + [c_float] + [P] * 6),
     "vq3d_causal_attn_bwd": (c_int, [c_int] * 6 + [c_float] + [P] * 7 + [c_size] + [P] * 4),
+    "vq3d_causal_attn_fwd_ex": (c_int, [c_int] * 6 + [c_float] + [P] * 7),
+    "vq3d_causal_attn_bwd_ex": (c_int, [c_int] * 6 + [c_float] + [P] * 8 + [c_size] + [P] * 4),
     "vq3d_elu_bwd_from_output": (c_int, [c_int, P, P, P, c_i64, P]),
     "vq3d_last_error": (ctypes.c_char_p, []),
     "vq3d_version": (ctypes.c_char_p, []),

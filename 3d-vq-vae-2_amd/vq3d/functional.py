@@ -177,10 +177,11 @@ class StackPlan:
     """Device tables of the parameter / gradient pointers of a run of blocks ([block][11], the
     order of vq3d_preact_stack_fwd), rebuilt when the parameters move (flat.py re-views)."""
 
-    def __init__(self, blocks):
+    def __init__(self, blocks, out_dtype=None):
         self.blocks = list(blocks)
         self.params = [_prm_tensor(b, n) for b in self.blocks for n in _PRM]
         self.key = None
+        self.out_dtype = out_dtype  # a run Function's output storage (None: its input's)
 
     def grad_ptrs(self, i):
         """gradient buffer addresses of block i (in the table order), after tables()"""
@@ -315,14 +316,20 @@ class PreActSmallRunFn(torch.autograd.Function):
     """A run of few-channel PreActFixupResBlocks ((C, branch) = (2, 1), (4, 2), (8, 4); preact_small.hip /
     preact_col.hip): the fused forward per block, the fused backward per block into slices of one
     run workspace, and the fixed-order gradient reductions of all blocks as one launch pair at the
-    end (instead of one or two small launches per block).  Numerics are the per-block path's."""
+    end (instead of one or two small launches per block).  The residual stream between the run's
+    blocks is fp32 (ops.fp32_stream(); the reference's autocast blocks return fp32,
+    layers.py:187-193); the run returns its input's dtype, or fp32 when plan.out_dtype says so (the
+    encoder's pre-quantize runs feed the fp32 Quantizer, layers.py:685-687)."""
 
     @staticmethod
     def forward(ctx, x, plan, *params):
         save = any(ctx.needs_input_grad)
         saved = []
-        for blk in plan.blocks:
-            out, t2, t3 = ops.preact_small_fwd(x, blk, save=save)
+        n = len(plan.blocks)
+        last_dt = plan.out_dtype or x.dtype
+        for i, blk in enumerate(plan.blocks):
+            odt = last_dt if i == n - 1 else (torch.float32 if ops.fp32_stream() else x.dtype)
+            out, t2, t3 = ops.preact_small_fwd(x, blk, save=save, out_dtype=odt)
             if save:
                 saved += [x, t2, t3]
             x = out
@@ -428,6 +435,45 @@ def conv(x, spec, x2=None, residual=None):
     return ConvFn.apply(x, x2, residual, spec, *spec.tensors)
 
 
+# ============================================================================================ parse_input
+class ParseInputFn(torch.autograd.Function):
+    """Encoder2.parse_input (layers.py:535): Conv3d(1 -> C, k = 1, bias) reading the fp32 input
+    volume and writing the bf16 activation (vq3d_parse_input_*): the volume is never rounded to
+    bf16 (the reference's autocast rounds it to fp16).  Weight / bias gradients only."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        bsz, _, h, wd, d = x.shape
+        c = w.shape[0]
+        nv = bsz * h * wd * d
+        y = ops.new_act(bsz, c, h, wd, d, torch.bfloat16, x.device)
+        L.call("vq3d_parse_input_fwd", nv, c, L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.stream())
+        ctx.save_for_backward(x)
+        ctx.params = (w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        w, b = ctx.params
+        g = _cl(g)
+        c = w.shape[0]
+        nv = x.numel()
+        nws = int(L.query("vq3d_parse_input_workspace_bytes", nv, c))
+        ws = ops.workspace(nws, x.device)
+        L.call("vq3d_parse_input_bwd", nv, c, L.ptr(x), L.ptr(g), L.ptr(grad_buf(w)), L.ptr(grad_buf(b)), L.ptr(ws),
+               nws, L.stream())
+        grads_ready((w, b))
+        return None, None, None
+
+
+def parse_input_fused(x, conv, compute_dtype):
+    """True when the fp32 volume can go through ParseInputFn (1 input channel, bf16 activations)."""
+    return (compute_dtype == torch.bfloat16 and x.dtype == torch.float32 and x.is_cuda and x.dim() == 5
+            and x.shape[1] == 1 and conv.in_channels == 1 and conv.out_channels in (2, 4, 8)
+            and conv.bias is not None and x.numel() % 4 == 0 and x.is_contiguous())
+
+
 # ============================================================================================ upsample
 class UpsampleFn(torch.autograd.Function):
     """nn.Upsample(trilinear, x2, align_corners=False) of ResizeConv3D (layers.py:591-597)."""
@@ -510,10 +556,12 @@ class QuantizeFn(torch.autograd.Function):
         if q.training:
             embed = ops.copy_(torch.empty_like(q.embed), q.embed)  # pre-update codebook for q / backward
         idx = torch.empty((b, h, w, dz), dtype=torch.int64, device=dev)
-        zst = torch.empty_like(z)
+        # z arrives fp32 from an fp32-stream run; the straight-through output goes on in the model's
+        # conv operand storage (its consumers are convs / the decoder's runs)
+        zst = torch.empty_like(z, dtype=getattr(q, "zst_dtype", None) or z.dtype)
         sq = torch.empty((), dtype=torch.float32, device=dev)
-        L.call("vq3d_vq_nearest", zc, L.ptr(z), n, d, L.ptr(embed), k, L.ptr(idx), zc, L.ptr(zst), L.ptr(sq),
-               L.ptr(ws), st)
+        L.call("vq3d_vq_nearest", zc, L.ptr(z), n, d, L.ptr(embed), k, L.ptr(idx), L.dtype_code(zst), L.ptr(zst),
+               L.ptr(sq), L.ptr(ws), st)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         L.call("vq3d_vq_commit_loss", L.ptr(sq), q.commitment_cost / float(n * d), L.ptr(loss), st)
         if q.training:

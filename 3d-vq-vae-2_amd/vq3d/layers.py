@@ -15,6 +15,7 @@ from torch import nn
 from . import _lib as L
 from . import functional as Fn
 from .evonorm import EvoNorm3DS0
+from . import ops
 from .ops import ConvGeom
 from .parallel import sum_allreduce
 
@@ -228,6 +229,9 @@ class BlockStack(nn.Sequential):
     Fn.PreActMidRunFn (preact_mid.hip), a run of few-channel blocks through Fn.PreActSmallRunFn
     (one reduction for the whole run); everything else runs module by module."""
 
+    out_fp32 = False  # set where the consumer takes an fp32 tensor (the encoder's Quantizers)
+    small_runs_only = False  # Down / UpBlock: only few-channel runs fused (their fp32 stream)
+
     def forward(self, x):
         mods = list(self)
         i = 0
@@ -239,7 +243,10 @@ class BlockStack(nn.Sequential):
                        and mods[j + 1].branch_conv1.weight.shape[0] == nb):
                     j += 1
             fn = None
-            if Fn.stack_eligible(mods[i]):
+            if self.small_runs_only:
+                if j > i and Fn.small_run_eligible(x, mods[i]):
+                    fn = Fn.PreActSmallRunFn
+            elif Fn.stack_eligible(mods[i]):
                 if j > i and self._stack_ok(x, mods[i]):
                     fn = Fn.PreActStackFn
                 elif Fn.wide_eligible(x, mods[i]):
@@ -255,6 +262,9 @@ class BlockStack(nn.Sequential):
                     if not hasattr(self, "_plans"):
                         self._plans = {}
                     plan = self._plans[(i, j)] = Fn.StackPlan(run)
+                # the stack's last run hands an fp32 stream on when the consumer takes it
+                plan.out_dtype = torch.float32 if (self.out_fp32 and j == len(mods) - 1 and
+                                                   fn is Fn.PreActSmallRunFn and ops.fp32_stream()) else None
                 x = fn.apply(x, plan, *plan.params)
                 i = j + 1
             else:
@@ -276,12 +286,15 @@ class DownBlock(nn.Module):
 
     def __init__(self, in_channels, n_down=2, resblock=FixupResBlock, n_post_downscale_blocks=0):
         super().__init__()
-        self.layers = nn.Sequential(*chain.from_iterable(
+        # a BlockStack (an nn.Sequential: same state_dict keys) so the post-downscale blocks run as
+        # one fused run where an engine takes them
+        self.layers = BlockStack(*chain.from_iterable(
             (resblock(in_channels * 2 ** i, in_channels * 2 ** (i + 1), mode='down'),
              *(resblock(in_channels * 2 ** (i + 1), in_channels * 2 ** (i + 1), mode='same')
                for _ in range(n_post_downscale_blocks)))
             for i in range(n_down)
         ))
+        self.layers.small_runs_only = True
 
     def forward(self, data):
         return self.layers(data)
@@ -294,13 +307,14 @@ class UpBlock(nn.Module):
                  n_post_upscale_blocks=0):
         super().__init__()
         assert mode in ('encoder', 'decoder')
-        self.layers = nn.Sequential(*chain.from_iterable((
+        self.layers = BlockStack(*chain.from_iterable((
             (resblock(in_channels if i == n_up - 1 else out_channels * (2 ** (i + 1)), out_channels * (2 ** i),
                       mode='up'),
              *(resblock(out_channels * (2 ** i), out_channels * (2 ** i), mode='same')
                for _ in range(n_post_upscale_blocks)))
             for i in range(n_up - 1, -1, -1)
         )))
+        self.layers.small_runs_only = True
 
     def forward(self, data):
         return self.layers(data)
@@ -345,22 +359,28 @@ class Encoder2(nn.Module):
                 n_up=n_down_per_enc, resblock=resblock, n_post_upscale_blocks=n_post_upscale_blocks))
             self.pre_quantize.append(BlockStack(
                 *(resblock(embedding_dim, embedding_dim, mode='same') for _ in range(n_pre_q_blocks))))
+            self.pre_quantize[-1].out_fp32 = True  # z goes to the fp32 Quantizer (layers.py:685-687)
             self.quantize.append(Quantizer(num_embeddings=num_embeddings[i], embedding_dim=embedding_dim,
                                            commitment_cost=0.1))
             before_channels = after_channels
         self.compute_dtype = torch.float32
 
     def forward(self, data):
-        if data.dtype != self.compute_dtype:
-            from .ops import cast
-            data = cast(data, self.compute_dtype)
-        down = self.parse_input(data)
+        if Fn.parse_input_fused(data, self.parse_input, self.compute_dtype):
+            # the fp32 volume straight into the bf16 activation (never rounded to bf16 itself)
+            down = Fn.ParseInputFn.apply(data, self.parse_input.weight, self.parse_input.bias)
+        else:
+            if data.dtype != self.compute_dtype:
+                data = ops.cast(data, self.compute_dtype)
+            down = self.parse_input(data)
         downsampled = []
         for downblock in self.down:
             down = downblock(down)
             downsampled.append(down)
         aux = None
         quantizations = []
+        for q in self.quantize:
+            q.zst_dtype = self.compute_dtype
         stats = self._ema_slots(data.device) if self.training else None
         try:
             for down, pre_quantize, pre_quantize_cond, quantize in reversed(

@@ -559,20 +559,34 @@ def preact_small_supported(x, branch):
     return _small[0] and bool(L.query("vq3d_preact_small_supported", L.dtype_code(x), b, c, branch, h, w, d))
 
 
-def preact_small_fwd(x, blk, save=True):
-    """Fused few-channel PreAct block forward (vq3d.h): returns out, t2, t3 (bf16 channels-last);
+_fp32_stream = [True]
+
+
+def set_fp32_stream(enabled=True):
+    """Carry the residual stream of a RUN of fused blocks in fp32 between its blocks (conv operands
+    stay bf16), as the reference's autocast blocks return fp32 (layers.py:187-193); off: bf16."""
+    _fp32_stream[0] = bool(enabled)
+
+
+def fp32_stream():
+    return _fp32_stream[0]
+
+
+def preact_small_fwd(x, blk, save=True, out_dtype=None):
+    """Fused few-channel PreAct block forward (vq3d.h): returns out, t2, t3 (channels-last; t2 / t3
+    bf16, out in out_dtype, default x's: the residual stream is bf16 or fp32 per tensor);
     save=False (no backward follows): t2 / t3 are not written (None)."""
     x = as_cl(x)
     b, c, h, w, d = x.shape
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     nb = w1.shape[0]
-    out = torch.empty_like(x, memory_format=CL)
-    t2 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
-    t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
+    out = torch.empty_like(x, memory_format=CL, dtype=out_dtype or x.dtype)
+    t2 = new_act(b, nb, h, w, d, torch.bfloat16, x.device) if save else None
+    t3 = new_act(b, nb, h, w, d, torch.bfloat16, x.device) if save else None
     prm = _preact_params(blk)
     _timed(lambda: _small_kind("fwd", b, c, nb, h, w, d), lambda: L.call(
-        "vq3d_preact_small_fwd", L.dtype_code(x), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3),
-        ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream()))
+        "vq3d_preact_small_fwd_io", L.dtype_code(x), L.dtype_code(out), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1),
+        L.ptr(w2), L.ptr(w3), ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream()))
     return out, t2, t3
 
 
@@ -594,14 +608,14 @@ def preact_small_bwd(g, x, t2, t3, blk, grads):
 
 def preact_small_run_bwd(g, plan, saved, on_done=None):
     """Backward of a run of fused few-channel blocks (the forward is per block, preact_small_fwd):
-    per block, in reverse, the fused data / partial-sum kernel (vq3d_preact_small_bwd_stages 1) into
-    its slice of one run workspace, then the fixed-order reductions of every block as one launch
-    pair (vq3d_preact_small_reduce_run, plan's device tables).  Returns gx of the run's input."""
+    per block, in reverse, the fused data / partial-sum kernel (vq3d_preact_small_bwd_stages_io 1)
+    into its slice of one run workspace, then the fixed-order reductions of every block as one
+    launch pair (vq3d_preact_small_reduce_run, plan's device tables).  Each block's g has its out's
+    storage and its gx its input's (the fp32 stream inside the run).  Returns gx of the run's input."""
     blocks = plan.blocks
     g = g if g.is_contiguous(memory_format=CL) else g.contiguous(memory_format=CL)
     b, c, h, w, d = g.shape
     nb = blocks[0].branch_conv1.weight.shape[0]
-    dc = L.dtype_code(g)
     nws = int(L.query("vq3d_preact_small_workspace_bytes", b, c, nb, h, w, d))
     stride = (nws + 255) // 256 * 256
     run_ws = workspace(stride * len(blocks), g.device)
@@ -613,10 +627,12 @@ def preact_small_run_bwd(g, plan, saved, on_done=None):
         gx = torch.empty_like(x, memory_format=CL)
         prm = _preact_params(blk)
         gr = L.PreactGrads(*[ctypes.c_void_p(int(gp)) for gp in plan.grad_ptrs(i)])
-        sargs = (dc, b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3), L.ptr(blk.branch_conv1.weight),
-                 L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), ctypes.byref(gr),
-                 ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws), L.ptr(gx), L.stream())
-        _timed(lambda: _small_kind("bwd", b, c, nb, h, w, d), lambda a=sargs: L.call("vq3d_preact_small_bwd_stages", 1, *a))
+        sargs = (L.dtype_code(x), L.dtype_code(g), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
+                 L.ptr(blk.branch_conv1.weight), L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight),
+                 ctypes.byref(prm), ctypes.byref(gr), ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws),
+                 L.ptr(gx), L.stream())
+        _timed(lambda: _small_kind("bwd", b, c, nb, h, w, d),
+               lambda a=sargs: L.call("vq3d_preact_small_bwd_stages_io", 1, *a))
         g = gx
     L.call("vq3d_preact_small_reduce_run", len(blocks), b, c, nb, h, w, d, ctypes.c_void_p(base),
            ctypes.c_size_t(stride), L.ptr(gtab), L.ptr(ptab), L.stream())

@@ -16,10 +16,14 @@ module API and state_dict of the reference, GPU path through libvq3d:
 
 A stack is the reference's (3, b, c, d, h, w) tensor (depth-, height-, width-wise streams); inside
 the model it travels as a list of three channels-last (b, c, d, h, w) tensors.  Dropout: the
-causal Dropout3d runs per stream as in the reference; attention dropout > 0 in training is not
-implemented (the published run uses 0.0, train_pixelsnail_mid_downscaled.job:84).
+causal Dropout3d runs per stream as in the reference; the attention's training-mode logits
+(dropout, then zero logits -> -1e3, layers.py:633-637) are computed inside the attention kernels
+from a device seed (CausalAttentionFn).  Mixup (pixelsnail.py:136-138, train_helpers.py:20-63)
+blends the one-hot inputs and the two targets' losses as the reference does.
 """
+import ctypes
 import math
+from random import randrange
 from argparse import ArgumentParser, Namespace
 from functools import partial
 from operator import attrgetter
@@ -299,10 +303,13 @@ class PreActFixupCausalResBlock(nn.Module):
 
 # ============================================================================================ attention
 class CausalAttentionFn(torch.autograd.Function):
-    """One stream's causal attention (attention.hip): q, k [b][n][nh * dk], v [b][n][nh * dv]."""
+    """One stream's causal attention (attention.hip): q, k [b][n][nh * dk], v [b][n][nh * dv].
+    train: None (eval) or (dropout p, device int64 seed tensor of this forward): the reference's
+    training-mode logits (layers.py:633-637) -- dropout, then every zero logit -> -1e3 -- with the
+    drop mask a hash of the seed that the backward recomputes."""
 
     @staticmethod
-    def forward(ctx, q, k, v, nh):
+    def forward(ctx, q, k, v, nh, train=None):
         b, ck = q.shape[:2]
         n = math.prod(q.shape[2:])
         cv = v.shape[1]
@@ -311,9 +318,11 @@ class CausalAttentionFn(torch.autograd.Function):
         q, k, v = (t.contiguous(memory_format=CL) for t in (q, k, v))
         out = torch.empty_like(v, memory_format=CL)
         lse = torch.empty((b, nh, n), dtype=torch.float32, device=q.device)
-        L.call("vq3d_causal_attn_fwd", L.dtype_code(q), b, n, nh, dk, dv, scale, L.ptr(q), L.ptr(k), L.ptr(v),
-               L.ptr(out), L.ptr(lse), L.stream())
+        tr, seed = _attn_train(train)
+        L.call("vq3d_causal_attn_fwd_ex", L.dtype_code(q), b, n, nh, dk, dv, scale, L.ptr(q), L.ptr(k), L.ptr(v),
+               None if tr is None else ctypes.byref(tr), L.ptr(out), L.ptr(lse), L.stream())
         ctx.dims = (b, n, nh, dk, dv, scale)
+        ctx.train = None if train is None else (train[0], seed)
         ctx.save_for_backward(q, k, v, out, lse)
         return out
 
@@ -325,10 +334,19 @@ class CausalAttentionFn(torch.autograd.Function):
         gq, gk, gv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         nws = int(L.query("vq3d_causal_attn_workspace_bytes", b, n, nh))
         ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=q.device)
-        L.call("vq3d_causal_attn_bwd", L.dtype_code(q), b, n, nh, dk, dv, scale, L.ptr(q), L.ptr(k), L.ptr(v),
-               L.ptr(out), L.ptr(g), L.ptr(lse), L.ptr(ws), ctypes_size(nws), L.ptr(gq), L.ptr(gk), L.ptr(gv),
-               L.stream())
-        return gq, gk, gv, None
+        tr, _ = _attn_train(ctx.train)
+        L.call("vq3d_causal_attn_bwd_ex", L.dtype_code(q), b, n, nh, dk, dv, scale, L.ptr(q), L.ptr(k), L.ptr(v),
+               None if tr is None else ctypes.byref(tr), L.ptr(out), L.ptr(g), L.ptr(lse), L.ptr(ws),
+               ctypes_size(nws), L.ptr(gq), L.ptr(gk), L.ptr(gv), L.stream())
+        return gq, gk, gv, None, None
+
+
+def _attn_train(train):
+    """(vq3d_attn_train struct or None, the seed tensor kept alive)"""
+    if train is None:
+        return None, None
+    p, seed = train
+    return L.AttnTrain(dropout_p=float(p), seed=None if seed is None else ctypes.c_void_p(seed.data_ptr())), seed
 
 
 def ctypes_size(n):
@@ -346,12 +364,24 @@ class CausalAttention(nn.Module):
         self.num_heads = num_heads
         self.dropout = nn.Dropout(dropout_prob)
 
+    def _seeds(self, device):
+        """one fresh device seed per stream and forward: a device counter advanced by a device add,
+        so a captured HIP graph draws new dropout masks on every replay"""
+        if getattr(self, "_seed", None) is None or self._seed.device != device:
+            base = int(torch.randint(0, 2 ** 62, (1,)).item())
+            self._seed = torch.tensor([base], dtype=torch.int64, device=device)
+        seeds = self._seed * 3 + torch.arange(3, dtype=torch.int64, device=device)
+        self._seed.add_(1)
+        return [seeds[i:i + 1] for i in range(3)]
+
     def run(self, keys, queries, values):
-        if self.dropout.training and self.dropout.p > 0:
-            raise NotImplementedError("attention dropout > 0 in training is not implemented "
-                                      "(the published prior uses --attention-dropout-prob 0.0)")
         nh = self.num_heads
         assert values[0].shape[1] % nh == 0 and keys[0].shape[1] % nh == 0
+        if self.dropout.training:
+            p = float(self.dropout.p)
+            seeds = self._seeds(keys[0].device) if p > 0 else [None] * 3
+            return [CausalAttentionFn.apply(cl(q), cl(k), cl(v), nh, (p, sd))
+                    for q, k, v, sd in zip(queries, keys, values, seeds)]
         return [CausalAttentionFn.apply(cl(q), cl(k), cl(v), nh) for q, k, v in zip(queries, keys, values)]
 
     def forward(self, keys, queries, values, attn_mask=None):
@@ -403,8 +433,10 @@ def background_list(b, dims, dtype, device):
 
 class PixelSNAIL(nn.Module):
     """pixel_model/pixelsnail.py:27-320 (module tree, argument parsing, init and loss of the
-    reference; conditioning and mixup are not implemented -- the published mid-level run disables
-    conditioning; mixup is a data-side blend, train_helpers.py:20-51)."""
+    reference; mixup as train_helpers.py:20-63.  Conditioning is not implemented: the published prior
+    runs disable it (train_pixelsnail_*.job: --use-conditioning False) and the reference's own
+    conditioned forward passes the condition tensor as `condition_cache` (layers.py:692), whose
+    `.popleft()` (layers.py:446) fails, so there is no working reference behaviour to match)."""
 
     def __init__(self, args, compute_dtype="bf16"):
         super().__init__()
@@ -486,21 +518,54 @@ class PixelSNAIL(nn.Module):
         return self.logits(data)
 
     def cross_entropy(self, batch, batch_idx=0, metrics=None, mode="train"):
-        """pixelsnail.py:112-161 without conditioning / mixup: mean cross-entropy of the logits
-        over every code position, plus the log dict's bits_per_dim."""
+        """pixelsnail.py:112-161 without conditioning: mean cross-entropy of the logits over every
+        code position (with mixup in training when mixup_alpha != 0), plus the log dict's
+        bits_per_dim."""
         codes = batch[0].squeeze(1)
-        onehot = F.one_hot(codes, num_classes=self.input_dim).permute(0, 4, 1, 2, 3)
-        return self.cross_entropy_onehot(onehot, codes)
+        onehot = F.one_hot(codes, num_classes=self.input_dim).permute(0, 4, 1, 2, 3).float()
+        mix = mixup_draw(codes.shape[0], self.mixup_alpha) if (self.mixup_alpha != 0 and mode == "train") else None
+        return self.cross_entropy_onehot(onehot, codes, mix)
 
-    def cross_entropy_onehot(self, onehot, codes):
+    def cross_entropy_onehot(self, onehot, codes, mix=None):
         """the loss from a prepared one-hot input (F.one_hot validates its input on the host, which
-        a captured HIP graph cannot do)"""
-        logits = self.logits(onehot)
-        loss = F.cross_entropy(logits, codes, reduction="none").mean()
+        a captured HIP graph cannot do).  mix = (lam, index) from mixup_draw: the input is
+        lam x + (1 - lam) x[index] and the loss lam CE(y) + (1 - lam) CE(y[index]), averaged
+        (train_helpers.py:20-63)."""
+        if mix is None:
+            logits = self.logits(onehot)
+            unreduced = F.cross_entropy(logits, codes, reduction="none")
+        else:
+            lam, index = mix
+            x = onehot.float()
+            lam_t = torch.as_tensor(lam, dtype=x.dtype, device=x.device)
+            logits = self.logits(lam_t * x + (1 - lam_t) * x[index])
+            unreduced = (lam_t * F.cross_entropy(logits, codes, reduction="none")
+                         + (1 - lam_t) * F.cross_entropy(logits, codes[index], reduction="none"))
+        loss = unreduced.mean()
         return loss, {"bits_per_dim": loss.detach() / np.log(2)}
 
     def training_step(self, batch, batch_idx):
         return self.cross_entropy(batch, batch_idx, mode="train")[0]
+
+
+def sattolo_cycle(n):
+    """train_helpers.py:23-37: a random cyclic permutation of range(n) (Sattolo's algorithm on
+    Python's global random), so no sample is mixed with itself when n > 1"""
+    out = np.arange(n)
+    i = n
+    while i > 1:
+        i -= 1
+        j = randrange(i)
+        out[j], out[i] = out[i], out[j]
+    return out
+
+
+def mixup_draw(batch_size, alpha):
+    """mixup_data's random draws (train_helpers.py:39-47): lam ~ Beta(alpha, alpha) from numpy's
+    global generator, then the Sattolo cycle -- the same global RNGs in the same order as the
+    reference, so a seeded run draws the same lam / index"""
+    lam = float(np.random.beta(alpha, alpha))
+    return lam, torch.as_tensor(sattolo_cycle(batch_size))
 
 
 def default_args(**kw):

@@ -561,7 +561,7 @@ def capture(step, warmup):
 # codes of the 3-layer published model's middle level at 512^2 x 128 (32 x 32 x 8, K = 256),
 # model-dim 256, 8 blocks x 5 layers, causal dropout 0.2, attention dropout 0, batch 1
 PRIOR = dict(dims=(32, 32, 8), num_embeddings=[256, 0], model_dim=256, num_blocks=8, num_layers_per_block=5,
-             causal_dropout_prob=0.2, attention_dropout_prob=0.0, bottleneck_divisor=4, lr=5e-5)
+             causal_dropout_prob=0.2, attention_dropout_prob=0.0, bottleneck_divisor=4, lr=5e-5, mixup_alpha=0.2)
 
 
 def prior_cpu_baseline(sample=(8, 8, 8), reps=2):
@@ -581,7 +581,7 @@ def prior_cpu_baseline(sample=(8, 8, 8), reps=2):
     ts = []
     for _ in range(reps + 1):
         t0 = time.perf_counter()
-        loss, _ = O.loss(P, data, kw["num_embeddings"][0], kw["num_blocks"], kw["num_layers_per_block"])
+        loss, _ = O.loss(P, data, kw["num_embeddings"][0], kw["num_blocks"], kw["num_layers_per_block"])  # no mixup
         loss.backward()
         ts.append(time.perf_counter() - t0)
     t = statistics.median(ts[1:])
@@ -612,7 +612,9 @@ def prior_main(a):
 
     def step(i):
         opt.zero_grad()
-        loss, _ = model.cross_entropy_onehot(onehot, codes)
+        # mixup (--mixup-alpha 0.2 of the published job): the blend and the two-target loss run in the
+        # step; lam / index are host draws (train_helpers.py:39-47), fixed in a captured graph
+        loss, _ = model.cross_entropy_onehot(onehot.float(), codes, PS.mixup_draw(1, kw["mixup_alpha"]))
         loss.backward()
         opt.step()
         return loss
@@ -669,7 +671,7 @@ def prior_main(a):
         "config": {"workload": "pixelsnail_mid_prior_train_step", "codes": list(dims), "num_embeddings": 256,
                    "model_dim": kw["model_dim"], "blocks_x_layers": [kw["num_blocks"], kw["num_layers_per_block"]],
                    "batch_per_gpu": 1, "global_batch": 1, "parallelism": "dp1", "final_loss": float(res.detach()),
-                   "mixup": "off (data-side blend, not part of the step's kernels)"},
+                   "mixup_alpha": kw["mixup_alpha"]},
         "attention_kernel": {"positions": n, "heads": nh, "head_dim": d, "fwd_ms": tf, "bwd_ms": tb,
                              "fwd_tflops": pairs * 4 * d / (tf * 1e-3) / 1e12,
                              "bwd_tflops": pairs * 8 * d / (tb * 1e-3) / 1e12,

@@ -299,6 +299,20 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
                                  const void *t3, const float *w1, const float *w2, const float *w3,
                                  const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                  size_t ws_bytes, void *gx, vq3d_stream_t stream);
+/* The same blocks with the residual stream stored per tensor: x (and gx) as x_dtype, out (and g) as
+ * out_dtype, each VQ3D_BF16 or VQ3D_F32; t2 / t3 and every conv operand stay bf16.  A run of blocks
+ * carries its stream in fp32 between blocks (bf16 -> fp32, fp32 -> fp32, ..., fp32 -> bf16), as the
+ * reference's autocast blocks return fp32 (`out * self.scale` with fp32 parameters, layers.py:187-193);
+ * the plain entries above are (bf16, bf16). */
+int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels, int32_t branch,
+                             int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
+                             const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,
+                             vq3d_stream_t stream);
+int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out_dtype, int32_t batch,
+                                    int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd, const void *g,
+                                    const void *x, const void *t2, const void *t3, const float *w1, const float *w2,
+                                    const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
+                                    void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream);
 /* Stage 2 of a whole RUN of these blocks in one launch pair: block i's workspace at
  * workspaces + i * workspace_stride (stride >= vq3d_preact_small_workspace_bytes, a multiple of
  * 256), grads / params as for vq3d_preact_mid_reduce_run ([nblocks][11] device pointer tables). */
@@ -337,6 +351,18 @@ int vq3d_vq_moments(int32_t z_dtype, const void *z, int64_t n, int32_t d, float 
 int vq3d_vq_init_apply(float *embed, float *embed_avg, float *cluster_size, int64_t *first_pass,
                        const float *mean, const float *std, int32_t k, int32_t d, float inv_world,
                        float n_total, vq3d_stream_t stream);
+
+/* --- Encoder2.parse_input (layers.py:535): Conv3d(1 -> channels, k = 1, bias) on the fp32 input
+ * volume [voxels] with a bf16 output [voxels][channels] (channels in {2, 4, 8}, voxels % 4 == 0).
+ * The volume stays fp32 (the reference's autocast rounds it to fp16, never to bf16).  The backward
+ * accumulates (+=) the weight [channels] and bias [channels] gradients, deterministically (fixed-
+ * order partial sums through a workspace of vq3d_parse_input_workspace_bytes); the input has no
+ * gradient. --- */
+int vq3d_parse_input_fwd(int64_t voxels, int32_t channels, const float *x, const float *w, const float *b, void *y,
+                         vq3d_stream_t stream);
+size_t vq3d_parse_input_workspace_bytes(int64_t voxels, int32_t channels);
+int vq3d_parse_input_bwd(int64_t voxels, int32_t channels, const float *x, const void *g, float *dw, float *db,
+                         void *workspace, size_t ws_bytes, vq3d_stream_t stream);
 
 /* --- reconstruction loss (VQVAE.loc_metric with F.smooth_l1_loss, model.py:115-163) ---
  * loc = elu(dec); loc[..., s >= nvs[b]] = 0; optional centre-cylinder gather
@@ -391,6 +417,18 @@ int vq3d_scale(float *x, float a, int64_t n, vq3d_stream_t stream);
  * gq, gk, gv (same layouts as q, k, v) through a workspace of vq3d_causal_attn_workspace_bytes.
  * The reference's CausalAttentionPixelBlock binds its projected queries to the parameter named
  * `keys` and vice versa (layers.py:694 vs 619); callers pass q = that block's keys projection. */
+/* Training mode (CausalAttention with its nn.Dropout in training, layers.py:633-637): the logits go
+ * through dropout (each dropped with probability dropout_p, the kept ones scaled by 1 / (1 - p)) and
+ * then every logit equal to 0 -- the dropped ones and any exact zero -- is replaced by -1e3 before
+ * the causal mask and the softmax; the replaced logits pass no gradient.  The drop decision is a
+ * counter-based hash of (*seed, problem * nh + head, i, j), recomputed by the backward, so one
+ * seed value must serve a forward and its backward (the caller keeps it on the device and
+ * advances it between forwards: HIP-graph replays draw fresh masks).  train == NULL: eval mode
+ * (the plain entries). */
+typedef struct vq3d_attn_train {
+    double dropout_p;       /* in [0, 1); 0 keeps every logit (the zero replacement still applies) */
+    const uint64_t *seed;   /* device scalar, required when dropout_p > 0 */
+} vq3d_attn_train;
 int vq3d_causal_attn_supported(int32_t nh, int32_t dk, int32_t dv);
 size_t vq3d_causal_attn_workspace_bytes(int32_t nprob, int32_t n, int32_t nh);
 int vq3d_causal_attn_fwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
@@ -399,6 +437,14 @@ int vq3d_causal_attn_bwd(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, in
                          const void *q, const void *k, const void *v, const void *out, const void *gout,
                          const float *lse, void *workspace, size_t workspace_bytes, void *gq, void *gk, void *gv,
                          vq3d_stream_t stream);
+
+int vq3d_causal_attn_fwd_ex(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                            const void *q, const void *k, const void *v, const vq3d_attn_train *train, void *out,
+                            float *lse, vq3d_stream_t stream);
+int vq3d_causal_attn_bwd_ex(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, float scale,
+                            const void *q, const void *k, const void *v, const vq3d_attn_train *train,
+                            const void *out, const void *gout, const float *lse, void *workspace,
+                            size_t workspace_bytes, void *gq, void *gk, void *gv, vq3d_stream_t stream);
 
 const char *vq3d_last_error(void);
 const char *vq3d_version(void);

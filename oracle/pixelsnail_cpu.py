@@ -76,10 +76,14 @@ def preact_causal_block(stack, P, pre, mask, k=3, aux=None):
 
 
 # ---------------------------------------------------------------- CausalAttention (layers.py:613-647)
-def causal_attention(keys, queries, values, nh):
+def causal_attention(keys, queries, values, nh, train=False, p=0.0, dropped=None):
     """The reference's parameter binding: `keys` / `queries` as CausalAttention.forward names
     them.  CausalAttentionPixelBlock passes (queries, keys, values) positionally
-    (layers.py:694), so the projected queries land in `keys` and vice versa."""
+    (layers.py:694), so the projected queries land in `keys` and vice versa.
+    train (the module's dropout in training mode, layers.py:633-637): logits through dropout --
+    `dropped` (bool, broadcastable to (sd, b, nh, n, n)) zeroed, the rest scaled by 1 / (1 - p);
+    the reference draws it from torch's RNG, a test passes the mask it wants -- then every logit
+    == 0 replaced by -1e3 (masked_fill: no gradient through the replaced entries)."""
     sd, b, ck = keys.shape[:3]
     dims = keys.shape[3:]
     n = math.prod(dims)
@@ -88,11 +92,35 @@ def causal_attention(keys, queries, values, nh):
     fk = keys.reshape(sd, b, nh, ck // nh, n)
     fv = values.reshape(sd, b, nh, cv // nh, n)
     logits = torch.matmul(fq.transpose(3, 4), fk)
+    if train:
+        if p > 0:
+            logits = torch.where(dropped, torch.zeros_like(logits), logits / (1.0 - p))
+        logits = logits.masked_fill(logits == 0, -1e3)
     mask = torch.tril(torch.ones((n, n), dtype=torch.bool))
     logits = logits.masked_fill(~mask, float("-inf"))
     wts = F.softmax(logits, -1)
     out = torch.matmul(wts, fv.transpose(3, 4)).transpose(3, 4)
     return out.reshape(sd, b, -1, *dims)
+
+
+def causal_attention_rows(keys, queries, values, nh, rows, train=False):
+    """causal_attention's output at the query positions `rows` only (flattened d, h, w order):
+    the same arithmetic restricted to those rows of the logits, so a sampled slice of an
+    8,192-position attention is checkable on the CPU.  Returns (sd, b, cv, len(rows))."""
+    sd, b, ck = keys.shape[:3]
+    n = math.prod(keys.shape[3:])
+    cv = values.shape[2]
+    rows = torch.as_tensor(rows)
+    fq = queries.reshape(sd, b, nh, ck // nh, n)[..., rows] * (ck // nh) ** -0.5
+    fk = keys.reshape(sd, b, nh, ck // nh, n)
+    fv = values.reshape(sd, b, nh, cv // nh, n)
+    logits = torch.matmul(fq.transpose(3, 4), fk)  # (sd, b, nh, len(rows), n)
+    if train:
+        logits = logits.masked_fill(logits == 0, -1e3)
+    mask = torch.arange(n).view(1, n) <= rows.view(-1, 1)
+    wts = F.softmax(logits.masked_fill(~mask, float("-inf")), -1)
+    out = torch.matmul(wts, fv.transpose(3, 4)).transpose(3, 4)  # (sd, b, nh, cv // nh, len(rows))
+    return out.reshape(sd, b, cv, len(rows))
 
 
 def background(b, dims):

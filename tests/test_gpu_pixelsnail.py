@@ -171,3 +171,124 @@ def test_pixelsnail_model_golden(gpu, dtype, tol, gtol):
         sl2 = np.linalg.norm(a - b) / np.linalg.norm(b)
         print(dtype, "scalar-parameter gradients as one vector: rel L2", sl2)
         assert sl2 <= 0.1
+
+
+def test_attention_train_mode_golden(gpu):
+    """training mode with dropout 0 (every exact-zero logit -> -1e3, pixel_model/layers.py:633-637)
+    against the reference's CausalAttention in train mode on inputs with zeroed key rows"""
+    from vq3d import pixelsnail as PS
+    d = np.load(G + "psnail_attn_train.npz")
+    nh = int(d["nh"])
+    att = PS.CausalAttention(dropout_prob=0.0, num_heads=nh).to(gpu)
+    att.train()
+    keys, queries, values = stack_in(d["keys"], gpu), stack_in(d["queries"], gpu), stack_in(d["values"], gpu)
+    y = att.run(keys, queries, values)
+    assert rel(torch.stack(y), d["out"]) < 1e-5
+    torch.autograd.backward(y, [torch.tensor(d["gy"][i]).to(gpu).contiguous(memory_format=CL) for i in range(3)])
+    assert rel(torch.stack([t.grad for t in keys]), d["g_keys"]) < 1e-4
+    assert rel(torch.stack([t.grad for t in queries]), d["g_queries"]) < 1e-4
+    assert rel(torch.stack([t.grad for t in values]), d["g_values"]) < 1e-4
+
+
+def _logit_hash(seed, ph, i, j):
+    """attention.hip logit_hash restated in numpy (uint32 wrap-around arithmetic)"""
+    M = np.uint64(0xFFFFFFFF)
+    u = lambda v: np.asarray(v, dtype=np.uint64)  # noqa: E731
+    s = u(seed)
+    x = (s & M) ^ ((u(int(seed) >> 32) * u(0x9E3779B1)) & M) ^ ((u(ph) * u(0xC2B2AE3D)) & M) \
+        ^ ((u(i) * u(0x85EBCA77)) & M) ^ ((u(j) * u(0x27D4EB2F)) & M)
+    x = x & M
+    x ^= x >> u(16)
+    x = (x * u(0x7FEB352D)) & M
+    x ^= x >> u(15)
+    x = (x * u(0x846CA68B)) & M
+    x ^= x >> u(16)
+    return x
+
+
+@pytest.mark.parametrize("p", [0.3, 0.5])
+def test_attention_dropout_matches_oracle(gpu, p):
+    """attention dropout p > 0 in training: the kernels drop logit (i, j) of (problem, head) when a
+    hash of the device seed is below p 2^32 and scale the rest by 1 / (1 - p); the oracle
+    (oracle/pixelsnail_cpu.causal_attention, the reference's dropout -> zero -> -1e3 semantics) is
+    given that same mask.  Output and input gradients within 1e-4; the kept fraction within 2 % of
+    1 - p; another seed draws another mask."""
+    from oracle import pixelsnail_cpu as O
+    from vq3d import pixelsnail as PS
+    g = torch.Generator().manual_seed(3)
+    b, c, nh, dims = 2, 16, 2, (4, 8, 8)
+    n = dims[0] * dims[1] * dims[2]
+    q, k, v = (torch.randn((b, c) + dims, generator=g) for _ in range(3))
+    gy = torch.randn((b, c) + dims, generator=g)
+    seed = 0x1234_5678_9ABC
+    qd, kd, vd = (t.to(gpu).contiguous(memory_format=CL).requires_grad_(True) for t in (q, k, v))
+    st = torch.tensor([seed], dtype=torch.int64, device=gpu)
+    y = PS.CausalAttentionFn.apply(qd, kd, vd, nh, (p, st))
+    y.backward(gy.to(gpu).contiguous(memory_format=CL))
+    ii, jj = np.arange(n).reshape(n, 1), np.arange(n).reshape(1, n)
+    thr = np.uint64(min(4294967295, int(p * 4294967296.0)))
+    dropped = np.stack([np.stack([_logit_hash(seed, bb * nh + h, ii, jj) < thr for h in range(nh)])
+                        for bb in range(b)])  # (b, nh, n, n)
+    low = np.tril(np.ones((n, n), dtype=bool))
+    kept = 1.0 - float((dropped & low).sum()) / float(low.sum() * b * nh)
+    assert abs(kept - (1 - p)) < 0.02, kept
+    qc, kc, vc = (t.clone().unsqueeze(0).requires_grad_(True) for t in (q, k, v))
+    yr = O.causal_attention(kc, qc, vc, nh, train=True, p=p, dropped=torch.from_numpy(dropped).unsqueeze(0))
+    yr.backward(gy.unsqueeze(0))
+    assert rel(y, yr.detach()[0].numpy()) < 1e-4
+    assert rel(qd.grad, qc.grad[0].numpy()) < 1e-4
+    assert rel(kd.grad, kc.grad[0].numpy()) < 1e-4
+    assert rel(vd.grad, vc.grad[0].numpy()) < 1e-4
+    y2 = PS.CausalAttentionFn.apply(qd, kd, vd, nh, (p, st + 1))
+    assert rel(y2, y.detach().cpu().numpy()) > 1e-3
+
+
+def test_published_mid_prior_step(gpu):
+    """The published mid-level prior (train_pixelsnail_mid_downscaled.job:76-90: K = 256, model-dim
+    256, 8 blocks x 5 layers, causal dropout 0.2, attention dropout 0, mixup 0.2, batch 1) on 32 x 32
+    x 8 codes, bf16: two training steps (forward with mixup, backward, Adam) with finite loss and
+    gradients, and the first block's attention inside the step equal, on 64 sampled query
+    positions, to the CPU oracle's restatement (training-mode logits) of the same q / k / v."""
+    from oracle import pixelsnail_cpu as O
+    from vq3d import pixelsnail as PS
+    from vq3d.flat import FlatParams
+    from vq3d.optim import FusedAdam
+    torch.manual_seed(0)
+    args = PS.default_args(num_embeddings=[256, 0], model_dim=256, num_blocks=8, num_layers_per_block=5,
+                           causal_dropout_prob=0.2, attention_dropout_prob=0.0, bottleneck_divisor=4,
+                           mixup_alpha=0.2, lr=5e-5)
+    m = PS.PixelSNAIL(args, compute_dtype="bf16").to(gpu)
+    flat = FlatParams(m.parameters(), gpu)
+    opt = FusedAdam(m.parameters(), flat, lr=5e-5, amsgrad=True)
+    m.train()
+    data = torch.randint(0, 256, (1, 1, 32, 32, 8), generator=torch.Generator().manual_seed(1)).to(gpu)
+    seen = []
+    orig = PS.CausalAttentionFn.apply
+
+    def spy(q, k, v, nh, train=None):
+        out = orig(q, k, v, nh, train)
+        if not seen:
+            seen.append(tuple(t.detach().float().cpu() for t in (q, k, v, out)) + (nh,))
+        return out
+    PS.CausalAttentionFn.apply = spy
+    try:
+        losses = []
+        for _ in range(2):
+            opt.zero_grad()
+            loss = m.training_step([data], 0)
+            loss.backward()
+            opt.step()
+            torch.cuda.synchronize()
+            losses.append(float(loss))
+            assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+    finally:
+        PS.CausalAttentionFn.apply = orig
+    assert all(np.isfinite(losses)) and 3.0 < losses[0] < 12.0, losses
+    q, k, v, out, nh = seen[0]
+    n = 32 * 32 * 8
+    rows = np.sort(np.random.default_rng(0).choice(n, 64, replace=False))
+    rows[0] = 0  # the first position attends to itself only
+    ref = O.causal_attention_rows(k.unsqueeze(0), q.unsqueeze(0), v.unsqueeze(0), nh, rows, train=True)[0]
+    got = out.reshape(out.shape[0], out.shape[1], -1)[..., torch.as_tensor(rows)]
+    print("published prior losses", losses, "attention rel", rel(got, ref.numpy()))
+    assert rel(got, ref.numpy()) < 2e-2  # bf16 q / k / v / out storage, fp32 arithmetic

@@ -43,7 +43,7 @@ def _pad(t):
     return F.pad(t, (1,) * 6, mode="circular")
 
 
-def _ref_strict(blk, x, g):
+def _ref_strict(blk, x, g, round_out=True, round_gx=True):
     P = {n: p.detach().double().cpu() for n, p in blk.named_parameters()}
     sc, b1a, b1b, b2a, b2b, b3a, b3b, b4 = (float(P[k]) for k in
                                              ("scale", "bias1a", "bias1b", "bias2a", "bias2b", "bias3a", "bias3b", "bias4"))
@@ -51,7 +51,8 @@ def _ref_strict(blk, x, g):
     u1 = F.elu(x + b1a) + b1b
     t2 = rb(F.elu(F.conv3d(u1, w1) + b2a) + b2b)
     t3 = rb(F.elu(F.conv3d(_pad(t2), rb(w2)) + b3a) + b3b)
-    out = rb(x + sc * F.conv3d(t3, w3) + b4)
+    out = x + sc * F.conv3d(t3, w3) + b4
+    out = rb(out) if round_out else out
     acc3 = F.conv3d(g, w3.permute(1, 0, 2, 3, 4))
     gt3 = sc * acc3
     z3 = gt3 * torch.where(t3 - b3b > 0, torch.ones_like(t3), t3 - b3b + 1)
@@ -64,7 +65,8 @@ def _ref_strict(blk, x, g):
     z1r = rb(z1)
     gt1 = F.conv3d(z1r, w1.permute(1, 0, 2, 3, 4))
     e1 = torch.where(x + b1a > 0, torch.ones_like(x), torch.exp(x + b1a))
-    gx = rb(g + gt1 * e1)
+    gx = g + gt1 * e1
+    gx = rb(gx) if round_gx else gx
     grads = {"branch_conv3.weight": (sc * torch.einsum("bchwd,bohwd->co", g, t3))[..., None, None, None],
              "scale": (acc3 * t3).sum(), "bias4": g.sum(), "bias3b": gt3.sum(), "bias3a": z3.sum(),
              "branch_conv2.weight": dw2, "bias2b": gt2.sum(), "bias2a": z1.sum(),
@@ -165,8 +167,7 @@ def test_col_block_fullsize_sampled(gpu):
     assert worst <= 1e-2, worst
 
 
-@pytest.mark.parametrize("shape,nblk", [((1, 2, 128, 128, 32), 3), ((1, 4, 16, 8, 64), 2), ((1, 8, 32, 32, 8), 3)])
-def test_small_run_matches_per_block(gpu, shape, nblk):
+def _check_run_vs_per_block(gpu, shape, nblk):
     """A run of few-channel blocks through layers.BlockStack (Fn.PreActSmallRunFn: per-block fused
     kernels into slices of one run workspace, one reduction launch pair for the whole run; the
     (8, 4) 32x32x8 case takes the brick kernels' reduction) against the blocks run one by one:
@@ -199,3 +200,73 @@ def test_small_run_matches_per_block(gpu, shape, nblk):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     for n in a[2]:
         assert torch.equal(a[2][n], b[2][n]), (n, float((a[2][n] - b[2][n]).abs().max()))
+
+
+@pytest.fixture
+def bf16_stream():
+    """runs carry a bf16 residual stream (the per-block path's numerics) for the duration of a test"""
+    from vq3d import ops
+    ops.set_fp32_stream(False)
+    yield
+    ops.set_fp32_stream(True)
+
+
+@pytest.mark.parametrize("shape,nblk", [((1, 2, 128, 128, 32), 3), ((1, 4, 16, 8, 64), 2), ((1, 8, 32, 32, 8), 3)])
+def test_small_run_bf16_stream_matches_per_block(gpu, shape, nblk, bf16_stream):
+    _check_run_vs_per_block(gpu, shape, nblk)
+
+
+@pytest.mark.parametrize("shape,nblk,out32", [((1, 2, 32, 32, 32), 3, True), ((1, 4, 16, 8, 64), 2, False),
+                                              ((1, 8, 32, 32, 8), 3, True), ((1, 8, 16, 16, 32), 2, False),
+                                              ((1, 2, 8, 8, 8), 3, False)])
+def test_small_run_fp32_stream_matches_float64(gpu, shape, nblk, out32):
+    """The residual stream of a run of few-channel blocks (column kernels, and the brick kernels for
+    the 32x32x8 / 8x8x8 grids) in fp32 between the blocks, as the reference's autocast blocks return
+    fp32 (vqvae/layers.py:187-193): against a float64 restatement that rounds only the conv operands
+    (t2, t3, gz3, gz1, k^3 weights) and the run's own bf16 ends (its input, its output unless the
+    run hands fp32 on -- out32, the encoder's pre-quantize runs into the Quantizer -- and gx of the
+    input).  Tolerances as the single-block test; intermediate outs / gxs are unrounded here."""
+    from vq3d import functional as Fn
+    from vq3d import layers as VL
+    from vq3d import ops
+    assert ops.fp32_stream()
+    c = shape[1]
+    blocks = [_block(c, seed=60 + i) for i in range(nblk)]
+    gen = torch.Generator().manual_seed(61)
+    x = rb(torch.randn(shape, generator=gen, dtype=torch.float64))
+    gy = rb(torch.randn(shape, generator=gen, dtype=torch.float64))
+    # float64 reference of the chain
+    xs = [x]
+    for i, blk in enumerate(blocks):
+        o, _, _ = _ref_strict(blk, xs[-1], torch.zeros_like(x), round_out=(i == nblk - 1 and not out32))
+        xs.append(o)
+    g = gy
+    rgrads = [None] * nblk
+    for i in reversed(range(nblk)):
+        _, g, rgrads[i] = _ref_strict(blocks[i], xs[i], g, round_gx=(i == 0))
+    stack = VL.BlockStack(*blocks).to(gpu)
+    stack.out_fp32 = out32
+    from vq3d.flat import FlatParams
+    FlatParams(stack.parameters(), gpu)
+    xd = x.float().to(gpu).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
+    assert Fn.small_run_eligible(xd, blocks[0])
+    out = stack(xd)
+    assert out.dtype == (torch.float32 if out32 else torch.bfloat16)
+    gd = gy.to(gpu).to(out.dtype).contiguous(memory_format=CL)
+    out.backward(gd)
+    torch.cuda.synchronize()
+    assert xd.grad.dtype == torch.bfloat16
+    errs = {"y": rel(out, xs[-1]), "gx": rel(xd.grad, g)}
+    for i, blk in enumerate(stack):
+        gs, rs = [], []
+        for n, p in blk.named_parameters():
+            if p.numel() > 1:
+                errs[f"{i}/{n}"] = rel(p.grad, rgrads[i][n].reshape(p.shape))
+            else:
+                gs.append(p.grad.double().cpu().reshape(-1))
+                rs.append(rgrads[i][n].double().reshape(-1))
+        gv, rv = torch.cat(gs), torch.cat(rs)
+        errs[f"{i}/scalars"] = float((gv - rv).norm() / rv.norm())
+    print(shape, nblk, out32, {k: f"{v:.1e}" for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items() if not v <= (2e-2 if k.endswith("scalars") else 1e-2)}
+    assert not bad, (shape, bad)

@@ -90,3 +90,38 @@ def test_product_module_tree_and_seeded_init():
     for n, p in mine.items():
         assert tuple(p.shape) == ref[n].shape, n
         assert np.array_equal(p.detach().numpy(), ref[n]), n
+
+
+def test_attention_train_mode_golden():
+    """training-mode logits (dropout p = 0: exact-zero logits -> -1e3, layers.py:633-637) against
+    the reference's CausalAttention in train mode on inputs with zeroed key rows"""
+    d = np.load(G + "psnail_attn_train.npz")
+    k, q, v = (torch.tensor(d[n], requires_grad=True) for n in ("keys", "queries", "values"))
+    y = O.causal_attention(k, q, v, int(d["nh"]), train=True)
+    assert rel(y.detach(), d["out"]) < 1e-5
+    y.backward(torch.tensor(d["gy"]))
+    for t, n in ((k, "g_keys"), (q, "g_queries"), (v, "g_values")):
+        assert rel(t.grad, d[n]) < 1e-4, n
+    # eval mode differs on these inputs: the replacement is exercised
+    ye = O.causal_attention(k, q, v, int(d["nh"]), train=False)
+    assert rel(ye.detach(), d["out"]) > 1e-3
+
+
+def test_mixup_draws_match_reference():
+    """vq3d.pixelsnail.mixup_draw: lam ~ Beta(alpha, alpha) from numpy's global generator and the
+    Sattolo cycle from Python's random, in the reference's order (train_helpers.py:20-51): the same
+    lam and index under the same seeds, and the same blend lam x + (1 - lam) x[index]"""
+    import random
+
+    from vq3d import pixelsnail as PS
+    d = np.load(G + "psnail_mixup.npz")
+    for i in range(len(d["seed"])):
+        random.seed(int(d["seed"][i]))
+        np.random.seed(int(d["seed"][i]))
+        b = int(d["batch"][i])
+        lam, index = PS.mixup_draw(b, float(d["alpha"][i]))
+        assert np.float32(lam) == np.float32(d["lam"][i])  # the reference keeps lam in x.dtype (fp32)
+        assert index.tolist() == d["index"][i][:b].tolist()
+        x = torch.arange(b, dtype=torch.float32)
+        lt = torch.as_tensor(lam, dtype=torch.float32)
+        assert torch.equal(lt * x + (1 - lt) * x[index], torch.tensor(d["mixed"][i][:b]))

@@ -4,7 +4,7 @@ set -o pipefail
 tag=${1:-r02}; shift || true
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_$tag.log 2>&1
 rc=$?
 tail -5 gpurun_out/pytest_$tag.log
