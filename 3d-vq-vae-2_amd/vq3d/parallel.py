@@ -76,6 +76,41 @@ def step_begin():
         r.begin_step()
 
 
+def graph_collectives_ok(dev):
+    """Capture + replay the step's collective pattern in a HIP graph on every rank -- a bucket
+    all-reduce issued asynchronously on a side communication stream and joined back (as
+    GradientAllReduce does), plus a plain all-reduce (the fused EMA statistics) -- and report
+    whether every rank got the right values (a collective; call on all ranks)."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ok = 1.0
+    try:
+        t = torch.full((256,), float(rank + 1), device=dev)
+        u = torch.full((64,), float(rank + 1), device=dev)
+        side, comm = torch.cuda.Stream(), torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                dist.all_reduce(u)
+                comm.wait_stream(side)
+                with torch.cuda.stream(comm):
+                    w = dist.all_reduce(t, op=dist.ReduceOp.AVG, async_op=True)
+                w.wait()
+                side.wait_stream(comm)
+        torch.cuda.synchronize()
+        t.fill_(float(rank + 1))
+        u.fill_(float(rank + 1))
+        g.replay()
+        torch.cuda.synchronize()
+        ok = 1.0 if (abs(float(t[0]) - (world + 1) / 2) < 1e-3 and abs(float(u[0]) - world * (world + 1) / 2) < 1e-3) \
+            else 0.0
+    except Exception:  # capture unsupported here: the callers fall back to eager launches
+        ok = 0.0
+    v = torch.tensor([ok], device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    return float(v) > 0.5
+
+
 class GradientAllReduce:
     """Average the model's flat gradient across ranks in buckets overlapped with backward (one
     RCCL all-reduce per bucket; gloo SUM + divide in CPU tests).

@@ -35,6 +35,7 @@ import torch
 from . import parallel
 from .checkpoint import load_checkpoint, save_checkpoint
 from .data import CTDataModule
+from .graph import StepGraph
 from .model import VQVAE
 
 
@@ -54,6 +55,8 @@ def add_trainer_args(parser):
     parser.add_argument("--default_root_dir", type=str, default=os.getcwd())
     parser.add_argument("--resume_from_checkpoint", type=str, default=None)
     parser.add_argument("--num_nodes", type=int, default=1)
+    parser.add_argument("--hip-graph", dest="hip_graph", type=int, default=1,
+                        help="replay each training step as a captured HIP graph (1) or launch eagerly (0)")
     return parser
 
 
@@ -200,6 +203,18 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
     vloader = torch.utils.data.DataLoader(val_ds, batch_size=datamodule.batch_size, shuffle=False, sampler=vsampler,
                                           num_workers=datamodule.num_workers, pin_memory=True, drop_last=True)
     n_batches = len(loader)
+
+    def train_step(x, nvs):
+        opt.zero_grad()
+        loss = model.training_step((x, nvs), 0)
+        loss.backward()
+        reducer()
+        opt.step()
+        return loss
+    # the whole step as a HIP graph per input shape (single rank, or ranks whose RCCL collectives
+    # replay correctly inside a graph: parallel.graph_collectives_ok)
+    use_graph = bool(getattr(args, "hip_graph", 1)) and (world == 1 or parallel.graph_collectives_ok(dev))
+    runner = StepGraph(train_step, warmup=2, enabled=use_graph)
     val_every = max(1, int(n_batches * args.val_check_interval)) if args.val_check_interval <= 1 else \
         int(args.val_check_interval)
     history = []
@@ -209,11 +224,7 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
             sampler.set_epoch(epoch)
         for i, batch in enumerate(loader):
             x, nvs = _to_device(batch, dev)
-            opt.zero_grad()
-            loss = model.training_step((x, nvs), i)
-            loss.backward()
-            reducer()
-            opt.step()
+            loss = runner(x, nvs)
             step += 1
             if step % args.log_every_n_steps == 0 or step == 1:
                 history.append((step, float(loss.detach())))

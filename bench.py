@@ -446,43 +446,6 @@ def rooflines(dev, live=None, top=5):
 
 
 # ---------------------------------------------------------------------------------------------- distributed
-def dist_graph_probe(dev, rank, world):
-    """Capture + replay the step's collective pattern in a HIP graph: a bucket all-reduce issued
-    asynchronously on a side communication stream and joined back (vq3d.parallel), plus a plain
-    all-reduce (the fused EMA statistics); True when every rank got the right values."""
-    import torch
-    import torch.distributed as dist
-    ok = 1.0
-    try:
-        t = torch.full((256,), float(rank + 1), device=dev)
-        u = torch.full((64,), float(rank + 1), device=dev)
-        side = torch.cuda.Stream()
-        comm = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(side):
-            with torch.cuda.graph(g, stream=side):
-                dist.all_reduce(u)
-                comm.wait_stream(side)
-                with torch.cuda.stream(comm):
-                    w = dist.all_reduce(t, op=dist.ReduceOp.AVG, async_op=True)
-                w.wait()
-                side.wait_stream(comm)
-        torch.cuda.synchronize()
-        t.fill_(float(rank + 1))
-        u.fill_(float(rank + 1))
-        g.replay()
-        torch.cuda.synchronize()
-        ok = 1.0 if (abs(float(t[0]) - (world + 1) / 2) < 1e-3 and abs(float(u[0]) - world * (world + 1) / 2) < 1e-3) \
-            else 0.0
-    except Exception as e:  # capture unsupported: fall back to eager launches
-        print(f"[bench] rank {rank}: graph capture of the collectives failed ({e}); eager", file=sys.stderr)
-        ok = 0.0
-    v = torch.tensor([ok], device=dev)
-    dist.all_reduce(v, op=dist.ReduceOp.MIN)
-    return float(v) > 0.5
-
-
 def host_cores():
     """CPU cores this process may actually use: the affinity mask (what `nproc` prints), capped by
     the cgroup CPU quota when one is set (a GPU box grants a share of a larger machine; nproc
@@ -747,7 +710,7 @@ def main():
     graph = None
     use_graph = not a.eager and a.warmup >= 2
     if use_graph and world > 1:
-        use_graph = not a.no_dist_graph and dist_graph_probe(dev, rank, world)
+        use_graph = not a.no_dist_graph and parallel.graph_collectives_ok(dev)
     if use_graph:
         graph, static = capture(step, a.warmup)
 

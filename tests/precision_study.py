@@ -49,7 +49,7 @@ def setup(size):
 
 def run(sd0, x, op_dt=None, stream="fp32", pre_q_fp32=True):
     """stream: 'fp32' (every block output kept), 'bf16' (every block output rounded), 'runs' (kept
-    only inside the product's fused runs)"""
+    only inside the product's fused runs), 'enc_runs' (only inside the encoder's fused runs)"""
     conv0, seq0, blk0 = O.conv, O._seq, O.BLOCKS["pre-activation"]
 
     def conv(t, w, *a, **k):
@@ -60,7 +60,7 @@ def run(sd0, x, op_dt=None, stream="fp32", pre_q_fp32=True):
     def keep(prefix, specs, j, t):
         if stream == "fp32":
             return True
-        if stream == "bf16":
+        if stream == "bf16" or (stream == "enc_runs" and not prefix.startswith("encoder.")):
             return False
         ci, co, mode = specs[j]
         fused = mode == "same" and ci == co and (ci in FUSED or (ci == 32 and t[0, 0].numel() <= 256))
@@ -98,6 +98,8 @@ def main():
     cases = [("bf16 operands, bf16 stream everywhere (round-2 product)", dict(op_dt=torch.bfloat16, stream="bf16")),
              ("bf16 operands, fp32 stream inside the fused runs (round-3 product)",
               dict(op_dt=torch.bfloat16, stream="runs")),
+             ("bf16 operands, fp32 stream inside the encoder's fused runs only",
+              dict(op_dt=torch.bfloat16, stream="enc_runs")),
              ("bf16 operands, fp32 stream everywhere", dict(op_dt=torch.bfloat16, stream="fp32")),
              ("fp16 operands, fp32 stream everywhere (the reference's AMP)", dict(op_dt=torch.float16, stream="fp32"))]
     for name, kw in cases:

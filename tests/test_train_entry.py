@@ -115,3 +115,39 @@ def test_train_two_steps_then_resume(gpu, tmp_path):
     assert opt2.step_count == 3, (opt2.step_count, {float(v["step"]) for v in r_st.values()})
     resumed = load_checkpoint(str(last))
     assert resumed["global_step"] == 3 and resumed["epoch"] == 2
+
+
+@pytest.mark.gpu
+def test_step_graph_replay_matches_eager(gpu):
+    """vq3d.graph.StepGraph (what vq3d.train and bench.py run): two eager warm-up steps, the step
+    captured once as a HIP graph, then replays with new inputs copied into its static buffers --
+    the losses and the trained weights follow the eager run (only fp32-atomic summation order in
+    some weight-gradient engines may differ)."""
+    import vq3d
+    from vq3d.graph import StepGraph
+
+    def run(graph):
+        torch.manual_seed(0)
+        m = vq3d.VQVAE(vq3d.default_args(n_bottleneck_blocks=2, compute_dtype="bf16", base_lr=1e-3)).to(gpu)
+        m.train()
+        opt = m.configure_optimizers()
+
+        def step(x, nvs):
+            opt.zero_grad()
+            loss = m.training_step((x, nvs), 0)
+            loss.backward()
+            opt.step()
+            return loss
+        runner = StepGraph(step, warmup=2, enabled=graph)
+        losses = []
+        for i in range(5):
+            x = (torch.rand((1, 1, 32, 32, 32), generator=torch.Generator().manual_seed(10 + i)) * 4.5 - 0.5).to(gpu)
+            nvs = torch.tensor([32 - i], device=gpu)
+            losses.append(float(runner(x, nvs)))
+        torch.cuda.synchronize()
+        return losses, m.flat.data.clone(), runner
+    le, we, _ = run(False)
+    lg, wg, r = run(True)
+    assert len(r.graphs) == 1
+    assert np.allclose(le, lg, rtol=2e-3), (le, lg)
+    assert float((we - wg).abs().max()) <= 1e-3 * float(we.abs().max())
