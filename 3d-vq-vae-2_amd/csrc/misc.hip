@@ -184,21 +184,24 @@ __global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, 
         }
     }
 }
-// fixed-order sum of the partials, accumulated into dw / db
+// fixed-order sum of the partials (one workgroup per entry, a block tree), added into dw / db
 template <int C>
-__global__ __launch_bounds__(64) void k_pin_wgrad_fin(const float *__restrict__ part, int nb, float *__restrict__ dw,
-                                                     float *__restrict__ db) {
-    const int e = threadIdx.x;
-    if (e >= 2 * C) return;
+__global__ __launch_bounds__(256) void k_pin_wgrad_fin(const float *__restrict__ part, int nb, float *__restrict__ dw,
+                                                      float *__restrict__ db) {
+    __shared__ float red[4];
+    const int e = blockIdx.x;
     float t = 0.f;
-    for (int j = 0; j < nb; ++j) t += part[int64_t(j) * 2 * C + e];
-    if (e < C) {
-        if (dw) dw[e] += t;
-    } else if (db) {
-        db[e - C] += t;
+    for (int j = threadIdx.x; j < nb; j += 256) t += part[int64_t(j) * 2 * C + e];
+    t = block_sum<float, 256>(t, red);
+    if (threadIdx.x == 0) {
+        if (e < C) {
+            if (dw) dw[e] += t;
+        } else if (db) {
+            db[e - C] += t;
+        }
     }
 }
-static int pin_blocks(int64_t voxels) { return int(std::min<int64_t>(2048, (voxels / 4 + 255) / 256)); }
+static int pin_blocks(int64_t voxels) { return int(std::min<int64_t>(512, (voxels / 4 + 255) / 256)); }
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_recon_fwd(const T *__restrict__ dec, const float *__restrict__ x,
@@ -519,13 +522,13 @@ int vq3d_parse_input_bwd(int64_t voxels, int32_t channels, const float *x, const
     float *part = static_cast<float *>(workspace);
     if (channels == 2) {
         k_pin_wgrad<2><<<nb, 256, 0, s>>>(x, G, n4, part);
-        k_pin_wgrad_fin<2><<<1, 64, 0, s>>>(part, nb, dw, db);
+        k_pin_wgrad_fin<2><<<2 * 2, 256, 0, s>>>(part, nb, dw, db);
     } else if (channels == 4) {
         k_pin_wgrad<4><<<nb, 256, 0, s>>>(x, G, n4, part);
-        k_pin_wgrad_fin<4><<<1, 64, 0, s>>>(part, nb, dw, db);
+        k_pin_wgrad_fin<4><<<2 * 4, 256, 0, s>>>(part, nb, dw, db);
     } else {
         k_pin_wgrad<8><<<nb, 256, 0, s>>>(x, G, n4, part);
-        k_pin_wgrad_fin<8><<<1, 64, 0, s>>>(part, nb, dw, db);
+        k_pin_wgrad_fin<8><<<2 * 8, 256, 0, s>>>(part, nb, dw, db);
     }
     return check_launch("parse_input_bwd");
 }

@@ -23,8 +23,8 @@
 //          k_pm_reduce: every gradient entry summed over the workgroups in a fixed order and
 //                      added into the gradient buffers (deterministic, one adder per entry).
 // Rounding points are the unfused per-conv path's (t2, t3, gz3, gz1, gx, out rounded to bf16,
-// fp32 accumulation), except that the W1 gradient reads u1 rounded to bf16 (the matrix-core
-// operand).
+// fp32 accumulation), except that the W1 gradient reads u1 rounded to bf16 and the backward's
+// 1x1 data gradients (W1^T gz1, W3^T g) take W1 / W3 rounded to bf16 (the matrix-core operands).
 //
 // The k^3 convs use a "windowed" reduction order: for a voxel and a tap row (kh, kw) the three
 // kd taps x 9 channels are 27 CONSECUTIVE elements of the halo D-line (channels-last, pitch 9),
@@ -36,10 +36,19 @@
 #include <algorithm>
 
 // Timing experiments only (tools builds: make -C 3d-vq-vae-2_amd exp EXP=N): bit 0 skips the
-// forward tile kernel's k^3 phase, 1 its 1x1 phase, 2 its stores, 3 its staging.  The product
-// library is built with PM_EXP = 0.
+// forward tile kernel's k^3 phase, 1 its 1x1 phase, 2 its stores, 3 its staging; bits 4 .. 8 the
+// backward data tile kernel's staging (loads + LDS writes), k^3 dgrad phase, gx phase, chained
+// previous-block phase and global stores.  The product library is built with PM_EXP = 0.
 #ifndef PM_EXP
 #define PM_EXP 0
+#endif
+// resident workgroups per CU of the forward / backward-data tile kernels: 0 = as many as fit
+// (timing experiments set a cap: make exp EXP=N EXPDEF=PM_FWD_PER)
+#ifndef PM_FWD_PER
+#define PM_FWD_PER 0
+#endif
+#ifndef PM_BWD_PER
+#define PM_BWD_PER 0
 #endif
 
 namespace vq3d {
@@ -176,16 +185,20 @@ __device__ __forceinline__ int64_t run_vox(const PmArgs &a, const Org &o, int r)
 }
 
 // Stage the (TH+2) x (TW+2) halo D-lines of a 9-channel tensor around the tile (circular wrap):
-// per line the 8 interior positions (144 contiguous, 16-B aligned bytes) as 9 16-B chunks and
-// the two edge positions as 9 bf16 each.  load() issues every global load into registers,
-// store() writes them to LDS, so several tensors' loads are in flight together.
+// per line the 8 interior positions (144 contiguous, 16-B aligned bytes) as 9 16-B chunks, and
+// each edge position (position -1 / 8, 18 bytes, wrapped along D) inside two aligned 16-B chunks:
+// the 32 bytes ending where position -1 ends land on line elements 0 .. 15 (position -1 at
+// LOFF = 7 .. 15, the rest never read), the 32 bytes starting at position 8 on elements 88 .. 103
+// (position 8 at LINT + 72 .. 96, the rest finite filler of the zero-weight window tails).  load()
+// issues every global load into registers, store() writes them to LDS, so several tensors'
+// loads are in flight together.
 template <int TH, int TW>
 struct LinesLd {
     using T = Tile<TH, TW>;
     static constexpr int NI = T::NL * 9, PI = (NI + NT - 1) / NT;
-    static constexpr int NEG = T::NL * 2 * BR, PE = (NEG + NT - 1) / NT;
+    static constexpr int NEG = T::NL * 4, PE = (NEG + NT - 1) / NT;  // (line, side, chunk)
     uint4 vi[PI];
-    uint32_t ve[PE];
+    uint4 ve[PE];
     // every load is unconditional (indices past the end are clamped): a branch around a load
     // makes hipcc wait for it on the spot
     __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
@@ -201,11 +214,14 @@ struct LinesLd {
 #pragma unroll
         for (int u = 0; u < PE; ++u) {
             const int i = min(tid + u * NT, NEG - 1);
-            const int pos = i / BR, c = i - BR * pos, line = pos >> 1, side = pos & 1;
+            const int line = i >> 2, side = (i >> 1) & 1, ch = i & 1;
             const int lh = line / T::LW, lw = line - lh * T::LW;
             const int gh = wrapm(o.h0 - 1 + lh, a.H), gw = wrapm(o.w0 - 1 + lw, a.W);
-            const int gd = side ? wrapm(o.d0 + TD, a.D) : wrapm(o.d0 - 1, a.D);
-            ve[u] = src[(((int64_t(o.b) * a.H + gh) * a.W + gw) * a.D + gd) * BR + c];
+            const int64_t lb = ((int64_t(o.b) * a.H + gh) * a.W + gw) * a.D * BR;  // line start (elements)
+            // left: the 32 bytes before position d0 (the line's end when d0 = 0); right: from
+            // position d0 + 8 (the line's start when that wraps)
+            const int e0 = side ? ((o.d0 + TD == a.D) ? 0 : (o.d0 + TD) * BR) : ((o.d0 == 0 ? a.D : o.d0) * BR - 16);
+            ve[u] = *reinterpret_cast<const uint4 *>(src + lb + e0 + 8 * ch);
         }
     }
     __device__ __forceinline__ void store(bf16_t *lines) const {
@@ -222,12 +238,13 @@ struct LinesLd {
         for (int u = 0; u < PE; ++u) {
             const int i = tid + u * NT;
             if (i < NEG) {
-                const int pos = i / BR, c = i - BR * pos, line = pos >> 1, side = pos & 1;
-                lines[line * LSP + (side ? LINT + 9 * TD : LOFF) + c] = bf16_t(ve[u]);
+                const int line = i >> 2, side = (i >> 1) & 1, ch = i & 1;
+                *reinterpret_cast<uint4 *>(lines + line * LSP + (side ? LINT + 9 * TD : 0) + 8 * ch) = ve[u];
             }
         }
     }
 };
+static_assert(LOFF + 9 == LINT && LINT + 9 * TD + 16 == LSP - 0, "edge chunks fill elements 0..15 and 88..103");
 
 // A tile of a channels-last tensor with CH channels (CH * 8 * 2 bytes per D-run, 16-B chunks)
 // into LDS [voxel][CH]
@@ -287,7 +304,8 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
                                               const float *__restrict__ w1, vq3d_preact_params p,
                                               bf16_t *__restrict__ t2o) {
     __shared__ float w1s[BR * C];
-    stage_w(w1s, w1, BR * C);
+    // W1 and u1 rounded to bf16: the operands of the chained forward's matrix-core t2 stage
+    for (int i = threadIdx.x; i < BR * C; i += NT) w1s[i] = bf(f2bf(w1[i]));
     __syncthreads();
     const Scal s = load_scal(p);
     const int64_t npair = nvox / 2;
@@ -306,7 +324,7 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
                 const int e = h * C + c;  // element of the 36 bf16 of the pair
                 const uint2 w = v[e / 4];
                 const uint32_t d = (e & 2) ? w.y : w.x;
-                uu[c] = elu(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b;
+                uu[c] = bf(f2bf(elu(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b));
             }
             float t2v[BR];
 #pragma unroll
@@ -331,30 +349,6 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
     }
 }
 
-// The next block's t2 (k_pm_t2's arithmetic, bit for bit) of the tile's voxels from its bf16 out
-// in LDS: the chained forward of a run of blocks writes it here instead of a k_pm_t2 launch
-// re-reading out from HBM.
-__device__ __forceinline__ void next_t2(const bf16_t *xs, const float *w1n, const Scal &sn, bf16_t *dst, int nv) {
-    for (int v = threadIdx.x; v < nv; v += NT) {
-        const uint32_t *xr = reinterpret_cast<const uint32_t *>(xs + v * C);
-        float uu[C];
-#pragma unroll
-        for (int j = 0; j < C / 2; ++j) {
-            const uint32_t q = xr[j];
-            uu[2 * j] = elu(bf(q & 0xffffu) + sn.b1a) + sn.b1b;
-            uu[2 * j + 1] = elu(bf(q >> 16) + sn.b1a) + sn.b1b;
-        }
-#pragma unroll
-        for (int o = 0; o < BR; ++o) {
-            asm volatile("" ::: "memory");  // one W1 row in registers at a time (not all 162 hoisted)
-            float acc = 0.f;
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc = fmaf(w1n[o * C + c], uu[c], acc);
-            dst[v * BR + o] = f2bf(elu(acc + sn.b2a) + sn.b2b);
-        }
-    }
-}
-
 // t3 and out of a TH x TW x 8 tile from t2 on its halo and x; CHAIN: also the next block's t2
 template <int TH, int TW, bool CHAIN>
 __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restrict__ t2, const bf16_t *__restrict__ x,
@@ -372,13 +366,22 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if constexpr (CHAIN) stage_w(w1ns, w1n, BR * C);
     const int row = lane & 15, kb = lane >> 4;
-    bf16x8 bw2[9], bw3[2];
+    bf16x8 bw2[9], bw3[2], bw1n[1] = {};
     {
         float *w2s = reinterpret_cast<float *>(smem), *w3s = w2s + NW2;  // scratch over the halo image
         static_assert(T::LINES * 2 >= (NW2 + C * BR) * 4, "weights fit the halo image");
         stage_w(w2s, w2, NW2);
         stage_w(w3s, w3, C * BR);
         __syncthreads();
+        if constexpr (CHAIN) {  // the next block's W1 as B[k = c][n = o] (k >= 18, n >= 9 zero)
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = 8 * kb + j;
+                v[j] = (c < C && row < BR) ? w1ns[row * C + c] : 0.f;
+            }
+            bw1n[0] = pack8(v);
+        }
 #pragma unroll
         for (int kk = 0; kk < 9; ++kk) bw2[kk] = w2_frag<false>(w2s, kk, lane);
 #pragma unroll
@@ -456,7 +459,27 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
             }
         }
         __syncthreads();
-        if constexpr (CHAIN) next_t2(xs, w1ns, sn, t2l, T::TV);
+        if constexpr (CHAIN) {
+            // the next block's t2 = elu(W1 u1 + b2a) + b2b, u1 = bf16(elu(out + b1a) + b1b) formed
+            // lane-wise from the out tile as the A fragment (k_pm_t2's rounding points), one MFMA
+            // per 16 voxels, into the free halo image
+            for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+                const uint4 q = __builtin_bit_cast(uint4, read8(xs, (mt * 16 + row) * C + 8 * kb));
+                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+                float u[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float ov = bf((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                    u[j] = 8 * kb + j < C ? elu(ov + sn.b1a) + sn.b1b : 0.f;
+                }
+                const f32x4 acc = mfma(pack8(u), bw1n[0], f32x4{0.f, 0.f, 0.f, 0.f});
+                if (row < BR) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        t2l[(mt * 16 + 4 * kb + j) * BR + row] = f2bf(elu(acc[j] + sn.b2a) + sn.b2b);
+                }
+            }
+        }
         if constexpr (!(PM_EXP & 4)) {
             if (t3o) store_tile<TH, TW, BR>(a, o, t3s, t3o);
             store_tile<TH, TW, C>(a, o, xs, out);
@@ -483,7 +506,8 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
     __shared__ float red[32];
     constexpr int NG = NT * C / 8, NTT = NT * BR / 8, PG = (NG + NT - 1) / NT, PT = (NTT + NT - 1) / NT;
     const int tid = threadIdx.x;
-    stage_w(w3s, w3, C * BR);
+    // W3 rounded to bf16: the operand the chained stage of k_pm_bwd2 feeds the matrix cores
+    for (int i = tid; i < C * BR; i += NT) w3s[i] = bf(f2bf(w3[i]));
     const Scal s = load_scal(p);
     float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f;
     const int64_t nblk = nvox / NT;
@@ -567,8 +591,8 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
     using T = Tile<TH, TW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     bf16_t *zl = reinterpret_cast<bf16_t *>(smem);  // gz3 halo lines; CHAIN: then the previous gz3 [TV][9]
-    bf16_t *tl = zl + T::LINES;                       // t2 halo lines
-    bf16_t *z1s = tl + T::LINES;                      // gz1 [TV][9]
+    bf16_t *t2s = zl + T::LINES;                      // t2 of the tile [TV][9] (only elu'(t2) is needed)
+    bf16_t *z1s = t2s + T::S9;                        // gz1 [TV][9]
     bf16_t *xs = z1s + T::S9;                         // x [TV][18]
     bf16_t *gs = xs + T::S18;                         // g [TV][18], then gx in place
     float *w1s = reinterpret_cast<float *>(gs + T::S18);  // W1 [o][c]
@@ -579,28 +603,51 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int row = lane & 15, kb = lane >> 4;
     if constexpr (CHAIN) stage_w(w3ps, w3p, C * BR);
-    bf16x8 bw2[9];
+    bf16x8 bw2[9], bw1[2], bw3p = {};
     {
-        float *w2s = reinterpret_cast<float *>(smem);  // scratch over the halo images
+        float *w2s = reinterpret_cast<float *>(smem);  // scratch over the halo image
+        static_assert(T::LINES * 2 >= NW2 * 4, "W2 fits the halo image");
         stage_w(w2s, w2, NW2);
         stage_w(w1s, w1, BR * C);
         __syncthreads();
 #pragma unroll
         for (int kk = 0; kk < 9; ++kk) bw2[kk] = w2_frag<true>(w2s, kk, lane);
+        // W1^T for gt1 = W1^T gz1 (B[k = o][n = c], two 16-channel n-tiles) and, chained, the
+        // previous block's W3^T for its gz3 (B[k = co][n = o]); k >= 9 / 18 rows are zero
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = 8 * kb + j, c = 16 * nt + row;
+                v[j] = (o < BR && c < C) ? w1s[o * C + c] : 0.f;
+            }
+            bw1[nt] = pack8(v);
+        }
+        if constexpr (CHAIN) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int co = 8 * kb + j;
+                v[j] = (co < C && row < BR) ? w3ps[co * BR + row] : 0.f;
+            }
+            bw3p = pack8(v);
+        }
         __syncthreads();
     }
     {
         bf16_t *tails[3] = {z1s, xs, gs};
         const int at[3] = {T::TV * BR, T::TV * C, T::TV * C};
-        zero_pads<TH, TW>(zl, 2, tails, at, 3);
+        zero_pads<TH, TW>(zl, 1, tails, at, 3);
     }
     const Scal s = load_scal(p);
     float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
     Scal sp{};
     if constexpr (CHAIN) sp = load_scal(pp);
     float q4 = 0.f, q3b = 0.f, q3a = 0.f, qsc = 0.f;  // CHAIN: the previous block's K1 sums
-    // the next tile's halo loads are in flight while the current tile computes
-    LinesLd<TH, TW> lz, lt;
+    // the next tile's gz3 halo and t2 loads are in flight while the current tile computes
+    LinesLd<TH, TW> lz;
+    TileLd<TH, TW, BR> lt;
     const TileSched sc = xcd_sched(a.ntiles);
     if (sc.t < sc.end) {
         const Org o0 = tile_org(a, sc.t, TH, TW);
@@ -610,14 +657,14 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
     for (int tile = sc.t; tile < sc.end; tile += sc.step) {
         const Org o = tile_org(a, tile, TH, TW);
         __syncthreads();
-        {
+        if constexpr (!(PM_EXP & 16)) {
             TileLd<TH, TW, C> lx, lg;
             TileLd<TH, TW, BR> l3;
             lx.load(a, o, x);
             lg.load(a, o, g);
             if constexpr (CHAIN) l3.load(a, o, t3p);
             lz.store(zl);
-            lt.store(tl);
+            lt.store(t2s);
             if (tile + sc.step < sc.end) {
                 const Org on = tile_org(a, tile + sc.step, TH, TW);
                 lz.load(a, on, gz3);
@@ -628,7 +675,7 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             if constexpr (CHAIN) l3.store(t3ps);
         }
         __syncthreads();
-        for (int mt = wave; mt < T::NMT; mt += NT / 64) {
+        for (int mt = (PM_EXP & 32) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
             const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
             const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -638,8 +685,8 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             if (row < BR) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int v = mt * 16 + 4 * kb + j, rr = v >> 3, dd = v & 7;
-                    const float t2v = bf(tl[((rr / TW + 1) * T::LW + rr % TW + 1) * LSP + LINT + 9 * dd + row]);
+                    const int v = mt * 16 + 4 * kb + j;
+                    const float t2v = bf(t2s[v * BR + row]);
                     const float z1 = acc[j] * elu_d_act(t2v, s.b2b);
                     s2b += acc[j];
                     s2a += z1;
@@ -648,67 +695,58 @@ __global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restri
             }
         }
         __syncthreads();
-        // gx = g + (W1^T gz1) * elu'(x + b1a)
-        for (int v = tid; v < T::TV; v += NT) {
-            float z1[BR];
+        // gx = g + (W1^T gz1) * elu'(x + b1a): gt1 on the matrix cores (16 voxels x 2 16-channel
+        // tiles per wave step, K = the 9 branch channels), the epilogue per (voxel, channel) lane
+        for (int mt = (PM_EXP & 64) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
+            const bf16x8 af = read8(z1s, (mt * 16 + row) * BR + 8 * kb);
 #pragma unroll
-            for (int oo = 0; oo < BR; ++oo) z1[oo] = bf(z1s[v * BR + oo]);
-            const uint32_t *xr = reinterpret_cast<const uint32_t *>(xs + v * C);
-            uint32_t *gr = reinterpret_cast<uint32_t *>(gs + v * C);
-#pragma unroll 1
-            for (int j = 0; j < C / 2; ++j) {
-                const uint32_t xq = xr[j], gq = gr[j];
-                float r2[2];
+            for (int nt = 0; nt < 2; ++nt) {
+                const f32x4 acc = mfma(af, bw1[nt], f32x4{0.f, 0.f, 0.f, 0.f});
+                const int c = 16 * nt + row;
+                if (c < C) {
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int c = 2 * j + h;
-                    float gt1 = 0.f;
-#pragma unroll
-                    for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1s[oo * C + c], z1[oo], gt1);
-                    const float zx = bf(h ? (xq >> 16) : (xq & 0xffffu)) + s.b1a;
-                    const float ez = zx > 0.f ? 1.f : expf(zx);
-                    s1b += gt1;
-                    s1a += gt1 * ez;
-                    r2[h] = bf(h ? (gq >> 16) : (gq & 0xffffu)) + gt1 * ez;
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = (mt * 16 + 4 * kb + j) * C + c;
+                        const float gt1 = acc[j];
+                        const float zx = bf(xs[i]) + s.b1a;
+                        const float ez = zx > 0.f ? 1.f : expf(zx);
+                        s1b += gt1;
+                        s1a += gt1 * ez;
+                        const bf16_t gb = f2bf(bf(gs[i]) + gt1 * ez);
+                        gs[i] = gb;
+                        if constexpr (CHAIN) q4 += bf(gb);  // the previous block's g = this gx
+                    }
                 }
-                gr[j] = uint32_t(f2bf(r2[0])) | (uint32_t(f2bf(r2[1])) << 16);
             }
         }
         __syncthreads();
         if constexpr (CHAIN) {
-            // previous block: gz3 = bf16(scale W3^T gx * elu'(t3)) into the free halo image
-            for (int v = tid; v < T::TV; v += NT) {
-                float gv[C], tv[BR];
-                const uint32_t *gr = reinterpret_cast<const uint32_t *>(gs + v * C);
+            // previous block: gz3 = bf16(scale W3^T gx * elu'(t3)) into the free halo image (one
+            // MFMA per 16 voxels, K = the 18 channels of gx)
+            for (int mt = (PM_EXP & 128) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
+                const f32x4 acc = mfma(read8(gs, (mt * 16 + row) * C + 8 * kb), bw3p, f32x4{0.f, 0.f, 0.f, 0.f});
+                if (row < BR) {
 #pragma unroll
-                for (int j = 0; j < C / 2; ++j) {
-                    const uint32_t q = gr[j];
-                    gv[2 * j] = bf(q & 0xffffu);
-                    gv[2 * j + 1] = bf(q >> 16);
-                    q4 += gv[2 * j] + gv[2 * j + 1];
-                }
-#pragma unroll
-                for (int oo = 0; oo < BR; ++oo) tv[oo] = bf(t3ps[v * BR + oo]);
-#pragma unroll
-                for (int oo = 0; oo < BR; ++oo) {
-                    asm volatile("" ::: "memory");  // one W3 column in registers at a time
-                    float a3 = 0.f;
-#pragma unroll
-                    for (int co = 0; co < C; ++co) a3 = fmaf(w3ps[co * BR + oo], gv[co], a3);
-                    const float gt3 = a3 * sp.sc;
-                    const float z = gt3 * elu_d_act(tv[oo], sp.b3b);
-                    q3b += gt3;
-                    q3a += z;
-                    qsc = fmaf(a3, tv[oo], qsc);
-                    zl[v * BR + oo] = f2bf(z);
+                    for (int j = 0; j < 4; ++j) {
+                        const int v = mt * 16 + 4 * kb + j;
+                        const float a3 = acc[j], tv = bf(t3ps[v * BR + row]);
+                        const float gt3 = a3 * sp.sc;
+                        const float z = gt3 * elu_d_act(tv, sp.b3b);
+                        q3b += gt3;
+                        q3a += z;
+                        qsc = fmaf(a3, tv, qsc);
+                        zl[v * BR + row] = f2bf(z);
+                    }
                 }
             }
         }
-        store_tile<TH, TW, C>(a, o, gs, gx);
-        store_tile<TH, TW, BR>(a, o, z1s, gz1o);
+        if constexpr (!(PM_EXP & 256)) {
+            store_tile<TH, TW, C>(a, o, gs, gx);
+            store_tile<TH, TW, BR>(a, o, z1s, gz1o);
+        }
         if constexpr (CHAIN) {
             __syncthreads();
-            store_tile<TH, TW, BR>(a, o, zl, gz3p);
+            if constexpr (!(PM_EXP & 256)) store_tile<TH, TW, BR>(a, o, zl, gz3p);
         }
     }
     if constexpr (CHAIN) {
@@ -1044,7 +1082,7 @@ size_t fwd_lds() {
 template <int TH, int TW, bool CHAIN>
 size_t bwd_lds() {
     using T = Tile<TH, TW>;
-    return size_t(2 * T::LINES + T::S9 + 2 * T::S18) * 2 + size_t(BR * C + 32) * 4 +
+    return size_t(T::LINES + 2 * T::S9 + 2 * T::S18) * 2 + size_t(BR * C + 32) * 4 +
            (CHAIN ? size_t(C * BR) * 4 + size_t(T::S9) * 2 : 0);
 }
 
@@ -1093,6 +1131,7 @@ int bwd2_blocks(const PmArgs &a) {
     if (!per)
         per = std::min(per_cu(k_pm_bwd2<BTH, BTW, false>, bwd_lds<BTH, BTW, false>()),
                        per_cu(k_pm_bwd2<BTH, BTW, true>, bwd_lds<BTH, BTW, true>()));
+    if (PM_BWD_PER > 0) per = std::min(per, PM_BWD_PER);
     return std::max(1, std::min(a.ntiles, per * n_cu()));
 }
 
@@ -1118,6 +1157,7 @@ void launch_fwd(int batch, int h, int w, int dd, const void *x, const float *w2,
     if (!per)
         per = std::min(per_cu(k_pm_fwd<FTH, FTW, false>, fwd_lds<FTH, FTW, false>()),
                        per_cu(k_pm_fwd<FTH, FTW, true>, fwd_lds<FTH, FTW, true>()));
+    if (PM_FWD_PER > 0) per = std::min(per, PM_FWD_PER);
     const unsigned g2 = unsigned(std::max(1, std::min(a.ntiles, per * n_cu())));
     if (w1n)
         k_pm_fwd<FTH, FTW, true><<<g2, NT, fwd_lds<FTH, FTW, true>(), s>>>(

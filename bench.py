@@ -376,20 +376,22 @@ def timed_launch(dev, launch, iters=20):
 
 def roofline_of(dev, kind, step_entry=None, live_us=None):
     """Roofline of one engine kernel.  Its launch time is taken, in order of preference, from
-    (1) `live_us`: HIP events around each of its launches inside a real training step of this run
-        (vq3d.ops.KernelTimer, on the stream the kernel is launched on),
-    (2) the committed rocprofv3 step trace (profiles/r03_step_top.json) average,
+    (1) the committed rocprofv3 kernel trace of the bench step (profiles/r03_step_top.json, the
+        same tree: tools/gpu_round.sh writes it from this command's step) average,
+    (2) `live_us`: HIP events around each of its launches inside one more (eager) training step of
+        this run (vq3d.ops.KernelTimer, on the stream the kernel is launched on; the events keep
+        neighbouring launches from overlapping, so it reads a few % above the trace),
     (3) the isolated probe (the kernel alone on resident inputs of its production shape, 20 launches
         captured in a HIP graph).
-    The other two are reported beside it (trace_avg_us, avg_launch_us_isolated / frac_isolated)
-    so the three can be checked against each other."""
+    All three are reported (trace_avg_us, live_avg_us, avg_launch_us_isolated / frac_isolated) so
+    they can be checked against each other."""
     launch, algo, flops, desc = PROBES[kind](dev, kind)
     t_iso = timed_launch(dev, launch)
     t_trace = step_entry["avg_us"] * 1e-6 if step_entry else None
-    if live_us:
+    if t_trace:
+        t, src = t_trace, f"rocprofv3 kernel trace of the bench step ({os.path.relpath(STEP_TOP, ROOT)})"
+    elif live_us:
         t, src = live_us * 1e-6, "live: HIP events around each launch inside an eager training step of this run"
-    elif t_trace:
-        t, src = t_trace, f"rocprofv3 step trace average ({os.path.relpath(STEP_TOP, ROOT)})"
     else:
         t, src = t_iso, "isolated probe (HIP-graph replay of 20 launches)"
     achieved = algo / t / 1e9
@@ -411,6 +413,7 @@ def roofline_of(dev, kind, step_entry=None, live_us=None):
         r["frac_trace"] = algo / t_trace / 1e9 / HBM_PEAK_GBS
     if live_us:
         r["live_avg_us"] = live_us
+        r["frac_live"] = algo / (live_us * 1e-6) / 1e9 / HBM_PEAK_GBS
     if step_entry:
         r["step_share"] = {"launches_per_step": step_entry["launches"], "us_per_step": step_entry["total_us"],
                            "trace_avg_us": step_entry["avg_us"]}

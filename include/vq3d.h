@@ -188,7 +188,8 @@ int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
  * neighbouring block's pointwise stage into its tile kernel's epilogue, while the tile is in LDS:
  *  - fwd_chain: the tile kernel only (t2 is an INPUT: stage 1 of the first block, or the previous
  *    block's chained forward); with next_w1 != NULL it also writes the next block's t2 (next_w1,
- *    next_p: that block's W1 and scalars) -- bit-identical to that block's own stage 1.
+ *    next_p: that block's W1 and scalars) -- stage 1's rounding points (u1 and W1 as bf16
+ *    operands), summed on the matrix cores.
  *  - bwd_chain: vq3d_preact_mid_bwd_stages; with prev_t3 != NULL the data stage (2, required) also
  *    computes the PREVIOUS block's stage 1 (its gz3 and scalar partials, from this block's gx = its
  *    g, prev_t3 / prev_w3 / prev_p) into prev_workspace, whose own call then omits stage 1. */

