@@ -362,6 +362,7 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
     bf16_t *t3s = t2l + T::LINES;                     // [TV][9]
     bf16_t *xs = t3s + T::S9;                         // [TV][18]: x, then out in place
     float *w1ns = reinterpret_cast<float *>(xs + T::S18);  // CHAIN: next block's W1 [o][c]
+    bf16_t *u1s = reinterpret_cast<bf16_t *>(w1ns + BR * C);  // CHAIN: next block's u1 [TV][18]
     static_assert(T::LINES >= T::TV * BR, "next t2 fits the halo image");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if constexpr (CHAIN) stage_w(w1ns, w1n, BR * C);
@@ -398,9 +399,9 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
         __syncthreads();
     }
     {
-        bf16_t *tails[2] = {t3s, xs};
-        const int at[2] = {T::TV * BR, T::TV * C};
-        zero_pads<TH, TW>(t2l, 1, tails, at, 2);
+        bf16_t *tails[3] = {t3s, xs, u1s};
+        const int at[3] = {T::TV * BR, T::TV * C, T::TV * C};
+        zero_pads<TH, TW>(t2l, 1, tails, at, CHAIN ? 3 : 2);
     }
     const Scal s = load_scal(p);
     Scal sn{};
@@ -442,7 +443,10 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
             }
         }
         __syncthreads();
-        // out = scale * W3 t3 + b4 + x (in place over x)
+        // out = scale * W3 t3 + b4 + x (in place over x); CHAIN: the wave also forms the next block's
+        // u1 = bf16(elu(out + b1a) + b1b) of its 16 voxels (k_pm_t2's rounding points) and, reading
+        // them back as the A fragment (its own LDS writes, in order: no barrier), the next block's
+        // t2 = elu(W1 u1 + b2a) + b2b into the free halo image
         for (int mt = (PM_EXP & 2) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
             const bf16x8 af = read8(t3s, (mt * 16 + row) * BR + 8 * kb);
 #pragma unroll
@@ -453,26 +457,16 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int xi = (mt * 16 + 4 * kb + j) * C + co;
-                        xs[xi] = f2bf(acc[j] * s.sc + s.b4 + bf(xs[xi]));
+                        const bf16_t ob = f2bf(acc[j] * s.sc + s.b4 + bf(xs[xi]));
+                        xs[xi] = ob;
+                        if constexpr (CHAIN) u1s[xi] = f2bf(elu(bf(ob) + sn.b1a) + sn.b1b);
                     }
                 }
             }
-        }
-        __syncthreads();
-        if constexpr (CHAIN) {
-            // the next block's t2 = elu(W1 u1 + b2a) + b2b, u1 = bf16(elu(out + b1a) + b1b) formed
-            // lane-wise from the out tile as the A fragment (k_pm_t2's rounding points), one MFMA
-            // per 16 voxels, into the free halo image
-            for (int mt = wave; mt < T::NMT; mt += NT / 64) {
-                const uint4 q = __builtin_bit_cast(uint4, read8(xs, (mt * 16 + row) * C + 8 * kb));
-                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-                float u[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float ov = bf((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
-                    u[j] = 8 * kb + j < C ? elu(ov + sn.b1a) + sn.b1b : 0.f;
-                }
-                const f32x4 acc = mfma(pack8(u), bw1n[0], f32x4{0.f, 0.f, 0.f, 0.f});
+            if constexpr (CHAIN && !(PM_EXP & 512)) {
+                uint4 q = __builtin_bit_cast(uint4, read8(u1s, (mt * 16 + row) * C + 8 * kb));
+                if (kb == 2) q.y = q.z = q.w = 0u;  // channels 18..23 are the next voxel's
+                const f32x4 acc = mfma(__builtin_bit_cast(bf16x8, q), bw1n[0], f32x4{0.f, 0.f, 0.f, 0.f});
                 if (row < BR) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
@@ -480,14 +474,12 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
                 }
             }
         }
+        __syncthreads();
         if constexpr (!(PM_EXP & 4)) {
             if (t3o) store_tile<TH, TW, BR>(a, o, t3s, t3o);
             store_tile<TH, TW, C>(a, o, xs, out);
         }
-        if constexpr (CHAIN) {
-            __syncthreads();
-            store_tile<TH, TW, BR>(a, o, t2l, t2n);
-        }
+        if constexpr (CHAIN) store_tile<TH, TW, BR>(a, o, t2l, t2n);
     }
 }
 
@@ -1077,7 +1069,7 @@ constexpr int BTH = 4, BTW = 8;  // backward tile
 template <int TH, int TW, bool CHAIN>
 size_t fwd_lds() {
     using T = Tile<TH, TW>;
-    return size_t(T::LINES + T::S9 + T::S18) * 2 + (CHAIN ? size_t(BR * C) * 4 : 0);
+    return size_t(T::LINES + T::S9 + T::S18) * 2 + (CHAIN ? size_t(BR * C) * 4 + size_t(T::S18) * 2 : 0);
 }
 template <int TH, int TW, bool CHAIN>
 size_t bwd_lds() {
