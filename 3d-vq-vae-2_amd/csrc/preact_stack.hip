@@ -419,6 +419,11 @@ __global__ __launch_bounds__(NT) void k_stack_bwd(SkArgs a, const T *__restrict_
 // operands, fp32 accumulation); the residual stream and the gradient stream stay fp32.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// STK_EXP: phase-skip bits for timing experiments (make exp EXPSRC=preact_stack EXPDEF=STK_EXP):
+// 1 W2 gradient, 2 W1 gradient, 4 W3 gradient.  The product library is built with STK_EXP = 0.
+#ifndef STK_EXP
+#define STK_EXP 0
+#endif
 constexpr int MC = 32, MB = 16;            // channels, branch
 constexpr int PF = 36, PU = 40, PT = 24;   // row pitches: fp32 streams, u1 (bf16), branch tensors (bf16)
 constexpr int MAXVM = 128;
@@ -776,7 +781,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 ps[3] += z;
                 m.z3[v * PT + row] = f2bf(z);
             }
-        } else if (wave < nmt + 2) {
+        } else if (!(STK_EXP & 4) && wave < nmt + 2) {
             // W3 gradient: M = co tile (wave - nmt), N = o, K = voxels; dscale = sum W3 . G3
             const int ct = wave - nmt;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -803,7 +808,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
 #pragma unroll
         for (int q = 0; q < 2; ++q) {  // M = co, N = ci, K = voxels: taps wave, wave + 16
             const int tap = wave + 16 * q;
-            if (tap >= 27) continue;
+            if ((STK_EXP & 1) || tap >= 27) continue;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
             for (int ks = 0; ks < nks; ++ks) {
@@ -855,7 +860,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 m.gs[i] += acc[j] * e;
             }
         }
-        if (wave < 2) {
+        if (!(STK_EXP & 2) && wave < 2) {
             // W1 gradient: M = o, N = channel tile (wave), K = voxels
             const int nt = wave;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};

@@ -156,20 +156,31 @@ class Vq3dError(RuntimeError):
     pass
 
 
+_fns = {}
+
+
+def _fn(name):
+    f = _fns.get(name)
+    if f is None:
+        f = _fns[name] = getattr(load(), name)
+    return f
+
+
 def call(name, *args):
-    rc = getattr(load(), name)(*args)
+    rc = _fn(name)(*args)
     if rc != 0:
         raise Vq3dError(f"{name}: {load().vq3d_last_error().decode()}")
     return rc
 
 
 def query(name, *args):
-    return getattr(load(), name)(*args)
+    return _fn(name)(*args)
 
 
 def stream():
-    """The current torch (HIP) stream: every launch goes there (graph-capture safe)."""
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The current torch (HIP) stream of the current device, as the raw handle (an int: ctypes
+    passes it for a void * argument): every launch goes there (graph-capture safe)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def ptr(t):
@@ -177,7 +188,7 @@ def ptr(t):
         return None
     if not t.is_cuda:
         raise Vq3dError("vq3d ops take GPU tensors only (no CPU path)")
-    return ctypes.c_void_p(t.data_ptr())
+    return t.data_ptr()
 
 
 def dtype_code(t_or_dtype):

@@ -9,6 +9,9 @@ import torch
 from . import ops
 
 ALIGN = 64  # elements: 256-byte aligned views
+# bumped whenever a parameter or gradient view is (re)attached, so pointer tables built from the
+# views (functional.StackPlan) know when to rebuild without walking every parameter per launch
+VERSION = [0]
 
 
 class FlatParams:
@@ -30,12 +33,16 @@ class FlatParams:
             p.data = v
             p.grad = self.grad[off:off + p.numel()].view(p.shape)
         self.device = torch.device(device)
+        VERSION[0] += 1
 
     def owns(self, p):
         return p.data.untyped_storage().data_ptr() == self.data.untyped_storage().data_ptr()
 
     def zero_grad(self):
         ops.zero_(self.grad)
-        for p, off in zip(self.params, self.offsets):
-            if p.grad is None or p.grad.data_ptr() != self.grad[off:].data_ptr():
+        base = self.grad.data_ptr()
+        for p, off in zip(self.params, self.offsets):  # re-attach any .grad a caller replaced
+            g = p.grad
+            if g is None or g.data_ptr() != base + 4 * off:
                 p.grad = self.grad[off:off + p.numel()].view(p.shape)
+                VERSION[0] += 1

@@ -12,9 +12,21 @@ import torch
 from . import _lib as L
 from . import ops
 from .ops import ConvGeom
+from . import flat as _flat
 from .parallel import grads_ready, sum_allreduce
 
 CL = torch.channels_last_3d
+
+
+def param_edges(params, *acts):
+    """The parameters as autograd inputs of a Function only when no activation input already ties
+    it into the graph.  The kernels accumulate parameter gradients straight into the flat buffer
+    (backward returns None for them), so an edge per parameter only costs the autograd engine time
+    (a 50-block run has 550 of them); a node fed by data alone keeps them so its backward runs."""
+    for a in acts:
+        if a is not None and a.requires_grad:
+            return ()
+    return params
 
 
 def grad_buf(p):
@@ -56,6 +68,7 @@ class PreActBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, blk, *params):
+        ctx.n_params = len(params)
         k, s, p, up = mode_geometry(blk.mode)
         g1 = ConvGeom(1)
         x = ops.as_cl(x)
@@ -121,7 +134,7 @@ class PreActBlockFn(torch.autograd.Function):
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
             g_x = ops.preact_tiny_bwd(g, x, saved, blk, {n: gb(t) for n, t in names.items()})
             grads_ready(blk._fn_params)
-            return (g_x, None) + (None,) * len(blk._fn_params)
+            return (g_x, None) + (None,) * ctx.n_params
         x, t2, t3, tup = ctx.saved_tensors
         if ctx.small or getattr(ctx, "mid", False):
             names = {"dw1": blk.branch_conv1.weight, "dw2": blk.branch_conv2.weight, "dw3": blk.branch_conv3.weight,
@@ -130,7 +143,7 @@ class PreActBlockFn(torch.autograd.Function):
             bwd = ops.preact_small_bwd if ctx.small else ops.preact_mid_bwd
             g_x = bwd(g, x, t2, t3, blk, {n: grad_buf(t) for n, t in names.items()})
             grads_ready(blk._fn_params)
-            return (g_x, None) + (None,) * len(blk._fn_params)
+            return (g_x, None) + (None,) * ctx.n_params
         k, s, p, up = mode_geometry(blk.mode)
         g1 = ConvGeom(1)
         gb = grad_buf
@@ -161,7 +174,7 @@ class PreActBlockFn(torch.autograd.Function):
                               addend=addend, dw=gb(blk.branch_conv1.weight), dpro_pre=gb(blk.bias1b),
                               dpro_post=gb(blk.bias1a))
         grads_ready(blk._fn_params)
-        return (g_x, None) + (None,) * len(blk._fn_params)
+        return (g_x, None) + (None,) * ctx.n_params
 
 
 # ============================================================================================ block stack
@@ -188,9 +201,14 @@ class StackPlan:
         return self.gptrs[i * len(_PRM): (i + 1) * len(_PRM)]
 
     def tables(self, dev):
+        # fast path: no view was re-attached since the last build (flat.VERSION) and every .grad is set
+        if (self.key is not None and self.key[0] == _flat.VERSION[0] and self.key[1] == dev
+                and all(p.grad is not None for p in self.params)):
+            return self.ptab, self.gtab
         for p in self.params:
             grad_buf(p)
-        key = tuple(p.data_ptr() for p in self.params) + tuple(p.grad.data_ptr() for p in self.params)
+        key = (_flat.VERSION[0], dev) + tuple(p.data_ptr() for p in self.params) + \
+            tuple(p.grad.data_ptr() for p in self.params)
         if key != self.key:
             self.gptrs = [p.grad.data_ptr() for p in self.params]
             n = len(self.params)
@@ -207,6 +225,7 @@ class PreActStackFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, plan, *params):
+        ctx.n_params = len(params)
         x = ops.as_cl(x)
         b, c, h, w, d = x.shape
         nb = plan.blocks[0].branch_conv1.weight.shape[0]
@@ -234,7 +253,7 @@ class PreActStackFn(torch.autograd.Function):
                                                   h, w, d, L.ptr(g), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
                                                   L.stream()))
         grads_ready(plan.params)
-        return (gx, None) + (None,) * len(plan.params)
+        return (gx, None) + (None,) * ctx.n_params
 
 
 class PreActWideFn(torch.autograd.Function):
@@ -246,6 +265,7 @@ class PreActWideFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, plan, *params):
+        ctx.n_params = len(params)
         x = ops.as_cl(x)
         b, c, h, w, d = x.shape
         nb = plan.blocks[0].branch_conv1.weight.shape[0]
@@ -282,7 +302,7 @@ class PreActWideFn(torch.autograd.Function):
                                      reduce=False)
         ops.preact_wide_reduce_run(plan, gs.shape, run_ws, stride)
         grads_ready(plan.params)
-        return (ops.cast(gs, ctx.in_dtype), None) + (None,) * len(plan.params)
+        return (ops.cast(gs, ctx.in_dtype), None) + (None,) * ctx.n_params
 
 
 class PreActMidRunFn(torch.autograd.Function):
@@ -295,6 +315,7 @@ class PreActMidRunFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, plan, *params):
+        ctx.n_params = len(params)
         save = any(ctx.needs_input_grad)
         out, saved = ops.preact_mid_run_fwd(x, plan.blocks, save=save)
         ctx.plan = plan
@@ -309,7 +330,7 @@ class PreActMidRunFn(torch.autograd.Function):
         saved = [flat[3 * i: 3 * i + 3] for i in range(len(plan.blocks))]
 
         gx = ops.preact_mid_run_bwd(g, plan, saved, on_done=lambda: grads_ready(plan.params))
-        return (gx, None) + (None,) * len(plan.params)
+        return (gx, None) + (None,) * ctx.n_params
 
 
 class PreActSmallRunFn(torch.autograd.Function):
@@ -323,6 +344,7 @@ class PreActSmallRunFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, plan, *params):
+        ctx.n_params = len(params)
         save = any(ctx.needs_input_grad)
         saved = []
         n = len(plan.blocks)
@@ -344,7 +366,7 @@ class PreActSmallRunFn(torch.autograd.Function):
         flat = ctx.saved_tensors
         saved = [flat[3 * i: 3 * i + 3] for i in range(len(plan.blocks))]
         gx = ops.preact_small_run_bwd(g, plan, saved, on_done=lambda: grads_ready(plan.params))
-        return (gx, None) + (None,) * len(plan.params)
+        return (gx, None) + (None,) * ctx.n_params
 
 
 def small_run_eligible(x, blk):
@@ -377,6 +399,7 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, x2, residual, spec, *tensors):
+        ctx.n_params = len(tensors)
         y = ops.conv_fwd(x, spec.w, spec.geom, pro=spec.pro, x2=x2, scale=spec.scale, bias=spec.bias,
                          cbias=spec.cbias, residual=residual, residual_up2=spec.residual_up2,
                          act="elu" if spec.post_elu else None)
@@ -416,7 +439,7 @@ class ConvFn(torch.autograd.Function):
         if not want:
             gx = gx2 = None
         grads_ready(spec.tensors)
-        return (gx, gx2, g_res, None) + (None,) * len(spec.tensors)
+        return (gx, gx2, g_res, None) + (None,) * ctx.n_params
 
 
 class ConvSpec:
@@ -432,7 +455,7 @@ class ConvSpec:
 
 
 def conv(x, spec, x2=None, residual=None):
-    return ConvFn.apply(x, x2, residual, spec, *spec.tensors)
+    return ConvFn.apply(x, x2, residual, spec, *param_edges(spec.tensors, x, x2, residual))
 
 
 # ============================================================================================ parse_input

@@ -90,14 +90,23 @@ class PreActFixupResBlock(nn.Module):
 
     @property
     def _fn_params(self):
-        ps = [self.bias1a, self.bias1b, self.bias2a, self.bias2b, self.bias3a, self.bias3b, self.bias4, self.scale,
-              self.branch_conv1.weight, self.branch_conv2.weight, self.branch_conv3.weight]
-        if self.skip_conv is not None:
-            ps += [self.bias1c, self.bias1d, self.skip_conv.weight]
+        # the Parameter objects in kernel order, cached (parameters keep their identity: .to() and
+        # load_state_dict write .data in place); a re-assigned attribute drops the cache (__setattr__)
+        ps = self.__dict__.get("_fn_params_cache")
+        if ps is None:
+            ps = [self.bias1a, self.bias1b, self.bias2a, self.bias2b, self.bias3a, self.bias3b, self.bias4,
+                  self.scale, self.branch_conv1.weight, self.branch_conv2.weight, self.branch_conv3.weight]
+            if self.skip_conv is not None:
+                ps += [self.bias1c, self.bias1d, self.skip_conv.weight]
+            self.__dict__["_fn_params_cache"] = ps
         return ps
 
+    def __setattr__(self, name, value):
+        self.__dict__.pop("_fn_params_cache", None)
+        super().__setattr__(name, value)
+
     def forward(self, input: torch.Tensor):
-        return Fn.PreActBlockFn.apply(input, self, *self._fn_params)
+        return Fn.PreActBlockFn.apply(input, self, *Fn.param_edges(self._fn_params, input))
 
     @torch.no_grad()
     def initialize_weights(self, num_layers):
@@ -265,7 +274,7 @@ class BlockStack(nn.Sequential):
                 # the stack's last run hands an fp32 stream on when the consumer takes it
                 plan.out_dtype = torch.float32 if (self.out_fp32 and j == len(mods) - 1 and
                                                    fn is Fn.PreActSmallRunFn and ops.fp32_stream()) else None
-                x = fn.apply(x, plan, *plan.params)
+                x = fn.apply(x, plan, *Fn.param_edges(plan.params, x))
                 i = j + 1
             else:
                 x = mods[i](x)

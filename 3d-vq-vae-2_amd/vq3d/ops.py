@@ -28,7 +28,7 @@ def as_cl(x):
 
 
 def _p(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    return None if t is None else t.data_ptr()
 
 
 def workspace(nbytes, device):
