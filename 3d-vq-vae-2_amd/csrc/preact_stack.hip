@@ -420,7 +420,7 @@ __global__ __launch_bounds__(NT) void k_stack_bwd(SkArgs a, const T *__restrict_
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 // STK_EXP: phase-skip bits for timing experiments (make exp EXPSRC=preact_stack EXPDEF=STK_EXP):
-// 1 W2 gradient, 2 W1 gradient, 4 W3 gradient.  The product library is built with STK_EXP = 0.
+// 1 W2 gradient, 2 W1 gradient, 4 W3 gradient, 8 weight staging.  The product library is built with STK_EXP = 0.
 #ifndef STK_EXP
 #define STK_EXP 0
 #endif
@@ -626,7 +626,7 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
         const Scal s = scal_lanes(vc);
         float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
         __syncthreads();
-        wr.store<false>(m.w, m.fr);
+        if constexpr (!(STK_EXP & 8)) wr.store<false>(m.w, m.fr);
         // the next block's weights and scalars, and the row after it
         if (blk + 1 < a.nblk) {
             wr.load(bcast_ptr(pn, 0), bcast_ptr(pn, 1), bcast_ptr(pn, 2));
@@ -681,9 +681,14 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
     for (int i = tid; i < nvc; i += NT) out[i] = f2bf(m.xs[(i / MC) * PF + i % MC]);
 }
 
+// SPLIT: the chain computes only the gradient stream and the scalar sums that ride it (gz3, gt2,
+// gz1, gx; b1a .. b4 but scale) and records each block's bf16 matrix operands (g, gz3, gz1) in
+// `rec`; the W1 / W2 / W3 and scale gradients, which nothing downstream in the chain needs, are
+// k_stackm_wgrad's, one workgroup per block in parallel after the chain.
+template <bool SPLIT>
 __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__restrict__ g, const float *const *tab,
                                                    float *const *gtab, const float *__restrict__ saved,
-                                                   bf16_t *__restrict__ gx) {
+                                                   bf16_t *__restrict__ gx, bf16_t *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Mk m = carve_m(a.nv, smem);
     const int tid0 = threadIdx.x;
@@ -733,19 +738,22 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
         // waves nmt, nmt + 1, W2 entries of taps wave / wave + 16, W1 entries of waves 0, 1, the
         // scalars on lanes 3 .. 10 of wave 0 (every load unconditional, clamped indices)
         float *gw1 = bcast_ptr(gc, 0), *gw2 = bcast_ptr(gc, 1), *gw3 = bcast_ptr(gc, 2);
-        float o3[4], o2[2][4], o1[4];
+        float o3[4] = {}, o2[2][4] = {}, o1[4] = {};
         const int ct = min(max(wave - nmt, 0), 1), nt1 = min(wave, 1);
+        if constexpr (!SPLIT) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            o3[j] = gw3[(16 * ct + 4 * kb + j) * MB + row];
+            for (int j = 0; j < 4; ++j) {
+                o3[j] = gw3[(16 * ct + 4 * kb + j) * MB + row];
 #pragma unroll
-            for (int q = 0; q < 2; ++q) o2[q][j] = gw2[((4 * kb + j) * MB + row) * 27 + min(wave + 16 * q, 26)];
+                for (int q = 0; q < 2; ++q) o2[q][j] = gw2[((4 * kb + j) * MB + row) * 27 + min(wave + 16 * q, 26)];
+            }
         }
+        bf16_t *rg = rec + size_t(blk) * nv * (MC + 2 * MB), *rz3 = rg + nvc, *rz1 = rz3 + nvb;
         const float osc = *gc;
         float *const gsc = gc;  // lanes 3 .. 10: this block's scalar-gradient pointers
         if (blk > 0) gc = row_ptr(gtab, blk - 1, lane);
         __syncthreads();
-        wr.store<true>(m.w, m.fr);
+        if constexpr (!(STK_EXP & 8)) wr.store<true>(m.w, m.fr);
 #pragma unroll
         for (int u = 0; u < SX; ++u) {
             const int i = tid + u * NT;
@@ -780,8 +788,9 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 ps[2] += g3;
                 ps[3] += z;
                 m.z3[v * PT + row] = f2bf(z);
+                if constexpr (SPLIT) rz3[v * MB + row] = f2bf(z);
             }
-        } else if (!(STK_EXP & 4) && wave < nmt + 2) {
+        } else if (!SPLIT && !(STK_EXP & 4) && wave < nmt + 2) {
             // W3 gradient: M = co tile (wave - nmt), N = o, K = voxels; dscale = sum W3 . G3
             const int ct = wave - nmt;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -796,7 +805,11 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 ps[1] = fmaf(m.w[W3O + co * MB + row], acc[j], ps[1]);
             }
         }
-        for (int i = tid; i < nvc; i += NT) ps[0] += m.gs[(i / MC) * PF + i % MC];
+        for (int i = tid; i < nvc; i += NT) {
+            const float gv = m.gs[(i / MC) * PF + i % MC];
+            ps[0] += gv;
+            if constexpr (SPLIT) rg[i] = f2bf(gv);
+        }
         __syncthreads();
         // gt2 = W2^T (*) gz3 (M-tile x half of the k-steps per wave); W2 gradient per tap
         if (wave < 2 * nmt) {
@@ -808,7 +821,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
 #pragma unroll
         for (int q = 0; q < 2; ++q) {  // M = co, N = ci, K = voxels: taps wave, wave + 16
             const int tap = wave + 16 * q;
-            if ((STK_EXP & 1) || tap >= 27) continue;
+            if (SPLIT || (STK_EXP & 1) || tap >= 27) continue;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
             for (int ks = 0; ks < nks; ++ks) {
@@ -835,8 +848,10 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
             pn = row_ptr(tab, max(blk - 2, 0), lane);
             load_saved(blk - 1);
         }
+        if constexpr (!SPLIT) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o1[j] = gw1[(4 * kb + j) * MC + 16 * nt1 + row];
+            for (int j = 0; j < 4; ++j) o1[j] = gw1[(4 * kb + j) * MC + 16 * nt1 + row];
+        }
         for (int i = tid; i < nvb; i += NT) {
             const int v = i / MB, o = i - v * MB;
             const float g2 = m.part[i] + m.part[nvb + i];
@@ -844,6 +859,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
             ps[4] += g2;
             ps[5] += z;
             m.z1[v * PT + o] = f2bf(z);
+            if constexpr (SPLIT) rz1[i] = f2bf(z);
         }
         __syncthreads();
         if (wave < 2 * nmt) {
@@ -860,7 +876,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 m.gs[i] += acc[j] * e;
             }
         }
-        if (!(STK_EXP & 2) && wave < 2) {
+        if (!SPLIT && !(STK_EXP & 2) && wave < 2) {
             // W1 gradient: M = o, N = channel tile (wave), K = voxels
             const int nt = wave;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -872,7 +888,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
             for (int j = 0; j < 4; ++j) gw1[(4 * kb + j) * MC + 16 * nt + row] = o1[j] + acc[j];
         }
         sum8(ps, m.red);
-        if (wave == 0 && lane >= 3 && lane < NPRM) {  // table slot k gets ps[10 - k]
+        if (wave == 0 && lane >= 3 && lane < NPRM && !(SPLIT && lane == 9)) {  // table slot k gets ps[10 - k]
             float add = ps[0];
 #pragma unroll
             for (int k = 3; k < NPRM - 1; ++k) add = lane == k ? ps[10 - k] : add;
@@ -882,6 +898,98 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
     __syncthreads();
     for (int i = tid; i < nvc; i += NT) gx[i] = f2bf(m.gs[(i / MC) * PF + i % MC]);
 }
+
+// The weight gradients of a SPLIT backward: one workgroup per block, from its saved x / t2 / t3
+// and the chain's record (g, gz3, gz1), with k_stackm_bwd's fragments and summation order, so the
+// result equals the fused kernel's.  W2: waves own taps (wave, wave + 16); W1: waves 0, 1; W3 and
+// the scale gradient (sum W3 . G3): waves 2, 3.  Each gradient entry has one adder.
+constexpr int PG = 40;  // row pitch of the bf16 g record copy
+__global__ __launch_bounds__(NT) void k_stackm_wgrad(SkArgs a, const float *const *tab, float *const *gtab,
+                                                     const float *__restrict__ saved, const bf16_t *__restrict__ rec) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nv = a.nv, nks = nv / 32, nvc = nv * MC, nvb = nv * MB, blk = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    bf16_t *t2 = reinterpret_cast<bf16_t *>(smem), *t3 = t2 + nv * PT, *z3 = t3 + nv * PT, *z1 = z3 + nv * PT;
+    bf16_t *u1 = z1 + nv * PT, *gs = u1 + nv * PU;
+    short *nb = reinterpret_cast<short *>(gs + nv * PG);
+    float *red = reinterpret_cast<float *>(nb + ((nv * 27 + 7) & ~7));
+    const float *pc = row_ptr(tab, blk, lane);
+    const Scal s = scal_lanes(*pc);
+    const float *w3 = bcast_ptr(pc, 2);
+    float *gc = row_ptr(gtab, blk, lane);
+    float *gw1 = bcast_ptr(gc, 0), *gw2 = bcast_ptr(gc, 1), *gw3 = bcast_ptr(gc, 2);
+    const float *sx = saved + size_t(blk) * nv * (MC + 2 * MB), *st2 = sx + nvc, *st3 = st2 + nvb;
+    const bf16_t *rg = rec + size_t(blk) * nv * (MC + 2 * MB), *rz3 = rg + nvc, *rz1 = rz3 + nvb;
+    for (int i = tid; i < nv * 27; i += NT) nb[i] = short(nbr(a, i / 27, i % 27, 1));
+    for (int i = tid; i < nvc; i += NT) {
+        const int v = i / MC, c = i - v * MC;
+        const float z = sx[i] + s.b1a;
+        u1[v * PU + c] = f2bf((z > 0.f ? z : expf(z) - 1.f) + s.b1b);
+        gs[v * PG + c] = rg[i];
+    }
+    for (int i = tid; i < nvb; i += NT) {
+        const int v = i / MB, o = i - v * MB;
+        t2[v * PT + o] = f2bf(st2[i]);
+        t3[v * PT + o] = f2bf(st3[i]);
+        z3[v * PT + o] = rz3[i];
+        z1[v * PT + o] = rz1[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // W2: M = co, N = ci, K = voxels
+        const int tap = wave + 16 * q;
+        if (tap >= 27) continue;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int ks = 0; ks < nks; ++ks) {
+            const int v0 = ks * 32 + 8 * kb;
+            uint32_t w[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int va = v0 + 2 * j, vb = va + 1;
+                w[j] = uint32_t(t2[int(nb[va * 27 + tap]) * PT + row]) | (uint32_t(t2[int(nb[vb * 27 + tap]) * PT + row]) << 16);
+            }
+            acc = mfma(gat8(z3 + v0 * PT + row, PT), __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]}), acc);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float *d = gw2 + ((4 * kb + j) * MB + row) * 27 + tap;
+            *d = *d + acc[j];
+        }
+    }
+    float dsc = 0.f;
+    if (wave < 2) {  // W1: M = o, N = channel tile (wave), K = voxels
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < nks; ++ks) {
+            const int v0 = ks * 32 + 8 * kb;
+            acc = mfma(gat8(z1 + v0 * PT + row, PT), gat8(u1 + v0 * PU + 16 * wave + row, PU), acc);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float *d = gw1 + (4 * kb + j) * MC + 16 * wave + row;
+            *d = *d + acc[j];
+        }
+    } else if (wave < 4) {  // W3: M = co tile, N = o, K = voxels; dscale = sum W3 . G3
+        const int ct = wave - 2;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < nks; ++ks) {
+            const int v0 = ks * 32 + 8 * kb;
+            acc = mfma(gat8(gs + v0 * PG + 16 * ct + row, PG), gat8(t3 + v0 * PT + row, PT), acc);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = 16 * ct + 4 * kb + j;
+            float *d = gw3 + co * MB + row;
+            *d = *d + s.sc * acc[j];
+            dsc = fmaf(w3[co * MB + row], acc[j], dsc);
+        }
+        dsc = wave_sum(dsc);
+        if (lane == 0) red[ct] = dsc;
+    }
+    __syncthreads();
+    if (wave == 0 && lane == 9) *gc = *gc + (0.f + red[0] + red[1]);  // lane 9 holds the scale slot
+}
+size_t lds_wgrad(int nv) { return size_t(nv) * (4 * PT + PU + PG) * 2 + size_t((nv * 27 + 7) & ~7) * 2 + 64; }
 
 bool mfma_ok(const SkArgs &a) { return a.C == MC && a.B == MB && a.nv % 32 == 0 && a.nv <= MAXVM; }
 
@@ -955,9 +1063,9 @@ int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
     hipStream_t s = as_stream(stream);
     const size_t lds = lds_bytes(a, true);
     if (dtype == VQ3D_BF16 && mfma_ok(a)) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(160 * 1024));
-        k_stackm_bwd<<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+        k_stackm_bwd<false><<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx, nullptr);
     } else if (dtype == VQ3D_BF16) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<bf16_t>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
@@ -970,6 +1078,34 @@ int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
         return fail("preact_stack_bwd: dtype");
     }
     return check_launch("preact_stack_bwd");
+}
+
+size_t vq3d_preact_stack_bwd_workspace_bytes(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch,
+                                             int32_t h, int32_t w, int32_t dd) {
+    SkArgs a;
+    if (check(nblocks, batch, channels, branch, h, w, dd, a) || !mfma_ok(a)) return 0;
+    return size_t(nblocks) * a.nv * (MC + 2 * MB) * 2;
+}
+
+int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch,
+                             int32_t h, int32_t w, int32_t dd, const void *g, const float *const *params,
+                             float *const *grads, const float *saved, void *gx, void *workspace, size_t ws_bytes,
+                             vq3d_stream_t stream) {
+    SkArgs a;
+    if (check(nblocks, batch, channels, branch, h, w, dd, a)) return fail("preact_stack_bwd_ws: unsupported shape");
+    const size_t need = vq3d_preact_stack_bwd_workspace_bytes(nblocks, batch, channels, branch, h, w, dd);
+    if (dtype != VQ3D_BF16 || need == 0)  // no split plan for this shape / dtype: the fused kernel
+        return vq3d_preact_stack_bwd(dtype, nblocks, batch, channels, branch, h, w, dd, g, params, grads, saved, gx,
+                                     stream);
+    if (!g || !params || !grads || !saved || !gx || !workspace) return fail("preact_stack_bwd_ws: null pointer");
+    if (ws_bytes < need) return fail("preact_stack_bwd_ws: workspace too small");
+    hipStream_t s = as_stream(stream);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+    k_stackm_bwd<true><<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx,
+                                                  (bf16_t *)workspace);
+    k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const bf16_t *)workspace);
+    return check_launch("preact_stack_bwd_ws");
 }
 
 }  // extern "C"

@@ -76,6 +76,8 @@ _SIGS = {
     "vq3d_preact_stack_saved_floats": (c_size, [c_int] * 7),
     "vq3d_preact_stack_fwd": (c_int, [c_int] * 8 + [P] * 5),
     "vq3d_preact_stack_bwd": (c_int, [c_int] * 8 + [P] * 6),
+    "vq3d_preact_stack_bwd_workspace_bytes": (c_size, [c_int] * 7),
+    "vq3d_preact_stack_bwd_ws": (c_int, [c_int] * 8 + [P] * 6 + [c_size, P]),
     "vq3d_preact_wide_supported": (c_int, [c_int] * 6),
     "vq3d_preact_wide_image_bytes": (c_size, [c_int] * 2),
     "vq3d_preact_wide_pack": (c_int, [c_int] * 3 + [P] * 3),

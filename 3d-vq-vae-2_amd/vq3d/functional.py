@@ -249,9 +249,12 @@ class PreActStackFn(torch.autograd.Function):
         g = _cl(g)
         ptab, gtab = plan.tables(g.device)
         gx = torch.empty_like(g, memory_format=ops.CL)
-        ops._timed("k_stackm_bwd", lambda: L.call("vq3d_preact_stack_bwd", L.dtype_code(g), len(plan.blocks), b, c, nb,
-                                                  h, w, d, L.ptr(g), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
-                                                  L.stream()))
+        nblk = len(plan.blocks)
+        nws = L.query("vq3d_preact_stack_bwd_workspace_bytes", nblk, b, c, nb, h, w, d)
+        ws = ops.workspace(nws, g.device)
+        ops._timed("k_stackm_bwd", lambda: L.call("vq3d_preact_stack_bwd_ws", L.dtype_code(g), nblk, b, c, nb, h, w, d,
+                                                  L.ptr(g), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
+                                                  L.ptr(ws), max(nws, 256), L.stream()))
         grads_ready(plan.params)
         return (gx, None) + (None,) * ctx.n_params
 

@@ -165,7 +165,7 @@ def probe_mid(dev, kind):
 
 def probe_stack(dev, kind):
     """The fused run of 50 top-level blocks (8x8x2, 32 channels, branch 16, bf16) through
-    vq3d_preact_stack_fwd / _bwd (one launch each)."""
+    vq3d_preact_stack_fwd (one launch) / vq3d_preact_stack_bwd_ws (chain + weight-gradient launch)."""
     import torch
 
     from vq3d import _lib as L
@@ -191,9 +191,12 @@ def probe_stack(dev, kind):
     def fwd():
         L.call("vq3d_preact_stack_fwd", *dims, L.ptr(x), L.ptr(ptab), L.ptr(out), L.ptr(saved), L.stream())
 
+    nws = L.query("vq3d_preact_stack_bwd_workspace_bytes", *dims[1:])
+    ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev)
+
     def bwd():
-        L.call("vq3d_preact_stack_bwd", *dims, L.ptr(gy), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
-               L.stream())
+        L.call("vq3d_preact_stack_bwd_ws", *dims, L.ptr(gy), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
+               L.ptr(ws), ws.numel(), L.stream())
     fwd()
     nv = 128
     wbytes = nblk * (c * nb * 2 + nb * nb * 27 + 8) * 4
@@ -206,7 +209,8 @@ def probe_stack(dev, kind):
             "k_stackm_fwd: 50 fused top-level blocks (8x8x2, 32 ch) forward, one launch"
     if kind == "k_stackm_bwd":
         return bwd, 2 * wbytes + sv + 2 * nv * c * 2, 2 * flops, \
-            "k_stackm_bwd: 50 fused top-level blocks (8x8x2, 32 ch) backward, one launch"
+            "k_stackm_bwd: 50 fused top-level blocks (8x8x2, 32 ch) backward: the gradient-stream chain (one " \
+            "workgroup) + the weight gradients (one workgroup per block)"
     raise KeyError(kind)
 
 

@@ -233,6 +233,17 @@ int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
 int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
                           int32_t w, int32_t dd, const void *g, const float *const *params, float *const *grads,
                           const float *saved, void *gx, vq3d_stream_t stream);
+/* vq3d_preact_stack_bwd with the weight gradients taken off the block chain: the one-workgroup
+ * chain carries only the gradient stream (and the scalar sums riding it) and records each block's
+ * bf16 matrix operands in `workspace`; then one workgroup per block computes the W1 / W2 / W3 and
+ * scale gradients in parallel.  Results equal vq3d_preact_stack_bwd's bit for bit.  Shapes or
+ * dtypes without a split plan (workspace_bytes 0) run the fused kernel. */
+size_t vq3d_preact_stack_bwd_workspace_bytes(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch,
+                                             int32_t h, int32_t w, int32_t dd);
+int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch,
+                             int32_t h, int32_t w, int32_t dd, const void *g, const float *const *params,
+                             float *const *grads, const float *saved, void *gx, void *workspace, size_t ws_bytes,
+                             vq3d_stream_t stream);
 
 /* The 72-channel / branch-36 PreActFixupResBlock (mode 'same', no skip conv) of the published
  * model's decoder level 1 (50 blocks at 32x32x8, layers.py:176-195, Decoder.up layers.py:395-405):

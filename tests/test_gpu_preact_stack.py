@@ -172,3 +172,42 @@ def test_stack_deterministic(gpu):
         res.append([xg.grad.clone()] + [p.grad.clone() for p in stack.parameters()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_stack_split_backward_equals_fused(gpu):
+    """vq3d_preact_stack_bwd_ws (gradient-stream chain + per-block weight-gradient workgroups) gives
+    the fused one-workgroup kernel's gx and parameter gradients bit for bit (same operands, same
+    fragment and summation order)."""
+    from vq3d import _lib as L
+    from vq3d.flat import FlatParams
+    from vq3d.functional import StackPlan
+    nblk, c, nb, shp = 6, 32, 16, (8, 8, 2)
+    stack = _stack(c, nb, nblk, seed=11).to(gpu)
+    fp = FlatParams(stack.parameters(), gpu)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn((1, c) + shp, generator=gen).to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    gy = torch.randn((1, c) + shp, generator=gen).to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    plan = StackPlan(list(stack))
+    ptab, gtab = plan.tables(gpu)
+    dims = (L.dtype_code(x), nblk, 1, c, nb) + shp
+    saved = torch.empty(L.query("vq3d_preact_stack_saved_floats", *dims[1:]), dtype=torch.float32, device=gpu)
+    out = torch.empty_like(x)
+    L.call("vq3d_preact_stack_fwd", *dims, L.ptr(x), L.ptr(ptab), L.ptr(out), L.ptr(saved), L.stream())
+    nws = L.query("vq3d_preact_stack_bwd_workspace_bytes", *dims[1:])
+    assert nws > 0
+    ws = torch.empty(nws, dtype=torch.uint8, device=gpu)
+    start = torch.randn(fp.grad.shape, generator=gen).to(gpu) * 1e-3  # both accumulate (+=) onto it
+    res = []
+    for split in (False, True):
+        fp.grad.copy_(start)
+        gx = torch.empty_like(x)
+        if split:
+            L.call("vq3d_preact_stack_bwd_ws", *dims, L.ptr(gy), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
+                   L.ptr(ws), nws, L.stream())
+        else:
+            L.call("vq3d_preact_stack_bwd", *dims, L.ptr(gy), L.ptr(ptab), L.ptr(gtab), L.ptr(saved), L.ptr(gx),
+                   L.stream())
+        torch.cuda.synchronize()
+        res.append((gx.clone(), fp.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]), float((res[0][1] - res[1][1]).abs().max())
