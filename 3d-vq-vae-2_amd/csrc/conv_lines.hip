@@ -56,6 +56,8 @@ struct LArgs {
     int vec_out;               // 16-B epilogue path allowed (one N group, bd*N % 8 == 0, no y2 / res_up2)
     int region_lines;          // bytes of the lines region (weights follow)
     int cin_split;             // dgrad: output channels < cin_split go to y, the rest to y2
+    int S;                     // D-shifts per A row: a row is S consecutive output voxels along D and
+                               // column n = (shift n / N, channel n % N) (S * N = 16 when S > 1)
 };
 
 __device__ __forceinline__ int wrapc(int i, int n) {
@@ -137,9 +139,11 @@ __device__ __forceinline__ uint4 pack_item(const LArgs &a, const float *__restri
     const int c = it / ntot, nn = it - c * ntot;
     const int n = gi * ntot + nn;
     const int t2 = c / a.nch, j = c - t2 * a.nch;
-    const bool live = c < a.NCH && n < a.N;
+    // shift mode: column n = (shift sh, channel co) reads window position pd = kd + sh * s
+    const int sh = a.S > 1 ? n / a.N : 0, co = a.S > 1 ? n - sh * a.N : n;
+    const bool live = c < a.NCH && (a.S > 1 ? n < 16 : n < a.N);
     int e = 8 * j;
-    int kd = int(a.fC.div(uint32_t(e))), ci = e - kd * a.C;
+    int kd = int(a.fC.div(uint32_t(e))) - sh * a.s, ci = e - (kd + sh * a.s) * a.C;
     uint32_t pk[4];
 #pragma unroll
     for (int t = 0; t < 8; t += 2) {
@@ -147,9 +151,9 @@ __device__ __forceinline__ uint4 pack_item(const LArgs &a, const float *__restri
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             float val = 0.f;
-            if (live && kd < a.k) {
+            if (live && kd >= 0 && kd < a.k) {
                 const int tap = t2 * a.k + kd;  // t2 = kh * k + kw
-                val = DGRAD ? w[(int64_t(ci) * wCt + n) * K3 + (K3 - 1 - tap)] : w[(int64_t(n) * wCt + ci) * K3 + tap];
+                val = DGRAD ? w[(int64_t(ci) * wCt + co) * K3 + (K3 - 1 - tap)] : w[(int64_t(co) * wCt + ci) * K3 + tap];
             }
             v2[h] = val;
             if (++ci == a.C) {
@@ -191,9 +195,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
     const int row = lane & 15, kq = lane >> 4;
     const int nlines = a.hh * a.hw;
     const int nvb = a.bh * a.bw * a.bd;
-    const int nmt = (nvb + 15) / 16;
+    const int nmt = (nvb / a.S + 15) / 16;  // m-tiles of 16 A rows (rows = groups of S voxels along D)
     const int gi = blockIdx.y;
-    const int nw = min(NTOT, a.N - gi * NTOT);  // output columns of this group
+    const int nw = min(NTOT, a.N - gi * NTOT);  // output channels of this group
+    const int ncol = a.S > 1 ? 16 : nw;           // MFMA columns holding outputs
 
     // ---- once per workgroup: weight image of this N group + chunk offset table
     {
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
     int rowbase[MTW];
 #pragma unroll
     for (int m = 0; m < MTW; ++m) {
-        int v = (wave + 4 * m) * 16 + row;
+        int v = ((wave + 4 * m) * 16 + row) * a.S;
         if (v >= nvb) v = 0;
         const int ld_ = v & (a.bd - 1), lw_ = (v >> a.lbd) & (a.bw - 1), lh_ = v >> (a.lbd + a.lbw);
         rowbase[m] = ((lh_ * a.s) * a.hw + lw_ * a.s) * a.LS + a.pad0 + ld_ * a.s * a.C;
@@ -348,11 +353,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
                 const int cl = n * 16 + row;
-                if (cl >= nw) continue;
+                if (cl >= ncol) continue;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int v = (wave + 4 * m) * 16 + kq * 4 + i;
-                    if (v < nvb) otile[v * nw + cl] = acc[m][n][i];
+                for (int i = 0; i < 4; ++i) {  // row g holds voxels g*S .. g*S + S-1: [v][nw] = [g][S*nw]
+                    const int g = (wave + 4 * m) * 16 + kq * 4 + i;
+                    if (g * a.S < nvb) otile[g * ncol + cl] = acc[m][n][i];
                 }
             }
         }
@@ -545,7 +550,7 @@ void set_brick(LArgs &a, int bh, int bw, int bd) {
 
 // GEMM-conv geometry: input (B, Ca+Cb, iH, iW, iD) -> output (B, N, oH, oW, oD)
 Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, int oD, int k, int s, int p,
-          int circ) {
+          int circ, int S) {
     Plan P = {};
     LArgs &a = P.a;
     a.B = B; a.Ca = Ca; a.Cb = Cb; a.C = Ca + Cb; a.N = N;
@@ -554,7 +559,8 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
     if (s != 1 && s != 2) return P;
     if (int64_t(B) * iH * iW * iD * a.C >= (int64_t(1) << 31) || int64_t(B) * oH * oW * oD * N >= (int64_t(1) << 31))
         return P;
-    a.nch = (k * a.C + 7) / 8;
+    a.S = S;
+    a.nch = (((a.S - 1) * s + k) * a.C + 7) / 8;
     a.NCH = k * k * a.nch;
     a.nks = (a.NCH + 3) / 4;
     auto div = [](int v, int d) { return v % d == 0; };
@@ -566,7 +572,7 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
         if (nt > ntr) continue;
         if (nt == 3 && ntr != 3) continue;
         const int mtw = nt <= 2 ? 8 : 4;
-        const int target = 64 * mtw;
+        const int target = 64 * mtw * a.S;
         int bd = std::min(pow2_ceil(oD), 32);
         int bw = std::min(pow2_ceil(oW), std::max(1, target / (bd * 4)));
         bw = 1 << ilog2(bw);
@@ -597,7 +603,7 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
         P.nt = nt;
         break;
     }
-    if (!P.nt) return P;
+    if (!P.nt || a.bd % a.S) return Plan{};
     a.ntg = (ntr + P.nt - 1) / P.nt;
     a.ntn = P.nt * 16;
     a.nbh = (oH + a.bh - 1) / a.bh;
@@ -608,7 +614,7 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
     a.fupl = FastDiv(uint32_t(a.upl));
     {
         // window element offsets are pad0 + ld*s*C + 8j (+ multiples of LS)
-        const int sc = s * a.C;
+        const int sc = s * a.C * a.S;
         int e = 8;
         while (e > 1 && (sc % e || a.pad0 % e)) e /= 2;
         P.aln = 2 * e;
@@ -634,19 +640,32 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
     if (verbose)
         std::fprintf(stderr, "[vq3d] lines plan C%d->N%d k%d s%d: brick %dx%dx%d nt %d groups %d aln %d vec %d mvec %d lds %zu wg %d\n",
                      a.C, N, k, s, a.bh, a.bw, a.bd, P.nt, a.ntg, P.aln, a.vec, a.mvec, P.lds, a.nbricks * a.ntg);
+    if (verbose && a.S > 1) std::fprintf(stderr, "[vq3d] lines plan: %d D-shifts per MFMA row\n", a.S);
     return P;
+}
+
+// S > 1 (several output voxels along D per MFMA row) when the 16 columns would otherwise hold
+// only 4 or 8 output channels and the output depth holds whole groups; else S = 1.  4 -> 4 @512^2x128
+// forward 719 -> 389 us, backward-data 828 -> 403 us (7 instead of 20 k-steps per 64 voxels)
+Plan plan_s(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, int oD, int k, int s, int p,
+            int circ) {
+    if ((N == 4 || N == 8) && s == 1 && oD % (16 / N) == 0) {  // stride 2: measured slower (larger halo)
+        const Plan P = plan(B, Ca, Cb, N, iH, iW, iD, oH, oW, oD, k, s, p, circ, 16 / N);
+        if (P.ok) return P;
+    }
+    return plan(B, Ca, Cb, N, iH, iW, iD, oH, oW, oD, k, s, p, circ, 1);
 }
 
 Plan plan_for(const vq3d_conv_desc *d, bool dgrad) {
     if (d->dtype != VQ3D_BF16 || d->kernel < 2) return Plan{};
     const int circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
     if (!dgrad)
-        return plan(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
-                    d->kernel, d->stride, d->pad, circ);
+        return plan_s(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
+                      d->kernel, d->stride, d->pad, circ);
     const int pp = d->kernel - 1 - d->pad;
     if (d->stride != 1 || pp < 0) return Plan{};
-    return plan(d->batch, d->cout, 0, d->cin + d->cin2, d->out_h, d->out_w, d->out_d, d->in_h, d->in_w, d->in_d,
-                d->kernel, 1, pp, circ);
+    return plan_s(d->batch, d->cout, 0, d->cin + d->cin2, d->out_h, d->out_w, d->out_d, d->in_h, d->in_w, d->in_d,
+                  d->kernel, 1, pp, circ);
 }
 
 // persistent grid: workgroups resident at the kernel's occupancy (per CU), bricks strided

@@ -440,6 +440,12 @@ __global__ __launch_bounds__(256) void k_scale(float *__restrict__ x, float a, i
     for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) x[i] *= a;
 }
 
+// every 16-B slot of this workgroup's LDS allocation := all ones (a NaN in bf16 and fp32)
+__global__ __launch_bounds__(256) void k_poison_lds(int nslots) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds_slots[];
+    for (int i = threadIdx.x; i < nslots; i += 256) lds_slots[i] = uint4{~0u, ~0u, ~0u, ~0u};
+    __syncthreads();
+}
 
 }  // namespace vq3d
 
@@ -700,6 +706,20 @@ int vq3d_copy(void *dst, const void *src, size_t bytes, vq3d_stream_t stream) {
     if (!dst || !src) return fail("copy: null pointer");
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, as_stream(stream));
     return e == hipSuccess ? 0 : fail(std::string("copy: ") + hipGetErrorString(e));
+}
+
+int vq3d_poison_lds(vq3d_stream_t stream) {
+    // 64 KB per workgroup, 8 x the CU count of workgroups: every CU hosts at least two at once
+    // over its whole run, so its 160 KB are overwritten in every placement the allocator uses
+    constexpr int kBytes = 64 * 1024;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_poison_lds),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kBytes);
+        attr = true;
+    }
+    k_poison_lds<<<256 * 8, 256, kBytes, as_stream(stream)>>>(kBytes / 16);
+    return check_launch("poison_lds");
 }
 
 int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *gz, int64_t n,

@@ -464,8 +464,13 @@ __global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restric
                 }
             }
             if constexpr (CHAIN && !(PM_EXP & 512)) {
-                uint4 q = __builtin_bit_cast(uint4, read8(u1s, (mt * 16 + row) * C + 8 * kb));
-                if (kb == 2) q.y = q.z = q.w = 0u;  // channels 18..23 are the next voxel's
+                // K entries 18..31 are the next voxel's channels and meet zero weights, but they must
+                // be finite: for row 15 they lie in the NEXT m-tile, which another wave may not have
+                // written yet (on a workgroup's first tile: whatever the previous kernel left in LDS,
+                // where a NaN bit pattern times the zero weight poisoned the next block's t2)
+                uint4 q = kb == 3 ? uint4{0u, 0u, 0u, 0u}
+                                  : __builtin_bit_cast(uint4, read8(u1s, (mt * 16 + row) * C + 8 * kb));
+                if (kb == 2) q.y = q.z = q.w = 0u;
                 const f32x4 acc = mfma(__builtin_bit_cast(bf16x8, q), bw1n[0], f32x4{0.f, 0.f, 0.f, 0.f});
                 if (row < BR) {
 #pragma unroll

@@ -119,6 +119,7 @@ _SIGS = {
     "vq3d_cast": (c_int, [c_int, P, c_int, P, c_i64, P]),
     "vq3d_zero": (c_int, [P, c_size, P]),
     "vq3d_copy": (c_int, [P, P, c_size, P]),
+    "vq3d_poison_lds": (c_int, [P]),
     "vq3d_scale": (c_int, [P, c_float, c_i64, P]),
     "vq3d_causal_attn_supported": (c_int, [c_int] * 3),
     "vq3d_causal_attn_workspace_bytes": (c_size, [c_int] * 3),

@@ -413,6 +413,10 @@ int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, 
               vq3d_stream_t stream);
 int vq3d_zero(void *p, size_t bytes, vq3d_stream_t stream);
 int vq3d_copy(void *dst, const void *src, size_t bytes, vq3d_stream_t stream);
+/* Test support: fill the LDS of every CU with all-ones words (bf16 / fp32 NaN) so a kernel that
+ * reads LDS it never wrote -- even only to multiply it by a zero weight -- shows up as NaN in its
+ * output instead of depending on what the previous kernel left behind. */
+int vq3d_poison_lds(vq3d_stream_t stream);
 /* gz = g * elu'(z) recovered from the OUTPUT y = elu(z): 1 if y > 0 else y + 1 (FixupResBlock's
  * post-activation, layers.py:287-288); n elements of dtype */
 int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *gz, int64_t n,

@@ -36,6 +36,17 @@ CASES = [
     (2, 2, (8, 8, 40), 3, 1, 1, True),
     (9, 9, (8, 8, 8), 3, 1, 1, False),
     (3, 6, (6, 6, 8), 4, 2, 1, True),
+    # 4 / 8 output channels: 4 / 2 output voxels along D per MFMA row (lines engine D-shifts),
+    # incl. a brick overhanging the grid in D, zero padding, stride 2 and a depth that falls back
+    (4, 4, (16, 16, 64), 3, 1, 1, True),
+    (8, 8, (8, 8, 32), 3, 1, 1, True),
+    (4, 8, (8, 16, 16), 3, 1, 1, False),
+    (8, 4, (8, 8, 12), 3, 1, 1, True),
+    (9, 4, (8, 8, 24), 3, 1, 1, True),
+    (4, 9, (8, 8, 16), 3, 1, 1, True),
+    (4, 4, (16, 16, 32), 4, 2, 1, True),
+    (8, 8, (16, 16, 16), 4, 2, 1, False),
+    (4, 4, (8, 8, 6), 3, 1, 1, True),
 ]
 
 

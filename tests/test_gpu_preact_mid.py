@@ -187,7 +187,12 @@ def test_fused_mid_block_side_stream(gpu, shape):
         assert torch.equal(a[2][n], b[2][n]), n
 
 
-def _run_chain(blocks, x, gy, gpu, chained, concurrent=False):
+def _poison():
+    from vq3d import _lib as L
+    L.call("vq3d_poison_lds", L.stream())
+
+
+def _run_chain(blocks, x, gy, gpu, chained, concurrent=False, poison=False):
     """A run of blocks through layers.BlockStack (chained: Fn.PreActMidRunFn) or block by block
     (Fn.PreActBlockFn); returns out, gx and every parameter gradient, all as float64 on the CPU."""
     from vq3d import functional as Fn, ops
@@ -198,13 +203,18 @@ def _run_chain(blocks, x, gy, gpu, chained, concurrent=False):
     xd = x.to(gpu).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
     ops.set_concurrent_wgrad(concurrent)
     try:
+        if poison:
+            _poison()
         if chained:
             out = stack(xd)
         else:
             out = xd
             for b in stack:
                 out = Fn.PreActBlockFn.apply(out, b, *b._fn_params)
-        out.backward(gy.to(gpu).bfloat16().contiguous(memory_format=CL))
+        gyd = gy.to(gpu).bfloat16().contiguous(memory_format=CL)
+        if poison:
+            _poison()
+        out.backward(gyd)
         ops.join_side()
     finally:
         ops.set_concurrent_wgrad(False)
@@ -231,3 +241,22 @@ def test_mid_run_chain_matches_per_block(gpu, shape, nblk, concurrent):
     assert rel(b[1], a[1]) <= 1e-2, rel(b[1], a[1])
     for n in a[2]:
         assert rel(b[2][n], a[2][n]) <= 1e-2, (n, rel(b[2][n], a[2][n]))
+
+
+@pytest.mark.parametrize("shape", [(2, 18, 16, 8, 16), (1, 18, 128, 128, 32)])
+def test_mid_run_chain_ignores_stale_lds(gpu, shape):
+    """Regression: the chained forward's next-block t2 stage read K entries past a voxel's 18
+    channels from LDS another wave had not written yet and multiplied them by zero weights; LDS
+    left holding a NaN pattern by an earlier kernel turned into NaN activations (the 3-layer
+    bench step went NaN after ~10 steps).  With every CU's LDS filled with NaN before the forward
+    and before the backward the run must give the same bits as without."""
+    blocks = [_block(seed=40 + i) for i in range(3)]
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(shape, generator=g).bfloat16().double()
+    gy = torch.randn(shape, generator=g).bfloat16().double()
+    a = _run_chain(blocks, x, gy, gpu, chained=True)
+    b = _run_chain(blocks, x, gy, gpu, chained=True, poison=True)
+    assert torch.isfinite(b[0]).all() and torch.isfinite(b[1]).all()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n
