@@ -34,6 +34,12 @@ struct FastDiv {
 __device__ __forceinline__ void st(float *p, float v) { *p = v; }
 __device__ __forceinline__ void st(bf16_t *p, float v) { *p = f2bf(v); }
 
+// Native 32-bit vectors for register-staged loads: an array of HIP's uint4 / uint2 (a class with
+// union members) held across a loop is NOT promoted to registers by hipcc -- it lives in scratch
+// memory, and every prefetch then waits on its scratch store -- while these are.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 // ---------------------------------------------------------------- N-element vector moves
 // N consecutive elements of storage type T (bf16 or fp32) as raw 32-bit words, so a kernel can
 // issue a whole voxel's (or a run of voxels') loads before it converts anything.  N * sizeof(T)

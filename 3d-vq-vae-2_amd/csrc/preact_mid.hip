@@ -197,8 +197,8 @@ struct LinesLd {
     using T = Tile<TH, TW>;
     static constexpr int NI = T::NL * 9, PI = (NI + NT - 1) / NT;
     static constexpr int NEG = T::NL * 4, PE = (NEG + NT - 1) / NT;  // (line, side, chunk)
-    uint4 vi[PI];
-    uint4 ve[PE];
+    u32x4 vi[PI];
+    u32x4 ve[PE];
     // every load is unconditional (indices past the end are clamped): a branch around a load
     // makes hipcc wait for it on the spot
     __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
@@ -209,7 +209,7 @@ struct LinesLd {
             const int line = i / 9, part = i - 9 * line, lh = line / T::LW, lw = line - lh * T::LW;
             const int gh = wrapm(o.h0 - 1 + lh, a.H), gw = wrapm(o.w0 - 1 + lw, a.W);
             const int64_t v0 = ((int64_t(o.b) * a.H + gh) * a.W + gw) * a.D + o.d0;
-            vi[u] = reinterpret_cast<const uint4 *>(src + v0 * BR)[part];
+            vi[u] = reinterpret_cast<const u32x4 *>(src + v0 * BR)[part];
         }
 #pragma unroll
         for (int u = 0; u < PE; ++u) {
@@ -221,7 +221,7 @@ struct LinesLd {
             // left: the 32 bytes before position d0 (the line's end when d0 = 0); right: from
             // position d0 + 8 (the line's start when that wraps)
             const int e0 = side ? ((o.d0 + TD == a.D) ? 0 : (o.d0 + TD) * BR) : ((o.d0 == 0 ? a.D : o.d0) * BR - 16);
-            ve[u] = *reinterpret_cast<const uint4 *>(src + lb + e0 + 8 * ch);
+            ve[u] = *reinterpret_cast<const u32x4 *>(src + lb + e0 + 8 * ch);
         }
     }
     __device__ __forceinline__ void store(bf16_t *lines) const {
@@ -231,7 +231,7 @@ struct LinesLd {
             const int i = tid + u * NT;
             if (i < NI) {
                 const int line = i / 9, part = i - 9 * line;
-                reinterpret_cast<uint4 *>(lines + line * LSP + LINT)[part] = vi[u];
+                reinterpret_cast<u32x4 *>(lines + line * LSP + LINT)[part] = vi[u];
             }
         }
 #pragma unroll
@@ -239,7 +239,7 @@ struct LinesLd {
             const int i = tid + u * NT;
             if (i < NEG) {
                 const int line = i >> 2, side = (i >> 1) & 1, ch = i & 1;
-                *reinterpret_cast<uint4 *>(lines + line * LSP + (side ? LINT + 9 * TD : 0) + 8 * ch) = ve[u];
+                *reinterpret_cast<u32x4 *>(lines + line * LSP + (side ? LINT + 9 * TD : 0) + 8 * ch) = ve[u];
             }
         }
     }
@@ -252,14 +252,14 @@ template <int TH, int TW, int CH>
 struct TileLd {
     using T = Tile<TH, TW>;
     static constexpr int PR = CH * TD / 8, N = T::NRUN * PR, P = (N + NT - 1) / NT;
-    uint4 v[P];
+    u32x4 v[P];
     __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
         const int tid = threadIdx.x;
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             const int i = min(tid + u * NT, N - 1);
             const int r = i / PR, part = i - PR * r;
-            v[u] = reinterpret_cast<const uint4 *>(src + run_vox<TW>(a, o, r) * CH)[part];
+            v[u] = reinterpret_cast<const u32x4 *>(src + run_vox<TW>(a, o, r) * CH)[part];
         }
     }
     __device__ __forceinline__ void store(bf16_t *dst) const {
@@ -267,7 +267,7 @@ struct TileLd {
 #pragma unroll
         for (int u = 0; u < P; ++u) {
             const int i = tid + u * NT;
-            if (i < N) reinterpret_cast<uint4 *>(dst)[i] = v[u];
+            if (i < N) reinterpret_cast<u32x4 *>(dst)[i] = v[u];
         }
     }
 };
@@ -508,13 +508,13 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
     const Scal s = load_scal(p);
     float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f;
     const int64_t nblk = nvox / NT;
-    uint4 vg[PG], vt[PT];
+    u32x4 vg[PG], vt[PT];
     auto load = [&](int64_t blk) {
         const int64_t v0 = blk * NT;
 #pragma unroll
-        for (int u = 0; u < PG; ++u) vg[u] = reinterpret_cast<const uint4 *>(g + v0 * C)[min(tid + u * NT, NG - 1)];
+        for (int u = 0; u < PG; ++u) vg[u] = reinterpret_cast<const u32x4 *>(g + v0 * C)[min(tid + u * NT, NG - 1)];
 #pragma unroll
-        for (int u = 0; u < PT; ++u) vt[u] = reinterpret_cast<const uint4 *>(t3 + v0 * BR)[min(tid + u * NT, NTT - 1)];
+        for (int u = 0; u < PT; ++u) vt[u] = reinterpret_cast<const u32x4 *>(t3 + v0 * BR)[min(tid + u * NT, NTT - 1)];
     };
     if (blockIdx.x < nblk) load(blockIdx.x);
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
@@ -522,10 +522,10 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < PG; ++u)
-            if (tid + u * NT < NG) reinterpret_cast<uint4 *>(gs)[tid + u * NT] = vg[u];
+            if (tid + u * NT < NG) reinterpret_cast<u32x4 *>(gs)[tid + u * NT] = vg[u];
 #pragma unroll
         for (int u = 0; u < PT; ++u)
-            if (tid + u * NT < NTT) reinterpret_cast<uint4 *>(ts)[tid + u * NT] = vt[u];
+            if (tid + u * NT < NTT) reinterpret_cast<u32x4 *>(ts)[tid + u * NT] = vt[u];
         if (blk + gridDim.x < nblk) load(blk + gridDim.x);
         __syncthreads();
         {
@@ -798,7 +798,7 @@ struct W2c {
     static_assert(NL * D == CHV && TH * TW == NL, "chunk");
 };
 
-__device__ __forceinline__ void scatter9(bf16_t *dst, int pitch, int e0, uint4 q, int base) {
+__device__ __forceinline__ void scatter9(bf16_t *dst, int pitch, int e0, u32x4 q, int base) {
     // the 8 elements e0 .. e0 + 7 of a 9-channel voxel-major run to dst[c * pitch + base + pos]
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
         const int e = min(16 * n + row, 26), kd = e / BR, ci = e - kd * BR;
         toff[n] = ci * K::CSTR + kd;
     }
-    uint4 vz[K::PZ], vt[K::PT];
+    u32x4 vz[K::PZ], vt[K::PT];
     auto load = [&](int c) {
         const int tw_i = c % ntw, r = c / ntw, th_i = r % nth, b = r / nth;
         const int h0 = th_i * K::TH, w0 = tw_i * K::TW;
@@ -838,14 +838,14 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
         for (int u = 0; u < K::PZ; ++u) {
             const int i = min(tid + u * NT9, K::ZQ - 1), l = i / K::QL, part = i - l * K::QL;
             const int64_t lv = ((int64_t(b) * a.H + h0 + l / K::TW) * a.W + w0 + l % K::TW) * D;
-            vz[u] = reinterpret_cast<const uint4 *>(gz3 + lv * BR)[part];
+            vz[u] = reinterpret_cast<const u32x4 *>(gz3 + lv * BR)[part];
         }
 #pragma unroll
         for (int u = 0; u < K::PT; ++u) {
             const int i = min(tid + u * NT9, K::TQ - 1), hl = i / K::QL, part = i - hl * K::QL;
             const int lh = hl / K::LW, lw = hl - lh * K::LW;
             const int64_t lv = ((int64_t(b) * a.H + wrapm(h0 - 1 + lh, a.H)) * a.W + wrapm(w0 - 1 + lw, a.W)) * D;
-            vt[u] = reinterpret_cast<const uint4 *>(t2 + lv * BR)[part];
+            vt[u] = reinterpret_cast<const u32x4 *>(t2 + lv * BR)[part];
         }
     };
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -920,17 +920,17 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const bf16_t *__rest
     const bf16_t *aT = isG3 ? t3T : z1T, *bT = isG3 ? gT : u1T;
     // per piece: gz1 / t3 SUBV * 9 / 8 16-B pieces each, x / g SUBV * 18 / 8 each
     constexpr int N9 = SUBV * BR / 8, N18 = SUBV * C / 8, NQ = 2 * N9 + 2 * N18, PQ = (NQ + NT - 1) / NT;
-    uint4 vq[PQ];
+    u32x4 vq[PQ];
     auto load = [&](int64_t v0) {
 #pragma unroll
         for (int u = 0; u < PQ; ++u) {
             const int i = min(tid + u * NT, NQ - 1);
-            const uint4 *src;
+            const u32x4 *src;
             int k;
-            if (i < N9) src = reinterpret_cast<const uint4 *>(gz1 + v0 * BR), k = i;
-            else if (i < 2 * N9) src = reinterpret_cast<const uint4 *>(t3 + v0 * BR), k = i - N9;
-            else if (i < 2 * N9 + N18) src = reinterpret_cast<const uint4 *>(x + v0 * C), k = i - 2 * N9;
-            else src = reinterpret_cast<const uint4 *>(g + v0 * C), k = i - 2 * N9 - N18;
+            if (i < N9) src = reinterpret_cast<const u32x4 *>(gz1 + v0 * BR), k = i;
+            else if (i < 2 * N9) src = reinterpret_cast<const u32x4 *>(t3 + v0 * BR), k = i - N9;
+            else if (i < 2 * N9 + N18) src = reinterpret_cast<const u32x4 *>(x + v0 * C), k = i - 2 * N9;
+            else src = reinterpret_cast<const u32x4 *>(g + v0 * C), k = i - 2 * N9 - N18;
             vq[u] = src[k];
         }
     };

@@ -136,6 +136,28 @@ def test_tiled_wgrad_matches_valu(gpu, case):
     assert abs(float(ms) - float(rs)) <= 2e-2 * (float((wt * rw).abs().sum()) / max(abs(float(sc)), 1e-3)) + 1e-3
 
 
+@pytest.mark.parametrize("case", [(2, (8, 8, 128)), (1, (4, 12, 128)), (1, (8, 8, 64))])
+def test_plain_wgrad_c4(gpu, case):
+    """The 4 -> 4 3x3x3 circular weight gradient without prologue / epilogue parameters (the
+    full-resolution ResizeConv branch conv: D-shifted MFMA kernel on 128-deep grids, the generic
+    engine elsewhere), bf16, accumulated into dW, vs the fp32 VALU engine on the same
+    bf16-representable inputs: only the summation order differs."""
+    from vq3d import ops
+    bsz, (h, w, d) = case
+    g = torch.Generator(device=gpu).manual_seed(5 + h)
+    geom = ops.ConvGeom(3, 1, 1, True)
+    x = rnd((bsz, 4, h, w, d), gpu, g).contiguous(memory_format=CL)
+    gy = rnd((bsz, 4, h, w, d), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((4, 4, 3, 3, 3), gpu, g, 0.3)
+    base = rnd((4, 4, 3, 3, 3), gpu, g)
+    outs = []
+    for dt in (torch.float32, torch.bfloat16):
+        dw = base.clone()
+        ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, want_gx=False, dw=dw)
+        outs.append(dw - base)
+    assert rel(outs[1], outs[0]) < 1e-3, rel(outs[1], outs[0])
+
+
 PW_CASES = [
     # (cin, cin2, cout, (h, w, d))
     (9, 0, 18, (16, 16, 8)),
