@@ -54,6 +54,8 @@ SHAPES = [
     (r"k_col_bwd<8, 4>", 1048576, "8-ch block bwd: 3x3x3 4->4 dgrad + wgrad @256^2x64", 4 * _V256 * (432 + 64),
      _V256 * 32 * 2),
     (r"k_col_fwd<2, 1>", 131072, "2-ch block fwd: 3x3x3 1->1 @128^2x32", 2 * _V128 * (27 + 4), _V128 * 6 * 2),
+    (r"k_wgrad_c4$", 131072, "up-block conv2 wgrad (D-shifted MFMA): 3x3x3 4->4 @512^2x128", 2 * _V512 * 432,
+     _V512 * 8 * 2),
     (r"k_col_bwd<2, 1>", 131072, "2-ch block bwd: 3x3x3 1->1 @128^2x32", 4 * _V128 * (27 + 4), _V128 * 8 * 2),
 ]
 
