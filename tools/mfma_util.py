@@ -47,16 +47,16 @@ SHAPES = [
      _V32 * (216 * 4 + 72 * 2)),
     (r"k_wide_wgrad", 79872, "72-ch block wgrad: 3x3x3 36->36 + 2x 1x1 @32^2x8", 2 * _V32 * (34992 + 5184),
      _V32 * (144 * 4 + 72 * 2)),
-    (r"k_col_fwd<4, 2>", 8388608, "4-ch block fwd: 3x3x3 2->2 @512^2x128", 2 * _V512 * (108 + 16), _V512 * 12 * 2),
-    (r"k_col_bwd<4, 2>", 8388608, "4-ch block bwd: 3x3x3 2->2 dgrad + wgrad @512^2x128", 4 * _V512 * (108 + 16),
+    (r"k_col_fwd<4, 2[,>]", 8388608, "4-ch block fwd: 3x3x3 2->2 @512^2x128", 2 * _V512 * (108 + 16), _V512 * 12 * 2),
+    (r"k_col_bwd<4, 2[,>]", 8388608, "4-ch block bwd: 3x3x3 2->2 dgrad + wgrad @512^2x128", 4 * _V512 * (108 + 16),
      _V512 * 16 * 2),
-    (r"k_col_fwd<8, 4>", 1048576, "8-ch block fwd: 3x3x3 4->4 @256^2x64", 2 * _V256 * (432 + 64), _V256 * 24 * 2),
-    (r"k_col_bwd<8, 4>", 1048576, "8-ch block bwd: 3x3x3 4->4 dgrad + wgrad @256^2x64", 4 * _V256 * (432 + 64),
+    (r"k_col_fwd<8, 4[,>]", 1048576, "8-ch block fwd: 3x3x3 4->4 @256^2x64", 2 * _V256 * (432 + 64), _V256 * 24 * 2),
+    (r"k_col_bwd<8, 4[,>]", 1048576, "8-ch block bwd: 3x3x3 4->4 dgrad + wgrad @256^2x64", 4 * _V256 * (432 + 64),
      _V256 * 32 * 2),
-    (r"k_col_fwd<2, 1>", 131072, "2-ch block fwd: 3x3x3 1->1 @128^2x32", 2 * _V128 * (27 + 4), _V128 * 6 * 2),
+    (r"k_col_fwd<2, 1[,>]", 131072, "2-ch block fwd: 3x3x3 1->1 @128^2x32", 2 * _V128 * (27 + 4), _V128 * 6 * 2),
     (r"k_wgrad_c4$", 131072, "up-block conv2 wgrad (D-shifted MFMA): 3x3x3 4->4 @512^2x128", 2 * _V512 * 432,
      _V512 * 8 * 2),
-    (r"k_col_bwd<2, 1>", 131072, "2-ch block bwd: 3x3x3 1->1 @128^2x32", 4 * _V128 * (27 + 4), _V128 * 8 * 2),
+    (r"k_col_bwd<2, 1[,>]", 131072, "2-ch block bwd: 3x3x3 1->1 @128^2x32", 4 * _V128 * (27 + 4), _V128 * 8 * 2),
 ]
 
 
