@@ -543,8 +543,8 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     if constexpr (std::is_same<T, bf16_t>::value) {
         if (mid_w2grad_ok(d) && dw && !escale && !dscale && !dbias && !dcbias && ws && ws_bytes >= mid_w2grad_ws(d))
             return mid_w2grad(d, x, g, dw, ws, ws_bytes, s);
-        if (wgrad_c4_ok(d) && dw && !escale && !dscale && !dbias && !dcbias && ws && ws_bytes >= wgrad_c4_ws(d))
-            return wgrad_c4(d, x, g, dw, ws, ws_bytes, s);
+        if (wgrad_ds_ok(d) && dw && !escale && !dscale && !dcbias && ws && ws_bytes >= wgrad_ds_ws(d))
+            return wgrad_ds(d, x, g, pa, pb, dw, dbias, ws, ws_bytes, s);
         if (use_lines_wgrad(d))
             return launch_lines_wgrad(d, x, x2, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
         {
@@ -637,7 +637,7 @@ size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
     if (pass == VQ3D_PASS_BWD_DATA) return is_pointwise(d) ? pw_dgrad_workspace(d) : lines_workspace(d, true);
     if (is_pointwise(d)) return pw_wgrad_workspace(d);
-    return std::max({use_lines_wgrad(d) ? lines_wgrad_workspace(d) : size_t(0), mid_w2grad_ws(d), wgrad_c4_ws(d)});
+    return std::max({use_lines_wgrad(d) ? lines_wgrad_workspace(d) : size_t(0), mid_w2grad_ws(d), wgrad_ds_ws(d)});
 }
 
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,

@@ -113,12 +113,14 @@ bool mid_w2grad_ok(const vq3d_conv_desc *d);
 size_t mid_w2grad_ws(const vq3d_conv_desc *d);
 int mid_w2grad(const vq3d_conv_desc *d, const void *x, const void *g, float *dw, void *ws, size_t ws_bytes,
                hipStream_t s);
-// 3x3x3 circular 4 -> 4 weight gradient on 128-deep grids (wgrad_c4.hip): D-shifted MFMA over whole
-// D-lines, per-workgroup partials in the workspace (wgrad_c4_ws bytes), fixed-order reduction
-bool wgrad_c4_ok(const vq3d_conv_desc *d);
-size_t wgrad_c4_ws(const vq3d_conv_desc *d);
-int wgrad_c4(const vq3d_conv_desc *d, const void *x, const void *g, float *dw, void *ws, size_t ws_bytes,
-             hipStream_t s);
+// few-channel k^3 weight gradients on the large grids (wgrad_ds.hip): D-shifted MFMA over whole
+// D-lines for the instantiated (cin, cout, k, stride, pad, depth) shapes, optional prologue and
+// sum-of-g (conv bias) gradient; per-workgroup partials in the workspace (wgrad_ds_ws bytes),
+// fixed-order reduction
+bool wgrad_ds_ok(const vq3d_conv_desc *d);
+size_t wgrad_ds_ws(const vq3d_conv_desc *d);
+int wgrad_ds(const vq3d_conv_desc *d, const void *x, const void *g, const float *pro_a, const float *pro_b, float *dw,
+             float *dbias, void *ws, size_t ws_bytes, hipStream_t s);
 int col_reduce_run(int nblocks, int batch, int C, int BR, int h, int w, int d, void *workspaces, size_t stride,
                    float *const *gtab, const float *const *ptab, hipStream_t s);
 

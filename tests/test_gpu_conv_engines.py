@@ -136,26 +136,44 @@ def test_tiled_wgrad_matches_valu(gpu, case):
     assert abs(float(ms) - float(rs)) <= 2e-2 * (float((wt * rw).abs().sum()) / max(abs(float(sc)), 1e-3)) + 1e-3
 
 
-@pytest.mark.parametrize("case", [(2, (8, 8, 128)), (1, (4, 12, 128)), (1, (8, 8, 64))])
-def test_plain_wgrad_c4(gpu, case):
-    """The 4 -> 4 3x3x3 circular weight gradient without prologue / epilogue parameters (the
-    full-resolution ResizeConv branch conv: D-shifted MFMA kernel on 128-deep grids, the generic
-    engine elsewhere), bf16, accumulated into dW, vs the fp32 VALU engine on the same
-    bf16-representable inputs: only the summation order differs."""
+WGRAD_DS_CASES = [
+    # (batch, cin, cout, (h, w, d) input, k, s, p, circular, prologue + bias gradient)
+    (2, 4, 4, (8, 8, 128), 3, 1, 1, True, False),    # up-block ResizeConv branch conv (D-shifted kernel)
+    (1, 4, 4, (4, 12, 128), 3, 1, 1, True, False),
+    (1, 4, 4, (8, 8, 128), 4, 2, 1, True, False),    # down-block branch convs
+    (2, 8, 8, (4, 8, 64), 4, 2, 1, True, False),
+    (1, 16, 16, (8, 8, 32), 4, 2, 1, True, False),
+    (1, 4, 8, (8, 8, 128), 2, 2, 0, False, True),    # down-block skip convs (+ bias1c, bias1d)
+    (2, 8, 16, (4, 8, 64), 2, 2, 0, False, True),
+    (1, 4, 4, (8, 8, 64), 3, 1, 1, True, False),     # depth without an instance: generic engine
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_DS_CASES)
+def test_wgrad_dshift(gpu, case):
+    """Few-channel weight gradients without scale / conv-bias epilogue parameters (wgrad_ds.hip: the
+    full-resolution up / down block convs, D-shifted MFMA over whole D-lines), bf16, accumulated
+    into dW (and, for the skip convs, the bias gradient sum(g) and the prologue x + b), vs the fp32
+    VALU engine on the same bf16-representable inputs: only the summation order differs."""
     from vq3d import ops
-    bsz, (h, w, d) = case
-    g = torch.Generator(device=gpu).manual_seed(5 + h)
-    geom = ops.ConvGeom(3, 1, 1, True)
-    x = rnd((bsz, 4, h, w, d), gpu, g).contiguous(memory_format=CL)
-    gy = rnd((bsz, 4, h, w, d), gpu, g).contiguous(memory_format=CL)
-    wt = rnd((4, 4, 3, 3, 3), gpu, g, 0.3)
-    base = rnd((4, 4, 3, 3, 3), gpu, g)
+    bsz, cin, cout, (h, w, d), k, s, p, circ, pro = case
+    g = torch.Generator(device=gpu).manual_seed(5 + h + cin)
+    geom = ops.ConvGeom(k, s, p, circ)
+    x = rnd((bsz, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    gy = rnd((bsz, cout, geom.out(h), geom.out(w), geom.out(d)), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((cout, cin, k, k, k), gpu, g, 0.3)
+    base = rnd((cout, cin, k, k, k), gpu, g)
+    b1c = rnd((1,), gpu, g, 0.1)
     outs = []
     for dt in (torch.float32, torch.bfloat16):
         dw = base.clone()
-        ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, want_gx=False, dw=dw)
-        outs.append(dw - base)
-    assert rel(outs[1], outs[0]) < 1e-3, rel(outs[1], outs[0])
+        db = torch.full((1,), 0.5, device=gpu)
+        ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, want_gx=False, dw=dw, pro=(b1c,) if pro else None,
+                     dbias=db if pro else None)
+        outs.append((dw - base, db - 0.5))
+    assert rel(outs[1][0], outs[0][0]) < 1e-3, rel(outs[1][0], outs[0][0])
+    if pro:
+        assert abs(float(outs[1][1]) - float(outs[0][1])) <= 1e-3 * float(gy.abs().sum()) ** 0.5 + 1e-3
 
 
 PW_CASES = [
