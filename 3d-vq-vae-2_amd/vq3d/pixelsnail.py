@@ -535,12 +535,16 @@ class PixelSNAIL(nn.Module):
             logits = self.logits(onehot)
             unreduced = F.cross_entropy(logits, codes, reduction="none")
         else:
-            lam, index = mix
+            lam, index = mix  # lam a Python float as in the reference (no host-to-device copy: capturable)
             x = onehot.float()
-            lam_t = torch.as_tensor(lam, dtype=x.dtype, device=x.device)
-            logits = self.logits(lam_t * x + (1 - lam_t) * x[index])
-            unreduced = (lam_t * F.cross_entropy(logits, codes, reduction="none")
-                         + (1 - lam_t) * F.cross_entropy(logits, codes[index], reduction="none"))
+            if torch.equal(index, torch.arange(index.numel())):  # host check (batch 1: always)
+                xi, ci = x, codes
+            else:
+                idx = index.to(x.device)
+                xi, ci = x[idx], codes[idx]
+            logits = self.logits(lam * x + (1 - lam) * xi)
+            unreduced = (lam * F.cross_entropy(logits, codes, reduction="none")
+                         + (1 - lam) * F.cross_entropy(logits, ci, reduction="none"))
         loss = unreduced.mean()
         return loss, {"bits_per_dim": loss.detach() / np.log(2)}
 

@@ -292,3 +292,40 @@ def test_published_mid_prior_step(gpu):
     got = out.reshape(out.shape[0], out.shape[1], -1)[..., torch.as_tensor(rows)]
     print("published prior losses", losses, "attention rel", rel(got, ref.numpy()))
     assert rel(got, ref.numpy()) < 2e-2  # bf16 q / k / v / out storage, fp32 arithmetic
+
+
+def test_prior_step_with_mixup_captures(gpu):
+    """bench.py --prior captures the training step (mixup forward, backward, Adam) as a HIP graph: no
+    host-to-device copy may happen inside it; one replay gives the same loss as the eager step."""
+    from vq3d import pixelsnail as PS
+    from vq3d.flat import FlatParams
+    from vq3d.optim import FusedAdam
+    torch.manual_seed(0)
+    args = PS.default_args(num_embeddings=[16, 0], model_dim=32, num_blocks=2, num_layers_per_block=2,
+                           causal_dropout_prob=0.0, attention_dropout_prob=0.0, mixup_alpha=0.2)
+    m = PS.PixelSNAIL(args, compute_dtype="bf16").to(gpu)
+    flat = FlatParams(m.parameters(), gpu)
+    opt = FusedAdam(m.parameters(), flat, lr=0.0, amsgrad=True)  # lr 0: replays see the same weights
+    m.train()
+    codes = torch.randint(0, 16, (1, 8, 8, 4), generator=torch.Generator().manual_seed(2)).to(gpu)
+    onehot = torch.nn.functional.one_hot(codes, 16).permute(0, 4, 1, 2, 3).contiguous()
+    mix = (0.3, torch.zeros(1, dtype=torch.int64))
+
+    def step():
+        opt.zero_grad()
+        loss, _ = m.cross_entropy_onehot(onehot.float(), codes, mix)
+        loss.backward()
+        opt.step()
+        return loss
+    eager = float(step().detach())
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static = step()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert np.isfinite(eager) and abs(float(static.detach()) - eager) <= 1e-6 * abs(eager), (eager, float(static))
