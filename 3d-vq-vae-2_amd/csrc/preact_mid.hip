@@ -50,6 +50,10 @@
 #ifndef PM_BWD_PER
 #define PM_BWD_PER 0
 #endif
+// minimum waves per SIMD the backward-data tile kernel is compiled for (1: the compiler's choice)
+#ifndef PM_BWD_WPE
+#define PM_BWD_WPE 1
+#endif
 
 namespace vq3d {
 
@@ -577,7 +581,7 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
 // scalar partials, k_pm_bwd1's arithmetic -- from this tile's gx while it is still in LDS (gx is
 // that block's g) and the previous block's t3, instead of a k_pm_bwd1 launch re-reading gx.
 template <int TH, int TW, bool CHAIN>
-__global__ __launch_bounds__(NT) void k_pm_bwd2(PmArgs a, const bf16_t *__restrict__ gz3, const bf16_t *__restrict__ t2,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE))) void k_pm_bwd2(PmArgs a, const bf16_t *__restrict__ gz3, const bf16_t *__restrict__ t2,
                                                 const bf16_t *__restrict__ x, const bf16_t *__restrict__ g,
                                                 const float *__restrict__ w1, const float *__restrict__ w2,
                                                 vq3d_preact_params p, bf16_t *__restrict__ gx,

@@ -136,6 +136,41 @@ def test_tiled_wgrad_matches_valu(gpu, case):
     assert abs(float(ms) - float(rs)) <= 2e-2 * (float((wt * rw).abs().sum()) / max(abs(float(sc)), 1e-3)) + 1e-3
 
 
+S2_DGRAD_CASES = [
+    # (cin, cout, (h, w, d) input, aux + addend + gscale): 4x4x4 stride-2 circular backward-data
+    # (k_dgrad_s2_pair: parity-class rows, the down blocks' branch conv), incl. a 2-deep grid that
+    # wraps inside one tile
+    (4, 4, (8, 8, 16), True), (4, 8, (8, 8, 16), False), (8, 4, (8, 16, 8), True), (8, 8, (4, 4, 2), True),
+    (8, 8, (16, 8, 32), False), (4, 4, (2, 4, 4), True),
+]
+
+
+@pytest.mark.parametrize("case", S2_DGRAD_CASES)
+def test_dgrad_s2_matches_valu(gpu, case):
+    """bf16 stride-2 backward-data (+ the activated-aux derivative, the addend, the gradient scale and
+    the prologue-scalar partial sums) vs the fp32 engine on the same bf16-representable inputs."""
+    from vq3d import ops
+    cin, cout, (h, w, d), epi = case
+    g = torch.Generator(device=gpu).manual_seed(11 + h + cin)
+    geom = ops.ConvGeom(4, 2, 1, True)
+    x = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((cout, cin, 4, 4, 4), gpu, g, 0.3)
+    gy = rnd((2, cout, geom.out(h), geom.out(w), geom.out(d)), gpu, g).contiguous(memory_format=CL)
+    add = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    ab, gs = rnd((1,), gpu, g, 0.3), rnd((1,), gpu, g)
+    outs = []
+    for dt in (torch.float32, torch.bfloat16):
+        pre, post = torch.zeros(1, device=gpu), torch.zeros(1, device=gpu)
+        kw = dict(gscale=gs, aux=x.to(dt), aux_b=ab, addend=add.to(dt), dpro_pre=pre, dpro_post=post) if epi else {}
+        gx, _ = ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, **kw)
+        outs.append((gx.float(), pre, post))
+    (r, rp, rq), (m, mp, mq) = outs
+    assert rel(m, r) < 1.5e-2, rel(m, r)
+    if epi:
+        tol = 2e-2 * float(r.abs().sum()) / r.numel() ** 0.5 + 1e-3
+        assert abs(float(mp) - float(rp)) <= tol and abs(float(mq) - float(rq)) <= tol
+
+
 WGRAD_DS_CASES = [
     # (batch, cin, cout, (h, w, d) input, k, s, p, circular, prologue + bias gradient)
     (2, 4, 4, (8, 8, 128), 3, 1, 1, True, False),    # up-block ResizeConv branch conv (D-shifted kernel)
