@@ -15,6 +15,8 @@
 #include "conv_epi.h"
 #include "engines.h"
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -648,6 +650,185 @@ static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, con
     return check_launch(dgrad ? "conv3d_bwd_data(pointwise sg)" : "conv3d_fwd(pointwise sg)");
 }
 
+// ---- matrix-core 1x1 conv for the up / down blocks' branch and skip convs on the mid grids
+// (8 .. 256 channels, 128 .. 1M voxels): Y[v][n] = epi(sum_k X[v][k] W'[k][n]) as
+// v_mfma_f32_16x16x32_bf16 over 16-voxel m-tiles.  The A fragment of lane (row, kb) is the 16
+// contiguous bytes of voxel row v0 + row at channel 32 ks + 8 kb, loaded straight from HBM
+// (channels-last rows, prologue applied in registers); W' (forward: W[n][k], backward-data:
+// W[k][n]) lives in LDS as packed B fragments.  Operands are bf16, as the reference's autocast
+// 1x1 convs run in fp16 (the VALU kernels above keep the weights fp32).
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct MmArgs {
+    int64_t nvox;
+    int Ca, Cb, K, N, KS;  // row channels (x | x2, or g), reduction length, outputs, 32-wide k-steps
+};
+
+template <int NTN, bool DG>
+__global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const bf16_t *__restrict__ in,
+                                               const bf16_t *__restrict__ in2, const float *__restrict__ w,
+                                               FwdEpi<bf16_t> fe, BwdEpi<bf16_t> be, const float *__restrict__ gscale,
+                                               bf16_t *__restrict__ out, bf16_t *__restrict__ out2, float *dpre,
+                                               float *dpost, float *part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    u32x4 *wB = reinterpret_cast<u32x4 *>(smem);  // [KS][NTN][64]: this workgroup's NTN n-tiles
+    __shared__ float red[8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
+    const int Ct = ca.Cin + ca.Cin2, nt0 = int(blockIdx.y) * NTN;
+    for (int i = tid; i < m.KS * NTN * 64; i += 256) {
+        const int l = i & 63, t = (i >> 6) % NTN, ks = i / (64 * NTN);
+        const int n = 16 * (nt0 + t) + (l & 15), k0 = 32 * ks + 8 * (l >> 4);
+        uint32_t q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float f2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = k0 + 2 * j + h;
+                f2[h] = (k < m.K && n < m.N) ? (DG ? w[int64_t(k) * Ct + n] : w[int64_t(n) * Ct + k]) : 0.f;
+            }
+            q[j] = uint32_t(f2bf(f2[0])) | (uint32_t(f2bf(f2[1])) << 16);
+        }
+        wB[i] = u32x4{q[0], q[1], q[2], q[3]};
+    }
+    __syncthreads();
+    const Prologue pro = make_prologue(DG ? VQ3D_PRO_NONE : ca.pro_kind, ca.pro_a, ca.pro_b);
+    const bool raw = DG || pro.kind == VQ3D_PRO_NONE;
+    const ActDeriv dv = make_deriv(be);
+    const float gs = gscale ? *gscale : 1.f;
+    const float sc = fe.scale ? *fe.scale : 1.f, bi = fe.bias ? *fe.bias : 0.f;
+    const float aa = fe.act_a ? *fe.act_a : 0.f, ab = fe.act_b ? *fe.act_b : 0.f;
+    float pre = 0.f, post = 0.f;
+    const int64_t ntile = (m.nvox + 15) / 16;
+    for (int64_t mt = int64_t(blockIdx.x) * 4 + wave; mt < ntile; mt += int64_t(gridDim.x) * 4) {
+        const int64_t v0 = mt * 16, vr = min(v0 + row, m.nvox - 1);
+        u32x4 av[8];  // every A fragment of the tile in flight together
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            av[ks] = u32x4{0u, 0u, 0u, 0u};
+            const int k0 = 32 * ks + 8 * kb;
+            if (ks < m.KS && k0 < m.K)
+                av[ks] = k0 < m.Ca ? *reinterpret_cast<const u32x4 *>(in + vr * m.Ca + k0)
+                                   : *reinterpret_cast<const u32x4 *>(in2 + vr * m.Cb + (k0 - m.Ca));
+        }
+        f32x4 acc[NTN];
+#pragma unroll
+        for (int t = 0; t < NTN; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            if (ks >= m.KS) break;
+            u32x4 a = av[ks];
+            if (!raw && 32 * ks + 8 * kb < m.K) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    a[j] = uint32_t(f2bf(pro.apply(__uint_as_float(a[j] << 16)))) |
+                           (uint32_t(f2bf(pro.apply(__uint_as_float(a[j] & 0xffff0000u)))) << 16);
+            }
+            const bf16x8 af = __builtin_bit_cast(bf16x8, a);
+#pragma unroll
+            for (int t = 0; t < NTN; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, wB[(ks * NTN + t) * 64 + lane]),
+                                                                 acc[t], 0, 0, 0);
+        }
+        // D[voxel 4 kb + j][column row] of n-tile t
+#pragma unroll
+        for (int t = 0; t < NTN; ++t) {
+            const int n = 16 * (nt0 + t) + row;
+            if (n >= m.N) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t v = v0 + 4 * kb + j;
+                if (v >= m.nvox) continue;
+                float val = acc[t][j];
+                if constexpr (!DG) {
+                    if (fe.scale) val = val * sc;
+                    if (fe.bias) val = val + bi;
+                    if (fe.cbias) val = val + fe.cbias[n];
+                    if (fe.res) val = val + ld(fe.res + v * m.N + n);
+                    st(out + v * m.N + n, epi_act(fe.act, val, aa, ab));
+                } else {
+                    if (gscale) val = val * gs;
+                    if (n < ca.Cin) {
+                        const int64_t o = v * ca.Cin + n;
+                        pre += val;
+                        if (dv.mode) val = val * dv(ld(be.aux + o));
+                        post += val;
+                        if (be.addend) val = val + ld(be.addend + o);
+                        st(out + o, val);
+                    } else {
+                        st(out2 + v * ca.Cin2 + (n - ca.Cin), val);
+                    }
+                }
+            }
+        }
+    }
+    if (DG && (dpre || dpost)) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (tid == 0) {
+            const int nb = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+            if (part) {
+                part[bid] = pre;
+                part[nb + bid] = post;
+            } else {
+                if (dpre) atomicAdd(dpre, pre);
+                if (dpost) atomicAdd(dpost, post);
+            }
+        }
+    }
+}
+}  // namespace
+
+// the matrix-core path, or false when the conv is not one of its shapes
+static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w,
+                          const float *pa, const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be,
+                          const float *gscale, void *out, void *out2, float *dpre, float *dpost, void *ws,
+                          size_t ws_bytes, hipStream_t s) {
+    const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    MmArgs m;
+    m.nvox = nvox;
+    m.Ca = dgrad ? d->cout : d->cin;
+    m.Cb = dgrad ? 0 : d->cin2;
+    m.K = m.Ca + m.Cb;
+    m.N = dgrad ? d->cin + d->cin2 : d->cout;
+    m.KS = (m.K + 31) / 32;
+    auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (m.K < 16 || m.K > 256 || m.N < 8 || m.N > 128 || m.Ca % 8 || m.Cb % 8 || nvox < 128 || nvox > (int64_t(1) << 20))
+        return false;
+    if (fe.res_up2 || !al(in) || !al(in2)) return false;
+    // n-tiles per workgroup: all of them, halved while the grid has fewer than 512 workgroups
+    // (small grids: the weight staging then splits over the second grid dimension)
+    const int ntn = (m.N + 15) / 16;
+    int NTN = ntn <= 1 ? 1 : ntn <= 2 ? 2 : ntn <= 4 ? 4 : 8;
+    const int64_t ntile = (nvox + 15) / 16, nbx0 = (ntile + 3) / 4;
+    while (NTN > 1 && nbx0 * ((ntn + NTN - 1) / NTN) < 512) NTN /= 2;
+    const int ny = (ntn + NTN - 1) / NTN;
+    const size_t lds = size_t(m.KS) * NTN * 64 * 16;
+    const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nbx0, 1024 / ny)));
+    const dim3 nb{nbx, unsigned(ny), 1u};
+    const bool want_part = dgrad && (dpre || dpost);
+    float *part = (want_part && ws && ws_bytes >= size_t(2) * nbx * ny * 4) ? static_cast<float *>(ws) : nullptr;
+    ConvArgs ca = make_args(d, pa, pb);
+#define MM(NT_)                                                                                                 \
+    if (dgrad)                                                                                                  \
+        k_pw_mma<NT_, true><<<nb, 256, lds, s>>>(m, ca, (const bf16_t *)in, nullptr, w, fe, be, gscale,         \
+                                                 (bf16_t *)out, (bf16_t *)out2, dpre, dpost, part);             \
+    else                                                                                                        \
+        k_pw_mma<NT_, false><<<nb, 256, lds, s>>>(m, ca, (const bf16_t *)in, (const bf16_t *)in2, w, fe, be,    \
+                                                  nullptr, (bf16_t *)out, nullptr, nullptr, nullptr, nullptr);
+    switch (NTN) {
+    case 1: MM(1) break;
+    case 2: MM(2) break;
+    case 4: MM(4) break;
+    default: MM(8) break;
+    }
+#undef MM
+    if (part) k_sum_partials<<<1, 256, 0, s>>>(part, int(nbx) * ny, dpre, dpost);
+    return true;
+}
+
 size_t pw_dgrad_workspace(const vq3d_conv_desc *) { return size_t(2) * kMaxPwBlocks * sizeof(float); }
 
 template <typename T>
@@ -661,6 +842,11 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     fe.oD = d->out_d;
     auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool want_part = dgrad && (dpre || dpost);
+    // ---- 8 .. 256 channels on the mid grids: matrix cores
+    if constexpr (std::is_same<T, bf16_t>::value) {
+        if (launch_pw_mma(d, dgrad, in, in2, w, pa, pb, fe, be, gscale, out, out2, dpre, dpost, ws, ws_bytes, s))
+            return check_launch(dgrad ? "conv3d_bwd_data(pointwise mma)" : "conv3d_fwd(pointwise mma)");
+    }
     // ---- mid-size grids: scalar-cache weights, one thread per (voxel, output group)
     if (nvox <= 65536)
         return launch_pw_sg<T>(d, dgrad, in, in2, w, pa, pb, fe, be, gscale, out, out2, dpre, dpost, ws, ws_bytes, s);

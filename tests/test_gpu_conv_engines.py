@@ -251,3 +251,58 @@ def test_pointwise_wgrad_vs_torch(gpu, case, dt):
     assert abs(float(dbias) - float(gy.double().sum())) <= tol * float(gy.abs().sum()) + 1e-4
     ref_s = float((wt.view(cout, -1).double() * G).sum())
     assert abs(float(dscale) - ref_s) <= tol * float((wt.view(cout, -1).double() * G).abs().sum()) + 1e-4
+
+
+PW_MMA_CASES = [
+    # (batch, cin, cin2, cout, (h, w, d)): the up / down blocks' 1x1 convs on the mid grids, a
+    # concatenated second input, a ragged voxel count, K < 32, 9 outputs, the largest K / N
+    (1, 16, 0, 8, (64, 64, 32)),
+    (1, 32, 0, 16, (32, 32, 16)),
+    (2, 128, 0, 64, (8, 8, 4)),
+    (1, 8, 0, 16, (32, 32, 32)),
+    (1, 8, 8, 16, (16, 16, 8)),
+    (2, 16, 0, 8, (5, 5, 5)),
+    (1, 24, 0, 9, (8, 8, 8)),
+    (1, 128, 128, 128, (8, 8, 4)),
+    (2, 64, 32, 40, (8, 8, 8)),
+]
+
+
+@pytest.mark.parametrize("case", PW_MMA_CASES)
+def test_pointwise_mma_matches_valu(gpu, case):
+    """bf16 matrix-core 1x1 conv (k_pw_mma: bf16 operands, fp32 accumulation) vs the fp32 pointwise
+    engine: forward with the ELU prologue and every epilogue term, backward-data with gscale, the
+    prologue derivative, the addend, the split output and the prologue-scalar sums."""
+    from vq3d import ops
+    bt, cin, cin2, cout, (h, w, d) = case
+    g = torch.Generator(device=gpu).manual_seed(7 + cin + cout + h)
+    geom = ops.ConvGeom(1, 1, 0, False)
+    x = rnd((bt, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    x2 = rnd((bt, cin2, h, w, d), gpu, g).contiguous(memory_format=CL) if cin2 else None
+    wt = rnd((cout, cin + cin2, 1, 1, 1), gpu, g, 0.3)
+    a, b = rnd((1,), gpu, g, 0.1), rnd((1,), gpu, g, 0.1)
+    sc, bi = rnd((1,), gpu, g), rnd((1,), gpu, g)
+    cb = rnd((cout,), gpu, g)
+    res = rnd((bt, cout, h, w, d), gpu, g).contiguous(memory_format=CL)
+    bf = lambda t: None if t is None else t.bfloat16()
+    ref = ops.conv_fwd(x, wt, geom, pro=(a, b), x2=x2, scale=sc, bias=bi, cbias=cb, residual=res, act=(b, a))
+    out = ops.conv_fwd(bf(x), wt, geom, pro=(a, b), x2=bf(x2), scale=sc, bias=bi, cbias=cb, residual=bf(res),
+                       act=(b, a))
+    assert torch.isfinite(out.float()).all()
+    assert rel(out.float(), ref) < 1.5e-2, ("fwd", case, rel(out.float(), ref))
+    gy = rnd((bt, cout, h, w, d), gpu, g).contiguous(memory_format=CL)
+    add = rnd((bt, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    gscale = rnd((1,), gpu, g)
+    res_ = []
+    for cast in (lambda t: t, bf):
+        pre, post = torch.zeros(1, device=gpu), torch.zeros(1, device=gpu)
+        gx, gx2 = ops.conv_bwd(cast(gy), cast(x), wt, geom, pro=(a, b), x2=cast(x2), gscale=gscale, aux=cast(x),
+                               addend=cast(add), dpro_pre=pre, dpro_post=post)
+        res_.append((gx, gx2, pre, post))
+    (gr, gr2, pre_r, post_r), (gm, gm2, pre_m, post_m) = res_
+    assert rel(gm.float(), gr) < 1.5e-2, ("dgrad", case, rel(gm.float(), gr))
+    if cin2:
+        assert rel(gm2.float(), gr2) < 1.5e-2, ("dgrad x2", case, rel(gm2.float(), gr2))
+    tol = 2e-2 * float((gr - add).abs().max()) * gr.numel() ** 0.5 + 1e-3
+    assert abs(float(pre_m) - float(pre_r)) <= tol
+    assert abs(float(post_m) - float(post_r)) <= tol
