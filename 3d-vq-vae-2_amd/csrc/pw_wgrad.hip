@@ -349,6 +349,294 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
     }
 }
 
+// ---- matrix cores (bf16): G^T = g^T x' over voxel chunks, v_mfma_f32_16x16x32_bf16 with
+// M = output channels (co tiles), N = input channels + the constant-1 column (ci tiles), K = voxels.
+// A chunk of VC voxels of x (prologue applied, rounded to bf16 as the reference's autocast conv
+// input), x2 and g is staged channels-last in LDS with 16-byte loads (any channel count: a slab of
+// VC voxels is contiguous); both operands come through the transposing ds_read_b64_tr_b16.  Waves
+// split the co tiles (nwm of them) and the chunk's K-steps (4 / nwm); per-workgroup partials are
+// combined over the K-split waves in a fixed order and written like k_pw_wgrad's.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ bf16x8 tr8(const bf16_t *p0, const bf16_t *p1) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+struct WmArgs {
+    int64_t nvox;
+    int Ca, Cb, N, Ct;
+    int VC;             // voxels per chunk (multiple of 32 x K-split)
+    int XP, GP;         // LDS row pitches (elements)
+    int MT, NT;         // co tiles, ci tiles (Ct + 1 columns)
+    int nwm;            // waves over co tiles (1, 2, 4); 4 / nwm waves split the K-steps
+    int ua, ub, ug;     // 16-byte units per chunk of x, x2, g
+    int tr;             // partials workgroup-major part[blk][entry] (many entries, few workgroups)
+};
+
+constexpr int kWmU = 4;  // 16-byte units in flight per thread
+
+template <int MPW, int NTT>
+__global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__restrict__ x,
+                                                     const bf16_t *__restrict__ x2, const bf16_t *__restrict__ g,
+                                                     int pro_kind, const float *pro_a, const float *pro_b,
+                                                     float *__restrict__ part, WgOut out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ float red[8];
+    bf16_t *xs = reinterpret_cast<bf16_t *>(smem);  // [VC][XP]
+    bf16_t *gs = xs + a.VC * a.XP;                  // [VC][GP]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+    const int wm = wave % a.nwm, wk = wave / a.nwm, nwk = 4 / a.nwm;
+    const Prologue pro = make_prologue(pro_kind, pro_a, pro_b);
+    const bool raw = pro.kind == VQ3D_PRO_NONE;
+    // columns staging never writes: the constant-1 column of x and the zero padding
+    for (int v = tid; v < a.VC; v += 256) {
+        for (int c = a.Ct; c < a.XP; ++c) xs[v * a.XP + c] = c == a.Ct ? bf16_t(0x3f80) : bf16_t(0);
+        for (int c = a.N; c < a.GP; ++c) gs[v * a.GP + c] = 0;
+    }
+
+    f32x4 acc[MPW][NTT];
+#pragma unroll
+    for (int i = 0; i < MPW; ++i)
+#pragma unroll
+        for (int t = 0; t < NTT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nu = a.ua + a.ub + a.ug;
+    const int64_t nch = (a.nvox + a.VC - 1) / a.VC;
+    // this thread's 16-byte units of a chunk (nu <= kWmU * 256: one round), held in registers so
+    // the next chunk's loads are in flight while the current one is multiplied
+    u32x4 r[kWmU];
+    auto load = [&](int64_t ch) {
+        const int64_t v0 = ch * a.VC;
+        const int nv = int(min<int64_t>(a.VC, a.nvox - v0));
+#pragma unroll
+        for (int k = 0; k < kWmU; ++k) {
+            const int u = tid + k * 256;
+            r[k] = u32x4{0u, 0u, 0u, 0u};
+            if (u >= nu) continue;
+            const bf16_t *src;
+            int e, C;
+            if (u < a.ua) src = x + v0 * a.Ca, e = 8 * u, C = a.Ca;
+            else if (u < a.ua + a.ub) src = x2 + v0 * a.Cb, e = 8 * (u - a.ua), C = a.Cb;
+            else src = g + v0 * a.N, e = 8 * (u - a.ua - a.ub), C = a.N;
+            const int lim = nv * C;
+            if (e + 8 <= lim) {
+                r[k] = *reinterpret_cast<const u32x4 *>(src + e);
+            } else {
+                uint32_t t[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (e + j < lim) t[j >> 1] |= uint32_t(src[e + j]) << (16 * (j & 1));
+                r[k] = u32x4{t[0], t[1], t[2], t[3]};
+            }
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int k = 0; k < kWmU; ++k) {
+            const int u = tid + k * 256;
+            if (u >= nu) continue;
+            bf16_t *dst;
+            int e, C, off, P;
+            bool isx = true;
+            if (u < a.ua) e = 8 * u, C = a.Ca, off = 0, P = a.XP, dst = xs;
+            else if (u < a.ua + a.ub) e = 8 * (u - a.ua), C = a.Cb, off = a.Ca, P = a.XP, dst = xs;
+            else e = 8 * (u - a.ua - a.ub), C = a.N, off = 0, P = a.GP, dst = gs, isx = false;
+            u32x4 w = r[k];
+            if (isx && !raw)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float lo = pro.apply(__uint_as_float(w[j] << 16));
+                    const float hi = pro.apply(__uint_as_float(w[j] & 0xffff0000u));
+                    w[j] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+                }
+            if (C % 8 == 0) {  // the unit is 8 channels of one voxel
+                const int v = e / C, c = e - v * C;
+                u32x2 *d2 = reinterpret_cast<u32x2 *>(dst + v * P + off + c);
+                d2[0] = u32x2{w[0], w[1]};
+                d2[1] = u32x2{w[2], w[3]};
+            } else {
+                int v = e / C, c = e - v * C;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (v < a.VC) dst[v * P + off + c] = bf16_t(w[j >> 1] >> (16 * (j & 1)));
+                    if (++c == C) c = 0, ++v;
+                }
+            }
+        }
+    };
+    if (int64_t(blockIdx.x) < nch) load(blockIdx.x);
+    for (int64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+        const int nv = int(min<int64_t>(a.VC, a.nvox - ch * a.VC));
+        __syncthreads();
+        store();
+        if (ch + gridDim.x < nch) load(ch + gridDim.x);
+        // a ragged last chunk: rows past the grid are zero (the prologue of a zero is not)
+        if (nv < a.VC) {
+            for (int e = tid; e < (a.VC - nv) * a.Ct; e += 256) xs[(nv + e / a.Ct) * a.XP + e % a.Ct] = 0;
+            for (int e = tid; e < (a.VC - nv) * a.N; e += 256) gs[(nv + e / a.N) * a.GP + e % a.N] = 0;
+        }
+        __syncthreads();
+        for (int ks = wk; ks < a.VC / 32; ks += nwk) {
+            const int r0 = ks * 32 + 8 * grp + q;
+            const bf16_t *ga = gs + r0 * a.GP + 4 * p4;
+            const bf16_t *xa = xs + r0 * a.XP + 4 * p4;
+            bf16x8 bfr[NTT];
+#pragma unroll
+            for (int t = 0; t < NTT; ++t)
+                if (t < a.NT) bfr[t] = tr8(xa + 16 * t, xa + 16 * t + 4 * a.XP);
+#pragma unroll
+            for (int i = 0; i < MPW; ++i) {
+                const int mt = wm + a.nwm * i;
+                if (mt >= a.MT) break;
+                const bf16x8 af = tr8(ga + 16 * mt, ga + 16 * mt + 4 * a.GP);
+#pragma unroll
+                for (int t = 0; t < NTT; ++t)
+                    if (t < a.NT) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[t], acc[i][t], 0, 0, 0);
+            }
+        }
+    }
+    // K-split waves: fixed-order sum through an LDS image [MT * 16][NT * 16]; then one pass writes
+    // the partials (D[co = 16 mt + 4 grp + j][ci = 16 t + li])
+    const int nblk = gridDim.x, W = a.NT * 16;
+    float *img = reinterpret_cast<float *>(smem);
+    float wg = 0.f, bs = 0.f;
+    auto emit = [&](int co, int ci, float sum) {
+        if (co >= a.N || ci > a.Ct) return;
+        const int e = co * (a.Ct + 1) + ci;
+        if (part) part[a.tr ? int64_t(blockIdx.x) * a.N * (a.Ct + 1) + e : int64_t(e) * nblk + blockIdx.x] = sum;
+        else finish_entry(out, e, a.Ct, sum, wg, bs);
+    };
+    if (nwk == 1) {
+#pragma unroll
+        for (int i = 0; i < MPW; ++i) {
+            const int mt = wm + a.nwm * i;
+            if (mt >= a.MT) break;
+#pragma unroll
+            for (int t = 0; t < NTT; ++t)
+                if (t < a.NT)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) emit(16 * mt + 4 * grp + j, 16 * t + li, acc[i][t][j]);
+        }
+    } else {
+        for (int k = 0; k < nwk; ++k) {
+            __syncthreads();
+            if (wk == k) {
+#pragma unroll
+                for (int i = 0; i < MPW; ++i) {
+                    const int mt = wm + a.nwm * i;
+                    if (mt >= a.MT) break;
+#pragma unroll
+                    for (int t = 0; t < NTT; ++t)
+                        if (t < a.NT)
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                float &d = img[(16 * mt + 4 * grp + j) * W + 16 * t + li];
+                                d = k == 0 ? acc[i][t][j] : d + acc[i][t][j];
+                            }
+                }
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < a.MT * 16 * W; e += 256) emit(e / W, e % W, img[e]);
+    }
+    if (!part) finish_block(out, wg, bs, red);
+}
+
+// the plan of the matrix-core path, or false (fp32, > 16 accumulator tiles per wave, tiny grids)
+bool plan_mma(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, WmArgs &m, int &mpw, int &ntt,
+              int &nbx, size_t &lds) {
+    auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (d->dtype != VQ3D_BF16 || !al(x) || !al(x2) || !al(g)) return false;
+    m = WmArgs{};
+    m.nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    m.Ca = d->cin;
+    m.Cb = d->cin2;
+    m.N = d->cout;
+    m.Ct = m.Ca + m.Cb;
+    if (m.nvox < 256 || m.Ct > 255 || m.N > 128) return false;
+    m.MT = (m.N + 15) / 16;
+    m.NT = (m.Ct + 1 + 15) / 16;
+    ntt = m.NT <= 1 ? 1 : m.NT <= 2 ? 2 : m.NT <= 4 ? 4 : m.NT <= 8 ? 8 : 16;
+    m.nwm = m.MT >= 4 ? 4 : m.MT >= 2 ? 2 : 1;
+    if (m.MT == 3) m.nwm = 4;
+    mpw = (m.MT + m.nwm - 1) / m.nwm;
+    if (mpw > 2 || mpw * ntt > 16) return false;
+    if (mpw == 2 && ntt > 8) return false;
+    m.XP = m.NT * 16 + 4;
+    m.GP = m.MT * 16 + 4;
+    const int nwk = 4 / m.nwm;
+    // chunk: one round of kWmU 16-byte units per thread, at least one K-step per K-split wave,
+    // at most 256 voxels
+    m.VC = 256;
+    while (m.VC > 32 * nwk && m.VC * (m.Ct + m.N) > kWmU * 256 * 8) m.VC /= 2;
+    if (m.VC * (m.Ct + m.N) > kWmU * 256 * 8 || size_t(m.VC) * (m.XP + m.GP) * 2 > 48 * 1024) return false;
+    m.ua = m.VC * m.Ca / 8;
+    m.ub = m.VC * m.Cb / 8;
+    m.ug = m.VC * m.N / 8;
+    if ((m.VC * m.Ca) % 8 || (m.VC * m.Cb) % 8 || (m.VC * m.N) % 8) return false;
+    lds = std::max(size_t(m.VC) * (m.XP + m.GP) * 2, nwk > 1 ? size_t(m.MT) * 16 * m.NT * 16 * 4 : size_t(0));
+    // workgroups: enough chunks in flight, partial traffic (ne floats per workgroup) << the data
+    const int64_t nch = (m.nvox + m.VC - 1) / m.VC;
+    const int64_t ne = int64_t(m.N) * (m.Ct + 1);
+    const int64_t data = m.nvox * (m.Ct + m.N) * 2;
+    // workgroups: a chunk each on small grids (the chunk loop is load-latency bound), about 4 chunks
+    // each on large ones (1024 .. 2048 workgroups; fewer partials)
+    (void)data;
+    (void)ne;
+    nbx = int(nch <= 1024 ? nch : std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1024, nch / 4)));
+    // entry-major partials cost a scattered store per entry and workgroup
+    m.tr = ne >= 64 * int64_t(nbx);
+    return true;
+}
+
+// k_pw_wgrad_reduce for workgroup-major partials part[blk][entry]: a workgroup takes 64 entries,
+// wave w sums blocks w, w + 4, ... (8 loads in flight, coalesced over the entries), the 4 wave sums
+// are added in a fixed order
+__global__ __launch_bounds__(256) void k_pw_wgrad_reduce_t(const float *__restrict__ part, int nblk, int ne, int Ct,
+                                                          const float *__restrict__ w, const float *__restrict__ escale,
+                                                          float *dw, float *dscale, float *dbias, float *dcbias) {
+    __shared__ float red[8];
+    __shared__ float ws4[4][64];
+    const int el = threadIdx.x & 63, bg = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + el;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (e < ne)
+        for (int b0 = bg; b0 < nblk; b0 += 32) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + 4 * u < nblk) acc[u] += part[int64_t(b0 + 4 * u) * ne + e];
+        }
+    ws4[bg][el] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    float wg = 0.f, bs = 0.f;
+    if (bg == 0 && e < ne) {
+        const float sum = (ws4[0][el] + ws4[1][el]) + (ws4[2][el] + ws4[3][el]);
+        const int co = e / (Ct + 1), ci = e - co * (Ct + 1);
+        if (ci < Ct) {
+            const int64_t o = int64_t(co) * Ct + ci;
+            if (dw) dw[o] += escale ? sum * *escale : sum;
+            if (dscale) wg = w[o] * sum;
+        } else {
+            if (dcbias) dcbias[co] += sum;
+            bs = sum;
+        }
+    }
+    if (dscale) {
+        wg = block_sum<float, 256>(wg, red);
+        if (threadIdx.x == 0) atomicAdd(dscale, wg);
+    }
+    if (dbias) {
+        bs = block_sum<float, 256>(bs, red + 4);
+        if (threadIdx.x == 0) atomicAdd(dbias, bs);
+    }
+}
+
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 bool reg_path(const vq3d_conv_desc *d) {
@@ -397,7 +685,12 @@ size_t pw_wgrad_workspace(const vq3d_conv_desc *d) {
     int ytiles, nbx;
     size_t lds;
     const PwwArgs a = plan(d, ytiles, nbx, lds);
-    return size_t(nbx) * a.ne * 4;
+    size_t bytes = size_t(nbx) * a.ne * 4;
+    WmArgs m;
+    int mpw, ntt;
+    if (d->dtype == VQ3D_BF16 && plan_mma(d, nullptr, nullptr, nullptr, m, mpw, ntt, nbx, lds))
+        bytes = std::max(bytes, size_t(nbx) * m.N * (m.Ct + 1) * 4);
+    return bytes;
 }
 
 int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
@@ -409,12 +702,31 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     if (!workspace || ws_bytes < size_t(nbx) * a.ne * 4) return fail("conv3d_bwd_weight: workspace too small");
     auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     a.vec = al(x) && al(g) && (!x2 || al(x2));
-    // few workgroups: each adds its partial straight into the gradients (no reduce launch)
-    const bool direct = nbx <= 16;
-    float *part = direct ? nullptr : static_cast<float *>(workspace);
     const WgOut out{w, escale, dw, dscale, dbias, dcbias};
     const dim3 grid{unsigned(nbx), unsigned(ytiles), 1u};
-    if (reg_path(d) && a.vec) {
+    WmArgs m;
+    int mpw, ntt, mbx;
+    size_t mlds;
+    const bool mma = !(reg_path(d) && a.vec) && plan_mma(d, x, x2, g, m, mpw, ntt, mbx, mlds) &&
+                     size_t(mbx) * m.N * (m.Ct + 1) * 4 <= ws_bytes;
+    if (mma) {
+        nbx = mbx;
+        a.ne = m.N * (m.Ct + 1);
+    }
+    // few workgroups: each adds its partial straight into the gradients (no reduce launch; the
+    // matrix-core kernel's partials are whole co x ci images, so only a single workgroup goes direct)
+    const bool direct = mma ? nbx == 1 : nbx <= 16;
+    float *part = direct ? nullptr : static_cast<float *>(workspace);
+    if (mma) {
+#define WM(M_, N_)                                                                                              \
+    else if (mpw == M_ && ntt == N_) k_pw_wgrad_mma<M_, N_><<<nbx, 256, mlds, s>>>(                            \
+        m, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g, d->pro_kind, pro_a, pro_b, part, out);
+        if (false) {
+        }
+        WM(1, 1) WM(1, 2) WM(1, 4) WM(1, 8) WM(1, 16) WM(2, 1) WM(2, 2) WM(2, 4) WM(2, 8)
+        else return fail("conv3d_bwd_weight: no matrix-core instance");
+#undef WM
+    } else if (reg_path(d) && a.vec) {
         const int key = d->cin * 16 + d->cout;
         const bool bf = d->dtype == VQ3D_BF16;
 #define REG(CX, CG)                                                                                            \
@@ -440,9 +752,13 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
                                                   d->pro_kind, pro_a, pro_b, part, out);
     if (direct) return check_launch("conv3d_bwd_weight(pointwise)");
     const int Ct = a.Ca + a.Cb;
+    if (mma && m.tr) {
+        k_pw_wgrad_reduce_t<<<(a.ne + 63) / 64, 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw, dscale, dbias, dcbias);
+        return check_launch("conv3d_bwd_weight(pointwise)");
+    }
     int lanes = 1;
-    while (lanes < 64 && lanes * 32 < nbx) lanes *= 2;
-    if (lanes == 64 && nbx > 1024) lanes = 256;  // a workgroup per entry: one round of 8 loads per thread
+    while (lanes < 64 && lanes * 8 < nbx) lanes *= 2;
+    if (lanes == 64 && nbx > 512) lanes = 256;  // a workgroup per entry: one round of loads per thread
 #define RED(L)                                                                                                 \
     k_pw_wgrad_reduce<L><<<(a.ne + 256 / L - 1) / (256 / L), 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw,    \
                                                                           dscale, dbias, dcbias)

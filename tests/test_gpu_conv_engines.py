@@ -222,6 +222,19 @@ PW_CASES = [
     (64, 8, 72, (4, 4, 2)),
     (256, 0, 32, (4, 4, 2)),
     (72, 0, 36, (8, 8, 8)),
+    # bf16 matrix-core path (k_pw_wgrad_mma): the step's shapes, odd channel counts (slab-staged),
+    # a concatenated second input, ragged voxel counts, 255 + 1 columns, 8 co tiles
+    (16, 0, 8, (64, 64, 32)),
+    (32, 0, 16, (32, 32, 16)),
+    (128, 0, 64, (16, 16, 4)),
+    (64, 0, 128, (16, 16, 4)),
+    (9, 0, 8, (32, 32, 16)),
+    (18, 0, 18, (16, 16, 8)),
+    (8, 8, 16, (16, 16, 8)),
+    (16, 0, 8, (7, 9, 5)),
+    (3, 5, 7, (9, 9, 9)),
+    (255, 0, 16, (8, 8, 4)),
+    (32, 0, 48, (8, 8, 8)),
 ]
 
 
