@@ -596,12 +596,19 @@ template <bool T>
 __device__ __forceinline__ f32x4 conv_half(const Mk &m, const bf16_t *src, int mt, int ks0, int lane) {
     const int row = lane & 15, kb = lane >> 4, v = mt * 16 + row;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int ks = ks0; ks < ks0 + 7; ++ks) {
-        const int tap = 2 * ks + (kb >> 1), c0 = 8 * (kb & 1);
-        const bf16x8 af = tap < 27 ? rd8(src + int(m.nb[v * 27 + (T ? 26 - tap : tap)]) * PT + c0) : zero8();
-        acc = mfma(af, frag(m.fr + FR_B, ks, lane), acc);
+    // all 7 neighbour indices, then all 7 operand rows, then the MFMAs: one LDS round trip per
+    // stage instead of two per k-step on the chain's critical path
+    int nbi[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const int tap = 2 * (ks0 + k) + (kb >> 1);
+        nbi[k] = tap < 27 ? int(m.nb[v * 27 + (T ? 26 - tap : tap)]) : -1;
     }
+    bf16x8 af[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) af[k] = nbi[k] >= 0 ? rd8(src + nbi[k] * PT + 8 * (kb & 1)) : zero8();
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc = mfma(af[k], frag(m.fr + FR_B, ks0 + k, lane), acc);
     return acc;
 }
 

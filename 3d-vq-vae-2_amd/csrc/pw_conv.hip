@@ -340,7 +340,8 @@ template <typename T, int CI, int CO, bool DGRAD>
 __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restrict__ in, const float *__restrict__ w,
                                                 int pro_kind, const float *pro_a, const float *pro_b,
                                                 FwdEpi<T> fe, BwdEpi<T> be, const float *__restrict__ gscale,
-                                                T *__restrict__ out, float *dpre, float *dpost, float *part) {
+                                                T *__restrict__ out, float *dpre, float *dpost, float *part,
+                                                FastDiv fD, FastDiv fW, FastDiv fH) {
     __shared__ float wsh[CO * CI];
     __shared__ float red[8];
     const int Ct = DGRAD ? CO : CI;
@@ -373,12 +374,11 @@ __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restri
                 if (!DGRAD && fe.res && fe.res_up2) {
                     // the half-grid residual upsampled x2 (trilinear, align_corners=False) on the
                     // fly: 8 neighbour rows of CO channels, the k_pw2 / k_up2_fwd weights and order
-                    int t = int(v);
-                    const int od = t % fe.oD;
-                    t /= fe.oD;
-                    const int ow = t % fe.oW;
-                    t /= fe.oW;
-                    const int oh = t % fe.oH, b = t / fe.oH;
+                    // voxel coordinates by magic-number division (three integer divisions per
+                    // voxel were the kernel's largest VALU cost)
+                    const uint32_t t0 = uint32_t(v), t1 = fD.div(t0), t2 = fW.div(t1), b = fH.div(t2);
+                    const int od = int(t0 - t1 * uint32_t(fe.oD)), ow = int(t1 - t2 * uint32_t(fe.oW));
+                    const int oh = int(t2 - b * uint32_t(fe.oH));
                     const int rH = fe.oH / 2, rW = fe.oW / 2, rD = fe.oD / 2;
                     int h0, h1, w0, w1, d0, d1;
                     float lh, lw, ld_;
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restri
                     const int hs[2] = {h0, h1}, wsx[2] = {w0, w1}, dsx[2] = {d0, d1};
 #pragma unroll
                     for (int q = 0; q < 8; ++q)
-                        row_ld<T, CO>(fe.res + ((int64_t(b * rH + hs[q >> 2]) * rW + wsx[(q >> 1) & 1]) * rD +
+                        row_ld<T, CO>(fe.res + ((int64_t(int(b) * rH + hs[q >> 2]) * rW + wsx[(q >> 1) & 1]) * rD +
                                                 dsx[q & 1]) * CO, R[q]);
 #pragma unroll
                     for (int o = 0; o < CO; ++o)
@@ -661,6 +661,30 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// 4 consecutive bf16 (8-byte aligned when `vec`) <-> fp32; `cnt` of them valid
+__device__ __forceinline__ void ld4(const bf16_t *p, bool vec, int cnt, float (&o)[4]) {
+    if (vec) {
+        const u32x2 u = *reinterpret_cast<const u32x2 *>(p);
+        o[0] = __uint_as_float(u[0] << 16);
+        o[1] = __uint_as_float(u[0] & 0xffff0000u);
+        o[2] = __uint_as_float(u[1] << 16);
+        o[3] = __uint_as_float(u[1] & 0xffff0000u);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = j < cnt ? ld(p + j) : 0.f;
+    }
+}
+__device__ __forceinline__ void st4(bf16_t *p, bool vec, int cnt, const float (&o)[4]) {
+    if (vec) {
+        *reinterpret_cast<u32x2 *>(p) = u32x2{uint32_t(f2bf(o[0])) | (uint32_t(f2bf(o[1])) << 16),
+                                             uint32_t(f2bf(o[2])) | (uint32_t(f2bf(o[3])) << 16)};
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < cnt) st(p + j, o[j]);
+    }
+}
+
 struct MmArgs {
     int64_t nvox;
     int Ca, Cb, K, N, KS;  // row channels (x | x2, or g), reduction length, outputs, 32-wide k-steps
@@ -727,38 +751,75 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const bf1
                            (uint32_t(f2bf(pro.apply(__uint_as_float(a[j] & 0xffff0000u)))) << 16);
             }
             const bf16x8 af = __builtin_bit_cast(bf16x8, a);
+            // D^T[n][v] = W'^T X^T: the weight fragment is the A operand, the voxel rows the B operand,
+            // so a lane ends with 4 consecutive output channels of one voxel (vector epilogue)
 #pragma unroll
             for (int t = 0; t < NTN; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, wB[(ks * NTN + t) * 64 + lane]),
-                                                                 acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wB[(ks * NTN + t) * 64 + lane]),
+                                                                 af, acc[t], 0, 0, 0);
         }
-        // D[voxel 4 kb + j][column row] of n-tile t
+        // D^T[channel 16 t' + 4 kb + j][voxel v0 + row] of n-tile t' = nt0 + t
+        const int64_t v = v0 + row;
+        if (v < m.nvox) {
 #pragma unroll
-        for (int t = 0; t < NTN; ++t) {
-            const int n = 16 * (nt0 + t) + row;
-            if (n >= m.N) continue;
+            for (int t = 0; t < NTN; ++t) {
+                const int n0 = 16 * (nt0 + t) + 4 * kb;
+                if (n0 >= m.N) continue;
+                float val[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t v = v0 + 4 * kb + j;
-                if (v >= m.nvox) continue;
-                float val = acc[t][j];
+                for (int j = 0; j < 4; ++j) val[j] = acc[t][j];
                 if constexpr (!DG) {
-                    if (fe.scale) val = val * sc;
-                    if (fe.bias) val = val + bi;
-                    if (fe.cbias) val = val + fe.cbias[n];
-                    if (fe.res) val = val + ld(fe.res + v * m.N + n);
-                    st(out + v * m.N + n, epi_act(fe.act, val, aa, ab));
+                    const int cnt = min(4, m.N - n0);
+                    const bool vec = cnt == 4 && (m.N & 3) == 0;
+                    float r4[4] = {0.f, 0.f, 0.f, 0.f};
+                    if (fe.res) ld4(fe.res + v * m.N + n0, vec, cnt, r4);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float x = val[j];
+                        if (fe.scale) x = x * sc;
+                        if (fe.bias) x = x + bi;
+                        if (fe.cbias && j < cnt) x = x + fe.cbias[n0 + j];
+                        if (fe.res) x = x + r4[j];
+                        val[j] = epi_act(fe.act, x, aa, ab);
+                    }
+                    st4(out + v * m.N + n0, vec, cnt, val);
                 } else {
-                    if (gscale) val = val * gs;
-                    if (n < ca.Cin) {
-                        const int64_t o = v * ca.Cin + n;
-                        pre += val;
-                        if (dv.mode) val = val * dv(ld(be.aux + o));
-                        post += val;
-                        if (be.addend) val = val + ld(be.addend + o);
-                        st(out + o, val);
+                    if (gscale)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) val[j] = val[j] * gs;
+                    if (n0 + 4 <= ca.Cin) {  // all 4 in gx
+                        const int64_t o = v * ca.Cin + n0;
+                        const bool vec = (ca.Cin & 3) == 0;
+                        float x4[4], d4[4] = {0.f, 0.f, 0.f, 0.f};
+                        if (dv.mode) ld4(be.aux + o, vec, 4, x4);
+                        if (be.addend) ld4(be.addend + o, vec, 4, d4);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            pre += val[j];
+                            if (dv.mode) val[j] = val[j] * dv(x4[j]);
+                            post += val[j];
+                            val[j] += d4[j];
+                        }
+                        st4(out + o, vec, 4, val);
+                    } else if (n0 >= ca.Cin && ((ca.Cin2 | (n0 - ca.Cin)) & 3) == 0) {  // all in gx2
+                        st4(out2 + v * ca.Cin2 + (n0 - ca.Cin), n0 + 4 <= ca.Cin + ca.Cin2, min(4, m.N - n0), val);
                     } else {
-                        st(out2 + v * ca.Cin2 + (n - ca.Cin), val);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int n = n0 + j;
+                            if (n >= m.N) break;
+                            float x = val[j];
+                            if (n < ca.Cin) {
+                                const int64_t o = v * ca.Cin + n;
+                                pre += x;
+                                if (dv.mode) x = x * dv(ld(be.aux + o));
+                                post += x;
+                                if (be.addend) x = x + ld(be.addend + o);
+                                st(out + o, x);
+                            } else {
+                                st(out2 + v * ca.Cin2 + (n - ca.Cin), x);
+                            }
+                        }
                     }
                 }
             }
@@ -795,7 +856,9 @@ static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, c
     m.N = dgrad ? d->cin + d->cin2 : d->cout;
     m.KS = (m.K + 31) / 32;
     auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    if (m.K < 16 || m.K > 256 || m.N < 8 || m.N > 128 || m.Ca % 8 || m.Cb % 8 || nvox < 128 || nvox > (int64_t(1) << 20))
+    // 8 -> 8 on the big grids: the row kernel is faster
+    if (m.K <= 8 && m.N <= 8) return false;
+    if (m.K < 8 || m.K > 256 || m.N < 8 || m.N > 128 || m.Ca % 8 || m.Cb % 8 || nvox < 128 || nvox > (int64_t(1) << 20))
         return false;
     if (fe.res_up2 || !al(in) || !al(in2)) return false;
     // n-tiles per workgroup: all of them, halved while the grid has fewer than 512 workgroups
@@ -857,14 +920,16 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
         float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
         const int key = ci * 16 + co;
         const int pk = dgrad ? VQ3D_PRO_NONE : d->pro_kind;
+        const FastDiv fD(uint32_t(d->out_d)), fW(uint32_t(d->out_w)), fH(uint32_t(d->out_h));
 #define R(CI, CO)                                                                                              \
     case CI * 16 + CO:                                                                                         \
         if (dgrad)                                                                                             \
             k_pw_rows<T, CI, CO, true><<<nbx, 256, 0, s>>>(nvox, (const T *)in, w, pk, pa, pb, fe, be, gscale, \
-                                                           (T *)out, dpre, dpost, part);                       \
+                                                           (T *)out, dpre, dpost, part, fD, fW, fH);           \
         else                                                                                                   \
             k_pw_rows<T, CI, CO, false><<<nbx, 256, 0, s>>>(nvox, (const T *)in, w, pk, pa, pb, fe, be,       \
-                                                            nullptr, (T *)out, nullptr, nullptr, nullptr);     \
+                                                            nullptr, (T *)out, nullptr, nullptr, nullptr, fD,  \
+                                                            fW, fH);                                           \
         break;
         switch (key) {
             R(1, 1) R(1, 2) R(1, 4) R(1, 8) R(2, 1) R(2, 2) R(2, 4) R(2, 8)

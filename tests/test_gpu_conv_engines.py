@@ -319,3 +319,22 @@ def test_pointwise_mma_matches_valu(gpu, case):
     tol = 2e-2 * float((gr - add).abs().max()) * gr.numel() ** 0.5 + 1e-3
     assert abs(float(pre_m) - float(pre_r)) <= tol
     assert abs(float(post_m) - float(post_r)) <= tol
+
+
+@pytest.mark.parametrize("case", [(4, 4, (16, 16, 32)), (2, 8, (8, 8, 8)), (4, 2, (6, 10, 4)), (8, 8, (4, 4, 4))])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pointwise_rows_residual_up2(gpu, case, dt):
+    """Few-channel 1x1 conv with the ResizeConv skip's half-grid residual upsampled x2 on the fly
+    (k_pw_rows; vqvae/layers.py:591-597) vs torch: conv * scale + bias + trilinear(res)."""
+    from vq3d import ops
+    cin, cout, (h, w, d) = case
+    g = torch.Generator(device=gpu).manual_seed(cin * 7 + cout + h)
+    x = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
+    wt = rnd((cout, cin, 1, 1, 1), gpu, g, 0.3)
+    res = rnd((2, cout, h // 2, w // 2, d // 2), gpu, g).contiguous(memory_format=CL)
+    sc, bi = rnd((1,), gpu, g), rnd((1,), gpu, g)
+    ref = (torch.nn.functional.conv3d(x.double(), wt.double()) * sc.double() + bi.double() +
+           torch.nn.functional.interpolate(res.double(), scale_factor=2, mode="trilinear", align_corners=False))
+    out = ops.conv_fwd(x.to(dt), wt, ops.ConvGeom(1), scale=sc, bias=bi, residual=res.to(dt), residual_up2=True)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert rel(out.float(), ref.float()) < tol, rel(out.float(), ref.float())
