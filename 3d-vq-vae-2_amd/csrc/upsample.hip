@@ -193,6 +193,108 @@ __global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ 
     }
 }
 
+// 4 bf16 channels, D % 4 == 0: a thread owns a run of 4 source voxels along D.  Their destination
+// rows 2 i0 - 1 .. 2 i0 + 8 of each (h, w) pair lie in one 96-byte window (destinations
+// 2 i0 - 2 .. 2 i0 + 9, six 16-byte loads; the ends past the grid carry weight 0 and are zero
+// here) instead of 16 separate 8-byte loads.  Same weights, same order of operations as k_up2_bwd,
+// so the same bits.
+__global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const bf16_t *__restrict__ gy, int dmode,
+                                                     const float *dparam, const bf16_t *__restrict__ aux,
+                                                     const bf16_t *__restrict__ addend, bf16_t *__restrict__ gx,
+                                                     float *dpre, float *dpost) {
+    __shared__ float red[8];
+    ActDeriv dv;
+    dv.mode = aux ? dmode : 0;
+    dv.p = (dv.mode && dparam) ? *dparam : 0.f;
+    float pre = 0.f, post = 0.f;
+    const int DQ = a.D / 4;
+    const uint32_t n = uint32_t(a.B) * a.H * a.W * DQ;
+    const int D2 = 2 * a.D, W2 = 2 * a.W, H2 = 2 * a.H;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
+        int ch, q, iw, ih, b;
+        split(a, e, DQ, a.W, a.H, ch, q, iw, ih, b);
+        const int i0 = 4 * q;
+        int jh[4], jw[4], jd[4];
+        float wh[4], ww[4], wd[4][4];
+        adj4(ih, a.H, jh, wh);
+        adj4(iw, a.W, jw, ww);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) adj4(i0 + s4, a.D, jd, wd[s4]);
+        float acc[4][4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[s4][c] = 0.f;
+        // one h row of windows in flight (24 loads; all 96 would cap the occupancy at one wave,
+        // 2 x 6 measured slower)
+#pragma unroll 1
+        for (int x0 = 0; x0 < 4; ++x0)
+#pragma unroll 4
+            for (int x1 = 0; x1 < 4; ++x1) {
+                const float whw = wh[x0] * ww[x1];
+                const int64_t rowb = ((int64_t(b) * H2 + jh[x0]) * W2 + jw[x1]) * D2;
+                // destinations 2 i0 - 2 + k, k = 0 .. 11, 4 channels each
+                float r[12][4];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const int j = 2 * i0 - 2 + 2 * k;
+                    u32x4 u = u32x4{0u, 0u, 0u, 0u};
+                    if (j >= 0 && j < D2) u = *reinterpret_cast<const u32x4 *>(gy + (rowb + j) * 4);
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2) {
+                        r[2 * k + h2][0] = __uint_as_float(u[2 * h2] << 16);
+                        r[2 * k + h2][1] = __uint_as_float(u[2 * h2] & 0xffff0000u);
+                        r[2 * k + h2][2] = __uint_as_float(u[2 * h2 + 1] << 16);
+                        r[2 * k + h2][3] = __uint_as_float(u[2 * h2 + 1] & 0xffff0000u);
+                    }
+                }
+                // source i0 + s4 reads destinations 2 (i0 + s4) - 1 + t = window slot 2 s4 + 1 + t
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float *w4 = wd[s4];
+                        const float sd = w4[0] * r[2 * s4 + 1][c] + w4[1] * r[2 * s4 + 2][c] + w4[2] * r[2 * s4 + 3][c] +
+                                         w4[3] * r[2 * s4 + 4][c];
+                        acc[s4][c] = fmaf(whw, sd, acc[s4][c]);
+                    }
+            }
+        const int64_t o = (((int64_t(b) * a.H + ih) * a.W + iw) * a.D + i0) * 4;
+        u32x4 xa[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}}, ad[2] = {xa[0], xa[1]};
+        if (dv.mode) xa[0] = *reinterpret_cast<const u32x4 *>(aux + o), xa[1] = *reinterpret_cast<const u32x4 *>(aux + o + 8);
+        if (addend) ad[0] = *reinterpret_cast<const u32x4 *>(addend + o), ad[1] = *reinterpret_cast<const u32x4 *>(addend + o + 8);
+        u32x4 res[2];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            float v2[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t wx = xa[s4 >> 1][2 * (s4 & 1) + (c >> 1)], wa = ad[s4 >> 1][2 * (s4 & 1) + (c >> 1)];
+                const float xv = __uint_as_float((c & 1) ? (wx & 0xffff0000u) : (wx << 16));
+                const float av = __uint_as_float((c & 1) ? (wa & 0xffff0000u) : (wa << 16));
+                float v = acc[s4][c];
+                pre += v;
+                if (dv.mode) v *= dv(xv);
+                post += v;
+                if (addend) v += av;
+                v2[c] = v;
+            }
+            res[s4 >> 1][2 * (s4 & 1)] = uint32_t(f2bf(v2[0])) | (uint32_t(f2bf(v2[1])) << 16);
+            res[s4 >> 1][2 * (s4 & 1) + 1] = uint32_t(f2bf(v2[2])) | (uint32_t(f2bf(v2[3])) << 16);
+        }
+        *reinterpret_cast<u32x4 *>(gx + o) = res[0];
+        *reinterpret_cast<u32x4 *>(gx + o + 8) = res[1];
+    }
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------- LDS-tiled (bf16)
 // A workgroup owns a SH x SW x SD brick of SOURCE voxels (all C channels) and writes its 8 x larger
 // destination brick from the source brick + a one-voxel halo staged in LDS (each destination voxel
@@ -372,6 +474,16 @@ int launch_up2_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, in
                    float *dpost, hipStream_t s) {
     if (int64_t(batch) * 8 * h * w * dd * channels >= (int64_t(1) << 31)) return fail("upsample2x: tensor too large");
     const int cv = pick_cv(dtype, channels, gy, gx, aux, add);
+    auto al16 = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (dtype == VQ3D_BF16 && channels == 4 && dd % 4 == 0 && al16(gy) && al16(gx) && al16(aux) && al16(add)) {
+        UArgs a = make_args(batch, channels, h, w, dd, 4, false);
+        a.f1 = FastDiv(uint32_t(dd / 4));
+        const int64_t n = int64_t(batch) * h * w * (dd / 4);
+        const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)));
+        k_up2_bwd_run4<<<nb, 256, 0, s>>>(a, (const bf16_t *)gy, dmode, dparam, (const bf16_t *)aux,
+                                          (const bf16_t *)add, (bf16_t *)gx, dpre, dpost);
+        return check_launch("upsample2x_bwd(run4)");
+    }
     const UArgs a = make_args(batch, channels, h, w, dd, cv, false);
     const int64_t n = int64_t(batch) * h * w * dd * a.nchunk;
     // grid-stride; bounded so the per-workgroup partial-sum atomics stay few
