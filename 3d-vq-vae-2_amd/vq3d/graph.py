@@ -49,7 +49,10 @@ class StepGraph:
         static = [t.clone() for t in inputs]
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread_local: a DataLoader's pin-memory thread (and its worker hand-offs) may keep
+        # calling into HIP while the training thread captures; the default global mode would make
+        # those calls invalidate the capture
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             loss = self.step_fn(*static)
         self.graphs[key] = (graph, static, loss)
         # the capture ran nothing: replay once so this call's step happens

@@ -166,10 +166,11 @@ class GradientAllReduce:
         self.bucket_of = {pid: bi for bi, (_, _, ids) in enumerate(self.buckets) for pid in ids}
 
     def begin_step(self):
-        if any(self.issued) or self.works:
-            for work, _ in self.works:
-                work.wait()
-            self._reset()
+        # unconditional: a backward that died after reporting part of a bucket leaves that
+        # bucket's pending set partly drained, which would issue its all-reduce early next step
+        for work, _ in self.works:
+            work.wait()
+        self._reset()
 
     def _reset(self):
         self.pending = [set(ids) for _, _, ids in self.buckets]

@@ -123,6 +123,16 @@ def _allreduce_worker(rank, world, port, out):
     parallel.grads_ready(ps[4:])
     ar()
     ok &= all(torch.allclose(p.grad, torch.full_like(p.grad, 2.0)) for p in m.ps)  # (1 + 3) / 2
+    # a backward that died after reporting PART of a multi-parameter bucket (nothing issued): the
+    # next forward's step_begin must refill every pending set, or that bucket would be issued
+    # before the parameters already struck off have this step's gradients
+    bi = next(i for i, (_, _, ids) in enumerate(ar.buckets) if len(ids) > 1)
+    p0 = next(p for p in ps if id(p) == ar.buckets[bi][2][0])
+    parallel.grads_ready([p0])
+    ok &= not any(ar.issued) and len(ar.pending[bi]) == len(ar.buckets[bi][2]) - 1
+    parallel.step_begin()
+    ok &= all(len(s) == len(ids) for s, (_, _, ids) in zip(ar.pending, ar.buckets))
+    ar()  # the reducer issues every bucket of the (fresh) step
     # a replacement reducer (e.g. after a resume) closes the old one: only the new one reports
     ar2 = parallel.GradientAllReduce(m, bucket_bytes=2048)
     ok &= parallel._active[0] is ar2

@@ -83,6 +83,57 @@ def test_fullsize_train_step_finite(gpu):
         assert int(q.first_pass) == 0 and torch.isfinite(q.embed).all()
 
 
+def test_fullsize_multistep_graph_replay(gpu):
+    """25 training steps of the headline configuration the way bench.py runs them (2 eager steps,
+    then one HIP graph of the whole step -- forward, loss, backward, Adam -- replayed): loss,
+    gradients, parameters and codebooks finite after EVERY step, codes in range every step, and
+    a falling loss over the window (least-squares slope < 0, last five below the first five).
+    The round-3 NaN (stale LDS x zero weight) appeared only after ~10 replayed steps."""
+    from vq3d.graph import StepGraph
+    from vq3d.utils import synthetic_volume
+    m = _model(gpu)
+    opt = m.configure_optimizers()
+    x = synthetic_volume((1, 1, 512, 512, 128), 0).to(gpu)
+    nvs = torch.tensor([128], device=gpu)
+    m.train()
+    cap = {}
+    fwd = m.forward
+
+    def capture(data):
+        cap["r"] = fwd(data)
+        return cap["r"]
+    m.forward = capture
+
+    def step(xx, nn):
+        opt.zero_grad()
+        loss = m.training_step((xx, nn), 0)
+        loss.backward()
+        opt.step()
+        return loss
+    sg = StepGraph(step, warmup=2)
+    losses = []
+    for i in range(25):
+        loss = sg(x, nvs)
+        torch.cuda.synchronize()
+        lv = float(loss)
+        losses.append(lv)
+        assert np.isfinite(lv), (i, losses)
+        assert bool(torch.isfinite(m.flat.grad).all()), i
+        assert bool(torch.isfinite(m.flat.data).all()), i
+        _, (_, _, idxs) = cap["r"]
+        for lvl, (ix, k) in enumerate(zip(idxs, PUB["num_embeddings"])):
+            assert tuple(ix.shape) == SHAPES[lvl]
+            assert int(ix.min()) >= 0 and int(ix.max()) < k, (i, lvl)
+        for q in m.encoder.quantize:
+            assert bool(torch.isfinite(q.embed).all()), i
+    del m.forward
+    assert len(sg.graphs) == 1  # steps 3.. were graph replays
+    slope = np.polyfit(np.arange(len(losses)), np.array(losses), 1)[0]
+    print("losses", [round(v, 5) for v in losses], "slope", slope)
+    assert slope < 0, losses
+    assert np.mean(losses[-5:]) < np.mean(losses[:5]), losses
+
+
 # ---------------------------------------------------------------------------------------- cfg2
 # BASELINE.json configs[1]: the 2-layer published model (150 pre-q / 150 post-q / 5 post-up /
 # 5 post-down, K = 128 / 256; slurm-jobs/train_vqvae_3d_downscaled.job) on 256 x 256 x 128

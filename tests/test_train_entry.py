@@ -151,3 +151,36 @@ def test_step_graph_replay_matches_eager(gpu):
     assert len(r.graphs) == 1
     assert np.allclose(le, lg, rtol=2e-3), (le, lg)
     assert float((we - wg).abs().max()) <= 1e-3 * float(we.abs().max())
+
+
+class _SmallCTWorkers(_SmallCT):
+    """The same scans through a DataLoader with worker processes and a pin-memory thread that keep
+    prefetching while the training thread captures its step graph."""
+
+    def __init__(self, path):
+        super().__init__(path)
+        self.num_workers = 2
+
+
+@pytest.mark.gpu
+def test_train_graph_capture_with_prefetching_loader(gpu, tmp_path):
+    """vq3d.train with --hip-graph 1 (the default) captures the step on step 3 while the loader's
+    workers and pin-memory thread are still prefetching; 6 steps must equal --hip-graph 0 (only
+    fp32-atomic summation order in some weight-gradient engines may differ)."""
+    from vq3d import train
+    rng = np.random.default_rng(1)
+    for i, d in enumerate((20, 40, 24)):
+        _write(str(tmp_path / f"scan{i}.nrrd"), rng.integers(-1500, 3000, size=(32, 32, d)).astype(np.int16))
+
+    def run(hip_graph):
+        base = [str(tmp_path), "--batch-size", "1", "--n-bottleneck-blocks", "2",
+                "--default_root_dir", str(tmp_path / f"run{hip_graph}"), "--val_check_interval", "1.0",
+                "--log_every_n_steps", "1", "--max_steps", "6", "--hip-graph", str(hip_graph)]
+        model, _, hist, _ = train.main(train.parse_arguments(base), datamodule=_SmallCTWorkers(tmp_path))
+        torch.cuda.synchronize()
+        return [v for _, v in hist], model.flat.data.clone()
+    le, we = run(0)
+    lg, wg = run(1)
+    assert len(le) == len(lg) == 6 and all(np.isfinite(le + lg))
+    assert np.allclose(le, lg, rtol=2e-3), (le, lg)
+    assert float((we - wg).abs().max()) <= 1e-3 * float(we.abs().max())
