@@ -369,7 +369,7 @@ void launch_bwd(const AttnArgs &a, float scale, const void *q, const void *k, co
 
 int check_args(int32_t dtype, int32_t nprob, int32_t n, int32_t nh, int32_t dk, int32_t dv, AttnArgs &a,
                float scale, const vq3d_attn_train *train) {
-    if (dtype != VQ3D_BF16 && dtype != VQ3D_F32) return 1;
+    if (dtype != VQ3D_HALF && dtype != VQ3D_F32) return 1;
     if (nprob < 1 || n < 1 || nh < 1 || dk < 1 || dv < 1 || !dmax_of(dk, dv)) return 1;
     if (int64_t(nprob) * nh > 65535) return 1;
     a.P = nprob;
@@ -424,10 +424,10 @@ int vq3d_causal_attn_fwd_ex(int32_t dtype, int32_t nprob, int32_t n, int32_t nh,
     if (!q || !k || !v || !out || !lse) return fail("causal_attn_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     const int dm = dmax_of(dk, dv);
-    if (dtype == VQ3D_BF16) {
-        if (dm == 4) launch_fwd<bf16_t, 4>(a, q, k, v, out, lse, s);
-        else if (dm == 8) launch_fwd<bf16_t, 8>(a, q, k, v, out, lse, s);
-        else launch_fwd<bf16_t, 16>(a, q, k, v, out, lse, s);
+    if (dtype == VQ3D_HALF) {
+        if (dm == 4) launch_fwd<h16_t, 4>(a, q, k, v, out, lse, s);
+        else if (dm == 8) launch_fwd<h16_t, 8>(a, q, k, v, out, lse, s);
+        else launch_fwd<h16_t, 16>(a, q, k, v, out, lse, s);
     } else {
         if (dm == 4) launch_fwd<float, 4>(a, q, k, v, out, lse, s);
         else if (dm == 8) launch_fwd<float, 8>(a, q, k, v, out, lse, s);
@@ -457,10 +457,10 @@ int vq3d_causal_attn_bwd_ex(int32_t dtype, int32_t nprob, int32_t n, int32_t nh,
     hipStream_t s = as_stream(stream);
     float *delta = static_cast<float *>(workspace);
     const int dm = dmax_of(dk, dv);
-    if (dtype == VQ3D_BF16) {
-        if (dm == 4) launch_bwd<bf16_t, 4>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
-        else if (dm == 8) launch_bwd<bf16_t, 8>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
-        else launch_bwd<bf16_t, 16>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+    if (dtype == VQ3D_HALF) {
+        if (dm == 4) launch_bwd<h16_t, 4>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+        else if (dm == 8) launch_bwd<h16_t, 8>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
+        else launch_bwd<h16_t, 16>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
     } else {
         if (dm == 4) launch_bwd<float, 4>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);
         else if (dm == 8) launch_bwd<float, 8>(a, scale, q, k, v, out, gout, lse, delta, gq, gk, gv, s);

@@ -4,21 +4,67 @@
 #include <stdint.h>
 #include <string>
 
+// The kernel sources are compiled twice (Makefile): with bf16 as the 16-bit activation / matrix-
+// core operand format, and with -DVQ3D_FP16 with IEEE fp16 (the reference trains with fp16 AMP,
+// vqvae/train.py:32).  The fp16 build's C++ symbols live in namespace vq3d_fp16 and its C entry
+// points carry the suffix __f16, the bf16 build's __bf16 (abi_names.h, generated from
+// include/vq3d.h by tools/gen_abi.py); the public entry points (abi_dispatch.cpp, generated too)
+// route each call to one build by its dtype arguments.  Error reporting is shared (vq3d_rt).
+#ifdef VQ3D_FP16
+#define vq3d vq3d_fp16
+#endif
+#include "abi_names.h"
 #include "../../include/vq3d.h"
+
+namespace vq3d_rt {
+void set_error(const std::string &msg);
+int fail(const std::string &msg);
+int check_launch(const char *what);
+}  // namespace vq3d_rt
 
 namespace vq3d {
 
 constexpr int kWave = 64;
 
 // ---------------------------------------------------------------- storage types
-using bf16_t = uint16_t;  // raw bf16 bits; arithmetic always in fp32
+using h16_t = uint16_t;  // raw 16-bit activation bits (bf16, or fp16 in the fp16 build); arithmetic in fp32
+#ifdef VQ3D_FP16
+using half_t = _Float16;
+constexpr int32_t VQ3D_HALF = VQ3D_F16;
+#else
+using half_t = __bf16;
+constexpr int32_t VQ3D_HALF = VQ3D_BF16;
+#endif
+typedef half_t hx8 __attribute__((ext_vector_type(8)));  // one MFMA A / B fragment (8 elements)
+#ifdef VQ3D_FP16
+#define VQ3D_MFMA_16X16X32 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#else
+#define VQ3D_MFMA_16X16X32 __builtin_amdgcn_mfma_f32_16x16x32_bf16
+#endif
+
+// the 16-bit value in the low / high half of a dword as fp32 (bf16: a shift or a mask; fp16:
+// v_cvt_f32_f16)
+__device__ __forceinline__ float h2f_lo(uint32_t u) {
+#ifdef VQ3D_FP16
+    return float(__builtin_bit_cast(_Float16, uint16_t(u)));
+#else
+    return __uint_as_float(u << 16);
+#endif
+}
+__device__ __forceinline__ float h2f_hi(uint32_t u) {
+#ifdef VQ3D_FP16
+    return float(__builtin_bit_cast(_Float16, uint16_t(u >> 16)));
+#else
+    return __uint_as_float(u & 0xffff0000u);
+#endif
+}
 
 __device__ __forceinline__ float ld(const float *p) { return *p; }
-__device__ __forceinline__ float ld(const bf16_t *p) { return __uint_as_float(uint32_t(*p) << 16); }
+__device__ __forceinline__ float ld(const h16_t *p) { return h2f_lo(*p); }
 
-// round-to-nearest-even f32 -> bf16 (torch's conversion; NaN stays NaN): the hardware
-// v_cvt_pk_bf16_f32 on gfx950
-__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, static_cast<__bf16>(f)); }
+// round-to-nearest-even f32 -> the 16-bit format (torch's conversion; NaN stays NaN): the hardware
+// v_cvt_pk_bf16_f32 / v_cvt_f16_f32 on gfx950
+__device__ __forceinline__ h16_t f2h(float f) { return __builtin_bit_cast(h16_t, static_cast<half_t>(f)); }
 
 // n / d for 0 <= n < 2^31 without an integer divide (Granlund-Montgomery, host-built)
 struct FastDiv {
@@ -32,7 +78,7 @@ struct FastDiv {
     __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> s; }
 };
 __device__ __forceinline__ void st(float *p, float v) { *p = v; }
-__device__ __forceinline__ void st(bf16_t *p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void st(h16_t *p, float v) { *p = f2h(v); }
 
 // Native 32-bit vectors for register-staged loads: an array of HIP's uint4 / uint2 (a class with
 // union members) held across a loop is NOT promoted to registers by hipcc -- it lives in scratch
@@ -82,7 +128,7 @@ __device__ __forceinline__ void unraw(const Raw<T, N> &r, float (&o)[N]) {
         for (int i = 0; i < N; ++i) o[i] = __uint_as_float(r.w[i]);
     } else {
 #pragma unroll
-        for (int i = 0; i < N; ++i) o[i] = (i & 1) ? __uint_as_float(r.w[i / 2] & 0xffff0000u) : __uint_as_float(r.w[i / 2] << 16);
+        for (int i = 0; i < N; ++i) o[i] = (i & 1) ? h2f_hi(r.w[i / 2]) : h2f_lo(r.w[i / 2]);
     }
 }
 template <typename T, int N>
@@ -98,10 +144,10 @@ __device__ __forceinline__ void stvec(T *__restrict__ p, const float (&v)[N]) {
 #pragma unroll
         for (int i = 0; i < N; ++i) r.w[i] = __float_as_uint(v[i]);
     } else if constexpr (N == 1) {
-        r.w[0] = f2bf(v[0]);
+        r.w[0] = f2h(v[0]);
     } else {
 #pragma unroll
-        for (int i = 0; i < N / 2; ++i) r.w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+        for (int i = 0; i < N / 2; ++i) r.w[i] = uint32_t(f2h(v[2 * i])) | (uint32_t(f2h(v[2 * i + 1])) << 16);
     }
     if constexpr (B == 2) {
         *reinterpret_cast<uint16_t *>(p) = uint16_t(r.w[0]);
@@ -254,8 +300,8 @@ __device__ __forceinline__ void up_coeff(int j, int n, int &i0, int &i1, float &
 
 // ---------------------------------------------------------------- error plumbing (host)
 namespace vq3d {
-void set_error(const std::string &msg);
-int fail(const std::string &msg);
-int check_launch(const char *what);
+using vq3d_rt::check_launch;
+using vq3d_rt::fail;
+using vq3d_rt::set_error;
 inline hipStream_t as_stream(vq3d_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 }  // namespace vq3d

@@ -324,7 +324,7 @@ static bool is_pointwise(const vq3d_conv_desc *d) { return d->kernel == 1 && d->
 
 static int validate(const vq3d_conv_desc *d) {
     if (!d) return fail("conv: null descriptor");
-    if (d->dtype != VQ3D_F32 && d->dtype != VQ3D_BF16) return fail("conv: bad dtype");
+    if (d->dtype != VQ3D_F32 && d->dtype != VQ3D_HALF) return fail("conv: bad dtype");
     if (d->batch <= 0 || d->cin <= 0 || d->cin2 < 0 || d->cout <= 0) return fail("conv: bad channel/batch");
     if (d->kernel <= 0 || d->stride <= 0 || d->pad < 0) return fail("conv: bad kernel/stride/pad");
     const int in[3] = {d->in_h, d->in_w, d->in_d}, out[3] = {d->out_h, d->out_w, d->out_d};
@@ -421,7 +421,7 @@ static int launch_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, co
         return launch_small<T>(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws, ws_bytes,
                                s);
     }
-    if constexpr (std::is_same<T, bf16_t>::value) {
+    if constexpr (std::is_same<T, h16_t>::value) {
         if (lines_applicable(d, false)) {
             BwdEpi<T> be = {};
             return launch_lines(d, false, x, x2, w, pa, pb, fe, be, nullptr, y, nullptr, nullptr, nullptr, ws,
@@ -479,7 +479,7 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
         return launch_small<T>(d, true, g, nullptr, w, pa, nullptr, fe, be, gscale, gx, gx2, dpre, dpost, ws, ws_bytes,
                                s);
     }
-    if constexpr (std::is_same<T, bf16_t>::value) {
+    if constexpr (std::is_same<T, h16_t>::value) {
         // stride-1 backward-data == forward conv of g with the flipped, transposed kernel
         if (lines_applicable(d, true)) {
             FwdEpi<T> fe = {};
@@ -520,7 +520,7 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
 // does not apply; the direct engine for the few-channel large grids, where it is measured
 // faster (9 -> 9 at 128^2 x 32 on par, 4 -> 4 at 256^2 x 64 1.9x).
 static bool use_lines_wgrad(const vq3d_conv_desc *d) {
-    if (d->dtype != VQ3D_BF16 || !lines_wgrad_applicable(d)) return false;
+    if (d->dtype != VQ3D_HALF || !lines_wgrad_applicable(d)) return false;
     if (d->cin + d->cin2 >= 32) return true;
     return !plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
                       d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)
@@ -540,7 +540,7 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
     }
     if (tc_applicable(d))
         return launch_tc_wgrad<T>(d, x, g, pa, pb, w, escale, dw, dscale, dbias, dcbias, ws, ws_bytes, s);
-    if constexpr (std::is_same<T, bf16_t>::value) {
+    if constexpr (std::is_same<T, h16_t>::value) {
         if (mid_w2grad_ok(d) && dw && !escale && !dscale && !dbias && !dcbias && ws && ws_bytes >= mid_w2grad_ws(d))
             return mid_w2grad(d, x, g, dw, ws, ws_bytes, s);
         if (wgrad_ds_ok(d) && dw && !escale && !dscale && !dcbias && ws && ws_bytes >= wgrad_ds_ws(d))
@@ -610,7 +610,7 @@ int vq3d_conv3d_fwd(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     hipStream_t s = as_stream(stream);
     return d->dtype == VQ3D_F32
                ? launch_fwd<float>(d, x, x2, w, pro_a, pro_b, epi, y, workspace, workspace_bytes, s)
-               : launch_fwd<bf16_t>(d, x, x2, w, pro_a, pro_b, epi, y, workspace, workspace_bytes, s);
+               : launch_fwd<h16_t>(d, x, x2, w, pro_a, pro_b, epi, y, workspace, workspace_bytes, s);
 }
 
 int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gscale, const float *w,
@@ -625,7 +625,7 @@ int vq3d_conv3d_bwd_data(const vq3d_conv_desc *d, const void *g, const float *gs
     return d->dtype == VQ3D_F32
                ? launch_dgrad<float>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, workspace,
                                      workspace_bytes, s)
-               : launch_dgrad<bf16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, workspace,
+               : launch_dgrad<h16_t>(d, g, gscale, w, pro_a, epi, gx, gx2, dpro_pre, dpro_post, workspace,
                                       workspace_bytes, s);
 }
 
@@ -652,7 +652,7 @@ int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x
     hipStream_t s = as_stream(stream);
     return d->dtype == VQ3D_F32 ? launch_wgrad<float>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias,
                                                       dcbias, workspace, workspace_bytes, s)
-                                : launch_wgrad<bf16_t>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias,
+                                : launch_wgrad<h16_t>(d, x, x2, g, pro_a, pro_b, w, epi_scale, dw, dscale, dbias,
                                                        dcbias, workspace, workspace_bytes, s);
 }
 

@@ -33,7 +33,6 @@ namespace vq3d {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct LArgs {
@@ -69,7 +68,7 @@ __device__ __forceinline__ int wrapc(int i, int n) {
 // 8 consecutive bf16 from LDS at element offset `off` of `base` (16-B aligned); the address is
 // aligned to ALN bytes (odd offsets when ALN == 2: five dwords + v_alignbyte)
 template <int ALN>
-__device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
+__device__ __forceinline__ hx8 read8(const h16_t *base, int off) {
     uint4 r;
     if constexpr (ALN == 16) {
         r = *reinterpret_cast<const uint4 *>(base + off);
@@ -87,16 +86,16 @@ __device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
         r = uint4{__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
                   __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
     }
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hx8, r);
 }
 
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-    return uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+    return uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16);
 }
 
 // copy VEC consecutive bf16 (prologue applied unless raw; zeros when !ok)
 template <int VEC>
-__device__ __forceinline__ void copy_unit(const bf16_t *__restrict__ src, bf16_t *dst, bool ok, const Prologue &pro,
+__device__ __forceinline__ void copy_unit(const h16_t *__restrict__ src, h16_t *dst, bool ok, const Prologue &pro,
                                           bool raw) {
     if constexpr (VEC == 8) {
         uint4 q = {0u, 0u, 0u, 0u};
@@ -106,7 +105,7 @@ __device__ __forceinline__ void copy_unit(const bf16_t *__restrict__ src, bf16_t
                 uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    w4[j] = pack2(pro.apply(__uint_as_float(w4[j] << 16)), pro.apply(__uint_as_float(w4[j] & 0xffff0000u)));
+                    w4[j] = pack2(pro.apply(h2f_lo(w4[j])), pro.apply(h2f_hi(w4[j])));
                 q = uint4{w4[0], w4[1], w4[2], w4[3]};
             }
         }
@@ -115,12 +114,12 @@ __device__ __forceinline__ void copy_unit(const bf16_t *__restrict__ src, bf16_t
         uint32_t q = 0u;
         if (ok) {
             q = *reinterpret_cast<const uint32_t *>(src);
-            if (!raw) q = pack2(pro.apply(__uint_as_float(q << 16)), pro.apply(__uint_as_float(q & 0xffff0000u)));
+            if (!raw) q = pack2(pro.apply(h2f_lo(q)), pro.apply(h2f_hi(q)));
         }
         *reinterpret_cast<uint32_t *>(dst) = q;
     } else {
-        bf16_t q = 0;
-        if (ok) q = raw ? *src : f2bf(pro.apply(ld(src)));
+        h16_t q = 0;
+        if (ok) q = raw ? *src : f2h(pro.apply(ld(src)));
         *dst = q;
     }
 }
@@ -176,16 +175,16 @@ __global__ __launch_bounds__(256) void k_lines_pack(LArgs a, const float *__rest
 }
 
 template <int NT, int ALN, bool DGRAD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 || NT == 3) ? 4 : 2))) void k_lines(LArgs a, const bf16_t *__restrict__ x, const bf16_t *__restrict__ x2,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 || NT == 3) ? 4 : 2))) void k_lines(LArgs a, const h16_t *__restrict__ x, const h16_t *__restrict__ x2,
                                               const float *__restrict__ w, int wCt, const uint4 *__restrict__ wpk,
-                                              FwdEpi<bf16_t> fe,
-                                              BwdEpi<bf16_t> be, const float *__restrict__ gscale,
-                                              bf16_t *__restrict__ y, bf16_t *__restrict__ y2, float *dpre,
+                                              FwdEpi<h16_t> fe,
+                                              BwdEpi<h16_t> be, const float *__restrict__ gscale,
+                                              h16_t *__restrict__ y, h16_t *__restrict__ y2, float *dpre,
                                               float *dpost) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MTW = MT<NT>::value;
     constexpr int NTOT = NT * 16;
-    bf16_t *lines = reinterpret_cast<bf16_t *>(smem);                     // [nlines][LS]
+    h16_t *lines = reinterpret_cast<h16_t *>(smem);                     // [nlines][LS]
     float *otile = reinterpret_cast<float *>(smem);                       // after the MFMAs: [nvb][nw] fp32
     uint4 *wl = reinterpret_cast<uint4 *>(smem + a.region_lines);         // [chunk][NTOT] fragments
     int *ctab = reinterpret_cast<int *>(wl + a.nks * 4 * NTOT);           // [chunk] element offsets
@@ -275,8 +274,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                     const int li = int(a.fmupl.div(uint32_t(u))), r = u - li * a.mupl;
                     bool ok;
                     const int64_t vox = line_src(li, od0 * a.s, ok);
-                    const bf16_t *src = x + vox * a.C + r * a.mvec;
-                    bf16_t *dst = lines + li * a.LS + a.pad0 + a.p * a.C + r * a.mvec;
+                    const h16_t *src = x + vox * a.C + r * a.mvec;
+                    h16_t *dst = lines + li * a.LS + a.pad0 + a.p * a.C + r * a.mvec;
                     if (a.mvec == 8) copy_unit<8>(src, dst, ok, pro, raw);
                     else if (a.mvec == 2) copy_unit<2>(src, dst, ok, pro, raw);
                     else copy_unit<1>(src, dst, ok, pro, raw);
@@ -291,8 +290,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                     const int pos = pe < a.p ? pe : pe + a.bd * a.s;
                     bool ok;
                     const int64_t vox = line_src(li, id0 + pos, ok);
-                    const bf16_t *src = x + vox * a.C + c;
-                    bf16_t *dst = lines + li * a.LS + a.pad0 + pos * a.C + c;
+                    const h16_t *src = x + vox * a.C + c;
+                    h16_t *dst = lines + li * a.LS + a.pad0 + pos * a.C + c;
                     if (a.vec == 8) copy_unit<8>(src, dst, ok, pro, raw);
                     else if (a.vec == 2) copy_unit<2>(src, dst, ok, pro, raw);
                     else copy_unit<1>(src, dst, ok, pro, raw);
@@ -305,9 +304,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                     const int pos = int(a.fC.div(uint32_t(e))), c = e - pos * a.C;
                     bool ok;
                     const int64_t vox = line_src(li, id0 + pos, ok);
-                    bf16_t *dst = lines + li * a.LS + a.pad0 + e;
+                    h16_t *dst = lines + li * a.LS + a.pad0 + e;
                     const bool second = c >= a.Ca;
-                    const bf16_t *src = second ? x2 + vox * a.Cb + (c - a.Ca) : x + vox * a.Ca + c;
+                    const h16_t *src = second ? x2 + vox * a.Cb + (c - a.Ca) : x + vox * a.Ca + c;
                     if (a.vec == 8) copy_unit<8>(src, dst, ok, pro, raw);
                     else if (a.vec == 2) copy_unit<2>(src, dst, ok, pro, raw);
                     else copy_unit<1>(src, dst, ok, pro, raw);
@@ -332,16 +331,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
         for (int ks = 0; ks < a.nks; ++ks) {
             const int c = ks * 4 + kq;
             const int off = ctab[c];
-            bf16x8 bfr[NT];
+            hx8 bfr[NT];
 #pragma unroll
-            for (int n = 0; n < NT; ++n) bfr[n] = __builtin_bit_cast(bf16x8, wl[c * NTOT + n * 16 + row]);
+            for (int n = 0; n < NT; ++n) bfr[n] = __builtin_bit_cast(hx8, wl[c * NTOT + n * 16 + row]);
 #pragma unroll
             for (int m = 0; m < MTW; ++m) {
                 if (wave + 4 * m >= nmt) break;
-                const bf16x8 afr = read8<ALN>(lines, rowbase[m] + off);
+                const hx8 afr = read8<ALN>(lines, rowbase[m] + off);
 #pragma unroll
                 for (int n = 0; n < NT; ++n)
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[n], acc[m][n], 0, 0, 0);
+                    acc[m][n] = VQ3D_MFMA_16X16X32(afr, bfr[n], acc[m][n], 0, 0, 0);
             }
         }
 
@@ -387,8 +386,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                         const uint32_t rw[4] = {rq.x, rq.y, rq.z, rq.w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            r8[2 * j] = __uint_as_float(rw[j] << 16);
-                            r8[2 * j + 1] = __uint_as_float(rw[j] & 0xffff0000u);
+                            r8[2 * j] = h2f_lo(rw[j]);
+                            r8[2 * j + 1] = h2f_hi(rw[j]);
                         }
                     }
                     uint32_t o4[4];
@@ -412,8 +411,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                         const uint32_t rw[4] = {rq.x, rq.y, rq.z, rq.w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            x8[2 * j] = __uint_as_float(rw[j] << 16);
-                            x8[2 * j + 1] = __uint_as_float(rw[j] & 0xffff0000u);
+                            x8[2 * j] = h2f_lo(rw[j]);
+                            x8[2 * j + 1] = h2f_hi(rw[j]);
                         }
                     }
                     if (be.addend) {
@@ -421,8 +420,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                         const uint32_t rw[4] = {rq.x, rq.y, rq.z, rq.w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            d8[2 * j] = __uint_as_float(rw[j] << 16);
-                            d8[2 * j + 1] = __uint_as_float(rw[j] & 0xffff0000u);
+                            d8[2 * j] = h2f_lo(rw[j]);
+                            d8[2 * j + 1] = h2f_hi(rw[j]);
                         }
                     }
                     uint32_t o4[4];
@@ -657,7 +656,7 @@ Plan plan_s(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW
 }
 
 Plan plan_for(const vq3d_conv_desc *d, bool dgrad) {
-    if (d->dtype != VQ3D_BF16 || d->kernel < 2) return Plan{};
+    if (d->dtype != VQ3D_HALF || d->kernel < 2) return Plan{};
     const int circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
     if (!dgrad)
         return plan_s(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
@@ -696,9 +695,9 @@ unsigned resident_blocks(K kernel, size_t lds, unsigned units) {
 }
 
 template <bool DGRAD>
-void launch(const Plan &P, const bf16_t *x, const bf16_t *x2, const float *w, int wCt, const uint4 *wpk,
-            const FwdEpi<bf16_t> &fe,
-            const BwdEpi<bf16_t> &be, const float *gscale, bf16_t *y, bf16_t *y2, float *dpre, float *dpost,
+void launch(const Plan &P, const h16_t *x, const h16_t *x2, const float *w, int wCt, const uint4 *wpk,
+            const FwdEpi<h16_t> &fe,
+            const BwdEpi<h16_t> &be, const float *gscale, h16_t *y, h16_t *y2, float *dpre, float *dpost,
             hipStream_t s) {
 #define K(NT, ALN)                                                                                            \
     {                                                                                                         \
@@ -744,7 +743,7 @@ size_t lines_workspace(const vq3d_conv_desc *d, bool dgrad) {
 bool lines_applicable(const vq3d_conv_desc *d, bool dgrad) { return plan_for(d, dgrad).ok; }
 
 int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void *x2, const float *w, const float *pa,
-                 const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
+                 const float *pb, const FwdEpi<h16_t> &fe, const BwdEpi<h16_t> &be, const float *gscale, void *y,
                  void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s) {
     Plan P = plan_for(d, dgrad);
     if (!P.ok) return fail("conv(lines): geometry not supported");
@@ -772,9 +771,9 @@ int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void 
         wpk = static_cast<const uint4 *>(ws);
     }
     if (dgrad)
-        launch<true>(P, (const bf16_t *)x, nullptr, w, wCt, wpk, fe, be, gscale, (bf16_t *)y, (bf16_t *)y2, dpre, dpost, s);
+        launch<true>(P, (const h16_t *)x, nullptr, w, wCt, wpk, fe, be, gscale, (h16_t *)y, (h16_t *)y2, dpre, dpost, s);
     else
-        launch<false>(P, (const bf16_t *)x, (const bf16_t *)x2, w, wCt, wpk, fe, be, nullptr, (bf16_t *)y, nullptr,
+        launch<false>(P, (const h16_t *)x, (const h16_t *)x2, w, wCt, wpk, fe, be, nullptr, (h16_t *)y, nullptr,
                       nullptr, nullptr, s);
     return check_launch(dgrad ? "conv3d_bwd_data(lines)" : "conv3d_fwd(lines)");
 }

@@ -27,7 +27,6 @@ namespace vq3d {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -54,12 +53,12 @@ struct WArgs {
     FastDiv fC, fhw, fN, fCr, fmc;
 };
 
-__device__ __forceinline__ s16x4 tr_read(const bf16_t *p) {
+__device__ __forceinline__ s16x4 tr_read(const h16_t *p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p));
 }
 
-__device__ __forceinline__ bf16x8 cat8(s16x4 lo, s16x4 hi) {
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+__device__ __forceinline__ hx8 cat8(s16x4 lo, s16x4 hi) {
+    return __builtin_bit_cast(hx8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 __device__ __forceinline__ int wrapw(int i, int n) {
@@ -69,13 +68,13 @@ __device__ __forceinline__ int wrapw(int i, int n) {
 }
 
 template <int NTM, int NPW>
-__global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__restrict__ x,
-                                                    const bf16_t *__restrict__ x2, const bf16_t *__restrict__ g,
+__global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const h16_t *__restrict__ x,
+                                                    const h16_t *__restrict__ x2, const h16_t *__restrict__ g,
                                                     float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nlines = a.hh * a.hw;
-    bf16_t *lines = reinterpret_cast<bf16_t *>(smem);                             // [nlines][LS]
-    bf16_t *gt = lines + ((nlines * a.LS + 7) / 8) * 8;                           // [nvp][GS]
+    h16_t *lines = reinterpret_cast<h16_t *>(smem);                             // [nlines][LS]
+    h16_t *gt = lines + ((nlines * a.LS + 7) / 8) * 8;                           // [nvp][GS]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int grp = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
     const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
@@ -132,24 +131,24 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                     const int64_t E0 = lbase + int64_t(pa + id0) * a.C, E1 = lbase + int64_t(pb + id0) * a.C;
                     const int64_t cs = (E0 & ~int64_t(7)) + int64_t(ch) * 8;
                     if (cs >= E1) continue;
-                    bf16_t el[8];
+                    h16_t el[8];
                     if (cs + 8 <= a.xtotal) {
                         const uint4 qv = *reinterpret_cast<const uint4 *>(x + cs);
-                        const bf16_t *q8 = reinterpret_cast<const bf16_t *>(&qv);
+                        const h16_t *q8 = reinterpret_cast<const h16_t *>(&qv);
 #pragma unroll
                         for (int j = 0; j < 8; ++j) el[j] = q8[j];
                     } else {
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) el[j] = cs + j < a.xtotal ? x[cs + j] : bf16_t(0);
+                        for (int j = 0; j < 8; ++j) el[j] = cs + j < a.xtotal ? x[cs + j] : h16_t(0);
                     }
                     const int j0 = cs < E0 ? int(E0 - cs) : 0;
                     const int rel = int(cs + j0 - lbase);
                     int idd = int(a.fCr.div(uint32_t(rel))), c = rel - idd * a.C;
-                    bf16_t *dst = lines + ln * a.LS + a.pad0 + (idd - id0) * a.CS;
+                    h16_t *dst = lines + ln * a.LS + a.pad0 + (idd - id0) * a.CS;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         if (j < j0 || cs + j >= E1) continue;
-                        dst[c] = raw ? el[j] : f2bf(pro.apply(__uint_as_float(uint32_t(el[j]) << 16)));
+                        dst[c] = raw ? el[j] : f2h(pro.apply(h2f_lo(uint32_t(el[j]))));
                         if (++c == a.C) {
                             c = 0;
                             dst += a.CS;
@@ -165,8 +164,8 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                     const int pos = pb > pa ? (k < pa ? k : pb + (k - pa)) : k;
                     const int lh_ = int(a.fhw.div(uint32_t(ln))), lw_ = ln - lh_ * a.hw;
                     const int ih = wrapw(ih0 + lh_, a.iH), iw = wrapw(iw0 + lw_, a.iW), id = wrapw(id0 + pos, a.iD);
-                    const bf16_t v = x[(((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id) * a.C + r];
-                    lines[ln * a.LS + a.pad0 + pos * a.CS + r] = raw ? v : f2bf(pro.apply(ld(&v)));
+                    const h16_t v = x[(((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id) * a.C + r];
+                    lines[ln * a.LS + a.pad0 + pos * a.CS + r] = raw ? v : f2h(pro.apply(ld(&v)));
                 }
             }
         } else {
@@ -187,16 +186,16 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                         ok = unsigned(ih) < unsigned(a.iH) && unsigned(iw) < unsigned(a.iW) && unsigned(id) < unsigned(a.iD);
                     }
                     const int64_t vox = bbase + (int64_t(ih) * a.iW + iw) * a.iD + id;
-                    bf16_t *dst = lines + ln * a.LS + a.pad0 + pos * a.CS;
+                    h16_t *dst = lines + ln * a.LS + a.pad0 + pos * a.CS;
                     if (ok && a.Cb == 0 && (a.C & 3) == 0) {
                         const uint2 *src = reinterpret_cast<const uint2 *>(x + vox * a.C);
                         for (int c4 = 0; c4 < a.C / 4; ++c4) {
                             uint2 qv = src[c4];
                             if (!raw) {
                                 auto f = [&](uint32_t uu) {
-                                    const float lo = pro.apply(__uint_as_float(uu << 16));
-                                    const float hi = pro.apply(__uint_as_float(uu & 0xffff0000u));
-                                    return uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+                                    const float lo = pro.apply(h2f_lo(uu));
+                                    const float hi = pro.apply(h2f_hi(uu));
+                                    return uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16);
                                 };
                                 qv = uint2{f(qv.x), f(qv.y)};
                             }
@@ -204,10 +203,10 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                         }
                     } else {
                         for (int c = 0; c < a.CS; ++c) {
-                            bf16_t v = 0;
+                            h16_t v = 0;
                             if (ok && c < a.C) {
-                                const bf16_t *src = c < a.Ca ? x + vox * a.Ca + c : x2 + vox * a.Cb + (c - a.Ca);
-                                v = raw ? *src : f2bf(pro.apply(ld(src)));
+                                const h16_t *src = c < a.Ca ? x + vox * a.Ca + c : x2 + vox * a.Cb + (c - a.Ca);
+                                v = raw ? *src : f2h(pro.apply(ld(src)));
                             }
                             dst[c] = v;
                         }
@@ -235,7 +234,7 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                     const int lh_ = r >> a.lbw, lw_ = r & (a.bw - 1);
                     const int64_t gb = ((((int64_t(b) * a.oH + oh0 + lh_) * a.oW) + ow0 + lw_) * a.oD + od0) * a.N;
                     const uint4 qv = *reinterpret_cast<const uint4 *>(g + gb + e0);
-                    const bf16_t *el = reinterpret_cast<const bf16_t *>(&qv);
+                    const h16_t *el = reinterpret_cast<const h16_t *>(&qv);
                     int ld_ = int(a.fN.div(uint32_t(e0))), co = e0 - ld_ * a.N;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
@@ -262,7 +261,7 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
         // ---- MFMA: K = 32 voxels per step
         for (int ks = 0; ks < a.nvp / 32; ++ks) {
             const int v1 = ks * 32 + 8 * grp + q, v2 = v1 + 4;
-            bf16x8 af[NTM];
+            hx8 af[NTM];
 #pragma unroll
             for (int m = 0; m < NTM; ++m)
                 af[m] = cat8(tr_read(gt + v1 * a.GS + m * 16 + 4 * pp), tr_read(gt + v2 * a.GS + m * 16 + 4 * pp));
@@ -273,10 +272,10 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const bf16_t *__re
                             a.pad0 + (u2 & (a.bd - 1)) * a.s * a.CS;
 #pragma unroll
             for (int t = 0; t < NPW; ++t) {
-                const bf16x8 bfr = cat8(tr_read(lines + rb1 + coff[t]), tr_read(lines + rb2 + coff[t]));
+                const hx8 bfr = cat8(tr_read(lines + rb1 + coff[t]), tr_read(lines + rb2 + coff[t]));
 #pragma unroll
                 for (int m = 0; m < NTM; ++m)
-                    acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr, acc[m][t], 0, 0, 0);
+                    acc[m][t] = VQ3D_MFMA_16X16X32(af[m], bfr, acc[m][t], 0, 0, 0);
             }
         }
     }
@@ -373,7 +372,7 @@ struct WPlan {
 WPlan plan_w(const vq3d_conv_desc *d) {
     WPlan P = {};
     WArgs &a = P.a;
-    if (d->dtype != VQ3D_BF16 || d->kernel < 1 || d->cout > 64 || (d->cin2 && (d->cin + d->cin2) % 4)) return P;
+    if (d->dtype != VQ3D_HALF || d->kernel < 1 || d->cout > 64 || (d->cin2 && (d->cin + d->cin2) % 4)) return P;
     a.B = d->batch; a.Ca = d->cin; a.Cb = d->cin2; a.C = a.Ca + a.Cb; a.N = d->cout;
     a.CS = (a.C + 3) / 4 * 4;
     a.iH = d->in_h; a.iW = d->in_w; a.iD = d->in_d; a.oH = d->out_h; a.oW = d->out_w; a.oD = d->out_d;
@@ -483,7 +482,7 @@ int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, c
             (void)hipGetLastError();
             attr = true;
         }
-        kern<<<grid, 256, P.lds, s>>>(P.a, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g, part);
+        kern<<<grid, 256, P.lds, s>>>(P.a, (const h16_t *)x, (const h16_t *)x2, (const h16_t *)g, part);
     };
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;

@@ -53,16 +53,16 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[N])
             const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                o[8 * q + 2 * j] = __uint_as_float(w4[j] << 16);
-                o[8 * q + 2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+                o[8 * q + 2 * j] = h2f_lo(w4[j]);
+                o[8 * q + 2 * j + 1] = h2f_hi(w4[j]);
             }
         }
     } else if constexpr (sizeof(T) == 2 && N == 4) {
         const uint2 u = *reinterpret_cast<const uint2 *>(p);
-        o[0] = __uint_as_float(u.x << 16);
-        o[1] = __uint_as_float(u.x & 0xffff0000u);
-        o[2] = __uint_as_float(u.y << 16);
-        o[3] = __uint_as_float(u.y & 0xffff0000u);
+        o[0] = h2f_lo(u.x);
+        o[1] = h2f_hi(u.x);
+        o[2] = h2f_lo(u.y);
+        o[3] = h2f_hi(u.y);
     } else {
 #pragma unroll
         for (int j = 0; j < N; ++j) o[j] = ld(p + j);
@@ -76,7 +76,7 @@ __device__ __forceinline__ void store_row(T *__restrict__ p, const float (&v)[N]
         for (int q = 0; q < N / 8; ++q) {
             uint32_t u[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) u[j] = uint32_t(f2bf(v[8 * q + 2 * j])) | (uint32_t(f2bf(v[8 * q + 2 * j + 1])) << 16);
+            for (int j = 0; j < 4; ++j) u[j] = uint32_t(f2h(v[8 * q + 2 * j])) | (uint32_t(f2h(v[8 * q + 2 * j + 1])) << 16);
             reinterpret_cast<uint4 *>(p)[q] = uint4{u[0], u[1], u[2], u[3]};
         }
     } else {
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict_
                 }
                 uint32_t qv[COT / 2];
 #pragma unroll
-                for (int j = 0; j < COT / 2; ++j) qv[j] = uint32_t(f2bf(o[2 * j])) | (uint32_t(f2bf(o[2 * j + 1])) << 16);
+                for (int j = 0; j < COT / 2; ++j) qv[j] = uint32_t(f2h(o[2 * j])) | (uint32_t(f2h(o[2 * j + 1])) << 16);
                 if constexpr (COT == 4) *reinterpret_cast<uint2 *>(gx + v * COT) = uint2{qv[0], qv[1]};
                 else *reinterpret_cast<uint4 *>(gx + v * COT) = uint4{qv[0], qv[1], qv[2], qv[3]};
                 continue;
@@ -340,7 +340,7 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
     if (int64_t(a.B) * a.iH * a.iW * a.iD >= (int64_t(1) << 31)) return fail("conv3d_bwd_data(s2): grid too large");
     {
         auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-        if (std::is_same<T, bf16_t>::value && a.circ && a.Cin2 == 0 && (a.Cin == 4 || a.Cin == 8) &&
+        if (std::is_same<T, h16_t>::value && a.circ && a.Cin2 == 0 && (a.Cin == 4 || a.Cin == 8) &&
             (a.Cout == 4 || a.Cout == 8) && a.p == a.k / 2 - 1 && a.iH == 2 * a.oH && a.iW == 2 * a.oW &&
             a.iD == 2 * a.oD && al16(g) && al16(gx) && (!be.aux || al16(be.aux)) && (!be.addend || al16(be.addend))) {
             S2Args c = a;
@@ -392,7 +392,7 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
 
 template int launch_dgrad_s2<float>(const vq3d_conv_desc *, const void *, const float *, const float *,
                                     const BwdEpi<float> &, void *, void *, float *, float *, hipStream_t);
-template int launch_dgrad_s2<bf16_t>(const vq3d_conv_desc *, const void *, const float *, const float *,
-                                     const BwdEpi<bf16_t> &, void *, void *, float *, float *, hipStream_t);
+template int launch_dgrad_s2<h16_t>(const vq3d_conv_desc *, const void *, const float *, const float *,
+                                     const BwdEpi<h16_t> &, void *, void *, float *, float *, hipStream_t);
 
 }  // namespace vq3d

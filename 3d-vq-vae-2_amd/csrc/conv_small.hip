@@ -37,10 +37,10 @@ __device__ __forceinline__ void load4(const T *p, bool vec, int n, float (&o)[4]
     if constexpr (sizeof(T) == 2) {
         if (vec) {
             const uint2 u = *reinterpret_cast<const uint2 *>(p);
-            o[0] = __uint_as_float(u.x << 16);
-            o[1] = __uint_as_float(u.x & 0xffff0000u);
-            o[2] = __uint_as_float(u.y << 16);
-            o[3] = __uint_as_float(u.y & 0xffff0000u);
+            o[0] = h2f_lo(u.x);
+            o[1] = h2f_hi(u.x);
+            o[2] = h2f_lo(u.y);
+            o[3] = h2f_hi(u.y);
             return;
         }
     } else {
@@ -291,8 +291,8 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
 template int launch_small<float>(const vq3d_conv_desc *, bool, const void *, const void *, const float *,
                                  const float *, const float *, const FwdEpi<float> &, const BwdEpi<float> &,
                                  const float *, void *, void *, float *, float *, void *, size_t, hipStream_t);
-template int launch_small<bf16_t>(const vq3d_conv_desc *, bool, const void *, const void *, const float *,
-                                  const float *, const float *, const FwdEpi<bf16_t> &, const BwdEpi<bf16_t> &,
+template int launch_small<h16_t>(const vq3d_conv_desc *, bool, const void *, const void *, const float *,
+                                  const float *, const float *, const FwdEpi<h16_t> &, const BwdEpi<h16_t> &,
                                   const float *, void *, void *, float *, float *, void *, size_t, hipStream_t);
 
 }  // namespace vq3d

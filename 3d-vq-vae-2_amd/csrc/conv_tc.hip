@@ -48,8 +48,8 @@ __device__ __forceinline__ void vload(const T *__restrict__ p, float (&o)[N]) {
             const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                o[8 * q + 2 * j] = __uint_as_float(w4[j] << 16);
-                o[8 * q + 2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+                o[8 * q + 2 * j] = h2f_lo(w4[j]);
+                o[8 * q + 2 * j + 1] = h2f_hi(w4[j]);
             }
         }
     } else if constexpr (sizeof(T) == 4 && (N % 4) == 0) {
@@ -75,7 +75,7 @@ __device__ __forceinline__ void vstore(T *__restrict__ p, const float (&v)[N]) {
             uint32_t w4[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                w4[j] = uint32_t(f2bf(v[8 * q + 2 * j])) | (uint32_t(f2bf(v[8 * q + 2 * j + 1])) << 16);
+                w4[j] = uint32_t(f2h(v[8 * q + 2 * j])) | (uint32_t(f2h(v[8 * q + 2 * j + 1])) << 16);
             reinterpret_cast<uint4 *>(p)[q] = uint4{w4[0], w4[1], w4[2], w4[3]};
         }
     } else if constexpr (sizeof(T) == 4 && (N % 4) == 0) {
@@ -411,7 +411,7 @@ TcArgs make_tc(const vq3d_conv_desc *d, const float *pa, const float *pb, int ci
     a.nbw = a.W / BW;
     a.nbd = a.D / BD;
     a.nbricks = a.B * a.nbh * a.nbw * a.nbd;
-    const int esz = d->dtype == VQ3D_BF16 ? 2 : 4;
+    const int esz = d->dtype == VQ3D_HALF ? 2 : 4;
     const int E = 16 / esz;
     a.pad = (E - ci % E) % E;  // position 1 (the main run) starts 16-B aligned
     a.LS = (a.pad + PL * ci + E - 1) / E * E;
@@ -523,13 +523,13 @@ int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const
 template int launch_tc<float>(const vq3d_conv_desc *, bool, const void *, const float *, const float *, const float *,
                               const FwdEpi<float> &, const BwdEpi<float> &, const float *, void *, float *, float *,
                               void *, size_t, hipStream_t);
-template int launch_tc<bf16_t>(const vq3d_conv_desc *, bool, const void *, const float *, const float *,
-                               const float *, const FwdEpi<bf16_t> &, const BwdEpi<bf16_t> &, const float *, void *,
+template int launch_tc<h16_t>(const vq3d_conv_desc *, bool, const void *, const float *, const float *,
+                               const float *, const FwdEpi<h16_t> &, const BwdEpi<h16_t> &, const float *, void *,
                                float *, float *, void *, size_t, hipStream_t);
 template int launch_tc_wgrad<float>(const vq3d_conv_desc *, const void *, const void *, const float *, const float *,
                                     const float *, const float *, float *, float *, float *, float *, void *, size_t,
                                     hipStream_t);
-template int launch_tc_wgrad<bf16_t>(const vq3d_conv_desc *, const void *, const void *, const float *,
+template int launch_tc_wgrad<h16_t>(const vq3d_conv_desc *, const void *, const void *, const float *,
                                      const float *, const float *, const float *, float *, float *, float *, float *,
                                      void *, size_t, hipStream_t);
 

@@ -41,7 +41,7 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
 bool lines_applicable(const vq3d_conv_desc *d, bool dgrad);
 size_t lines_workspace(const vq3d_conv_desc *d, bool dgrad);
 int launch_lines(const vq3d_conv_desc *d, bool dgrad, const void *x, const void *x2, const float *w, const float *pa,
-                 const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be, const float *gscale, void *y,
+                 const float *pb, const FwdEpi<h16_t> &fe, const BwdEpi<h16_t> &be, const float *gscale, void *y,
                  void *y2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t s);
 
 // k^3 weight gradient on the lines layout (conv_lines_wgrad.hip), bf16, cout <= 64: per-workgroup
@@ -101,7 +101,7 @@ int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const
 // few-channel blocks on the big grids (preact_col.hip), behind vq3d_preact_small_*
 bool col_supported(int batch, int C, int BR, int h, int w, int d);
 size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d);
-// xdt / odt: storage (VQ3D_BF16 | VQ3D_F32) of the residual stream in (x, gx) and out (out, g)
+// xdt / odt: storage (VQ3D_HALF | VQ3D_F32) of the residual stream in (x, gx) and out (out, g)
 int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1,
             const float *w2, const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3,
             hipStream_t s);

@@ -7,8 +7,8 @@
 #include <cmath>
 #include <cstring>
 
-namespace vq3d {
-
+#ifndef VQ3D_FP16  // one error state for both builds (common.h: vq3d_rt)
+namespace vq3d_rt {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 int fail(const std::string &msg) {
@@ -20,6 +20,11 @@ int check_launch(const char *what) {
     if (e != hipSuccess) return fail(std::string(what) + ": " + hipGetErrorString(e));
     return 0;
 }
+const char *last_error() { return g_last_error.c_str(); }
+}  // namespace vq3d_rt
+#endif
+
+namespace vq3d {
 
 static unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048))); }
 
@@ -141,7 +146,7 @@ __device__ __forceinline__ float huber_grad(float d) {
 // A thread owns 4 consecutive voxels (one 16-byte load, 4 C bf16 of output).
 template <int C>
 __global__ __launch_bounds__(256) void k_pin_fwd(const float *__restrict__ x, int64_t n4, const float *__restrict__ w,
-                                                const float *__restrict__ b, bf16_t *__restrict__ y) {
+                                                const float *__restrict__ b, h16_t *__restrict__ y) {
     const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
     if (i >= n4) return;
     const float4 xv = reinterpret_cast<const float4 *>(x)[i];
@@ -151,11 +156,11 @@ __global__ __launch_bounds__(256) void k_pin_fwd(const float *__restrict__ x, in
     for (int v = 0; v < 4; ++v)
 #pragma unroll
         for (int c = 0; c < C; ++c) o[v * C + c] = fmaf(w[c], xs[v], b[c]);
-    stvec<bf16_t, 4 * C>(y + i * 4 * C, o);
+    stvec<h16_t, 4 * C>(y + i * 4 * C, o);
 }
 // weight / bias gradient partials per workgroup: [block][2 C] = (sum g x, sum g) per channel
 template <int C>
-__global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, const bf16_t *__restrict__ g, int64_t n4,
+__global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, const h16_t *__restrict__ g, int64_t n4,
                                                   float *__restrict__ part) {
     __shared__ float red[4];
     float sw[C], sb[C];
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, 
         const float4 xv = reinterpret_cast<const float4 *>(x)[i];
         const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
         float gv[4 * C];
-        ldvec<bf16_t, 4 * C>(g + i * 4 * C, gv);
+        ldvec<h16_t, 4 * C>(g + i * 4 * C, gv);
 #pragma unroll
         for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -453,8 +458,10 @@ using namespace vq3d;
 
 extern "C" {
 
-const char *vq3d_last_error(void) { return g_last_error.c_str(); }
-const char *vq3d_version(void) { return "vq3d 0.1 gfx950"; }
+#ifndef VQ3D_FP16  // format-independent, defined once (not renamed: abi_names.h)
+const char *vq3d_last_error(void) { return vq3d_rt::last_error(); }
+const char *vq3d_version(void) { return "vq3d 0.2 gfx950 (bf16 + fp16 builds)"; }
+#endif
 
 int vq3d_upsample2x_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd,
                         const void *x, int32_t pro_kind, const float *pro_a, const float *pro_b, void *y,
@@ -496,15 +503,20 @@ int64_t vq3d_cylinder_count(int32_t h, int32_t w) {
     return c;
 }
 
-int vq3d_parse_input_fwd(int64_t voxels, int32_t channels, const float *x, const float *w, const float *b, void *y,
-                         vq3d_stream_t stream) {
+static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int vq3d_parse_input_fwd(int32_t dtype, int64_t voxels, int32_t channels, const float *x, const float *w,
+                         const float *b, void *y, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("parse_input_fwd: dtype must be the 16-bit format of this build");
     if (voxels <= 0 || voxels % 4 || !(channels == 2 || channels == 4 || channels == 8))
         return fail("parse_input_fwd: voxels % 4 == 0 and channels in {2, 4, 8}");
     if (!x || !w || !b || !y) return fail("parse_input_fwd: null pointer");
+    // float4 input loads, 16- to 64-byte output stores
+    if (!al16(x) || !al16(y)) return fail("parse_input_fwd: x and y must be 16-byte aligned");
     const int64_t n4 = voxels / 4;
     const unsigned nb = unsigned((n4 + 255) / 256);
     hipStream_t s = as_stream(stream);
-    bf16_t *Y = static_cast<bf16_t *>(y);
+    h16_t *Y = static_cast<h16_t *>(y);
     if (channels == 2) k_pin_fwd<2><<<nb, 256, 0, s>>>(x, n4, w, b, Y);
     else if (channels == 4) k_pin_fwd<4><<<nb, 256, 0, s>>>(x, n4, w, b, Y);
     else k_pin_fwd<8><<<nb, 256, 0, s>>>(x, n4, w, b, Y);
@@ -515,16 +527,18 @@ size_t vq3d_parse_input_workspace_bytes(int64_t voxels, int32_t channels) {
     return size_t(pin_blocks(voxels)) * 2 * size_t(channels > 0 ? channels : 1) * 4;
 }
 
-int vq3d_parse_input_bwd(int64_t voxels, int32_t channels, const float *x, const void *g, float *dw, float *db,
-                         void *workspace, size_t ws_bytes, vq3d_stream_t stream) {
+int vq3d_parse_input_bwd(int32_t dtype, int64_t voxels, int32_t channels, const float *x, const void *g, float *dw,
+                         float *db, void *workspace, size_t ws_bytes, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("parse_input_bwd: dtype must be the 16-bit format of this build");
     if (voxels <= 0 || voxels % 4 || !(channels == 2 || channels == 4 || channels == 8))
         return fail("parse_input_bwd: voxels % 4 == 0 and channels in {2, 4, 8}");
     if (!x || !g || !workspace) return fail("parse_input_bwd: null pointer");
+    if (!al16(x) || !al16(g)) return fail("parse_input_bwd: x and g must be 16-byte aligned");
     if (ws_bytes < vq3d_parse_input_workspace_bytes(voxels, channels)) return fail("parse_input_bwd: workspace too small");
     const int nb = pin_blocks(voxels);
     const int64_t n4 = voxels / 4;
     hipStream_t s = as_stream(stream);
-    const bf16_t *G = static_cast<const bf16_t *>(g);
+    const h16_t *G = static_cast<const h16_t *>(g);
     float *part = static_cast<float *>(workspace);
     if (channels == 2) {
         k_pin_wgrad<2><<<nb, 256, 0, s>>>(x, G, n4, part);
@@ -560,7 +574,7 @@ int vq3d_recon_loss_fwd(int32_t dtype, const void *dec, const float *x, const in
     if (dtype == VQ3D_F32)
         k_recon_fwd<float><<<nb, 256, 0, s>>>((const float *)dec, x, nvs, batch, h, w, dd, cylinder, part);
     else
-        k_recon_fwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)dec, x, nvs, batch, h, w, dd, cylinder, part);
+        k_recon_fwd<h16_t><<<nb, 256, 0, s>>>((const h16_t *)dec, x, nvs, batch, h, w, dd, cylinder, part);
     k_recon_fin<<<1, 256, 0, s>>>(part, nb, float(1.0 / double(cnt)), cp, n_commit, recon, total);
     return check_launch("recon_loss_fwd");
 }
@@ -579,8 +593,8 @@ int vq3d_recon_loss_bwd(int32_t dtype, const void *dec, const float *x, const in
         k_recon_bwd<float><<<nb, 256, 0, s>>>((const float *)dec, x, nvs, batch, h, w, dd, cylinder, g_total, ic,
                                               (float *)gdec);
     else
-        k_recon_bwd<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)dec, x, nvs, batch, h, w, dd, cylinder, g_total, ic,
-                                               (bf16_t *)gdec);
+        k_recon_bwd<h16_t><<<nb, 256, 0, s>>>((const h16_t *)dec, x, nvs, batch, h, w, dd, cylinder, g_total, ic,
+                                               (h16_t *)gdec);
     return check_launch("recon_loss_bwd");
 }
 
@@ -611,7 +625,7 @@ int vq3d_evonorm_fwd(int32_t dtype, const void *x, int32_t channels, int64_t vox
             k_evo_stats_part<float><<<unsigned(nb), 256, 0, s>>>((const float *)x, channels, G, voxels, vpb, mean,
                                                                  part);
         else
-            k_evo_stats_part<bf16_t><<<unsigned(nb), 256, 0, s>>>((const bf16_t *)x, channels, G, voxels, vpb, mean,
+            k_evo_stats_part<h16_t><<<unsigned(nb), 256, 0, s>>>((const h16_t *)x, channels, G, voxels, vpb, mean,
                                                                   part);
         k_evo_stats_fin<<<1, 64 * ((G + 63) / 64), 0, s>>>(part, int(nb), G, m, stats, pass);
     }
@@ -620,8 +634,8 @@ int vq3d_evonorm_fwd(int32_t dtype, const void *x, int32_t channels, int64_t vox
         k_evo_apply<float><<<na, 256, 0, s>>>((const float *)x, channels, G, voxels, v, gamma, beta, stats,
                                               (float *)y);
     else
-        k_evo_apply<bf16_t><<<na, 256, 0, s>>>((const bf16_t *)x, channels, G, voxels, v, gamma, beta, stats,
-                                               (bf16_t *)y);
+        k_evo_apply<h16_t><<<na, 256, 0, s>>>((const h16_t *)x, channels, G, voxels, v, gamma, beta, stats,
+                                               (h16_t *)y);
     return check_launch("evonorm_fwd");
 }
 
@@ -640,7 +654,7 @@ int vq3d_evonorm_bwd(int32_t dtype, const void *x, const void *gy, int32_t chann
         k_evo_bwd_part<float><<<unsigned(nb), 256, 0, s>>>((const float *)x, (const float *)gy, channels, G, voxels,
                                                            vpb, v, gamma, stats, part);
     else
-        k_evo_bwd_part<bf16_t><<<unsigned(nb), 256, 0, s>>>((const bf16_t *)x, (const bf16_t *)gy, channels, G,
+        k_evo_bwd_part<h16_t><<<unsigned(nb), 256, 0, s>>>((const h16_t *)x, (const h16_t *)gy, channels, G,
                                                             voxels, vpb, v, gamma, stats, part);
     k_evo_bwd_fin<<<1, 256, 0, s>>>(part, int(nb), channels, G, gsum, dv, dgamma, dbeta);
     const unsigned na = unsigned((voxels * channels + 255) / 256);
@@ -648,8 +662,8 @@ int vq3d_evonorm_bwd(int32_t dtype, const void *x, const void *gy, int32_t chann
         k_evo_bwd_apply<float><<<na, 256, 0, s>>>((const float *)x, (const float *)gy, channels, G, voxels, v, gamma,
                                                   stats, gsum, (float *)gx);
     else
-        k_evo_bwd_apply<bf16_t><<<na, 256, 0, s>>>((const bf16_t *)x, (const bf16_t *)gy, channels, G, voxels, v,
-                                                   gamma, stats, gsum, (bf16_t *)gx);
+        k_evo_bwd_apply<h16_t><<<na, 256, 0, s>>>((const h16_t *)x, (const h16_t *)gy, channels, G, voxels, v,
+                                                   gamma, stats, gsum, (h16_t *)gx);
     return check_launch("evonorm_bwd");
 }
 
@@ -683,10 +697,10 @@ int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, 
     if (n == 0) return 0;
     hipStream_t s = as_stream(stream);
     const unsigned nb = grid_for(n);
-    if (src_dtype == VQ3D_F32 && dst_dtype == VQ3D_BF16)
-        k_cast<float, bf16_t><<<nb, 256, 0, s>>>((const float *)src, (bf16_t *)dst, n);
-    else if (src_dtype == VQ3D_BF16 && dst_dtype == VQ3D_F32)
-        k_cast<bf16_t, float><<<nb, 256, 0, s>>>((const bf16_t *)src, (float *)dst, n);
+    if (src_dtype == VQ3D_F32 && dst_dtype == VQ3D_HALF)
+        k_cast<float, h16_t><<<nb, 256, 0, s>>>((const float *)src, (h16_t *)dst, n);
+    else if (src_dtype == VQ3D_HALF && dst_dtype == VQ3D_F32)
+        k_cast<h16_t, float><<<nb, 256, 0, s>>>((const h16_t *)src, (float *)dst, n);
     else if (src_dtype == dst_dtype)
         return vq3d_copy(dst, src, size_t(n) * (src_dtype == VQ3D_F32 ? 4 : 2), stream);
     else
@@ -730,8 +744,8 @@ int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *
         k_elu_bwd_out<float><<<grid_for(n), 256, 0, as_stream(stream)>>>((const float *)g, (const float *)y,
                                                                           (float *)gz, n);
     else
-        k_elu_bwd_out<bf16_t><<<grid_for(n), 256, 0, as_stream(stream)>>>((const bf16_t *)g, (const bf16_t *)y,
-                                                                           (bf16_t *)gz, n);
+        k_elu_bwd_out<h16_t><<<grid_for(n), 256, 0, as_stream(stream)>>>((const h16_t *)g, (const h16_t *)y,
+                                                                           (h16_t *)gz, n);
     return check_launch("elu_bwd_from_output");
 }
 

@@ -48,7 +48,6 @@ namespace vq3d {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BH = 8, BW = 8, BD = 16, DV = 4;  // brick; voxels per thread along D
@@ -84,40 +83,40 @@ struct CArgs {
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
-__device__ __forceinline__ float bf(uint32_t u16) { return __uint_as_float(u16 << 16); }
-__device__ __forceinline__ float rbf(float v) { return bf(f2bf(v)); }
+__device__ __forceinline__ float bf(uint32_t u16) { return h2f_lo(u16); }
+__device__ __forceinline__ float rbf(float v) { return bf(f2h(v)); }
 __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : __expf(z) - 1.f; }
 __device__ __forceinline__ float elu_d_act(float t, float b) {
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
 }
-__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma(hx8 a, hx8 b, f32x4 c) {
+    return VQ3D_MFMA_16X16X32(a, b, c, 0, 0, 0);
 }
 // 8 consecutive bf16 from LDS at any element offset of a 4-byte aligned base
-__device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
+__device__ __forceinline__ hx8 read8(const h16_t *base, int off) {
     const uint32_t *q = reinterpret_cast<const uint32_t *>(base + (off & ~1));
     const uint32_t sh = uint32_t(off & 1) * 2u;
     const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3], u4 = q[4];
     const uint4 r = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
                      __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hx8, r);
 }
 // 8 bf16 at an even element offset (4-byte aligned)
-__device__ __forceinline__ bf16x8 read8e(const bf16_t *p) {
+__device__ __forceinline__ hx8 read8e(const h16_t *p) {
     const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
-    return __builtin_bit_cast(bf16x8, uint4{q[0], q[1], q[2], q[3]});
+    return __builtin_bit_cast(hx8, uint4{q[0], q[1], q[2], q[3]});
 }
-__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+__device__ __forceinline__ hx8 pack8(const float (&v)[8]) {
     uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
-    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2h(v[2 * j])) | (uint32_t(f2h(v[2 * j + 1])) << 16);
+    return __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]});
 }
 
 // NW dwords (2, 4 or 8) to global memory as 8- / 16-byte stores
 template <int NW>
-__device__ __forceinline__ void store_words(bf16_t *__restrict__ p, const uint32_t (&w)[NW]) {
+__device__ __forceinline__ void store_words(h16_t *__restrict__ p, const uint32_t (&w)[NW]) {
     if constexpr (NW == 2) {
         *reinterpret_cast<uint2 *>(p) = uint2{w[0], w[1]};
     } else {
@@ -139,30 +138,30 @@ __device__ __forceinline__ void unpack(const typename Vec<N>::U &u, float (&o)[N
     if constexpr (N == 1) {
         o[0] = bf(u);
     } else if constexpr (N == 2) {
-        o[0] = __uint_as_float(u << 16);
-        o[1] = __uint_as_float(u & 0xffff0000u);
+        o[0] = h2f_lo(u);
+        o[1] = h2f_hi(u);
     } else if constexpr (N == 4) {
-        o[0] = __uint_as_float(u.x << 16);
-        o[1] = __uint_as_float(u.x & 0xffff0000u);
-        o[2] = __uint_as_float(u.y << 16);
-        o[3] = __uint_as_float(u.y & 0xffff0000u);
+        o[0] = h2f_lo(u.x);
+        o[1] = h2f_hi(u.x);
+        o[2] = h2f_lo(u.y);
+        o[3] = h2f_hi(u.y);
     } else {
         const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            o[2 * i] = __uint_as_float(w[i] << 16);
-            o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+            o[2 * i] = h2f_lo(w[i]);
+            o[2 * i + 1] = h2f_hi(w[i]);
         }
     }
 }
 template <int N>
 __device__ __forceinline__ typename Vec<N>::U packv(const float (&v)[N]) {
     if constexpr (N == 1) {
-        return f2bf(v[0]);
+        return f2h(v[0]);
     } else {
         uint32_t w[(N + 1) / 2];
 #pragma unroll
-        for (int i = 0; i < N / 2; ++i) w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+        for (int i = 0; i < N / 2; ++i) w[i] = uint32_t(f2h(v[2 * i])) | (uint32_t(f2h(v[2 * i + 1])) << 16);
         if constexpr (N == 2) return w[0];
         else if constexpr (N == 4) return uint2{w[0], w[1]};
         else return uint4{w[0], w[1], w[2], w[3]};
@@ -210,7 +209,7 @@ __device__ __forceinline__ bool interior(int line, int pos) {
 
 // B fragment of k-step s of the row-windowed W2 (DGRAD: transposed, flipped taps)
 template <int BR, bool DGRAD>
-__device__ __forceinline__ bf16x8 w2_frag(const float *__restrict__ w2, int s, int lane) {
+__device__ __forceinline__ hx8 w2_frag(const float *__restrict__ w2, int s, int lane) {
     using K = K3<BR>;
     const int n = lane & 15, kb = lane >> 4;
     float v[8];
@@ -243,7 +242,7 @@ __device__ __forceinline__ int win_base(int mt, int BR) {  // m-tile mt = brick 
     return ((mt >> 3) * WL + (mt & 7)) * PL * BR;
 }
 template <int BR>
-__device__ __forceinline__ bf16x8 win_frag(const bf16_t *h, int off) {
+__device__ __forceinline__ hx8 win_frag(const h16_t *h, int off) {
     if constexpr (BR == 1) return read8(h, off);
     else return read8e(h + off);
 }
@@ -255,16 +254,16 @@ template <int C, int BR, typename TX, typename TO>
 __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ x, const float *__restrict__ w1,
                                                 const float *__restrict__ w2, const float *__restrict__ w3,
                                                 vq3d_preact_params p, TO *__restrict__ out,
-                                                bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
+                                                h16_t *__restrict__ t2o, h16_t *__restrict__ t3o) {
     using K = K3<BR>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *t2h = reinterpret_cast<bf16_t *>(smem);            // [HVX][BR] + PADE
+    h16_t *t2h = reinterpret_cast<h16_t *>(smem);            // [HVX][BR] + PADE
     float *accs = reinterpret_cast<float *>(t2h + HVX * BR + PADE);  // [NV][BR] raw W2 (*) t2
     int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
     const Org o = brick_org(a, a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x));
     const Scal s = load_scal(p);
-    bf16x8 fw[K::KS];
+    hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, false>(w2, k, lane);
     line_table(a, o, lbase);
@@ -323,7 +322,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
     if constexpr ((COL_EXP & 16) != 0) return;
     const int v0 = ln * BD + dg * DV;
     if (t2o) {
-        const bf16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
+        const h16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
         uint32_t w[DV * BR / 2];
         if constexpr (BR == 1) {  // 4 positions at an odd element offset
             const uint4 u4 = __builtin_bit_cast(uint4, read8(t2h, int(src - t2h)));
@@ -344,7 +343,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
 #pragma unroll
         for (int i = 0; i < DV * BR / 2; ++i) {
             const int e0 = 2 * i, e1 = 2 * i + 1;
-            w[i] = uint32_t(f2bf(t3v[e0 / BR][e0 % BR])) | (uint32_t(f2bf(t3v[e1 / BR][e1 % BR])) << 16);
+            w[i] = uint32_t(f2h(t3v[e0 / BR][e0 % BR])) | (uint32_t(f2h(t3v[e1 / BR][e1 % BR])) << 16);
         }
         if (t3o) store_words<DV * BR / 2>(t3o + vox0 * BR, w);  // NULL: eval forward, nothing saved
     }
@@ -365,16 +364,16 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
 // g has the storage of the forward's out (TO), x and gx that of its input (TX)
 template <int C, int BR, typename TX, typename TO>
 __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ g, const TX *__restrict__ x,
-                                                const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
+                                                const h16_t *__restrict__ t2, const h16_t *__restrict__ t3,
                                                 const float *__restrict__ w1, const float *__restrict__ w2,
                                                 const float *__restrict__ w3, vq3d_preact_params p,
                                                 float *__restrict__ part, TX *__restrict__ gx) {
     using K = K3<BR>;
     constexpr int NE = n_entries<C, BR>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *z3h = reinterpret_cast<bf16_t *>(smem);  // gz3 on the halo [HVX][BR] + PADE
-    bf16_t *t2T = z3h + HVX * BR + PADE;             // t2 on the halo, channel-major [BR][NLN][TP]
-    bf16_t *z3T = t2T + BR * NLN * TP;                // gz3 of the brick, channel-major [BR][ZP]
+    h16_t *z3h = reinterpret_cast<h16_t *>(smem);  // gz3 on the halo [HVX][BR] + PADE
+    h16_t *t2T = z3h + HVX * BR + PADE;             // t2 on the halo, channel-major [BR][NLN][TP]
+    h16_t *z3T = t2T + BR * NLN * TP;                // gz3 of the brick, channel-major [BR][ZP]
     float *accs = reinterpret_cast<float *>(z3T + BR * ZP);  // [NV][BR] raw W2^T (*) gz3
     int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     float *red = reinterpret_cast<float *>(lbase + NLN);  // [4 waves][NE]
@@ -383,7 +382,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
     const Org o = brick_org(a, a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x));
     const Scal s = load_scal(p);
-    bf16x8 fw[K::KS];
+    hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, true>(w2, k, lane);
     line_table(a, o, lbase);
@@ -443,7 +442,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
 #pragma unroll
                         for (int c = 0; c < C; ++c) g3[oo][c] = fmaf(t3f[oo], gf[c], g3[oo][c]);
                     }
-                    t2T[(oo * NLN + line) * TP + pos] = f2bf(t2f[oo]);
+                    t2T[(oo * NLN + line) * TP + pos] = f2h(t2f[oo]);
                 }
                 const typename Vec<BR>::U zp = packv<BR>(z);
                 *reinterpret_cast<typename Vec<BR>::U *>(z3h + q * BR) = zp;
@@ -453,7 +452,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                     const int lh = line / WL, lw = line - lh * WL;
                     const int v = ((lh - 1) * BW + lw - 1) * BD + pos - 1;
 #pragma unroll
-                    for (int oo = 0; oo < BR; ++oo) z3T[oo * ZP + v] = f2bf(z[oo]);
+                    for (int oo = 0; oo < BR; ++oo) z3T[oo * ZP + v] = f2h(z[oo]);
                 }
             }
         }
@@ -492,7 +491,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
 #pragma unroll 2
     for (int ks = 8 * wave; ks < ((COL_EXP & 8) ? 0 : 8 * wave + 8); ++ks) {
         // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
-        const bf16x8 af = *reinterpret_cast<const bf16x8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
+        const hx8 af = *reinterpret_cast<const hx8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
         const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
 #pragma unroll
         for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
@@ -694,7 +693,7 @@ void allow(Kern k, size_t lds) {
 
 template <int C, int BR, typename TX, typename TO>
 void launch_fwd(const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
-                const vq3d_preact_params &p, void *out, bf16_t *t2, bf16_t *t3, hipStream_t s) {
+                const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         allow(k_col_fwd<C, BR, TX, TO>, fwd_lds<C, BR>());
@@ -704,7 +703,7 @@ void launch_fwd(const CArgs &a, const void *x, const float *w1, const float *w2,
                                                                      static_cast<TO *>(out), t2, t3);
 }
 template <int C, int BR, typename TX, typename TO>
-void launch_bwd(const CArgs &a, const void *g, const void *x, const bf16_t *t2, const bf16_t *t3, const float *w1,
+void launch_bwd(const CArgs &a, const void *g, const void *x, const h16_t *t2, const h16_t *t3, const float *w1,
                 const float *w2, const float *w3, const vq3d_preact_params &p, const vq3d_preact_grads &gr, float *part,
                 void *gx, int stages, hipStream_t s) {
     static bool attr = false;
@@ -724,23 +723,23 @@ void launch_bwd(const CArgs &a, const void *g, const void *x, const bf16_t *t2, 
     }
 }
 
-// the (x, out) storage pair: VQ3D_BF16 / VQ3D_F32 each
+// the (x, out) storage pair: VQ3D_HALF / VQ3D_F32 each
 template <int C, int BR>
 void fwd_io(int xdt, int odt, const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
-            const vq3d_preact_params &p, void *out, bf16_t *t2, bf16_t *t3, hipStream_t s) {
-    if (xdt == VQ3D_BF16 && odt == VQ3D_BF16) launch_fwd<C, BR, bf16_t, bf16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
-    else if (xdt == VQ3D_BF16) launch_fwd<C, BR, bf16_t, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
-    else if (odt == VQ3D_BF16) launch_fwd<C, BR, float, bf16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
+            const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, hipStream_t s) {
+    if (xdt == VQ3D_HALF && odt == VQ3D_HALF) launch_fwd<C, BR, h16_t, h16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
+    else if (xdt == VQ3D_HALF) launch_fwd<C, BR, h16_t, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
+    else if (odt == VQ3D_HALF) launch_fwd<C, BR, float, h16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
     else launch_fwd<C, BR, float, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
 }
 template <int C, int BR>
-void bwd_io(int xdt, int odt, const CArgs &a, const void *g, const void *x, const bf16_t *t2, const bf16_t *t3,
+void bwd_io(int xdt, int odt, const CArgs &a, const void *g, const void *x, const h16_t *t2, const h16_t *t3,
             const float *w1, const float *w2, const float *w3, const vq3d_preact_params &p, const vq3d_preact_grads &gr,
             float *part, void *gx, int stages, hipStream_t s) {
-    if (xdt == VQ3D_BF16 && odt == VQ3D_BF16)
-        launch_bwd<C, BR, bf16_t, bf16_t>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
-    else if (xdt == VQ3D_BF16) launch_bwd<C, BR, bf16_t, float>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
-    else if (odt == VQ3D_BF16) launch_bwd<C, BR, float, bf16_t>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
+    if (xdt == VQ3D_HALF && odt == VQ3D_HALF)
+        launch_bwd<C, BR, h16_t, h16_t>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else if (xdt == VQ3D_HALF) launch_bwd<C, BR, h16_t, float>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
+    else if (odt == VQ3D_HALF) launch_bwd<C, BR, float, h16_t>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
     else launch_bwd<C, BR, float, float>(a, g, x, t2, t3, w1, w2, w3, p, gr, part, gx, stages, s);
 }
 
@@ -783,7 +782,7 @@ int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, con
             const float *w2, const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3,
             hipStream_t s) {
     const CArgs a = make_args(batch, h, w, d);
-    auto T2 = static_cast<bf16_t *>(t2), T3 = static_cast<bf16_t *>(t3);
+    auto T2 = static_cast<h16_t *>(t2), T3 = static_cast<h16_t *>(t3);
     if (C == 2) fwd_io<2, 1>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
     else if (C == 4) fwd_io<4, 2>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
     else fwd_io<8, 4>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
@@ -795,7 +794,7 @@ int col_bwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, con
             const vq3d_preact_params &p, const vq3d_preact_grads &gr, void *workspace, void *gx, int stages,
             hipStream_t s) {
     const CArgs a = make_args(batch, h, w, d);
-    auto T2 = static_cast<const bf16_t *>(t2), T3 = static_cast<const bf16_t *>(t3);
+    auto T2 = static_cast<const h16_t *>(t2), T3 = static_cast<const h16_t *>(t3);
     float *part = static_cast<float *>(workspace);
     if (C == 2) bwd_io<2, 1>(xdt, odt, a, g, x, T2, T3, w1, w2, w3, p, gr, part, gx, stages, s);
     else if (C == 4) bwd_io<4, 2>(xdt, odt, a, g, x, T2, T3, w1, w2, w3, p, gr, part, gx, stages, s);

@@ -38,7 +38,8 @@
 // Timing experiments only (tools builds: make -C 3d-vq-vae-2_amd exp EXP=N): bit 0 skips the
 // forward tile kernel's k^3 phase, 1 its 1x1 phase, 2 its stores, 3 its staging; bits 4 .. 8 the
 // backward data tile kernel's staging (loads + LDS writes), k^3 dgrad phase, gx phase, chained
-// previous-block phase and global stores.  The product library is built with PM_EXP = 0.
+// previous-block phase and global stores, 9 / 10 its next-tile epilogue-operand / halo loads, 11 the
+// forward tile kernel's next-tile loads.  The product library is built with PM_EXP = 0.
 #ifndef PM_EXP
 #define PM_EXP 0
 #endif
@@ -50,16 +51,19 @@
 #ifndef PM_BWD_PER
 #define PM_BWD_PER 0
 #endif
-// minimum waves per SIMD the backward-data tile kernel is compiled for (1: the compiler's choice)
+// 1: the D16 tile kernels keep one run's epilogue at a time (a scheduling barrier between runs)
+#ifndef PM_SB
+#define PM_SB 1
+#endif
+// minimum waves per SIMD the backward-data tile kernel is compiled for (2: at most 256 registers)
 #ifndef PM_BWD_WPE
-#define PM_BWD_WPE 1
+#define PM_BWD_WPE 2
 #endif
 
 namespace vq3d {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int C = 18, BR = 9, TD = 8;  // block channels, branch channels, tile depth (one D-run)
@@ -96,7 +100,10 @@ struct Tile {
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
-__device__ __forceinline__ float bf(uint32_t u16) { return __uint_as_float(u16 << 16); }
+__device__ __forceinline__ float bf(uint32_t u16) { return h2f_lo(u16); }
+// ELU on the hardware exp (v_exp_f32 of z log2 e: ~1e-7 relative, far inside the bf16 rounding that
+// follows every use in the tile kernels; the libm expf is ~10 instructions)
+__device__ __forceinline__ float elu_fast(float z) { return z > 0.f ? z : __expf(z) - 1.f; }
 __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
@@ -104,35 +111,35 @@ __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from 
 
 // 8 consecutive bf16 from LDS at element offset `off` (any parity; base 16-B aligned): five
 // dwords + v_alignbyte when odd
-__device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
+__device__ __forceinline__ hx8 read8(const h16_t *base, int off) {
     const uint32_t *q = reinterpret_cast<const uint32_t *>(base + (off & ~1));
     const uint32_t sh = uint32_t(off & 1) * 2u;
     const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3], u4 = q[4];
     const uint4 r = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
                      __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hx8, r);
 }
 
 // 8 bf16 at element offsets off + j * stride (j = 0..7) from LDS; zeros when !ok
-__device__ __forceinline__ bf16x8 gather8(const bf16_t *base, int off, int stride, bool ok) {
+__device__ __forceinline__ hx8 gather8(const h16_t *base, int off, int stride, bool ok) {
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     if (ok) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             w[j] = uint32_t(base[off + 2 * j * stride]) | (uint32_t(base[off + (2 * j + 1) * stride]) << 16);
     }
-    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+    return __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]});
 }
 
-__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+__device__ __forceinline__ hx8 pack8(const float (&v)[8]) {
     uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
-    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2h(v[2 * j])) | (uint32_t(f2h(v[2 * j + 1])) << 16);
+    return __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]});
 }
 
-__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma(hx8 a, hx8 b, f32x4 c) {
+    return VQ3D_MFMA_16X16X32(a, b, c, 0, 0, 0);
 }
 
 // copy n fp32 weights to LDS (coalesced; the fragments are then built from LDS instead of from
@@ -146,7 +153,7 @@ __device__ __forceinline__ void stage_w(float *dst, const float *__restrict__ sr
 // Forward: n = co, c = ci, tap kk * 3 + kd.  Backward-data (transposed, flipped): n = ci,
 // c = co, tap 26 - (kk * 3 + kd).
 template <bool DGRAD>
-__device__ __forceinline__ bf16x8 w2_frag(const float *w2, int kk, int lane) {
+__device__ __forceinline__ hx8 w2_frag(const float *w2, int kk, int lane) {
     const int n = lane & 15, kb = lane >> 4;
     float v[8];
 #pragma unroll
@@ -205,7 +212,7 @@ struct LinesLd {
     u32x4 ve[PE];
     // every load is unconditional (indices past the end are clamped): a branch around a load
     // makes hipcc wait for it on the spot
-    __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
+    __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const h16_t *__restrict__ src) {
         const int tid = threadIdx.x;
 #pragma unroll
         for (int u = 0; u < PI; ++u) {
@@ -228,7 +235,7 @@ struct LinesLd {
             ve[u] = *reinterpret_cast<const u32x4 *>(src + lb + e0 + 8 * ch);
         }
     }
-    __device__ __forceinline__ void store(bf16_t *lines) const {
+    __device__ __forceinline__ void store(h16_t *lines) const {
         const int tid = threadIdx.x;
 #pragma unroll
         for (int u = 0; u < PI; ++u) {
@@ -257,7 +264,7 @@ struct TileLd {
     using T = Tile<TH, TW>;
     static constexpr int PR = CH * TD / 8, N = T::NRUN * PR, P = (N + NT - 1) / NT;
     u32x4 v[P];
-    __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const bf16_t *__restrict__ src) {
+    __device__ __forceinline__ void load(const PmArgs &a, const Org &o, const h16_t *__restrict__ src) {
         const int tid = threadIdx.x;
 #pragma unroll
         for (int u = 0; u < P; ++u) {
@@ -266,7 +273,7 @@ struct TileLd {
             v[u] = reinterpret_cast<const u32x4 *>(src + run_vox<TW>(a, o, r) * CH)[part];
         }
     }
-    __device__ __forceinline__ void store(bf16_t *dst) const {
+    __device__ __forceinline__ void store(h16_t *dst) const {
         const int tid = threadIdx.x;
 #pragma unroll
         for (int u = 0; u < P; ++u) {
@@ -277,7 +284,7 @@ struct TileLd {
 };
 
 template <int TH, int TW, int CH>
-__device__ __forceinline__ void store_tile(const PmArgs &a, const Org &o, const bf16_t *src, bf16_t *__restrict__ dst) {
+__device__ __forceinline__ void store_tile(const PmArgs &a, const Org &o, const h16_t *src, h16_t *__restrict__ dst) {
     using T = Tile<TH, TW>;
     constexpr int PR = CH * TD / 8, N = T::NRUN * PR;
     for (int i = threadIdx.x; i < N; i += NT) {
@@ -289,7 +296,7 @@ __device__ __forceinline__ void store_tile(const PmArgs &a, const Org &o, const 
 // zero the never-staged tails of the halo lines and of the tile buffers (read by the windows /
 // fragments that run past the valid data and meet zero weights: they must be finite)
 template <int TH, int TW>
-__device__ __forceinline__ void zero_pads(bf16_t *lines, int nimg, bf16_t *const *tails, const int *tail_at,
+__device__ __forceinline__ void zero_pads(h16_t *lines, int nimg, h16_t *const *tails, const int *tail_at,
                                           int ntails) {
     using T = Tile<TH, TW>;
     for (int i = threadIdx.x; i < nimg * T::NL * (LSP - LEND); i += NT) {
@@ -304,12 +311,12 @@ __device__ __forceinline__ void zero_pads(bf16_t *lines, int nimg, bf16_t *const
 // t2 = elu(W1 (elu(x + b1a) + b1b) + b2a) + b2b.  A thread owns a PAIR of voxels: 72 bytes of x
 // (9 8-byte loads, all issued before any math) in, 36 bytes of t2 (9 dword stores) out; no LDS
 // staging, no barriers.  W1 is broadcast from LDS.
-__global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__restrict__ x,
+__global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const h16_t *__restrict__ x,
                                               const float *__restrict__ w1, vq3d_preact_params p,
-                                              bf16_t *__restrict__ t2o) {
+                                              h16_t *__restrict__ t2o) {
     __shared__ float w1s[BR * C];
     // W1 and u1 rounded to bf16: the operands of the chained forward's matrix-core t2 stage
-    for (int i = threadIdx.x; i < BR * C; i += NT) w1s[i] = bf(f2bf(w1[i]));
+    for (int i = threadIdx.x; i < BR * C; i += NT) w1s[i] = bf(f2h(w1[i]));
     __syncthreads();
     const Scal s = load_scal(p);
     const int64_t npair = nvox / 2;
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
                 const int e = h * C + c;  // element of the 36 bf16 of the pair
                 const uint2 w = v[e / 4];
                 const uint32_t d = (e & 2) ? w.y : w.x;
-                uu[c] = bf(f2bf(elu(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b));
+                uu[c] = bf(f2h(elu(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b));
             }
             float t2v[BR];
 #pragma unroll
@@ -341,7 +348,7 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
             }
 #pragma unroll
             for (int o = 0; o < BR; ++o) {
-                const uint32_t hb = f2bf(t2v[o]);
+                const uint32_t hb = f2h(t2v[o]);
                 const int e = h * BR + o;  // element of the 18 bf16 of the pair's t2
                 if (e & 1) outw[e / 2] |= hb << 16;
                 else outw[e / 2] = hb;
@@ -353,162 +360,23 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const bf16_t *__rest
     }
 }
 
-// t3 and out of a TH x TW x 8 tile from t2 on its halo and x; CHAIN: also the next block's t2
-template <int TH, int TW, bool CHAIN>
-__global__ __launch_bounds__(NT) void k_pm_fwd(PmArgs a, const bf16_t *__restrict__ t2, const bf16_t *__restrict__ x,
-                                               const float *__restrict__ w2, const float *__restrict__ w3,
-                                               vq3d_preact_params p, bf16_t *__restrict__ t3o,
-                                               bf16_t *__restrict__ out, const float *__restrict__ w1n,
-                                               vq3d_preact_params pn, bf16_t *__restrict__ t2n) {
-    using T = Tile<TH, TW>;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *t2l = reinterpret_cast<bf16_t *>(smem);  // halo lines [NL][LSP]; CHAIN: then next t2 [TV][9]
-    bf16_t *t3s = t2l + T::LINES;                     // [TV][9]
-    bf16_t *xs = t3s + T::S9;                         // [TV][18]: x, then out in place
-    float *w1ns = reinterpret_cast<float *>(xs + T::S18);  // CHAIN: next block's W1 [o][c]
-    bf16_t *u1s = reinterpret_cast<bf16_t *>(w1ns + BR * C);  // CHAIN: next block's u1 [TV][18]
-    static_assert(T::LINES >= T::TV * BR, "next t2 fits the halo image");
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if constexpr (CHAIN) stage_w(w1ns, w1n, BR * C);
-    const int row = lane & 15, kb = lane >> 4;
-    bf16x8 bw2[9], bw3[2], bw1n[1] = {};
-    {
-        float *w2s = reinterpret_cast<float *>(smem), *w3s = w2s + NW2;  // scratch over the halo image
-        static_assert(T::LINES * 2 >= (NW2 + C * BR) * 4, "weights fit the halo image");
-        stage_w(w2s, w2, NW2);
-        stage_w(w3s, w3, C * BR);
-        __syncthreads();
-        if constexpr (CHAIN) {  // the next block's W1 as B[k = c][n = o] (k >= 18, n >= 9 zero)
-            float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int c = 8 * kb + j;
-                v[j] = (c < C && row < BR) ? w1ns[row * C + c] : 0.f;
-            }
-            bw1n[0] = pack8(v);
-        }
-#pragma unroll
-        for (int kk = 0; kk < 9; ++kk) bw2[kk] = w2_frag<false>(w2s, kk, lane);
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {  // W3 as B[k = o][n = co]
-            float v[8];
-            const int co = 16 * nt + row;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int o = 8 * kb + j;
-                v[j] = (o < BR && co < C) ? w3s[co * BR + o] : 0.f;
-            }
-            bw3[nt] = pack8(v);
-        }
-        __syncthreads();
-    }
-    {
-        bf16_t *tails[3] = {t3s, xs, u1s};
-        const int at[3] = {T::TV * BR, T::TV * C, T::TV * C};
-        zero_pads<TH, TW>(t2l, 1, tails, at, CHAIN ? 3 : 2);
-    }
-    const Scal s = load_scal(p);
-    Scal sn{};
-    if constexpr (CHAIN) sn = load_scal(pn);
-    // the next tile's loads are in flight while the current tile computes
-    LinesLd<TH, TW> lt;
-    TileLd<TH, TW, C> lx;
-    const TileSched sc = xcd_sched(a.ntiles);
-    if (sc.t < sc.end) {
-        const Org o0 = tile_org(a, sc.t, TH, TW);
-        lt.load(a, o0, t2);
-        lx.load(a, o0, x);
-    }
-    for (int tile = sc.t; tile < sc.end; tile += sc.step) {
-        const Org o = tile_org(a, tile, TH, TW);
-        __syncthreads();
-        if constexpr (!(PM_EXP & 8)) {
-            lt.store(t2l);
-            lx.store(xs);
-            if (tile + sc.step < sc.end) {
-                const Org on = tile_org(a, tile + sc.step, TH, TW);
-                lt.load(a, on, t2);
-                lx.load(a, on, x);
-            }
-        }
-        __syncthreads();
-        // t3 = elu(W2 (*) t2 + b3a) + b3b: 16-voxel x 9-channel tiles, 9 windowed k-steps
-        for (int mt = (PM_EXP & 1) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
-            const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
-            const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kk = 0; kk < 9; ++kk)
-                acc = mfma(read8(t2l, base + ((kk / 3) * T::LW + kk % 3) * LSP), bw2[kk], acc);
-            if (row < BR) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    t3s[(mt * 16 + 4 * kb + j) * BR + row] = f2bf(elu(acc[j] + s.b3a) + s.b3b);
-            }
-        }
-        __syncthreads();
-        // out = scale * W3 t3 + b4 + x (in place over x); CHAIN: the wave also forms the next block's
-        // u1 = bf16(elu(out + b1a) + b1b) of its 16 voxels (k_pm_t2's rounding points) and, reading
-        // them back as the A fragment (its own LDS writes, in order: no barrier), the next block's
-        // t2 = elu(W1 u1 + b2a) + b2b into the free halo image
-        for (int mt = (PM_EXP & 2) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
-            const bf16x8 af = read8(t3s, (mt * 16 + row) * BR + 8 * kb);
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                const f32x4 acc = mfma(af, bw3[nt], f32x4{0.f, 0.f, 0.f, 0.f});
-                const int co = 16 * nt + row;
-                if (co < C) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int xi = (mt * 16 + 4 * kb + j) * C + co;
-                        const bf16_t ob = f2bf(acc[j] * s.sc + s.b4 + bf(xs[xi]));
-                        xs[xi] = ob;
-                        if constexpr (CHAIN) u1s[xi] = f2bf(elu(bf(ob) + sn.b1a) + sn.b1b);
-                    }
-                }
-            }
-            if constexpr (CHAIN && !(PM_EXP & 512)) {
-                // K entries 18..31 are the next voxel's channels and meet zero weights, but they must
-                // be finite: for row 15 they lie in the NEXT m-tile, which another wave may not have
-                // written yet (on a workgroup's first tile: whatever the previous kernel left in LDS,
-                // where a NaN bit pattern times the zero weight poisoned the next block's t2)
-                uint4 q = kb == 3 ? uint4{0u, 0u, 0u, 0u}
-                                  : __builtin_bit_cast(uint4, read8(u1s, (mt * 16 + row) * C + 8 * kb));
-                if (kb == 2) q.y = q.z = q.w = 0u;
-                const f32x4 acc = mfma(__builtin_bit_cast(bf16x8, q), bw1n[0], f32x4{0.f, 0.f, 0.f, 0.f});
-                if (row < BR) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        t2l[(mt * 16 + 4 * kb + j) * BR + row] = f2bf(elu(acc[j] + sn.b2a) + sn.b2b);
-                }
-            }
-        }
-        __syncthreads();
-        if constexpr (!(PM_EXP & 4)) {
-            if (t3o) store_tile<TH, TW, BR>(a, o, t3s, t3o);
-            store_tile<TH, TW, C>(a, o, xs, out);
-        }
-        if constexpr (CHAIN) store_tile<TH, TW, BR>(a, o, t2l, t2n);
-    }
-}
-
 // ============================================================================================ backward
 // K1: gz3 = bf16(scale * W3^T g * elu'(t3 - b3b)) and the sums of g (b4), of scale W3^T g (b3b),
 // of gz3 (b3a) and of g . (W3 t3) (scale).  Blocks of 256 voxels; the next block's loads are in
 // flight during the current one.  (The W3 gradient, sum t3 (x) g, is k_pm_w13grad's.)
-__global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__restrict__ g,
-                                                const bf16_t *__restrict__ t3, const float *__restrict__ w3,
-                                                vq3d_preact_params p, bf16_t *__restrict__ gz3o,
+__global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const h16_t *__restrict__ g,
+                                                const h16_t *__restrict__ t3, const float *__restrict__ w3,
+                                                vq3d_preact_params p, h16_t *__restrict__ gz3o,
                                                 float *__restrict__ part) {
     __shared__ float w3s[C * BR];
-    __shared__ __attribute__((aligned(16))) bf16_t gs[NT * C];
-    __shared__ __attribute__((aligned(16))) bf16_t ts[NT * BR];
-    __shared__ __attribute__((aligned(16))) bf16_t zs[NT * BR];
+    __shared__ __attribute__((aligned(16))) h16_t gs[NT * C];
+    __shared__ __attribute__((aligned(16))) h16_t ts[NT * BR];
+    __shared__ __attribute__((aligned(16))) h16_t zs[NT * BR];
     __shared__ float red[32];
     constexpr int NG = NT * C / 8, NTT = NT * BR / 8, PG = (NG + NT - 1) / NT, PT = (NTT + NT - 1) / NT;
     const int tid = threadIdx.x;
     // W3 rounded to bf16: the operand the chained stage of k_pm_bwd2 feeds the matrix cores
-    for (int i = tid; i < C * BR; i += NT) w3s[i] = bf(f2bf(w3[i]));
+    for (int i = tid; i < C * BR; i += NT) w3s[i] = bf(f2h(w3[i]));
     const Scal s = load_scal(p);
     float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f;
     const int64_t nblk = nvox / NT;
@@ -554,7 +422,7 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
                 s3b += gt3;
                 s3a += z;
                 ssc = fmaf(a3, tv[o], ssc);  // sum_co g[co] (W3 t3)[co] == sum_o t3[o] (W3^T g)[o]
-                zs[tid * BR + o] = f2bf(z);
+                zs[tid * BR + o] = f2h(z);
             }
         }
         __syncthreads();
@@ -575,187 +443,444 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const bf16_t *__re
     }
 }
 
-// K2: per TH x TW x 8 tile: gt2 = W2^T (*) gz3 (flipped taps) -> gz1 = bf16(gt2 * elu'(t2)) ->
-// gx = g + (W1^T gz1) * elu'(x + b1a); gz1 to the workspace (k_pm_w13grad) and the b2 / b1 sums
+// ============================================================================================ D16 tiles
+// The backward data tile kernel (k_pm_bwd2) works on tiles of 4 x 4 D-runs of 16 voxels (256
+// voxels): an MFMA column block is one whole D-run and each of the 8 waves owns 2 runs.
+//  * k^3: the gz3 halo D-lines are staged in LDS with a 10-element position pitch (9 channels + a
+//    zero), so the window of a tap row (3 kd taps x 10 elements) is 4 aligned dwords per lane; the
+//    WEIGHTS are the A operand and the window the B operand, and each staged window feeds both of
+//    the wave's runs where both use its line (12 window reads for 18 MFMAs).
+//  * With the weights in the A slot the accumulator of lane (n, kb) holds channels 4kb .. 4kb + 3
+//    of voxel n.  The 1x1 convs that follow take exactly those 4 values as their own B operand
+//    (their K axis is ordered to match: k = 8kb + i <-> channel 4kb + i), so gz1 and gx never leave
+//    the registers; the epilogue operands (x, g, t2, the previous block's t3) are loaded straight
+//    from HBM into that layout one tile ahead (no LDS staging), gx leaves as 8-byte stores and the
+//    9-channel outputs through a per-wave 288-byte LDS image as 16-byte stores.
+//  * One barrier per tile: the halo image is double-buffered.
+constexpr int QTH = 4, QTW = 4, QTD = 16;
+constexpr int QLW = QTW + 2, QNL = (QTH + 2) * QLW;  // 36 halo lines
+constexpr int QPP = 10;                               // LDS elements per halo position
+constexpr int QLP = 184;                              // LDS elements per halo line: 18 positions + zero tail (>= 182)
+constexpr int QIMG = QNL * QLP;                       // one halo image (elements)
+constexpr int QSTG = 576;                             // per-wave output image of a run: [16][18] + 2 x [16][9]
+constexpr int QNT = 512, QNW = QNT / 64;              // threads / waves per workgroup: a wave owns 2 D-runs
+
+PmArgs make_args_q(int B, int H, int W, int D) {
+    PmArgs a;
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    a.D = D;
+    a.nth = H / QTH;
+    a.ntw = W / QTW;
+    a.ntd = D / QTD;
+    a.ntiles = B * a.nth * a.ntw * a.ntd;
+    return a;
+}
+__device__ __forceinline__ Org tile_org_q(const PmArgs &a, int t) {
+    Org o;
+    o.d0 = (t % a.ntd) * QTD;
+    t /= a.ntd;
+    o.w0 = (t % a.ntw) * QTW;
+    t /= a.ntw;
+    o.h0 = (t % a.nth) * QTH;
+    o.b = t / a.nth;
+    return o;
+}
+
+// The (QTH+2) x (QTW+2) halo D-lines of a 9-channel tensor around a tile (circular wrap), one work
+// item per thread: the 8 interior position PAIRS of a line (positions d, d + 1 with d even: 36
+// contiguous dword-aligned bytes, 9 dwords) or one of its 2 edge positions (d0 - 1 / d0 + 16,
+// wrapped: the 20 bytes from the dword at or below the row).  load() issues the global loads
+// into registers, store() writes each position as 5 dwords (9 channels + the zero pad) into the
+// pitch-10 image with naturally aligned b32 / b64 stores (a position starts 4 or 0 mod 8).
+constexpr int QPAIRS = QNL * 8, QITEMS = QPAIRS + QNL * 2;
+static_assert(QITEMS <= QNT, "one halo item per thread");
+struct HaloQ {
+    uint32_t w[9];
+    // element offsets fit 32 bits (vq3d_preact_mid_supported bounds the tensor)
+    __device__ __forceinline__ void load(int tid, const PmArgs &a, const Org &o, const h16_t *__restrict__ src) {
+        const int i = min(tid, QITEMS - 1);
+        const bool pair = i < QPAIRS;
+        const int line = pair ? i >> 3 : (i - QPAIRS) >> 1;
+        const int lh = line / QLW, lw = line - lh * QLW;
+        const uint32_t gh = wrapm(o.h0 - 1 + lh, a.H), gw = wrapm(o.w0 - 1 + lw, a.W);
+        const uint32_t lb = ((uint32_t(o.b) * a.H + gh) * a.W + gw) * a.D;  // first voxel of the line
+        const char *base = reinterpret_cast<const char *>(src);
+        const int side = (i - QPAIRS) & 1;
+        const int d = pair ? o.d0 + 2 * (i & 7)  // a 36-byte pair: dword aligned
+                           : side ? (o.d0 + QTD == a.D ? 0 : o.d0 + QTD) : (o.d0 == 0 ? a.D - 1 : o.d0 - 1);
+        const uint32_t off = ((lb + d) * (2 * BR)) & ~3u;  // an odd voxel's row starts at 2 mod 4
+        // unconditional loads (a branch around a load makes hipcc wait for it on the spot)
+        __builtin_memcpy(w, base + off, 20);
+        __builtin_memcpy(w + 5, base + (pair ? off + 20 : off), 16);
+    }
+    __device__ __forceinline__ void store(int tid, h16_t *img) const {
+        if (tid >= QITEMS) return;
+        const bool pair = tid < QPAIRS;
+        const int line = pair ? tid >> 3 : (tid - QPAIRS) >> 1;
+        uint32_t *ln = reinterpret_cast<uint32_t *>(img + line * QLP);  // 16-B aligned (QLP * 2 = 368)
+        if (pair) {
+            // positions p = 2k + 1, 2k + 2 (d = 2k, 2k + 1) at dwords 5p .. 5p + 9: 5p = 4 mod 8 bytes
+            const int q = 5 * (2 * (tid & 7) + 1);
+            const uint32_t c[10] = {w[0], w[1], w[2], w[3], w[4] & 0xffffu, __builtin_amdgcn_alignbyte(w[5], w[4], 2),
+                                    __builtin_amdgcn_alignbyte(w[6], w[5], 2), __builtin_amdgcn_alignbyte(w[7], w[6], 2),
+                                    __builtin_amdgcn_alignbyte(w[8], w[7], 2), w[8] >> 16};
+            ln[q] = c[0];
+            *reinterpret_cast<u32x2 *>(ln + q + 1) = u32x2{c[1], c[2]};
+            *reinterpret_cast<u32x2 *>(ln + q + 3) = u32x2{c[3], c[4]};
+            *reinterpret_cast<u32x2 *>(ln + q + 5) = u32x2{c[5], c[6]};
+            *reinterpret_cast<u32x2 *>(ln + q + 7) = u32x2{c[7], c[8]};
+            ln[q + 9] = c[9];
+        } else {
+            // position 0 (dwords 0 .. 4): voxel d0 - 1 (or D - 1), odd, its row 2 bytes into w; position
+            // 17 (dwords 85 .. 89): voxel d0 + 16 (or 0), even, its row at w
+            const int side = (tid - QPAIRS) & 1;
+            if (side) {  // dword 85: 4 mod 8 bytes
+                ln[85] = w[0];
+                *reinterpret_cast<u32x2 *>(ln + 86) = u32x2{w[1], w[2]};
+                *reinterpret_cast<u32x2 *>(ln + 88) = u32x2{w[3], w[4] & 0xffffu};
+            } else {
+                *reinterpret_cast<u32x2 *>(ln) =
+                    u32x2{__builtin_amdgcn_alignbyte(w[1], w[0], 2), __builtin_amdgcn_alignbyte(w[2], w[1], 2)};
+                *reinterpret_cast<u32x2 *>(ln + 2) =
+                    u32x2{__builtin_amdgcn_alignbyte(w[3], w[2], 2), __builtin_amdgcn_alignbyte(w[4], w[3], 2)};
+                ln[4] = w[4] >> 16;
+            }
+        }
+    }
+};
+
+// zero the line tails of n halo images (never staged; the last windows read them against zero
+// weights); the channel pads are written with every position
+__device__ __forceinline__ void zero_pads_q(h16_t *img, int n) {
+    constexpr int PER = QLP - 18 * QPP;
+    for (int i = threadIdx.x; i < n * QNL * PER; i += QNT) {
+        const int l = i / PER, k = i - l * PER;
+        img[l * QLP + 18 * QPP + k] = 0;
+    }
+}
+
+// The window of one tap row for lane (n, kb): 8 elements at an even element offset (4 dwords)
+__device__ __forceinline__ hx8 win8(const h16_t *p) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+    return __builtin_bit_cast(hx8, uint4{q[0], q[1], q[2], q[3]});
+}
+
+// k^3 weights as the A operand, one fragment per tap row kk = kh * 3 + kw: A[m][k] with
+// k = kd * 10 + c (c < 9, kd < 3; the pad channel and k = 30, 31 zero).  Forward: m = co, c = ci,
+// tap kk * 3 + kd.  Backward-data (transposed, flipped): m = ci, c = co, tap 26 - (kk * 3 + kd).
+template <bool DGRAD>
+__device__ __forceinline__ hx8 w2_afrag(const float *w2, int kk, int lane) {
+    const int m = lane & 15, kb = lane >> 4;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * kb + j, kd = k / QPP, c = k - QPP * kd;
+        float x = 0.f;
+        if (m < BR && c < BR && kd < 3) {
+            const int tap = kk * 3 + kd;
+            x = DGRAD ? w2[(c * BR + m) * 27 + 26 - tap] : w2[(m * BR + c) * 27 + tap];
+        }
+        v[j] = x;
+    }
+    return pack8(v);
+}
+
+// The K order of the 1x1 convs fed from a k^3 / 1x1 accumulator: lane-group kb supplies channels
+// 4kb .. 4kb + 3 as k = 8kb .. 8kb + 3 (9-channel inputs), and for 18-channel inputs (two
+// accumulator tiles; the second tile's rows 12, 13 are channels 16, 17, so lane-group 3 holds
+// channels 12 .. 17) kb = 3 also channels 16, 17 as k = 28, 29.  Channel of K entry k (-1: zero).
+__device__ __forceinline__ int k_chan9(int k) {
+    const int kb = k >> 3, i = k & 7;
+    return (i < 4 && 4 * kb + i < BR) ? 4 * kb + i : -1;
+}
+__device__ __forceinline__ int k_chan18(int k) {
+    const int kb = k >> 3, i = k & 7;
+    return i < 4 ? 4 * kb + i : (kb == 3 && i < 6) ? 16 + i - 4 : -1;
+}
+
+// 9-channel voxel rows (18 bytes, only 2-byte aligned) in the accumulator layout: lane-group kb
+// (< 2) needs channels 4kb .. 4kb + 3 of voxel v, kb = 2 channel 8.  Every lane loads the 3
+// dwords around its values with one dword-aligned load that stays inside the tensor (the only
+// voxel whose row ends the tensor is odd, and odd rows never read past their own end).
+// (one native 3-dword vector: the register tuple a dwordx3 load writes is then the loop-carried
+// value itself -- a struct of three scalars made the tile loop copy every prefetched operand at its
+// back edge, which waits for the loads to land)
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+using Raw9 = u32x3;
+__device__ __forceinline__ int q9_kb(int kb) { return kb == 3 ? 0 : kb; }
+__device__ __forceinline__ Raw9 ld9(const h16_t *__restrict__ base, uint32_t v, int kb) {
+    const int k = q9_kb(kb);
+    const uint32_t s = v * (2 * BR) + 8 * k;
+    const uint32_t a = (s & ~3u) - (k == 2 ? 8 : 0);
+    u32x3 r;
+    __builtin_memcpy(&r, reinterpret_cast<const char *>(base) + a, 12);
+    return r;
+}
+// the 4 values of lane-group kb (kb 2: one value; kb 3: none) as floats, 0 where invalid
+__device__ __forceinline__ void ex9(const Raw9 &r, uint32_t v, int kb, float (&o)[4]) {
+    const int k = q9_kb(kb);
+    const uint32_t sub = uint32_t(v & 1) * 2u;  // 18 v mod 4
+    const bool hi = k == 2;
+    const uint32_t lo = hi ? r.z : r.x, mid = hi ? 0u : r.y, top = hi ? 0u : r.z;
+    const uint32_t p0 = __builtin_amdgcn_alignbyte(mid, lo, sub), p1 = __builtin_amdgcn_alignbyte(top, mid, sub);
+    o[0] = kb == 3 ? 0.f : bf(p0 & 0xffffu);
+    o[1] = kb >= 2 ? 0.f : bf(p0 >> 16);
+    o[2] = kb >= 2 ? 0.f : bf(p1 & 0xffffu);
+    o[3] = kb >= 2 ? 0.f : bf(p1 >> 16);
+}
+// 18-channel rows (36 bytes, dword aligned): channels 4kb .. 4kb + 5 (one dwordx3; lane-group 3
+// uses all six: 12 .. 15 and 16, 17)
+using Raw18 = u32x3;
+__device__ __forceinline__ Raw18 ld18(const h16_t *__restrict__ base, uint32_t v, int kb) {
+    u32x3 r;
+    __builtin_memcpy(&r, reinterpret_cast<const char *>(base) + size_t(v * (2 * C) + 8 * kb), 12);
+    return r;
+}
+
+// Outputs leave through a per-wave LDS image of the run (16 voxels: an 18-channel tensor's 576
+// contiguous bytes, then two 9-channel tensors' 288 each = 72 16-byte chunks) and one pass of
+// contiguous 16-byte stores: stored straight from the accumulator layout they would be 8-byte
+// pieces at a 36-byte stride, which the store path moves several times slower.  The image is
+// written and read by the same wave (LDS keeps a wave's accesses in order: no barrier).
+constexpr int QO9A = 16 * C, QO9B = QO9A + 16 * BR;  // element offsets of the 9-channel images
+__device__ __forceinline__ uint32_t pk2(float a, float b) { return uint32_t(f2h(a)) | (uint32_t(f2h(b)) << 16); }
+// channels 4kb .. 4kb + 3 of voxel n (lane-group 3 also 16, 17) of the 18-channel image
+__device__ __forceinline__ void put18(h16_t *st, int n, int kb, const float (&v)[6]) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(st + n * C + 4 * kb);  // 36 n + 8 kb bytes: dword aligned
+    // separate b32 stores: merged into a b64 they would be misaligned for odd n (64-cycle replays)
+    p[0] = pk2(v[0], v[1]);
+    asm volatile("" ::: "memory");
+    p[1] = pk2(v[2], v[3]);
+    asm volatile("" ::: "memory");
+    if (kb == 3) p[2] = pk2(v[4], v[5]);
+}
+// channels 4kb .. 4kb + 3 (kb 2: channel 8) of voxel n of a 9-channel image
+__device__ __forceinline__ void put9(h16_t *st, int n, int kb, const float (&v)[4]) {
+    h16_t *p = st + n * BR + 4 * kb;
+    if (kb < 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) p[j] = f2h(v[j]);
+    } else if (kb == 2) {
+        p[0] = f2h(v[0]);
+    }
+}
+// the image to the run's rows (d18: 18-channel rows, d9a / d9b: 9-channel rows; null = absent)
+__device__ __forceinline__ void flush_run(const h16_t *st, int lane, h16_t *__restrict__ d18,
+                                          h16_t *__restrict__ d9a, h16_t *__restrict__ d9b) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(st);
+    const uint4 q0 = src[lane];
+    if (lane < 36) {
+        reinterpret_cast<uint4 *>(d18)[lane] = q0;
+    } else if (lane < 54) {
+        if (d9a) reinterpret_cast<uint4 *>(d9a)[lane - 36] = q0;
+    } else if (d9b) {
+        reinterpret_cast<uint4 *>(d9b)[lane - 54] = q0;
+    }
+    if (lane < 8 && d9b) reinterpret_cast<uint4 *>(d9b)[10 + lane] = src[64 + lane];
+}
+
+// K2: per 4 x 4 x 16 tile: gt2 = W2^T (*) gz3 (flipped taps) -> gz1 = bf16(gt2 * elu'(t2)) ->
+// gx = g + (W1^T gz1) * elu'(x + b1a); gz1 to the workspace (k_pm_w13grad) and the b2 / b1 sums.
 // CHAIN (the chained backward of a run of blocks): the PREVIOUS block's K1 -- its gz3 and its four
-// scalar partials, k_pm_bwd1's arithmetic -- from this tile's gx while it is still in LDS (gx is
-// that block's g) and the previous block's t3, instead of a k_pm_bwd1 launch re-reading gx.
-template <int TH, int TW, bool CHAIN>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE))) void k_pm_bwd2(PmArgs a, const bf16_t *__restrict__ gz3, const bf16_t *__restrict__ t2,
-                                                const bf16_t *__restrict__ x, const bf16_t *__restrict__ g,
-                                                const float *__restrict__ w1, const float *__restrict__ w2,
-                                                vq3d_preact_params p, bf16_t *__restrict__ gx,
-                                                bf16_t *__restrict__ gz1o, float *__restrict__ part,
-                                                const bf16_t *__restrict__ t3p, const float *__restrict__ w3p,
-                                                vq3d_preact_params pp, bf16_t *__restrict__ gz3p,
-                                                float *__restrict__ part1p) {
-    using T = Tile<TH, TW>;
+// scalar partials, k_pm_bwd1's arithmetic -- from this tile's gx still in registers (gx is that
+// block's g) and the previous block's t3, instead of a k_pm_bwd1 launch re-reading gx.
+template <bool CHAIN>
+__global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE))) void k_pm_bwd2(
+    PmArgs a, const h16_t *__restrict__ gz3, const h16_t *__restrict__ t2, const h16_t *__restrict__ x,
+    const h16_t *__restrict__ g, const float *__restrict__ w1, const float *__restrict__ w2, vq3d_preact_params p,
+    h16_t *__restrict__ gx, h16_t *__restrict__ gz1o, float *__restrict__ part, const h16_t *__restrict__ t3p,
+    const float *__restrict__ w3p, vq3d_preact_params pp, h16_t *__restrict__ gz3p, float *__restrict__ part1p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *zl = reinterpret_cast<bf16_t *>(smem);  // gz3 halo lines; CHAIN: then the previous gz3 [TV][9]
-    bf16_t *t2s = zl + T::LINES;                      // t2 of the tile [TV][9] (only elu'(t2) is needed)
-    bf16_t *z1s = t2s + T::S9;                        // gz1 [TV][9]
-    bf16_t *xs = z1s + T::S9;                         // x [TV][18]
-    bf16_t *gs = xs + T::S18;                         // g [TV][18], then gx in place
-    float *w1s = reinterpret_cast<float *>(gs + T::S18);  // W1 [o][c]
-    float *red = w1s + BR * C;                            // [32] block sums
-    float *w3ps = red + 32;                               // CHAIN: previous W3 [co][o]
-    bf16_t *t3ps = reinterpret_cast<bf16_t *>(w3ps + C * BR);  // CHAIN: previous t3 [TV][9]
-    static_assert(T::LINES >= T::TV * BR, "previous gz3 fits the halo image");
+    h16_t *img = reinterpret_cast<h16_t *>(smem);              // 2 halo images [QNL][QLP]
+    hx8 *frag = reinterpret_cast<hx8 *>(img + 2 * QIMG);  // A fragments [12][64]: W2 tap rows, W1^T x 2, W3^T
+    h16_t *stg = reinterpret_cast<h16_t *>(frag + 12 * 64);    // [QNW waves][QSTG] output images
+    float *red = reinterpret_cast<float *>(stg + QNW * QSTG);  // [32] block sums
+    // prologue only: the fp32 weights W2 [NW2], W1 [o][c], previous W3 [co][o] over the halo images
+    float *ws2 = reinterpret_cast<float *>(smem), *ws1 = ws2 + NW2, *ws3 = ws1 + BR * C;
+    static_assert((2 * QIMG * 2) % 16 == 0 && (QNW * QSTG * 2) % 16 == 0, "carve alignment");
+    static_assert(size_t(NW2 + 2 * BR * C) * 4 <= size_t(2 * QIMG) * 2, "weights fit the halo images");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int row = lane & 15, kb = lane >> 4;
-    if constexpr (CHAIN) stage_w(w3ps, w3p, C * BR);
-    bf16x8 bw2[9], bw1[2], bw3p = {};
-    {
-        float *w2s = reinterpret_cast<float *>(smem);  // scratch over the halo image
-        static_assert(T::LINES * 2 >= NW2 * 4, "W2 fits the halo image");
-        stage_w(w2s, w2, NW2);
-        stage_w(w1s, w1, BR * C);
-        __syncthreads();
+    const int n = lane & 15, kb = lane >> 4;
+    for (int i = tid; i < NW2; i += QNT) ws2[i] = w2[i];
+    for (int i = tid; i < BR * C; i += QNT) ws1[i] = w1[i];
+    if constexpr (CHAIN)
+        for (int i = tid; i < C * BR; i += QNT) ws3[i] = w3p[i];
+    __syncthreads();
+    // the MFMA A fragments (lane-linear images, one ds_read_b128 per use: weights in VGPRs would
+    // leave no room for the tile-ahead prefetch), fragment f built by wave f % 8
+    for (int f = wave; f < 12; f += QNW) {
+        hx8 fr = {};
+        if (f < 9) {
+            fr = w2_afrag<true>(ws2, f, lane);
+        } else if (f < 11) {  // W1^T: A[m -> c][k -> o]; tile 1: rows 12, 13 = channels 16, 17
+            float v[8];
+            const int c = f == 10 ? (n >= 12 ? 16 + n - 12 : C) : n;
 #pragma unroll
-        for (int kk = 0; kk < 9; ++kk) bw2[kk] = w2_frag<true>(w2s, kk, lane);
-        // W1^T for gt1 = W1^T gz1 (B[k = o][n = c], two 16-channel n-tiles) and, chained, the
-        // previous block's W3^T for its gz3 (B[k = co][n = o]); k >= 9 / 18 rows are zero
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
+            for (int j = 0; j < 8; ++j) {
+                const int o = k_chan9(8 * kb + j);
+                v[j] = (o >= 0 && c < C) ? ws1[o * C + c] : 0.f;
+            }
+            fr = pack8(v);
+        } else if (CHAIN) {  // previous W3^T: A[m = o][k -> co]
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int o = 8 * kb + j, c = 16 * nt + row;
-                v[j] = (o < BR && c < C) ? w1s[o * C + c] : 0.f;
+                const int co = k_chan18(8 * kb + j);
+                v[j] = (co >= 0 && n < BR) ? ws3[co * BR + n] : 0.f;
             }
-            bw1[nt] = pack8(v);
+            fr = pack8(v);
         }
-        if constexpr (CHAIN) {
-            float v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int co = 8 * kb + j;
-                v[j] = (co < C && row < BR) ? w3ps[co * BR + row] : 0.f;
-            }
-            bw3p = pack8(v);
-        }
-        __syncthreads();
+        frag[f * 64 + lane] = fr;
     }
-    {
-        bf16_t *tails[3] = {z1s, xs, gs};
-        const int at[3] = {T::TV * BR, T::TV * C, T::TV * C};
-        zero_pads<TH, TW>(zl, 1, tails, at, 3);
-    }
+    __syncthreads();  // the weights are read: the halo images' pads can be zeroed
+    zero_pads_q(img, 2);
     const Scal s = load_scal(p);
-    float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
     Scal sp{};
     if constexpr (CHAIN) sp = load_scal(pp);
+    float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f;
     float q4 = 0.f, q3b = 0.f, q3a = 0.f, qsc = 0.f;  // CHAIN: the previous block's K1 sums
-    // the next tile's gz3 halo and t2 loads are in flight while the current tile computes
-    LinesLd<TH, TW> lz;
-    TileLd<TH, TW, BR> lt;
+    // the wave's two D-runs: rows ph, ph + 1 of tile column pw (run coordinates inside the tile)
+    const int ph = (wave >> 2) * 2, pw = wave & 3;
+    HaloQ hz;
+    Raw9 et2[2], et3[2];
+    Raw18 ex[2], eg[2];
+    // every per-thread index below derives from a copy of the thread index laundered once per tile:
+    // the address arithmetic is then recomputed per tile (a few VALU ops) instead of being hoisted
+    // out of the tile loop as dozens of live loop invariants
+    auto launder = [](int v) {
+        asm volatile("" : "+v"(v));
+        return v;
+    };
+    auto run_vox0 = [&](const Org &o, int r) {  // first voxel of the wave's run r (0, 1)
+        return ((uint32_t(o.b) * a.H + o.h0 + ph + r) * a.W + o.w0 + pw) * a.D + o.d0;
+    };
+    auto load_ep = [&](int ln, const Org &o, int r) {
+        const int nn = ln & 15, kq = ln >> 4;
+        const uint32_t v = run_vox0(o, r) + nn;
+        et2[r] = ld9(t2, v, kq);
+        ex[r] = ld18(x, v, kq);
+        eg[r] = ld18(g, v, kq);
+        if constexpr (CHAIN) et3[r] = ld9(t3p, v, kq);
+    };
     const TileSched sc = xcd_sched(a.ntiles);
     if (sc.t < sc.end) {
-        const Org o0 = tile_org(a, sc.t, TH, TW);
-        lz.load(a, o0, gz3);
-        lt.load(a, o0, t2);
+        const Org o0 = tile_org_q(a, sc.t);
+        hz.load(tid, a, o0, gz3);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) load_ep(lane, o0, r);
     }
-    for (int tile = sc.t; tile < sc.end; tile += sc.step) {
-        const Org o = tile_org(a, tile, TH, TW);
+    int it = 0;
+    for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) {
+        const Org o = tile_org_q(a, tile);
+        const bool more = tile + sc.step < sc.end;
+        const Org on = tile_org_q(a, more ? tile + sc.step : tile);
+        const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
+        h16_t *hl = img + (it & 1) * QIMG;
+        if constexpr (!(PM_EXP & 16)) hz.store(tl, hl);
+        if constexpr (!(PM_EXP & 1024)) hz.load(tl, a, on, gz3);
         __syncthreads();
-        if constexpr (!(PM_EXP & 16)) {
-            TileLd<TH, TW, C> lx, lg;
-            TileLd<TH, TW, BR> l3;
-            lx.load(a, o, x);
-            lg.load(a, o, g);
-            if constexpr (CHAIN) l3.load(a, o, t3p);
-            lz.store(zl);
-            lt.store(t2s);
-            if (tile + sc.step < sc.end) {
-                const Org on = tile_org(a, tile + sc.step, TH, TW);
-                lz.load(a, on, gz3);
-                lt.load(a, on, t2);
-            }
-            lx.store(xs);
-            lg.store(gs);
-            if constexpr (CHAIN) l3.store(t3ps);
-        }
-        __syncthreads();
-        for (int mt = (PM_EXP & 32) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
-            const int vt = mt * 16 + row, r = vt >> 3, d = vt & 7;
-            const int base = ((r / TW) * T::LW + r % TW) * LSP + LOFF + 9 * d + 8 * kb;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        // gt2 of the wave's 2 runs: input line (i, j) of the 4 x 3 they need feeds run r through tap
+        // row (i - r, j)
+        f32x4 acc[2];
 #pragma unroll
-            for (int kk = 0; kk < 9; ++kk)
-                acc = mfma(read8(zl, base + ((kk / 3) * T::LW + kk % 3) * LSP), bw2[kk], acc);
-            if (row < BR) {
+        for (int r = 0; r < 2; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (!(PM_EXP & 32)) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int v = mt * 16 + 4 * kb + j;
-                    const float t2v = bf(t2s[v * BR + row]);
-                    const float z1 = acc[j] * elu_d_act(t2v, s.b2b);
-                    s2b += acc[j];
-                    s2a += z1;
-                    z1s[v * BR + row] = f2bf(z1);
-                }
-            }
-        }
-        __syncthreads();
-        // gx = g + (W1^T gz1) * elu'(x + b1a): gt1 on the matrix cores (16 voxels x 2 16-channel
-        // tiles per wave step, K = the 9 branch channels), the epilogue per (voxel, channel) lane
-        for (int mt = (PM_EXP & 64) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
-            const bf16x8 af = read8(z1s, (mt * 16 + row) * BR + 8 * kb);
+            for (int i = 0; i < 4; ++i) {
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                const f32x4 acc = mfma(af, bw1[nt], f32x4{0.f, 0.f, 0.f, 0.f});
-                const int c = 16 * nt + row;
-                if (c < C) {
+                for (int j = 0; j < 3; ++j) {
+                    const hx8 bw = win8(hl + ((ph + i) * QLW + pw + j) * QLP + nl * QPP + 8 * kl);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int i = (mt * 16 + 4 * kb + j) * C + c;
-                        const float gt1 = acc[j];
-                        const float zx = bf(xs[i]) + s.b1a;
-                        const float ez = zx > 0.f ? 1.f : expf(zx);
-                        s1b += gt1;
-                        s1a += gt1 * ez;
-                        const bf16_t gb = f2bf(bf(gs[i]) + gt1 * ez);
-                        gs[i] = gb;
-                        if constexpr (CHAIN) q4 += bf(gb);  // the previous block's g = this gx
+                    for (int r = 0; r < 2; ++r) {
+                        const int kh = i - r;
+                        if (kh >= 0 && kh < 3) acc[r] = mfma(frag[(kh * 3 + j) * 64 + ln], bw, acc[r]);
                     }
                 }
+                asm volatile("" ::: "memory");  // one row of windows in registers at a time
             }
         }
-        __syncthreads();
-        if constexpr (CHAIN) {
-            // previous block: gz3 = bf16(scale W3^T gx * elu'(t3)) into the free halo image (one
-            // MFMA per 16 voxels, K = the 18 channels of gx)
-            for (int mt = (PM_EXP & 128) ? T::NMT : wave; mt < T::NMT; mt += NT / 64) {
-                const f32x4 acc = mfma(read8(gs, (mt * 16 + row) * C + 8 * kb), bw3p, f32x4{0.f, 0.f, 0.f, 0.f});
-                if (row < BR) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t v0 = run_vox0(o, r), v = v0 + nl;
+            h16_t *st = stg + wave * QSTG;
+            // gz1 = bf16(gt2 * elu'(t2)) for channels 4kb + j
+            float t2v[4], z1[4];
+            ex9(et2[r], v, kl, t2v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = 4 * kl + j < BR;
+                const float z = acc[r][j] * elu_d_act(t2v[j], s.b2b);
+                z1[j] = ok ? bf(f2h(z)) : 0.f;
+                s2b += ok ? acc[r][j] : 0.f;
+                s2a += ok ? z : 0.f;
+            }
+            // gt1 = W1^T gz1 (two channel tiles), gx = g + gt1 * elu'(x + b1a)
+            float gxv[6];
+            if constexpr (!(PM_EXP & 64)) {
+                const hx8 bz = pack8({z1[0], z1[1], z1[2], z1[3], 0.f, 0.f, 0.f, 0.f});
+                const f32x4 a0 = mfma(frag[9 * 64 + ln], bz, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a1 = mfma(frag[10 * 64 + ln], bz, f32x4{0.f, 0.f, 0.f, 0.f});
+                const Raw18 &xr = ex[r], &gr = eg[r];
+                const float xv[6] = {bf(xr.x & 0xffffu), bf(xr.x >> 16), bf(xr.y & 0xffffu), bf(xr.y >> 16),
+                                     bf(xr.z & 0xffffu), bf(xr.z >> 16)};
+                const float gv[6] = {bf(gr.x & 0xffffu), bf(gr.x >> 16), bf(gr.y & 0xffffu), bf(gr.y >> 16),
+                                     bf(gr.z & 0xffffu), bf(gr.z >> 16)};
+                const float gt1[6] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1]};
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const bool ok = j < 4 || kl == 3;  // channels 4kb + j, then (kb 3) 16 / 17
+                    const float zx = xv[j] + s.b1a;
+                    const float ez = zx > 0.f ? 1.f : __expf(zx);
+                    s1b += ok ? gt1[j] : 0.f;
+                    s1a += ok ? gt1[j] * ez : 0.f;
+                    gxv[j] = ok ? bf(f2h(gv[j] + gt1[j] * ez)) : 0.f;
+                    if constexpr (CHAIN) q4 += gxv[j];  // the previous block's g = this gx
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) gxv[j] = z1[j & 3];
+            }
+            if constexpr (!(PM_EXP & 256)) {
+                put18(st, nl, kl, gxv);
+                put9(st + QO9A, nl, kl, z1);
+            }
+            if constexpr (CHAIN) {
+                // previous block: gz3 = bf16(scale W3^T gx * elu'(t3)) (one MFMA, K = the 18 channels
+                // of gx in the k_chan18 order)
+                if constexpr (!(PM_EXP & 128)) {
+                    const hx8 bg = pack8({gxv[0], gxv[1], gxv[2], gxv[3], gxv[4], gxv[5], 0.f, 0.f});
+                    const f32x4 a3 = mfma(frag[11 * 64 + ln], bg, f32x4{0.f, 0.f, 0.f, 0.f});
+                    float t3v[4], zq[4];
+                    ex9(et3[r], v, kl, t3v);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const int v = mt * 16 + 4 * kb + j;
-                        const float a3 = acc[j], tv = bf(t3ps[v * BR + row]);
-                        const float gt3 = a3 * sp.sc;
-                        const float z = gt3 * elu_d_act(tv, sp.b3b);
-                        q3b += gt3;
-                        q3a += z;
-                        qsc = fmaf(a3, tv, qsc);
-                        zl[v * BR + row] = f2bf(z);
+                        const bool ok = 4 * kl + j < BR;
+                        const float gt3 = a3[j] * sp.sc;
+                        const float z = gt3 * elu_d_act(t3v[j], sp.b3b);
+                        q3b += ok ? gt3 : 0.f;
+                        q3a += ok ? z : 0.f;
+                        qsc += ok ? a3[j] * t3v[j] : 0.f;
+                        zq[j] = z;
                     }
+                    if constexpr (!(PM_EXP & 256)) put9(st + QO9B, nl, kl, zq);
                 }
             }
-        }
-        if constexpr (!(PM_EXP & 256)) {
-            store_tile<TH, TW, C>(a, o, gs, gx);
-            store_tile<TH, TW, BR>(a, o, z1s, gz1o);
-        }
-        if constexpr (CHAIN) {
-            __syncthreads();
-            if constexpr (!(PM_EXP & 256)) store_tile<TH, TW, BR>(a, o, zl, gz3p);
+            if constexpr (!(PM_EXP & 256))
+                flush_run(st, ln, gx + size_t(v0) * C, gz1o + size_t(v0) * BR, CHAIN ? gz3p + size_t(v0) * BR : nullptr);
+            // the next tile's operands of this run (unconditional: on = this tile at the end; a
+            // branch would keep the old values live)
+            if constexpr (!(PM_EXP & 512)) load_ep(ln, on, r);
+            if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);  // one run's epilogue at a time (no interleaving)
         }
     }
     if constexpr (CHAIN) {
         float *dp = part1p + int64_t(blockIdx.x) * NE1;
-        const float t4 = block_sum<float, NT>(q4, red);
-        const float t3b = block_sum<float, NT>(q3b, red + 8);
-        const float t3a = block_sum<float, NT>(q3a, red + 16);
-        const float tsc = block_sum<float, NT>(qsc, red + 24);
+        const float t4 = block_sum<float, QNT>(q4, red);
+        const float t3b = block_sum<float, QNT>(q3b, red + 8);
+        const float t3a = block_sum<float, QNT>(q3a, red + 16);
+        const float tsc = block_sum<float, QNT>(qsc, red + 24);
         if (tid == 0) {
             dp[0] = t4;
             dp[1] = t3b;
@@ -764,15 +889,167 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE))
         }
     }
     float *dst = part + int64_t(blockIdx.x) * NE2;
-    const float t2b = block_sum<float, NT>(s2b, red);
-    const float t2a = block_sum<float, NT>(s2a, red + 8);
-    const float t1b = block_sum<float, NT>(s1b, red + 16);
-    const float t1a = block_sum<float, NT>(s1a, red + 24);
+    const float t2b = block_sum<float, QNT>(s2b, red);
+    const float t2a = block_sum<float, QNT>(s2a, red + 8);
+    const float t1b = block_sum<float, QNT>(s1b, red + 16);
+    const float t1a = block_sum<float, QNT>(s1a, red + 24);
     if (tid == 0) {
         dst[0] = t2b;
         dst[1] = t2a;
         dst[2] = t1b;
         dst[3] = t1a;
+    }
+}
+
+// The forward tile kernel on the same 4 x 4 x 16 tiles: t3 = elu(W2 (*) t2 + b3a) + b3b from t2 on
+// the tile's halo, out = scale W3 t3 + b4 + x, and CHAIN: the next block's t2 = elu(W1' u1 + b2a')
+// + b2b' with u1 = elu(out + b1a') + b1b' -- each stage's accumulator the next stage's B operand
+// (the k_chan9 / k_chan18 K orders), x loaded straight into the accumulator layout a tile ahead.
+// Rounding points: t3, out, u1 and the next t2 to bf16 (the per-conv path's; W2 / W3 / W1' as bf16
+// matrix-core operands).
+template <bool CHAIN>
+__global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE))) void k_pm_fwd(
+    PmArgs a, const h16_t *__restrict__ t2, const h16_t *__restrict__ x, const float *__restrict__ w2,
+    const float *__restrict__ w3, vq3d_preact_params p, h16_t *__restrict__ t3o, h16_t *__restrict__ out,
+    const float *__restrict__ w1n, vq3d_preact_params pn, h16_t *__restrict__ t2n) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    h16_t *img = reinterpret_cast<h16_t *>(smem);              // 2 halo images [QNL][QLP]
+    hx8 *frag = reinterpret_cast<hx8 *>(img + 2 * QIMG);  // A fragments [12][64]: W2 tap rows, W3 x 2, W1'
+    h16_t *stg = reinterpret_cast<h16_t *>(frag + 12 * 64);    // [QNW waves][QSTG] output images
+    float *ws2 = reinterpret_cast<float *>(smem), *ws3 = ws2 + NW2, *ws1 = ws3 + C * BR;  // prologue only
+    static_assert(size_t(NW2 + 2 * BR * C) * 4 <= size_t(2 * QIMG) * 2, "weights fit the halo images");
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = lane & 15, kb = lane >> 4;
+    for (int i = tid; i < NW2; i += QNT) ws2[i] = w2[i];
+    for (int i = tid; i < C * BR; i += QNT) ws3[i] = w3[i];
+    if constexpr (CHAIN)
+        for (int i = tid; i < BR * C; i += QNT) ws1[i] = w1n[i];
+    __syncthreads();
+    for (int f = wave; f < 12; f += QNW) {
+        hx8 fr = {};
+        if (f < 9) {
+            fr = w2_afrag<false>(ws2, f, lane);
+        } else if (f < 11) {  // W3: A[m -> co][k -> o]; tile 1: rows 12, 13 = channels 16, 17
+            float v[8];
+            const int co = f == 10 ? (n >= 12 ? 16 + n - 12 : C) : n;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int o = k_chan9(8 * kb + j);
+                v[j] = (o >= 0 && co < C) ? ws3[co * BR + o] : 0.f;
+            }
+            fr = pack8(v);
+        } else if (CHAIN) {  // the next block's W1: A[m = o][k -> c]
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = k_chan18(8 * kb + j);
+                v[j] = (c >= 0 && n < BR) ? ws1[n * C + c] : 0.f;
+            }
+            fr = pack8(v);
+        }
+        frag[f * 64 + lane] = fr;
+    }
+    __syncthreads();
+    zero_pads_q(img, 2);
+    const Scal s = load_scal(p);
+    Scal sn{};
+    if constexpr (CHAIN) sn = load_scal(pn);
+    const int ph = (wave >> 2) * 2, pw = wave & 3;
+    HaloQ ht;
+    Raw18 ex[2];
+    auto launder = [](int v) {
+        asm volatile("" : "+v"(v));
+        return v;
+    };
+    auto run_vox0 = [&](const Org &o, int r) {
+        return ((uint32_t(o.b) * a.H + o.h0 + ph + r) * a.W + o.w0 + pw) * a.D + o.d0;
+    };
+    const TileSched sc = xcd_sched(a.ntiles);
+    if (sc.t < sc.end) {
+        const Org o0 = tile_org_q(a, sc.t);
+        ht.load(tid, a, o0, t2);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) ex[r] = ld18(x, run_vox0(o0, r) + n, kb);
+    }
+    int it = 0;
+    for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) {
+        const Org o = tile_org_q(a, tile);
+        const bool more = tile + sc.step < sc.end;
+        const Org on = tile_org_q(a, more ? tile + sc.step : tile);
+        const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
+        h16_t *hl = img + (it & 1) * QIMG;
+        if constexpr (!(PM_EXP & 8)) ht.store(tl, hl);
+        if constexpr (!(PM_EXP & 2048)) ht.load(tl, a, on, t2);
+        __syncthreads();
+        f32x4 acc[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (!(PM_EXP & 1)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const hx8 bw = win8(hl + ((ph + i) * QLW + pw + j) * QLP + nl * QPP + 8 * kl);
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const int kh = i - r;
+                        if (kh >= 0 && kh < 3) acc[r] = mfma(frag[(kh * 3 + j) * 64 + ln], bw, acc[r]);
+                    }
+                }
+                asm volatile("" ::: "memory");  // one row of windows in registers at a time
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t v0 = run_vox0(o, r);
+            h16_t *st = stg + wave * QSTG;
+            float t3v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                t3v[j] = 4 * kl + j < BR ? bf(f2h(elu_fast(acc[r][j] + s.b3a) + s.b3b)) : 0.f;
+            float ov[6];
+            if constexpr (!(PM_EXP & 2)) {
+                const hx8 bt = pack8({t3v[0], t3v[1], t3v[2], t3v[3], 0.f, 0.f, 0.f, 0.f});
+                const f32x4 a0 = mfma(frag[9 * 64 + ln], bt, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a1 = mfma(frag[10 * 64 + ln], bt, f32x4{0.f, 0.f, 0.f, 0.f});
+                const Raw18 &xr = ex[r];
+                const float xv[6] = {bf(xr.x & 0xffffu), bf(xr.x >> 16), bf(xr.y & 0xffffu), bf(xr.y >> 16),
+                                     bf(xr.z & 0xffffu), bf(xr.z >> 16)};
+                const float o3[6] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1]};
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const bool ok = j < 4 || kl == 3;  // channels 4kb + j, then (kb 3) 16 / 17
+                    ov[j] = ok ? bf(f2h(o3[j] * s.sc + s.b4 + xv[j])) : 0.f;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) ov[j] = t3v[j & 3];
+            }
+            if constexpr (!(PM_EXP & 4)) {
+                put18(st, nl, kl, ov);
+                if (t3o) put9(st + QO9A, nl, kl, t3v);
+            }
+            if constexpr (CHAIN) {
+                // the next block's u1 (k_pm_t2's rounding points) and t2
+                float u1[6];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const bool ok = j < 4 || kl == 3;
+                    u1[j] = ok ? bf(f2h(elu_fast(ov[j] + sn.b1a) + sn.b1b)) : 0.f;
+                }
+                const hx8 bu = pack8({u1[0], u1[1], u1[2], u1[3], u1[4], u1[5], 0.f, 0.f});
+                const f32x4 a2 = mfma(frag[11 * 64 + ln], bu, f32x4{0.f, 0.f, 0.f, 0.f});
+                float tn[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) tn[j] = elu_fast(a2[j] + sn.b2a) + sn.b2b;
+                if constexpr (!(PM_EXP & 4)) put9(st + QO9B, nl, kl, tn);
+            }
+            if constexpr (!(PM_EXP & 4))
+                flush_run(st, ln, out + size_t(v0) * C, t3o ? t3o + size_t(v0) * BR : nullptr,
+                          CHAIN ? t2n + size_t(v0) * BR : nullptr);
+            if constexpr (!(PM_EXP & 2048)) ex[r] = ld18(x, run_vox0(on, r) + nl, kl);  // next tile's x (unconditional)
+            if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);
+        }
     }
 }
 
@@ -802,23 +1079,23 @@ struct W2c {
     static_assert(NL * D == CHV && TH * TW == NL, "chunk");
 };
 
-__device__ __forceinline__ void scatter9(bf16_t *dst, int pitch, int e0, u32x4 q, int base) {
+__device__ __forceinline__ void scatter9(h16_t *dst, int pitch, int e0, u32x4 q, int base) {
     // the 8 elements e0 .. e0 + 7 of a 9-channel voxel-major run to dst[c * pitch + base + pos]
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int e = e0 + j, pos = e / BR, c = e - pos * BR;
-        dst[c * pitch + base + pos] = bf16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+        dst[c * pitch + base + pos] = h16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
     }
 }
 
 template <int D>
-__global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const bf16_t *__restrict__ gz3,
-                                                   const bf16_t *__restrict__ t2, float *__restrict__ p2a) {
+__global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const h16_t *__restrict__ gz3,
+                                                   const h16_t *__restrict__ t2, float *__restrict__ p2a) {
     using K = W2c<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *zT = reinterpret_cast<bf16_t *>(smem);  // gz3 [16][ZP] channel-major (rows >= 9 never read into results)
-    bf16_t *tT = zT + 16 * ZP;                      // t2 [9][HL][RPD] (+ tail)
+    h16_t *zT = reinterpret_cast<h16_t *>(smem);  // gz3 [16][ZP] channel-major (rows >= 9 never read into results)
+    h16_t *tT = zT + 16 * ZP;                      // t2 [9][HL][RPD] (+ tail)
     const int tid = threadIdx.x, lane = tid & 63, kk = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int kh = kk / 3, kw = kk - 3 * kh;
     const int nth = a.H / K::TH, ntw = a.W / K::TW;
@@ -872,11 +1149,11 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
             if (i < K::TQ) {
                 const int hl = i / K::QL, part = i - hl * K::QL;
                 const uint32_t w[4] = {vt[u].x, vt[u].y, vt[u].z, vt[u].w};
-                bf16_t *ln = tT + hl * K::RPD;
+                h16_t *ln = tT + hl * K::RPD;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int e = part * 8 + j, pos = e / BR, ci = e - pos * BR;
-                    const bf16_t v = bf16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                    const h16_t v = h16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
                     ln[ci * K::CSTR + pos + 1] = v;
                     if (pos == 0) ln[ci * K::CSTR + D + 1] = v;  // position D wraps to 0
                     if (pos == D - 1) ln[ci * K::CSTR] = v;      // position -1 wraps to D - 1
@@ -889,7 +1166,7 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
         for (int ks = 0; ks < CHV / 32; ++ks) {
             const int v = 32 * ks + 8 * kb, l = v / D, d0 = v - l * D;
             const int hl = (l / K::TW + kh) * K::LW + l % K::TW + kw;
-            const bf16x8 af = *reinterpret_cast<const bf16x8 *>(zT + row * ZP + v);
+            const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + v);
             const int off = hl * K::RPD + d0;
 #pragma unroll
             for (int n = 0; n < 2; ++n) acc[n] = mfma(af, read8(tT, toff[n] + off), acc[n]);
@@ -908,20 +1185,20 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
 // k_pm_w13grad: W1 (sum gz1 (x) u1, u1 = bf16(elu(x + b1a) + b1b)) and G3 (sum t3 (x) g) over npb
 // pieces of SUBV voxels per workgroup (the next piece's loads in flight); wave w: (W1 | G3,
 // 16-column tile)
-__global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const bf16_t *__restrict__ gz1,
-                                                   const bf16_t *__restrict__ t3, const bf16_t *__restrict__ x,
-                                                   const bf16_t *__restrict__ g, vq3d_preact_params p,
+__global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restrict__ gz1,
+                                                   const h16_t *__restrict__ t3, const h16_t *__restrict__ x,
+                                                   const h16_t *__restrict__ g, vq3d_preact_params p,
                                                    float *__restrict__ p2b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int ch = blockIdx.x;
     const Scal s = load_scal(p);
-    bf16_t *z1T = reinterpret_cast<bf16_t *>(smem);  // [16][SP] gz1
-    bf16_t *t3T = z1T + 16 * SP;                     // [16][SP] t3
-    bf16_t *u1T = t3T + 16 * SP;                     // [32][SP] u1
-    bf16_t *gT = u1T + 32 * SP;                      // [32][SP] g
+    h16_t *z1T = reinterpret_cast<h16_t *>(smem);  // [16][SP] gz1
+    h16_t *t3T = z1T + 16 * SP;                     // [16][SP] t3
+    h16_t *u1T = t3T + 16 * SP;                     // [32][SP] u1
+    h16_t *gT = u1T + 32 * SP;                      // [32][SP] g
     const int isG3 = wave >> 1, nt = wave & 1;
-    const bf16_t *aT = isG3 ? t3T : z1T, *bT = isG3 ? gT : u1T;
+    const h16_t *aT = isG3 ? t3T : z1T, *bT = isG3 ? gT : u1T;
     // per piece: gz1 / t3 SUBV * 9 / 8 16-B pieces each, x / g SUBV * 18 / 8 each
     constexpr int N9 = SUBV * BR / 8, N18 = SUBV * C / 8, NQ = 2 * N9 + 2 * N18, PQ = (NQ + NT - 1) / NT;
     u32x4 vq[PQ];
@@ -949,23 +1226,23 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const bf16_t *__rest
             if (i < NQ) {
                 const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
                 if (i < 2 * N9) {
-                    bf16_t *dT = i < N9 ? z1T : t3T;
+                    h16_t *dT = i < N9 ? z1T : t3T;
                     const int e0 = (i < N9 ? i : i - N9) * 8;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int e = e0 + j, v = e / BR, c = e - v * BR;
-                        dT[c * SP + v] = bf16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+                        dT[c * SP + v] = h16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
                     }
                 } else {
                     const bool isx = i < 2 * N9 + N18;
-                    bf16_t *dT = isx ? u1T : gT;
+                    h16_t *dT = isx ? u1T : gT;
                     const int e0 = (isx ? i - 2 * N9 : i - 2 * N9 - N18) * 8;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const int e = e0 + j, v = e / C, c = e - v * C;
                         uint32_t h = (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                        if (isx) h = f2bf(elu(bf(h) + s.b1a) + s.b1b);
-                        dT[c * SP + v] = bf16_t(h);
+                        if (isx) h = f2h(elu(bf(h) + s.b1a) + s.b1b);
+                        dT[c * SP + v] = h16_t(h);
                     }
                 }
             }
@@ -975,8 +1252,8 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const bf16_t *__rest
 #pragma unroll
         for (int ks = 0; ks < SUBV / 32; ++ks) {
             const int ko = 32 * ks + 8 * kb;
-            acc = mfma(*reinterpret_cast<const bf16x8 *>(aT + row * SP + ko),
-                       *reinterpret_cast<const bf16x8 *>(bT + (16 * nt + row) * SP + ko), acc);
+            acc = mfma(*reinterpret_cast<const hx8 *>(aT + row * SP + ko),
+                       *reinterpret_cast<const hx8 *>(bT + (16 * nt + row) * SP + ko), acc);
         }
     }
     float *dst = p2b + int64_t(ch) * NEB + isG3 * BR * C;
@@ -1072,20 +1349,13 @@ __global__ __launch_bounds__(NT) void k_pm_reduce_run(const char *__restrict__ b
 }
 
 // ============================================================================================ host
-constexpr int FTH = 4, FTW = 8;  // forward tile 4 x 8 x 8 (256 voxels)
 constexpr int BTH = 4, BTW = 8;  // backward tile
 
-template <int TH, int TW, bool CHAIN>
-size_t fwd_lds() {
-    using T = Tile<TH, TW>;
-    return size_t(T::LINES + T::S9 + T::S18) * 2 + (CHAIN ? size_t(BR * C) * 4 + size_t(T::S18) * 2 : 0);
-}
-template <int TH, int TW, bool CHAIN>
-size_t bwd_lds() {
-    using T = Tile<TH, TW>;
-    return size_t(T::LINES + 2 * T::S9 + 2 * T::S18) * 2 + size_t(BR * C + 32) * 4 +
-           (CHAIN ? size_t(C * BR) * 4 + size_t(T::S9) * 2 : 0);
-}
+// k_pm_fwd: the same carve as k_pm_bwd2 without the block sums
+constexpr size_t fwd_lds() { return size_t(2 * QIMG) * 2 + size_t(12 * 64) * 16 + size_t(QNW * QSTG) * 2; }
+// k_pm_bwd2: 2 halo images (the fp32 weights over them in the prologue), 12 A-fragment images, 8 waves' output
+// images, 32 sums
+constexpr size_t bwd_lds() { return size_t(2 * QIMG) * 2 + size_t(12 * 64) * 16 + size_t(QNW * QSTG) * 2 + 32 * 4; }
 
 int n_cu() {
     static int n = 0;
@@ -1098,9 +1368,9 @@ int n_cu() {
 }
 
 template <class K>
-int resident(K kern, size_t lds) {
+int resident(K kern, size_t lds, int threads = NT) {
     int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, NT, lds) != hipSuccess || per < 1) per = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, lds) != hipSuccess || per < 1) per = 1;
     (void)hipGetLastError();
     return per;
 }
@@ -1120,18 +1390,17 @@ PmArgs make_args(int B, int H, int W, int D, int TH, int TW) {
 
 // resident workgroups per CU of a tile kernel (dynamic LDS opted in once)
 template <class K>
-int per_cu(K kern, size_t lds) {
+int per_cu(K kern, size_t lds, int threads = NT) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               int(lds));
-    return resident(kern, lds);
+    return resident(kern, lds, threads);
 }
 // K2 grid: both variants must give the same count (the chained variant writes the previous
 // block's K1 partial rows, whose count the reduction assumes to be the K2 grid)
 int bwd2_blocks(const PmArgs &a) {
     static int per = 0;
     if (!per)
-        per = std::min(per_cu(k_pm_bwd2<BTH, BTW, false>, bwd_lds<BTH, BTW, false>()),
-                       per_cu(k_pm_bwd2<BTH, BTW, true>, bwd_lds<BTH, BTW, true>()));
+        per = std::min(per_cu(k_pm_bwd2<false>, bwd_lds(), QNT), per_cu(k_pm_bwd2<true>, bwd_lds(), QNT));
     if (PM_BWD_PER > 0) per = std::min(per, PM_BWD_PER);
     return std::max(1, std::min(a.ntiles, per * n_cu()));
 }
@@ -1140,7 +1409,7 @@ int bwd2_blocks(const PmArgs &a) {
 constexpr size_t w13_lds() { return size_t(96 * SP) * 2; }
 
 template <int D>
-void launch_w2(const PmArgs &a, int nwa, int npc, const bf16_t *gz3, const bf16_t *t2, float *p2a, hipStream_t s) {
+void launch_w2(const PmArgs &a, int nwa, int npc, const h16_t *gz3, const h16_t *t2, float *p2a, hipStream_t s) {
     static bool init = false;
     if (!init) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad<D>),
@@ -1153,27 +1422,24 @@ void launch_w2(const PmArgs &a, int nwa, int npc, const bf16_t *gz3, const bf16_
 void launch_fwd(int batch, int h, int w, int dd, const void *x, const float *w2, const float *w3,
                 const vq3d_preact_params &p, void *out, const void *t2, void *t3, const float *w1n,
                 const vq3d_preact_params *pn, void *t2n, hipStream_t s) {
-    const PmArgs a = make_args(batch, h, w, dd, FTH, FTW);
+    const PmArgs a = make_args_q(batch, h, w, dd);
     static int per = 0;
-    if (!per)
-        per = std::min(per_cu(k_pm_fwd<FTH, FTW, false>, fwd_lds<FTH, FTW, false>()),
-                       per_cu(k_pm_fwd<FTH, FTW, true>, fwd_lds<FTH, FTW, true>()));
+    if (!per) per = std::min(per_cu(k_pm_fwd<false>, fwd_lds(), QNT), per_cu(k_pm_fwd<true>, fwd_lds(), QNT));
     if (PM_FWD_PER > 0) per = std::min(per, PM_FWD_PER);
     const unsigned g2 = unsigned(std::max(1, std::min(a.ntiles, per * n_cu())));
     if (w1n)
-        k_pm_fwd<FTH, FTW, true><<<g2, NT, fwd_lds<FTH, FTW, true>(), s>>>(
-            a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, p, (bf16_t *)t3, (bf16_t *)out, w1n, *pn,
-            (bf16_t *)t2n);
+        k_pm_fwd<true><<<g2, QNT, fwd_lds(), s>>>(a, (const h16_t *)t2, (const h16_t *)x, w2, w3, p, (h16_t *)t3,
+                                                   (h16_t *)out, w1n, *pn, (h16_t *)t2n);
     else
-        k_pm_fwd<FTH, FTW, false><<<g2, NT, fwd_lds<FTH, FTW, false>(), s>>>(
-            a, (const bf16_t *)t2, (const bf16_t *)x, w2, w3, p, (bf16_t *)t3, (bf16_t *)out, nullptr, p, nullptr);
+        k_pm_fwd<false><<<g2, QNT, fwd_lds(), s>>>(a, (const h16_t *)t2, (const h16_t *)x, w2, w3, p, (h16_t *)t3,
+                                                    (h16_t *)out, nullptr, p, nullptr);
 }
 
 // backward workspace: K1 / K2 scalar partial rows, the W2 partials [nwa][9][NER], the W1 / G3
 // partials [nchb][NEB], then gz3 and gz1 (bf16 [nvox][9] each, 256-B aligned)
 struct MidWs {
     float *p1, *p2, *p2a, *p2b;
-    bf16_t *gz3, *gz1;
+    h16_t *gz3, *gz1;
     int n1, n2, nwa, nchb, npc, npb;
     size_t bytes;
 };
@@ -1212,8 +1478,8 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
     m.p2 = reinterpret_cast<float *>(c + o2);
     m.p2a = reinterpret_cast<float *>(c + oa);
     m.p2b = reinterpret_cast<float *>(c + ob);
-    m.gz3 = reinterpret_cast<bf16_t *>(c + oz3);
-    m.gz1 = reinterpret_cast<bf16_t *>(c + oz1);
+    m.gz3 = reinterpret_cast<h16_t *>(c + oz3);
+    m.gz1 = reinterpret_cast<h16_t *>(c + oz1);
     return m;
 }
 
@@ -1224,10 +1490,10 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
 // x[v + tap][ci] is exactly k_pm_w2grad's gz3 (x) t2 window sum; its partials are summed by the
 // W2 section of k_pm_reduce (fixed order, deterministic) straight into dw.
 bool mid_w2grad_ok(const vq3d_conv_desc *d) {
-    return d->dtype == VQ3D_BF16 && d->cin == BR && d->cin2 == 0 && d->cout == BR && d->kernel == 3 &&
+    return d->dtype == VQ3D_HALF && d->cin == BR && d->cin2 == 0 && d->cout == BR && d->kernel == 3 &&
            d->stride == 1 && d->pad == 1 && d->pad_mode == VQ3D_PAD_CIRCULAR && d->pro_kind == VQ3D_PRO_NONE &&
            d->in_h == d->out_h && d->in_w == d->out_w && d->in_d == d->out_d &&
-           vq3d_preact_mid_supported(VQ3D_BF16, d->batch, C, BR, d->in_h, d->in_w, d->in_d);
+           vq3d_preact_mid_supported(VQ3D_HALF, d->batch, C, BR, d->in_h, d->in_w, d->in_d);
 }
 
 namespace {
@@ -1254,7 +1520,7 @@ int mid_w2grad(const vq3d_conv_desc *d, const void *x, const void *g, float *dw,
     if (!mid_w2grad_ok(d) || !dw || !ws || ws_bytes < p.bytes) return fail("conv3d_bwd_weight(9->9 windowed): bad call");
     const PmArgs a = make_args(d->batch, d->in_h, d->in_w, d->in_d, BTH, BTW);
     float *p2a = static_cast<float *>(ws);
-    const bf16_t *gz = static_cast<const bf16_t *>(g), *xt = static_cast<const bf16_t *>(x);
+    const h16_t *gz = static_cast<const h16_t *>(g), *xt = static_cast<const h16_t *>(x);
     switch (d->in_d) {
         case 8: launch_w2<8>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
         case 16: launch_w2<16>(a, p.nwa, p.npc, gz, xt, p2a, s); break;
@@ -1276,9 +1542,11 @@ extern "C" {
 
 int vq3d_preact_mid_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                               int32_t dd) {
-    // D a power of two in [8, 128]: the weight-gradient chunks are tiles of whole D-lines
-    return dtype == VQ3D_BF16 && batch >= 1 && channels == C && branch == BR && h >= 8 && w >= 8 && h % 8 == 0 &&
-           w % 8 == 0 && dd >= TD && dd <= 128 && (dd & (dd - 1)) == 0;
+    // D a power of two in [16, 128]: the backward data tiles are 16 deep, the weight-gradient chunks
+    // are tiles of whole D-lines
+    return dtype == VQ3D_HALF && batch >= 1 && channels == C && branch == BR && h >= 8 && w >= 8 && h % 8 == 0 &&
+           w % 8 == 0 && dd >= QTD && dd <= 128 && (dd & (dd - 1)) == 0 &&
+           int64_t(batch) * h * w * dd * C * 2 < (int64_t(1) << 31);  // 32-bit byte offsets in the tile kernels
 }
 
 int vq3d_preact_mid_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
@@ -1298,7 +1566,7 @@ int vq3d_preact_mid_fwd_stages(int32_t stages, int32_t dtype, int32_t batch, int
     hipStream_t s = as_stream(stream);
     const int64_t nvox = int64_t(batch) * h * w * dd;
     const unsigned g1 = unsigned(std::max<int64_t>(1, std::min<int64_t>(nvox / 2 / NT, 2048)));
-    if (stages & 1) k_pm_t2<<<g1, NT, 0, s>>>(nvox, (const bf16_t *)x, w1, *p, (bf16_t *)t2);
+    if (stages & 1) k_pm_t2<<<g1, NT, 0, s>>>(nvox, (const h16_t *)x, w1, *p, (h16_t *)t2);
     if (stages & 2) launch_fwd(batch, h, w, dd, x, w2, w3, *p, out, t2, t3, nullptr, nullptr, nullptr, s);
     return check_launch("preact_mid_fwd");
 }
@@ -1331,7 +1599,7 @@ int vq3d_preact_mid_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t 
 int vq3d_preact_mid_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
                                const void *workspaces, size_t workspace_stride, float *const *grads,
                                const float *const *params, vq3d_stream_t stream) {
-    if (!vq3d_preact_mid_supported(VQ3D_BF16, batch, C, BR, h, w, dd))
+    if (!vq3d_preact_mid_supported(VQ3D_HALF, batch, C, BR, h, w, dd))
         return fail("preact_mid_reduce_run: shape outside the fused mid-level block kernels");
     if (nblocks < 1 || nblocks > 65535 || !workspaces || !grads || !params)
         return fail("preact_mid_reduce_run: bad arguments");
@@ -1386,17 +1654,18 @@ int vq3d_preact_mid_bwd_chain(int32_t stages, int32_t dtype, int32_t batch, int3
     hipStream_t s = as_stream(stream);
     const int64_t nvox = int64_t(batch) * h * w * dd;
     const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
-    if (stages & 1) k_pm_bwd1<<<m.n1, NT, 0, s>>>(nvox, (const bf16_t *)g, (const bf16_t *)t3, w3, *p, m.gz3, m.p1);
+    if (stages & 1) k_pm_bwd1<<<m.n1, NT, 0, s>>>(nvox, (const h16_t *)g, (const h16_t *)t3, w3, *p, m.gz3, m.p1);
+    const PmArgs aq = make_args_q(batch, h, w, dd);
     if ((stages & 2) && chain)
-        k_pm_bwd2<BTH, BTW, true><<<m.n2, NT, bwd_lds<BTH, BTW, true>(), s>>>(
-            a, m.gz3, (const bf16_t *)t2, (const bf16_t *)x, (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, m.gz1, m.p2,
-            (const bf16_t *)prev_t3, prev_w3, *prev_p, mp.gz3, mp.p1);
+        k_pm_bwd2<true><<<m.n2, QNT, bwd_lds(), s>>>(aq, m.gz3, (const h16_t *)t2, (const h16_t *)x, (const h16_t *)g,
+                                                     w1, w2, *p, (h16_t *)gx, m.gz1, m.p2, (const h16_t *)prev_t3,
+                                                     prev_w3, *prev_p, mp.gz3, mp.p1);
     else if (stages & 2)
-        k_pm_bwd2<BTH, BTW, false><<<m.n2, NT, bwd_lds<BTH, BTW, false>(), s>>>(
-            a, m.gz3, (const bf16_t *)t2, (const bf16_t *)x, (const bf16_t *)g, w1, w2, *p, (bf16_t *)gx, m.gz1, m.p2,
-            nullptr, nullptr, *p, nullptr, nullptr);
+        k_pm_bwd2<false><<<m.n2, QNT, bwd_lds(), s>>>(aq, m.gz3, (const h16_t *)t2, (const h16_t *)x,
+                                                      (const h16_t *)g, w1, w2, *p, (h16_t *)gx, m.gz1, m.p2,
+                                                      nullptr, nullptr, *p, nullptr, nullptr);
     if (stages & 4) {
-        const bf16_t *t2b = static_cast<const bf16_t *>(t2);
+        const h16_t *t2b = static_cast<const h16_t *>(t2);
         switch (dd) {
             case 8: launch_w2<8>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
             case 16: launch_w2<16>(a, m.nwa, m.npc, m.gz3, t2b, m.p2a, s); break;
@@ -1406,8 +1675,8 @@ int vq3d_preact_mid_bwd_chain(int32_t stages, int32_t dtype, int32_t batch, int3
         }
     }
     if (stages & 8) {
-        k_pm_w13grad<<<m.nchb, NT, w13_lds(), s>>>(m.npb, m.gz1, (const bf16_t *)t3, (const bf16_t *)x,
-                                                   (const bf16_t *)g, *p, m.p2b);
+        k_pm_w13grad<<<m.nchb, NT, w13_lds(), s>>>(m.npb, m.gz1, (const h16_t *)t3, (const h16_t *)x,
+                                                   (const h16_t *)g, *p, m.p2b);
     }
     RedOut o{G.dw1, G.dw2, G.dw3, G.dbias1a, G.dbias1b, G.dbias2a, G.dbias2b, G.dbias3a, G.dbias3b,
              G.dscale, G.dbias4, p->scale};

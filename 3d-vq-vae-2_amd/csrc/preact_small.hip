@@ -44,7 +44,7 @@ constexpr int n_entries(int C, int BR) { return C * BR + 27 * BR * BR + BR * C; 
 constexpr int s2_of(int BR) { return BR >= 4 ? 14 : 28; }  // W2-gradient sub-streams (9 each)
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
-__device__ __forceinline__ float rbf(float v) { return __uint_as_float(uint32_t(f2bf(v)) << 16); }
+__device__ __forceinline__ float rbf(float v) { return h2f_lo(uint32_t(f2h(v))); }
 __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
@@ -52,20 +52,20 @@ __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from 
 
 // N consecutive bf16 (N in 1, 2, 4, 8; the address is N * 2-byte aligned) <-> fp32 registers
 template <int N>
-__device__ __forceinline__ void ldv(const bf16_t *__restrict__ p, float (&o)[N]) {
+__device__ __forceinline__ void ldv(const h16_t *__restrict__ p, float (&o)[N]) {
     if constexpr (N == 1) {
         o[0] = ld(p);
     } else if constexpr (N == 2) {
         const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
-        o[0] = __uint_as_float(u << 16);
-        o[1] = __uint_as_float(u & 0xffff0000u);
+        o[0] = h2f_lo(u);
+        o[1] = h2f_hi(u);
     } else if constexpr (N == 4) {
         const uint2 u = *reinterpret_cast<const uint2 *>(p);
         const uint32_t w[2] = {u.x, u.y};
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            o[2 * i] = __uint_as_float(w[i] << 16);
-            o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+            o[2 * i] = h2f_lo(w[i]);
+            o[2 * i + 1] = h2f_hi(w[i]);
         }
     } else {
         static_assert(N == 8, "channel count");
@@ -73,20 +73,20 @@ __device__ __forceinline__ void ldv(const bf16_t *__restrict__ p, float (&o)[N])
         const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            o[2 * i] = __uint_as_float(w[i] << 16);
-            o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+            o[2 * i] = h2f_lo(w[i]);
+            o[2 * i + 1] = h2f_hi(w[i]);
         }
     }
 }
 
 template <int N>
-__device__ __forceinline__ void stv(bf16_t *__restrict__ p, const float (&v)[N]) {
+__device__ __forceinline__ void stv(h16_t *__restrict__ p, const float (&v)[N]) {
     if constexpr (N == 1) {
-        *p = f2bf(v[0]);
+        *p = f2h(v[0]);
     } else {
         uint32_t w[N / 2];
 #pragma unroll
-        for (int i = 0; i < N / 2; ++i) w[i] = uint32_t(f2bf(v[2 * i])) | (uint32_t(f2bf(v[2 * i + 1])) << 16);
+        for (int i = 0; i < N / 2; ++i) w[i] = uint32_t(f2h(v[2 * i])) | (uint32_t(f2h(v[2 * i + 1])) << 16);
         if constexpr (N == 2) *reinterpret_cast<uint32_t *>(p) = w[0];
         else if constexpr (N == 4) *reinterpret_cast<uint2 *>(p) = uint2{w[0], w[1]};
         else *reinterpret_cast<uint4 *>(p) = uint4{w[0], w[1], w[2], w[3]};
@@ -149,7 +149,7 @@ template <int C, int BR, typename TX, typename TO, int UA = (C <= 4 ? 8 : 4)>
 __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict__ x, const float *__restrict__ w1,
                                                  const float *__restrict__ w2, const float *__restrict__ w3,
                                                  vq3d_preact_params p, TO *__restrict__ out,
-                                                 bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
+                                                 h16_t *__restrict__ t2o, h16_t *__restrict__ t3o) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *w2s = sm;                  // [tap][c][o]
     float *t2h = w2s + 27 * BR * BR;  // [halo position][BR]
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
 // g has the forward out's storage (TO), x and gx the input's (TX)
 template <int C, int BR, typename TX, typename TO, int UB = (C <= 4 ? 4 : 2), int S2 = s2_of(BR)>
 __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict__ g, const TX *__restrict__ x,
-                                                 const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
+                                                 const h16_t *__restrict__ t2, const h16_t *__restrict__ t3,
                                                  const float *__restrict__ w1, const float *__restrict__ w2,
                                                  const float *__restrict__ w3, vq3d_preact_params p,
                                                  float *__restrict__ part, TX *__restrict__ gx) {
@@ -564,7 +564,7 @@ extern "C" {
 int vq3d_preact_small_supported(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                                 int32_t dd) {
     SArgs a;
-    return dtype == VQ3D_BF16 && (col_supported(batch, channels, branch, h, w, dd) ||
+    return dtype == VQ3D_HALF && (col_supported(batch, channels, branch, h, w, dd) ||
                                   plan(batch, channels, branch, h, w, dd, a))
                ? 1
                : 0;
@@ -587,14 +587,14 @@ size_t vq3d_preact_small_workspace_bytes(int32_t batch, int32_t channels, int32_
 int vq3d_preact_small_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                           int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                           const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
-    if (dtype != VQ3D_BF16) return fail("preact_small_fwd: the fused few-channel kernels take bf16 operands");
+    if (dtype != VQ3D_HALF) return fail("preact_small_fwd: the fused few-channel kernels take bf16 operands");
     return vq3d_preact_small_fwd_io(dtype, dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, p, out, t2, t3,
                                     stream);
 }
 
 namespace {
-bool io_ok(int32_t xdt, int32_t odt) {
-    return (xdt == VQ3D_BF16 || xdt == VQ3D_F32) && (odt == VQ3D_BF16 || odt == VQ3D_F32);
+static bool io_ok(int32_t xdt, int32_t odt) {
+    return (xdt == VQ3D_HALF || xdt == VQ3D_F32) && (odt == VQ3D_HALF || odt == VQ3D_F32);
 }
 }  // namespace
 
@@ -604,7 +604,7 @@ int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, 
                              vq3d_stream_t stream) {
     SArgs a;
     if (!x || !w1 || !w2 || !w3 || !p || !out) return fail("preact_small_fwd: null pointer");
-    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_fwd: stream storage must be VQ3D_BF16 or VQ3D_F32");
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_fwd: stream storage must be VQ3D_HALF or VQ3D_F32");
     if (col_supported(batch, channels, branch, h, w, dd))
         return col_fwd(x_dtype, out_dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, *p, out, t2, t3,
                        as_stream(stream));
@@ -620,13 +620,13 @@ int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, 
             attr = true;                                                                                       \
         }                                                                                                      \
         k_small_fwd<C_, B_, TX_, TO_><<<unsigned(a.nbricks), NT, lds, s>>>(a, (const TX_ *)x, w1, w2, w3, *p,  \
-                                                                          (TO_ *)out, (bf16_t *)t2, (bf16_t *)t3); \
+                                                                          (TO_ *)out, (h16_t *)t2, (h16_t *)t3); \
     }
 #define F(C_, B_)                                                                                              \
     if (channels == C_ && branch == B_) {                                                                      \
-        if (x_dtype == VQ3D_BF16 && out_dtype == VQ3D_BF16) F2(C_, B_, bf16_t, bf16_t)                         \
-        else if (x_dtype == VQ3D_BF16) F2(C_, B_, bf16_t, float)                                               \
-        else if (out_dtype == VQ3D_BF16) F2(C_, B_, float, bf16_t)                                             \
+        if (x_dtype == VQ3D_HALF && out_dtype == VQ3D_HALF) F2(C_, B_, h16_t, h16_t)                         \
+        else if (x_dtype == VQ3D_HALF) F2(C_, B_, h16_t, float)                                               \
+        else if (out_dtype == VQ3D_HALF) F2(C_, B_, float, h16_t)                                             \
         else F2(C_, B_, float, float)                                                                          \
     }
     F(2, 1) else F(4, 2) else F(8, 4)
@@ -648,7 +648,7 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
                                  const void *t3, const float *w1, const float *w2, const float *w3,
                                  const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                  size_t ws_bytes, void *gx, vq3d_stream_t stream) {
-    if (dtype != VQ3D_BF16) return fail("preact_small_bwd: the fused few-channel kernels take bf16 operands");
+    if (dtype != VQ3D_HALF) return fail("preact_small_bwd: the fused few-channel kernels take bf16 operands");
     return vq3d_preact_small_bwd_stages_io(stages, dtype, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1,
                                            w2, w3, p, gr, workspace, ws_bytes, gx, stream);
 }
@@ -662,7 +662,7 @@ int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out
     if (stages < 1 || stages > 3) return fail("preact_small_bwd: stages must be a mask of 1 | 2");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx)
         return fail("preact_small_bwd: null pointer");
-    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_bwd: stream storage must be VQ3D_BF16 or VQ3D_F32");
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_bwd: stream storage must be VQ3D_HALF or VQ3D_F32");
     if (col_supported(batch, channels, branch, h, w, dd)) {
         const vq3d_preact_grads &G = *gr;
         if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||
@@ -689,14 +689,14 @@ int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out
         }                                                                                                      \
         if (stages & 1)                                                                                        \
             k_small_bwd<C_, B_, TX_, TO_><<<unsigned(a.nbricks), NT, lds, s>>>(                                \
-                a, (const TO_ *)g, (const TX_ *)x, (const bf16_t *)t2, (const bf16_t *)t3, w1, w2, w3, *p, part,  \
+                a, (const TO_ *)g, (const TX_ *)x, (const h16_t *)t2, (const h16_t *)t3, w1, w2, w3, *p, part,  \
                 (TX_ *)gx);                                                                                    \
     }
 #define Bk(C_, B_)                                                                                             \
     if (channels == C_ && branch == B_) {                                                                      \
-        if (x_dtype == VQ3D_BF16 && out_dtype == VQ3D_BF16) B2(C_, B_, bf16_t, bf16_t)                         \
-        else if (x_dtype == VQ3D_BF16) B2(C_, B_, bf16_t, float)                                               \
-        else if (out_dtype == VQ3D_BF16) B2(C_, B_, float, bf16_t)                                             \
+        if (x_dtype == VQ3D_HALF && out_dtype == VQ3D_HALF) B2(C_, B_, h16_t, h16_t)                         \
+        else if (x_dtype == VQ3D_HALF) B2(C_, B_, h16_t, float)                                               \
+        else if (out_dtype == VQ3D_HALF) B2(C_, B_, float, h16_t)                                             \
         else B2(C_, B_, float, float)                                                                          \
         if (stages & 2) k_small_bwd_reduce<C_, B_><<<unsigned(ne), NT, 0, s>>>(part, a.nbricks, p->scale, *gr); \
     }

@@ -417,7 +417,6 @@ __global__ __launch_bounds__(NT) void k_stack_bwd(SkArgs a, const T *__restrict_
 // transposed conv, gx and the three weight gradients with the voxels as the reduction axis).
 // Rounding points are the unfused bf16 path's (u1, t2, t3, gz3, gz1 rounded to bf16 as matrix
 // operands, fp32 accumulation); the residual stream and the gradient stream stay fp32.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 // STK_EXP: phase-skip bits for timing experiments (make exp EXPSRC=preact_stack EXPDEF=STK_EXP):
 // 1 W2 gradient, 2 W1 gradient, 4 W3 gradient, 8 weight staging.  The product library is built with STK_EXP = 0.
@@ -428,33 +427,33 @@ constexpr int MC = 32, MB = 16;            // channels, branch
 constexpr int PF = 36, PU = 40, PT = 24;   // row pitches: fp32 streams, u1 (bf16), branch tensors (bf16)
 constexpr int MAXVM = 128;
 
-__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma(hx8 a, hx8 b, f32x4 c) {
+    return VQ3D_MFMA_16X16X32(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+__device__ __forceinline__ hx8 pack8(const float (&v)[8]) {
     uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
-    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+    for (int j = 0; j < 4; ++j) w[j] = uint32_t(f2h(v[2 * j])) | (uint32_t(f2h(v[2 * j + 1])) << 16);
+    return __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]});
 }
-__device__ __forceinline__ bf16x8 rd8(const bf16_t *p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(p)); }
-__device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, uint4{0u, 0u, 0u, 0u}); }
+__device__ __forceinline__ hx8 rd8(const h16_t *p) { return __builtin_bit_cast(hx8, *reinterpret_cast<const uint4 *>(p)); }
+__device__ __forceinline__ hx8 zero8() { return __builtin_bit_cast(hx8, uint4{0u, 0u, 0u, 0u}); }
 // 8 bf16 at p[j * stride] (LDS)
-__device__ __forceinline__ bf16x8 gat8(const bf16_t *p, int stride) {
+__device__ __forceinline__ hx8 gat8(const h16_t *p, int stride) {
     uint32_t w[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = uint32_t(p[2 * j * stride]) | (uint32_t(p[(2 * j + 1) * stride]) << 16);
-    return __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+    return __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]});
 }
 // 8 fp32 at p[j * stride] (LDS), rounded to bf16
-__device__ __forceinline__ bf16x8 gat8f(const float *p, int stride) {
+__device__ __forceinline__ hx8 gat8f(const float *p, int stride) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = p[j * stride];
     return pack8(v);
 }
 // 8 consecutive fp32 (16-B aligned), rounded to bf16
-__device__ __forceinline__ bf16x8 rd8f(const float *p) {
+__device__ __forceinline__ hx8 rd8f(const float *p) {
     const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     return pack8(v);
@@ -462,8 +461,8 @@ __device__ __forceinline__ bf16x8 rd8f(const float *p) {
 
 struct Mk {
     float *xs, *gs, *part, *w;   // fp32: residual / gradient stream, conv partials [2][nv][16], weights
-    bf16_t *fr;                  // the block's weights as packed bf16 MFMA B fragments (FR_* below)
-    bf16_t *u1, *t2, *t3, *z3, *z1;
+    h16_t *fr;                  // the block's weights as packed bf16 MFMA B fragments (FR_* below)
+    h16_t *u1, *t2, *t3, *z3, *z1;
     short *nb;
     float *red;
 };
@@ -482,8 +481,8 @@ __device__ __forceinline__ int frpos(int ktile, int kb, int n, int j) { return k
 
 // weight element (torch-order image index i, value v) -> its fragment slots
 template <bool BWD>
-__device__ __forceinline__ void frag_store(bf16_t *fr, int i, float v) {
-    const bf16_t b = f2bf(v);
+__device__ __forceinline__ void frag_store(h16_t *fr, int i, float v) {
+    const h16_t b = f2h(v);
     if (i < W3O) {  // W1 [o][c]
         const int o = i / MC, c = i - o * MC;
         if (!BWD) fr[FR_A + frpos(0, c >> 3, o, c & 7)] = b;
@@ -498,15 +497,15 @@ __device__ __forceinline__ void frag_store(bf16_t *fr, int i, float v) {
         fr[FR_B + frpos(tap >> 1, 2 * (tap & 1) + (kc >> 3), n, kc & 7)] = b;
     }
 }
-__device__ __forceinline__ void frag_zero(bf16_t *fr) {
+__device__ __forceinline__ void frag_zero(h16_t *fr) {
     // tap 27 (k-step 13, kb 2 / 3) and the k-halves o >= 16 of the two FC tiles (kb 2 / 3)
     for (int i = threadIdx.x; i < 3 * 32 * 8; i += NT) {
         const int t = i / 256, r = i - t * 256, lane = 32 + (r >> 3), j = r & 7;
         fr[(t == 0 ? FR_B + 13 * FRT : FR_C + (t - 1) * FRT) + lane * 8 + j] = 0;
     }
 }
-__device__ __forceinline__ bf16x8 frag(const bf16_t *fr, int ktile, int lane) {
-    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(fr + ktile * FRT + lane * 8));
+__device__ __forceinline__ hx8 frag(const h16_t *fr, int ktile, int lane) {
+    return __builtin_bit_cast(hx8, *reinterpret_cast<const uint4 *>(fr + ktile * FRT + lane * 8));
 }
 
 __device__ __forceinline__ Mk carve_m(int nv, char *smem) {
@@ -522,7 +521,7 @@ __device__ __forceinline__ Mk carve_m(int nv, char *smem) {
     p += 2 * nv * MB;
     m.red = p;
     p += 16 * 8;
-    bf16_t *q = reinterpret_cast<bf16_t *>(p);
+    h16_t *q = reinterpret_cast<h16_t *>(p);
     m.fr = q;
     q += FR_N;
     m.u1 = q;
@@ -553,7 +552,7 @@ struct WReg {  // register prefetch of one block's weights (fp32, torch order)
         }
     }
     template <bool BWD>
-    __device__ __forceinline__ void store(float *w, bf16_t *fr) const {
+    __device__ __forceinline__ void store(float *w, h16_t *fr) const {
 #pragma unroll
         for (int u = 0; u < (WN + NT - 1) / NT; ++u) {
             const int i = threadIdx.x + u * NT;
@@ -593,7 +592,7 @@ __device__ __forceinline__ Scal scal_lanes(float v) {
 // [ks0, ks0 + 7); B[k][n] built from the fp32 image: forward n = co, k = (tap, ci); transposed
 // n = ci, k = (tap, co) with the flipped tap
 template <bool T>
-__device__ __forceinline__ f32x4 conv_half(const Mk &m, const bf16_t *src, int mt, int ks0, int lane) {
+__device__ __forceinline__ f32x4 conv_half(const Mk &m, const h16_t *src, int mt, int ks0, int lane) {
     const int row = lane & 15, kb = lane >> 4, v = mt * 16 + row;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     // all 7 neighbour indices, then all 7 operand rows, then the MFMAs: one LDS round trip per
@@ -604,7 +603,7 @@ __device__ __forceinline__ f32x4 conv_half(const Mk &m, const bf16_t *src, int m
         const int tap = 2 * (ks0 + k) + (kb >> 1);
         nbi[k] = tap < 27 ? int(m.nb[v * 27 + (T ? 26 - tap : tap)]) : -1;
     }
-    bf16x8 af[7];
+    hx8 af[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) af[k] = nbi[k] >= 0 ? rd8(src + nbi[k] * PT + 8 * (kb & 1)) : zero8();
 #pragma unroll
@@ -612,8 +611,8 @@ __device__ __forceinline__ f32x4 conv_half(const Mk &m, const bf16_t *src, int m
     return acc;
 }
 
-__global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__restrict__ x, const float *const *tab,
-                                                   bf16_t *__restrict__ out, float *__restrict__ saved) {
+__global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const h16_t *__restrict__ x, const float *const *tab,
+                                                   h16_t *__restrict__ out, float *__restrict__ saved) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Mk m = carve_m(a.nv, smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
@@ -644,7 +643,7 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
             const int v = i / MC, c = i - v * MC;
             const float xv = m.xs[v * PF + c];
             sx[i] = xv;
-            m.u1[v * PU + c] = f2bf(elu(xv + s.b1a) + s.b1b);
+            m.u1[v * PU + c] = f2h(elu(xv + s.b1a) + s.b1b);
         }
         __syncthreads();
         // t2: M-tile per wave, K = 32 channels, N = 16
@@ -654,7 +653,7 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int v = wave * 16 + 4 * kb + j;
-                const bf16_t tv = f2bf(elu(acc[j] + s.b2a) + s.b2b);
+                const h16_t tv = f2h(elu(acc[j] + s.b2a) + s.b2b);
                 m.t2[v * PT + row] = tv;
                 st2[v * MB + row] = ld(&tv);
             }
@@ -670,7 +669,7 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
         __syncthreads();
         for (int i = tid; i < nvb; i += NT) {
             const int v = i / MB, o = i - v * MB;
-            const bf16_t tv = f2bf(elu(m.part[i] + m.part[nvb + i] + s.b3a) + s.b3b);
+            const h16_t tv = f2h(elu(m.part[i] + m.part[nvb + i] + s.b3a) + s.b3b);
             m.t3[v * PT + o] = tv;
             st3[i] = ld(&tv);
         }
@@ -685,7 +684,7 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
         }
     }
     __syncthreads();
-    for (int i = tid; i < nvc; i += NT) out[i] = f2bf(m.xs[(i / MC) * PF + i % MC]);
+    for (int i = tid; i < nvc; i += NT) out[i] = f2h(m.xs[(i / MC) * PF + i % MC]);
 }
 
 // SPLIT: the chain computes only the gradient stream and the scalar sums that ride it (gz3, gt2,
@@ -693,9 +692,9 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const bf16_t *__res
 // `rec`; the W1 / W2 / W3 and scale gradients, which nothing downstream in the chain needs, are
 // k_stackm_wgrad's, one workgroup per block in parallel after the chain.
 template <bool SPLIT>
-__global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__restrict__ g, const float *const *tab,
+__global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__restrict__ g, const float *const *tab,
                                                    float *const *gtab, const float *__restrict__ saved,
-                                                   bf16_t *__restrict__ gx, bf16_t *__restrict__ rec) {
+                                                   h16_t *__restrict__ gx, h16_t *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Mk m = carve_m(a.nv, smem);
     const int tid0 = threadIdx.x;
@@ -755,7 +754,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 for (int q = 0; q < 2; ++q) o2[q][j] = gw2[((4 * kb + j) * MB + row) * 27 + min(wave + 16 * q, 26)];
             }
         }
-        bf16_t *rg = rec + size_t(blk) * nv * (MC + 2 * MB), *rz3 = rg + nvc, *rz1 = rz3 + nvb;
+        h16_t *rg = rec + size_t(blk) * nv * (MC + 2 * MB), *rz3 = rg + nvc, *rz1 = rz3 + nvb;
         const float osc = *gc;
         float *const gsc = gc;  // lanes 3 .. 10: this block's scalar-gradient pointers
         if (blk > 0) gc = row_ptr(gtab, blk - 1, lane);
@@ -768,7 +767,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 const int v = i / MC, c = i - v * MC;
                 const float z = svx[u] + s.b1a;
                 const float e = z > 0.f ? 1.f : expf(z);
-                m.u1[v * PU + c] = f2bf((z > 0.f ? z : e - 1.f) + s.b1b);
+                m.u1[v * PU + c] = f2h((z > 0.f ? z : e - 1.f) + s.b1b);
                 m.xs[v * PF + c] = e;
             }
         }
@@ -777,8 +776,8 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
             const int i = tid + u * NT;
             if (i < nvb) {
                 const int v = i / MB, o = i - v * MB;
-                m.t2[v * PT + o] = f2bf(sv2[u]);
-                m.t3[v * PT + o] = f2bf(sv3[u]);
+                m.t2[v * PT + o] = f2h(sv2[u]);
+                m.t3[v * PT + o] = f2h(sv3[u]);
             }
         }
         __syncthreads();
@@ -794,8 +793,8 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                 const float z = g3 * elu_d_act(ld(&m.t3[v * PT + row]), s.b3b);
                 ps[2] += g3;
                 ps[3] += z;
-                m.z3[v * PT + row] = f2bf(z);
-                if constexpr (SPLIT) rz3[v * MB + row] = f2bf(z);
+                m.z3[v * PT + row] = f2h(z);
+                if constexpr (SPLIT) rz3[v * MB + row] = f2h(z);
             }
         } else if (!SPLIT && !(STK_EXP & 4) && wave < nmt + 2) {
             // W3 gradient: M = co tile (wave - nmt), N = o, K = voxels; dscale = sum W3 . G3
@@ -815,7 +814,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
         for (int i = tid; i < nvc; i += NT) {
             const float gv = m.gs[(i / MC) * PF + i % MC];
             ps[0] += gv;
-            if constexpr (SPLIT) rg[i] = f2bf(gv);
+            if constexpr (SPLIT) rg[i] = f2h(gv);
         }
         __syncthreads();
         // gt2 = W2^T (*) gz3 (M-tile x half of the k-steps per wave); W2 gradient per tap
@@ -840,7 +839,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
                     w[j] = uint32_t(m.t2[int(m.nb[va * 27 + tap]) * PT + row]) |
                            (uint32_t(m.t2[int(m.nb[vb * 27 + tap]) * PT + row]) << 16);
                 }
-                acc = mfma(gat8(m.z3 + v0 * PT + row, PT), __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]}),
+                acc = mfma(gat8(m.z3 + v0 * PT + row, PT), __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]}),
                            acc);
             }
 #pragma unroll
@@ -865,8 +864,8 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
             const float z = g2 * elu_d_act(ld(&m.t2[v * PT + o]), s.b2b);
             ps[4] += g2;
             ps[5] += z;
-            m.z1[v * PT + o] = f2bf(z);
-            if constexpr (SPLIT) rz1[i] = f2bf(z);
+            m.z1[v * PT + o] = f2h(z);
+            if constexpr (SPLIT) rz1[i] = f2h(z);
         }
         __syncthreads();
         if (wave < 2 * nmt) {
@@ -903,7 +902,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
         }
     }
     __syncthreads();
-    for (int i = tid; i < nvc; i += NT) gx[i] = f2bf(m.gs[(i / MC) * PF + i % MC]);
+    for (int i = tid; i < nvc; i += NT) gx[i] = f2h(m.gs[(i / MC) * PF + i % MC]);
 }
 
 // The weight gradients of a SPLIT backward: one workgroup per block, from its saved x / t2 / t3
@@ -912,12 +911,12 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const bf16_t *__res
 // the scale gradient (sum W3 . G3): waves 2, 3.  Each gradient entry has one adder.
 constexpr int PG = 40;  // row pitch of the bf16 g record copy
 __global__ __launch_bounds__(NT) void k_stackm_wgrad(SkArgs a, const float *const *tab, float *const *gtab,
-                                                     const float *__restrict__ saved, const bf16_t *__restrict__ rec) {
+                                                     const float *__restrict__ saved, const h16_t *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nv = a.nv, nks = nv / 32, nvc = nv * MC, nvb = nv * MB, blk = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
-    bf16_t *t2 = reinterpret_cast<bf16_t *>(smem), *t3 = t2 + nv * PT, *z3 = t3 + nv * PT, *z1 = z3 + nv * PT;
-    bf16_t *u1 = z1 + nv * PT, *gs = u1 + nv * PU;
+    h16_t *t2 = reinterpret_cast<h16_t *>(smem), *t3 = t2 + nv * PT, *z3 = t3 + nv * PT, *z1 = z3 + nv * PT;
+    h16_t *u1 = z1 + nv * PT, *gs = u1 + nv * PU;
     short *nb = reinterpret_cast<short *>(gs + nv * PG);
     float *red = reinterpret_cast<float *>(nb + ((nv * 27 + 7) & ~7));
     const float *pc = row_ptr(tab, blk, lane);
@@ -926,18 +925,18 @@ __global__ __launch_bounds__(NT) void k_stackm_wgrad(SkArgs a, const float *cons
     float *gc = row_ptr(gtab, blk, lane);
     float *gw1 = bcast_ptr(gc, 0), *gw2 = bcast_ptr(gc, 1), *gw3 = bcast_ptr(gc, 2);
     const float *sx = saved + size_t(blk) * nv * (MC + 2 * MB), *st2 = sx + nvc, *st3 = st2 + nvb;
-    const bf16_t *rg = rec + size_t(blk) * nv * (MC + 2 * MB), *rz3 = rg + nvc, *rz1 = rz3 + nvb;
+    const h16_t *rg = rec + size_t(blk) * nv * (MC + 2 * MB), *rz3 = rg + nvc, *rz1 = rz3 + nvb;
     for (int i = tid; i < nv * 27; i += NT) nb[i] = short(nbr(a, i / 27, i % 27, 1));
     for (int i = tid; i < nvc; i += NT) {
         const int v = i / MC, c = i - v * MC;
         const float z = sx[i] + s.b1a;
-        u1[v * PU + c] = f2bf((z > 0.f ? z : expf(z) - 1.f) + s.b1b);
+        u1[v * PU + c] = f2h((z > 0.f ? z : expf(z) - 1.f) + s.b1b);
         gs[v * PG + c] = rg[i];
     }
     for (int i = tid; i < nvb; i += NT) {
         const int v = i / MB, o = i - v * MB;
-        t2[v * PT + o] = f2bf(st2[i]);
-        t3[v * PT + o] = f2bf(st3[i]);
+        t2[v * PT + o] = f2h(st2[i]);
+        t3[v * PT + o] = f2h(st3[i]);
         z3[v * PT + o] = rz3[i];
         z1[v * PT + o] = rz1[i];
     }
@@ -956,7 +955,7 @@ __global__ __launch_bounds__(NT) void k_stackm_wgrad(SkArgs a, const float *cons
                 const int va = v0 + 2 * j, vb = va + 1;
                 w[j] = uint32_t(t2[int(nb[va * 27 + tap]) * PT + row]) | (uint32_t(t2[int(nb[vb * 27 + tap]) * PT + row]) << 16);
             }
-            acc = mfma(gat8(z3 + v0 * PT + row, PT), __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]}), acc);
+            acc = mfma(gat8(z3 + v0 * PT + row, PT), __builtin_bit_cast(hx8, uint4{w[0], w[1], w[2], w[3]}), acc);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1043,14 +1042,14 @@ int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
     if (!x || !params || !out || !saved) return fail("preact_stack_fwd: null pointer");
     hipStream_t s = as_stream(stream);
     const size_t lds = lds_bytes(a, false);
-    if (dtype == VQ3D_BF16 && mfma_ok(a)) {
+    if (dtype == VQ3D_HALF && mfma_ok(a)) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   int(160 * 1024));
-        k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)x, params, (bf16_t *)out, saved);
-    } else if (dtype == VQ3D_BF16) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<bf16_t>),
+        k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved);
+    } else if (dtype == VQ3D_HALF) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<h16_t>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
-        k_stack_fwd<bf16_t><<<1, NT, lds, s>>>(a, (const bf16_t *)x, params, (bf16_t *)out, saved);
+        k_stack_fwd<h16_t><<<1, NT, lds, s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved);
     } else if (dtype == VQ3D_F32) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<float>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
@@ -1069,14 +1068,14 @@ int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
     if (!g || !params || !grads || !saved || !gx) return fail("preact_stack_bwd: null pointer");
     hipStream_t s = as_stream(stream);
     const size_t lds = lds_bytes(a, true);
-    if (dtype == VQ3D_BF16 && mfma_ok(a)) {
+    if (dtype == VQ3D_HALF && mfma_ok(a)) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
-        k_stackm_bwd<false><<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx, nullptr);
-    } else if (dtype == VQ3D_BF16) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<bf16_t>),
+        k_stackm_bwd<false><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx, nullptr);
+    } else if (dtype == VQ3D_HALF) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<h16_t>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
-        k_stack_bwd<bf16_t><<<1, NT, lds, s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx);
+        k_stack_bwd<h16_t><<<1, NT, lds, s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx);
     } else if (dtype == VQ3D_F32) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<float>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
@@ -1101,7 +1100,7 @@ int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int3
     SkArgs a;
     if (check(nblocks, batch, channels, branch, h, w, dd, a)) return fail("preact_stack_bwd_ws: unsupported shape");
     const size_t need = vq3d_preact_stack_bwd_workspace_bytes(nblocks, batch, channels, branch, h, w, dd);
-    if (dtype != VQ3D_BF16 || need == 0)  // no split plan for this shape / dtype: the fused kernel
+    if (dtype != VQ3D_HALF || need == 0)  // no split plan for this shape / dtype: the fused kernel
         return vq3d_preact_stack_bwd(dtype, nblocks, batch, channels, branch, h, w, dd, g, params, grads, saved, gx,
                                      stream);
     if (!g || !params || !grads || !saved || !gx || !workspace) return fail("preact_stack_bwd_ws: null pointer");
@@ -1109,9 +1108,9 @@ int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int3
     hipStream_t s = as_stream(stream);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
-    k_stackm_bwd<true><<<1, NT, lds_m(a.nv), s>>>(a, (const bf16_t *)g, params, grads, saved, (bf16_t *)gx,
-                                                  (bf16_t *)workspace);
-    k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const bf16_t *)workspace);
+    k_stackm_bwd<true><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx,
+                                                  (h16_t *)workspace);
+    k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const h16_t *)workspace);
     return check_launch("preact_stack_bwd_ws");
 }
 

@@ -44,7 +44,6 @@ namespace vq3d {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int C = 72, BR = 36;                         // block / branch channels
@@ -79,37 +78,37 @@ struct WArgs {
 };
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
-__device__ __forceinline__ float bf(uint32_t u16) { return __uint_as_float(u16 << 16); }
+__device__ __forceinline__ float bf(uint32_t u16) { return h2f_lo(u16); }
 __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
 }
 // elu with the hardware exp (v_exp_f32): every result is rounded to bf16 or feeds a bf16 operand
 __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : __expf(z) - 1.f; }
-__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma(hx8 a, hx8 b, f32x4 c) {
+    return VQ3D_MFMA_16X16X32(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ uint32_t pk(float a, float b) { return uint32_t(f2bf(a)) | (uint32_t(f2bf(b)) << 16); }
+__device__ __forceinline__ uint32_t pk(float a, float b) { return uint32_t(f2h(a)) | (uint32_t(f2h(b)) << 16); }
 // 8 bf16 from LDS, 8-byte aligned
-__device__ __forceinline__ bf16x8 ld8(const bf16_t *p) {
+__device__ __forceinline__ hx8 ld8(const h16_t *p) {
     const uint2 *q = reinterpret_cast<const uint2 *>(p);
     const uint2 a = q[0], b = q[1];
-    return __builtin_bit_cast(bf16x8, uint4{a.x, a.y, b.x, b.y});
+    return __builtin_bit_cast(hx8, uint4{a.x, a.y, b.x, b.y});
 }
 // 8 bf16 from LDS, 16-byte aligned
-__device__ __forceinline__ bf16x8 ld16(const bf16_t *p) { return *reinterpret_cast<const bf16x8 *>(p); }
+__device__ __forceinline__ hx8 ld16(const h16_t *p) { return *reinterpret_cast<const hx8 *>(p); }
 // 8 consecutive bf16 at any element offset (4-byte aligned base): five dwords + v_alignbyte
-__device__ __forceinline__ bf16x8 read8(const bf16_t *base, int off) {
+__device__ __forceinline__ hx8 read8(const h16_t *base, int off) {
     const uint32_t *q = reinterpret_cast<const uint32_t *>(base + (off & ~1));
     const uint32_t sh = uint32_t(off & 1) * 2u;
     const uint32_t u0 = q[0], u1 = q[1], u2 = q[2], u3 = q[3], u4 = q[4];
     const uint4 r = {__builtin_amdgcn_alignbyte(u1, u0, sh), __builtin_amdgcn_alignbyte(u2, u1, sh),
                      __builtin_amdgcn_alignbyte(u3, u2, sh), __builtin_amdgcn_alignbyte(u4, u3, sh)};
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(hx8, r);
 }
 // fragment f of a block image for this lane
-__device__ __forceinline__ bf16x8 frag(const uint4 *__restrict__ img, int f, int lane) {
-    return __builtin_bit_cast(bf16x8, img[f * 64 + lane]);
+__device__ __forceinline__ hx8 frag(const uint4 *__restrict__ img, int f, int lane) {
+    return __builtin_bit_cast(hx8, img[f * 64 + lane]);
 }
 // two bf16 pairs (channels 2k, 2k+1 of voxels p and p + 1) -> the channel-major dword of channel
 // 2k (lo) and 2k + 1 (hi)
@@ -175,7 +174,7 @@ __device__ __forceinline__ void make_tables(const WArgs &a, const Org &o, int *s
 // (ELU) or g rounded; returns the thread's sum of the interior values (fp32, unrounded) when !ELU.
 // Every 16-B load is issued before any conversion.
 template <bool ELU>
-__device__ __forceinline__ float stage_halo_f32(const int *segv, const float *__restrict__ src, bf16_t *dst, float b1a,
+__device__ __forceinline__ float stage_halo_f32(const int *segv, const float *__restrict__ src, h16_t *dst, float b1a,
                                                 float b1b, float *interior = nullptr) {
     constexpr int Q = C / 4, N4 = HV * Q, P = (N4 + NT - 1) / NT;
     const int tid = threadIdx.x;
@@ -211,7 +210,7 @@ __device__ __forceinline__ float stage_halo_f32(const int *segv, const float *__
 }
 
 // Stage a bf16 [V][BR] tensor on the tile halo into LDS [HV][BR] (8-byte pieces, loads first)
-__device__ __forceinline__ void stage_halo_br(const int *segv, const bf16_t *__restrict__ src, bf16_t *dst) {
+__device__ __forceinline__ void stage_halo_br(const int *segv, const h16_t *__restrict__ src, h16_t *dst) {
     constexpr int Q = BR / 4, N = HV * Q, P = (N + NT - 1) / NT;
     const int tid = threadIdx.x;
     uint2 v[P];
@@ -230,7 +229,7 @@ __device__ __forceinline__ void stage_halo_br(const int *segv, const bf16_t *__r
 // the tile's [64][BR] bf16 between LDS and global (8-byte pieces; LDS_HALO: the LDS side is the
 // halo layout [HV][BR], otherwise [64][BR]); global -> LDS issues every load first
 template <bool LDS_HALO>
-__device__ __forceinline__ void tile_to_global(const int *runv, const bf16_t *lds, bf16_t *__restrict__ gl) {
+__device__ __forceinline__ void tile_to_global(const int *runv, const h16_t *lds, h16_t *__restrict__ gl) {
     constexpr int Q = BR / 4, PR = TD * Q, N = TH * TW * PR;
     for (int i = threadIdx.x; i < N; i += NT) {
         const int r = i / PR, q = i - r * PR, rh = r / TW, rw = r - rh * TW;
@@ -238,7 +237,7 @@ __device__ __forceinline__ void tile_to_global(const int *runv, const bf16_t *ld
         reinterpret_cast<uint2 *>(gl + int64_t(runv[r]) * BR)[q] = reinterpret_cast<const uint2 *>(lds + l0)[q];
     }
 }
-__device__ __forceinline__ void tile_from_global(const int *runv, const bf16_t *__restrict__ gl, bf16_t *lds) {
+__device__ __forceinline__ void tile_from_global(const int *runv, const h16_t *__restrict__ gl, h16_t *lds) {
     constexpr int Q = BR / 4, PR = TD * Q, N = TH * TW * PR, P = (N + NT - 1) / NT;
     uint2 v[P];
 #pragma unroll
@@ -292,21 +291,21 @@ __global__ __launch_bounds__(64) void k_wide_pack(const float *const *__restrict
 // Wave w: branch n-tile nt = w % 3 (channels 16 nt ..), m-tiles of parity / half hf = w / 3.
 __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restrict__ x, const uint4 *__restrict__ img,
                                                  vq3d_preact_params p, float *__restrict__ out,
-                                                 bf16_t *__restrict__ t2o, bf16_t *__restrict__ t3o) {
+                                                 h16_t *__restrict__ t2o, h16_t *__restrict__ t3o) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *u1h = reinterpret_cast<bf16_t *>(smem);  // [HV][C], then t3 [TV][BR]
-    bf16_t *t2h = u1h + HV * C + PADE;               // [HV][BR]
+    h16_t *u1h = reinterpret_cast<h16_t *>(smem);  // [HV][C], then t3 [TV][BR]
+    h16_t *t2h = u1h + HV * C + PADE;               // [HV][BR]
     int *segv = reinterpret_cast<int *>(t2h + HV * BR + PADE);
     int *runv = segv + HV;
-    bf16_t *t3s = u1h;
+    h16_t *t3s = u1h;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int nt = wave % NTB, hf = wave / NTB;
     // this wave's W1 and W2 fragments, in flight during the staging
-    bf16x8 f1[KS1], f2[9 * KSW];
+    hx8 f1[KS1], f2[9 * KSW];
 #pragma unroll
     for (int k = 0; k < KS1; ++k) f1[k] = frag(img, OF1 + k * NTB + nt, lane);
 #pragma unroll
-    for (int k = 0; k < 9 * KSW; ++k) f2[k] = (WIDE_EXP & 16) ? bf16x8{} : frag(img, OF2 + k * NTB + nt, lane);
+    for (int k = 0; k < 9 * KSW; ++k) f2[k] = (WIDE_EXP & 16) ? hx8{} : frag(img, OF2 + k * NTB + nt, lane);
     const Org o = tile_org(a, blockIdx.x);
     const Scal s = load_scal(p);
     make_tables(a, o, segv, runv);
@@ -325,7 +324,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         for (int k = 0; k < KS1; ++k) acc = mfma(ld16(u1h + (16 * m + row) * C + 32 * k + 8 * kb), f1[k], acc);
         if (ob < BR) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) t2h[(16 * m + 4 * kb + j) * BR + ob] = f2bf(elu_f(acc[j] + s.b2a) + s.b2b);
+            for (int j = 0; j < 4; ++j) t2h[(16 * m + 4 * kb + j) * BR + ob] = f2h(elu_f(acc[j] + s.b2a) + s.b2b);
         }
     }
     __syncthreads();
@@ -352,7 +351,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         const int v = 16 * (2 * hf + mm) + row, d = v & 7;
 #pragma unroll
         for (int kk = 0; kk < ((WIDE_EXP & 4) ? 0 : 9); ++kk) {
-            const bf16_t *wbase = t2h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
+            const h16_t *wbase = t2h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
 #pragma unroll
             for (int k = 0; k < KSW; ++k) acc3[mm] = mfma(ld8(wbase + 32 * k), f2[kk * KSW + k], acc3[mm]);
         }
@@ -363,7 +362,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         for (int mm = 0; mm < 2; ++mm)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                t3s[(16 * (2 * hf + mm) + 4 * kb + j) * BR + ob] = f2bf(elu_f(acc3[mm][j] + s.b3a) + s.b3b);
+                t3s[(16 * (2 * hf + mm) + 4 * kb + j) * BR + ob] = f2h(elu_f(acc3[mm][j] + s.b3a) + s.b3b);
     }
     __syncthreads();
     if (!(WIDE_EXP & 8) && t3o) tile_to_global<false>(runv, t3s, t3o);
@@ -372,7 +371,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
     for (int q = 0; q < 2; ++q) {
         const int ntc = nt + NTB * q;
         if (!(WIDE_EXP & 8) && ntc < NTC) {
-            bf16x8 f3[KSB];
+            hx8 f3[KSB];
 #pragma unroll
             for (int k = 0; k < KSB; ++k) f3[k] = frag(img, OF3 + k * NTC + ntc, lane);
             const int co = 16 * ntc + row;
@@ -394,16 +393,16 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
 // ============================================================================================ backward
 // gx and the activation gradients of one tile; gz3 / gz1 (bf16) and 8 scalar partials out.
 __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__restrict__ g, const float *__restrict__ x,
-                                                      const bf16_t *__restrict__ t2, const bf16_t *__restrict__ t3,
+                                                      const h16_t *__restrict__ t2, const h16_t *__restrict__ t3,
                                                       const uint4 *__restrict__ img, vq3d_preact_params p,
-                                                      float *__restrict__ gx, bf16_t *__restrict__ gz3o,
-                                                      bf16_t *__restrict__ gz1o, float *__restrict__ part) {
+                                                      float *__restrict__ gx, h16_t *__restrict__ gz3o,
+                                                      h16_t *__restrict__ gz1o, float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *gh = reinterpret_cast<bf16_t *>(smem);  // g (bf16) on the halo [HV][C]
-    bf16_t *t3h = gh + HV * C + PADE;                // t3 on the halo [HV][BR]
-    bf16_t *z3h = t3h + HV * BR;                     // gz3 on the halo [HV][BR]
-    bf16_t *t2s = z3h + HV * BR + PADE;              // t2 on the tile [TV][BR]
-    bf16_t *z1s = t2s + TV * BR;                     // gz1 on the tile [TV][BR]
+    h16_t *gh = reinterpret_cast<h16_t *>(smem);  // g (bf16) on the halo [HV][C]
+    h16_t *t3h = gh + HV * C + PADE;                // t3 on the halo [HV][BR]
+    h16_t *z3h = t3h + HV * BR;                     // gz3 on the halo [HV][BR]
+    h16_t *t2s = z3h + HV * BR + PADE;              // t2 on the tile [TV][BR]
+    h16_t *z1s = t2s + TV * BR;                     // gz1 on the tile [TV][BR]
     float *gI = reinterpret_cast<float *>(z1s + TV * BR + PADE);  // g (fp32) on the tile [TV][C]
     float *xI = gI + TV * C;                                        // x (fp32) on the tile [TV][C]
     int *segv = reinterpret_cast<int *>(xI + TV * C);
@@ -448,7 +447,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         const int i = min(tid + u * NT, NG - 1), seg = i / QX, c4 = i - seg * QX;
         vg[u] = reinterpret_cast<const float4 *>(g + int64_t(segv[seg]) * C)[c4];
     }
-    bf16x8 f3[KS1];
+    hx8 f3[KS1];
 #pragma unroll
     for (int k = 0; k < KS1; ++k) f3[k] = frag(img, OG3 + k * NTB + nt, lane);
 #pragma unroll
@@ -476,9 +475,9 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         }
     }
     __syncthreads();
-    bf16x8 f2[9 * KSW];
+    hx8 f2[9 * KSW];
 #pragma unroll
-    for (int k = 0; k < 9 * KSW; ++k) f2[k] = (WIDE_EXP & 16) ? bf16x8{} : frag(img, OG2 + k * NTB + nt, lane);
+    for (int k = 0; k < 9 * KSW; ++k) f2[k] = (WIDE_EXP & 16) ? hx8{} : frag(img, OG2 + k * NTB + nt, lane);
     // gz3 = bf16(scale * W3^T g * elu'(t3)) on the halo
     float s3b = 0.f, s3a = 0.f, ssc = 0.f;
     const int ob = 16 * nt + row;
@@ -495,7 +494,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
                 const int hv = 16 * m + 4 * kb + j;
                 const float t3v = bf(t3h[hv * BR + ob]), gt3 = s.sc * acc[j];
                 const float z = gt3 * elu_d_act(t3v, s.b3b);
-                z3h[hv * BR + ob] = f2bf(z);
+                z3h[hv * BR + ob] = f2h(z);
                 if (mj & (1u << j)) {
                     s3b += gt3;
                     s3a += z;
@@ -518,7 +517,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         const int v = 16 * m + row, d = v & 7;
 #pragma unroll
         for (int kk = 0; kk < ((WIDE_EXP & 4) ? 0 : 9); ++kk) {
-            const bf16_t *wbase = z3h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
+            const h16_t *wbase = z3h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
 #pragma unroll
             for (int k = 0; k < KSW; ++k) acc = mfma(ld8(wbase + 32 * k), f2[kk * KSW + k], acc);
         }
@@ -529,7 +528,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
                 const float z1 = acc[j] * elu_d_act(bf(t2s[vv * BR + ob]), s.b2b);
                 s2b += acc[j];
                 s2a += z1;
-                z1s[vv * BR + ob] = f2bf(z1);
+                z1s[vv * BR + ob] = f2h(z1);
             }
         }
     }
@@ -541,7 +540,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
     for (int q = 0; q < 2; ++q) {
         const int ntc = nt + NTB * q;
         if (!(WIDE_EXP & 8) && ntc < NTC) {
-            bf16x8 f1[KSB];
+            hx8 f1[KSB];
 #pragma unroll
             for (int k = 0; k < KSB; ++k) f1[k] = frag(img, OG1 + k * NTC + ntc, lane);
             const int c = 16 * ntc + row;
@@ -580,17 +579,17 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
 // W1 (sum gz1 (x) u1) and G3 (sum t3 (x) g) over a 128-voxel chunk; wave (m-tile w % 3 of o,
 // W1 or G3).  Voxels are the MFMA reduction axis: channel-major LDS copies.
 __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float *__restrict__ g,
-                                                   const float *__restrict__ x, const bf16_t *__restrict__ t2,
-                                                   const bf16_t *__restrict__ t3, const bf16_t *__restrict__ gz3,
-                                                   const bf16_t *__restrict__ gz1, vq3d_preact_params p,
+                                                   const float *__restrict__ x, const h16_t *__restrict__ t2,
+                                                   const h16_t *__restrict__ t3, const h16_t *__restrict__ gz3,
+                                                   const h16_t *__restrict__ gz1, vq3d_preact_params p,
                                                    float *__restrict__ p2a, float *__restrict__ p2b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int mt = wave % 3, hf = wave / 3;
     if (int(blockIdx.x) < 9 * nch) {
         const int kk = blockIdx.x / nch, ch = blockIdx.x - kk * nch, kh = kk / 3, kw = kk - 3 * kh;
-        bf16_t *zT = reinterpret_cast<bf16_t *>(smem);  // gz3 channel-major [48][ZP]
-        bf16_t *tT = zT + 48 * ZP;                      // t2 shifted by the tap row, [36][CST]: [run][RP]
+        h16_t *zT = reinterpret_cast<h16_t *>(smem);  // gz3 channel-major [48][ZP]
+        h16_t *tT = zT + 48 * ZP;                      // t2 shifted by the tap row, [36][CST]: [run][RP]
         int *rline = reinterpret_cast<int *>(tT + BR * CST);  // per run: source line base, d0
         int *rd0 = rline + NRUNC;
         const int v0 = ch * CHV;
@@ -661,7 +660,7 @@ __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float
         }
 #pragma unroll 2
         for (int ks = 0; ks < CHV / 32; ++ks) {
-            const bf16x8 af = ld16(zT + (16 * mt + row) * ZP + 32 * ks + 8 * kb);
+            const hx8 af = ld16(zT + (16 * mt + row) * ZP + 32 * ks + 8 * kb);
             const int roff = (4 * ks + kb) * RP;
 #pragma unroll
             for (int n = 0; n < 4; ++n)
@@ -684,10 +683,10 @@ __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float
     // W1 / G3 of a 128-voxel chunk
     const int ch = blockIdx.x - 9 * nch;
     const Scal s = load_scal(p);
-    bf16_t *z1T = reinterpret_cast<bf16_t *>(smem);  // [48][SP] gz1
-    bf16_t *t3T = z1T + 48 * SP;                     // [48][SP] t3
-    bf16_t *u1T = t3T + 48 * SP;                     // [80][SP] u1
-    bf16_t *grT = u1T + 80 * SP;                     // [80][SP] g
+    h16_t *z1T = reinterpret_cast<h16_t *>(smem);  // [48][SP] gz1
+    h16_t *t3T = z1T + 48 * SP;                     // [48][SP] t3
+    h16_t *u1T = t3T + 48 * SP;                     // [80][SP] u1
+    h16_t *grT = u1T + 80 * SP;                     // [80][SP] g
     const int v0 = ch * SUBV;
     {
         constexpr int Q = BR / 4, N = 2 * (SUBV / 2) * Q, P = (N + NT - 1) / NT;
@@ -698,7 +697,7 @@ __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float
         for (int u = 0; u < P; ++u) {
             const int i = min(tid + u * NT, N - 1), which = i / (N / 2), ii = i - which * (N / 2), pr = ii / Q,
                       q = ii - pr * Q;
-            const bf16_t *src = which ? t3 : gz1;
+            const h16_t *src = which ? t3 : gz1;
             bl[u] = reinterpret_cast<const uint2 *>(src + int64_t(v0 + 2 * pr) * BR)[q];
             bh[u] = reinterpret_cast<const uint2 *>(src + int64_t(v0 + 2 * pr + 1) * BR)[q];
         }
@@ -728,7 +727,7 @@ __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float
             if (i < NC) {
                 const int which = i / (NC / 2), ii = i - which * (NC / 2), pr = ii / QC, q = ii - pr * QC;
                 float l4[4] = {fl[u].x, fl[u].y, fl[u].z, fl[u].w}, h4[4] = {fh[u].x, fh[u].y, fh[u].z, fh[u].w};
-                bf16_t *dT = which ? grT : u1T;
+                h16_t *dT = which ? grT : u1T;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     float lv = l4[k], hv = h4[k];
@@ -743,14 +742,14 @@ __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float
     }
     __syncthreads();
     // wave: o m-tile mt; hf 0: W1 [o][c] (gz1 x u1), hf 1: G3 [o][co] (t3 x g)
-    const bf16_t *aT = hf ? t3T : z1T, *bT = hf ? grT : u1T;
+    const h16_t *aT = hf ? t3T : z1T, *bT = hf ? grT : u1T;
     f32x4 acc[NTC];
 #pragma unroll
     for (int n = 0; n < NTC; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < SUBV / 32; ++ks) {
         const int ko = 32 * ks + 8 * kb;
-        const bf16x8 af = ld16(aT + (16 * mt + row) * SP + ko);
+        const hx8 af = ld16(aT + (16 * mt + row) * SP + ko);
 #pragma unroll
         for (int n = 0; n < NTC; ++n) acc[n] = mfma(af, ld16(bT + (16 * n + row) * SP + ko), acc[n]);
     }
@@ -901,17 +900,19 @@ size_t vq3d_preact_wide_image_bytes(int32_t channels, int32_t branch) {
     return (channels == C && branch == BR) ? size_t(NFRAG) * 64 * 16 : 0;
 }
 
-int vq3d_preact_wide_pack(int32_t nblocks, int32_t channels, int32_t branch, const float *const *params, void *image,
-                          vq3d_stream_t stream) {
+int vq3d_preact_wide_pack(int32_t dtype, int32_t nblocks, int32_t channels, int32_t branch, const float *const *params,
+                          void *image, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("preact_wide_pack: dtype must be the 16-bit format of this build");
     if (channels != C || branch != BR || nblocks < 1) return fail("preact_wide_pack: unsupported block shape");
     if (!params || !image) return fail("preact_wide_pack: null pointer");
     k_wide_pack<<<dim3(NFRAG, nblocks), 64, 0, as_stream(stream)>>>(params, static_cast<uint4 *>(image));
     return check_launch("preact_wide_pack");
 }
 
-int vq3d_preact_wide_fwd(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+int vq3d_preact_wide_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
                          const float *x, const void *image, const vq3d_preact_params *p, float *out, void *t2, void *t3,
                          vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("preact_wide_fwd: dtype must be the 16-bit format of this build");
     if (!vq3d_preact_wide_supported(batch, channels, branch, h, w, dd))
         return fail("preact_wide_fwd: shape outside the fused wide-block kernels");
     if (!x || !image || !p || !out) return fail("preact_wide_fwd: null pointer");
@@ -919,7 +920,7 @@ int vq3d_preact_wide_fwd(int32_t batch, int32_t channels, int32_t branch, int32_
     set_lds_limits();
     const WArgs a = make_args(batch, h, w, dd);
     k_wide_fwd<<<a.ntiles, NT, kFwdLds, as_stream(stream)>>>(a, x, static_cast<const uint4 *>(image), *p, out,
-                                                             static_cast<bf16_t *>(t2), static_cast<bf16_t *>(t3));
+                                                             static_cast<h16_t *>(t2), static_cast<h16_t *>(t3));
     return check_launch("preact_wide_fwd");
 }
 
@@ -927,10 +928,11 @@ size_t vq3d_preact_wide_workspace_bytes(int32_t batch, int32_t h, int32_t w, int
     return ws_layout(batch, h, w, dd).total;
 }
 
-int vq3d_preact_wide_bwd_data(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
-                              const float *g, const float *x, const void *t2, const void *t3, const void *image,
-                              const vq3d_preact_params *p, void *workspace, size_t workspace_bytes, float *gx,
-                              vq3d_stream_t stream) {
+int vq3d_preact_wide_bwd_data(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                              int32_t dd, const float *g, const float *x, const void *t2, const void *t3,
+                              const void *image, const vq3d_preact_params *p, void *workspace, size_t workspace_bytes,
+                              float *gx, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("preact_wide_bwd_data: dtype must be the 16-bit format of this build");
     if (!vq3d_preact_wide_supported(batch, channels, branch, h, w, dd))
         return fail("preact_wide_bwd_data: shape outside the fused wide-block kernels");
     if (!g || !x || !t2 || !t3 || !image || !p || !workspace || !gx) return fail("preact_wide_bwd_data: null pointer");
@@ -941,18 +943,18 @@ int vq3d_preact_wide_bwd_data(int32_t batch, int32_t channels, int32_t branch, i
     char *ws = static_cast<char *>(workspace);
     const WArgs a = make_args(batch, h, w, dd);
     k_wide_bwd_data<<<a.ntiles, NT, kBwdLds, as_stream(stream)>>>(
-        a, g, x, static_cast<const bf16_t *>(t2), static_cast<const bf16_t *>(t3), static_cast<const uint4 *>(image),
-        *p, gx, reinterpret_cast<bf16_t *>(ws + l.gz3), reinterpret_cast<bf16_t *>(ws + l.gz1),
+        a, g, x, static_cast<const h16_t *>(t2), static_cast<const h16_t *>(t3), static_cast<const uint4 *>(image),
+        *p, gx, reinterpret_cast<h16_t *>(ws + l.gz3), reinterpret_cast<h16_t *>(ws + l.gz1),
         reinterpret_cast<float *>(ws + l.p1));
     return check_launch("preact_wide_bwd_data");
 }
 
-int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
-                                const float *g, const float *x, const void *t2, const void *t3,
+int vq3d_preact_wide_bwd_weight(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                                int32_t dd, const float *g, const float *x, const void *t2, const void *t3,
                                 const vq3d_preact_params *p, const vq3d_preact_grads *gr, const void *workspace,
                                 size_t workspace_bytes, vq3d_stream_t stream) {
-    return vq3d_preact_wide_bwd_weight_stages(3, batch, channels, branch, h, w, dd, g, x, t2, t3, p, gr, workspace,
-                                              workspace_bytes, stream);
+    return vq3d_preact_wide_bwd_weight_stages(3, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, p, gr,
+                                              workspace, workspace_bytes, stream);
 }
 
 int vq3d_preact_wide_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
@@ -974,10 +976,11 @@ int vq3d_preact_wide_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32
     return check_launch("preact_wide_reduce_run");
 }
 
-int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t batch, int32_t channels, int32_t branch, int32_t h,
-                                       int32_t w, int32_t dd, const float *g, const float *x, const void *t2,
+int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                                       int32_t h, int32_t w, int32_t dd, const float *g, const float *x, const void *t2,
                                        const void *t3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                                        const void *workspace, size_t workspace_bytes, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("preact_wide_bwd_weight: dtype must be the 16-bit format of this build");
     if (stages < 1 || stages > 3) return fail("preact_wide_bwd_weight: stages must be a mask of 1 | 2");
     if (!vq3d_preact_wide_supported(batch, channels, branch, h, w, dd))
         return fail("preact_wide_bwd_weight: shape outside the fused wide-block kernels");
@@ -996,10 +999,10 @@ int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t batch, int32_t ch
     float *p2a = reinterpret_cast<float *>(const_cast<char *>(ws) + l.p2a);
     float *p2b = reinterpret_cast<float *>(const_cast<char *>(ws) + l.p2b);
     if (stages & 1)
-        k_wide_wgrad<<<9 * nch + nchb, NT, kWgLds, s>>>(a, nch, g, x, static_cast<const bf16_t *>(t2),
-                                                   static_cast<const bf16_t *>(t3),
-                                                   reinterpret_cast<const bf16_t *>(ws + l.gz3),
-                                                   reinterpret_cast<const bf16_t *>(ws + l.gz1), *p, p2a, p2b);
+        k_wide_wgrad<<<9 * nch + nchb, NT, kWgLds, s>>>(a, nch, g, x, static_cast<const h16_t *>(t2),
+                                                   static_cast<const h16_t *>(t3),
+                                                   reinterpret_cast<const h16_t *>(ws + l.gz3),
+                                                   reinterpret_cast<const h16_t *>(ws + l.gz1), *p, p2a, p2b);
     if (!(stages & 2)) return check_launch("preact_wide_bwd_weight");
     RedOut o{G.dw1, G.dw2, G.dw3, G.dbias1a, G.dbias1b, G.dbias2a, G.dbias2b, G.dbias3a, G.dbias3b,
              G.dscale, G.dbias4, p->scale};

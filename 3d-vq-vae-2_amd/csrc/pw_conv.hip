@@ -82,9 +82,9 @@ __device__ __forceinline__ void copy_in_pro(T *__restrict__ dst, const T *__rest
                 uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float lo = pro.apply(__uint_as_float(w4[j] << 16));
-                    const float hi = pro.apply(__uint_as_float(w4[j] & 0xffff0000u));
-                    w4[j] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+                    const float lo = pro.apply(h2f_lo(w4[j]));
+                    const float hi = pro.apply(h2f_hi(w4[j]));
+                    w4[j] = uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16);
                 }
                 u = uint4{w4[0], w4[1], w4[2], w4[3]};
             } else {
@@ -272,23 +272,23 @@ __device__ __forceinline__ void row_ld(const T *__restrict__ p, float (&o)[C]) {
             o[0] = ld(p);
         } else if constexpr (C == 2) {
             const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
-            o[0] = __uint_as_float(u << 16);
-            o[1] = __uint_as_float(u & 0xffff0000u);
+            o[0] = h2f_lo(u);
+            o[1] = h2f_hi(u);
         } else if constexpr (C == 4) {
             const uint2 u = *reinterpret_cast<const uint2 *>(p);
             const uint32_t q[2] = {u.x, u.y};
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                o[2 * j] = __uint_as_float(q[j] << 16);
-                o[2 * j + 1] = __uint_as_float(q[j] & 0xffff0000u);
+                o[2 * j] = h2f_lo(q[j]);
+                o[2 * j + 1] = h2f_hi(q[j]);
             }
         } else {
             const uint4 u = *reinterpret_cast<const uint4 *>(p);
             const uint32_t q[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                o[2 * j] = __uint_as_float(q[j] << 16);
-                o[2 * j + 1] = __uint_as_float(q[j] & 0xffff0000u);
+                o[2 * j] = h2f_lo(q[j]);
+                o[2 * j + 1] = h2f_hi(q[j]);
             }
         }
     } else {
@@ -305,7 +305,7 @@ __device__ __forceinline__ void row_st(T *__restrict__ p, const float (&v)[C]) {
         } else {
             uint32_t q[C / 2];
 #pragma unroll
-            for (int j = 0; j < C / 2; ++j) q[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+            for (int j = 0; j < C / 2; ++j) q[j] = uint32_t(f2h(v[2 * j])) | (uint32_t(f2h(v[2 * j + 1])) << 16);
             if constexpr (C == 2) *reinterpret_cast<uint32_t *>(p) = q[0];
             else if constexpr (C == 4) *reinterpret_cast<uint2 *>(p) = uint2{q[0], q[1]};
             else *reinterpret_cast<uint4 *>(p) = uint4{q[0], q[1], q[2], q[3]};
@@ -471,8 +471,8 @@ __device__ __forceinline__ void load_run(const T *__restrict__ p, int vw, float 
                 const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    o[8 * q + 2 * j] = __uint_as_float(w4[j] << 16);
-                    o[8 * q + 2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+                    o[8 * q + 2 * j] = h2f_lo(w4[j]);
+                    o[8 * q + 2 * j + 1] = h2f_hi(w4[j]);
                 }
             }
             return;
@@ -481,10 +481,10 @@ __device__ __forceinline__ void load_run(const T *__restrict__ p, int vw, float 
 #pragma unroll
             for (int q = 0; q < N / 4; ++q) {
                 const uint2 u = reinterpret_cast<const uint2 *>(p)[q];
-                o[4 * q] = __uint_as_float(u.x << 16);
-                o[4 * q + 1] = __uint_as_float(u.x & 0xffff0000u);
-                o[4 * q + 2] = __uint_as_float(u.y << 16);
-                o[4 * q + 3] = __uint_as_float(u.y & 0xffff0000u);
+                o[4 * q] = h2f_lo(u.x);
+                o[4 * q + 1] = h2f_hi(u.x);
+                o[4 * q + 2] = h2f_lo(u.y);
+                o[4 * q + 3] = h2f_hi(u.y);
             }
             return;
         }
@@ -658,26 +658,25 @@ static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, con
 // W[k][n]) lives in LDS as packed B fragments.  Operands are bf16, as the reference's autocast
 // 1x1 convs run in fp16 (the VALU kernels above keep the weights fp32).
 namespace {
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // 4 consecutive bf16 (8-byte aligned when `vec`) <-> fp32; `cnt` of them valid
-__device__ __forceinline__ void ld4(const bf16_t *p, bool vec, int cnt, float (&o)[4]) {
+__device__ __forceinline__ void ld4(const h16_t *p, bool vec, int cnt, float (&o)[4]) {
     if (vec) {
         const u32x2 u = *reinterpret_cast<const u32x2 *>(p);
-        o[0] = __uint_as_float(u[0] << 16);
-        o[1] = __uint_as_float(u[0] & 0xffff0000u);
-        o[2] = __uint_as_float(u[1] << 16);
-        o[3] = __uint_as_float(u[1] & 0xffff0000u);
+        o[0] = h2f_lo(u[0]);
+        o[1] = h2f_hi(u[0]);
+        o[2] = h2f_lo(u[1]);
+        o[3] = h2f_hi(u[1]);
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = j < cnt ? ld(p + j) : 0.f;
     }
 }
-__device__ __forceinline__ void st4(bf16_t *p, bool vec, int cnt, const float (&o)[4]) {
+__device__ __forceinline__ void st4(h16_t *p, bool vec, int cnt, const float (&o)[4]) {
     if (vec) {
-        *reinterpret_cast<u32x2 *>(p) = u32x2{uint32_t(f2bf(o[0])) | (uint32_t(f2bf(o[1])) << 16),
-                                             uint32_t(f2bf(o[2])) | (uint32_t(f2bf(o[3])) << 16)};
+        *reinterpret_cast<u32x2 *>(p) = u32x2{uint32_t(f2h(o[0])) | (uint32_t(f2h(o[1])) << 16),
+                                             uint32_t(f2h(o[2])) | (uint32_t(f2h(o[3])) << 16)};
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -691,10 +690,10 @@ struct MmArgs {
 };
 
 template <int NTN, bool DG>
-__global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const bf16_t *__restrict__ in,
-                                               const bf16_t *__restrict__ in2, const float *__restrict__ w,
-                                               FwdEpi<bf16_t> fe, BwdEpi<bf16_t> be, const float *__restrict__ gscale,
-                                               bf16_t *__restrict__ out, bf16_t *__restrict__ out2, float *dpre,
+__global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16_t *__restrict__ in,
+                                               const h16_t *__restrict__ in2, const float *__restrict__ w,
+                                               FwdEpi<h16_t> fe, BwdEpi<h16_t> be, const float *__restrict__ gscale,
+                                               h16_t *__restrict__ out, h16_t *__restrict__ out2, float *dpre,
                                                float *dpost, float *part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     u32x4 *wB = reinterpret_cast<u32x4 *>(smem);  // [KS][NTN][64]: this workgroup's NTN n-tiles
@@ -713,7 +712,7 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const bf1
                 const int k = k0 + 2 * j + h;
                 f2[h] = (k < m.K && n < m.N) ? (DG ? w[int64_t(k) * Ct + n] : w[int64_t(n) * Ct + k]) : 0.f;
             }
-            q[j] = uint32_t(f2bf(f2[0])) | (uint32_t(f2bf(f2[1])) << 16);
+            q[j] = uint32_t(f2h(f2[0])) | (uint32_t(f2h(f2[1])) << 16);
         }
         wB[i] = u32x4{q[0], q[1], q[2], q[3]};
     }
@@ -747,15 +746,15 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const bf1
             if (!raw && 32 * ks + 8 * kb < m.K) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    a[j] = uint32_t(f2bf(pro.apply(__uint_as_float(a[j] << 16)))) |
-                           (uint32_t(f2bf(pro.apply(__uint_as_float(a[j] & 0xffff0000u)))) << 16);
+                    a[j] = uint32_t(f2h(pro.apply(h2f_lo(a[j])))) |
+                           (uint32_t(f2h(pro.apply(h2f_hi(a[j])))) << 16);
             }
-            const bf16x8 af = __builtin_bit_cast(bf16x8, a);
+            const hx8 af = __builtin_bit_cast(hx8, a);
             // D^T[n][v] = W'^T X^T: the weight fragment is the A operand, the voxel rows the B operand,
             // so a lane ends with 4 consecutive output channels of one voxel (vector epilogue)
 #pragma unroll
             for (int t = 0; t < NTN; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wB[(ks * NTN + t) * 64 + lane]),
+                acc[t] = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, wB[(ks * NTN + t) * 64 + lane]),
                                                                  af, acc[t], 0, 0, 0);
         }
         // D^T[channel 16 t' + 4 kb + j][voxel v0 + row] of n-tile t' = nt0 + t
@@ -844,7 +843,7 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const bf1
 
 // the matrix-core path, or false when the conv is not one of its shapes
 static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w,
-                          const float *pa, const float *pb, const FwdEpi<bf16_t> &fe, const BwdEpi<bf16_t> &be,
+                          const float *pa, const float *pb, const FwdEpi<h16_t> &fe, const BwdEpi<h16_t> &be,
                           const float *gscale, void *out, void *out2, float *dpre, float *dpost, void *ws,
                           size_t ws_bytes, hipStream_t s) {
     const int64_t nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
@@ -876,11 +875,11 @@ static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, c
     ConvArgs ca = make_args(d, pa, pb);
 #define MM(NT_)                                                                                                 \
     if (dgrad)                                                                                                  \
-        k_pw_mma<NT_, true><<<nb, 256, lds, s>>>(m, ca, (const bf16_t *)in, nullptr, w, fe, be, gscale,         \
-                                                 (bf16_t *)out, (bf16_t *)out2, dpre, dpost, part);             \
+        k_pw_mma<NT_, true><<<nb, 256, lds, s>>>(m, ca, (const h16_t *)in, nullptr, w, fe, be, gscale,         \
+                                                 (h16_t *)out, (h16_t *)out2, dpre, dpost, part);             \
     else                                                                                                        \
-        k_pw_mma<NT_, false><<<nb, 256, lds, s>>>(m, ca, (const bf16_t *)in, (const bf16_t *)in2, w, fe, be,    \
-                                                  nullptr, (bf16_t *)out, nullptr, nullptr, nullptr, nullptr);
+        k_pw_mma<NT_, false><<<nb, 256, lds, s>>>(m, ca, (const h16_t *)in, (const h16_t *)in2, w, fe, be,    \
+                                                  nullptr, (h16_t *)out, nullptr, nullptr, nullptr, nullptr);
     switch (NTN) {
     case 1: MM(1) break;
     case 2: MM(2) break;
@@ -906,7 +905,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     const bool want_part = dgrad && (dpre || dpost);
     // ---- 8 .. 256 channels on the mid grids: matrix cores
-    if constexpr (std::is_same<T, bf16_t>::value) {
+    if constexpr (std::is_same<T, h16_t>::value) {
         if (launch_pw_mma(d, dgrad, in, in2, w, pa, pb, fe, be, gscale, out, out2, dpre, dpost, ws, ws_bytes, s))
             return check_launch(dgrad ? "conv3d_bwd_data(pointwise mma)" : "conv3d_fwd(pointwise mma)");
     }
@@ -1019,8 +1018,8 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
 template int launch_pw1<float>(const vq3d_conv_desc *, bool, const void *, const void *, const float *, const float *,
                                const float *, const FwdEpi<float> &, const BwdEpi<float> &, const float *, void *,
                                void *, float *, float *, void *, size_t, hipStream_t);
-template int launch_pw1<bf16_t>(const vq3d_conv_desc *, bool, const void *, const void *, const float *,
-                                const float *, const float *, const FwdEpi<bf16_t> &, const BwdEpi<bf16_t> &,
+template int launch_pw1<h16_t>(const vq3d_conv_desc *, bool, const void *, const void *, const float *,
+                                const float *, const float *, const FwdEpi<h16_t> &, const BwdEpi<h16_t> &,
                                 const float *, void *, void *, float *, float *, void *, size_t, hipStream_t);
 
 }  // namespace vq3d

@@ -198,31 +198,31 @@ __device__ __forceinline__ void load_row(const T *__restrict__ p, float (&o)[C])
             o[0] = ld(p);
         } else if constexpr (C == 2) {
             const uint32_t u = *reinterpret_cast<const uint32_t *>(p);
-            o[0] = __uint_as_float(u << 16);
-            o[1] = __uint_as_float(u & 0xffff0000u);
+            o[0] = h2f_lo(u);
+            o[1] = h2f_hi(u);
         } else if constexpr (C == 4) {
             const uint2 u = *reinterpret_cast<const uint2 *>(p);
             const uint32_t w[2] = {u.x, u.y};
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                o[2 * j] = __uint_as_float(w[j] << 16);
-                o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+                o[2 * j] = h2f_lo(w[j]);
+                o[2 * j + 1] = h2f_hi(w[j]);
             }
         } else if constexpr (C == 8) {
             const uint4 u = *reinterpret_cast<const uint4 *>(p);
             const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                o[2 * j] = __uint_as_float(w[j] << 16);
-                o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+                o[2 * j] = h2f_lo(w[j]);
+                o[2 * j + 1] = h2f_hi(w[j]);
             }
         } else if constexpr (C % 2 == 0) {  // rows 4-byte aligned
             const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
 #pragma unroll
             for (int j = 0; j < C / 2; ++j) {
                 const uint32_t u = q[j];
-                o[2 * j] = __uint_as_float(u << 16);
-                o[2 * j + 1] = __uint_as_float(u & 0xffff0000u);
+                o[2 * j] = h2f_lo(u);
+                o[2 * j + 1] = h2f_hi(u);
             }
         } else {
 #pragma unroll
@@ -356,15 +356,14 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
 // VC voxels is contiguous); both operands come through the transposing ds_read_b64_tr_b16.  Waves
 // split the co tiles (nwm of them) and the chunk's K-steps (4 / nwm); per-workgroup partials are
 // combined over the K-split waves in a fixed order and written like k_pw_wgrad's.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-__device__ __forceinline__ bf16x8 tr8(const bf16_t *p0, const bf16_t *p1) {
+__device__ __forceinline__ hx8 tr8(const h16_t *p0, const h16_t *p1) {
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return __builtin_bit_cast(hx8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 struct WmArgs {
@@ -381,14 +380,14 @@ struct WmArgs {
 constexpr int kWmU = 4;  // 16-byte units in flight per thread
 
 template <int MPW, int NTT>
-__global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__restrict__ x,
-                                                     const bf16_t *__restrict__ x2, const bf16_t *__restrict__ g,
+__global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const h16_t *__restrict__ x,
+                                                     const h16_t *__restrict__ x2, const h16_t *__restrict__ g,
                                                      int pro_kind, const float *pro_a, const float *pro_b,
                                                      float *__restrict__ part, WgOut out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ float red[8];
-    bf16_t *xs = reinterpret_cast<bf16_t *>(smem);  // [VC][XP]
-    bf16_t *gs = xs + a.VC * a.XP;                  // [VC][GP]
+    h16_t *xs = reinterpret_cast<h16_t *>(smem);  // [VC][XP]
+    h16_t *gs = xs + a.VC * a.XP;                  // [VC][GP]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int grp = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
     const int wm = wave % a.nwm, wk = wave / a.nwm, nwk = 4 / a.nwm;
@@ -396,7 +395,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
     const bool raw = pro.kind == VQ3D_PRO_NONE;
     // columns staging never writes: the constant-1 column of x and the zero padding
     for (int v = tid; v < a.VC; v += 256) {
-        for (int c = a.Ct; c < a.XP; ++c) xs[v * a.XP + c] = c == a.Ct ? bf16_t(0x3f80) : bf16_t(0);
+        for (int c = a.Ct; c < a.XP; ++c) xs[v * a.XP + c] = c == a.Ct ? h16_t(0x3f80) : h16_t(0);
         for (int c = a.N; c < a.GP; ++c) gs[v * a.GP + c] = 0;
     }
 
@@ -419,7 +418,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
             const int u = tid + k * 256;
             r[k] = u32x4{0u, 0u, 0u, 0u};
             if (u >= nu) continue;
-            const bf16_t *src;
+            const h16_t *src;
             int e, C;
             if (u < a.ua) src = x + v0 * a.Ca, e = 8 * u, C = a.Ca;
             else if (u < a.ua + a.ub) src = x2 + v0 * a.Cb, e = 8 * (u - a.ua), C = a.Cb;
@@ -441,7 +440,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
         for (int k = 0; k < kWmU; ++k) {
             const int u = tid + k * 256;
             if (u >= nu) continue;
-            bf16_t *dst;
+            h16_t *dst;
             int e, C, off, P;
             bool isx = true;
             if (u < a.ua) e = 8 * u, C = a.Ca, off = 0, P = a.XP, dst = xs;
@@ -451,9 +450,9 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
             if (isx && !raw)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float lo = pro.apply(__uint_as_float(w[j] << 16));
-                    const float hi = pro.apply(__uint_as_float(w[j] & 0xffff0000u));
-                    w[j] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+                    const float lo = pro.apply(h2f_lo(w[j]));
+                    const float hi = pro.apply(h2f_hi(w[j]));
+                    w[j] = uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16);
                 }
             if (C % 8 == 0) {  // the unit is 8 channels of one voxel
                 const int v = e / C, c = e - v * C;
@@ -464,7 +463,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
                 int v = e / C, c = e - v * C;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    if (v < a.VC) dst[v * P + off + c] = bf16_t(w[j >> 1] >> (16 * (j & 1)));
+                    if (v < a.VC) dst[v * P + off + c] = h16_t(w[j >> 1] >> (16 * (j & 1)));
                     if (++c == C) c = 0, ++v;
                 }
             }
@@ -484,9 +483,9 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
         __syncthreads();
         for (int ks = wk; ks < a.VC / 32; ks += nwk) {
             const int r0 = ks * 32 + 8 * grp + q;
-            const bf16_t *ga = gs + r0 * a.GP + 4 * p4;
-            const bf16_t *xa = xs + r0 * a.XP + 4 * p4;
-            bf16x8 bfr[NTT];
+            const h16_t *ga = gs + r0 * a.GP + 4 * p4;
+            const h16_t *xa = xs + r0 * a.XP + 4 * p4;
+            hx8 bfr[NTT];
 #pragma unroll
             for (int t = 0; t < NTT; ++t)
                 if (t < a.NT) bfr[t] = tr8(xa + 16 * t, xa + 16 * t + 4 * a.XP);
@@ -494,10 +493,10 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
             for (int i = 0; i < MPW; ++i) {
                 const int mt = wm + a.nwm * i;
                 if (mt >= a.MT) break;
-                const bf16x8 af = tr8(ga + 16 * mt, ga + 16 * mt + 4 * a.GP);
+                const hx8 af = tr8(ga + 16 * mt, ga + 16 * mt + 4 * a.GP);
 #pragma unroll
                 for (int t = 0; t < NTT; ++t)
-                    if (t < a.NT) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[t], acc[i][t], 0, 0, 0);
+                    if (t < a.NT) acc[i][t] = VQ3D_MFMA_16X16X32(af, bfr[t], acc[i][t], 0, 0, 0);
             }
         }
     }
@@ -552,7 +551,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const bf16_t *__
 bool plan_mma(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, WmArgs &m, int &mpw, int &ntt,
               int &nbx, size_t &lds) {
     auto al = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    if (d->dtype != VQ3D_BF16 || !al(x) || !al(x2) || !al(g)) return false;
+    if (d->dtype != VQ3D_HALF || !al(x) || !al(x2) || !al(g)) return false;
     m = WmArgs{};
     m.nvox = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
     m.Ca = d->cin;
@@ -688,7 +687,7 @@ size_t pw_wgrad_workspace(const vq3d_conv_desc *d) {
     size_t bytes = size_t(nbx) * a.ne * 4;
     WmArgs m;
     int mpw, ntt;
-    if (d->dtype == VQ3D_BF16 && plan_mma(d, nullptr, nullptr, nullptr, m, mpw, ntt, nbx, lds))
+    if (d->dtype == VQ3D_HALF && plan_mma(d, nullptr, nullptr, nullptr, m, mpw, ntt, nbx, lds))
         bytes = std::max(bytes, size_t(nbx) * m.N * (m.Ct + 1) * 4);
     return bytes;
 }
@@ -720,7 +719,7 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     if (mma) {
 #define WM(M_, N_)                                                                                              \
     else if (mpw == M_ && ntt == N_) k_pw_wgrad_mma<M_, N_><<<nbx, 256, mlds, s>>>(                            \
-        m, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g, d->pro_kind, pro_a, pro_b, part, out);
+        m, (const h16_t *)x, (const h16_t *)x2, (const h16_t *)g, d->pro_kind, pro_a, pro_b, part, out);
         if (false) {
         }
         WM(1, 1) WM(1, 2) WM(1, 4) WM(1, 8) WM(1, 16) WM(2, 1) WM(2, 2) WM(2, 4) WM(2, 8)
@@ -728,11 +727,11 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
 #undef WM
     } else if (reg_path(d) && a.vec) {
         const int key = d->cin * 16 + d->cout;
-        const bool bf = d->dtype == VQ3D_BF16;
+        const bool bf = d->dtype == VQ3D_HALF;
 #define REG(CX, CG)                                                                                            \
     case CX * 16 + CG:                                                                                         \
         if (bf)                                                                                                \
-            k_pw_wgrad_reg<bf16_t, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const bf16_t *)x, (const bf16_t *)g,  \
+            k_pw_wgrad_reg<h16_t, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const h16_t *)x, (const h16_t *)g,  \
                                                                d->pro_kind, pro_a, pro_b, part, out);         \
         else                                                                                                   \
             k_pw_wgrad_reg<float, CX, CG><<<nbx, 256, 0, s>>>(a.nvox, (const float *)x, (const float *)g,     \
@@ -744,8 +743,8 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
         default: return fail("conv3d_bwd_weight: no register-path kernel");
         }
 #undef REG
-    } else if (d->dtype == VQ3D_BF16)
-        k_pw_wgrad<bf16_t><<<grid, 256, lds, s>>>(a, (const bf16_t *)x, (const bf16_t *)x2, (const bf16_t *)g,
+    } else if (d->dtype == VQ3D_HALF)
+        k_pw_wgrad<h16_t><<<grid, 256, lds, s>>>(a, (const h16_t *)x, (const h16_t *)x2, (const h16_t *)g,
                                                    d->pro_kind, pro_a, pro_b, part, out);
     else
         k_pw_wgrad<float><<<grid, 256, lds, s>>>(a, (const float *)x, (const float *)x2, (const float *)g,

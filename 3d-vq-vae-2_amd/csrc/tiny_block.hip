@@ -437,13 +437,13 @@ int vq3d_preact_tiny_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t
     hipStream_t s = as_stream(stream);
     static bool attr = false;
     if (!attr) {
-        allow_lds(k_tiny_fwd<bf16_t>);
+        allow_lds(k_tiny_fwd<h16_t>);
         allow_lds(k_tiny_fwd<float>);
         attr = true;
     }
     const unsigned nwg = unsigned((a.nv + VPW - 1) / VPW);
-    if (dtype == VQ3D_BF16)
-        k_tiny_fwd<bf16_t><<<nwg, NTF, lds_fwd(a), s>>>(a, (const bf16_t *)x, w1, w2, w3, *p, (bf16_t *)out, saved);
+    if (dtype == VQ3D_HALF)
+        k_tiny_fwd<h16_t><<<nwg, NTF, lds_fwd(a), s>>>(a, (const h16_t *)x, w1, w2, w3, *p, (h16_t *)out, saved);
     else
         k_tiny_fwd<float><<<nwg, NTF, lds_fwd(a), s>>>(a, (const float *)x, w1, w2, w3, *p, (float *)out, saved);
     return check_launch("preact_tiny_fwd");
@@ -460,16 +460,16 @@ int vq3d_preact_tiny_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t
     hipStream_t s = as_stream(stream);
     static bool attr = false;
     if (!attr) {
-        allow_lds(k_tiny_bwd_a<bf16_t>);
+        allow_lds(k_tiny_bwd_a<h16_t>);
         allow_lds(k_tiny_bwd_a<float>);
-        allow_lds(k_tiny_bwd_b<bf16_t>);
+        allow_lds(k_tiny_bwd_b<h16_t>);
         allow_lds(k_tiny_bwd_b<float>);
         attr = true;
     }
-    if (dtype == VQ3D_BF16) {
-        k_tiny_bwd_a<bf16_t><<<28, NTA, lds_a(a), s>>>(a, (const bf16_t *)g, w2, w3, *p, *gr, saved, workspace);
-        k_tiny_bwd_b<bf16_t><<<1, NTB, lds_b(a), s>>>(a, (const bf16_t *)x, (const bf16_t *)g, w1, *p, *gr, saved,
-                                                      workspace, (bf16_t *)gx);
+    if (dtype == VQ3D_HALF) {
+        k_tiny_bwd_a<h16_t><<<28, NTA, lds_a(a), s>>>(a, (const h16_t *)g, w2, w3, *p, *gr, saved, workspace);
+        k_tiny_bwd_b<h16_t><<<1, NTB, lds_b(a), s>>>(a, (const h16_t *)x, (const h16_t *)g, w1, *p, *gr, saved,
+                                                      workspace, (h16_t *)gx);
     } else {
         k_tiny_bwd_a<float><<<28, NTA, lds_a(a), s>>>(a, (const float *)g, w2, w3, *p, *gr, saved, workspace);
         k_tiny_bwd_b<float><<<1, NTB, lds_b(a), s>>>(a, (const float *)x, (const float *)g, w1, *p, *gr, saved,

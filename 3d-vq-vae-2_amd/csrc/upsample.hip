@@ -26,17 +26,17 @@ template <typename T, int CV>
 __device__ __forceinline__ void ldv(const T *__restrict__ p, float (&o)[CV]) {
     if constexpr (sizeof(T) == 2 && CV == 4) {
         const uint2 u = *reinterpret_cast<const uint2 *>(p);
-        o[0] = __uint_as_float(u.x << 16);
-        o[1] = __uint_as_float(u.x & 0xffff0000u);
-        o[2] = __uint_as_float(u.y << 16);
-        o[3] = __uint_as_float(u.y & 0xffff0000u);
+        o[0] = h2f_lo(u.x);
+        o[1] = h2f_hi(u.x);
+        o[2] = h2f_lo(u.y);
+        o[3] = h2f_hi(u.y);
     } else if constexpr (sizeof(T) == 2 && CV == 8) {
         const uint4 u = *reinterpret_cast<const uint4 *>(p);
         const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            o[2 * j] = __uint_as_float(w4[j] << 16);
-            o[2 * j + 1] = __uint_as_float(w4[j] & 0xffff0000u);
+            o[2 * j] = h2f_lo(w4[j]);
+            o[2 * j + 1] = h2f_hi(w4[j]);
         }
     } else {
 #pragma unroll
@@ -47,12 +47,12 @@ __device__ __forceinline__ void ldv(const T *__restrict__ p, float (&o)[CV]) {
 template <typename T, int CV>
 __device__ __forceinline__ void stv(T *__restrict__ p, const float (&v)[CV]) {
     if constexpr (sizeof(T) == 2 && CV == 4) {
-        *reinterpret_cast<uint2 *>(p) = uint2{uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
-                                              uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
+        *reinterpret_cast<uint2 *>(p) = uint2{uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16),
+                                              uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16)};
     } else if constexpr (sizeof(T) == 2 && CV == 8) {
         uint32_t q[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = uint32_t(f2bf(v[2 * j])) | (uint32_t(f2bf(v[2 * j + 1])) << 16);
+        for (int j = 0; j < 4; ++j) q[j] = uint32_t(f2h(v[2 * j])) | (uint32_t(f2h(v[2 * j + 1])) << 16);
         *reinterpret_cast<uint4 *>(p) = uint4{q[0], q[1], q[2], q[3]};
     } else {
 #pragma unroll
@@ -198,9 +198,9 @@ __global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ 
 // 2 i0 - 2 .. 2 i0 + 9, six 16-byte loads; the ends past the grid carry weight 0 and are zero
 // here) instead of 16 separate 8-byte loads.  Same weights, same order of operations as k_up2_bwd,
 // so the same bits.
-__global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const bf16_t *__restrict__ gy, int dmode,
-                                                     const float *dparam, const bf16_t *__restrict__ aux,
-                                                     const bf16_t *__restrict__ addend, bf16_t *__restrict__ gx,
+__global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const h16_t *__restrict__ gy, int dmode,
+                                                     const float *dparam, const h16_t *__restrict__ aux,
+                                                     const h16_t *__restrict__ addend, h16_t *__restrict__ gx,
                                                      float *dpre, float *dpost) {
     __shared__ float red[8];
     ActDeriv dv;
@@ -242,10 +242,10 @@ __global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const bf16_t *__r
                     if (j >= 0 && j < D2) u = *reinterpret_cast<const u32x4 *>(gy + (rowb + j) * 4);
 #pragma unroll
                     for (int h2 = 0; h2 < 2; ++h2) {
-                        r[2 * k + h2][0] = __uint_as_float(u[2 * h2] << 16);
-                        r[2 * k + h2][1] = __uint_as_float(u[2 * h2] & 0xffff0000u);
-                        r[2 * k + h2][2] = __uint_as_float(u[2 * h2 + 1] << 16);
-                        r[2 * k + h2][3] = __uint_as_float(u[2 * h2 + 1] & 0xffff0000u);
+                        r[2 * k + h2][0] = h2f_lo(u[2 * h2]);
+                        r[2 * k + h2][1] = h2f_hi(u[2 * h2]);
+                        r[2 * k + h2][2] = h2f_lo(u[2 * h2 + 1]);
+                        r[2 * k + h2][3] = h2f_hi(u[2 * h2 + 1]);
                     }
                 }
                 // source i0 + s4 reads destinations 2 (i0 + s4) - 1 + t = window slot 2 s4 + 1 + t
@@ -270,8 +270,8 @@ __global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const bf16_t *__r
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const uint32_t wx = xa[s4 >> 1][2 * (s4 & 1) + (c >> 1)], wa = ad[s4 >> 1][2 * (s4 & 1) + (c >> 1)];
-                const float xv = __uint_as_float((c & 1) ? (wx & 0xffff0000u) : (wx << 16));
-                const float av = __uint_as_float((c & 1) ? (wa & 0xffff0000u) : (wa << 16));
+                const float xv = ((c & 1) ? h2f_hi(wx) : h2f_lo(wx));
+                const float av = ((c & 1) ? h2f_hi(wa) : h2f_lo(wa));
                 float v = acc[s4][c];
                 pre += v;
                 if (dv.mode) v *= dv(xv);
@@ -279,8 +279,8 @@ __global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const bf16_t *__r
                 if (addend) v += av;
                 v2[c] = v;
             }
-            res[s4 >> 1][2 * (s4 & 1)] = uint32_t(f2bf(v2[0])) | (uint32_t(f2bf(v2[1])) << 16);
-            res[s4 >> 1][2 * (s4 & 1) + 1] = uint32_t(f2bf(v2[2])) | (uint32_t(f2bf(v2[3])) << 16);
+            res[s4 >> 1][2 * (s4 & 1)] = uint32_t(f2h(v2[0])) | (uint32_t(f2h(v2[1])) << 16);
+            res[s4 >> 1][2 * (s4 & 1) + 1] = uint32_t(f2h(v2[2])) | (uint32_t(f2h(v2[3])) << 16);
         }
         *reinterpret_cast<u32x4 *>(gx + o) = res[0];
         *reinterpret_cast<u32x4 *>(gx + o + 8) = res[1];
@@ -311,27 +311,27 @@ struct UT {
 
 // C consecutive bf16 at LDS element offset e (8-byte reads when C % 4 == 0) as fp32
 template <int C>
-__device__ __forceinline__ void lds_vox(const bf16_t *s, int e, float (&o)[C]) {
+__device__ __forceinline__ void lds_vox(const h16_t *s, int e, float (&o)[C]) {
     if constexpr (C % 4 == 0) {
 #pragma unroll
         for (int j = 0; j < C / 4; ++j) {
             const u32x2 u = *reinterpret_cast<const u32x2 *>(s + e + 4 * j);
-            o[4 * j] = __uint_as_float(u[0] << 16);
-            o[4 * j + 1] = __uint_as_float(u[0] & 0xffff0000u);
-            o[4 * j + 2] = __uint_as_float(u[1] << 16);
-            o[4 * j + 3] = __uint_as_float(u[1] & 0xffff0000u);
+            o[4 * j] = h2f_lo(u[0]);
+            o[4 * j + 1] = h2f_hi(u[0]);
+            o[4 * j + 2] = h2f_lo(u[1]);
+            o[4 * j + 3] = h2f_hi(u[1]);
         }
     } else {
 #pragma unroll
-        for (int c = 0; c < C; ++c) o[c] = __uint_as_float(uint32_t(s[e + c]) << 16);
+        for (int c = 0; c < C; ++c) o[c] = h2f_lo(uint32_t(s[e + c]));
     }
 }
 
 // stage a (LH x LW x LD) box of a channels-last bf16 grid (n = H x W x D, rows clamped into it)
 // whose first voxel is (h0, w0, d0) into LDS [LH][LW][LD][C]: 8-byte units when C % 4 == 0
 template <int C, int LH, int LW, int LD>
-__device__ __forceinline__ void stage_box(const bf16_t *__restrict__ src, int b, int H, int W, int D, int h0, int w0,
-                                          int d0, bf16_t *s) {
+__device__ __forceinline__ void stage_box(const h16_t *__restrict__ src, int b, int H, int W, int D, int h0, int w0,
+                                          int d0, h16_t *s) {
     constexpr int U = C % 4 == 0 ? 4 : 1, NU = LH * LW * LD * C / U;
     for (int u = threadIdx.x; u < NU; u += 256) {
         const int e = u * U, v = e / C, c = e - v * C;
@@ -344,10 +344,10 @@ __device__ __forceinline__ void stage_box(const bf16_t *__restrict__ src, int b,
 }
 
 template <int C, int SH, int SW, int SD>
-__global__ __launch_bounds__(256) void k_up2t_fwd(UT a, const bf16_t *__restrict__ x, bf16_t *__restrict__ y) {
+__global__ __launch_bounds__(256) void k_up2t_fwd(UT a, const h16_t *__restrict__ x, h16_t *__restrict__ y) {
     constexpr int HH = SH + 2, HW = SW + 2, HD = SD + 2;
     constexpr int CG = C % 4 == 0 ? 4 : 1;  // channels per LDS read
-    __shared__ __attribute__((aligned(16))) bf16_t hs[HH * HW * HD * C];
+    __shared__ __attribute__((aligned(16))) h16_t hs[HH * HW * HD * C];
     int t = blockIdx.x;
     const int td = t % a.ntd;
     t /= a.ntd;
@@ -391,17 +391,17 @@ __global__ __launch_bounds__(256) void k_up2t_fwd(UT a, const bf16_t *__restrict
                                      lh * ((1.f - lw) * ((1.f - ld) * v[4] + ld * v[5]) + lw * ((1.f - ld) * v[6] + ld * v[7]));
                 }
             }
-            bf16_t *dst = y + (vo + tt) * C;
+            h16_t *dst = y + (vo + tt) * C;
             if constexpr (C % 8 == 0) {
 #pragma unroll
                 for (int j = 0; j < C / 8; ++j) {
                     float f[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) f[k] = o[8 * j + k];
-                    stvec<bf16_t, 8>(dst + 8 * j, f);
+                    stvec<h16_t, 8>(dst + 8 * j, f);
                 }
             } else if constexpr (C == 4) {
-                stvec<bf16_t, 4>(dst, o);
+                stvec<h16_t, 4>(dst, o);
             } else {
 #pragma unroll
                 for (int c = 0; c < C; ++c) st(dst + c, o[c]);
@@ -423,7 +423,7 @@ bool up2_tiled_fwd(int batch, int h, int w, int dd, const void *x, int pro_kind,
     a.nth = h / SH; a.ntw = w / SW; a.ntd = dd / SD;
     a.pro_kind = pro_kind; a.pro_a = pa; a.pro_b = pb;
     const unsigned nb = unsigned(batch * a.nth * a.ntw * a.ntd);
-    k_up2t_fwd<C, SH, SW, SD><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, (bf16_t *)y);
+    k_up2t_fwd<C, SH, SW, SD><<<nb, 256, 0, s>>>(a, (const h16_t *)x, (h16_t *)y);
     return true;
 }
 
@@ -441,7 +441,7 @@ UArgs make_args(int B, int C, int H, int W, int D, int cv, bool fwd) {
 
 int pick_cv(int dtype, int C, const void *p0, const void *p1, const void *p2, const void *p3) {
     auto al = [](const void *p, int b) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % b) == 0; };
-    if (dtype != VQ3D_BF16) return 1;
+    if (dtype != VQ3D_HALF) return 1;
     if (C % 8 == 0 && al(p0, 16) && al(p1, 16) && al(p2, 16) && al(p3, 16)) return 8;
     if (C % 4 == 0 && al(p0, 8) && al(p1, 8) && al(p2, 8) && al(p3, 8)) return 4;
     return 1;
@@ -452,7 +452,7 @@ int pick_cv(int dtype, int C, const void *p0, const void *p1, const void *p2, co
 int launch_up2_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, int32_t w, int32_t dd, const void *x,
                    int32_t pro_kind, const float *pro_a, const float *pro_b, void *y, hipStream_t s) {
     if (int64_t(batch) * 8 * h * w * dd * channels >= (int64_t(1) << 31)) return fail("upsample2x: tensor too large");
-    if (dtype == VQ3D_BF16 && channels == 9 && up2_tiled_fwd<9, 4, 8, 16>(batch, h, w, dd, x, pro_kind, pro_a, pro_b, y, s))
+    if (dtype == VQ3D_HALF && channels == 9 && up2_tiled_fwd<9, 4, 8, 16>(batch, h, w, dd, x, pro_kind, pro_a, pro_b, y, s))
         return check_launch("upsample2x_fwd(tiled)");
     const int cv = pick_cv(dtype, channels, x, y, nullptr, nullptr);
     const UArgs a = make_args(batch, channels, h, w, dd, cv, true);
@@ -461,11 +461,11 @@ int launch_up2_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, in
     if (dtype == VQ3D_F32)
         k_up2_fwd<float, 1><<<nb, 256, 0, s>>>(a, (const float *)x, pro_kind, pro_a, pro_b, (float *)y);
     else if (cv == 8)
-        k_up2_fwd<bf16_t, 8><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, pro_kind, pro_a, pro_b, (bf16_t *)y);
+        k_up2_fwd<h16_t, 8><<<nb, 256, 0, s>>>(a, (const h16_t *)x, pro_kind, pro_a, pro_b, (h16_t *)y);
     else if (cv == 4)
-        k_up2_fwd<bf16_t, 4><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, pro_kind, pro_a, pro_b, (bf16_t *)y);
+        k_up2_fwd<h16_t, 4><<<nb, 256, 0, s>>>(a, (const h16_t *)x, pro_kind, pro_a, pro_b, (h16_t *)y);
     else
-        k_up2_fwd<bf16_t, 1><<<nb, 256, 0, s>>>(a, (const bf16_t *)x, pro_kind, pro_a, pro_b, (bf16_t *)y);
+        k_up2_fwd<h16_t, 1><<<nb, 256, 0, s>>>(a, (const h16_t *)x, pro_kind, pro_a, pro_b, (h16_t *)y);
     return check_launch("upsample2x_fwd");
 }
 
@@ -475,13 +475,13 @@ int launch_up2_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, in
     if (int64_t(batch) * 8 * h * w * dd * channels >= (int64_t(1) << 31)) return fail("upsample2x: tensor too large");
     const int cv = pick_cv(dtype, channels, gy, gx, aux, add);
     auto al16 = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    if (dtype == VQ3D_BF16 && channels == 4 && dd % 4 == 0 && al16(gy) && al16(gx) && al16(aux) && al16(add)) {
+    if (dtype == VQ3D_HALF && channels == 4 && dd % 4 == 0 && al16(gy) && al16(gx) && al16(aux) && al16(add)) {
         UArgs a = make_args(batch, channels, h, w, dd, 4, false);
         a.f1 = FastDiv(uint32_t(dd / 4));
         const int64_t n = int64_t(batch) * h * w * (dd / 4);
         const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)));
-        k_up2_bwd_run4<<<nb, 256, 0, s>>>(a, (const bf16_t *)gy, dmode, dparam, (const bf16_t *)aux,
-                                          (const bf16_t *)add, (bf16_t *)gx, dpre, dpost);
+        k_up2_bwd_run4<<<nb, 256, 0, s>>>(a, (const h16_t *)gy, dmode, dparam, (const h16_t *)aux,
+                                          (const h16_t *)add, (h16_t *)gx, dpre, dpost);
         return check_launch("upsample2x_bwd(run4)");
     }
     const UArgs a = make_args(batch, channels, h, w, dd, cv, false);
@@ -492,9 +492,9 @@ int launch_up2_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, in
     k_up2_bwd<T, CV><<<nb, 256, 0, s>>>(a, (const T *)gy, dmode, dparam, (const T *)aux, (const T *)add, (T *)gx, \
                                         dpre, dpost)
     if (dtype == VQ3D_F32) UB(float, 1);
-    else if (cv == 8) UB(bf16_t, 8);
-    else if (cv == 4) UB(bf16_t, 4);
-    else UB(bf16_t, 1);
+    else if (cv == 8) UB(h16_t, 8);
+    else if (cv == 4) UB(h16_t, 4);
+    else UB(h16_t, 1);
 #undef UB
     return check_launch("upsample2x_bwd");
 }

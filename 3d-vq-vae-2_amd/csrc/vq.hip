@@ -452,20 +452,20 @@ int vq3d_vq_nearest(int32_t z_dtype, const void *z, int64_t n, int32_t d, const 
         if (zf) {
             part(float{});
             if (qf) k_vq_nearest_finish<float, float><<<nb, kVqThreads, 0, s>>>((const float *)z, n, d, embed, p.nchunk, pb, pi, idx, (float *)zst, sqpart);
-            else k_vq_nearest_finish<float, bf16_t><<<nb, kVqThreads, 0, s>>>((const float *)z, n, d, embed, p.nchunk, pb, pi, idx, (bf16_t *)zst, sqpart);
+            else k_vq_nearest_finish<float, h16_t><<<nb, kVqThreads, 0, s>>>((const float *)z, n, d, embed, p.nchunk, pb, pi, idx, (h16_t *)zst, sqpart);
         } else {
-            part(bf16_t{});
-            if (qf) k_vq_nearest_finish<bf16_t, float><<<nb, kVqThreads, 0, s>>>((const bf16_t *)z, n, d, embed, p.nchunk, pb, pi, idx, (float *)zst, sqpart);
-            else k_vq_nearest_finish<bf16_t, bf16_t><<<nb, kVqThreads, 0, s>>>((const bf16_t *)z, n, d, embed, p.nchunk, pb, pi, idx, (bf16_t *)zst, sqpart);
+            part(h16_t{});
+            if (qf) k_vq_nearest_finish<h16_t, float><<<nb, kVqThreads, 0, s>>>((const h16_t *)z, n, d, embed, p.nchunk, pb, pi, idx, (float *)zst, sqpart);
+            else k_vq_nearest_finish<h16_t, h16_t><<<nb, kVqThreads, 0, s>>>((const h16_t *)z, n, d, embed, p.nchunk, pb, pi, idx, (h16_t *)zst, sqpart);
         }
         if (int r = check_launch("vq_nearest(split)")) return r;
         k_sum_partials<<<1, 256, 0, s>>>(sqpart, int(p.nb_near), sqerr_out, 0.f, nullptr);
         return check_launch("vq_nearest(sum)");
     }
     if (zf && qf) launch_nearest<float, float>(z, n, d, embed, k, idx, zst, sqpart, s);
-    else if (zf) launch_nearest<float, bf16_t>(z, n, d, embed, k, idx, zst, sqpart, s);
-    else if (qf) launch_nearest<bf16_t, float>(z, n, d, embed, k, idx, zst, sqpart, s);
-    else launch_nearest<bf16_t, bf16_t>(z, n, d, embed, k, idx, zst, sqpart, s);
+    else if (zf) launch_nearest<float, h16_t>(z, n, d, embed, k, idx, zst, sqpart, s);
+    else if (qf) launch_nearest<h16_t, float>(z, n, d, embed, k, idx, zst, sqpart, s);
+    else launch_nearest<h16_t, h16_t>(z, n, d, embed, k, idx, zst, sqpart, s);
     if (int r = check_launch("vq_nearest")) return r;
     k_sum_partials<<<1, 256, 0, s>>>(sqpart, int(p.nb_near), sqerr_out, 0.f, nullptr);
     return check_launch("vq_nearest(sum)");
@@ -489,14 +489,14 @@ int vq3d_vq_bwd(int32_t z_dtype, const void *z, int64_t n, int32_t d, const floa
         k_vq_bwd<float, float><<<nb, 256, 0, s>>>((const float *)z, n, d, embed, idx, (const float *)g_zst, g_loss,
                                                   coef, (float *)gz);
     else if (zf)
-        k_vq_bwd<float, bf16_t><<<nb, 256, 0, s>>>((const float *)z, n, d, embed, idx, (const bf16_t *)g_zst,
+        k_vq_bwd<float, h16_t><<<nb, 256, 0, s>>>((const float *)z, n, d, embed, idx, (const h16_t *)g_zst,
                                                    g_loss, coef, (float *)gz);
     else if (gf)
-        k_vq_bwd<bf16_t, float><<<nb, 256, 0, s>>>((const bf16_t *)z, n, d, embed, idx, (const float *)g_zst,
-                                                   g_loss, coef, (bf16_t *)gz);
+        k_vq_bwd<h16_t, float><<<nb, 256, 0, s>>>((const h16_t *)z, n, d, embed, idx, (const float *)g_zst,
+                                                   g_loss, coef, (h16_t *)gz);
     else
-        k_vq_bwd<bf16_t, bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)z, n, d, embed, idx, (const bf16_t *)g_zst,
-                                                    g_loss, coef, (bf16_t *)gz);
+        k_vq_bwd<h16_t, h16_t><<<nb, 256, 0, s>>>((const h16_t *)z, n, d, embed, idx, (const h16_t *)g_zst,
+                                                    g_loss, coef, (h16_t *)gz);
     return check_launch("vq_bwd");
 }
 
@@ -512,7 +512,7 @@ int vq3d_vq_ema_stats(int32_t z_dtype, const void *z, int64_t n, int32_t d, cons
     if (z_dtype == VQ3D_F32)
         k_vq_ema_stats<float><<<grid, 256, 0, s>>>((const float *)z, n, d, idx, k, part);
     else
-        k_vq_ema_stats<bf16_t><<<grid, 256, 0, s>>>((const bf16_t *)z, n, d, idx, k, part);
+        k_vq_ema_stats<h16_t><<<grid, 256, 0, s>>>((const h16_t *)z, n, d, idx, k, part);
     if (int r = check_launch("vq_ema_stats")) return r;
     int lanes = 1;
     while (lanes < 64 && lanes * 16 < p.nb_stats) lanes *= 2;
@@ -558,7 +558,7 @@ int vq3d_vq_moments(int32_t z_dtype, const void *z, int64_t n, int32_t d, float 
         if (z_dtype == VQ3D_F32)
             k_vq_moments_part<float><<<nb, 256, 0, s>>>((const float *)z, n, d, rpb, mu, part);
         else
-            k_vq_moments_part<bf16_t><<<nb, 256, 0, s>>>((const bf16_t *)z, n, d, rpb, mu, part);
+            k_vq_moments_part<h16_t><<<nb, 256, 0, s>>>((const h16_t *)z, n, d, rpb, mu, part);
         k_vq_moments_fin<<<fb, 64, 0, s>>>(part, nb, d, n, pass ? std : mean, pass);
     }
     return check_launch("vq_moments");

@@ -31,7 +31,6 @@ namespace vq3d {
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -80,25 +79,25 @@ struct WArgs {
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
-__device__ __forceinline__ bf16x8 tr8(const bf16_t *p0, const bf16_t *p1) {
+__device__ __forceinline__ hx8 tr8(const h16_t *p0, const h16_t *p1) {
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return __builtin_bit_cast(hx8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 // the prologue over 2 packed bf16 (zero padding stays zero: only loaded words come here)
 __device__ __forceinline__ uint32_t pro2(uint32_t w, const Prologue &pro) {
-    const float lo = pro.apply(__uint_as_float(w << 16)), hi = pro.apply(__uint_as_float(w & 0xffff0000u));
-    return uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+    const float lo = pro.apply(h2f_lo(w)), hi = pro.apply(h2f_hi(w));
+    return uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16);
 }
 
 template <int CI, int CO, int KS, int ST, int PAD, int DO, int TH, int TW>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_wgrad_ds(
-    WArgs a, const bf16_t *__restrict__ x, const bf16_t *__restrict__ g, float *__restrict__ part, int want_gsum) {
+    WArgs a, const h16_t *__restrict__ x, const h16_t *__restrict__ g, float *__restrict__ part, int want_gsum) {
     using Gm = Geo<CI, CO, KS, ST, PAD, DO, TH, TW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    bf16_t *gl = reinterpret_cast<bf16_t *>(smem);  // [NL][GLP]
-    bf16_t *xl = gl + Gm::NL * Gm::GLP;              // [XL][XP]
+    h16_t *gl = reinterpret_cast<h16_t *>(smem);  // [NL][GLP]
+    h16_t *xl = gl + Gm::NL * Gm::GLP;              // [XL][XP]
     __shared__ float red[8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int grp = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
@@ -170,7 +169,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 if (want_gsum) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        gsum += __uint_as_float(gv[u][j] << 16) + __uint_as_float(gv[u][j] & 0xffff0000u);
+                        gsum += h2f_lo(gv[u][j]) + h2f_hi(gv[u][j]);
                 }
             }
         }
@@ -214,19 +213,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_
             // K rows 8 grp + q (and + 4) of this step: group G -> (line, m); 8 rows stay in one line
             const int G = ks * 32 + 8 * grp + q, line = G / Gm::MPL, m = G % Gm::MPL;
             const int lh = line / TW, lw = line % TW;
-            const bf16_t *ga = gl + line * Gm::GLP + m * 16 + 4 * p4;
-            const bf16x8 af = tr8(ga, ga + 64);
-            const bf16_t *xb0 = xl + Gm::XOFF + (ST * Gm::S * m - PAD) * CI + 4 * p4;
+            const h16_t *ga = gl + line * Gm::GLP + m * 16 + 4 * p4;
+            const hx8 af = tr8(ga, ga + 64);
+            const h16_t *xb0 = xl + Gm::XOFF + (ST * Gm::S * m - PAD) * CI + 4 * p4;
 #pragma unroll
             for (int j = 0; j < Gm::TPW; ++j) {
                 const int kk = Gm::BYK ? j : wave + 4 * j;
                 if (kk < Gm::NTAP) {
                     const int kh = kk / KS, kw = kk % KS;
-                    const bf16_t *xb = xb0 + ((lh * ST + kh) * Gm::XW + lw * ST + kw) * Gm::XP;
+                    const h16_t *xb = xb0 + ((lh * ST + kh) * Gm::XW + lw * ST + kw) * Gm::XP;
 #pragma unroll
                     for (int t = 0; t < Gm::NTN; ++t) {
-                        const bf16x8 bf = tr8(xb + 16 * t, xb + 16 * t + 4 * ST * Gm::S * CI);
-                        acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[j][t], 0, 0, 0);
+                        const hx8 bf = tr8(xb + 16 * t, xb + 16 * t + 4 * ST * Gm::S * CI);
+                        acc[j][t] = VQ3D_MFMA_16X16X32(af, bf, acc[j][t], 0, 0, 0);
                     }
                 }
             }
@@ -287,11 +286,11 @@ struct Inst {
     const void *kern;
     size_t lds;
     int ne, ntiles_h, ntiles_w;  // tile extents TH, TW
-    void (*launch)(dim3, size_t, hipStream_t, const WArgs &, const bf16_t *, const bf16_t *, float *, int);
+    void (*launch)(dim3, size_t, hipStream_t, const WArgs &, const h16_t *, const h16_t *, float *, int);
 };
 
 template <int CI, int CO, int KS, int ST, int PAD, int DO, int TH, int TW>
-void launch_inst(dim3 grid, size_t lds, hipStream_t s, const WArgs &a, const bf16_t *x, const bf16_t *g, float *part,
+void launch_inst(dim3 grid, size_t lds, hipStream_t s, const WArgs &a, const h16_t *x, const h16_t *g, float *part,
                  int want_gsum) {
     k_wgrad_ds<CI, CO, KS, ST, PAD, DO, TH, TW><<<grid, NT, lds, s>>>(a, x, g, part, want_gsum);
 }
@@ -312,7 +311,7 @@ const Inst *find_inst(const vq3d_conv_desc *d) {
         make_inst<4, 8, 2, 2, 0, 64, 2, 4>(0),    // down block skip conv 4 -> 8
         make_inst<8, 16, 2, 2, 0, 32, 2, 4>(0),   // 8 -> 16
     };
-    if (d->dtype != VQ3D_BF16 || d->cin2 != 0) return nullptr;
+    if (d->dtype != VQ3D_HALF || d->cin2 != 0) return nullptr;
     const int circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
     for (const Inst &in : table) {
         if (in.ci != d->cin || in.co != d->cout || in.ks != d->kernel || in.st != d->stride || in.pad != d->pad ||
@@ -382,7 +381,7 @@ int wgrad_ds(const vq3d_conv_desc *d, const void *x, const void *g, const float 
     a.pro_a = pro_a;
     a.pro_b = pro_b;
     const int nwg = nwg_of(d, *in);
-    in->launch(dim3(unsigned(nwg)), in->lds, s, a, static_cast<const bf16_t *>(x), static_cast<const bf16_t *>(g),
+    in->launch(dim3(unsigned(nwg)), in->lds, s, a, static_cast<const h16_t *>(x), static_cast<const h16_t *>(g),
                static_cast<float *>(ws), dbias ? 1 : 0);
     const int ne1 = in->ne + 1;
     k_wgrad_ds_reduce<<<unsigned((ne1 + NT / 32 - 1) / (NT / 32)), NT, 0, s>>>(static_cast<const float *>(ws), nwg,

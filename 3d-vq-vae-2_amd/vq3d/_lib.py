@@ -11,7 +11,7 @@ import torch
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("VQ3D_LIB", os.path.join(_PKG_ROOT, "lib", "libvq3d.so"))
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 PAD_ZEROS, PAD_CIRCULAR = 0, 1
 PRO_NONE, PRO_ADD, PRO_ELU_ADD = 0, 1, 2
 PASS_FWD, PASS_BWD_DATA, PASS_BWD_WEIGHT = 0, 1, 2
@@ -80,12 +80,12 @@ _SIGS = {
     "vq3d_preact_stack_bwd_ws": (c_int, [c_int] * 8 + [P] * 6 + [c_size, P]),
     "vq3d_preact_wide_supported": (c_int, [c_int] * 6),
     "vq3d_preact_wide_image_bytes": (c_size, [c_int] * 2),
-    "vq3d_preact_wide_pack": (c_int, [c_int] * 3 + [P] * 3),
-    "vq3d_preact_wide_fwd": (c_int, [c_int] * 6 + [P] * 7),
+    "vq3d_preact_wide_pack": (c_int, [c_int] * 4 + [P] * 3),
+    "vq3d_preact_wide_fwd": (c_int, [c_int] * 7 + [P] * 7),
     "vq3d_preact_wide_workspace_bytes": (c_size, [c_int] * 4),
-    "vq3d_preact_wide_bwd_data": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P, P]),
-    "vq3d_preact_wide_bwd_weight": (c_int, [c_int] * 6 + [P] * 7 + [c_size, P]),
-    "vq3d_preact_wide_bwd_weight_stages": (c_int, [c_int] * 7 + [P] * 7 + [c_size, P]),
+    "vq3d_preact_wide_bwd_data": (c_int, [c_int] * 7 + [P] * 7 + [c_size, P, P]),
+    "vq3d_preact_wide_bwd_weight": (c_int, [c_int] * 7 + [P] * 7 + [c_size, P]),
+    "vq3d_preact_wide_bwd_weight_stages": (c_int, [c_int] * 8 + [P] * 7 + [c_size, P]),
     "vq3d_preact_wide_reduce_run": (c_int, [c_int] * 5 + [P, c_size, P, P, P]),
     "vq3d_preact_small_supported": (c_int, [c_int] * 7),
     "vq3d_preact_small_workspace_bytes": (c_size, [c_int] * 6),
@@ -104,9 +104,9 @@ _SIGS = {
     "vq3d_vq_ema_update": (c_int, [P, P, P, P, P, c_int, c_int, c_float, c_float, P]),
     "vq3d_vq_moments": (c_int, [c_int, P, c_i64, c_int, P, P, P, P]),
     "vq3d_vq_init_apply": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, c_float, P]),
-    "vq3d_parse_input_fwd": (c_int, [c_i64, c_int, P, P, P, P, P]),
+    "vq3d_parse_input_fwd": (c_int, [c_int, c_i64, c_int, P, P, P, P, P]),
     "vq3d_parse_input_workspace_bytes": (c_size, [c_i64, c_int]),
-    "vq3d_parse_input_bwd": (c_int, [c_i64, c_int, P, P, P, P, P, c_size, P]),
+    "vq3d_parse_input_bwd": (c_int, [c_int, c_i64, c_int, P, P, P, P, P, c_size, P]),
     "vq3d_recon_loss_workspace_size": (c_size, [c_int] * 4),
     "vq3d_recon_loss_fwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "vq3d_recon_loss_bwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
@@ -200,4 +200,6 @@ def dtype_code(t_or_dtype):
         return F32
     if dt == torch.bfloat16:
         return BF16
+    if dt == torch.float16:
+        return F16
     raise Vq3dError(f"unsupported activation dtype {dt}")

@@ -273,13 +273,13 @@ class PreActWideFn(torch.autograd.Function):
         b, c, h, w, d = x.shape
         nb = plan.blocks[0].branch_conv1.weight.shape[0]
         ptab, _ = plan.tables(x.device)
-        img, per = ops.preact_wide_pack(ptab, len(plan.blocks), c, nb, x.device)
+        img, per = ops.preact_wide_pack(ptab, len(plan.blocks), c, nb, x.device, dtype=x.dtype)
         base = img.data_ptr()
         xs = ops.cast(x, torch.float32)
         save = any(ctx.needs_input_grad)
         saved = []
         for i, blk in enumerate(plan.blocks):
-            out, t2, t3 = ops.preact_wide_fwd(xs, base + i * per, blk, save=save)
+            out, t2, t3 = ops.preact_wide_fwd(xs, base + i * per, blk, save=save, dtype=x.dtype)
             if save:
                 saved += [xs, t2, t3]
             xs = out
@@ -464,16 +464,17 @@ def conv(x, spec, x2=None, residual=None):
 # ============================================================================================ parse_input
 class ParseInputFn(torch.autograd.Function):
     """Encoder2.parse_input (layers.py:535): Conv3d(1 -> C, k = 1, bias) reading the fp32 input
-    volume and writing the bf16 activation (vq3d_parse_input_*): the volume is never rounded to
-    bf16 (the reference's autocast rounds it to fp16).  Weight / bias gradients only."""
+    volume and writing the 16-bit activation (half: bf16 or fp16; vq3d_parse_input_*): the volume is
+    never rounded to bf16 (the reference's autocast rounds it to fp16).  Weight / bias gradients
+    only."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, half):
         bsz, _, h, wd, d = x.shape
         c = w.shape[0]
         nv = bsz * h * wd * d
-        y = ops.new_act(bsz, c, h, wd, d, torch.bfloat16, x.device)
-        L.call("vq3d_parse_input_fwd", nv, c, L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.stream())
+        y = ops.new_act(bsz, c, h, wd, d, half, x.device)
+        L.call("vq3d_parse_input_fwd", L.dtype_code(half), nv, c, L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(y), L.stream())
         ctx.save_for_backward(x)
         ctx.params = (w, b)
         return y
@@ -487,15 +488,15 @@ class ParseInputFn(torch.autograd.Function):
         nv = x.numel()
         nws = int(L.query("vq3d_parse_input_workspace_bytes", nv, c))
         ws = ops.workspace(nws, x.device)
-        L.call("vq3d_parse_input_bwd", nv, c, L.ptr(x), L.ptr(g), L.ptr(grad_buf(w)), L.ptr(grad_buf(b)), L.ptr(ws),
+        L.call("vq3d_parse_input_bwd", L.dtype_code(g), nv, c, L.ptr(x), L.ptr(g), L.ptr(grad_buf(w)), L.ptr(grad_buf(b)), L.ptr(ws),
                nws, L.stream())
         grads_ready((w, b))
-        return None, None, None
+        return None, None, None, None
 
 
 def parse_input_fused(x, conv, compute_dtype):
     """True when the fp32 volume can go through ParseInputFn (1 input channel, bf16 activations)."""
-    return (compute_dtype == torch.bfloat16 and x.dtype == torch.float32 and x.is_cuda and x.dim() == 5
+    return (compute_dtype in (torch.bfloat16, torch.float16) and x.dtype == torch.float32 and x.is_cuda and x.dim() == 5
             and x.shape[1] == 1 and conv.in_channels == 1 and conv.out_channels in (2, 4, 8)
             and conv.bias is not None and x.numel() % 4 == 0 and x.is_contiguous())
 

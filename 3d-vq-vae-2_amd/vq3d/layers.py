@@ -376,8 +376,8 @@ class Encoder2(nn.Module):
 
     def forward(self, data):
         if Fn.parse_input_fused(data, self.parse_input, self.compute_dtype):
-            # the fp32 volume straight into the bf16 activation (never rounded to bf16 itself)
-            down = Fn.ParseInputFn.apply(data, self.parse_input.weight, self.parse_input.bias)
+            # the fp32 volume straight into the 16-bit activation (never rounded to bf16 itself)
+            down = Fn.ParseInputFn.apply(data, self.parse_input.weight, self.parse_input.bias, self.compute_dtype)
         else:
             if data.dtype != self.compute_dtype:
                 data = ops.cast(data, self.compute_dtype)

@@ -21,7 +21,7 @@ from .layers import Decoder, Encoder2, EvonormResBlock, FixupResBlock, PreActFix
 from .optim import FusedAdam
 from .utils import booltype
 
-DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
+DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
 
 
 class VQVAE(nn.Module):

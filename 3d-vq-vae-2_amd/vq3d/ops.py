@@ -581,8 +581,8 @@ def preact_small_fwd(x, blk, save=True, out_dtype=None):
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     nb = w1.shape[0]
     out = torch.empty_like(x, memory_format=CL, dtype=out_dtype or x.dtype)
-    t2 = new_act(b, nb, h, w, d, torch.bfloat16, x.device) if save else None
-    t3 = new_act(b, nb, h, w, d, torch.bfloat16, x.device) if save else None
+    t2 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
+    t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
     prm = _preact_params(blk)
     _timed(lambda: _small_kind("fwd", b, c, nb, h, w, d), lambda: L.call(
         "vq3d_preact_small_fwd_io", L.dtype_code(x), L.dtype_code(out), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1),
@@ -652,28 +652,29 @@ def set_wide_blocks(enabled):
 
 def preact_wide_supported(x, branch):
     b, c, h, w, d = x.shape
-    return (_wide[0] and x.dtype == torch.bfloat16
+    return (_wide[0] and x.dtype in (torch.bfloat16, torch.float16)
             and bool(L.query("vq3d_preact_wide_supported", b, c, branch, h, w, d)))
 
 
-def preact_wide_pack(ptab, nblocks, c, nb, device):
-    """Packed bf16 fragment images of a run's weights (one per block, consecutive)."""
+def preact_wide_pack(ptab, nblocks, c, nb, device, dtype=torch.bfloat16):
+    """Packed 16-bit (dtype) fragment images of a run's weights (one per block, consecutive)."""
     per = int(L.query("vq3d_preact_wide_image_bytes", c, nb))
     img = torch.empty(nblocks * per, dtype=torch.uint8, device=device)
-    L.call("vq3d_preact_wide_pack", nblocks, c, nb, L.ptr(ptab), L.ptr(img), L.stream())
+    L.call("vq3d_preact_wide_pack", L.dtype_code(dtype), nblocks, c, nb, L.ptr(ptab), L.ptr(img), L.stream())
     return img, per
 
 
-def preact_wide_fwd(x32, img_ptr, blk, save=True):
-    """One block on the fp32 residual stream: returns out (fp32), t2, t3 (bf16), channels-last;
-    save=False (no backward follows): t2 / t3 are not written (None)."""
+def preact_wide_fwd(x32, img_ptr, blk, save=True, dtype=torch.bfloat16):
+    """One block on the fp32 residual stream: returns out (fp32), t2, t3 (16-bit dtype, the
+    fragment image's format), channels-last; save=False (no backward follows): t2 / t3 are not
+    written (None)."""
     b, c, h, w, d = x32.shape
     nb = blk.branch_conv1.weight.shape[0]
     out = torch.empty_like(x32, memory_format=CL)
-    t2 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device) if save else None
-    t3 = new_act(b, nb, h, w, d, torch.bfloat16, x32.device) if save else None
+    t2 = new_act(b, nb, h, w, d, dtype, x32.device) if save else None
+    t3 = new_act(b, nb, h, w, d, dtype, x32.device) if save else None
     prm = _preact_params(blk)
-    L.call("vq3d_preact_wide_fwd", b, c, nb, h, w, d, L.ptr(x32), ctypes.c_void_p(img_ptr), ctypes.byref(prm),
+    L.call("vq3d_preact_wide_fwd", L.dtype_code(dtype), b, c, nb, h, w, d, L.ptr(x32), ctypes.c_void_p(img_ptr), ctypes.byref(prm),
            L.ptr(out), _p(t2), _p(t3), L.stream())
     return out, t2, t3
 
@@ -693,10 +694,11 @@ def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads, ws_ptr=None, reduce=T
         ws_ptr = ws.data_ptr()
     wsp = ctypes.c_void_p(ws_ptr)
     prm = _preact_params(blk)
-    L.call("vq3d_preact_wide_bwd_data", b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
+    dc = L.dtype_code(t2)
+    L.call("vq3d_preact_wide_bwd_data", dc, b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
            ctypes.c_void_p(img_ptr), ctypes.byref(prm), wsp, ctypes.c_size_t(nws), L.ptr(gx), L.stream())
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
-    args = (1 | (2 if reduce else 0), b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
+    args = (1 | (2 if reduce else 0), dc, b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
             ctypes.byref(prm), ctypes.byref(gr), wsp, ctypes.c_size_t(nws))
     if _concurrent:
         _on_side(x32.device, lambda: L.call("vq3d_preact_wide_bwd_weight_stages", *args, L.stream()),

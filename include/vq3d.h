@@ -11,8 +11,12 @@
  * the ATen work behind one reference call site, cited per function.
  *
  * Activation layout: channels-last NDHWC, i.e. the reference tensor (B, C, H, W, D)
- * stored as [B][H][W][D][C].  Storage dtype per call (VQ3D_F32 or VQ3D_BF16);
+ * stored as [B][H][W][D][C].  Storage dtype per call (VQ3D_F32, VQ3D_BF16 or VQ3D_F16);
  * arithmetic is fp32.  Weights are fp32 in the reference layout (Cout, Cin, k, k, k).
+ * Wherever these comments say "bf16" for an activation or a matrix-core operand, a VQ3D_F16 call
+ * uses IEEE fp16 instead (the reference's AMP precision, vqvae/train.py:32): the kernels exist in
+ * both 16-bit formats and every entry point routes a call by its dtype arguments; one call's
+ * 16-bit tensors share one format (mixing VQ3D_BF16 and VQ3D_F16 fails).
  */
 #ifndef VQ3D_H
 #define VQ3D_H
@@ -26,7 +30,7 @@ extern "C" {
 
 typedef struct ihipStream_t *vq3d_stream_t; /* == hipStream_t */
 
-enum { VQ3D_F32 = 0, VQ3D_BF16 = 1 };
+enum { VQ3D_F32 = 0, VQ3D_BF16 = 1, VQ3D_F16 = 2 };
 enum { VQ3D_PAD_ZEROS = 0, VQ3D_PAD_CIRCULAR = 1 };
 /* prologue applied to every input element as it is loaded (reference glue, layers.py:178-185) */
 enum { VQ3D_PRO_NONE = 0, VQ3D_PRO_ADD = 1 /* x + a */, VQ3D_PRO_ELU_ADD = 2 /* elu(x + a) + b */ };
@@ -34,7 +38,7 @@ enum { VQ3D_PRO_NONE = 0, VQ3D_PRO_ADD = 1 /* x + a */, VQ3D_PRO_ELU_ADD = 2 /* 
 /* One 3-D convolution as nn.Conv3d computes it (padding_mode 'zeros' or 'circular';
  * circular == F.pad(x, p, 'circular') then a valid conv). */
 typedef struct vq3d_conv_desc {
-    int32_t dtype;      /* activation storage: VQ3D_F32 | VQ3D_BF16 */
+    int32_t dtype;      /* activation storage: VQ3D_F32 | VQ3D_BF16 | VQ3D_F16 */
     int32_t batch;
     int32_t cin;        /* channels of input 1 */
     int32_t cin2;       /* channels of input 2, concatenated after input 1 (torch.cat dim=1); 0 = none */
@@ -256,17 +260,20 @@ int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int3
  * accumulated (+=) deterministically); bwd_weight may run on another stream after bwd_data. */
 int vq3d_preact_wide_supported(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd);
 size_t vq3d_preact_wide_image_bytes(int32_t channels, int32_t branch);
-int vq3d_preact_wide_pack(int32_t nblocks, int32_t channels, int32_t branch, const float *const *params, void *image,
-                          vq3d_stream_t stream);
-int vq3d_preact_wide_fwd(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+/* dtype (VQ3D_BF16 | VQ3D_F16): the format of the fragment image and of t2 / t3 */
+int vq3d_preact_wide_pack(int32_t dtype, int32_t nblocks, int32_t channels, int32_t branch, const float *const *params,
+                          void *image, vq3d_stream_t stream);
+int vq3d_preact_wide_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
                          const float *x, const void *image, const vq3d_preact_params *p, float *out, void *t2,
                          void *t3, vq3d_stream_t stream);
 size_t vq3d_preact_wide_workspace_bytes(int32_t batch, int32_t h, int32_t w, int32_t dd);
-int vq3d_preact_wide_bwd_data(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+int vq3d_preact_wide_bwd_data(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                              int32_t dd,
                               const float *g, const float *x, const void *t2, const void *t3, const void *image,
                               const vq3d_preact_params *p, void *workspace, size_t workspace_bytes, float *gx,
                               vq3d_stream_t stream);
-int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
+int vq3d_preact_wide_bwd_weight(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
+                                int32_t dd,
                                 const float *g, const float *x, const void *t2, const void *t3,
                                 const vq3d_preact_params *p, const vq3d_preact_grads *gr, const void *workspace,
                                 size_t workspace_bytes, vq3d_stream_t stream);
@@ -274,7 +281,8 @@ int vq3d_preact_wide_bwd_weight(int32_t batch, int32_t channels, int32_t branch,
  * reduce_run = stage 2 of a whole RUN in one launch (block i's workspace at workspaces + i *
  * workspace_stride, stride >= vq3d_preact_wide_workspace_bytes and a multiple of 256; grads /
  * params as for vq3d_preact_mid_reduce_run). */
-int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t batch, int32_t channels, int32_t branch, int32_t h,
+int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,
+                                       int32_t h,
                                        int32_t w, int32_t dd, const float *g, const float *x, const void *t2,
                                        const void *t3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                                        const void *workspace, size_t workspace_bytes, vq3d_stream_t stream);
@@ -365,16 +373,17 @@ int vq3d_vq_init_apply(float *embed, float *embed_avg, float *cluster_size, int6
                        float n_total, vq3d_stream_t stream);
 
 /* --- Encoder2.parse_input (layers.py:535): Conv3d(1 -> channels, k = 1, bias) on the fp32 input
- * volume [voxels] with a bf16 output [voxels][channels] (channels in {2, 4, 8}, voxels % 4 == 0).
+ * volume [voxels] with a 16-bit output [voxels][channels] (dtype VQ3D_BF16 | VQ3D_F16; channels in {2, 4,
+ * 8}, voxels % 4 == 0).
  * The volume stays fp32 (the reference's autocast rounds it to fp16, never to bf16).  The backward
  * accumulates (+=) the weight [channels] and bias [channels] gradients, deterministically (fixed-
  * order partial sums through a workspace of vq3d_parse_input_workspace_bytes); the input has no
  * gradient. --- */
-int vq3d_parse_input_fwd(int64_t voxels, int32_t channels, const float *x, const float *w, const float *b, void *y,
-                         vq3d_stream_t stream);
+int vq3d_parse_input_fwd(int32_t dtype, int64_t voxels, int32_t channels, const float *x, const float *w,
+                         const float *b, void *y, vq3d_stream_t stream);
 size_t vq3d_parse_input_workspace_bytes(int64_t voxels, int32_t channels);
-int vq3d_parse_input_bwd(int64_t voxels, int32_t channels, const float *x, const void *g, float *dw, float *db,
-                         void *workspace, size_t ws_bytes, vq3d_stream_t stream);
+int vq3d_parse_input_bwd(int32_t dtype, int64_t voxels, int32_t channels, const float *x, const void *g, float *dw,
+                         float *db, void *workspace, size_t ws_bytes, vq3d_stream_t stream);
 
 /* --- reconstruction loss (VQVAE.loc_metric with F.smooth_l1_loss, model.py:115-163) ---
  * loc = elu(dec); loc[..., s >= nvs[b]] = 0; optional centre-cylinder gather

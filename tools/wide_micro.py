@@ -49,20 +49,20 @@ def main():
     gr = L.PreactGrads(*[ops._p(names[n].grad) for n, _ in L.PreactGrads._fields_])
 
     def fwd():
-        L.call("vq3d_preact_wide_fwd", 1, 72, 36, h, w, d, L.ptr(x), ctypes.c_void_p(img.data_ptr()),
+        L.call("vq3d_preact_wide_fwd", L.BF16, 1, 72, 36, h, w, d, L.ptr(x), ctypes.c_void_p(img.data_ptr()),
                ctypes.byref(prm), L.ptr(out), L.ptr(t2), L.ptr(t3), L.stream())
 
     def bwd_data():
-        L.call("vq3d_preact_wide_bwd_data", 1, 72, 36, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
+        L.call("vq3d_preact_wide_bwd_data", L.BF16, 1, 72, 36, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
                ctypes.c_void_p(img.data_ptr()), ctypes.byref(prm), L.ptr(ws), ctypes.c_size_t(nws), L.ptr(gx),
                L.stream())
 
     def bwd_weight():
-        L.call("vq3d_preact_wide_bwd_weight", 1, 72, 36, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
+        L.call("vq3d_preact_wide_bwd_weight", L.BF16, 1, 72, 36, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
                ctypes.byref(prm), ctypes.byref(gr), L.ptr(ws), ctypes.c_size_t(nws), L.stream())
 
     def pack():
-        L.call("vq3d_preact_wide_pack", 1, 72, 36, L.ptr(ptab), L.ptr(img), L.stream())
+        L.call("vq3d_preact_wide_pack", L.BF16, 1, 72, 36, L.ptr(ptab), L.ptr(img), L.stream())
     bwd_data()
     res = {n: timed(f, iters) for n, f in (("pack", pack), ("fwd", fwd), ("bwd_data", bwd_data),
                                             ("bwd_weight", bwd_weight))}
