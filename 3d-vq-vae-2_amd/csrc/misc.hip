@@ -400,8 +400,10 @@ __global__ __launch_bounds__(256) void k_adam_amsgrad(float *__restrict__ p, con
                                                      float *__restrict__ m, float *__restrict__ v,
                                                      float *__restrict__ vmax, int64_t n, float beta1, float omb1,
                                                      float beta2, float omb2, float step_size, float bc2_sqrt,
-                                                     float eps, const int64_t *__restrict__ step_dev, float lr) {
+                                                     float eps, const int64_t *__restrict__ step_dev, float lr,
+                                                     const float *__restrict__ skip) {
 #pragma clang fp contract(off)
+    if (skip && *skip != 0.f) return;  // the loss scaler found a non-finite gradient: no step
     if (step_dev) {  // bias corrections of step *step_dev + 1, as the host path computes them (double)
         const double st = double(*step_dev + 1);
         const double bc1 = 1.0 - pow(double(beta1), st);
@@ -423,7 +425,42 @@ __global__ __launch_bounds__(256) void k_adam_amsgrad(float *__restrict__ p, con
     }
 }
 
-__global__ void k_step_inc(int64_t *step) { *step += 1; }
+__global__ void k_step_inc(int64_t *step, const float *skip) {
+    if (!skip || *skip == 0.f) *step += 1;
+}
+
+// ============================================================================ dynamic loss scaling
+// torch.cuda.amp.GradScaler's device work (the reference trains with PL native AMP, precision=16,
+// vqvae/train.py:32): unscale the gradients in place and flag a non-finite one, then update the
+// scale (backoff on a flagged step, growth after `interval` clean steps)
+__global__ void k_zero1(float *p) { *p = 0.f; }
+__global__ __launch_bounds__(256) void k_grad_unscale(float *__restrict__ g, int64_t n, const float *__restrict__ scale,
+                                                      float *__restrict__ found_inf) {
+    const float inv = float(1.0 / double(*scale));  // GradScaler: scale.double().reciprocal().float()
+    bool bad = false;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        const float v = g[i];
+        bad |= !isfinite(v);
+        g[i] = v * inv;
+    }
+    if (bad) *found_inf = 1.f;  // every writer stores the same value
+}
+__global__ void k_scale_update(float *scale, int32_t *tracker, const float *found_inf, float growth, float backoff,
+                               int32_t interval) {
+    if (*found_inf != 0.f) {
+        *scale = *scale * backoff;
+        *tracker = 0;
+    } else {
+        const int32_t t = *tracker + 1;
+        if (t == interval) {
+            const float ns = *scale * growth;
+            if (isfinite(ns)) *scale = ns;
+            *tracker = 0;
+        } else {
+            *tracker = t;
+        }
+    }
+}
 
 // ============================================================================ casts
 template <typename S, typename D>
@@ -677,19 +714,35 @@ int vq3d_adam_amsgrad(float *p, const float *g, float *m, float *v, float *vmax,
     const float bc2_sqrt = float(std::sqrt(bc2));
     k_adam_amsgrad<<<grid_for(n), 256, 0, as_stream(stream)>>>(p, g, m, v, vmax, n, beta1, float(1.0 - beta1), beta2,
                                                                float(1.0 - beta2), step_size, bc2_sqrt, eps,
-                                                               nullptr, lr);
+                                                               nullptr, lr, nullptr);
     return check_launch("adam_amsgrad");
 }
 
 int vq3d_adam_amsgrad_dev(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr,
-                          float beta1, float beta2, float eps, int64_t *step, vq3d_stream_t stream) {
+                          float beta1, float beta2, float eps, int64_t *step, const float *skip,
+                          vq3d_stream_t stream) {
     if (n <= 0 || !step) return fail("adam: bad sizes/step");
     if (!p || !g || !m || !v || !vmax) return fail("adam: null pointer");
     hipStream_t s = as_stream(stream);
     k_adam_amsgrad<<<grid_for(n), 256, 0, s>>>(p, g, m, v, vmax, n, beta1, float(1.0 - beta1), beta2,
-                                              float(1.0 - beta2), 0.f, 1.f, eps, step, lr);
-    k_step_inc<<<1, 1, 0, s>>>(step);
+                                              float(1.0 - beta2), 0.f, 1.f, eps, step, lr, skip);
+    k_step_inc<<<1, 1, 0, s>>>(step, skip);
     return check_launch("adam_amsgrad_dev");
+}
+
+int vq3d_grad_unscale(float *g, int64_t n, const float *scale, float *found_inf, vq3d_stream_t stream) {
+    if (n <= 0 || !g || !scale || !found_inf) return fail("grad_unscale: bad arguments");
+    hipStream_t s = as_stream(stream);
+    k_zero1<<<1, 1, 0, s>>>(found_inf);
+    k_grad_unscale<<<grid_for(n), 256, 0, s>>>(g, n, scale, found_inf);
+    return check_launch("grad_unscale");
+}
+
+int vq3d_loss_scale_update(float *scale, int32_t *growth_tracker, const float *found_inf, float growth,
+                           float backoff, int32_t interval, vq3d_stream_t stream) {
+    if (!scale || !growth_tracker || !found_inf || interval < 1) return fail("loss_scale_update: bad arguments");
+    k_scale_update<<<1, 1, 0, as_stream(stream)>>>(scale, growth_tracker, found_inf, growth, backoff, interval);
+    return check_launch("loss_scale_update");
 }
 
 int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, int64_t n, vq3d_stream_t stream) {

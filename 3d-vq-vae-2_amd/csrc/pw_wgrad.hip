@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_mma(WmArgs a, const h16_t *__r
     const bool raw = pro.kind == VQ3D_PRO_NONE;
     // columns staging never writes: the constant-1 column of x and the zero padding
     for (int v = tid; v < a.VC; v += 256) {
-        for (int c = a.Ct; c < a.XP; ++c) xs[v * a.XP + c] = c == a.Ct ? h16_t(0x3f80) : h16_t(0);
+        for (int c = a.Ct; c < a.XP; ++c) xs[v * a.XP + c] = c == a.Ct ? f2h(1.f) : h16_t(0);
         for (int c = a.N; c < a.GP; ++c) gs[v * a.GP + c] = 0;
     }
 

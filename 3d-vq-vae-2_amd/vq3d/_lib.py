@@ -115,7 +115,9 @@ _SIGS = {
     "vq3d_evonorm_fwd": (c_int, [c_int, P, c_int, c_i64, P, P, P, P, P, P, P]),
     "vq3d_evonorm_bwd": (c_int, [c_int, P, P, c_int, c_i64, P, P, P, P, P, P, P, P, P]),
     "vq3d_adam_amsgrad": (c_int, [P, P, P, P, P, c_i64, c_float, c_float, c_float, c_float, c_i64, P]),
-    "vq3d_adam_amsgrad_dev": (c_int, [P, P, P, P, P, c_i64, c_float, c_float, c_float, c_float, P, P]),
+    "vq3d_adam_amsgrad_dev": (c_int, [P, P, P, P, P, c_i64, c_float, c_float, c_float, c_float, P, P, P]),
+    "vq3d_grad_unscale": (c_int, [P, c_i64, P, P, P]),
+    "vq3d_loss_scale_update": (c_int, [P, P, P, c_float, c_float, c_int, P]),
     "vq3d_cast": (c_int, [c_int, P, c_int, P, c_i64, P]),
     "vq3d_zero": (c_int, [P, c_size, P]),
     "vq3d_copy": (c_int, [P, P, c_size, P]),

@@ -41,8 +41,9 @@ _PATHS = [pathlib.PosixPath, pathlib.PurePosixPath, pathlib.WindowsPath, pathlib
 _SAFE = [Namespace] + _PATHS + [(_stub(q), q) for q in _PL_CALLBACKS]
 
 
-def save_checkpoint(path, model, optimizer=None, epoch: int = 0, global_step: int = 0, callbacks=None):
-    """Write a PL 1.2-layout checkpoint of `model` (and its optimizer's state) to `path`."""
+def save_checkpoint(path, model, optimizer=None, epoch: int = 0, global_step: int = 0, callbacks=None, scaler=None):
+    """Write a PL 1.2-layout checkpoint of `model` (and its optimizer's state) to `path`; with an
+    enabled loss scaler (the fp16 path) also its state as PL's native AMP plugin stores it."""
     ck = {
         "epoch": int(epoch),
         "global_step": int(global_step),
@@ -55,6 +56,8 @@ def save_checkpoint(path, model, optimizer=None, epoch: int = 0, global_step: in
         "hparams_name": "kwargs",
         "hyper_parameters": {"args": Namespace(**vars(model.hparams["args"]))},
     }
+    if scaler is not None and scaler.enabled:
+        ck["native_amp_scaling_state"] = scaler.state_dict()
     torch.save(ck, path)
 
 

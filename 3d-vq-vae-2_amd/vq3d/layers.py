@@ -283,7 +283,7 @@ class BlockStack(nn.Sequential):
 
     @staticmethod
     def _stack_ok(x, blk):
-        if not (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)):
+        if not (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16)):
             return False
         b, c, h, w, d = x.shape
         return c == blk.in_channels and bool(L.query("vq3d_preact_stack_supported", b, c,

@@ -29,7 +29,9 @@ class FusedAdam(torch.optim.Optimizer):
         return int(self.step_t.item())
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, skip=None):
+        """skip: optional device flag (GradScaler.found_inf): when non-zero the update and the step
+        count are skipped on the device."""
         loss = closure() if closure is not None else None
         ops.join_side()  # weight gradients issued on the side stream are complete
         g = self.param_groups[0]
@@ -37,7 +39,7 @@ class FusedAdam(torch.optim.Optimizer):
         f = self.flat
         L.call("vq3d_adam_amsgrad_dev", L.ptr(f.data), L.ptr(f.grad), L.ptr(self.m), L.ptr(self.v),
                L.ptr(self.vmax), f.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]), L.ptr(self.step_t),
-               L.stream())
+               L.ptr(skip) if skip is not None else None, L.stream())
         return loss
 
     def zero_grad(self, set_to_none: bool = False):
@@ -81,3 +83,69 @@ class FusedAdam(torch.optim.Optimizer):
         self.step_t.fill_(steps.pop() if steps else 0)
         for g, sg in zip(self.param_groups, state_dict["param_groups"]):
             g["lr"] = sg["lr"]
+
+
+class GradScaler:
+    """Dynamic loss scaling for the fp16 path: torch.cuda.amp.GradScaler as PL 1.2.10's native AMP
+    plugin uses it for the reference's precision=16 (vqvae/train.py:32; init_scale 2**16, growth
+    x2 after 2000 clean steps, backoff x0.5), over the model's flat fp32 gradient with every piece
+    of state on the device, so a captured step graph replays it:
+
+        scaler.scale(loss).backward(); allreduce(); scaler.step(opt); scaler.update()
+
+    step() unscales the flat gradient in place and flags a non-finite value (vq3d_grad_unscale);
+    FusedAdam then skips the update and its step count on a flagged step; update() backs the
+    scale off or grows it (vq3d_loss_scale_update).  enabled=False (bf16 / fp32): pass-through."""
+
+    def __init__(self, device, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000,
+                 enabled=True):
+        self.enabled = enabled
+        self.growth_factor, self.backoff_factor, self.growth_interval = growth_factor, backoff_factor, growth_interval
+        self.scale_t = torch.full((), float(init_scale), dtype=torch.float32, device=device)
+        self.tracker = torch.zeros((), dtype=torch.int32, device=device)
+        self.found_inf = torch.zeros((), dtype=torch.float32, device=device)
+        self._unscaled = False
+
+    def scale(self, loss):
+        return loss * self.scale_t if self.enabled else loss
+
+    def unscale_(self, opt):
+        """The flat gradient divided by the scale in place (+ the non-finite flag), as
+        torch.cuda.amp.GradScaler.unscale_; step() then does not unscale again."""
+        if not self.enabled or self._unscaled:
+            return
+        ops.join_side()
+        f = opt.flat
+        L.call("vq3d_grad_unscale", L.ptr(f.grad), f.numel, L.ptr(self.scale_t), L.ptr(self.found_inf), L.stream())
+        self._unscaled = True
+
+    def step(self, opt):
+        if not self.enabled:
+            return opt.step()
+        self.unscale_(opt)
+        self._unscaled = False
+        return opt.step(skip=self.found_inf)
+
+    def update(self):
+        if self.enabled:
+            L.call("vq3d_loss_scale_update", L.ptr(self.scale_t), L.ptr(self.tracker), L.ptr(self.found_inf),
+                   float(self.growth_factor), float(self.backoff_factor), int(self.growth_interval), L.stream())
+
+    def get_scale(self):
+        return float(self.scale_t) if self.enabled else 1.0
+
+    def state_dict(self):
+        """torch GradScaler.state_dict()'s keys (PL stores it as 'native_amp_scaling_state')."""
+        if not self.enabled:
+            return {}
+        return {"scale": float(self.scale_t), "growth_factor": self.growth_factor,
+                "backoff_factor": self.backoff_factor, "growth_interval": self.growth_interval,
+                "_growth_tracker": int(self.tracker)}
+
+    def load_state_dict(self, sd):
+        if not sd:
+            return
+        self.scale_t.fill_(float(sd["scale"]))
+        self.tracker.fill_(int(sd["_growth_tracker"]))
+        self.growth_factor, self.backoff_factor = float(sd["growth_factor"]), float(sd["backoff_factor"])
+        self.growth_interval = int(sd["growth_interval"])

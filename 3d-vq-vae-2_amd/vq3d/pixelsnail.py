@@ -441,7 +441,7 @@ class PixelSNAIL(nn.Module):
     def __init__(self, args, compute_dtype="bf16"):
         super().__init__()
         self._parse_input_args(args)
-        self.compute_dtype = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self.compute_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(compute_dtype, torch.float32)
         self.parse_input = nn.Conv3d(in_channels=self.input_dim, out_channels=self.model_dim, kernel_size=1)
         condition_dim = self.model_dim if self.use_conditioning else 0
         self.embed_condition = nn.Conv3d(in_channels=self.condition_dim, out_channels=condition_dim,

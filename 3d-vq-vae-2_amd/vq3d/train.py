@@ -22,7 +22,8 @@ ModelCheckpoint), restated here without that dependency:
     PL 1.2.10's counter convention (pl_checkpoint_counters / resume_counters), so a checkpoint
     written by the reference resumes here at the epoch PL would resume it at, and vice versa;
     last.ckpt is also written when training stops (max_steps / max_epochs).
-precision=16 is recorded (the path computes in bf16 activations per --compute-dtype).
+precision=16 is recorded; the path computes in the --compute-dtype format: bf16 (default) or fp16 with
+the reference's AMP loss scaling (optim.GradScaler, its state saved as native_amp_scaling_state).
 """
 import os
 import random
@@ -37,6 +38,7 @@ from .checkpoint import load_checkpoint, save_checkpoint
 from .data import CTDataModule
 from .graph import StepGraph
 from .model import VQVAE
+from .optim import GradScaler
 
 
 def add_trainer_args(parser):
@@ -123,19 +125,19 @@ class Checkpointer:
         return {"monitor": self.monitor, "best_model_score": self.best_score, "best_model_path": self.best_path,
                 "dirpath": str(self.dirpath)}
 
-    def __call__(self, model, opt, epoch, pl_global_step, score, max_steps=None):
+    def __call__(self, model, opt, epoch, pl_global_step, score, max_steps=None, scaler=None):
         self.dirpath.mkdir(parents=True, exist_ok=True)
         ep, gs = pl_checkpoint_counters(epoch, pl_global_step, max_steps)
         if score is not None and (self.best_score is None or score < self.best_score):
             old = self.best_path
             self.best_score = float(score)
             self.best_path = str(self.dirpath / f"epoch={epoch}-step={pl_global_step}.ckpt")
-            save_checkpoint(self.best_path, model, opt, epoch=ep, global_step=gs, callbacks={"ModelCheckpoint":
-                                                                                            self.state()})
+            save_checkpoint(self.best_path, model, opt, epoch=ep, global_step=gs,
+                            callbacks={"ModelCheckpoint": self.state()}, scaler=scaler)
             if old and old != self.best_path and os.path.exists(old):
                 os.remove(old)
         save_checkpoint(str(self.dirpath / "last.ckpt"), model, opt, epoch=ep, global_step=gs,
-                        callbacks={"ModelCheckpoint": self.state()})
+                        callbacks={"ModelCheckpoint": self.state()}, scaler=scaler)
 
 
 def _to_device(batch, dev):
@@ -173,6 +175,8 @@ def main(args: Namespace, datamodule=None):
     model = VQVAE(args).to(dev)
     model.train()
     opt = model.configure_optimizers()
+    # --compute-dtype fp16 trains like the reference's precision=16: PL native AMP's loss scaling
+    scaler = GradScaler(dev, enabled=model.compute_dtype == torch.float16)
     ckpt = Checkpointer(Path(args.default_root_dir) / "checkpoints")
     epoch0, step = 0, 0
     if args.resume_from_checkpoint:
@@ -180,18 +184,19 @@ def main(args: Namespace, datamodule=None):
         model.load_state_dict(ck["state_dict"])
         if ck.get("optimizer_states"):
             opt.load_state_dict(ck["optimizer_states"][0])
+        scaler.load_state_dict(ck.get("native_amp_scaling_state"))
         epoch0, step = resume_counters(ck)
         st = ck.get("callbacks", {}).get("ModelCheckpoint") or {}
         ckpt.best_score, ckpt.best_path = st.get("best_model_score"), st.get("best_model_path")
     # built after any resume, so the replicas start from the restored (identical) state
     reducer = parallel.GradientAllReduce(model)
     try:
-        return _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, step)
+        return _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, step, scaler)
     finally:
         reducer.close()
 
 
-def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, step):
+def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, step, scaler):
     train_ds, val_ds = datamodule.train_dataset, datamodule.val_dataset
     sampler = (torch.utils.data.distributed.DistributedSampler(train_ds, world, rank, shuffle=True, seed=42,
                                                                drop_last=True) if world > 1 else None)
@@ -207,9 +212,10 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
     def train_step(x, nvs):
         opt.zero_grad()
         loss = model.training_step((x, nvs), 0)
-        loss.backward()
+        scaler.scale(loss).backward()
         reducer()
-        opt.step()
+        scaler.step(opt)
+        scaler.update()
         return loss
     # the whole step as a HIP graph per input shape (single rank, or ranks whose RCCL collectives
     # replay correctly inside a graph: parallel.graph_collectives_ok)
@@ -233,13 +239,13 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
             if (i + 1) % val_every == 0 or (i + 1) == n_batches:
                 score = validate(model, vloader, dev) if len(val_ds) else None
                 if rank == 0:  # PL's global_step is still this batch's 0-based index here
-                    ckpt(model, opt, epoch, step - 1, score, args.max_steps)
+                    ckpt(model, opt, epoch, step - 1, score, args.max_steps, scaler)
             if args.max_steps is not None and step >= args.max_steps:
                 break
         if args.max_steps is not None and step >= args.max_steps:
             break
     if rank == 0 and step > 0:  # training ended (max_steps / max_epochs): last.ckpt holds the final state
-        ckpt(model, opt, epoch, step - 1, None, args.max_steps)
+        ckpt(model, opt, epoch, step - 1, None, args.max_steps, scaler)
     return model, opt, history, ckpt
 
 

@@ -60,7 +60,9 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="3l_pub", choices=sorted(CONFIGS))
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
+                   help="activation / matrix-core format: bf16 (BASELINE's), fp16 (the reference's AMP, with dynamic "
+                        "loss scaling) or fp32")
     p.add_argument("--size", type=int, nargs=3, default=None, help="override the volume H W D")
     p.add_argument("--encode-only", action="store_true", help="eval encode + codebook search (configs[3])")
     p.add_argument("--prior", action="store_true",
@@ -692,16 +694,20 @@ def main():
             with torch.no_grad():
                 return next(extract_samples(model, [x]))[0]
     else:
+        from vq3d.optim import GradScaler
         model.train()
         opt = model.configure_optimizers()
         allreduce = parallel.GradientAllReduce(model)
+        # fp16: the reference's native AMP loss scaling (device-resident, captured with the step)
+        scaler = GradScaler(dev, enabled=a.dtype == "fp16")
 
         def step(i):
             opt.zero_grad()
             loss = model.training_step((x, nvs), i)
-            loss.backward()
+            scaler.scale(loss).backward()
             allreduce()
-            opt.step()
+            scaler.step(opt)
+            scaler.update()
             return loss
 
     for i in range(a.warmup):

@@ -413,9 +413,19 @@ int vq3d_adam_amsgrad(float *p, const float *g, float *m, float *v, float *vmax,
                       float beta1, float beta2, float eps, int64_t step, vq3d_stream_t stream);
 /* Same update with the step count on the device: uses *step + 1 for the bias corrections, then
  * increments *step -- no host value baked into the launch, so a captured HIP graph of the
- * training step replays correctly. */
+ * training step replays correctly.  skip (NULL: never): a device flag; when *skip != 0 (the loss
+ * scaler found a non-finite gradient) neither the parameters nor *step change (GradScaler.step). */
 int vq3d_adam_amsgrad_dev(float *p, const float *g, float *m, float *v, float *vmax, int64_t n, float lr,
-                          float beta1, float beta2, float eps, int64_t *step, vq3d_stream_t stream);
+                          float beta1, float beta2, float eps, int64_t *step, const float *skip,
+                          vq3d_stream_t stream);
+/* --- dynamic loss scaling: torch.cuda.amp.GradScaler's device work for the fp16 path (the
+ * reference's PL native AMP, vqvae/train.py:32).  grad_unscale: g *= 1 / *scale over the flat
+ * gradient, *found_inf = 1 when any value was inf / NaN (else 0).  loss_scale_update: on a flagged
+ * step *scale *= backoff and *growth_tracker = 0, else after `interval` clean steps in a row
+ * *scale *= growth (if finite).  All state on the device (graph-capturable). --- */
+int vq3d_grad_unscale(float *g, int64_t n, const float *scale, float *found_inf, vq3d_stream_t stream);
+int vq3d_loss_scale_update(float *scale, int32_t *growth_tracker, const float *found_inf, float growth,
+                           float backoff, int32_t interval, vq3d_stream_t stream);
 
 /* --- utilities --- */
 int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, int64_t n,

@@ -1,4 +1,5 @@
-"""Parity of the BENCHMARKED path: the published 3-layer model (50 pre-q / 50 post-q / 3 post-up /
+"""Parity of the BENCHMARKED path (bf16) and of the reference's own precision (fp16 with AMP loss
+scaling): the published 3-layer model (50 pre-q / 50 post-q / 3 post-up /
 2 post-down blocks, K = 128 / 256 / 512; slurm-jobs/train_vqvae_3d.job:76-86) with bf16
 activations, one full training step on the GPU against the fp32 CPU oracle (oracle/vqvae_cpu,
 pinned to the reference by the golden tests) from the same perturbed weights
@@ -22,14 +23,20 @@ this path rounds activations to bf16, 8 mantissa bits):
     either (profiles/r03_precision_study.txt);
   * decoded volume: relative MSE ||dec - ref||^2 / ||ref||^2 <= 1e-3 (north_star's
     "reconstruction MSE within stated fp tolerance"; measured 6.1e-5);
-  * gradients: the whole gradient vector within 3 % relative L2 (measured 1.18 %) and cosine >= 0.999; every
-    weight tensor within 60 % relative L2 and cosine >= 0.975 (the worst, 55 % / 0.978, are the
+  * gradients: the whole gradient vector within 3 % relative L2 (measured 1.40 %) and cosine >= 0.999; every
+    weight tensor within 50 % relative L2 and cosine >= 0.98 (the worst, 41.5 % / 0.987, are the
     bottom-level pre-quantize blocks next to the Quantizer, whose gradient changes with every flipped
     code; the 18-channel engine's 1x1 weights are bf16 matrix-core operands in both directions, as
     the reference's autocast casts every conv weight to fp16); the
-    scalar biases / scales of each block stack, as one vector, within 10 % (measured <= 5 %; single
+    scalar biases / scales of each block stack, as one vector, within 10 % (measured <= 5.2 %; single
     scalars are sums over ~10^5..10^6 terms that nearly cancel, so a lone scalar has no meaningful
     relative error).
+fp16 (--compute-dtype fp16: every 16-bit activation / matrix-core operand IEEE fp16 as under the
+reference's autocast, the gradient through vq3d.optim.GradScaler's scaled backward and unscale):
+code match >= 99 / 99.5 / 100 % (measured 99.30 / 99.61 / 100 %), every weight tensor within 15 %
+relative L2 and cosine >= 0.99 (measured 11.7 % / 0.9956), the whole gradient within 1 % (0.116 %),
+the scalar groups within 5 % (0.9 %), decoded rel-MSE <= 1e-4 (7.6e-6), loss within 0.2 % (9e-4 %);
+identical at loss scales 2^16 and 2^24.
 """
 import numpy as np
 import pytest
@@ -40,7 +47,13 @@ pytestmark = pytest.mark.gpu
 PUB3 = dict(n_bottleneck_blocks=3, n_pre_quantization_blocks=50, n_post_quantization_blocks=50,
             n_post_upscale_blocks=3, n_post_downscale_blocks=2, num_embeddings=[128, 256, 512])
 SIZE = (256, 256, 128)
-FLOORS = (0.945, 0.965, 0.99)
+# per compute dtype: code-match floors, (loss rel, decoded rel-MSE, all-gradient rel-L2 / cosine,
+# per-tensor rel-L2 / cosine, scalar-group rel-L2)
+BOUNDS = {"bf16": ((0.945, 0.965, 0.99), (1e-2, 1e-3, 0.03, 0.999, 0.5, 0.98, 0.1)),
+          "fp16": ((0.99, 0.995, 1.0), (2e-3, 1e-4, 0.01, 0.9999, 0.15, 0.99, 0.05))}
+
+
+_REF = {}
 
 
 def _perturb(m, seed=1, std=0.02):
@@ -50,15 +63,17 @@ def _perturb(m, seed=1, std=0.02):
             p.add_(std * torch.randn(p.shape, generator=g))
 
 
-def test_bf16_published_model_step_vs_oracle(gpu):
+@pytest.mark.parametrize("dt,scale", [("bf16", 1.0), ("fp16", 2.0 ** 16), ("fp16", 2.0 ** 24)])
+def test_published_model_step_vs_oracle(gpu, dt, scale):
     import vq3d
     from oracle import vqvae_cpu as O
+    from vq3d.optim import GradScaler
     torch.manual_seed(0)
-    m = vq3d.VQVAE(vq3d.default_args(compute_dtype="bf16", base_lr=1e-4, **PUB3))
+    m = vq3d.VQVAE(vq3d.default_args(compute_dtype=dt, base_lr=1e-4, **PUB3))
     _perturb(m)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
     x = torch.rand((1, 1) + SIZE, generator=torch.Generator().manual_seed(1234)) * 4.5 - 0.5
-    # GPU bf16 step
+    # GPU step
     m = m.to(gpu)
     m.train()
     opt = m.configure_optimizers()
@@ -72,17 +87,21 @@ def test_bf16_published_model_step_vs_oracle(gpu):
     m.forward = capture
     loss = m.training_step((x.to(gpu), torch.tensor([SIZE[2]])), 0)
     del m.forward
-    loss.backward()
+    scaler = GradScaler(gpu, init_scale=scale, enabled=dt == "fp16")
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
     vq3d.ops.join_side()
+    assert float(scaler.found_inf) == 0.0
     torch.cuda.synchronize()
     dec, (_, _, idxs) = cap["r"]
     grads = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
-    # CPU oracle fp32 step
-    torch.set_num_threads(min(16, torch.get_num_threads()))
-    cfg = O.Config(**PUB3)
-    loss_ref, grads_ref, aux = O.train_step(cfg, sd, {}, x, [SIZE[2]], 1e-4)
+    # CPU oracle fp32 step (same weights and volume for both dtypes: computed once)
+    if "ref" not in _REF:
+        torch.set_num_threads(min(16, torch.get_num_threads()))
+        _REF["ref"] = O.train_step(O.Config(**PUB3), sd, {}, x, [SIZE[2]], 1e-4)
+    loss_ref, grads_ref, aux = _REF["ref"]
     # loss
-    lr = abs(float(loss) - float(loss_ref)) / abs(float(loss_ref))
+    lr = abs(float(loss.detach()) - float(loss_ref)) / abs(float(loss_ref))
     # codes
     match = [float((a.cpu() == b).float().mean()) for a, b in zip(idxs, aux["idxs"])]
     # decoded
@@ -109,17 +128,18 @@ def test_bf16_published_model_step_vs_oracle(gpu):
                    for k, (gs, rs) in groups.items()), reverse=True)
     worst_rel = max(tensors)
     worst_cos = min(tensors, key=lambda t: t[1])
-    print(f"bf16 3L-pub {SIZE}: loss gpu {float(loss):.6f} ref {float(loss_ref):.6f} rel {lr:.2e}; "
+    print(f"{dt} (loss scale {scale:g}) 3L-pub {SIZE}: loss gpu {float(loss):.6f} ref {float(loss_ref):.6f} rel {lr:.2e}; "
           f"code match bottom/mid/top {match}; decoded rel-MSE {rmse:.2e}; all-gradient rel-L2 {flat_rel:.3e} "
           f"cosine {flat_cos:.6f}; worst weight tensor rel-L2 {worst_rel[0]:.3f} ({worst_rel[2]}), worst cosine "
           f"{worst_cos[1]:.4f} ({worst_cos[2]}); worst scalar-group rel-L2 {scal[0][0]:.3f} ({scal[0][1]}); "
           f"scalar groups {[(k, round(v, 4)) for v, k in scal]}")
-    assert lr <= 1e-2, lr
-    for lvl, (mm, fl) in enumerate(zip(match, FLOORS)):
+    floors, (b_loss, b_mse, b_rel, b_cos, b_trel, b_tcos, b_scal) = BOUNDS[dt]
+    assert lr <= b_loss, lr
+    for lvl, (mm, fl) in enumerate(zip(match, floors)):
         assert mm >= fl, (lvl, mm)
-    assert rmse <= 1e-3, rmse
-    assert flat_rel <= 0.03 and flat_cos >= 0.999, (flat_rel, flat_cos)
-    assert worst_rel[0] <= 0.6 and worst_cos[1] >= 0.975, (worst_rel, worst_cos)
-    assert scal[0][0] <= 0.1, scal[0]
+    assert rmse <= b_mse, rmse
+    assert flat_rel <= b_rel and flat_cos >= b_cos, (flat_rel, flat_cos)
+    assert worst_rel[0] <= b_trel and worst_cos[1] >= b_tcos, (worst_rel, worst_cos)
+    assert scal[0][0] <= b_scal, scal[0]
     assert np.isfinite(float(loss))
 

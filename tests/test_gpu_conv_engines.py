@@ -50,8 +50,19 @@ CASES = [
 ]
 
 
+HALF = [torch.bfloat16, torch.float16]  # the two 16-bit builds of the kernels
+_H = [torch.bfloat16]  # the 16-bit format of the test being run (set per test)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_by_default():
+    """Tests that do not pick a format run bf16 (a parametrized fp16 test must not leak its choice)."""
+    _H[0] = torch.bfloat16
+    yield
+
+
 def rnd(shape, dev, g, scale=1.0):
-    return (torch.randn(shape, device=dev, generator=g) * scale).to(torch.bfloat16).float()
+    return (torch.randn(shape, device=dev, generator=g) * scale).to(_H[0]).float()
 
 
 def rel(a, b):
@@ -60,7 +71,9 @@ def rel(a, b):
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_mfma_forward_and_dgrad_match_valu(gpu, case):
+@pytest.mark.parametrize("half", HALF)
+def test_mfma_forward_and_dgrad_match_valu(gpu, case, half):
+    _H[0] = half
     from vq3d import ops
     cin, cout, (h, w, d), k, s, p, circ = case
     g = torch.Generator(device=gpu).manual_seed(hash(case) % 1000)
@@ -70,7 +83,7 @@ def test_mfma_forward_and_dgrad_match_valu(gpu, case):
     a = rnd((1,), gpu, g, 0.1)
     b = rnd((1,), gpu, g, 0.1)
     ref = ops.conv_fwd(x, wt, geom, pro=(a, b), act=(b, a))
-    out = ops.conv_fwd(x.to(torch.bfloat16), wt, geom, pro=(a, b), act=(b, a))
+    out = ops.conv_fwd(x.to(_H[0]), wt, geom, pro=(a, b), act=(b, a))
     assert rel(out.float(), ref) < 1.5e-2, ("fwd", case, rel(out.float(), ref))
     if s != 1:
         return
@@ -84,13 +97,15 @@ def test_mfma_forward_and_dgrad_match_valu(gpu, case):
     gscale = rnd((1,), gpu, g)
     gr, _ = ops.conv_bwd(gy, x, wt, geom, pro=(a, b), gscale=gscale, aux=x, addend=add, dpro_pre=dpre_r,
                          dpro_post=dpost_r)
-    gm, _ = ops.conv_bwd(gy.to(torch.bfloat16), x.to(torch.bfloat16), wt, geom, pro=(a, b), gscale=gscale,
-                         aux=x.to(torch.bfloat16), addend=add.to(torch.bfloat16), dpro_pre=dpre, dpro_post=dpost)
+    gm, _ = ops.conv_bwd(gy.to(_H[0]), x.to(_H[0]), wt, geom, pro=(a, b), gscale=gscale,
+                         aux=x.to(_H[0]), addend=add.to(_H[0]), dpro_pre=dpre, dpro_post=dpost)
     assert rel(gm.float(), gr) < 1.5e-2, ("dgrad", case, rel(gm.float(), gr))
     assert abs(float(dpre) - float(dpre_r)) <= 2e-2 * float(gr.abs().sum()) / gr.numel() * gr.numel() ** 0.5 + 1e-3
 
 
-def test_mfma_dual_input_and_residual(gpu):
+@pytest.mark.parametrize("half", HALF)
+def test_mfma_dual_input_and_residual(gpu, half):
+    _H[0] = half
     from vq3d import ops
     g = torch.Generator(device=gpu).manual_seed(3)
     x1 = rnd((1, 8, 8, 8, 4), gpu, g).contiguous(memory_format=CL)
@@ -101,14 +116,16 @@ def test_mfma_dual_input_and_residual(gpu):
     bi = rnd((1,), gpu, g)
     geom = ops.ConvGeom(3, 1, 1, True)
     ref = ops.conv_fwd(x1, wt, geom, x2=x2, scale=sc, bias=bi, residual=res, residual_up2=True)
-    out = ops.conv_fwd(x1.bfloat16(), wt, geom, x2=x2.bfloat16(), scale=sc, bias=bi, residual=res.bfloat16(),
+    out = ops.conv_fwd(x1.to(_H[0]), wt, geom, x2=x2.to(_H[0]), scale=sc, bias=bi, residual=res.to(_H[0]),
                        residual_up2=True)
     assert rel(out.float(), ref) < 1.5e-2
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_tiled_wgrad_matches_valu(gpu, case):
+@pytest.mark.parametrize("half", HALF)
+def test_tiled_wgrad_matches_valu(gpu, case, half):
     """bf16 MFMA / LDS-tiled weight gradient (+ epilogue scalar / conv-bias gradients) vs the fp32 engine."""
+    _H[0] = half
     from vq3d import ops
     cin, cout, (h, w, d), k, s, p, circ = case
     g = torch.Generator(device=gpu).manual_seed(1 + hash(case) % 1000)
@@ -121,7 +138,7 @@ def test_tiled_wgrad_matches_valu(gpu, case):
     oh, ow, od = geom.out(h), geom.out(w), geom.out(d)
     gy = rnd((2, cout, oh, ow, od), gpu, g).contiguous(memory_format=CL)
     outs = []
-    for dt in (torch.float32, torch.bfloat16):
+    for dt in (torch.float32, _H[0]):
         dw = torch.zeros_like(wt)
         dscale = torch.zeros(1, device=gpu)
         dbias = torch.zeros(1, device=gpu)
@@ -146,9 +163,11 @@ S2_DGRAD_CASES = [
 
 
 @pytest.mark.parametrize("case", S2_DGRAD_CASES)
-def test_dgrad_s2_matches_valu(gpu, case):
+@pytest.mark.parametrize("half", HALF)
+def test_dgrad_s2_matches_valu(gpu, case, half):
     """bf16 stride-2 backward-data (+ the activated-aux derivative, the addend, the gradient scale and
     the prologue-scalar partial sums) vs the fp32 engine on the same bf16-representable inputs."""
+    _H[0] = half
     from vq3d import ops
     cin, cout, (h, w, d), epi = case
     g = torch.Generator(device=gpu).manual_seed(11 + h + cin)
@@ -159,7 +178,7 @@ def test_dgrad_s2_matches_valu(gpu, case):
     add = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
     ab, gs = rnd((1,), gpu, g, 0.3), rnd((1,), gpu, g)
     outs = []
-    for dt in (torch.float32, torch.bfloat16):
+    for dt in (torch.float32, _H[0]):
         pre, post = torch.zeros(1, device=gpu), torch.zeros(1, device=gpu)
         kw = dict(gscale=gs, aux=x.to(dt), aux_b=ab, addend=add.to(dt), dpro_pre=pre, dpro_post=post) if epi else {}
         gx, _ = ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, **kw)
@@ -185,11 +204,13 @@ WGRAD_DS_CASES = [
 
 
 @pytest.mark.parametrize("case", WGRAD_DS_CASES)
-def test_wgrad_dshift(gpu, case):
+@pytest.mark.parametrize("half", HALF)
+def test_wgrad_dshift(gpu, case, half):
     """Few-channel weight gradients without scale / conv-bias epilogue parameters (wgrad_ds.hip: the
     full-resolution up / down block convs, D-shifted MFMA over whole D-lines), bf16, accumulated
     into dW (and, for the skip convs, the bias gradient sum(g) and the prologue x + b), vs the fp32
     VALU engine on the same bf16-representable inputs: only the summation order differs."""
+    _H[0] = half
     from vq3d import ops
     bsz, cin, cout, (h, w, d), k, s, p, circ, pro = case
     g = torch.Generator(device=gpu).manual_seed(5 + h + cin)
@@ -200,7 +221,7 @@ def test_wgrad_dshift(gpu, case):
     base = rnd((cout, cin, k, k, k), gpu, g)
     b1c = rnd((1,), gpu, g, 0.1)
     outs = []
-    for dt in (torch.float32, torch.bfloat16):
+    for dt in (torch.float32, _H[0]):
         dw = base.clone()
         db = torch.full((1,), 0.5, device=gpu)
         ops.conv_bwd(gy.to(dt), x.to(dt), wt, geom, want_gx=False, dw=dw, pro=(b1c,) if pro else None,
@@ -239,10 +260,11 @@ PW_CASES = [
 
 
 @pytest.mark.parametrize("case", PW_CASES)
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_pointwise_wgrad_vs_torch(gpu, case, dt):
     """1x1x1 weight / conv-bias / scalar gradients vs a plain torch fp32 einsum of the same
     (bf16-representable) inputs, with the ELU-affine prologue and a concatenated second input."""
+    _H[0] = dt if dt != torch.float32 else torch.bfloat16  # inputs representable in the tested format
     from vq3d import ops
     cin, cin2, cout, (h, w, d) = case
     g = torch.Generator(device=gpu).manual_seed(7 + cin * 31 + cout)
@@ -282,10 +304,12 @@ PW_MMA_CASES = [
 
 
 @pytest.mark.parametrize("case", PW_MMA_CASES)
-def test_pointwise_mma_matches_valu(gpu, case):
+@pytest.mark.parametrize("half", HALF)
+def test_pointwise_mma_matches_valu(gpu, case, half):
     """bf16 matrix-core 1x1 conv (k_pw_mma: bf16 operands, fp32 accumulation) vs the fp32 pointwise
     engine: forward with the ELU prologue and every epilogue term, backward-data with gscale, the
     prologue derivative, the addend, the split output and the prologue-scalar sums."""
+    _H[0] = half
     from vq3d import ops
     bt, cin, cin2, cout, (h, w, d) = case
     g = torch.Generator(device=gpu).manual_seed(7 + cin + cout + h)
@@ -297,7 +321,7 @@ def test_pointwise_mma_matches_valu(gpu, case):
     sc, bi = rnd((1,), gpu, g), rnd((1,), gpu, g)
     cb = rnd((cout,), gpu, g)
     res = rnd((bt, cout, h, w, d), gpu, g).contiguous(memory_format=CL)
-    bf = lambda t: None if t is None else t.bfloat16()
+    bf = lambda t: None if t is None else t.to(_H[0])
     ref = ops.conv_fwd(x, wt, geom, pro=(a, b), x2=x2, scale=sc, bias=bi, cbias=cb, residual=res, act=(b, a))
     out = ops.conv_fwd(bf(x), wt, geom, pro=(a, b), x2=bf(x2), scale=sc, bias=bi, cbias=cb, residual=bf(res),
                        act=(b, a))
@@ -322,10 +346,11 @@ def test_pointwise_mma_matches_valu(gpu, case):
 
 
 @pytest.mark.parametrize("case", [(4, 4, (16, 16, 32)), (2, 8, (8, 8, 8)), (4, 2, (6, 10, 4)), (8, 8, (4, 4, 4))])
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
 def test_pointwise_rows_residual_up2(gpu, case, dt):
     """Few-channel 1x1 conv with the ResizeConv skip's half-grid residual upsampled x2 on the fly
     (k_pw_rows; vqvae/layers.py:591-597) vs torch: conv * scale + bias + trilinear(res)."""
+    _H[0] = dt if dt != torch.float32 else torch.bfloat16  # inputs representable in the tested format
     from vq3d import ops
     cin, cout, (h, w, d) = case
     g = torch.Generator(device=gpu).manual_seed(cin * 7 + cout + h)

@@ -11,7 +11,8 @@ CL = torch.channels_last_3d
 
 
 @pytest.mark.parametrize("c,shape", [(4, (1, 1, 64, 64, 32)), (2, (2, 1, 32, 32, 16)), (8, (1, 1, 16, 16, 16))])
-def test_parse_input_matches_float64(gpu, c, shape):
+@pytest.mark.parametrize("half", [torch.bfloat16, torch.float16])
+def test_parse_input_matches_float64(gpu, c, shape, half):
     from vq3d import functional as Fn
     from vq3d.flat import FlatParams
     torch.manual_seed(c)
@@ -19,15 +20,15 @@ def test_parse_input_matches_float64(gpu, c, shape):
     FlatParams(conv.parameters(), gpu)
     gen = torch.Generator().manual_seed(3)
     x = torch.rand(shape, generator=gen) * 4.5 - 0.5
-    g = torch.randn(shape[:1] + (c,) + shape[2:], generator=gen).bfloat16()
+    g = torch.randn(shape[:1] + (c,) + shape[2:], generator=gen).to(half)
     xd = x.to(gpu)
-    assert Fn.parse_input_fused(xd, conv, torch.bfloat16)
+    assert Fn.parse_input_fused(xd, conv, half)
     outs = []
     for _ in range(2):
         conv.weight.grad.zero_()
         conv.bias.grad.zero_()
-        y = Fn.ParseInputFn.apply(xd, conv.weight, conv.bias)
-        assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=CL)
+        y = Fn.ParseInputFn.apply(xd, conv.weight, conv.bias, half)
+        assert y.dtype == half and y.is_contiguous(memory_format=CL)
         y.backward(g.to(gpu).contiguous(memory_format=CL))
         torch.cuda.synchronize()
         outs.append((y.float().cpu(), conv.weight.grad.cpu().clone(), conv.bias.grad.cpu().clone()))

@@ -35,8 +35,19 @@ def _block(c, seed):
     return blk
 
 
+HALF = [torch.bfloat16, torch.float16]  # the two 16-bit builds of the kernels
+_H = [torch.bfloat16]  # the 16-bit format of the test being run (set per test)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_by_default():
+    """Tests that do not pick a format run bf16 (a parametrized fp16 test must not leak its choice)."""
+    _H[0] = torch.bfloat16
+    yield
+
+
 def rb(t):
-    return t.float().bfloat16().double()
+    return t.float().to(_H[0]).double()
 
 
 def _pad(t):
@@ -88,16 +99,18 @@ def _run(blk, x, gy, dev):
     assert int(L.query("vq3d_preact_small_plan", b, c, c // 2, h, w, d)) == 2  # the column kernels
     m = blk.to(dev)
     FlatParams(m.parameters(), dev)
-    xg = x.to(dev).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
+    xg = x.to(dev).to(_H[0]).contiguous(memory_format=CL).requires_grad_(True)
     assert ops.preact_small_supported(xg, c // 2) and ops.small_backward_fused(xg)
     y = m(xg)
-    y.backward(gy.to(dev).bfloat16().contiguous(memory_format=CL))
+    y.backward(gy.to(dev).to(_H[0]).contiguous(memory_format=CL))
     torch.cuda.synchronize()
     return m, y, xg
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_col_block_matches_float64(gpu, shape):
+@pytest.mark.parametrize("half", HALF)
+def test_col_block_matches_float64(gpu, shape, half):
+    _H[0] = half
     b, c, h, w, d = shape
     blk = _block(c, seed=h + d + c)
     gen = torch.Generator().manual_seed(7)
@@ -134,14 +147,16 @@ def test_col_block_deterministic(gpu):
         assert torch.equal(a, b)
 
 
-def test_col_block_fullsize_sampled(gpu):
+@pytest.mark.parametrize("half", HALF)
+def test_col_block_fullsize_sampled(gpu, half):
     """(4, 2) at 512x512x128 (the decoder's post-upscale blocks): finite, and out / gx on sampled
     voxels equal a float64 recompute of those voxels' 3x3x3 neighbourhoods."""
+    _H[0] = half
     shape = (1, 4, 512, 512, 128)
     blk = _block(4, seed=11)
     gen = torch.Generator(device=gpu).manual_seed(5)
-    x = torch.randn(shape, generator=gen, device=gpu).bfloat16()
-    gy = torch.randn(shape, generator=gen, device=gpu).bfloat16()
+    x = torch.randn(shape, generator=gen, device=gpu).to(_H[0])
+    gy = torch.randn(shape, generator=gen, device=gpu).to(_H[0])
     m, y, xg = _run(blk, x.float(), gy.float(), gpu)
     assert torch.isfinite(y.float()).all() and torch.isfinite(xg.grad.float()).all()
     for p in m.parameters():

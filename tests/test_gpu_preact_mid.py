@@ -37,9 +37,24 @@ def _block(seed):
     return blk
 
 
+HALF = [torch.bfloat16, torch.float16]  # the two 16-bit builds of the kernels
+_H = [torch.bfloat16]  # the 16-bit format of the test being run (set per test)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_by_default():
+    """Tests that do not pick a format run bf16 (a parametrized fp16 test must not leak its choice)."""
+    _H[0] = torch.bfloat16
+    yield
+
+
 def rb(t):
-    """round float64 -> bf16 -> float64 (round-to-nearest-even, torch's conversion)"""
-    return t.float().bfloat16().double()
+    """round float64 -> the 16-bit format -> float64 (round-to-nearest-even, torch's conversion)"""
+    return t.float().to(_H[0]).double()
+
+
+def rnd(t):
+    return t.to(_H[0]).double()
 
 
 def pad(t):
@@ -112,9 +127,9 @@ def _run(blk, x, gy, dev, mid):
         for p in m.parameters():
             p.grad = None
         FlatParams(m.parameters(), dev)
-        xg = x.to(dev).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        xg = x.to(dev).to(_H[0]).contiguous(memory_format=CL).requires_grad_(True)
         y = m(xg)
-        y.backward(gy.to(dev).to(torch.bfloat16).contiguous(memory_format=CL))
+        y.backward(gy.to(dev).to(_H[0]).contiguous(memory_format=CL))
         torch.cuda.synchronize()
         return y.detach().float().cpu(), xg.grad.float().cpu(), {n: p.grad.cpu().clone()
                                                                   for n, p in m.named_parameters()}
@@ -123,13 +138,15 @@ def _run(blk, x, gy, dev, mid):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_fused_mid_block(gpu, shape):
+@pytest.mark.parametrize("half", HALF)
+def test_fused_mid_block(gpu, shape, half):
+    _H[0] = half
     from vq3d import ops
     blk = _block(seed=shape[2] + shape[4])
     g = torch.Generator().manual_seed(11)
-    x = torch.randn(shape, generator=g).bfloat16().double()
-    gy = torch.randn(shape, generator=g).bfloat16().double()
-    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    x = rnd(torch.randn(shape, generator=g))
+    gy = rnd(torch.randn(shape, generator=g))
+    xg = x.to(gpu).to(_H[0]).contiguous(memory_format=CL)
     assert ops.preact_mid_supported(xg, 9)
     P = {n: p.detach().double().clone() for n, p in blk.named_parameters()}
     sy, sgx, sgp = _ref_strict(P, x, gy)
@@ -153,13 +170,15 @@ def test_fused_mid_block(gpu, shape):
         assert not bad, bad
 
 
-def test_fused_mid_block_deterministic(gpu):
+@pytest.mark.parametrize("half", HALF)
+def test_fused_mid_block_deterministic(gpu, half):
     """Two backward passes give bit-identical gradients (fixed-order partial reductions)."""
+    _H[0] = half
     blk = _block(seed=3)
     g = torch.Generator().manual_seed(5)
     shape = (1, 18, 32, 32, 16)
-    x = torch.randn(shape, generator=g).bfloat16().double()
-    gy = torch.randn(shape, generator=g).bfloat16().double()
+    x = rnd(torch.randn(shape, generator=g))
+    gy = rnd(torch.randn(shape, generator=g))
     a = _run(blk, x, gy, gpu, mid=True)
     b = _run(blk, x, gy, gpu, mid=True)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
@@ -168,14 +187,16 @@ def test_fused_mid_block_deterministic(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 18, 16, 8, 16), (1, 18, 128, 128, 32)])
-def test_fused_mid_block_side_stream(gpu, shape):
+@pytest.mark.parametrize("half", HALF)
+def test_fused_mid_block_side_stream(gpu, shape, half):
     """Weight-gradient stages on the side stream (the product's concurrent mode) give the same
     bits as the single-stream backward."""
+    _H[0] = half
     from vq3d import ops
     blk = _block(seed=9)
     g = torch.Generator().manual_seed(13)
-    x = torch.randn(shape, generator=g).bfloat16().double()
-    gy = torch.randn(shape, generator=g).bfloat16().double()
+    x = rnd(torch.randn(shape, generator=g))
+    gy = rnd(torch.randn(shape, generator=g))
     a = _run(blk, x, gy, gpu, mid=True)
     ops.set_concurrent_wgrad(True)
     try:
@@ -200,7 +221,7 @@ def _run_chain(blocks, x, gy, gpu, chained, concurrent=False, poison=False):
     stack = VL.BlockStack(*[b for b in blocks]).to(gpu)
     for p in stack.parameters():
         p.grad = None
-    xd = x.to(gpu).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
+    xd = x.to(gpu).to(_H[0]).contiguous(memory_format=CL).requires_grad_(True)
     ops.set_concurrent_wgrad(concurrent)
     try:
         if poison:
@@ -211,7 +232,7 @@ def _run_chain(blocks, x, gy, gpu, chained, concurrent=False, poison=False):
             out = xd
             for b in stack:
                 out = Fn.PreActBlockFn.apply(out, b, *b._fn_params)
-        gyd = gy.to(gpu).bfloat16().contiguous(memory_format=CL)
+        gyd = gy.to(gpu).to(_H[0]).contiguous(memory_format=CL)
         if poison:
             _poison()
         out.backward(gyd)
@@ -225,16 +246,18 @@ def _run_chain(blocks, x, gy, gpu, chained, concurrent=False, poison=False):
 
 @pytest.mark.parametrize("shape,nblk,concurrent", [((2, 18, 16, 8, 16), 4, False), ((1, 18, 32, 16, 16), 3, True),
                                                    ((1, 18, 128, 128, 32), 3, False)])
-def test_mid_run_chain_matches_per_block(gpu, shape, nblk, concurrent):
+@pytest.mark.parametrize("half", HALF)
+def test_mid_run_chain_matches_per_block(gpu, shape, nblk, concurrent, half):
     """The chained run (next block's t2 in the forward tile epilogue, previous block's gz3 in the
     backward tile epilogue) against the same blocks run one by one: out, gx and every gradient
     within 1e-2 of its max -- the chained t2 / gz3 are matrix-core sums of the same bf16 operands
     the per-block pointwise kernels sum on the VALU, so an odd bf16 rounding may land one ulp
     apart."""
+    _H[0] = half
     blocks = [_block(seed=20 + i) for i in range(nblk)]
     g = torch.Generator().manual_seed(21)
-    x = torch.randn(shape, generator=g).bfloat16().double()
-    gy = torch.randn(shape, generator=g).bfloat16().double()
+    x = rnd(torch.randn(shape, generator=g))
+    gy = rnd(torch.randn(shape, generator=g))
     a = _run_chain(blocks, x, gy, gpu, chained=False)
     b = _run_chain(blocks, x, gy, gpu, chained=True, concurrent=concurrent)
     assert rel(b[0], a[0]) <= 1e-2, rel(b[0], a[0])
@@ -244,16 +267,18 @@ def test_mid_run_chain_matches_per_block(gpu, shape, nblk, concurrent):
 
 
 @pytest.mark.parametrize("shape", [(2, 18, 16, 8, 16), (1, 18, 128, 128, 32)])
-def test_mid_run_chain_ignores_stale_lds(gpu, shape):
+@pytest.mark.parametrize("half", HALF)
+def test_mid_run_chain_ignores_stale_lds(gpu, shape, half):
     """Regression: the chained forward's next-block t2 stage read K entries past a voxel's 18
     channels from LDS another wave had not written yet and multiplied them by zero weights; LDS
     left holding a NaN pattern by an earlier kernel turned into NaN activations (the 3-layer
     bench step went NaN after ~10 steps).  With every CU's LDS filled with NaN before the forward
     and before the backward the run must give the same bits as without."""
+    _H[0] = half
     blocks = [_block(seed=40 + i) for i in range(3)]
     g = torch.Generator().manual_seed(41)
-    x = torch.randn(shape, generator=g).bfloat16().double()
-    gy = torch.randn(shape, generator=g).bfloat16().double()
+    x = rnd(torch.randn(shape, generator=g))
+    gy = rnd(torch.randn(shape, generator=g))
     a = _run_chain(blocks, x, gy, gpu, chained=True)
     b = _run_chain(blocks, x, gy, gpu, chained=True, poison=True)
     assert torch.isfinite(b[0]).all() and torch.isfinite(b[1]).all()

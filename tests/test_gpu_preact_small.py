@@ -17,6 +17,17 @@ SHAPES = [(1, 2, 16, 16, 32), (1, 2, 128, 128, 32), (1, 4, 32, 16, 16), (1, 8, 3
           (1, 4, 4, 8, 2)]
 
 
+HALF = [torch.bfloat16, torch.float16]  # the two 16-bit builds of the kernels
+_H = [torch.bfloat16]  # the 16-bit format of the test being run (set per test)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_by_default():
+    """Tests that do not pick a format run bf16 (a parametrized fp16 test must not leak its choice)."""
+    _H[0] = torch.bfloat16
+    yield
+
+
 def _block(c, seed):
     from vq3d import layers as VL
     torch.manual_seed(seed)
@@ -60,9 +71,9 @@ def _run(blk, x, gy, dev, small, fused_bwd=True):
         for p in m.parameters():
             p.grad = None
         FlatParams(m.parameters(), dev)
-        xg = x.to(dev).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        xg = x.to(dev).to(_H[0]).contiguous(memory_format=CL).requires_grad_(True)
         y = m(xg)
-        y.backward(gy.to(dev).to(torch.bfloat16).contiguous(memory_format=CL))
+        y.backward(gy.to(dev).to(_H[0]).contiguous(memory_format=CL))
         torch.cuda.synchronize()
         return y.detach().float().cpu(), xg.grad.float().cpu(), {n: p.grad.cpu().clone()
                                                                   for n, p in m.named_parameters()}
@@ -71,14 +82,16 @@ def _run(blk, x, gy, dev, small, fused_bwd=True):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_fused_small_block(gpu, shape):
+@pytest.mark.parametrize("half", HALF)
+def test_fused_small_block(gpu, shape, half):
+    _H[0] = half
     from vq3d import ops
     c = shape[1]
     blk = _block(c, seed=shape[2] + shape[4] + c)
     g = torch.Generator().manual_seed(11)
-    x = torch.randn(shape, generator=g).bfloat16().float()
-    gy = torch.randn(shape, generator=g).bfloat16().float()
-    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    x = torch.randn(shape, generator=g).to(_H[0]).float()
+    gy = torch.randn(shape, generator=g).to(_H[0]).float()
+    xg = x.to(gpu).to(_H[0]).contiguous(memory_format=CL)
     assert ops.preact_small_supported(xg, max(c // 2, 1))
     ry, rgx, rgp = _ref(blk, x, gy)
     y1, gx1, gp1 = _run(blk, x, gy, gpu, small=True)

@@ -51,8 +51,18 @@ def _ref(stack, x, g):
     return out.detach(), xr.grad, {k: v.grad for k, v in sd.items()}
 
 
+_H = [torch.bfloat16]  # the 16-bit format of the matrix-core operands in _ref_strict (set per test)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_by_default():
+    """Tests that do not pick a format run bf16 (a parametrized fp16 test must not leak its choice)."""
+    _H[0] = torch.bfloat16
+    yield
+
+
 def rb(t):
-    return t.float().bfloat16().double()
+    return t.float().to(_H[0]).double()
 
 
 def _pad(t):
@@ -110,13 +120,14 @@ def rel(a, b):
     return float((a - b).abs().max() / max(float(b.abs().max()), 1e-12))
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", CASES)
 def test_stack_matches_float64_chain(gpu, case, dtype):
     from vq3d import functional as Fn
     from vq3d.flat import FlatParams
     b, c, nbr, h, w, d, n = case
-    dt = torch.float32 if dtype == "fp32" else torch.bfloat16
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    _H[0] = dt if dtype != "fp32" else torch.bfloat16
     stack = _stack(c, nbr, n, seed=h * 10 + d)
     gen = torch.Generator().manual_seed(3)
     x = torch.randn((b, c, h, w, d), generator=gen).to(dt).double()

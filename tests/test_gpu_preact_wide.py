@@ -19,6 +19,17 @@ CASES = [  # (batch, H, W, D, blocks): the published decoder level-1 grid, D hal
     (1, 32, 32, 8, 3), (1, 4, 8, 16, 2), (2, 4, 8, 8, 2), (1, 2, 4, 64, 1)]
 
 
+HALF = [torch.bfloat16, torch.float16]  # the two 16-bit builds of the kernels
+_H = [torch.bfloat16]  # the 16-bit format of the test being run (set per test)
+
+
+@pytest.fixture(autouse=True)
+def _bf16_by_default():
+    """Tests that do not pick a format run bf16 (a parametrized fp16 test must not leak its choice)."""
+    _H[0] = torch.bfloat16
+    yield
+
+
 def _run(gpu, case, seed=0, concurrent=True):
     from vq3d import functional as Fn
     from vq3d import ops
@@ -26,8 +37,8 @@ def _run(gpu, case, seed=0, concurrent=True):
     b, h, w, d, n = case
     stack = _stack(72, 36, n, seed=h * 10 + d + seed)
     gen = torch.Generator().manual_seed(3 + seed)
-    x = torch.randn((b, 72, h, w, d), generator=gen).to(torch.bfloat16).double()
-    gy = torch.randn((b, 72, h, w, d), generator=gen).to(torch.bfloat16).double()
+    x = torch.randn((b, 72, h, w, d), generator=gen).to(_H[0]).double()
+    gy = torch.randn((b, 72, h, w, d), generator=gen).to(_H[0]).double()
     ref = _ref_strict(stack, x, gy)
     m = stack.to(gpu)
     FlatParams(m.parameters(), gpu)
@@ -36,9 +47,9 @@ def _run(gpu, case, seed=0, concurrent=True):
     Fn.PreActWideFn.apply = lambda *a: calls.append(1) or orig(*a)
     ops.set_concurrent_wgrad(concurrent)
     try:
-        xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        xg = x.to(gpu).to(_H[0]).contiguous(memory_format=CL).requires_grad_(True)
         y = m(xg)
-        y.backward(gy.to(gpu).to(torch.bfloat16).contiguous(memory_format=CL))
+        y.backward(gy.to(gpu).to(_H[0]).contiguous(memory_format=CL))
         ops.join_side()
         torch.cuda.synchronize()
     finally:
@@ -49,7 +60,11 @@ def _run(gpu, case, seed=0, concurrent=True):
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_wide_matches_float64_chain(gpu, case):
+@pytest.mark.parametrize("half", HALF)
+def test_wide_matches_float64_chain(gpu, case, half):
+    _H[0] = half
+    import test_gpu_preact_stack as S
+    S._H[0] = half  # _ref_strict's operand rounding
     m, y, xg, (ry, rgx, rgp) = _run(gpu, case)
     errs = {"y": rel(y.float(), ry), "gx": rel(xg.grad.float(), rgx)}
     scal = {}

@@ -70,7 +70,7 @@ def _run(blk, x, gy, dev, tdt, tiny):
         ops.set_tiny_blocks(True)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("shape", SHAPES)
 def test_tiny_block_vs_reference(gpu, shape, dtype):
     from vq3d import ops
@@ -80,9 +80,9 @@ def test_tiny_block_vs_reference(gpu, shape, dtype):
     g = torch.Generator().manual_seed(7)
     x = torch.randn(shape, generator=g)
     gy = torch.randn(shape, generator=g)
-    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
-    if dtype == "bf16":  # compare against the reference on the same rounded inputs
-        x, gy = x.bfloat16().float(), gy.bfloat16().float()
+    tdt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    if dtype != "fp32":  # compare against the reference on the same rounded inputs
+        x, gy = x.to(tdt).float(), gy.to(tdt).float()
     ry, rgx, rgp = _ref(blk, x, gy)
     y, gx, gp = _run(blk, x, gy, gpu, tdt, tiny=True)
     tol = 2e-4 if dtype == "fp32" else 3e-2
