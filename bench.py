@@ -13,10 +13,10 @@ Rank 0 prints ONE JSON line.  Default workload = the BASELINE metric's configura
 
 The line carries:
   roofline       the dominant kernel of the step -- the top kernel of the step's own rocprofv3
-                 kernel-time ranking (profiles/r02_step_top.json, tools/step_profile.py) that has
+                 kernel-time ranking (profiles/rNN_step_top.json of the newest round, tools/step_profile.py) that has
                  a probe below -- launched alone on resident inputs and timed with HIP events on
                  its stream; achieved = algorithmic bytes / average launch time; traffic = PMC HBM
-                 bytes per launch (profiles/r02_pmc_<kernel>.json) when collected
+                 bytes per launch (profiles/rNN_pmc_<kernel>.json, tools/gpu_traffic.sh) when collected
   roofline_top   the same for the top probe-able kernels of the ranking
   step_conv_roofline_frac  the per-layer conv roofline of the whole step (SURVEY.md 8(d):
                  5.55 ms per 3L-pub volume) / the measured step time
@@ -49,9 +49,9 @@ ENC_ROOF_MS = {"3l_pub": 0.42, "3l_dflt": 0.27}  # encoder-only 
 ENC_BYTES = {"3l_pub": 3.39e9, "3l_dflt": 2.19e9}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0  # dense bf16
-STEP_TOP = os.path.join(ROOT, "profiles", "r03_step_top.json")
-if not os.path.exists(STEP_TOP):
-    STEP_TOP = os.path.join(ROOT, "profiles", "r02_step_top.json")
+ROUNDS = ("r04", "r03", "r02")  # newest first: committed profiles of the most recent round win
+STEP_TOP = next((p for p in (os.path.join(ROOT, "profiles", f"{r}_step_top.json") for r in ROUNDS)
+                 if os.path.exists(p)), os.path.join(ROOT, "profiles", "r02_step_top.json"))
 
 
 def parse():
@@ -382,7 +382,7 @@ def timed_launch(dev, launch, iters=20):
 
 def roofline_of(dev, kind, step_entry=None, live_us=None):
     """Roofline of one engine kernel.  Its launch time is taken, in order of preference, from
-    (1) the committed rocprofv3 kernel trace of the bench step (profiles/r03_step_top.json, the
+    (1) the committed rocprofv3 kernel trace of the bench step (profiles/rNN_step_top.json, the
         same tree: tools/gpu_round.sh writes it from this command's step) average,
     (2) `live_us`: HIP events around each of its launches inside one more (eager) training step of
         this run (vq3d.ops.KernelTimer, on the stream the kernel is launched on; the events keep
@@ -402,7 +402,7 @@ def roofline_of(dev, kind, step_entry=None, live_us=None):
         t, src = t_iso, "isolated probe (HIP-graph replay of 20 launches)"
     achieved = algo / t / 1e9
     traffic = None
-    for rnd in ("r03", "r02"):
+    for rnd in ROUNDS:
         pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{kind}.json")
         if os.path.exists(pmc):
             try:

@@ -18,7 +18,7 @@ def per_dispatch(d, kernel, counter):
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     vals = {}
     for r in csv.DictReader(open(path)):
-        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if kernel in r["Kernel_Name"].replace(", ", "_") and r["Counter_Name"] == counter:
             k = int(r["Dispatch_Id"])
             vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
     v = [vals[k] for k in sorted(vals)]
