@@ -18,6 +18,74 @@ from .parallel import grads_ready, sum_allreduce
 CL = torch.channels_last_3d
 
 
+_BINDING = ["ctypes"]
+
+
+def set_binding(name):
+    """How the model's layers reach the kernels: "ctypes" (default) -- the autograd Functions below
+    call the C-ABI; "library" -- through the registered `torch.ops.vq3d.*` operators (vq3d.library),
+    which run the same Function bodies, so the two give bit-identical steps."""
+    if name not in ("ctypes", "library"):
+        raise ValueError(f"binding must be 'ctypes' or 'library', not {name!r}")
+    if name == "library":
+        from . import library  # noqa: F401  (registers the operators)
+    _BINDING[0] = name
+
+
+def binding():
+    return _BINDING[0]
+
+
+def _library():
+    if _BINDING[0] != "library":
+        return None
+    from . import library
+    return library
+
+
+def preact_block(x, blk):
+    lb = _library()
+    if lb is not None:
+        return lb.block(x, blk)
+    return PreActBlockFn.apply(x, blk, *param_edges(blk._fn_params, x))
+
+
+def preact_run(fn, x, plan):
+    lb = _library()
+    if lb is not None:
+        return lb.run(fn, x, plan)
+    return fn.apply(x, plan, *param_edges(plan.params, x))
+
+
+def upsample(x):
+    lb = _library()
+    if lb is not None:
+        return torch.ops.vq3d.upsample2x(x)
+    return UpsampleFn.apply(x)
+
+
+def parse_input(x, w, b, half):
+    lb = _library()
+    if lb is not None:
+        return torch.ops.vq3d.parse_input(x, w, b, half)[0]
+    return ParseInputFn.apply(x, w, b, half)
+
+
+def quantize(z, q):
+    lb = _library()
+    if lb is not None:
+        return lb.quantize(z, q)
+    return QuantizeFn.apply(z, q)
+
+
+def recon_loss(dec, x, nvs, cylinder, *commit):
+    lb = _library()
+    if lb is not None:
+        total, recon = torch.ops.vq3d.recon_loss(dec, x, nvs, bool(cylinder), list(commit))[:2]
+        return total, recon
+    return ReconLossFn.apply(dec, x, nvs, cylinder, *commit)
+
+
 def param_edges(params, *acts):
     """The parameters as autograd inputs of a Function only when no activation input already ties
     it into the graph.  The kernels accumulate parameter gradients straight into the flat buffer
@@ -458,6 +526,9 @@ class ConvSpec:
 
 
 def conv(x, spec, x2=None, residual=None):
+    lb = _library()
+    if lb is not None:
+        return lb.conv(x, spec, x2, residual)
     return ConvFn.apply(x, x2, residual, spec, *param_edges(spec.tensors, x, x2, residual))
 
 
@@ -554,6 +625,76 @@ class EvoNormFn(torch.autograd.Function):
 
 
 # ============================================================================================ quantizer
+def vq_init(z, q):
+    """_init_ema (layers.py:665-683) on the first training pass: mean / unbiased std of this rank's
+    rows, summed over the ranks in one all-reduce (C3) and divided by the world size in the init
+    kernel."""
+    b, d, h, w, dz = z.shape
+    n = b * h * w * dz
+    k = q.num_embeddings
+    dev = z.device
+    st = L.stream()
+    ws = ops.workspace(L.query("vq3d_vq_workspace_size", n, d, k), dev)
+    ms = torch.empty(2 * d, dtype=torch.float32, device=dev)
+    mean, std = ms[:d], ms[d:]
+    L.call("vq3d_vq_moments", L.dtype_code(z), L.ptr(z), n, d, L.ptr(mean), L.ptr(std), L.ptr(ws), st)
+    world = sum_allreduce(ms)
+    n_tot = float(n) * world
+    L.call("vq3d_vq_init_apply", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size),
+           L.ptr(q.first_pass), L.ptr(mean), L.ptr(std), k, d, 1.0 / world, n_tot, st)
+    q.first_pass_host = False
+
+
+def vq_search(z, embed, commitment_cost, zst_dtype=None):
+    """The codebook search (exact torch-CPU cdist arithmetic), the straight-through output (in
+    zst_dtype: the model's conv operand storage, its consumers are convs / the decoder's runs) and
+    the commitment loss: returns loss, zst, idx."""
+    b, d, h, w, dz = z.shape
+    n = b * h * w * dz
+    k = embed.shape[0]
+    dev = z.device
+    st = L.stream()
+    ws = ops.workspace(L.query("vq3d_vq_workspace_size", n, d, k), dev)
+    idx = torch.empty((b, h, w, dz), dtype=torch.int64, device=dev)
+    zst = torch.empty_like(z, dtype=zst_dtype or z.dtype)
+    sq = torch.empty((), dtype=torch.float32, device=dev)
+    L.call("vq3d_vq_nearest", L.dtype_code(z), L.ptr(z), n, d, L.ptr(embed), k, L.ptr(idx), L.dtype_code(zst),
+           L.ptr(zst), L.ptr(sq), L.ptr(ws), st)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    L.call("vq3d_vq_commit_loss", L.ptr(sq), commitment_cost / float(n * d), L.ptr(loss), st)
+    return loss, zst, idx
+
+
+def vq_ema(z, idx, q):
+    """_update_ema (layers.py:636-663).  Inside Encoder2 the statistics land in the encoder's fused
+    buffer (q.ema_slot) and the update waits for its single all-reduce."""
+    b, d, h, w, dz = z.shape
+    n = b * h * w * dz
+    k = q.num_embeddings
+    ws = ops.workspace(L.query("vq3d_vq_workspace_size", n, d, k), z.device)
+    slot = q.ema_slot
+    stats = torch.empty(k * (d + 1), dtype=torch.float32, device=z.device) if slot is None else slot
+    counts, dw = stats[:k], stats[k:]
+    L.call("vq3d_vq_ema_stats", L.dtype_code(z), L.ptr(z), n, d, L.ptr(idx), k, L.ptr(counts), L.ptr(dw), L.ptr(ws),
+           L.stream())
+    if slot is None:
+        sum_allreduce(stats)
+        ema_update(q, stats)
+
+
+def vq_backward(z, embed, idx, coef, g_loss, g_zst):
+    """Straight-through gradient plus the commitment term 2 cc (z - e_idx) / (n d) (layers.py:713-728)."""
+    b, d, h, w, dz = z.shape
+    n = b * h * w * dz
+    if g_zst is None:
+        g_zst = ops.zero_(torch.empty_like(z))
+    g_zst = _cl(g_zst)
+    gz = torch.empty_like(z)
+    L.call("vq3d_vq_bwd", L.dtype_code(z), L.ptr(z), n, d, L.ptr(embed), L.ptr(idx), L.dtype_code(g_zst),
+           L.ptr(g_zst), None if g_loss is None else L.ptr(g_loss), coef, L.ptr(gz), L.stream())
+    return gz
+
+
 class QuantizeFn(torch.autograd.Function):
     """Quantizer.forward (layers.py:685-728): fp32 codebook search (exact torch-CPU cdist
     arithmetic), EMA update in train mode, commitment loss, straight-through output."""
@@ -562,47 +703,16 @@ class QuantizeFn(torch.autograd.Function):
     def forward(ctx, z, q):
         z = ops.as_cl(z)
         b, d, h, w, dz = z.shape
-        n = b * h * w * dz
-        k = q.num_embeddings
-        dev = z.device
-        st = L.stream()
-        ws = ops.workspace(L.query("vq3d_vq_workspace_size", n, d, k), dev)
-        zc = L.dtype_code(z)
         if q.training and q.first_pass_host:
-            # _init_ema (layers.py:665-683): mean / unbiased std of this rank's rows, summed over
-            # the ranks in one all-reduce (C3) and divided by the world size in the init kernel
-            ms = torch.empty(2 * d, dtype=torch.float32, device=dev)
-            mean, std = ms[:d], ms[d:]
-            L.call("vq3d_vq_moments", zc, L.ptr(z), n, d, L.ptr(mean), L.ptr(std), L.ptr(ws), st)
-            world = sum_allreduce(ms)
-            n_tot = float(n) * world
-            L.call("vq3d_vq_init_apply", L.ptr(q.embed), L.ptr(q.embed_avg), L.ptr(q.cluster_size),
-                   L.ptr(q.first_pass), L.ptr(mean), L.ptr(std), k, d, 1.0 / world, n_tot, st)
-            q.first_pass_host = False
+            vq_init(z, q)
         embed = q.embed
         if q.training:
-            embed = ops.copy_(torch.empty_like(q.embed), q.embed)  # pre-update codebook for q / backward
-        idx = torch.empty((b, h, w, dz), dtype=torch.int64, device=dev)
-        # z arrives fp32 from an fp32-stream run; the straight-through output goes on in the model's
-        # conv operand storage (its consumers are convs / the decoder's runs)
-        zst = torch.empty_like(z, dtype=getattr(q, "zst_dtype", None) or z.dtype)
-        sq = torch.empty((), dtype=torch.float32, device=dev)
-        L.call("vq3d_vq_nearest", zc, L.ptr(z), n, d, L.ptr(embed), k, L.ptr(idx), L.dtype_code(zst), L.ptr(zst),
-               L.ptr(sq), L.ptr(ws), st)
-        loss = torch.empty((), dtype=torch.float32, device=dev)
-        L.call("vq3d_vq_commit_loss", L.ptr(sq), q.commitment_cost / float(n * d), L.ptr(loss), st)
+            # the pre-update codebook for q / backward (the updated one is first read by the NEXT step)
+            embed = ops.copy_(torch.empty_like(q.embed), q.embed)
+        loss, zst, idx = vq_search(z, embed, q.commitment_cost, getattr(q, "zst_dtype", None))
         if q.training:
-            # _update_ema (layers.py:636-663).  Inside Encoder2 the statistics land in the
-            # encoder's fused buffer and the update waits for its single all-reduce (the updated
-            # codebook is first read by the NEXT step: q and backward use the copy above)
-            slot = q.ema_slot
-            stats = torch.empty(k * (d + 1), dtype=torch.float32, device=dev) if slot is None else slot
-            counts, dw = stats[:k], stats[k:]
-            L.call("vq3d_vq_ema_stats", zc, L.ptr(z), n, d, L.ptr(idx), k, L.ptr(counts), L.ptr(dw), L.ptr(ws), st)
-            if slot is None:
-                sum_allreduce(stats)
-                ema_update(q, stats)
-        ctx.coef = 2.0 * q.commitment_cost / float(n * d)
+            vq_ema(z, idx, q)
+        ctx.coef = 2.0 * q.commitment_cost / float(b * h * w * dz * d)
         ctx.save_for_backward(z, embed, idx)
         ctx.mark_non_differentiable(idx)
         return loss, zst, idx
@@ -610,15 +720,7 @@ class QuantizeFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_zst, g_idx):
         z, embed, idx = ctx.saved_tensors
-        b, d, h, w, dz = z.shape
-        n = b * h * w * dz
-        if g_zst is None:
-            g_zst = ops.zero_(torch.empty_like(z))
-        g_zst = _cl(g_zst)
-        gz = torch.empty_like(z)
-        L.call("vq3d_vq_bwd", L.dtype_code(z), L.ptr(z), n, d, L.ptr(embed), L.ptr(idx), L.dtype_code(g_zst),
-               L.ptr(g_zst), None if g_loss is None else L.ptr(g_loss), ctx.coef, L.ptr(gz), L.stream())
-        return gz, None
+        return vq_backward(z, embed, idx, ctx.coef, g_loss, g_zst), None
 
 
 def ema_update(q, stats):

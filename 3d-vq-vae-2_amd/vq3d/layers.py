@@ -47,7 +47,7 @@ class ResizeConv3D(Conv3d):
 
     def forward(self, x, x2=None):
         assert x2 is None
-        return Fn.conv(Fn.UpsampleFn.apply(x), self._spec())
+        return Fn.conv(Fn.upsample(x), self._spec())
 
 
 def _mode_conv(mode):
@@ -106,7 +106,7 @@ class PreActFixupResBlock(nn.Module):
         super().__setattr__(name, value)
 
     def forward(self, input: torch.Tensor):
-        return Fn.PreActBlockFn.apply(input, self, *Fn.param_edges(self._fn_params, input))
+        return Fn.preact_block(input, self)
 
     @torch.no_grad()
     def initialize_weights(self, num_layers):
@@ -154,7 +154,7 @@ class FixupResBlock(nn.Module):
             self._build_specs()
         s1, s2, sk = self._specs
         # up mode: upsample(x + b1a) == upsample(x) + b1a (trilinear weights sum to 1)
-        x = Fn.UpsampleFn.apply(input) if self.mode == 'up' else input
+        x = Fn.upsample(input) if self.mode == 'up' else input
         h = Fn.conv(x, s1)
         skip = Fn.conv(x, sk)
         return Fn.conv(h, s2, residual=skip)
@@ -212,12 +212,12 @@ class EvonormResBlock(nn.Module):
         out = Fn.conv(self.evonorm_1(input), s1)
         t = self.evonorm_2(out)
         if up:
-            t = Fn.UpsampleFn.apply(t)
+            t = Fn.upsample(t)
         out = Fn.conv(t, s2)
         if sk is None:
             res = input
         else:
-            res = Fn.conv(Fn.UpsampleFn.apply(input) if up else input, sk)
+            res = Fn.conv(Fn.upsample(input) if up else input, sk)
         return Fn.conv(self.evonorm_3(out), s3, residual=res)
 
     @torch.no_grad()
@@ -274,7 +274,7 @@ class BlockStack(nn.Sequential):
                 # the stack's last run hands an fp32 stream on when the consumer takes it
                 plan.out_dtype = torch.float32 if (self.out_fp32 and j == len(mods) - 1 and
                                                    fn is Fn.PreActSmallRunFn and ops.fp32_stream()) else None
-                x = fn.apply(x, plan, *Fn.param_edges(plan.params, x))
+                x = Fn.preact_run(fn, x, plan)
                 i = j + 1
             else:
                 x = mods[i](x)
@@ -377,7 +377,7 @@ class Encoder2(nn.Module):
     def forward(self, data):
         if Fn.parse_input_fused(data, self.parse_input, self.compute_dtype):
             # the fp32 volume straight into the 16-bit activation (never rounded to bf16 itself)
-            down = Fn.ParseInputFn.apply(data, self.parse_input.weight, self.parse_input.bias, self.compute_dtype)
+            down = Fn.parse_input(data, self.parse_input.weight, self.parse_input.bias, self.compute_dtype)
         else:
             if data.dtype != self.compute_dtype:
                 data = ops.cast(data, self.compute_dtype)
@@ -490,5 +490,5 @@ class Quantizer(nn.Module):
         return self.embed[embed_idx]
 
     def forward(self, inputs):
-        loss, zst, idx = Fn.QuantizeFn.apply(inputs, self)
+        loss, zst, idx = Fn.quantize(inputs, self)
         return loss, zst, idx

@@ -139,7 +139,7 @@ class VQVAE(nn.Module):
         if not torch.is_tensor(num_valid_slices):
             num_valid_slices = torch.as_tensor(num_valid_slices)
         nvs = num_valid_slices.to(device=x.device, dtype=torch.int64)
-        loss, recon = Fn.ReconLossFn.apply(loc, x, nvs, bool(self.pre_loss_f), *commitment_loss)
+        loss, recon = Fn.recon_loss(loc, x, nvs, bool(self.pre_loss_f), *commitment_loss)
         log_dict = {'recon_loss_mean': recon}
         log_dict.update({f'commitment_loss_{i}': c for i, c in enumerate(commitment_loss)})
         self.log('recon loss', recon, prog_bar=True, logger=False)

@@ -78,6 +78,9 @@ def parse():
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
     p.add_argument("--no-dist-graph", action="store_true", help="N > 1: never capture the collectives")
+    p.add_argument("--binding", default="ctypes", choices=["ctypes", "library"],
+                   help="library: the layers call the registered torch.ops.vq3d.* operators (vq3d.library) "
+                        "instead of the ctypes autograd Functions (same kernels)")
     return p.parse_args()
 
 
@@ -676,6 +679,9 @@ def main():
     ops.set_concurrent_wgrad(a.concurrent_wgrad and not a.serial_wgrad)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
+    if a.binding != "ctypes":
+        from vq3d import functional as Fn
+        Fn.set_binding(a.binding)
     if a.encode_only:
         batch = 1
     # this rank's synthetic volumes, resident in HBM before timing
@@ -774,6 +780,7 @@ def main():
         "dtype": a.dtype,
         "data": "synthetic (torch.rand*4.5-0.5 volumes, reference init weights, seed 0)",
         "launch": "hip_graph" if graph is not None else "eager",
+        "binding": a.binding,
         "config": {"workload": workload, "volume": list(size), "batch_per_gpu": batch, "global_batch": batch * world,
                    "parallelism": f"dp{world}" if not a.encode_only else f"replicas{world}"},
     }

@@ -120,3 +120,14 @@ def test_argparse_defaults_mirror_reference():
     m = vq3d.VQVAE(vq3d.default_args(n_bottleneck_blocks=2))
     assert sum(p.numel() for p in m.parameters()) == 166281
     assert m.num_layers == 2 + 2 * 4 + 1
+
+
+def test_library_operators_registered():
+    """vq3d.library registers every hot-path operator with a typed schema (no GPU needed)."""
+    import torch
+
+    from vq3d import library as lb
+    for name in lb.OPS:
+        schema = str(getattr(torch.ops.vq3d, name).default._schema)
+        assert schema.startswith(f"vq3d::{name}("), schema
+    assert "Tensor(a" in str(torch.ops.vq3d.conv3d_backward.default._schema)  # gradient buffers are mutated

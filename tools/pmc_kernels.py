@@ -16,7 +16,7 @@ names = {}
 for path in sorted(glob.glob(pat)):
     for f in glob.glob(f"{path}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if sub not in r["Kernel_Name"]:
+            if sub not in r["Kernel_Name"].replace(", ", "_"):
                 continue
             k = re.sub(r"\(.*$", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))[:60]
             key = (f, r["Dispatch_Id"])
