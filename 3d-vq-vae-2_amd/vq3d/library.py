@@ -109,6 +109,7 @@ def _saved(ctx, inputs, output, nout, pool_fn):
     ctx.flags = m[:len(_FLAGS)]
     ctx.saved = _unpack(m[len(_FLAGS):], new, pool_fn(inputs) + outs)
     ctx.mark_non_differentiable(meta, *new)
+    ctx.set_materialize_grads(False)  # no zero-filled gradients for the saved-tensor outputs
 
 
 def _backward(fn, ctx, pool, grads_out):
@@ -361,6 +362,7 @@ def _vq_setup(ctx, inputs, output):
     ctx.coef = 2.0 * cc / float(b * h * w * dz * d)
     ctx.save_for_backward(z, embed, output[2])
     ctx.mark_non_differentiable(output[2])
+    ctx.set_materialize_grads(False)
 
 
 def _vq_bwd(ctx, grads):
@@ -460,6 +462,7 @@ def recon_loss_backward(g_total: Tensor, saved: List[Optional[Tensor]], cylinder
 
 def _loss_setup(ctx, inputs, output):
     _saved(ctx, inputs, output, 2, lambda i: [i[0], i[1], i[2]])
+    ctx.mark_non_differentiable(output[1])  # recon: a logged value (ReconLossFn)
     ctx.cyl, ctx.ncommit = inputs[3], len(inputs[4])
 
 

@@ -1,6 +1,6 @@
 """The torch.library binding (vq3d.library, SURVEY.md 8(b) "Binding"): training steps of a 2-layer
-and of the published 3-layer model through `torch.ops.vq3d.*` equal the ctypes path's bit for bit --
-loss, codes, every parameter gradient, and after the Adam step every parameter and codebook / EMA
+and of the published 3-layer model through `torch.ops.vq3d.*` against the ctypes path -- loss,
+codes, every parameter gradient, and after the Adam step every parameter and codebook / EMA
 buffer.  Two steps each: the first runs the Quantizers' first-pass init (vq3d::vq_init), the second
 the EMA path on initialised codebooks.  The 3-layer model at 128 x 128 x 64 exercises every fused
 run engine (stack, wide, mid, small / column) through vq3d::preact_run and the single blocks / convs
@@ -61,25 +61,56 @@ def _steps(gpu, binding, cfg, size, nsteps=2):
         Fn.set_binding("ctypes")
 
 
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+def _diff(ra, rb):
+    """{name: relative max-abs difference} of the tensors of two step records that are not bitwise
+    equal (loss and codes compare exactly: inf when they differ)"""
+    out = {}
+    for step, (x, y) in enumerate(zip(ra, rb)):
+        if x[0] != y[0]:
+            out[(step, "loss")] = float("inf")
+        for i, (p, q) in enumerate(zip(x[1], y[1])):
+            if not torch.equal(p, q):
+                out[(step, "codes", i)] = float("inf")
+        for k in (2, 3):
+            for n in x[k]:
+                if not torch.equal(x[k][n], y[k][n]):
+                    out[(step, "grad" if k == 2 else "state", n)] = _rel(y[k][n], x[k][n])
+    return out
+
+
 @pytest.mark.parametrize("name", sorted(CFGS))
-def test_library_step_bit_identical(gpu, name):
+def test_library_step_matches_ctypes(gpu, name):
+    """The ctypes path is not bitwise reproducible itself: the per-conv backward of the up / down
+    blocks (and the few unfused convs) reduce bias / prologue / k^3 weight gradients with fp32
+    atomics, so two ctypes runs differ in those sums' last bits (measured: 186 of the 2-layer
+    model's step tensors, 902 of the 3-layer's, all gradients or their Adam updates).  So: the
+    forward (loss, codes) bit for bit on both steps, and every tensor either bitwise equal or
+    within the ctypes path's own run-to-run spread (4x its largest relative difference, >= 1e-5)."""
     import vq3d.library  # noqa: F401
     cfg, size = CFGS[name]
     a = _steps(gpu, "ctypes", cfg, size)
+    a2 = _steps(gpu, "ctypes", cfg, size)
     b = _steps(gpu, "library", cfg, size)
-    for step, (ra, rb) in enumerate(zip(a, b)):
-        assert ra[0] == rb[0], (step, ra[0], rb[0])
-        for ia, ib in zip(ra[1], rb[1]):
-            assert torch.equal(ia, ib), step
-        for n in ra[2]:
-            assert torch.equal(ra[2][n], rb[2][n]), (step, "grad", n)
-        for n in ra[3]:
-            assert torch.equal(ra[3][n], rb[3][n]), (step, "state", n)
-    print(name, "losses", [r[0] for r in a])
+    noise = _diff(a, a2)
+    d = _diff(a, b)
+    spread = max([v for v in noise.values()] + [0.0])
+    tol = max(4 * spread, 1e-5)
+    worst = max(d.items(), key=lambda kv: kv[1]) if d else None
+    print(f"{name}: losses {[r[0] for r in a]}; ctypes run-to-run: {len(noise)} tensors differ, largest rel "
+          f"{spread:.2e}; library vs ctypes: {len(d)} differ, worst {worst}")
+    assert all(v != float("inf") for v in noise.values()), "ctypes forward not reproducible"
+    assert all(v <= tol for v in d.values()), worst
 
 
 def test_library_ops_are_the_kernels(gpu):
-    """A conv through torch.ops.vq3d.conv3d (+ its autograd backward) equals vq3d.functional.conv."""
+    """A circular 3x3x3 conv through torch.ops.vq3d.conv3d (+ its autograd backward) against
+    vq3d.functional.conv: output and input gradient bit for bit; the weight / bias gradients
+    (fp32 atomics, see above) within 1e-5."""
     from vq3d import functional as Fn
     from vq3d import library as lb
     from vq3d.flat import FlatParams
@@ -98,5 +129,7 @@ def test_library_ops_are_the_kernels(gpu):
         y.float().square().sum().backward()
         torch.cuda.synchronize()
         out.append((y.detach().clone(), xa.grad.clone(), conv.weight.grad.clone(), conv.bias.grad.clone()))
-    for ta, tb in zip(*out):
-        assert torch.equal(ta, tb)
+    (ya, gxa, gwa, gba), (yb, gxb, gwb, gbb) = out
+    assert torch.equal(ya, yb)
+    assert torch.equal(gxa, gxb)
+    assert _rel(gwb, gwa) <= 1e-5 and _rel(gbb, gba) <= 1e-5, (_rel(gwb, gwa), _rel(gbb, gba))
