@@ -33,6 +33,8 @@
 // next position and meet zero weights.
 #include "engines.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 // Timing experiments only (tools builds: make -C 3d-vq-vae-2_amd exp EXP=N): bit 0 skips the
@@ -1062,31 +1064,53 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
 // circular (TH + 2) x (TW + 2) halo (positions -1 .. D of each line), and wave kk (9 waves) owns
 // tap row kk = (kh, kw): its 2 accumulators (co x the 27 (kd, ci) window entries) sum over the
 // workgroup's npc chunks, the next chunk's loads in flight during the current one's MFMAs.
-// Chunks of one workgroup are consecutive and each XCD takes a contiguous eighth of them (the
-// halo re-reads hit that XCD's L2).
+// Staging unit: an item = 8 consecutive voxels of a line x 9 channels (144 contiguous bytes).  The
+// global loads are coalesced 16-B pieces (consecutive lanes, consecutive pieces) written as they
+// come to a voxel-major LDS area; then each thread takes one item (nine conflict-free 16-B reads:
+// the 144-B item stride walks all 16 bank slots), transposes it in registers (one v_perm_b32 per
+// output dword) and writes 9 channel rows of 8 voxels (16-B stores; 2 x 8 B for t2).  The t2 rows hold position
+// p at index p + 8 so every group lands aligned (position -1 at 7, D at D + 8: the circular
+// wrap copies).  Chunks of one workgroup are consecutive and each XCD takes a contiguous eighth of
+// them (the halo re-reads hit that XCD's L2).
 constexpr int NT9 = 9 * 64;
+#ifndef W2_PAD
+#define W2_PAD 4  // t2 channel-stride padding (elements, even); timing experiments: make exp EXPDEF=W2_PAD
+#endif
 template <int D>
 struct W2c {
     static constexpr int NL = CHV / D;  // lines per chunk
     static constexpr int TH = NL >= 64 ? 8 : NL >= 16 ? 4 : NL >= 4 ? 2 : 1, TW = NL / TH;
     static constexpr int LW = TW + 2, HL = (TH + 2) * LW;  // halo lines
-    static constexpr int RPD = D + 2;                       // positions -1 .. D
-    static constexpr int CSTR = HL * RPD + 8;               // per channel (read8 reads one dword past)
-    static constexpr int QL = D * BR / 8;                   // 16-B pieces of one 9-channel line
-    static constexpr int ZQ = NL * QL, TQ = HL * QL;
-    static constexpr int PZ = (ZQ + NT9 - 1) / NT9, PT = (TQ + NT9 - 1) / NT9;
-    static constexpr size_t LDS = size_t(16 * ZP + BR * CSTR) * 2;
-    static_assert(NL * D == CHV && TH * TW == NL, "chunk");
+    static constexpr int GPL = D / 8;                       // 8-voxel groups per line
+    static constexpr int RP = D + 16;                       // t2 row: position p at index p + 8
+    // per channel: + 4 elements (8 B) so the 9 channel rows of one B-operand read spread over the
+    // banks (2-way at most; a 16-B multiple stride puts them 3- to 9-way on one bank)
+    static constexpr int CSTR = HL * RP + W2_PAD;
+    static constexpr int ZI = NL * GPL, TI = HL * GPL;      // staging items (gz3, t2)
+    static constexpr int NPC = (ZI + TI) * 9;               // 16-B pieces per chunk
+    static constexpr int NP = (NPC + NT9 - 1) / NT9;        // pieces per thread
+    static constexpr int TSZ = (BR * CSTR + 7) & ~7;        // t2 rows, rounded to 16 B (the raw area's b128s)
+    static constexpr int RAW = (ZI + TI) * 72;              // voxel-major staging area (elements)
+    static constexpr size_t LDS = size_t(16 * ZP + TSZ + RAW) * 2;
+    static_assert(NL * D == CHV && TH * TW == NL && D % 8 == 0, "chunk");
+    static_assert(ZI + TI <= NT9, "one staging item per thread");
 };
 
-__device__ __forceinline__ void scatter9(h16_t *dst, int pitch, int e0, u32x4 q, int base) {
-    // the 8 elements e0 .. e0 + 7 of a 9-channel voxel-major run to dst[c * pitch + base + pos]
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+// element e (0..71) of a staged 8-voxel x 9-channel item (voxel-major, 16-bit)
+__device__ __forceinline__ uint32_t item_el(const uint32_t (&w)[36], int e) {
+    return (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+}
+// channel c of the item's 8 voxels as 4 dwords (voxels 2k, 2k + 1 in dword k): one byte permute each
+__device__ __forceinline__ u32x4 item_row(const uint32_t (&w)[36], int c) {
+    uint32_t o[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int e = e0 + j, pos = e / BR, c = e - pos * BR;
-        dst[c * pitch + base + pos] = h16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+    for (int k = 0; k < 4; ++k) {
+        const int ea = 18 * k + c, eb = ea + 9;
+        // v_perm_b32: selector values 0-3 pick bytes of the second source, 4-7 of the first
+        const uint32_t sel = (ea & 1 ? 0x0302u : 0x0100u) | ((eb & 1 ? 0x0706u : 0x0504u) << 16);
+        o[k] = __builtin_amdgcn_perm(w[eb >> 1], w[ea >> 1], sel);
     }
+    return u32x4{o[0], o[1], o[2], o[3]};
 }
 
 template <int D>
@@ -1095,7 +1119,8 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
     using K = W2c<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     h16_t *zT = reinterpret_cast<h16_t *>(smem);  // gz3 [16][ZP] channel-major (rows >= 9 never read into results)
-    h16_t *tT = zT + 16 * ZP;                      // t2 [9][HL][RPD] (+ tail)
+    h16_t *tT = zT + 16 * ZP;                      // t2 [9][HL][RP]
+    h16_t *raw = tT + K::TSZ;                      // [items][72] voxel-major (16-B aligned)
     const int tid = threadIdx.x, lane = tid & 63, kk = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int kh = kk / 3, kw = kk - 3 * kh;
     const int nth = a.H / K::TH, ntw = a.W / K::TW;
@@ -1104,59 +1129,86 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
     const int bid = blockIdx.x;
     const int slot = (nwg & 7) ? bid : (bid & 7) * (nwg >> 3) + (bid >> 3);
     const int c0 = slot * npc;
-    for (int i = tid; i < BR * 8; i += NT9) tT[(i >> 3) * K::CSTR + K::HL * K::RPD + (i & 7)] = 0;
     int toff[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
         const int e = min(16 * n + row, 26), kd = e / BR, ci = e - kd * BR;
         toff[n] = ci * K::CSTR + kd;
     }
-    u32x4 vz[K::PZ], vt[K::PT];
+    u32x4 v[K::NP];
     auto load = [&](int c) {
         const int tw_i = c % ntw, r = c / ntw, th_i = r % nth, b = r / nth;
         const int h0 = th_i * K::TH, w0 = tw_i * K::TW;
 #pragma unroll
-        for (int u = 0; u < K::PZ; ++u) {
-            const int i = min(tid + u * NT9, K::ZQ - 1), l = i / K::QL, part = i - l * K::QL;
-            const int64_t lv = ((int64_t(b) * a.H + h0 + l / K::TW) * a.W + w0 + l % K::TW) * D;
-            vz[u] = reinterpret_cast<const u32x4 *>(gz3 + lv * BR)[part];
-        }
-#pragma unroll
-        for (int u = 0; u < K::PT; ++u) {
-            const int i = min(tid + u * NT9, K::TQ - 1), hl = i / K::QL, part = i - hl * K::QL;
-            const int lh = hl / K::LW, lw = hl - lh * K::LW;
-            const int64_t lv = ((int64_t(b) * a.H + wrapm(h0 - 1 + lh, a.H)) * a.W + wrapm(w0 - 1 + lw, a.W)) * D;
-            vt[u] = reinterpret_cast<const u32x4 *>(t2 + lv * BR)[part];
+        for (int u = 0; u < K::NP; ++u) {
+            const int p = min(tid + u * NT9, K::NPC - 1), item = p / 9, j = p - item * 9;
+            const bool z = item < K::ZI;
+            const int it = z ? item : item - K::ZI, il = it / K::GPL, ig = it - il * K::GPL;
+            int hh, ww;
+            if (z) {
+                hh = h0 + il / K::TW;
+                ww = w0 + il % K::TW;
+            } else {
+                const int lh = il / K::LW, lw = il - lh * K::LW;
+                hh = wrapm(h0 - 1 + lh, a.H);
+                ww = wrapm(w0 - 1 + lw, a.W);
+            }
+            const h16_t *src = (z ? gz3 : t2) + (((int64_t(b) * a.H + hh) * a.W + ww) * D + 8 * ig) * BR;
+            v[u] = reinterpret_cast<const u32x4 *>(src)[j];
         }
     };
+    // this thread's staging item (transpose phase): gz3 line il (tid < ZI) or t2 halo line il, group ig
+    const bool zitem = tid < K::ZI, titem = !zitem && tid < K::ZI + K::TI;
+    const int it = zitem ? tid : min(tid - K::ZI, K::TI - 1);
+    const int il = it / K::GPL, ig = it - il * K::GPL;
+    h16_t *dst = zitem ? zT + il * D + 8 * ig : tT + il * K::RP + 8 + 8 * ig;
+    const int pitch = zitem ? ZP : K::CSTR;
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int cend = min(c0 + npc, nchunk);
     if (c0 < cend) load(c0);
 #pragma unroll 1
     for (int c = c0; c < cend; ++c) {
-        __syncthreads();  // the previous chunk's fragments are read
 #pragma unroll
-        for (int u = 0; u < K::PZ; ++u) {
-            const int i = tid + u * NT9;
-            if (i < K::ZQ) {
-                const int l = i / K::QL, part = i - l * K::QL;
-                scatter9(zT, ZP, part * 8, vz[u], l * D);
-            }
+        for (int u = 0; u < K::NP; ++u) {  // raw pieces (the area's previous readers passed the last barrier)
+            const int p = tid + u * NT9;
+            if (p < K::NPC) reinterpret_cast<u32x4 *>(raw)[p] = v[u];
         }
+        __syncthreads();  // raw complete; the previous chunk's fragments are read
+        if (zitem || titem) {
+            uint32_t w[36];
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(raw) + (zitem ? tid : K::ZI + it) * 9;
 #pragma unroll
-        for (int u = 0; u < K::PT; ++u) {
-            const int i = tid + u * NT9;
-            if (i < K::TQ) {
-                const int hl = i / K::QL, part = i - hl * K::QL;
-                const uint32_t w[4] = {vt[u].x, vt[u].y, vt[u].z, vt[u].w};
-                h16_t *ln = tT + hl * K::RPD;
+            for (int j = 0; j < 9; ++j) {
+                const u32x4 q = src[j];
+                w[4 * j] = q.x;
+                w[4 * j + 1] = q.y;
+                w[4 * j + 2] = q.z;
+                w[4 * j + 3] = q.w;
+            }
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int e = part * 8 + j, pos = e / BR, ci = e - pos * BR;
-                    const h16_t v = h16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
-                    ln[ci * K::CSTR + pos + 1] = v;
-                    if (pos == 0) ln[ci * K::CSTR + D + 1] = v;  // position D wraps to 0
-                    if (pos == D - 1) ln[ci * K::CSTR] = v;      // position -1 wraps to D - 1
+            for (int ch = 0; ch < BR; ++ch) {
+                const u32x4 r = item_row(w, ch);
+                if (zitem || W2_PAD % 8 == 0) {
+                    *reinterpret_cast<u32x4 *>(dst + ch * pitch) = r;
+                } else if (W2_PAD % 4 == 0) {  // t2 rows 8-B aligned
+                    reinterpret_cast<u32x2 *>(dst + ch * pitch)[0] = u32x2{r.x, r.y};
+                    reinterpret_cast<u32x2 *>(dst + ch * pitch)[1] = u32x2{r.z, r.w};
+                } else {  // 4-B aligned
+                    uint32_t *q = reinterpret_cast<uint32_t *>(dst + ch * pitch);
+                    q[0] = r.x;
+                    q[1] = r.y;
+                    q[2] = r.z;
+                    q[3] = r.w;
+                }
+            }
+            if (titem) {  // circular wrap copies: position -1 = D - 1, position D = 0
+                if (ig == K::GPL - 1) {
+#pragma unroll
+                    for (int ch = 0; ch < BR; ++ch) dst[ch * pitch - 1 - 8 * ig] = h16_t(item_el(w, 63 + ch));  // index 7
+                }
+                if (ig == 0) {
+#pragma unroll
+                    for (int ch = 0; ch < BR; ++ch) dst[ch * pitch + D] = h16_t(item_el(w, ch));  // index D + 8
                 }
             }
         }
@@ -1164,21 +1216,21 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
         if (c + 1 < cend) load(c + 1);
 #pragma unroll 4
         for (int ks = 0; ks < CHV / 32; ++ks) {
-            const int v = 32 * ks + 8 * kb, l = v / D, d0 = v - l * D;
+            const int vv = 32 * ks + 8 * kb, l = vv / D, d0 = vv - l * D;
             const int hl = (l / K::TW + kh) * K::LW + l % K::TW + kw;
-            const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + v);
-            const int off = hl * K::RPD + d0;
+            const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + vv);
+            const int off = hl * K::RP + d0 + 7;  // position d0 - 1 + kd at index d0 + 7 + kd
 #pragma unroll
             for (int n = 0; n < 2; ++n) acc[n] = mfma(af, read8(tT, toff[n] + off), acc[n]);
         }
     }
-    float *dst = p2a + (int64_t(bid) * 9 + kk) * NER;
+    float *dstp = p2a + (int64_t(bid) * 9 + kk) * NER;
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int co = 4 * kb + j, col = 16 * n + row;
-            if (co < BR && col < 27) dst[co * 27 + col] = acc[n][j];
+            if (co < BR && col < 27) dstp[co * 27 + col] = acc[n][j];
         }
 }
 
@@ -1443,7 +1495,16 @@ struct MidWs {
     int n1, n2, nwa, nchb, npc, npb;
     size_t bytes;
 };
-constexpr int kW2Chunks = 2;  // 512-voxel chunks per k_pm_w2grad workgroup (when they divide)
+constexpr int kW2Chunks = 4;  // 512-voxel chunks per k_pm_w2grad workgroup (when they divide; measured 2: 25.6, 4: 23.8 us)
+// timing experiments only: VQ3D_W2_CHUNKS overrides the chunks per workgroup (read once)
+int w2_chunks() {
+    static const int n = [] {
+        const char *e = std::getenv("VQ3D_W2_CHUNKS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : kW2Chunks;
+    }();
+    return n;
+}
 constexpr int kW13Pieces = 4;  // SUBV-voxel pieces per k_pm_w13grad workgroup (when they divide)
 
 MidWs mid_ws(int B, int H, int W, int D, void *base) {
@@ -1452,7 +1513,7 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
     const PmArgs a = make_args(B, H, W, D, BTH, BTW);
     m.n2 = bwd2_blocks(a);
     m.n1 = m.n2;  // K1 rows: k_pm_bwd1's grid, or the next block's chained K2 grid
-    m.npc = kW2Chunks;
+    m.npc = w2_chunks();
     while ((nvox / CHV) % m.npc) m.npc >>= 1;
     m.npb = kW13Pieces;
     while ((nvox / SUBV) % m.npb) m.npb >>= 1;
@@ -1492,8 +1553,9 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
 bool mid_w2grad_ok(const vq3d_conv_desc *d) {
     return d->dtype == VQ3D_HALF && d->cin == BR && d->cin2 == 0 && d->cout == BR && d->kernel == 3 &&
            d->stride == 1 && d->pad == 1 && d->pad_mode == VQ3D_PAD_CIRCULAR && d->pro_kind == VQ3D_PRO_NONE &&
-           d->in_h == d->out_h && d->in_w == d->out_w && d->in_d == d->out_d &&
-           vq3d_preact_mid_supported(VQ3D_HALF, d->batch, C, BR, d->in_h, d->in_w, d->in_d);
+           d->in_h == d->out_h && d->in_w == d->out_w && d->in_d == d->out_d && d->batch >= 1 && d->in_h % 8 == 0 &&
+           d->in_w % 8 == 0 && d->in_d >= 8 && d->in_d <= 128 && (d->in_d & (d->in_d - 1)) == 0 &&
+           int64_t(d->batch) * d->in_h * d->in_w * d->in_d * BR * 2 < (int64_t(1) << 31);  // k_pm_w2grad's tiles
 }
 
 namespace {
@@ -1504,7 +1566,7 @@ struct W2Plan {
 W2Plan w2_plan(const vq3d_conv_desc *d) {
     W2Plan p;
     p.nchunk = int(int64_t(d->batch) * d->in_h * d->in_w * d->in_d / CHV);
-    p.npc = kW2Chunks;
+    p.npc = w2_chunks();
     while (p.nchunk % p.npc) p.npc >>= 1;
     p.nwa = p.nchunk / p.npc;
     p.bytes = size_t(9) * p.nwa * NER * 4;
