@@ -1236,7 +1236,14 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
 
 // k_pm_w13grad: W1 (sum gz1 (x) u1, u1 = bf16(elu(x + b1a) + b1b)) and G3 (sum t3 (x) g) over npb
 // pieces of SUBV voxels per workgroup (the next piece's loads in flight); wave w: (W1 | G3,
-// 16-column tile)
+// 16-column tile).  Staging as k_pm_w2grad's: the piece's gz1 | t3 | x | g arrive as coalesced 16-B
+// pieces written as they come to a voxel-major LDS area (x already turned into u1 by the loading
+// thread), then 96 threads each transpose one item -- 8 voxels x 9 channels of gz1 / t3, or 4
+// voxels x 18 channels of u1 / g, 144 contiguous bytes -- into channel rows (16- / 8-B stores).
+constexpr int W13_ZI = SUBV / 8, W13_XI = SUBV / 4;  // items per 9-channel / 18-channel array
+constexpr int W13_RAW = (2 * SUBV * BR + 2 * SUBV * C);  // raw area (elements): gz1 | t3 | u1 | g
+static_assert(2 * W13_ZI + 2 * W13_XI <= NT, "one staging item per thread");
+
 __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restrict__ gz1,
                                                    const h16_t *__restrict__ t3, const h16_t *__restrict__ x,
                                                    const h16_t *__restrict__ g, vq3d_preact_params p,
@@ -1249,6 +1256,7 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restr
     h16_t *t3T = z1T + 16 * SP;                     // [16][SP] t3
     h16_t *u1T = t3T + 16 * SP;                     // [32][SP] u1
     h16_t *gT = u1T + 32 * SP;                      // [32][SP] g
+    h16_t *raw = gT + 32 * SP;                      // [W13_RAW] voxel-major
     const int isG3 = wave >> 1, nt = wave & 1;
     const h16_t *aT = isG3 ? t3T : z1T, *bT = isG3 ? gT : u1T;
     // per piece: gz1 / t3 SUBV * 9 / 8 16-B pieces each, x / g SUBV * 18 / 8 each
@@ -1267,35 +1275,58 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restr
             vq[u] = src[k];
         }
     };
+    // this thread's item: [0, ZI) gz1, [ZI, 2 ZI) t3 (8 voxels x 9), then u1, g (4 voxels x 18)
+    const int nine = tid < 2 * W13_ZI, item = tid;
+    const bool active = tid < 2 * W13_ZI + 2 * W13_XI;
+    h16_t *dst;
+    if (nine) dst = (item < W13_ZI ? z1T : t3T) + 8 * (item % W13_ZI);
+    else dst = (item < 2 * W13_ZI + W13_XI ? u1T : gT) + 4 * ((item - 2 * W13_ZI) % W13_XI);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     load(int64_t(ch) * npb * SUBV);
 #pragma unroll 1
     for (int pc = 0; pc < npb; ++pc) {
-        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < PQ; ++u) {
+        for (int u = 0; u < PQ; ++u) {  // raw pieces (x as u1); the area's readers passed the last barrier
             const int i = tid + u * NT;
             if (i < NQ) {
-                const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
-                if (i < 2 * N9) {
-                    h16_t *dT = i < N9 ? z1T : t3T;
-                    const int e0 = (i < N9 ? i : i - N9) * 8;
+                u32x4 q = vq[u];
+                if (i >= 2 * N9 && i < 2 * N9 + N18) {
+                    uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int e = e0 + j, v = e / BR, c = e - v * BR;
-                        dT[c * SP + v] = h16_t((w[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
-                    }
-                } else {
-                    const bool isx = i < 2 * N9 + N18;
-                    h16_t *dT = isx ? u1T : gT;
-                    const int e0 = (isx ? i - 2 * N9 : i - 2 * N9 - N18) * 8;
+                    for (int j = 0; j < 4; ++j)
+                        w[j] = uint32_t(f2h(elu(h2f_lo(w[j]) + s.b1a) + s.b1b)) |
+                               (uint32_t(f2h(elu(h2f_hi(w[j]) + s.b1a) + s.b1b)) << 16);
+                    q = u32x4{w[0], w[1], w[2], w[3]};
+                }
+                reinterpret_cast<u32x4 *>(raw)[i] = q;
+            }
+        }
+        __syncthreads();  // raw complete; the previous piece's fragments are read
+        if (active) {
+            uint32_t w[36];
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(raw) + 9 * item;  // every item is 144 B
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        const int e = e0 + j, v = e / C, c = e - v * C;
-                        uint32_t h = (w[j >> 1] >> ((j & 1) * 16)) & 0xffffu;
-                        if (isx) h = f2h(elu(bf(h) + s.b1a) + s.b1b);
-                        dT[c * SP + v] = h16_t(h);
+            for (int j = 0; j < 9; ++j) {
+                const u32x4 q = src[j];
+                w[4 * j] = q.x;
+                w[4 * j + 1] = q.y;
+                w[4 * j + 2] = q.z;
+                w[4 * j + 3] = q.w;
+            }
+            if (nine) {
+#pragma unroll
+                for (int c = 0; c < BR; ++c) *reinterpret_cast<u32x4 *>(dst + c * SP) = item_row(w, c);
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    uint32_t o[2];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {  // voxels 2k, 2k + 1 of channel c: elements 36 k + c, + 18
+                        const int ea = 36 * k + c, eb = ea + 18;
+                        const uint32_t sel = (ea & 1 ? 0x0302u : 0x0100u) | ((eb & 1 ? 0x0706u : 0x0504u) << 16);
+                        o[k] = __builtin_amdgcn_perm(w[eb >> 1], w[ea >> 1], sel);
                     }
+                    *reinterpret_cast<u32x2 *>(dst + c * SP) = u32x2{o[0], o[1]};
                 }
             }
         }
@@ -1308,12 +1339,12 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restr
                        *reinterpret_cast<const hx8 *>(bT + (16 * nt + row) * SP + ko), acc);
         }
     }
-    float *dst = p2b + int64_t(ch) * NEB + isG3 * BR * C;
+    float *dsto = p2b + int64_t(ch) * NEB + isG3 * BR * C;
     const int c = 16 * nt + row;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int oo = 4 * kb + j;
-        if (oo < BR && c < C) dst[oo * C + c] = acc[j];
+        if (oo < BR && c < C) dsto[oo * C + c] = acc[j];
     }
 }
 
@@ -1457,8 +1488,8 @@ int bwd2_blocks(const PmArgs &a) {
     return std::max(1, std::min(a.ntiles, per * n_cu()));
 }
 
-// k_pm_w13grad LDS: z1T, t3T [16][SP] + u1T, gT [32][SP]
-constexpr size_t w13_lds() { return size_t(96 * SP) * 2; }
+// k_pm_w13grad LDS: z1T, t3T [16][SP] + u1T, gT [32][SP] + raw
+constexpr size_t w13_lds() { return size_t(96 * SP + W13_RAW) * 2; }  // + the raw area
 
 template <int D>
 void launch_w2(const PmArgs &a, int nwa, int npc, const h16_t *gz3, const h16_t *t2, float *p2a, hipStream_t s) {
@@ -1496,6 +1527,7 @@ struct MidWs {
     size_t bytes;
 };
 constexpr int kW2Chunks = 4;  // 512-voxel chunks per k_pm_w2grad workgroup (when they divide; measured 2: 25.6, 4: 23.8 us)
+constexpr int kW13Pieces = 4;  // SUBV-voxel pieces per k_pm_w13grad workgroup (when they divide)
 // timing experiments only: VQ3D_W2_CHUNKS overrides the chunks per workgroup (read once)
 int w2_chunks() {
     static const int n = [] {
@@ -1505,7 +1537,14 @@ int w2_chunks() {
     }();
     return n;
 }
-constexpr int kW13Pieces = 4;  // SUBV-voxel pieces per k_pm_w13grad workgroup (when they divide)
+int w13_pieces() {  // timing experiments only: VQ3D_W13_PIECES
+    static const int n = [] {
+        const char *e = std::getenv("VQ3D_W13_PIECES");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : kW13Pieces;
+    }();
+    return n;
+}
 
 MidWs mid_ws(int B, int H, int W, int D, void *base) {
     MidWs m;
@@ -1515,7 +1554,7 @@ MidWs mid_ws(int B, int H, int W, int D, void *base) {
     m.n1 = m.n2;  // K1 rows: k_pm_bwd1's grid, or the next block's chained K2 grid
     m.npc = w2_chunks();
     while ((nvox / CHV) % m.npc) m.npc >>= 1;
-    m.npb = kW13Pieces;
+    m.npb = w13_pieces();
     while ((nvox / SUBV) % m.npb) m.npb >>= 1;
     m.nwa = int(nvox / (int64_t(m.npc) * CHV));
     m.nchb = int(nvox / (int64_t(m.npb) * SUBV));
