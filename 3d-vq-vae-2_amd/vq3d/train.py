@@ -200,13 +200,18 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
     train_ds, val_ds = datamodule.train_dataset, datamodule.val_dataset
     sampler = (torch.utils.data.distributed.DistributedSampler(train_ds, world, rank, shuffle=True, seed=42,
                                                                drop_last=True) if world > 1 else None)
+    # persistent workers: the worker processes are forked once, before the step graph is captured,
+    # not again at every epoch from a process whose GPU work (and pin-memory thread) is in flight
+    # (an epoch-boundary re-fork after capture was seen to hang the next host-to-device copy)
+    persist = datamodule.num_workers > 0
     loader = torch.utils.data.DataLoader(train_ds, batch_size=datamodule.batch_size, shuffle=sampler is None,
                                          sampler=sampler, num_workers=datamodule.num_workers, pin_memory=True,
-                                         drop_last=True)
+                                         drop_last=True, persistent_workers=persist)
     vsampler = (torch.utils.data.distributed.DistributedSampler(val_ds, world, rank, shuffle=False)
                 if world > 1 else None)
     vloader = torch.utils.data.DataLoader(val_ds, batch_size=datamodule.batch_size, shuffle=False, sampler=vsampler,
-                                          num_workers=datamodule.num_workers, pin_memory=True, drop_last=True)
+                                          num_workers=datamodule.num_workers, pin_memory=True, drop_last=True,
+                                          persistent_workers=persist)
     n_batches = len(loader)
 
     def train_step(x, nvs):
