@@ -10,7 +10,7 @@
 //   k_wide_pack      once per RUN of blocks: every block's W1 / W2 / W3 (and their transposed,
 //                    tap-flipped backward forms) as bf16 MFMA B-fragment images, 1 KiB per
 //                    fragment, lane-major, so a wave loads a fragment with one 16-B load per lane
-//   k_wide_fwd       one launch per block: per 2x4x8 tile, u1 -> t2 on the tile's circular halo
+//   k_wide_fwd       one launch per block: per 2x2x8 tile, u1 -> t2 on the tile's circular halo
 //                    (matrix cores), t3 on the tile (windowed 3x3x3 on the matrix cores), out;
 //                    t2 / t3 saved (bf16) for the backward
 //   k_wide_bwd_data  one launch per block (the critical path): gz3 on the halo (W3^T g, matrix
@@ -47,8 +47,12 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int C = 72, BR = 36;                         // block / branch channels
-constexpr int TH = 2, TW = 4, TD = 8;                  // tile (one D-run of 8 per (h, w))
-constexpr int TV = TH * TW * TD, NMT = TV / 16;        // 64 voxels, 4 m-tiles
+#ifndef WIDE_TW
+#define WIDE_TW 2  // tile width: 2 x 2 x 8 tiles fill the chip at 32x32x8 (fwd 13.2 -> 10.3, bwd_data 16.3 -> 12.4 us vs 2 x 4 x 8)
+#endif
+constexpr int TH = 2, TW = WIDE_TW, TD = 8;            // tile (one D-run of 8 per (h, w))
+constexpr int TV = TH * TW * TD, NMT = TV / 16;        // 32 voxels, 2 m-tiles
+constexpr int MPW = NMT / 2;                           // m-tiles per wave (its half)
 constexpr int LH = TH + 2, LW = TW + 2, NL = LH * LW;  // halo lines
 constexpr int NP = TD + 2, HV = NL * NP, NHM = HV / 16;  // 10 positions, 240 halo voxels, 15 m-tiles
 constexpr int NW = 6, NT = 64 * NW;                    // waves: (branch n-tile, half of the m-tiles)
@@ -60,7 +64,7 @@ constexpr int KS1 = (C + 31) / 32, NTB = (BR + 15) / 16, NTC = (C + 15) / 16, KS
 constexpr int KSW = (3 * BR + 31) / 32;  // windowed k-steps per tap row (kd x 36 = 108 elements)
 constexpr int OF1 = 0, OF2 = OF1 + KS1 * NTB, OF3 = OF2 + 9 * KSW * NTB, OG2 = OF3 + KSB * NTC,
               OG1 = OG2 + 9 * KSW * NTB, OG3 = OG1 + KSB * NTC, NFRAG = OG3 + KS1 * NTB;
-static_assert(2 * NTB == NW && NMT == 4, "wave = (branch n-tile, m-tile half)");
+static_assert(2 * NTB == NW && NMT % 2 == 0, "wave = (branch n-tile, m-tile half)");
 
 // weight gradient decomposition
 constexpr int CHV = 512, NRUNC = CHV / TD;  // voxels / D-runs per chunk
@@ -331,24 +335,24 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
     if (!(WIDE_EXP & 8) && t2o) tile_to_global<true>(runv, t2h, t2o);
     // x of this lane's output entries, in flight during the 3x3x3 phase: m-tiles 2 hf + mm,
     // channel tiles nt + 3 q; voxel 16 m + 4 kb + j = run 2 m + (kb >> 1), d = 4 (kb & 1) + j
-    int vb[2];
+    int vb[MPW];
 #pragma unroll
-    for (int mm = 0; mm < 2; ++mm) vb[mm] = runv[2 * (2 * hf + mm) + (kb >> 1)] + 4 * (kb & 1);
-    float xv[2][2][4];
+    for (int mm = 0; mm < MPW; ++mm) vb[mm] = runv[2 * (MPW * hf + mm) + (kb >> 1)] + 4 * (kb & 1);
+    float xv[2][MPW][4];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int co = min(16 * (nt + NTB * q) + row, C - 1);
 #pragma unroll
-        for (int mm = 0; mm < 2; ++mm)
+        for (int mm = 0; mm < MPW; ++mm)
 #pragma unroll
             for (int j = 0; j < 4; ++j) xv[q][mm][j] = x[int64_t(vb[mm] + j) * C + co];
     }
     // t3 = elu(W2 (*) t2 + b3a) + b3b on the tile
-    f32x4 acc3[2];
+    f32x4 acc3[MPW];
 #pragma unroll
-    for (int mm = 0; mm < 2; ++mm) {
+    for (int mm = 0; mm < MPW; ++mm) {
         acc3[mm] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int v = 16 * (2 * hf + mm) + row, d = v & 7;
+        const int v = 16 * (MPW * hf + mm) + row, d = v & 7;
 #pragma unroll
         for (int kk = 0; kk < ((WIDE_EXP & 4) ? 0 : 9); ++kk) {
             const h16_t *wbase = t2h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
@@ -359,10 +363,10 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
     __syncthreads();  // every wave is done with u1h (t3 goes over it)
     if (ob < BR) {
 #pragma unroll
-        for (int mm = 0; mm < 2; ++mm)
+        for (int mm = 0; mm < MPW; ++mm)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                t3s[(16 * (2 * hf + mm) + 4 * kb + j) * BR + ob] = f2h(elu_f(acc3[mm][j] + s.b3a) + s.b3b);
+                t3s[(16 * (MPW * hf + mm) + 4 * kb + j) * BR + ob] = f2h(elu_f(acc3[mm][j] + s.b3a) + s.b3b);
     }
     __syncthreads();
     if (!(WIDE_EXP & 8) && t3o) tile_to_global<false>(runv, t3s, t3o);
@@ -376,8 +380,8 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
             for (int k = 0; k < KSB; ++k) f3[k] = frag(img, OF3 + k * NTC + ntc, lane);
             const int co = 16 * ntc + row;
 #pragma unroll
-            for (int mm = 0; mm < 2; ++mm) {
-                const int m = 2 * hf + mm;
+            for (int mm = 0; mm < MPW; ++mm) {
+                const int m = MPW * hf + mm;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int k = 0; k < KSB; ++k) acc = mfma(ld8(t3s + (16 * m + row) * BR + 32 * k + 8 * kb), f3[k], acc);
@@ -505,14 +509,14 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
     }
     __syncthreads();
     if constexpr (!(WIDE_EXP & 8)) tile_to_global<true>(runv, z3h, gz3o);
-    int vb[2];
+    int vb[MPW];
 #pragma unroll
-    for (int mm = 0; mm < 2; ++mm) vb[mm] = runv[2 * (2 * hf + mm) + (kb >> 1)] + 4 * (kb & 1);
+    for (int mm = 0; mm < MPW; ++mm) vb[mm] = runv[2 * (MPW * hf + mm) + (kb >> 1)] + 4 * (kb & 1);
     // gt2 = W2^T (*) gz3 -> gz1 = bf16(gt2 * elu'(t2))
     float s2b = 0.f, s2a = 0.f;
 #pragma unroll
-    for (int mm = 0; mm < 2; ++mm) {
-        const int m = 2 * hf + mm;
+    for (int mm = 0; mm < MPW; ++mm) {
+        const int m = MPW * hf + mm;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         const int v = 16 * m + row, d = v & 7;
 #pragma unroll
@@ -545,8 +549,8 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
             for (int k = 0; k < KSB; ++k) f1[k] = frag(img, OG1 + k * NTC + ntc, lane);
             const int c = 16 * ntc + row;
 #pragma unroll
-            for (int mm = 0; mm < 2; ++mm) {
-                const int m = 2 * hf + mm;
+            for (int mm = 0; mm < MPW; ++mm) {
+                const int m = MPW * hf + mm;
                 f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int k = 0; k < KSB; ++k) acc = mfma(ld8(z1s + (16 * m + row) * BR + 32 * k + 8 * kb), f1[k], acc);
