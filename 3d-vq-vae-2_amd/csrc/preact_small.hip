@@ -31,6 +31,9 @@ namespace {
 constexpr int NT = 256;           // threads per workgroup (both kernels)
 constexpr int kNScal = 8;         // scalar partials: b4, scale, b3b, b3a, b2b, b2a, b1b, b1a
 constexpr size_t kLdsTarget = 80 * 1024;
+#ifndef SMALL_MINV
+#define SMALL_MINV 64  // smallest brick halved to for more workgroups (timing experiments: EXPDEF=SMALL_MINV)
+#endif
 
 struct SArgs {
     int B, H, W, D;
@@ -537,7 +540,7 @@ bool plan(int batch, int C, int BR, int h, int w, int d, SArgs &a) {
         a.nbricks = batch * a.nbh * a.nbw * a.nbd;
     };
     set(std::min(h, 8), std::min(w, 8), std::min(d, 16));
-    while (lds_bwd(a, C, BR) > kLdsTarget || (a.nbricks < 256 && a.nvb > 64)) {
+    while (lds_bwd(a, C, BR) > kLdsTarget || (a.nbricks < 256 && a.nvb > SMALL_MINV)) {
         if (a.bd >= a.bh && a.bd >= a.bw && a.bd > 1) set(a.bh, a.bw, a.bd / 2);
         else if (a.bh >= a.bw && a.bh > 1) set(a.bh / 2, a.bw, a.bd);
         else if (a.bw > 1) set(a.bh, a.bw / 2, a.bd);
