@@ -54,6 +54,9 @@
 #define PM_BWD_PER 0
 #endif
 // 1: the D16 tile kernels keep one run's epilogue at a time (a scheduling barrier between runs)
+#ifndef PM_DEPTH
+#define PM_DEPTH 1  // tiles of operands in flight ahead of k_pm_bwd2's current tile (1 or 2)
+#endif
 #ifndef PM_SB
 #define PM_SB 1
 #endif
@@ -745,9 +748,12 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
     float q4 = 0.f, q3b = 0.f, q3a = 0.f, qsc = 0.f;  // CHAIN: the previous block's K1 sums
     // the wave's two D-runs: rows ph, ph + 1 of tile column pw (run coordinates inside the tile)
     const int ph = (wave >> 2) * 2, pw = wave & 3;
-    HaloQ hz;
-    Raw9 et2[2], et3[2];
-    Raw18 ex[2], eg[2];
+    // the operands of the tiles ahead of the current one, PM_DEPTH deep: with depth 2 the tile loop
+    // is unrolled by two over two register sets (no loop-carried copies, which would wait for the
+    // loads at the back edge), and each tile refills its set with the tile two steps ahead
+    HaloQ hzA, hzB;
+    Raw9 et2A[2], et3A[2], et2B[2], et3B[2];
+    Raw18 exA[2], egA[2], exB[2], egB[2];
     // every per-thread index below derives from a copy of the thread index laundered once per tile:
     // the address arithmetic is then recomputed per tile (a few VALU ops) instead of being hoisted
     // out of the tile loop as dozens of live loop invariants
@@ -758,7 +764,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
     auto run_vox0 = [&](const Org &o, int r) {  // first voxel of the wave's run r (0, 1)
         return ((uint32_t(o.b) * a.H + o.h0 + ph + r) * a.W + o.w0 + pw) * a.D + o.d0;
     };
-    auto load_ep = [&](int ln, const Org &o, int r) {
+    auto load_ep = [&](Raw9 (&et2)[2], Raw9 (&et3)[2], Raw18 (&ex)[2], Raw18 (&eg)[2], int ln, const Org &o, int r) {
         const int nn = ln & 15, kq = ln >> 4;
         const uint32_t v = run_vox0(o, r) + nn;
         et2[r] = ld9(t2, v, kq);
@@ -767,17 +773,24 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
         if constexpr (CHAIN) et3[r] = ld9(t3p, v, kq);
     };
     const TileSched sc = xcd_sched(a.ntiles);
+    constexpr int DEPTH = PM_DEPTH;
+    static_assert(DEPTH == 1 || DEPTH == 2, "prefetch depth");
     if (sc.t < sc.end) {
         const Org o0 = tile_org_q(a, sc.t);
-        hz.load(tid, a, o0, gz3);
+        hzA.load(tid, a, o0, gz3);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) load_ep(lane, o0, r);
+        for (int r = 0; r < 2; ++r) load_ep(et2A, et3A, exA, egA, lane, o0, r);
+        if constexpr (DEPTH == 2) {
+            const Org o1 = tile_org_q(a, sc.t + sc.step < sc.end ? sc.t + sc.step : sc.t);
+            hzB.load(tid, a, o1, gz3);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) load_ep(et2B, et3B, exB, egB, lane, o1, r);
+        }
     }
-    int it = 0;
-    for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) {
+    auto body = [&](HaloQ &hz, Raw9 (&et2)[2], Raw9 (&et3)[2], Raw18 (&ex)[2], Raw18 (&eg)[2], int tile, int it) {
         const Org o = tile_org_q(a, tile);
-        const bool more = tile + sc.step < sc.end;
-        const Org on = tile_org_q(a, more ? tile + sc.step : tile);
+        const int tn = tile + DEPTH * sc.step;
+        const Org on = tile_org_q(a, tn < sc.end ? tn : tile);
         const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
         h16_t *hl = img + (it & 1) * QIMG;
         if constexpr (!(PM_EXP & 16)) hz.store(tl, hl);
@@ -871,10 +884,20 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             }
             if constexpr (!(PM_EXP & 256))
                 flush_run(st, ln, gx + size_t(v0) * C, gz1o + size_t(v0) * BR, CHAIN ? gz3p + size_t(v0) * BR : nullptr);
-            // the next tile's operands of this run (unconditional: on = this tile at the end; a
-            // branch would keep the old values live)
-            if constexpr (!(PM_EXP & 512)) load_ep(ln, on, r);
+            // the operands of the tile DEPTH steps ahead for this run (unconditional: on = this tile
+            // at the end; a branch would keep the old values live)
+            if constexpr (!(PM_EXP & 512)) load_ep(et2, et3, ex, eg, ln, on, r);
             if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);  // one run's epilogue at a time (no interleaving)
+        }
+    };
+    if constexpr (DEPTH == 1) {
+        int it = 0;
+        for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) body(hzA, et2A, et3A, exA, egA, tile, it);
+    } else {
+        int it = 0;
+        for (int tile = sc.t; tile < sc.end; tile += 2 * sc.step, it += 2) {
+            body(hzA, et2A, et3A, exA, egA, tile, it);
+            if (tile + sc.step < sc.end) body(hzB, et2B, et3B, exB, egB, tile + sc.step, it + 1);
         }
     }
     if constexpr (CHAIN) {
