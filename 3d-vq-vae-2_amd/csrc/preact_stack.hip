@@ -564,6 +564,38 @@ struct WReg {  // register prefetch of one block's weights (fp32, torch order)
     }
 };
 
+// Every block's packed fragment image, built once per run by k_stackm_pack (in parallel, one
+// workgroup per block) so the chain kernels only copy 17 KiB per block from L2 into LDS (two
+// 16-byte pieces per thread, fetched a block ahead) instead of converting and scattering the fp32
+// weights on the chain's critical path (that staging was ~45 % of the forward chain's time).
+constexpr int FR_CH = FR_N * 2 / 16;  // 16-byte pieces per image
+constexpr int FR_CPT = (FR_CH + NT - 1) / NT;
+static_assert((FR_N * 2) % 16 == 0, "image pieces");
+template <bool BWD>
+__global__ __launch_bounds__(NT) void k_stackm_pack(const float *const *tab, h16_t *__restrict__ img) {
+    const int blk = blockIdx.x;
+    const float *w1 = tab[blk * NPRM + 0], *w2 = tab[blk * NPRM + 1], *w3 = tab[blk * NPRM + 2];
+    h16_t *fr = img + size_t(blk) * FR_N;
+    for (int i = threadIdx.x; i < WN; i += NT)
+        frag_store<BWD>(fr, i, i < W3O ? w1[i - W1O] : (i < W2O ? w3[i - W3O] : w2[i - W2O]));
+    frag_zero(fr);
+}
+struct ImgReg {  // register prefetch of one block's packed image
+    u32x4 v[FR_CPT];
+    __device__ __forceinline__ void load(const h16_t *img, int blk) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(img + size_t(blk) * FR_N);
+#pragma unroll
+        for (int u = 0; u < FR_CPT; ++u) v[u] = src[min(int(threadIdx.x) + u * NT, FR_CH - 1)];
+    }
+    __device__ __forceinline__ void store(h16_t *fr) const {
+#pragma unroll
+        for (int u = 0; u < FR_CPT; ++u) {
+            const int i = threadIdx.x + u * NT;
+            if (i < FR_CH) reinterpret_cast<u32x4 *>(fr)[i] = v[u];
+        }
+    }
+};
+
 // A block's parameter-table row, lane-distributed in VECTOR registers: lane k (< NPRM) holds
 // the row's k-th pointer, and after deref() lanes 3 .. 10 hold the scalar values.  Rows are
 // fetched one block ahead, so the waits ride vmcnt a whole block after the issue (scalar loads
@@ -612,7 +644,8 @@ __device__ __forceinline__ f32x4 conv_half(const Mk &m, const h16_t *src, int mt
 }
 
 __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const h16_t *__restrict__ x, const float *const *tab,
-                                                   h16_t *__restrict__ out, float *__restrict__ saved) {
+                                                   h16_t *__restrict__ out, float *__restrict__ saved,
+                                                   const h16_t *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Mk m = carve_m(a.nv, smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
@@ -621,21 +654,20 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const h16_t *__rest
     for (int i = tid; i < nv * 27; i += NT) m.nb[i] = short(nbr(a, i / 27, i % 27, 1));
     for (int i = tid; i < nvc; i += NT) m.xs[(i / MC) * PF + i % MC] = ld(x + i);
     for (int i = tid; i < 32; i += NT) m.t3[nv * PT + i] = 0;  // zero tail / row pads read by the fragments
-    frag_zero(m.fr);
     for (int i = tid; i < nv * (PT - MB); i += NT) m.t3[(i / (PT - MB)) * PT + MB + i % (PT - MB)] = 0;
-    WReg wr;
+    ImgReg ir;
     const float *pc = row_ptr(tab, 0, lane);
     float vc = *pc;
-    wr.load(bcast_ptr(pc, 0), bcast_ptr(pc, 1), bcast_ptr(pc, 2));
+    ir.load(img, 0);
     const float *pn = row_ptr(tab, min(1, a.nblk - 1), lane);
     for (int blk = 0; blk < a.nblk; ++blk) {
         const Scal s = scal_lanes(vc);
         float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
         __syncthreads();
-        if constexpr (!(STK_EXP & 8)) wr.store<false>(m.w, m.fr);
+        if constexpr (!(STK_EXP & 8)) ir.store(m.fr);
         // the next block's weights and scalars, and the row after it
         if (blk + 1 < a.nblk) {
-            wr.load(bcast_ptr(pn, 0), bcast_ptr(pn, 1), bcast_ptr(pn, 2));
+            ir.load(img, blk + 1);
             vc = *pn;
             pn = row_ptr(tab, min(blk + 2, a.nblk - 1), lane);
         }
@@ -694,7 +726,8 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const h16_t *__rest
 template <bool SPLIT>
 __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__restrict__ g, const float *const *tab,
                                                    float *const *gtab, const float *__restrict__ saved,
-                                                   h16_t *__restrict__ gx, h16_t *__restrict__ rec) {
+                                                   h16_t *__restrict__ gx, h16_t *__restrict__ rec,
+                                                   const h16_t *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Mk m = carve_m(a.nv, smem);
     const int tid0 = threadIdx.x;
@@ -708,15 +741,18 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
         m.z1[v * PT + e] = 0;
     }
     for (int i = tid; i < 32; i += NT) m.z1[nv * PT + i] = 0;
-    frag_zero(m.fr);
-    // prefetched one block ahead (the walk is in reverse): weights, scalars, gradient pointers,
+    if constexpr (!SPLIT) frag_zero(m.fr);
+    // prefetched one block ahead (the walk is in reverse): weights (SPLIT: the packed image, else
+    // the fp32 weights, whose W3 the fused scale gradient reads), scalars, gradient pointers,
     // the saved x / t2 / t3; the current block's old gradient values at its top
     constexpr int SX = MAXVM * MC / NT, SB = MAXVM * MB / NT;
     WReg wr;
+    ImgReg ir;
     const int last = a.nblk - 1;
     const float *pc = row_ptr(tab, last, lane);
     float vc = *pc;
-    wr.load(bcast_ptr(pc, 0), bcast_ptr(pc, 1), bcast_ptr(pc, 2));
+    if constexpr (SPLIT) ir.load(img, last);
+    else wr.load(bcast_ptr(pc, 0), bcast_ptr(pc, 1), bcast_ptr(pc, 2));
     const float *pn = row_ptr(tab, max(last - 1, 0), lane);
     float *gc = row_ptr(gtab, last, lane);
     float svx[SX], sv2[SB], sv3[SB];
@@ -759,7 +795,10 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
         float *const gsc = gc;  // lanes 3 .. 10: this block's scalar-gradient pointers
         if (blk > 0) gc = row_ptr(gtab, blk - 1, lane);
         __syncthreads();
-        if constexpr (!(STK_EXP & 8)) wr.store<true>(m.w, m.fr);
+        if constexpr (!(STK_EXP & 8)) {
+            if constexpr (SPLIT) ir.store(m.fr);
+            else wr.store<true>(m.w, m.fr);
+        }
 #pragma unroll
         for (int u = 0; u < SX; ++u) {
             const int i = tid + u * NT;
@@ -849,7 +888,8 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
         // the next block's weights / scalars / saved tensors and this block's old W1 gradient
         // (issued here, after the register-heavy k^3 phases)
         if (blk > 0) {
-            wr.load(bcast_ptr(pn, 0), bcast_ptr(pn, 1), bcast_ptr(pn, 2));
+            if constexpr (SPLIT) ir.load(img, blk - 1);
+            else wr.load(bcast_ptr(pn, 0), bcast_ptr(pn, 1), bcast_ptr(pn, 2));
             vc = *pn;
             pn = row_ptr(tab, max(blk - 2, 0), lane);
             load_saved(blk - 1);
@@ -1031,7 +1071,8 @@ int vq3d_preact_stack_supported(int32_t batch, int32_t channels, int32_t branch,
 
 size_t vq3d_preact_stack_saved_floats(int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
                                       int32_t w, int32_t dd) {
-    return size_t(nblocks) * batch * h * w * dd * (channels + 2 * branch);
+    // per block x / t2 / t3, then the matrix-core forward's packed fragment images (FR_N 16-bit each)
+    return size_t(nblocks) * batch * h * w * dd * (channels + 2 * branch) + size_t(nblocks) * FR_N / 2;
 }
 
 int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch, int32_t h,
@@ -1045,7 +1086,9 @@ int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
     if (dtype == VQ3D_HALF && mfma_ok(a)) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   int(160 * 1024));
-        k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved);
+        h16_t *img = reinterpret_cast<h16_t *>(saved + size_t(nblocks) * a.nv * (a.C + 2 * a.B));
+        k_stackm_pack<false><<<nblocks, NT, 0, s>>>(params, img);
+        k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved, img);
     } else if (dtype == VQ3D_HALF) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<h16_t>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
@@ -1071,7 +1114,8 @@ int vq3d_preact_stack_bwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
     if (dtype == VQ3D_HALF && mfma_ok(a)) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
-        k_stackm_bwd<false><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx, nullptr);
+        k_stackm_bwd<false><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx, nullptr,
+                                                       nullptr);
     } else if (dtype == VQ3D_HALF) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_bwd<h16_t>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
@@ -1090,7 +1134,7 @@ size_t vq3d_preact_stack_bwd_workspace_bytes(int32_t nblocks, int32_t batch, int
                                              int32_t h, int32_t w, int32_t dd) {
     SkArgs a;
     if (check(nblocks, batch, channels, branch, h, w, dd, a) || !mfma_ok(a)) return 0;
-    return size_t(nblocks) * a.nv * (MC + 2 * MB) * 2;
+    return size_t(nblocks) * a.nv * (MC + 2 * MB) * 2 + size_t(nblocks) * FR_N * 2;  // + the packed images
 }
 
 int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch,
@@ -1108,8 +1152,10 @@ int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int3
     hipStream_t s = as_stream(stream);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+    h16_t *img = static_cast<h16_t *>(workspace) + size_t(nblocks) * a.nv * (MC + 2 * MB);
+    k_stackm_pack<true><<<nblocks, NT, 0, s>>>(params, img);
     k_stackm_bwd<true><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx,
-                                                  (h16_t *)workspace);
+                                                  (h16_t *)workspace, img);
     k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const h16_t *)workspace);
     return check_launch("preact_stack_bwd_ws");
 }
