@@ -27,7 +27,9 @@
 //               sum_v gz3[v][co] t2[v + tap][ci] with voxels as the MFMA reduction axis
 //            C: per thread 4 voxels: gz1 = bf16(gt2 * elu'(t2)), gx = g + (W1^T gz1) * elu'(x + b1a),
 //               the W1 gradient (sum gz1 (x) u1) and the b2 / b1 sums
-//            per-brick partial rows [brick][entry], summed in a fixed order by k_col_reduce1 / 2.
+//            per-workgroup partial rows [workgroup][entry] (the backward is persistent: a
+//            workgroup walks a brick range, its sums in registers), summed in a fixed order by
+//            k_col_reduce1 / 2.
 // Rounding points are the unfused path's: t2, t3, gz3, gz1 rounded to bf16 (the conv operands), fp32
 // accumulation; the W1 gradient reads u1 rounded to bf16 (the unfused wgrad's operand).  The
 // residual stream x / out (and g / gx) is stored bf16 or fp32 per tensor (template TX / TO): a run
@@ -35,6 +37,7 @@
 #include "engines.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 // Timing experiments only (make exp EXP=N EXPSRC=preact_col EXPDEF=COL_EXP): bit 0 skips the halo
@@ -79,6 +82,7 @@ constexpr int n_entries() {
 struct CArgs {
     int B, H, W, D;
     int nbh, nbw, nbd, nbricks;
+    int nwg;  // persistent backward grid (workgroups walking brick ranges; its partial rows)
     int xcd;  // XCD-contiguous brick order (measured: faster up to 4096 bricks, slower at 32768)
 };
 
@@ -380,105 +384,23 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
     float *wred = reinterpret_cast<float *>(smem);        // after phase C: [4][NTN][64][4] over z3h / t2T
     static_assert(size_t(HVX * BR + PADE + BR * NLN * TP) * 2 >= size_t(4 * K::NTN * 256) * 4, "W2 sums fit z3h + t2T");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
-    const Org o = brick_org(a, a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x));
     const Scal s = load_scal(p);
     hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, true>(w2, k, lane);
-    line_table(a, o, lbase);
     for (int i = tid; i < PADE; i += NT) z3h[HVX * BR + i] = 0;
     for (int i = tid; i < BR * NLN * (TP - PL) / 2; i += NT) {  // zero the channel-major line tails
         const int l = i / ((TP - PL) / 2), e = i - l * ((TP - PL) / 2);
         reinterpret_cast<uint32_t *>(t2T + l * TP + PL)[e] = 0u;
     }
-    __syncthreads();
-    // A. gz3 on the halo; t2 on the halo (channel-major); interior sums and G3 = sum t3 (x) g
+    // every partial sum of the workgroup's bricks accumulates in registers (the W2 gradient in the
+    // MFMA accumulators) and is reduced once, after the last brick
     float s4 = 0.f, s3b = 0.f, s3a = 0.f, ssc = 0.f, g3[BR][C];
+    float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f, dw1[BR][C];
 #pragma unroll
     for (int oo = 0; oo < BR; ++oo)
 #pragma unroll
-        for (int c = 0; c < C; ++c) g3[oo][c] = 0.f;
-    // two batches of halo items: every load of a batch issued before its math (registers)
-    constexpr int PH = ((HVX + NT - 1) / NT + 1) / 2;
-#pragma unroll 1
-    for (int half = 0; half < 2; ++half) {
-        constexpr int P = PH;
-        Raw<TO, C> gv[P];
-        typename Vec<BR>::U tv3[P], tv2[P];
-#pragma unroll
-        for (int u = 0; u < P; ++u) {
-            int line, pos;
-            const int vx = halo_voxel(a, o, lbase, min(tid + (half * PH + u) * NT, HVX - 1), line, pos);
-            if constexpr (!(COL_EXP & 1)) {
-                gv[u] = ldraw<TO, C>(g + int64_t(vx) * C);
-                tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
-                tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
-            } else {
-                gv[u] = Raw<TO, C>{};
-                tv3[u] = tv2[u] = typename Vec<BR>::U{};
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < P; ++u) {
-            const int q = tid + (half * PH + u) * NT;
-            if (!(COL_EXP & 2) && q < HVX) {
-                const int line = q / PL, pos = q - line * PL;
-                const bool in = interior(line, pos);
-                float gf[C], t3f[BR], t2f[BR], z[BR];
-                unraw<TO, C>(gv[u], gf);
-                unpack<BR>(tv3[u], t3f);
-                unpack<BR>(tv2[u], t2f);
-#pragma unroll
-                for (int oo = 0; oo < BR; ++oo) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int c = 0; c < C; ++c) acc = fmaf(w3[c * BR + oo], gf[c], acc);
-                    const float gt3 = s.sc * acc;
-                    z[oo] = gt3 * elu_d_act(t3f[oo], s.b3b);
-                    if (in) {
-                        s3b += gt3;
-                        s3a += z[oo];
-                        ssc = fmaf(acc, t3f[oo], ssc);
-#pragma unroll
-                        for (int c = 0; c < C; ++c) g3[oo][c] = fmaf(t3f[oo], gf[c], g3[oo][c]);
-                    }
-                    t2T[(oo * NLN + line) * TP + pos] = f2h(t2f[oo]);
-                }
-                const typename Vec<BR>::U zp = packv<BR>(z);
-                *reinterpret_cast<typename Vec<BR>::U *>(z3h + q * BR) = zp;
-                if (in) {
-#pragma unroll
-                    for (int c = 0; c < C; ++c) s4 += gf[c];
-                    const int lh = line / WL, lw = line - lh * WL;
-                    const int v = ((lh - 1) * BW + lw - 1) * BD + pos - 1;
-#pragma unroll
-                    for (int oo = 0; oo < BR; ++oo) z3T[oo * ZP + v] = f2h(z[oo]);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // the thread's 4 voxels (phase C): g and x in flight during phase B
-    const int ln = tid / (BD / DV), dg = tid % (BD / DV);
-    const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
-    constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
-    // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
-    int woff[K::KS];
-    win_offsets<BR>(row, kb, woff);
-#pragma unroll 2
-    for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        const int wb = win_base(mt, BR);
-#pragma unroll
-        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, wb + woff[k]), fw[k], acc);
-        if (row < BR) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
-        }
-    }
-    // B2. W2 gradient: D[co][col] += sum_v gz3[v][co] * t2win[v][col], col = r * 3B + kd * B + ci;
-    // wave w takes the 32-voxel k-steps 8 w .. 8 w + 7 (two brick lines each; lane kb: line
-    // 2 ks + kb / 2, d = 8 (kb & 1) + j)
+        for (int c = 0; c < C; ++c) g3[oo][c] = dw1[oo][c] = 0.f;
     f32x4 aw[K::NTN];
     int toff[K::NTN];
 #pragma unroll
@@ -488,75 +410,161 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                   ci = e - kd * BR, kh = r / 3, kw = r - 3 * kh;
         toff[n] = (ci * NLN + kh * WL + kw) * TP + kd + 8 * (kb & 1);  // + line offset of the k-step
     }
-#pragma unroll 2
-    for (int ks = 8 * wave; ks < ((COL_EXP & 8) ? 0 : 8 * wave + 8); ++ks) {
-        // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
-        const hx8 af = *reinterpret_cast<const hx8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
-        const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
-#pragma unroll
-        for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
-    }
-    __syncthreads();
-    // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 4 voxels
-    if constexpr ((COL_EXP & 16) != 0) return;
-    const int v0 = ln * BD + dg * DV;
-    float s2b = 0.f, s2a = 0.f, s1b = 0.f, s1a = 0.f, dw1[BR][C];
-#pragma unroll
-    for (int oo = 0; oo < BR; ++oo)
-#pragma unroll
-        for (int c = 0; c < C; ++c) dw1[oo][c] = 0.f;
-    // 8-element pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
-    // flight during the current one's math (one piece of registers at a time: occupancy)
-    constexpr int PV = 8 / C;
-    const int hl0 = ((ln >> 3) + 1) * WL + (ln & 7) + 1;
-    const TX *xp = x + vox0 * C;
-    const TO *gp = g + vox0 * C;
-    Raw<TX, 8> xq = ldraw<TX, 8>(xp);
-    Raw<TO, 8> gq = ldraw<TO, 8>(gp);
+    int woff[K::KS];
+    win_offsets<BR>(row, kb, woff);
+    // persistent: the workgroup walks a range of bricks (XCD-contiguous)
+    const TileSched sc = xcd_sched(a.nbricks);
 #pragma unroll 1
-    for (int pc = 0; pc < NXB; ++pc) {
-        Raw<TX, 8> xn = xq;
-        Raw<TO, 8> gn = gq;
-        if (pc + 1 < NXB) {
-            xn = ldraw<TX, 8>(xp + 8 * (pc + 1));
-            gn = ldraw<TO, 8>(gp + 8 * (pc + 1));
-        }
-        float xe[8], ge[8], ov[8];
-        unraw<TX, 8>(xq, xe);
-        unraw<TO, 8>(gq, ge);
+    for (int brick = sc.t; brick < sc.end; brick += sc.step) {
+        const Org o = brick_org(a, brick);
+        __syncthreads();  // the previous brick's readers of the LDS tiles are done
+        line_table(a, o, lbase);
+        __syncthreads();
+        // A. gz3 on the halo; t2 on the halo (channel-major); interior sums and G3 = sum t3 (x) g
+        // two batches of halo items: every load of a batch issued before its math (registers)
+        constexpr int PH = ((HVX + NT - 1) / NT + 1) / 2;
+#pragma unroll 1
+        for (int half = 0; half < 2; ++half) {
+            constexpr int P = PH;
+            Raw<TO, C> gv[P];
+            typename Vec<BR>::U tv3[P], tv2[P];
 #pragma unroll
-        for (int vi = 0; vi < PV; ++vi) {
-            const int i = pc * PV + vi;
-            float z1[BR];
-#pragma unroll
-            for (int oo = 0; oo < BR; ++oo) {
-                const float gt2 = accs[acc_at(v0 + i, BR) + oo];
-                const float t2v = bf(t2T[(oo * NLN + hl0) * TP + dg * DV + i + 1]);
-                const float zz = gt2 * elu_d_act(t2v, s.b2b);
-                s2b += gt2;
-                s2a += zz;
-                z1[oo] = rbf(zz);
+            for (int u = 0; u < P; ++u) {
+                int line, pos;
+                const int vx = halo_voxel(a, o, lbase, min(tid + (half * PH + u) * NT, HVX - 1), line, pos);
+                if constexpr (!(COL_EXP & 1)) {
+                    gv[u] = ldraw<TO, C>(g + int64_t(vx) * C);
+                    tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
+                    tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
+                } else {
+                    gv[u] = Raw<TO, C>{};
+                    tv3[u] = tv2[u] = typename Vec<BR>::U{};
+                }
             }
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                float gt1 = 0.f;
+            for (int u = 0; u < P; ++u) {
+                const int q = tid + (half * PH + u) * NT;
+                if (!(COL_EXP & 2) && q < HVX) {
+                    const int line = q / PL, pos = q - line * PL;
+                    const bool in = interior(line, pos);
+                    float gf[C], t3f[BR], t2f[BR], z[BR];
+                    unraw<TO, C>(gv[u], gf);
+                    unpack<BR>(tv3[u], t3f);
+                    unpack<BR>(tv2[u], t2f);
 #pragma unroll
-                for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
-                const int e = vi * C + c;
-                const float zx = xe[e] + s.b1a;
-                const float e1 = zx > 0.f ? 1.f : __expf(zx);
-                const float u1 = rbf((zx > 0.f ? zx : e1 - 1.f) + s.b1b);
-                s1b += gt1;
-                s1a = fmaf(gt1, e1, s1a);
-                ov[e] = ge[e] + gt1 * e1;
+                    for (int oo = 0; oo < BR; ++oo) {
+                        float acc = 0.f;
 #pragma unroll
-                for (int oo = 0; oo < BR; ++oo) dw1[oo][c] = fmaf(z1[oo], u1, dw1[oo][c]);
+                        for (int c = 0; c < C; ++c) acc = fmaf(w3[c * BR + oo], gf[c], acc);
+                        const float gt3 = s.sc * acc;
+                        z[oo] = gt3 * elu_d_act(t3f[oo], s.b3b);
+                        if (in) {
+                            s3b += gt3;
+                            s3a += z[oo];
+                            ssc = fmaf(acc, t3f[oo], ssc);
+#pragma unroll
+                            for (int c = 0; c < C; ++c) g3[oo][c] = fmaf(t3f[oo], gf[c], g3[oo][c]);
+                        }
+                        t2T[(oo * NLN + line) * TP + pos] = f2h(t2f[oo]);
+                    }
+                    const typename Vec<BR>::U zp = packv<BR>(z);
+                    *reinterpret_cast<typename Vec<BR>::U *>(z3h + q * BR) = zp;
+                    if (in) {
+#pragma unroll
+                        for (int c = 0; c < C; ++c) s4 += gf[c];
+                        const int lh = line / WL, lw = line - lh * WL;
+                        const int v = ((lh - 1) * BW + lw - 1) * BD + pos - 1;
+#pragma unroll
+                        for (int oo = 0; oo < BR; ++oo) z3T[oo * ZP + v] = f2h(z[oo]);
+                    }
+                }
             }
         }
-        stvec<TX, 8>(gx + vox0 * C + 8 * pc, ov);
-        xq = xn;
-        gq = gn;
-    }
+        __syncthreads();
+        // the thread's 4 voxels (phase C): g and x in flight during phase B
+        const int ln = tid / (BD / DV), dg = tid % (BD / DV);
+        const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
+        constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
+        // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
+#pragma unroll 2
+        for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            const int wb = win_base(mt, BR);
+#pragma unroll
+            for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, wb + woff[k]), fw[k], acc);
+            if (row < BR) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+            }
+        }
+        // B2. W2 gradient: D[co][col] += sum_v gz3[v][co] * t2win[v][col], col = r * 3B + kd * B + ci;
+        // wave w takes the 32-voxel k-steps 8 w .. 8 w + 7 (two brick lines each; lane kb: line
+        // 2 ks + kb / 2, d = 8 (kb & 1) + j)
+#pragma unroll 2
+        for (int ks = 8 * wave; ks < ((COL_EXP & 8) ? 0 : 8 * wave + 8); ++ks) {
+            // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
+            const hx8 af = *reinterpret_cast<const hx8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
+            const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
+#pragma unroll
+            for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
+        }
+        __syncthreads();
+        // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 4 voxels
+        if constexpr ((COL_EXP & 16) != 0) continue;
+        const int v0 = ln * BD + dg * DV;
+        // 8-element pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
+        // flight during the current one's math (one piece of registers at a time: occupancy)
+        constexpr int PV = 8 / C;
+        const int hl0 = ((ln >> 3) + 1) * WL + (ln & 7) + 1;
+        const TX *xp = x + vox0 * C;
+        const TO *gp = g + vox0 * C;
+        Raw<TX, 8> xq = ldraw<TX, 8>(xp);
+        Raw<TO, 8> gq = ldraw<TO, 8>(gp);
+#pragma unroll 1
+        for (int pc = 0; pc < NXB; ++pc) {
+            Raw<TX, 8> xn = xq;
+            Raw<TO, 8> gn = gq;
+            if (pc + 1 < NXB) {
+                xn = ldraw<TX, 8>(xp + 8 * (pc + 1));
+                gn = ldraw<TO, 8>(gp + 8 * (pc + 1));
+            }
+            float xe[8], ge[8], ov[8];
+            unraw<TX, 8>(xq, xe);
+            unraw<TO, 8>(gq, ge);
+#pragma unroll
+            for (int vi = 0; vi < PV; ++vi) {
+                const int i = pc * PV + vi;
+                float z1[BR];
+#pragma unroll
+                for (int oo = 0; oo < BR; ++oo) {
+                    const float gt2 = accs[acc_at(v0 + i, BR) + oo];
+                    const float t2v = bf(t2T[(oo * NLN + hl0) * TP + dg * DV + i + 1]);
+                    const float zz = gt2 * elu_d_act(t2v, s.b2b);
+                    s2b += gt2;
+                    s2a += zz;
+                    z1[oo] = rbf(zz);
+                }
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    float gt1 = 0.f;
+#pragma unroll
+                    for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
+                    const int e = vi * C + c;
+                    const float zx = xe[e] + s.b1a;
+                    const float e1 = zx > 0.f ? 1.f : __expf(zx);
+                    const float u1 = rbf((zx > 0.f ? zx : e1 - 1.f) + s.b1b);
+                    s1b += gt1;
+                    s1a = fmaf(gt1, e1, s1a);
+                    ov[e] = ge[e] + gt1 * e1;
+#pragma unroll
+                    for (int oo = 0; oo < BR; ++oo) dw1[oo][c] = fmaf(z1[oo], u1, dw1[oo][c]);
+                }
+            }
+            stvec<TX, 8>(gx + vox0 * C + 8 * pc, ov);
+            xq = xn;
+            gq = gn;
+        }
+    }  // bricks
     // partial row of this brick: per-wave shuffle sums, then the 4 waves in order
     {
         auto put = [&](int e, float v) {
@@ -592,11 +600,11 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
 #pragma unroll
             for (int w = 0; w < NT / 64; ++w) t += red[w * NE + e];
         }
-        part[int64_t(blockIdx.x) * NE + e] = t;  // the brick's row: one contiguous write
+        part[int64_t(blockIdx.x) * NE + e] = t;  // the workgroup's row: one contiguous write
     }
 }
 
-// Fixed-order sum of the brick rows [brick][NE]: stage 1, workgroup r sums bricks
+// Fixed-order sum of the partial rows [row][NE]: stage 1, workgroup r sums rows
 // [r * RCH, (r + 1) * RCH) per entry (threads over entries: coalesced rows) into part2[r][e];
 // stage 2 sums the stage-1 rows per entry in order and adds into the gradient buffers.
 constexpr int RCH = 128;
@@ -671,6 +679,18 @@ constexpr size_t bwd_lds() {
            size_t(4 * n_entries<C, BR>()) * 4;
 }
 
+// persistent backward: max(512, bricks / 16) workgroups (a multiple of 8: XCD-contiguous ranges),
+// each reducing its bricks' partial sums in registers into one partial row (measured: (4, 2) at
+// 512^2 x 128, 32,768 bricks: 771 us one brick per workgroup, 746 at 1,024 workgroups, 641 at
+// 2,048, 644 at 4,096; (8, 4) at 256^2 x 64, 4,096 bricks: 256 / 185 at 512 / 216 at 2,048)
+int col_wg(int nbricks) {
+    static const int env = [] {  // timing experiments only: VQ3D_COL_WG fixes the cap (read once)
+        const char *e = std::getenv("VQ3D_COL_WG");
+        return e ? std::atoi(e) : 0;
+    }();
+    return env > 0 ? env : std::max(512, (nbricks / 16) & ~7);
+}
+
 CArgs make_args(int B, int H, int W, int D) {
     CArgs a;
     a.B = B;
@@ -682,6 +702,7 @@ CArgs make_args(int B, int H, int W, int D) {
     a.nbd = D / BD;
     a.nbricks = B * a.nbh * a.nbw * a.nbd;
     a.xcd = a.nbricks <= 4096;
+    a.nwg = std::min(a.nbricks, col_wg(a.nbricks));
     return a;
 }
 
@@ -712,13 +733,13 @@ void launch_bwd(const CArgs &a, const void *g, const void *x, const h16_t *t2, c
         attr = true;
     }
     if (stages & 1)
-        k_col_bwd<C, BR, TX, TO><<<a.nbricks, NT, bwd_lds<C, BR>(), s>>>(a, static_cast<const TO *>(g),
-                                                                         static_cast<const TX *>(x), t2, t3, w1, w2, w3,
-                                                                         p, part, static_cast<TX *>(gx));
-    const int nr = (a.nbricks + RCH - 1) / RCH;
-    float *part2 = part + size_t(a.nbricks) * n_entries<C, BR>();
+        k_col_bwd<C, BR, TX, TO><<<a.nwg, NT, bwd_lds<C, BR>(), s>>>(a, static_cast<const TO *>(g),
+                                                                     static_cast<const TX *>(x), t2, t3, w1, w2, w3, p,
+                                                                     part, static_cast<TX *>(gx));
+    const int nr = (a.nwg + RCH - 1) / RCH;
+    float *part2 = part + size_t(a.nwg) * n_entries<C, BR>();
     if (stages & 2) {
-        k_col_reduce1<C, BR><<<nr, 256, 0, s>>>(part, a.nbricks, part2);
+        k_col_reduce1<C, BR><<<nr, 256, 0, s>>>(part, a.nwg, part2);
         k_col_reduce2<C, BR><<<(n_entries<C, BR>() + 255) / 256, 256, 0, s>>>(part2, nr, p.scale, gr);
     }
 }
@@ -748,10 +769,10 @@ void bwd_io(int xdt, int odt, const CArgs &a, const void *g, const void *x, cons
 template <int C, int BR>
 void launch_reduce_run(const CArgs &a, int nblocks, float *ws, size_t stride_f, float *const *gtab,
                        const float *const *ptab, hipStream_t s) {
-    const int nr = (a.nbricks + RCH - 1) / RCH;
-    k_col_reduce1_run<C, BR><<<dim3(nr, nblocks), 256, 0, s>>>(ws, stride_f, a.nbricks);
-    k_col_reduce2_run<C, BR><<<dim3((n_entries<C, BR>() + 255) / 256, nblocks), 256, 0, s>>>(ws, stride_f, a.nbricks,
-                                                                                        nr, gtab, ptab);
+    const int nr = (a.nwg + RCH - 1) / RCH;
+    k_col_reduce1_run<C, BR><<<dim3(nr, nblocks), 256, 0, s>>>(ws, stride_f, a.nwg);
+    k_col_reduce2_run<C, BR><<<dim3((n_entries<C, BR>() + 255) / 256, nblocks), 256, 0, s>>>(ws, stride_f, a.nwg, nr,
+                                                                                        gtab, ptab);
 }
 
 int col_reduce_run(int nblocks, int batch, int C, int BR, int h, int w, int d, void *workspaces, size_t stride,
@@ -775,7 +796,7 @@ size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d) {
     if (!col_supported(batch, C, BR, h, w, d)) return 0;
     const CArgs a = make_args(batch, h, w, d);
     const int ne = C == 2 ? n_entries<2, 1>() : C == 4 ? n_entries<4, 2>() : n_entries<8, 4>();
-    return (size_t(a.nbricks) + (a.nbricks + RCH - 1) / RCH) * ne * 4;
+    return (size_t(a.nwg) + (a.nwg + RCH - 1) / RCH) * ne * 4;
 }
 
 int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1,
