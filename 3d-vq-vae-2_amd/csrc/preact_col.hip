@@ -46,6 +46,9 @@
 #ifndef COL_EXP
 #define COL_EXP 0
 #endif
+#ifndef FWD_PERSIST
+#define FWD_PERSIST 1  // the forward walks brick ranges too (its grid: CArgs::nwg)
+#endif
 
 namespace vq3d {
 
@@ -265,103 +268,110 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
     float *accs = reinterpret_cast<float *>(t2h + HVX * BR + PADE);  // [NV][BR] raw W2 (*) t2
     int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
-    const Org o = brick_org(a, a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x));
     const Scal s = load_scal(p);
     hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, false>(w2, k, lane);
-    line_table(a, o, lbase);
     for (int i = tid; i < PADE; i += NT) t2h[HVX * BR + i] = 0;
-    __syncthreads();
-    // A. t2 on the halo, every x load issued first
-    {
-        constexpr int P = (HVX + NT - 1) / NT;
-        Raw<TX, C> xv[P];
-#pragma unroll
-        for (int u = 0; u < P; ++u) {
-            int line, pos;
-            const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
-            xv[u] = (COL_EXP & 1) ? Raw<TX, C>{} : ldraw<TX, C>(x + int64_t(vx) * C);
-        }
-#pragma unroll
-        for (int u = 0; u < P; ++u) {
-            const int q = tid + u * NT;
-            if (!(COL_EXP & 2) && q < HVX) {
-                float xf[C], t[BR];
-                unraw<TX, C>(xv[u], xf);
-#pragma unroll
-                for (int c = 0; c < C; ++c) xf[c] = elu_f(xf[c] + s.b1a) + s.b1b;
-#pragma unroll
-                for (int oo = 0; oo < BR; ++oo) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int c = 0; c < C; ++c) acc = fmaf(w1[oo * C + c], xf[c], acc);
-                    t[oo] = elu_f(acc + s.b2a) + s.b2b;
-                }
-                *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = packv<BR>(t);
-            }
-        }
-    }
-    __syncthreads();
-    // this thread's 4 voxels (phase C): brick line ln, D-group dg; x in flight during phase B
-    const int ln = tid / (BD / DV), dg = tid % (BD / DV);
-    const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
-    const Raw<TX, DV * C> xr = ldraw<TX, DV * C>(x + vox0 * C);
-    // B. raw W2 (*) t2 per m-tile
     int woff[K::KS];
     win_offsets<BR>(row, kb, woff);
+    // persistent (FWD_PERSIST): the workgroup walks an XCD-contiguous brick range
+    const TileSched sc = FWD_PERSIST ? xcd_sched(a.nbricks)
+                                     : TileSched{a.xcd ? xcd_tile(a.nbricks) : int(blockIdx.x), a.nbricks, a.nbricks};
+#pragma unroll 1
+    for (int brick = sc.t; brick < sc.end; brick += sc.step) {
+        const Org o = brick_org(a, brick);
+        __syncthreads();  // the previous brick's readers of the LDS tiles are done
+        line_table(a, o, lbase);
+        __syncthreads();
+        // A. t2 on the halo, every x load issued first
+        {
+            constexpr int P = (HVX + NT - 1) / NT;
+            Raw<TX, C> xv[P];
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                int line, pos;
+                const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
+                xv[u] = (COL_EXP & 1) ? Raw<TX, C>{} : ldraw<TX, C>(x + int64_t(vx) * C);
+            }
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const int q = tid + u * NT;
+                if (!(COL_EXP & 2) && q < HVX) {
+                    float xf[C], t[BR];
+                    unraw<TX, C>(xv[u], xf);
+#pragma unroll
+                    for (int c = 0; c < C; ++c) xf[c] = elu_f(xf[c] + s.b1a) + s.b1b;
+#pragma unroll
+                    for (int oo = 0; oo < BR; ++oo) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int c = 0; c < C; ++c) acc = fmaf(w1[oo * C + c], xf[c], acc);
+                        t[oo] = elu_f(acc + s.b2a) + s.b2b;
+                    }
+                    *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = packv<BR>(t);
+                }
+            }
+        }
+        __syncthreads();
+        // this thread's 4 voxels (phase C): brick line ln, D-group dg; x in flight during phase B
+        const int ln = tid / (BD / DV), dg = tid % (BD / DV);
+        const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
+        const Raw<TX, DV * C> xr = ldraw<TX, DV * C>(x + vox0 * C);
+        // B. raw W2 (*) t2 per m-tile
 #pragma unroll 4
-    for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        const int wb = win_base(mt, BR);
+        for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            const int wb = win_base(mt, BR);
 #pragma unroll
-        for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, wb + woff[k]), fw[k], acc);
-        if (row < BR) {
+            for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, wb + woff[k]), fw[k], acc);
+            if (row < BR) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+                for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+            }
         }
-    }
-    __syncthreads();
-    // C. t3 and out of the thread's 4 voxels (and their t2, saved for the backward)
-    if constexpr ((COL_EXP & 16) != 0) return;
-    const int v0 = ln * BD + dg * DV;
-    if (t2o) {
-        const h16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
-        uint32_t w[DV * BR / 2];
-        if constexpr (BR == 1) {  // 4 positions at an odd element offset
-            const uint4 u4 = __builtin_bit_cast(uint4, read8(t2h, int(src - t2h)));
-            w[0] = u4.x, w[1] = u4.y;
-        } else {
+        __syncthreads();
+        // C. t3 and out of the thread's 4 voxels (and their t2, saved for the backward)
+        if constexpr ((COL_EXP & 16) != 0) continue;
+        const int v0 = ln * BD + dg * DV;
+        if (t2o) {
+            const h16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
+            uint32_t w[DV * BR / 2];
+            if constexpr (BR == 1) {  // 4 positions at an odd element offset
+                const uint4 u4 = __builtin_bit_cast(uint4, read8(t2h, int(src - t2h)));
+                w[0] = u4.x, w[1] = u4.y;
+            } else {
 #pragma unroll
-            for (int i = 0; i < DV * BR / 2; ++i) w[i] = reinterpret_cast<const uint32_t *>(src)[i];
+                for (int i = 0; i < DV * BR / 2; ++i) w[i] = reinterpret_cast<const uint32_t *>(src)[i];
+            }
+            store_words<DV * BR / 2>(t2o + vox0 * BR, w);
         }
-        store_words<DV * BR / 2>(t2o + vox0 * BR, w);
-    }
-    float t3v[DV][BR];
+        float t3v[DV][BR];
 #pragma unroll
-    for (int i = 0; i < DV; ++i)
+        for (int i = 0; i < DV; ++i)
 #pragma unroll
-        for (int oo = 0; oo < BR; ++oo) t3v[i][oo] = rbf(elu_f(accs[acc_at(v0 + i, BR) + oo] + s.b3a) + s.b3b);
-    {
-        uint32_t w[DV * BR / 2];
+            for (int oo = 0; oo < BR; ++oo) t3v[i][oo] = rbf(elu_f(accs[acc_at(v0 + i, BR) + oo] + s.b3a) + s.b3b);
+        {
+            uint32_t w[DV * BR / 2];
 #pragma unroll
-        for (int i = 0; i < DV * BR / 2; ++i) {
-            const int e0 = 2 * i, e1 = 2 * i + 1;
-            w[i] = uint32_t(f2h(t3v[e0 / BR][e0 % BR])) | (uint32_t(f2h(t3v[e1 / BR][e1 % BR])) << 16);
+            for (int i = 0; i < DV * BR / 2; ++i) {
+                const int e0 = 2 * i, e1 = 2 * i + 1;
+                w[i] = uint32_t(f2h(t3v[e0 / BR][e0 % BR])) | (uint32_t(f2h(t3v[e1 / BR][e1 % BR])) << 16);
+            }
+            if (t3o) store_words<DV * BR / 2>(t3o + vox0 * BR, w);  // NULL: eval forward, nothing saved
         }
-        if (t3o) store_words<DV * BR / 2>(t3o + vox0 * BR, w);  // NULL: eval forward, nothing saved
-    }
-    float xf[DV * C];
-    unraw<TX, DV * C>(xr, xf);
+        float xf[DV * C];
+        unraw<TX, DV * C>(xr, xf);
 #pragma unroll
-    for (int e = 0; e < DV * C; ++e) {
-        const int vv = e / C, c = e - vv * C;
-        float r = 0.f;
+        for (int e = 0; e < DV * C; ++e) {
+            const int vv = e / C, c = e - vv * C;
+            float r = 0.f;
 #pragma unroll
-        for (int oo = 0; oo < BR; ++oo) r = fmaf(w3[c * BR + oo], t3v[vv][oo], r);
-        xf[e] = r * s.sc + s.b4 + xf[e];
-    }
-    stvec<TO, DV * C>(out + vox0 * C, xf);
+            for (int oo = 0; oo < BR; ++oo) r = fmaf(w3[c * BR + oo], t3v[vv][oo], r);
+            xf[e] = r * s.sc + s.b4 + xf[e];
+        }
+        stvec<TO, DV * C>(out + vox0 * C, xf);
+    }  // bricks
 }
 
 // ============================================================================================ backward
@@ -720,8 +730,8 @@ void launch_fwd(const CArgs &a, const void *x, const float *w1, const float *w2,
         allow(k_col_fwd<C, BR, TX, TO>, fwd_lds<C, BR>());
         attr = true;
     }
-    k_col_fwd<C, BR, TX, TO><<<a.nbricks, NT, fwd_lds<C, BR>(), s>>>(a, static_cast<const TX *>(x), w1, w2, w3, p,
-                                                                     static_cast<TO *>(out), t2, t3);
+    k_col_fwd<C, BR, TX, TO><<<FWD_PERSIST ? a.nwg : a.nbricks, NT, fwd_lds<C, BR>(), s>>>(
+        a, static_cast<const TX *>(x), w1, w2, w3, p, static_cast<TO *>(out), t2, t3);
 }
 template <int C, int BR, typename TX, typename TO>
 void launch_bwd(const CArgs &a, const void *g, const void *x, const h16_t *t2, const h16_t *t3, const float *w1,
