@@ -1096,27 +1096,35 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
 // wrap copies).  Chunks of one workgroup are consecutive and each XCD takes a contiguous eighth of
 // them (the halo re-reads hit that XCD's L2).
 constexpr int NT9 = 9 * 64;
-#ifndef W2_PAD
-#define W2_PAD 4  // t2 channel-stride padding (elements, even); timing experiments: make exp EXPDEF=W2_PAD
-#endif
+// t2 is staged as THREE copies shifted by kd - 1 positions, copy kd holding position j + kd - 1
+// (circular) at index j of each D-line, so the B operand of lane (kd, ci) -- 8 consecutive
+// positions starting at d0 + kd - 1 -- is ONE aligned 16-byte read (a single unshifted copy needs
+// five dword reads and four v_alignbyte per operand, 9 waves x 16 k-steps x 2 per chunk).  The
+// channel stride CS has CS / 8 = 1 and the copy stride CK = 9 CS has CK / 8 = 9 (mod 16), so the 16
+// lanes of a lane group read 16 distinct 16-byte bank slots.  Copy 1 is the items' transpose;
+// copies 0 and 2 are built from it (dword reads + v_alignbyte once per row group, not per use).
 template <int D>
 struct W2c {
     static constexpr int NL = CHV / D;  // lines per chunk
     static constexpr int TH = NL >= 64 ? 8 : NL >= 16 ? 4 : NL >= 4 ? 2 : 1, TW = NL / TH;
     static constexpr int LW = TW + 2, HL = (TH + 2) * LW;  // halo lines
     static constexpr int GPL = D / 8;                       // 8-voxel groups per line
-    static constexpr int RP = D + 16;                       // t2 row: position p at index p + 8
-    // per channel: + 4 elements (8 B) so the 9 channel rows of one B-operand read spread over the
-    // banks (2-way at most; a 16-B multiple stride puts them 3- to 9-way on one bank)
-    static constexpr int CSTR = HL * RP + W2_PAD;
+    static constexpr int CS = 8 * (HL * D / 8 + ((1 - HL * D / 8) % 16 + 16) % 16);  // channel stride
+    static constexpr int CK = 9 * CS;                       // copy stride
     static constexpr int ZI = NL * GPL, TI = HL * GPL;      // staging items (gz3, t2)
     static constexpr int NPC = (ZI + TI) * 9;               // 16-B pieces per chunk
     static constexpr int NP = (NPC + NT9 - 1) / NT9;        // pieces per thread
-    static constexpr int TSZ = (BR * CSTR + 7) & ~7;        // t2 rows, rounded to 16 B (the raw area's b128s)
     static constexpr int RAW = (ZI + TI) * 72;              // voxel-major staging area (elements)
-    static constexpr size_t LDS = size_t(16 * ZP + TSZ + RAW) * 2;
+    static constexpr int NRG = BR * HL * GPL;               // row groups of copies 0 / 2 to build
+    // the raw area after the copies, or (when that would not fit) over copy 2: dead once the items
+    // are transposed, before copy 2 is built (one more barrier per chunk then)
+    static constexpr bool ALIAS = size_t(16 * ZP + 3 * CK + RAW) * 2 > 160 * 1024;
+    static constexpr int RAWO = ALIAS ? 2 * CK : 3 * CK;    // raw offset in the t2 area
+    static constexpr size_t LDS = size_t(16 * ZP + (ALIAS ? std::max(3 * CK, 2 * CK + RAW) : 3 * CK + RAW)) * 2;
     static_assert(NL * D == CHV && TH * TW == NL && D % 8 == 0, "chunk");
     static_assert(ZI + TI <= NT9, "one staging item per thread");
+    static_assert((CS / 8) % 16 == 1 && (CK / 8) % 16 == 9, "bank slots");
+    static_assert(LDS <= 160 * 1024, "LDS");
 };
 
 // element e (0..71) of a staged 8-voxel x 9-channel item (voxel-major, 16-bit)
@@ -1142,8 +1150,8 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
     using K = W2c<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     h16_t *zT = reinterpret_cast<h16_t *>(smem);  // gz3 [16][ZP] channel-major (rows >= 9 never read into results)
-    h16_t *tT = zT + 16 * ZP;                      // t2 [9][HL][RP]
-    h16_t *raw = tT + K::TSZ;                      // [items][72] voxel-major (16-B aligned)
+    h16_t *tT = zT + 16 * ZP;                      // t2 copies [3 (kd)][9][HL][D] (strides CK, CS)
+    h16_t *raw = tT + K::RAWO;                     // [items][72] voxel-major (16-B aligned)
     const int tid = threadIdx.x, lane = tid & 63, kk = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int kh = kk / 3, kw = kk - 3 * kh;
     const int nth = a.H / K::TH, ntw = a.W / K::TW;
@@ -1156,7 +1164,7 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
         const int e = min(16 * n + row, 26), kd = e / BR, ci = e - kd * BR;
-        toff[n] = ci * K::CSTR + kd;
+        toff[n] = kd * K::CK + ci * K::CS;
     }
     u32x4 v[K::NP];
     auto load = [&](int c) {
@@ -1184,15 +1192,16 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
     const bool zitem = tid < K::ZI, titem = !zitem && tid < K::ZI + K::TI;
     const int it = zitem ? tid : min(tid - K::ZI, K::TI - 1);
     const int il = it / K::GPL, ig = it - il * K::GPL;
-    h16_t *dst = zitem ? zT + il * D + 8 * ig : tT + il * K::RP + 8 + 8 * ig;
-    const int pitch = zitem ? ZP : K::CSTR;
+    h16_t *dst = zitem ? zT + il * D + 8 * ig : tT + K::CK + il * D + 8 * ig;  // copy 1
+    const int pitch = zitem ? ZP : K::CS;
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int cend = min(c0 + npc, nchunk);
     if (c0 < cend) load(c0);
 #pragma unroll 1
     for (int c = c0; c < cend; ++c) {
+        if constexpr (K::ALIAS) __syncthreads();  // the previous chunk's readers of copy 2 (= raw) are done
 #pragma unroll
-        for (int u = 0; u < K::NP; ++u) {  // raw pieces (the area's previous readers passed the last barrier)
+        for (int u = 0; u < K::NP; ++u) {  // raw pieces (non-aliased: the area's readers passed the last barrier)
             const int p = tid + u * NT9;
             if (p < K::NPC) reinterpret_cast<u32x4 *>(raw)[p] = v[u];
         }
@@ -1209,31 +1218,23 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
                 w[4 * j + 3] = q.w;
             }
 #pragma unroll
-            for (int ch = 0; ch < BR; ++ch) {
-                const u32x4 r = item_row(w, ch);
-                if (zitem || W2_PAD % 8 == 0) {
-                    *reinterpret_cast<u32x4 *>(dst + ch * pitch) = r;
-                } else if (W2_PAD % 4 == 0) {  // t2 rows 8-B aligned
-                    reinterpret_cast<u32x2 *>(dst + ch * pitch)[0] = u32x2{r.x, r.y};
-                    reinterpret_cast<u32x2 *>(dst + ch * pitch)[1] = u32x2{r.z, r.w};
-                } else {  // 4-B aligned
-                    uint32_t *q = reinterpret_cast<uint32_t *>(dst + ch * pitch);
-                    q[0] = r.x;
-                    q[1] = r.y;
-                    q[2] = r.z;
-                    q[3] = r.w;
-                }
-            }
-            if (titem) {  // circular wrap copies: position -1 = D - 1, position D = 0
-                if (ig == K::GPL - 1) {
-#pragma unroll
-                    for (int ch = 0; ch < BR; ++ch) dst[ch * pitch - 1 - 8 * ig] = h16_t(item_el(w, 63 + ch));  // index 7
-                }
-                if (ig == 0) {
-#pragma unroll
-                    for (int ch = 0; ch < BR; ++ch) dst[ch * pitch + D] = h16_t(item_el(w, ch));  // index D + 8
-                }
-            }
+            for (int ch = 0; ch < BR; ++ch) *reinterpret_cast<u32x4 *>(dst + ch * pitch) = item_row(w, ch);
+        }
+        __syncthreads();  // copy 1 complete (and raw dead)
+        // copies 0 and 2 of row group (channel, line, group) from copy 1: dwords 4g - 1 .. 4g + 4
+        // of the line (circular), each output dword one v_alignbyte
+        for (int q = tid; q < K::NRG; q += NT9) {
+            const int g = q % K::GPL, lr = q / K::GPL;  // lr = channel * HL + line
+            const uint32_t *r1 = reinterpret_cast<const uint32_t *>(tT + K::CK + (lr / K::HL) * K::CS + (lr % K::HL) * D);
+            const u32x4 m = reinterpret_cast<const u32x4 *>(r1)[g];
+            const uint32_t um = r1[g == 0 ? D / 2 - 1 : 4 * g - 1], up = r1[g == K::GPL - 1 ? 0 : 4 * g + 4];
+            const size_t ro = size_t(lr / K::HL) * K::CS + (lr % K::HL) * D + 8 * g;
+            *reinterpret_cast<u32x4 *>(tT + ro) =
+                u32x4{__builtin_amdgcn_alignbyte(m.x, um, 2), __builtin_amdgcn_alignbyte(m.y, m.x, 2),
+                      __builtin_amdgcn_alignbyte(m.z, m.y, 2), __builtin_amdgcn_alignbyte(m.w, m.z, 2)};
+            *reinterpret_cast<u32x4 *>(tT + 2 * K::CK + ro) =
+                u32x4{__builtin_amdgcn_alignbyte(m.y, m.x, 2), __builtin_amdgcn_alignbyte(m.z, m.y, 2),
+                      __builtin_amdgcn_alignbyte(m.w, m.z, 2), __builtin_amdgcn_alignbyte(up, m.w, 2)};
         }
         __syncthreads();
         if (c + 1 < cend) load(c + 1);
@@ -1242,9 +1243,9 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
             const int vv = 32 * ks + 8 * kb, l = vv / D, d0 = vv - l * D;
             const int hl = (l / K::TW + kh) * K::LW + l % K::TW + kw;
             const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + vv);
-            const int off = hl * K::RP + d0 + 7;  // position d0 - 1 + kd at index d0 + 7 + kd
+            const int off = hl * D + d0;  // copy kd: position d0 - 1 + kd at index d0
 #pragma unroll
-            for (int n = 0; n < 2; ++n) acc[n] = mfma(af, read8(tT, toff[n] + off), acc[n]);
+            for (int n = 0; n < 2; ++n) acc[n] = mfma(af, *reinterpret_cast<const hx8 *>(tT + toff[n] + off), acc[n]);
         }
     }
     float *dstp = p2a + (int64_t(bid) * 9 + kk) * NER;
