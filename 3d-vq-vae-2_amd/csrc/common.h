@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <atomic>
 
 // The kernel sources are compiled twice (Makefile): with bf16 as the 16-bit activation / matrix-
 // core operand format, and with -DVQ3D_FP16 with IEEE fp16 (the reference trains with fp16 AMP,
@@ -283,6 +284,75 @@ __device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {
 #pragma unroll
     for (int i = 0; i < NT / 64; ++i) t += scratch[i];
     return t;
+}
+
+// ---------------------------------------------------------------- in-grid partial sums
+// A grid's per-workgroup partials summed by its LAST workgroup to finish, in the order a separate
+// one-workgroup pass over them would use (deterministic, bit-identical to that pass) without the
+// extra launch.  The hand-off needs no release fence (which would write back the XCD's whole L2,
+// the kernel's outputs included: measured 17.7 -> 44 us on a 1024-workgroup 1x1 conv): each
+// workgroup's lane 0 stores its {pre, post} pair write-through (relaxed agent-scope 8-byte store),
+// drains it, then takes a completion ticket (agent-scope adds); the workgroup whose add completes
+// the grid reads every pair with agent-scope (L1-bypassing) loads -- MI355X_MICROARCH.md's
+// hand-off table, first row.  The ticket is two-level: same-address atomics serialise (one
+// counter for 1,024 workgroups added ~11 us), so workgroup b adds to shard b % 16 (counters a
+// 128-B line apart) and the workgroup completing a shard adds to the top counter.  Tickets: a
+// per-module array, the host hands each launch the next slot (ticket_slot), the finishing
+// workgroup re-arms it to 0; a slot is reused 64 launches later.
+constexpr unsigned kTickets = 64, kShards = 16, kTicketLine = 32;
+static __device__ unsigned g_tickets[kTickets * (kShards + 1) * kTicketLine];
+static inline unsigned ticket_slot() {
+    static std::atomic<unsigned> next{0};
+    return next.fetch_add(1, std::memory_order_relaxed) % kTickets;
+}
+// every thread of the (1-D, NT-thread) workgroup calls this with the workgroup's sums in thread 0;
+// part holds nb {pre, post} float pairs; *dpre += the pres' sum, *dpost += the posts'
+template <int NT>
+__device__ __forceinline__ void finish_partials(float *part, int nb, int bid, float pre, float post, float *dpre,
+                                                float *dpost, unsigned slot, float *red /* >= 8 */) {
+    static_assert(NT > int(kShards), "one re-arming thread per counter");
+    __shared__ unsigned last;
+    uint64_t *pp = reinterpret_cast<uint64_t *>(part);
+    unsigned *tk = g_tickets + slot * (kShards + 1) * kTicketLine;
+    const int nsh = min(nb, int(kShards));
+    if (threadIdx.x == 0) {
+        const uint64_t v = uint64_t(__float_as_uint(pre)) | (uint64_t(__float_as_uint(post)) << 32);
+        __hip_atomic_store(pp + bid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int sh = bid % int(kShards);
+        const unsigned nin = unsigned((nb - sh + int(kShards) - 1) / int(kShards));  // workgroups of the shard
+        bool l = atomicAdd(tk + sh * kTicketLine, 1u) == nin - 1;
+        if (l) l = atomicAdd(tk + kShards * kTicketLine, 1u) == unsigned(nsh - 1);
+        last = l;
+    }
+    __syncthreads();
+    if (!last) return;
+    // every load of a pass in flight before the first add (one dependent cross-XCD round trip per
+    // strided load); summed in the strided order all the same
+    constexpr int PASS = 8;
+    float s0 = 0.f, s1 = 0.f;
+    for (int i0 = threadIdx.x; i0 < nb; i0 += PASS * NT) {
+        uint64_t v[PASS];
+#pragma unroll
+        for (int u = 0; u < PASS; ++u) {
+            const int i = min(i0 + u * NT, nb - 1);
+            v[u] = __hip_atomic_load(pp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int u = 0; u < PASS; ++u)
+            if (i0 + u * NT < nb) {
+                s0 += __uint_as_float(uint32_t(v[u]));
+                s1 += __uint_as_float(uint32_t(v[u] >> 32));
+            }
+    }
+    s0 = block_sum<float, NT>(s0, red);
+    s1 = block_sum<float, NT>(s1, red + 4);
+    if (threadIdx.x == 0) {
+        if (dpre) *dpre += s0;
+        if (dpost) *dpost += s1;
+    }
+    if (threadIdx.x < nsh) atomicExch(tk + threadIdx.x * kTicketLine, 0u);
+    if (threadIdx.x == kShards) atomicExch(tk + kShards * kTicketLine, 0u);
 }
 
 // ---------------------------------------------------------------- trilinear x2 (align_corners=False)

@@ -102,7 +102,7 @@ template <typename T, int COT, bool DGRAD>
 __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in, const T *__restrict__ in2,
                                             const float *__restrict__ w, FwdEpi<T> fe, BwdEpi<T> be,
                                             const float *__restrict__ gscale, T *__restrict__ out,
-                                            T *__restrict__ out2, float *dpre, float *dpost, float *part) {
+                                            T *__restrict__ out2, float *dpre, float *dpost, float *part, unsigned slot) {
     extern __shared__ __attribute__((aligned(16))) float ws[];  // [N pad COT][CinP] then slabs
     __shared__ float red[8];
     const int tid = threadIdx.x;
@@ -233,32 +233,12 @@ __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in,
     if (DGRAD && (dpre || dpost)) {
         pre = block_sum<float, SEG>(pre, red);
         post = block_sum<float, SEG>(post, red + 4);
-        if (tid == 0) {
-            if (part) {  // per-workgroup partials, summed in order by k_sum_partials
-                part[blockIdx.x] = pre;
-                part[gridDim.x + blockIdx.x] = post;
-            } else {
-                if (dpre) atomicAdd(dpre, pre);
-                if (dpost) atomicAdd(dpost, post);
-            }
+        if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
+            finish_partials<256>(part, int(gridDim.x), int(blockIdx.x), pre, post, dpre, dpost, slot, red);
+        } else if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
         }
-    }
-}
-
-// *dpre += sum(part[0..n)), *dpost += sum(part[n..2n)) in a fixed order (one workgroup)
-__global__ __launch_bounds__(256) void k_sum_partials(const float *__restrict__ part, int n, float *dpre,
-                                                     float *dpost) {
-    __shared__ float red[8];
-    float s0 = 0.f, s1 = 0.f;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        s0 += part[i];
-        s1 += part[n + i];
-    }
-    s0 = block_sum<float, 256>(s0, red);
-    s1 = block_sum<float, 256>(s1, red + 4);
-    if (threadIdx.x == 0) {
-        if (dpre) *dpre += s0;
-        if (dpost) *dpost += s1;
     }
 }
 
@@ -340,7 +320,7 @@ template <typename T, int CI, int CO, bool DGRAD>
 __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restrict__ in, const float *__restrict__ w,
                                                 int pro_kind, const float *pro_a, const float *pro_b,
                                                 FwdEpi<T> fe, BwdEpi<T> be, const float *__restrict__ gscale,
-                                                T *__restrict__ out, float *dpre, float *dpost, float *part,
+                                                T *__restrict__ out, float *dpre, float *dpost, float *part, unsigned slot,
                                                 FastDiv fD, FastDiv fW, FastDiv fH) {
     __shared__ float wsh[CO * CI];
     __shared__ float red[8];
@@ -437,14 +417,11 @@ __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restri
     if (DGRAD && (dpre || dpost)) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (part) {
-                part[blockIdx.x] = pre;
-                part[gridDim.x + blockIdx.x] = post;
-            } else {
-                if (dpre) atomicAdd(dpre, pre);
-                if (dpost) atomicAdd(dpost, post);
-            }
+        if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
+            finish_partials<256>(part, int(gridDim.x), int(blockIdx.x), pre, post, dpre, dpost, slot, red);
+        } else if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
         }
     }
 }
@@ -552,7 +529,7 @@ template <typename T, bool DG, int OPT>
 __global__ __launch_bounds__(256) void k_pw_sg(SgArgs s, ConvArgs ca, const T *__restrict__ in,
                                               const T *__restrict__ in2, const float *__restrict__ w, FwdEpi<T> fe,
                                               BwdEpi<T> be, const float *__restrict__ gscale, T *__restrict__ out,
-                                              T *__restrict__ out2, float *dpre, float *dpost, float *part) {
+                                              T *__restrict__ out2, float *dpre, float *dpost, float *part, unsigned slot) {
     __shared__ float red[8];
     const int o0 = blockIdx.y * OPT;
     const Prologue pro = make_prologue(DG ? VQ3D_PRO_NONE : ca.pro_kind, ca.pro_a, ca.pro_b);
@@ -574,15 +551,11 @@ __global__ __launch_bounds__(256) void k_pw_sg(SgArgs s, ConvArgs ca, const T *_
     if (DG && (dpre || dpost)) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            const int nb = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
-            if (part) {
-                part[bid] = pre;
-                part[nb + bid] = post;
-            } else {
-                if (dpre) atomicAdd(dpre, pre);
-                if (dpost) atomicAdd(dpost, post);
-            }
+        if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
+            finish_partials<256>(part, int(gridDim.x * gridDim.y), int(blockIdx.y * gridDim.x + blockIdx.x), pre, post, dpre, dpost, slot, red);
+        } else if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
         }
     }
 }
@@ -629,14 +602,15 @@ static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, con
     const bool want_part = dgrad && (dpre || dpost);
     const int nb = int(nbx) * ny;
     float *part = (want_part && nb > 1024 && ws && ws_bytes >= size_t(2) * nb * 4) ? static_cast<float *>(ws) : nullptr;
+    const unsigned tk = part ? ticket_slot() : 0u;
 #define SG(O)                                                                                                    \
     case O:                                                                                                      \
         if (dgrad)                                                                                               \
             k_pw_sg<T, true, O><<<grid, 256, 0, st>>>(s, ca, (const T *)in, nullptr, w, fe, be, gscale, (T *)out, \
-                                                      (T *)out2, dpre, dpost, part);                             \
+                                                      (T *)out2, dpre, dpost, part, tk);                         \
         else                                                                                                     \
             k_pw_sg<T, false, O><<<grid, 256, 0, st>>>(s, ca, (const T *)in, (const T *)in2, w, fe, be, nullptr,  \
-                                                       (T *)out, nullptr, nullptr, nullptr, nullptr);            \
+                                                       (T *)out, nullptr, nullptr, nullptr, nullptr, 0u);        \
         break;
     switch (opt) {
         SG(1)
@@ -646,7 +620,6 @@ static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, con
         SG(16)
     }
 #undef SG
-    if (part) k_sum_partials<<<1, 256, 0, st>>>(part, nb, dpre, dpost);
     return check_launch(dgrad ? "conv3d_bwd_data(pointwise sg)" : "conv3d_fwd(pointwise sg)");
 }
 
@@ -694,7 +667,7 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
                                                const h16_t *__restrict__ in2, const float *__restrict__ w,
                                                FwdEpi<h16_t> fe, BwdEpi<h16_t> be, const float *__restrict__ gscale,
                                                h16_t *__restrict__ out, h16_t *__restrict__ out2, float *dpre,
-                                               float *dpost, float *part) {
+                                               float *dpost, float *part, unsigned slot) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     u32x4 *wB = reinterpret_cast<u32x4 *>(smem);  // [KS][NTN][64]: this workgroup's NTN n-tiles
     __shared__ float red[8];
@@ -827,15 +800,11 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
     if (DG && (dpre || dpost)) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (tid == 0) {
-            const int nb = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
-            if (part) {
-                part[bid] = pre;
-                part[nb + bid] = post;
-            } else {
-                if (dpre) atomicAdd(dpre, pre);
-                if (dpost) atomicAdd(dpost, post);
-            }
+        if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
+            finish_partials<256>(part, int(gridDim.x * gridDim.y), int(blockIdx.y * gridDim.x + blockIdx.x), pre, post, dpre, dpost, slot, red);
+        } else if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
         }
     }
 }
@@ -872,14 +841,15 @@ static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, c
     const dim3 nb{nbx, unsigned(ny), 1u};
     const bool want_part = dgrad && (dpre || dpost);
     float *part = (want_part && ws && ws_bytes >= size_t(2) * nbx * ny * 4) ? static_cast<float *>(ws) : nullptr;
+    const unsigned tk = part ? ticket_slot() : 0u;
     ConvArgs ca = make_args(d, pa, pb);
 #define MM(NT_)                                                                                                 \
     if (dgrad)                                                                                                  \
         k_pw_mma<NT_, true><<<nb, 256, lds, s>>>(m, ca, (const h16_t *)in, nullptr, w, fe, be, gscale,         \
-                                                 (h16_t *)out, (h16_t *)out2, dpre, dpost, part);             \
+                                                 (h16_t *)out, (h16_t *)out2, dpre, dpost, part, tk);         \
     else                                                                                                        \
         k_pw_mma<NT_, false><<<nb, 256, lds, s>>>(m, ca, (const h16_t *)in, (const h16_t *)in2, w, fe, be,    \
-                                                  nullptr, (h16_t *)out, nullptr, nullptr, nullptr, nullptr);
+                                                  nullptr, (h16_t *)out, nullptr, nullptr, nullptr, nullptr, 0u);
     switch (NTN) {
     case 1: MM(1) break;
     case 2: MM(2) break;
@@ -887,7 +857,6 @@ static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, c
     default: MM(8) break;
     }
 #undef MM
-    if (part) k_sum_partials<<<1, 256, 0, s>>>(part, int(nbx) * ny, dpre, dpost);
     return true;
 }
 
@@ -917,6 +886,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
         const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
         const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 1023) / 1024, kMaxPwBlocks)));
         float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
+        const unsigned tk = part ? ticket_slot() : 0u;
         const int key = ci * 16 + co;
         const int pk = dgrad ? VQ3D_PRO_NONE : d->pro_kind;
         const FastDiv fD(uint32_t(d->out_d)), fW(uint32_t(d->out_w)), fH(uint32_t(d->out_h));
@@ -924,10 +894,10 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     case CI * 16 + CO:                                                                                         \
         if (dgrad)                                                                                             \
             k_pw_rows<T, CI, CO, true><<<nbx, 256, 0, s>>>(nvox, (const T *)in, w, pk, pa, pb, fe, be, gscale, \
-                                                           (T *)out, dpre, dpost, part, fD, fW, fH);           \
+                                                           (T *)out, dpre, dpost, part, tk, fD, fW, fH);       \
         else                                                                                                   \
             k_pw_rows<T, CI, CO, false><<<nbx, 256, 0, s>>>(nvox, (const T *)in, w, pk, pa, pb, fe, be,       \
-                                                            nullptr, (T *)out, nullptr, nullptr, nullptr, fD,  \
+                                                            nullptr, (T *)out, nullptr, nullptr, nullptr, 0u, fD, \
                                                             fW, fH);                                           \
         break;
         switch (key) {
@@ -936,7 +906,6 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
         default: return fail("conv(pointwise): no row kernel");
         }
 #undef R
-        if (part) k_sum_partials<<<1, 256, 0, s>>>(part, int(nbx), dpre, dpost);
         return check_launch(dgrad ? "conv3d_bwd_data(pointwise rows)" : "conv3d_fwd(pointwise rows)");
     }
     // ---- LDS slabs
@@ -994,6 +963,7 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     const int slab_cap = std::min(kMaxPwBlocks, 1024);  // measured: 1024 >= 2048 > 512 workgroups
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, slab_cap)));
     float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
+    const unsigned tk = part ? ticket_slot() : 0u;
 #define L(C)                                                                                                    \
     case C: {                                                                                                   \
         auto kern = dgrad ? k_pw2<T, C, true> : k_pw2<T, C, false>;                                             \
@@ -1007,11 +977,10 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
             attr = true;                                                                                        \
         }                                                                                                       \
         kern<<<nbx, SEG, lds, s>>>(a, (const T *)in, (const T *)in2, w, fe, be, gscale, (T *)out, (T *)out2,    \
-                                   dpre, dpost, part);                                                          \
+                                   dpre, dpost, part, tk);                                                      \
     } break;
     switch (cot) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
-    if (part) k_sum_partials<<<1, 256, 0, s>>>(part, int(nbx), dpre, dpost);
     return check_launch(dgrad ? "conv3d_bwd_data(pointwise)" : "conv3d_fwd(pointwise)");
 }
 
