@@ -60,14 +60,14 @@ def preact_run(fn, x, plan):
 def upsample(x):
     lb = _library()
     if lb is not None:
-        return torch.ops.vq3d.upsample2x(x)
+        return lb.upsample(x)
     return UpsampleFn.apply(x)
 
 
 def parse_input(x, w, b, half):
     lb = _library()
     if lb is not None:
-        return torch.ops.vq3d.parse_input(x, w, b, half)[0]
+        return lb.parse_input(x, w, b, half)
     return ParseInputFn.apply(x, w, b, half)
 
 
@@ -81,7 +81,7 @@ def quantize(z, q):
 def recon_loss(dec, x, nvs, cylinder, *commit):
     lb = _library()
     if lb is not None:
-        total, recon = torch.ops.vq3d.recon_loss(dec, x, nvs, bool(cylinder), list(commit))[:2]
+        total, recon = lb.recon_loss(dec, x, nvs, cylinder, *commit)
         return total, recon
     return ReconLossFn.apply(dec, x, nvs, cylinder, *commit)
 

@@ -129,8 +129,58 @@ def _check_grads(params, grads):
             raise ValueError("vq3d: `grads` must be the parameters' .grad buffers (vq3d.flat.FlatParams)")
 
 
+def _needs(ctx, n):
+    """needs_input_grad of the first n inputs (under _Call: of its differentiable inputs)"""
+    return list(ctx.needs) if hasattr(ctx, "needs") else list(ctx.needs_input_grad[:n])
+
+
 def _save_flag(*ts):
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in _flat(ts))
+
+
+# ------------------------------------------------------------------------------------------------ calls
+_BELOW = torch._C._AutoDispatchBelowAutograd
+_FORMULAS = {}  # operator -> (setup_context, backward, differentiable input positions)
+
+
+class _Call(torch.autograd.Function):
+    """One differentiable operator of this module, dispatched BELOW the autograd key, with its
+    registered formula (the setup_context / backward given to torch.library.register_autograd)
+    applied by this Function: the same gradients as calling torch.ops.vq3d.<op> under autograd,
+    without the custom-op autograd layer's Python cost (~30 us of a ~45 us call; the step's ~700
+    calls otherwise outrun the GPU).  `tracked`: the operator's differentiable inputs (in
+    `_FORMULAS` order), then the parameter edges (Fn.param_edges) the node needs to exist."""
+
+    @staticmethod
+    def forward(ctx, name, args, *tracked):
+        setup, _, diff = _FORMULAS[name]
+        ctx.name, ctx.ntr = name, len(tracked)
+        ctx.needs = [t is not None and t.requires_grad for t in tracked[:3]]  # conv3d's x, x2, residual
+        with _BELOW():
+            out = getattr(torch.ops.vq3d, name)(*args)
+        setup(ctx, args, out)
+        return tuple(out) if isinstance(out, (list, tuple)) else out
+
+    @staticmethod
+    def backward(ctx, *grads):
+        _, bwd, diff = _FORMULAS[ctx.name]
+        with _BELOW():
+            res = bwd(ctx, list(grads) if len(grads) > 1 or ctx.name != "upsample2x" else grads[0])
+        res = res if isinstance(res, tuple) else (res,)
+        gs = []
+        for i in diff:  # a list input (recon_loss's commitment losses) contributes one gradient per tensor
+            gs.extend(res[i] if isinstance(res[i], list) else [res[i]])
+        return (None, None) + tuple(gs) + (None,) * (ctx.ntr - len(gs))
+
+
+def _register(name, bwd, setup, diff):
+    torch.library.register_autograd(f"vq3d::{name}", bwd, setup_context=setup)
+    _FORMULAS[name] = (setup, bwd, diff)
+
+
+def _call(name, args, diff_inputs, params=()):
+    """torch.ops.vq3d.<name>(*args) with autograd through _Call."""
+    return _Call.apply(name, args, *diff_inputs, *Fn.param_edges(params, *diff_inputs))
 
 
 # ------------------------------------------------------------------------------------------------ block views
@@ -226,13 +276,13 @@ def _conv_bwd(ctx, grads):
     spec = _spec(weight, scale, bias, cbias, pro, geom, residual_up2, post_elu)
     g = grads[0]
     res = torch.ops.vq3d.conv3d_backward(g, ctx.saved, weight, scale, bias, cbias, pro, geom, residual_up2, post_elu,
-                                         ctx.has_res, list(ctx.needs_input_grad[:3]),
+                                         ctx.has_res, _needs(ctx, 3),
                                          [Fn.grad_buf(t) for t in spec.tensors])
     gx, gx2, gres = _grads_of(res, [g])[:3]
     return gx, gx2, gres, None, None, None, None, [None] * len(pro), None, None, None, None
 
 
-torch.library.register_autograd("vq3d::conv3d", _conv_bwd, setup_context=_conv_setup)
+_register("conv3d", _conv_bwd, _conv_setup, (0, 1, 2))
 
 
 def conv(x, spec, x2=None, residual=None):
@@ -240,8 +290,9 @@ def conv(x, spec, x2=None, residual=None):
     pro = list(spec.pro) if spec.pro else []
     save = _save_flag(x, x2, residual, *spec.tensors)
     g = spec.geom
-    return torch.ops.vq3d.conv3d(x, x2, residual, spec.w, spec.scale, spec.bias, spec.cbias, pro,
-                                 [g.k, g.s, g.p, int(g.circular)], spec.residual_up2, spec.post_elu, save)[0]
+    args = (x, x2, residual, spec.w, spec.scale, spec.bias, spec.cbias, pro, [g.k, g.s, g.p, int(g.circular)],
+            spec.residual_up2, spec.post_elu, save)
+    return _call("conv3d", args, (x, x2, residual), spec.tensors)[0]
 
 
 # ------------------------------------------------------------------------------------------------ blocks
@@ -275,13 +326,13 @@ def _block_bwd(ctx, grads):
     return _grads_of(res, [g])[0], [None] * len(ctx.params), None, None
 
 
-torch.library.register_autograd("vq3d::preact_block", _block_bwd, setup_context=_block_setup)
+_register("preact_block", _block_bwd, _block_setup, (0,))
 
 
 def block(x, blk):
     """Fn.PreActBlockFn through the registered operator."""
     params = list(blk._fn_params)
-    return torch.ops.vq3d.preact_block(x, params, blk.mode, _save_flag(x, *params))[0]
+    return _call("preact_block", (x, params, blk.mode, _save_flag(x, *params)), (x,), params)[0]
 
 
 @torch.library.custom_op("vq3d::preact_run", mutates_args=())
@@ -317,14 +368,14 @@ def _run_bwd(ctx, grads):
     return _grads_of(res, [g])[0], [None] * len(ctx.params), None, None, None
 
 
-torch.library.register_autograd("vq3d::preact_run", _run_bwd, setup_context=_run_setup)
+_register("preact_run", _run_bwd, _run_setup, (0,))
 
 
 def run(fn, x, plan):
     """A run Function (Fn.PreAct{Stack,Wide,MidRun,SmallRun}Fn) through the registered operator."""
     params = [p for b in plan.blocks for p in b._fn_params]
-    return torch.ops.vq3d.preact_run(x, params, RUN_KINDS[fn], plan.out_dtype is torch.float32,
-                                     _save_flag(x, *params))[0]
+    args = (x, params, RUN_KINDS[fn], plan.out_dtype is torch.float32, _save_flag(x, *params))
+    return _call("preact_run", args, (x,), params)[0]
 
 
 # ------------------------------------------------------------------------------------------------ quantizer
@@ -370,7 +421,7 @@ def _vq_bwd(ctx, grads):
     return torch.ops.vq3d.vq_nearest_backward(z, embed, idx, ctx.coef, grads[0], grads[1]), None, None, None
 
 
-torch.library.register_autograd("vq3d::vq_nearest", _vq_bwd, setup_context=_vq_setup)
+_register("vq_nearest", _vq_bwd, _vq_setup, (0,))
 
 
 @torch.library.custom_op("vq3d::vq_ema", mutates_args=("embed", "embed_avg", "cluster_size", "ema_slot"))
@@ -387,13 +438,15 @@ def quantize(z, q):
     autograd-registered operator, on the pre-update codebook), EMA statistics."""
     z = ops.as_cl(z)
     if q.training and q.first_pass_host:
-        torch.ops.vq3d.vq_init(z.detach(), q.embed, q.embed_avg, q.cluster_size, q.first_pass)
+        with _BELOW():  # mutating, no autograd formula
+            torch.ops.vq3d.vq_init(z.detach(), q.embed, q.embed_avg, q.cluster_size, q.first_pass)
         q.first_pass_host = False
     embed = ops.copy_(torch.empty_like(q.embed), q.embed) if q.training else q.embed
-    loss, zst, idx = torch.ops.vq3d.vq_nearest(z, embed, float(q.commitment_cost), getattr(q, "zst_dtype", None))
+    loss, zst, idx = _call("vq_nearest", (z, embed, float(q.commitment_cost), getattr(q, "zst_dtype", None)), (z,))
     if q.training:
-        torch.ops.vq3d.vq_ema(z.detach(), idx, q.embed, q.embed_avg, q.cluster_size, q.ema_slot, float(q.decay),
-                              float(q.laplace_alpha))
+        with _BELOW():
+            torch.ops.vq3d.vq_ema(z.detach(), idx, q.embed, q.embed_avg, q.cluster_size, q.ema_slot, float(q.decay),
+                                  float(q.laplace_alpha))
     return loss, zst, idx
 
 
@@ -422,7 +475,7 @@ def _pi_bwd(ctx, grads):
     return None, None, None, None
 
 
-torch.library.register_autograd("vq3d::parse_input", _pi_bwd, setup_context=_pi_setup)
+_register("parse_input", _pi_bwd, _pi_setup, (0, 1, 2))
 
 
 @torch.library.custom_op("vq3d::upsample2x", mutates_args=())
@@ -445,7 +498,7 @@ def _up_bwd(ctx, g):
     return torch.ops.vq3d.upsample2x_backward(g, ctx.shape)
 
 
-torch.library.register_autograd("vq3d::upsample2x", _up_bwd, setup_context=_up_setup)
+_register("upsample2x", _up_bwd, _up_setup, (0,))
 
 
 @torch.library.custom_op("vq3d::recon_loss", mutates_args=())
@@ -472,7 +525,19 @@ def _loss_bwd(ctx, grads):
     return gs[0], None, None, None, list(gs[4:])
 
 
-torch.library.register_autograd("vq3d::recon_loss", _loss_bwd, setup_context=_loss_setup)
+_register("recon_loss", _loss_bwd, _loss_setup, (0, 4))
+
+
+def upsample(x):
+    return _call("upsample2x", (x,), (x,))
+
+
+def parse_input(x, w, b, half):
+    return _call("parse_input", (x, w, b, half), (x, w, b))[0]
+
+
+def recon_loss(dec, x, nvs, cylinder, *commit):
+    return _call("recon_loss", (dec, x, nvs, bool(cylinder), list(commit)), (dec, *commit))[:2]
 
 
 OPS = ("conv3d", "conv3d_backward", "preact_block", "preact_block_backward", "preact_run", "preact_run_backward",

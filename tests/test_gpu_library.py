@@ -108,8 +108,9 @@ def test_library_step_matches_ctypes(gpu, name):
 
 
 def test_library_ops_are_the_kernels(gpu):
-    """A circular 3x3x3 conv through torch.ops.vq3d.conv3d (+ its autograd backward) against
-    vq3d.functional.conv: output and input gradient bit for bit; the weight / bias gradients
+    """A circular 3x3x3 conv through the library binding (lb.conv: the operator below the autograd
+    key + its formula), and through torch.ops.vq3d.conv3d called directly under autograd (the
+    register_autograd formula), against vq3d.functional.conv: output and input gradient bit for bit; the weight / bias gradients
     (fp32 atomics, see above) within 1e-5."""
     from vq3d import functional as Fn
     from vq3d import library as lb
@@ -120,8 +121,11 @@ def test_library_ops_are_the_kernels(gpu):
     FlatParams(conv.parameters(), gpu)
     x = torch.randn(1, 8, 16, 16, 16, device=gpu).bfloat16().contiguous(memory_format=torch.channels_last_3d)
     spec = Fn.ConvSpec(conv.weight, ConvGeom(3, 1, 1, True), cbias=conv.bias)
+    def direct(xa, spec):  # the registered operator under autograd (torch.library.register_autograd)
+        return torch.ops.vq3d.conv3d(xa, None, None, spec.w, None, None, spec.cbias, [], [3, 1, 1, 1], False, False,
+                                     True)[0]
     out = []
-    for path in (Fn.conv, lb.conv):
+    for path in (Fn.conv, lb.conv, direct):
         conv.weight.grad.zero_()
         conv.bias.grad.zero_()
         xa = x.clone().requires_grad_(True)
@@ -129,7 +133,8 @@ def test_library_ops_are_the_kernels(gpu):
         y.float().square().sum().backward()
         torch.cuda.synchronize()
         out.append((y.detach().clone(), xa.grad.clone(), conv.weight.grad.clone(), conv.bias.grad.clone()))
-    (ya, gxa, gwa, gba), (yb, gxb, gwb, gbb) = out
-    assert torch.equal(ya, yb)
-    assert torch.equal(gxa, gxb)
-    assert _rel(gwb, gwa) <= 1e-5 and _rel(gbb, gba) <= 1e-5, (_rel(gwb, gwa), _rel(gbb, gba))
+    (ya, gxa, gwa, gba) = out[0]
+    for yb, gxb, gwb, gbb in out[1:]:
+        assert torch.equal(ya, yb)
+        assert torch.equal(gxa, gxb)
+        assert _rel(gwb, gwa) <= 1e-5 and _rel(gbb, gba) <= 1e-5, (_rel(gwb, gwa), _rel(gbb, gba))
