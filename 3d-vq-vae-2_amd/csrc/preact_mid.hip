@@ -61,6 +61,12 @@
 #define PM_SB 1
 #endif
 // minimum waves per SIMD the backward-data tile kernel is compiled for (2: at most 256 registers)
+#ifndef PM_FREG
+#define PM_FREG 1  // k_pm_bwd2: the 12 weight fragments in registers for the whole run (else one LDS read per use)
+#endif
+#ifndef PM_FREG_FWD
+#define PM_FREG_FWD 0  // k_pm_fwd likewise (it runs 3 workgroups per CU on 64 VGPRs)
+#endif
 #ifndef PM_BWD_WPE
 #define PM_BWD_WPE 2
 #endif
@@ -740,6 +746,17 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
         frag[f * 64 + lane] = fr;
     }
     __syncthreads();  // the weights are read: the halo images' pads can be zeroed
+    // the A fragments in registers for the whole run (PM_FREG: 48 VGPRs; two waves per SIMD leave
+    // room) -- an LDS read per use put a ~100-cycle wait in front of every 1x1 stage's MFMA
+    hx8 fr[PM_FREG ? 12 : 1];
+    if constexpr (PM_FREG) {
+#pragma unroll
+        for (int f = 0; f < 12; ++f) fr[f] = frag[f * 64 + lane];
+    }
+    auto wf = [&](int f, int l) -> hx8 {
+        if constexpr (PM_FREG) return fr[f];
+        else return frag[f * 64 + l];
+    };
     zero_pads_q(img, 2);
     const Scal s = load_scal(p);
     Scal sp{};
@@ -787,8 +804,10 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             for (int r = 0; r < 2; ++r) load_ep(et2B, et3B, exB, egB, lane, o1, r);
         }
     }
-    auto body = [&](HaloQ &hz, Raw9 (&et2)[2], Raw9 (&et3)[2], Raw18 (&ex)[2], Raw18 (&eg)[2], int tile, int it) {
-        const Org o = tile_org_q(a, tile);
+    // o: the tile's origin (carried from the previous tile's `on` at depth 1: one set of runtime
+    // divisions per tile); returns the origin of the tile DEPTH steps ahead
+    auto body = [&](HaloQ &hz, Raw9 (&et2)[2], Raw9 (&et3)[2], Raw18 (&ex)[2], Raw18 (&eg)[2], int tile, int it,
+                    const Org o) -> Org {
         const int tn = tile + DEPTH * sc.step;
         const Org on = tile_org_q(a, tn < sc.end ? tn : tile);
         const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
@@ -810,7 +829,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
                         const int kh = i - r;
-                        if (kh >= 0 && kh < 3) acc[r] = mfma(frag[(kh * 3 + j) * 64 + ln], bw, acc[r]);
+                        if (kh >= 0 && kh < 3) acc[r] = mfma(wf(kh * 3 + j, ln), bw, acc[r]);
                     }
                 }
                 asm volatile("" ::: "memory");  // one row of windows in registers at a time
@@ -835,8 +854,8 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             float gxv[6];
             if constexpr (!(PM_EXP & 64)) {
                 const hx8 bz = pack8({z1[0], z1[1], z1[2], z1[3], 0.f, 0.f, 0.f, 0.f});
-                const f32x4 a0 = mfma(frag[9 * 64 + ln], bz, f32x4{0.f, 0.f, 0.f, 0.f});
-                const f32x4 a1 = mfma(frag[10 * 64 + ln], bz, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a0 = mfma(wf(9, ln), bz, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a1 = mfma(wf(10, ln), bz, f32x4{0.f, 0.f, 0.f, 0.f});
                 const Raw18 &xr = ex[r], &gr = eg[r];
                 const float xv[6] = {bf(xr.x & 0xffffu), bf(xr.x >> 16), bf(xr.y & 0xffffu), bf(xr.y >> 16),
                                      bf(xr.z & 0xffffu), bf(xr.z >> 16)};
@@ -866,7 +885,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                 // of gx in the k_chan18 order)
                 if constexpr (!(PM_EXP & 128)) {
                     const hx8 bg = pack8({gxv[0], gxv[1], gxv[2], gxv[3], gxv[4], gxv[5], 0.f, 0.f});
-                    const f32x4 a3 = mfma(frag[11 * 64 + ln], bg, f32x4{0.f, 0.f, 0.f, 0.f});
+                    const f32x4 a3 = mfma(wf(11, ln), bg, f32x4{0.f, 0.f, 0.f, 0.f});
                     float t3v[4], zq[4];
                     ex9(et3[r], v, kl, t3v);
 #pragma unroll
@@ -889,15 +908,18 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             if constexpr (!(PM_EXP & 512)) load_ep(et2, et3, ex, eg, ln, on, r);
             if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);  // one run's epilogue at a time (no interleaving)
         }
+        return on;
     };
     if constexpr (DEPTH == 1) {
         int it = 0;
-        for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) body(hzA, et2A, et3A, exA, egA, tile, it);
+        Org o = tile_org_q(a, sc.t < sc.end ? sc.t : 0);
+        for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) o = body(hzA, et2A, et3A, exA, egA, tile, it, o);
     } else {
         int it = 0;
         for (int tile = sc.t; tile < sc.end; tile += 2 * sc.step, it += 2) {
-            body(hzA, et2A, et3A, exA, egA, tile, it);
-            if (tile + sc.step < sc.end) body(hzB, et2B, et3B, exB, egB, tile + sc.step, it + 1);
+            body(hzA, et2A, et3A, exA, egA, tile, it, tile_org_q(a, tile));
+            if (tile + sc.step < sc.end)
+                body(hzB, et2B, et3B, exB, egB, tile + sc.step, it + 1, tile_org_q(a, tile + sc.step));
         }
     }
     if constexpr (CHAIN) {
@@ -975,6 +997,15 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
         frag[f * 64 + lane] = fr;
     }
     __syncthreads();
+    hx8 fr[PM_FREG_FWD ? 12 : 1];  // as k_pm_bwd2 (PM_FREG_FWD)
+    if constexpr (PM_FREG_FWD) {
+#pragma unroll
+        for (int f = 0; f < 12; ++f) fr[f] = frag[f * 64 + lane];
+    }
+    auto wf = [&](int f, int l) -> hx8 {
+        if constexpr (PM_FREG_FWD) return fr[f];
+        else return frag[f * 64 + l];
+    };
     zero_pads_q(img, 2);
     const Scal s = load_scal(p);
     Scal sn{};
@@ -997,8 +1028,8 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
         for (int r = 0; r < 2; ++r) ex[r] = ld18(x, run_vox0(o0, r) + n, kb);
     }
     int it = 0;
+    Org o = tile_org_q(a, sc.t < sc.end ? sc.t : 0);  // carried: one set of runtime divisions per tile
     for (int tile = sc.t; tile < sc.end; tile += sc.step, ++it) {
-        const Org o = tile_org_q(a, tile);
         const bool more = tile + sc.step < sc.end;
         const Org on = tile_org_q(a, more ? tile + sc.step : tile);
         const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
@@ -1018,7 +1049,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
                         const int kh = i - r;
-                        if (kh >= 0 && kh < 3) acc[r] = mfma(frag[(kh * 3 + j) * 64 + ln], bw, acc[r]);
+                        if (kh >= 0 && kh < 3) acc[r] = mfma(wf(kh * 3 + j, ln), bw, acc[r]);
                     }
                 }
                 asm volatile("" ::: "memory");  // one row of windows in registers at a time
@@ -1035,8 +1066,8 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             float ov[6];
             if constexpr (!(PM_EXP & 2)) {
                 const hx8 bt = pack8({t3v[0], t3v[1], t3v[2], t3v[3], 0.f, 0.f, 0.f, 0.f});
-                const f32x4 a0 = mfma(frag[9 * 64 + ln], bt, f32x4{0.f, 0.f, 0.f, 0.f});
-                const f32x4 a1 = mfma(frag[10 * 64 + ln], bt, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a0 = mfma(wf(9, ln), bt, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a1 = mfma(wf(10, ln), bt, f32x4{0.f, 0.f, 0.f, 0.f});
                 const Raw18 &xr = ex[r];
                 const float xv[6] = {bf(xr.x & 0xffffu), bf(xr.x >> 16), bf(xr.y & 0xffffu), bf(xr.y >> 16),
                                      bf(xr.z & 0xffffu), bf(xr.z >> 16)};
@@ -1063,7 +1094,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                     u1[j] = ok ? bf(f2h(elu_fast(ov[j] + sn.b1a) + sn.b1b)) : 0.f;
                 }
                 const hx8 bu = pack8({u1[0], u1[1], u1[2], u1[3], u1[4], u1[5], 0.f, 0.f});
-                const f32x4 a2 = mfma(frag[11 * 64 + ln], bu, f32x4{0.f, 0.f, 0.f, 0.f});
+                const f32x4 a2 = mfma(wf(11, ln), bu, f32x4{0.f, 0.f, 0.f, 0.f});
                 float tn[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) tn[j] = elu_fast(a2[j] + sn.b2a) + sn.b2b;
@@ -1075,6 +1106,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             if constexpr (!(PM_EXP & 2048)) ex[r] = ld18(x, run_vox0(on, r) + nl, kl);  // next tile's x (unconditional)
             if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);
         }
+        o = on;
     }
 }
 
