@@ -27,6 +27,9 @@ gives a bit-identical step (tests/test_gpu_library.py).  Operator contracts:
     [codes, new...] for the input gradients in the same encoding over its own tensor inputs;
   * parameters are operator inputs, so autograd sees every edge; their gradients arrive through
     `grads`, and the autograd formulas return None for them.
+The model's layers (set_binding("library")) reach the operators through `_Call`: the operator
+dispatched below the autograd key, its registered formula applied by one autograd.Function (a
+direct torch.ops.vq3d call under autograd uses the same formula through register_autograd).
 No fake (meta-device) kernels are registered: the operators are for eager execution and HIP-graph
 capture of it, not for tracing compilers."""
 from typing import List, Optional
