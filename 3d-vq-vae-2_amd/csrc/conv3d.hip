@@ -555,11 +555,9 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
                 m.a.pro_a = pa;
                 m.a.pro_b = pb;
                 m.a.wCt = Ct;
-                if (d->cout <= 64)  // MFMA engine holds up to 4 tiles of 16 output channels
-                    return launch_wgrad_mfma(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
-                                             dbias, dcbias, s);
-                return launch_wgrad_tiled(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
-                                          dbias, dcbias, s);
+                // up to 4 tiles of 16 output channels per workgroup, more as 64-channel chunks
+                return launch_wgrad_mfma(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
+                                         dbias, dcbias, s);
             }
         }
     }

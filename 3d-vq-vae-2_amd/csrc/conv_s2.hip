@@ -16,6 +16,8 @@ namespace vq3d {
 
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 struct S2Args {
     int B, Cin1, Cin2, Cin, Cout;
     int iH, iW, iD, oH, oW, oD;
@@ -313,6 +315,140 @@ __global__ __launch_bounds__(256) void k_dgrad_s2_pair(S2Args a, const T *__rest
     }
 }
 
+
+// Matrix-core form for the wide layers (one input, Cin % 16 == 0, Cout % 8 == 0: the down blocks'
+// branch conv2 4x4x4 and skip conv 2x2x2 from 16 channels up, vqvae/layers.py:124-126,164-171).
+// blockIdx.y = the (h, w, d) parity class of the input voxels: every voxel of a class meets the
+// same (k/2)^3 taps, so per class the backward-data is one GEMM
+//     gx^T[ci][v] = sum over (j, co) of W[co][ci][tap_j] * g[o_j(v)][co]
+// with K = (k/2)^3 * Cout.  The weights are the MFMA A operand (so each lane's accumulator holds 4
+// consecutive input channels of one voxel: one 8-byte store), packed per (channel tile, k-step)
+// into LDS once per workgroup; the g rows are B (8 consecutive co of one tap: one 16-byte load per
+// lane and k-step).  The epilogue is k_dgrad_s2's (activation derivative from aux, addend, gscale,
+// prologue-scalar partial sums).
+__device__ __forceinline__ int s2_src(int i, int t, int p, int n_in, int n_out, int circ) {
+    int r = i + p - t;
+    if (circ) r = r < 0 ? r + n_in : (r >= n_in ? r - n_in : r);
+    else if (r < 0) return -1;
+    r >>= 1;
+    return r < n_out ? r : -1;
+}
+
+template <int K, int NTM>
+__global__ __launch_bounds__(256) void k_dgrad_s2_mma(S2Args a, const h16_t *__restrict__ g,
+                                                     const float *__restrict__ gscale, const float *__restrict__ w,
+                                                     BwdEpi<h16_t> be, h16_t *__restrict__ gx, float *dpre,
+                                                     float *dpost, int nks) {
+    constexpr int NT_ = K / 2, NJ = NT_ * NT_ * NT_, K3 = K * K * K;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint4 *afr = reinterpret_cast<uint4 *>(smem);  // [NTM][nks][64] packed A fragments
+    __shared__ float red[8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, n = lane & 15;
+    const int cls = int(blockIdx.y), rh = cls >> 2, rw = (cls >> 1) & 1, rd = cls & 1;
+    const int t0h = (rh + a.p) & 1, t0w = (rw + a.p) & 1, t0d = (rd + a.p) & 1;  // the class's first taps
+    const int c0 = int(blockIdx.z) * NTM * 16;
+    for (int idx = tid; idx < NTM * nks * 64; idx += 256) {
+        const int l = idx & 63, r = idx >> 6, s = r % nks, mt = r / nks;
+        const int ci = c0 + 16 * mt + (l & 15);
+        const int f0 = 32 * s + 8 * (l >> 4), j = f0 / a.Cout, co0 = f0 - j * a.Cout;
+        uint32_t u[4] = {0u, 0u, 0u, 0u};
+        if (j < NJ) {
+            const int xd = j % NT_, xw = (j / NT_) % NT_, xh = j / (NT_ * NT_);
+            const int tap = ((t0h + 2 * xh) * K + t0w + 2 * xw) * K + t0d + 2 * xd;
+            const float *wp = w + (int64_t(co0) * a.Cin + ci) * K3 + tap;
+            const int64_t st_ = int64_t(a.Cin) * K3;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                u[e] = uint32_t(f2h(wp[(2 * e) * st_])) | (uint32_t(f2h(wp[(2 * e + 1) * st_])) << 16);
+        }
+        afr[idx] = uint4{u[0], u[1], u[2], u[3]};
+    }
+    __syncthreads();
+    ActDeriv dv;
+    dv.mode = be.aux ? be.mode : 0;
+    dv.p = (dv.mode && be.p) ? *be.p : 0.f;
+    const float gs = gscale ? *gscale : 1.f;
+    float pre = 0.f, post = 0.f;
+    const int hh = a.iH >> 1, hw = a.iW >> 1, hd = a.iD >> 1;
+    const int nvc = a.B * hh * hw * hd;  // voxels of the class
+    const int ntile = (nvc + 15) >> 4;
+    for (int t = int(blockIdx.x) * 4 + wave; t < ntile; t += int(gridDim.x) * 4) {
+        const int vi = 16 * t + n;
+        const bool live = vi < nvc;
+        int q = live ? vi : 0;
+        const int md = q % hd;
+        q /= hd;
+        const int mw = q % hw;
+        q /= hw;
+        const int mh = q % hh;
+        const int b = q / hh;
+        const int ih = 2 * mh + rh, iw = 2 * mw + rw, id = 2 * md + rd;
+        int oh[NT_], ow[NT_], od[NT_];
+#pragma unroll
+        for (int x = 0; x < NT_; ++x) {
+            oh[x] = s2_src(ih, t0h + 2 * x, a.p, a.iH, a.oH, a.circ);
+            ow[x] = s2_src(iw, t0w + 2 * x, a.p, a.iW, a.oW, a.circ);
+            od[x] = s2_src(id, t0d + 2 * x, a.p, a.iD, a.oD, a.circ);
+        }
+        f32x4 acc[NTM];
+#pragma unroll
+        for (int m = 0; m < NTM; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // the lane's k entries of step s: tap j, channels co .. co + 7 (advanced by 32 per step)
+        int j = (8 * kb) / a.Cout, co = 8 * kb - j * a.Cout;
+#pragma unroll 4
+        for (int s = 0; s < nks; ++s) {
+            uint4 bv = uint4{0u, 0u, 0u, 0u};
+            if (live && j < NJ) {
+                const int xd = j % NT_, xw = (j / NT_) % NT_, xh = j / (NT_ * NT_);
+                const int hh_ = NT_ == 1 ? oh[0] : (xh ? oh[NT_ - 1] : oh[0]);
+                const int ww_ = NT_ == 1 ? ow[0] : (xw ? ow[NT_ - 1] : ow[0]);
+                const int dd_ = NT_ == 1 ? od[0] : (xd ? od[NT_ - 1] : od[0]);
+                if (hh_ >= 0 && ww_ >= 0 && dd_ >= 0)
+                    bv = *reinterpret_cast<const uint4 *>(
+                        g + ((((int64_t(b) * a.oH + hh_) * a.oW + ww_) * a.oD + dd_) * a.Cout + co));
+            }
+            const hx8 bf = __builtin_bit_cast(hx8, bv);
+#pragma unroll
+            for (int m = 0; m < NTM; ++m)
+                acc[m] = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, afr[(m * nks + s) * 64 + lane]), bf, acc[m], 0, 0, 0);
+            co += 32;
+            while (co >= a.Cout) {
+                co -= a.Cout;
+                ++j;
+            }
+        }
+        if (!live) continue;
+        const int64_t vox = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + id;
+#pragma unroll
+        for (int m = 0; m < NTM; ++m) {
+            const int64_t o = vox * a.Cin + c0 + 16 * m + 4 * kb;
+            float aux[4], add[4], v[4];
+            if (dv.mode) load_row<h16_t, 4>(be.aux + o, aux);
+            if (be.addend) load_row<h16_t, 4>(be.addend + o, add);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float val = acc[m][c];
+                if (gscale) val = val * gs;
+                pre += val;
+                if (dv.mode) val = val * dv(aux[c]);
+                post += val;
+                if (be.addend) val = val + add[c];
+                v[c] = val;
+            }
+            *reinterpret_cast<uint2 *>(gx + o) = uint2{uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16),
+                                                       uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16)};
+        }
+    }
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        if (threadIdx.x == 0) {
+            if (dpre) atomicAdd(dpre, pre);
+            if (dpost) atomicAdd(dpost, post);
+        }
+    }
+}
+
 }  // namespace
 
 bool dgrad_s2_applicable(const vq3d_conv_desc *d) {
@@ -340,7 +476,10 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
     if (int64_t(a.B) * a.iH * a.iW * a.iD >= (int64_t(1) << 31)) return fail("conv3d_bwd_data(s2): grid too large");
     {
         auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-        if (std::is_same<T, h16_t>::value && a.circ && a.Cin2 == 0 && (a.Cin == 4 || a.Cin == 8) &&
+        // k = 2, p = 0: every tap lands inside the grid, so the padding mode does not matter (the
+        // down blocks' zero-padded skip conv takes the circular pair kernel)
+        if (std::is_same<T, h16_t>::value && (a.circ || (a.k == 2 && a.p == 0)) && a.Cin2 == 0 &&
+            (a.Cin == 4 || a.Cin == 8) &&
             (a.Cout == 4 || a.Cout == 8) && a.p == a.k / 2 - 1 && a.iH == 2 * a.oH && a.iW == 2 * a.oW &&
             a.iD == 2 * a.oD && al16(g) && al16(gx) && (!be.aux || al16(be.aux)) && (!be.addend || al16(be.addend))) {
             S2Args c = a;
@@ -357,6 +496,36 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
             }
             PK(4, 4, 4) PK(4, 8, 4) PK(8, 4, 4) PK(8, 8, 4) PK(4, 4, 2) PK(4, 8, 2) PK(8, 4, 2) PK(8, 8, 2)
 #undef PK
+        }
+    }
+    if constexpr (std::is_same<T, h16_t>::value) {
+        // matrix-core parity classes: one input, 16-channel input tiles, 8-channel g rows, K >= 32
+        auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+        const int nj = (a.k / 2) * (a.k / 2) * (a.k / 2);
+        if (a.Cin2 == 0 && a.Cin % 16 == 0 && a.Cout % 8 == 0 && nj * a.Cout >= 32 && al16(g) && al16(gx) &&
+            (!be.aux || al16(be.aux)) && (!be.addend || al16(be.addend)) &&
+            int64_t(a.B) * a.oH * a.oW * a.oD * a.Cout < (int64_t(1) << 31)) {
+            const int nks = (nj * a.Cout + 31) / 32;
+            const int64_t nvc = int64_t(a.B) * (a.iH / 2) * (a.iW / 2) * (a.iD / 2);
+            int ntm = 4;
+            while (ntm > 1 && (a.Cin % (16 * ntm) || size_t(ntm) * nks * 1024 > 48 * 1024)) ntm /= 2;
+            if (nvc <= 4096) ntm = 1;  // few voxels: spread the channel tiles over workgroups instead
+            if (size_t(ntm) * nks * 1024 <= 48 * 1024) {
+                const int nz = a.Cin / (16 * ntm);
+                const int64_t ntile = (nvc + 15) / 16;
+                const unsigned gxn = unsigned(std::max<int64_t>(1, std::min<int64_t>((ntile + 3) / 4,
+                                                                                     std::max(1, 2048 / (8 * nz)))));
+                const dim3 grid(gxn, 8u, unsigned(nz));
+                const size_t lds = size_t(ntm) * nks * 1024;
+#define MM(K_, NTM_)                                                                                          \
+                if (a.k == K_ && ntm == NTM_) {                                                                  \
+                    k_dgrad_s2_mma<K_, NTM_><<<grid, 256, lds, s>>>(a, (const h16_t *)g, gscale, w, be,           \
+                                                                   (h16_t *)gx, dpre, dpost, nks);               \
+                    return check_launch("conv3d_bwd_data(s2 mma)");                                              \
+                }
+                MM(2, 1) MM(2, 2) MM(2, 4) MM(4, 1) MM(4, 2) MM(4, 4)
+#undef MM
+            }
         }
     }
     const int K3 = a.k * a.k * a.k;

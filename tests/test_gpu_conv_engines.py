@@ -121,7 +121,18 @@ def test_mfma_dual_input_and_residual(gpu, half):
     assert rel(out.float(), ref) < 1.5e-2
 
 
-@pytest.mark.parametrize("case", CASES)
+# more than 64 output channels: the MFMA weight gradient in 64-channel chunks (the top level's
+# stride-2 down convs and 128-channel branch convs), incl. a partial last chunk
+WGRAD_WIDE = [
+    (64, 128, (8, 8, 4), 4, 2, 1, True),
+    (128, 128, (8, 8, 4), 4, 2, 1, True),
+    (16, 96, (8, 8, 4), 3, 1, 1, True),
+    (32, 72, (6, 6, 4), 4, 2, 1, False),
+    (128, 256, (8, 8, 4), 2, 2, 0, False),
+]
+
+
+@pytest.mark.parametrize("case", CASES + WGRAD_WIDE)
 @pytest.mark.parametrize("half", HALF)
 def test_tiled_wgrad_matches_valu(gpu, case, half):
     """bf16 MFMA / LDS-tiled weight gradient (+ epilogue scalar / conv-bias gradients) vs the fp32 engine."""
@@ -159,6 +170,17 @@ S2_DGRAD_CASES = [
     # wraps inside one tile
     (4, 4, (8, 8, 16), True), (4, 8, (8, 8, 16), False), (8, 4, (8, 16, 8), True), (8, 8, (4, 4, 2), True),
     (8, 8, (16, 8, 32), False), (4, 4, (2, 4, 4), True),
+    # 16+ input channels (k_dgrad_s2_mma: one GEMM per parity class on the matrix cores): the down
+    # blocks' 4x4x4 branch convs and 2x2x2 zero-padded skip convs (k, p, circular), incl. channel
+    # tiles spread over workgroups (48), 8-channel g rows and a single-tap K of 32; more than 512
+    # input voxels (fewer go to the small-grid engine)
+    (16, 16, (16, 16, 8), True, 4, 1, True), (32, 32, (8, 8, 8), True, 4, 1, True),
+    (64, 64, (16, 8, 4), False, 4, 1, True), (128, 128, (8, 8, 8), True, 4, 1, True),
+    (48, 24, (12, 8, 6), True, 4, 1, True), (16, 8, (8, 8, 8), True, 4, 1, True),
+    (16, 32, (16, 8, 8), True, 2, 0, False), (64, 128, (8, 8, 8), True, 2, 0, False),
+    (128, 256, (8, 8, 8), False, 2, 0, False),
+    # the zero-padded 2x2x2 skip convs of the few-channel levels (pair kernel: no tap leaves the grid)
+    (4, 8, (8, 8, 16), True, 2, 0, False), (8, 4, (16, 8, 8), True, 2, 0, False), (8, 8, (8, 8, 8), False, 2, 0, False),
 ]
 
 
@@ -169,11 +191,12 @@ def test_dgrad_s2_matches_valu(gpu, case, half):
     the prologue-scalar partial sums) vs the fp32 engine on the same bf16-representable inputs."""
     _H[0] = half
     from vq3d import ops
-    cin, cout, (h, w, d), epi = case
+    cin, cout, (h, w, d), epi = case[:4]
+    k, p, circ = case[4:] if len(case) > 4 else (4, 1, True)
     g = torch.Generator(device=gpu).manual_seed(11 + h + cin)
-    geom = ops.ConvGeom(4, 2, 1, True)
+    geom = ops.ConvGeom(k, 2, p, circ)
     x = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
-    wt = rnd((cout, cin, 4, 4, 4), gpu, g, 0.3)
+    wt = rnd((cout, cin, k, k, k), gpu, g, 0.3)
     gy = rnd((2, cout, geom.out(h), geom.out(w), geom.out(d)), gpu, g).contiguous(memory_format=CL)
     add = rnd((2, cin, h, w, d), gpu, g).contiguous(memory_format=CL)
     ab, gs = rnd((1,), gpu, g, 0.3), rnd((1,), gpu, g)
