@@ -19,6 +19,8 @@ namespace vq3d {
 
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int VT = 32;  // voxels per tile
 constexpr int OT = 64;  // output channels per tile
 constexpr int CPT = 8;  // output channels per thread: OT / (256 / VT)
@@ -171,6 +173,108 @@ __global__ __launch_bounds__(256) void k_small(SArgs s, const T *__restrict__ in
         if (o0 + j < s.Ot) pp[o0 + j] = acc[j];
 }
 
+
+// Matrix-core form (16-bit builds; reduction channels in chunks of 32, outputs in tiles of 16,
+// 16-byte rows): the same partials [z][voxel][out] as k_small, z = (32-channel chunk, group of TG
+// taps) -- the taps are split too, so a 128-voxel grid still spreads over ~100 workgroups.  A
+// workgroup owns 32 voxels x 64 outputs; its (TG taps x 32 channels x 64 outputs) weight block is
+// packed into MFMA A fragments in LDS (rows = outputs), each lane loads its voxel's 32-channel
+// row of every tap as B fragments (16 bytes per tap, all in flight together), and each wave
+// computes 16 voxels x 32 outputs: every lane ends with 4 consecutive outputs of one voxel, one
+// 16-byte partial store per output tile.
+template <bool DG, int TG>
+__global__ __launch_bounds__(256) void k_small_mma(SArgs s, const h16_t *__restrict__ in, const h16_t *__restrict__ in2,
+                                                  const float *__restrict__ w, float *__restrict__ part, int ntg) {
+    extern __shared__ __attribute__((aligned(16))) uint4 wfr[];  // [TG][4 o-tiles][64 lanes]
+    const ConvArgs &a = s.c;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
+    const int o_base = int(blockIdx.y) * OT;
+    const int zc = int(blockIdx.z) / ntg, t0 = int(blockIdx.z) % ntg * TG;
+    const int r0 = zc * 32;
+    const int Ct = a.Cin + a.Cin2, K3 = s.K3;
+    const int ntap = min(TG, K3 - t0);
+    // pack: thread per (output, channel) reads the group's TG consecutive taps of W(o, r, .)
+    h16_t *wh = reinterpret_cast<h16_t *>(wfr);
+    for (int pr = tid; pr < OT * 32; pr += 256) {
+        const int rl = pr & 31, ol = pr >> 5, o = o_base + ol, r = r0 + rl;
+        const bool ok = o < s.Ot && r < s.Rt;
+        const float *src = w + (ok ? (DG ? (int64_t(r) * Ct + o) * K3 : (int64_t(o) * Ct + r) * K3) + t0 : 0);
+        const int e0 = ((ol >> 4) * 64 + (ol & 15) + 16 * (rl >> 3)) * 8 + (rl & 7);
+#pragma unroll
+        for (int ti = 0; ti < TG; ++ti) wh[ti * 4 * 64 * 8 + e0] = f2h(ok && ti < ntap ? src[ti] : 0.f);
+    }
+    // this lane's voxel (B column) in the pass's output grid
+    const int v = int(blockIdx.x) * VT + (wave & 1) * 16 + row;
+    const bool live = v < s.nvox;
+    int gd, gw, gh, b;
+    {
+        const int nD = DG ? a.iD : a.oD, nW = DG ? a.iW : a.oW, nH = DG ? a.iH : a.oH;
+        int t = live ? v : 0;
+        gd = t % nD;
+        t /= nD;
+        gw = t % nW;
+        t /= nW;
+        gh = t % nH;
+        b = t / nH;
+    }
+    const h16_t *src = in;
+    int ldr = DG ? a.Cout : a.Cin, roff = r0;
+    if (!DG && r0 >= a.Cin) {
+        src = in2;
+        ldr = a.Cin2;
+        roff = r0 - a.Cin;
+    }
+    const int sH = DG ? a.oH : a.iH, sW = DG ? a.oW : a.iW, sD = DG ? a.oD : a.iD;
+    uint4 bv[TG];
+#pragma unroll
+    for (int ti = 0; ti < TG; ++ti) {
+        bv[ti] = uint4{0u, 0u, 0u, 0u};
+        const int t = t0 + ti;
+        if (!live || ti >= ntap) continue;
+        const int kh = t / (a.k * a.k), kw = (t / a.k) % a.k, kd = t % a.k;
+        const int ih = DG ? bwd_index(gh, kh, a.s, a.p, a.iH, a.oH, a.circ) : fwd_index(gh, kh, a.s, a.p, a.iH, a.circ);
+        const int iw = DG ? bwd_index(gw, kw, a.s, a.p, a.iW, a.oW, a.circ) : fwd_index(gw, kw, a.s, a.p, a.iW, a.circ);
+        const int id = DG ? bwd_index(gd, kd, a.s, a.p, a.iD, a.oD, a.circ) : fwd_index(gd, kd, a.s, a.p, a.iD, a.circ);
+        if ((ih | iw | id) < 0) continue;
+        const int64_t pos = ((int64_t(b) * sH + ih) * sW + iw) * sD + id;
+        bv[ti] = *reinterpret_cast<const uint4 *>(src + pos * ldr + roff + 8 * kb);
+    }
+    if (!DG) {
+        const Prologue pro = make_prologue(a.pro_kind, a.pro_a, a.pro_b);
+        if (pro.kind != VQ3D_PRO_NONE) {
+#pragma unroll
+            for (int ti = 0; ti < TG; ++ti) {
+                const int t = t0 + ti;
+                if (!live || ti >= ntap) continue;
+                const int kh = t / (a.k * a.k), kw = (t / a.k) % a.k, kd = t % a.k;
+                // padded taps stay zero (k_small skips them); live rows get the prologue
+                if ((fwd_index(gh, kh, a.s, a.p, a.iH, a.circ) | fwd_index(gw, kw, a.s, a.p, a.iW, a.circ) |
+                     fwd_index(gd, kd, a.s, a.p, a.iD, a.circ)) < 0)
+                    continue;
+                uint32_t q[4] = {bv[ti].x, bv[ti].y, bv[ti].z, bv[ti].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    q[j] = uint32_t(f2h(pro.apply(h2f_lo(q[j])))) | (uint32_t(f2h(pro.apply(h2f_hi(q[j])))) << 16);
+                bv[ti] = uint4{q[0], q[1], q[2], q[3]};
+            }
+        }
+    }
+    __syncthreads();
+    const int ot0 = 2 * (wave >> 1);  // the wave's two 16-output tiles
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ti = 0; ti < TG; ++ti) {
+        const hx8 bf = __builtin_bit_cast(hx8, bv[ti]);
+        acc0 = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, wfr[(ti * 4 + ot0) * 64 + lane]), bf, acc0, 0, 0, 0);
+        acc1 = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, wfr[(ti * 4 + ot0 + 1) * 64 + lane]), bf, acc1, 0, 0, 0);
+    }
+    if (!live) return;
+    float *pp = part + (int64_t(blockIdx.z) * s.nvox + v) * s.Ot;
+    const int o0 = o_base + 16 * ot0 + 4 * kb, o1 = o0 + 16;
+    if (o0 < s.Ot) *reinterpret_cast<float4 *>(pp + o0) = float4{acc0[0], acc0[1], acc0[2], acc0[3]};
+    if (o1 < s.Ot) *reinterpret_cast<float4 *>(pp + o1) = float4{acc1[0], acc1[1], acc1[2], acc1[3]};
+}
+
 template <typename T, bool DG>
 __global__ __launch_bounds__(256) void k_small_epi(SArgs s, const float *__restrict__ part, FwdEpi<T> fe,
                                                   BwdEpi<T> be, const float *__restrict__ gscale, T *__restrict__ out,
@@ -205,6 +309,7 @@ __global__ __launch_bounds__(256) void k_small_epi(SArgs s, const float *__restr
 struct SPlan {
     SArgs s;
     int cc, nvt, nct;
+    int mma, tg, ntg;  // matrix-core form: taps per group, tap groups
 };
 
 SPlan plan_small(const vq3d_conv_desc *d, bool dgrad, const float *pa, const float *pb) {
@@ -227,6 +332,16 @@ SPlan plan_small(const vq3d_conv_desc *d, bool dgrad, const float *pa, const flo
         }
     }
     p.s.nsplit = (p.s.Rt + p.cc - 1) / p.cc;
+    // matrix cores: 16-bit data, 32-channel reduction chunks that never straddle x | x2, 16-output
+    // tiles (the codebook levels' 64- / 128-channel convs)
+    p.mma = d->dtype == VQ3D_HALF && p.s.Rt % 32 == 0 && p.s.Ot % 16 == 0 &&
+            (dgrad ? d->cout % 32 == 0 : d->cin % 32 == 0 && d->cin2 % 32 == 0);
+    p.tg = d->kernel == 3 ? 9 : 8;
+    p.ntg = (p.s.K3 + p.tg - 1) / p.tg;
+    if (p.mma) {
+        p.cc = 32;
+        p.s.nsplit = p.s.Rt / 32 * p.ntg;
+    }
     return p;
 }
 
@@ -263,14 +378,46 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
     p.s.vec = dgrad ? al(in, d->cout, esz) && d->cout % 4 == 0
                     : al(in, d->cin, esz) && al(in2, d->cin2, esz) && d->cin % 4 == 0 && d->cin2 % 4 == 0;
     const dim3 grid{unsigned(p.nvt), unsigned(p.nct), unsigned(p.s.nsplit)};
-    const size_t lds = size_t(p.s.K3) * p.cc * OT * 4;
     float *part = static_cast<float *>(ws);
+    if constexpr (std::is_same<T, h16_t>::value) {
+        auto al16 = [](const void *q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+        if (p.mma && al16(in) && al16(in2)) {
+            const size_t lds = size_t(p.tg) * 4 * 64 * 16;
+            if (p.tg == 9) {
+                if (dgrad) k_small_mma<true, 9><<<grid, 256, lds, st>>>(p.s, (const h16_t *)in, nullptr, w, part, p.ntg);
+                else k_small_mma<false, 9><<<grid, 256, lds, st>>>(p.s, (const h16_t *)in, (const h16_t *)in2, w, part, p.ntg);
+            } else {
+                if (dgrad) k_small_mma<true, 8><<<grid, 256, lds, st>>>(p.s, (const h16_t *)in, nullptr, w, part, p.ntg);
+                else k_small_mma<false, 8><<<grid, 256, lds, st>>>(p.s, (const h16_t *)in, (const h16_t *)in2, w, part, p.ntg);
+            }
+            const int64_t n = int64_t(p.s.nvox) * p.s.Ot;
+            const unsigned eb = unsigned(std::min<int64_t>((n + 255) / 256, 1024));
+            if (dgrad)
+                k_small_epi<T, true><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, (T *)out2, dpre, dpost);
+            else
+                k_small_epi<T, false><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, nullptr, nullptr, nullptr);
+            return check_launch(dgrad ? "conv3d_bwd_data(small grid mma)" : "conv3d_fwd(small grid mma)");
+        }
+    }
+    if (p.mma) {  // the VALU kernel's own split (the workspace was sized for the larger one)
+        p.cc = 4;
+        for (int cc : {16, 8}) {
+            const int64_t wgs = int64_t(p.nvt) * p.nct * ((p.s.Rt + cc - 1) / cc);
+            if (wgs >= 256 && size_t(p.s.K3) * cc * OT * 4 <= kSmallLds) {
+                p.cc = cc;
+                break;
+            }
+        }
+        p.s.nsplit = (p.s.Rt + p.cc - 1) / p.cc;
+    }
+    const dim3 grid2{unsigned(p.nvt), unsigned(p.nct), unsigned(p.s.nsplit)};
+    const size_t lds = size_t(p.s.K3) * p.cc * OT * 4;
 #define KS(CC)                                                                                                  \
     case CC:                                                                                                    \
         if (dgrad)                                                                                              \
-            k_small<T, true, CC><<<grid, 256, lds, st>>>(p.s, (const T *)in, nullptr, w, part);                 \
+            k_small<T, true, CC><<<grid2, 256, lds, st>>>(p.s, (const T *)in, nullptr, w, part);                \
         else                                                                                                    \
-            k_small<T, false, CC><<<grid, 256, lds, st>>>(p.s, (const T *)in, (const T *)in2, w, part);         \
+            k_small<T, false, CC><<<grid2, 256, lds, st>>>(p.s, (const T *)in, (const T *)in2, w, part);        \
         break;
     switch (p.cc) {
         KS(4)

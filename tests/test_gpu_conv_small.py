@@ -1,7 +1,8 @@
 """GPU: the small-grid / many-channel conv engine (csrc/conv_small.hip: reduction channels split
 over workgroups, fixed-order partial sums) against a float64 torch CPU restatement of
 nn.Conv3d (+ F.pad 'circular') with the fused prologue / epilogue, forward and
-backward-data.  Tolerances: fp32 1e-4, bf16 1.5e-2 of the output's max magnitude."""
+backward-data.  Tolerances: fp32 1e-4, bf16 1.5e-2 of the output's max magnitude.  bf16
+runs the matrix-core form (k_small_mma) where the channel counts are multiples of 32 / 16."""
 import ctypes
 
 import pytest
@@ -22,6 +23,9 @@ CASES = [
     (33, 17, (4, 4, 2), 3, 1, 1, True, 0),
     (128, 64, (4, 4, 2), 2, 2, 0, False, 0),
     (32, 96, (8, 4, 4), 4, 2, 1, False, 0),
+    # 16-bit: the matrix-core form (32-channel chunks x tap groups) incl. a dual input split at 64
+    (64, 64, (8, 8, 2), 3, 1, 1, True, 64),
+    (64, 32, (8, 8, 8), 3, 1, 1, False, 0),
 ]
 
 
