@@ -393,6 +393,12 @@ static bool use_small(const vq3d_conv_desc *d, bool dgrad) {
     const int64_t nv = dgrad ? int64_t(d->batch) * d->in_h * d->in_w * d->in_d
                              : int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
     if (nv <= 512) return true;
+    // matrix-core form up to VQ3D_SMALL_MMA_MAX voxels (default 512: the lines engine above)
+    static const int64_t mma_max = [] {
+        const char *e = std::getenv("VQ3D_SMALL_MMA_MAX");
+        return e ? std::atoll(e) : int64_t(512);
+    }();
+    if (nv <= mma_max && small_mma_form(d, dgrad)) return true;
     if (dgrad && dgrad_s2_applicable(d)) return false;  // parity-tap engine measured 2x faster there
     return !lines_applicable(d, dgrad);
 }

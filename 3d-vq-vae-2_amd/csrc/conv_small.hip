@@ -358,6 +358,10 @@ bool small_applicable(const vq3d_conv_desc *d, bool dgrad) {
     return size_t(d->kernel) * d->kernel * d->kernel * 4 * OT * 4 <= kSmallLds;
 }
 
+bool small_mma_form(const vq3d_conv_desc *d, bool dgrad) {
+    return small_applicable(d, dgrad) && plan_small(d, dgrad, nullptr, nullptr).mma;
+}
+
 size_t small_workspace(const vq3d_conv_desc *d, bool dgrad) {
     if (!small_applicable(d, dgrad)) return 0;
     const SPlan p = plan_small(d, dgrad, nullptr, nullptr);

@@ -78,6 +78,8 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
 // reduction channels split over workgroups, partials [split][voxel][out] in the workspace
 // (small_workspace bytes), summed in a fixed order by an epilogue kernel (conv_small.hip)
 bool small_applicable(const vq3d_conv_desc *d, bool dgrad);
+// the small-grid engine would run its matrix-core form (16-bit, 32-channel reduction chunks)
+bool small_mma_form(const vq3d_conv_desc *d, bool dgrad);
 size_t small_workspace(const vq3d_conv_desc *d, bool dgrad);
 template <typename T>
 int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *in2, const float *w,
