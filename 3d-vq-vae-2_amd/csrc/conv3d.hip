@@ -527,6 +527,17 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
 // faster (9 -> 9 at 128^2 x 32 on par, 4 -> 4 at 256^2 x 64 1.9x).
 static bool use_lines_wgrad(const vq3d_conv_desc *d) {
     if (d->dtype != VQ3D_HALF || !lines_wgrad_applicable(d)) return false;
+    // grids up to VQ3D_WGRAD_MFMA_MAX output voxels go to the direct engine even when wide (A/B;
+    // default 0: the lines engine for every wide input)
+    static const int64_t mfma_max = [] {
+        const char *e = std::getenv("VQ3D_WGRAD_MFMA_MAX");
+        return e ? std::atoll(e) : int64_t(0);
+    }();
+    const int64_t nv = int64_t(d->batch) * d->out_h * d->out_w * d->out_d;
+    if (nv <= mfma_max && plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w,
+                                    d->out_d, d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)
+                              .ok)
+        return false;
     if (d->cin + d->cin2 >= 32) return true;
     return !plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
                       d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)
