@@ -241,7 +241,11 @@ class PreActFixupCausalResBlock(nn.Module):
                  *args, **kwargs):
         super().__init__()
         if concat_activation:
-            raise NotImplementedError("concat_activation is not implemented")
+            # the reference cannot run this variant either: ExpandRFConv(branch_channels * 2)
+            # (pixel_model/layers.py:399) receives branch_conv1's branch_channels outputs (:370-377,
+            # :432), so its forward raises "expected input ... to have 2B channels, but got B"
+            raise NotImplementedError("concat_activation: the reference's forward fails on it (ExpandRFConv "
+                                      "channel mismatch, pixel_model/layers.py:399,432)")
         self.bias1a, self.bias1b, self.bias2a, self.bias2b, self.bias3a, self.bias3b, self.bias4 = (
             nn.Parameter(torch.zeros(1)) for _ in range(7))
         self.scale = nn.Parameter(torch.ones(1))
