@@ -662,11 +662,7 @@ struct MmArgs {
     int Ca, Cb, K, N, KS;  // row channels (x | x2, or g), reduction length, outputs, 32-wide k-steps
 };
 
-// DIRECT (one n-tile per workgroup and at most one voxel tile per wave: the top levels' 128..1,024-
-// voxel grids): no LDS image -- each wave loads its weight fragments from global memory into
-// registers once, in flight together with its voxel rows, instead of a workgroup-wide pack of the
-// whole image and a barrier in front of every load of the tile.
-template <int NTN, bool DG, bool DIRECT = false>
+template <int NTN, bool DG>
 __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16_t *__restrict__ in,
                                                const h16_t *__restrict__ in2, const float *__restrict__ w,
                                                FwdEpi<h16_t> fe, BwdEpi<h16_t> be, const float *__restrict__ gscale,
@@ -677,30 +673,7 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
     __shared__ float red[8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int Ct = ca.Cin + ca.Cin2, nt0 = int(blockIdx.y) * NTN;
-    static_assert(!DIRECT || NTN == 1, "direct weight fragments: one n-tile");
-    u32x4 wr[DIRECT ? 8 : 1];  // DIRECT: the lane's weight fragment of every k-step
-    if constexpr (DIRECT) {
-        const int n = 16 * nt0 + row;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            float f[8];
-            const int k0 = 32 * ks + 8 * kb;
-            if (!DG && n < m.N && k0 + 8 <= m.K && (Ct & 3) == 0) {
-                const float4 lo = *reinterpret_cast<const float4 *>(w + int64_t(n) * Ct + k0);
-                const float4 hi = *reinterpret_cast<const float4 *>(w + int64_t(n) * Ct + k0 + 4);
-                f[0] = lo.x, f[1] = lo.y, f[2] = lo.z, f[3] = lo.w, f[4] = hi.x, f[5] = hi.y, f[6] = hi.z, f[7] = hi.w;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int k = k0 + e;
-                    f[e] = (ks < m.KS && k < m.K && n < m.N) ? (DG ? w[int64_t(k) * Ct + n] : w[int64_t(n) * Ct + k]) : 0.f;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) wr[ks][j] = uint32_t(f2h(f[2 * j])) | (uint32_t(f2h(f[2 * j + 1])) << 16);
-        }
-    }
-    for (int i = tid; i < (DIRECT ? 0 : m.KS * NTN * 64); i += 256) {
+    for (int i = tid; i < m.KS * NTN * 64; i += 256) {
         const int l = i & 63, t = (i >> 6) % NTN, ks = i / (64 * NTN);
         const int n = 16 * (nt0 + t) + (l & 15), k0 = 32 * ks + 8 * (l >> 4);
         uint32_t q[4];
@@ -716,7 +689,7 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
         }
         wB[i] = u32x4{q[0], q[1], q[2], q[3]};
     }
-    if constexpr (!DIRECT) __syncthreads();
+    __syncthreads();
     const Prologue pro = make_prologue(DG ? VQ3D_PRO_NONE : ca.pro_kind, ca.pro_a, ca.pro_b);
     const bool raw = DG || pro.kind == VQ3D_PRO_NONE;
     const ActDeriv dv = make_deriv(be);
@@ -754,7 +727,7 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
             // so a lane ends with 4 consecutive output channels of one voxel (vector epilogue)
 #pragma unroll
             for (int t = 0; t < NTN; ++t)
-                acc[t] = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, DIRECT ? wr[ks] : wB[(ks * NTN + t) * 64 + lane]),
+                acc[t] = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, wB[(ks * NTN + t) * 64 + lane]),
                                                                  af, acc[t], 0, 0, 0);
         }
         // D^T[channel 16 t' + 4 kb + j][voxel v0 + row] of n-tile t' = nt0 + t
@@ -863,24 +836,13 @@ static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, c
     const int64_t ntile = (nvox + 15) / 16, nbx0 = (ntile + 3) / 4;
     while (NTN > 1 && nbx0 * ((ntn + NTN - 1) / NTN) < 512) NTN /= 2;
     const int ny = (ntn + NTN - 1) / NTN;
+    const size_t lds = size_t(m.KS) * NTN * 64 * 16;
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nbx0, 1024 / ny)));
-    // every wave at most one voxel tile, one n-tile per workgroup: weight fragments straight to registers
-    const bool direct = NTN == 1 && int64_t(nbx) == nbx0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0;
-    const size_t lds = direct ? 0 : size_t(m.KS) * NTN * 64 * 16;
     const dim3 nb{nbx, unsigned(ny), 1u};
     const bool want_part = dgrad && (dpre || dpost);
     float *part = (want_part && ws && ws_bytes >= size_t(2) * nbx * ny * 4) ? static_cast<float *>(ws) : nullptr;
     const unsigned tk = part ? ticket_slot() : 0u;
     ConvArgs ca = make_args(d, pa, pb);
-    if (direct) {
-        if (dgrad)
-            k_pw_mma<1, true, true><<<nb, 256, 0, s>>>(m, ca, (const h16_t *)in, nullptr, w, fe, be, gscale,
-                                                       (h16_t *)out, (h16_t *)out2, dpre, dpost, part, tk);
-        else
-            k_pw_mma<1, false, true><<<nb, 256, 0, s>>>(m, ca, (const h16_t *)in, (const h16_t *)in2, w, fe, be,
-                                                        nullptr, (h16_t *)out, nullptr, nullptr, nullptr, nullptr, 0u);
-        return true;
-    }
 #define MM(NT_)                                                                                                 \
     if (dgrad)                                                                                                  \
         k_pw_mma<NT_, true><<<nb, 256, lds, s>>>(m, ca, (const h16_t *)in, nullptr, w, fe, be, gscale,         \

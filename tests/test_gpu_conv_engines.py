@@ -181,6 +181,7 @@ S2_DGRAD_CASES = [
     (128, 256, (8, 8, 8), False, 2, 0, False),
     # the zero-padded 2x2x2 skip convs of the few-channel levels (pair kernel: no tap leaves the grid)
     (4, 8, (8, 8, 16), True, 2, 0, False), (8, 4, (16, 8, 8), True, 2, 0, False), (8, 8, (8, 8, 8), False, 2, 0, False),
+    (8, 16, (16, 8, 8), True, 2, 0, False),
 ]
 
 
