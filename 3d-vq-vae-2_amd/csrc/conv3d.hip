@@ -572,9 +572,15 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
                 m.a.pro_a = pa;
                 m.a.pro_b = pb;
                 m.a.wCt = Ct;
-                // up to 4 tiles of 16 output channels per workgroup, more as 64-channel chunks
-                return launch_wgrad_mfma(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
-                                         dbias, dcbias, s);
+                // MFMA engine holds up to 4 tiles of 16 output channels; wider outputs (the top levels'
+                // 128-channel convs on 128..1,024 voxels) stay on the VALU tiled kernel: 64-channel
+                // chunks on the matrix cores measured slower there (r04f / r04g: 57 vs 48.7 us at
+                // 128 -> 128 @8x8x2, 212 vs 155 us at 64 -> 128 k4 s2 @32x32x8)
+                if (d->cout <= 64)
+                    return launch_wgrad_mfma(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
+                                             dbias, dcbias, s);
+                return launch_wgrad_tiled(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
+                                          dbias, dcbias, s);
             }
         }
     }

@@ -193,18 +193,16 @@ __global__ __launch_bounds__(256) void k_small_mma(SArgs s, const h16_t *__restr
     const int r0 = zc * 32;
     const int Ct = a.Cin + a.Cin2, K3 = s.K3;
     const int ntap = min(TG, K3 - t0);
-    // pack: consecutive threads read the group's consecutive taps, then the next channel (forward)
-    // or output (backward-data) -- runs of TG contiguous floats, K3 apart
+    // pack: thread per (output, channel) reads the group's TG consecutive taps of W(o, r, .)
+    // (a thread per element with coalesced runs measured slower: 23.8 -> 46.7 us, r04g)
     h16_t *wh = reinterpret_cast<h16_t *>(wfr);
-    for (int f = tid; f < OT * 32 * TG; f += 256) {
-        const int ti = f % TG, q = f / TG;
-        const int ol = DG ? q % OT : q / 32, rl = DG ? q / OT : q % 32;
-        const int o = o_base + ol, r = r0 + rl;
-        float val = 0.f;
-        if (o < s.Ot && r < s.Rt && ti < ntap)
-            val = DG ? w[(int64_t(r) * Ct + o) * K3 + t0 + ti] : w[(int64_t(o) * Ct + r) * K3 + t0 + ti];
+    for (int pr = tid; pr < OT * 32; pr += 256) {
+        const int rl = pr & 31, ol = pr >> 5, o = o_base + ol, r = r0 + rl;
+        const bool ok = o < s.Ot && r < s.Rt;
+        const float *src = w + (ok ? (DG ? (int64_t(r) * Ct + o) * K3 : (int64_t(o) * Ct + r) * K3) + t0 : 0);
         const int e0 = ((ol >> 4) * 64 + (ol & 15) + 16 * (rl >> 3)) * 8 + (rl & 7);
-        wh[ti * 4 * 64 * 8 + e0] = f2h(val);
+#pragma unroll
+        for (int ti = 0; ti < TG; ++ti) wh[ti * 4 * 64 * 8 + e0] = f2h(ok && ti < ntap ? src[ti] : 0.f);
     }
     // this lane's voxel (B column) in the pass's output grid
     const int v = int(blockIdx.x) * VT + (wave & 1) * 16 + row;
