@@ -480,7 +480,7 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
         // down blocks' zero-padded skip conv takes the circular pair kernel)
         if (std::is_same<T, h16_t>::value && (a.circ || (a.k == 2 && a.p == 0)) && a.Cin2 == 0 &&
             (a.Cin == 4 || a.Cin == 8) &&
-            (a.Cout == 4 || a.Cout == 8 || (a.Cout == 16 && a.k == 2)) && a.p == a.k / 2 - 1 && a.iH == 2 * a.oH && a.iW == 2 * a.oW &&
+            (a.Cout == 4 || a.Cout == 8) && a.p == a.k / 2 - 1 && a.iH == 2 * a.oH && a.iW == 2 * a.oW &&
             a.iD == 2 * a.oD && al16(g) && al16(gx) && (!be.aux || al16(be.aux)) && (!be.addend || al16(be.addend))) {
             S2Args c = a;
             c.fD = FastDiv(uint32_t(a.oD));
@@ -494,7 +494,7 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
                                                                    dpre, dpost);                               \
                 return check_launch("conv3d_bwd_data(s2 pairs)");                                              \
             }
-            PK(4, 4, 4) PK(4, 8, 4) PK(8, 4, 4) PK(8, 8, 4) PK(4, 4, 2) PK(4, 8, 2) PK(8, 4, 2) PK(8, 8, 2) PK(8, 16, 2)
+            PK(4, 4, 4) PK(4, 8, 4) PK(8, 4, 4) PK(8, 8, 4) PK(4, 4, 2) PK(4, 8, 2) PK(8, 4, 2) PK(8, 8, 2)
 #undef PK
         }
     }
