@@ -516,7 +516,7 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
                 // each workgroup packs its class's A fragments once (8 strided weight loads per entry):
                 // with large packs ~256 workgroups amortise that (32 -> 32 @64^2x16 38.5 -> 31.0 us), with
                 // small ones ~2,048 keep the big grids busy (16 -> 16 @128^2x32; r04f / r04g)
-                const int wg_target = ntm * nks <= 8 ? 2048 : 256;
+                const int wg_target = a.k == 4 && ntm * nks <= 8 ? 2048 : 256;  // 2x2x2: 256 (12.4 vs 20.8 us)
                 const unsigned gxn = unsigned(std::max<int64_t>(
                     1, std::min<int64_t>((ntile + 3) / 4, std::max(1, wg_target / (8 * nz)))));
                 const dim3 grid(gxn, 8u, unsigned(nz));
