@@ -673,23 +673,6 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
     __shared__ float red[8];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int Ct = ca.Cin + ca.Cin2, nt0 = int(blockIdx.y) * NTN;
-    // the voxel rows of a tile (every A fragment in flight together); the first tile's are issued
-    // before the weight image is packed, so that round trip overlaps the pack and the barrier
-    const int64_t ntile = (m.nvox + 15) / 16;
-    u32x4 av[8];
-    auto load_rows = [&](int64_t mt_) {
-        const int64_t vr = min(mt_ * 16 + row, m.nvox - 1);
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            av[ks] = u32x4{0u, 0u, 0u, 0u};
-            const int k0 = 32 * ks + 8 * kb;
-            if (ks < m.KS && k0 < m.K)
-                av[ks] = k0 < m.Ca ? *reinterpret_cast<const u32x4 *>(in + vr * m.Ca + k0)
-                                   : *reinterpret_cast<const u32x4 *>(in2 + vr * m.Cb + (k0 - m.Ca));
-        }
-    };
-    const int64_t mt_first = int64_t(blockIdx.x) * 4 + wave;
-    if (mt_first < ntile) load_rows(mt_first);
     for (int i = tid; i < m.KS * NTN * 64; i += 256) {
         const int l = i & 63, t = (i >> 6) % NTN, ks = i / (64 * NTN);
         const int n = 16 * (nt0 + t) + (l & 15), k0 = 32 * ks + 8 * (l >> 4);
@@ -714,9 +697,18 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
     const float sc = fe.scale ? *fe.scale : 1.f, bi = fe.bias ? *fe.bias : 0.f;
     const float aa = fe.act_a ? *fe.act_a : 0.f, ab = fe.act_b ? *fe.act_b : 0.f;
     float pre = 0.f, post = 0.f;
-    for (int64_t mt = mt_first; mt < ntile; mt += int64_t(gridDim.x) * 4) {
-        const int64_t v0 = mt * 16;
-        if (mt != mt_first) load_rows(mt);
+    const int64_t ntile = (m.nvox + 15) / 16;
+    for (int64_t mt = int64_t(blockIdx.x) * 4 + wave; mt < ntile; mt += int64_t(gridDim.x) * 4) {
+        const int64_t v0 = mt * 16, vr = min(v0 + row, m.nvox - 1);
+        u32x4 av[8];  // every A fragment of the tile in flight together
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            av[ks] = u32x4{0u, 0u, 0u, 0u};
+            const int k0 = 32 * ks + 8 * kb;
+            if (ks < m.KS && k0 < m.K)
+                av[ks] = k0 < m.Ca ? *reinterpret_cast<const u32x4 *>(in + vr * m.Ca + k0)
+                                   : *reinterpret_cast<const u32x4 *>(in2 + vr * m.Cb + (k0 - m.Ca));
+        }
         f32x4 acc[NTN];
 #pragma unroll
         for (int t = 0; t < NTN; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
