@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <string>
 #include <atomic>
+#include <mutex>
 
 // The kernel sources are compiled twice (Makefile): with bf16 as the 16-bit activation / matrix-
 // core operand format, and with -DVQ3D_FP16 with IEEE fp16 (the reference trains with fp16 AMP,
@@ -297,13 +298,34 @@ __device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {
 // hand-off table, first row.  The ticket is two-level: same-address atomics serialise (one
 // counter for 1,024 workgroups added ~11 us), so workgroup b adds to shard b % 16 (counters a
 // 128-B line apart) and the workgroup completing a shard adds to the top counter.  Tickets: a
-// per-module array, the host hands each launch the next slot (ticket_slot), the finishing
-// workgroup re-arms it to 0; a slot is reused 64 launches later.
-constexpr unsigned kTickets = 64, kShards = 16, kTicketLine = 32;
+// per-module array, the host hands each launch a slot (ticket_slot) and the finishing workgroup
+// re-arms it to 0.
+// Invariant: two launches holding the same slot must never run at the same time.  Slots are
+// therefore keyed by STREAM: each stream that launches ticketed kernels owns a region of
+// kTicketSlots slots and cycles through it; launches on one stream (or captured from one stream
+// into a graph) are ordered, so a slot is free again by the time its stream reuses it, and
+// launches on different streams -- a side stream, a second level chain -- never share one.  Up
+// to kTicketRegions streams hold regions at once; a further stream takes over the least recently
+// claimed region, so more than that many streams must not run ticketed launches concurrently.
+constexpr unsigned kTicketRegions = 16, kTicketSlots = 4, kTickets = kTicketRegions * kTicketSlots;
+constexpr unsigned kShards = 16, kTicketLine = 32;
 static __device__ unsigned g_tickets[kTickets * (kShards + 1) * kTicketLine];
-static inline unsigned ticket_slot() {
-    static std::atomic<unsigned> next{0};
-    return next.fetch_add(1, std::memory_order_relaxed) % kTickets;
+static inline unsigned ticket_slot(hipStream_t st) {
+    static std::mutex mu;
+    static hipStream_t owner[kTicketRegions] = {};
+    static bool used[kTicketRegions] = {};
+    static unsigned next[kTicketRegions] = {}, claims = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    unsigned r = kTicketRegions;
+    for (unsigned i = 0; i < kTicketRegions; ++i)
+        if (used[i] && owner[i] == st) r = i;
+    if (r == kTicketRegions) {
+        r = claims++ % kTicketRegions;
+        owner[r] = st;
+        used[r] = true;
+        next[r] = 0;
+    }
+    return r * kTicketSlots + (next[r]++ % kTicketSlots);
 }
 // every thread of the (1-D, NT-thread) workgroup calls this with the workgroup's sums in thread 0;
 // part holds nb {pre, post} float pairs; *dpre += the pres' sum, *dpost += the posts'

@@ -313,6 +313,20 @@ struct SPlan {
     int mma, tg, ntg;  // matrix-core form: taps per group, tap groups
 };
 
+// reduction chunk of the VALU kernel k_small: the largest of 16 / 8 channels that still gives
+// >= 256 workgroups and fits the LDS weight block, else 4
+void valu_chunking(SPlan &p) {
+    p.cc = 4;
+    for (int cc : {16, 8}) {
+        const int64_t wgs = int64_t(p.nvt) * p.nct * ((p.s.Rt + cc - 1) / cc);
+        if (wgs >= 256 && size_t(p.s.K3) * cc * OT * 4 <= kSmallLds) {
+            p.cc = cc;
+            break;
+        }
+    }
+    p.s.nsplit = (p.s.Rt + p.cc - 1) / p.cc;
+}
+
 SPlan plan_small(const vq3d_conv_desc *d, bool dgrad, const float *pa, const float *pb) {
     SPlan p;
     p.s.c = make_args(d, pa, pb);
@@ -324,15 +338,7 @@ SPlan plan_small(const vq3d_conv_desc *d, bool dgrad, const float *pa, const flo
     p.s.K3 = d->kernel * d->kernel * d->kernel;
     p.nvt = int((nv + VT - 1) / VT);
     p.nct = (p.s.Ot + OT - 1) / OT;
-    p.cc = 4;
-    for (int cc : {16, 8}) {
-        const int64_t wgs = int64_t(p.nvt) * p.nct * ((p.s.Rt + cc - 1) / cc);
-        if (wgs >= 256 && size_t(p.s.K3) * cc * OT * 4 <= kSmallLds) {
-            p.cc = cc;
-            break;
-        }
-    }
-    p.s.nsplit = (p.s.Rt + p.cc - 1) / p.cc;
+    valu_chunking(p);
     // matrix cores: 16-bit data, 32-channel reduction chunks that never straddle x | x2, 16-output
     // tiles (the codebook levels' 64- / 128-channel convs)
     p.mma = d->dtype == VQ3D_HALF && p.s.Rt % 32 == 0 && p.s.Ot % 16 == 0 &&
@@ -363,10 +369,21 @@ bool small_mma_form(const vq3d_conv_desc *d, bool dgrad) {
     return small_applicable(d, dgrad) && plan_small(d, dgrad, nullptr, nullptr).mma;
 }
 
+// partial rows of either form: a matrix-core plan falls back to k_small (its own, possibly
+// larger, split) when an operand is not 16-byte aligned, so the workspace covers both
+static size_t small_partials_bytes(const SPlan &p) {
+    size_t n = size_t(p.s.nsplit) * p.s.nvox * p.s.Ot * 4;
+    if (p.mma) {
+        SPlan q = p;
+        valu_chunking(q);
+        n = std::max(n, size_t(q.s.nsplit) * q.s.nvox * q.s.Ot * 4);
+    }
+    return n;
+}
+
 size_t small_workspace(const vq3d_conv_desc *d, bool dgrad) {
     if (!small_applicable(d, dgrad)) return 0;
-    const SPlan p = plan_small(d, dgrad, nullptr, nullptr);
-    return size_t(p.s.nsplit) * p.s.nvox * p.s.Ot * 4;
+    return small_partials_bytes(plan_small(d, dgrad, nullptr, nullptr));
 }
 
 template <typename T>
@@ -374,8 +391,7 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
                  const float *pa, const float *pb, const FwdEpi<T> &fe, const BwdEpi<T> &be, const float *gscale,
                  void *out, void *out2, float *dpre, float *dpost, void *ws, size_t ws_bytes, hipStream_t st) {
     SPlan p = plan_small(d, dgrad, pa, pb);
-    const size_t need = size_t(p.s.nsplit) * p.s.nvox * p.s.Ot * 4;
-    if (!ws || ws_bytes < need) return fail("conv3d(small grid): workspace too small");
+    if (!ws || ws_bytes < small_partials_bytes(p)) return fail("conv3d(small grid): workspace too small");
     auto al = [](const void *q, int ch, int esz) {
         return q == nullptr || ((reinterpret_cast<uintptr_t>(q) & 15) == 0 && (ch * esz) % 8 == 0);
     };
@@ -404,17 +420,7 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
             return check_launch(dgrad ? "conv3d_bwd_data(small grid mma)" : "conv3d_fwd(small grid mma)");
         }
     }
-    if (p.mma) {  // the VALU kernel's own split (the workspace was sized for the larger one)
-        p.cc = 4;
-        for (int cc : {16, 8}) {
-            const int64_t wgs = int64_t(p.nvt) * p.nct * ((p.s.Rt + cc - 1) / cc);
-            if (wgs >= 256 && size_t(p.s.K3) * cc * OT * 4 <= kSmallLds) {
-                p.cc = cc;
-                break;
-            }
-        }
-        p.s.nsplit = (p.s.Rt + p.cc - 1) / p.cc;
-    }
+    if (p.mma) valu_chunking(p);  // the VALU kernel's own split (small_partials_bytes covers it)
     const dim3 grid2{unsigned(p.nvt), unsigned(p.nct), unsigned(p.s.nsplit)};
     const size_t lds = size_t(p.s.K3) * p.cc * OT * 4;
 #define KS(CC)                                                                                                  \

@@ -28,9 +28,15 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of N ranks on a one-GPU box: every rank on device 0, collectives over gloo (RCCL
+    # refuses two ranks on one device); never set for a real multi-GPU run
+    share = os.environ.get("VQ3D_RANKS_SHARE_GPU") == "1"
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        dev_index = 0 if share else local
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
+        if share:
+            backend = backend or "gloo"
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():

@@ -3,7 +3,12 @@
     python -m vq3d.train DATASET [--batch-size 1] [model flags of VQVAE.add_model_specific_args]
                          [--max_epochs N] [--max_steps N] [--default_root_dir DIR]
                          [--resume_from_checkpoint last.ckpt]
-    python -m torch.distributed.run --nproc-per-node 8 -m vq3d.train DATASET ...   (one rank per GPU)
+
+--gpus follows the reference (train.py:25-27: gpus=-1, accelerator='ddp'): -1 = every visible GPU,
+N = N GPUs.  With more than one, the command starts its own ranks -- `python -m
+torch.distributed.run --nproc-per-node N -m vq3d.train ...` as a child process (vq3d/launch.py),
+before this process touches a GPU -- and exits with its code; started by an existing torchrun
+(WORLD_SIZE set) it is simply that rank.
 
 What the reference gets from PyTorch-Lightning 1.2.10 (Trainer.from_argparse_args +
 ModelCheckpoint), restated here without that dependency:
@@ -224,7 +229,8 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
         return loss
     # the whole step as a HIP graph per input shape (single rank, or ranks whose RCCL collectives
     # replay correctly inside a graph: parallel.graph_collectives_ok)
-    use_graph = bool(getattr(args, "hip_graph", 1)) and (world == 1 or parallel.graph_collectives_ok(dev))
+    use_graph = bool(getattr(args, "hip_graph", 1)) and (
+        world == 1 or (torch.distributed.get_backend() == "nccl" and parallel.graph_collectives_ok(dev)))
     runner = StepGraph(train_step, warmup=2, enabled=use_graph)
     val_every = max(1, int(n_batches * args.val_check_interval)) if args.val_check_interval <= 1 else \
         int(args.val_check_interval)
@@ -254,5 +260,31 @@ def _fit(args, model, opt, reducer, ckpt, datamodule, rank, world, dev, epoch0, 
     return model, opt, history, ckpt
 
 
+def launch_ranks(args, argv):
+    """The 'ddp' self-launch (train.py:25-27): the exit code of the N ranks this command started
+    when --gpus asks for more than one GPU and this process is not already a rank, else None."""
+    from . import launch
+    if launch.is_rank_process() or args.accelerator not in (None, "ddp"):
+        return None
+    n = launch.resolve_gpus(args.gpus)
+    if n <= 1:
+        return None
+    env = dict(os.environ)
+    pkg = str(Path(__file__).resolve().parent.parent)  # the ranks import vq3d from the same tree
+    env["PYTHONPATH"] = pkg + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return launch.run_ranks(n, "vq3d.train", list(argv), module=True, env=env)
+
+
+def cli(argv=None):
+    import sys
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_arguments(argv)
+    rc = launch_ranks(args, argv)
+    if rc is not None:
+        return rc
+    main(args)
+    return 0
+
+
 if __name__ == '__main__':
-    main(parse_arguments())
+    raise SystemExit(cli())

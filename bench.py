@@ -3,8 +3,12 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3l_pub] [--eager] [--encode-only]
 
-N > 1 runs under torch.distributed.run, one process per GPU (RCCL); each rank trains on its
-own synthetic 512x512x128 volume (weak scaling: batch 1 per GPU, BASELINE.json configs[2]).
+N > 1 runs one process per GPU (RCCL); each rank trains on its own synthetic 512x512x128 volume
+(weak scaling: batch 1 per GPU, BASELINE.json configs[2]).  Started bare (`python bench.py --gpus
+N`), the script launches its own N ranks -- `python -m torch.distributed.run --nproc-per-node N
+bench.py ...` as a child process, before anything imports torch or touches a GPU (vq3d/launch.py,
+the reference's gpus=-1 / accelerator='ddp', vqvae/train.py:25-27) -- forwards rank 0's JSON line
+and exits with the child's code; under an existing torchrun (WORLD_SIZE set) it is that rank.
 Rank 0 prints ONE JSON line.  Default workload = the BASELINE metric's configuration:
 3-layer VQ-VAE with the reference's published block counts (50 pre-q / 50 post-q / 3 post-up /
 2 post-down, K = 128/256/512, slurm-jobs/train_vqvae_3d.job:76-86), bf16 activations.
@@ -70,14 +74,15 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--profile-steps", action="store_true", help="print per-step times to stderr")
-    p.add_argument("--serial-wgrad", action="store_true",
-                   help="run weight gradients on the main stream (the default; kept for old command lines)")
     p.add_argument("--concurrent-wgrad", action="store_true",
                    help="run weight gradients on a side stream, overlapped with backward-data (measured "
                         "0.3 ms/step slower than serial on the 3L-pub step now that the big blocks are fused)")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
     p.add_argument("--no-dist-graph", action="store_true", help="N > 1: never capture the collectives")
+    p.add_argument("--cpu-plumbing", action="store_true",
+                   help="tests only: exercise the rank launch / barrier / max-over-ranks / JSON plumbing on CPU "
+                        "ranks over gloo with a stand-in step (one all-reduce of a gradient-sized buffer); no model")
     p.add_argument("--binding", default="ctypes", choices=["ctypes", "library"],
                    help="library: the layers call the registered torch.ops.vq3d.* operators (vq3d.library) "
                         "instead of the ctypes autograd Functions (same kernels)")
@@ -658,8 +663,92 @@ def prior_main(a):
     print(json.dumps(res_line), flush=True)
 
 
+def _launcher():
+    """vq3d/launch.py loaded by path: standard library only, so the decision to start ranks is
+    taken before the vq3d package (and torch) is imported."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("vq3d_launch", os.path.join(ROOT, "3d-vq-vae-2_amd", "vq3d",
+                                                                                "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def timed_steps(step, a, world, dev):
+    """The timed region of the contract: barrier + device sync, exactly a.steps steps, barrier +
+    device sync; returns (max elapsed seconds over the ranks, last result, per-step seconds)."""
+    import torch
+    import torch.distributed as dist
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    per, res = [], None
+    for i in range(a.steps):
+        ts = time.perf_counter()
+        res = step(a.warmup + i)
+        if a.profile_steps:
+            sync()
+            per.append(time.perf_counter() - ts)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    return elapsed, res, per
+
+
+def plumbing_main(a):
+    """--cpu-plumbing (tests only): the same launch, timing and reporting path on CPU ranks over
+    gloo, with one all-reduce of a 3L-pub-gradient-sized fp32 buffer standing in for the step."""
+    import torch
+    import torch.distributed as dist
+
+    from vq3d import parallel
+    rank, world, _, dev = parallel.init_from_env(backend="gloo")
+    if dev.type != "cpu":
+        dev = torch.device("cpu")
+    buf = torch.full((1 << 16,), float(rank + 1))
+
+    def step(i):
+        if world > 1:
+            dist.all_reduce(buf)
+            buf.div_(world)
+        return buf
+    for i in range(a.warmup):
+        step(i)
+    elapsed, res, _ = timed_steps(step, a, world, dev)
+    ok = abs(float(res[0]) - (world + 1) / 2.0) < 1e-6
+    if rank == 0:
+        print(json.dumps({"metric": "launcher plumbing self-test (no model)", "value": world * a.steps / elapsed,
+                          "unit": "steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": 1000.0 * elapsed / a.steps, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "fp32", "data": "stand-in all-reduce on CPU ranks (gloo)",
+                          "allreduce_ok": ok,
+                          "config": {"workload": "cpu_plumbing", "global_batch": world,
+                                     "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("stand-in all-reduce returned the wrong average")
+
+
 def main():
     a = parse()
+    launch = _launcher()
+    if a.gpus > 1 and not launch.is_rank_process():
+        # bare `bench.py --gpus N`: start the N ranks as a child process (no GPU touched here)
+        raise SystemExit(launch.run_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:], json_only_stdout=True))
+    if a.cpu_plumbing:
+        return plumbing_main(a)
     if a.prior:
         return prior_main(a)
     import torch
@@ -671,12 +760,12 @@ def main():
 
     rank, world, local, dev = parallel.init_from_env()
     if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     mkw, size, batch, roof_ms = CONFIGS[a.config]
     if a.size:
         size = tuple(a.size)
     torch.manual_seed(0)
-    ops.set_concurrent_wgrad(a.concurrent_wgrad and not a.serial_wgrad)
+    ops.set_concurrent_wgrad(a.concurrent_wgrad)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
     if a.binding != "ctypes":
@@ -729,33 +818,15 @@ def main():
     graph = None
     use_graph = not a.eager and a.warmup >= 2
     if use_graph and world > 1:
-        use_graph = not a.no_dist_graph and parallel.graph_collectives_ok(dev)
+        # gloo (the one-GPU rank rehearsal) has no graph-capturable collectives: eager there
+        use_graph = (not a.no_dist_graph and dist.get_backend() == "nccl" and parallel.graph_collectives_ok(dev))
     if use_graph:
         graph, static = capture(step, a.warmup)
 
         def step(i):  # noqa: F811
             graph.replay()
             return static
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    per = []
-    for i in range(a.steps):
-        ts = time.perf_counter()
-        res = step(a.warmup + i)
-        if a.profile_steps:
-            torch.cuda.synchronize()
-            per.append(time.perf_counter() - ts)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    elapsed, res, per = timed_steps(step, a, world, dev)
     if a.profile_steps and rank == 0:
         print("per-step s:", [round(v, 4) for v in per], file=sys.stderr)
     vols = world * batch * a.steps

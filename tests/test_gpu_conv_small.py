@@ -92,3 +92,37 @@ def test_small_grid_conv_vs_torch(gpu, case, dt):
     scale = float(pre_t.abs().sum())
     assert abs(float(dpre) - float(pre_t.sum())) <= tol * scale
     assert abs(float(dpost) - float(post_t.sum())) <= tol * scale
+
+
+def test_small_grid_misaligned_input_fits_workspace(gpu):
+    """A 16-bit input that is not 16-byte aligned makes the matrix-core plan fall back to the VALU
+    kernel with its own (larger) split: the queried workspace must cover that split.  The launch
+    gets exactly the queried bytes followed by a canary region, which must stay untouched."""
+    from vq3d import ops
+    from vq3d import _lib as L
+    cin = cout = 64
+    h, w, d = 8, 8, 2
+    geom = ops.ConvGeom(3, 1, 1, True)
+    desc, _ = ops.conv_desc(torch.bfloat16, 1, cin, 0, cout, h, w, d, geom, L.PRO_NONE)
+    nws = int(L.query("vq3d_conv3d_workspace_size", ctypes.byref(desc), L.PASS_FWD))
+    assert nws > 0
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn((1, cin, h, w, d), generator=g)).to(torch.bfloat16)
+    wt = torch.randn((cout, cin, 3, 3, 3), generator=g) * 0.05
+    n = x.numel()
+    buf = torch.empty(n + 4, dtype=torch.bfloat16, device=gpu)
+    xm = buf[4:].view(1, h, w, d, cin).permute(0, 4, 1, 2, 3)  # channels-last, 8 bytes off 16-B alignment
+    xm.copy_(x.to(gpu))
+    assert xm.data_ptr() % 16 == 8 and xm.is_contiguous(memory_format=CL)
+    canary = 1 << 20
+    ws = torch.full((nws + canary,), 0x5A, dtype=torch.uint8, device=gpu)
+    y = torch.empty_like(xm, memory_format=CL)
+    epi = L.ConvEpilogue(scale=None, bias=None, cbias=None, residual=None, residual_up2=0, act=L.ACT_NONE,
+                         act_a=None, act_b=None)
+    wf = wt.to(gpu)
+    L.call("vq3d_conv3d_fwd", ctypes.byref(desc), L.ptr(xm), None, L.ptr(wf), None, None, ctypes.byref(epi),
+           L.ptr(y), ws.data_ptr(), nws, L.stream())
+    torch.cuda.synchronize()
+    assert bool((ws[nws:] == 0x5A).all()), "the launch wrote past the queried workspace"
+    ref = _conv_ref(x.double(), wt.double(), 3, 1, 1, True)
+    assert rel(y.float(), ref) < 1.5e-2
