@@ -374,7 +374,9 @@ class Encoder2(nn.Module):
             before_channels = after_channels
         self.compute_dtype = torch.float32
 
-    def forward(self, data):
+    def forward(self, data, on_quantized=None):
+        """on_quantized(quantization): called after each level's Quantizer, top level first (the
+        model uses it to start the decoder's top-level chain early, VQVAE.forward)."""
         if Fn.parse_input_fused(data, self.parse_input, self.compute_dtype):
             # the fp32 volume straight into the 16-bit activation (never rounded to bf16 itself)
             down = Fn.parse_input(data, self.parse_input.weight, self.parse_input.bias, self.compute_dtype)
@@ -397,6 +399,8 @@ class Encoder2(nn.Module):
                 quantization = quantize(pre_quantize(pre_quantize_cond(down, aux)))
                 quantizations.append(quantization)
                 _, aux, *_ = quantization
+                if on_quantized is not None:
+                    on_quantized(quantization)
         finally:
             for q in self.quantize:
                 q.ema_slot = None
@@ -448,8 +452,14 @@ class Decoder(nn.Module):
             after_channels = before_channels
         self.out = Conv3d(base_network_channels, out_channels, kernel_size=1)
 
-    def forward(self, quantizations):
+    def forward(self, quantizations, top=None):
+        """top: (output of up[-1] on the top code, the stream it was issued on) when the caller
+        already started the top-level chain (VQVAE.forward); the current stream joins it here."""
         for i, (quantization, up) in enumerate(reversed(list(zip(quantizations, self.up)))):
+            if i == 0 and top is not None:
+                out, stream = top
+                torch.cuda.current_stream().wait_stream(stream)
+                continue
             out = quantization if i == 0 else self.proj[-i](quantization, out)
             out = up(out)
         return self.out(out)

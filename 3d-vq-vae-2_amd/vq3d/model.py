@@ -15,6 +15,7 @@ import torch
 from torch import nn
 
 from . import functional as Fn
+from . import ops
 from . import parallel
 from .flat import FlatParams
 from .layers import Decoder, Encoder2, EvonormResBlock, FixupResBlock, PreActFixupResBlock
@@ -102,8 +103,21 @@ class VQVAE(nn.Module):
     def forward(self, data):
         if torch.is_grad_enabled():
             parallel.step_begin()
-        commitment_loss, quantizations, encoding_idx = zip(*self.encode(data))
-        decoded = self.decode(quantizations)
+        top, hook = {}, None
+        if ops.overlap_levels() and data.is_cuda and len(self.decoder.up) > 1:
+            # the decoder's top-level chain (post-quantize blocks + up block, layers.py:510-514)
+            # needs only the top code: start it on the level stream as soon as the top Quantizer
+            # is done, beside the encoder's lower levels (layers.py:583-586); same arithmetic
+            def hook(quantization):
+                if "out" in top:
+                    return
+                cur = torch.cuda.current_stream()
+                s = ops.level_stream(data.device)
+                s.wait_stream(cur)
+                with torch.cuda.stream(s):
+                    top["out"] = (self.decoder.up[-1](quantization[1]), s)
+        commitment_loss, quantizations, encoding_idx = zip(*self.encoder(data, on_quantized=hook))
+        decoded = self.decoder(quantizations, top=top.get("out"))
         return decoded, (commitment_loss, quantizations, encoding_idx)
 
     def encode(self, data):

@@ -260,15 +260,40 @@ def _side_stream(device):
     return s
 
 
+_levels = {}
+_overlap = [True]
+
+
+def set_overlap_levels(enabled=True):
+    """Run the decoder's top-level chain (its post-quantize blocks and up block, which need only
+    the top code) on a second stream beside the encoder's lower levels (VQVAE.forward); autograd
+    runs their backward on that stream too."""
+    _overlap[0] = bool(enabled)
+
+
+def overlap_levels():
+    return _overlap[0]
+
+
+def level_stream(device):
+    s = _levels.get(device.index)
+    if s is None:
+        s = _levels[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
 def side_streams():
-    return list(_side.values())
+    """Every stream besides the current one that may hold work of the step: the weight-gradient
+    side streams and the level streams."""
+    return list(_side.values()) + list(_levels.values())
 
 
 def join_side():
-    """Current stream waits for all weight-gradient work issued on the side streams."""
-    if _side:
+    """Current stream waits for all work issued on the weight-gradient side streams and the
+    level streams (the optimizer and the gradient all-reduce call it before reading gradients)."""
+    if _side or _levels:
         cur = torch.cuda.current_stream()
-        for s in _side.values():
+        for s in side_streams():
             cur.wait_stream(s)
 
 

@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--concurrent-wgrad", action="store_true",
                    help="run weight gradients on a side stream, overlapped with backward-data (measured "
                         "0.3 ms/step slower than serial on the 3L-pub step now that the big blocks are fused)")
+    p.add_argument("--no-overlap-levels", action="store_true",
+                   help="run the decoder's top-level chain on the main stream (default: on the level stream, "
+                        "beside the encoder's lower levels)")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
     p.add_argument("--no-dist-graph", action="store_true", help="N > 1: never capture the collectives")
@@ -766,6 +769,7 @@ def main():
         size = tuple(a.size)
     torch.manual_seed(0)
     ops.set_concurrent_wgrad(a.concurrent_wgrad)
+    ops.set_overlap_levels(not a.no_overlap_levels)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
     if a.binding != "ctypes":

@@ -1,0 +1,133 @@
+"""The HEADLINE configuration pinned against the REFERENCE ITSELF at full size: one training
+step of the published 3-layer model at 512 x 512 x 128 (vqvae/model.py:95-163;
+slurm-jobs/train_vqvae_3d.job:76-86) on the GPU, bf16 (BASELINE's dtype) and fp16 (the
+reference's own AMP format), against tests/golden/model_3l_pub_512.npz -- written by
+tools/make_golden_fullsize.py, which imports /root/reference and runs the reference's own
+VQVAE.training_step + backward in fp32 on this container's CPU from the same perturbed seed-0
+weights (p += 0.02 randn, seed 1) and the same seed-1234 volume.
+
+What the fixture holds and how it is compared (bounds below, stated with the measured values):
+  * per-level code match, floored per dtype (bf16 >= 94 / 91 / 94 %, fp16 >= 99 / 99.5 / 100 %);
+    codes are bit-exact given identical fp32 z (test_gpu_fullsize.py), so a mismatch is a z that
+    16-bit rounding moved across a Voronoi boundary;
+  * the loss and the three commitment losses (relative);
+  * the decoded volume on the fixture's stride-8 lattice (relative MSE);
+  * gradients: every parameter's norm (relative), the whole sampled gradient vector (relative L2
+    and cosine), every weight tensor's sampled entries (relative L2 and cosine; tensors of more
+    than 4,096 entries are represented by 512 seeded positions, so their error is an estimate),
+    the scalar biases / scales per block stack as one vector.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+PUB3 = dict(n_bottleneck_blocks=3, n_pre_quantization_blocks=50, n_post_quantization_blocks=50,
+            n_post_upscale_blocks=3, n_post_downscale_blocks=2, num_embeddings=[128, 256, 512])
+PATH = os.path.join(GOLDEN, "model_3l_pub_512.npz")
+# per dtype: code floors (bottom, mid, top), (loss rel, commitment rel, decoded rel-MSE, sampled-
+# gradient rel-L2 / cosine, per-tensor rel-L2 / cosine, scalar-group rel-L2, gradient-norm rel).
+# Measured (r05): bf16 codes 94.70 / 92.00 / 95.31 %, loss 1.3e-3, decoded 7.7e-4, sampled gradient
+# 2.46 % / 0.99976, worst tensor 0.387 / 0.990; fp16 codes 99.35 / 99.65 / 100 %, loss 2.4e-6, decoded
+# 5.5e-6, sampled gradient 1.67 % / 0.99986, worst tensor 0.116 / 0.9956.  bf16's mid level sits
+# below its 256^2 floor because 6 of the 128 top codes flip at this size and every mid voxel is
+# conditioned on the top level's ST output through the UpBlock (two ResizeConvs + 3 + 3 blocks:
+# a receptive field spanning most of the 32 x 32 x 8 mid grid); fp16 flips none.
+BOUNDS = {"bf16": ((0.94, 0.91, 0.94), (1e-2, 5e-2, 1.5e-3, 0.04, 0.999, 0.5, 0.98, 0.1, 0.5)),
+          "fp16": ((0.99, 0.995, 1.0), (2e-3, 1e-2, 2e-5, 0.025, 0.9998, 0.15, 0.99, 0.05, 0.1))}
+
+
+def _perturb(m, seed=1, std=0.02):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for _, p in sorted(m.named_parameters()):
+            p.add_(std * torch.randn(p.shape, generator=g))
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+def test_published_model_fullsize_vs_reference(gpu, dt):
+    import vq3d
+    from vq3d.optim import GradScaler
+    ref = np.load(PATH)
+    size = tuple(int(v) for v in ref["size"])
+    torch.manual_seed(0)
+    m = vq3d.VQVAE(vq3d.default_args(compute_dtype=dt, base_lr=1e-4, **PUB3))
+    _perturb(m)
+    x = torch.rand((1, 1) + size, generator=torch.Generator().manual_seed(1234)) * 4.5 - 0.5
+    m = m.to(gpu)
+    m.train()
+    opt = m.configure_optimizers()
+    opt.zero_grad()
+    cap = {}
+    fwd = m.forward
+
+    def capture(data):
+        cap["r"] = fwd(data)
+        return cap["r"]
+    m.forward = capture
+    loss = m.training_step((x.to(gpu), torch.tensor([size[2]])), 0)
+    del m.forward
+    scaler = GradScaler(gpu, init_scale=2.0 ** 16, enabled=dt == "fp16")
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
+    vq3d.ops.join_side()
+    torch.cuda.synchronize()
+    assert float(scaler.found_inf) == 0.0
+    dec, (commit, _, idxs) = cap["r"]
+    s = int(ref["dec_stride"])
+    d_gpu = dec.detach()[0, 0, ::s, ::s, ::s].float().cpu().double()
+    d_ref = torch.from_numpy(ref["dec"]).double()
+    rmse = float(((d_gpu - d_ref) ** 2).sum() / (d_ref ** 2).sum())
+    match = [float((a.cpu().numpy() == ref[f"idx{lvl}"]).mean()) for lvl, a in enumerate(idxs)]
+    lr = abs(float(loss.detach()) - float(ref["loss"])) / abs(float(ref["loss"]))
+    crel = max(abs(float(c) - float(ref[f"commit{lvl}"])) / abs(float(ref[f"commit{lvl}"]))
+               for lvl, c in enumerate(commit))
+    # gradients at the fixture's positions
+    gs, rs, tensors, groups, norms = [], [], [], {}, []
+    for n, p in m.named_parameters():
+        g = p.grad.detach().reshape(-1).double().cpu()
+        r = torch.from_numpy(ref[f"grad/{n}"]).double()
+        rn = float(ref[f"gnorm/{n}"])
+        if rn > 0 and g.numel() > 1:  # a lone scalar is a near-cancelling sum: no meaningful relative error
+            norms.append((abs(float(g.norm()) - rn) / rn, n))
+        if f"gpos/{n}" in ref:
+            g = g[torch.from_numpy(ref[f"gpos/{n}"])]
+        if float(r.norm()) == 0:
+            continue
+        gs.append(g)
+        rs.append(r)
+        if g.numel() > 1:
+            tensors.append((float((g - r).norm() / r.norm()), float((g * r).sum() / (g.norm() * r.norm())), n))
+        else:
+            key = ".".join(n.split(".")[:3])
+            groups.setdefault(key, ([], []))
+            groups[key][0].append(g)
+            groups[key][1].append(r)
+    fg, fr = torch.cat(gs), torch.cat(rs)
+    flat_rel = float((fg - fr).norm() / fr.norm())
+    flat_cos = float((fg * fr).sum() / (fg.norm() * fr.norm()))
+    # scalar groups of >= 2 entries (a lone scalar, e.g. decoder.out.bias, is a near-cancelling
+    # sum over ~10^7 voxels: no meaningful relative error)
+    scal = sorted(((float((torch.cat(a) - torch.cat(b)).norm() / torch.cat(b).norm()), k)
+                   for k, (a, b) in groups.items() if len(a) > 1), reverse=True)
+    worst_rel, worst_cos, worst_norm = max(tensors), min(tensors, key=lambda t: t[1]), max(norms)
+    print(f"{dt} 3L-pub {size} vs the reference: loss gpu {float(loss):.6f} ref {float(ref['loss']):.6f} rel {lr:.2e}; "
+          f"commitment worst rel {crel:.2e}; code match bottom/mid/top {match}; decoded rel-MSE (stride {s}) "
+          f"{rmse:.2e}; sampled gradient rel-L2 {flat_rel:.3e} cosine {flat_cos:.6f}; worst tensor rel-L2 "
+          f"{worst_rel[0]:.3f} ({worst_rel[2]}), worst cosine {worst_cos[1]:.4f} ({worst_cos[2]}); worst "
+          f"gradient-norm rel {worst_norm[0]:.3f} ({worst_norm[1]}); worst scalar group {scal[0][0]:.3f} ({scal[0][1]})")
+    floors, (b_loss, b_commit, b_mse, b_rel, b_cos, b_trel, b_tcos, b_scal, b_norm) = BOUNDS[dt]
+    for lvl, (mm, fl) in enumerate(zip(match, floors)):
+        assert mm >= fl, (lvl, mm)
+    assert lr <= b_loss, lr
+    assert crel <= b_commit, crel
+    assert rmse <= b_mse, rmse
+    assert flat_rel <= b_rel and flat_cos >= b_cos, (flat_rel, flat_cos)
+    assert worst_rel[0] <= b_trel and worst_cos[1] >= b_tcos, (worst_rel, worst_cos)
+    assert scal[0][0] <= b_scal, scal[0]
+    assert worst_norm[0] <= b_norm, worst_norm

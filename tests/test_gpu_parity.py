@@ -245,13 +245,14 @@ def test_model_bf16_step(gpu):
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_concurrent_wgrad_and_graph_replay_match_serial(gpu, graph):
-    """Weight gradients on the side stream (and the whole step captured / replayed as a HIP
-    graph) give the same gradients and updated weights as the serial eager step: only the
-    fp32-atomic summation order may differ."""
+    """Weight gradients on the side stream and the decoder's top-level chain on the level stream
+    (and the whole step captured / replayed as a HIP graph) give the same gradients and updated
+    weights as the serial eager step: only the fp32-atomic summation order may differ."""
     from vq3d import ops
 
     def run(concurrent, use_graph):
         ops.set_concurrent_wgrad(concurrent)
+        ops.set_overlap_levels(concurrent)
         try:
             m, _ = load_model("model_2l_blocks_32", gpu, "bf16")
             opt = m.configure_optimizers()
@@ -283,9 +284,66 @@ def test_concurrent_wgrad_and_graph_replay_match_serial(gpu, graph):
             return m.flat.grad.clone(), m.flat.data.clone()
         finally:
             ops.set_concurrent_wgrad(False)
+            ops.set_overlap_levels(True)
 
     g0, w0 = run(False, False)
     g1, w1 = run(True, graph)
     scale = g0.abs().max()
     assert float((g1 - g0).abs().max()) <= 2e-2 * float(scale), float((g1 - g0).abs().max() / scale)
     assert float((w1 - w0).abs().max()) <= 1e-3 * float(w0.abs().max())
+
+
+def test_level_overlap_matches_serial_3l(gpu):
+    """The 3-layer model (tests/golden/model_3l_b2_64 weights, batch 2): with the decoder's top-level
+    chain on the level stream the forward is bit-identical to the serial one (loss, decoded, codes)
+    and the gradients agree up to the fp32-atomic summation order; eager and captured."""
+    from vq3d import ops
+
+    def run(overlap, use_graph):
+        ops.set_overlap_levels(overlap)
+        try:
+            m, _ = load_model("model_3l_b2_64", gpu, "bf16")
+            x = (torch.rand((2, 1, 64, 64, 64), generator=torch.Generator().manual_seed(9)) * 4.5 - 0.5).to(gpu)
+            nvs = torch.tensor([64, 64], device=gpu)
+            m.train()
+            cap = {}
+            fwd = m.forward
+
+            def capture(data):
+                cap["r"] = fwd(data)
+                return cap["r"]
+            m.forward = capture
+
+            def step():
+                m.flat.zero_grad()
+                loss = m.training_step((x, nvs), 0)
+                loss.backward()
+                ops.join_side()
+                return loss
+            step()  # first pass
+            if use_graph:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    step()
+                torch.cuda.current_stream().wait_stream(side)
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    loss = step()
+                gr.replay()
+            else:  # the same three training-mode steps (each moves the codebooks' EMA state)
+                step()
+                loss = step()
+            torch.cuda.synchronize()
+            dec, (_, _, idx) = cap["r"]
+            return float(loss), dec.float().clone(), [i.clone() for i in idx], m.flat.grad.clone()
+        finally:
+            ops.set_overlap_levels(True)
+
+    l0, d0, i0, g0 = run(False, False)
+    for use_graph in (False, True):
+        l1, d1, i1, g1 = run(True, use_graph)
+        assert l1 == l0 and torch.equal(d1, d0), (use_graph, l1, l0)
+        assert all(torch.equal(a, b) for a, b in zip(i1, i0))
+        scale = float(g0.abs().max())
+        assert float((g1 - g0).abs().max()) <= 2e-2 * scale, (use_graph, float((g1 - g0).abs().max()) / scale)
