@@ -452,17 +452,25 @@ class Decoder(nn.Module):
             after_channels = before_channels
         self.out = Conv3d(base_network_channels, out_channels, kernel_size=1)
 
-    def forward(self, quantizations, top=None):
-        """top: (output of up[-1] on the top code, the stream it was issued on) when the caller
-        already started the top-level chain (VQVAE.forward); the current stream joins it here."""
+    def forward(self, quantizations, pre=None):
+        """pre: (output of the first k level chains, top first; the stream they were issued on; k)
+        when the caller already ran them (VQVAE.forward); the current stream joins it here."""
+        k, out = 0, None
+        if pre is not None:
+            out, stream, k = pre
+            torch.cuda.current_stream().wait_stream(stream)
         for i, (quantization, up) in enumerate(reversed(list(zip(quantizations, self.up)))):
-            if i == 0 and top is not None:
-                out, stream = top
-                torch.cuda.current_stream().wait_stream(stream)
+            if i < k:
                 continue
             out = quantization if i == 0 else self.proj[-i](quantization, out)
             out = up(out)
         return self.out(out)
+
+    def level_chain(self, i, quantization, out):
+        """The decoder's i-th level chain, top first (layers.py:511-514): proj(cat[q, out]) for
+        i > 0, then the level's post-quantize blocks and up block."""
+        out = quantization if i == 0 else self.proj[-i](quantization, out)
+        return self.up[-1 - i](out)
 
 
 # ============================================================================================ quantizer

@@ -103,21 +103,25 @@ class VQVAE(nn.Module):
     def forward(self, data):
         if torch.is_grad_enabled():
             parallel.step_begin()
-        top, hook = {}, None
-        if ops.overlap_levels() and data.is_cuda and len(self.decoder.up) > 1:
-            # the decoder's top-level chain (post-quantize blocks + up block, layers.py:510-514)
-            # needs only the top code: start it on the level stream as soon as the top Quantizer
-            # is done, beside the encoder's lower levels (layers.py:583-586); same arithmetic
+        pre, hook = {"k": 0}, None
+        levels = len(self.decoder.up)
+        if ops.overlap_levels() and data.is_cuda and levels > 1:
+            # Each decoder level chain above the bottom (layers.py:511-514: proj(cat[q_l, out]),
+            # post-quantize blocks, up block) needs only its own code and the chain above it, so it
+            # starts on the level stream as soon as that level's Quantizer is done, beside the
+            # encoder's lower levels (layers.py:583-586).  Same launches, same arithmetic.
             def hook(quantization):
-                if "out" in top:
+                i = pre["k"]
+                if i >= levels - 1:  # the bottom chain needs the last code: nothing left to overlap
                     return
-                cur = torch.cuda.current_stream()
                 s = ops.level_stream(data.device)
-                s.wait_stream(cur)
+                s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    top["out"] = (self.decoder.up[-1](quantization[1]), s)
+                    pre["out"] = self.decoder.level_chain(i, quantization[1], pre.get("out"))
+                pre["k"] = i + 1
         commitment_loss, quantizations, encoding_idx = zip(*self.encoder(data, on_quantized=hook))
-        decoded = self.decoder(quantizations, top=top.get("out"))
+        decoded = self.decoder(quantizations, pre=(pre["out"], ops.level_stream(data.device), pre["k"])
+                               if pre["k"] else None)
         return decoded, (commitment_loss, quantizations, encoding_idx)
 
     def encode(self, data):
