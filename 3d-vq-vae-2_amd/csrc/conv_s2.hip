@@ -9,6 +9,7 @@
 // stride-2 layers carry few channels on large grids (4..16 at 512^2..128^2) or few voxels.
 #include "engines.h"
 
+
 #include <algorithm>
 #include <type_traits>
 
@@ -219,92 +220,196 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict_
     }
 }
 
-// Parity-class form (one input of CI = 4 / 8 channels, Cout CO = 4 / 8, circular, pad k / 2 - 1,
-// every extent even): blockIdx.y = the (h, w) parity class (a, b) of the input voxels, a thread
-// owns the D-pair i = (2 oh + a, 2 ow + b, 2 od + {0, 1}) -- one 8 / 16-byte run of gx.  Every tap
-// index is then the same for all lanes (the weights come through the scalar cache, no LDS
-// broadcast), and the pair shares its h / w rows of g: (k/2)^2 x (k/2 + 1) rows for 2 voxels.
-template <typename T, int CI, int CO, int K>
-__global__ __launch_bounds__(256) void k_dgrad_s2_pair(S2Args a, const T *__restrict__ g,
+// Few-channel matrix-core form (CI, CO in {4, 8}; 4x4x4 circular p = 1 or 2x2x2 p = 0, one input,
+// every extent even, 16-bit): the full-resolution down blocks' branch conv2 (4 -> 4 at 512^2 x 128,
+// 8 -> 8 at 256^2 x 64) and skip conv (4 -> 8).  The input grid is cut into 2 x 2 x 2 CELLS; cell
+// (mh, mw, md) holds the 8 input voxels i = 2 m + v that read the g rows o = m + e, e in {-1, 0, 1}^3
+// (tap t = v + p - 2 e per dimension, 0 <= t < k; for k = 2 only e = 0).  So a cell's backward-data
+// is one dense product gx[v][ci] = sum_(e, co) A[(v, ci)][(e, co)] g[m + e][co] with the tap weights
+// (and zeros where t falls outside the kernel) as the MFMA A operand -- rows (v, ci) in 16-row tiles,
+// staged once per workgroup in LDS -- and 16 cells along D as the B columns (lane (n, kb): the 8 k
+// entries of g rows e for cell n, one 8- / 16-byte load per row).  Every lane's accumulator then
+// holds 4 channels of one voxel of its cell, and lanes kb, kb + 1 own neighbouring voxels / channel
+// halves: 16 cells x 16 (or 32) contiguous bytes per store.  The index math is one line (b, mh, mw)
+// per tile of 16 cells (128 input voxels).  The epilogue is k_dgrad_s2's.
+template <int CI, int CO, int K>
+__global__ __launch_bounds__(256) void k_dgrad_s2_cell(S2Args a, const h16_t *__restrict__ g,
                                                       const float *__restrict__ gscale, const float *__restrict__ w,
-                                                      BwdEpi<T> be, T *__restrict__ gx, float *dpre, float *dpost) {
-    constexpr int P = K / 2 - 1, NT_ = K / 2, K3 = K * K * K;
+                                                      BwdEpi<h16_t> be, h16_t *__restrict__ gx, float *dpre,
+                                                      float *dpost) {
+    constexpr int NR = K == 4 ? 27 : 1, K3 = K * K * K, NKS = (NR * CO + 31) / 32, NM = 8 * CI / 16;
+    constexpr int EPL = CO == 4 ? 2 : 1;  // g rows per lane and k-step
+    static_assert((CI == 4 || CI == 8) && (CO == 4 || CO == 8) && (K == 2 || K == 4), "few-channel form");
+    __shared__ uint4 afr[NM * NKS * 64];  // packed A fragments [m-tile][k-step][lane]
     __shared__ float red[8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, n = lane & 15;
+    for (int idx = tid; idx < NM * NKS * 64; idx += 256) {
+        const int l = idx & 63, ms = idx >> 6, st = ms % NKS, m = ms / NKS;
+        const int R = 16 * m + (l & 15), v = R / CI, ci = R - v * CI;
+        const int vh = v >> 2, vw = (v >> 1) & 1, vd = v & 1;
+        uint32_t u[4];
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+            float x2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = 32 * st + 8 * (l >> 4) + 2 * e2 + h, r = k / CO, co = k - r * CO;
+                float x = 0.f;
+                if (r < NR) {
+                    const int eh = K == 4 ? r / 9 - 1 : 0, ew = K == 4 ? (r / 3) % 3 - 1 : 0, ed = K == 4 ? r % 3 - 1 : 0;
+                    const int th = vh + a.p - 2 * eh, tw = vw + a.p - 2 * ew, td = vd + a.p - 2 * ed;
+                    if (th >= 0 && th < K && tw >= 0 && tw < K && td >= 0 && td < K)
+                        x = w[(co * CI + ci) * K3 + (th * K + tw) * K + td];
+                }
+                x2[h] = x;
+            }
+            u[e2] = uint32_t(f2h(x2[0])) | (uint32_t(f2h(x2[1])) << 16);
+        }
+        afr[idx] = uint4{u[0], u[1], u[2], u[3]};
+    }
+    __syncthreads();
     ActDeriv dv;
     dv.mode = be.aux ? be.mode : 0;
     dv.p = (dv.mode && be.p) ? *be.p : 0.f;
     const float gs = gscale ? *gscale : 1.f;
-    const int pa = int(blockIdx.y) >> 1, pb = int(blockIdx.y) & 1;
     float pre = 0.f, post = 0.f;
-    const int64_t npair = int64_t(a.B) * a.oH * a.oW * a.oD;
-    for (int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x; e < npair; e += int64_t(gridDim.x) * 256) {
-        uint32_t q = uint32_t(e);
-        uint32_t q2 = a.fD.div(q);
-        const int od = int(q - q2 * uint32_t(a.oD));
-        q = a.fW.div(q2);
-        const int ow = int(q2 - q * uint32_t(a.oW));
-        q2 = a.fH.div(q);
-        const int oh = int(q - q2 * uint32_t(a.oH));
-        const int b = int(q2);
-        const int ih = 2 * oh + pa, iw = 2 * ow + pb;
-        // per dimension: tap t meets g row (i + P - t) / 2 (circular); h / w taps: parity-fixed
-        int rh[NT_], rw[NT_];
+    const int hh = a.iH >> 1, hw = a.iW >> 1, hd = a.iD >> 1;  // cells per dimension (= the g grid)
+    const int ntl = (hd + 15) >> 4;                              // 16-cell tiles per line
+    const int ntile = a.B * hh * hw * ntl;
+    // one tile's operands: the B fragments, the epilogue's aux / addend rows, the output offsets
+    struct Tile {
+        uint4 bv[NKS];
+        uint2 aux[NM], add[NM];
+        int64_t ev[NM];
+        bool live;
+    };
+    // tile coordinates (line (b, mh, mw), first cell md0), advanced incrementally along a wave's
+    // contiguous tile range (no divisions per tile)
+    struct Pos {
+        int md0, mw, mh, b;
+    };
+    auto fetch = [&](const Pos &P, Tile &T) {
+        const int md = P.md0 + n;
+        T.live = md < hd;
+        const int mdc = T.live ? md : hd - 1;  // dead lanes read a real row (never stored)
+        // the g rows this lane's k entries read: o = m + e per dimension (circular on the g grid)
+        int rowh[3], roww[3], rowd[3];
 #pragma unroll
-        for (int x = 0; x < NT_; ++x) {
-            const int th = ((pa + P) & 1) + 2 * x, tw = ((pb + P) & 1) + 2 * x;
-            int r = ih + P - th;
-            r = r < 0 ? r + a.iH : (r >= a.iH ? r - a.iH : r);
-            rh[x] = r >> 1;
-            r = iw + P - tw;
-            r = r < 0 ? r + a.iW : (r >= a.iW ? r - a.iW : r);
-            rw[x] = r >> 1;
+        for (int e = 0; e < 3; ++e) {
+            const int oh_ = P.mh + e - 1, ow_ = P.mw + e - 1, od_ = mdc + e - 1;
+            rowh[e] = oh_ < 0 ? oh_ + a.oH : (oh_ >= a.oH ? oh_ - a.oH : oh_);
+            roww[e] = ow_ < 0 ? ow_ + a.oW : (ow_ >= a.oW ? ow_ - a.oW : ow_);
+            rowd[e] = od_ < 0 ? od_ + a.oD : (od_ >= a.oD ? od_ - a.oD : od_);
         }
-        float acc[2][CI];
+        const int64_t gb = int64_t(P.b) * a.oH;
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+        for (int st = 0; st < NKS; ++st) {
+            uint32_t u[4];
 #pragma unroll
-            for (int c = 0; c < CI; ++c) acc[v][c] = 0.f;
-#pragma unroll
-        for (int x = 0; x < NT_; ++x)
-#pragma unroll
-            for (int y = 0; y < NT_; ++y) {
-                const int th = ((pa + P) & 1) + 2 * x, tw = ((pb + P) & 1) + 2 * y;
-                const int64_t rowb = (int64_t(b) * a.oH + rh[x]) * a.oW + rw[y];
-#pragma unroll
-                for (int v = 0; v < 2; ++v)
-#pragma unroll
-                    for (int z = 0; z < NT_; ++z) {
-                        const int td = ((v + P) & 1) + 2 * z;
-                        int r = 2 * od + v + P - td;
-                        r = r < 0 ? r + a.iD : (r >= a.iD ? r - a.iD : r);
-                        float gr[CO];
-                        load_row<T, CO>(g + (rowb * a.oD + (r >> 1)) * CO, gr);
-                        const int tap = (th * K + tw) * K + td;
-#pragma unroll
-                        for (int co = 0; co < CO; ++co)
-#pragma unroll
-                            for (int c = 0; c < CI; ++c)
-                                acc[v][c] = fmaf(gr[co], w[(co * CI + c) * K3 + tap], acc[v][c]);
-                    }
+            for (int h2 = 0; h2 < EPL; ++h2) {
+                // k entries past the 27 rows meet zero weights: they read row NR - 1 (finite data)
+                const int r = min((32 * st + 8 * kb) / CO + h2, NR - 1);
+                const int eh = K == 4 ? r / 9 : 1, ew = K == 4 ? (r / 3) % 3 : 1, ed = K == 4 ? r % 3 : 1;
+                const h16_t *src = g + (((gb + rowh[eh]) * a.oW + roww[ew]) * a.oD + rowd[ed]) * CO;
+                if constexpr (CO == 8) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(src);
+                    u[0] = x.x, u[1] = x.y, u[2] = x.z, u[3] = x.w;
+                } else {
+                    const uint2 x = *reinterpret_cast<const uint2 *>(src);
+                    u[2 * h2] = x.x, u[2 * h2 + 1] = x.y;
+                }
             }
-        const int64_t vox = ((int64_t(b) * a.iH + ih) * a.iW + iw) * a.iD + 2 * od;  // first of the pair
-        float aux[2 * CI], add[2 * CI], o[2 * CI];
-        if (dv.mode) load_row<T, 2 * CI>(be.aux + vox * CI, aux);
-        if (be.addend) load_row<T, 2 * CI>(be.addend + vox * CI, add);
+            if constexpr (CO == 4 && EPL == 1) u[2] = u[3] = 0u;
+            T.bv[st] = uint4{u[0], u[1], u[2], u[3]};
+        }
+        // lane (n, kb) of m-tile m: rows 16 m + 4 kb .. + 3 = 4 channels of voxel v of cell n
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+        for (int m = 0; m < NM; ++m) {
+            const int R = 16 * m + 4 * kb, v = R / CI, c0 = R - v * CI;
+            const int vh = v >> 2, vw = (v >> 1) & 1, vd = v & 1;
+            T.ev[m] = (((int64_t(P.b) * a.iH + 2 * P.mh + vh) * a.iW + 2 * P.mw + vw) * a.iD + 2 * mdc + vd) * CI + c0;
+            T.aux[m] = dv.mode ? *reinterpret_cast<const uint2 *>(be.aux + T.ev[m]) : uint2{0u, 0u};
+            T.add[m] = be.addend ? *reinterpret_cast<const uint2 *>(be.addend + T.ev[m]) : uint2{0u, 0u};
+        }
+    };
+    auto advance = [&](Pos &P) {
+        P.md0 += 16;
+        if (P.md0 >= hd) {
+            P.md0 = 0;
+            if (++P.mw == hw) {
+                P.mw = 0;
+                if (++P.mh == hh) {
+                    P.mh = 0;
+                    ++P.b;
+                }
+            }
+        }
+    };
+    auto compute = [&](const Tile &T) {
 #pragma unroll
-            for (int c = 0; c < CI; ++c) {
-                float val = acc[v][c];
+        for (int m = 0; m < NM; ++m) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int st = 0; st < NKS; ++st)
+                acc = VQ3D_MFMA_16X16X32(__builtin_bit_cast(hx8, afr[(m * NKS + st) * 64 + lane]),
+                                         __builtin_bit_cast(hx8, T.bv[st]), acc, 0, 0, 0);
+            if (!T.live) continue;
+            const float ax[4] = {h2f_lo(T.aux[m].x), h2f_hi(T.aux[m].x), h2f_lo(T.aux[m].y), h2f_hi(T.aux[m].y)};
+            const float ad[4] = {h2f_lo(T.add[m].x), h2f_hi(T.add[m].x), h2f_lo(T.add[m].y), h2f_hi(T.add[m].y)};
+            float o[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float val = acc[c];
                 if (gscale) val = val * gs;
                 pre += val;
-                if (dv.mode) val = val * dv(aux[v * CI + c]);
+                if (dv.mode) val = val * dv(ax[c]);
                 post += val;
-                if (be.addend) val = val + add[v * CI + c];
-                o[v * CI + c] = val;
+                if (be.addend) val = val + ad[c];
+                o[c] = val;
             }
-        store_row<T, 2 * CI>(gx + vox * CI, o);
+            *reinterpret_cast<uint2 *>(gx + T.ev[m]) = uint2{uint32_t(f2h(o[0])) | (uint32_t(f2h(o[1])) << 16),
+                                                             uint32_t(f2h(o[2])) | (uint32_t(f2h(o[3])) << 16)};
+        }
+    };
+    // each wave walks a contiguous range of tiles (consecutive 16-cell runs of the lines)
+    const int nw = int(gridDim.x) * 4, wid = int(blockIdx.x) * 4 + wave;
+    const int per = (ntile + nw - 1) / nw, t0 = min(wid * per, ntile), t1 = min(t0 + per, ntile);
+    if (t0 >= t1) goto done;
+    {
+        Pos P;
+        {
+            const int line = t0 / ntl;
+            P.md0 = (t0 - line * ntl) * 16;
+            P.mw = line % hw;
+            const int q = line / hw;
+            P.mh = q % hh;
+            P.b = q / hh;
+        }
+        // small tiles (<= 16 B-fragment registers x m-tiles): software-pipelined, the next tile's
+        // loads in flight while this one computes; the wide ones keep one tile (their registers
+        // would halve the occupancy)
+        constexpr bool PIPE = CI * NKS <= 16;
+        if constexpr (PIPE) {
+            Tile nxt;
+            fetch(P, nxt);
+            for (int t = t0; t < t1; ++t) {
+                const Tile T = nxt;
+                if (t + 1 < t1) {
+                    advance(P);
+                    fetch(P, nxt);
+                }
+                compute(T);
+            }
+        } else {
+            for (int t = t0; t < t1; ++t) {
+                Tile T;
+                fetch(P, T);
+                compute(T);
+                advance(P);
+            }
+        }
     }
+done:
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
@@ -313,25 +418,6 @@ __global__ __launch_bounds__(256) void k_dgrad_s2_pair(S2Args a, const T *__rest
             if (dpost) atomicAdd(dpost, post);
         }
     }
-}
-
-
-// Matrix-core form for the wide layers (one input, Cin % 16 == 0, Cout % 8 == 0: the down blocks'
-// branch conv2 4x4x4 and skip conv 2x2x2 from 16 channels up, vqvae/layers.py:124-126,164-171).
-// blockIdx.y = the (h, w, d) parity class of the input voxels: every voxel of a class meets the
-// same (k/2)^3 taps, so per class the backward-data is one GEMM
-//     gx^T[ci][v] = sum over (j, co) of W[co][ci][tap_j] * g[o_j(v)][co]
-// with K = (k/2)^3 * Cout.  The weights are the MFMA A operand (so each lane's accumulator holds 4
-// consecutive input channels of one voxel: one 8-byte store), packed per (channel tile, k-step)
-// into LDS once per workgroup; the g rows are B (8 consecutive co of one tap: one 16-byte load per
-// lane and k-step).  The epilogue is k_dgrad_s2's (activation derivative from aux, addend, gscale,
-// prologue-scalar partial sums).
-__device__ __forceinline__ int s2_src(int i, int t, int p, int n_in, int n_out, int circ) {
-    int r = i + p - t;
-    if (circ) r = r < 0 ? r + n_in : (r >= n_in ? r - n_in : r);
-    else if (r < 0) return -1;
-    r >>= 1;
-    return r < n_out ? r : -1;
 }
 
 template <int K, int NTM>
@@ -476,23 +562,22 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
     if (int64_t(a.B) * a.iH * a.iW * a.iD >= (int64_t(1) << 31)) return fail("conv3d_bwd_data(s2): grid too large");
     {
         auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-        // k = 2, p = 0: every tap lands inside the grid, so the padding mode does not matter (the
-        // down blocks' zero-padded skip conv takes the circular pair kernel)
+        // few channels on the matrix cores over 2 x 2 x 2 cells (k_dgrad_s2_cell); k = 2, p = 0:
+        // every tap lands inside the grid, so the padding mode does not matter (the down blocks'
+        // zero-padded skip conv takes it too)
         if (std::is_same<T, h16_t>::value && (a.circ || (a.k == 2 && a.p == 0)) && a.Cin2 == 0 &&
             (a.Cin == 4 || a.Cin == 8) &&
             (a.Cout == 4 || a.Cout == 8) && a.p == a.k / 2 - 1 && a.iH == 2 * a.oH && a.iW == 2 * a.oW &&
             a.iD == 2 * a.oD && al16(g) && al16(gx) && (!be.aux || al16(be.aux)) && (!be.addend || al16(be.addend))) {
-            S2Args c = a;
-            c.fD = FastDiv(uint32_t(a.oD));
-            c.fW = FastDiv(uint32_t(a.oW));
-            c.fH = FastDiv(uint32_t(a.oH));
-            const int64_t npair = int64_t(a.B) * a.oH * a.oW * a.oD;
-            const dim3 pg(unsigned(std::max<int64_t>(1, std::min<int64_t>((npair + 255) / 256, 2048))), 4u, 1u);
+            // ~2,048 workgroups, each wave a contiguous range of 16-cell tiles
+            const int64_t ntile = int64_t(a.B) * a.oH * a.oW * ((a.oD + 15) / 16);
+            const dim3 fg(unsigned(std::max<int64_t>(1, std::min<int64_t>((ntile + 3) / 4, 2048))), 1u, 1u);
 #define PK(CI_, CO_, K_)                                                                                      \
             if (a.Cin == CI_ && a.Cout == CO_ && a.k == K_) {                                                  \
-                k_dgrad_s2_pair<T, CI_, CO_, K_><<<pg, 256, 0, s>>>(c, (const T *)g, gscale, w, be, (T *)gx,     \
-                                                                   dpre, dpost);                               \
-                return check_launch("conv3d_bwd_data(s2 pairs)");                                              \
+                k_dgrad_s2_cell<CI_, CO_, K_><<<fg, 256, 0, s>>>(a, (const h16_t *)g, gscale, w,                \
+                                                                 reinterpret_cast<const BwdEpi<h16_t> &>(be),    \
+                                                                 (h16_t *)gx, dpre, dpost);                    \
+                return check_launch("conv3d_bwd_data(s2 cell mma)");                                           \
             }
             PK(4, 4, 4) PK(4, 8, 4) PK(8, 4, 4) PK(8, 8, 4) PK(4, 4, 2) PK(4, 8, 2) PK(8, 4, 2) PK(8, 8, 2)
 #undef PK
