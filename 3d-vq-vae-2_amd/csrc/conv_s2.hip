@@ -420,6 +420,24 @@ done:
     }
 }
 
+// Matrix-core form for the wide layers (one input, Cin % 16 == 0, Cout % 8 == 0: the down blocks'
+// branch conv2 4x4x4 and skip conv 2x2x2 from 16 channels up, vqvae/layers.py:124-126,164-171).
+// blockIdx.y = the (h, w, d) parity class of the input voxels: every voxel of a class meets the
+// same (k/2)^3 taps, so per class the backward-data is one GEMM
+//     gx^T[ci][v] = sum over (j, co) of W[co][ci][tap_j] * g[o_j(v)][co]
+// with K = (k/2)^3 * Cout.  The weights are the MFMA A operand (so each lane's accumulator holds 4
+// consecutive input channels of one voxel: one 8-byte store), packed per (channel tile, k-step)
+// into LDS once per workgroup; the g rows are B (8 consecutive co of one tap: one 16-byte load per
+// lane and k-step).  The epilogue is k_dgrad_s2's (activation derivative from aux, addend, gscale,
+// prologue-scalar partial sums).
+__device__ __forceinline__ int s2_src(int i, int t, int p, int n_in, int n_out, int circ) {
+    int r = i + p - t;
+    if (circ) r = r < 0 ? r + n_in : (r >= n_in ? r - n_in : r);
+    else if (r < 0) return -1;
+    r >>= 1;
+    return r < n_out ? r : -1;
+}
+
 template <int K, int NTM>
 __global__ __launch_bounds__(256) void k_dgrad_s2_mma(S2Args a, const h16_t *__restrict__ g,
                                                      const float *__restrict__ gscale, const float *__restrict__ w,
