@@ -104,9 +104,11 @@ int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const
 bool col_supported(int batch, int C, int BR, int h, int w, int d);
 size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d);
 // xdt / odt: storage (VQ3D_HALF | VQ3D_F32) of the residual stream in (x, gx) and out (out, g)
+// chain: vq3d_preact_small_fwd_chain's mode bits (0: an unchained launch, the rest unused)
 int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1,
             const float *w2, const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3,
-            hipStream_t s);
+            hipStream_t s, int chain = 0, const void *t2in = nullptr, const float *w1n = nullptr,
+            const vq3d_preact_params *pn = nullptr, void *t2n = nullptr);
 int col_bwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *g, const void *x,
             const void *t2, const void *t3, const float *w1, const float *w2, const float *w3,
             const vq3d_preact_params &p, const vq3d_preact_grads &gr, void *workspace, void *gx, int stages,

@@ -257,11 +257,36 @@ __device__ __forceinline__ hx8 win_frag(const h16_t *h, int off) {
 // ============================================================================================ forward
 // TX / TO: storage of the residual stream in / out (bf16 or fp32; a run of blocks carries it in
 // fp32 between its blocks like the reference's autocast blocks, layers.py:187-193)
-template <int C, int BR, typename TX, typename TO>
+// CH (chained runs, vq3d_preact_small_fwd_chain): bit 0 -- this block's t2 was written by the
+// previous block's epilogue (t2in): phase A loads it on the halo instead of forming it from x;
+// bit 1 -- the epilogue also forms the NEXT block's t2 from this block's output (as stored, TO) with
+// that block's W1 / biases (w1n, pn) and writes it to t2n, so the next launch skips its halo math.
+// The formulas and their order are phase A's, so a chained run is bit-identical to an unchained one.
+template <typename T>
+__device__ __forceinline__ float as_stored(float v) {
+    if constexpr (sizeof(T) == 4) return v;
+    else return rbf(v);
+}
+template <int C, int BR>
+__device__ __forceinline__ void t2_of(const float (&xf)[C], const float *__restrict__ w1, const Scal &s, float (&t)[BR]) {
+    float u[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) u[c] = elu_f(xf[c] + s.b1a) + s.b1b;
+#pragma unroll
+    for (int oo = 0; oo < BR; ++oo) {
+        float acc = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc = fmaf(w1[oo * C + c], u[c], acc);
+        t[oo] = elu_f(acc + s.b2a) + s.b2b;
+    }
+}
+template <int C, int BR, typename TX, typename TO, int CH = 0>
 __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ x, const float *__restrict__ w1,
                                                 const float *__restrict__ w2, const float *__restrict__ w3,
                                                 vq3d_preact_params p, TO *__restrict__ out,
-                                                h16_t *__restrict__ t2o, h16_t *__restrict__ t3o) {
+                                                h16_t *__restrict__ t2o, h16_t *__restrict__ t3o,
+                                                const h16_t *__restrict__ t2in, const float *__restrict__ w1n,
+                                                vq3d_preact_params pn, h16_t *__restrict__ t2n) {
     using K = K3<BR>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     h16_t *t2h = reinterpret_cast<h16_t *>(smem);            // [HVX][BR] + PADE
@@ -269,6 +294,8 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
     int *lbase = reinterpret_cast<int *>(accs + acc_floats(BR));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
     const Scal s = load_scal(p);
+    Scal sn{};
+    if constexpr ((CH & 2) != 0) sn = load_scal(pn);
     hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, false>(w2, k, lane);
@@ -284,8 +311,22 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
         __syncthreads();  // the previous brick's readers of the LDS tiles are done
         line_table(a, o, lbase);
         __syncthreads();
-        // A. t2 on the halo, every x load issued first
-        {
+        // A. t2 on the halo: loaded (chained), or formed from x with every x load issued first
+        if constexpr ((CH & 1) != 0) {
+            constexpr int P = (HVX + NT - 1) / NT;
+            typename Vec<BR>::U tv[P];
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                int line, pos;
+                const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
+                tv[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2in + int64_t(vx) * BR);
+            }
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const int q = tid + u * NT;
+                if (q < HVX) *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = tv[u];
+            }
+        } else {
             constexpr int P = (HVX + NT - 1) / NT;
             Raw<TX, C> xv[P];
 #pragma unroll
@@ -300,15 +341,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
                 if (!(COL_EXP & 2) && q < HVX) {
                     float xf[C], t[BR];
                     unraw<TX, C>(xv[u], xf);
-#pragma unroll
-                    for (int c = 0; c < C; ++c) xf[c] = elu_f(xf[c] + s.b1a) + s.b1b;
-#pragma unroll
-                    for (int oo = 0; oo < BR; ++oo) {
-                        float acc = 0.f;
-#pragma unroll
-                        for (int c = 0; c < C; ++c) acc = fmaf(w1[oo * C + c], xf[c], acc);
-                        t[oo] = elu_f(acc + s.b2a) + s.b2b;
-                    }
+                    t2_of<C, BR>(xf, w1, s, t);
                     *reinterpret_cast<typename Vec<BR>::U *>(t2h + q * BR) = packv<BR>(t);
                 }
             }
@@ -334,7 +367,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
         // C. t3 and out of the thread's 4 voxels (and their t2, saved for the backward)
         if constexpr ((COL_EXP & 16) != 0) continue;
         const int v0 = ln * BD + dg * DV;
-        if (t2o) {
+        if (t2o && (CH & 1) == 0) {  // chained: this block's t2 is already in memory
             const h16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
             uint32_t w[DV * BR / 2];
             if constexpr (BR == 1) {  // 4 positions at an odd element offset
@@ -371,6 +404,23 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
             xf[e] = r * s.sc + s.b4 + xf[e];
         }
         stvec<TO, DV * C>(out + vox0 * C, xf);
+        if constexpr ((CH & 2) != 0) {  // the next block's t2 from this output as stored
+            float tn[DV][BR];
+#pragma unroll
+            for (int vv = 0; vv < DV; ++vv) {
+                float xs[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) xs[c] = as_stored<TO>(xf[vv * C + c]);
+                t2_of<C, BR>(xs, w1n, sn, tn[vv]);
+            }
+            uint32_t w[DV * BR / 2];
+#pragma unroll
+            for (int i = 0; i < DV * BR / 2; ++i) {
+                const int e0 = 2 * i, e1 = 2 * i + 1;
+                w[i] = uint32_t(f2h(tn[e0 / BR][e0 % BR])) | (uint32_t(f2h(tn[e1 / BR][e1 % BR])) << 16);
+            }
+            store_words<DV * BR / 2>(t2n + vox0 * BR, w);
+        }
     }  // bricks
 }
 
@@ -722,16 +772,35 @@ void allow(Kern k, size_t lds) {
     (void)hipGetLastError();
 }
 
-template <int C, int BR, typename TX, typename TO>
-void launch_fwd(const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
-                const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, hipStream_t s) {
+// the chain links of one forward launch (CH bits: 1 chained in, 2 chained out)
+struct FwdChain {
+    int ch = 0;
+    const h16_t *t2in = nullptr;
+    const float *w1n = nullptr;
+    vq3d_preact_params pn{};
+    h16_t *t2n = nullptr;
+};
+
+template <int C, int BR, typename TX, typename TO, int CH>
+void launch_fwd_ch(const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
+                   const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, const FwdChain &c, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        allow(k_col_fwd<C, BR, TX, TO>, fwd_lds<C, BR>());
+        allow(k_col_fwd<C, BR, TX, TO, CH>, fwd_lds<C, BR>());
         attr = true;
     }
-    k_col_fwd<C, BR, TX, TO><<<FWD_PERSIST ? a.nwg : a.nbricks, NT, fwd_lds<C, BR>(), s>>>(
-        a, static_cast<const TX *>(x), w1, w2, w3, p, static_cast<TO *>(out), t2, t3);
+    k_col_fwd<C, BR, TX, TO, CH><<<FWD_PERSIST ? a.nwg : a.nbricks, NT, fwd_lds<C, BR>(), s>>>(
+        a, static_cast<const TX *>(x), w1, w2, w3, p, static_cast<TO *>(out), t2, t3, c.t2in, c.w1n, c.pn, c.t2n);
+}
+template <int C, int BR, typename TX, typename TO>
+void launch_fwd(const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
+                const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, const FwdChain &c, hipStream_t s) {
+    switch (c.ch) {
+    case 1: launch_fwd_ch<C, BR, TX, TO, 1>(a, x, w1, w2, w3, p, out, t2, t3, c, s); break;
+    case 2: launch_fwd_ch<C, BR, TX, TO, 2>(a, x, w1, w2, w3, p, out, t2, t3, c, s); break;
+    case 3: launch_fwd_ch<C, BR, TX, TO, 3>(a, x, w1, w2, w3, p, out, t2, t3, c, s); break;
+    default: launch_fwd_ch<C, BR, TX, TO, 0>(a, x, w1, w2, w3, p, out, t2, t3, c, s); break;
+    }
 }
 template <int C, int BR, typename TX, typename TO>
 void launch_bwd(const CArgs &a, const void *g, const void *x, const h16_t *t2, const h16_t *t3, const float *w1,
@@ -757,11 +826,11 @@ void launch_bwd(const CArgs &a, const void *g, const void *x, const h16_t *t2, c
 // the (x, out) storage pair: VQ3D_HALF / VQ3D_F32 each
 template <int C, int BR>
 void fwd_io(int xdt, int odt, const CArgs &a, const void *x, const float *w1, const float *w2, const float *w3,
-            const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, hipStream_t s) {
-    if (xdt == VQ3D_HALF && odt == VQ3D_HALF) launch_fwd<C, BR, h16_t, h16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
-    else if (xdt == VQ3D_HALF) launch_fwd<C, BR, h16_t, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
-    else if (odt == VQ3D_HALF) launch_fwd<C, BR, float, h16_t>(a, x, w1, w2, w3, p, out, t2, t3, s);
-    else launch_fwd<C, BR, float, float>(a, x, w1, w2, w3, p, out, t2, t3, s);
+            const vq3d_preact_params &p, void *out, h16_t *t2, h16_t *t3, const FwdChain &c, hipStream_t s) {
+    if (xdt == VQ3D_HALF && odt == VQ3D_HALF) launch_fwd<C, BR, h16_t, h16_t>(a, x, w1, w2, w3, p, out, t2, t3, c, s);
+    else if (xdt == VQ3D_HALF) launch_fwd<C, BR, h16_t, float>(a, x, w1, w2, w3, p, out, t2, t3, c, s);
+    else if (odt == VQ3D_HALF) launch_fwd<C, BR, float, h16_t>(a, x, w1, w2, w3, p, out, t2, t3, c, s);
+    else launch_fwd<C, BR, float, float>(a, x, w1, w2, w3, p, out, t2, t3, c, s);
 }
 template <int C, int BR>
 void bwd_io(int xdt, int odt, const CArgs &a, const void *g, const void *x, const h16_t *t2, const h16_t *t3,
@@ -811,12 +880,18 @@ size_t col_workspace_bytes(int batch, int C, int BR, int h, int w, int d) {
 
 int col_fwd(int xdt, int odt, int batch, int C, int BR, int h, int w, int d, const void *x, const float *w1,
             const float *w2, const float *w3, const vq3d_preact_params &p, void *out, void *t2, void *t3,
-            hipStream_t s) {
+            hipStream_t s, int chain, const void *t2in, const float *w1n, const vq3d_preact_params *pn, void *t2n) {
     const CArgs a = make_args(batch, h, w, d);
     auto T2 = static_cast<h16_t *>(t2), T3 = static_cast<h16_t *>(t3);
-    if (C == 2) fwd_io<2, 1>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
-    else if (C == 4) fwd_io<4, 2>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
-    else fwd_io<8, 4>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, s);
+    FwdChain c;
+    c.ch = chain;
+    c.t2in = static_cast<const h16_t *>(t2in);
+    c.w1n = w1n;
+    if (pn) c.pn = *pn;
+    c.t2n = static_cast<h16_t *>(t2n);
+    if (C == 2) fwd_io<2, 1>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, c, s);
+    else if (C == 4) fwd_io<4, 2>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, c, s);
+    else fwd_io<8, 4>(xdt, odt, a, x, w1, w2, w3, p, out, T2, T3, c, s);
     return check_launch("preact_small_fwd (column kernels)");
 }
 

@@ -591,8 +591,8 @@ int vq3d_preact_small_fwd(int32_t dtype, int32_t batch, int32_t channels, int32_
                           int32_t dd, const void *x, const float *w1, const float *w2, const float *w3,
                           const vq3d_preact_params *p, void *out, void *t2, void *t3, vq3d_stream_t stream) {
     if (dtype != VQ3D_HALF) return fail("preact_small_fwd: the fused few-channel kernels take bf16 operands");
-    return vq3d_preact_small_fwd_io(dtype, dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, p, out, t2, t3,
-                                    stream);
+    return vq3d_preact_small_fwd_io(dtype, dtype, dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, p, out, t2,
+                                    t3, stream);
 }
 
 namespace {
@@ -601,13 +601,14 @@ static bool io_ok(int32_t xdt, int32_t odt) {
 }
 }  // namespace
 
-int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels, int32_t branch,
+int vq3d_preact_small_fwd_io(int32_t dtype, int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels, int32_t branch,
                              int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
                              const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,
                              vq3d_stream_t stream) {
     SArgs a;
     if (!x || !w1 || !w2 || !w3 || !p || !out) return fail("preact_small_fwd: null pointer");
-    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_fwd: stream storage must be VQ3D_HALF or VQ3D_F32");
+    if (dtype != VQ3D_HALF) return fail("preact_small_fwd: dtype must be the 16-bit format");
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_fwd: stream storage must be dtype or VQ3D_F32");
     if (col_supported(batch, channels, branch, h, w, dd))
         return col_fwd(x_dtype, out_dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, *p, out, t2, t3,
                        as_stream(stream));
@@ -638,6 +639,23 @@ int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, 
     return check_launch("preact_small_fwd");
 }
 
+int vq3d_preact_small_fwd_chain(int32_t mode, int32_t dtype, int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels,
+                                int32_t branch, int32_t h, int32_t w, int32_t dd, const void *x, const void *t2_in,
+                                const float *w1, const float *w2, const float *w3, const vq3d_preact_params *p,
+                                void *out, void *t2, void *t3, const float *w1_next,
+                                const vq3d_preact_params *params_next, void *t2_next, vq3d_stream_t stream) {
+    if (mode < 0 || mode > 3) return fail("preact_small_fwd_chain: mode must be a mask of 1 | 2");
+    if (!col_supported(batch, channels, branch, h, w, dd))
+        return fail("preact_small_fwd_chain: chained runs need the column kernels (vq3d_preact_small_plan == 2)");
+    if (dtype != VQ3D_HALF) return fail("preact_small_fwd_chain: dtype must be the 16-bit format");
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_fwd_chain: stream storage must be dtype or VQ3D_F32");
+    if (!x || !w1 || !w2 || !w3 || !p || !out) return fail("preact_small_fwd_chain: null pointer");
+    if ((mode & 1) && !t2_in) return fail("preact_small_fwd_chain: mode 1 needs t2_in");
+    if ((mode & 2) && (!w1_next || !params_next || !t2_next)) return fail("preact_small_fwd_chain: mode 2 needs the next block");
+    return col_fwd(x_dtype, out_dtype, batch, channels, branch, h, w, dd, x, w1, w2, w3, *p, out, (mode & 1) ? nullptr : t2,
+                   t3, as_stream(stream), mode, t2_in, w1_next, params_next, t2_next);
+}
+
 int vq3d_preact_small_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w,
                           int32_t dd, const void *g, const void *x, const void *t2, const void *t3, const float *w1,
                           const float *w2, const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
@@ -652,11 +670,11 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
                                  const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                  size_t ws_bytes, void *gx, vq3d_stream_t stream) {
     if (dtype != VQ3D_HALF) return fail("preact_small_bwd: the fused few-channel kernels take bf16 operands");
-    return vq3d_preact_small_bwd_stages_io(stages, dtype, dtype, batch, channels, branch, h, w, dd, g, x, t2, t3, w1,
-                                           w2, w3, p, gr, workspace, ws_bytes, gx, stream);
+    return vq3d_preact_small_bwd_stages_io(stages, dtype, dtype, dtype, batch, channels, branch, h, w, dd, g, x, t2,
+                                           t3, w1, w2, w3, p, gr, workspace, ws_bytes, gx, stream);
 }
 
-int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out_dtype, int32_t batch,
+int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t dtype, int32_t x_dtype, int32_t out_dtype, int32_t batch,
                                     int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd, const void *g,
                                     const void *x, const void *t2, const void *t3, const float *w1, const float *w2,
                                     const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
@@ -665,7 +683,8 @@ int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out
     if (stages < 1 || stages > 3) return fail("preact_small_bwd: stages must be a mask of 1 | 2");
     if (!g || !x || !t2 || !t3 || !w1 || !w2 || !w3 || !p || !gr || !gx)
         return fail("preact_small_bwd: null pointer");
-    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_bwd: stream storage must be VQ3D_HALF or VQ3D_F32");
+    if (dtype != VQ3D_HALF) return fail("preact_small_bwd: dtype must be the 16-bit format");
+    if (!io_ok(x_dtype, out_dtype)) return fail("preact_small_bwd: stream storage must be dtype or VQ3D_F32");
     if (col_supported(batch, channels, branch, h, w, dd)) {
         const vq3d_preact_grads &G = *gr;
         if (!G.dw1 || !G.dw2 || !G.dw3 || !G.dbias1a || !G.dbias1b || !G.dbias2a || !G.dbias2b || !G.dbias3a ||

@@ -94,8 +94,9 @@ _SIGS = {
     "vq3d_preact_small_bwd": (c_int, [c_int] * 7 + [P] * 10 + [c_size, P, P]),
     "vq3d_preact_small_bwd_stages": (c_int, [c_int] * 8 + [P] * 10 + [c_size, P, P]),
     "vq3d_preact_small_reduce_run": (c_int, [c_int] * 7 + [P, c_size, P, P, P]),
-    "vq3d_preact_small_fwd_io": (c_int, [c_int] * 8 + [P] * 9),
-    "vq3d_preact_small_bwd_stages_io": (c_int, [c_int] * 9 + [P] * 10 + [c_size, P, P]),
+    "vq3d_preact_small_fwd_io": (c_int, [c_int] * 9 + [P] * 9),
+    "vq3d_preact_small_bwd_stages_io": (c_int, [c_int] * 10 + [P] * 10 + [c_size, P, P]),
+    "vq3d_preact_small_fwd_chain": (c_int, [c_int] * 10 + [P] * 13),
     "vq3d_vq_workspace_size": (c_size, [c_i64, c_int, c_int]),
     "vq3d_vq_nearest": (c_int, [c_int, P, c_i64, c_int, P, c_int, P, c_int, P, P, P, P]),
     "vq3d_vq_commit_loss": (c_int, [P, c_float, P, P]),

@@ -420,12 +420,17 @@ class PreActSmallRunFn(torch.autograd.Function):
         saved = []
         n = len(plan.blocks)
         last_dt = plan.out_dtype or x.dtype
-        for i, blk in enumerate(plan.blocks):
-            odt = last_dt if i == n - 1 else (torch.float32 if ops.fp32_stream() else x.dtype)
-            out, t2, t3 = ops.preact_small_fwd(x, blk, save=save, out_dtype=odt)
-            if save:
-                saved += [x, t2, t3]
-            x = out
+        odts = [last_dt if i == n - 1 else (torch.float32 if ops.fp32_stream() else x.dtype) for i in range(n)]
+        if ops.small_chain_ok(x, n):  # column kernels: each launch hands the next block its t2
+            x, runs = ops.preact_small_run_fwd(x, plan.blocks, save, odts)
+            saved = [t for r in runs for t in r]
+        else:
+            fmt = ops._fmt16(x)
+            for i, blk in enumerate(plan.blocks):
+                out, t2, t3 = ops.preact_small_fwd(x, blk, save=save, out_dtype=odts[i], fmt=fmt)
+                if save:
+                    saved += [x, t2, t3]
+                x = out
         ctx.plan = plan
         if save:
             ctx.save_for_backward(*saved)

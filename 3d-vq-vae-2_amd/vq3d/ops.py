@@ -597,22 +597,75 @@ def fp32_stream():
     return _fp32_stream[0]
 
 
-def preact_small_fwd(x, blk, save=True, out_dtype=None):
+def _fmt16(x):
+    """The 16-bit format of a few-channel run (t2 / t3 and every conv operand): its input's, or
+    bf16 when the input is already fp32."""
+    return x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
+
+
+def preact_small_fwd(x, blk, save=True, out_dtype=None, fmt=None):
     """Fused few-channel PreAct block forward (vq3d.h): returns out, t2, t3 (channels-last; t2 / t3
-    bf16, out in out_dtype, default x's: the residual stream is bf16 or fp32 per tensor);
-    save=False (no backward follows): t2 / t3 are not written (None)."""
+    in the 16-bit format fmt (default: x's), out in out_dtype, default x's: the residual stream is
+    16-bit or fp32 per tensor); save=False (no backward follows): t2 / t3 are not written (None)."""
     x = as_cl(x)
     b, c, h, w, d = x.shape
+    fmt = fmt or _fmt16(x)
     w1, w2, w3 = blk.branch_conv1.weight, blk.branch_conv2.weight, blk.branch_conv3.weight
     nb = w1.shape[0]
     out = torch.empty_like(x, memory_format=CL, dtype=out_dtype or x.dtype)
-    t2 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
-    t3 = new_act(b, nb, h, w, d, x.dtype, x.device) if save else None
+    t2 = new_act(b, nb, h, w, d, fmt, x.device) if save else None
+    t3 = new_act(b, nb, h, w, d, fmt, x.device) if save else None
     prm = _preact_params(blk)
     _timed(lambda: _small_kind("fwd", b, c, nb, h, w, d), lambda: L.call(
-        "vq3d_preact_small_fwd_io", L.dtype_code(x), L.dtype_code(out), b, c, nb, h, w, d, L.ptr(x), L.ptr(w1),
-        L.ptr(w2), L.ptr(w3), ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream()))
+        "vq3d_preact_small_fwd_io", L.dtype_code(fmt), L.dtype_code(x), L.dtype_code(out), b, c, nb, h, w, d,
+        L.ptr(x), L.ptr(w1), L.ptr(w2), L.ptr(w3), ctypes.byref(prm), L.ptr(out), _p(t2), _p(t3), L.stream()))
     return out, t2, t3
+
+
+_chain = [True]
+
+
+def set_small_chain(enabled=True):
+    """Chain the column-kernel runs' forward (vq3d_preact_small_fwd_chain): each block's t2 formed
+    once per voxel in the previous block's epilogue instead of on every brick's halo."""
+    _chain[0] = bool(enabled)
+
+
+def small_chain_ok(x, nblocks):
+    b, c, h, w, d = x.shape
+    return (_chain[0] and nblocks > 1 and
+            int(L.query("vq3d_preact_small_plan", b, c, c // 2, h, w, d)) == 2)
+
+
+def preact_small_run_fwd(x, blocks, save, out_dtypes):
+    """Forward of a chained run of column-kernel blocks: per block one launch that reads its t2 from
+    the previous launch and writes the next block's.  out_dtypes[i]: block i's output storage.
+    Returns (out, [(x_i, t2_i, t3_i)] if save else [])."""
+    x = as_cl(x)
+    b, c, h, w, d = x.shape
+    fmt = _fmt16(x)
+    nb = blocks[0].branch_conv1.weight.shape[0]
+    n = len(blocks)
+    saved = []
+    t2 = new_act(b, nb, h, w, d, fmt, x.device)
+    prms = [_preact_params(blk) for blk in blocks]
+    for i, blk in enumerate(blocks):
+        out = torch.empty_like(x, memory_format=CL, dtype=out_dtypes[i])
+        t3 = new_act(b, nb, h, w, d, fmt, x.device) if save else None
+        t2n = new_act(b, nb, h, w, d, fmt, x.device) if i + 1 < n else None
+        mode = (1 if i else 0) | (2 if i + 1 < n else 0)
+        nxt = blocks[i + 1] if i + 1 < n else None
+        args = (mode, L.dtype_code(fmt), L.dtype_code(x), L.dtype_code(out), b, c, nb, h, w, d, L.ptr(x),
+                L.ptr(t2) if i else None, L.ptr(blk.branch_conv1.weight), L.ptr(blk.branch_conv2.weight),
+                L.ptr(blk.branch_conv3.weight), ctypes.byref(prms[i]), L.ptr(out), L.ptr(t2), _p(t3),
+                _p(nxt.branch_conv1.weight) if nxt is not None else None,
+                ctypes.byref(prms[i + 1]) if nxt is not None else None, _p(t2n), L.stream())
+        _timed(lambda: _small_kind("fwd", b, c, nb, h, w, d),
+               lambda a=args: L.call("vq3d_preact_small_fwd_chain", *a))
+        if save:
+            saved.append((x, t2, t3))
+        x, t2 = out, t2n
+    return x, saved
 
 
 def preact_small_bwd(g, x, t2, t3, blk, grads):
@@ -632,15 +685,18 @@ def preact_small_bwd(g, x, t2, t3, blk, grads):
 
 
 def preact_small_run_bwd(g, plan, saved, on_done=None):
-    """Backward of a run of fused few-channel blocks (the forward is per block, preact_small_fwd):
-    per block, in reverse, the fused data / partial-sum kernel (vq3d_preact_small_bwd_stages_io 1)
-    into its slice of one run workspace, then the fixed-order reductions of every block as one
-    launch pair (vq3d_preact_small_reduce_run, plan's device tables).  Each block's g has its out's
-    storage and its gx its input's (the fp32 stream inside the run).  Returns gx of the run's input."""
+    """Backward of a run of fused few-channel blocks: per block, in reverse, the fused data /
+    partial-sum kernel into its slice of one run workspace, then the fixed-order reductions of every
+    block as one launch pair (vq3d_preact_small_reduce_run, plan's device tables).  Each block's g
+    has its out's storage and its gx its input's (the fp32 stream inside the run).  (A backward
+    chained like the forward -- each launch forming the previous block's gz3 in its epilogue --
+    was measured slower: the epilogue's extra registers cost more than the halo math it saves.)
+    Returns gx of the run's input."""
     blocks = plan.blocks
     g = g if g.is_contiguous(memory_format=CL) else g.contiguous(memory_format=CL)
     b, c, h, w, d = g.shape
     nb = blocks[0].branch_conv1.weight.shape[0]
+    fmt = saved[0][1].dtype
     nws = int(L.query("vq3d_preact_small_workspace_bytes", b, c, nb, h, w, d))
     stride = (nws + 255) // 256 * 256
     run_ws = workspace(stride * len(blocks), g.device)
@@ -652,10 +708,10 @@ def preact_small_run_bwd(g, plan, saved, on_done=None):
         gx = torch.empty_like(x, memory_format=CL)
         prm = _preact_params(blk)
         gr = L.PreactGrads(*[ctypes.c_void_p(int(gp)) for gp in plan.grad_ptrs(i)])
-        sargs = (L.dtype_code(x), L.dtype_code(g), b, c, nb, h, w, d, L.ptr(g), L.ptr(x), L.ptr(t2), L.ptr(t3),
-                 L.ptr(blk.branch_conv1.weight), L.ptr(blk.branch_conv2.weight), L.ptr(blk.branch_conv3.weight),
-                 ctypes.byref(prm), ctypes.byref(gr), ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws),
-                 L.ptr(gx), L.stream())
+        sargs = (L.dtype_code(fmt), L.dtype_code(x), L.dtype_code(g), b, c, nb, h, w, d, L.ptr(g), L.ptr(x),
+                 L.ptr(t2), L.ptr(t3), L.ptr(blk.branch_conv1.weight), L.ptr(blk.branch_conv2.weight),
+                 L.ptr(blk.branch_conv3.weight), ctypes.byref(prm), ctypes.byref(gr),
+                 ctypes.c_void_p(base + i * stride), ctypes.c_size_t(nws), L.ptr(gx), L.stream())
         _timed(lambda: _small_kind("bwd", b, c, nb, h, w, d),
                lambda a=sargs: L.call("vq3d_preact_small_bwd_stages_io", 1, *a))
         g = gx

@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--no-overlap-levels", action="store_true",
                    help="run the decoder's top-level chain on the main stream (default: on the level stream, "
                         "beside the encoder's lower levels)")
+    p.add_argument("--no-small-chain", action="store_true",
+                   help="unchained column-kernel runs (each block forms its t2 / gz3 on its bricks' halos)")
     p.add_argument("--eager", action="store_true",
                    help="launch every kernel from Python each step instead of replaying a captured HIP graph")
     p.add_argument("--no-dist-graph", action="store_true", help="N > 1: never capture the collectives")
@@ -770,6 +772,7 @@ def main():
     torch.manual_seed(0)
     ops.set_concurrent_wgrad(a.concurrent_wgrad)
     ops.set_overlap_levels(not a.no_overlap_levels)
+    ops.set_small_chain(not a.no_small_chain)
     args = vq3d.default_args(compute_dtype=a.dtype, base_lr=1e-4 * world, **mkw)
     model = vq3d.VQVAE(args).to(dev)
     if a.binding != "ctypes":

@@ -320,19 +320,31 @@ int vq3d_preact_small_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, i
                                  const vq3d_preact_params *p, const vq3d_preact_grads *gr, void *workspace,
                                  size_t ws_bytes, void *gx, vq3d_stream_t stream);
 /* The same blocks with the residual stream stored per tensor: x (and gx) as x_dtype, out (and g) as
- * out_dtype, each VQ3D_BF16 or VQ3D_F32; t2 / t3 and every conv operand stay bf16.  A run of blocks
- * carries its stream in fp32 between blocks (bf16 -> fp32, fp32 -> fp32, ..., fp32 -> bf16), as the
- * reference's autocast blocks return fp32 (`out * self.scale` with fp32 parameters, layers.py:187-193);
- * the plain entries above are (bf16, bf16). */
-int vq3d_preact_small_fwd_io(int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels, int32_t branch,
+ * out_dtype, each dtype (the 16-bit format, VQ3D_BF16 | VQ3D_F16, of t2 / t3 and of every conv
+ * operand) or VQ3D_F32.  A run of blocks carries its stream in fp32 between blocks (16-bit -> fp32,
+ * fp32 -> fp32, ..., fp32 -> 16-bit), as the reference's autocast blocks return fp32
+ * (`out * self.scale` with fp32 parameters, layers.py:187-193); the plain entries above are
+ * (dtype, dtype). */
+int vq3d_preact_small_fwd_io(int32_t dtype, int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels, int32_t branch,
                              int32_t h, int32_t w, int32_t dd, const void *x, const float *w1, const float *w2,
                              const float *w3, const vq3d_preact_params *p, void *out, void *t2, void *t3,
                              vq3d_stream_t stream);
-int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t x_dtype, int32_t out_dtype, int32_t batch,
+int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t dtype, int32_t x_dtype, int32_t out_dtype, int32_t batch,
                                     int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd, const void *g,
                                     const void *x, const void *t2, const void *t3, const float *w1, const float *w2,
                                     const float *w3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                                     void *workspace, size_t ws_bytes, void *gx, vq3d_stream_t stream);
+/* Chained RUNS of the column-kernel blocks (vq3d_preact_small_plan == 2): links between consecutive
+ * blocks that skip the halo recompute (each block's t2 is formed once per voxel, in the previous
+ * block's epilogue, instead of on every brick's halo).  Forward, mode bit 0: this
+ * block's t2 was written by the previous block's launch (t2_in; the t2 argument is then not
+ * written); bit 1: the launch also writes the NEXT block's t2 (t2_next) from this block's out as
+ * stored, with that block's W1 (w1_next) and params_next.  Bit-identical to unchained launches. */
+int vq3d_preact_small_fwd_chain(int32_t mode, int32_t dtype, int32_t x_dtype, int32_t out_dtype, int32_t batch, int32_t channels,
+                                int32_t branch, int32_t h, int32_t w, int32_t dd, const void *x, const void *t2_in,
+                                const float *w1, const float *w2, const float *w3, const vq3d_preact_params *p,
+                                void *out, void *t2, void *t3, const float *w1_next,
+                                const vq3d_preact_params *params_next, void *t2_next, vq3d_stream_t stream);
 /* Stage 2 of a whole RUN of these blocks in one launch pair: block i's workspace at
  * workspaces + i * workspace_stride (stride >= vq3d_preact_small_workspace_bytes, a multiple of
  * 256), grads / params as for vq3d_preact_mid_reduce_run ([nblocks][11] device pointer tables). */

@@ -186,9 +186,19 @@ def _check_run_vs_per_block(gpu, shape, nblk):
     """A run of few-channel blocks through layers.BlockStack (Fn.PreActSmallRunFn: per-block fused
     kernels into slices of one run workspace, one reduction launch pair for the whole run; the
     (8, 4) 32x32x8 case takes the brick kernels' reduction) against the blocks run one by one:
-    out, gx and every parameter gradient bit-identical (same kernels, same fixed-order sums)."""
+    out, gx and every parameter gradient bit-identical (same kernels, same fixed-order sums).  The run
+    is unchained here (test_small_run_chained_matches_unchained covers the links)."""
     from vq3d import functional as Fn
     from vq3d import layers as VL
+    from vq3d import ops
+    ops.set_small_chain(False)
+    try:
+        _run_vs_per_block(gpu, shape, nblk, Fn, VL)
+    finally:
+        ops.set_small_chain(True)
+
+
+def _run_vs_per_block(gpu, shape, nblk, Fn, VL):
     c = shape[1]
     blocks = [_block(c, seed=40 + i) for i in range(nblk)]
     g = torch.Generator().manual_seed(41)
@@ -285,3 +295,60 @@ def test_small_run_fp32_stream_matches_float64(gpu, shape, nblk, out32):
     print(shape, nblk, out32, {k: f"{v:.1e}" for k, v in errs.items()})
     bad = {k: v for k, v in errs.items() if not v <= (2e-2 if k.endswith("scalars") else 1e-2)}
     assert not bad, (shape, bad)
+
+
+@pytest.mark.parametrize("fmt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape,nblk", [((1, 4, 32, 16, 32), 3), ((2, 2, 16, 16, 32), 4), ((1, 8, 16, 16, 32), 2),
+                                        ((1, 4, 8, 8, 16), 2)])
+def test_small_run_chained_matches_unchained(gpu, shape, nblk, fmt):
+    """Chained column-kernel runs (vq3d_preact_small_fwd_chain: each block's t2 formed in the previous
+    block's epilogue) against the unchained run: out, gx and every parameter gradient bit-identical
+    (same formulas, same order per voxel).  fp32 residual stream, both 16-bit formats."""
+    from vq3d import layers as VL
+    from vq3d import ops
+    c = shape[1]
+    blocks = [_block(c, seed=70 + i) for i in range(nblk)]
+    g = torch.Generator().manual_seed(71)
+    x = torch.randn(shape, generator=g).to(fmt)
+    gy = torch.randn(shape, generator=g).to(fmt)
+    res = []
+    for chained in (False, True):
+        ops.set_small_chain(chained)
+        try:
+            stack = VL.BlockStack(*blocks).to(gpu)
+            for p in stack.parameters():
+                p.grad = None
+            xd = x.to(gpu).contiguous(memory_format=CL).requires_grad_(True)
+            assert ops.small_chain_ok(xd, nblk) == chained
+            out = stack(xd)
+            out.backward(gy.to(gpu).contiguous(memory_format=CL))
+            torch.cuda.synchronize()
+            res.append((out.float().cpu(), xd.grad.float().cpu(),
+                        {n: p.grad.cpu().clone() for n, p in stack.named_parameters()}))
+        finally:
+            ops.set_small_chain(True)
+    a, b = res
+    assert torch.equal(a[0], b[0]), float((a[0] - b[0]).abs().max())
+    assert torch.equal(a[1], b[1]), float((a[1] - b[1]).abs().max())
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), (n, float((a[2][n] - b[2][n]).abs().max()))
+
+
+def test_small_run_chain_saved_tensors(gpu):
+    """The chained forward's saved t2 / t3 equal the unchained forward's, block by block."""
+    from vq3d import ops
+    c, shape, nblk = 4, (1, 4, 16, 16, 32), 3
+    blocks = [_block(c, seed=80 + i).to(gpu) for i in range(nblk)]
+    x = torch.randn(shape, generator=torch.Generator().manual_seed(81)).bfloat16().to(gpu).contiguous(
+        memory_format=CL)
+    odts = [torch.float32] * (nblk - 1) + [torch.bfloat16]
+    out_c, saved_c = ops.preact_small_run_fwd(x, blocks, True, odts)
+    xs, outs = x, []
+    for i, blk in enumerate(blocks):
+        o, t2, t3 = ops.preact_small_fwd(xs, blk, out_dtype=odts[i], fmt=torch.bfloat16)
+        outs.append((t2, t3))
+        xs = o
+    torch.cuda.synchronize()
+    assert torch.equal(out_c, xs)
+    for (_, t2c, t3c), (t2, t3) in zip(saved_c, outs):
+        assert torch.equal(t2c, t2) and torch.equal(t3c, t3)
