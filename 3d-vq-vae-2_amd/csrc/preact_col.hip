@@ -40,12 +40,6 @@
 #include <cstdlib>
 #include <type_traits>
 
-// Timing experiments only (make exp EXP=N EXPSRC=preact_col EXPDEF=COL_EXP): bit 0 skips the halo
-// loads, 1 the halo math, 2 the k^3 MFMA phase, 3 the W2-gradient MFMAs, 4 the per-voxel epilogue.
-// The product library is built with COL_EXP = 0.
-#ifndef COL_EXP
-#define COL_EXP 0
-#endif
 #ifndef FWD_PERSIST
 #define FWD_PERSIST 1  // the forward walks brick ranges too (its grid: CArgs::nwg)
 #endif
@@ -333,12 +327,12 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
             for (int u = 0; u < P; ++u) {
                 int line, pos;
                 const int vx = halo_voxel(a, o, lbase, min(tid + u * NT, HVX - 1), line, pos);
-                xv[u] = (COL_EXP & 1) ? Raw<TX, C>{} : ldraw<TX, C>(x + int64_t(vx) * C);
+                xv[u] = ldraw<TX, C>(x + int64_t(vx) * C);
             }
 #pragma unroll
             for (int u = 0; u < P; ++u) {
                 const int q = tid + u * NT;
-                if (!(COL_EXP & 2) && q < HVX) {
+                if (q < HVX) {
                     float xf[C], t[BR];
                     unraw<TX, C>(xv[u], xf);
                     t2_of<C, BR>(xf, w1, s, t);
@@ -353,7 +347,7 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
         const Raw<TX, DV * C> xr = ldraw<TX, DV * C>(x + vox0 * C);
         // B. raw W2 (*) t2 per m-tile
 #pragma unroll 4
-        for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
+        for (int mt = wave; mt < NMT; mt += NT / 64) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             const int wb = win_base(mt, BR);
 #pragma unroll
@@ -365,7 +359,6 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
         }
         __syncthreads();
         // C. t3 and out of the thread's 4 voxels (and their t2, saved for the backward)
-        if constexpr ((COL_EXP & 16) != 0) continue;
         const int v0 = ln * BD + dg * DV;
         if (t2o && (CH & 1) == 0) {  // chained: this block's t2 is already in memory
             const h16_t *src = t2h + ((((ln >> 3) + 1) * WL + (ln & 7) + 1) * PL + dg * DV + 1) * BR;
@@ -492,19 +485,14 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
             for (int u = 0; u < P; ++u) {
                 int line, pos;
                 const int vx = halo_voxel(a, o, lbase, min(tid + (half * PH + u) * NT, HVX - 1), line, pos);
-                if constexpr (!(COL_EXP & 1)) {
-                    gv[u] = ldraw<TO, C>(g + int64_t(vx) * C);
-                    tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
-                    tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
-                } else {
-                    gv[u] = Raw<TO, C>{};
-                    tv3[u] = tv2[u] = typename Vec<BR>::U{};
-                }
+                gv[u] = ldraw<TO, C>(g + int64_t(vx) * C);
+                tv3[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
+                tv2[u] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
             }
 #pragma unroll
             for (int u = 0; u < P; ++u) {
                 const int q = tid + (half * PH + u) * NT;
-                if (!(COL_EXP & 2) && q < HVX) {
+                if (q < HVX) {
                     const int line = q / PL, pos = q - line * PL;
                     const bool in = interior(line, pos);
                     float gf[C], t3f[BR], t2f[BR], z[BR];
@@ -547,7 +535,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
         // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
 #pragma unroll 2
-        for (int mt = (COL_EXP & 4) ? NMT : wave; mt < NMT; mt += NT / 64) {
+        for (int mt = wave; mt < NMT; mt += NT / 64) {
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             const int wb = win_base(mt, BR);
 #pragma unroll
@@ -561,7 +549,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         // wave w takes the 32-voxel k-steps 8 w .. 8 w + 7 (two brick lines each; lane kb: line
         // 2 ks + kb / 2, d = 8 (kb & 1) + j)
 #pragma unroll 2
-        for (int ks = 8 * wave; ks < ((COL_EXP & 8) ? 0 : 8 * wave + 8); ++ks) {
+        for (int ks = 8 * wave; ks < 8 * wave + 8; ++ks) {
             // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
             const hx8 af = *reinterpret_cast<const hx8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
             const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
@@ -570,7 +558,6 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         }
         __syncthreads();
         // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 4 voxels
-        if constexpr ((COL_EXP & 16) != 0) continue;
         const int v0 = ln * BD + dg * DV;
         // 8-element pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
         // flight during the current one's math (one piece of registers at a time: occupancy)

@@ -37,14 +37,6 @@
 
 #include <algorithm>
 
-// Timing experiments only (tools builds: make -C 3d-vq-vae-2_amd exp EXP=N): bit 0 skips the
-// forward tile kernel's k^3 phase, 1 its 1x1 phase, 2 its stores, 3 its staging; bits 4 .. 8 the
-// backward data tile kernel's staging (loads + LDS writes), k^3 dgrad phase, gx phase, chained
-// previous-block phase and global stores, 9 / 10 its next-tile epilogue-operand / halo loads, 11 the
-// forward tile kernel's next-tile loads.  The product library is built with PM_EXP = 0.
-#ifndef PM_EXP
-#define PM_EXP 0
-#endif
 // resident workgroups per CU of the forward / backward-data tile kernels: 0 = as many as fit
 // (timing experiments set a cap: make exp EXP=N EXPDEF=PM_FWD_PER)
 #ifndef PM_FWD_PER
@@ -812,15 +804,15 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
         const Org on = tile_org_q(a, tn < sc.end ? tn : tile);
         const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
         h16_t *hl = img + (it & 1) * QIMG;
-        if constexpr (!(PM_EXP & 16)) hz.store(tl, hl);
-        if constexpr (!(PM_EXP & 1024)) hz.load(tl, a, on, gz3);
+        hz.store(tl, hl);
+        hz.load(tl, a, on, gz3);
         __syncthreads();
         // gt2 of the wave's 2 runs: input line (i, j) of the 4 x 3 they need feeds run r through tap
         // row (i - r, j)
         f32x4 acc[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (!(PM_EXP & 32)) {
+        {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -852,7 +844,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             }
             // gt1 = W1^T gz1 (two channel tiles), gx = g + gt1 * elu'(x + b1a)
             float gxv[6];
-            if constexpr (!(PM_EXP & 64)) {
+            {
                 const hx8 bz = pack8({z1[0], z1[1], z1[2], z1[3], 0.f, 0.f, 0.f, 0.f});
                 const f32x4 a0 = mfma(wf(9, ln), bz, f32x4{0.f, 0.f, 0.f, 0.f});
                 const f32x4 a1 = mfma(wf(10, ln), bz, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -872,18 +864,15 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                     gxv[j] = ok ? bf(f2h(gv[j] + gt1[j] * ez)) : 0.f;
                     if constexpr (CHAIN) q4 += gxv[j];  // the previous block's g = this gx
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) gxv[j] = z1[j & 3];
             }
-            if constexpr (!(PM_EXP & 256)) {
+            {
                 put18(st, nl, kl, gxv);
                 put9(st + QO9A, nl, kl, z1);
             }
             if constexpr (CHAIN) {
                 // previous block: gz3 = bf16(scale W3^T gx * elu'(t3)) (one MFMA, K = the 18 channels
                 // of gx in the k_chan18 order)
-                if constexpr (!(PM_EXP & 128)) {
+                {
                     const hx8 bg = pack8({gxv[0], gxv[1], gxv[2], gxv[3], gxv[4], gxv[5], 0.f, 0.f});
                     const f32x4 a3 = mfma(wf(11, ln), bg, f32x4{0.f, 0.f, 0.f, 0.f});
                     float t3v[4], zq[4];
@@ -898,14 +887,13 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                         qsc += ok ? a3[j] * t3v[j] : 0.f;
                         zq[j] = z;
                     }
-                    if constexpr (!(PM_EXP & 256)) put9(st + QO9B, nl, kl, zq);
+                    put9(st + QO9B, nl, kl, zq);
                 }
             }
-            if constexpr (!(PM_EXP & 256))
-                flush_run(st, ln, gx + size_t(v0) * C, gz1o + size_t(v0) * BR, CHAIN ? gz3p + size_t(v0) * BR : nullptr);
+            flush_run(st, ln, gx + size_t(v0) * C, gz1o + size_t(v0) * BR, CHAIN ? gz3p + size_t(v0) * BR : nullptr);
             // the operands of the tile DEPTH steps ahead for this run (unconditional: on = this tile
             // at the end; a branch would keep the old values live)
-            if constexpr (!(PM_EXP & 512)) load_ep(et2, et3, ex, eg, ln, on, r);
+            load_ep(et2, et3, ex, eg, ln, on, r);
             if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);  // one run's epilogue at a time (no interleaving)
         }
         return on;
@@ -1034,13 +1022,13 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
         const Org on = tile_org_q(a, more ? tile + sc.step : tile);
         const int tl = launder(tid), ln = tl & 63, nl = ln & 15, kl = ln >> 4;
         h16_t *hl = img + (it & 1) * QIMG;
-        if constexpr (!(PM_EXP & 8)) ht.store(tl, hl);
-        if constexpr (!(PM_EXP & 2048)) ht.load(tl, a, on, t2);
+        ht.store(tl, hl);
+        ht.load(tl, a, on, t2);
         __syncthreads();
         f32x4 acc[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (!(PM_EXP & 1)) {
+        {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -1064,7 +1052,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             for (int j = 0; j < 4; ++j)
                 t3v[j] = 4 * kl + j < BR ? bf(f2h(elu_fast(acc[r][j] + s.b3a) + s.b3b)) : 0.f;
             float ov[6];
-            if constexpr (!(PM_EXP & 2)) {
+            {
                 const hx8 bt = pack8({t3v[0], t3v[1], t3v[2], t3v[3], 0.f, 0.f, 0.f, 0.f});
                 const f32x4 a0 = mfma(wf(9, ln), bt, f32x4{0.f, 0.f, 0.f, 0.f});
                 const f32x4 a1 = mfma(wf(10, ln), bt, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -1077,11 +1065,8 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                     const bool ok = j < 4 || kl == 3;  // channels 4kb + j, then (kb 3) 16 / 17
                     ov[j] = ok ? bf(f2h(o3[j] * s.sc + s.b4 + xv[j])) : 0.f;
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) ov[j] = t3v[j & 3];
             }
-            if constexpr (!(PM_EXP & 4)) {
+            {
                 put18(st, nl, kl, ov);
                 if (t3o) put9(st + QO9A, nl, kl, t3v);
             }
@@ -1098,12 +1083,11 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                 float tn[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) tn[j] = elu_fast(a2[j] + sn.b2a) + sn.b2b;
-                if constexpr (!(PM_EXP & 4)) put9(st + QO9B, nl, kl, tn);
+                put9(st + QO9B, nl, kl, tn);
             }
-            if constexpr (!(PM_EXP & 4))
-                flush_run(st, ln, out + size_t(v0) * C, t3o ? t3o + size_t(v0) * BR : nullptr,
+            flush_run(st, ln, out + size_t(v0) * C, t3o ? t3o + size_t(v0) * BR : nullptr,
                           CHAIN ? t2n + size_t(v0) * BR : nullptr);
-            if constexpr (!(PM_EXP & 2048)) ex[r] = ld18(x, run_vox0(on, r) + nl, kl);  // next tile's x (unconditional)
+            ex[r] = ld18(x, run_vox0(on, r) + nl, kl);  // next tile's x (unconditional)
             if constexpr (PM_SB) __builtin_amdgcn_sched_barrier(0);
         }
         o = on;

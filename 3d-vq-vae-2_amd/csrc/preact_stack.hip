@@ -418,11 +418,6 @@ __global__ __launch_bounds__(NT) void k_stack_bwd(SkArgs a, const T *__restrict_
 // Rounding points are the unfused bf16 path's (u1, t2, t3, gz3, gz1 rounded to bf16 as matrix
 // operands, fp32 accumulation); the residual stream and the gradient stream stay fp32.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-// STK_EXP: phase-skip bits for timing experiments (make exp EXPSRC=preact_stack EXPDEF=STK_EXP):
-// 1 W2 gradient, 2 W1 gradient, 4 W3 gradient, 8 weight staging.  The product library is built with STK_EXP = 0.
-#ifndef STK_EXP
-#define STK_EXP 0
-#endif
 constexpr int MC = 32, MB = 16;            // channels, branch
 constexpr int PF = 36, PU = 40, PT = 24;   // row pitches: fp32 streams, u1 (bf16), branch tensors (bf16)
 constexpr int MAXVM = 128;
@@ -664,7 +659,7 @@ __global__ __launch_bounds__(NT) void k_stackm_fwd(SkArgs a, const h16_t *__rest
         const Scal s = scal_lanes(vc);
         float *sx = saved + blk * stride, *st2 = sx + nvc, *st3 = st2 + nvb;
         __syncthreads();
-        if constexpr (!(STK_EXP & 8)) ir.store(m.fr);
+        ir.store(m.fr);
         // the next block's weights and scalars, and the row after it
         if (blk + 1 < a.nblk) {
             ir.load(img, blk + 1);
@@ -795,7 +790,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
         float *const gsc = gc;  // lanes 3 .. 10: this block's scalar-gradient pointers
         if (blk > 0) gc = row_ptr(gtab, blk - 1, lane);
         __syncthreads();
-        if constexpr (!(STK_EXP & 8)) {
+        {
             if constexpr (SPLIT) ir.store(m.fr);
             else wr.store<true>(m.w, m.fr);
         }
@@ -835,7 +830,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
                 m.z3[v * PT + row] = f2h(z);
                 if constexpr (SPLIT) rz3[v * MB + row] = f2h(z);
             }
-        } else if (!SPLIT && !(STK_EXP & 4) && wave < nmt + 2) {
+        } else if (!SPLIT && wave < nmt + 2) {
             // W3 gradient: M = co tile (wave - nmt), N = o, K = voxels; dscale = sum W3 . G3
             const int ct = wave - nmt;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -866,7 +861,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
 #pragma unroll
         for (int q = 0; q < 2; ++q) {  // M = co, N = ci, K = voxels: taps wave, wave + 16
             const int tap = wave + 16 * q;
-            if (SPLIT || (STK_EXP & 1) || tap >= 27) continue;
+            if (SPLIT || tap >= 27) continue;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
             for (int ks = 0; ks < nks; ++ks) {
@@ -922,7 +917,7 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
                 m.gs[i] += acc[j] * e;
             }
         }
-        if (!SPLIT && !(STK_EXP & 2) && wave < 2) {
+        if (!SPLIT && wave < 2) {
             // W1 gradient: M = o, N = channel tile (wave), K = voxels
             const int nt = wave;
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};

@@ -33,12 +33,6 @@
 
 #include <algorithm>
 
-// Timing experiments only (make exp EXP=N EXPSRC=preact_wide EXPDEF=WIDE_EXP): bit 0 skips the
-// staging loads, 1 the halo MFMA phase, 2 the 3x3x3 phase, 3 the epilogue phase and the global
-// stores, 4 the W2 fragment loads.  The product library is built with WIDE_EXP = 0.
-#ifndef WIDE_EXP
-#define WIDE_EXP 0
-#endif
 
 namespace vq3d {
 
@@ -309,7 +303,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
 #pragma unroll
     for (int k = 0; k < KS1; ++k) f1[k] = frag(img, OF1 + k * NTB + nt, lane);
 #pragma unroll
-    for (int k = 0; k < 9 * KSW; ++k) f2[k] = (WIDE_EXP & 16) ? hx8{} : frag(img, OF2 + k * NTB + nt, lane);
+    for (int k = 0; k < 9 * KSW; ++k) f2[k] = frag(img, OF2 + k * NTB + nt, lane);
     const Org o = tile_org(a, blockIdx.x);
     const Scal s = load_scal(p);
     make_tables(a, o, segv, runv);
@@ -318,11 +312,11 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         t2h[HV * BR + i] = 0;
     }
     __syncthreads();
-    if constexpr (!(WIDE_EXP & 1)) stage_halo_f32<true>(segv, x, u1h, s.b1a, s.b1b);
+    stage_halo_f32<true>(segv, x, u1h, s.b1a, s.b1b);
     __syncthreads();
     // t2 = elu(W1 u1 + b2a) + b2b on the halo
     const int ob = 16 * nt + row;
-    for (int m = (WIDE_EXP & 2) ? NHM : hf; m < NHM; m += 2) {
+    for (int m = hf; m < NHM; m += 2) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < KS1; ++k) acc = mfma(ld16(u1h + (16 * m + row) * C + 32 * k + 8 * kb), f1[k], acc);
@@ -332,7 +326,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         }
     }
     __syncthreads();
-    if (!(WIDE_EXP & 8) && t2o) tile_to_global<true>(runv, t2h, t2o);
+    if (t2o) tile_to_global<true>(runv, t2h, t2o);
     // x of this lane's output entries, in flight during the 3x3x3 phase: m-tiles 2 hf + mm,
     // channel tiles nt + 3 q; voxel 16 m + 4 kb + j = run 2 m + (kb >> 1), d = 4 (kb & 1) + j
     int vb[MPW];
@@ -354,7 +348,7 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
         acc3[mm] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int v = 16 * (MPW * hf + mm) + row, d = v & 7;
 #pragma unroll
-        for (int kk = 0; kk < ((WIDE_EXP & 4) ? 0 : 9); ++kk) {
+        for (int kk = 0; kk < 9; ++kk) {
             const h16_t *wbase = t2h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
 #pragma unroll
             for (int k = 0; k < KSW; ++k) acc3[mm] = mfma(ld8(wbase + 32 * k), f2[kk * KSW + k], acc3[mm]);
@@ -369,12 +363,12 @@ __global__ __launch_bounds__(NT) void k_wide_fwd(WArgs a, const float *__restric
                 t3s[(16 * (MPW * hf + mm) + 4 * kb + j) * BR + ob] = f2h(elu_f(acc3[mm][j] + s.b3a) + s.b3b);
     }
     __syncthreads();
-    if (!(WIDE_EXP & 8) && t3o) tile_to_global<false>(runv, t3s, t3o);
+    if (t3o) tile_to_global<false>(runv, t3s, t3o);
     // out = x + scale * W3 t3 + b4
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int ntc = nt + NTB * q;
-        if (!(WIDE_EXP & 8) && ntc < NTC) {
+        if (ntc < NTC) {
             hx8 f3[KSB];
 #pragma unroll
             for (int k = 0; k < KSB; ++k) f3[k] = frag(img, OF3 + k * NTC + ntc, lane);
@@ -432,22 +426,22 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
     float4 vx[PX], vg[PG];
     uint2 v3[P3], v2[P2];
 #pragma unroll
-    for (int u = 0; u < ((WIDE_EXP & 1) ? 0 : PX); ++u) {
+    for (int u = 0; u < PX; ++u) {
         const int i = min(tid + u * NT, NX - 1), vv = i / QX, c4 = i - vv * QX;
         vx[u] = reinterpret_cast<const float4 *>(x + int64_t(runv[vv >> 3] + (vv & 7)) * C)[c4];
     }
 #pragma unroll
-    for (int u = 0; u < ((WIDE_EXP & 1) ? 0 : P3); ++u) {
+    for (int u = 0; u < P3; ++u) {
         const int i = min(tid + u * NT, N3 - 1), seg = i / Q3, q = i - seg * Q3;
         v3[u] = reinterpret_cast<const uint2 *>(t3 + int64_t(segv[seg]) * BR)[q];
     }
 #pragma unroll
-    for (int u = 0; u < ((WIDE_EXP & 1) ? 0 : P2); ++u) {
+    for (int u = 0; u < P2; ++u) {
         const int i = min(tid + u * NT, N2 - 1), r = i / PR2, q = i - r * PR2;
         v2[u] = reinterpret_cast<const uint2 *>(t2 + int64_t(runv[r]) * BR)[q];
     }
 #pragma unroll
-    for (int u = 0; u < ((WIDE_EXP & 1) ? 0 : PG); ++u) {
+    for (int u = 0; u < PG; ++u) {
         const int i = min(tid + u * NT, NG - 1), seg = i / QX, c4 = i - seg * QX;
         vg[u] = reinterpret_cast<const float4 *>(g + int64_t(segv[seg]) * C)[c4];
     }
@@ -481,13 +475,13 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
     __syncthreads();
     hx8 f2[9 * KSW];
 #pragma unroll
-    for (int k = 0; k < 9 * KSW; ++k) f2[k] = (WIDE_EXP & 16) ? hx8{} : frag(img, OG2 + k * NTB + nt, lane);
+    for (int k = 0; k < 9 * KSW; ++k) f2[k] = frag(img, OG2 + k * NTB + nt, lane);
     // gz3 = bf16(scale * W3^T g * elu'(t3)) on the halo
     float s3b = 0.f, s3a = 0.f, ssc = 0.f;
     const int ob = 16 * nt + row;
     const uint64_t imsk = kb == 0 ? interior_mask(0) : kb == 1 ? interior_mask(1) : kb == 2 ? interior_mask(2)
                                                                                            : interior_mask(3);
-    for (int m = (WIDE_EXP & 2) ? NHM : hf; m < NHM; m += 2) {
+    for (int m = hf; m < NHM; m += 2) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < KS1; ++k) acc = mfma(ld16(gh + (16 * m + row) * C + 32 * k + 8 * kb), f3[k], acc);
@@ -508,7 +502,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         }
     }
     __syncthreads();
-    if constexpr (!(WIDE_EXP & 8)) tile_to_global<true>(runv, z3h, gz3o);
+    tile_to_global<true>(runv, z3h, gz3o);
     int vb[MPW];
 #pragma unroll
     for (int mm = 0; mm < MPW; ++mm) vb[mm] = runv[2 * (MPW * hf + mm) + (kb >> 1)] + 4 * (kb & 1);
@@ -520,7 +514,7 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         const int v = 16 * m + row, d = v & 7;
 #pragma unroll
-        for (int kk = 0; kk < ((WIDE_EXP & 4) ? 0 : 9); ++kk) {
+        for (int kk = 0; kk < 9; ++kk) {
             const h16_t *wbase = z3h + (tap_line(v, kk / 3, kk % 3) * NP + d) * BR + 8 * kb;
 #pragma unroll
             for (int k = 0; k < KSW; ++k) acc = mfma(ld8(wbase + 32 * k), f2[kk * KSW + k], acc);
@@ -537,13 +531,13 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         }
     }
     __syncthreads();
-    if constexpr (!(WIDE_EXP & 8)) tile_to_global<false>(runv, z1s, gz1o);
+    tile_to_global<false>(runv, z1s, gz1o);
     // gt1 = W1^T gz1; gx = g + gt1 * elu'(x + b1a)
     float s1b = 0.f, s1a = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int ntc = nt + NTB * q;
-        if (!(WIDE_EXP & 8) && ntc < NTC) {
+        if (ntc < NTC) {
             hx8 f1[KSB];
 #pragma unroll
             for (int k = 0; k < KSB; ++k) f1[k] = frag(img, OG1 + k * NTC + ntc, lane);

@@ -182,7 +182,11 @@ def _register(name, bwd, setup, diff):
 
 
 def _call(name, args, diff_inputs, params=()):
-    """torch.ops.vq3d.<name>(*args) with autograd through _Call."""
+    """torch.ops.vq3d.<name>(*args) with autograd through _Call; with gradients off (eval,
+    torch.no_grad: the traceable inference path) the operator itself."""
+    if not torch.is_grad_enabled():
+        out = getattr(torch.ops.vq3d, name)(*args)
+        return tuple(out) if isinstance(out, (list, tuple)) else out
     return _Call.apply(name, args, *diff_inputs, *Fn.param_edges(params, *diff_inputs))
 
 
@@ -541,6 +545,111 @@ def parse_input(x, w, b, half):
 
 def recon_loss(dec, x, nvs, cylinder, *commit):
     return _call("recon_loss", (dec, x, nvs, bool(cylinder), list(commit)), (dec, *commit))[:2]
+
+
+# ------------------------------------------------------------------------------------------------ fake kernels
+# Shape / dtype / stride propagation for tracing (torch.compile, torch.export): every operator has
+# a fake implementation.  The forward operators' outputs are [result(s), meta, saved...]: with
+# save=False (inference: eval / torch.no_grad, what a traced deployment runs) no intermediate is
+# saved and the structure is fixed, [result, meta (3 path flags)].  With save=True the saved set
+# depends on the engine the forward picks at run time (tiny / few-channel / mid / per-conv paths),
+# so a training-mode forward is not traceable: its fake says so.  The backward operators (called by
+# the registered autograd formulas only) return engine-dependent lists too and are likewise
+# eager-only.
+_CL = torch.channels_last_3d
+
+
+def _act_like(ref, shape, dtype=None):
+    return torch.empty(tuple(shape), dtype=dtype or ref.dtype, device=ref.device).contiguous(memory_format=_CL)
+
+
+def _meta(ref, nsaved=0):
+    return torch.empty(len(_FLAGS) + nsaved, dtype=torch.int64)
+
+
+def _inference_only(name, save):
+    if save:
+        raise NotImplementedError(f"vq3d::{name}: a gradient-recording forward saves engine-dependent intermediates "
+                                  "and is not traceable; trace the model in eval mode / under torch.no_grad()")
+
+
+def _eager_only(name):
+    def fake(*args, **kw):
+        raise NotImplementedError(f"vq3d::{name} runs inside the eager backward only (engine-dependent outputs)")
+    return fake
+
+
+@torch.library.register_fake("vq3d::conv3d")
+def _conv3d_fake(x, x2, residual, weight, scale, bias, cbias, pro, geom, residual_up2, post_elu, save):
+    _inference_only("conv3d", save)
+    k, st, pd, _ = geom
+    b, _, h, w, d = x.shape
+    out = [(n + 2 * pd - k) // st + 1 for n in (h, w, d)]
+    return [_act_like(x, (b, weight.shape[0], *out)), _meta(x)]
+
+
+@torch.library.register_fake("vq3d::preact_block")
+def _preact_block_fake(x, params, mode, save):
+    _inference_only("preact_block", save)
+    b, _, h, w, d = x.shape
+    f = 0.5 if mode == "down" else (2 if mode == "up" else 1)
+    return [_act_like(x, (b, params[10].shape[0], int(h * f), int(w * f), int(d * f))), _meta(x)]
+
+
+@torch.library.register_fake("vq3d::preact_run")
+def _preact_run_fake(x, params, kind, out_fp32, save):
+    _inference_only("preact_run", save)
+    return [_act_like(x, x.shape, torch.float32 if out_fp32 else x.dtype), _meta(x)]
+
+
+@torch.library.register_fake("vq3d::vq_nearest")
+def _vq_nearest_fake(z, embed, commitment_cost, zst_dtype):
+    b, _, h, w, d = z.shape
+    return [torch.empty((), dtype=torch.float32, device=z.device), _act_like(z, z.shape, zst_dtype or z.dtype),
+            torch.empty((b, h, w, d), dtype=torch.int64, device=z.device)]
+
+
+@torch.library.register_fake("vq3d::vq_nearest_backward")
+def _vq_nearest_backward_fake(z, embed, idx, coef, g_loss, g_zst):
+    return _act_like(z, z.shape)
+
+
+@torch.library.register_fake("vq3d::vq_init")
+def _vq_init_fake(z, embed, embed_avg, cluster_size, first_pass):
+    return None
+
+
+@torch.library.register_fake("vq3d::vq_ema")
+def _vq_ema_fake(z, idx, embed, embed_avg, cluster_size, ema_slot, decay, laplace_alpha):
+    return None
+
+
+@torch.library.register_fake("vq3d::parse_input")
+def _parse_input_fake(x, weight, bias, half):
+    b, _, h, w, d = x.shape
+    return [_act_like(x, (b, weight.shape[0], h, w, d), half), _meta(x, 1)]  # saves x (an input)
+
+
+@torch.library.register_fake("vq3d::upsample2x")
+def _upsample2x_fake(x):
+    b, c, h, w, d = x.shape
+    return _act_like(x, (b, c, 2 * h, 2 * w, 2 * d))
+
+
+@torch.library.register_fake("vq3d::upsample2x_backward")
+def _upsample2x_backward_fake(g, src_shape):
+    return _act_like(g, src_shape)
+
+
+@torch.library.register_fake("vq3d::recon_loss")
+def _recon_loss_fake(dec, x, nvs, cylinder, commit):
+    s = torch.empty((), dtype=torch.float32, device=dec.device)
+    return [s, torch.empty_like(s), _meta(dec, 3)]  # saves dec, x, nvs (inputs)
+
+
+for _n in ("conv3d_backward", "preact_block_backward", "preact_run_backward", "parse_input_backward",
+           "recon_loss_backward"):
+    torch.library.register_fake(f"vq3d::{_n}")(_eager_only(_n))
 
 
 OPS = ("conv3d", "conv3d_backward", "preact_block", "preact_block_backward", "preact_run", "preact_run_backward",

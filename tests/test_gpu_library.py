@@ -138,3 +138,33 @@ def test_library_ops_are_the_kernels(gpu):
         assert torch.equal(ya, yb)
         assert torch.equal(gxa, gxb)
         assert _rel(gwb, gwa) <= 1e-5 and _rel(gbb, gba) <= 1e-5, (_rel(gwb, gwa), _rel(gbb, gba))
+
+
+def test_exported_block_operator_replays(gpu):
+    """torch.export captures the vq3d::preact_block operator (its fake kernel propagates the
+    shapes); the exported program, run on the GPU, gives the eager operator's output bit for bit."""
+    from vq3d import layers as VL
+
+    class Block(torch.nn.Module):
+        def __init__(self, blk):
+            super().__init__()
+            self.blk = blk
+
+        def forward(self, x):
+            return torch.ops.vq3d.preact_block(x, list(self.blk._fn_params), self.blk.mode, False)[0]
+
+    torch.manual_seed(0)
+    blk = VL.PreActFixupResBlock(18, 18, mode="same")
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    m = Block(blk).to(gpu).eval()
+    x = torch.randn(1, 18, 32, 32, 32, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last_3d)
+    with torch.no_grad():
+        ref = m(x).clone()
+        ep = torch.export.export(m, (x,))
+        got = ep.module()(x)
+    torch.cuda.synchronize()
+    calls = [n for n in ep.graph.nodes if n.op == "call_function" and "vq3d" in str(n.target)]
+    assert len(calls) == 1 and "preact_block" in str(calls[0].target)
+    assert torch.equal(got, ref)
