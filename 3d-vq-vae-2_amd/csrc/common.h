@@ -22,6 +22,10 @@ namespace vq3d_rt {
 void set_error(const std::string &msg);
 int fail(const std::string &msg);
 int check_launch(const char *what);
+constexpr int kPairCap = 65536;
+constexpr unsigned kTicketRegions = 16, kTicketSlots = 4;
+unsigned ticket_slot(hipStream_t st);
+float *pair_pool(unsigned slot);
 }  // namespace vq3d_rt
 
 namespace vq3d {
@@ -307,26 +311,17 @@ __device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {
 // launches on different streams -- a side stream, a second level chain -- never share one.  Up
 // to kTicketRegions streams hold regions at once; a further stream takes over the least recently
 // claimed region, so more than that many streams must not run ticketed launches concurrently.
-constexpr unsigned kTicketRegions = 16, kTicketSlots = 4, kTickets = kTicketRegions * kTicketSlots;
+constexpr unsigned kTicketRegions = vq3d_rt::kTicketRegions, kTicketSlots = vq3d_rt::kTicketSlots,
+                   kTickets = kTicketRegions * kTicketSlots;
 constexpr unsigned kShards = 16, kTicketLine = 32;
 static __device__ unsigned g_tickets[kTickets * (kShards + 1) * kTicketLine];
-static inline unsigned ticket_slot(hipStream_t st) {
-    static std::mutex mu;
-    static hipStream_t owner[kTicketRegions] = {};
-    static bool used[kTicketRegions] = {};
-    static unsigned next[kTicketRegions] = {}, claims = 0;
-    std::lock_guard<std::mutex> lk(mu);
-    unsigned r = kTicketRegions;
-    for (unsigned i = 0; i < kTicketRegions; ++i)
-        if (used[i] && owner[i] == st) r = i;
-    if (r == kTicketRegions) {
-        r = claims++ % kTicketRegions;
-        owner[r] = st;
-        used[r] = true;
-        next[r] = 0;
-    }
-    return r * kTicketSlots + (next[r]++ % kTicketSlots);
-}
+// the stream's next slot (misc.hip: ONE slot table for the library, both 16-bit builds)
+inline unsigned ticket_slot(hipStream_t st) { return vq3d_rt::ticket_slot(st); }
+// Pair storage for the in-grid sums: kPairCap {pre, post} pairs per slot, one device array for the
+// library (misc.hip), so a kernel needs no workspace for them.  A slot is held by one launch at a
+// time (the invariant above), so its pairs are too.
+constexpr int kPairCap = vq3d_rt::kPairCap;
+inline float *pair_pool(unsigned slot) { return vq3d_rt::pair_pool(slot); }
 // every thread of the (1-D, NT-thread) workgroup calls this with the workgroup's sums in thread 0;
 // part holds nb {pre, post} float pairs; *dpre += the pres' sum, *dpost += the posts'
 template <int NT>
@@ -375,6 +370,35 @@ __device__ __forceinline__ void finish_partials(float *part, int nb, int bid, fl
     }
     if (threadIdx.x < nsh) atomicExch(tk + threadIdx.x * kTicketLine, 0u);
     if (threadIdx.x == kShards) atomicExch(tk + kShards * kTicketLine, 0u);
+}
+
+// The grid-wide {pre, post} sums of a kernel whose workgroups hold their block sums (every thread
+// calls this; thread 0's values count): summed in fixed order by the last workgroup when the host
+// passed pair storage (GridSum from grid_sum_for), else -- grids beyond kPairCap workgroups --
+// float atomics.
+struct GridSum {
+    float *pairs;
+    unsigned slot;
+};
+template <int NT>
+__device__ __forceinline__ void grid_sum2(const GridSum &gs, float pre, float post, float *dpre, float *dpost,
+                                          float *red /* >= 8 */) {
+    if (!dpre && !dpost) return;
+    if (gs.pairs) {
+        const int nb = int(gridDim.x * gridDim.y * gridDim.z);
+        const int bid = int(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+        finish_partials<NT>(gs.pairs, nb, bid, pre, post, dpre, dpost, gs.slot, red);
+    } else if (threadIdx.x == 0) {
+        if (dpre) atomicAdd(dpre, pre);
+        if (dpost) atomicAdd(dpost, post);
+    }
+}
+// host: the GridSum of a launch of nblocks workgroups on stream s that sums (want)
+inline GridSum grid_sum_for(hipStream_t s, int64_t nblocks, bool want) {
+    // one workgroup: its own sum is the total (a single add, deterministic)
+    if (!want || nblocks <= 1 || nblocks > kPairCap) return GridSum{nullptr, 0u};
+    const unsigned k = ticket_slot(s);
+    return GridSum{pair_pool(k), k};
 }
 
 // ---------------------------------------------------------------- trilinear x2 (align_corners=False)

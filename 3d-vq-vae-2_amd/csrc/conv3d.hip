@@ -118,7 +118,7 @@ template <typename T, int CIT>
 __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restrict__ g, const float *__restrict__ gscale,
                                                    const float *__restrict__ w, BwdEpi<T> be, int all_taps,
                                                    T *__restrict__ gx, T *__restrict__ gx2, float *dpre,
-                                                   float *dpost) {
+                                                   float *dpost, GridSum gsum) {
     extern __shared__ __attribute__((aligned(16))) float wsh[];  // [taps][Cout][CIT]
     __shared__ float red[8];
     const int Ct = a.Cin + a.Cin2;
@@ -187,10 +187,7 @@ __global__ __launch_bounds__(256) void k_conv_dgrad(ConvArgs a, const T *__restr
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            atomic_add_f(dpre, pre);
-            atomic_add_f(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -514,7 +511,8 @@ static int launch_dgrad(const vq3d_conv_desc *d, const void *g, const float *gsc
 #define L(C)                                                                                                  \
     case C:                                                                                                   \
         k_conv_dgrad<T, C><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, be, all_taps, (T *)gx, (T *)gx2,  \
-                                                  dpre, dpost);                                               \
+                                                  dpre, dpost, grid_sum_for(s, int64_t(grid.x) * grid.y,     \
+                                                                            dpre || dpost));                  \
         break;
     switch (cit) { L(1) L(2) L(4) L(8) L(12) L(16) }
 #undef L
@@ -542,6 +540,16 @@ static bool use_lines_wgrad(const vq3d_conv_desc *d) {
     return !plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
                       d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true)
                 .ok;
+}
+
+// the generic engines' image workspace (deterministic path; without it they fall back to atomics)
+static size_t generic_wgrad_ws(const vq3d_conv_desc *d) {
+    if (d->dtype != VQ3D_HALF || use_lines_wgrad(d) || d->kernel == 1) return 0;
+    MPlan m = plan_mfma(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
+                        d->kernel, d->stride, d->pad, d->pad_mode == VQ3D_PAD_CIRCULAR, true);
+    if (!m.ok) return 0;
+    m.a.wCt = d->cin + d->cin2;
+    return gen_wgrad_bytes(gen_wgrad_geom(m), d->cout);
 }
 
 template <typename T>
@@ -578,9 +586,9 @@ static int launch_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, 
                 // 128 -> 128 @8x8x2, 212 vs 155 us at 64 -> 128 k4 s2 @32x32x8)
                 if (d->cout <= 64)
                     return launch_wgrad_mfma(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
-                                             dbias, dcbias, s);
+                                             dbias, dcbias, ws, ws_bytes, s);
                 return launch_wgrad_tiled(m, (const T *)x, (const T *)x2, (const T *)g, w, escale, dw, dscale,
-                                          dbias, dcbias, s);
+                                          dbias, dcbias, ws, ws_bytes, s);
             }
         }
     }
@@ -658,7 +666,8 @@ size_t vq3d_conv3d_workspace_size(const vq3d_conv_desc *d, int32_t pass) {
     if (pass == VQ3D_PASS_FWD) return lines_workspace(d, false);
     if (pass == VQ3D_PASS_BWD_DATA) return is_pointwise(d) ? pw_dgrad_workspace(d) : lines_workspace(d, true);
     if (is_pointwise(d)) return pw_wgrad_workspace(d);
-    return std::max({use_lines_wgrad(d) ? lines_wgrad_workspace(d) : size_t(0), mid_w2grad_ws(d), wgrad_ds_ws(d)});
+    return std::max({use_lines_wgrad(d) ? lines_wgrad_workspace(d) : size_t(0), mid_w2grad_ws(d), wgrad_ds_ws(d),
+                     generic_wgrad_ws(d)});
 }
 
 int vq3d_conv3d_bwd_weight(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,

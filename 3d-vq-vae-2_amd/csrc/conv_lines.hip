@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
                                               FwdEpi<h16_t> fe,
                                               BwdEpi<h16_t> be, const float *__restrict__ gscale,
                                               h16_t *__restrict__ y, h16_t *__restrict__ y2, float *dpre,
-                                              float *dpost) {
+                                              float *dpost, GridSum gsum) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MTW = MT<NT>::value;
     constexpr int NTOT = NT * 16;
@@ -495,10 +495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
     if (DGRAD && (dpre || dpost)) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (tid == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -711,7 +708,8 @@ void launch(const Plan &P, const h16_t *x, const h16_t *x2, const float *w, int 
         }                                                                                                     \
         const unsigned nb = resident_blocks(kern, P.lds, unsigned(P.a.nbricks));                              \
         const dim3 grid{nb, unsigned(P.a.ntg), 1u};                                                           \
-        kern<<<grid, 256, P.lds, s>>>(P.a, x, x2, w, wCt, wpk, fe, be, gscale, y, y2, dpre, dpost);           \
+        const GridSum gs = grid_sum_for(s, int64_t(nb) * P.a.ntg, DGRAD && (dpre || dpost));                    \
+        kern<<<grid, 256, P.lds, s>>>(P.a, x, x2, w, wCt, wpk, fe, be, gscale, y, y2, dpre, dpost, gs);       \
     }
 #define ALNS(NT)                                                                                              \
     switch (P.aln) {                                                                                          \

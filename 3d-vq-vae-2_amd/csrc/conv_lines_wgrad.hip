@@ -302,7 +302,7 @@ template <int LANES>
 __global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, const float *__restrict__ part,
                                                            int nblk, const float *__restrict__ w,
                                                            const float *__restrict__ escale, float *dw,
-                                                           float *dscale, float *dbias, float *dcbias) {
+                                                           float *dscale, float *dbias, float *dcbias, GridSum gsum) {
     __shared__ float red[8];
     const int lane = threadIdx.x % LANES;
     const int f = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
@@ -339,13 +339,10 @@ __global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, co
             bs = sum;
         }
     }
-    if (dscale) {
+    if (dscale || dbias) {
         wg = block_sum<float, 256>(wg, red);
-        if (threadIdx.x == 0) atomicAdd(dscale, wg);
-    }
-    if (dbias) {
         bs = block_sum<float, 256>(bs, red + 4);
-        if (threadIdx.x == 0) atomicAdd(dbias, bs);
+        grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }
 
@@ -512,8 +509,9 @@ int launch_lines_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, c
     int lanes = 1;
     while (lanes < 64 && lanes * 32 < P.nbx) lanes *= 2;
 #define RED(L)                                                                                                 \
-    k_lines_wgrad_reduce<L><<<(P.a.nent + 256 / L - 1) / (256 / L), 256, 0, s>>>(P.a, P.ntm, part, P.nbx, w,    \
-                                                                                 escale, dw, dscale, dbias, dcbias)
+    k_lines_wgrad_reduce<L><<<(P.a.nent + 256 / L - 1) / (256 / L), 256, 0, s>>>(                                \
+        P.a, P.ntm, part, P.nbx, w, escale, dw, dscale, dbias, dcbias,                                           \
+        grid_sum_for(s, (P.a.nent + 256 / L - 1) / (256 / L), dscale || dbias))
     switch (lanes) {
     case 1: RED(1); break;
     case 2: RED(2); break;

@@ -92,7 +92,7 @@ __device__ __forceinline__ void store_row(T *__restrict__ p, const float (&v)[N]
 template <typename T, int COT, int CO>
 __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict__ g, const float *__restrict__ gscale,
                                                  const float *__restrict__ w, BwdEpi<T> be, T *__restrict__ gx,
-                                                 T *__restrict__ gx2, float *dpre, float *dpost) {
+                                                 T *__restrict__ gx2, float *dpre, float *dpost, GridSum gsum) {
     extern __shared__ __attribute__((aligned(16))) float wsh[];  // [tap][Cout][COT]
     __shared__ float red[8];
     const int K3 = a.k * a.k * a.k;
@@ -213,10 +213,7 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict_
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -236,7 +233,7 @@ template <int CI, int CO, int K>
 __global__ __launch_bounds__(256) void k_dgrad_s2_cell(S2Args a, const h16_t *__restrict__ g,
                                                       const float *__restrict__ gscale, const float *__restrict__ w,
                                                       BwdEpi<h16_t> be, h16_t *__restrict__ gx, float *dpre,
-                                                      float *dpost) {
+                                                      float *dpost, GridSum gsum) {
     constexpr int NR = K == 4 ? 27 : 1, K3 = K * K * K, NKS = (NR * CO + 31) / 32, NM = 8 * CI / 16;
     constexpr int EPL = CO == 4 ? 2 : 1;  // g rows per lane and k-step
     static_assert((CI == 4 || CI == 8) && (CO == 4 || CO == 8) && (K == 2 || K == 4), "few-channel form");
@@ -413,10 +410,7 @@ done:
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -442,7 +436,7 @@ template <int K, int NTM>
 __global__ __launch_bounds__(256) void k_dgrad_s2_mma(S2Args a, const h16_t *__restrict__ g,
                                                      const float *__restrict__ gscale, const float *__restrict__ w,
                                                      BwdEpi<h16_t> be, h16_t *__restrict__ gx, float *dpre,
-                                                     float *dpost, int nks) {
+                                                     float *dpost, int nks, GridSum gsum) {
     constexpr int NT_ = K / 2, NJ = NT_ * NT_ * NT_, K3 = K * K * K;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint4 *afr = reinterpret_cast<uint4 *>(smem);  // [NTM][nks][64] packed A fragments
@@ -546,10 +540,7 @@ __global__ __launch_bounds__(256) void k_dgrad_s2_mma(S2Args a, const h16_t *__r
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -594,7 +585,8 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
             if (a.Cin == CI_ && a.Cout == CO_ && a.k == K_) {                                                  \
                 k_dgrad_s2_cell<CI_, CO_, K_><<<fg, 256, 0, s>>>(a, (const h16_t *)g, gscale, w,                \
                                                                  reinterpret_cast<const BwdEpi<h16_t> &>(be),    \
-                                                                 (h16_t *)gx, dpre, dpost);                    \
+                                                                 (h16_t *)gx, dpre, dpost,               \
+                                                                 grid_sum_for(s, fg.x, dpre || dpost));         \
                 return check_launch("conv3d_bwd_data(s2 cell mma)");                                           \
             }
             PK(4, 4, 4) PK(4, 8, 4) PK(8, 4, 4) PK(8, 8, 4) PK(4, 4, 2) PK(4, 8, 2) PK(8, 4, 2) PK(8, 8, 2)
@@ -627,7 +619,9 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
 #define MM(K_, NTM_)                                                                                          \
                 if (a.k == K_ && ntm == NTM_) {                                                                  \
                     k_dgrad_s2_mma<K_, NTM_><<<grid, 256, lds, s>>>(a, (const h16_t *)g, gscale, w, be,           \
-                                                                   (h16_t *)gx, dpre, dpost, nks);               \
+                                                                   (h16_t *)gx, dpre, dpost, nks,                 \
+                                                                   grid_sum_for(s, int64_t(gxn) * 8 * nz,          \
+                                                                                dpre || dpost));                 \
                     return check_launch("conv3d_bwd_data(s2 mma)");                                              \
                 }
                 MM(2, 1) MM(2, 2) MM(2, 4) MM(4, 1) MM(4, 2) MM(4, 4)
@@ -651,7 +645,7 @@ int launch_dgrad_s2(const vq3d_conv_desc *d, const void *g, const float *gscale,
 #define L(C, CO)                                                                                              \
     case C:                                                                                                   \
         k_dgrad_s2<T, C, CO><<<grid, 256, lds, s>>>(a, (const T *)g, gscale, w, be, (T *)gx, (T *)gx2, dpre,  \
-                                                    dpost);                                                   \
+                                                    dpost, grid_sum_for(s, int64_t(nbx) * ych, dpre || dpost)); \
         break;
 #define LS(CO)                                                                                                \
     switch (cot) { L(1, CO) L(2, CO) L(4, CO) L(8, CO) L(16, CO) }

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void k_small_mma(SArgs s, const h16_t *__restr
 template <typename T, bool DG>
 __global__ __launch_bounds__(256) void k_small_epi(SArgs s, const float *__restrict__ part, FwdEpi<T> fe,
                                                   BwdEpi<T> be, const float *__restrict__ gscale, T *__restrict__ out,
-                                                  T *__restrict__ out2, float *dpre, float *dpost) {
+                                                  T *__restrict__ out2, float *dpre, float *dpost, GridSum gsum) {
     __shared__ float red[8];
     const ConvArgs &a = s.c;
     const ActDeriv dv = make_deriv(be);
@@ -300,10 +300,7 @@ __global__ __launch_bounds__(256) void k_small_epi(SArgs s, const float *__restr
     if (DG && (dpre || dpost)) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -414,9 +411,10 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
             const int64_t n = int64_t(p.s.nvox) * p.s.Ot;
             const unsigned eb = unsigned(std::min<int64_t>((n + 255) / 256, 1024));
             if (dgrad)
-                k_small_epi<T, true><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, (T *)out2, dpre, dpost);
+                k_small_epi<T, true><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, (T *)out2, dpre, dpost,
+                                                      grid_sum_for(st, eb, dpre || dpost));
             else
-                k_small_epi<T, false><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, nullptr, nullptr, nullptr);
+                k_small_epi<T, false><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, nullptr, nullptr, nullptr, GridSum{});
             return check_launch(dgrad ? "conv3d_bwd_data(small grid mma)" : "conv3d_fwd(small grid mma)");
         }
     }
@@ -440,9 +438,10 @@ int launch_small(const vq3d_conv_desc *d, bool dgrad, const void *in, const void
     const int64_t n = int64_t(p.s.nvox) * p.s.Ot;
     const unsigned eb = unsigned(std::min<int64_t>((n + 255) / 256, 1024));
     if (dgrad)
-        k_small_epi<T, true><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, (T *)out2, dpre, dpost);
+        k_small_epi<T, true><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, (T *)out2, dpre, dpost,
+                                                      grid_sum_for(st, eb, dpre || dpost));
     else
-        k_small_epi<T, false><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, nullptr, nullptr, nullptr);
+        k_small_epi<T, false><<<eb, 256, 0, st>>>(p.s, part, fe, be, gscale, (T *)out, nullptr, nullptr, nullptr, GridSum{});
     return check_launch(dgrad ? "conv3d_bwd_data(small grid)" : "conv3d_fwd(small grid)");
 }
 

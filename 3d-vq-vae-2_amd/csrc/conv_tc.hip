@@ -354,7 +354,8 @@ __global__ __launch_bounds__(NTC) void k_tc_wgrad(TcArgs a, const T *__restrict_
 template <int CI, int CO, int KW, int LANES>
 __global__ __launch_bounds__(256) void k_tc_wgrad_reduce(const float *__restrict__ part, int nblk,
                                                         const float *__restrict__ w, const float *__restrict__ escale,
-                                                        float *dw, float *dscale, float *dbias, float *dcbias) {
+                                                        float *dw, float *dscale, float *dbias, float *dcbias,
+                                                        GridSum gsum) {
     constexpr int NE = 3 * KW * CI * CO + CO;
     constexpr int NPL = 9 / KW;
     __shared__ float red[8];
@@ -385,13 +386,10 @@ __global__ __launch_bounds__(256) void k_tc_wgrad_reduce(const float *__restrict
             bs = sum;
         }
     }
-    if (dscale) {
+    if (dscale || dbias) {
         wg = block_sum<float, 256>(wg, red);
-        if (threadIdx.x == 0) atomicAdd(dscale, wg);
-    }
-    if (dbias) {
         bs = block_sum<float, 256>(bs, red + 4);
-        if (threadIdx.x == 0) atomicAdd(dbias, bs);
+        grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }
 
@@ -497,7 +495,8 @@ int launch_tc_wgrad(const vq3d_conv_desc *d, const void *x, const void *g, const
     k_tc_wgrad_reduce<CI_, CO_, (CI_ * CO_ > 4 ? 1 : 3), L>                                                    \
         <<<((9 / (CI_ * CO_ > 4 ? 1 : 3)) * (3 * (CI_ * CO_ > 4 ? 1 : 3) * CI_ * CO_ + CO_) + 256 / L - 1) /      \
                (256 / L),                                                                                       \
-           256, 0, s>>>(part, int(nb), w, escale, dw, dscale, dbias, dcbias)
+           256, 0, s>>>(part, int(nb), w, escale, dw, dscale, dbias, dcbias,                                   \
+                        grid_sum_for(s, int64_t(npl) * (3 * kw * ci * co + co), dscale || dbias))
 #define TW(CI_, CO_)                                                                                            \
     if (ci == CI_ && co == CO_) {                                                                               \
         k_tc_wgrad<T, CI_, CO_, (CI_ * CO_ > 4 ? 1 : 3)><<<grid, NTC, lds, s>>>(a, (const T *)x, (const T *)g,  \

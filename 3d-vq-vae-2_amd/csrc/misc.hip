@@ -1,4 +1,4 @@
-// Upsample (ResizeConv3D's nn.Upsample), reconstruction loss, EvoNorm-S0, Adam(amsgrad),
+// Reconstruction loss, EvoNorm-S0, Adam(amsgrad),
 // casts, and the error plumbing of libvq3d.
 #include "common.h"
 #include "engines.h"
@@ -21,108 +21,47 @@ int check_launch(const char *what) {
     return 0;
 }
 const char *last_error() { return g_last_error.c_str(); }
+
+// The ticket-slot table (common.h: keyed by stream; one table for both builds, so every ticketed
+// launch of the library on one stream draws from that stream's region) and the pair storage the
+// slots index.
+unsigned ticket_slot(hipStream_t st) {
+    static std::mutex mu;
+    static hipStream_t owner[kTicketRegions] = {};
+    static bool used[kTicketRegions] = {};
+    static unsigned next[kTicketRegions] = {}, claims = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    unsigned r = kTicketRegions;
+    for (unsigned i = 0; i < kTicketRegions; ++i)
+        if (used[i] && owner[i] == st) r = i;
+    if (r == kTicketRegions) {
+        r = claims++ % kTicketRegions;
+        owner[r] = st;
+        used[r] = true;
+        next[r] = 0;
+    }
+    return r * kTicketSlots + (next[r]++ % kTicketSlots);
+}
+static __device__ uint64_t g_pair_pool[size_t(kTicketRegions) * kTicketSlots * kPairCap];
+float *pair_pool(unsigned slot) {
+    static std::mutex mu;
+    static float *base[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    if (!base[dev]) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_pair_pool)) != hipSuccess) return nullptr;
+        base[dev] = static_cast<float *>(p);
+    }
+    return base[dev] + size_t(slot) * kPairCap * 2;
+}
 }  // namespace vq3d_rt
 #endif
 
 namespace vq3d {
 
 static unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048))); }
-
-// ============================================================================ upsample x2
-// y[b, 2h', 2w', 2d', c] = trilinear(prologue(x)) ; thread per output element
-template <typename T>
-__global__ __launch_bounds__(256) void k_up_fwd(const T *__restrict__ x, int B, int C, int H, int W, int D,
-                                               int pk, const float *pa, const float *pb, T *__restrict__ y) {
-    const int64_t n = int64_t(B) * 8 * H * W * D * C;
-    const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
-    if (i >= n) return;
-    const Prologue pro = make_prologue(pk, pa, pb);
-    int64_t t = i;
-    const int c = int(t % C); t /= C;
-    const int od = int(t % (2 * D)); t /= 2 * D;
-    const int ow = int(t % (2 * W)); t /= 2 * W;
-    const int oh = int(t % (2 * H));
-    const int b = int(t / (2 * H));
-    int h0, h1, w0, w1, d0, d1;
-    float lh, lw, ldd;
-    up_coeff(oh, H, h0, h1, lh);
-    up_coeff(ow, W, w0, w1, lw);
-    up_coeff(od, D, d0, d1, ldd);
-    auto X = [&](int hh, int ww, int dd) {
-        return pro.apply(ld(x + (((int64_t(b) * H + hh) * W + ww) * D + dd) * C + c));
-    };
-    const float v = (1.f - lh) * ((1.f - lw) * ((1.f - ldd) * X(h0, w0, d0) + ldd * X(h0, w0, d1)) +
-                                  lw * ((1.f - ldd) * X(h0, w1, d0) + ldd * X(h0, w1, d1))) +
-                    lh * ((1.f - lw) * ((1.f - ldd) * X(h1, w0, d0) + ldd * X(h1, w0, d1)) +
-                          lw * ((1.f - ldd) * X(h1, w1, d0) + ldd * X(h1, w1, d1)));
-    st(y + i, v);
-}
-
-// list of (destination index, weight) pairs that read source index i along one axis
-__device__ __forceinline__ int up_adjoint(int i, int n, int *js, float *ws) {
-    int cnt = 0;
-    for (int j = max(0, 2 * i - 2); j <= min(2 * n - 1, 2 * i + 2); ++j) {
-        int a0, a1;
-        float l1;
-        up_coeff(j, n, a0, a1, l1);
-        float wv = 0.f;
-        if (a0 == i) wv += 1.f - l1;
-        if (a1 == i) wv += l1;
-        if (wv != 0.f) {
-            js[cnt] = j;
-            ws[cnt] = wv;
-            ++cnt;
-        }
-    }
-    return cnt;
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_up_bwd(const T *__restrict__ gy, int B, int C, int H, int W, int D,
-                                               int dmode, const float *dparam, const T *__restrict__ aux,
-                                               const T *__restrict__ addend, T *__restrict__ gx, float *dpre,
-                                               float *dpost) {
-    __shared__ float red[8];
-    const int64_t n = int64_t(B) * H * W * D * C;
-    ActDeriv dv;
-    dv.mode = aux ? dmode : 0;
-    dv.p = (dv.mode && dparam) ? *dparam : 0.f;
-    float pre = 0.f, post = 0.f;
-    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
-        int64_t t = i;
-        const int c = int(t % C); t /= C;
-        const int id = int(t % D); t /= D;
-        const int iw = int(t % W); t /= W;
-        const int ih = int(t % H);
-        const int b = int(t / H);
-        int jh[5], jw[5], jd[5];
-        float wh[5], ww[5], wd[5];
-        const int nh = up_adjoint(ih, H, jh, wh), nw = up_adjoint(iw, W, jw, ww), nd = up_adjoint(id, D, jd, wd);
-        float acc = 0.f;
-        for (int a = 0; a < nh; ++a)
-            for (int bb = 0; bb < nw; ++bb) {
-                float s = 0.f;
-                for (int cc = 0; cc < nd; ++cc)
-                    s = fmaf(wd[cc],
-                             ld(gy + (((int64_t(b) * 2 * H + jh[a]) * 2 * W + jw[bb]) * 2 * D + jd[cc]) * C + c), s);
-                acc = fmaf(wh[a] * ww[bb], s, acc);
-            }
-        float v = acc;
-        pre += v;
-        if (dv.mode) v *= dv(ld(aux + i));
-        post += v;
-        if (addend) v += ld(addend + i);
-        st(gx + i, v);
-    }
-    if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
-    }
-}
 
 // ============================================================================ reconstruction loss
 __device__ __forceinline__ bool in_cylinder(int h, int w, int H, int W) {

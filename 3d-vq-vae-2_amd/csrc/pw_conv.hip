@@ -601,8 +601,9 @@ static int launch_pw_sg(const vq3d_conv_desc *d, bool dgrad, const void *in, con
     const dim3 grid{nbx, unsigned(ny), 1u};
     const bool want_part = dgrad && (dpre || dpost);
     const int nb = int(nbx) * ny;
-    float *part = (want_part && nb > 1024 && ws && ws_bytes >= size_t(2) * nb * 4) ? static_cast<float *>(ws) : nullptr;
-    const unsigned tk = part ? ticket_slot(st) : 0u;
+    const GridSum gsm = grid_sum_for(st, nb, want_part);  // fixed-order sums (pair pool)
+    float *part = gsm.pairs;
+    const unsigned tk = gsm.slot;
 #define SG(O)                                                                                                    \
     case O:                                                                                                      \
         if (dgrad)                                                                                               \
@@ -840,8 +841,9 @@ static bool launch_pw_mma(const vq3d_conv_desc *d, bool dgrad, const void *in, c
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nbx0, 1024 / ny)));
     const dim3 nb{nbx, unsigned(ny), 1u};
     const bool want_part = dgrad && (dpre || dpost);
-    float *part = (want_part && ws && ws_bytes >= size_t(2) * nbx * ny * 4) ? static_cast<float *>(ws) : nullptr;
-    const unsigned tk = part ? ticket_slot(s) : 0u;
+    const GridSum gsm = grid_sum_for(s, int64_t(nbx) * ny, want_part);  // fixed-order sums (pair pool)
+    float *part = gsm.pairs;
+    const unsigned tk = gsm.slot;
     ConvArgs ca = make_args(d, pa, pb);
 #define MM(NT_)                                                                                                 \
     if (dgrad)                                                                                                  \
@@ -885,8 +887,9 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     if (rows_path(d, dgrad, fe.res_up2 ? fe.res : nullptr) && al(in) && al(out) && al(fe.res) && al(be.aux) && al(be.addend)) {
         const int ci = dgrad ? d->cout : d->cin, co = dgrad ? d->cin : d->cout;
         const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>((nvox + 1023) / 1024, kMaxPwBlocks)));
-        float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
-        const unsigned tk = part ? ticket_slot(s) : 0u;
+        const GridSum gsm = grid_sum_for(s, nbx, want_part);  // fixed-order sums (pair pool)
+        float *part = gsm.pairs;
+        const unsigned tk = gsm.slot;
         const int key = ci * 16 + co;
         const int pk = dgrad ? VQ3D_PRO_NONE : d->pro_kind;
         const FastDiv fD(uint32_t(d->out_d)), fW(uint32_t(d->out_w)), fH(uint32_t(d->out_h));
@@ -962,8 +965,9 @@ int launch_pw1(const vq3d_conv_desc *d, bool dgrad, const void *in, const void *
     const int64_t nseg = (a.nvox + a.segv - 1) / a.segv;
     const int slab_cap = std::min(kMaxPwBlocks, 1024);  // measured: 1024 >= 2048 > 512 workgroups
     const unsigned nbx = unsigned(std::max<int64_t>(1, std::min<int64_t>(nseg, slab_cap)));
-    float *part = (want_part && nbx > 512 && ws && ws_bytes >= size_t(2) * nbx * 4) ? static_cast<float *>(ws) : nullptr;
-    const unsigned tk = part ? ticket_slot(s) : 0u;
+    const GridSum gsm = grid_sum_for(s, nbx, want_part);  // fixed-order sums (pair pool)
+    float *part = gsm.pairs;
+    const unsigned tk = gsm.slot;
 #define L(C)                                                                                                    \
     case C: {                                                                                                   \
         auto kern = dgrad ? k_pw2<T, C, true> : k_pw2<T, C, false>;                                             \

@@ -84,6 +84,7 @@ __device__ __forceinline__ void stage(float *__restrict__ dst, int P, int off, c
 struct WgOut {
     const float *w, *escale;
     float *dw, *dscale, *dbias, *dcbias;
+    GridSum gsum;  // direct mode over several workgroups (the 2-D k_pw_wgrad grid): the scalar sums
 };
 
 __device__ __forceinline__ void finish_entry(const WgOut &o, int e, int Ct, float sum, float &wg, float &bs) {
@@ -99,14 +100,10 @@ __device__ __forceinline__ void finish_entry(const WgOut &o, int e, int Ct, floa
 }
 
 __device__ __forceinline__ void finish_block(const WgOut &o, float wg, float bs, float *red) {
-    if (o.dscale) {
-        wg = block_sum<float, 256>(wg, red);
-        if (threadIdx.x == 0) atomicAdd(o.dscale, wg);
-    }
-    if (o.dbias) {
-        bs = block_sum<float, 256>(bs, red + 4);
-        if (threadIdx.x == 0) atomicAdd(o.dbias, bs);
-    }
+    if (!o.dscale && !o.dbias) return;
+    wg = block_sum<float, 256>(wg, red);
+    bs = block_sum<float, 256>(bs, red + 4);
+    grid_sum2<256>(o.gsum, wg, bs, o.dscale, o.dbias, red);
 }
 
 template <typename T>
@@ -301,7 +298,8 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reg(int64_t nvox, const T *__r
 template <int LANES>
 __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict__ part, int nblk, int ne, int Ct,
                                                         const float *__restrict__ w, const float *__restrict__ escale,
-                                                        float *dw, float *dscale, float *dbias, float *dcbias) {
+                                                        float *dw, float *dscale, float *dbias, float *dcbias,
+                                                        GridSum gsum) {
     __shared__ float red[8];
     const int lane = threadIdx.x % LANES;
     const int e = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
@@ -339,13 +337,10 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
             bs = sum;
         }
     }
-    if (dscale) {
+    if (dscale || dbias) {
         wg = block_sum<float, 256>(wg, red);
-        if (threadIdx.x == 0) atomicAdd(dscale, wg);
-    }
-    if (dbias) {
         bs = block_sum<float, 256>(bs, red + 4);
-        if (threadIdx.x == 0) atomicAdd(dbias, bs);
+        grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }
 
@@ -599,7 +594,8 @@ bool plan_mma(const vq3d_conv_desc *d, const void *x, const void *x2, const void
 // are added in a fixed order
 __global__ __launch_bounds__(256) void k_pw_wgrad_reduce_t(const float *__restrict__ part, int nblk, int ne, int Ct,
                                                           const float *__restrict__ w, const float *__restrict__ escale,
-                                                          float *dw, float *dscale, float *dbias, float *dcbias) {
+                                                          float *dw, float *dscale, float *dbias, float *dcbias,
+                                                          GridSum gsum) {
     __shared__ float red[8];
     __shared__ float ws4[4][64];
     const int el = threadIdx.x & 63, bg = threadIdx.x >> 6;
@@ -626,13 +622,10 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce_t(const float *__restri
             bs = sum;
         }
     }
-    if (dscale) {
+    if (dscale || dbias) {
         wg = block_sum<float, 256>(wg, red);
-        if (threadIdx.x == 0) atomicAdd(dscale, wg);
-    }
-    if (dbias) {
         bs = block_sum<float, 256>(bs, red + 4);
-        if (threadIdx.x == 0) atomicAdd(dbias, bs);
+        grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }
 
@@ -701,7 +694,7 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     if (!workspace || ws_bytes < size_t(nbx) * a.ne * 4) return fail("conv3d_bwd_weight: workspace too small");
     auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     a.vec = al(x) && al(g) && (!x2 || al(x2));
-    const WgOut out{w, escale, dw, dscale, dbias, dcbias};
+    WgOut out{w, escale, dw, dscale, dbias, dcbias, GridSum{}};
     const dim3 grid{unsigned(nbx), unsigned(ytiles), 1u};
     WmArgs m;
     int mpw, ntt, mbx;
@@ -714,8 +707,12 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     }
     // few workgroups: each adds its partial straight into the gradients (no reduce launch; the
     // matrix-core kernel's partials are whole co x ci images, so only a single workgroup goes direct)
-    const bool direct = mma ? nbx == 1 : nbx <= 16;
+    // one workgroup column (nbx == 1) adds its entries straight into the gradients (each entry has
+    // one adder, so the sums stay deterministic); the scalar sums over the column's y tiles go
+    // through the fixed-order in-grid sum
+    const bool direct = nbx == 1;
     float *part = direct ? nullptr : static_cast<float *>(workspace);
+    if (direct && !mma && !(reg_path(d) && a.vec)) out.gsum = grid_sum_for(s, ytiles, dscale || dbias);
     if (mma) {
 #define WM(M_, N_)                                                                                              \
     else if (mpw == M_ && ntt == N_) k_pw_wgrad_mma<M_, N_><<<nbx, 256, mlds, s>>>(                            \
@@ -752,15 +749,18 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     if (direct) return check_launch("conv3d_bwd_weight(pointwise)");
     const int Ct = a.Ca + a.Cb;
     if (mma && m.tr) {
-        k_pw_wgrad_reduce_t<<<(a.ne + 63) / 64, 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw, dscale, dbias, dcbias);
+        const unsigned nr = unsigned((a.ne + 63) / 64);
+        k_pw_wgrad_reduce_t<<<nr, 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw, dscale, dbias, dcbias,
+                                               grid_sum_for(s, nr, dscale || dbias));
         return check_launch("conv3d_bwd_weight(pointwise)");
     }
     int lanes = 1;
     while (lanes < 64 && lanes * 8 < nbx) lanes *= 2;
     if (lanes == 64 && nbx > 512) lanes = 256;  // a workgroup per entry: one round of loads per thread
 #define RED(L)                                                                                                 \
-    k_pw_wgrad_reduce<L><<<(a.ne + 256 / L - 1) / (256 / L), 256, 0, s>>>(part, nbx, a.ne, Ct, w, escale, dw,    \
-                                                                          dscale, dbias, dcbias)
+    k_pw_wgrad_reduce<L><<<(a.ne + 256 / L - 1) / (256 / L), 256, 0, s>>>(                                       \
+        part, nbx, a.ne, Ct, w, escale, dw, dscale, dbias, dcbias,                                               \
+        grid_sum_for(s, (a.ne + 256 / L - 1) / (256 / L), dscale || dbias))
     switch (lanes) {
     case 1: RED(1); break;
     case 2: RED(2); break;

@@ -134,7 +134,7 @@ __device__ __forceinline__ void adj4(int i, int n, int (&j)[4], float (&wt)[4]) 
 template <typename T, int CV>
 __global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ gy, int dmode, const float *dparam,
                                                 const T *__restrict__ aux, const T *__restrict__ addend,
-                                                T *__restrict__ gx, float *dpre, float *dpost) {
+                                                T *__restrict__ gx, float *dpre, float *dpost, GridSum gsum) {
     __shared__ float red[8];
     ActDeriv dv;
     dv.mode = aux ? dmode : 0;
@@ -186,10 +186,7 @@ __global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ 
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
-        }
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -201,7 +198,7 @@ __global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ 
 __global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const h16_t *__restrict__ gy, int dmode,
                                                      const float *dparam, const h16_t *__restrict__ aux,
                                                      const h16_t *__restrict__ addend, h16_t *__restrict__ gx,
-                                                     float *dpre, float *dpost) {
+                                                     float *dpre, float *dpost, GridSum gsum) {
     __shared__ float red[8];
     ActDeriv dv;
     dv.mode = aux ? dmode : 0;
@@ -288,10 +285,135 @@ __global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const h16_t *__re
     if (dpre || dpost) {
         pre = block_sum<float, 256>(pre, red);
         post = block_sum<float, 256>(post, red + 4);
-        if (threadIdx.x == 0) {
-            if (dpre) atomicAdd(dpre, pre);
-            if (dpost) atomicAdd(dpost, post);
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
+    }
+}
+
+// The same adjoint with a thread owning 2 x 2 source lines (h, h + 1) x (w, w + 1) of 4 voxels along D
+// (even H and W): the four lines' destination rows are the 6 x 6 (h, w) rows 2 h - 1 .. 2 h + 4 x
+// 2 w - 1 .. 2 w + 4, each 96-byte D window loaded and reduced along D ONCE for all four lines
+// (216 16-byte loads for 16 source voxels instead of 384).  Each line accumulates its 4 x 4 rows
+// in run4's order (h row outer, w row inner; weight-0 clamped rows included), so the same bits.
+__global__ __launch_bounds__(256) void k_up2_bwd_quad(UArgs a, const h16_t *__restrict__ gy, int dmode,
+                                                     const float *dparam, const h16_t *__restrict__ aux,
+                                                     const h16_t *__restrict__ addend, h16_t *__restrict__ gx,
+                                                     float *dpre, float *dpost, GridSum gsum) {
+    __shared__ float red[8];
+    ActDeriv dv;
+    dv.mode = aux ? dmode : 0;
+    dv.p = (dv.mode && dparam) ? *dparam : 0.f;
+    float pre = 0.f, post = 0.f;
+    const int DQ = a.D / 4, HQ = a.H / 2, WQ = a.W / 2;
+    const uint32_t n = uint32_t(a.B) * HQ * WQ * DQ;
+    const int D2 = 2 * a.D, W2 = 2 * a.W, H2 = 2 * a.H;
+    for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < n; e += gridDim.x * 256u) {
+        int ch, q, iwq, ihq, b;
+        split(a, e, DQ, WQ, HQ, ch, q, iwq, ihq, b);
+        const int i0 = 4 * q, ih0 = 2 * ihq, iw0 = 2 * iwq;
+        int jh[2][4], jw[2][4], jd[4];
+        float wh[2][4], ww[2][4], wd[4][4];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            adj4(ih0 + r, a.H, jh[r], wh[r]);
+            adj4(iw0 + r, a.W, jw[r], ww[r]);
         }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) adj4(i0 + s4, a.D, jd, wd[s4]);
+        // the 6 destination rows per axis: slot x of line r is row index x + 2 r (adj4's clamped rows)
+        int rowh[6], roww[6];
+#pragma unroll
+        for (int x = 0; x < 6; ++x) {
+            rowh[x] = x < 4 ? jh[0][x] : jh[1][x - 2];
+            roww[x] = x < 4 ? jw[0][x] : jw[1][x - 2];
+        }
+        float acc[2][2][4][4];
+#pragma unroll
+        for (int rh = 0; rh < 2; ++rh)
+#pragma unroll
+            for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[rh][rw][s4][c] = 0.f;
+#pragma unroll 1
+        for (int xh = 0; xh < 6; ++xh)
+#pragma unroll 2
+            for (int xw = 0; xw < 6; ++xw) {
+                const int64_t rowb = ((int64_t(b) * H2 + rowh[xh]) * W2 + roww[xw]) * D2;
+                float r[12][4];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const int j = 2 * i0 - 2 + 2 * k;
+                    u32x4 u = u32x4{0u, 0u, 0u, 0u};
+                    if (j >= 0 && j < D2) u = *reinterpret_cast<const u32x4 *>(gy + (rowb + j) * 4);
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2) {
+                        r[2 * k + h2][0] = h2f_lo(u[2 * h2]);
+                        r[2 * k + h2][1] = h2f_hi(u[2 * h2]);
+                        r[2 * k + h2][2] = h2f_lo(u[2 * h2 + 1]);
+                        r[2 * k + h2][3] = h2f_hi(u[2 * h2 + 1]);
+                    }
+                }
+                float sd[4][4];
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const float *w4 = wd[s4];
+                        sd[s4][c] = w4[0] * r[2 * s4 + 1][c] + w4[1] * r[2 * s4 + 2][c] + w4[2] * r[2 * s4 + 3][c] +
+                                    w4[3] * r[2 * s4 + 4][c];
+                    }
+#pragma unroll
+                for (int rh = 0; rh < 2; ++rh) {
+                    const int x0 = xh - 2 * rh;
+                    if (x0 < 0 || x0 > 3) continue;
+#pragma unroll
+                    for (int rw = 0; rw < 2; ++rw) {
+                        const int x1 = xw - 2 * rw;
+                        if (x1 < 0 || x1 > 3) continue;
+                        const float whw = wh[rh][x0] * ww[rw][x1];
+#pragma unroll
+                        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) acc[rh][rw][s4][c] = fmaf(whw, sd[s4][c], acc[rh][rw][s4][c]);
+                    }
+                }
+            }
+#pragma unroll
+        for (int rh = 0; rh < 2; ++rh)
+#pragma unroll
+            for (int rw = 0; rw < 2; ++rw) {
+                const int64_t o = (((int64_t(b) * a.H + ih0 + rh) * a.W + iw0 + rw) * a.D + i0) * 4;
+                u32x4 xa[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}}, ad[2] = {xa[0], xa[1]};
+                if (dv.mode) xa[0] = *reinterpret_cast<const u32x4 *>(aux + o), xa[1] = *reinterpret_cast<const u32x4 *>(aux + o + 8);
+                if (addend) ad[0] = *reinterpret_cast<const u32x4 *>(addend + o), ad[1] = *reinterpret_cast<const u32x4 *>(addend + o + 8);
+                u32x4 res[2];
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    float v2[4];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const uint32_t wx = xa[s4 >> 1][2 * (s4 & 1) + (c >> 1)], wa = ad[s4 >> 1][2 * (s4 & 1) + (c >> 1)];
+                        const float xv = ((c & 1) ? h2f_hi(wx) : h2f_lo(wx));
+                        const float av = ((c & 1) ? h2f_hi(wa) : h2f_lo(wa));
+                        float v = acc[rh][rw][s4][c];
+                        pre += v;
+                        if (dv.mode) v *= dv(xv);
+                        post += v;
+                        if (addend) v += av;
+                        v2[c] = v;
+                    }
+                    res[s4 >> 1][2 * (s4 & 1)] = uint32_t(f2h(v2[0])) | (uint32_t(f2h(v2[1])) << 16);
+                    res[s4 >> 1][2 * (s4 & 1) + 1] = uint32_t(f2h(v2[2])) | (uint32_t(f2h(v2[3])) << 16);
+                }
+                *reinterpret_cast<u32x4 *>(gx + o) = res[0];
+                *reinterpret_cast<u32x4 *>(gx + o + 8) = res[1];
+            }
+    }
+    if (dpre || dpost) {
+        pre = block_sum<float, 256>(pre, red);
+        post = block_sum<float, 256>(post, red + 4);
+        grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
 
@@ -475,22 +597,40 @@ int launch_up2_bwd(int32_t dtype, int32_t batch, int32_t channels, int32_t h, in
     if (int64_t(batch) * 8 * h * w * dd * channels >= (int64_t(1) << 31)) return fail("upsample2x: tensor too large");
     const int cv = pick_cv(dtype, channels, gy, gx, aux, add);
     auto al16 = [](const void *p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    if (dtype == VQ3D_HALF && channels == 4 && dd % 4 == 0 && al16(gy) && al16(gx) && al16(aux) && al16(add)) {
+    // the run forms give a thread 4 (run4) or 16 (quad) source voxels: only grids that still fill the
+    // chip take them (a 2-workgroup quad grid ran 49 us where the per-voxel kernel needs ~10)
+    const int64_t nsrc = int64_t(batch) * h * w * dd;
+    if (dtype == VQ3D_HALF && channels == 4 && dd % 4 == 0 && h % 2 == 0 && w % 2 == 0 && nsrc >= (int64_t(1) << 22) &&
+        al16(gy) && al16(gx) && al16(aux) && al16(add)) {
+        UArgs a = make_args(batch, channels, h, w, dd, 4, false);
+        a.f1 = FastDiv(uint32_t(dd / 4));
+        a.f2 = FastDiv(uint32_t(w / 2));
+        a.f3 = FastDiv(uint32_t(h / 2));
+        const int64_t n = int64_t(batch) * (h / 2) * (w / 2) * (dd / 4);
+        const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)));
+        k_up2_bwd_quad<<<nb, 256, 0, s>>>(a, (const h16_t *)gy, dmode, dparam, (const h16_t *)aux,
+                                          (const h16_t *)add, (h16_t *)gx, dpre, dpost,
+                                          grid_sum_for(s, nb, dpre || dpost));
+        return check_launch("upsample2x_bwd(quad)");
+    }
+    if (dtype == VQ3D_HALF && channels == 4 && dd % 4 == 0 && nsrc >= (int64_t(1) << 20) && al16(gy) && al16(gx) &&
+        al16(aux) && al16(add)) {
         UArgs a = make_args(batch, channels, h, w, dd, 4, false);
         a.f1 = FastDiv(uint32_t(dd / 4));
         const int64_t n = int64_t(batch) * h * w * (dd / 4);
         const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)));
         k_up2_bwd_run4<<<nb, 256, 0, s>>>(a, (const h16_t *)gy, dmode, dparam, (const h16_t *)aux,
-                                          (const h16_t *)add, (h16_t *)gx, dpre, dpost);
+                                          (const h16_t *)add, (h16_t *)gx, dpre, dpost,
+                                          grid_sum_for(s, nb, dpre || dpost));
         return check_launch("upsample2x_bwd(run4)");
     }
     const UArgs a = make_args(batch, channels, h, w, dd, cv, false);
     const int64_t n = int64_t(batch) * h * w * dd * a.nchunk;
-    // grid-stride; bounded so the per-workgroup partial-sum atomics stay few
+    // grid-stride, <= 1,024 workgroups
     const unsigned nb = unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024)));
 #define UB(T, CV)                                                                                             \
     k_up2_bwd<T, CV><<<nb, 256, 0, s>>>(a, (const T *)gy, dmode, dparam, (const T *)aux, (const T *)add, (T *)gx, \
-                                        dpre, dpost)
+                                        dpre, dpost, grid_sum_for(s, nb, dpre || dpost))
     if (dtype == VQ3D_F32) UB(float, 1);
     else if (cv == 8) UB(h16_t, 8);
     else if (cv == 4) UB(h16_t, 4);

@@ -1,5 +1,6 @@
 """GPU: the trilinear x2 upsample (ResizeConv3D, vqvae/layers.py:591-597) and its adjoint in bf16
-(the LDS-tiled forward for 9 channels, the per-voxel kernels otherwise) against the per-voxel fp32
+(the LDS-tiled forward for 9 channels, the 4-channel adjoint's run forms, the per-voxel kernels
+otherwise) against the per-voxel fp32
 kernels on the same bf16-representable inputs.  All compute every value with the same fp32
 operations in the same order (no FP contraction in upsample.hip; the tiled kernel reads a halo of
 clamped copies with the per-voxel kernel's weights), so the bf16 results must equal the fp32
@@ -13,7 +14,10 @@ pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last_3d
 SHAPES = [(1, 4, 8, 16, 32), (2, 8, 8, 8, 16), (1, 9, 4, 8, 16), (2, 9, 8, 16, 32), (1, 9, 6, 8, 16),
-          (1, 16, 4, 4, 16), (1, 4, 64, 64, 32)]
+          (1, 16, 4, 4, 16), (1, 4, 64, 64, 32), (1, 4, 4, 4, 4), (2, 4, 6, 2, 8),
+          # grids large enough for the run forms of the 4-channel adjoint (upsample.hip
+          # launch_up2_bwd): 2 x 2 source lines (even H, W; >= 4M source voxels), runs of 4 along D
+          (1, 4, 256, 256, 64), (1, 4, 130, 128, 64)]
 
 
 def rnd(shape, dev, g, scale=1.0):
