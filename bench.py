@@ -69,6 +69,8 @@ def parse():
                         "loss scaling) or fp32")
     p.add_argument("--size", type=int, nargs=3, default=None, help="override the volume H W D")
     p.add_argument("--encode-only", action="store_true", help="eval encode + codebook search (configs[3])")
+    p.add_argument("--encode-batch", type=int, default=1,
+                   help="--encode-only: volumes per encode call (codes are per volume whatever the batch)")
     p.add_argument("--prior", action="store_true",
                    help="PixelSNAIL mid-level prior training step (configs[4]) instead of the VQ-VAE step")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -779,7 +781,7 @@ def main():
         from vq3d import functional as Fn
         Fn.set_binding(a.binding)
     if a.encode_only:
-        batch = 1
+        batch = a.encode_batch
     # this rank's synthetic volumes, resident in HBM before timing
     idx = parallel.shard_indices(0, rank, world, batch)
     x = torch.cat([synthetic_volume((1, 1) + size, i) for i in idx]).to(dev)

@@ -179,3 +179,21 @@ def test_cfg2_train_step_and_codes_bitexact(gpu):
         assert np.array_equal(ix.reshape(-1).cpu().numpy(), ref_idx), lvl
         ref_loss = q.commitment_cost * sq / z.size
         assert abs(float(c) - ref_loss) <= 1e-4 * abs(ref_loss) + 1e-12, (lvl, float(c), ref_loss)
+
+
+def test_batched_encode_codes_equal_per_volume(gpu):
+    """bench.py --encode-batch B: B volumes in one eval encode give every volume exactly the codes
+    it gets alone (no op mixes volumes; the fused engines index the batch dimension)."""
+    from vq3d.extract import extract_samples
+    from vq3d.utils import synthetic_volume
+    m = _model(gpu)
+    m.eval()
+    for q in m.encoder.quantize:
+        q.first_pass.zero_()
+        q.first_pass_host = False
+    vols = [synthetic_volume((1, 1, 256, 256, 64), i).to(gpu) for i in range(3)]
+    alone = [next(extract_samples(m, [v])) for v in vols]
+    together = next(extract_samples(m, [torch.cat(vols)]))
+    for lvl in range(3):
+        for b in range(3):
+            assert torch.equal(together[lvl][b], alone[b][lvl][0]), (lvl, b)
