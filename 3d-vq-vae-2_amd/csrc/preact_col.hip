@@ -40,6 +40,12 @@
 #include <cstdlib>
 #include <type_traits>
 
+#ifndef COL_UNROLL_F
+#define COL_UNROLL_F 2  // m-tiles per unrolled step of the forward's phase B
+#endif
+#ifndef COL_UNROLL_B
+#define COL_UNROLL_B 2  // ... and of the backward's phase B1
+#endif
 #ifndef FWD_PERSIST
 #define FWD_PERSIST 1  // the forward walks brick ranges too (its grid: CArgs::nwg)
 #endif
@@ -345,9 +351,11 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
         const int ln = tid / (BD / DV), dg = tid % (BD / DV);
         const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
         const Raw<TX, DV * C> xr = ldraw<TX, DV * C>(x + vox0 * C);
-        // B. raw W2 (*) t2 per m-tile
-#pragma unroll 4
-        for (int mt = wave; mt < NMT; mt += NT / 64) {
+        // B. raw W2 (*) t2 per m-tile (a fixed trip count, unrolled: the next m-tiles' window reads
+        // are in flight during this one's MFMA chain)
+#pragma unroll COL_UNROLL_F
+        for (int i = 0; i < NMT / (NT / 64); ++i) {
+            const int mt = wave + i * (NT / 64);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             const int wb = win_base(mt, BR);
 #pragma unroll
@@ -533,9 +541,10 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         const int ln = tid / (BD / DV), dg = tid % (BD / DV);
         const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
         constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
-        // B1. raw W2^T (*) gz3 per m-tile (flipped taps)
-#pragma unroll 2
-        for (int mt = wave; mt < NMT; mt += NT / 64) {
+        // B1. raw W2^T (*) gz3 per m-tile (flipped taps; fixed trip count, unrolled as the forward's)
+#pragma unroll COL_UNROLL_B
+        for (int i = 0; i < NMT / (NT / 64); ++i) {
+            const int mt = wave + i * (NT / 64);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             const int wb = win_base(mt, BR);
 #pragma unroll
