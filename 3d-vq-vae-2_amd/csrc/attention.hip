@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 namespace vq3d {
 
@@ -147,21 +148,21 @@ __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict
     }
     float m = -INFINITY, l = 0.f;
     const uint64_t seed = a.drop_below ? *a.seed : 0;
-    for (int kt = 0; kt <= qt; ++kt) {
-        __syncthreads();
-        stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
-        stage<T, DM>(vs, v, a, p, h, a.dv, kt * QR, QR);
-        __syncthreads();
-        const int jlim = kt < qt ? QR : r + 1;  // local keys j <= i
+    // one staged key tile; FULL: every key of it precedes the wave's queries (no per-key masks --
+    // all tiles but the diagonal one)
+    auto tile = [&](auto fullc, int kt) {
+        constexpr bool FULL = decltype(fullc)::value;
+        const int jlim = FULL ? QR : r + 1;  // local keys j <= i
 #pragma unroll
         for (int c0 = 0; c0 < SUB; c0 += CH) {
             const int j0 = w * SUB + c0;
-            if (j0 >= jlim) break;
+            if (!FULL && j0 >= jlim) break;
             float s[CH], cm = m;
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
-                s[u] = j0 + u < jlim ? dot<DM>(qr, ks + (j0 + u) * DM) : -INFINITY;
-                if (a.train && j0 + u < jlim) {
+                const bool in = FULL || j0 + u < jlim;
+                s[u] = in ? dot<DM>(qr, ks + (j0 + u) * DM) : -INFINITY;
+                if (a.train && in) {
                     bool live;
                     s[u] = train_logit(a, seed, int(blockIdx.y), i, kt * QR + j0 + u, s[u], live);
                 }
@@ -179,6 +180,14 @@ __global__ __launch_bounds__(NT) void k_attn_fwd(AttnArgs a, const T *__restrict
             }
             m = cm;
         }
+    };
+    for (int kt = 0; kt <= qt; ++kt) {
+        __syncthreads();
+        stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
+        stage<T, DM>(vs, v, a, p, h, a.dv, kt * QR, QR);
+        __syncthreads();
+        if (kt < qt) tile(std::true_type{}, kt);
+        else tile(std::false_type{}, kt);
     }
     // merge the 4 waves' partial softmaxes (a wave that met no key has m = -inf, l = 0)
     pm[w][r] = m;
@@ -245,22 +254,27 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_q(AttnArgs a, float scale, cons
         stage<T, DM>(ks, k, a, p, h, a.dk, kt * QR, 0);
         stage<T, DM>(vs, v, a, p, h, a.dv, kt * QR, QR);
         __syncthreads();
-        const int jlim = kt < qt ? QR : r + 1;
+        auto tile = [&](auto fullc) {  // FULL: no per-key causal mask (every tile but the diagonal)
+            constexpr bool FULL = decltype(fullc)::value;
+            const int jlim = FULL ? QR : r + 1;
 #pragma unroll 4
-        for (int u = 0; u < SUB; ++u) {
-            const int j = w * SUB + u;
-            if (j < jlim) {
-                float sc = dot<DM>(qr, ks + j * DM), gf = 1.f;
-                if (a.train) {
-                    bool live;
-                    sc = train_logit(a, seed, int(blockIdx.y), i, kt * QR + j, sc, live);
-                    gf = live ? a.keep_scale : 0.f;
+            for (int u = 0; u < SUB; ++u) {
+                const int j = w * SUB + u;
+                if (FULL || j < jlim) {
+                    float sc = dot<DM>(qr, ks + j * DM), gf = 1.f;
+                    if (a.train) {
+                        bool live;
+                        sc = train_logit(a, seed, int(blockIdx.y), i, kt * QR + j, sc, live);
+                        gf = live ? a.keep_scale : 0.f;
+                    }
+                    const float pr = exp2f(sc - lz);
+                    const float ds = gf * pr * (dot<DM>(go, vs + j * DM) - dl);
+                    axpy<DM>(dq, ds, ks + j * DM);
                 }
-                const float pr = exp2f(sc - lz);
-                const float ds = gf * pr * (dot<DM>(go, vs + j * DM) - dl);
-                axpy<DM>(dq, ds, ks + j * DM);
             }
-        }
+        };
+        if (kt < qt) tile(std::true_type{});
+        else tile(std::false_type{});
     }
 #pragma unroll
     for (int c = 0; c < DM; ++c) pq[w][r][c] = dq[c];
@@ -311,22 +325,27 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
         __syncthreads();
         const int i0 = qt > kt ? 0 : r;  // local queries i >= j
         const int iend = min(QR, a.n - qt * QR);
+        auto tile = [&](auto fullc) {  // FULL: every query of the tile follows every key (no masks)
+            constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll 4
-        for (int u = 0; u < SUB; ++u) {
-            const int ii = w * SUB + u;
-            if (ii >= i0 && ii < iend) {
-                float sc = dot<DM>(kr, qs + ii * DM), gf = 1.f;
-                if (a.train) {
-                    bool live;
-                    sc = train_logit(a, seed, int(blockIdx.y), qt * QR + ii, j, sc, live);
-                    gf = live ? a.keep_scale : 0.f;
+            for (int u = 0; u < SUB; ++u) {
+                const int ii = w * SUB + u;
+                if (FULL || (ii >= i0 && ii < iend)) {
+                    float sc = dot<DM>(kr, qs + ii * DM), gf = 1.f;
+                    if (a.train) {
+                        bool live;
+                        sc = train_logit(a, seed, int(blockIdx.y), qt * QR + ii, j, sc, live);
+                        gf = live ? a.keep_scale : 0.f;
+                    }
+                    const float pr = exp2f(sc - ls[ii]);
+                    axpy<DM>(dv, pr, gs + ii * DM);
+                    const float ds = gf * pr * (dot<DM>(vr, gs + ii * DM) - dls[ii]);
+                    axpy<DM>(dk, ds, qs + ii * DM);
                 }
-                const float pr = exp2f(sc - ls[ii]);
-                axpy<DM>(dv, pr, gs + ii * DM);
-                const float ds = gf * pr * (dot<DM>(vr, gs + ii * DM) - dls[ii]);
-                axpy<DM>(dk, ds, qs + ii * DM);
             }
-        }
+        };
+        if (qt > kt && iend == QR) tile(std::true_type{});
+        else tile(std::false_type{});
     }
 #pragma unroll
     for (int c = 0; c < DM; ++c) {
