@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 namespace vq3d {
@@ -364,6 +365,133 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
     }
 }
 
+// ---------------------------------------------------------------------------- matrix-core forward
+// 16-bit builds, head dims dk = dv = 8 (the published prior: model-dim 256 / bottleneck 4 / 8 heads).
+// Workgroup = 128 queries of one (problem, head), a wave owns 32 of them; keys stream through LDS in
+// 128-key tiles.  Per 32-key block a wave forms S^T = K Q^T on the matrix cores
+// (v_mfma_f32_32x32x8, K = the 8 head dims): lane (column n = query, half h) holds the 16 keys
+// (r & 3) + 8 (r >> 2) + 4 h of its query's column in accumulator r, so the online softmax's max is
+// the lane's 16 values and its partner half's (one cross-half shuffle), and the probabilities are,
+// unmoved, the B operand of O^T += V^T P^T (v_mfma_f32_32x32x16_f16, K = 16 keys: element j of lane
+// half h <-> key (j & 3) + 8 (j >> 2) + 4 h; V^T is read in that key order).  O^T's rows are the 8
+// value dims (rows 8 .. 31 of the A operand are zero): lane (n, h) ends with dims 4h .. 4h + 3 of
+// query n.  Arithmetic: q . k products of the stored 16-bit values accumulated in fp32 and scaled in
+// fp32 (the VALU kernel scales q first), P and V as fp16 in the P V product (P in [0, 1]: 11-bit
+// mantissa) with fp32 accumulation, l summed in fp32.
+#ifndef ATTN_MQ
+#define ATTN_MQ 128
+#endif
+constexpr int MQ = ATTN_MQ, MK = 128, VTP = MK + 8, MNT = 2 * MQ;  // MNT: threads (a wave per 32 queries)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mma_qk(u32x2 kf, u32x2 qf, f32x16 acc) {
+#ifdef VQ3D_FP16
+    typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
+    return __builtin_amdgcn_mfma_f32_32x32x8f16(__builtin_bit_cast(f16x4v, kf), __builtin_bit_cast(f16x4v, qf), acc,
+                                                0, 0, 0);
+#else
+    typedef short s16x4v __attribute__((ext_vector_type(4)));
+    return __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(s16x4v, kf), __builtin_bit_cast(s16x4v, qf),
+                                                    acc, 0, 0, 0);
+#endif
+}
+
+__global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *__restrict__ q,
+                                                      const h16_t *__restrict__ k, const h16_t *__restrict__ v,
+                                                      h16_t *__restrict__ out, float *__restrict__ lse) {
+    __shared__ __attribute__((aligned(16))) h16_t ks[MK * 8];    // [key][dim], the stored format
+    __shared__ __attribute__((aligned(16))) _Float16 vt[8 * VTP];  // [dim][key], fp16
+    const int nqt = (a.n + MQ - 1) / MQ, qt = nqt - 1 - int(blockIdx.x);
+    const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
+    const int tid = int(threadIdx.x), lane = tid & 63, w = tid >> 6, col = lane & 31, hh = lane >> 5;
+    const int qb = qt * (MQ / 32) + w;  // the wave's 32-query block
+    const int i = qb * 32 + col;        // the lane's query
+    const int rs = a.nh * 8;
+    const u32x2 qf = *reinterpret_cast<const u32x2 *>(q + (int64_t(p) * a.n + min(i, a.n - 1)) * rs + hd * 8 + 4 * hh);
+    f32x16 o = {};
+    float m = -INFINITY, l = 0.f;
+    const uint64_t seed = a.drop_below ? *a.seed : 0;
+    const float c2k = a.train ? a.c2 * a.keep_scale : a.c2;  // train_logit's two factors in one
+    const bool zrep = a.train != 0, drop = a.drop_below != 0;
+    const int nkt = (qt * MQ + MQ + MK - 1) / MK;  // key tiles up to the workgroup's last query
+    for (int kt = 0; kt < nkt; ++kt) {
+        __syncthreads();
+        for (int e = tid; e < 2 * MK; e += MNT) {  // K rows, then V rows (transposed to fp16 V^T)
+            const int t = e & (MK - 1), kc = min(kt * MK + t, a.n - 1);
+            const u32x4 row = *reinterpret_cast<const u32x4 *>((e < MK ? k : v) + (int64_t(p) * a.n + kc) * rs + hd * 8);
+            if (e < MK) {
+                *reinterpret_cast<u32x4 *>(ks + t * 8) = row;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    vt[(2 * c) * VTP + t] = _Float16(h2f_lo(row[c]));
+                    vt[(2 * c + 1) * VTP + t] = _Float16(h2f_hi(row[c]));
+                }
+            }
+        }
+        __syncthreads();
+        const int b0 = kt * (MK / 32), nb = min(MK / 32, qb - b0 + 1);
+        // one 32-key block; DIAG: the wave's own block (keys after the query masked).  The logit
+        // transform of the VALU kernel, branch-free: t = c2 * ks * s, a zero t -> the -1e3 logit
+        // (train mode), a dropped logit (hash below drop_below) -> the -1e3 logit
+        auto block = [&](auto diagc, int bb) {
+            constexpr bool DIAG = decltype(diagc)::value;
+            const int kb = b0 + bb;
+            f32x16 st = mma_qk(*reinterpret_cast<const u32x2 *>(ks + (bb * 32 + col) * 8 + 4 * hh), qf, f32x16{});
+            float bm = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;  // key within the block
+                float t = st[r] * c2k;
+                if (zrep) t = t != 0.f ? t : ZERO_LOGIT2;
+                if (drop && logit_hash(seed, int(blockIdx.y), i, kb * 32 + row) < a.drop_below) t = ZERO_LOGIT2;
+                if (DIAG) t = row > col ? -INFINITY : t;
+                st[r] = t;
+                bm = fmaxf(bm, t);
+            }
+            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+            const float mn = fmaxf(m, bm);  // finite: key 0 of the block precedes every query of it
+            const float alpha = exp2f(m - mn);
+            m = mn;
+            l *= alpha;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] *= alpha;  // rows 8 .. 31 of O^T stay zero
+            f16x8v pb0, pb1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pr = exp2f(st[r] - mn);
+                l += pr;
+                if (r < 8) pb0[r] = _Float16(pr);
+                else pb1[r - 8] = _Float16(pr);
+            }
+            u32x4 a0 = {0u, 0u, 0u, 0u}, a1 = {0u, 0u, 0u, 0u};  // V^T rows 8 .. 31: zero
+            if (col < 8) {
+                const _Float16 *vr = vt + col * VTP + bb * 32 + 4 * hh;  // 4 keys = one 8-byte read
+                const u32x2 r0 = *reinterpret_cast<const u32x2 *>(vr), r1 = *reinterpret_cast<const u32x2 *>(vr + 8);
+                const u32x2 r2 = *reinterpret_cast<const u32x2 *>(vr + 16), r3 = *reinterpret_cast<const u32x2 *>(vr + 24);
+                a0 = u32x4{r0[0], r0[1], r1[0], r1[1]};
+                a1 = u32x4{r2[0], r2[1], r3[0], r3[1]};
+            }
+            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, a0), pb0, o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, a1), pb1, o, 0, 0, 0);
+        };
+        for (int bb = 0; bb < nb; ++bb) {
+            if (b0 + bb < qb) block(std::false_type{}, bb);
+            else block(std::true_type{}, bb);
+        }
+    }
+    l += __shfl_xor(l, 32, 64);
+    if (i < a.n) {
+        const float inv = 1.f / l;
+        float ov[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[r] = o[r] * inv;
+        stvec<h16_t, 4>(out + (int64_t(p) * a.n + i) * rs + hd * 8 + 4 * hh, ov);
+        if (hh == 0) lse[(int64_t(p) * a.nh + hd) * a.n + i] = m + log2f(l);
+    }
+}
+
 int dmax_of(int dk, int dv) {
     const int d = std::max(dk, dv);
     return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 0;
@@ -372,6 +500,13 @@ int dmax_of(int dk, int dv) {
 template <typename T, int DM>
 void launch_fwd(const AttnArgs &a, const void *q, const void *k, const void *v, void *out, float *lse,
                 hipStream_t s) {
+    if constexpr (std::is_same<T, h16_t>::value && DM == 8) {
+        if (a.dk == 8 && a.dv == 8 && !std::getenv("VQ3D_ATTN_VALU")) {  // the matrix-core form (A/B switch)
+            const dim3 mg((a.n + MQ - 1) / MQ, a.P * a.nh);
+            k_attn_fwd_mma<<<mg, MNT, 0, s>>>(a, (const h16_t *)q, (const h16_t *)k, (const h16_t *)v, (h16_t *)out, lse);
+            return;
+        }
+    }
     const dim3 grid((a.n + QR - 1) / QR, a.P * a.nh);
     k_attn_fwd<T, DM><<<grid, NT, 0, s>>>(a, (const T *)q, (const T *)k, (const T *)v, (T *)out, lse);
 }

@@ -1,0 +1,9 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -m gpu -q -s --timeout 300 --timeout-method thread tests/test_gpu_pixelsnail.py > gpurun_out/y.log 2>&1; rc=$?
+grep -E "rel|passed|failed|^E " gpurun_out/y.log | head -30; echo "rc=$rc"
+[ $rc -le 1 ] || exit $rc
+for set in "VQ3D_ATTN_VALU=1" ""; do
+  env $set timeout -k 10 400 python3 bench.py --prior --no-cpu-baseline > gpurun_out/by.json 2> gpurun_out/by.err || { tail -5 gpurun_out/by.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(repr(sys.argv[2]), round(d['ms_per_step'],3), 'ms', 'fwd', round(d['attention_kernel']['fwd_ms'],4), 'bwd', round(d['attention_kernel']['bwd_ms'],4), 'loss', d['config']['final_loss'])" gpurun_out/by.json "$set"
+done
