@@ -492,6 +492,219 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
     }
 }
 
+// ---------------------------------------------------------------------------- matrix-core backward
+// The same tiling as k_attn_fwd_mma (32 rows per wave, 128-row tiles of the other side through LDS,
+// 16-bit builds, head dims 8).  Query side (dQ, and delta = dO . O to the workspace): lane (query n,
+// half h) holds the 16 keys (r & 3) + 8 (r >> 2) + 4 h of S^T = K Q^T and of dP^T = V dO^T (both
+// 32x32x8, the query's q / dO as the register-resident B operand), so lse_n and delta_n are the
+// lane's own; dS^T feeds dQ^T += K^T dS^T (32x32x16 f16, K^T read in the accumulator's key order).
+// Key side (dK, dV): lane (key n, half h) holds the 16 queries of S = Q K^T and dP = dO V^T, with
+// lse / delta of those queries from LDS (four 16-byte reads each); dV^T += dO^T P and dK^T += Q^T dS
+// (32x32x16 f16).  P and dS are rounded to fp16 for the products, accumulation fp32; the logit
+// transform (dropout, zero -> -1e3, its gradient factor) is the VALU kernels'.
+__device__ __forceinline__ f16x8v vt_frag(const _Float16 *base) {  // 4 + 4 keys in the accumulator's order
+    const u32x2 r0 = *reinterpret_cast<const u32x2 *>(base), r1 = *reinterpret_cast<const u32x2 *>(base + 8);
+    return __builtin_bit_cast(f16x8v, u32x4{r0[0], r0[1], r1[0], r1[1]});
+}
+
+// stage 128 rows of a [P][n][nh * 8] 16-bit tensor's head hd: native rows [row][8] (nat, may be
+// null) and / or fp16 transposed [dim][row] (tr, may be null)
+__device__ __forceinline__ void stage_rows(const h16_t *__restrict__ src, const AttnArgs &a, int p, int hd, int r0,
+                                           int t, h16_t *nat, _Float16 *tr) {
+    const int rc = min(r0 + t, a.n - 1);
+    const u32x4 row = *reinterpret_cast<const u32x4 *>(src + (int64_t(p) * a.n + rc) * (a.nh * 8) + hd * 8);
+    if (nat) *reinterpret_cast<u32x4 *>(nat + t * 8) = row;
+    if (tr) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            tr[(2 * c) * VTP + t] = _Float16(h2f_lo(row[c]));
+            tr[(2 * c + 1) * VTP + t] = _Float16(h2f_hi(row[c]));
+        }
+    }
+}
+
+// the logit transform + gradient factor of one score (raw q . k), as the VALU kernels apply it
+__device__ __forceinline__ float tlogit(const AttnArgs &a, float c2k, bool zrep, bool drop, uint64_t seed, int ph,
+                                        int i, int j, float raw, float &gf) {
+    float t = raw * c2k;
+    bool live = true;
+    if (zrep) live = t != 0.f;
+    if (drop && logit_hash(seed, ph, i, j) < a.drop_below) live = false;
+    gf = zrep ? (live ? a.keep_scale : 0.f) : 1.f;
+    return (zrep && !live) ? ZERO_LOGIT2 : t;
+}
+
+__global__ __launch_bounds__(MNT) void k_attn_bwd_q_mma(AttnArgs a, float scale, const h16_t *__restrict__ q,
+                                                        const h16_t *__restrict__ k, const h16_t *__restrict__ v,
+                                                        const h16_t *__restrict__ out, const h16_t *__restrict__ gout,
+                                                        const float *__restrict__ lse, float *__restrict__ delta,
+                                                        h16_t *__restrict__ gq) {
+    __shared__ __attribute__((aligned(16))) h16_t ks[MK * 8], vs[MK * 8];
+    __shared__ __attribute__((aligned(16))) _Float16 kt_[8 * VTP];
+    const int nqt = (a.n + MQ - 1) / MQ, qt = nqt - 1 - int(blockIdx.x);
+    const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
+    const int tid = int(threadIdx.x), lane = tid & 63, w = tid >> 6, col = lane & 31, hh = lane >> 5;
+    const int qb = qt * (MQ / 32) + w, i = qb * 32 + col, ic = min(i, a.n - 1);
+    const int rs = a.nh * 8;
+    const int64_t rowo = (int64_t(p) * a.n + ic) * rs + hd * 8 + 4 * hh;
+    const u32x2 qf = *reinterpret_cast<const u32x2 *>(q + rowo);
+    const u32x2 gf2 = *reinterpret_cast<const u32x2 *>(gout + rowo);
+    // delta_i = dO_i . O_i: the lane's 4 dims and its partner half's
+    float dl;
+    {
+        const u32x2 of = *reinterpret_cast<const u32x2 *>(out + rowo);
+        dl = h2f_lo(gf2[0]) * h2f_lo(of[0]);
+        dl = fmaf(h2f_hi(gf2[0]), h2f_hi(of[0]), dl);
+        dl = fmaf(h2f_lo(gf2[1]), h2f_lo(of[1]), dl);
+        dl = fmaf(h2f_hi(gf2[1]), h2f_hi(of[1]), dl);
+        dl += __shfl_xor(dl, 32, 64);
+    }
+    const int64_t lrow = (int64_t(p) * a.nh + hd) * a.n + ic;
+    const float lz = lse[lrow];
+    if (i < a.n && hh == 0) delta[lrow] = dl;
+    const uint64_t seed = a.drop_below ? *a.seed : 0;
+    const float c2k = a.train ? a.c2 * a.keep_scale : a.c2;
+    const bool zrep = a.train != 0, drop = a.drop_below != 0;
+    f32x16 dq = {};
+    const int nkt = (qt * MQ + MQ + MK - 1) / MK;
+    for (int kt = 0; kt < nkt; ++kt) {
+        __syncthreads();
+        for (int e = tid; e < 2 * MK; e += MNT) {
+            const int t = e & (MK - 1);
+            if (e < MK) stage_rows(k, a, p, hd, kt * MK, t, ks, kt_);
+            else stage_rows(v, a, p, hd, kt * MK, t, vs, nullptr);
+        }
+        __syncthreads();
+        const int b0 = kt * (MK / 32), nb = min(MK / 32, qb - b0 + 1);
+        auto block = [&](auto diagc, int bb) {
+            constexpr bool DIAG = decltype(diagc)::value;
+            const int kb = b0 + bb;
+            const f32x16 st = mma_qk(*reinterpret_cast<const u32x2 *>(ks + (bb * 32 + col) * 8 + 4 * hh), qf, f32x16{});
+            const f32x16 dp = mma_qk(*reinterpret_cast<const u32x2 *>(vs + (bb * 32 + col) * 8 + 4 * hh), gf2, f32x16{});
+            f16x8v d0, d1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+                float g;
+                const float t = tlogit(a, c2k, zrep, drop, seed, int(blockIdx.y), i, kb * 32 + row, st[r], g);
+                float pr = exp2f(t - lz);
+                if (DIAG) pr = row > col ? 0.f : pr;
+                const _Float16 ds = _Float16(g * pr * (dp[r] - dl));
+                if (r < 8) d0[r] = ds;
+                else d1[r - 8] = ds;
+            }
+            const _Float16 *kr = col < 8 ? kt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
+            const f16x8v a0 = kr ? vt_frag(kr) : f16x8v{}, a1 = kr ? vt_frag(kr + 16) : f16x8v{};
+            dq = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, d0, dq, 0, 0, 0);
+            dq = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, d1, dq, 0, 0, 0);
+        };
+        for (int bb = 0; bb < nb; ++bb) {
+            if (b0 + bb < qb) block(std::false_type{}, bb);
+            else block(std::true_type{}, bb);
+        }
+    }
+    if (i < a.n) {
+        float ov[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[r] = scale * dq[r];
+        stvec<h16_t, 4>(gq + rowo, ov);
+    }
+}
+
+__global__ __launch_bounds__(MNT) void k_attn_bwd_kv_mma(AttnArgs a, float scale, const h16_t *__restrict__ q,
+                                                         const h16_t *__restrict__ k, const h16_t *__restrict__ v,
+                                                         const h16_t *__restrict__ gout,
+                                                         const float *__restrict__ lse,
+                                                         const float *__restrict__ delta, h16_t *__restrict__ gk,
+                                                         h16_t *__restrict__ gv) {
+    __shared__ __attribute__((aligned(16))) h16_t qs[MK * 8], gs[MK * 8];
+    __shared__ __attribute__((aligned(16))) _Float16 qt_[8 * VTP], gt_[8 * VTP];
+    __shared__ __attribute__((aligned(16))) float ls[MK], dls[MK];
+    const int nt = (a.n + MQ - 1) / MQ, ktile = int(blockIdx.x);  // key tile 0 meets every query tile: first
+    const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
+    const int tid = int(threadIdx.x), lane = tid & 63, w = tid >> 6, col = lane & 31, hh = lane >> 5;
+    const int kbw = ktile * (MQ / 32) + w, j = kbw * 32 + col, jc = min(j, a.n - 1);
+    const int rs = a.nh * 8;
+    const int64_t rowk = (int64_t(p) * a.n + jc) * rs + hd * 8 + 4 * hh;
+    const u32x2 kf = *reinterpret_cast<const u32x2 *>(k + rowk);
+    const u32x2 vf = *reinterpret_cast<const u32x2 *>(v + rowk);
+    const int64_t rb = (int64_t(p) * a.nh + hd) * a.n;
+    const uint64_t seed = a.drop_below ? *a.seed : 0;
+    const float c2k = a.train ? a.c2 * a.keep_scale : a.c2;
+    const bool zrep = a.train != 0, drop = a.drop_below != 0;
+    f32x16 dk = {}, dv = {};
+    // query tiles from the workgroup's first key to the end (MK-row tiles)
+    for (int qtile = (ktile * MQ) / MK; qtile * MK < a.n; ++qtile) {
+        __syncthreads();
+        for (int e = tid; e < 2 * MK; e += MNT) {
+            const int t = e & (MK - 1);
+            if (e < MK) {
+                stage_rows(q, a, p, hd, qtile * MK, t, qs, qt_);
+                const int r = qtile * MK + t;
+                ls[t] = r < a.n ? lse[rb + r] : INFINITY;  // past the end: p = 0
+                dls[t] = r < a.n ? delta[rb + r] : 0.f;
+            } else {
+                stage_rows(gout, a, p, hd, qtile * MK, t, gs, gt_);
+            }
+        }
+        __syncthreads();
+        const int b0 = qtile * (MK / 32);
+        auto block = [&](auto diagc, int bb) {
+            constexpr bool DIAG = decltype(diagc)::value;
+            const int ib = b0 + bb;
+            const f32x16 st = mma_qk(*reinterpret_cast<const u32x2 *>(qs + (bb * 32 + col) * 8 + 4 * hh), kf, f32x16{});
+            const f32x16 dp = mma_qk(*reinterpret_cast<const u32x2 *>(gs + (bb * 32 + col) * 8 + 4 * hh), vf, f32x16{});
+            f16x8v p0, p1, d0, d1;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int rb4 = bb * 32 + 8 * jj + 4 * hh;  // local rows (queries) of registers 4 jj .. 4 jj + 3
+                const float4 l4 = *reinterpret_cast<const float4 *>(ls + rb4);
+                const float4 d4 = *reinterpret_cast<const float4 *>(dls + rb4);
+                const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = 4 * jj + u, row = u + 8 * jj + 4 * hh;  // query within the block
+                    float g;
+                    const float t = tlogit(a, c2k, zrep, drop, seed, int(blockIdx.y), ib * 32 + row, j, st[r], g);
+                    float pr = exp2f(t - lv[u]);
+                    if (DIAG) pr = row < col ? 0.f : pr;
+                    const _Float16 ph = _Float16(pr), ds = _Float16(g * pr * (dp[r] - dv4[u]));
+                    if (r < 8) {
+                        p0[r] = ph;
+                        d0[r] = ds;
+                    } else {
+                        p1[r - 8] = ph;
+                        d1[r - 8] = ds;
+                    }
+                }
+            }
+            const _Float16 *gr = col < 8 ? gt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
+            const _Float16 *qr = col < 8 ? qt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
+            dv = __builtin_amdgcn_mfma_f32_32x32x16_f16(gr ? vt_frag(gr) : f16x8v{}, p0, dv, 0, 0, 0);
+            dv = __builtin_amdgcn_mfma_f32_32x32x16_f16(gr ? vt_frag(gr + 16) : f16x8v{}, p1, dv, 0, 0, 0);
+            dk = __builtin_amdgcn_mfma_f32_32x32x16_f16(qr ? vt_frag(qr) : f16x8v{}, d0, dk, 0, 0, 0);
+            dk = __builtin_amdgcn_mfma_f32_32x32x16_f16(qr ? vt_frag(qr + 16) : f16x8v{}, d1, dk, 0, 0, 0);
+        };
+        for (int bb = 0; bb < MK / 32; ++bb) {
+            const int ib = b0 + bb;
+            if (ib < kbw) continue;  // queries before this wave's keys
+            if (ib > kbw) block(std::false_type{}, bb);
+            else block(std::true_type{}, bb);
+        }
+    }
+    if (j < a.n) {
+        float ok[4], ov[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            ok[r] = scale * dk[r];
+            ov[r] = dv[r];
+        }
+        const int64_t ro = (int64_t(p) * a.n + j) * rs + hd * 8 + 4 * hh;
+        stvec<h16_t, 4>(gk + ro, ok);
+        stvec<h16_t, 4>(gv + ro, ov);
+    }
+}
+
 int dmax_of(int dk, int dv) {
     const int d = std::max(dk, dv);
     return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : 0;
@@ -514,6 +727,16 @@ void launch_fwd(const AttnArgs &a, const void *q, const void *k, const void *v, 
 template <typename T, int DM>
 void launch_bwd(const AttnArgs &a, float scale, const void *q, const void *k, const void *v, const void *out,
                 const void *gout, const float *lse, float *delta, void *gq, void *gk, void *gv, hipStream_t s) {
+    if constexpr (std::is_same<T, h16_t>::value && DM == 8) {
+        if (a.dk == 8 && a.dv == 8 && !std::getenv("VQ3D_ATTN_VALU")) {  // the matrix-core forms (A/B switch)
+            const dim3 mg((a.n + MQ - 1) / MQ, a.P * a.nh);
+            k_attn_bwd_q_mma<<<mg, MNT, 0, s>>>(a, scale, (const h16_t *)q, (const h16_t *)k, (const h16_t *)v,
+                                                (const h16_t *)out, (const h16_t *)gout, lse, delta, (h16_t *)gq);
+            k_attn_bwd_kv_mma<<<mg, MNT, 0, s>>>(a, scale, (const h16_t *)q, (const h16_t *)k, (const h16_t *)v,
+                                                 (const h16_t *)gout, lse, delta, (h16_t *)gk, (h16_t *)gv);
+            return;
+        }
+    }
     const dim3 grid((a.n + QR - 1) / QR, a.P * a.nh);
     k_attn_bwd_q<T, DM><<<grid, NT, 0, s>>>(a, scale, (const T *)q, (const T *)k, (const T *)v, (const T *)out,
                                             (const T *)gout, lse, delta, (T *)gq);

@@ -329,3 +329,25 @@ def test_prior_step_with_mixup_captures(gpu):
     graph.replay()
     torch.cuda.synchronize()
     assert np.isfinite(eager) and abs(float(static.detach()) - eager) <= 1e-6 * abs(eager), (eager, float(static))
+
+
+@pytest.mark.parametrize("dims,p", [((4, 8, 8), 0.3), ((3, 5, 7), 0.0), ((3, 5, 7), None), ((2, 16, 9), 0.5)])
+def test_attention_matrix_core_matches_valu(gpu, dims, p):
+    """The 16-bit builds' matrix-core attention (head dim 8: forward and both backward kernels)
+    against the fp32 VALU kernels (pinned by the oracle above) on the same bf16-representable
+    inputs: eval (p None), training without dropout (p 0: the zero-logit replacement) and with
+    dropout (the same device-seeded mask), odd position counts (partial 32- and 128-row tiles).
+    Output and gradients within 2e-2 / 4e-2 relative (fp16 P / dS operands, bf16 storage)."""
+    from vq3d import pixelsnail as PS
+    g = torch.Generator().manual_seed(11)
+    b, c, nh = 2, 16, 2
+    src = [torch.randn((b, c) + dims, generator=g).to(torch.bfloat16).float() for _ in range(4)]
+    st = torch.tensor([0x5EED_1234_ABCD], dtype=torch.int64, device=gpu)
+    res = []
+    for dt in (torch.float32, torch.bfloat16):
+        q, k, v = (t.to(gpu).to(dt).contiguous(memory_format=CL).requires_grad_(True) for t in src[:3])
+        y = PS.CausalAttentionFn.apply(q, k, v, nh, None if p is None else (p, st))
+        y.backward(src[3].to(gpu).to(dt).contiguous(memory_format=CL))
+        res.append([t.detach().float().cpu() for t in (y, q.grad, k.grad, v.grad)])
+    for i, (a32, a16) in enumerate(zip(*res)):
+        assert rel(a16, a32.numpy()) < (2e-2 if i == 0 else 4e-2), (i, rel(a16, a32.numpy()))
