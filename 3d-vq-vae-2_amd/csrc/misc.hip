@@ -421,6 +421,59 @@ __global__ __launch_bounds__(256) void k_scale(float *__restrict__ x, float a, i
     for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) x[i] *= a;
 }
 
+// PixelSNAIL glue: y = elu(x + a) + b; its backward with the a / b sums (fixed order, grid_sum2)
+template <typename TX, typename TY>
+__global__ __launch_bounds__(256) void k_preact_act_fwd(int64_t n, const TX *__restrict__ x, const float *a,
+                                                       const float *b, TY *__restrict__ y) {
+    const float av = *a, bv = *b;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+        st(y + i, elu(ld(x + i) + av) + bv);
+}
+template <typename TG, typename TX>
+__global__ __launch_bounds__(256) void k_preact_act_bwd(int64_t n, const TG *__restrict__ g, const TX *__restrict__ x,
+                                                       const float *a, TX *__restrict__ gx, float *da, float *db,
+                                                       GridSum gsum) {
+    __shared__ float red[8];
+    const float av = *a;
+    float sa = 0.f, sb = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        const float gv = ld(g + i), v = gv * elu_grad(ld(x + i) + av);
+        if (gx) st(gx + i, v);
+        sa += v;
+        sb += gv;
+    }
+    sa = block_sum<float, 256>(sa, red);
+    sb = block_sum<float, 256>(sb, red + 4);
+    grid_sum2<256>(gsum, sa, sb, da, db, red);
+}
+// out = o * scale + bias + s; backward go = g * scale, the scale / bias sums
+template <typename TO>
+__global__ __launch_bounds__(256) void k_scale_bias_res_fwd(int64_t n, const TO *__restrict__ o, const float *scale,
+                                                           const float *bias, const float *__restrict__ s,
+                                                           float *__restrict__ out) {
+    const float sc = *scale, bv = *bias;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+        out[i] = (ld(o + i) * sc + bv) + s[i];
+}
+template <typename TO>
+__global__ __launch_bounds__(256) void k_scale_bias_res_bwd(int64_t n, const float *__restrict__ g,
+                                                           const TO *__restrict__ o, const float *scale,
+                                                           TO *__restrict__ go, float *dscale, float *dbias,
+                                                           GridSum gsum) {
+    __shared__ float red[8];
+    const float sc = *scale;
+    float ss = 0.f, sb = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+        const float gv = g[i];
+        if (go) st(go + i, gv * sc);
+        ss = fmaf(gv, ld(o + i), ss);
+        sb += gv;
+    }
+    ss = block_sum<float, 256>(ss, red);
+    sb = block_sum<float, 256>(sb, red + 4);
+    grid_sum2<256>(gsum, ss, sb, dscale, dbias, red);
+}
+
 // every 16-B slot of this workgroup's LDS allocation := all ones (a NaN in bf16 and fp32)
 __global__ __launch_bounds__(256) void k_poison_lds(int nslots) {
     extern __shared__ __attribute__((aligned(16))) uint4 lds_slots[];
@@ -746,6 +799,72 @@ int vq3d_scale(float *x, float a, int64_t n, vq3d_stream_t stream) {
     if (!x) return fail("scale: null pointer");
     k_scale<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, a, n);
     return check_launch("scale");
+}
+
+static bool glue_dtype(int32_t d) { return d == VQ3D_F32 || d == VQ3D_HALF; }
+
+int vq3d_preact_act_fwd(int32_t x_dtype, int32_t y_dtype, int64_t n, const void *x, const float *a, const float *b,
+                        void *y, vq3d_stream_t stream) {
+    if (n <= 0) return 0;
+    if (!glue_dtype(x_dtype) || !glue_dtype(y_dtype)) return fail("preact_act_fwd: dtype");
+    if (!x || !a || !b || !y) return fail("preact_act_fwd: null pointer");
+    hipStream_t s = as_stream(stream);
+#define PAF(TX, TY) k_preact_act_fwd<TX, TY><<<grid_for(n), 256, 0, s>>>(n, (const TX *)x, a, b, (TY *)y)
+    if (x_dtype == VQ3D_F32) {
+        if (y_dtype == VQ3D_F32) PAF(float, float);
+        else PAF(float, h16_t);
+    } else {
+        if (y_dtype == VQ3D_F32) PAF(h16_t, float);
+        else PAF(h16_t, h16_t);
+    }
+#undef PAF
+    return check_launch("preact_act_fwd");
+}
+
+int vq3d_preact_act_bwd(int32_t g_dtype, int32_t x_dtype, int64_t n, const void *g, const void *x, const float *a,
+                        void *gx, float *da, float *db, vq3d_stream_t stream) {
+    if (n <= 0) return 0;
+    if (!glue_dtype(g_dtype) || !glue_dtype(x_dtype)) return fail("preact_act_bwd: dtype");
+    if (!g || !x || !a) return fail("preact_act_bwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    const unsigned nb = grid_for(n);
+    const GridSum gs = grid_sum_for(s, nb, da || db);
+#define PAB(TG, TX) k_preact_act_bwd<TG, TX><<<nb, 256, 0, s>>>(n, (const TG *)g, (const TX *)x, a, (TX *)gx, da, db, gs)
+    if (g_dtype == VQ3D_F32) {
+        if (x_dtype == VQ3D_F32) PAB(float, float);
+        else PAB(float, h16_t);
+    } else {
+        if (x_dtype == VQ3D_F32) PAB(h16_t, float);
+        else PAB(h16_t, h16_t);
+    }
+#undef PAB
+    return check_launch("preact_act_bwd");
+}
+
+int vq3d_scale_bias_res_fwd(int32_t o_dtype, int64_t n, const void *o, const float *scale, const float *bias,
+                            const float *s_, float *out, vq3d_stream_t stream) {
+    if (n <= 0) return 0;
+    if (!glue_dtype(o_dtype)) return fail("scale_bias_res_fwd: dtype");
+    if (!o || !scale || !bias || !s_ || !out) return fail("scale_bias_res_fwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    if (o_dtype == VQ3D_F32) k_scale_bias_res_fwd<float><<<grid_for(n), 256, 0, s>>>(n, (const float *)o, scale, bias, s_, out);
+    else k_scale_bias_res_fwd<h16_t><<<grid_for(n), 256, 0, s>>>(n, (const h16_t *)o, scale, bias, s_, out);
+    return check_launch("scale_bias_res_fwd");
+}
+
+int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const void *o, const float *scale, void *go,
+                            float *dscale, float *dbias, vq3d_stream_t stream) {
+    if (n <= 0) return 0;
+    if (!glue_dtype(o_dtype)) return fail("scale_bias_res_bwd: dtype");
+    if (!g || !o || !scale) return fail("scale_bias_res_bwd: null pointer");
+    hipStream_t s = as_stream(stream);
+    const unsigned nb = grid_for(n);
+    const GridSum gs = grid_sum_for(s, nb, dscale || dbias);
+    if (o_dtype == VQ3D_F32)
+        k_scale_bias_res_bwd<float><<<nb, 256, 0, s>>>(n, g, (const float *)o, scale, (float *)go, dscale, dbias, gs);
+    else
+        k_scale_bias_res_bwd<h16_t><<<nb, 256, 0, s>>>(n, g, (const h16_t *)o, scale, (h16_t *)go, dscale, dbias, gs);
+    return check_launch("scale_bias_res_bwd");
 }
 
 }  // extern "C"

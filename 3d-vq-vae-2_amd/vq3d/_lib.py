@@ -124,6 +124,10 @@ _SIGS = {
     "vq3d_copy": (c_int, [P, P, c_size, P]),
     "vq3d_poison_lds": (c_int, [P]),
     "vq3d_scale": (c_int, [P, c_float, c_i64, P]),
+    "vq3d_preact_act_fwd": (c_int, [c_int, c_int, c_i64, P, P, P, P, P]),
+    "vq3d_preact_act_bwd": (c_int, [c_int, c_int, c_i64, P, P, P, P, P, P, P]),
+    "vq3d_scale_bias_res_fwd": (c_int, [c_int, c_i64, P, P, P, P, P, P]),
+    "vq3d_scale_bias_res_bwd": (c_int, [c_int, c_i64, P, P, P, P, P, P, P]),
     "vq3d_causal_attn_supported": (c_int, [c_int] * 3),
     "vq3d_causal_attn_workspace_bytes": (c_size, [c_int] * 3),
     "vq3d_causal_attn_fwd": (c_int, [c_int] * 6 + [c_float] + [P] * 6),

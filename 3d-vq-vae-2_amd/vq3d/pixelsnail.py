@@ -58,6 +58,74 @@ def _operand(x):
     return cl(x if x.dtype == _compute[0] else x.to(_compute[0]))
 
 
+def _fused_glue():
+    """16-bit runs put the block glue on the libvq3d kernels below; fp32 runs (the exact-parity
+    path against the reference goldens) keep torch's elementwise ops"""
+    return _compute[0] != torch.float32
+
+
+class PreActFn(torch.autograd.Function):
+    """elu(x + a) + b straight into the conv operand format (layers.py:425-432 pre-activation +
+    the autocast of the conv input): one launch; backward one launch with the a / b gradient sums
+    added into the parameters' gradient buffers (fixed order)."""
+
+    @staticmethod
+    def forward(ctx, x, a, b):
+        x = cl(x)
+        y = torch.empty_like(x, dtype=_compute[0], memory_format=CL)
+        L.call("vq3d_preact_act_fwd", L.dtype_code(x), L.dtype_code(y), x.numel(), L.ptr(x), L.ptr(a), L.ptr(b),
+               L.ptr(y), L.stream())
+        ctx.save_for_backward(x)
+        ctx.prm = (a, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from .functional import grad_buf
+        (x,) = ctx.saved_tensors
+        a, b = ctx.prm
+        g = cl(g)
+        gx = torch.empty_like(x, memory_format=CL) if ctx.needs_input_grad[0] else None
+        L.call("vq3d_preact_act_bwd", L.dtype_code(g), L.dtype_code(x), x.numel(), L.ptr(g), L.ptr(x), L.ptr(a),
+               None if gx is None else L.ptr(gx), L.ptr(grad_buf(a)), L.ptr(grad_buf(b)), L.stream())
+        return gx, None, None
+
+
+class ScaleBiasResFn(torch.autograd.Function):
+    """out = o * scale + bias4 + skip (layers.py:463-465, fp32 as the 1-element fp32 parameters
+    promote): one launch; backward one launch (go = g * scale and the two sums), skip's gradient g."""
+
+    @staticmethod
+    def forward(ctx, o, scale, bias, s):
+        o, s = cl(o), cl(s)
+        if s.dtype != torch.float32:
+            s = s.float().contiguous(memory_format=CL)
+        out = torch.empty_like(o, dtype=torch.float32, memory_format=CL)
+        L.call("vq3d_scale_bias_res_fwd", L.dtype_code(o), o.numel(), L.ptr(o), L.ptr(scale), L.ptr(bias), L.ptr(s),
+               L.ptr(out), L.stream())
+        ctx.save_for_backward(o)
+        ctx.prm = (scale, bias)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .functional import grad_buf
+        (o,) = ctx.saved_tensors
+        scale, bias = ctx.prm
+        g = cl(g).float()
+        go = torch.empty_like(o, memory_format=CL) if ctx.needs_input_grad[0] else None
+        L.call("vq3d_scale_bias_res_bwd", L.dtype_code(o), o.numel(), L.ptr(g), L.ptr(o), L.ptr(scale),
+               None if go is None else L.ptr(go), L.ptr(grad_buf(scale)), L.ptr(grad_buf(bias)), L.stream())
+        return go, None, None, (g if ctx.needs_input_grad[3] else None)
+
+
+def _preact(x, pro):
+    """the conv operand of elu(x + a) + b"""
+    if _fused_glue():
+        return PreActFn.apply(x, pro[0], pro[1])
+    return _operand(F.elu(x + pro[0]) + pro[1])
+
+
 # ============================================================================================ conv
 class CausalConvFn(torch.autograd.Function):
     """y = conv(prologue(x), w) + cbias on the libvq3d engines; w is the (embedded) k^3 weight.
@@ -181,18 +249,14 @@ class CausalConv3dAdd(nn.Module):
         out = []
         for i, (x, w, b) in enumerate(zip(stack, ws, bs)):
             if k == 1:  # a plain GEMM over the voxels (hipBLASLt): pre-activation + shift as glue
-                if pro is not None:
-                    x = F.elu(x + pro[0]) + pro[1]
-                x = _operand(x)
+                x = _operand(x) if pro is None else _preact(x, pro)
                 if self.mask == "A":
                     x = _shift(x, i)
                 out.append(pointwise(x, w, b))
                 continue
             pa = pb = None
             if self.mask == "A":
-                if pro is not None:
-                    x = F.elu(x + pro[0]) + pro[1]
-                x = _shift(_operand(x), i)
+                x = _shift(_operand(x) if pro is None else _preact(x, pro), i)
             elif pro is not None:
                 pa, pb = pro
             out.append(CausalConvFn.apply(_operand(x), w, b, pa, pb, k))
@@ -280,6 +344,8 @@ class PreActFixupCausalResBlock(nn.Module):
         out = self.branch_conv3.run(out, pro=(self.bias3a, self.bias3b))
         skip = stack if self.skip_conv is None else self.skip_conv.run(stack)
         # out * scale + bias4 + skip: fp32 (the 1-element fp32 parameters promote, as in the reference)
+        if _fused_glue():
+            return [ScaleBiasResFn.apply(o, self.scale, self.bias4, s) for o, s in zip(out, skip)]
         return [cl(o * self.scale + self.bias4 + s) for o, s in zip(out, skip)]
 
     def forward(self, stack, aux=None, condition=None, condition_cache=None):

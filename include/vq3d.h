@@ -455,6 +455,21 @@ int vq3d_elu_bwd_from_output(int32_t dtype, const void *g, const void *y, void *
 /* x *= a over n fp32 values (gradient averaging after the all-reduce uses a = 1/world) */
 int vq3d_scale(float *x, float a, int64_t n, vq3d_stream_t stream);
 
+/* --- PixelSNAIL block glue (pixel_model/layers.py:425-465), the elementwise steps around the
+ * 1x1 causal convs, each one launch with its scalar-parameter gradient sums (fixed order) ---
+ * pre-activation of a conv input: y = elu(x + *a) + *b (x: x_dtype, y: y_dtype, n elements); its
+ * backward gx = g * elu'(x + a) (gx: x_dtype, may be NULL), *da += sum gx, *db += sum g */
+int vq3d_preact_act_fwd(int32_t x_dtype, int32_t y_dtype, int64_t n, const void *x, const float *a, const float *b,
+                        void *y, vq3d_stream_t stream);
+int vq3d_preact_act_bwd(int32_t g_dtype, int32_t x_dtype, int64_t n, const void *g, const void *x, const float *a,
+                        void *gx, float *da, float *db, vq3d_stream_t stream);
+/* the block's output out = o * *scale + *bias + s (o: o_dtype, s / out fp32); its backward
+ * go = g * scale (o_dtype), *dscale += sum g * o, *dbias += sum g (the skip's gradient is g) */
+int vq3d_scale_bias_res_fwd(int32_t o_dtype, int64_t n, const void *o, const float *scale, const float *bias,
+                            const float *s, float *out, vq3d_stream_t stream);
+int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const void *o, const float *scale, void *go,
+                            float *dscale, float *dbias, vq3d_stream_t stream);
+
 /* --- PixelSNAIL prior: dense causal attention (pixel_model/layers.py:613-647) ---
  * For each of nprob problems (stack x batch) and nh heads: out[i] = sum_{j <= i} softmax_j(scale *
  * q_i . k_j) v_j over n positions, without the n x n logits.  q, k: [nprob][n][nh * dk], v, out:

@@ -351,3 +351,40 @@ def test_attention_matrix_core_matches_valu(gpu, dims, p):
         res.append([t.detach().float().cpu() for t in (y, q.grad, k.grad, v.grad)])
     for i, (a32, a16) in enumerate(zip(*res)):
         assert rel(a16, a32.numpy()) < (2e-2 if i == 0 else 4e-2), (i, rel(a16, a32.numpy()))
+
+
+def test_block_glue_kernels_match_torch(gpu):
+    """The 16-bit runs' fused block glue (PreActFn: elu(x + a) + b into the conv operand;
+    ScaleBiasResFn: o * scale + bias4 + skip) against the torch ops they replace: outputs, input
+    gradients and the scalar-parameter gradients (accumulated into the parameters' .grad)."""
+    from vq3d import pixelsnail as PS
+    g = torch.Generator(device=gpu).manual_seed(5)
+    shp = (1, 64, 8, 8, 16)
+    x = torch.randn(shp, device=gpu, generator=g).contiguous(memory_format=CL)
+    o = torch.randn(shp, device=gpu, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    sk = torch.randn(shp, device=gpu, generator=g).contiguous(memory_format=CL)
+    gy = torch.randn(shp, device=gpu, generator=g).to(torch.bfloat16).contiguous(memory_format=CL)
+    gz = torch.randn(shp, device=gpu, generator=g).contiguous(memory_format=CL)
+    prev = PS._compute[0]
+    PS._compute[0] = torch.bfloat16
+    try:
+        res = []
+        for fused in (True, False):
+            a, b, sc, b4 = (torch.nn.Parameter(torch.tensor([v], device=gpu)) for v in (0.3, -0.2, 0.7, 0.1))
+            for p in (a, b, sc, b4):
+                p.grad = torch.zeros_like(p)
+            xa, oa, ska = (t.clone().requires_grad_(True) for t in (x, o, sk))
+            if fused:
+                y = PS.PreActFn.apply(xa, a, b)
+                z = PS.ScaleBiasResFn.apply(oa, sc, b4, ska)
+            else:
+                y = (torch.nn.functional.elu(xa + a) + b).to(torch.bfloat16)
+                z = oa * sc + b4 + ska
+            torch.autograd.backward([y, z], [gy, gz])
+            res.append([t.detach().float() for t in (y, z, xa.grad, oa.grad, ska.grad, a.grad, b.grad, sc.grad,
+                                                        b4.grad)])
+    finally:
+        PS._compute[0] = prev
+    for i, (f, t) in enumerate(zip(*res)):
+        tol = 1e-2 if i in (0, 3) else 1e-4  # bf16 outputs: one rounding apart at most
+        assert rel(f, t.cpu().numpy()) < tol, (i, rel(f, t.cpu().numpy()))
