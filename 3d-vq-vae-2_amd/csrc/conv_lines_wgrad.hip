@@ -409,6 +409,28 @@ WPlan plan_w(const vq3d_conv_desc *d) {
         else if (a.bd > 1) set(a.bh, a.bw, a.bd / 2);
         else return P;
     }
+    // few bricks (small grids: the top levels' convs): smaller bricks, down to 64 voxels, until the
+    // bricks x column groups cover the chip
+    {
+        const int cand[] = {1, 2, 4, 7, 14};
+        int npw = 1;
+        for (int c : cand) {
+            if (c > cap) break;
+            npw = c;
+            if (4 * c >= a.ntiles) break;
+        }
+        const int yg = (a.ntiles + 4 * npw - 1) / (4 * npw);
+        auto nbr = [&]() {
+            return int64_t(a.B) * ((a.oH + a.bh - 1) / a.bh) * ((a.oW + a.bw - 1) / a.bw) * ((a.oD + a.bd - 1) / a.bd);
+        };
+        // (the partial rows the reduction reads grow with the bricks: at most ~8 MB of them)
+        const int64_t nent = int64_t(a.ntiles) * P.ntm * 256 + a.N;
+        while (nbr() * yg < 256 && a.bh * a.bw * a.bd > 64 && 2 * nbr() * nent * 4 <= (int64_t(8) << 20)) {
+            if (a.bh >= a.bw && a.bh > 1) set(a.bh / 2, a.bw, a.bd);
+            else if (a.bw > 1) set(a.bh, a.bw / 2, a.bd);
+            else set(a.bh, a.bw, a.bd / 2);
+        }
+    }
     a.nbh = (a.oH + a.bh - 1) / a.bh;
     a.nbw = (a.oW + a.bw - 1) / a.bw;
     a.nbd = (a.oD + a.bd - 1) / a.bd;

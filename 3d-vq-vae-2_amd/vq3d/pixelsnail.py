@@ -48,6 +48,15 @@ def _zeros_like(t):
     return ops.zero_(torch.empty_like(t))
 
 
+def _param_grad(p):
+    """the gradient buffer a kernel may add into directly: a leaf parameter's own .grad (the flat
+    buffer's view); anything else gets a zeroed temporary that autograd then accumulates"""
+    if isinstance(p, nn.Parameter) and p.is_leaf:
+        from .functional import grad_buf
+        return grad_buf(p)
+    return _zeros_like(p)
+
+
 # the conv operand dtype of the model being run (PixelSNAIL.logits sets it): the residual streams
 # stay fp32 between blocks as under the reference's fp16 autocast (`out * self.scale` with the
 # fp32 parameter promotes, layers.py:463-465); every conv reads its operand in this dtype
@@ -139,6 +148,7 @@ class CausalConvFn(torch.autograd.Function):
         y = ops.conv_fwd(x, w, geom, pro=pro, cbias=cbias)
         ctx.geom, ctx.pro = geom, pro
         ctx.has_bias = cbias is not None
+        ctx.cbias = cbias
         ctx.save_for_backward(x, w)
         return y
 
@@ -147,13 +157,18 @@ class CausalConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         g = cl(g)
         dw = _zeros_like(w)
-        dcb = torch.zeros(w.shape[0], dtype=torch.float32, device=w.device) if ctx.has_bias else None
-        da = db = None
+        # the conv bias and the prologue scalars are parameters themselves: their sums go straight
+        # into their gradient buffers (the kernels add), no zeroed temporaries and accumulations
+        dcb = da = db = None
+        if ctx.has_bias:
+            dcb = _param_grad(ctx.cbias)
         if ctx.pro is not None:
-            da, db = _zeros_like(ctx.pro[0]), _zeros_like(ctx.pro[1])
+            da, db = _param_grad(ctx.pro[0]), _param_grad(ctx.pro[1])
         gx, _ = ops.conv_bwd(g, x, w, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
                              dcbias=dcb, dpro_pre=db, dpro_post=da)
-        return gx, dw, dcb, da, db, None
+        return (gx, dw, None if ctx.has_bias and dcb is ctx.cbias.grad else dcb,
+                None if da is not None and da is ctx.pro[0].grad else da,
+                None if db is not None and db is ctx.pro[1].grad else db, None)
 
 
 class PointwiseFn(torch.autograd.Function):
