@@ -298,7 +298,7 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
     __shared__ __attribute__((aligned(16))) float qs[QR * DM], gs[QR * DM];
     __shared__ float ls[QR], dls[QR];
     __shared__ __attribute__((aligned(16))) float pk[NW][QR][DM], pv[NW][QR][DM];
-    const int nt = (a.n + QR - 1) / QR, kt = int(blockIdx.x);  // key tile 0 meets every query tile: first
+    [[maybe_unused]] const int nt = (a.n + QR - 1) / QR, kt = int(blockIdx.x);  // key tile 0 meets every query tile: first
     const int p = int(blockIdx.y) / a.nh, h = int(blockIdx.y) - p * a.nh;
     const int r = int(threadIdx.x) & (QR - 1), w = int(threadIdx.x) / QR;
     const int j = kt * QR + r;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_kv_mma(AttnArgs a, float scale
     __shared__ __attribute__((aligned(16))) h16_t qs[MK * 8], gs[MK * 8];
     __shared__ __attribute__((aligned(16))) _Float16 qt_[8 * VTP], gt_[8 * VTP];
     __shared__ __attribute__((aligned(16))) float ls[MK], dls[MK];
-    const int nt = (a.n + MQ - 1) / MQ, ktile = int(blockIdx.x);  // key tile 0 meets every query tile: first
+    [[maybe_unused]] const int nt = (a.n + MQ - 1) / MQ, ktile = int(blockIdx.x);  // key tile 0 meets every query tile: first
     const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
     const int tid = int(threadIdx.x), lane = tid & 63, w = tid >> 6, col = lane & 31, hh = lane >> 5;
     const int kbw = ktile * (MQ / 32) + w, j = kbw * 32 + col, jc = min(j, a.n - 1);

@@ -35,6 +35,11 @@ size_t pw_wgrad_workspace(const vq3d_conv_desc *d);
 int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, const void *g, const float *pro_a,
                     const float *pro_b, const float *w, const float *escale, float *dw, float *dscale, float *dbias,
                     float *dcbias, void *workspace, size_t ws_bytes, hipStream_t s);
+// PixelSNAIL 1x1x1 weight gradient over 16-bit voxel rows (ACCUMULATED, deterministic):
+//   dw[cg][cx] += sum_v g[v * ldg + co] x[v * ldx + ci], db[cg] += sum_v g[v * ldg + co] (db may be null)
+size_t rows_wgrad_workspace(int64_t nrows, int cg, int cx);
+int launch_rows_wgrad(int64_t nrows, int cg, int cx, const void *g, int64_t ldg, const void *x, int64_t ldx, float *dw,
+                      float *db, void *workspace, size_t ws_bytes, hipStream_t s);
 
 // k^3 conv on the MFMA "lines" engine (conv_lines.hip): forward, or (dgrad) stride-1 backward-data.
 // lines_applicable: bf16 and a geometry the engine plans; lines_workspace: packed-weight bytes.

@@ -867,4 +867,14 @@ int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const vo
     return check_launch("scale_bias_res_bwd");
 }
 
+size_t vq3d_rows_wgrad_workspace_bytes(int64_t nrows, int32_t cg, int32_t cx) {
+    return rows_wgrad_workspace(nrows, cg, cx);
+}
+
+int vq3d_rows_wgrad(int32_t dtype, int64_t nrows, int32_t cg, int32_t cx, const void *g, int64_t ldg, const void *x,
+                    int64_t ldx, float *dw, float *db, void *workspace, size_t ws_bytes, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("rows_wgrad: 16-bit rows only");
+    return launch_rows_wgrad(nrows, cg, cx, g, ldg, x, ldx, dw, db, workspace, ws_bytes, as_stream(stream));
+}
+
 }  // extern "C"

@@ -629,6 +629,144 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce_t(const float *__restri
     }
 }
 
+// ---- PixelSNAIL 1x1x1 conv weight gradient over voxel rows (the Conv3d(kernel_size=1) backward of
+// pixel_model/layers.py:122-248, 650-703): dW[cg][cx] += sum_v g[v][cg] x[v][cx] and
+// db[cg] += sum_v g[v][cg] for 16-bit channels-last rows of any channel count (multiples of 8).
+// A workgroup owns one 64 x 64 (cg x cx) tile and a contiguous split of the rows; chunks of RW_VC
+// rows are staged channels-last in LDS (16-byte loads, the next chunk's in registers while the
+// current one is multiplied) and read through ds_read_b64_tr_b16 as in k_pw_wgrad_mma; each wave
+// owns a 32 x 32 quadrant (2 x 2 v_mfma_f32_16x16x32 tiles) over all K-steps.  The bias sums ride
+// on the cx-tile-0 workgroups (fixed-order column sums of the staged g rows).  Per-split partials
+// part[split][cg][cx + 1] are summed in split order by k_pw_wgrad_reduce_t: deterministic.
+constexpr int RW_VC = 128;  // rows per chunk
+constexpr int RW_P = 68;    // LDS row pitch (halves)
+
+struct RwArgs {
+    int64_t nrows, rps;  // rows, rows per split (multiple of RW_VC)
+    int cg, cx, ldg, ldx;
+    int tx;  // cx tiles
+};
+
+__global__ __launch_bounds__(256) void k_rows_wgrad(RwArgs a, const h16_t *__restrict__ g,
+                                                   const h16_t *__restrict__ x, float *__restrict__ part) {
+    __shared__ __attribute__((aligned(16))) h16_t gs[RW_VC * RW_P];
+    __shared__ __attribute__((aligned(16))) h16_t xs[RW_VC * RW_P];
+    __shared__ float bred[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = lane >> 4, li = lane & 15, q = li >> 2, p4 = li & 3;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int tcx = blockIdx.x % a.tx, tcg = blockIdx.x / a.tx;
+    const int cg0 = 64 * tcg, cx0 = 64 * tcx;
+    const int64_t r_begin = int64_t(blockIdx.y) * a.rps;
+    const int64_t r_end = min<int64_t>(a.nrows, r_begin + a.rps);
+    const bool with_bias = tcx == 0;
+
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+
+    // 2 x RW_VC rows x 8 units of 16 bytes per chunk: 8 per thread (unit u: operand u >> 10,
+    // row (u & 1023) >> 3, channels 8 (u & 7) .. + 7 of the tile)
+    u32x4 r[8];
+    auto load = [&](int64_t row0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int u = tid + 256 * k;
+            const bool isg = u < 1024;
+            const int row = (u & 1023) >> 3, c = 8 * (u & 7);
+            const int64_t v = row0 + row;
+            const int ch = (isg ? cg0 : cx0) + c;
+            r[k] = u32x4{0u, 0u, 0u, 0u};
+            if (v < r_end && ch < (isg ? a.cg : a.cx))
+                r[k] = *reinterpret_cast<const u32x4 *>(isg ? g + v * a.ldg + ch : x + v * a.ldx + ch);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int u = tid + 256 * k;
+            const int row = (u & 1023) >> 3, c = 8 * (u & 7);
+            u32x2 *d2 = reinterpret_cast<u32x2 *>((u < 1024 ? gs : xs) + row * RW_P + c);
+            d2[0] = u32x2{r[k][0], r[k][1]};
+            d2[1] = u32x2{r[k][2], r[k][3]};
+        }
+    };
+    if (r_begin < r_end) load(r_begin);
+    for (int64_t row0 = r_begin; row0 < r_end; row0 += RW_VC) {
+        __syncthreads();
+        store();
+        if (row0 + RW_VC < r_end) load(row0 + RW_VC);
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < RW_VC / 32; ++ks) {
+            const int r0 = ks * 32 + 8 * grp + q;
+            const h16_t *ga = gs + r0 * RW_P + 4 * p4;
+            const h16_t *xa = xs + r0 * RW_P + 4 * p4;
+            hx8 af[2], bf[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int mt = 2 * wm + i, t = 2 * wn + i;
+                af[i] = tr8(ga + 16 * mt, ga + 16 * mt + 4 * RW_P);
+                bf[i] = tr8(xa + 16 * t, xa + 16 * t + 4 * RW_P);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = VQ3D_MFMA_16X16X32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (with_bias) {  // column lane, rows 32 wave .. 32 wave + 31 of the chunk, in order
+            float s = 0.f;
+#pragma unroll 8
+            for (int rr = 0; rr < 32; ++rr) s += ld(gs + (32 * wave + rr) * RW_P + lane);
+            bsum += s;
+        }
+    }
+    const int ne1 = a.cx + 1;
+    float *dst = part + int64_t(blockIdx.y) * a.cg * ne1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ci = cx0 + 16 * (2 * wn + j) + li;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int co = cg0 + 16 * (2 * wm + i) + 4 * grp + e;
+                if (co < a.cg && ci < a.cx) dst[int64_t(co) * ne1 + ci] = acc[i][j][e];
+            }
+        }
+    if (with_bias) {
+        bred[wave][lane] = bsum;
+        __syncthreads();
+        if (wave == 0 && cg0 + lane < a.cg)
+            dst[int64_t(cg0 + lane) * ne1 + a.cx] = (bred[0][lane] + bred[1][lane]) + (bred[2][lane] + bred[3][lane]);
+    }
+}
+
+struct RwPlan {
+    RwArgs a;
+    int tiles, splits;
+};
+
+RwPlan rows_wgrad_plan(int64_t nrows, int cg, int cx) {
+    RwPlan p{};
+    p.a.nrows = nrows;
+    p.a.cg = cg;
+    p.a.cx = cx;
+    p.a.tx = (cx + 63) / 64;
+    p.tiles = p.a.tx * ((cg + 63) / 64);
+    const int64_t nch = std::max<int64_t>(1, (nrows + RW_VC - 1) / RW_VC);
+    // about 256 workgroups: a chunk or more each, the split count bounded by the partial traffic
+    const int64_t want = std::max<int64_t>(1, 256 / p.tiles);
+    p.splits = int(std::min<int64_t>({nch, want, 1024}));
+    p.a.rps = (nch + p.splits - 1) / p.splits * RW_VC;
+    p.splits = int((nrows + p.a.rps - 1) / p.a.rps);
+    if (p.splits < 1) p.splits = 1;
+    return p;
+}
+
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 bool reg_path(const vq3d_conv_desc *d) {
@@ -773,6 +911,34 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
     }
 #undef RED
     return check_launch("conv3d_bwd_weight(pointwise)");
+}
+
+size_t rows_wgrad_workspace(int64_t nrows, int cg, int cx) {
+    if (nrows <= 0 || cg <= 0 || cx <= 0) return 0;
+    const RwPlan p = rows_wgrad_plan(nrows, cg, cx);
+    return size_t(p.splits) * cg * (cx + 1) * sizeof(float);
+}
+
+int launch_rows_wgrad(int64_t nrows, int cg, int cx, const void *g, int64_t ldg, const void *x, int64_t ldx, float *dw,
+                      float *db, void *workspace, size_t ws_bytes, hipStream_t s) {
+    if (nrows <= 0) return 0;
+    auto al = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (cg <= 0 || cx <= 0 || cg % 8 || cx % 8 || ldg % 8 || ldx % 8 || ldg < cg || ldx < cx)
+        return fail("rows_wgrad: channel counts and row strides must be multiples of 8");
+    if (!g || !x || !dw || !al(g) || !al(x)) return fail("rows_wgrad: g / x must be 16-byte aligned");
+    RwPlan p = rows_wgrad_plan(nrows, cg, cx);
+    p.a.ldg = int(ldg);
+    p.a.ldx = int(ldx);
+    const size_t need = size_t(p.splits) * cg * (cx + 1) * sizeof(float);
+    if (!workspace || ws_bytes < need) return fail("rows_wgrad: workspace too small");
+    float *part = static_cast<float *>(workspace);
+    k_rows_wgrad<<<dim3(unsigned(p.tiles), unsigned(p.splits), 1u), 256, 0, s>>>(p.a, (const h16_t *)g,
+                                                                               (const h16_t *)x, part);
+    const int ne = cg * (cx + 1);
+    const unsigned nr = unsigned((ne + 63) / 64);
+    k_pw_wgrad_reduce_t<<<nr, 256, 0, s>>>(part, p.splits, ne, cx, nullptr, nullptr, dw, nullptr, nullptr, db,
+                                           GridSum{});
+    return check_launch("rows_wgrad");
 }
 
 }  // namespace vq3d

@@ -48,10 +48,14 @@ def _zeros_like(t):
     return ops.zero_(torch.empty_like(t))
 
 
+def _is_param(p):
+    return isinstance(p, nn.Parameter) and p.is_leaf
+
+
 def _param_grad(p):
     """the gradient buffer a kernel may add into directly: a leaf parameter's own .grad (the flat
     buffer's view); anything else gets a zeroed temporary that autograd then accumulates"""
-    if isinstance(p, nn.Parameter) and p.is_leaf:
+    if _is_param(p):
         from .functional import grad_buf
         return grad_buf(p)
     return _zeros_like(p)
@@ -171,26 +175,46 @@ class CausalConvFn(torch.autograd.Function):
                 None if db is not None and db is ctx.pro[1].grad else db, None)
 
 
+# the 16-bit weight shadow of the current forward: (FlatParams, dtype) when the parameters live in
+# a flat buffer (PixelSNAIL.logits refreshes it once per forward), else None (per-call casts)
+_shadow = [None]
+
+
+def _w16(p, dtype):
+    """parameter p as a GEMM operand of dtype: its slice of the refreshed flat shadow, or a cast"""
+    sh = _shadow[0]
+    if sh is not None and sh[1] == dtype and p.dtype == torch.float32 and sh[0].owns(p):
+        return sh[0].shadow_view(p, dtype)
+    return p.to(dtype)
+
+
+def _rows_ok(t):
+    return (t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and t.stride(1) == 1
+            and t.shape[1] % 8 == 0 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
 class PointwiseFn(torch.autograd.Function):
     """1x1x1 conv of a channels-last (b, c, d, h, w) tensor as GEMMs over its voxel rows
-    (hipBLASLt, fp32 accumulation).  The weight gradient sum_v g[v] (x) x[v] has the voxels as
-    its K dimension and only co x ci outputs: it runs as a batched GEMM over 256-voxel slices
-    (split K, enough workgroups to fill the chip) plus one sum over the slices."""
+    (hipBLASLt, fp32 accumulation) for y and gx.  The weight gradient sum_v g[v] (x) x[v] has the
+    voxels as its K dimension and only co x ci outputs: on 16-bit rows it is vq3d_rows_wgrad
+    (matrix cores, split K, fixed-order sum, bias sums included) adding straight into the
+    parameters' gradient buffers; fp32 rows (the reference-parity path) run a batched fp32 GEMM over
+    256-voxel slices plus one sum over the slices."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         xv = x.permute(0, 2, 3, 4, 1).reshape(-1, x.shape[1])
-        w2 = w.reshape(w.shape[0], -1)
-        y = F.linear(xv, w2.to(x.dtype), None if b is None else b.to(x.dtype))
+        w2 = _w16(w, x.dtype).reshape(w.shape[0], -1)
+        y = F.linear(xv, w2, None if b is None else _w16(b, x.dtype))
         ctx.save_for_backward(xv, w2)
         ctx.shape = (x.shape[0],) + tuple(x.shape[2:])
-        ctx.has_b = b is not None
-        ctx.wshape = w.shape
+        ctx.prm = (w, b)
         return y.reshape(ctx.shape + (w.shape[0],)).permute(0, 4, 1, 2, 3)
 
     @staticmethod
     def backward(ctx, g):
         xv, w2 = ctx.saved_tensors
+        w, b = ctx.prm
         co = w2.shape[0]
         gv = g.permute(0, 2, 3, 4, 1).reshape(-1, co)
         if not gv.is_contiguous():
@@ -199,10 +223,18 @@ class PointwiseFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (gv @ w2.to(gv.dtype)).reshape(ctx.shape + (w2.shape[1],)).permute(0, 4, 1, 2, 3)
         n = gv.shape[0]
+        if gv.dtype == xv.dtype and _rows_ok(gv) and _rows_ok(xv):
+            dw = _param_grad(w)
+            db = None if b is None else _param_grad(b)
+            nws = int(L.query("vq3d_rows_wgrad_workspace_bytes", n, co, xv.shape[1]))
+            ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=gv.device)
+            L.call("vq3d_rows_wgrad", L.dtype_code(gv), n, co, xv.shape[1], L.ptr(gv), gv.stride(0), L.ptr(xv),
+                   xv.stride(0), L.ptr(dw), L.ptr(db), L.ptr(ws), ctypes_size(nws), L.stream())
+            return gx, None if _is_param(w) else dw, None if b is None or _is_param(b) else db
         sk = 256 if n % 256 == 0 and n >= 4096 else n
         gw = torch.bmm(gv.reshape(-1, sk, co).transpose(1, 2).float(), xv.reshape(-1, sk, xv.shape[1]).float()).sum(0)
-        gb = gv.float().sum(0) if ctx.has_b else None
-        return gx, gw.reshape(ctx.wshape), gb
+        gb = gv.float().sum(0) if b is not None else None
+        return gx, gw.reshape(w.shape), gb
 
 
 def pointwise(x, w, b):
@@ -589,6 +621,14 @@ class PixelSNAIL(nn.Module):
         dims = tuple(onehot.shape[2:])
         _compute[0] = self.compute_dtype
         x = cl(onehot.to(self.compute_dtype))
+        # the GEMM weights of this forward: one cast of the flat parameter buffer (if there is one)
+        _shadow[0] = None
+        if self.compute_dtype != torch.float32:
+            from .flat import flat_of
+            fl = flat_of(self.parse_input.weight)
+            if fl is not None:
+                fl.refresh_shadow(self.compute_dtype)
+                _shadow[0] = (fl, self.compute_dtype)
         x = cl(pointwise(x, self.parse_input.weight, self.parse_input.bias))
         stack = self.to_causal.run([x, x, x])
         bg = background_list(b, dims, self.compute_dtype, x.device)

@@ -662,7 +662,7 @@ def prior_main(a):
         "attention_kernel": {"positions": n, "heads": nh, "head_dim": d, "fwd_ms": tf, "bwd_ms": tb,
                              "fwd_tflops": pairs * 4 * d / (tf * 1e-3) / 1e12,
                              "bwd_tflops": pairs * 8 * d / (tb * 1e-3) / 1e12,
-                             "note": "fp32 VALU online softmax; per stream and block (24 per step)"},
+                             "note": "matrix-core kernels (16-bit, head dim 8), fp32 online softmax; per stream and block (24 per step)"},
     }
     if not a.no_cpu_baseline:
         print("[bench] prior CPU baseline", file=sys.stderr, flush=True)

@@ -469,6 +469,15 @@ int vq3d_scale_bias_res_fwd(int32_t o_dtype, int64_t n, const void *o, const flo
                             const float *s, float *out, vq3d_stream_t stream);
 int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const void *o, const float *scale, void *go,
                             float *dscale, float *dbias, vq3d_stream_t stream);
+/* the 1x1x1 convs' weight gradient over voxel rows (the Conv3d(kernel_size=1) backward of
+ * layers.py:122-248 / 650-703, the GEMMs' K = voxels side): dw[cg][cx] += sum_v g[v][co] x[v][ci]
+ * and (db != NULL) db[co] += sum_v g[v][co], fp32 accumulation in a fixed order.  g: nrows rows of
+ * cg channels at row stride ldg, x: rows of cx channels at stride ldx, both 16-bit (dtype BF16 / F16),
+ * 16-byte aligned, channel counts and strides multiples of 8; workspace of
+ * vq3d_rows_wgrad_workspace_bytes bytes. */
+size_t vq3d_rows_wgrad_workspace_bytes(int64_t nrows, int32_t cg, int32_t cx);
+int vq3d_rows_wgrad(int32_t dtype, int64_t nrows, int32_t cg, int32_t cx, const void *g, int64_t ldg, const void *x,
+                    int64_t ldx, float *dw, float *db, void *workspace, size_t ws_bytes, vq3d_stream_t stream);
 
 /* --- PixelSNAIL prior: dense causal attention (pixel_model/layers.py:613-647) ---
  * For each of nprob problems (stack x batch) and nh heads: out[i] = sum_{j <= i} softmax_j(scale *

@@ -388,3 +388,89 @@ def test_block_glue_kernels_match_torch(gpu):
     for i, (f, t) in enumerate(zip(*res)):
         tol = 1e-2 if i in (0, 3) else 1e-4  # bf16 outputs: one rounding apart at most
         assert rel(f, t.cpu().numpy()) < tol, (i, rel(f, t.cpu().numpy()))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,cg,cx,ldg,ldx,bias", [(8192, 64, 256, 64, 256, True), (8192, 256, 64, 256, 64, False),
+                                                  (8192, 128, 64, 128, 64, True), (1000, 64, 64, 128, 72, True),
+                                                  (300, 8, 24, 8, 24, True), (70, 136, 200, 136, 208, True)])
+def test_rows_wgrad_matches_fp32(gpu, dt, n, cg, cx, ldg, ldx, bias):
+    """vq3d_rows_wgrad (the 16-bit 1x1x1 convs' weight gradient, PointwiseFn.backward) against an
+    fp32 torch GEMM of the same 16-bit rows: dw / db ACCUMULATED into preset buffers, ragged row
+    counts, channel counts off the 64-tile, row strides wider than the rows (views), and bitwise
+    equal on a second run (fixed-order split-K sum).  Tolerance 1e-5 of max |sum| (fp32 order)."""
+    import ctypes
+    from vq3d import _lib as L
+    g0 = torch.Generator(device=gpu).manual_seed(n + cg + cx)
+    gb = torch.randn((n, ldg), device=gpu, generator=g0).to(dt)
+    xb = torch.randn((n, ldx), device=gpu, generator=g0).to(dt)
+    gv, xv = gb[:, :cg], xb[:, :cx]
+    want_w = gv.float().t() @ xv.float() + 0.5
+    want_b = gv.float().sum(0) - 1.0
+    outs = []
+    for _ in range(2):
+        dw = torch.full((cg, cx), 0.5, device=gpu)
+        db = torch.full((cg,), -1.0, device=gpu) if bias else None
+        nws = int(L.query("vq3d_rows_wgrad_workspace_bytes", n, cg, cx))
+        ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=gpu)
+        L.call("vq3d_rows_wgrad", L.dtype_code(gv), n, cg, cx, L.ptr(gv), ldg, L.ptr(xv), ldx, L.ptr(dw), L.ptr(db),
+               L.ptr(ws), ctypes.c_size_t(nws), L.stream())
+        torch.cuda.synchronize()
+        outs.append((dw, db))
+    dw, db = outs[0]
+    assert rel(dw, want_w.cpu().numpy()) < 1e-5
+    if bias:
+        assert rel(db, want_b.cpu().numpy()) < 1e-5
+    assert torch.equal(outs[0][0], outs[1][0])
+    if bias:
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_rows_wgrad_rejects_unaligned(gpu):
+    """channel counts / strides off a multiple of 8 fail loudly (PointwiseFn keeps those on the
+    fp32 batched GEMM)"""
+    import ctypes
+    from vq3d import _lib as L
+    gv = torch.zeros((64, 12), device=gpu, dtype=torch.bfloat16)
+    xv = torch.zeros((64, 16), device=gpu, dtype=torch.bfloat16)
+    dw = torch.zeros((12, 16), device=gpu)
+    ws = torch.empty(1 << 16, dtype=torch.uint8, device=gpu)
+    with pytest.raises(L.Vq3dError):
+        L.call("vq3d_rows_wgrad", L.dtype_code(gv), 64, 12, 16, L.ptr(gv), 12, L.ptr(xv), 16, L.ptr(dw), None,
+               L.ptr(ws), ctypes.c_size_t(1 << 16), L.stream())
+
+
+def test_flat_weight_shadow_bitwise(gpu):
+    """PixelSNAIL.logits on FlatParams reads its GEMM weights from one 16-bit cast of the flat
+    buffer (FlatParams.refresh_shadow) instead of per-call casts: loss and every gradient equal to
+    the per-call-cast run bit for bit, and again after the parameters change (the shadow follows)."""
+    from vq3d import pixelsnail as PS
+    from vq3d.flat import FlatParams
+    kw = dict(num_embeddings=[64, 0], model_dim=64, num_blocks=1, num_layers_per_block=2, causal_dropout_prob=0.0,
+              attention_dropout_prob=0.0)
+    codes = torch.randint(0, 64, (1, 8, 8, 4), generator=torch.Generator().manual_seed(3)).to(gpu)
+    onehot = torch.nn.functional.one_hot(codes, 64).permute(0, 4, 1, 2, 3).float().contiguous()
+    res = []
+    for flat in (False, True):
+        torch.manual_seed(0)
+        m = PS.PixelSNAIL(PS.default_args(**kw), compute_dtype="bf16").to(gpu)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(0.01 * torch.randn_like(p))
+        fl = FlatParams(m.parameters(), gpu) if flat else None
+        out = []
+        for it in range(2):
+            for p in m.parameters():
+                p.grad = None if fl is None else p.grad
+            if fl is not None:
+                fl.zero_grad()
+            loss, _ = m.cross_entropy_onehot(onehot, codes)
+            loss.backward()
+            out.append([float(loss)] + [p.grad.detach().clone() for p in m.parameters()])
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.mul_(1.01)
+        res.append(out)
+    for a, b in zip(res[0], res[1]):
+        assert a[0] == b[0]
+        assert all(torch.equal(x, y) for x, y in zip(a[1:], b[1:]))
