@@ -57,7 +57,39 @@ struct LArgs {
     int cin_split;             // dgrad: output channels < cin_split go to y, the rest to y2
     int S;                     // D-shifts per A row: a row is S consecutive output voxels along D and
                                // column n = (shift n / N, channel n % N) (S * N = 16 when S > 1)
+    unsigned tapmask;          // 0, or the weight taps that may be nonzero (vq3d_conv_desc.tap_mask):
+                               // the k-steps then run over the live chunks only (S == 1)
 };
+
+// chunk c = ((kh*k + kw)*nch + j) of the window order holds a live tap (mask bit of tap
+// (kh*k + kw)*k + kd, flipped for the backward-data kernel); chunks past the window are dead
+__host__ __device__ inline bool chunk_live(int c, int nch, int k, int C, unsigned mask, bool dgrad) {
+    const int t2 = c / nch, j = c - t2 * nch;
+    const int e0 = 8 * j;
+    if (e0 >= k * C) return false;
+    const int e1 = (e0 + 7 < k * C - 1) ? e0 + 7 : k * C - 1;
+    const int K3 = k * k * k;
+    for (int kd = e0 / C; kd <= e1 / C; ++kd) {
+        const int tap = t2 * k + kd;
+        if ((mask >> (dgrad ? K3 - 1 - tap : tap)) & 1u) return true;
+    }
+    return false;
+}
+
+// the live chunks in order into cmap[0 .. nlive), padded with NCH (dead) up to `total`: one wave
+// (ballot prefix sums), the caller synchronises
+template <bool DGRAD>
+__device__ void live_chunk_map(const LArgs &a, int *cmap, int total, int lane) {
+    int cnt = 0;
+    for (int base = 0; base < a.NCH; base += 64) {
+        const int c = base + lane;
+        const bool lv = c < a.NCH && chunk_live(c, a.nch, a.k, a.C, a.tapmask, DGRAD);
+        const uint64_t bal = __ballot(lv);
+        if (lv) cmap[cnt + __popcll(bal & ((uint64_t(1) << lane) - 1))] = c;
+        cnt += __popcll(bal);
+    }
+    for (int i = cnt + lane; i < total; i += 64) cmap[i] = a.NCH;
+}
 
 __device__ __forceinline__ int wrapc(int i, int n) {
     while (i < 0) i += n;
@@ -133,9 +165,10 @@ struct MT {
 // c = ((kh*k + kw)*nch + j) holds window elements e = 8j + t = (kd, ci)
 template <bool DGRAD>
 __device__ __forceinline__ uint4 pack_item(const LArgs &a, const float *__restrict__ w, int wCt, int gi, int ntot,
-                                           int it) {
+                                           int it, const int *cmap) {
     const int K3 = a.k * a.k * a.k;
-    const int c = it / ntot, nn = it - c * ntot;
+    const int ci_ = it / ntot, nn = it - ci_ * ntot;
+    const int c = cmap ? cmap[ci_] : ci_;  // the compacted k-step order's chunk
     const int n = gi * ntot + nn;
     const int t2 = c / a.nch, j = c - t2 * a.nch;
     // shift mode: column n = (shift sh, channel co) reads window position pd = kd + sh * s
@@ -169,9 +202,15 @@ __device__ __forceinline__ uint4 pack_item(const LArgs &a, const float *__restri
 template <bool DGRAD>
 __global__ __launch_bounds__(256) void k_lines_pack(LArgs a, const float *__restrict__ w, int wCt, int ntot,
                                                     uint4 *__restrict__ out) {
+    __shared__ int cmap[1024];
     const int items = a.nks * 4 * ntot;
+    if (a.tapmask) {
+        if (threadIdx.x < 64) live_chunk_map<DGRAD>(a, cmap, a.nks * 4, threadIdx.x);
+        __syncthreads();
+    }
     const int it = blockIdx.x * 256 + threadIdx.x;
-    if (it < items) out[int64_t(blockIdx.y) * items + it] = pack_item<DGRAD>(a, w, wCt, blockIdx.y, ntot, it);
+    if (it < items)
+        out[int64_t(blockIdx.y) * items + it] = pack_item<DGRAD>(a, w, wCt, blockIdx.y, ntot, it, a.tapmask ? cmap : nullptr);
 }
 
 template <int NT, int ALN, bool DGRAD>
@@ -199,24 +238,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 1 ||
     const int nw = min(NTOT, a.N - gi * NTOT);  // output channels of this group
     const int ncol = a.S > 1 ? 16 : nw;           // MFMA columns holding outputs
 
-    // ---- once per workgroup: weight image of this N group + chunk offset table
+    // ---- once per workgroup: weight image of this N group + chunk offset table (with a tap mask:
+    // the live chunks in order, ctab first holding their chunk indices)
+    if (a.tapmask) {
+        if (wave == 0) live_chunk_map<DGRAD>(a, ctab, a.nks * 4, lane);
+        __syncthreads();
+    }
     {
         const int items = a.nks * 4 * NTOT;
         if (wpk) {  // pre-packed image: 16-byte copies
             const uint4 *src = wpk + int64_t(gi) * items;
             for (int it = tid; it < items; it += 256) wl[it] = src[it];
         } else {
-            for (int it = tid; it < items; it += 256) wl[it] = pack_item<DGRAD>(a, w, wCt, gi, NTOT, it);
+            for (int it = tid; it < items; it += 256)
+                wl[it] = pack_item<DGRAD>(a, w, wCt, gi, NTOT, it, a.tapmask ? ctab : nullptr);
         }
     }
-    for (int c = tid; c < a.nks * 4; c += 256) {
+    if (a.tapmask) __syncthreads();  // the chunk indices are read above, rewritten as offsets below
+    for (int i = tid; i < a.nks * 4; i += 256) {
+        const int c = a.tapmask ? ctab[i] : i;
         int off = 0;  // padding chunks: zero weights, any valid window
         if (c < a.NCH) {
             const int t2 = c / a.nch, j = c - t2 * a.nch;
             const int kh = t2 / a.k, kw = t2 - kh * a.k;
             off = (kh * a.hw + kw) * a.LS + 8 * j;
         }
-        ctab[c] = off;
+        ctab[i] = off;
     }
     // this lane's A-row window base per M tile (wave w owns tiles w, w + 4, ...)
     int rowbase[MTW];
@@ -546,7 +593,7 @@ void set_brick(LArgs &a, int bh, int bw, int bd) {
 
 // GEMM-conv geometry: input (B, Ca+Cb, iH, iW, iD) -> output (B, N, oH, oW, oD)
 Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, int oD, int k, int s, int p,
-          int circ, int S) {
+          int circ, int S, unsigned tapmask, bool dgrad) {
     Plan P = {};
     LArgs &a = P.a;
     a.B = B; a.Ca = Ca; a.Cb = Cb; a.C = Ca + Cb; a.N = N;
@@ -559,6 +606,13 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
     a.nch = (((a.S - 1) * s + k) * a.C + 7) / 8;
     a.NCH = k * k * a.nch;
     a.nks = (a.NCH + 3) / 4;
+    a.tapmask = 0;
+    if (tapmask && S == 1 && k <= 3 && a.NCH <= 1016) {  // k-steps over the live chunks only
+        int nlive = 0;
+        for (int c = 0; c < a.NCH; ++c) nlive += chunk_live(c, a.nch, k, a.C, tapmask, dgrad);
+        a.tapmask = tapmask;
+        a.nks = std::max(1, (nlive + 3) / 4);
+    }
     auto div = [](int v, int d) { return v % d == 0; };
     a.vec = (div(Ca, 8) && div(Cb, 8)) ? 8 : ((div(Ca, 2) && div(Cb, 2)) ? 2 : 1);
     const int ntr = (N + 15) / 16;
@@ -644,12 +698,12 @@ Plan plan(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, 
 // only 4 or 8 output channels and the output depth holds whole groups; else S = 1.  4 -> 4 @512^2x128
 // forward 719 -> 389 us, backward-data 828 -> 403 us (7 instead of 20 k-steps per 64 voxels)
 Plan plan_s(int B, int Ca, int Cb, int N, int iH, int iW, int iD, int oH, int oW, int oD, int k, int s, int p,
-            int circ) {
+            int circ, unsigned tapmask, bool dgrad) {
     if ((N == 4 || N == 8) && s == 1 && oD % (16 / N) == 0) {  // stride 2: measured slower (larger halo)
-        const Plan P = plan(B, Ca, Cb, N, iH, iW, iD, oH, oW, oD, k, s, p, circ, 16 / N);
+        const Plan P = plan(B, Ca, Cb, N, iH, iW, iD, oH, oW, oD, k, s, p, circ, 16 / N, 0u, dgrad);
         if (P.ok) return P;
     }
-    return plan(B, Ca, Cb, N, iH, iW, iD, oH, oW, oD, k, s, p, circ, 1);
+    return plan(B, Ca, Cb, N, iH, iW, iD, oH, oW, oD, k, s, p, circ, 1, tapmask, dgrad);
 }
 
 Plan plan_for(const vq3d_conv_desc *d, bool dgrad) {
@@ -657,11 +711,11 @@ Plan plan_for(const vq3d_conv_desc *d, bool dgrad) {
     const int circ = d->pad_mode == VQ3D_PAD_CIRCULAR;
     if (!dgrad)
         return plan_s(d->batch, d->cin, d->cin2, d->cout, d->in_h, d->in_w, d->in_d, d->out_h, d->out_w, d->out_d,
-                      d->kernel, d->stride, d->pad, circ);
+                      d->kernel, d->stride, d->pad, circ, d->tap_mask, false);
     const int pp = d->kernel - 1 - d->pad;
     if (d->stride != 1 || pp < 0) return Plan{};
     return plan_s(d->batch, d->cout, 0, d->cin + d->cin2, d->out_h, d->out_w, d->out_d, d->in_h, d->in_w, d->in_d,
-                  d->kernel, 1, pp, circ);
+                  d->kernel, 1, pp, circ, d->tap_mask, true);
 }
 
 // persistent grid: workgroups resident at the kernel's occupancy (per CU), bricks strided

@@ -51,7 +51,33 @@ struct WArgs {
     int nent;                  // partial slots per workgroup: ntiles * NTM * 256 fragments + N g sums
     int64_t xtotal;            // elements of x
     FastDiv fC, fhw, fN, fCr, fmc;
+    unsigned tapmask;          // 0, or the weight taps that may be nonzero (vq3d_conv_desc.tap_mask)
+    int ntl;                   // column tiles computed: ntiles, or the live ones (tile_map order)
 };
+
+// column tile tt (t2 = kh*k + kw, 16 window columns from 16 jt) holds a live tap
+__host__ __device__ inline bool wtile_live(int tt, const WArgs &a) {
+    const int t2 = tt / a.ctile, jt = tt - t2 * a.ctile;
+    const int e0 = 16 * jt;
+    if (e0 >= a.k * a.CS) return false;
+    const int e1 = (e0 + 15 < a.k * a.CS - 1) ? e0 + 15 : a.k * a.CS - 1;
+    for (int kd = e0 / a.CS; kd <= e1 / a.CS; ++kd)
+        if ((a.tapmask >> (t2 * a.k + kd)) & 1u) return true;
+    return false;
+}
+
+// the live tiles in order into tmap[0 .. ntl): one wave (ballot prefix sums), caller synchronises
+__device__ void live_tile_map(const WArgs &a, short *tmap, int lane) {
+    int cnt = 0;
+    for (int base = 0; base < a.ntiles; base += 64) {
+        const int tt = base + lane;
+        const bool lv = tt < a.ntiles && wtile_live(tt, a);
+        const uint64_t bal = __ballot(lv);
+        if (lv) tmap[cnt + __popcll(bal & ((uint64_t(1) << lane) - 1))] = short(tt);
+        cnt += __popcll(bal);
+    }
+}
+constexpr int kMaxMaskTiles = 1024;
 
 __device__ __forceinline__ s16x4 tr_read(const h16_t *p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p));
@@ -81,13 +107,19 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const h16_t *__res
     const bool raw = pro.kind == VQ3D_PRO_NONE;
     const int tile0 = blockIdx.y * 4 * NPW;
     const bool do_bias = blockIdx.y == 0;
+    short *tmap = reinterpret_cast<short *>(gt + a.nvp * a.GS);  // [ntiles] (tap mask only)
+    if (a.tapmask) {
+        if (wave == 0) live_tile_map(a, tmap, lane);
+        __syncthreads();
+    }
 
     // this lane's B column offset (element) per owned tile: (kh, kw) line delta + column chunk
     int coff[NPW];
 #pragma unroll
     for (int t = 0; t < NPW; ++t) {
-        int tt = tile0 + wave + 4 * t;
-        if (tt >= a.ntiles) tt = 0;  // padded tiles read valid addresses, are never written
+        int tt = tile0 + wave + 4 * t;  // index into the computed tiles
+        if (tt >= a.ntl) tt = 0;        // padded tiles read valid addresses, are never written
+        else if (a.tapmask) tt = tmap[tt];
         const int t2 = tt / a.ctile, jt = tt - t2 * a.ctile;
         const int kh = t2 / a.k, kw = t2 - kh * a.k;
         coff[t] = (kh * a.hw + kw) * a.LS + 16 * jt + 4 * pp;
@@ -286,12 +318,12 @@ __global__ __launch_bounds__(256) void k_lines_wgrad(WArgs a, const h16_t *__res
 #pragma unroll
     for (int t = 0; t < NPW; ++t) {
         const int tt = tile0 + wave + 4 * t;
-        if (tt >= a.ntiles) continue;
+        if (tt >= a.ntl) continue;
 #pragma unroll
         for (int m = 0; m < NTM; ++m)
             *reinterpret_cast<f32x4 *>(pw + ((tt * NTM + m) * 64 + lane) * 4) = acc[m][t];
     }
-    if (do_bias && tid < a.N) pw[a.ntiles * NTM * 256 + tid] = gsum;
+    if (do_bias && tid < a.N) pw[a.ntl * NTM * 256 + tid] = gsum;
 }
 
 // Sum the workgroup partials of every fragment slot (LANES lanes per slot, strided slices, 8
@@ -304,6 +336,11 @@ __global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, co
                                                            const float *__restrict__ escale, float *dw,
                                                            float *dscale, float *dbias, float *dcbias, GridSum gsum) {
     __shared__ float red[8];
+    __shared__ short tmap[kMaxMaskTiles];
+    if (a.tapmask) {
+        if (threadIdx.x < 64) live_tile_map(a, tmap, threadIdx.x);
+        __syncthreads();
+    }
     const int lane = threadIdx.x % LANES;
     const int f = blockIdx.x * (256 / LANES) + threadIdx.x / LANES;
     const int ne = a.nent;
@@ -319,11 +356,13 @@ __global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, co
     }
     sum = group_sum<LANES>(sum);
     float wg = 0.f, bs = 0.f;
-    const int nfr = a.ntiles * ntm * 256;
+    const int nfr = a.ntl * ntm * 256;
     if (f < ne && lane == 0) {
         if (f < nfr) {
             const int i = f & 3, ln = (f >> 2) & 63, q = f >> 8;  // q = tile * NTM + m
-            const int tt = q / ntm, m = q - tt * ntm;
+            int tt = q / ntm;
+            const int m = q - tt * ntm;
+            if (a.tapmask) tt = tmap[tt];
             const int co = m * 16 + (ln >> 4) * 4 + i;
             const int t2 = tt / a.ctile, jt = tt - t2 * a.ctile;
             const int e = 16 * jt + (ln & 15);
@@ -380,6 +419,15 @@ WPlan plan_w(const vq3d_conv_desc *d) {
     a.ncol = a.k * a.CS;
     a.ctile = (a.ncol + 15) / 16;
     a.ntiles = a.k * a.k * a.ctile;
+    a.tapmask = 0;
+    a.ntl = a.ntiles;
+    if (d->tap_mask && a.k <= 3 && a.ntiles <= kMaxMaskTiles) {  // only the tiles of live taps
+        a.tapmask = d->tap_mask;
+        int n = 0;
+        for (int tt = 0; tt < a.ntiles; ++tt) n += wtile_live(tt, a);
+        if (n > 0) a.ntl = n;
+        else a.tapmask = 0;
+    }
     // column tiles per wave: accumulators NTM * NPW * 4 VGPRs <= 112 (chosen after the bricks)
     const int cap = P.ntm == 1 ? 14 : (P.ntm == 2 ? 14 : 7);
     // brick: up to 512 voxels, full D when it fits
@@ -393,8 +441,9 @@ WPlan plan_w(const vq3d_conv_desc *d) {
         a.nvb = bh * bw * bd;
         a.nvp = (a.nvb + 31) / 32 * 32;
     };
-    auto lds_of = [&]() {
-        return ((size_t(a.hh) * a.hw * a.LS + 7) / 8 * 8) * 2 + size_t(a.nvp) * a.GS * 2;
+    auto lds_of = [&]() {  // lines, g tile, the live-tile map
+        return ((size_t(a.hh) * a.hw * a.LS + 7) / 8 * 8) * 2 + size_t(a.nvp) * a.GS * 2 +
+               (a.tapmask ? size_t(a.ntiles) * 2 : size_t(0));
     };
     int bd = std::min(pow2c(a.oD), 32);
     int bw = std::min(pow2c(a.oW), std::max(1, 512 / (bd * 4)));
@@ -417,14 +466,14 @@ WPlan plan_w(const vq3d_conv_desc *d) {
         for (int c : cand) {
             if (c > cap) break;
             npw = c;
-            if (4 * c >= a.ntiles) break;
+            if (4 * c >= a.ntl) break;
         }
-        const int yg = (a.ntiles + 4 * npw - 1) / (4 * npw);
+        const int yg = (a.ntl + 4 * npw - 1) / (4 * npw);
         auto nbr = [&]() {
             return int64_t(a.B) * ((a.oH + a.bh - 1) / a.bh) * ((a.oW + a.bw - 1) / a.bw) * ((a.oD + a.bd - 1) / a.bd);
         };
         // (the partial rows the reduction reads grow with the bricks: at most ~8 MB of them)
-        const int64_t nent = int64_t(a.ntiles) * P.ntm * 256 + a.N;
+        const int64_t nent = int64_t(a.ntl) * P.ntm * 256 + a.N;
         while (nbr() * yg < 256 && a.bh * a.bw * a.bd > 64 && 2 * nbr() * nent * 4 <= (int64_t(8) << 20)) {
             if (a.bh >= a.bw && a.bh > 1) set(a.bh / 2, a.bw, a.bd);
             else if (a.bw > 1) set(a.bh, a.bw / 2, a.bd);
@@ -452,10 +501,10 @@ WPlan plan_w(const vq3d_conv_desc *d) {
     for (int c : cands) {
         if (c > cap) break;
         P.npw = c;
-        if (4 * c >= a.ntiles) break;
+        if (4 * c >= a.ntl) break;
     }
-    P.ygroups = (a.ntiles + 4 * P.npw - 1) / (4 * P.npw);
-    a.nent = a.ntiles * P.ntm * 256 + a.N;
+    P.ygroups = (a.ntl + 4 * P.npw - 1) / (4 * P.npw);
+    a.nent = a.ntl * P.ntm * 256 + a.N;
     int64_t nbx = std::max<int64_t>(1, std::min<int64_t>(a.nbricks, 1024 / P.ygroups));
     while (nbx > 1 && nbx * a.nent * 4 > (int64_t(16) << 20)) nbx /= 2;
     P.nbx = int(nbx);

@@ -23,7 +23,7 @@ P = ctypes.c_void_p
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("dtype", "batch", "cin", "cin2", "cout", "in_h", "in_w", "in_d",
                                      "out_h", "out_w", "out_d", "kernel", "stride", "pad", "pad_mode",
-                                     "pro_kind")]
+                                     "pro_kind")] + [("tap_mask", ctypes.c_uint32)]
 
 
 ACT_NONE, ACT_ELU, ACT_ELU_AFFINE = 0, 1, 2

@@ -53,14 +53,15 @@ class ConvGeom:
 _desc_cache = {}
 
 
-def conv_desc(dtype, b, cin, cin2, cout, h, w, d, geom, pro_kind):
-    key = (dtype, b, cin, cin2, cout, h, w, d, geom.key(), pro_kind)
+def conv_desc(dtype, b, cin, cin2, cout, h, w, d, geom, pro_kind, taps=0):
+    key = (dtype, b, cin, cin2, cout, h, w, d, geom.key(), pro_kind, taps)
     r = _desc_cache.get(key)
     if r is None:
         oh, ow, od = geom.out(h), geom.out(w), geom.out(d)
         desc = L.ConvDesc(dtype=L.dtype_code(dtype), batch=b, cin=cin, cin2=cin2, cout=cout, in_h=h, in_w=w,
                           in_d=d, out_h=oh, out_w=ow, out_d=od, kernel=geom.k, stride=geom.s, pad=geom.p,
-                          pad_mode=L.PAD_CIRCULAR if geom.circular else L.PAD_ZEROS, pro_kind=pro_kind)
+                          pad_mode=L.PAD_CIRCULAR if geom.circular else L.PAD_ZEROS, pro_kind=pro_kind,
+                          tap_mask=taps)
         r = (desc, (oh, ow, od))
         _desc_cache[key] = r
     return r
@@ -85,13 +86,14 @@ def _act(act):
 
 
 def conv_fwd(x, w, geom, pro=None, x2=None, scale=None, bias=None, cbias=None, residual=None,
-             residual_up2=False, act=None, out=None):
+             residual_up2=False, act=None, out=None, taps=0):
+    """taps: vq3d_conv_desc.tap_mask (0 = dense; else the weight taps that may be nonzero)"""
     x = as_cl(x)
     b, cin, h, wd, d = x.shape
     cin2 = 0 if x2 is None else x2.shape[1]
     cout = w.shape[0]
     kind, pa, pb = pro_kind_of(pro)
-    desc, (oh, ow, od) = conv_desc(x.dtype, b, cin, cin2, cout, h, wd, d, geom, kind)
+    desc, (oh, ow, od) = conv_desc(x.dtype, b, cin, cin2, cout, h, wd, d, geom, kind, taps)
     if w.shape[1] != cin + cin2 or w.shape[2] != geom.k:
         raise L.Vq3dError(f"weight {tuple(w.shape)} does not match conv ({cin}+{cin2} -> {cout}, k={geom.k})")
     y = out if out is not None else new_act(b, cout, oh, ow, od, x.dtype, x.device)
@@ -133,15 +135,16 @@ def _depi(aux, aux_b, addend):
 
 
 def conv_bwd(g, x, w, geom, pro=None, x2=None, gscale=None, aux=None, aux_b=None, addend=None, want_gx=True,
-             dw=None, dscale=None, dbias=None, dcbias=None, dpro_pre=None, dpro_post=None, escale=None):
+             dw=None, dscale=None, dbias=None, dcbias=None, dpro_pre=None, dpro_post=None, escale=None, taps=0):
     """Backward of conv_fwd: returns (gx, gx2); parameter gradients are ACCUMULATED (fp32
     atomics) into the given buffers (dw: weight, dscale/dbias: epilogue scalars, dcbias: conv
-    bias, dpro_pre/dpro_post: prologue scalars (+b / +a of elu(x+a)+b, or a of x+a))."""
+    bias, dpro_pre/dpro_post: prologue scalars (+b / +a of elu(x+a)+b, or a of x+a)); with a tap
+    mask the weight-gradient entries of the clear taps may be left unwritten."""
     x = as_cl(x)
     b, cin, h, wd, d = x.shape
     cin2 = 0 if x2 is None else x2.shape[1]
     kind, pa, pb = pro_kind_of(pro)
-    desc, _ = conv_desc(x.dtype, b, cin, cin2, w.shape[0], h, wd, d, geom, kind)
+    desc, _ = conv_desc(x.dtype, b, cin, cin2, w.shape[0], h, wd, d, geom, kind, taps)
     s = L.stream()
     gx = gx2 = None
     if want_gx or dpro_pre is not None or dpro_post is not None:

@@ -146,11 +146,11 @@ class CausalConvFn(torch.autograd.Function):
     onto the reference-shaped parameters through the embedding)."""
 
     @staticmethod
-    def forward(ctx, x, w, cbias, pa, pb, k):
+    def forward(ctx, x, w, cbias, pa, pb, k, taps=0):
         geom = ConvGeom(k, 1, k // 2, False)
         pro = None if pa is None else (pa, pb)
-        y = ops.conv_fwd(x, w, geom, pro=pro, cbias=cbias)
-        ctx.geom, ctx.pro = geom, pro
+        y = ops.conv_fwd(x, w, geom, pro=pro, cbias=cbias, taps=taps)
+        ctx.geom, ctx.pro, ctx.taps = geom, pro, taps
         ctx.has_bias = cbias is not None
         ctx.cbias = cbias
         ctx.save_for_backward(x, w)
@@ -169,10 +169,10 @@ class CausalConvFn(torch.autograd.Function):
         if ctx.pro is not None:
             da, db = _param_grad(ctx.pro[0]), _param_grad(ctx.pro[1])
         gx, _ = ops.conv_bwd(g, x, w, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
-                             dcbias=dcb, dpro_pre=db, dpro_post=da)
+                             dcbias=dcb, dpro_pre=db, dpro_post=da, taps=ctx.taps)
         return (gx, dw, None if ctx.has_bias and dcb is ctx.cbias.grad else dcb,
                 None if da is not None and da is ctx.pro[0].grad else da,
-                None if db is not None and db is ctx.pro[1].grad else db, None)
+                None if db is not None and db is ctx.pro[1].grad else db, None, None)
 
 
 # the 16-bit weight shadow of the current forward: (FlatParams, dtype) when the parameters live in
@@ -254,6 +254,15 @@ def _embed(depth_w, height_w, width_w, k):
     return ed, eh, ew
 
 
+def _tap_mask(stream, k, wk):
+    """vq3d_conv_desc.tap_mask of the embedded kernel of stream 0 / 1 / 2 (_embed): bit
+    (i0*k + i1)*k + i2 for the taps the causal kernel occupies; the conv engines skip the others"""
+    live = {0: lambda a, b, c: a <= k - 2,
+            1: lambda a, b, c: a == 1 and b <= k - 2,
+            2: lambda a, b, c: a == 1 and b == 1 and c < wk}[stream]
+    return sum(1 << ((a * k + b) * k + c) for a in range(k) for b in range(k) for c in range(k) if live(a, b, c))
+
+
 def _shift(t, axis):
     """front-pad spatial axis (0 = d, 1 = h, 2 = w) by one and drop the last slice (the mask 'A'
     shifts, layers.py:13-100)"""
@@ -306,7 +315,8 @@ class CausalConv3dAdd(nn.Module):
                 x = _shift(_operand(x) if pro is None else _preact(x, pro), i)
             elif pro is not None:
                 pa, pb = pro
-            out.append(CausalConvFn.apply(_operand(x), w, b, pa, pb, k))
+            out.append(CausalConvFn.apply(_operand(x), w, b, pa, pb, k,
+                                          _tap_mask(i, k, self.width_conv.weight.shape[-1])))
         return out
 
     def forward(self, stack):

@@ -47,6 +47,10 @@ typedef struct vq3d_conv_desc {
     int32_t out_h, out_w, out_d;
     int32_t kernel, stride, pad, pad_mode;
     int32_t pro_kind;   /* VQ3D_PRO_* applied to the input on load */
+    uint32_t tap_mask;  /* 0: dense kernel.  Else (kernel <= 3) bit (i0*k + i1)*k + i2 set for every
+                           weight tap w[:, :, i0, i1, i2] that may be nonzero: the caller guarantees the
+                           other taps are zero (e.g. a causal kernel embedded in a k^3 one), engines may
+                           skip their products and leave their weight-gradient entries unwritten. */
 } vq3d_conv_desc;
 
 /* Forward epilogue: y = act( acc*scale + bias + cbias[co] + residual ) */

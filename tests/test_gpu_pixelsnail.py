@@ -474,3 +474,41 @@ def test_flat_weight_shadow_bitwise(gpu):
     for a, b in zip(res[0], res[1]):
         assert a[0] == b[0]
         assert all(torch.equal(x, y) for x, y in zip(a[1:], b[1:]))
+
+
+@pytest.mark.parametrize("stream", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(1, 64, 8, 32, 32), (1, 64, 5, 6, 7), (2, 32, 4, 8, 16)])
+def test_tap_mask_conv_matches_dense(gpu, stream, shape):
+    """The causal convs' tap mask (vq3d_conv_desc.tap_mask: the lines engines run their k-steps and
+    weight-gradient tiles over the live taps only) against the dense conv of the same embedded
+    kernel: forward, input gradient, prologue / bias sums and the live taps' weight gradient within
+    fp32 summation order (1e-5 of max; 1e-2 for the bf16 outputs), dead taps' gradient unwritten."""
+    from vq3d import ops, pixelsnail as PS
+    from vq3d.ops import ConvGeom
+    torch.manual_seed(stream)
+    b, c = shape[:2]
+    x = torch.randn(shape, device=gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    g = torch.randn(shape, device=gpu).to(torch.bfloat16).contiguous(memory_format=CL)
+    mask = PS._tap_mask(stream, 3, 2)
+    live = torch.tensor([(mask >> t) & 1 for t in range(27)], device=gpu, dtype=torch.bool).view(3, 3, 3)
+    w = torch.randn((c, c, 3, 3, 3), device=gpu) * 0.05 * live
+    cb = torch.randn(c, device=gpu)
+    pa, pb = torch.tensor([0.1], device=gpu), torch.tensor([-0.2], device=gpu)
+    geom = ConvGeom(3, 1, 1, False)
+    res = []
+    for taps in (0, mask):
+        y = ops.conv_fwd(x, w, geom, pro=(pa, pb), cbias=cb, taps=taps)
+        dw = torch.zeros_like(w)
+        dcb, da, db = torch.zeros_like(cb), torch.zeros(1, device=gpu), torch.zeros(1, device=gpu)
+        gx, _ = ops.conv_bwd(g, x, w, geom, pro=(pa, pb), aux=x, dw=dw, dcbias=dcb, dpro_pre=db, dpro_post=da,
+                             taps=taps)
+        ops.join_side()
+        torch.cuda.synchronize()
+        res.append((y.float(), gx.float(), dw, dcb, da, db))
+    (y0, gx0, dw0, cb0, da0, db0), (y1, gx1, dw1, cb1, da1, db1) = res
+    assert rel(y1, y0.cpu().numpy()) < 1e-2
+    assert rel(gx1, gx0.cpu().numpy()) < 1e-2
+    assert rel(dw1[..., live], dw0[..., live].cpu().numpy()) < 1e-5
+    assert not dw1[..., ~live].any()
+    for a1, a0 in ((cb1, cb0), (da1, da0), (db1, db0)):
+        assert rel(a1, a0.cpu().numpy()) < 1e-4
