@@ -285,9 +285,22 @@ def level_stream(device):
     return s
 
 
+_aux = {}
+
+
+def aux_stream(device, key):
+    """a named per-device stream (PixelSNAIL's per-stack-stream lanes), created once"""
+    k = (device.index, key)
+    s = _aux.get(k)
+    if s is None:
+        s = _aux[k] = torch.cuda.Stream(device=device)
+    return s
+
+
 def side_streams():
     """Every stream besides the current one that may hold work of the step: the weight-gradient
-    side streams and the level streams."""
+    side streams and the level streams (the aux streams are joined by their users: PixelSNAIL's
+    lanes through its forward's end and autograd's cross-stream gradient hand-offs)."""
     return list(_side.values()) + list(_levels.values())
 
 

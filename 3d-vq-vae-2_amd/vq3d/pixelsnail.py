@@ -21,6 +21,7 @@ causal Dropout3d runs per stream as in the reference; the attention's training-m
 from a device seed (CausalAttentionFn).  Mixup (pixelsnail.py:136-138, train_helpers.py:20-63)
 blends the one-hot inputs and the two targets' losses as the reference does.
 """
+import contextlib
 import ctypes
 import math
 from random import randrange
@@ -77,6 +78,101 @@ def _fused_glue():
     return _compute[0] != torch.float32
 
 
+# ---- lanes: 16-bit GPU runs put the three stack streams (depth / height / width) on three HIP
+# streams.  The streams meet only in ExpandRFConv (height and width add projections of the depth
+# / height branches) and at the output, so each stream's chain of small kernels runs concurrently
+# with the other two's; autograd runs every backward op on its forward's stream and synchronises
+# the gradient hand-offs between them.
+#
+# The one-element parameters (the blocks' bias1a .. bias4, scale) are shared by the three streams:
+# their gradient sums would be added into the same address from three streams at once.  Under
+# lanes each lane adds into its own row of a [3][n] buffer and one callback at the end of the
+# backward adds the rows in lane order into the gradients: race-free and deterministic.
+_lanes_on = [False]
+_LANES = [None]
+_CUR = [0]       # the lane the current code runs on
+_LSTATE = [None]  # the forward's _LaneGrads
+
+
+def set_lanes(enabled=True):
+    """per-stack-stream HIP streams in 16-bit GPU runs (off by default: see DESIGN.md 9)"""
+    _lanes_on[0] = bool(enabled)
+
+
+@contextlib.contextmanager
+def _lane(i):
+    """run on stream i's lane (no stream switch without lanes)"""
+    lanes = _LANES[0]
+    prev = _CUR[0]
+    _CUR[0] = i
+    try:
+        if lanes is None:
+            yield
+        else:
+            with torch.cuda.stream(lanes[i]):
+                yield
+    finally:
+        _CUR[0] = prev
+
+
+class _LaneGrads:
+    """per-lane gradient rows of the shared one-element parameters of one forward"""
+
+    def __init__(self, params, lanes, device):
+        self.params = params
+        self.slot = {id(p): j for j, p in enumerate(params)}
+        self.lanes = lanes
+        self.buf = torch.zeros((3, max(1, len(params))), dtype=torch.float32, device=device)
+        self.queued = False
+
+    def row(self, lane, p):
+        """lane's gradient slot of p (queues the flush of this backward on first use)"""
+        if not self.queued:
+            self.queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+        j = self.slot[id(p)]
+        return self.buf[lane, j:j + 1]
+
+    def flush(self):
+        """on the forward's main lane (the callback may run on autograd's device thread, whose
+        current stream is not the caller's): wait for the other lanes, add the rows in order"""
+        from .functional import grad_buf
+        main = self.lanes[0]
+        with torch.cuda.stream(main):
+            for s in self.lanes[1:]:
+                main.wait_stream(s)
+            sums = self.buf.sum(0).view(-1, 1)
+            torch._foreach_add_([grad_buf(p) for p in self.params], list(sums[:len(self.params)].unbind()))
+        self.queued = False
+
+
+def _lane_ctx():
+    """(the forward's _LaneGrads, this op's lane) for an autograd Function's ctx, or None"""
+    st = _LSTATE[0]
+    return None if st is None else (st, _CUR[0])
+
+
+def _sgrad(lst, p):
+    """the buffer a kernel adds p's gradient into: the lane row of a shared one-element parameter
+    under lanes, else _param_grad(p)"""
+    if lst is not None and id(p) in lst[0].slot:
+        return lst[0].row(lst[1], p)
+    return _param_grad(p)
+
+
+
+def _take(i, j, *ts):
+    """lane i is about to use tensors made on lane j: it waits for lane j's work so far, and the
+    allocator keeps the tensors' memory until lane i's use is done"""
+    lanes = _LANES[0]
+    if lanes is None or i == j:
+        return
+    lanes[i].wait_stream(lanes[j])
+    for t in ts:
+        if t is not None:
+            t.record_stream(lanes[i])
+
+
 class PreActFn(torch.autograd.Function):
     """elu(x + a) + b straight into the conv operand format (layers.py:425-432 pre-activation +
     the autocast of the conv input): one launch; backward one launch with the a / b gradient sums
@@ -90,18 +186,19 @@ class PreActFn(torch.autograd.Function):
                L.ptr(y), L.stream())
         ctx.save_for_backward(x)
         ctx.prm = (a, b)
+        ctx.lst = _lane_ctx()
         return y
 
     @staticmethod
     def backward(ctx, g):
-        from .functional import grad_buf
         (x,) = ctx.saved_tensors
         a, b = ctx.prm
         g = cl(g)
         gx = torch.empty_like(x, memory_format=CL) if ctx.needs_input_grad[0] else None
+        da, db = _sgrad(ctx.lst, a), _sgrad(ctx.lst, b)
         L.call("vq3d_preact_act_bwd", L.dtype_code(g), L.dtype_code(x), x.numel(), L.ptr(g), L.ptr(x), L.ptr(a),
-               None if gx is None else L.ptr(gx), L.ptr(grad_buf(a)), L.ptr(grad_buf(b)), L.stream())
-        return gx, None, None
+               None if gx is None else L.ptr(gx), L.ptr(da), L.ptr(db), L.stream())
+        return gx, None if _is_param(a) else da, None if _is_param(b) else db
 
 
 class ScaleBiasResFn(torch.autograd.Function):
@@ -118,18 +215,20 @@ class ScaleBiasResFn(torch.autograd.Function):
                L.ptr(out), L.stream())
         ctx.save_for_backward(o)
         ctx.prm = (scale, bias)
+        ctx.lst = _lane_ctx()
         return out
 
     @staticmethod
     def backward(ctx, g):
-        from .functional import grad_buf
         (o,) = ctx.saved_tensors
         scale, bias = ctx.prm
         g = cl(g).float()
         go = torch.empty_like(o, memory_format=CL) if ctx.needs_input_grad[0] else None
+        ds, dbi = _sgrad(ctx.lst, scale), _sgrad(ctx.lst, bias)
         L.call("vq3d_scale_bias_res_bwd", L.dtype_code(o), o.numel(), L.ptr(g), L.ptr(o), L.ptr(scale),
-               None if go is None else L.ptr(go), L.ptr(grad_buf(scale)), L.ptr(grad_buf(bias)), L.stream())
-        return go, None, None, (g if ctx.needs_input_grad[3] else None)
+               None if go is None else L.ptr(go), L.ptr(ds), L.ptr(dbi), L.stream())
+        return (go, None if _is_param(scale) else ds, None if _is_param(bias) else dbi,
+                (g if ctx.needs_input_grad[3] else None))
 
 
 def _preact(x, pro):
@@ -151,6 +250,7 @@ class CausalConvFn(torch.autograd.Function):
         pro = None if pa is None else (pa, pb)
         y = ops.conv_fwd(x, w, geom, pro=pro, cbias=cbias, taps=taps)
         ctx.geom, ctx.pro, ctx.taps = geom, pro, taps
+        ctx.lst = _lane_ctx()
         ctx.has_bias = cbias is not None
         ctx.cbias = cbias
         ctx.save_for_backward(x, w)
@@ -165,14 +265,14 @@ class CausalConvFn(torch.autograd.Function):
         # into their gradient buffers (the kernels add), no zeroed temporaries and accumulations
         dcb = da = db = None
         if ctx.has_bias:
-            dcb = _param_grad(ctx.cbias)
+            dcb = _sgrad(ctx.lst, ctx.cbias)
         if ctx.pro is not None:
-            da, db = _param_grad(ctx.pro[0]), _param_grad(ctx.pro[1])
+            da, db = _sgrad(ctx.lst, ctx.pro[0]), _sgrad(ctx.lst, ctx.pro[1])
         gx, _ = ops.conv_bwd(g, x, w, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
                              dcbias=dcb, dpro_pre=db, dpro_post=da, taps=ctx.taps)
-        return (gx, dw, None if ctx.has_bias and dcb is ctx.cbias.grad else dcb,
-                None if da is not None and da is ctx.pro[0].grad else da,
-                None if db is not None and db is ctx.pro[1].grad else db, None, None)
+        return (gx, dw, None if dcb is None or _is_param(ctx.cbias) else dcb,
+                None if da is None or _is_param(ctx.pro[0]) else da,
+                None if db is None or _is_param(ctx.pro[1]) else db, None, None)
 
 
 # the 16-bit weight shadow of the current forward: (FlatParams, dtype) when the parameters live in
@@ -245,13 +345,18 @@ def _embed(depth_w, height_w, width_w, k):
     """the three causal kernels inside k^3 kernels (k = 3): taps the reference never reads are 0.
     depth (k-1, k, k) at kd = 0 .. k-2 (front pad k-2 = offsets -1, 0); height (1, k-1, k) at
     kd = 1, kh = 0 .. k-2; width (1, 1, wk) at kd = kh = 1, kw = 0 .. wk-1."""
+    return tuple(_embed_one(i, w, k) for i, w in enumerate((depth_w, height_w, width_w)))
+
+
+def _embed_one(i, w, k):
+    """stream i's kernel of _embed"""
     if k == 1:
-        return depth_w, height_w, width_w
-    wk = width_w.shape[-1]
-    ed = F.pad(depth_w, (0, 0, 0, 0, 0, 1))
-    eh = F.pad(height_w, (0, 0, 0, 1, 1, 1))
-    ew = F.pad(width_w, (0, 3 - wk, 1, 1, 1, 1))
-    return ed, eh, ew
+        return w
+    if i == 0:
+        return F.pad(w, (0, 0, 0, 0, 0, 1))
+    if i == 1:
+        return F.pad(w, (0, 0, 0, 1, 1, 1))
+    return F.pad(w, (0, 3 - w.shape[-1], 1, 1, 1, 1))
 
 
 def _tap_mask(stream, k, wk):
@@ -296,28 +401,32 @@ class CausalConv3dAdd(nn.Module):
 
     def run(self, stack, pro=None):
         """stack: list of 3 channels-last tensors; pro = (a, b): every input goes through
-        elu(x + a) + b first (fused as the conv prologue unless mask 'A' has to shift it)."""
+        elu(x + a) + b first (fused as the conv prologue unless mask 'A' has to shift it).
+        Stream i runs on its lane."""
+        out = []
+        for i, x in enumerate(stack):
+            with _lane(i):
+                out.append(self.run_one(i, x, pro))
+        return out
+
+    def run_one(self, i, x, pro=None):
+        """stream i (0 depth, 1 height, 2 width) of run, on the current stream"""
         k = self.kernel_size
         if k not in (1, 3):
             raise NotImplementedError("causal conv kernel sizes 1 and 3 (the reference's default) are supported")
-        ws = _embed(self.depth_conv.weight, self.height_conv.weight, self.width_conv.weight, k)
-        bs = (self.depth_conv.bias, self.height_conv.bias, self.width_conv.bias)
-        out = []
-        for i, (x, w, b) in enumerate(zip(stack, ws, bs)):
-            if k == 1:  # a plain GEMM over the voxels (hipBLASLt): pre-activation + shift as glue
-                x = _operand(x) if pro is None else _preact(x, pro)
-                if self.mask == "A":
-                    x = _shift(x, i)
-                out.append(pointwise(x, w, b))
-                continue
-            pa = pb = None
+        conv = (self.depth_conv, self.height_conv, self.width_conv)[i]
+        w, b = _embed_one(i, conv.weight, k), conv.bias
+        if k == 1:  # a plain GEMM over the voxels (hipBLASLt): pre-activation + shift as glue
+            x = _operand(x) if pro is None else _preact(x, pro)
             if self.mask == "A":
-                x = _shift(_operand(x) if pro is None else _preact(x, pro), i)
-            elif pro is not None:
-                pa, pb = pro
-            out.append(CausalConvFn.apply(_operand(x), w, b, pa, pb, k,
-                                          _tap_mask(i, k, self.width_conv.weight.shape[-1])))
-        return out
+                x = _shift(x, i)
+            return pointwise(x, w, b)
+        pa = pb = None
+        if self.mask == "A":
+            x = _shift(_operand(x) if pro is None else _preact(x, pro), i)
+        elif pro is not None:
+            pa, pb = pro
+        return CausalConvFn.apply(_operand(x), w, b, pa, pb, k, _tap_mask(i, k, self.width_conv.weight.shape[-1]))
 
     def forward(self, stack):
         return torch.stack(self.run(to_list(stack)))
@@ -339,10 +448,19 @@ class ExpandRFConv(nn.Module):
 
     def run(self, stack):
         d, h, w = stack
-        dc = pointwise(_operand(d), self.depth_conv.weight, self.depth_conv.bias)
-        dch, dcw = torch.chunk(dc, 2, dim=1)
-        hc = pointwise(_operand(h), self.height_conv.weight, self.height_conv.bias)
-        return [d, cl(h + dch), cl(w + hc + dcw)]
+        # on lane 0 (the lanes only ever synchronise with lane 0: side-to-side waits inside a
+        # captured multi-stream backward crash hipStreamEndCapture on this ROCm)
+        with _lane(0):
+            _take(0, 1, h)
+            _take(0, 2, w)
+            dc = pointwise(_operand(d), self.depth_conv.weight, self.depth_conv.bias)
+            dch, dcw = torch.chunk(dc, 2, dim=1)
+            hc = pointwise(_operand(h), self.height_conv.weight, self.height_conv.bias)
+            h2 = cl(h + dch)
+            w2 = cl(w + hc + dcw)
+        _take(1, 0, h2)
+        _take(2, 0, w2)
+        return [d, h2, w2]
 
     def forward(self, stack):
         return torch.stack(self.run(to_list(stack)))
@@ -390,20 +508,26 @@ class PreActFixupCausalResBlock(nn.Module):
         self.dropout = nn.Dropout3d(dropout_prob) if dropout_prob > 0 else None
 
     def run(self, stack, aux=None):
+        """each stream on its lane; the streams meet in expand_rf"""
         out = self.branch_conv1.run(stack, pro=(self.bias1a, self.bias1b))
         out = self.expand_rf.run(out)
-        if aux is not None:
-            assert self.aux is not None
-            a = self.aux.run([cl(F.elu(t)) for t in aux])
-            out = [cl(o + t) for o, t in zip(out, a)]
-        out = self.branch_conv2.run(out, pro=(self.bias2a, self.bias2b))
-        out = _dropout3d(out, self.dropout)
-        out = self.branch_conv3.run(out, pro=(self.bias3a, self.bias3b))
-        skip = stack if self.skip_conv is None else self.skip_conv.run(stack)
-        # out * scale + bias4 + skip: fp32 (the 1-element fp32 parameters promote, as in the reference)
-        if _fused_glue():
-            return [ScaleBiasResFn.apply(o, self.scale, self.bias4, s) for o, s in zip(out, skip)]
-        return [cl(o * self.scale + self.bias4 + s) for o, s in zip(out, skip)]
+        res = []
+        for i in range(3):
+            with _lane(i):
+                o = out[i]
+                if aux is not None:
+                    assert self.aux is not None
+                    o = cl(o + self.aux.run_one(i, cl(F.elu(aux[i]))))
+                o = self.branch_conv2.run_one(i, o, pro=(self.bias2a, self.bias2b))
+                o = _dropout3d([o], self.dropout)[0]
+                o = self.branch_conv3.run_one(i, o, pro=(self.bias3a, self.bias3b))
+                s = stack[i] if self.skip_conv is None else self.skip_conv.run_one(i, stack[i])
+                # o * scale + bias4 + skip: fp32 (the 1-element fp32 parameters promote, as in the reference)
+                if _fused_glue():
+                    res.append(ScaleBiasResFn.apply(o, self.scale, self.bias4, s))
+                else:
+                    res.append(cl(o * self.scale + self.bias4 + s))
+        return res
 
     def forward(self, stack, aux=None, condition=None, condition_cache=None):
         if condition is not None or condition_cache is not None:
@@ -502,14 +626,22 @@ class CausalAttention(nn.Module):
         return [seeds[i:i + 1] for i in range(3)]
 
     def run(self, keys, queries, values):
+        """stream i on its lane (the training seeds are drawn on lane 0)"""
         nh = self.num_heads
         assert values[0].shape[1] % nh == 0 and keys[0].shape[1] % nh == 0
+        train = [None] * 3
         if self.dropout.training:
             p = float(self.dropout.p)
-            seeds = self._seeds(keys[0].device) if p > 0 else [None] * 3
-            return [CausalAttentionFn.apply(cl(q), cl(k), cl(v), nh, (p, sd))
-                    for q, k, v, sd in zip(queries, keys, values, seeds)]
-        return [CausalAttentionFn.apply(cl(q), cl(k), cl(v), nh) for q, k, v in zip(queries, keys, values)]
+            with _lane(0):
+                seeds = self._seeds(keys[0].device) if p > 0 else [None] * 3
+            train = [(p, sd) for sd in seeds]
+        out = []
+        for i, (q, k, v) in enumerate(zip(queries, keys, values)):
+            with _lane(i):
+                if train[i] is not None and train[i][1] is not None:
+                    _take(i, 0, train[i][1])
+                out.append(CausalAttentionFn.apply(cl(q), cl(k), cl(v), nh, train[i]))
+        return out
 
     def forward(self, keys, queries, values, attn_mask=None):
         return torch.stack(self.run(to_list(keys), to_list(queries), to_list(values)))
@@ -533,10 +665,15 @@ class CausalAttentionPixelBlock(nn.Module):
         out = stack
         for layer in self.causal_layers:
             out = layer.run(out)
-        kv = self.key_value_proj.run([cl(torch.cat([s, o, g], dim=1)) for s, o, g in zip(stack, out, bg)])
-        keys, values = zip(*(torch.chunk(t, 2, dim=1) for t in kv))
-        queries = self.query_proj.run([cl(torch.cat([o, g], dim=1)) for o, g in zip(out, bg)])
-        att = self.causal_attention.run(list(queries), list(keys), list(values))
+        keys, values, queries = [], [], []
+        for i in range(3):
+            with _lane(i):
+                kv = self.key_value_proj.run_one(i, cl(torch.cat([stack[i], out[i], bg[i]], dim=1)))
+                k, v = torch.chunk(kv, 2, dim=1)
+                keys.append(k)
+                values.append(v)
+                queries.append(self.query_proj.run_one(i, cl(torch.cat([out[i], bg[i]], dim=1))))
+        att = self.causal_attention.run(queries, keys, values)
         return self.out_proj.run(out, aux=att)
 
     def forward(self, stack, background, attn_mask=None, condition=None, condition_cache=None):
@@ -640,10 +777,28 @@ class PixelSNAIL(nn.Module):
                 fl.refresh_shadow(self.compute_dtype)
                 _shadow[0] = (fl, self.compute_dtype)
         x = cl(pointwise(x, self.parse_input.weight, self.parse_input.bias))
-        stack = self.to_causal.run([x, x, x])
         bg = background_list(b, dims, self.compute_dtype, x.device)
-        for layer in self.layers:
-            stack = layer.run(stack, bg)
+        lanes = None
+        if _lanes_on[0] and self.compute_dtype != torch.float32 and x.is_cuda:
+            main = torch.cuda.current_stream()
+            lanes = [main, ops.aux_stream(x.device, "psnail_lane1"), ops.aux_stream(x.device, "psnail_lane2")]
+        _LANES[0] = lanes
+        if lanes is not None:
+            shared = [p for p in self.parameters() if p.numel() == 1]
+            _LSTATE[0] = _LaneGrads(shared, lanes, x.device)
+        try:
+            for i in (1, 2):
+                _take(i, 0, x, bg[0])
+            stack = self.to_causal.run([x, x, x])
+            for layer in self.layers:
+                stack = layer.run(stack, bg)
+            for i in (1, 2):
+                if lanes is not None:
+                    lanes[0].wait_stream(lanes[i])
+                    stack[i].record_stream(lanes[0])
+        finally:
+            _LANES[0] = None
+            _LSTATE[0] = None
         s = _operand(stack[0] + stack[1] + stack[2])
         return pointwise(s, self.parse_output.weight, self.parse_output.bias).float()
 
