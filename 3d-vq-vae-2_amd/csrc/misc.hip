@@ -62,6 +62,7 @@ float *pair_pool(unsigned slot) {
 namespace vq3d {
 
 static unsigned grid_for(int64_t n) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048))); }
+static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // ============================================================================ reconstruction loss
 __device__ __forceinline__ bool in_cylinder(int h, int w, int H, int W) {
@@ -446,6 +447,73 @@ __global__ __launch_bounds__(256) void k_preact_act_bwd(int64_t n, const TG *__r
     sb = block_sum<float, 256>(sb, red + 4);
     grid_sum2<256>(gsum, sa, sb, da, db, red);
 }
+// 4 consecutive elements (16-byte fp32 / 8-byte 16-bit accesses)
+__device__ __forceinline__ void ld4(const float *p, float v[4]) {
+    const float4 q = *reinterpret_cast<const float4 *>(p);
+    v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+}
+__device__ __forceinline__ void ld4(const h16_t *p, float v[4]) {
+    const u32x2 q = *reinterpret_cast<const u32x2 *>(p);
+    v[0] = h2f_lo(q[0]), v[1] = h2f_hi(q[0]), v[2] = h2f_lo(q[1]), v[3] = h2f_hi(q[1]);
+}
+__device__ __forceinline__ void st4(float *p, const float v[4]) {
+    *reinterpret_cast<float4 *>(p) = float4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ void st4(h16_t *p, const float v[4]) {
+    *reinterpret_cast<u32x2 *>(p) = u32x2{uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16),
+                                          uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16)};
+}
+// the backward glue reductions 4 elements per thread-step on <= 512 workgroups (fewer partials
+// for the in-grid sum): n4 = n / 4
+template <typename TG, typename TX>
+__global__ __launch_bounds__(256) void k_preact_act_bwd4(int64_t n4, const TG *__restrict__ g,
+                                                        const TX *__restrict__ x, const float *a,
+                                                        TX *__restrict__ gx, float *da, float *db, GridSum gsum) {
+    __shared__ float red[8];
+    const float av = *a;
+    float sa = 0.f, sb = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
+        float gv[4], xv[4], v[4];
+        ld4(g + 4 * i, gv);
+        ld4(x + 4 * i, xv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = gv[j] * elu_grad(xv[j] + av);
+            sa += v[j];
+            sb += gv[j];
+        }
+        if (gx) st4(gx + 4 * i, v);
+    }
+    sa = block_sum<float, 256>(sa, red);
+    sb = block_sum<float, 256>(sb, red + 4);
+    grid_sum2<256>(gsum, sa, sb, da, db, red);
+}
+template <typename TO>
+__global__ __launch_bounds__(256) void k_scale_bias_res_bwd4(int64_t n4, const float *__restrict__ g,
+                                                            const TO *__restrict__ o, const float *scale,
+                                                            TO *__restrict__ go, float *dscale, float *dbias,
+                                                            GridSum gsum) {
+    __shared__ float red[8];
+    const float sc = *scale;
+    float ss = 0.f, sb = 0.f;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
+        float gv[4], ov[4], v[4];
+        ld4(g + 4 * i, gv);
+        ld4(o + 4 * i, ov);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = gv[j] * sc;
+            ss = fmaf(gv[j], ov[j], ss);
+            sb += gv[j];
+        }
+        if (go) st4(go + 4 * i, v);
+    }
+    ss = block_sum<float, 256>(ss, red);
+    sb = block_sum<float, 256>(sb, red + 4);
+    grid_sum2<256>(gsum, ss, sb, dscale, dbias, red);
+}
+static unsigned grid4_for(int64_t n4) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 512))); }
+
 // out = o * scale + bias + s; backward go = g * scale, the scale / bias sums
 template <typename TO>
 __global__ __launch_bounds__(256) void k_scale_bias_res_fwd(int64_t n, const TO *__restrict__ o, const float *scale,
@@ -532,7 +600,6 @@ int64_t vq3d_cylinder_count(int32_t h, int32_t w) {
     return c;
 }
 
-static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int vq3d_parse_input_fwd(int32_t dtype, int64_t voxels, int32_t channels, const float *x, const float *w,
                          const float *b, void *y, vq3d_stream_t stream) {
@@ -827,6 +894,20 @@ int vq3d_preact_act_bwd(int32_t g_dtype, int32_t x_dtype, int64_t n, const void 
     if (!glue_dtype(g_dtype) || !glue_dtype(x_dtype)) return fail("preact_act_bwd: dtype");
     if (!g || !x || !a) return fail("preact_act_bwd: null pointer");
     hipStream_t s = as_stream(stream);
+    if (n % 4 == 0 && al16(g) && al16(x) && (!gx || al16(gx))) {
+        const unsigned nb4 = grid4_for(n / 4);
+        const GridSum gs4 = grid_sum_for(s, nb4, da || db);
+#define PAB4(TG, TX) k_preact_act_bwd4<TG, TX><<<nb4, 256, 0, s>>>(n / 4, (const TG *)g, (const TX *)x, a, (TX *)gx, da, db, gs4)
+        if (g_dtype == VQ3D_F32) {
+            if (x_dtype == VQ3D_F32) PAB4(float, float);
+            else PAB4(float, h16_t);
+        } else {
+            if (x_dtype == VQ3D_F32) PAB4(h16_t, float);
+            else PAB4(h16_t, h16_t);
+        }
+#undef PAB4
+        return check_launch("preact_act_bwd");
+    }
     const unsigned nb = grid_for(n);
     const GridSum gs = grid_sum_for(s, nb, da || db);
 #define PAB(TG, TX) k_preact_act_bwd<TG, TX><<<nb, 256, 0, s>>>(n, (const TG *)g, (const TX *)x, a, (TX *)gx, da, db, gs)
@@ -860,6 +941,17 @@ int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const vo
     hipStream_t s = as_stream(stream);
     const unsigned nb = grid_for(n);
     const GridSum gs = grid_sum_for(s, nb, dscale || dbias);
+    if (n % 4 == 0 && al16(g) && al16(o) && (!go || al16(go))) {
+        const unsigned nb4 = grid4_for(n / 4);
+        const GridSum gs4 = grid_sum_for(s, nb4, dscale || dbias);
+        if (o_dtype == VQ3D_F32)
+            k_scale_bias_res_bwd4<float><<<nb4, 256, 0, s>>>(n / 4, g, (const float *)o, scale, (float *)go, dscale,
+                                                             dbias, gs4);
+        else
+            k_scale_bias_res_bwd4<h16_t><<<nb4, 256, 0, s>>>(n / 4, g, (const h16_t *)o, scale, (h16_t *)go, dscale,
+                                                             dbias, gs4);
+        return check_launch("scale_bias_res_bwd");
+    }
     if (o_dtype == VQ3D_F32)
         k_scale_bias_res_bwd<float><<<nb, 256, 0, s>>>(n, g, (const float *)o, scale, (float *)go, dscale, dbias, gs);
     else

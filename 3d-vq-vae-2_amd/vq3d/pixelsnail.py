@@ -88,14 +88,14 @@ def _fused_glue():
 # their gradient sums would be added into the same address from three streams at once.  Under
 # lanes each lane adds into its own row of a [3][n] buffer and one callback at the end of the
 # backward adds the rows in lane order into the gradients: race-free and deterministic.
-_lanes_on = [False]
+_lanes_on = [True]
 _LANES = [None]
 _CUR = [0]       # the lane the current code runs on
 _LSTATE = [None]  # the forward's _LaneGrads
 
 
 def set_lanes(enabled=True):
-    """per-stack-stream HIP streams in 16-bit GPU runs (off by default: see DESIGN.md 9)"""
+    """per-stack-stream HIP streams in 16-bit GPU runs (on by default)"""
     _lanes_on[0] = bool(enabled)
 
 

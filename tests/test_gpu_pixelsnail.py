@@ -541,7 +541,7 @@ def test_lanes_match_single_stream_and_repeat_bitwise(gpu):
             torch.cuda.synchronize()
             res.append([float(loss)] + [p.grad.detach().clone() for p in m.parameters()])
     finally:
-        PS.set_lanes(False)
+        PS.set_lanes(True)
     single, lane_a, lane_b = res
     assert lane_a[0] == lane_b[0] and all(torch.equal(x, y) for x, y in zip(lane_a[1:], lane_b[1:]))
     assert abs(single[0] - lane_a[0]) <= 1e-6 * abs(single[0])

@@ -15,8 +15,7 @@ if mode == "bwd_emptyflush":
     def _nop(self):
         self.queued = False
     PS._LaneGrads.flush = _nop
-if mode == "bwd_nolanes":
-    PS.set_lanes(False)
+PS.set_lanes(mode != "bwd_nolanes")
 gpu = torch.device("cuda:0")
 torch.manual_seed(0)
 args = PS.default_args(num_embeddings=[16, 0], model_dim=32, num_blocks=1, num_layers_per_block=1,
