@@ -6,6 +6,8 @@ tag=${1:-r05x}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$tag.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_$tag.log; [ $rc -eq 0 ] || { grep -E "^FAILED|^E " gpurun_out/pytest_$tag.log | head; exit $rc; }
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$tag.log 2>&1 || { tail -20 gpurun_out/smoke_$tag.log; exit 1; }
+tail -2 gpurun_out/smoke_$tag.log
 rm -rf gpurun_out/trace_$tag
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_$tag -o run --output-format csv -- \
     python3 bench.py --steps 4 --warmup 3 --no-cpu-baseline --no-roofline > gpurun_out/trace_$tag.log 2>&1 \
