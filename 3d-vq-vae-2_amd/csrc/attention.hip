@@ -385,6 +385,10 @@ constexpr int MQ = ATTN_MQ, MK = 128, VTP = MK + 8, MNT = 2 * MQ;  // MNT: threa
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
 
+// 2^x as the bare v_exp_f32 (results below 2^-126 flush to zero -- probabilities that round to
+// zero in the fp16 P / dS operands anyway; -inf -> 0): the matrix-core kernels' per-score exps
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 mma_qk(u32x2 kf, u32x2 qf, f32x16 acc) {
 #ifdef VQ3D_FP16
     typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
             }
             bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
             const float mn = fmaxf(m, bm);  // finite: key 0 of the block precedes every query of it
-            const float alpha = exp2f(m - mn);
+            const float alpha = fexp2(m - mn);
             m = mn;
             l *= alpha;
 #pragma unroll
@@ -460,7 +464,7 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
             f16x8v pb0, pb1;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float pr = exp2f(st[r] - mn);
+                const float pr = fexp2(st[r] - mn);
                 l += pr;
                 if (r < 8) pb0[r] = _Float16(pr);
                 else pb1[r - 8] = _Float16(pr);
@@ -587,7 +591,7 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_q_mma(AttnArgs a, float scale,
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
                 float g;
                 const float t = tlogit(a, c2k, zrep, drop, seed, int(blockIdx.y), i, kb * 32 + row, st[r], g);
-                float pr = exp2f(t - lz);
+                float pr = fexp2(t - lz);
                 if (DIAG) pr = row > col ? 0.f : pr;
                 const _Float16 ds = _Float16(g * pr * (dp[r] - dl));
                 if (r < 8) d0[r] = ds;
@@ -666,7 +670,7 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_kv_mma(AttnArgs a, float scale
                     const int r = 4 * jj + u, row = u + 8 * jj + 4 * hh;  // query within the block
                     float g;
                     const float t = tlogit(a, c2k, zrep, drop, seed, int(blockIdx.y), ib * 32 + row, j, st[r], g);
-                    float pr = exp2f(t - lv[u]);
+                    float pr = fexp2(t - lv[u]);
                     if (DIAG) pr = row < col ? 0.f : pr;
                     const _Float16 ph = _Float16(pr), ds = _Float16(g * pr * (dp[r] - dv4[u]));
                     if (r < 8) {
