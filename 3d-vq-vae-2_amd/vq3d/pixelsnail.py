@@ -88,15 +88,17 @@ def _fused_glue():
 # their gradient sums would be added into the same address from three streams at once.  Under
 # lanes each lane adds into its own row of a [3][n] buffer and one callback at the end of the
 # backward adds the rows in lane order into the gradients: race-free and deterministic.
-_lanes_on = [True]
+_lanes_on = [False]  # off: a captured lanes step's gradients differ between replays
 _LANES = [None]
 _CUR = [0]       # the lane the current code runs on
 _LSTATE = [None]  # the forward's _LaneGrads
 
 
-def set_lanes(enabled=True):
-    """per-stack-stream HIP streams in 16-bit GPU runs (on by default)"""
-    _lanes_on[0] = bool(enabled)
+def set_lanes(enabled="graph"):
+    """per-stack-stream HIP streams in 16-bit GPU runs: "graph" inside HIP-graph captures only, True
+    also in eager runs, False never (the default: see DESIGN.md 9 -- a captured lanes step's
+    gradients differ between replays, a cross-stream race not yet found)"""
+    _lanes_on[0] = enabled if enabled == "graph" else bool(enabled)
 
 
 @contextlib.contextmanager
@@ -161,16 +163,42 @@ def _sgrad(lst, p):
 
 
 
+class _Handoff(torch.autograd.Function):
+    """a tensor crossing from lane j to lane i (applied on lane i).  Backward runs on lane i and hands
+    the gradient back to lane j: the gradient's memory (allocated on lane i) is recorded on lane j,
+    so the allocator cannot give it to lane i's next allocation while lane j still reads it (the
+    cross-stream reuse hazard autograd leaves to the caller)."""
+
+    @staticmethod
+    def forward(ctx, t, src):
+        ctx.src = src
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g.record_stream(ctx.src)
+        return g, None
+
+
 def _take(i, j, *ts):
-    """lane i is about to use tensors made on lane j: it waits for lane j's work so far, and the
-    allocator keeps the tensors' memory until lane i's use is done"""
+    """lane i is about to use tensors made on lane j: it waits for lane j's work so far, the
+    allocator keeps the tensors' memory until lane i's use is done, and the tensors that need a
+    gradient come back wrapped in _Handoff (their gradients cross back to lane j).  Returns the
+    tensors (unchanged without lanes)."""
     lanes = _LANES[0]
     if lanes is None or i == j:
-        return
+        return ts if len(ts) != 1 else ts[0]
     lanes[i].wait_stream(lanes[j])
-    for t in ts:
-        if t is not None:
-            t.record_stream(lanes[i])
+    out = []
+    with torch.cuda.stream(lanes[i]):
+        for t in ts:
+            if t is not None:
+                t.record_stream(lanes[i])
+                if t.requires_grad:
+                    t = _Handoff.apply(t, lanes[j])
+            out.append(t)
+    return out if len(out) != 1 else out[0]
 
 
 class PreActFn(torch.autograd.Function):
@@ -451,16 +479,14 @@ class ExpandRFConv(nn.Module):
         # on lane 0 (the lanes only ever synchronise with lane 0: side-to-side waits inside a
         # captured multi-stream backward crash hipStreamEndCapture on this ROCm)
         with _lane(0):
-            _take(0, 1, h)
-            _take(0, 2, w)
+            h = _take(0, 1, h)
+            w = _take(0, 2, w)
             dc = pointwise(_operand(d), self.depth_conv.weight, self.depth_conv.bias)
             dch, dcw = torch.chunk(dc, 2, dim=1)
             hc = pointwise(_operand(h), self.height_conv.weight, self.height_conv.bias)
             h2 = cl(h + dch)
             w2 = cl(w + hc + dcw)
-        _take(1, 0, h2)
-        _take(2, 0, w2)
-        return [d, h2, w2]
+        return [d, _take(1, 0, h2), _take(2, 0, w2)]
 
     def forward(self, stack):
         return torch.stack(self.run(to_list(stack)))
@@ -780,22 +806,20 @@ class PixelSNAIL(nn.Module):
         bg = background_list(b, dims, self.compute_dtype, x.device)
         lanes = None
         if _lanes_on[0] and self.compute_dtype != torch.float32 and x.is_cuda:
-            main = torch.cuda.current_stream()
-            lanes = [main, ops.aux_stream(x.device, "psnail_lane1"), ops.aux_stream(x.device, "psnail_lane2")]
+            # (the lane streams exist before any capture: created on the first eager forward)
+            aux = [ops.aux_stream(x.device, "psnail_lane1"), ops.aux_stream(x.device, "psnail_lane2")]
+            if _lanes_on[0] is True or torch.cuda.is_current_stream_capturing():
+                lanes = [torch.cuda.current_stream()] + aux
         _LANES[0] = lanes
         if lanes is not None:
             shared = [p for p in self.parameters() if p.numel() == 1]
             _LSTATE[0] = _LaneGrads(shared, lanes, x.device)
         try:
-            for i in (1, 2):
-                _take(i, 0, x, bg[0])
-            stack = self.to_causal.run([x, x, x])
+            xs = [x] + [_take(i, 0, x, bg[0])[0] for i in (1, 2)]
+            stack = self.to_causal.run(xs)
             for layer in self.layers:
                 stack = layer.run(stack, bg)
-            for i in (1, 2):
-                if lanes is not None:
-                    lanes[0].wait_stream(lanes[i])
-                    stack[i].record_stream(lanes[0])
+            stack = [stack[0]] + [_take(0, i, stack[i]) for i in (1, 2)]
         finally:
             _LANES[0] = None
             _LSTATE[0] = None
