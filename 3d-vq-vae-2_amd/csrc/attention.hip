@@ -376,17 +376,27 @@ __global__ __launch_bounds__(NT) void k_attn_bwd_kv(AttnArgs a, float scale, con
 // half h <-> key (j & 3) + 8 (j >> 2) + 4 h; V^T is read in that key order).  O^T's rows are the 8
 // value dims (rows 8 .. 31 of the A operand are zero): lane (n, h) ends with dims 4h .. 4h + 3 of
 // query n.  Arithmetic: q . k products of the stored 16-bit values accumulated in fp32 and scaled in
-// fp32 (the VALU kernel scales q first), P and V as fp16 in the P V product (P in [0, 1]: 11-bit
-// mantissa) with fp32 accumulation, l summed in fp32.
+// fp32 (the VALU kernel scales q first), P and V in the build's 16-bit format in the P V product
+// with fp32 accumulation, l summed in fp32.
 #ifndef ATTN_MQ
 #define ATTN_MQ 128
 #endif
 constexpr int MQ = ATTN_MQ, MK = 128, VTP = MK + 8, MNT = 2 * MQ;  // MNT: threads (a wave per 32 queries)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+// the second products' operand format (P, V^T, dO^T, dS, K^T, Q^T): the build's own 16-bit format.
+// bf16 builds run them on v_mfma_f32_32x32x16_bf16: bf16 keeps fp32's exponent range, so the small
+// dO / dS of an unscaled bf16 loss (1e-5 .. 1e-8 per element) and large V rows stay representable
+// (fp16 operands would flush them below 6.1e-5 / overflow above 65504).
+typedef half_t f16x8v __attribute__((ext_vector_type(8)));
+#ifdef VQ3D_FP16
+#define ATT_MFMA_32X32X16 __builtin_amdgcn_mfma_f32_32x32x16_f16
+#else
+#define ATT_MFMA_32X32X16 __builtin_amdgcn_mfma_f32_32x32x16_bf16
+#endif
 
-// 2^x as the bare v_exp_f32 (results below 2^-126 flush to zero -- probabilities that round to
-// zero in the fp16 P / dS operands anyway; -inf -> 0): the matrix-core kernels' per-score exps
+// 2^x as the bare v_exp_f32 (results below 2^-126 flush to zero: probabilities below 2^-126 of the
+// row's largest, which the fp16 build's P / dS operands flush anyway; -inf -> 0): the matrix-core
+// kernels' per-score exps
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ f32x16 mma_qk(u32x2 kf, u32x2 qf, f32x16 acc) {
@@ -405,7 +415,7 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
                                                       const h16_t *__restrict__ k, const h16_t *__restrict__ v,
                                                       h16_t *__restrict__ out, float *__restrict__ lse) {
     __shared__ __attribute__((aligned(16))) h16_t ks[MK * 8];    // [key][dim], the stored format
-    __shared__ __attribute__((aligned(16))) _Float16 vt[8 * VTP];  // [dim][key], fp16
+    __shared__ __attribute__((aligned(16))) half_t vt[8 * VTP];  // [dim][key], the 16-bit format
     const int nqt = (a.n + MQ - 1) / MQ, qt = nqt - 1 - int(blockIdx.x);
     const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
     const int tid = int(threadIdx.x), lane = tid & 63, w = tid >> 6, col = lane & 31, hh = lane >> 5;
@@ -421,7 +431,7 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
     const int nkt = (qt * MQ + MQ + MK - 1) / MK;  // key tiles up to the workgroup's last query
     for (int kt = 0; kt < nkt; ++kt) {
         __syncthreads();
-        for (int e = tid; e < 2 * MK; e += MNT) {  // K rows, then V rows (transposed to fp16 V^T)
+        for (int e = tid; e < 2 * MK; e += MNT) {  // K rows, then V rows (transposed V^T)
             const int t = e & (MK - 1), kc = min(kt * MK + t, a.n - 1);
             const u32x4 row = *reinterpret_cast<const u32x4 *>((e < MK ? k : v) + (int64_t(p) * a.n + kc) * rs + hd * 8);
             if (e < MK) {
@@ -429,8 +439,8 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
             } else {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    vt[(2 * c) * VTP + t] = _Float16(h2f_lo(row[c]));
-                    vt[(2 * c + 1) * VTP + t] = _Float16(h2f_hi(row[c]));
+                    vt[(2 * c) * VTP + t] = half_t(h2f_lo(row[c]));
+                    vt[(2 * c + 1) * VTP + t] = half_t(h2f_hi(row[c]));
                 }
             }
         }
@@ -466,19 +476,19 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
             for (int r = 0; r < 16; ++r) {
                 const float pr = fexp2(st[r] - mn);
                 l += pr;
-                if (r < 8) pb0[r] = _Float16(pr);
-                else pb1[r - 8] = _Float16(pr);
+                if (r < 8) pb0[r] = half_t(pr);
+                else pb1[r - 8] = half_t(pr);
             }
             u32x4 a0 = {0u, 0u, 0u, 0u}, a1 = {0u, 0u, 0u, 0u};  // V^T rows 8 .. 31: zero
             if (col < 8) {
-                const _Float16 *vr = vt + col * VTP + bb * 32 + 4 * hh;  // 4 keys = one 8-byte read
+                const half_t *vr = vt + col * VTP + bb * 32 + 4 * hh;  // 4 keys = one 8-byte read
                 const u32x2 r0 = *reinterpret_cast<const u32x2 *>(vr), r1 = *reinterpret_cast<const u32x2 *>(vr + 8);
                 const u32x2 r2 = *reinterpret_cast<const u32x2 *>(vr + 16), r3 = *reinterpret_cast<const u32x2 *>(vr + 24);
                 a0 = u32x4{r0[0], r0[1], r1[0], r1[1]};
                 a1 = u32x4{r2[0], r2[1], r3[0], r3[1]};
             }
-            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, a0), pb0, o, 0, 0, 0);
-            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, a1), pb1, o, 0, 0, 0);
+            o = ATT_MFMA_32X32X16(__builtin_bit_cast(f16x8v, a0), pb0, o, 0, 0, 0);
+            o = ATT_MFMA_32X32X16(__builtin_bit_cast(f16x8v, a1), pb1, o, 0, 0, 0);
         };
         for (int bb = 0; bb < nb; ++bb) {
             if (b0 + bb < qb) block(std::false_type{}, bb);
@@ -504,25 +514,25 @@ __global__ __launch_bounds__(MNT) void k_attn_fwd_mma(AttnArgs a, const h16_t *_
 // lane's own; dS^T feeds dQ^T += K^T dS^T (32x32x16 f16, K^T read in the accumulator's key order).
 // Key side (dK, dV): lane (key n, half h) holds the 16 queries of S = Q K^T and dP = dO V^T, with
 // lse / delta of those queries from LDS (four 16-byte reads each); dV^T += dO^T P and dK^T += Q^T dS
-// (32x32x16 f16).  P and dS are rounded to fp16 for the products, accumulation fp32; the logit
+// (32x32x16).  P and dS are rounded to the 16-bit format for the products, accumulation fp32; the logit
 // transform (dropout, zero -> -1e3, its gradient factor) is the VALU kernels'.
-__device__ __forceinline__ f16x8v vt_frag(const _Float16 *base) {  // 4 + 4 keys in the accumulator's order
+__device__ __forceinline__ f16x8v vt_frag(const half_t *base) {  // 4 + 4 keys in the accumulator's order
     const u32x2 r0 = *reinterpret_cast<const u32x2 *>(base), r1 = *reinterpret_cast<const u32x2 *>(base + 8);
     return __builtin_bit_cast(f16x8v, u32x4{r0[0], r0[1], r1[0], r1[1]});
 }
 
 // stage 128 rows of a [P][n][nh * 8] 16-bit tensor's head hd: native rows [row][8] (nat, may be
-// null) and / or fp16 transposed [dim][row] (tr, may be null)
+// null) and / or transposed [dim][row] (tr, may be null)
 __device__ __forceinline__ void stage_rows(const h16_t *__restrict__ src, const AttnArgs &a, int p, int hd, int r0,
-                                           int t, h16_t *nat, _Float16 *tr) {
+                                           int t, h16_t *nat, half_t *tr) {
     const int rc = min(r0 + t, a.n - 1);
     const u32x4 row = *reinterpret_cast<const u32x4 *>(src + (int64_t(p) * a.n + rc) * (a.nh * 8) + hd * 8);
     if (nat) *reinterpret_cast<u32x4 *>(nat + t * 8) = row;
     if (tr) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            tr[(2 * c) * VTP + t] = _Float16(h2f_lo(row[c]));
-            tr[(2 * c + 1) * VTP + t] = _Float16(h2f_hi(row[c]));
+            tr[(2 * c) * VTP + t] = half_t(h2f_lo(row[c]));
+            tr[(2 * c + 1) * VTP + t] = half_t(h2f_hi(row[c]));
         }
     }
 }
@@ -544,7 +554,7 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_q_mma(AttnArgs a, float scale,
                                                         const float *__restrict__ lse, float *__restrict__ delta,
                                                         h16_t *__restrict__ gq) {
     __shared__ __attribute__((aligned(16))) h16_t ks[MK * 8], vs[MK * 8];
-    __shared__ __attribute__((aligned(16))) _Float16 kt_[8 * VTP];
+    __shared__ __attribute__((aligned(16))) half_t kt_[8 * VTP];
     const int nqt = (a.n + MQ - 1) / MQ, qt = nqt - 1 - int(blockIdx.x);
     const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
     const int tid = int(threadIdx.x), lane = tid & 63, w = tid >> 6, col = lane & 31, hh = lane >> 5;
@@ -593,14 +603,14 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_q_mma(AttnArgs a, float scale,
                 const float t = tlogit(a, c2k, zrep, drop, seed, int(blockIdx.y), i, kb * 32 + row, st[r], g);
                 float pr = fexp2(t - lz);
                 if (DIAG) pr = row > col ? 0.f : pr;
-                const _Float16 ds = _Float16(g * pr * (dp[r] - dl));
+                const half_t ds = half_t(g * pr * (dp[r] - dl));
                 if (r < 8) d0[r] = ds;
                 else d1[r - 8] = ds;
             }
-            const _Float16 *kr = col < 8 ? kt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
+            const half_t *kr = col < 8 ? kt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
             const f16x8v a0 = kr ? vt_frag(kr) : f16x8v{}, a1 = kr ? vt_frag(kr + 16) : f16x8v{};
-            dq = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, d0, dq, 0, 0, 0);
-            dq = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, d1, dq, 0, 0, 0);
+            dq = ATT_MFMA_32X32X16(a0, d0, dq, 0, 0, 0);
+            dq = ATT_MFMA_32X32X16(a1, d1, dq, 0, 0, 0);
         };
         for (int bb = 0; bb < nb; ++bb) {
             if (b0 + bb < qb) block(std::false_type{}, bb);
@@ -622,7 +632,7 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_kv_mma(AttnArgs a, float scale
                                                          const float *__restrict__ delta, h16_t *__restrict__ gk,
                                                          h16_t *__restrict__ gv) {
     __shared__ __attribute__((aligned(16))) h16_t qs[MK * 8], gs[MK * 8];
-    __shared__ __attribute__((aligned(16))) _Float16 qt_[8 * VTP], gt_[8 * VTP];
+    __shared__ __attribute__((aligned(16))) half_t qt_[8 * VTP], gt_[8 * VTP];
     __shared__ __attribute__((aligned(16))) float ls[MK], dls[MK];
     [[maybe_unused]] const int nt = (a.n + MQ - 1) / MQ, ktile = int(blockIdx.x);  // key tile 0 meets every query tile: first
     const int p = int(blockIdx.y) / a.nh, hd = int(blockIdx.y) - p * a.nh;
@@ -672,7 +682,7 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_kv_mma(AttnArgs a, float scale
                     const float t = tlogit(a, c2k, zrep, drop, seed, int(blockIdx.y), ib * 32 + row, j, st[r], g);
                     float pr = fexp2(t - lv[u]);
                     if (DIAG) pr = row < col ? 0.f : pr;
-                    const _Float16 ph = _Float16(pr), ds = _Float16(g * pr * (dp[r] - dv4[u]));
+                    const half_t ph = half_t(pr), ds = half_t(g * pr * (dp[r] - dv4[u]));
                     if (r < 8) {
                         p0[r] = ph;
                         d0[r] = ds;
@@ -682,12 +692,12 @@ __global__ __launch_bounds__(MNT) void k_attn_bwd_kv_mma(AttnArgs a, float scale
                     }
                 }
             }
-            const _Float16 *gr = col < 8 ? gt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
-            const _Float16 *qr = col < 8 ? qt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
-            dv = __builtin_amdgcn_mfma_f32_32x32x16_f16(gr ? vt_frag(gr) : f16x8v{}, p0, dv, 0, 0, 0);
-            dv = __builtin_amdgcn_mfma_f32_32x32x16_f16(gr ? vt_frag(gr + 16) : f16x8v{}, p1, dv, 0, 0, 0);
-            dk = __builtin_amdgcn_mfma_f32_32x32x16_f16(qr ? vt_frag(qr) : f16x8v{}, d0, dk, 0, 0, 0);
-            dk = __builtin_amdgcn_mfma_f32_32x32x16_f16(qr ? vt_frag(qr + 16) : f16x8v{}, d1, dk, 0, 0, 0);
+            const half_t *gr = col < 8 ? gt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
+            const half_t *qr = col < 8 ? qt_ + col * VTP + bb * 32 + 4 * hh : nullptr;
+            dv = ATT_MFMA_32X32X16(gr ? vt_frag(gr) : f16x8v{}, p0, dv, 0, 0, 0);
+            dv = ATT_MFMA_32X32X16(gr ? vt_frag(gr + 16) : f16x8v{}, p1, dv, 0, 0, 0);
+            dk = ATT_MFMA_32X32X16(qr ? vt_frag(qr) : f16x8v{}, d0, dk, 0, 0, 0);
+            dk = ATT_MFMA_32X32X16(qr ? vt_frag(qr + 16) : f16x8v{}, d1, dk, 0, 0, 0);
         };
         for (int bb = 0; bb < MK / 32; ++bb) {
             const int ib = b0 + bb;

@@ -23,7 +23,7 @@ void set_error(const std::string &msg);
 int fail(const std::string &msg);
 int check_launch(const char *what);
 constexpr int kPairCap = 65536;
-constexpr unsigned kTicketRegions = 16, kTicketSlots = 4;
+constexpr unsigned kTicketRegions = 64, kTicketSlots = 4, kNoTicket = ~0u;
 unsigned ticket_slot(hipStream_t st);
 float *pair_pool(unsigned slot);
 }  // namespace vq3d_rt
@@ -306,11 +306,11 @@ __device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {
 // re-arms it to 0.
 // Invariant: two launches holding the same slot must never run at the same time.  Slots are
 // therefore keyed by STREAM: each stream that launches ticketed kernels owns a region of
-// kTicketSlots slots and cycles through it; launches on one stream (or captured from one stream
-// into a graph) are ordered, so a slot is free again by the time its stream reuses it, and
-// launches on different streams -- a side stream, a second level chain -- never share one.  Up
-// to kTicketRegions streams hold regions at once; a further stream takes over the least recently
-// claimed region, so more than that many streams must not run ticketed launches concurrently.
+// kTicketSlots slots for the life of the process and cycles through it; launches on one stream (or
+// captured from one stream into a graph) are ordered, so a slot is free again by the time its
+// stream reuses it, and launches on different streams -- a side stream, a second level chain, the
+// PixelSNAIL lanes -- never share one.  A graph must be replayed on a stream that runs no ticketed
+// launches concurrently with it (its slots are those of the streams it was captured from).
 constexpr unsigned kTicketRegions = vq3d_rt::kTicketRegions, kTicketSlots = vq3d_rt::kTicketSlots,
                    kTickets = kTicketRegions * kTicketSlots;
 constexpr unsigned kShards = 16, kTicketLine = 32;
@@ -398,6 +398,7 @@ inline GridSum grid_sum_for(hipStream_t s, int64_t nblocks, bool want) {
     // one workgroup: its own sum is the total (a single add, deterministic)
     if (!want || nblocks <= 1 || nblocks > kPairCap) return GridSum{nullptr, 0u};
     const unsigned k = ticket_slot(s);
+    if (k == vq3d_rt::kNoTicket) return GridSum{nullptr, 0u};  // regions exhausted: atomics
     return GridSum{pair_pool(k), k};
 }
 

@@ -24,21 +24,26 @@ const char *last_error() { return g_last_error.c_str(); }
 
 // The ticket-slot table (common.h: keyed by stream; one table for both builds, so every ticketed
 // launch of the library on one stream draws from that stream's region) and the pair storage the
-// slots index.
+// slots index.  A stream keeps its region for the life of the process: a region handed to another
+// stream while its first owner still had launches in flight -- or baked into a captured graph that
+// is replayed later -- would let two concurrent launches share a completion ticket.  torch hands out
+// streams from fixed pools (32 per priority per device), so kTicketRegions covers every stream a
+// process can create; beyond it, launches get kNoTicket and their grid sums fall back to float
+// atomics (correct, not bitwise reproducible).
 unsigned ticket_slot(hipStream_t st) {
     static std::mutex mu;
     static hipStream_t owner[kTicketRegions] = {};
-    static bool used[kTicketRegions] = {};
-    static unsigned next[kTicketRegions] = {}, claims = 0;
+    static unsigned next[kTicketRegions] = {}, nreg = 0;
     std::lock_guard<std::mutex> lk(mu);
-    unsigned r = kTicketRegions;
-    for (unsigned i = 0; i < kTicketRegions; ++i)
-        if (used[i] && owner[i] == st) r = i;
-    if (r == kTicketRegions) {
-        r = claims++ % kTicketRegions;
-        owner[r] = st;
-        used[r] = true;
-        next[r] = 0;
+    unsigned r = nreg;
+    for (unsigned i = 0; i < nreg; ++i)
+        if (owner[i] == st) {
+            r = i;
+            break;
+        }
+    if (r == nreg) {
+        if (nreg == kTicketRegions) return kNoTicket;
+        owner[nreg++] = st;
     }
     return r * kTicketSlots + (next[r]++ % kTicketSlots);
 }

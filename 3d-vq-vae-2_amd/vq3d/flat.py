@@ -51,11 +51,10 @@ class FlatParams:
     def refresh_shadow(self, dtype):
         """a 16-bit copy of every parameter in one launch (torch's round-to-nearest-even cast, as
         p.to(dtype)): the GEMM operands of a forward / backward read their weights from it instead
-        of casting each weight per call.  Call it after the parameters change (once per forward)."""
-        sh = self._shadow.get(dtype)
-        if sh is None:
-            sh = self._shadow[dtype] = torch.empty(self.numel, dtype=dtype, device=self.device)
-        sh.copy_(self.data)
+        of casting each weight per call.  Call it after the parameters change (once per forward).
+        Every call writes a FRESH buffer: a previous forward's backward may still hold views of
+        the old one (saved GEMM operands), which an in-place refresh would bump the version of."""
+        sh = self._shadow[dtype] = self.data.to(dtype)
         return sh
 
     def shadow_view(self, p, dtype):

@@ -82,13 +82,15 @@ def step_begin():
         r.begin_step()
 
 
-def graph_collectives_ok(dev):
+def graph_collectives_ok(dev, why=None):
     """Capture + replay the step's collective pattern in a HIP graph on every rank -- a bucket
     all-reduce issued asynchronously on a side communication stream and joined back (as
     GradientAllReduce does), plus a plain all-reduce (the fused EMA statistics) -- and report
-    whether every rank got the right values (a collective; call on all ranks)."""
+    whether every rank got the right values (a collective; call on all ranks).  `why`: a list that
+    receives this rank's reason (the exception, or the wrong values) when the probe fails."""
     rank, world = dist.get_rank(), dist.get_world_size()
     ok = 1.0
+    why = why if why is not None else []
     try:
         t = torch.full((256,), float(rank + 1), device=dev)
         u = torch.full((64,), float(rank + 1), device=dev)
@@ -110,10 +112,16 @@ def graph_collectives_ok(dev):
         torch.cuda.synchronize()
         ok = 1.0 if (abs(float(t[0]) - (world + 1) / 2) < 1e-3 and abs(float(u[0]) - world * (world + 1) / 2) < 1e-3) \
             else 0.0
-    except Exception:  # capture unsupported here: the callers fall back to eager launches
+        if not ok:
+            why.append(f"rank {rank}: replayed collectives gave {float(t[0])} / {float(u[0])}, expected "
+                       f"{(world + 1) / 2} / {world * (world + 1) / 2}")
+    except Exception as e:  # capture unsupported here: the callers fall back to eager launches
         ok = 0.0
+        why.append(f"rank {rank}: {type(e).__name__}: {e}"[:300])
     v = torch.tensor([ok], device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    if float(v) <= 0.5 and not why:
+        why.append(f"rank {rank}: another rank's probe failed")
     return float(v) > 0.5
 
 
@@ -181,6 +189,7 @@ class GradientAllReduce:
     def _reset(self):
         self.pending = [set(ids) for _, _, ids in self.buckets]
         self.issued = [False] * len(self.buckets)
+        self.next_issue = 0
         self.works = []
 
     def _stream(self):
@@ -205,16 +214,22 @@ class GradientAllReduce:
             self.works.append((dist.all_reduce(view, op=op, group=self.group, async_op=True), view))
 
     def ready(self, params):
+        """Strike `params` off their buckets' pending sets and issue, IN BUCKET ORDER, every bucket
+        that is complete and whose predecessors are issued.  Collectives must be issued in the
+        same order on every rank; the order in which backward reports parameters may differ (the
+        decoder's level chains run on their own streams), so a bucket that completes early waits
+        for the buckets before it."""
         for p in params:
             if p is None:
                 continue
             bi = self.bucket_of.get(id(p))
             if bi is None or self.issued[bi]:
                 continue
-            s = self.pending[bi]
-            s.discard(id(p))
-            if not s:
-                self._issue(bi)
+            self.pending[bi].discard(id(p))
+        while self.next_issue < len(self.buckets) and not self.pending[self.next_issue]:
+            if not self.issued[self.next_issue]:
+                self._issue(self.next_issue)
+            self.next_issue += 1
 
     def __call__(self):
         """Issue the buckets still pending, then make the current stream wait for every
@@ -223,7 +238,7 @@ class GradientAllReduce:
             return
         from . import ops
         ops.join_side()
-        for bi in range(len(self.buckets)):
+        for bi in range(len(self.buckets)):  # in bucket order, as ready() issues them
             if not self.issued[bi]:
                 self._issue(bi)
         for work, view in self.works:

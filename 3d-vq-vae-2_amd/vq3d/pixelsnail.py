@@ -53,10 +53,19 @@ def _is_param(p):
     return isinstance(p, nn.Parameter) and p.is_leaf
 
 
+def _direct(p):
+    """p's gradient is added straight into p.grad by the kernel (and autograd gets None for it):
+    leaf parameters that require a gradient.  Everything else -- frozen parameters included --
+    gets a temporary that goes back through autograd (so autograd.grad / hooks see it, and a
+    frozen parameter never grows a .grad).  torch.autograd.grad(loss, params) on these
+    parameters is not supported on the 16-bit path: their gradients go to .grad directly."""
+    return _is_param(p) and p.requires_grad
+
+
 def _param_grad(p):
     """the gradient buffer a kernel may add into directly: a leaf parameter's own .grad (the flat
     buffer's view); anything else gets a zeroed temporary that autograd then accumulates"""
-    if _is_param(p):
+    if _direct(p):
         from .functional import grad_buf
         return grad_buf(p)
     return _zeros_like(p)
@@ -80,25 +89,40 @@ def _fused_glue():
 
 # ---- lanes: 16-bit GPU runs put the three stack streams (depth / height / width) on three HIP
 # streams.  The streams meet only in ExpandRFConv (height and width add projections of the depth
-# / height branches) and at the output, so each stream's chain of small kernels runs concurrently
-# with the other two's; autograd runs every backward op on its forward's stream and synchronises
-# the gradient hand-offs between them.
+# / height branches), at the input and at the output, so each stream's chain of small kernels runs
+# concurrently with the other two's; autograd runs every backward op on its forward's stream.
 #
-# The one-element parameters (the blocks' bias1a .. bias4, scale) are shared by the three streams:
-# their gradient sums would be added into the same address from three streams at once.  Under
-# lanes each lane adds into its own row of a [3][n] buffer and one callback at the end of the
-# backward adds the rows in lane order into the gradients: race-free and deterministic.
-_lanes_on = [False]  # off: a captured lanes step's gradients differ between replays
+# Cross-lane rules (each one closes a race the round-5 lanes had):
+# * a tensor made on lane j and used on lane i goes through _Fork, a node created ON LANE j whose
+#   one output is used on lane i only.  Every autograd input buffer therefore collects gradients
+#   from ONE lane: autograd never accumulates across lanes (its accumulation stream is the first
+#   producer's, so a lane-0 tensor could be read on lane 1 with no stream record and its block
+#   handed to lane 0's next allocation while the read was pending), and the only cross-lane
+#   gradient hand-off is _Fork's own, which waits for lane i, records the gradient on lane j and
+#   HOLDS a reference to it until the end of the backward;
+# * the hold matters because autograd accumulates in place into a gradient whose host reference
+#   count has dropped to one -- host order, not GPU order: a gradient that reached two lanes (an
+#   add's backward hands the same tensor to both inputs) could be overwritten by one lane's
+#   accumulation while the other lane's kernels still read it;
+# * the one-element parameters (the blocks' bias1a .. bias4, scale) are shared by the three
+#   streams: each lane adds their gradient sums into its own row of a [3][n] buffer and one callback
+#   at the end of the backward adds the rows in lane order into the gradients (deterministic).
+# Ticketed kernels on the three lanes draw completion tickets from three disjoint per-stream
+# regions, held for the process's life (csrc/misc.hip ticket_slot).
+_lanes_on = [False]
 _LANES = [None]
 _CUR = [0]       # the lane the current code runs on
 _LSTATE = [None]  # the forward's _LaneGrads
 
 
 def set_lanes(enabled="graph"):
-    """per-stack-stream HIP streams in 16-bit GPU runs: "graph" inside HIP-graph captures only, True
-    also in eager runs, False never (the default: see DESIGN.md 9 -- a captured lanes step's
-    gradients differ between replays, a cross-stream race not yet found)"""
+    """per-stack-stream HIP streams in 16-bit GPU runs: "graph" (the default) inside HIP-graph
+    captures only, True also in eager runs, False never"""
     _lanes_on[0] = enabled if enabled == "graph" else bool(enabled)
+
+
+def lanes_mode():
+    return _lanes_on[0]
 
 
 @contextlib.contextmanager
@@ -118,22 +142,34 @@ def _lane(i):
 
 
 class _LaneGrads:
-    """per-lane gradient rows of the shared one-element parameters of one forward"""
+    """the lanes' backward state of one forward: per-lane gradient rows of the shared one-element
+    parameters, the cross-lane gradients held until the end of the backward, the final join"""
 
     def __init__(self, params, lanes, device):
         self.params = params
         self.slot = {id(p): j for j, p in enumerate(params)}
         self.lanes = lanes
         self.buf = torch.zeros((3, max(1, len(params))), dtype=torch.float32, device=device)
+        for s in lanes[1:]:  # written on the side lanes: its block must outlive their writes
+            self.buf.record_stream(s)
+        self.held = []
         self.queued = False
 
-    def row(self, lane, p):
-        """lane's gradient slot of p (queues the flush of this backward on first use)"""
+    def _queue(self):
         if not self.queued:
             self.queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+
+    def row(self, lane, p):
+        """lane's gradient slot of p (queues the flush of this backward on first use)"""
+        self._queue()
         j = self.slot[id(p)]
         return self.buf[lane, j:j + 1]
+
+    def hold(self, t):
+        """keep a cross-lane gradient referenced until the backward ends (no in-place reuse)"""
+        self._queue()
+        self.held.append(t)
 
     def flush(self):
         """on the forward's main lane (the callback may run on autograd's device thread, whose
@@ -143,8 +179,10 @@ class _LaneGrads:
         with torch.cuda.stream(main):
             for s in self.lanes[1:]:
                 main.wait_stream(s)
-            sums = self.buf.sum(0).view(-1, 1)
-            torch._foreach_add_([grad_buf(p) for p in self.params], list(sums[:len(self.params)].unbind()))
+            if self.params:
+                sums = self.buf.sum(0).view(-1, 1)
+                torch._foreach_add_([grad_buf(p) for p in self.params], list(sums[:len(self.params)].unbind()))
+        self.held = []
         self.queued = False
 
 
@@ -157,47 +195,53 @@ def _lane_ctx():
 def _sgrad(lst, p):
     """the buffer a kernel adds p's gradient into: the lane row of a shared one-element parameter
     under lanes, else _param_grad(p)"""
-    if lst is not None and id(p) in lst[0].slot:
+    if lst is not None and id(p) in lst[0].slot and _direct(p):
         return lst[0].row(lst[1], p)
     return _param_grad(p)
 
 
 
-class _Handoff(torch.autograd.Function):
-    """a tensor crossing from lane j to lane i (applied on lane i).  Backward runs on lane i and hands
-    the gradient back to lane j: the gradient's memory (allocated on lane i) is recorded on lane j,
-    so the allocator cannot give it to lane i's next allocation while lane j still reads it (the
-    cross-stream reuse hazard autograd leaves to the caller)."""
+class _Fork(torch.autograd.Function):
+    """a tensor made on lane j, used on lane i: applied ON LANE j, so its backward runs on lane j.
+    Its one output is used on lane i only, hence its input buffer collects lane i's gradients alone
+    and the tensor's own producer collects lane j's (its direct uses) plus this node's -- every
+    accumulation stays on one lane.  Backward: lane j waits for lane i, the gradient (lane i's
+    memory) is recorded on lane j and held until the backward ends, and goes on as lane j's."""
 
     @staticmethod
-    def forward(ctx, t, src):
-        ctx.src = src
+    def forward(ctx, t, st, i, j):
+        ctx.st, ctx.i, ctx.j = st, i, j
         return t.view_as(t)
 
     @staticmethod
     def backward(ctx, g):
         if g is not None:
-            g.record_stream(ctx.src)
-        return g, None
+            lanes = ctx.st.lanes
+            lanes[ctx.j].wait_stream(lanes[ctx.i])
+            g.record_stream(lanes[ctx.j])
+            ctx.st.hold(g)
+        return g, None, None, None
 
 
 def _take(i, j, *ts):
     """lane i is about to use tensors made on lane j: it waits for lane j's work so far, the
     allocator keeps the tensors' memory until lane i's use is done, and the tensors that need a
-    gradient come back wrapped in _Handoff (their gradients cross back to lane j).  Returns the
+    gradient come back through _Fork (their gradients cross back to lane j).  Returns the
     tensors (unchanged without lanes)."""
     lanes = _LANES[0]
     if lanes is None or i == j:
         return ts if len(ts) != 1 else ts[0]
-    lanes[i].wait_stream(lanes[j])
+    st = _LSTATE[0]
     out = []
-    with torch.cuda.stream(lanes[i]):
+    with torch.cuda.stream(lanes[j]):
         for t in ts:
-            if t is not None:
-                t.record_stream(lanes[i])
-                if t.requires_grad:
-                    t = _Handoff.apply(t, lanes[j])
+            if t is not None and t.requires_grad:
+                t = _Fork.apply(t, st, i, j)
             out.append(t)
+    lanes[i].wait_stream(lanes[j])
+    for t in out:
+        if t is not None:
+            t.record_stream(lanes[i])
     return out if len(out) != 1 else out[0]
 
 
@@ -226,7 +270,7 @@ class PreActFn(torch.autograd.Function):
         da, db = _sgrad(ctx.lst, a), _sgrad(ctx.lst, b)
         L.call("vq3d_preact_act_bwd", L.dtype_code(g), L.dtype_code(x), x.numel(), L.ptr(g), L.ptr(x), L.ptr(a),
                None if gx is None else L.ptr(gx), L.ptr(da), L.ptr(db), L.stream())
-        return gx, None if _is_param(a) else da, None if _is_param(b) else db
+        return gx, None if _direct(a) else da, None if _direct(b) else db
 
 
 class ScaleBiasResFn(torch.autograd.Function):
@@ -255,7 +299,7 @@ class ScaleBiasResFn(torch.autograd.Function):
         ds, dbi = _sgrad(ctx.lst, scale), _sgrad(ctx.lst, bias)
         L.call("vq3d_scale_bias_res_bwd", L.dtype_code(o), o.numel(), L.ptr(g), L.ptr(o), L.ptr(scale),
                None if go is None else L.ptr(go), L.ptr(ds), L.ptr(dbi), L.stream())
-        return (go, None if _is_param(scale) else ds, None if _is_param(bias) else dbi,
+        return (go, None if _direct(scale) else ds, None if _direct(bias) else dbi,
                 (g if ctx.needs_input_grad[3] else None))
 
 
@@ -298,9 +342,9 @@ class CausalConvFn(torch.autograd.Function):
             da, db = _sgrad(ctx.lst, ctx.pro[0]), _sgrad(ctx.lst, ctx.pro[1])
         gx, _ = ops.conv_bwd(g, x, w, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
                              dcbias=dcb, dpro_pre=db, dpro_post=da, taps=ctx.taps)
-        return (gx, dw, None if dcb is None or _is_param(ctx.cbias) else dcb,
-                None if da is None or _is_param(ctx.pro[0]) else da,
-                None if db is None or _is_param(ctx.pro[1]) else db, None, None)
+        return (gx, dw, None if dcb is None or _direct(ctx.cbias) else dcb,
+                None if da is None or _direct(ctx.pro[0]) else da,
+                None if db is None or _direct(ctx.pro[1]) else db, None, None)
 
 
 # the 16-bit weight shadow of the current forward: (FlatParams, dtype) when the parameters live in
@@ -358,7 +402,7 @@ class PointwiseFn(torch.autograd.Function):
             ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=gv.device)
             L.call("vq3d_rows_wgrad", L.dtype_code(gv), n, co, xv.shape[1], L.ptr(gv), gv.stride(0), L.ptr(xv),
                    xv.stride(0), L.ptr(dw), L.ptr(db), L.ptr(ws), ctypes_size(nws), L.stream())
-            return gx, None if _is_param(w) else dw, None if b is None or _is_param(b) else db
+            return gx, None if _direct(w) else dw, None if b is None or _direct(b) else db
         sk = 256 if n % 256 == 0 and n >= 4096 else n
         gw = torch.bmm(gv.reshape(-1, sk, co).transpose(1, 2).float(), xv.reshape(-1, sk, xv.shape[1]).float()).sum(0)
         gb = gv.float().sum(0) if b is not None else None
@@ -476,11 +520,11 @@ class ExpandRFConv(nn.Module):
 
     def run(self, stack):
         d, h, w = stack
-        # on lane 0 (the lanes only ever synchronise with lane 0: side-to-side waits inside a
-        # captured multi-stream backward crash hipStreamEndCapture on this ROCm)
+        # on lane 0 (the lanes only ever synchronise with lane 0, forward and backward: side-to-side
+        # waits inside a captured multi-stream backward crashed hipStreamEndCapture on this ROCm)
+        h = _take(0, 1, h)
+        w = _take(0, 2, w)
         with _lane(0):
-            h = _take(0, 1, h)
-            w = _take(0, 2, w)
             dc = pointwise(_operand(d), self.depth_conv.weight, self.depth_conv.bias)
             dch, dcw = torch.chunk(dc, 2, dim=1)
             hc = pointwise(_operand(h), self.height_conv.weight, self.height_conv.bias)
@@ -812,7 +856,7 @@ class PixelSNAIL(nn.Module):
                 lanes = [torch.cuda.current_stream()] + aux
         _LANES[0] = lanes
         if lanes is not None:
-            shared = [p for p in self.parameters() if p.numel() == 1]
+            shared = [p for p in self.parameters() if p.numel() == 1 and p.requires_grad]
             _LSTATE[0] = _LaneGrads(shared, lanes, x.device)
         try:
             xs = [x] + [_take(i, 0, x, bg[0])[0] for i in (1, 2)]

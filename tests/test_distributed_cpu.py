@@ -150,3 +150,47 @@ def test_gradient_allreduce_and_sharding_two_ranks():
     assert all(bool(r["ok"]) for r in res)
     seen = [i for r in res for s in r["shards"] for i in s]
     assert len(seen) == len(set(seen)) == 12  # disjoint volumes, every index once
+
+
+def _order_worker(rank, world, port, out):
+    """Backward reports parameters in a rank-dependent order (the decoder's level chains run on
+    their own streams, so which bucket completes first can differ between ranks); the reducer must
+    still issue its collectives in bucket order on every rank -- gloo would otherwise pair
+    different buckets (different sizes) across the ranks."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "3d-vq-vae-2_amd"))
+    from vq3d import parallel
+    _init(rank, world, port)
+    models = [_FakeModel(r) for r in range(world)]
+    m = models[rank]
+    expect = sum(mm.flat.grad for mm in models) / world
+    ar = parallel.GradientAllReduce(m, bucket_bytes=2048)
+    log = []
+    issue = ar._issue
+
+    def logged(bi):
+        log.append(bi)
+        issue(bi)
+    ar._issue = logged
+    ps = list(m.ps)
+    order = ps if rank == 1 else ps[::-1]  # rank 1: the LAST bucket's parameters first
+    for i, p in enumerate(order):
+        parallel.grads_ready([p])
+        if rank == 1 and i < len(order) - 1:
+            ok_early = not ar.issued[0]  # bucket 0 (highest offsets) not complete yet: nothing issued
+            if not ok_early:
+                break
+    ar()
+    ok = log == sorted(log) and len(log) == len(ar.buckets)
+    ok &= torch.allclose(m.flat.grad, expect, atol=1e-6)
+    ar.close()
+    torch.save({"ok": torch.tensor(bool(ok)), "log": log}, out + f".{rank}")
+    dist.destroy_process_group()
+
+
+def test_gradient_allreduce_issues_buckets_in_order_two_ranks():
+    out = tempfile.mktemp()
+    mp.spawn(_order_worker, args=(2, free_port(), out), nprocs=2, join=True)
+    res = [torch.load(out + f".{r}", weights_only=False) for r in range(2)]
+    assert all(bool(r["ok"]) for r in res), [r["log"] for r in res]
+    assert res[0]["log"] == res[1]["log"]
