@@ -38,6 +38,8 @@ int launch_pw_wgrad(const vq3d_conv_desc *d, const void *x, const void *x2, cons
 // PixelSNAIL 1x1x1 weight gradient over 16-bit voxel rows (ACCUMULATED, deterministic):
 //   dw[cg][cx] += sum_v g[v * ldg + co] x[v * ldx + ci], db[cg] += sum_v g[v * ldg + co] (db may be null)
 size_t rows_wgrad_workspace(int64_t nrows, int cg, int cx);
+int launch_rows_gemm(int64_t nrows, int k, int n, const void *x, int64_t ldx, const void *w, int64_t ldw, int trans_w,
+                     const float *bias, void *y, int64_t ldy, hipStream_t s);
 int launch_rows_wgrad(int64_t nrows, int cg, int cx, const void *g, int64_t ldg, const void *x, int64_t ldx, float *dw,
                       float *db, void *workspace, size_t ws_bytes, hipStream_t s);
 

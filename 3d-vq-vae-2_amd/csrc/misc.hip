@@ -423,6 +423,21 @@ __global__ __launch_bounds__(256) void k_elu_bwd_out(const T *__restrict__ g, co
     }
 }
 
+// Zero fill / device copy as KERNELS.  hipMemsetAsync / hipMemcpyAsync captured into a HIP graph
+// become memset / memcpy nodes, and on this ROCm a replayed graph's memset nodes were measured NOT to
+// be ordered with the kernels around them: a captured PixelSNAIL step whose zero fills were memset
+// nodes gave different (growing) gradients on every replay, the same step with fill kernels replays
+// bit for bit (tools/dbg/replay_bisect.py).  16-byte vectors when both ends allow, else dwords /
+// bytes; grid-stride.
+template <typename V>
+__global__ __launch_bounds__(256) void k_fill0(V *__restrict__ p, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) p[i] = V{};
+}
+template <typename V>
+__global__ __launch_bounds__(256) void k_copyv(V *__restrict__ d, const V *__restrict__ s, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) d[i] = s[i];
+}
+
 __global__ __launch_bounds__(256) void k_scale(float *__restrict__ x, float a, int64_t n) {
     for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) x[i] *= a;
 }
@@ -828,15 +843,27 @@ int vq3d_cast(int32_t src_dtype, const void *src, int32_t dst_dtype, void *dst, 
 int vq3d_zero(void *p, size_t bytes, vq3d_stream_t stream) {
     if (!bytes) return 0;
     if (!p) return fail("zero: null pointer");
-    hipError_t e = hipMemsetAsync(p, 0, bytes, as_stream(stream));
-    return e == hipSuccess ? 0 : fail(std::string("zero: ") + hipGetErrorString(e));
+    hipStream_t s = as_stream(stream);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) | bytes;
+    if (a % 16 == 0) k_fill0<u32x4><<<grid_for(int64_t(bytes / 16)), 256, 0, s>>>((u32x4 *)p, int64_t(bytes / 16));
+    else if (a % 4 == 0) k_fill0<uint32_t><<<grid_for(int64_t(bytes / 4)), 256, 0, s>>>((uint32_t *)p, int64_t(bytes / 4));
+    else k_fill0<uint8_t><<<grid_for(int64_t(bytes)), 256, 0, s>>>((uint8_t *)p, int64_t(bytes));
+    return check_launch("zero");
 }
 
 int vq3d_copy(void *dst, const void *src, size_t bytes, vq3d_stream_t stream) {
     if (!bytes) return 0;
     if (!dst || !src) return fail("copy: null pointer");
-    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, as_stream(stream));
-    return e == hipSuccess ? 0 : fail(std::string("copy: ") + hipGetErrorString(e));
+    hipStream_t s = as_stream(stream);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | bytes;
+    if (a % 16 == 0)
+        k_copyv<u32x4><<<grid_for(int64_t(bytes / 16)), 256, 0, s>>>((u32x4 *)dst, (const u32x4 *)src, int64_t(bytes / 16));
+    else if (a % 4 == 0)
+        k_copyv<uint32_t><<<grid_for(int64_t(bytes / 4)), 256, 0, s>>>((uint32_t *)dst, (const uint32_t *)src,
+                                                                     int64_t(bytes / 4));
+    else
+        k_copyv<uint8_t><<<grid_for(int64_t(bytes)), 256, 0, s>>>((uint8_t *)dst, (const uint8_t *)src, int64_t(bytes));
+    return check_launch("copy");
 }
 
 int vq3d_poison_lds(vq3d_stream_t stream) {
@@ -966,6 +993,12 @@ int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const vo
 
 size_t vq3d_rows_wgrad_workspace_bytes(int64_t nrows, int32_t cg, int32_t cx) {
     return rows_wgrad_workspace(nrows, cg, cx);
+}
+
+int vq3d_rows_gemm(int32_t dtype, int64_t nrows, int32_t k, int32_t n, const void *x, int64_t ldx, const void *w,
+                   int64_t ldw, int32_t trans_w, const float *bias, void *y, int64_t ldy, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("rows_gemm: 16-bit rows only");
+    return launch_rows_gemm(nrows, k, n, x, ldx, w, ldw, trans_w, bias, y, ldy, as_stream(stream));
 }
 
 int vq3d_rows_wgrad(int32_t dtype, int64_t nrows, int32_t cg, int32_t cx, const void *g, int64_t ldg, const void *x,

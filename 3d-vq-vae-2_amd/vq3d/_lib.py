@@ -128,6 +128,7 @@ _SIGS = {
     "vq3d_preact_act_bwd": (c_int, [c_int, c_int, c_i64, P, P, P, P, P, P, P]),
     "vq3d_scale_bias_res_fwd": (c_int, [c_int, c_i64, P, P, P, P, P, P]),
     "vq3d_scale_bias_res_bwd": (c_int, [c_int, c_i64, P, P, P, P, P, P, P]),
+    "vq3d_rows_gemm": (c_int, [c_int, c_i64, c_int, c_int, P, c_i64, P, c_i64, c_int, P, P, c_i64, P]),
     "vq3d_rows_wgrad_workspace_bytes": (c_size, [c_i64, c_int, c_int]),
     "vq3d_rows_wgrad": (c_int, [c_int, c_i64, c_int, c_int, P, c_i64, P, c_i64, P, P, P, c_size, P]),
     "vq3d_causal_attn_supported": (c_int, [c_int] * 3),

@@ -473,6 +473,16 @@ int vq3d_scale_bias_res_fwd(int32_t o_dtype, int64_t n, const void *o, const flo
                             const float *s, float *out, vq3d_stream_t stream);
 int vq3d_scale_bias_res_bwd(int32_t o_dtype, int64_t n, const float *g, const void *o, const float *scale, void *go,
                             float *dscale, float *dbias, vq3d_stream_t stream);
+/* the 1x1x1 convs' forward and backward-data over voxel rows (Conv3d(kernel_size=1) of
+ * pixel_model/layers.py:225-248 / 370-404 / 665-675 and pixelsnail.py:39-43 / 78-82 on
+ * channels-last activations; replaces the GEMM those convs run as torch F.linear / matmul):
+ * y[v][j] = sum_i x[v][i] w'[j][i] (+ bias[j], fp32, may be NULL) for v < nrows, j < n, i < k, with
+ * w' = w (trans_w = 0: w[n][k] rows at stride ldw -- the forward, w = [cout][cin]) or w' = w^T
+ * (trans_w = 1: w[k][n] -- the backward-data gx = g W).  x, w, y 16-bit (dtype BF16 / F16), fp32
+ * accumulation on the matrix cores, y rounded once; k, n, ldx, ldw multiples of 8, ldy of 4, k <= 1024,
+ * x / w 16-byte and y 8-byte aligned. */
+int vq3d_rows_gemm(int32_t dtype, int64_t nrows, int32_t k, int32_t n, const void *x, int64_t ldx, const void *w,
+                   int64_t ldw, int32_t trans_w, const float *bias, void *y, int64_t ldy, vq3d_stream_t stream);
 /* the 1x1x1 convs' weight gradient over voxel rows (the Conv3d(kernel_size=1) backward of
  * layers.py:122-248 / 650-703, the GEMMs' K = voxels side): dw[cg][cx] += sum_v g[v][co] x[v][ci]
  * and (db != NULL) db[co] += sum_v g[v][co], fp32 accumulation in a fixed order.  g: nrows rows of

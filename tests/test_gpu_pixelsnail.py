@@ -452,6 +452,41 @@ def test_rows_wgrad_matches_fp32(gpu, dt, n, cg, cx, ldg, ldx, bias):
         assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,k,co,ldx,ldy,trans,bias", [
+    (8192, 256, 64, 256, 64, 0, True),     # branch_conv1 forward (cin 256 -> branch 64)
+    (8192, 64, 256, 64, 256, 1, False),    # its backward-data (g 64 -> gx 256)
+    (8192, 64, 256, 64, 256, 0, False),    # branch_conv3 forward
+    (8192, 520, 128, 520, 128, 0, True),   # key-value projection (515 inputs, padded to 520)
+    (8192, 128, 520, 128, 520, 1, False),  # its backward-data
+    (1000, 264, 72, 272, 80, 0, True),     # ragged rows, row strides wider than the rows
+    (70, 8, 8, 8, 8, 1, False)])
+def test_rows_gemm_matches_fp32(gpu, dt, n, k, co, ldx, ldy, trans, bias):
+    """vq3d_rows_gemm (the 16-bit 1x1x1 convs' forward and backward-data, PointwiseFn) against an
+    fp32 torch GEMM of the same 16-bit operands: y = x w^T (+ b) / gx = g w, rows of the published
+    prior's shapes, K past the 64 KB LDS opt-in (520), ragged row counts, strided rows.  Tolerance:
+    one rounding of the 16-bit output (2^-8 of max |y|) plus fp32 order."""
+    import ctypes
+    from vq3d import _lib as L
+    g0 = torch.Generator(device=gpu).manual_seed(n + k + co)
+    xb = torch.randn((n, ldx), device=gpu, generator=g0).to(dt)
+    x = xb[:, :k]
+    w = (torch.randn((k, co) if trans else (co, k), device=gpu, generator=g0) * 0.1).to(dt).contiguous()
+    b = torch.randn(co, device=gpu, generator=g0) if bias else None
+    want = x.float() @ (w.float() if trans else w.float().t())
+    if b is not None:
+        want = want + b
+    yb = torch.full((n, ldy), float("nan"), device=gpu, dtype=dt)
+    L.call("vq3d_rows_gemm", L.dtype_code(x), n, k, co, L.ptr(x), ldx, L.ptr(w), w.stride(0), trans, L.ptr(b),
+           L.ptr(yb), ldy, L.stream())
+    torch.cuda.synchronize()
+    y = yb[:, :co].float()
+    assert torch.isfinite(y).all()
+    assert rel(y, want.cpu().numpy()) < 8e-3, rel(y, want.cpu().numpy())
+    if ldy > co:
+        assert torch.isnan(yb[:, co:].float()).all()  # nothing written past the rows
+
+
 def test_rows_wgrad_rejects_unaligned(gpu):
     """channel counts / strides off a multiple of 8 fail loudly (PointwiseFn keeps those on the
     fp32 batched GEMM)"""
@@ -617,6 +652,7 @@ def test_lanes_match_single_stream_and_repeat_bitwise(gpu):
         loss.backward()
         torch.cuda.synchronize()
         single = [float(loss)] + [p.grad.detach().clone() for p in m.parameters()]
+        del loss  # (its graph would keep autograd nodes made on this stream alive into the capture)
     finally:
         PS.set_lanes(prev)
     runs = _captured_grads(gpu, m, fl, onehot, codes, "graph", 4)

@@ -53,19 +53,10 @@ def _is_param(p):
     return isinstance(p, nn.Parameter) and p.is_leaf
 
 
-def _direct(p):
-    """p's gradient is added straight into p.grad by the kernel (and autograd gets None for it):
-    leaf parameters that require a gradient.  Everything else -- frozen parameters included --
-    gets a temporary that goes back through autograd (so autograd.grad / hooks see it, and a
-    frozen parameter never grows a .grad).  torch.autograd.grad(loss, params) on these
-    parameters is not supported on the 16-bit path: their gradients go to .grad directly."""
-    return _is_param(p) and p.requires_grad
-
-
 def _param_grad(p):
     """the gradient buffer a kernel may add into directly: a leaf parameter's own .grad (the flat
     buffer's view); anything else gets a zeroed temporary that autograd then accumulates"""
-    if _direct(p):
+    if _is_param(p):
         from .functional import grad_buf
         return grad_buf(p)
     return _zeros_like(p)
@@ -89,40 +80,25 @@ def _fused_glue():
 
 # ---- lanes: 16-bit GPU runs put the three stack streams (depth / height / width) on three HIP
 # streams.  The streams meet only in ExpandRFConv (height and width add projections of the depth
-# / height branches), at the input and at the output, so each stream's chain of small kernels runs
-# concurrently with the other two's; autograd runs every backward op on its forward's stream.
+# / height branches) and at the output, so each stream's chain of small kernels runs concurrently
+# with the other two's; autograd runs every backward op on its forward's stream and synchronises
+# the gradient hand-offs between them.
 #
-# Cross-lane rules (each one closes a race the round-5 lanes had):
-# * a tensor made on lane j and used on lane i goes through _Fork, a node created ON LANE j whose
-#   one output is used on lane i only.  Every autograd input buffer therefore collects gradients
-#   from ONE lane: autograd never accumulates across lanes (its accumulation stream is the first
-#   producer's, so a lane-0 tensor could be read on lane 1 with no stream record and its block
-#   handed to lane 0's next allocation while the read was pending), and the only cross-lane
-#   gradient hand-off is _Fork's own, which waits for lane i, records the gradient on lane j and
-#   HOLDS a reference to it until the end of the backward;
-# * the hold matters because autograd accumulates in place into a gradient whose host reference
-#   count has dropped to one -- host order, not GPU order: a gradient that reached two lanes (an
-#   add's backward hands the same tensor to both inputs) could be overwritten by one lane's
-#   accumulation while the other lane's kernels still read it;
-# * the one-element parameters (the blocks' bias1a .. bias4, scale) are shared by the three
-#   streams: each lane adds their gradient sums into its own row of a [3][n] buffer and one callback
-#   at the end of the backward adds the rows in lane order into the gradients (deterministic).
-# Ticketed kernels on the three lanes draw completion tickets from three disjoint per-stream
-# regions, held for the process's life (csrc/misc.hip ticket_slot).
-_lanes_on = ["graph"]
+# The one-element parameters (the blocks' bias1a .. bias4, scale) are shared by the three streams:
+# their gradient sums would be added into the same address from three streams at once.  Under
+# lanes each lane adds into its own row of a [3][n] buffer and one callback at the end of the
+# backward adds the rows in lane order into the gradients: race-free and deterministic.
+_lanes_on = [False]  # off: a captured lanes step's gradients differ between replays
 _LANES = [None]
 _CUR = [0]       # the lane the current code runs on
 _LSTATE = [None]  # the forward's _LaneGrads
 
 
 def set_lanes(enabled="graph"):
-    """per-stack-stream HIP streams in 16-bit GPU runs: "graph" (the default) inside HIP-graph
-    captures only, True also in eager runs, False never"""
+    """per-stack-stream HIP streams in 16-bit GPU runs: "graph" inside HIP-graph captures only, True
+    also in eager runs, False never (the default: see DESIGN.md 9 -- a captured lanes step's
+    gradients differ between replays, a cross-stream race not yet found)"""
     _lanes_on[0] = enabled if enabled == "graph" else bool(enabled)
-
-
-def lanes_mode():
-    return _lanes_on[0]
 
 
 @contextlib.contextmanager
@@ -142,34 +118,22 @@ def _lane(i):
 
 
 class _LaneGrads:
-    """the lanes' backward state of one forward: per-lane gradient rows of the shared one-element
-    parameters, the cross-lane gradients held until the end of the backward, the final join"""
+    """per-lane gradient rows of the shared one-element parameters of one forward"""
 
     def __init__(self, params, lanes, device):
         self.params = params
         self.slot = {id(p): j for j, p in enumerate(params)}
         self.lanes = lanes
         self.buf = torch.zeros((3, max(1, len(params))), dtype=torch.float32, device=device)
-        for s in lanes[1:]:  # written on the side lanes: its block must outlive their writes
-            self.buf.record_stream(s)
-        self.held = []
         self.queued = False
-
-    def _queue(self):
-        if not self.queued:
-            self.queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
 
     def row(self, lane, p):
         """lane's gradient slot of p (queues the flush of this backward on first use)"""
-        self._queue()
+        if not self.queued:
+            self.queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self.flush)
         j = self.slot[id(p)]
         return self.buf[lane, j:j + 1]
-
-    def hold(self, t):
-        """keep a cross-lane gradient referenced until the backward ends (no in-place reuse)"""
-        self._queue()
-        self.held.append(t)
 
     def flush(self):
         """on the forward's main lane (the callback may run on autograd's device thread, whose
@@ -179,10 +143,8 @@ class _LaneGrads:
         with torch.cuda.stream(main):
             for s in self.lanes[1:]:
                 main.wait_stream(s)
-            if self.params:
-                sums = self.buf.sum(0).view(-1, 1)
-                torch._foreach_add_([grad_buf(p) for p in self.params], list(sums[:len(self.params)].unbind()))
-        self.held = []
+            sums = self.buf.sum(0).view(-1, 1)
+            torch._foreach_add_([grad_buf(p) for p in self.params], list(sums[:len(self.params)].unbind()))
         self.queued = False
 
 
@@ -195,53 +157,47 @@ def _lane_ctx():
 def _sgrad(lst, p):
     """the buffer a kernel adds p's gradient into: the lane row of a shared one-element parameter
     under lanes, else _param_grad(p)"""
-    if lst is not None and id(p) in lst[0].slot and _direct(p):
+    if lst is not None and id(p) in lst[0].slot:
         return lst[0].row(lst[1], p)
     return _param_grad(p)
 
 
 
-class _Fork(torch.autograd.Function):
-    """a tensor made on lane j, used on lane i: applied ON LANE j, so its backward runs on lane j.
-    Its one output is used on lane i only, hence its input buffer collects lane i's gradients alone
-    and the tensor's own producer collects lane j's (its direct uses) plus this node's -- every
-    accumulation stays on one lane.  Backward: lane j waits for lane i, the gradient (lane i's
-    memory) is recorded on lane j and held until the backward ends, and goes on as lane j's."""
+class _Handoff(torch.autograd.Function):
+    """a tensor crossing from lane j to lane i (applied on lane i).  Backward runs on lane i and hands
+    the gradient back to lane j: the gradient's memory (allocated on lane i) is recorded on lane j,
+    so the allocator cannot give it to lane i's next allocation while lane j still reads it (the
+    cross-stream reuse hazard autograd leaves to the caller)."""
 
     @staticmethod
-    def forward(ctx, t, st, i, j):
-        ctx.st, ctx.i, ctx.j = st, i, j
+    def forward(ctx, t, src):
+        ctx.src = src
         return t.view_as(t)
 
     @staticmethod
     def backward(ctx, g):
         if g is not None:
-            lanes = ctx.st.lanes
-            lanes[ctx.j].wait_stream(lanes[ctx.i])
-            g.record_stream(lanes[ctx.j])
-            ctx.st.hold(g)
-        return g, None, None, None
+            g.record_stream(ctx.src)
+        return g, None
 
 
 def _take(i, j, *ts):
     """lane i is about to use tensors made on lane j: it waits for lane j's work so far, the
     allocator keeps the tensors' memory until lane i's use is done, and the tensors that need a
-    gradient come back through _Fork (their gradients cross back to lane j).  Returns the
+    gradient come back wrapped in _Handoff (their gradients cross back to lane j).  Returns the
     tensors (unchanged without lanes)."""
     lanes = _LANES[0]
     if lanes is None or i == j:
         return ts if len(ts) != 1 else ts[0]
-    st = _LSTATE[0]
-    out = []
-    with torch.cuda.stream(lanes[j]):
-        for t in ts:
-            if t is not None and t.requires_grad:
-                t = _Fork.apply(t, st, i, j)
-            out.append(t)
     lanes[i].wait_stream(lanes[j])
-    for t in out:
-        if t is not None:
-            t.record_stream(lanes[i])
+    out = []
+    with torch.cuda.stream(lanes[i]):
+        for t in ts:
+            if t is not None:
+                t.record_stream(lanes[i])
+                if t.requires_grad:
+                    t = _Handoff.apply(t, lanes[j])
+            out.append(t)
     return out if len(out) != 1 else out[0]
 
 
@@ -270,7 +226,7 @@ class PreActFn(torch.autograd.Function):
         da, db = _sgrad(ctx.lst, a), _sgrad(ctx.lst, b)
         L.call("vq3d_preact_act_bwd", L.dtype_code(g), L.dtype_code(x), x.numel(), L.ptr(g), L.ptr(x), L.ptr(a),
                None if gx is None else L.ptr(gx), L.ptr(da), L.ptr(db), L.stream())
-        return gx, None if _direct(a) else da, None if _direct(b) else db
+        return gx, None if _is_param(a) else da, None if _is_param(b) else db
 
 
 class ScaleBiasResFn(torch.autograd.Function):
@@ -299,7 +255,7 @@ class ScaleBiasResFn(torch.autograd.Function):
         ds, dbi = _sgrad(ctx.lst, scale), _sgrad(ctx.lst, bias)
         L.call("vq3d_scale_bias_res_bwd", L.dtype_code(o), o.numel(), L.ptr(g), L.ptr(o), L.ptr(scale),
                None if go is None else L.ptr(go), L.ptr(ds), L.ptr(dbi), L.stream())
-        return (go, None if _direct(scale) else ds, None if _direct(bias) else dbi,
+        return (go, None if _is_param(scale) else ds, None if _is_param(bias) else dbi,
                 (g if ctx.needs_input_grad[3] else None))
 
 
@@ -312,33 +268,27 @@ def _preact(x, pro):
 
 # ============================================================================================ conv
 class CausalConvFn(torch.autograd.Function):
-    """y = conv(prologue(x), W) + cbias on the libvq3d engines, W = stream `i`'s causal kernel
-    (the reference-shaped parameter `w`) embedded in a k^3 kernel whose other taps are zero
-    (_embed_one).  Every parameter gradient -- W's live taps, the conv bias, the prologue scalars
-    -- is added by this backward straight into the parameter's gradient buffer (_direct), so no
-    AccumulateGrad node exists for them: under lanes such a node would keep the stream of the
-    forward that first created it (a stale one across steps, or the default stream inside a
-    capture)."""
+    """y = conv(prologue(x), w) + cbias on the libvq3d engines; w is the (embedded) k^3 weight.
+    Gradients of w / cbias / the prologue scalars come back as tensors (torch autograd maps them
+    onto the reference-shaped parameters through the embedding)."""
 
     @staticmethod
-    def forward(ctx, x, w, cbias, pa, pb, k, taps, i):
+    def forward(ctx, x, w, cbias, pa, pb, k, taps=0):
         geom = ConvGeom(k, 1, k // 2, False)
         pro = None if pa is None else (pa, pb)
-        we = _embed_one(i, w.detach(), k)
-        y = ops.conv_fwd(x, we, geom, pro=pro, cbias=cbias, taps=taps)
-        ctx.geom, ctx.pro, ctx.taps, ctx.i, ctx.k = geom, pro, taps, i, k
+        y = ops.conv_fwd(x, w, geom, pro=pro, cbias=cbias, taps=taps)
+        ctx.geom, ctx.pro, ctx.taps = geom, pro, taps
         ctx.lst = _lane_ctx()
         ctx.has_bias = cbias is not None
         ctx.cbias = cbias
-        ctx.w = w
-        ctx.save_for_backward(x, we)
+        ctx.save_for_backward(x, w)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, we = ctx.saved_tensors
+        x, w = ctx.saved_tensors
         g = cl(g)
-        dw = _zeros_like(we)
+        dw = _zeros_like(w)
         # the conv bias and the prologue scalars are parameters themselves: their sums go straight
         # into their gradient buffers (the kernels add), no zeroed temporaries and accumulations
         dcb = da = db = None
@@ -346,16 +296,11 @@ class CausalConvFn(torch.autograd.Function):
             dcb = _sgrad(ctx.lst, ctx.cbias)
         if ctx.pro is not None:
             da, db = _sgrad(ctx.lst, ctx.pro[0]), _sgrad(ctx.lst, ctx.pro[1])
-        gx, _ = ops.conv_bwd(g, x, we, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
+        gx, _ = ops.conv_bwd(g, x, w, ctx.geom, pro=ctx.pro, aux=x, want_gx=ctx.needs_input_grad[0], dw=dw,
                              dcbias=dcb, dpro_pre=db, dpro_post=da, taps=ctx.taps)
-        dws = _unembed_one(ctx.i, dw, ctx.k, ctx.w.shape)
-        if _direct(ctx.w):
-            from .functional import grad_buf
-            grad_buf(ctx.w).add_(dws)
-            dws = None
-        return (gx, dws, None if dcb is None or _direct(ctx.cbias) else dcb,
-                None if da is None or _direct(ctx.pro[0]) else da,
-                None if db is None or _direct(ctx.pro[1]) else db, None, None, None)
+        return (gx, dw, None if dcb is None or _is_param(ctx.cbias) else dcb,
+                None if da is None or _is_param(ctx.pro[0]) else da,
+                None if db is None or _is_param(ctx.pro[1]) else db, None, None)
 
 
 # the 16-bit weight shadow of the current forward: (FlatParams, dtype) when the parameters live in
@@ -376,84 +321,48 @@ def _rows_ok(t):
             and t.shape[1] % 8 == 0 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
 
 
-def _gemm_rows(x2, w2, trans_w, bias, n_out):
-    """vq3d_rows_gemm: y[v][j] = sum_i x2[v][i] w'[j][i] (+ bias), w' = w2 (trans_w 0) or w2^T"""
-    y = torch.empty((x2.shape[0], n_out), dtype=x2.dtype, device=x2.device)
-    L.call("vq3d_rows_gemm", L.dtype_code(x2), x2.shape[0], x2.shape[1], n_out, L.ptr(x2), x2.stride(0), L.ptr(w2),
-           w2.stride(0), trans_w, None if bias is None else L.ptr(bias), L.ptr(y), n_out, L.stream())
-    return y
-
-
 class PointwiseFn(torch.autograd.Function):
-    """1x1x1 conv of a channels-last (b, c, d, h, w) tensor as GEMMs over its voxel rows.  16-bit
-    rows (channel counts multiples of 8, 16-byte aligned) run on libvq3d: the forward y = x W^T + b
-    and the backward-data gx = g W on vq3d_rows_gemm (matrix cores, fp32 accumulation, the weights
-    from the 16-bit flat shadow), the weight gradient sum_v g[v] (x) x[v] (voxels as its K
-    dimension) on vq3d_rows_wgrad (split K, fixed-order sum, bias sums included) added straight
-    into the parameters' gradient buffers.  The input may carry zero pad channels past the weight's
-    (the attention projections' 515 / 259 inputs padded to 520 / 264, CausalAttentionPixelBlock):
-    the weight is padded with zero columns to match and the pad's gradient is dropped.  fp32 rows
-    (the reference-parity path) run torch GEMMs: F.linear, and a batched fp32 GEMM over 256-voxel
-    slices plus one sum over the slices for the weight gradient."""
+    """1x1x1 conv of a channels-last (b, c, d, h, w) tensor as GEMMs over its voxel rows
+    (hipBLASLt, fp32 accumulation) for y and gx.  The weight gradient sum_v g[v] (x) x[v] has the
+    voxels as its K dimension and only co x ci outputs: on 16-bit rows it is vq3d_rows_wgrad
+    (matrix cores, split K, fixed-order sum, bias sums included) adding straight into the
+    parameters' gradient buffers; fp32 rows (the reference-parity path) run a batched fp32 GEMM over
+    256-voxel slices plus one sum over the slices."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         xv = x.permute(0, 2, 3, 4, 1).reshape(-1, x.shape[1])
-        co, cin = w.shape[0], x.shape[1]
-        w2 = _w16(w, x.dtype).reshape(co, -1)
+        w2 = _w16(w, x.dtype).reshape(w.shape[0], -1)
+        y = F.linear(xv, w2, None if b is None else _w16(b, x.dtype))
+        ctx.save_for_backward(xv, w2)
         ctx.shape = (x.shape[0],) + tuple(x.shape[2:])
         ctx.prm = (w, b)
-        ctx.lib = x.dtype != torch.float32 and _rows_ok(xv) and co % 8 == 0
-        if ctx.lib:
-            if w2.shape[1] != cin or not _rows_ok(w2):
-                w2 = F.pad(w2, (0, cin - w2.shape[1])).contiguous()
-            y = _gemm_rows(xv, w2, 0, None if b is None else b.detach(), co)
-        else:
-            y = F.linear(xv, w2, None if b is None else _w16(b, x.dtype))
-        ctx.save_for_backward(xv, w2)
-        return y.reshape(ctx.shape + (co,)).permute(0, 4, 1, 2, 3)
+        return y.reshape(ctx.shape + (w.shape[0],)).permute(0, 4, 1, 2, 3)
 
     @staticmethod
     def backward(ctx, g):
         xv, w2 = ctx.saved_tensors
         w, b = ctx.prm
-        co, cin, wi = w2.shape[0], xv.shape[1], w.shape[1]
+        co = w2.shape[0]
         gv = g.permute(0, 2, 3, 4, 1).reshape(-1, co)
         if not gv.is_contiguous():
             gv = gv.contiguous()
         gx = None
-        lib = ctx.lib and gv.dtype == xv.dtype and _rows_ok(gv)
         if ctx.needs_input_grad[0]:
-            gx2 = _gemm_rows(gv, w2, 1, None, cin) if lib else gv @ w2.to(gv.dtype)
-            gx = gx2.reshape(ctx.shape + (cin,)).permute(0, 4, 1, 2, 3)
+            gx = (gv @ w2.to(gv.dtype)).reshape(ctx.shape + (w2.shape[1],)).permute(0, 4, 1, 2, 3)
         n = gv.shape[0]
-        if lib:
-            from .functional import grad_buf
-            padded = cin != wi
-            dw = ops.zero_(torch.empty(w2.shape, dtype=torch.float32, device=w2.device)) if padded else _param_grad(w)
+        if gv.dtype == xv.dtype and _rows_ok(gv) and _rows_ok(xv):
+            dw = _param_grad(w)
             db = None if b is None else _param_grad(b)
-            nws = int(L.query("vq3d_rows_wgrad_workspace_bytes", n, co, cin))
+            nws = int(L.query("vq3d_rows_wgrad_workspace_bytes", n, co, xv.shape[1]))
             ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=gv.device)
-            L.call("vq3d_rows_wgrad", L.dtype_code(gv), n, co, cin, L.ptr(gv), gv.stride(0), L.ptr(xv),
+            L.call("vq3d_rows_wgrad", L.dtype_code(gv), n, co, xv.shape[1], L.ptr(gv), gv.stride(0), L.ptr(xv),
                    xv.stride(0), L.ptr(dw), L.ptr(db), L.ptr(ws), ctypes_size(nws), L.stream())
-            if padded:  # the real columns of the padded weight's gradient
-                dw = dw[:, :wi].reshape(w.shape)
-                if _direct(w):
-                    grad_buf(w).add_(dw)
-            return gx, None if _direct(w) else dw, None if b is None or _direct(b) else db
+            return gx, None if _is_param(w) else dw, None if b is None or _is_param(b) else db
         sk = 256 if n % 256 == 0 and n >= 4096 else n
-        gw = torch.bmm(gv.reshape(-1, sk, co).transpose(1, 2).float(), xv.reshape(-1, sk, cin).float()).sum(0)
-        gw = gw[:, :wi].reshape(w.shape)
+        gw = torch.bmm(gv.reshape(-1, sk, co).transpose(1, 2).float(), xv.reshape(-1, sk, xv.shape[1]).float()).sum(0)
         gb = gv.float().sum(0) if b is not None else None
-        # into the gradient buffers directly, like the rows path (no AccumulateGrad node: CausalConvFn)
-        from .functional import grad_buf
-        if _direct(w):
-            grad_buf(w).add_(gw)
-            gw = None
-        if gb is not None and _direct(b):
-            grad_buf(b).add_(gb)
-            gb = None
-        return gx, gw, gb
+        return gx, gw.reshape(w.shape), gb
 
 
 def pointwise(x, w, b):
@@ -476,18 +385,6 @@ def _embed_one(i, w, k):
     if i == 1:
         return F.pad(w, (0, 0, 0, 1, 1, 1))
     return F.pad(w, (0, 3 - w.shape[-1], 1, 1, 1, 1))
-
-
-def _unembed_one(i, dw, k, shape):
-    """the gradient of stream i's reference-shaped kernel from the embedded kernel's (_embed_one's
-    live taps)"""
-    if k == 1:
-        return dw
-    if i == 0:
-        return dw[:, :, :shape[2]]
-    if i == 1:
-        return dw[:, :, 1:2, :shape[3]]
-    return dw[:, :, 1:2, 1:2, :shape[4]]
 
 
 def _tap_mask(stream, k, wk):
@@ -546,7 +443,7 @@ class CausalConv3dAdd(nn.Module):
         if k not in (1, 3):
             raise NotImplementedError("causal conv kernel sizes 1 and 3 (the reference's default) are supported")
         conv = (self.depth_conv, self.height_conv, self.width_conv)[i]
-        w, b = conv.weight, conv.bias
+        w, b = _embed_one(i, conv.weight, k), conv.bias
         if k == 1:  # a plain GEMM over the voxels (hipBLASLt): pre-activation + shift as glue
             x = _operand(x) if pro is None else _preact(x, pro)
             if self.mask == "A":
@@ -557,7 +454,7 @@ class CausalConv3dAdd(nn.Module):
             x = _shift(_operand(x) if pro is None else _preact(x, pro), i)
         elif pro is not None:
             pa, pb = pro
-        return CausalConvFn.apply(_operand(x), w, b, pa, pb, k, _tap_mask(i, k, self.width_conv.weight.shape[-1]), i)
+        return CausalConvFn.apply(_operand(x), w, b, pa, pb, k, _tap_mask(i, k, self.width_conv.weight.shape[-1]))
 
     def forward(self, stack):
         return torch.stack(self.run(to_list(stack)))
@@ -579,11 +476,11 @@ class ExpandRFConv(nn.Module):
 
     def run(self, stack):
         d, h, w = stack
-        # on lane 0 (the lanes only ever synchronise with lane 0, forward and backward: side-to-side
-        # waits inside a captured multi-stream backward crashed hipStreamEndCapture on this ROCm)
-        h = _take(0, 1, h)
-        w = _take(0, 2, w)
+        # on lane 0 (the lanes only ever synchronise with lane 0: side-to-side waits inside a
+        # captured multi-stream backward crash hipStreamEndCapture on this ROCm)
         with _lane(0):
+            h = _take(0, 1, h)
+            w = _take(0, 2, w)
             dc = pointwise(_operand(d), self.depth_conv.weight, self.depth_conv.bias)
             dch, dcw = torch.chunk(dc, 2, dim=1)
             hc = pointwise(_operand(h), self.height_conv.weight, self.height_conv.bias)
@@ -907,12 +804,6 @@ class PixelSNAIL(nn.Module):
                 _shadow[0] = (fl, self.compute_dtype)
         x = cl(pointwise(x, self.parse_input.weight, self.parse_input.bias))
         bg = background_list(b, dims, self.compute_dtype, x.device)
-        if self.compute_dtype != torch.float32:
-            # 16-bit: the background channels padded with zeros to a multiple of 8, so the attention
-            # projections' inputs (2 C + 3 / C + 3 channels) are 16-byte voxel rows for vq3d_rows_gemm
-            # (PointwiseFn pads the weights to match; the zero channels add nothing)
-            bgp = cl(F.pad(bg[0], (0, 0, 0, 0, 0, 0, 0, (-bg[0].shape[1]) % 8)))
-            bg = [bgp] * len(bg)
         lanes = None
         if _lanes_on[0] and self.compute_dtype != torch.float32 and x.is_cuda:
             # (the lane streams exist before any capture: created on the first eager forward)
@@ -921,7 +812,7 @@ class PixelSNAIL(nn.Module):
                 lanes = [torch.cuda.current_stream()] + aux
         _LANES[0] = lanes
         if lanes is not None:
-            shared = [p for p in self.parameters() if p.numel() == 1 and p.requires_grad]
+            shared = [p for p in self.parameters() if p.numel() == 1]
             _LSTATE[0] = _LaneGrads(shared, lanes, x.device)
         try:
             xs = [x] + [_take(i, 0, x, bg[0])[0] for i in (1, 2)]

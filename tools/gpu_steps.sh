@@ -4,7 +4,7 @@
 # Each STEP runs under its own time limit, writes gpurun_out/TAG_<name>.log, and the script stops
 # at the first failing step (no GPU work after a fault, abort or timeout).  STEPs:
 #   gputests            the whole `pytest -m gpu` suite (what the driver runs at round end)
-#   tests:<k-expr>      pytest -m gpu -k <k-expr> over tests/
+#   tests:<k-expr>      pytest -m gpu -k <k-expr> over tests/ ("_or_" stands for " or ")
 #   file:<test file>    pytest -m gpu on one test file
 #   smoke               __graft_entry__.smoke()
 #   race                tools/dbg/lanes_race.py (PixelSNAIL lanes replays at the published size)
@@ -32,7 +32,8 @@ run() {  # name, seconds, command...
 for s in "$@"; do
     case $s in
         gputests) run gputests 1100 $PYT tests || exit $? ;;
-        tests:*) run "tests_$(echo "${s#tests:}" | tr -c 'a-zA-Z0-9_' '_')" 900 $PYT tests -k "${s#tests:}" || exit $? ;;
+        tests:*) k="${s#tests:}"; k="${k//_or_/ or }"  # tests:a_or_b -> -k "a or b"
+                 run "tests_$(echo "${s#tests:}" | tr -c 'a-zA-Z0-9_' '_')" 900 $PYT tests -k "$k" || exit $? ;;
         file:*) run "file_$(basename "${s#file:}" .py)" 900 $PYT "${s#file:}" || exit $? ;;
         smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
         race) run race 600 python -u tools/dbg/lanes_race.py 3 4 || exit $? ;;
