@@ -53,7 +53,7 @@ ENC_ROOF_MS = {"3l_pub": 0.42, "3l_dflt": 0.27}  # encoder-only 
 ENC_BYTES = {"3l_pub": 3.39e9, "3l_dflt": 2.19e9}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0  # dense bf16
-ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: committed profiles of the most recent round win
+ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # newest first: committed profiles of the most recent round win
 STEP_TOP = next((p for p in (os.path.join(ROOT, "profiles", f"{r}_step_top.json") for r in ROUNDS)
                  if os.path.exists(p)), os.path.join(ROOT, "profiles", "r02_step_top.json"))
 

@@ -15,7 +15,12 @@ What the fixture holds and how it is compared (bounds below, stated with the mea
   * gradients: every parameter's norm (relative), the whole sampled gradient vector (relative L2
     and cosine), every weight tensor's sampled entries (relative L2 and cosine; tensors of more
     than 4,096 entries are represented by 512 seeded positions, so their error is an estimate),
-    the scalar biases / scales per block stack as one vector.
+    the scalar biases / scales per block stack as one vector;
+  * fp32 (the north star's "code indices bit-exact vs reference"): the same forward in fp32 against
+    the reference's codes, >= 99.9 % per level, and every differing row shown to be a Voronoi-boundary
+    flip from the fixture's own Quantizer inputs z{lvl} and search codebooks cb{lvl} (measured r06:
+    99.9994 / 100 / 100 %, 3 of 524,288 bottom rows, each within 0.55 of its z / codebook movement
+    from the bisector; z within 7e-7 of the reference's, loss 7e-8 relative).
 """
 import os
 
@@ -33,13 +38,14 @@ PATH = os.path.join(GOLDEN, "model_3l_pub_512.npz")
 # per dtype: code floors (bottom, mid, top), (loss rel, commitment rel, decoded rel-MSE, sampled-
 # gradient rel-L2 / cosine, per-tensor rel-L2 / cosine, scalar-group rel-L2, gradient-norm rel).
 # Measured (r05): bf16 codes 94.70 / 92.00 / 95.31 %, loss 1.3e-3, decoded 7.7e-4, sampled gradient
-# 2.46 % / 0.99976, worst tensor 0.387 / 0.990; fp16 codes 99.35 / 99.65 / 100 %, loss 2.4e-6, decoded
-# 5.5e-6, sampled gradient 1.67 % / 0.99986, worst tensor 0.116 / 0.9956.  bf16's mid level sits
+# 2.46 % / 0.99976, worst tensor 0.387 / 0.990; fp16 codes 99.34 / 99.62 / 100 %, loss 2.8e-6, decoded
+# 6.4e-6, sampled gradient 1.67 % / 0.99986, worst tensor 0.032 / 0.99995 (r06: libvq3d's zero fills as
+# kernels; round 5, with hipMemsetAsync fills, 0.116 / 0.9956).  bf16's mid level sits
 # below its 256^2 floor because 6 of the 128 top codes flip at this size and every mid voxel is
 # conditioned on the top level's ST output through the UpBlock (two ResizeConvs + 3 + 3 blocks:
 # a receptive field spanning most of the 32 x 32 x 8 mid grid); fp16 flips none.
 BOUNDS = {"bf16": ((0.94, 0.91, 0.94), (1e-2, 5e-2, 1.5e-3, 0.04, 0.999, 0.5, 0.98, 0.1, 0.5)),
-          "fp16": ((0.99, 0.995, 1.0), (2e-3, 1e-2, 2e-5, 0.025, 0.9998, 0.15, 0.99, 0.05, 0.1))}
+          "fp16": ((0.99, 0.995, 1.0), (2e-3, 1e-2, 2e-5, 0.025, 0.9998, 0.06, 0.999, 0.05, 0.06))}
 
 
 def _perturb(m, seed=1, std=0.02):
