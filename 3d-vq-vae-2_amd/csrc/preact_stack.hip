@@ -945,8 +945,13 @@ __global__ __launch_bounds__(NT) void k_stackm_bwd(SkArgs a, const h16_t *__rest
 // result equals the fused kernel's.  W2: waves own taps (wave, wave + 16); W1: waves 0, 1; W3 and
 // the scale gradient (sum W3 . G3): waves 2, 3.  Each gradient entry has one adder.
 constexpr int PG = 40;  // row pitch of the bf16 g record copy
+#ifndef VQ3D_STACK_RCW
+#define VQ3D_STACK_RCW 4
+#endif
+constexpr int RPART = VQ3D_STACK_RCW;  // k_stackr_bwd's scalar partials per block (one per compute wave)
 __global__ __launch_bounds__(NT) void k_stackm_wgrad(SkArgs a, const float *const *tab, float *const *gtab,
-                                                     const float *__restrict__ saved, const h16_t *__restrict__ rec) {
+                                                     const float *__restrict__ saved, const h16_t *__restrict__ rec,
+                                                     const float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nv = a.nv, nks = nv / 32, nvc = nv * MC, nvb = nv * MB, blk = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
@@ -1029,10 +1034,551 @@ __global__ __launch_bounds__(NT) void k_stackm_wgrad(SkArgs a, const float *cons
     }
     __syncthreads();
     if (wave == 0 && lane == 9) *gc = *gc + (0.f + red[0] + red[1]);  // lane 9 holds the scale slot
+    if (part && wave == 0 && lane >= 3 && lane < NPRM && lane != 9) {
+        // k_stackr_bwd's scalar partials of this block: table slot k gets ps[10 - k], waves in order
+        const float *pp = part + size_t(blk) * RPART * 8 + (10 - lane);  // [block][compute wave][8]
+        float add = 0.f;
+#pragma unroll
+        for (int w = 0; w < RPART; ++w) add += pp[8 * w];
+        *gc = *gc + add;
+    }
 }
+// ============================================================================================ register chain
+// The published top level's chains with ONE barrier per block (round 6; k_stackm_* above needed
+// five per block plus the scalar-sum barriers).  Layout of one MFMA: the block's weights are the A
+// operand and 16 voxels the N columns, so a lane's accumulator holds 4 consecutive output channels
+// of ONE voxel; with the 1x1 stages' K axis ordered to match (rch: k = 8 kb + j <-> channel 4 kb + j
+// for j < 4, 16 + 4 kb + j - 4 above) every stage's accumulator is the next stage's B operand and
+// the residual / gradient stream (channels rch(kb, 0..7) of the lane's voxel) never leaves the
+// registers.  Only the k^3 conv meets other voxels: t2 (forward) / gz3 (backward) go to LDS, one
+// barrier, and each lane gathers its 14 neighbour rows (offsets precomputed once).
+//
+// Roles.  Waves 0..3 compute, each on two 16-voxel column blocks (w, w + 4), and hold the block's
+// 17 A fragments (packed per lane by k_stackr_pack) in registers, each refilled with the next
+// block's right after its last use.  Waves 4..7 only store: everything the chain saves (forward:
+// x, t2, t3; backward: the record g, gz3, gz1 and the scalar partials) is written to an LDS ring by
+// the compute waves and copied out by the store waves one block later.  The split is what makes
+// the prefetch work: on gfx9 loads and stores share vmcnt and complete out of order with respect
+// to each other, so a wave with a store in flight can only wait for a load with vmcnt(0) -- every
+// use of a prefetched fragment then waited for the block's stores too (2.7 / 3.1 us per block
+// forward / backward when the compute waves stored).  Compute waves without stores wait with
+// exact counts.  The ring is 3 deep (block b's slot is rewritten in block b + 3, after the store
+// waves' reads in block b + 1 and two barriers).  Rounding points are k_stackm_*'s.
+#ifndef VQ3D_STACK_RCW
+#define VQ3D_STACK_RCW 4
+#endif
+constexpr int RCW = VQ3D_STACK_RCW;      // compute waves; wave w owns column blocks w, w + RCW, ...
+constexpr int RSW = 4;                   // store waves
+constexpr int NH = MAXVM / 16 / RCW;     // column blocks per compute wave
+constexpr int RNT = (RCW + RSW) * 64;
+static_assert(NH * RCW * 16 == MAXVM, "column blocks");
+constexpr int RF = 17;                   // A fragments per block
+constexpr int RIMG = RF * 64 * 8;        // halves per block image
+static_assert(RPART == RCW, "one scalar partial per compute wave");
+static_assert(RIMG == FR_N, "the register chain's images fit the k_stackm image slots");
+constexpr int RPS = 8;                   // scalar partials per compute wave and block (k_stackm_bwd's ps order)
+constexpr int RRING = 3;
+constexpr int RPF = 3;                   // store waves' L2 prefetch distance (blocks)
+#if defined(VQ3D_STACK_EXP) && VQ3D_STACK_EXP == 2
+#define FR_REFILL(k0, k1)
+#else
+#define FR_REFILL(k0, k1) fr.load(img, nx, lane, k0, k1)
+#endif
+
+// phase clock probe (tools/probes/stack_probe.hip builds this file with VQ3D_STACK_PROBE): wave 0
+// stamps s_memtime at 5 points of every block into LDS and dumps them at the end
+#ifdef VQ3D_STACK_PROBE
+__device__ unsigned long long g_stack_probe[2][64][5];
+#define RPROBE_DECL __shared__ unsigned long long rprobe[64][5];
+#define RPROBE(b, k) \
+    if (wave == 0 && lane == 0 && (b) < 64) rprobe[b][k] = __builtin_amdgcn_s_memtime();
+#define RPROBE_DUMP(dir)                                          \
+    if (wave == 0)                                                \
+        for (int i = lane; i < 64 * 5; i += 64) g_stack_probe[dir][i / 5][i % 5] = rprobe[i / 5][i % 5];
+#else
+#define RPROBE_DECL
+#define RPROBE(b, k)
+#define RPROBE_DUMP(dir)
+#endif
+
+// a load through a pointer read from the parameter table, as a GLOBAL load: the generic (flat) load
+// the compiler emits otherwise counts in both vmcnt and lgkmcnt, and its use then waits for every
+// memory operation in flight (vmcnt(0) lgkmcnt(0)), prefetched fragments included
+__device__ __forceinline__ float ldg(const float *p) {
+    typedef const __attribute__((address_space(1))) float gfloat;
+    return *(gfloat *)(p);
+}
+
+__device__ __forceinline__ int rch(int kb, int j) { return j < 4 ? 4 * kb + j : 16 + 4 * kb + (j - 4); }
+
+// Fragment f of a block, lane l = kb * 16 + m, element j (k = 8 kb + j).  Forward: f 0 W1 (A[o][k] =
+// W1[o][rch(k)]), f 1 .. 14 W2 tap pairs (A[co][k] = W2[co][ci][tap], tap = 2 (f - 1) + (kb >> 1),
+// ci = 8 (kb & 1) + j), f 15 / 16 W3 tiles (A[co][k] = W3[co][4 kb + j], j < 4).  Backward: f 0 W3^T
+// (A[o][k] = W3[rch(k)][o]), f 1 .. 14 W2 transposed (A[ci][k] = W2[co][ci][tap], co = 8 (kb & 1) +
+// j; the B rows come from the flipped tap's neighbour), f 15 / 16 W1^T tiles (A[c][k] = W1[4 kb + j][c]).
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_stackr_pack(const float *const *tab, h16_t *__restrict__ img) {
+    const int blk = blockIdx.x;
+    const float *w1 = tab[blk * NPRM + 0], *w2 = tab[blk * NPRM + 1], *w3 = tab[blk * NPRM + 2];
+    h16_t *dst = img + size_t(blk) * RIMG;
+    for (int i = threadIdx.x; i < RF * 64; i += 256) {
+        const int f = i >> 6, lane = i & 63, m = lane & 15, kb = lane >> 4;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x = 0.f;
+            if (f == 0) {
+                x = BWD ? w3[rch(kb, j) * MB + m] : w1[m * MC + rch(kb, j)];
+            } else if (f < 15) {
+                const int tap = 2 * (f - 1) + (kb >> 1), c = 8 * (kb & 1) + j;
+                if (tap < 27) x = BWD ? w2[(c * MB + m) * 27 + tap] : w2[(m * MB + c) * 27 + tap];
+            } else if (j < 4) {
+                const int t = 16 * (f - 15) + m;
+                x = BWD ? w1[(4 * kb + j) * MC + t] : w3[t * MB + 4 * kb + j];
+            }
+            v[j] = x;
+        }
+        *reinterpret_cast<uint4 *>(dst + size_t(i) * 8) = __builtin_bit_cast(uint4, pack8(v));
+    }
+}
+
+struct RFrag {  // one block's 17 A fragments of this lane
+    u32x4 f[RF];
+    __device__ __forceinline__ void load(const h16_t *img, int blk, int lane, int k0 = 0, int k1 = RF) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(img + size_t(blk) * RIMG) + lane;
+#pragma unroll
+        for (int k = 0; k < RF; ++k)
+            if (k >= k0 && k < k1) f[k] = src[64 * k];
+    }
+    __device__ __forceinline__ hx8 operator[](int k) const { return __builtin_bit_cast(hx8, f[k]); }
+};
+
+// the 14 neighbour rows lane (voxel v, kb) gathers, as element offsets into a [nv][PT] branch image
+// packed two per dword: tap 2 s + (kb >> 1) (backward: its flip), channels 8 (kb & 1) .. + 7.  Tap
+// 27 (s = 13, kb >= 2) has no row: those lanes read zeros.
+template <bool BWD>
+__device__ __forceinline__ void nbr_rows(const SkArgs &a, int v, int kb, uint32_t (&o)[7]) {
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+        uint32_t lo = 0, hi = 0;
+        const int t0 = 4 * s + (kb >> 1), t1 = t0 + 2;
+        lo = uint32_t(nbr(a, v, BWD ? 26 - t0 : t0, 1) * PT + 8 * (kb & 1));
+        if (t1 < 27) hi = uint32_t(nbr(a, v, BWD ? 26 - t1 : t1, 1) * PT + 8 * (kb & 1));
+        o[s] = lo | (hi << 16);
+    }
+}
+__device__ __forceinline__ void gather14(const h16_t *src, const uint32_t (&o)[7], int kb, hx8 (&nb)[14]) {
+#pragma unroll
+    for (int s = 0; s < 14; ++s) {
+        const uint32_t off = (o[s >> 1] >> (16 * (s & 1))) & 0xffffu;
+        nb[s] = (s == 13 && kb >= 2) ? zero8() : rd8(src + off);
+    }
+}
+// the two halves of the 14 tap-pair k-steps (k_stackm's summation order)
+__device__ __forceinline__ f32x4 conv14(const RFrag &fr, const hx8 (&nb)[14]) {
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        c0 = mfma(fr[1 + k], nb[k], c0);
+        c1 = mfma(fr[8 + k], nb[7 + k], c1);
+    }
+    return c0 + c1;
+}
+// exp through v_exp_f32 (2^x) directly: the chain is VALU-issue bound (one compute wave per SIMD,
+// 4 cycles per instruction), and expf's range reduction was ~11 instructions per call, a third of
+// the forward loop; the results are rounded to 16 bits (t2, t3) or feed fp32 gradients
+__device__ __forceinline__ float exp_f(float z) { return __builtin_amdgcn_exp2f(z * 1.44269504088896341f); }
+__device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : exp_f(z) - 1.f; }
+__device__ __forceinline__ uint32_t pk2h(float a, float b) { return uint32_t(f2h(a)) | (uint32_t(f2h(b)) << 16); }
+__device__ __forceinline__ float lo_h(uint32_t u) { return h2f_lo(u & 0xffffu); }
+__device__ __forceinline__ float hi_h(uint32_t u) { return h2f_lo(u >> 16); }
+
+struct RfLds {  // the forward's LDS ring (RRING slots)
+    float *xs;    // [nv][PF] the block's input x (fp32)
+    h16_t *t2s;   // [nv][PT] t2 (16-bit): the conv's gather source
+    h16_t *t3s;   // [nv][PT] t3 (16-bit)
+};
+__device__ __forceinline__ RfLds rf_slot(char *smem, int nv, int slot) {
+    RfLds l;
+    char *p = smem + size_t(slot) * (size_t(nv) * PF * 4 + size_t(nv) * PT * 4);
+    l.xs = reinterpret_cast<float *>(p);
+    l.t2s = reinterpret_cast<h16_t *>(p + size_t(nv) * PF * 4);
+    l.t3s = l.t2s + nv * PT;
+    return l;
+}
+size_t lds_rf(int nv) { return RRING * (size_t(nv) * PF * 4 + size_t(nv) * PT * 4); }
+
+// store waves: block b's x / t2 / t3 from ring slot b % 3 to `saved` (fp32, k_stackm_fwd's layout)
+__device__ __forceinline__ void rf_store(const RfLds &l, int nv, float *sx, int t) {
+    float *st2 = sx + nv * MC, *st3 = st2 + nv * MB;
+    for (int i = t; i < nv * (MC / 4); i += 256) {
+        const int v = i >> 3, c = 4 * (i & 7);
+        *reinterpret_cast<float4 *>(sx + v * MC + c) = *reinterpret_cast<const float4 *>(l.xs + v * PF + c);
+    }
+    for (int i = t; i < nv * (MB / 4); i += 256) {
+        const int v = i >> 2, o = 4 * (i & 3);
+        const u32x2 a = *reinterpret_cast<const u32x2 *>(l.t2s + v * PT + o);
+        const u32x2 b = *reinterpret_cast<const u32x2 *>(l.t3s + v * PT + o);
+        *reinterpret_cast<float4 *>(st2 + v * MB + o) = float4{lo_h(a[0]), hi_h(a[0]), lo_h(a[1]), hi_h(a[1])};
+        *reinterpret_cast<float4 *>(st3 + v * MB + o) = float4{lo_h(b[0]), hi_h(b[0]), lo_h(b[1]), hi_h(b[1])};
+    }
+}
+
+template <bool FULL>  // FULL: nv = 128, every column block active (the published top level)
+__global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__restrict__ x, const float *const *tab,
+                                                    h16_t *__restrict__ out, float *__restrict__ saved,
+                                                    const h16_t *__restrict__ img) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    RPROBE_DECL
+    // the wave index through readfirstlane: the compiler then knows it (and the column-block masks
+    // below) wave-uniform and branches instead of masking exec around every load
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), n = lane & 15,
+              kb = lane >> 4;
+    const int nv = a.nv, nmt = nv / 16;
+    const size_t stride = size_t(nv) * (MC + 2 * MB);
+    if (wave >= RCW) {  // store waves: block b - 1's tensors after barrier b, the last block's after the loop
+        const int t = tid - RCW * 64;  // 0 .. RSW * 64 - 1
+        // and the L2 prefetch of the fragment images RPF blocks ahead (one dword per 128-B line; the
+        // value is only "used" a block later, so this wave never waits on it)
+        uint32_t pf = 0;
+        auto touch = [&](int b) {
+            return t < RIMG * 2 / 128 ? *reinterpret_cast<const uint32_t *>(img + size_t(b) * RIMG + t * 64) : 0u;
+        };
+        for (int b = 0; b < RPF && b < a.nblk; ++b) pf ^= touch(b);
+        for (int blk = 0; blk < a.nblk; ++blk) {
+            __syncthreads();
+            asm volatile("" ::"v"(pf));
+            if (blk > 0) rf_store(rf_slot(smem, nv, (blk - 1) % RRING), nv, saved + (blk - 1) * stride, t);
+            pf = blk + RPF < a.nblk ? touch(blk + RPF) : 0u;
+        }
+        asm volatile("" ::"v"(pf));
+        __syncthreads();
+        rf_store(rf_slot(smem, nv, (a.nblk - 1) % RRING), nv, saved + (a.nblk - 1) * stride, t);
+        return;
+    }
+    bool act[NH];
+    int vv[NH];
+    uint32_t nbo[NH][7];
+    float xv[NH][8];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int cb = wave + RCW * h;
+        act[h] = FULL || cb < nmt;
+        vv[h] = min(cb, nmt - 1) * 16 + n;
+        nbr_rows<false>(a, vv[h], kb, nbo[h]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[h][j] = ld(x + size_t(vv[h]) * MC + rch(kb, j));
+    }
+    RFrag fr;
+    fr.load(img, 0, lane);
+    float vc = ldg(row_ptr(tab, 0, lane));
+    const float *pn = row_ptr(tab, min(1, a.nblk - 1), lane);
+    for (int blk = 0; blk < a.nblk; ++blk) {
+        const Scal s = scal_lanes(vc);
+        RPROBE(blk, 0)
+        // the next block (the last block reloads itself: every load unconditional, so the
+        // compiler's waits count exactly), its scalars a block ahead
+#if defined(VQ3D_STACK_EXP) && VQ3D_STACK_EXP == 1
+        const int nx = 0;
+#else
+        const int nx = min(blk + 1, a.nblk - 1);
+#endif
+        vc = ldg(pn);
+        pn = row_ptr(tab, min(blk + 2, a.nblk - 1), lane);
+        const RfLds l = rf_slot(smem, nv, blk % RRING);
+        // t2 = elu_f(W1 u1 + b2a) + b2b, u1 = elu_f(x + b1a) + b1b (K in the rch order)
+        f32x4 a2[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const int v = vv[h];
+            *reinterpret_cast<float4 *>(l.xs + v * PF + 4 * kb) = float4{xv[h][0], xv[h][1], xv[h][2], xv[h][3]};
+            *reinterpret_cast<float4 *>(l.xs + v * PF + 16 + 4 * kb) = float4{xv[h][4], xv[h][5], xv[h][6], xv[h][7]};
+            float u[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) u[j] = elu_f(xv[h][j] + s.b1a) + s.b1b;
+            a2[h] = mfma(fr[0], pack8(u), f32x4{0.f, 0.f, 0.f, 0.f});
+        }
+        FR_REFILL(0, 1);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const f32x4 c = a2[h];
+            *reinterpret_cast<u32x2 *>(l.t2s + vv[h] * PT + 4 * kb) =
+                u32x2{pk2h(elu_f(c[0] + s.b2a) + s.b2b, elu_f(c[1] + s.b2a) + s.b2b),
+                      pk2h(elu_f(c[2] + s.b2a) + s.b2b, elu_f(c[3] + s.b2a) + s.b2b)};
+        }
+        RPROBE(blk, 1)
+        __syncthreads();
+        RPROBE(blk, 2)
+        // t3 = elu_f(W2 (*) t2 + b3a) + b3b over the gathered neighbour rows
+        u32x2 t3p[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            hx8 nb[14];
+            gather14(l.t2s, nbo[h], kb, nb);
+            const f32x4 c = conv14(fr, nb);
+            t3p[h] = u32x2{pk2h(elu_f(c[0] + s.b3a) + s.b3b, elu_f(c[1] + s.b3a) + s.b3b),
+                           pk2h(elu_f(c[2] + s.b3a) + s.b3b, elu_f(c[3] + s.b3a) + s.b3b)};
+            *reinterpret_cast<u32x2 *>(l.t3s + vv[h] * PT + 4 * kb) = t3p[h];
+        }
+        RPROBE(blk, 3)
+        FR_REFILL(1, 15);
+        // x += scale * W3 t3 + b4 (two channel tiles; K = the lane's 4 t3 channels + zeros)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const hx8 b3 = __builtin_bit_cast(hx8, u32x4{t3p[h][0], t3p[h][1], 0u, 0u});
+            const f32x4 o0 = mfma(fr[15], b3, f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 o1 = mfma(fr[16], b3, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xv[h][i] += o0[i] * s.sc + s.b4;
+                xv[h][4 + i] += o1[i] * s.sc + s.b4;
+            }
+        }
+        FR_REFILL(15, RF);
+        RPROBE(blk, 4)
+    }
+    __syncthreads();  // the store waves' last block
+    RPROBE_DUMP(0)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        if (!act[h]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) out[size_t(vv[h]) * MC + rch(kb, j)] = f2h(xv[h][j]);
+    }
+}
+
+struct RbLds {  // the backward's LDS ring
+    h16_t *gs;    // [nv][PG] the block's incoming gradient g (16-bit, the record)
+    h16_t *z3s;   // [nv][PT] gz3: the transposed conv's gather source
+    h16_t *z1s;   // [nv][PT] gz1
+    float *ps;    // [RCW][64][RPS] the compute lanes' scalar partials
+};
+__device__ __forceinline__ RbLds rb_slot(char *smem, int nv, int slot) {
+    RbLds l;
+    char *p = smem + size_t(slot) * (size_t(nv) * (PG + 2 * PT) * 2 + RCW * 64 * RPS * 4);
+    l.gs = reinterpret_cast<h16_t *>(p);
+    l.z3s = l.gs + nv * PG;
+    l.z1s = l.z3s + nv * PT;
+    l.ps = reinterpret_cast<float *>(l.z1s + nv * PT);
+    return l;
+}
+size_t lds_rb(int nv) { return RRING * (size_t(nv) * (PG + 2 * PT) * 2 + RCW * 64 * RPS * 4); }
+
+// store waves: block b's record (g, gz3, gz1: k_stackm_bwd's layout) and scalar partials
+__device__ __forceinline__ void rb_store(const RbLds &l, int nv, h16_t *rg, float *part, int t) {
+    h16_t *rz3 = rg + nv * MC, *rz1 = rz3 + nv * MB;
+    for (int i = t; i < nv * (MC / 8); i += 256) {
+        const int v = i >> 2, c = 8 * (i & 3);
+        *reinterpret_cast<u32x4 *>(rg + v * MC + c) = *reinterpret_cast<const u32x4 *>(l.gs + v * PG + c);
+    }
+    for (int i = t; i < nv * (MB / 4); i += 256) {
+        const int v = i >> 2, o = 4 * (i & 3);
+        *reinterpret_cast<u32x2 *>(rz3 + v * MB + o) = *reinterpret_cast<const u32x2 *>(l.z3s + v * PT + o);
+        *reinterpret_cast<u32x2 *>(rz1 + v * MB + o) = *reinterpret_cast<const u32x2 *>(l.z1s + v * PT + o);
+    }
+    // store wave q sums compute waves q, q + RSW, ... (DPP, fixed order); part [block][wave][RPS]
+    const int lane = t & 63;
+    for (int cw = t >> 6; cw < RCW; cw += RSW) {
+        const float *src = l.ps + (cw * 64 + lane) * RPS;
+        const float4 pa = *reinterpret_cast<const float4 *>(src), pb = *reinterpret_cast<const float4 *>(src + 4);
+        float ps[RPS] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+#pragma unroll
+        for (int k = 0; k < RPS; ++k) ps[k] = wave_sum(ps[k]);
+        if (lane < RPS) {
+            float pv = ps[0];
+#pragma unroll
+            for (int k = 1; k < RPS; ++k) pv = lane == k ? ps[k] : pv;
+            part[cw * RPS + lane] = pv;
+        }
+    }
+}
+
+// the backward chain: gradient stream in registers, gz3 through LDS for the transposed conv; the
+// record and the per-wave scalar partials leave through the store waves
+template <bool FULL>
+__global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__restrict__ g, const float *const *tab,
+                                                    const float *__restrict__ saved, h16_t *__restrict__ gx,
+                                                    h16_t *__restrict__ rec, float *__restrict__ part,
+                                                    const h16_t *__restrict__ img) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    RPROBE_DECL
+    // the wave index through readfirstlane: the compiler then knows it (and the column-block masks
+    // below) wave-uniform and branches instead of masking exec around every load
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), n = lane & 15,
+              kb = lane >> 4;
+    const int nv = a.nv, nmt = nv / 16, nvc = nv * MC, nvb = nv * MB;
+    const size_t stride = size_t(nv) * (MC + 2 * MB);
+    const int last = a.nblk - 1;
+    if (wave >= RCW) {  // store waves (the walk is in reverse)
+        const int t = tid - RCW * 64;  // 0 .. RSW * 64 - 1
+        // L2 prefetch RPF blocks ahead: the fragment image (136 lines) and the saved x / t2 / t3
+        // (nv / 2 lines of 128 B), one dword per line
+        uint32_t pf = 0;
+        const int sl = int(stride / 32);  // 128-B lines of one block's saved tensors
+        auto touch = [&](int b) {
+            uint32_t r = t < RIMG * 2 / 128 ? *reinterpret_cast<const uint32_t *>(img + size_t(b) * RIMG + t * 64) : 0u;
+            for (int i = t; i < sl; i += 256) r ^= *reinterpret_cast<const uint32_t *>(saved + b * stride + i * 32);
+            return r;
+        };
+        for (int b = last; b > last - RPF && b >= 0; --b) pf ^= touch(b);
+        for (int blk = last; blk >= 0; --blk) {
+            __syncthreads();
+            asm volatile("" ::"v"(pf));
+            pf = blk - RPF >= 0 ? touch(blk - RPF) : 0u;
+            if (blk < last)
+                rb_store(rb_slot(smem, nv, (blk + 1) % RRING), nv, rec + (blk + 1) * stride,
+                         part + (blk + 1) * RCW * RPS, t);
+        }
+        __syncthreads();
+        asm volatile("" ::"v"(pf));
+        rb_store(rb_slot(smem, nv, 0), nv, rec, part, t);
+        return;
+    }
+    bool act[NH];
+    int vv[NH];
+    uint32_t nbo[NH][7];
+    float gv[NH][8];
+    float4 s3[NH], s2[NH], sxa[NH], sxb[NH];  // the block's saved t3 / t2 (the lane's 4 branch channels), x (its 8)
+    auto sv4 = [&](int b, int off) { return *reinterpret_cast<const float4 *>(saved + b * stride + off); };
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int cb = wave + RCW * h;
+        act[h] = FULL || cb < nmt;
+        vv[h] = min(cb, nmt - 1) * 16 + n;
+        nbr_rows<true>(a, vv[h], kb, nbo[h]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[h][j] = ld(g + size_t(vv[h]) * MC + rch(kb, j));
+        const int ox = vv[h] * MC + 4 * kb, ob = vv[h] * MB + 4 * kb;
+        s3[h] = sv4(last, nvc + nvb + ob);
+        s2[h] = sv4(last, nvc + ob);
+        sxa[h] = sv4(last, ox);
+        sxb[h] = sv4(last, ox + 16);
+    }
+    RFrag fr;
+    fr.load(img, last, lane);
+    float vc = ldg(row_ptr(tab, last, lane));
+    const float *pn = row_ptr(tab, max(last - 1, 0), lane);
+    for (int blk = last; blk >= 0; --blk) {
+        const Scal s = scal_lanes(vc);
+        RPROBE(blk, 0)
+        const int nx = max(blk - 1, 0);  // the next block (unconditional loads, as in the forward)
+        vc = ldg(pn);
+        pn = row_ptr(tab, max(blk - 2, 0), lane);
+        const RbLds l = rb_slot(smem, nv, blk % RRING);
+        float ps[RPS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // b4, (scale), b3b, b3a, b2b, b2a, b1b, b1a
+        // gz3 = scale W3^T g * elu'(t3 - b3b)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const int v = vv[h];
+            const float *q = gv[h];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ps[0] += q[j];
+            *reinterpret_cast<u32x2 *>(l.gs + v * PG + 4 * kb) = u32x2{pk2h(q[0], q[1]), pk2h(q[2], q[3])};
+            *reinterpret_cast<u32x2 *>(l.gs + v * PG + 16 + 4 * kb) = u32x2{pk2h(q[4], q[5]), pk2h(q[6], q[7])};
+            const f32x4 a3 = mfma(fr[0], pack8(gv[h]), f32x4{0.f, 0.f, 0.f, 0.f});
+            const float t3v[4] = {s3[h].x, s3[h].y, s3[h].z, s3[h].w};
+            float zq[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float g3 = a3[i] * s.sc;
+                zq[i] = g3 * elu_d_act(t3v[i], s.b3b);
+                ps[2] += g3;
+                ps[3] += zq[i];
+            }
+            *reinterpret_cast<u32x2 *>(l.z3s + v * PT + 4 * kb) = u32x2{pk2h(zq[0], zq[1]), pk2h(zq[2], zq[3])};
+        }
+        fr.load(img, nx, lane, 0, 1);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) s3[h] = sv4(nx, nvc + nvb + vv[h] * MB + 4 * kb);
+        RPROBE(blk, 1)
+        __syncthreads();
+        RPROBE(blk, 2)
+        // gt2 = W2^T (*) gz3 over the flipped taps' neighbour rows; gz1 = gt2 * elu'(t2 - b2b)
+        u32x2 z1p[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            hx8 nb[14];
+            gather14(l.z3s, nbo[h], kb, nb);
+            const f32x4 c = conv14(fr, nb);
+            const float t2v[4] = {s2[h].x, s2[h].y, s2[h].z, s2[h].w};
+            float z[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                z[i] = c[i] * elu_d_act(t2v[i], s.b2b);
+                ps[4] += c[i];
+                ps[5] += z[i];
+            }
+            z1p[h] = u32x2{pk2h(z[0], z[1]), pk2h(z[2], z[3])};
+            *reinterpret_cast<u32x2 *>(l.z1s + vv[h] * PT + 4 * kb) = z1p[h];
+        }
+        RPROBE(blk, 3)
+        fr.load(img, nx, lane, 1, 15);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) s2[h] = sv4(nx, nvc + vv[h] * MB + 4 * kb);
+        // g += (W1^T gz1) * elu'(x + b1a), in the stream's channel order
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const hx8 bz = __builtin_bit_cast(hx8, u32x4{z1p[h][0], z1p[h][1], 0u, 0u});
+            const f32x4 o0 = mfma(fr[15], bz, f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 o1 = mfma(fr[16], bz, f32x4{0.f, 0.f, 0.f, 0.f});
+            const float xs[8] = {sxa[h].x, sxa[h].y, sxa[h].z, sxa[h].w, sxb[h].x, sxb[h].y, sxb[h].z, sxb[h].w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float gt1 = j < 4 ? o0[j] : o1[j - 4];
+                const float zx = xs[j] + s.b1a;
+                const float e = zx > 0.f ? 1.f : exp_f(zx);
+                ps[6] += gt1;
+                ps[7] += gt1 * e;
+                gv[h][j] += gt1 * e;
+            }
+        }
+        fr.load(img, nx, lane, 15, RF);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            sxa[h] = sv4(nx, vv[h] * MC + 4 * kb);
+            sxb[h] = sv4(nx, vv[h] * MC + 16 + 4 * kb);
+        }
+        // this lane's scalar partials of the block: the store waves reduce them (fixed order)
+        *reinterpret_cast<float4 *>(l.ps + (wave * 64 + lane) * RPS) = float4{ps[0], ps[1], ps[2], ps[3]};
+        *reinterpret_cast<float4 *>(l.ps + (wave * 64 + lane) * RPS + 4) = float4{ps[4], ps[5], ps[6], ps[7]};
+        RPROBE(blk, 4)
+    }
+    __syncthreads();  // the store waves' last block
+    RPROBE_DUMP(1)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        if (!act[h]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gx[size_t(vv[h]) * MC + rch(kb, j)] = f2h(gv[h][j]);
+    }
+}
+
 size_t lds_wgrad(int nv) { return size_t(nv) * (4 * PT + PU + PG) * 2 + size_t((nv * 27 + 7) & ~7) * 2 + 64; }
 
 bool mfma_ok(const SkArgs &a) { return a.C == MC && a.B == MB && a.nv % 32 == 0 && a.nv <= MAXVM; }
+
+bool lds_opt_in(const void *k) {
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+    (void)hipGetLastError();
+    return true;
+}
+
+// which matrix-core chain runs: 'r' the register chain (default), 'm' the LDS-phase k_stackm_*
+// (VQ3D_STACK_CHAIN=m, kept for A/B measurements)
+char stack_chain() {
+    static const char c = [] {
+        const char *e = getenv("VQ3D_STACK_CHAIN");
+        return e && e[0] == 'm' ? 'm' : 'r';
+    }();
+    return c;
+}
 
 int check(int32_t nblk, int32_t batch, int32_t channels, int32_t branch, int32_t h, int32_t w, int32_t dd,
           SkArgs &a) {
@@ -1082,8 +1628,19 @@ int vq3d_preact_stack_fwd(int32_t dtype, int32_t nblocks, int32_t batch, int32_t
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   int(160 * 1024));
         h16_t *img = reinterpret_cast<h16_t *>(saved + size_t(nblocks) * a.nv * (a.C + 2 * a.B));
-        k_stackm_pack<false><<<nblocks, NT, 0, s>>>(params, img);
-        k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved, img);
+        if (stack_chain() == 'r') {
+            k_stackr_pack<false><<<nblocks, 256, 0, s>>>(params, img);
+            static const bool opt = lds_opt_in(reinterpret_cast<const void *>(k_stackr_fwd<true>)) &&
+                                    lds_opt_in(reinterpret_cast<const void *>(k_stackr_fwd<false>));
+            (void)opt;
+            if (a.nv == MAXVM)
+                k_stackr_fwd<true><<<1, RNT, lds_rf(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved, img);
+            else
+                k_stackr_fwd<false><<<1, RNT, lds_rf(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved, img);
+        } else {
+            k_stackm_pack<false><<<nblocks, NT, 0, s>>>(params, img);
+            k_stackm_fwd<<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)x, params, (h16_t *)out, saved, img);
+        }
     } else if (dtype == VQ3D_HALF) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stack_fwd<h16_t>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
@@ -1129,7 +1686,8 @@ size_t vq3d_preact_stack_bwd_workspace_bytes(int32_t nblocks, int32_t batch, int
                                              int32_t h, int32_t w, int32_t dd) {
     SkArgs a;
     if (check(nblocks, batch, channels, branch, h, w, dd, a) || !mfma_ok(a)) return 0;
-    return size_t(nblocks) * a.nv * (MC + 2 * MB) * 2 + size_t(nblocks) * FR_N * 2;  // + the packed images
+    // the record, the packed images, k_stackr_bwd's scalar partials (8 waves x 8 per block)
+    return size_t(nblocks) * a.nv * (MC + 2 * MB) * 2 + size_t(nblocks) * FR_N * 2 + size_t(nblocks) * RCW * RPS * 4;
 }
 
 int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int32_t channels, int32_t branch,
@@ -1145,13 +1703,29 @@ int vq3d_preact_stack_bwd_ws(int32_t dtype, int32_t nblocks, int32_t batch, int3
     if (!g || !params || !grads || !saved || !gx || !workspace) return fail("preact_stack_bwd_ws: null pointer");
     if (ws_bytes < need) return fail("preact_stack_bwd_ws: workspace too small");
     hipStream_t s = as_stream(stream);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
     h16_t *img = static_cast<h16_t *>(workspace) + size_t(nblocks) * a.nv * (MC + 2 * MB);
-    k_stackm_pack<true><<<nblocks, NT, 0, s>>>(params, img);
-    k_stackm_bwd<true><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx,
-                                                  (h16_t *)workspace, img);
-    k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const h16_t *)workspace);
+    float *part = reinterpret_cast<float *>(img + size_t(nblocks) * FR_N);
+    if (stack_chain() == 'r') {
+        k_stackr_pack<true><<<nblocks, 256, 0, s>>>(params, img);
+        static const bool opt = lds_opt_in(reinterpret_cast<const void *>(k_stackr_bwd<true>)) &&
+                                lds_opt_in(reinterpret_cast<const void *>(k_stackr_bwd<false>));
+        (void)opt;
+        if (a.nv == MAXVM)
+            k_stackr_bwd<true><<<1, RNT, lds_rb(a.nv), s>>>(a, (const h16_t *)g, params, saved, (h16_t *)gx,
+                                                            (h16_t *)workspace, part, img);
+        else
+            k_stackr_bwd<false><<<1, RNT, lds_rb(a.nv), s>>>(a, (const h16_t *)g, params, saved, (h16_t *)gx,
+                                                             (h16_t *)workspace, part, img);
+        k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const h16_t *)workspace, part);
+    } else {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_stackm_bwd<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(160 * 1024));
+        k_stackm_pack<true><<<nblocks, NT, 0, s>>>(params, img);
+        k_stackm_bwd<true><<<1, NT, lds_m(a.nv), s>>>(a, (const h16_t *)g, params, grads, saved, (h16_t *)gx,
+                                                      (h16_t *)workspace, img);
+        k_stackm_wgrad<<<nblocks, NT, lds_wgrad(a.nv), s>>>(a, params, grads, saved, (const h16_t *)workspace,
+                                                            nullptr);
+    }
     return check_launch("preact_stack_bwd_ws");
 }
 

@@ -185,10 +185,11 @@ def test_stack_deterministic(gpu):
         assert torch.equal(a, b)
 
 
-def test_stack_split_backward_equals_fused(gpu):
-    """vq3d_preact_stack_bwd_ws (gradient-stream chain + per-block weight-gradient workgroups) gives
-    the fused one-workgroup kernel's gx and parameter gradients bit for bit (same operands, same
-    fragment and summation order)."""
+def test_stack_split_backward_matches_fused(gpu):
+    """vq3d_preact_stack_bwd_ws (the register-resident gradient-stream chain k_stackr_bwd + per-block
+    weight-gradient workgroups) against the fused one-workgroup kernel: same rounding points, but the
+    chain's 1x1 contractions run with a permuted K order and its scalar sums per wave, so the two
+    agree to accumulation-order noise (a gz3 / gz1 bf16 rounding may flip), not bit for bit."""
     from vq3d import _lib as L
     from vq3d.flat import FlatParams
     from vq3d.functional import StackPlan
@@ -220,5 +221,18 @@ def test_stack_split_backward_equals_fused(gpu):
                    L.stream())
         torch.cuda.synchronize()
         res.append((gx.clone(), fp.grad.clone()))
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1]), float((res[0][1] - res[1][1]).abs().max())
+    assert rel(res[1][0].float(), res[0][0].float()) <= 2e-2
+    d = (res[1][1] - start).double()
+    r = (res[0][1] - start).double()
+    assert float((d - r).norm() / r.norm()) <= 5e-3, float((d - r).norm() / r.norm())
+    sd, sr = [], []
+    for name, p in stack.named_parameters():  # every weight tensor; the scalars as one vector
+        off = (p.grad.data_ptr() - fp.grad.data_ptr()) // 4
+        dp, rp = d[off:off + p.numel()], r[off:off + p.numel()]
+        if p.numel() > 1:
+            assert rel(dp, rp) <= 2e-2, (name, rel(dp, rp))
+        else:
+            sd.append(dp)
+            sr.append(rp)
+    sd, sr = torch.cat(sd), torch.cat(sr)
+    assert float((sd - sr).norm() / sr.norm()) <= 1e-2, float((sd - sr).norm() / sr.norm())
