@@ -1109,6 +1109,11 @@ __device__ __forceinline__ float ldg(const float *p) {
     return *(gfloat *)(p);
 }
 
+// vmcnt(0) once, after the prologue's loads: the compiler's wait counts at the loop top merge the
+// prologue's issue order with the loop's, and a prologue load still pending there made every
+// block's first wait vmcnt(2) (all of the previous block's refills, issued moments earlier)
+__device__ __forceinline__ void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ int rch(int kb, int j) { return j < 4 ? 4 * kb + j : 16 + 4 * kb + (j - 4); }
 
 // Fragment f of a block, lane l = kb * 16 + m, element j (k = 8 kb + j).  Forward: f 0 W1 (A[o][k] =
@@ -1153,7 +1158,15 @@ struct RFrag {  // one block's 17 A fragments of this lane
     __device__ __forceinline__ hx8 operator[](int k) const { return __builtin_bit_cast(hx8, f[k]); }
 };
 
-// the 14 neighbour rows lane (voxel v, kb) gathers, as element offsets into a [nv][PT] branch image
+// Branch images (t2 / t3 forward, gz3 / gz1 backward) are PLANAR in the ring: channels 0..7 of every
+// voxel (16 B rows) in plane 0, channels 8..15 in plane 1, PLN halves apart (a multiple of 256 B).  A
+// gather's 16-lane LDS group then reads 16 distinct voxels' rows whose 16-B chunks are distinct mod
+// 256 B (the 16 voxels of a column block are one (h) row, and a tap maps it onto another row):
+// conflict-free.  The [voxel][PT] rows had 44 % of the chains' LDS cycles in bank conflicts.
+constexpr int PLN = MAXVM * 8;
+__device__ __forceinline__ int pl_off(int v, int c) { return (c >> 3) * PLN + v * 8 + (c & 7); }
+
+// the 14 neighbour rows lane (voxel v, kb) gathers, as element offsets into a planar branch image
 // packed two per dword: tap 2 s + (kb >> 1) (backward: its flip), channels 8 (kb & 1) .. + 7.  Tap
 // 27 (s = 13, kb >= 2) has no row: those lanes read zeros.
 template <bool BWD>
@@ -1162,8 +1175,8 @@ __device__ __forceinline__ void nbr_rows(const SkArgs &a, int v, int kb, uint32_
     for (int s = 0; s < 7; ++s) {
         uint32_t lo = 0, hi = 0;
         const int t0 = 4 * s + (kb >> 1), t1 = t0 + 2;
-        lo = uint32_t(nbr(a, v, BWD ? 26 - t0 : t0, 1) * PT + 8 * (kb & 1));
-        if (t1 < 27) hi = uint32_t(nbr(a, v, BWD ? 26 - t1 : t1, 1) * PT + 8 * (kb & 1));
+        lo = uint32_t(pl_off(nbr(a, v, BWD ? 26 - t0 : t0, 1), 8 * (kb & 1)));
+        if (t1 < 27) hi = uint32_t(pl_off(nbr(a, v, BWD ? 26 - t1 : t1, 1), 8 * (kb & 1)));
         o[s] = lo | (hi << 16);
     }
 }
@@ -1189,24 +1202,34 @@ __device__ __forceinline__ f32x4 conv14(const RFrag &fr, const hx8 (&nb)[14]) {
 // the forward loop; the results are rounded to 16 bits (t2, t3) or feed fp32 gradients
 __device__ __forceinline__ float exp_f(float z) { return __builtin_amdgcn_exp2f(z * 1.44269504088896341f); }
 __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : exp_f(z) - 1.f; }
+// elu(z + a) + b with the bias folds precomputed per block (EluB): one compare, one add, one fma,
+// the exp and one add per element instead of two adds, a multiply, the exp, an add and the compare
+struct EluB {
+    float na, ab, al, bm;  // -a, a + b, a log2(e), b - 1
+    __device__ __forceinline__ EluB(float a, float b) : na(-a), ab(a + b), al(a * 1.44269504088896341f), bm(b - 1.f) {}
+    __device__ __forceinline__ float operator()(float z) const {
+        const float e = __builtin_amdgcn_exp2f(fmaf(z, 1.44269504088896341f, al)) + bm;
+        return z > na ? z + ab : e;
+    }
+};
 __device__ __forceinline__ uint32_t pk2h(float a, float b) { return uint32_t(f2h(a)) | (uint32_t(f2h(b)) << 16); }
 __device__ __forceinline__ float lo_h(uint32_t u) { return h2f_lo(u & 0xffffu); }
 __device__ __forceinline__ float hi_h(uint32_t u) { return h2f_lo(u >> 16); }
 
 struct RfLds {  // the forward's LDS ring (RRING slots)
     float *xs;    // [nv][PF] the block's input x (fp32)
-    h16_t *t2s;   // [nv][PT] t2 (16-bit): the conv's gather source
-    h16_t *t3s;   // [nv][PT] t3 (16-bit)
+    h16_t *t2s;   // planar t2 (16-bit): the conv's gather source
+    h16_t *t3s;   // planar t3 (16-bit)
 };
 __device__ __forceinline__ RfLds rf_slot(char *smem, int nv, int slot) {
     RfLds l;
-    char *p = smem + size_t(slot) * (size_t(nv) * PF * 4 + size_t(nv) * PT * 4);
+    char *p = smem + size_t(slot) * (size_t(nv) * PF * 4 + size_t(PLN) * 8);
     l.xs = reinterpret_cast<float *>(p);
     l.t2s = reinterpret_cast<h16_t *>(p + size_t(nv) * PF * 4);
-    l.t3s = l.t2s + nv * PT;
+    l.t3s = l.t2s + 2 * PLN;
     return l;
 }
-size_t lds_rf(int nv) { return RRING * (size_t(nv) * PF * 4 + size_t(nv) * PT * 4); }
+size_t lds_rf(int nv) { return RRING * (size_t(nv) * PF * 4 + size_t(PLN) * 8); }
 
 // store waves: block b's x / t2 / t3 from ring slot b % 3 to `saved` (fp32, k_stackm_fwd's layout)
 __device__ __forceinline__ void rf_store(const RfLds &l, int nv, float *sx, int t) {
@@ -1217,8 +1240,8 @@ __device__ __forceinline__ void rf_store(const RfLds &l, int nv, float *sx, int 
     }
     for (int i = t; i < nv * (MB / 4); i += 256) {
         const int v = i >> 2, o = 4 * (i & 3);
-        const u32x2 a = *reinterpret_cast<const u32x2 *>(l.t2s + v * PT + o);
-        const u32x2 b = *reinterpret_cast<const u32x2 *>(l.t3s + v * PT + o);
+        const u32x2 a = *reinterpret_cast<const u32x2 *>(l.t2s + pl_off(v, o));
+        const u32x2 b = *reinterpret_cast<const u32x2 *>(l.t3s + pl_off(v, o));
         *reinterpret_cast<float4 *>(st2 + v * MB + o) = float4{lo_h(a[0]), hi_h(a[0]), lo_h(a[1]), hi_h(a[1])};
         *reinterpret_cast<float4 *>(st3 + v * MB + o) = float4{lo_h(b[0]), hi_h(b[0]), lo_h(b[1]), hi_h(b[1])};
     }
@@ -1273,6 +1296,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
     fr.load(img, 0, lane);
     float vc = ldg(row_ptr(tab, 0, lane));
     const float *pn = row_ptr(tab, min(1, a.nblk - 1), lane);
+    drain_vmem();
     for (int blk = 0; blk < a.nblk; ++blk) {
         const Scal s = scal_lanes(vc);
         RPROBE(blk, 0)
@@ -1286,6 +1310,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
         vc = ldg(pn);
         pn = row_ptr(tab, min(blk + 2, a.nblk - 1), lane);
         const RfLds l = rf_slot(smem, nv, blk % RRING);
+        const EluB e1(s.b1a, s.b1b), e2(s.b2a, s.b2b), e3(s.b3a, s.b3b);
         // t2 = elu_f(W1 u1 + b2a) + b2b, u1 = elu_f(x + b1a) + b1b (K in the rch order)
         f32x4 a2[NH];
 #pragma unroll
@@ -1296,7 +1321,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
             *reinterpret_cast<float4 *>(l.xs + v * PF + 16 + 4 * kb) = float4{xv[h][4], xv[h][5], xv[h][6], xv[h][7]};
             float u[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) u[j] = elu_f(xv[h][j] + s.b1a) + s.b1b;
+            for (int j = 0; j < 8; ++j) u[j] = e1(xv[h][j]);
             a2[h] = mfma(fr[0], pack8(u), f32x4{0.f, 0.f, 0.f, 0.f});
         }
         FR_REFILL(0, 1);
@@ -1304,9 +1329,8 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
         for (int h = 0; h < NH; ++h) {
             if (!act[h]) continue;
             const f32x4 c = a2[h];
-            *reinterpret_cast<u32x2 *>(l.t2s + vv[h] * PT + 4 * kb) =
-                u32x2{pk2h(elu_f(c[0] + s.b2a) + s.b2b, elu_f(c[1] + s.b2a) + s.b2b),
-                      pk2h(elu_f(c[2] + s.b2a) + s.b2b, elu_f(c[3] + s.b2a) + s.b2b)};
+            *reinterpret_cast<u32x2 *>(l.t2s + pl_off(vv[h], 4 * kb)) =
+                u32x2{pk2h(e2(c[0]), e2(c[1])), pk2h(e2(c[2]), e2(c[3]))};
         }
         RPROBE(blk, 1)
         __syncthreads();
@@ -1319,9 +1343,8 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
             hx8 nb[14];
             gather14(l.t2s, nbo[h], kb, nb);
             const f32x4 c = conv14(fr, nb);
-            t3p[h] = u32x2{pk2h(elu_f(c[0] + s.b3a) + s.b3b, elu_f(c[1] + s.b3a) + s.b3b),
-                           pk2h(elu_f(c[2] + s.b3a) + s.b3b, elu_f(c[3] + s.b3a) + s.b3b)};
-            *reinterpret_cast<u32x2 *>(l.t3s + vv[h] * PT + 4 * kb) = t3p[h];
+            t3p[h] = u32x2{pk2h(e3(c[0]), e3(c[1])), pk2h(e3(c[2]), e3(c[3]))};
+            *reinterpret_cast<u32x2 *>(l.t3s + pl_off(vv[h], 4 * kb)) = t3p[h];
         }
         RPROBE(blk, 3)
         FR_REFILL(1, 15);
@@ -1353,20 +1376,20 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
 
 struct RbLds {  // the backward's LDS ring
     h16_t *gs;    // [nv][PG] the block's incoming gradient g (16-bit, the record)
-    h16_t *z3s;   // [nv][PT] gz3: the transposed conv's gather source
-    h16_t *z1s;   // [nv][PT] gz1
+    h16_t *z3s;   // planar gz3: the transposed conv's gather source
+    h16_t *z1s;   // planar gz1
     float *ps;    // [RCW][64][RPS] the compute lanes' scalar partials
 };
 __device__ __forceinline__ RbLds rb_slot(char *smem, int nv, int slot) {
     RbLds l;
-    char *p = smem + size_t(slot) * (size_t(nv) * (PG + 2 * PT) * 2 + RCW * 64 * RPS * 4);
+    char *p = smem + size_t(slot) * (size_t(nv) * PG * 2 + size_t(PLN) * 8 + RCW * 64 * RPS * 4);
     l.gs = reinterpret_cast<h16_t *>(p);
     l.z3s = l.gs + nv * PG;
-    l.z1s = l.z3s + nv * PT;
-    l.ps = reinterpret_cast<float *>(l.z1s + nv * PT);
+    l.z1s = l.z3s + 2 * PLN;
+    l.ps = reinterpret_cast<float *>(l.z1s + 2 * PLN);
     return l;
 }
-size_t lds_rb(int nv) { return RRING * (size_t(nv) * (PG + 2 * PT) * 2 + RCW * 64 * RPS * 4); }
+size_t lds_rb(int nv) { return RRING * (size_t(nv) * PG * 2 + size_t(PLN) * 8 + RCW * 64 * RPS * 4); }
 
 // store waves: block b's record (g, gz3, gz1: k_stackm_bwd's layout) and scalar partials
 __device__ __forceinline__ void rb_store(const RbLds &l, int nv, h16_t *rg, float *part, int t) {
@@ -1377,8 +1400,8 @@ __device__ __forceinline__ void rb_store(const RbLds &l, int nv, h16_t *rg, floa
     }
     for (int i = t; i < nv * (MB / 4); i += 256) {
         const int v = i >> 2, o = 4 * (i & 3);
-        *reinterpret_cast<u32x2 *>(rz3 + v * MB + o) = *reinterpret_cast<const u32x2 *>(l.z3s + v * PT + o);
-        *reinterpret_cast<u32x2 *>(rz1 + v * MB + o) = *reinterpret_cast<const u32x2 *>(l.z1s + v * PT + o);
+        *reinterpret_cast<u32x2 *>(rz3 + v * MB + o) = *reinterpret_cast<const u32x2 *>(l.z3s + pl_off(v, o));
+        *reinterpret_cast<u32x2 *>(rz1 + v * MB + o) = *reinterpret_cast<const u32x2 *>(l.z1s + pl_off(v, o));
     }
     // store wave q sums compute waves q, q + RSW, ... (DPP, fixed order); part [block][wave][RPS]
     const int lane = t & 63;
@@ -1462,6 +1485,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
     fr.load(img, last, lane);
     float vc = ldg(row_ptr(tab, last, lane));
     const float *pn = row_ptr(tab, max(last - 1, 0), lane);
+    drain_vmem();
     for (int blk = last; blk >= 0; --blk) {
         const Scal s = scal_lanes(vc);
         RPROBE(blk, 0)
@@ -1469,6 +1493,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
         vc = ldg(pn);
         pn = row_ptr(tab, max(blk - 2, 0), lane);
         const RbLds l = rb_slot(smem, nv, blk % RRING);
+        const float nb1a = -s.b1a, b1al = s.b1a * 1.44269504088896341f;  // elu'(x + b1a) folds
         float ps[RPS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // b4, (scale), b3b, b3a, b2b, b2a, b1b, b1a
         // gz3 = scale W3^T g * elu'(t3 - b3b)
 #pragma unroll
@@ -1490,7 +1515,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
                 ps[2] += g3;
                 ps[3] += zq[i];
             }
-            *reinterpret_cast<u32x2 *>(l.z3s + v * PT + 4 * kb) = u32x2{pk2h(zq[0], zq[1]), pk2h(zq[2], zq[3])};
+            *reinterpret_cast<u32x2 *>(l.z3s + pl_off(v, 4 * kb)) = u32x2{pk2h(zq[0], zq[1]), pk2h(zq[2], zq[3])};
         }
         fr.load(img, nx, lane, 0, 1);
 #pragma unroll
@@ -1515,7 +1540,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
                 ps[5] += z[i];
             }
             z1p[h] = u32x2{pk2h(z[0], z[1]), pk2h(z[2], z[3])};
-            *reinterpret_cast<u32x2 *>(l.z1s + vv[h] * PT + 4 * kb) = z1p[h];
+            *reinterpret_cast<u32x2 *>(l.z1s + pl_off(vv[h], 4 * kb)) = z1p[h];
         }
         RPROBE(blk, 3)
         fr.load(img, nx, lane, 1, 15);
@@ -1532,8 +1557,7 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float gt1 = j < 4 ? o0[j] : o1[j - 4];
-                const float zx = xs[j] + s.b1a;
-                const float e = zx > 0.f ? 1.f : exp_f(zx);
+                const float e = xs[j] > nb1a ? 1.f : __builtin_amdgcn_exp2f(fmaf(xs[j], 1.44269504088896341f, b1al));
                 ps[6] += gt1;
                 ps[7] += gt1 * e;
                 gv[h][j] += gt1 * e;
