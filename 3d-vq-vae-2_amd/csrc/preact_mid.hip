@@ -836,11 +836,13 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             ex9(et2[r], v, kl, t2v);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const bool ok = 4 * kl + j < BR;
+                // channels past 8 (4 kb + j >= BR) need no masks here or below: their A rows are
+                // zero, so acc, z, gt1 and the previous block's a3 are exactly 0 there (operands
+                // finite), adding nothing to the sums and meeting zero weights as K entries
                 const float z = acc[r][j] * elu_d_act(t2v[j], s.b2b);
-                z1[j] = ok ? bf(f2h(z)) : 0.f;
-                s2b += ok ? acc[r][j] : 0.f;
-                s2a += ok ? z : 0.f;
+                z1[j] = bf(f2h(z));
+                s2b += acc[r][j];
+                s2a += z;
             }
             // gt1 = W1^T gz1 (two channel tiles), gx = g + gt1 * elu'(x + b1a)
             float gxv[6];
@@ -859,8 +861,8 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                     const bool ok = j < 4 || kl == 3;  // channels 4kb + j, then (kb 3) 16 / 17
                     const float zx = xv[j] + s.b1a;
                     const float ez = zx > 0.f ? 1.f : __expf(zx);
-                    s1b += ok ? gt1[j] : 0.f;
-                    s1a += ok ? gt1[j] * ez : 0.f;
+                    s1b += gt1[j];
+                    s1a += gt1[j] * ez;
                     gxv[j] = ok ? bf(f2h(gv[j] + gt1[j] * ez)) : 0.f;
                     if constexpr (CHAIN) q4 += gxv[j];  // the previous block's g = this gx
                 }
@@ -879,12 +881,11 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                     ex9(et3[r], v, kl, t3v);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const bool ok = 4 * kl + j < BR;
                         const float gt3 = a3[j] * sp.sc;
                         const float z = gt3 * elu_d_act(t3v[j], sp.b3b);
-                        q3b += ok ? gt3 : 0.f;
-                        q3a += ok ? z : 0.f;
-                        qsc += ok ? a3[j] * t3v[j] : 0.f;
+                        q3b += gt3;
+                        q3a += z;
+                        qsc += a3[j] * t3v[j];
                         zq[j] = z;
                     }
                     put9(st + QO9B, nl, kl, zq);
@@ -1049,8 +1050,8 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
             h16_t *st = stg + wave * QSTG;
             float t3v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                t3v[j] = 4 * kl + j < BR ? bf(f2h(elu_fast(acc[r][j] + s.b3a) + s.b3b)) : 0.f;
+            for (int j = 0; j < 4; ++j)  // channels past 8 meet zero weights (finite: no masks)
+                t3v[j] = bf(f2h(elu_fast(acc[r][j] + s.b3a) + s.b3b));
             float ov[6];
             {
                 const hx8 bt = pack8({t3v[0], t3v[1], t3v[2], t3v[3], 0.f, 0.f, 0.f, 0.f});
@@ -1061,10 +1062,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                                      bf(xr.z & 0xffffu), bf(xr.z >> 16)};
                 const float o3[6] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1]};
 #pragma unroll
-                for (int j = 0; j < 6; ++j) {
-                    const bool ok = j < 4 || kl == 3;  // channels 4kb + j, then (kb 3) 16 / 17
-                    ov[j] = ok ? bf(f2h(o3[j] * s.sc + s.b4 + xv[j])) : 0.f;
-                }
+                for (int j = 0; j < 6; ++j) ov[j] = bf(f2h(o3[j] * s.sc + s.b4 + xv[j]));  // j >= 4 used by kb 3 only
             }
             {
                 put18(st, nl, kl, ov);
@@ -1074,10 +1072,7 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
                 // the next block's u1 (k_pm_t2's rounding points) and t2
                 float u1[6];
 #pragma unroll
-                for (int j = 0; j < 6; ++j) {
-                    const bool ok = j < 4 || kl == 3;
-                    u1[j] = ok ? bf(f2h(elu_fast(ov[j] + sn.b1a) + sn.b1b)) : 0.f;
-                }
+                for (int j = 0; j < 6; ++j) u1[j] = bf(f2h(elu_fast(ov[j] + sn.b1a) + sn.b1b));  // zero-weight K past 17
                 const hx8 bu = pack8({u1[0], u1[1], u1[2], u1[3], u1[4], u1[5], 0.f, 0.f});
                 const f32x4 a2 = mfma(wf(11, ln), bu, f32x4{0.f, 0.f, 0.f, 0.f});
                 float tn[4];

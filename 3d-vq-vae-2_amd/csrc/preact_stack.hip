@@ -1200,7 +1200,13 @@ __device__ __forceinline__ f32x4 conv14(const RFrag &fr, const hx8 (&nb)[14]) {
 // exp through v_exp_f32 (2^x) directly: the chain is VALU-issue bound (one compute wave per SIMD,
 // 4 cycles per instruction), and expf's range reduction was ~11 instructions per call, a third of
 // the forward loop; the results are rounded to 16 bits (t2, t3) or feed fp32 gradients
-__device__ __forceinline__ float exp_f(float z) { return __builtin_amdgcn_exp2f(z * 1.44269504088896341f); }
+#ifndef VQ3D_STACK_FAST_EXP
+#define VQ3D_STACK_FAST_EXP 1
+#endif
+__device__ __forceinline__ float exp_f(float z) {
+    if constexpr (VQ3D_STACK_FAST_EXP) return __builtin_amdgcn_exp2f(z * 1.44269504088896341f);
+    else return expf(z);
+}
 __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : exp_f(z) - 1.f; }
 // elu(z + a) + b with the bias folds precomputed per block (EluB): one compare, one add, one fma,
 // the exp and one add per element instead of two adds, a multiply, the exp, an add and the compare
@@ -1208,7 +1214,9 @@ struct EluB {
     float na, ab, al, bm;  // -a, a + b, a log2(e), b - 1
     __device__ __forceinline__ EluB(float a, float b) : na(-a), ab(a + b), al(a * 1.44269504088896341f), bm(b - 1.f) {}
     __device__ __forceinline__ float operator()(float z) const {
-        const float e = __builtin_amdgcn_exp2f(fmaf(z, 1.44269504088896341f, al)) + bm;
+        float e;
+        if constexpr (VQ3D_STACK_FAST_EXP) e = __builtin_amdgcn_exp2f(fmaf(z, 1.44269504088896341f, al)) + bm;
+        else e = expf(z - na) + bm;
         return z > na ? z + ab : e;
     }
 };
@@ -1557,7 +1565,9 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float gt1 = j < 4 ? o0[j] : o1[j - 4];
-                const float e = xs[j] > nb1a ? 1.f : __builtin_amdgcn_exp2f(fmaf(xs[j], 1.44269504088896341f, b1al));
+                const float e = xs[j] > nb1a ? 1.f
+                                : (VQ3D_STACK_FAST_EXP ? __builtin_amdgcn_exp2f(fmaf(xs[j], 1.44269504088896341f, b1al))
+                                                       : expf(xs[j] - nb1a));
                 ps[6] += gt1;
                 ps[7] += gt1 * e;
                 gv[h][j] += gt1 * e;

@@ -17,7 +17,7 @@ body = lines[start:end + 1]
 blocks, cur = [], None
 for k, l in enumerate(body):
     if re.match(r'^(\.LBB\d+_\d+|; %bb\.\d+):', l.strip()) or (l.startswith('.LBB') and ':' in l):
-        m = re.search(r'Header=(BB\d+_\d+)', l)
+        m = re.search(r'Header=(BB\d+_\d+)', l) or re.search(r'Parent Loop (BB\d+_\d+)', l)
         own = re.match(r'^\.L(BB\d+_\d+):', l.strip())
         depth1 = 'Loop Header: Depth=1' in l
         cur = {'hdr': m.group(1) if m else None, 'own': own.group(1) if own else None, 'd1': depth1, 'ins': []}
