@@ -621,17 +621,19 @@ __device__ __forceinline__ Raw9 ld9(const h16_t *__restrict__ base, uint32_t v, 
     __builtin_memcpy(&r, reinterpret_cast<const char *>(base) + a, 12);
     return r;
 }
-// the 4 values of lane-group kb (kb 2: one value; kb 3: none) as floats, 0 where invalid
+// the 4 values of lane-group kb (kb 2: one value; kb 3: none) as floats.  The entries past channel 8
+// are other finite elements of the tensor, not zeros: every use multiplies them by an accumulator
+// row whose weights are zero (k_pm_bwd2), so they need no masks
 __device__ __forceinline__ void ex9(const Raw9 &r, uint32_t v, int kb, float (&o)[4]) {
     const int k = q9_kb(kb);
     const uint32_t sub = uint32_t(v & 1) * 2u;  // 18 v mod 4
     const bool hi = k == 2;
     const uint32_t lo = hi ? r.z : r.x, mid = hi ? 0u : r.y, top = hi ? 0u : r.z;
     const uint32_t p0 = __builtin_amdgcn_alignbyte(mid, lo, sub), p1 = __builtin_amdgcn_alignbyte(top, mid, sub);
-    o[0] = kb == 3 ? 0.f : bf(p0 & 0xffffu);
-    o[1] = kb >= 2 ? 0.f : bf(p0 >> 16);
-    o[2] = kb >= 2 ? 0.f : bf(p1 & 0xffffu);
-    o[3] = kb >= 2 ? 0.f : bf(p1 >> 16);
+    o[0] = bf(p0 & 0xffffu);
+    o[1] = bf(p0 >> 16);
+    o[2] = bf(p1 & 0xffffu);
+    o[3] = bf(p1 >> 16);
 }
 // 18-channel rows (36 bytes, dword aligned): channels 4kb .. 4kb + 5 (one dwordx3; lane-group 3
 // uses all six: 12 .. 15 and 16, 17)
