@@ -221,12 +221,12 @@ def probe_stack(dev, kind):
     # weights, the saved-tensor round trip (fp32) and the bf16 input / output
     sv = saved.numel() * 4
     flops = nblk * 2.0 * nv * (c * nb * 2 + nb * nb * 27)
-    if kind == "k_stackm_fwd":
+    if kind == "k_stackr_fwd":
         return fwd, wbytes + sv + 2 * nv * c * 2, flops, \
-            "k_stackm_fwd: 50 fused top-level blocks (8x8x2, 32 ch) forward, one launch"
-    if kind == "k_stackm_bwd":
+            "k_stackr_fwd: 50 fused top-level blocks (8x8x2, 32 ch) forward, one launch"
+    if kind == "k_stackr_bwd":
         return bwd, 2 * wbytes + sv + 2 * nv * c * 2, 2 * flops, \
-            "k_stackm_bwd: 50 fused top-level blocks (8x8x2, 32 ch) backward: the gradient-stream chain (one " \
+            "k_stackr_bwd: 50 fused top-level blocks (8x8x2, 32 ch) backward: the gradient-stream chain (one " \
             "workgroup) + the weight gradients (one workgroup per block)"
     raise KeyError(kind)
 
@@ -355,14 +355,20 @@ PROBES = {
     "k_col_bwd<4_2": probe_col, "k_col_fwd<4_2": probe_col, "k_col_bwd<8_4": probe_col, "k_col_fwd<8_4": probe_col,
     "k_col_bwd<2_1": probe_col, "k_col_fwd<2_1": probe_col,
     "k_pm_bwd2": probe_mid, "k_pm_w2grad": probe_mid, "k_pm_w13grad": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
-    "k_stackm_bwd": probe_stack, "k_stackm_fwd": probe_stack,
+    "k_stackr_bwd": probe_stack, "k_stackr_fwd": probe_stack,
 }
 
 
 # probes whose kernels are bounded by a chain of dependent phases on one workgroup, not by HBM
-LATENCY_BOUND = {k: "one workgroup walks the 50-block top-level run (8x8x2 voxels, 32 channels): each block's "
-                    "dependent phases (1x1, 3x3x3, 1x1 and their syncs) set the time; PMC 3.5 MB per backward launch"
-                 for k in ("k_stackm_bwd", "k_stackm_fwd")}
+# (no HBM roofline applies: a few MB per launch).  Their bound is the compute waves' instruction
+# issue: 4 compute waves, one per SIMD, each issuing ~490 (forward) / ~550 (backward) instructions
+# per block (tools/probes/loop_mix.py), a VALU instruction per 4 cycles -> a floor of ~0.9 us per
+# block; measured ~1.7 / 2.3 us per block (profiles/r06_stack_phase_probe.txt, PMC in
+# profiles/r06_stack_pmc.txt: VALU busy ~45 % of the chain, the rest dependent MFMA / LDS latency)
+LATENCY_BOUND = {k: "one workgroup walks the 50-block top-level run (8x8x2 voxels, 32 channels) with one barrier per "
+                    "block: bounded by its compute waves' instruction issue (~0.9 us per block floor at one VALU "
+                    "instruction per 4 cycles per SIMD), not by HBM"
+                 for k in ("k_stackr_bwd", "k_stackr_fwd")}
 
 
 def probe_for(name):
@@ -404,7 +410,7 @@ def timed_launch(dev, launch, iters=20):
 def roofline_of(dev, kind, step_entry=None, live_us=None):
     """Roofline of one engine kernel.  Its launch time is taken, in order of preference, from
     (1) the committed rocprofv3 kernel trace of the bench step (profiles/rNN_step_top.json, the
-        same tree: tools/gpu_round.sh writes it from this command's step) average,
+        same tree: `tools/gpu_steps.sh TAG prof` writes it from this command's step) average,
     (2) `live_us`: HIP events around each of its launches inside one more (eager) training step of
         this run (vq3d.ops.KernelTimer, on the stream the kernel is launched on; the events keep
         neighbouring launches from overlapping, so it reads a few % above the trace),

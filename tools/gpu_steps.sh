@@ -9,6 +9,7 @@
 #   smoke               __graft_entry__.smoke()
 #   race                tools/dbg/lanes_race.py (PixelSNAIL lanes replays at the published size)
 #   bench               bench.py (the headline line) -> gpurun_out/TAG_bench.json
+#   eager               bench.py --eager (no HIP graph) -> gpurun_out/TAG_eager.json
 #   prior|cfg2|cfg4|cfg4b8   bench.py --prior / --config 2l_pub / --encode-only [--encode-batch 8]
 #   prof                rocprofv3 kernel trace + stats of the bench step -> gpurun_out/TAG_prof/, the
 #                       step ranking gpurun_out/TAG_step.txt / TAG_step_top.json (tools/step_profile.py)
@@ -39,6 +40,8 @@ for s in "$@"; do
         race) run race 600 python -u tools/dbg/lanes_race.py 3 4 || exit $? ;;
         bench) run bench 600 python -u bench.py || exit $?
                tail -1 "gpurun_out/${TAG}_bench.log" > "gpurun_out/${TAG}_bench.json" ;;
+        eager) run eager 600 python -u bench.py --eager --no-cpu-baseline || exit $?
+               tail -1 "gpurun_out/${TAG}_eager.log" > "gpurun_out/${TAG}_eager.json" ;;
         prior) run prior 600 python -u bench.py --prior || exit $?
                tail -1 "gpurun_out/${TAG}_prior.log" > "gpurun_out/${TAG}_prior.json" ;;
         cfg2) run cfg2 600 python -u bench.py --config 2l_pub || exit $?
