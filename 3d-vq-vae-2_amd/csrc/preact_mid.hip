@@ -1158,8 +1158,8 @@ __device__ __forceinline__ u32x4 item_row(const uint32_t (&w)[36], int c) {
 }
 
 template <int D>
-__global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const h16_t *__restrict__ gz3,
-                                                   const h16_t *__restrict__ t2, float *__restrict__ p2a) {
+__device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, const h16_t *__restrict__ gz3,
+                                          const h16_t *__restrict__ t2, float *__restrict__ p2a) {
     using K = W2c<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     h16_t *zT = reinterpret_cast<h16_t *>(smem);  // gz3 [16][ZP] channel-major (rows >= 9 never read into results)
@@ -1270,6 +1270,32 @@ __global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc
             if (co < BR && col < 27) dstp[co * 27 + col] = acc[n][j];
         }
 }
+template <int D>
+__global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const h16_t *__restrict__ gz3,
+                                                   const h16_t *__restrict__ t2, float *__restrict__ p2a) {
+    pm_w2grad<D>(a, nchunk, npc, gz3, t2, p2a);
+}
+// A whole run's W2 gradients in ONE launch (round 6): grid.y = the run's blocks, each block's gz3 and
+// partial rows in its workspace slice (base + i stride), its t2 from the pointer table.  Same
+// workgroups and arithmetic per block as k_pm_w2grad (the partial rows are bit-identical); the
+// chain of data kernels no longer waits behind 50 x 2 small weight-gradient launches, and one
+// launch of 50 x the work fills the chip.
+constexpr int MAXRUN = 64;
+struct MidRunPtrs {
+    const h16_t *t2[MAXRUN], *t3[MAXRUN], *x[MAXRUN], *g[MAXRUN];
+};
+struct MidRunWs {
+    const char *base;
+    size_t stride;
+    int64_t ogz3, ogz1, op2a, op2b;  // byte offsets inside a block's workspace slice
+};
+template <int D>
+__global__ __launch_bounds__(NT9) void k_pm_w2grad_run(PmArgs a, int nchunk, int npc, MidRunWs w, MidRunPtrs r) {
+    const int i = blockIdx.y;
+    const char *b = w.base + size_t(i) * w.stride;
+    pm_w2grad<D>(a, nchunk, npc, reinterpret_cast<const h16_t *>(b + w.ogz3), r.t2[i],
+                 reinterpret_cast<float *>(const_cast<char *>(b + w.op2a)));
+}
 
 // k_pm_w13grad: W1 (sum gz1 (x) u1, u1 = bf16(elu(x + b1a) + b1b)) and G3 (sum t3 (x) g) over npb
 // pieces of SUBV voxels per workgroup (the next piece's loads in flight); wave w: (W1 | G3,
@@ -1281,14 +1307,15 @@ constexpr int W13_ZI = SUBV / 8, W13_XI = SUBV / 4;  // items per 9-channel / 18
 constexpr int W13_RAW = (2 * SUBV * BR + 2 * SUBV * C);  // raw area (elements): gz1 | t3 | u1 | g
 static_assert(2 * W13_ZI + 2 * W13_XI <= NT, "one staging item per thread");
 
-__global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restrict__ gz1,
-                                                   const h16_t *__restrict__ t3, const h16_t *__restrict__ x,
-                                                   const h16_t *__restrict__ g, vq3d_preact_params p,
-                                                   float *__restrict__ p2b) {
+__device__ __forceinline__ void pm_w13grad(int npb, const h16_t *__restrict__ gz1, const h16_t *__restrict__ t3,
+                                           const h16_t *__restrict__ x, const h16_t *__restrict__ g, float b1a,
+                                           float b1b, float *__restrict__ p2b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int ch = blockIdx.x;
-    const Scal s = load_scal(p);
+    Scal s{};
+    s.b1a = b1a;
+    s.b1b = b1b;
     h16_t *z1T = reinterpret_cast<h16_t *>(smem);  // [16][SP] gz1
     h16_t *t3T = z1T + 16 * SP;                     // [16][SP] t3
     h16_t *u1T = t3T + 16 * SP;                     // [32][SP] u1
@@ -1383,6 +1410,20 @@ __global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restr
         const int oo = 4 * kb + j;
         if (oo < BR && c < C) dsto[oo * C + c] = acc[j];
     }
+}
+__global__ __launch_bounds__(NT) void k_pm_w13grad(int npb, const h16_t *__restrict__ gz1,
+                                                   const h16_t *__restrict__ t3, const h16_t *__restrict__ x,
+                                                   const h16_t *__restrict__ g, vq3d_preact_params p,
+                                                   float *__restrict__ p2b) {
+    pm_w13grad(npb, gz1, t3, x, g, *p.bias1a, *p.bias1b, p2b);
+}
+// the run's W1 / G3 gradients in one launch (grid.y = block; params: the run's [nblocks][11] table)
+__global__ __launch_bounds__(NT) void k_pm_w13grad_run(int npb, MidRunWs w, MidRunPtrs r,
+                                                       const float *const *__restrict__ params) {
+    const int i = blockIdx.y;
+    const char *b = w.base + size_t(i) * w.stride;
+    pm_w13grad(npb, reinterpret_cast<const h16_t *>(b + w.ogz1), r.t3[i], r.x[i], r.g[i], *params[i * 11 + 3],
+               *params[i * 11 + 4], reinterpret_cast<float *>(const_cast<char *>(b + w.op2b)));
 }
 
 // K4: every gradient entry summed over its partial rows in a fixed order and added into its
@@ -1749,6 +1790,56 @@ int vq3d_preact_mid_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_
     k_pm_reduce_run<<<dim3(NBA + NBB + 1, unsigned(nblocks)), NT, 0, as_stream(stream)>>>(
         b0, workspace_stride, off(m.p1), m.n1, off(m.p2), m.n2, off(m.p2a), m.nwa, off(m.p2b), m.nchb, grads, params);
     return check_launch("preact_mid_reduce_run");
+}
+
+int vq3d_preact_mid_wgrad_run(int32_t dtype, int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                              const void *const *t2, const void *const *t3, const void *const *x,
+                              const void *const *g, const float *const *params, void *workspaces,
+                              size_t workspace_stride, vq3d_stream_t stream) {
+    if (!vq3d_preact_mid_supported(dtype, batch, C, BR, h, w, dd))
+        return fail("preact_mid_wgrad_run: shape / dtype outside the fused mid-level block kernels");
+    if (nblocks < 1 || nblocks > 65535 || !t2 || !t3 || !x || !g || !params || !workspaces)
+        return fail("preact_mid_wgrad_run: bad arguments");
+    char *const b0 = static_cast<char *>(workspaces);
+    const MidWs m = mid_ws(batch, h, w, dd, b0);
+    if (workspace_stride < m.bytes || workspace_stride % 256)
+        return fail("preact_mid_wgrad_run: workspace stride below vq3d_preact_mid_workspace_bytes or unaligned");
+    for (int i = 0; i < nblocks; ++i)
+        if (!t2[i] || !t3[i] || !x[i] || !g[i]) return fail("preact_mid_wgrad_run: null tensor pointer");
+    hipStream_t s = as_stream(stream);
+    const PmArgs a = make_args(batch, h, w, dd, BTH, BTW);
+    const int nchunk = int(int64_t(batch) * h * w * dd / CHV);
+    auto off = [&](const void *p) { return int64_t(static_cast<const char *>(p) - b0); };
+    static bool init = false;
+    if (!init) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad_run<8>), hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<8>::LDS));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad_run<16>), hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<16>::LDS));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad_run<32>), hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<32>::LDS));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad_run<64>), hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<64>::LDS));
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_pm_w2grad_run<128>), hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<128>::LDS));
+        init = true;
+    }
+    for (int i0 = 0; i0 < nblocks; i0 += MAXRUN) {  // MAXRUN blocks per launch (kernel-argument tables)
+        const int nb = std::min(MAXRUN, nblocks - i0);
+        MidRunPtrs r{};
+        for (int i = 0; i < nb; ++i) {
+            r.t2[i] = static_cast<const h16_t *>(t2[i0 + i]);
+            r.t3[i] = static_cast<const h16_t *>(t3[i0 + i]);
+            r.x[i] = static_cast<const h16_t *>(x[i0 + i]);
+            r.g[i] = static_cast<const h16_t *>(g[i0 + i]);
+        }
+        MidRunWs wr{b0 + size_t(i0) * workspace_stride, workspace_stride, off(m.gz3), off(m.gz1), off(m.p2a), off(m.p2b)};
+        const dim3 ga(unsigned(m.nwa), unsigned(nb));
+        switch (dd) {
+            case 8: k_pm_w2grad_run<8><<<ga, NT9, W2c<8>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 16: k_pm_w2grad_run<16><<<ga, NT9, W2c<16>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 32: k_pm_w2grad_run<32><<<ga, NT9, W2c<32>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 64: k_pm_w2grad_run<64><<<ga, NT9, W2c<64>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            default: k_pm_w2grad_run<128><<<ga, NT9, W2c<128>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+        }
+        k_pm_w13grad_run<<<dim3(unsigned(m.nchb), unsigned(nb)), NT, w13_lds(), s>>>(m.npb, wr, r, params + size_t(i0) * 11);
+    }
+    return check_launch("preact_mid_wgrad_run");
 }
 
 int vq3d_preact_mid_bwd_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,

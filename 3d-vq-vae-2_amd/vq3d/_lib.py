@@ -72,6 +72,7 @@ _SIGS = {
     "vq3d_preact_mid_fwd_chain": (c_int, [c_int] * 7 + [P] * 11),
     "vq3d_preact_mid_bwd_chain": (c_int, [c_int] * 8 + [P] * 10 + [c_size, P] + [P] * 4 + [c_size, P]),
     "vq3d_preact_mid_reduce_run": (c_int, [c_int] * 5 + [P, c_size, P, P, P]),
+    "vq3d_preact_mid_wgrad_run": (c_int, [c_int] * 6 + [P, P, P, P, P, P, c_size, P]),
     "vq3d_preact_stack_supported": (c_int, [c_int] * 6),
     "vq3d_preact_stack_saved_floats": (c_size, [c_int] * 7),
     "vq3d_preact_stack_fwd": (c_int, [c_int] * 8 + [P] * 5),

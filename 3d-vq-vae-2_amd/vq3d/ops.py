@@ -391,6 +391,16 @@ def preact_tiny_bwd(g, x, saved, blk, grads):
 _mid = [True]
 
 
+_batched_wgrad = True
+
+
+def set_batched_wgrad(enabled):
+    """Mid-level runs: the weight gradients of all blocks as one launch per kind after the data
+    chain (vq3d_preact_mid_wgrad_run, default) or per block between the data kernels."""
+    global _batched_wgrad
+    _batched_wgrad = bool(enabled)
+
+
 def set_mid_blocks(enabled):
     """Route eligible bf16 PreAct blocks of the 18-channel level through the fused forward."""
     _mid[0] = bool(enabled)
@@ -513,6 +523,7 @@ def preact_mid_run_bwd(g, plan, saved, on_done=None):
     run_ws = workspace(stride * len(blocks), g.device)
     base = run_ws.data_ptr()
     ptab, gtab = plan.tables(g.device)
+    run_g = []  # batched weight gradients: every block's incoming gradient, kept for the run launch
     for i in reversed(range(len(blocks))):
         blk = blocks[i]
         x, t2, t3 = saved[i]
@@ -541,9 +552,21 @@ def preact_mid_run_bwd(g, plan, saved, on_done=None):
                    lambda a=args, ch=chain: L.call("vq3d_preact_mid_bwd_chain", first | 2, *a, *ch, L.stream()))
             _timed("k_pm_w2grad", lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 4, *a, L.stream()))
             _timed("k_pm_w13grad", lambda a=args: L.call("vq3d_preact_mid_bwd_stages", 8, *a, L.stream()))
+        elif _batched_wgrad:
+            # the data stage only; the run's weight gradients follow as one launch per kind
+            L.call("vq3d_preact_mid_bwd_chain", first | 2, *args, *chain, L.stream())
+            run_g.append(g)
         else:
             L.call("vq3d_preact_mid_bwd_chain", first | 14, *args, *chain, L.stream())
         g = gx
+    if run_g:
+        n = len(blocks)
+        arr = ctypes.c_void_p * n
+        run_g.reverse()  # run_g[i]: block i's incoming gradient
+        L.call("vq3d_preact_mid_wgrad_run", dc, n, b, h, w, d, arr(*[s_[1].data_ptr() for s_ in saved]),
+               arr(*[s_[2].data_ptr() for s_ in saved]), arr(*[s_[0].data_ptr() for s_ in saved]),
+               arr(*[t.data_ptr() for t in run_g]), L.ptr(ptab), ctypes.c_void_p(base), ctypes.c_size_t(stride),
+               L.stream())
     red = (len(blocks), b, h, w, d, ctypes.c_void_p(base), ctypes.c_size_t(stride), L.ptr(gtab), L.ptr(ptab))
     if _concurrent:
         _on_side(g.device, lambda: L.call("vq3d_preact_mid_reduce_run", *red, L.stream()), run_ws, ptab, gtab)
@@ -718,6 +741,7 @@ def preact_small_run_bwd(g, plan, saved, on_done=None):
     run_ws = workspace(stride * len(blocks), g.device)
     base = run_ws.data_ptr()
     ptab, gtab = plan.tables(g.device)
+    run_g = []  # batched weight gradients: every block's incoming gradient, kept for the run launch
     for i in reversed(range(len(blocks))):
         blk = blocks[i]
         x, t2, t3 = saved[i]

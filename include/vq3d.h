@@ -221,6 +221,19 @@ int vq3d_preact_mid_bwd_chain(int32_t stages, int32_t dtype, int32_t batch, int3
 int vq3d_preact_mid_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
                                const void *workspaces, size_t workspace_stride, float *const *grads,
                                const float *const *params, vq3d_stream_t stream);
+/* Stages 4 and 8 (the W2 and W1 / G3 weight-gradient partial rows) of a whole run in one launch
+ * each, after the run's data stages (bwd_chain with stages 2 | first): block i's gz3 / gz1 and
+ * partial rows in its workspace slice (workspaces + i * workspace_stride, as for reduce_run), its
+ * saved t2 / t3, its input x and its incoming gradient g given as HOST arrays [nblocks] of device
+ * pointers, params the run's device table [nblocks][11] (bias1a / bias1b are read).  The partial
+ * rows are bit-identical to per-block stages 4 | 8; vq3d_preact_mid_reduce_run then sums them.
+ * dtype: the activations' 16-bit format (VQ3D_HALF with the build's format, as for the stages).
+ * (Replaces the per-block reference call sites vqvae/layers.py:176-195's weight gradients, which
+ * autograd runs interleaved with the data chain.) */
+int vq3d_preact_mid_wgrad_run(int32_t dtype, int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                              const void *const *t2, const void *const *t3, const void *const *x,
+                              const void *const *g, const float *const *params, void *workspaces,
+                              size_t workspace_stride, vq3d_stream_t stream);
 
 /* A RUN of nblocks identical PreActFixupResBlocks (mode 'same', no skip conv) on a tiny grid
  * (batch*h*w*d <= 256, channels <= 32, branch <= 16, both multiples of 4): forward in ONE launch,

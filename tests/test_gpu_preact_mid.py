@@ -297,3 +297,27 @@ def test_mid_run_chain_ignores_stale_lds(gpu, shape, half):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     for n in a[2]:
         assert torch.equal(a[2][n], b[2][n]), n
+
+
+@pytest.mark.parametrize("shape,nblk", [((2, 18, 16, 8, 16), 4), ((1, 18, 128, 128, 32), 5)])
+@pytest.mark.parametrize("half", HALF)
+def test_mid_run_batched_wgrad_bitwise(gpu, shape, nblk, half):
+    """The run's weight gradients as one launch per kind after the data chain
+    (vq3d_preact_mid_wgrad_run, the default) against the per-block stages 4 | 8 between the data
+    kernels: the same workgroups and arithmetic per block, so out, gx and every gradient are equal
+    bit for bit (the fixed-order reduction sums the same partial rows)."""
+    from vq3d import ops
+    _H[0] = half
+    blocks = [_block(seed=60 + i) for i in range(nblk)]
+    g = torch.Generator().manual_seed(61)
+    x = rnd(torch.randn(shape, generator=g))
+    gy = rnd(torch.randn(shape, generator=g))
+    ops.set_batched_wgrad(False)
+    try:
+        a = _run_chain(blocks, x, gy, gpu, chained=True)
+    finally:
+        ops.set_batched_wgrad(True)
+    b = _run_chain(blocks, x, gy, gpu, chained=True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for n in a[2]:
+        assert torch.equal(a[2][n], b[2][n]), n
