@@ -161,6 +161,21 @@ __device__ __forceinline__ void unpack(const typename Vec<N>::U &u, float (&o)[N
         }
     }
 }
+// element i of N packed 16-bit values, as stored (no float round trip)
+template <int N>
+__device__ __forceinline__ h16_t half_of(const typename Vec<N>::U &u, int i) {
+    if constexpr (N == 1) {
+        return h16_t(u);
+    } else if constexpr (N == 2) {
+        return h16_t(i ? u >> 16 : u & 0xffffu);
+    } else if constexpr (N == 4) {
+        const uint32_t w = i < 2 ? u.x : u.y;
+        return h16_t(i & 1 ? w >> 16 : w & 0xffffu);
+    } else {
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+        return h16_t(i & 1 ? w[i >> 1] >> 16 : w[i >> 1] & 0xffffu);
+    }
+}
 template <int N>
 __device__ __forceinline__ typename Vec<N>::U packv(const float (&v)[N]) {
     if constexpr (N == 1) {
@@ -521,7 +536,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
 #pragma unroll
                             for (int c = 0; c < C; ++c) g3[oo][c] = fmaf(t3f[oo], gf[c], g3[oo][c]);
                         }
-                        t2T[(oo * NLN + line) * TP + pos] = f2h(t2f[oo]);
+                        t2T[(oo * NLN + line) * TP + pos] = half_of<BR>(tv2[u], oo);  // the stored bits
                     }
                     const typename Vec<BR>::U zp = packv<BR>(z);
                     *reinterpret_cast<typename Vec<BR>::U *>(z3h + q * BR) = zp;

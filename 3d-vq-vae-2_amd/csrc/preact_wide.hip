@@ -576,11 +576,11 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
 // wave (m-tile w % 3 of co, column tiles 4 (w / 3) ..).  Workgroups [9 * nch, 9 * nch + nchb):
 // W1 (sum gz1 (x) u1) and G3 (sum t3 (x) g) over a 128-voxel chunk; wave (m-tile w % 3 of o,
 // W1 or G3).  Voxels are the MFMA reduction axis: channel-major LDS copies.
-__global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float *__restrict__ g,
-                                                   const float *__restrict__ x, const h16_t *__restrict__ t2,
-                                                   const h16_t *__restrict__ t3, const h16_t *__restrict__ gz3,
-                                                   const h16_t *__restrict__ gz1, vq3d_preact_params p,
-                                                   float *__restrict__ p2a, float *__restrict__ p2b) {
+__device__ __forceinline__ void wide_wgrad(const WArgs &a, int nch, const float *__restrict__ g,
+                                           const float *__restrict__ x, const h16_t *__restrict__ t2,
+                                           const h16_t *__restrict__ t3, const h16_t *__restrict__ gz3,
+                                           const h16_t *__restrict__ gz1, const vq3d_preact_params &p,
+                                           float *__restrict__ p2a, float *__restrict__ p2b) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, row = lane & 15, kb = lane >> 4;
     const int mt = wave % 3, hf = wave / 3;
@@ -761,6 +761,34 @@ __global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float
             if (oo < BR && c < C) dst[oo * C + c] = acc[n][j];
         }
     }
+}
+
+__global__ __launch_bounds__(NT) void k_wide_wgrad(WArgs a, int nch, const float *__restrict__ g,
+                                                   const float *__restrict__ x, const h16_t *__restrict__ t2,
+                                                   const h16_t *__restrict__ t3, const h16_t *__restrict__ gz3,
+                                                   const h16_t *__restrict__ gz1, vq3d_preact_params p,
+                                                   float *__restrict__ p2a, float *__restrict__ p2b) {
+    wide_wgrad(a, nch, g, x, t2, t3, gz3, gz1, p, p2a, p2b);
+}
+// A whole run's weight-gradient partial rows in one launch (round 6, as preact_mid's
+// k_pm_w2grad_run): grid.y = the run's blocks, their gz3 / gz1 / partial rows in their workspace
+// slices, their g / x / t2 / t3 from kernel-argument tables, their scalars from the run's
+// [nblocks][11] parameter table.  The same workgroups and arithmetic as k_wide_wgrad per block.
+constexpr int WMAXRUN = 56;
+struct WideRunPtrs {
+    const float *g[WMAXRUN], *x[WMAXRUN];
+    const h16_t *t2[WMAXRUN], *t3[WMAXRUN];
+};
+__global__ __launch_bounds__(NT) void k_wide_wgrad_run(WArgs a, int nch, const char *__restrict__ base, size_t stride,
+                                                       int64_t ogz3, int64_t ogz1, int64_t op2a, int64_t op2b,
+                                                       WideRunPtrs r, const float *const *__restrict__ params) {
+    const int i = blockIdx.y;
+    char *b = const_cast<char *>(base) + size_t(i) * stride;
+    const float *const *t = params + size_t(i) * 11;
+    const vq3d_preact_params p{t[3], t[4], t[5], t[6], t[7], t[8], t[9], t[10]};
+    wide_wgrad(a, nch, r.g[i], r.x[i], r.t2[i], r.t3[i], reinterpret_cast<const h16_t *>(b + ogz3),
+               reinterpret_cast<const h16_t *>(b + ogz1), p, reinterpret_cast<float *>(b + op2a),
+               reinterpret_cast<float *>(b + op2b));
 }
 
 struct RedOut {
@@ -972,6 +1000,46 @@ int vq3d_preact_wide_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32
         nch, nchb, a.ntiles, static_cast<const char *>(workspaces), workspace_stride, int64_t(l.p2a), int64_t(l.p2b),
         int64_t(l.p1), grads, params);
     return check_launch("preact_wide_reduce_run");
+}
+
+int vq3d_preact_wide_wgrad_run(int32_t dtype, int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                               const float *const *g, const float *const *x, const void *const *t2,
+                               const void *const *t3, const float *const *params, void *workspaces,
+                               size_t workspace_stride, vq3d_stream_t stream) {
+    if (dtype != VQ3D_HALF) return fail("preact_wide_wgrad_run: dtype must be the 16-bit format of this build");
+    if (!vq3d_preact_wide_supported(batch, C, BR, h, w, dd))
+        return fail("preact_wide_wgrad_run: shape outside the fused wide-block kernels");
+    if (nblocks < 1 || nblocks > 65535 || !g || !x || !t2 || !t3 || !params || !workspaces)
+        return fail("preact_wide_wgrad_run: bad arguments");
+    const WsLayout l = ws_layout(batch, h, w, dd);
+    if (workspace_stride < l.total || workspace_stride % 256)
+        return fail("preact_wide_wgrad_run: stride below the workspace size or unaligned");
+    for (int i = 0; i < nblocks; ++i)
+        if (!g[i] || !x[i] || !t2[i] || !t3[i]) return fail("preact_wide_wgrad_run: null tensor pointer");
+    set_lds_limits();
+    static bool init = false;
+    if (!init) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_wide_wgrad_run),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, int(kWgLds));
+        init = true;
+    }
+    const WArgs a = make_args(batch, h, w, dd);
+    const int nch = int(int64_t(batch) * h * w * dd / CHV), nchb = int(int64_t(batch) * h * w * dd / SUBV);
+    const char *b0 = static_cast<const char *>(workspaces);
+    for (int i0 = 0; i0 < nblocks; i0 += WMAXRUN) {
+        const int nb = std::min(WMAXRUN, nblocks - i0);
+        WideRunPtrs r{};
+        for (int i = 0; i < nb; ++i) {
+            r.g[i] = g[i0 + i];
+            r.x[i] = x[i0 + i];
+            r.t2[i] = static_cast<const h16_t *>(t2[i0 + i]);
+            r.t3[i] = static_cast<const h16_t *>(t3[i0 + i]);
+        }
+        k_wide_wgrad_run<<<dim3(unsigned(9 * nch + nchb), unsigned(nb)), NT, kWgLds, as_stream(stream)>>>(
+            a, nch, b0 + size_t(i0) * workspace_stride, workspace_stride, int64_t(l.gz3), int64_t(l.gz1),
+            int64_t(l.p2a), int64_t(l.p2b), r, params + size_t(i0) * 11);
+    }
+    return check_launch("preact_wide_wgrad_run");
 }
 
 int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t dtype, int32_t batch, int32_t channels, int32_t branch,

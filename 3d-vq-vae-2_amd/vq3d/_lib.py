@@ -88,6 +88,7 @@ _SIGS = {
     "vq3d_preact_wide_bwd_weight": (c_int, [c_int] * 7 + [P] * 7 + [c_size, P]),
     "vq3d_preact_wide_bwd_weight_stages": (c_int, [c_int] * 8 + [P] * 7 + [c_size, P]),
     "vq3d_preact_wide_reduce_run": (c_int, [c_int] * 5 + [P, c_size, P, P, P]),
+    "vq3d_preact_wide_wgrad_run": (c_int, [c_int] * 6 + [P, P, P, P, P, P, c_size, P]),
     "vq3d_preact_small_supported": (c_int, [c_int] * 7),
     "vq3d_preact_small_workspace_bytes": (c_size, [c_int] * 6),
     "vq3d_preact_small_plan": (c_int, [c_int] * 6),

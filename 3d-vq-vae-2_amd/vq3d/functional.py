@@ -362,15 +362,21 @@ class PreActWideFn(torch.autograd.Function):
         base = img.data_ptr()
         gs = ops.cast(_cl(g), torch.float32)
         run_ws, wbase, stride = ops.preact_wide_run_workspace(plan, gs.shape, gs.device)
+        batched = ops.batched_wgrad() and not ops.concurrent_wgrad()
+        run = [None] * len(plan.blocks)  # batched: (g, x, t2, t3) per block for one weight launch
         for i in reversed(range(len(plan.blocks))):
             blk = plan.blocks[i]
             xs, t2, t3 = saved[3 * i: 3 * i + 3]
             names = {"dw1": blk.branch_conv1.weight, "dw2": blk.branch_conv2.weight, "dw3": blk.branch_conv3.weight,
                      "dbias1a": blk.bias1a, "dbias1b": blk.bias1b, "dbias2a": blk.bias2a, "dbias2b": blk.bias2b,
                      "dbias3a": blk.bias3a, "dbias3b": blk.bias3b, "dscale": blk.scale, "dbias4": blk.bias4}
+            if batched:
+                run[i] = (gs, xs, t2, t3)
             gs = ops.preact_wide_bwd(gs, xs, t2, t3, base + i * ctx.per, blk,
                                      {n: grad_buf(t) for n, t in names.items()}, ws_ptr=wbase + i * stride,
-                                     reduce=False)
+                                     reduce=False, weights=not batched)
+        if batched:
+            ops.preact_wide_wgrad_run(plan, gs.shape, run_ws, stride, *[list(v) for v in zip(*run)])
         ops.preact_wide_reduce_run(plan, gs.shape, run_ws, stride)
         grads_ready(plan.params)
         return (ops.cast(gs, ctx.in_dtype), None) + (None,) * ctx.n_params

@@ -395,10 +395,19 @@ _batched_wgrad = True
 
 
 def set_batched_wgrad(enabled):
-    """Mid-level runs: the weight gradients of all blocks as one launch per kind after the data
-    chain (vq3d_preact_mid_wgrad_run, default) or per block between the data kernels."""
+    """Mid-level (18-channel) and wide (72-channel) runs: the weight gradients of all blocks as one
+    launch per kind after the data chain (vq3d_preact_mid_wgrad_run / vq3d_preact_wide_wgrad_run,
+    the default) or per block between the data kernels."""
     global _batched_wgrad
     _batched_wgrad = bool(enabled)
+
+
+def batched_wgrad():
+    return _batched_wgrad
+
+
+def concurrent_wgrad():
+    return _concurrent
 
 
 def set_mid_blocks(enabled):
@@ -800,11 +809,12 @@ def preact_wide_fwd(x32, img_ptr, blk, save=True, dtype=torch.bfloat16):
     return out, t2, t3
 
 
-def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads, ws_ptr=None, reduce=True):
+def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads, ws_ptr=None, reduce=True, weights=True):
     """gx (fp32) of preact_wide_fwd; the parameter gradients (grads: name -> fp32 buffer, +=) on
     the side stream when concurrent weight gradients are on.  ws_ptr: the block's slice of a run
     workspace (else one is allocated); reduce=False leaves the fixed-order reduction to the
-    caller's vq3d_preact_wide_reduce_run."""
+    caller's vq3d_preact_wide_reduce_run; weights=False also leaves the weight-gradient stage to
+    the caller's vq3d_preact_wide_wgrad_run (preact_wide_wgrad_run)."""
     b, c, h, w, d = x32.shape
     nb = blk.branch_conv1.weight.shape[0]
     gx = torch.empty_like(x32, memory_format=CL)
@@ -818,6 +828,8 @@ def preact_wide_bwd(g32, x32, t2, t3, img_ptr, blk, grads, ws_ptr=None, reduce=T
     dc = L.dtype_code(t2)
     L.call("vq3d_preact_wide_bwd_data", dc, b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
            ctypes.c_void_p(img_ptr), ctypes.byref(prm), wsp, ctypes.c_size_t(nws), L.ptr(gx), L.stream())
+    if not weights:
+        return gx
     gr = L.PreactGrads(*[_p(grads.get(n)) for n, _ in L.PreactGrads._fields_])
     args = (1 | (2 if reduce else 0), dc, b, c, nb, h, w, d, L.ptr(g32), L.ptr(x32), L.ptr(t2), L.ptr(t3),
             ctypes.byref(prm), ctypes.byref(gr), wsp, ctypes.c_size_t(nws))
@@ -836,6 +848,18 @@ def preact_wide_run_workspace(plan, shape, device):
     stride = (nws + 255) // 256 * 256
     buf = workspace(stride * len(plan.blocks), device)
     return buf, buf.data_ptr(), stride
+
+
+def preact_wide_wgrad_run(plan, shape, run_ws, stride, gs, xs, t2s, t3s):
+    """Every block's weight-gradient partial rows of a wide run, one launch (after the data chain;
+    per-block lists: incoming gradient, input, saved t2 / t3)."""
+    b, c, h, w, d = shape
+    n = len(plan.blocks)
+    ptab, _ = plan.tables(run_ws.device)
+    arr = ctypes.c_void_p * n
+    L.call("vq3d_preact_wide_wgrad_run", L.dtype_code(t2s[0]), n, b, h, w, d, arr(*[t.data_ptr() for t in gs]),
+           arr(*[t.data_ptr() for t in xs]), arr(*[t.data_ptr() for t in t2s]), arr(*[t.data_ptr() for t in t3s]),
+           L.ptr(ptab), L.ptr(run_ws), ctypes.c_size_t(stride), L.stream())
 
 
 def preact_wide_reduce_run(plan, shape, run_ws, stride):

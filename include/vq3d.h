@@ -303,6 +303,15 @@ int vq3d_preact_wide_bwd_weight_stages(int32_t stages, int32_t dtype, int32_t ba
                                        int32_t w, int32_t dd, const float *g, const float *x, const void *t2,
                                        const void *t3, const vq3d_preact_params *p, const vq3d_preact_grads *gr,
                                        const void *workspace, size_t workspace_bytes, vq3d_stream_t stream);
+/* The weight-gradient stage (1 of vq3d_preact_wide_bwd_weight_stages) of a whole run in one
+ * launch, after the run's data kernels: block i's gz3 / gz1 and partial rows in its workspace slice
+ * (workspaces + i * workspace_stride, as for vq3d_preact_wide_reduce_run), its incoming gradient g
+ * and input x (fp32) and its saved t2 / t3 as HOST arrays [nblocks] of device pointers, params the
+ * run's device table [nblocks][11].  Partial rows bit-identical to the per-block stage. */
+int vq3d_preact_wide_wgrad_run(int32_t dtype, int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
+                               const float *const *g, const float *const *x, const void *const *t2,
+                               const void *const *t3, const float *const *params, void *workspaces,
+                               size_t workspace_stride, vq3d_stream_t stream);
 int vq3d_preact_wide_reduce_run(int32_t nblocks, int32_t batch, int32_t h, int32_t w, int32_t dd,
                                 const void *workspaces, size_t workspace_stride, float *const *grads,
                                 const float *const *params, vq3d_stream_t stream);

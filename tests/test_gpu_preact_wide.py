@@ -30,7 +30,7 @@ def _bf16_by_default():
     yield
 
 
-def _run(gpu, case, seed=0, concurrent=True):
+def _run(gpu, case, seed=0, concurrent=True, batched=True):
     from vq3d import functional as Fn
     from vq3d import ops
     from vq3d.flat import FlatParams
@@ -46,6 +46,7 @@ def _run(gpu, case, seed=0, concurrent=True):
     orig = Fn.PreActWideFn.apply
     Fn.PreActWideFn.apply = lambda *a: calls.append(1) or orig(*a)
     ops.set_concurrent_wgrad(concurrent)
+    ops.set_batched_wgrad(batched)
     try:
         xg = x.to(gpu).to(_H[0]).contiguous(memory_format=CL).requires_grad_(True)
         y = m(xg)
@@ -55,6 +56,7 @@ def _run(gpu, case, seed=0, concurrent=True):
     finally:
         Fn.PreActWideFn.apply = orig
         ops.set_concurrent_wgrad(False)
+        ops.set_batched_wgrad(True)
     assert calls == [1]  # the whole run went through the wide kernels
     return m, y, xg, ref
 
@@ -93,3 +95,16 @@ def test_wide_deterministic_and_stream_independent(gpu):
     for r in res[1:]:
         for a, b in zip(res[0], r):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", [(1, 32, 32, 8, 3), (2, 4, 8, 8, 2)])
+def test_wide_batched_wgrad_bitwise(gpu, case):
+    """The run's weight gradients as one launch after the data chain (vq3d_preact_wide_wgrad_run,
+    the default on the main stream) against the per-block weight stage: bit for bit (the per-block
+    path itself is held to the float64 chain by test_wide_matches_float64_chain)."""
+    res = []
+    for batched in (False, True):
+        m, y, xg, _ = _run(gpu, case, seed=7, concurrent=False, batched=batched)
+        res.append([y.detach().clone(), xg.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
