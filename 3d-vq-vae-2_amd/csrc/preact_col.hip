@@ -46,6 +46,9 @@
 #ifndef COL_UNROLL_B
 #define COL_UNROLL_B 2  // ... and of the backward's phase B1
 #endif
+#ifndef COL_SWEIGHTS
+#define COL_SWEIGHTS 1  // the backward's W1 / W3 held in SGPRs (0: plain loads, for A/B timing)
+#endif
 #ifndef FWD_PERSIST
 #define FWD_PERSIST 1  // the forward walks brick ranges too (its grid: CArgs::nwg)
 #endif
@@ -93,6 +96,22 @@ __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >
 __device__ __forceinline__ float bf(uint32_t u16) { return h2f_lo(u16); }
 __device__ __forceinline__ float rbf(float v) { return bf(f2h(v)); }
 __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : __expf(z) - 1.f; }
+// N wave-uniform weights loaded once into SGPRs and laundered, so the compiler keeps them there: as
+// plain loads it re-issued them inside the halo / epilogue loops (32 s_load_dword per 4 halo items
+// of the (4, 2) backward, each with a lgkmcnt wait that also waited for the LDS stores)
+template <int N>
+struct SWeights {
+    float v[N];
+    __device__ __forceinline__ explicit SWeights(const float *__restrict__ w) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            float x = w[i];
+            if constexpr (COL_SWEIGHTS) asm volatile("" : "+s"(x));
+            v[i] = x;
+        }
+    }
+    __device__ __forceinline__ float operator[](int i) const { return v[i]; }
+};
 __device__ __forceinline__ float elu_d_act(float t, float b) {
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
@@ -461,6 +480,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
     static_assert(size_t(HVX * BR + PADE + BR * NLN * TP) * 2 >= size_t(4 * K::NTN * 256) * 4, "W2 sums fit z3h + t2T");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
     const Scal s = load_scal(p);
+    const SWeights<C * BR> w3s(w3), w1s(w1);
     hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, true>(w2, k, lane);
@@ -526,7 +546,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                     for (int oo = 0; oo < BR; ++oo) {
                         float acc = 0.f;
 #pragma unroll
-                        for (int c = 0; c < C; ++c) acc = fmaf(w3[c * BR + oo], gf[c], acc);
+                        for (int c = 0; c < C; ++c) acc = fmaf(w3s[c * BR + oo], gf[c], acc);
                         const float gt3 = s.sc * acc;
                         z[oo] = gt3 * elu_d_act(t3f[oo], s.b3b);
                         if (in) {
@@ -619,7 +639,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                 for (int c = 0; c < C; ++c) {
                     float gt1 = 0.f;
 #pragma unroll
-                    for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1[oo * C + c], z1[oo], gt1);
+                    for (int oo = 0; oo < BR; ++oo) gt1 = fmaf(w1s[oo * C + c], z1[oo], gt1);
                     const int e = vi * C + c;
                     const float zx = xe[e] + s.b1a;
                     const float e1 = zx > 0.f ? 1.f : __expf(zx);

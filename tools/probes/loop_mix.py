@@ -44,3 +44,15 @@ for h in heads:
             c.update(b['ins'])
     print(f"loop {h}: {sum(c.values())} instructions")
     print('  ', sorted(c.items(), key=lambda t: -t[1])[:top])
+
+if len(sys.argv) > 4 and sys.argv[4] == "nested":
+    # every loop (any depth): instructions of the blocks whose innermost header it is
+    own = collections.defaultdict(collections.Counter)
+    for b in blocks:
+        h = b['own'] if any(x.get('hdr') == b['own'] for x in blocks) and b['own'] else b['hdr']
+        own[h].update(b['ins'])
+    for h, c in own.items():
+        if h:
+            print(f"  loop {h} (own blocks): {sum(c.values())} instructions; "
+                  f"VALU {sum(v for k, v in c.items() if k.startswith('v_'))}, MFMA {c['v_mfma_f32_16x16x32_bf16']}, "
+                  f"LDS {sum(v for k, v in c.items() if k.startswith('ds_'))}, VMEM {sum(v for k, v in c.items() if k.startswith(('global_', 'buffer_')))}")
