@@ -64,7 +64,10 @@ constexpr int HL = BH + 2, WL = BW + 2, PL = BD + 2, NLN = HL * WL, HVX = NLN * 
 constexpr int NV = BH * BW * BD, NMT = NV / 16;  // 1024 voxels, 64 m-tiles (one per brick line)
 constexpr int NT = 256;
 static_assert(BD == 16 && NT / (BD / DV) == BH * BW, "m-tile = brick line; thread = (line, D-group)");
-constexpr int TP = 24;        // channel-major halo line pitch (positions 0..17, zero pad)
+#ifndef COL_TP
+#define COL_TP 28  // 28: the W2-gradient window reads 2.25 -> 1.5-way (4,2) and 3.7 -> 1.3-way (8,4) bank conflicts (modelled); 24 measured 1.6 % / 6.5 % slower
+#endif
+constexpr int TP = COL_TP;    // channel-major halo line pitch (positions 0..17, zero pad)
 constexpr int ZP = NV + 16;   // channel-major interior pitch
 constexpr int PADE = 32;      // zero tail of the position-major halo buffers
 constexpr int NSC = 8;        // scalar partials: b4, b3b, b3a, scale, b2b, b2a, b1b, b1a
