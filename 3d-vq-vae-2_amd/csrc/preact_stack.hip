@@ -1344,13 +1344,22 @@ __global__ __launch_bounds__(RNT) void k_stackr_fwd(SkArgs a, const h16_t *__res
         __syncthreads();
         RPROBE(blk, 2)
         // t3 = elu_f(W2 (*) t2 + b3a) + b3b over the gathered neighbour rows
+        // all column blocks' gathers and MFMAs first, then their epilogues: the next block's
+        // LDS gathers are issued while the previous one's MFMA chain runs, and the epilogues
+        // overlap the last MFMAs (in-order issue: an epilogue first would wait for its chain)
         u32x2 t3p[NH];
+        f32x4 cc[NH];
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
             if (!act[h]) continue;
             hx8 nb[14];
             gather14(l.t2s, nbo[h], kb, nb);
-            const f32x4 c = conv14(fr, nb);
+            cc[h] = conv14(fr, nb);
+        }
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const f32x4 c = cc[h];
             t3p[h] = u32x2{pk2h(e3(c[0]), e3(c[1])), pk2h(e3(c[2]), e3(c[3]))};
             *reinterpret_cast<u32x2 *>(l.t3s + pl_off(vv[h], 4 * kb)) = t3p[h];
         }
@@ -1533,12 +1542,18 @@ __global__ __launch_bounds__(RNT) void k_stackr_bwd(SkArgs a, const h16_t *__res
         RPROBE(blk, 2)
         // gt2 = W2^T (*) gz3 over the flipped taps' neighbour rows; gz1 = gt2 * elu'(t2 - b2b)
         u32x2 z1p[NH];
+        f32x4 cc[NH];
 #pragma unroll
-        for (int h = 0; h < NH; ++h) {
+        for (int h = 0; h < NH; ++h) {  // gathers and MFMAs of every column block, then the epilogues
             if (!act[h]) continue;
             hx8 nb[14];
             gather14(l.z3s, nbo[h], kb, nb);
-            const f32x4 c = conv14(fr, nb);
+            cc[h] = conv14(fr, nb);
+        }
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            if (!act[h]) continue;
+            const f32x4 c = cc[h];
             const float t2v[4] = {s2[h].x, s2[h].y, s2[h].z, s2[h].w};
             float z[4];
 #pragma unroll
