@@ -49,6 +49,9 @@
 #ifndef COL_SWEIGHTS
 #define COL_SWEIGHTS 1  // the backward's W1 / W3 held in SGPRs (0: plain loads, for A/B timing)
 #endif
+#ifndef COL_PAIRS
+#define COL_PAIRS 1  // the backward's halo phase on position pairs (0: one position per item, A/B)
+#endif
 #ifndef FWD_PERSIST
 #define FWD_PERSIST 1  // the forward walks brick ranges too (its grid: CArgs::nwg)
 #endif
@@ -519,7 +522,86 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         __syncthreads();  // the previous brick's readers of the LDS tiles are done
         line_table(a, o, lbase);
         __syncthreads();
-        // A. gz3 on the halo; t2 on the halo (channel-major); interior sums and G3 = sum t3 (x) g
+        // A. gz3 on the halo; t2 on the halo (channel-major); interior sums and G3 = sum t3 (x) g.
+#if COL_PAIRS
+        // Work items are PAIRS of consecutive positions of a halo line (PL is even): one line /
+        // position computation per pair, and the channel-major t2 copy and the position-major gz3
+        // leave as whole-dword (pair) LDS stores instead of two 16-bit stores into one dword.
+        // Two batches of pairs, every load of a batch issued before its math (registers).
+        constexpr int NPAIR = HVX / 2, HP = PL / 2;
+        static_assert(PL % 2 == 0 && TP % 2 == 0 && 2 * BR <= 8, "position pairs are dword aligned");
+        constexpr int PH = ((NPAIR + NT - 1) / NT + 1) / 2;
+#pragma unroll 1
+        for (int half = 0; half < 2; ++half) {
+            constexpr int P = PH;
+            Raw<TO, C> gv[P][2];
+            typename Vec<BR>::U tv3[P][2], tv2[P][2];
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const int qq = min(tid + (half * PH + u) * NT, NPAIR - 1), line = qq / HP, pos0 = 2 * (qq - line * HP);
+                const int lb = lbase[line] - o.d0;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int d = o.d0 - 1 + pos0 + e;
+                    const int vx = lb + (d < 0 ? d + a.D : (d >= a.D ? d - a.D : d));
+                    gv[u][e] = ldraw<TO, C>(g + int64_t(vx) * C);
+                    tv3[u][e] = *reinterpret_cast<const typename Vec<BR>::U *>(t3 + int64_t(vx) * BR);
+                    tv2[u][e] = *reinterpret_cast<const typename Vec<BR>::U *>(t2 + int64_t(vx) * BR);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const int qp = tid + (half * PH + u) * NT;
+                if (qp < NPAIR) {
+                    const int line = qp / HP, pos0 = 2 * (qp - line * HP);
+                    const int lh = line / WL, lw = line - lh * WL;
+                    const bool lin = lh >= 1 && lh <= BH && lw >= 1 && lw <= BW;  // an interior line
+                    const int vb = ((lh - 1) * BW + lw - 1) * BD - 1;            // interior index of position 0
+                    float z[2][BR];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int pos = pos0 + e;
+                        const bool in = lin && pos >= 1 && pos <= BD;
+                        float gf[C], t3f[BR];
+                        unraw<TO, C>(gv[u][e], gf);
+                        unpack<BR>(tv3[u][e], t3f);
+#pragma unroll
+                        for (int oo = 0; oo < BR; ++oo) {
+                            float acc = 0.f;
+#pragma unroll
+                            for (int c = 0; c < C; ++c) acc = fmaf(w3s[c * BR + oo], gf[c], acc);
+                            const float gt3 = s.sc * acc;
+                            z[e][oo] = gt3 * elu_d_act(t3f[oo], s.b3b);
+                            if (in) {
+                                s3b += gt3;
+                                s3a += z[e][oo];
+                                ssc = fmaf(acc, t3f[oo], ssc);
+#pragma unroll
+                                for (int c = 0; c < C; ++c) g3[oo][c] = fmaf(t3f[oo], gf[c], g3[oo][c]);
+                            }
+                        }
+                        if (in) {
+#pragma unroll
+                            for (int c = 0; c < C; ++c) s4 += gf[c];
+#pragma unroll
+                            for (int oo = 0; oo < BR; ++oo) z3T[oo * ZP + vb + pos] = f2h(z[e][oo]);
+                        }
+                    }
+#pragma unroll
+                    for (int oo = 0; oo < BR; ++oo)  // the stored bits of the pair's t2, channel oo
+                        *reinterpret_cast<uint32_t *>(t2T + (oo * NLN + line) * TP + pos0) =
+                            uint32_t(half_of<BR>(tv2[u][0], oo)) | (uint32_t(half_of<BR>(tv2[u][1], oo)) << 16);
+                    // gz3 of the pair: 2 BR contiguous 16-bit values at (line, pos0)
+                    float zz[2 * BR];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e)
+#pragma unroll
+                        for (int oo = 0; oo < BR; ++oo) zz[e * BR + oo] = z[e][oo];
+                    *reinterpret_cast<typename Vec<2 * BR>::U *>(z3h + (line * PL + pos0) * BR) = packv<2 * BR>(zz);
+                }
+            }
+        }
+#else
         // two batches of halo items: every load of a batch issued before its math (registers)
         constexpr int PH = ((HVX + NT - 1) / NT + 1) / 2;
 #pragma unroll 1
@@ -574,6 +656,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                 }
             }
         }
+#endif
         __syncthreads();
         // the thread's 4 voxels (phase C): g and x in flight during phase B
         const int ln = tid / (BD / DV), dg = tid % (BD / DV);
