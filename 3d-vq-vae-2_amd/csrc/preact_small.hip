@@ -31,6 +31,9 @@ namespace {
 constexpr int NT = 256;           // threads per workgroup (both kernels)
 constexpr int kNScal = 8;         // scalar partials: b4, scale, b3b, b3a, b2b, b2a, b1b, b1a
 constexpr size_t kLdsTarget = 80 * 1024;
+#ifndef SMALL_TSPLIT
+#define SMALL_TSPLIT 1  // bricks below NT voxels: the 27 taps over NT / nvb thread groups (0: one voxel per thread)
+#endif
 #ifndef SMALL_MINV
 #define SMALL_MINV 64  // smallest brick halved to for more workgroups (timing experiments: EXPDEF=SMALL_MINV)
 #endif
@@ -156,6 +159,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *w2s = sm;                  // [tap][c][o]
     float *t2h = w2s + 27 * BR * BR;  // [halo position][BR]
+    float *tps = t2h + a.hp * BR;     // [NT][BR] tap-group partials (bricks below NT voxels)
     __shared__ float w1s[BR * C], w3s[C * BR];  // W1 [o][c], W3 [co][o] (torch order)
     const int tid = threadIdx.x;
     for (int i = tid; i < 27 * BR * BR; i += NT) {
@@ -200,27 +204,12 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
             }
         }
         __syncthreads();
-        // B. t3 and out of the brick's voxels, one voxel per thread
-        for (int v = tid; v < a.nvb; v += NT) {
-            const int pos = halo_pos(a, v);
+        // B. t3 and out of the brick's voxels.  A brick smaller than the workgroup (the 64-voxel
+        // bricks of a 32x32x8 grid) splits the 27 taps over G = NT / nvb thread groups: a quarter of
+        // the dependent tap chain per thread, the partials summed by group 0 in group order.
+        auto epi = [&](int v, const float (&acc)[BR], const float (&xv)[C]) {
             const int64_t vox = brick_vox(a, k, v);
-            float xv[C], ov[C];
-            ldvec<TX, C>(x + vox * C, xv);  // in flight during the taps
-            float acc[BR];
-#pragma unroll
-            for (int o = 0; o < BR; ++o) acc[o] = 0.f;
-#pragma unroll 1
-            for (int tap = 0; tap < 27; ++tap) {
-                const float *tr = t2h + (pos + tap_off(a, tap)) * BR;
-                const float *wr = w2s + tap * BR * BR;
-#pragma unroll
-                for (int c = 0; c < BR; ++c) {
-                    const float tv = tr[c];
-#pragma unroll
-                    for (int o = 0; o < BR; ++o) acc[o] = fmaf(tv, wr[c * BR + o], acc[o]);
-                }
-            }
-            float t3v[BR];
+            float t3v[BR], ov[C];
 #pragma unroll
             for (int o = 0; o < BR; ++o) t3v[o] = rbf(elu(acc[o] + s.b3a) + s.b3b);
             if (t3o) stv<BR>(t3o + vox * BR, t3v);
@@ -232,6 +221,45 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
                 ov[co] = r * s.sc + s.b4 + xv[co];
             }
             stvec<TO, C>(out + vox * C, ov);
+        };
+        auto taps = [&](int pos, int t0, int t1, float (&acc)[BR]) {
+#pragma unroll
+            for (int o = 0; o < BR; ++o) acc[o] = 0.f;
+#pragma unroll 1
+            for (int tap = t0; tap < t1; ++tap) {
+                const float *tr = t2h + (pos + tap_off(a, tap)) * BR;
+                const float *wr = w2s + tap * BR * BR;
+#pragma unroll
+                for (int c = 0; c < BR; ++c) {
+                    const float tv = tr[c];
+#pragma unroll
+                    for (int o = 0; o < BR; ++o) acc[o] = fmaf(tv, wr[c * BR + o], acc[o]);
+                }
+            }
+        };
+        if (SMALL_TSPLIT && a.nvb < NT) {
+            const int G = NT / a.nvb, v = tid & (a.nvb - 1), tg = tid / a.nvb;
+            float xv[C], acc[BR];
+            if (tg == 0) ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // in flight during the taps
+            taps(halo_pos(a, v), 27 * tg / G, 27 * (tg + 1) / G, acc);
+            if (tg > 0) {
+#pragma unroll
+                for (int o = 0; o < BR; ++o) tps[tid * BR + o] = acc[o];
+            }
+            __syncthreads();
+            if (tg == 0) {
+                for (int gi = 1; gi < G; ++gi)
+#pragma unroll
+                    for (int o = 0; o < BR; ++o) acc[o] += tps[(gi * a.nvb + v) * BR + o];
+                epi(v, acc, xv);
+            }
+        } else {
+            for (int v = tid; v < a.nvb; v += NT) {
+                float xv[C], acc[BR];
+                ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // in flight during the taps
+                taps(halo_pos(a, v), 0, 27, acc);
+                epi(v, acc, xv);
+            }
         }
     }
 }
@@ -252,6 +280,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
     float *gs = t2h + a.hp * BR;          // [brick voxel][C]   g
     float *t3s = gs + a.nvb * C;          // [brick voxel][BR]  t3
     float *scr = t3s + a.nvb * BR;        // [S2][E2] W2 sub-stream sums
+    float *tps = scr + S2 * E2;           // [NT][BR] tap-group partials (bricks below NT voxels)
     __shared__ float w1s[BR * C], w3s[C * BR], g3s[C * BR];
     __shared__ float red2[4 * (2 * C * BR + kNScal)];
     const int tid = threadIdx.x;
@@ -320,16 +349,11 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
     for (int i = 0; i < C; ++i)
 #pragma unroll
         for (int j = 0; j < BR; ++j) acc1[i][j] = acc3[j][i] = 0.f;
-    for (int v = tid; v < a.nvb; v += NT) {
-        const int pos = halo_pos(a, v);
-        const int64_t vox = brick_vox(a, k, v);
-        float xv[C], gxv[C];
-        ldvec<TX, C>(x + vox * C, xv);  // in flight during the taps
-        float dt[BR];
+    auto taps = [&](int pos, int t0, int t1, float (&dt)[BR]) {
 #pragma unroll
         for (int c = 0; c < BR; ++c) dt[c] = 0.f;
 #pragma unroll 1
-        for (int tap = 0; tap < 27; ++tap) {
+        for (int tap = t0; tap < t1; ++tap) {
             const float *zr = gzh + (pos - tap_off(a, tap)) * BR;
             const float *wr = w2t + tap * BR * BR;
 #pragma unroll
@@ -339,6 +363,11 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
                 for (int c = 0; c < BR; ++c) dt[c] = fmaf(zv, wr[o * BR + c], dt[c]);
             }
         }
+    };
+    auto epi = [&](int v, const float (&dt)[BR], const float (&xv)[C]) {
+        const int pos = halo_pos(a, v);
+        const int64_t vox = brick_vox(a, k, v);
+        float gxv[C];
         float z1[BR], t3v[BR];
 #pragma unroll
         for (int c = 0; c < BR; ++c) {
@@ -366,6 +395,30 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
             }
         }
         stvec<TX, C>(gx + vox * C, gxv);
+    };
+    if (SMALL_TSPLIT && a.nvb < NT) {  // the 27 taps over NT / nvb thread groups, as the forward's
+        const int G = NT / a.nvb, v = tid & (a.nvb - 1), tg = tid / a.nvb;
+        float xv[C], dt[BR];
+        if (tg == 0) ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // in flight during the taps
+        taps(halo_pos(a, v), 27 * tg / G, 27 * (tg + 1) / G, dt);
+        if (tg > 0) {
+#pragma unroll
+            for (int c = 0; c < BR; ++c) tps[tid * BR + c] = dt[c];
+        }
+        __syncthreads();
+        if (tg == 0) {
+            for (int gi = 1; gi < G; ++gi)
+#pragma unroll
+                for (int c = 0; c < BR; ++c) dt[c] += tps[(gi * a.nvb + v) * BR + c];
+            epi(v, dt, xv);
+        }
+    } else {
+        for (int v = tid; v < a.nvb; v += NT) {
+            float xv[C], dt[BR];
+            ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // in flight during the taps
+            taps(halo_pos(a, v), 0, 27, dt);
+            epi(v, dt, xv);
+        }
     }
     const int nb = gridDim.x;
     // 3. W2 weight-gradient partial: thread (g9 = (kh, kw), sub) runs over D-lines of the brick,
@@ -615,7 +668,7 @@ int vq3d_preact_small_fwd_io(int32_t dtype, int32_t x_dtype, int32_t out_dtype, 
     if (!plan(batch, channels, branch, h, w, dd, a))
         return fail("preact_small_fwd: shape outside the fused few-channel block kernels");
     hipStream_t s = as_stream(stream);
-    const size_t lds = lds_fwd(a, branch);
+    const size_t lds = lds_fwd(a, branch) + size_t(NT) * branch * 4;  // + the tap-group partials
 #define F2(C_, B_, TX_, TO_)                                                                                   \
     {                                                                                                          \
         static bool attr = false;                                                                              \
@@ -700,7 +753,7 @@ int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t dtype, int32_t x_dty
     const int ne = n_entries(channels, branch) + kNScal;
     if (!workspace || ws_bytes < size_t(a.nbricks) * ne * 4) return fail("preact_small_bwd: workspace too small");
     hipStream_t s = as_stream(stream);
-    const size_t lds = lds_bwd(a, channels, branch);
+    const size_t lds = lds_bwd(a, channels, branch) + size_t(NT) * branch * 4;  // + the tap-group partials
     float *part = static_cast<float *>(workspace);
 #define B2(C_, B_, TX_, TO_)                                                                                   \
     {                                                                                                          \

@@ -242,6 +242,8 @@ def probe_col(dev, kind):
     from vq3d.flat import FlatParams
     c = {"4_2": 4, "8_4": 8, "2_1": 2}[kind.split("<")[-1]] if "<" in kind else 4
     shp = {4: (512, 512, 128), 8: (256, 256, 64), 2: (128, 128, 32)}[c]
+    if kind.startswith("k_small"):  # the brick kernels: (8, 4) at the 32x32x8 pre-quantize level
+        shp = (32, 32, 8)
     torch.manual_seed(5)
     blk = VL.PreActFixupResBlock(c, c, mode="same").to(dev)
     FlatParams(blk.parameters(), dev)
@@ -260,12 +262,13 @@ def probe_col(dev, kind):
     nv = shp[0] * shp[1] * shp[2]
     nb = c // 2
     fl = 2.0 * nv * (c * nb * 2 + nb * nb * 27)
-    if kind.startswith("k_col_fwd"):  # reads x c, writes out c + t2 nb + t3 nb
+    kn = kind.split("_")[1]
+    if kind.startswith(("k_col_fwd", "k_small_fwd")):  # reads x c, writes out c + t2 nb + t3 nb
         return (lambda: ops.preact_small_fwd(x, blk), nv * (2 * c + 2 * nb) * 2, fl,
-                f"k_col_fwd<{c},{nb}>: fused few-channel block forward @{shp[0]}x{shp[1]}x{shp[2]}")
+                f"k_{kn}_fwd<{c},{nb}>: fused few-channel block forward @{shp[0]}x{shp[1]}x{shp[2]}")
     # reads g c + x c + t2 nb + t3 nb, writes gx c (+ per-brick partial rows)
     return (lambda: ops.preact_small_bwd(gy, x, t2, t3, blk, grads), nv * (3 * c + 2 * nb) * 2, 2 * fl,
-            f"k_col_bwd<{c},{nb}>: fused few-channel block backward + reduction @{shp[0]}x{shp[1]}x{shp[2]}")
+            f"k_{kn}_bwd<{c},{nb}>: fused few-channel block backward + reduction @{shp[0]}x{shp[1]}x{shp[2]}")
 
 
 def probe_wgrad(dev, kind):
@@ -353,7 +356,7 @@ PROBES = {
     "k_pw_rows<4_4": probe_pw, "k_pw2<4": probe_pw,
     "k_wgrad_mfma<8_1_4": probe_wgrad,
     "k_col_bwd<4_2": probe_col, "k_col_fwd<4_2": probe_col, "k_col_bwd<8_4": probe_col, "k_col_fwd<8_4": probe_col,
-    "k_col_bwd<2_1": probe_col, "k_col_fwd<2_1": probe_col,
+    "k_col_bwd<2_1": probe_col, "k_col_fwd<2_1": probe_col, "k_small_bwd<8_4": probe_col, "k_small_fwd<8_4": probe_col,
     "k_pm_bwd2": probe_mid, "k_pm_w2grad": probe_mid, "k_pm_w13grad": probe_mid, "k_pm_fwd": probe_mid, "k_pm_bwd1": probe_mid, "k_pm_t2": probe_mid,
     "k_stackr_bwd": probe_stack, "k_stackr_fwd": probe_stack,
 }
