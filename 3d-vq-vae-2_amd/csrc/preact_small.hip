@@ -30,9 +30,31 @@ namespace {
 
 constexpr int NT = 256;           // threads per workgroup (both kernels)
 constexpr int kNScal = 8;         // scalar partials: b4, scale, b3b, b3a, b2b, b2a, b1b, b1a
+constexpr int RP = NT + 4;        // pitch (16-byte slots) of the backward's per-thread sums in LDS
 constexpr size_t kLdsTarget = 80 * 1024;
+#ifdef SMALL_PROBE  // phase clocks of k_small_bwd (tools/probes/small_probe.hip), held in registers
+__device__ unsigned long long g_small_probe[1024][12];  // and stored at the end (no stores in between)
+#define SPROBE_DECL unsigned long long sprobe_t[12] = {};
+#define SPROBE(k)                              \
+    __builtin_amdgcn_sched_barrier(0);         \
+    sprobe_t[k] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);
+#define SPROBE_DUMP                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                             \
+        for (int i_ = 0; i_ < 12; ++i_) g_small_probe[blockIdx.x][i_] = sprobe_t[i_];
+#else
+#define SPROBE_DECL
+#define SPROBE(k)
+#define SPROBE_DUMP
+#endif
 #ifndef SMALL_TSPLIT
 #define SMALL_TSPLIT 1  // bricks below NT voxels: the 27 taps over NT / nvb thread groups (0: one voxel per thread)
+#endif
+#ifndef SMALL_BPRE
+#define SMALL_BPRE 1  // backward prologue: 0 weights staged first, 1 + halo loads before, 2 + the voxel x too
+#endif
+#ifndef SMALL_TU
+#define SMALL_TU 1  // unroll of the per-voxel tap loops (timing experiments)
 #endif
 #ifndef SMALL_MINV
 #define SMALL_MINV 64  // smallest brick halved to for more workgroups (timing experiments: EXPDEF=SMALL_MINV)
@@ -47,7 +69,10 @@ struct SArgs {
 };
 
 constexpr int n_entries(int C, int BR) { return C * BR + 27 * BR * BR + BR * C; }
-constexpr int s2_of(int BR) { return BR >= 4 ? 14 : 28; }  // W2-gradient sub-streams (9 each)
+#ifndef SMALL_S2
+#define SMALL_S2 16  // W2-gradient sub-streams of the 4-branch backward (timing experiments; 14 before)
+#endif
+constexpr int s2_of(int BR) { return BR >= 4 ? SMALL_S2 : 28; }  // W2-gradient sub-streams (9 each)
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 __device__ __forceinline__ float rbf(float v) { return h2f_lo(uint32_t(f2h(v))); }
@@ -149,6 +174,37 @@ __device__ __forceinline__ Scal load_scal(const vq3d_preact_params &p) {
     return Scal{*p.bias1a, *p.bias1b, *p.bias2a, *p.bias2b, *p.bias3a, *p.bias3b, *p.scale, *p.bias4};
 }
 
+// A workgroup's weights staged through registers: loaded (clamped, unconditional) before the
+// kernel's first data loads, stored to LDS after them.  W2 goes to [tap][c][o] (forward) or
+// [tap][o][c] (backward, transposed), W1 / W3 in torch order.
+template <int C, int BR>
+struct WStage {
+    static constexpr int N2 = 27 * BR * BR, J2 = (N2 + NT - 1) / NT;
+    static_assert(BR * C <= NT, "one W1 / W3 element per thread");
+    float v2[J2], v1, v3;
+    __device__ __forceinline__ WStage(const float *__restrict__ w1, const float *__restrict__ w2,
+                                      const float *__restrict__ w3, int tid) {
+#pragma unroll
+        for (int j = 0; j < J2; ++j) v2[j] = w2[min(tid + j * NT, N2 - 1)];
+        v1 = w1[min(tid, BR * C - 1)];
+        v3 = w3[min(tid, BR * C - 1)];
+    }
+    __device__ __forceinline__ void store(float *w2s, float *w1s, float *w3s, int tid, bool transposed) const {
+#pragma unroll
+        for (int j = 0; j < J2; ++j) {
+            const int i = tid + j * NT;
+            if (i < N2) {
+                const int tap = i % 27, r = i / 27, c = r % BR, o = r / BR;
+                w2s[transposed ? (tap * BR + o) * BR + c : (tap * BR + c) * BR + o] = v2[j];
+            }
+        }
+        if (tid < BR * C) {
+            w1s[tid] = v1;
+            w3s[tid] = v3;
+        }
+    }
+};
+
 // ------------------------------------------------------------------------------------ forward
 // TX / TO: storage of the residual stream in / out (bf16 or fp32, as preact_col.hip)
 template <int C, int BR, typename TX, typename TO, int UA = (C <= 4 ? 8 : 4)>
@@ -162,41 +218,44 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
     float *tps = t2h + a.hp * BR;     // [NT][BR] tap-group partials (bricks below NT voxels)
     __shared__ float w1s[BR * C], w3s[C * BR];  // W1 [o][c], W3 [co][o] (torch order)
     const int tid = threadIdx.x;
-    for (int i = tid; i < 27 * BR * BR; i += NT) {
-        const int tap = i % 27, r = i / 27, c = r % BR, o = r / BR;
-        w2s[(tap * BR + c) * BR + o] = w2[i];
-    }
-    for (int i = tid; i < BR * C; i += NT) {
-        w1s[i] = w1[i];
-        w3s[i] = w3[i];
-    }
-    const Scal s = load_scal(p);
-    for (int brick = blockIdx.x; brick < a.nbricks; brick += gridDim.x) {
-        const Brick k = brick_of(a, brick);
-        __syncthreads();
-        // A. t2 on the halo (UA positions' x loads in flight per thread before any compute)
-        for (int q0 = tid; q0 < a.hp; q0 += UA * NT) {
-            int vi[UA];
-            int64_t vox[UA];
-            float xv[UA][C];
+    const Brick k = brick_of(a, blockIdx.x);  // one brick per workgroup (grid = nbricks)
+    // A. t2 on the halo, UA positions per thread.  The first batch's x loads are issued before the
+    // weight staging and its barrier (raw words, converted after): the two load latencies overlap.
+    int vi[UA];
+    int64_t vox[UA];
+    Raw<TX, C> xr[UA];
+    auto loadA = [&](int q0) {
 #pragma unroll
-            for (int u = 0; u < UA; ++u) {
-                const int q = q0 + u * NT;
-                vox[u] = halo_vox(a, k, q < a.hp ? q : q0, vi[u]);
-                ldvec<TX, C>(x + vox[u] * C, xv[u]);
-            }
+        for (int u = 0; u < UA; ++u) {
+            const int q = q0 + u * NT;
+            vox[u] = halo_vox(a, k, q < a.hp ? q : q0, vi[u]);
+            xr[u] = ldraw<TX, C>(x + vox[u] * C);
+        }
+    };
+    // weights first (registers), then the halo loads, then the weights' LDS stores: the stores wait
+    // for the weight loads only (loads complete in order); every load unconditional (clamped)
+    const WStage<C, BR> ws(w1, w2, w3, tid);
+    loadA(min(tid, a.hp - 1));
+    ws.store(w2s, w1s, w3s, tid, false);
+    const Scal s = load_scal(p);
+    __syncthreads();
+    {
+        for (int q0 = tid; q0 < a.hp; q0 += UA * NT) {
+            if (q0 != tid) loadA(q0);
 #pragma unroll
             for (int u = 0; u < UA; ++u) {
                 const int q = q0 + u * NT;
                 if (q >= a.hp) break;
+                float xv[C];
+                unraw<TX, C>(xr[u], xv);
 #pragma unroll
-                for (int c = 0; c < C; ++c) xv[u][c] = elu(xv[u][c] + s.b1a) + s.b1b;
+                for (int c = 0; c < C; ++c) xv[c] = elu(xv[c] + s.b1a) + s.b1b;
                 float t[BR];
 #pragma unroll
                 for (int o = 0; o < BR; ++o) {
                     float acc = 0.f;
 #pragma unroll
-                    for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], xv[u][c], acc);
+                    for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], xv[c], acc);
                     t[o] = rbf(elu(acc + s.b2a) + s.b2b);
                     t2h[q * BR + o] = t[o];
                 }
@@ -225,7 +284,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
         auto taps = [&](int pos, int t0, int t1, float (&acc)[BR]) {
 #pragma unroll
             for (int o = 0; o < BR; ++o) acc[o] = 0.f;
-#pragma unroll 1
+#pragma unroll SMALL_TU
             for (int tap = t0; tap < t1; ++tap) {
                 const float *tr = t2h + (pos + tap_off(a, tap)) * BR;
                 const float *wr = w2s + tap * BR * BR;
@@ -281,43 +340,56 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
     float *t3s = gs + a.nvb * C;          // [brick voxel][BR]  t3
     float *scr = t3s + a.nvb * BR;        // [S2][E2] W2 sub-stream sums
     float *tps = scr + S2 * E2;           // [NT][BR] tap-group partials (bricks below NT voxels)
+    float *rt = sm + ((tps + NT * BR - sm + 3) & ~3);  // [(2 C BR + 8) / 4][RP][4] per-thread W3 / W1 sums,
+                                                        // scalar partials (16-byte aligned)
     __shared__ float w1s[BR * C], w3s[C * BR], g3s[C * BR];
-    __shared__ float red2[4 * (2 * C * BR + kNScal)];
     const int tid = threadIdx.x;
-    for (int i = tid; i < 27 * BR * BR; i += NT) {
-        const int tap = i % 27, r = i / 27, c = r % BR, o = r / BR;
-        w2t[(tap * BR + o) * BR + c] = w2[i];
-    }
-    for (int i = tid; i < BR * C; i += NT) {
-        w1s[i] = w1[i];
-        w3s[i] = w3[i];
-    }
-    const Scal s = load_scal(p);
+    SPROBE_DECL
+    SPROBE(0)
     const Brick k = brick_of(a, blockIdx.x);
+    // phase 1's first UB positions (and, split taps, phase 2's voxel x) are loaded before the weight
+    // staging and its barrier as raw words: the load latencies overlap
+    int vis[UB];
+    Raw<TO, C> gr_[UB];
+    Raw<h16_t, BR> t3r[UB], t2r[UB];
+    auto load1 = [&](int q0) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {  // UB positions' loads in flight before any compute
+            const int q = q0 + u * NT;
+            const int64_t vox = halo_vox(a, k, q < a.hp ? q : q0, vis[u]);
+            gr_[u] = ldraw<TO, C>(g + vox * C);
+            t3r[u] = ldraw<h16_t, BR>(t3 + vox * BR);
+            t2r[u] = ldraw<h16_t, BR>(t2 + vox * BR);
+        }
+    };
+    const WStage<C, BR> ws(w1, w2, w3, tid);  // weights first: their LDS stores wait for them only
+    if (SMALL_BPRE == 0) {
+        ws.store(w2t, w1s, w3s, tid, true);
+        __syncthreads();
+    }
+    load1(min(tid, a.hp - 1));
+    const bool split = SMALL_TSPLIT && a.nvb < NT;
+    Raw<TX, C> xr2;
+    if (split && SMALL_BPRE >= 2) xr2 = ldraw<TX, C>(x + brick_vox(a, k, tid & (a.nvb - 1)) * C);
+    if (SMALL_BPRE != 0) ws.store(w2t, w1s, w3s, tid, true);
+    const Scal s = load_scal(p);
     float sp[kNScal];
 #pragma unroll
     for (int j = 0; j < kNScal; ++j) sp[j] = 0.f;
     __syncthreads();
+    SPROBE(1)
     // 1. gz3 and t2 on the halo; g and t3 of the interior
     for (int q0 = tid; q0 < a.hp; q0 += UB * NT) {
-      int vis[UB];
-      float gvs[UB][C], t3vs[UB][BR], t2vs[UB][BR];
-#pragma unroll
-      for (int u = 0; u < UB; ++u) {  // UB positions' loads in flight before any compute
-        const int q = q0 + u * NT;
-        const int64_t vox = halo_vox(a, k, q < a.hp ? q : q0, vis[u]);
-        ldvec<TO, C>(g + vox * C, gvs[u]);
-        ldv<BR>(t3 + vox * BR, t3vs[u]);
-        ldv<BR>(t2 + vox * BR, t2vs[u]);
-      }
+      if (q0 != tid) load1(q0);
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
         const int q = q0 + u * NT;
         if (q >= a.hp) break;
         const int vi = vis[u];
-        const float(&gv)[C] = gvs[u];
-        const float(&t3v)[BR] = t3vs[u];
-        const float(&t2v)[BR] = t2vs[u];
+        float gv[C], t3v[BR], t2v[BR];
+        unraw<TO, C>(gr_[u], gv);
+        unraw<h16_t, BR>(t3r[u], t3v);
+        unraw<h16_t, BR>(t2r[u], t2v);
 #pragma unroll
         for (int o = 0; o < BR; ++o) {
             float h = 0.f;
@@ -343,6 +415,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
       }
     }
     __syncthreads();
+    SPROBE(2)
     // 2. per voxel: dL/dt2 = W2^T (*) gz3, gz1, gx; W3 and W1 weight-gradient sums in registers
     float acc1[C][BR], acc3[BR][C];
 #pragma unroll
@@ -352,7 +425,7 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
     auto taps = [&](int pos, int t0, int t1, float (&dt)[BR]) {
 #pragma unroll
         for (int c = 0; c < BR; ++c) dt[c] = 0.f;
-#pragma unroll 1
+#pragma unroll SMALL_TU
         for (int tap = t0; tap < t1; ++tap) {
             const float *zr = gzh + (pos - tap_off(a, tap)) * BR;
             const float *wr = w2t + tap * BR * BR;
@@ -364,10 +437,8 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
             }
         }
     };
-    auto epi = [&](int v, const float (&dt)[BR], const float (&xv)[C]) {
+    auto epi = [&](int v, const float (&dt)[BR], const float (&xv)[C], float (&gxv)[C]) {
         const int pos = halo_pos(a, v);
-        const int64_t vox = brick_vox(a, k, v);
-        float gxv[C];
         float z1[BR], t3v[BR];
 #pragma unroll
         for (int c = 0; c < BR; ++c) {
@@ -394,33 +465,66 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
                 acc3[o][ci] = fmaf(z1[o], u, acc3[o][ci]);
             }
         }
-        stvec<TX, C>(gx + vox * C, gxv);
     };
-    if (SMALL_TSPLIT && a.nvb < NT) {  // the 27 taps over NT / nvb thread groups, as the forward's
+    // the split path's gx goes out after the sums' LDS stores (4a): stores pending behind them
+    // would make the compiler wait for their completion first
+    float gxs[C];
+    if (split) {  // the 27 taps over NT / nvb thread groups, as the forward's
         const int G = NT / a.nvb, v = tid & (a.nvb - 1), tg = tid / a.nvb;
         float xv[C], dt[BR];
-        if (tg == 0) ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // in flight during the taps
+        if (SMALL_BPRE >= 2) unraw<TX, C>(xr2, xv);
+        else ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // every thread (exact wait counts)
         taps(halo_pos(a, v), 27 * tg / G, 27 * (tg + 1) / G, dt);
         if (tg > 0) {
 #pragma unroll
             for (int c = 0; c < BR; ++c) tps[tid * BR + c] = dt[c];
         }
+        SPROBE(8)
         __syncthreads();
+        SPROBE(9)
         if (tg == 0) {
             for (int gi = 1; gi < G; ++gi)
 #pragma unroll
                 for (int c = 0; c < BR; ++c) dt[c] += tps[(gi * a.nvb + v) * BR + c];
-            epi(v, dt, xv);
+            epi(v, dt, xv, gxs);
         }
     } else {
         for (int v = tid; v < a.nvb; v += NT) {
-            float xv[C], dt[BR];
+            float xv[C], dt[BR], gxv[C];
             ldvec<TX, C>(x + brick_vox(a, k, v) * C, xv);  // in flight during the taps
             taps(halo_pos(a, v), 0, 27, dt);
-            epi(v, dt, xv);
+            epi(v, dt, xv, gxv);
+            stvec<TX, C>(gx + brick_vox(a, k, v) * C, gxv);
         }
     }
+    SPROBE(3)
     const int nb = gridDim.x;
+    // 4a. the W3 / W1 sums and scalar partials into LDS in groups of 4 values, [group][thread][4]
+    //     (one 16-byte store per group).  Group 16 (the phase-1 scalars) comes from every thread;
+    //     the rest only from the phase-2 voxel threads (split taps: the first nvb threads).
+    constexpr int NR2 = 2 * C * BR + kNScal, NG = NR2 / 4;
+    static_assert(NR2 % 4 == 0 && (2 * C * BR) % 4 == 0, "groups of 4");
+    const int nsrc = split ? a.nvb : NT;
+    {
+        float vals[NR2];
+#pragma unroll
+        for (int i = 0; i < C; ++i)
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                vals[i * BR + j] = acc1[i][j];
+                vals[E1 + j * C + i] = acc3[j][i];
+            }
+#pragma unroll
+        for (int j = 0; j < kNScal; ++j) vals[2 * E1 + j] = sp[j];
+        const bool vox = tid < nsrc;
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi)
+            if (gi == NG - 2 || vox)
+                *reinterpret_cast<float4 *>(rt + (gi * RP + tid) * 4) =
+                    make_float4(vals[4 * gi], vals[4 * gi + 1], vals[4 * gi + 2], vals[4 * gi + 3]);
+    }
+    if (split && tid < a.nvb) stvec<TX, C>(gx + brick_vox(a, k, tid) * C, gxs);
+    SPROBE(10)
     // 3. W2 weight-gradient partial: thread (g9 = (kh, kw), sub) runs over D-lines of the brick,
     //    3 kd taps x BR x BR sums in registers; the S2 sub-streams summed in a fixed order
     {
@@ -439,19 +543,30 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
                 const int lh = r / a.bw, lw = r - lh * a.bw;
                 const int base = ((lh + 1) * a.hw + lw + 1) * a.hd + 1;         // voxel j = 0
                 const int tb = base + ((kh - 1) * a.hw + kw - 1) * a.hd - 1;    // its kd = 0 tap
+                // a sliding window of the line's t2 rows: row j + 2 is the one new row per voxel
+                float tw[3][BR];
+#pragma unroll
+                for (int c = 0; c < BR; ++c) {
+                    tw[0][c] = t2h[tb * BR + c];
+                    tw[1][c] = t2h[(tb + 1) * BR + c];
+                }
+#pragma unroll 2
                 for (int j = 0; j < a.bd; ++j) {
                     float gz[BR];
 #pragma unroll
                     for (int o = 0; o < BR; ++o) gz[o] = gzh[(base + j) * BR + o];
 #pragma unroll
-                    for (int kd = 0; kd < 3; ++kd) {
-                        float tv[BR];
+                    for (int c = 0; c < BR; ++c) tw[2][c] = t2h[(tb + j + 2) * BR + c];
 #pragma unroll
-                        for (int c = 0; c < BR; ++c) tv[c] = t2h[(tb + j + kd) * BR + c];
+                    for (int kd = 0; kd < 3; ++kd)
 #pragma unroll
                         for (int o = 0; o < BR; ++o)
 #pragma unroll
-                            for (int c = 0; c < BR; ++c) acc2[kd][o][c] = fmaf(gz[o], tv[c], acc2[kd][o][c]);
+                            for (int c = 0; c < BR; ++c) acc2[kd][o][c] = fmaf(gz[o], tw[kd][c], acc2[kd][o][c]);
+#pragma unroll
+                    for (int c = 0; c < BR; ++c) {
+                        tw[0][c] = tw[1][c];
+                        tw[1][c] = tw[2][c];
                     }
                 }
             }
@@ -463,50 +578,53 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
                     for (int c = 0; c < BR; ++c) scr[sub * E2 + ((g9 * 3 + kd) * BR + o) * BR + c] = acc2[kd][o][c];
         }
         __syncthreads();
+        SPROBE(4)
         for (int e = tid; e < E2; e += NT) {
             float t = 0.f;
             for (int j = 0; j < S2; ++j) t += scr[j * E2 + e];
             part[int64_t(E1 + e) * nb + blockIdx.x] = t;
         }
     }
-    // 4. W3 / W1 sums and the scalar partials: wave trees, then the 4 waves in order
-    constexpr int NR2 = 2 * C * BR + kNScal;
-    {
-        float vals[NR2];
-#pragma unroll
-        for (int i = 0; i < C; ++i)
-#pragma unroll
-            for (int j = 0; j < BR; ++j) {
-                vals[i * BR + j] = acc1[i][j];
-                vals[E1 + j * C + i] = acc3[j][i];
+    // 4b. a row of 16 threads per group: thread q of the row sums the group's words of threads
+    //     16 i + q (16-byte reads; RP = 4 mod 8 spreads a half-wave's 8 group rows over the banks),
+    //     then the row on the DPP network.  A fixed order: deterministic.
+    for (int g0 = 0; g0 < NG; g0 += NT / 16) {
+        const int gi = g0 + (tid >> 4), q = tid & 15;
+        if (gi < NG) {
+            const int cnt = gi == NG - 2 ? NT : nsrc;
+            float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int i = q; i < cnt; i += 16) {
+                const float4 v = *reinterpret_cast<const float4 *>(rt + (gi * RP + i) * 4);
+                t.x += v.x;
+                t.y += v.y;
+                t.z += v.z;
+                t.w += v.w;
             }
-#pragma unroll
-        for (int j = 0; j < kNScal; ++j) vals[2 * E1 + j] = sp[j];
-        const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-        for (int n = 0; n < NR2; ++n) {
-            const float t = wave_sum(vals[n]);
-            if (lane == 0) red2[wv * NR2 + n] = t;
+            const float tv[4] = {group_sum<16>(t.x), group_sum<16>(t.y), group_sum<16>(t.z), group_sum<16>(t.w)};
+            if (q < 4) {
+                const int n = 4 * gi + q;
+                const float r = tv[q];
+                if (n < E1) {
+                    part[int64_t(n) * nb + blockIdx.x] = r;
+                    g3s[n] = r;
+                } else if (n < 2 * E1) {
+                    part[int64_t(E1 + E2 + n - E1) * nb + blockIdx.x] = r;
+                } else if (n != 2 * E1 + 1) {
+                    part[int64_t(E + n - 2 * E1) * nb + blockIdx.x] = r;
+                }
+            }
         }
     }
+    SPROBE(5)
     __syncthreads();
-    for (int n = tid; n < NR2; n += NT) {
-        const float t = red2[n] + red2[NR2 + n] + red2[2 * NR2 + n] + red2[3 * NR2 + n];
-        if (n < E1) {
-            part[int64_t(n) * nb + blockIdx.x] = t;
-            g3s[n] = t;
-        } else if (n < 2 * E1) {
-            part[int64_t(E1 + E2 + n - E1) * nb + blockIdx.x] = t;
-        } else if (n != 2 * E1 + 1) {
-            part[int64_t(E + n - 2 * E1) * nb + blockIdx.x] = t;
-        }
-    }
-    __syncthreads();
+    SPROBE(6)
     if (tid == 0) {  // dscale partial: sum W3 o (sum_v g t3)
         float psc = 0.f;
         for (int n = 0; n < E1; ++n) psc = fmaf(w3s[n], g3s[n], psc);
         part[int64_t(E + 1) * nb + blockIdx.x] = psc;
     }
+    SPROBE(7)
+    SPROBE_DUMP
 }
 
 // sum of one gradient entry's per-brick partials (fixed order), added to its gradient
@@ -558,6 +676,10 @@ size_t lds_fwd(const SArgs &a, int BR) { return (size_t(27) * BR * BR + size_t(a
 size_t lds_bwd(const SArgs &a, int C, int BR) {
     return (size_t(27) * BR * BR * (1 + s2_of(BR)) + 2 * size_t(a.hp) * BR + size_t(a.nvb) * (C + BR)) * 4;
 }
+// what the backward launches with: + the tap-group partials and the per-thread sums
+size_t lds_bwd_launch(const SArgs &a, int C, int BR) {
+    return lds_bwd(a, C, BR) + (size_t(NT) * BR + 3 + size_t(2 * C * BR + kNScal) * RP) * 4;
+}
 
 int ilog2(int v) {
     int r = 0;
@@ -593,7 +715,8 @@ bool plan(int batch, int C, int BR, int h, int w, int d, SArgs &a) {
         a.nbricks = batch * a.nbh * a.nbw * a.nbd;
     };
     set(std::min(h, 8), std::min(w, 8), std::min(d, 16));
-    while (lds_bwd(a, C, BR) > kLdsTarget || (a.nbricks < 256 && a.nvb > SMALL_MINV)) {
+    while (lds_bwd(a, C, BR) > kLdsTarget || lds_bwd_launch(a, C, BR) > 159 * 1024 ||
+           (a.nbricks < 256 && a.nvb > SMALL_MINV)) {
         if (a.bd >= a.bh && a.bd >= a.bw && a.bd > 1) set(a.bh, a.bw, a.bd / 2);
         else if (a.bh >= a.bw && a.bh > 1) set(a.bh / 2, a.bw, a.bd);
         else if (a.bw > 1) set(a.bh, a.bw / 2, a.bd);
@@ -753,7 +876,7 @@ int vq3d_preact_small_bwd_stages_io(int32_t stages, int32_t dtype, int32_t x_dty
     const int ne = n_entries(channels, branch) + kNScal;
     if (!workspace || ws_bytes < size_t(a.nbricks) * ne * 4) return fail("preact_small_bwd: workspace too small");
     hipStream_t s = as_stream(stream);
-    const size_t lds = lds_bwd(a, channels, branch) + size_t(NT) * branch * 4;  // + the tap-group partials
+    const size_t lds = lds_bwd_launch(a, channels, branch);
     float *part = static_cast<float *>(workspace);
 #define B2(C_, B_, TX_, TO_)                                                                                   \
     {                                                                                                          \
