@@ -49,6 +49,24 @@
 #ifndef COL_SWEIGHTS
 #define COL_SWEIGHTS 1  // the backward's W1 / W3 held in SGPRs (0: plain loads, for A/B timing)
 #endif
+#ifdef COL_PROBE  // phase clocks of k_col_bwd's first brick per workgroup (tools/probes/col_probe.hip)
+__device__ unsigned long long g_col_probe[4096][8];
+#define CPROBE_DECL unsigned long long cprobe_t[8] = {};
+#define CPROBE(k)                              \
+    __builtin_amdgcn_sched_barrier(0);         \
+    if (cprobe_t[k] == 0) cprobe_t[k] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);
+#define CPROBE_DUMP                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                             \
+        for (int i_ = 0; i_ < 8; ++i_) g_col_probe[blockIdx.x][i_] = cprobe_t[i_];
+#else
+#define CPROBE_DECL
+#define CPROBE(k)
+#define CPROBE_DUMP
+#endif
+#ifndef COL_VSTENCIL
+#define COL_VSTENCIL 1  // (2, 1) backward: phase B as VALU stencils + an LDS-grouped reduction (0: MFMA, A/B)
+#endif
 #ifndef COL_PAIRS
 #define COL_PAIRS 1  // the backward's halo phase on position pairs (0: one position per item, A/B)
 #endif
@@ -74,6 +92,7 @@ constexpr int TP = COL_TP;    // channel-major halo line pitch (positions 0..17,
 constexpr int ZP = NV + 16;   // channel-major interior pitch
 constexpr int PADE = 32;      // zero tail of the position-major halo buffers
 constexpr int NSC = 8;        // scalar partials: b4, b3b, b3a, scale, b2b, b2a, b1b, b1a
+constexpr int RPC = NT + 4;   // pitch (16-byte slots) of the (2, 1) backward's grouped partial row
 // raw k^3 sums [voxel][B] fp32 with one pad float per brick line (16 voxels), so the per-thread
 // epilogue reads of 16 lines do not share a bank
 __host__ __device__ constexpr int acc_at(int v, int BR_) { return v * BR_ + v / BD; }
@@ -485,8 +504,11 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
     float *wred = reinterpret_cast<float *>(smem);        // after phase C: [4][NTN][64][4] over z3h / t2T
     static_assert(size_t(HVX * BR + PADE + BR * NLN * TP) * 2 >= size_t(4 * K::NTN * 256) * 4, "W2 sums fit z3h + t2T");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kb = lane >> 4, row = lane & 15;
+    CPROBE_DECL
+    CPROBE(0)
     const Scal s = load_scal(p);
     const SWeights<C * BR> w3s(w3), w1s(w1);
+    const SWeights<(BR == 1 && COL_VSTENCIL) ? 27 : 1> w2s(w2);
     hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, true>(w2, k, lane);
@@ -503,6 +525,12 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
     for (int oo = 0; oo < BR; ++oo)
 #pragma unroll
         for (int c = 0; c < C; ++c) g3[oo][c] = dw1[oo][c] = 0.f;
+    // one branch channel (BR = 1): phase B runs as VALU stencils over the thread's own 4 voxels
+    // (no MFMA: a single W2 row / column would use 1 / 16 of each), the W2 sums in 27 registers
+    constexpr bool VS = BR == 1 && COL_VSTENCIL;
+    float dw2[VS ? 27 : 1];
+#pragma unroll
+    for (int i = 0; i < (VS ? 27 : 1); ++i) dw2[i] = 0.f;
     f32x4 aw[K::NTN];
     int toff[K::NTN];
 #pragma unroll
@@ -522,6 +550,7 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         __syncthreads();  // the previous brick's readers of the LDS tiles are done
         line_table(a, o, lbase);
         __syncthreads();
+        CPROBE(1)
         // A. gz3 on the halo; t2 on the halo (channel-major); interior sums and G3 = sum t3 (x) g.
 #if COL_PAIRS
         // Work items are PAIRS of consecutive positions of a halo line (PL is even): one line /
@@ -658,10 +687,48 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         }
 #endif
         __syncthreads();
+        CPROBE(2)
         // the thread's 4 voxels (phase C): g and x in flight during phase B
         const int ln = tid / (BD / DV), dg = tid % (BD / DV);
         const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
         constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
+        float raw1[DV];  // VS: the thread's raw W2^T (*) gz3
+        if constexpr (VS) {
+            // B (BR = 1). Voxel d of the thread's line takes positions d .. d + 2 of the 9 neighbour
+            // lines: one aligned 6-position run (3 dwords) of gz3 and of t2 per line for all 4 voxels.
+            const int lh = ln >> 3, lw = ln & 7, d0 = dg * DV;
+            float wr[27];  // the flipped taps as the 16-bit operands the MFMA path rounds them to
+#pragma unroll
+            for (int t = 0; t < 27; ++t) wr[t] = rbf(w2s[26 - t]);
+            const uint2 zq = *reinterpret_cast<const uint2 *>(z3T + ln * BD + d0);  // the 4 voxels' gz3
+            const float gz[DV] = {bf(zq.x & 0xffffu), bf(zq.x >> 16), bf(zq.y & 0xffffu), bf(zq.y >> 16)};
+#pragma unroll
+            for (int i = 0; i < DV; ++i) raw1[i] = 0.f;
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {
+                const int L = (lh + r / 3) * WL + lw + r % 3;
+                const uint32_t *zp = reinterpret_cast<const uint32_t *>(z3h + L * PL + d0);
+                const uint32_t *tp = reinterpret_cast<const uint32_t *>(t2T + L * TP + d0);
+                float zz[DV + 2], tt[DV + 2];
+#pragma unroll
+                for (int k = 0; k < (DV + 2) / 2; ++k) {
+                    const uint32_t zw = zp[k], tw = tp[k];
+                    zz[2 * k] = bf(zw & 0xffffu);
+                    zz[2 * k + 1] = bf(zw >> 16);
+                    tt[2 * k] = bf(tw & 0xffffu);
+                    tt[2 * k + 1] = bf(tw >> 16);
+                }
+#pragma unroll
+                for (int kd = 0; kd < 3; ++kd) {
+                    const float wf = wr[3 * r + kd];
+#pragma unroll
+                    for (int i = 0; i < DV; ++i) {
+                        raw1[i] = fmaf(wf, zz[i + kd], raw1[i]);
+                        dw2[3 * r + kd] = fmaf(gz[i], tt[i + kd], dw2[3 * r + kd]);
+                    }
+                }
+            }
+        } else {
         // B1. raw W2^T (*) gz3 per m-tile (flipped taps; fixed trip count, unrolled as the forward's)
 #pragma unroll COL_UNROLL_B
         for (int i = 0; i < NMT / (NT / 64); ++i) {
@@ -686,7 +753,9 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
 #pragma unroll
             for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
         }
-        __syncthreads();
+        }
+        if constexpr (!VS) __syncthreads();  // accs complete (VS: phase C reads registers and phase-A LDS)
+        CPROBE(3)
         // C. gz1, gx, W1 gradient, b2 / b1 sums over the thread's 4 voxels
         const int v0 = ln * BD + dg * DV;
         // 8-element pieces of the thread's 4 voxels' x / g (PV voxels each), the next piece's loads in
@@ -714,7 +783,9 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                 float z1[BR];
 #pragma unroll
                 for (int oo = 0; oo < BR; ++oo) {
-                    const float gt2 = accs[acc_at(v0 + i, BR) + oo];
+                    float gt2;
+                    if constexpr (VS) gt2 = raw1[i];
+                    else gt2 = accs[acc_at(v0 + i, BR) + oo];
                     const float t2v = bf(t2T[(oo * NLN + hl0) * TP + dg * DV + i + 1]);
                     const float zz = gt2 * elu_d_act(t2v, s.b2b);
                     s2b += gt2;
@@ -742,43 +813,91 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
             gq = gn;
         }
     }  // bricks
-    // partial row of this brick: per-wave shuffle sums, then the 4 waves in order
-    {
-        auto put = [&](int e, float v) {
-            const float t = wave_sum(v);
-            if (lane == 0) red[wave * NE + e] = t;
-        };
+    CPROBE(4)
+    if constexpr (VS) {
+        // every entry of the partial row, in row order, to LDS as groups of 4 ([group][RPC][4] over
+        // the dead tiles; one 16-byte store per group), then a row of 16 threads per group sums its
+        // NT slots and reduces on the DPP network: 10 short chains instead of 39 wave-wide DPP trees
+        constexpr int NG = (NE + 3) / 4;
+        float vals[NG * 4];
 #pragma unroll
-        for (int oo = 0; oo < BR; ++oo)
+        for (int c = 0; c < C; ++c) {
+            vals[c] = g3[0][c];
+            vals[C + 27 + c] = dw1[0][c];
+        }
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                put(oo * C + c, g3[oo][c]);
-                put(BR * C + 27 * BR * BR + oo * C + c, dw1[oo][c]);
-            }
+        for (int i = 0; i < 27; ++i) vals[C + i] = dw2[i];
         const float sc8[NSC] = {s4, s3b, s3a, ssc, s2b, s2a, s1b, s1a};
 #pragma unroll
-        for (int k = 0; k < NSC; ++k) put(2 * BR * C + 27 * BR * BR + k, sc8[k]);
-    }
-    __syncthreads();  // every wave is past phase C (t2T) before the W2 sums go over it
-    // W2 accumulators: D rows 4 kb + j = co, columns 16 n + row = col
+        for (int k = 0; k < NSC; ++k) vals[2 * C + 27 + k] = sc8[k];
 #pragma unroll
-    for (int n = 0; n < K::NTN; ++n)
+        for (int i = NE; i < NG * 4; ++i) vals[i] = 0.f;
+        float4 *grp = reinterpret_cast<float4 *>(smem);
+        __syncthreads();  // every wave is past phase C (the LDS tiles are dead)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wred[((wave * K::NTN + n) * 64 + lane) * 4 + j] = aw[n][j];
-    __syncthreads();
-    for (int e = tid; e < NE; e += NT) {
-        float t = 0.f;
-        if (e >= BR * C && e < BR * C + 27 * BR * BR) {
-            const int r2 = e - BR * C, co = r2 / (27 * BR), col = r2 - co * 27 * BR;
-            const int n = col >> 4, l = 16 * (co >> 2) + (col & 15), j = co & 3;
+        for (int gi = 0; gi < NG; ++gi)
+            grp[gi * RPC + tid] = make_float4(vals[4 * gi], vals[4 * gi + 1], vals[4 * gi + 2], vals[4 * gi + 3]);
+        __syncthreads();
+        CPROBE(4)
+        CPROBE(5)
+        for (int g0 = 0; g0 < NG; g0 += NT / 16) {
+            const int gi = g0 + (tid >> 4), q = tid & 15;
+            if (gi < NG) {
+                float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-            for (int w = 0; w < NT / 64; ++w) t += wred[((w * K::NTN + n) * 64 + l) * 4 + j];
-        } else {
-#pragma unroll
-            for (int w = 0; w < NT / 64; ++w) t += red[w * NE + e];
+                for (int i = q; i < NT; i += 16) {
+                    const float4 v = grp[gi * RPC + i];
+                    t.x += v.x;
+                    t.y += v.y;
+                    t.z += v.z;
+                    t.w += v.w;
+                }
+                const float tv[4] = {group_sum<16>(t.x), group_sum<16>(t.y), group_sum<16>(t.z), group_sum<16>(t.w)};
+                if (q < 4 && 4 * gi + q < NE) part[int64_t(blockIdx.x) * NE + 4 * gi + q] = tv[q];
+            }
         }
-        part[int64_t(blockIdx.x) * NE + e] = t;  // the workgroup's row: one contiguous write
+    } else {
+        // partial row of this brick: per-wave shuffle sums, then the 4 waves in order
+        {
+            auto put = [&](int e, float v) {
+                const float t = wave_sum(v);
+                if (lane == 0) red[wave * NE + e] = t;
+            };
+#pragma unroll
+            for (int oo = 0; oo < BR; ++oo)
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    put(oo * C + c, g3[oo][c]);
+                    put(BR * C + 27 * BR * BR + oo * C + c, dw1[oo][c]);
+                }
+            const float sc8[NSC] = {s4, s3b, s3a, ssc, s2b, s2a, s1b, s1a};
+#pragma unroll
+            for (int k = 0; k < NSC; ++k) put(2 * BR * C + 27 * BR * BR + k, sc8[k]);
+        }
+        CPROBE(5)
+        __syncthreads();  // every wave is past phase C (t2T) before the W2 sums go over it
+        // W2 accumulators: D rows 4 kb + j = co, columns 16 n + row = col
+#pragma unroll
+        for (int n = 0; n < K::NTN; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wred[((wave * K::NTN + n) * 64 + lane) * 4 + j] = aw[n][j];
+        __syncthreads();
+        for (int e = tid; e < NE; e += NT) {
+            float t = 0.f;
+            if (e >= BR * C && e < BR * C + 27 * BR * BR) {
+                const int r2 = e - BR * C, co = r2 / (27 * BR), col = r2 - co * 27 * BR;
+                const int n = col >> 4, l = 16 * (co >> 2) + (col & 15), j = co & 3;
+#pragma unroll
+                for (int w = 0; w < NT / 64; ++w) t += wred[((w * K::NTN + n) * 64 + l) * 4 + j];
+            } else {
+#pragma unroll
+                for (int w = 0; w < NT / 64; ++w) t += red[w * NE + e];
+            }
+            part[int64_t(blockIdx.x) * NE + e] = t;  // the workgroup's row: one contiguous write
+        }
     }
+    CPROBE(6)
+    CPROBE_DUMP
 }
 
 // Fixed-order sum of the partial rows [row][NE]: stage 1, workgroup r sums rows
@@ -852,8 +971,11 @@ constexpr size_t fwd_lds() {
 }
 template <int C, int BR>
 constexpr size_t bwd_lds() {
-    return size_t(HVX * BR + PADE + BR * NLN * TP + BR * ZP) * 2 + size_t(acc_floats(BR)) * 4 + NLN * 4 +
-           size_t(4 * n_entries<C, BR>()) * 4;
+    const size_t tiles = size_t(HVX * BR + PADE + BR * NLN * TP + BR * ZP) * 2 + size_t(acc_floats(BR)) * 4 +
+                         NLN * 4 + size_t(4 * n_entries<C, BR>()) * 4;
+    if (BR == 1 && COL_VSTENCIL)  // + room for the grouped partial-row reduction over the tiles
+        return std::max(tiles, size_t((n_entries<C, BR>() + 3) / 4) * RPC * 16);
+    return tiles;
 }
 
 // persistent backward: max(512, bricks / 16) workgroups (a multiple of 8: XCD-contiguous ranges),
