@@ -355,6 +355,9 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
     const Scal s = load_scal(p);
     Scal sn{};
     if constexpr ((CH & 2) != 0) sn = load_scal(pn);
+    // one branch channel (BR = 1): phase B as a VALU stencil over the thread's own 4 voxels
+    constexpr bool VS = BR == 1 && COL_VSTENCIL;
+    const SWeights<VS ? 27 : 1> w2s(w2);
     hx8 fw[K::KS];
 #pragma unroll
     for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, false>(w2, k, lane);
@@ -410,21 +413,49 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
         const int ln = tid / (BD / DV), dg = tid % (BD / DV);
         const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
         const Raw<TX, DV * C> xr = ldraw<TX, DV * C>(x + vox0 * C);
-        // B. raw W2 (*) t2 per m-tile (a fixed trip count, unrolled: the next m-tiles' window reads
-        // are in flight during this one's MFMA chain)
+        float raw1[DV];  // VS: the thread's raw W2 (*) t2
+        if constexpr (VS) {
+            // B (BR = 1): voxel d takes positions d .. d + 2 of the 9 neighbour lines, one aligned
+            // 6-position run (3 dwords) per line for the thread's 4 voxels; the taps rounded to the
+            // 16-bit operands of the MFMA path
+            const int lh = ln >> 3, lw = ln & 7, d0 = dg * DV;
+            float wr[27];
+#pragma unroll
+            for (int t = 0; t < 27; ++t) wr[t] = rbf(w2s[t]);
+#pragma unroll
+            for (int i = 0; i < DV; ++i) raw1[i] = 0.f;
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {
+                const uint32_t *tp = reinterpret_cast<const uint32_t *>(t2h + ((lh + r / 3) * WL + lw + r % 3) * PL + d0);
+                float tt[DV + 2];
+#pragma unroll
+                for (int k = 0; k < (DV + 2) / 2; ++k) {
+                    const uint32_t tw = tp[k];
+                    tt[2 * k] = bf(tw & 0xffffu);
+                    tt[2 * k + 1] = bf(tw >> 16);
+                }
+#pragma unroll
+                for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+                    for (int i = 0; i < DV; ++i) raw1[i] = fmaf(wr[3 * r + kd], tt[i + kd], raw1[i]);
+            }
+        } else {
+            // B. raw W2 (*) t2 per m-tile (a fixed trip count, unrolled: the next m-tiles' window reads
+            // are in flight during this one's MFMA chain)
 #pragma unroll COL_UNROLL_F
-        for (int i = 0; i < NMT / (NT / 64); ++i) {
-            const int mt = wave + i * (NT / 64);
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            const int wb = win_base(mt, BR);
+            for (int i = 0; i < NMT / (NT / 64); ++i) {
+                const int mt = wave + i * (NT / 64);
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                const int wb = win_base(mt, BR);
 #pragma unroll
-            for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, wb + woff[k]), fw[k], acc);
-            if (row < BR) {
+                for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(t2h, wb + woff[k]), fw[k], acc);
+                if (row < BR) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+                    for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+                }
             }
         }
-        __syncthreads();
+        if constexpr (!VS) __syncthreads();  // accs complete
         // C. t3 and out of the thread's 4 voxels (and their t2, saved for the backward)
         const int v0 = ln * BD + dg * DV;
         if (t2o && (CH & 1) == 0) {  // chained: this block's t2 is already in memory
@@ -443,7 +474,8 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
 #pragma unroll
         for (int i = 0; i < DV; ++i)
 #pragma unroll
-            for (int oo = 0; oo < BR; ++oo) t3v[i][oo] = rbf(elu_f(accs[acc_at(v0 + i, BR) + oo] + s.b3a) + s.b3b);
+            for (int oo = 0; oo < BR; ++oo)
+                t3v[i][oo] = rbf(elu_f((VS ? raw1[i] : accs[acc_at(v0 + i, BR) + oo]) + s.b3a) + s.b3b);
         {
             uint32_t w[DV * BR / 2];
 #pragma unroll
@@ -692,6 +724,16 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         const int ln = tid / (BD / DV), dg = tid % (BD / DV);
         const int64_t vox0 = int64_t(lbase[((ln >> 3) + 1) * WL + (ln & 7) + 1]) + dg * DV;
         constexpr int NXB = DV * C / 8;  // 8-element pieces of the thread's 4 voxels
+        // phase C's first x / g piece: VS issues it before the stencils, the MFMA path after phase B
+        // (registers: occupancy)
+        const TX *xp = x + vox0 * C;
+        const TO *gp = g + vox0 * C;
+        Raw<TX, 8> xq;
+        Raw<TO, 8> gq;
+        if constexpr (VS) {
+            xq = ldraw<TX, 8>(xp);
+            gq = ldraw<TO, 8>(gp);
+        }
         float raw1[DV];  // VS: the thread's raw W2^T (*) gz3
         if constexpr (VS) {
             // B (BR = 1). Voxel d of the thread's line takes positions d .. d + 2 of the 9 neighbour
@@ -729,30 +771,30 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
                 }
             }
         } else {
-        // B1. raw W2^T (*) gz3 per m-tile (flipped taps; fixed trip count, unrolled as the forward's)
+            // B1. raw W2^T (*) gz3 per m-tile (flipped taps; fixed trip count, unrolled as the forward's)
 #pragma unroll COL_UNROLL_B
-        for (int i = 0; i < NMT / (NT / 64); ++i) {
-            const int mt = wave + i * (NT / 64);
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            const int wb = win_base(mt, BR);
+            for (int i = 0; i < NMT / (NT / 64); ++i) {
+                const int mt = wave + i * (NT / 64);
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                const int wb = win_base(mt, BR);
 #pragma unroll
-            for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, wb + woff[k]), fw[k], acc);
-            if (row < BR) {
+                for (int k = 0; k < K::KS; ++k) acc = mfma(win_frag<BR>(z3h, wb + woff[k]), fw[k], acc);
+                if (row < BR) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+                    for (int j = 0; j < 4; ++j) accs[acc_at(16 * mt + 4 * kb + j, BR) + row] = acc[j];
+                }
             }
-        }
-        // B2. W2 gradient: D[co][col] += sum_v gz3[v][co] * t2win[v][col], col = r * 3B + kd * B + ci;
-        // wave w takes the 32-voxel k-steps 8 w .. 8 w + 7 (two brick lines each; lane kb: line
-        // 2 ks + kb / 2, d = 8 (kb & 1) + j)
+            // B2. W2 gradient: D[co][col] += sum_v gz3[v][co] * t2win[v][col], col = r * 3B + kd * B + ci;
+            // wave w takes the 32-voxel k-steps 8 w .. 8 w + 7 (two brick lines each; lane kb: line
+            // 2 ks + kb / 2, d = 8 (kb & 1) + j)
 #pragma unroll 2
-        for (int ks = 8 * wave; ks < 8 * wave + 8; ++ks) {
-            // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
-            const hx8 af = *reinterpret_cast<const hx8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
-            const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
+            for (int ks = 8 * wave; ks < 8 * wave + 8; ++ks) {
+                // rows >= B of the A operand only feed discarded D rows: read row B - 1 again
+                const hx8 af = *reinterpret_cast<const hx8 *>(z3T + min(row, BR - 1) * ZP + 32 * ks + 8 * kb);
+                const int lk = 2 * ks + (kb >> 1), lo = ((lk >> 3) * WL + (lk & 7)) * TP;
 #pragma unroll
-            for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
-        }
+                for (int n = 0; n < K::NTN; ++n) aw[n] = mfma(af, read8(t2T, toff[n] + lo), aw[n]);
+            }
         }
         if constexpr (!VS) __syncthreads();  // accs complete (VS: phase C reads registers and phase-A LDS)
         CPROBE(3)
@@ -762,10 +804,10 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         // flight during the current one's math (one piece of registers at a time: occupancy)
         constexpr int PV = 8 / C;
         const int hl0 = ((ln >> 3) + 1) * WL + (ln & 7) + 1;
-        const TX *xp = x + vox0 * C;
-        const TO *gp = g + vox0 * C;
-        Raw<TX, 8> xq = ldraw<TX, 8>(xp);
-        Raw<TO, 8> gq = ldraw<TO, 8>(gp);
+        if constexpr (!VS) {
+            xq = ldraw<TX, 8>(xp);
+            gq = ldraw<TO, 8>(gp);
+        }
 #pragma unroll 1
         for (int pc = 0; pc < NXB; ++pc) {
             Raw<TX, 8> xn = xq;
