@@ -67,6 +67,9 @@ __device__ unsigned long long g_col_probe[4096][8];
 #ifndef COL_VSTENCIL
 #define COL_VSTENCIL 1  // (2, 1) backward: phase B as VALU stencils + an LDS-grouped reduction (0: MFMA, A/B)
 #endif
+#ifndef COL_NHB2
+#define COL_NHB2 2  // load batches of the (2, 1) backward's halo phase
+#endif
 #ifndef COL_PAIRS
 #define COL_PAIRS 1  // the backward's halo phase on position pairs (0: one position per item, A/B)
 #endif
@@ -360,7 +363,8 @@ __global__ __launch_bounds__(NT) void k_col_fwd(CArgs a, const TX *__restrict__ 
     const SWeights<VS ? 27 : 1> w2s(w2);
     hx8 fw[K::KS];
 #pragma unroll
-    for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, false>(w2, k, lane);
+    for (int k = 0; k < K::KS; ++k)
+        if constexpr (!VS) fw[k] = w2_frag<BR, false>(w2, k, lane);  // MFMA path only
     for (int i = tid; i < PADE; i += NT) t2h[HVX * BR + i] = 0;
     int woff[K::KS];
     win_offsets<BR>(row, kb, woff);
@@ -543,7 +547,8 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
     const SWeights<(BR == 1 && COL_VSTENCIL) ? 27 : 1> w2s(w2);
     hx8 fw[K::KS];
 #pragma unroll
-    for (int k = 0; k < K::KS; ++k) fw[k] = w2_frag<BR, true>(w2, k, lane);
+    for (int k = 0; k < K::KS; ++k)
+        if constexpr (!(BR == 1 && COL_VSTENCIL)) fw[k] = w2_frag<BR, true>(w2, k, lane);  // MFMA path only
     for (int i = tid; i < PADE; i += NT) z3h[HVX * BR + i] = 0;
     for (int i = tid; i < BR * NLN * (TP - PL) / 2; i += NT) {  // zero the channel-major line tails
         const int l = i / ((TP - PL) / 2), e = i - l * ((TP - PL) / 2);
@@ -588,12 +593,13 @@ __global__ __launch_bounds__(NT) void k_col_bwd(CArgs a, const TO *__restrict__ 
         // Work items are PAIRS of consecutive positions of a halo line (PL is even): one line /
         // position computation per pair, and the channel-major t2 copy and the position-major gz3
         // leave as whole-dword (pair) LDS stores instead of two 16-bit stores into one dword.
-        // Two batches of pairs, every load of a batch issued before its math (registers).
-        constexpr int NPAIR = HVX / 2, HP = PL / 2;
+        // Two batches of pairs (COL_NHB2 = 1 for 2 channels measured no faster), every load of a
+        // batch issued before its math.
+        constexpr int NPAIR = HVX / 2, HP = PL / 2, NHB = C <= 2 ? COL_NHB2 : 2;
         static_assert(PL % 2 == 0 && TP % 2 == 0 && 2 * BR <= 8, "position pairs are dword aligned");
-        constexpr int PH = ((NPAIR + NT - 1) / NT + 1) / 2;
+        constexpr int PH = ((NPAIR + NT - 1) / NT + NHB - 1) / NHB;
 #pragma unroll 1
-        for (int half = 0; half < 2; ++half) {
+        for (int half = 0; half < NHB; ++half) {
             constexpr int P = PH;
             Raw<TO, C> gv[P][2];
             typename Vec<BR>::U tv3[P][2], tv2[P][2];
