@@ -4,8 +4,11 @@
 // (0 start, 1 line table, 2 phase A barrier, 3 phase B barrier, 4 phase C done, 5 partial sums
 // put, 6 partial row written).  Sched barriers keep code on its side of a probe.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -o tools/probes/col_probe tools/probes/col_probe.hip
-//   tools/probes/col_probe 2      (C = 2, 4 or 8)
+//   tools/probes/col_probe 2 [h|f] [c]  (C = 2, 4 or 8; "h": 16-bit x / g, else fp32; "c": cold caches
+//   between launches; -DNO_COL_PROBE: no clocks)
+#ifndef NO_COL_PROBE
 #define COL_PROBE 1
+#endif
 #include "../../3d-vq-vae-2_amd/csrc/preact_col.hip"
 
 #include <algorithm>
@@ -44,6 +47,10 @@ static int upload(std::vector<float> &h, float **d) {
 
 int main(int argc, char **argv) {
     const int C = argc > 1 ? atoi(argv[1]) : 2, B = C / 2;
+    const int dt = argc > 2 && argv[2][0] == 'h' ? int(vq3d::VQ3D_HALF) : int(VQ3D_F32);  // x / g storage ("h": 16-bit)
+    const bool cold = argc > 3 && argv[3][0] == 'c';  // "c": a 1 GiB memset between launches (cold L2 / MALL)
+    void *flush = nullptr;
+    if (cold) CK(hipMalloc(&flush, size_t(1) << 30));
     const int H = C == 2 ? 128 : C == 4 ? 512 : 256, W = H, D = C == 2 ? 32 : C == 4 ? 128 : 64;
     const size_t nv = size_t(H) * W * D;
     std::mt19937 rng(1);
@@ -92,8 +99,9 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e1));
     float ms = 0.f;
     for (int r = 0; r < reps + 2; ++r) {
+        if (cold) CK(hipMemsetAsync(flush, r & 0xff, size_t(1) << 30, 0));
         CK(hipEventRecord(e0, 0));
-        if (vq3d::col_bwd(VQ3D_F32, VQ3D_F32, 1, C, B, H, W, D, g, x, t2, t3, w1, w2, w3, p, G, ws, gx, 1, nullptr))
+        if (vq3d::col_bwd(dt, dt, 1, C, B, H, W, D, g, x, t2, t3, w1, w2, w3, p, G, ws, gx, 1, nullptr))
             return 1;
         CK(hipEventRecord(e1, 0));
         CK(hipDeviceSynchronize());
@@ -101,15 +109,19 @@ int main(int argc, char **argv) {
         float t;
         CK(hipEventElapsedTime(&t, e0, e1));
         ms += t;
+#ifndef NO_COL_PROBE
         static unsigned long long pr[4096][8];
         CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_col_probe), sizeof(pr)));
         for (int b = 0; b < nb; ++b)
             for (int k = 0; k < 6; ++k) ph[k].push_back((long long)(pr[b][k + 1] - pr[b][k]));
+#else
+        (void)nb;
+#endif
     }
     printf("k_col_bwd<%d,%d,f32,f32> @%dx%dx%d (%d bricks, %d workgroups): %.1f us per launch (events); "
            "medians over workgroups x %d runs, s_memtime ticks\n", C, B, H, W, D, a.nbricks, a.nwg, 1e3f * ms / reps, reps);
     const char *lab[6] = {"line table", "A halo", "B mfma", "C voxels", "sums put", "row out"};
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 6 && !ph[k].empty(); ++k) {
         std::sort(ph[k].begin(), ph[k].end());
         printf("  %-12s %6lld  (p90 %lld)\n", lab[k], ph[k][ph[k].size() / 2], ph[k][ph[k].size() * 9 / 10]);
     }
