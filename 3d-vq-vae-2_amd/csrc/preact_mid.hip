@@ -1116,8 +1116,16 @@ constexpr int NT9 = 9 * 64;
 // channel stride CS has CS / 8 = 1 and the copy stride CK = 9 CS has CK / 8 = 9 (mod 16), so the 16
 // lanes of a lane group read 16 distinct 16-byte bank slots.  Copy 1 is the items' transpose;
 // copies 0 and 2 are built from it (dword reads + v_alignbyte once per row group, not per use).
+#ifndef PM_W2ROWS
+#define PM_W2ROWS 1  // D = 32: a wave per (tap row kh, chunk row), B fragments slid along the row (0: a wave per tap row)
+#endif
 template <int D>
 struct W2c {
+    // D = 32 (PM_W2ROWS): 12 waves, wave (kh, r) sums taps (kh, 0..2) over chunk row r -- its TW
+    // lines' A fragments are read once for 3 taps and the B fragments of halo columns c, c + 1,
+    // c + 2 are shared by neighbouring lines (TW + 2 column reads instead of 3 TW): 192 instead of
+    // 432 16-byte LDS reads per chunk for the same 288 MFMAs.  Otherwise 9 waves, one per tap row.
+    static constexpr bool ROWS = PM_W2ROWS && D == 32;
     static constexpr int NL = CHV / D;  // lines per chunk
     static constexpr int TH = NL >= 64 ? 8 : NL >= 16 ? 4 : NL >= 4 ? 2 : 1, TW = NL / TH;
     static constexpr int LW = TW + 2, HL = (TH + 2) * LW;  // halo lines
@@ -1126,7 +1134,8 @@ struct W2c {
     static constexpr int CK = 9 * CS;                       // copy stride
     static constexpr int ZI = NL * GPL, TI = HL * GPL;      // staging items (gz3, t2)
     static constexpr int NPC = (ZI + TI) * 9;               // 16-B pieces per chunk
-    static constexpr int NP = (NPC + NT9 - 1) / NT9;        // pieces per thread
+    static constexpr int NTW = ROWS ? 3 * TH * 64 : NT9;    // threads
+    static constexpr int NP = (NPC + NTW - 1) / NTW;        // pieces per thread
     static constexpr int RAW = (ZI + TI) * 72;              // voxel-major staging area (elements)
     static constexpr int NRG = BR * HL * GPL;               // row groups of copies 0 / 2 to build
     // the raw area after the copies, or (when that would not fit) over copy 2: dead once the items
@@ -1135,7 +1144,8 @@ struct W2c {
     static constexpr int RAWO = ALIAS ? 2 * CK : 3 * CK;    // raw offset in the t2 area
     static constexpr size_t LDS = size_t(16 * ZP + (ALIAS ? std::max(3 * CK, 2 * CK + RAW) : 3 * CK + RAW)) * 2;
     static_assert(NL * D == CHV && TH * TW == NL && D % 8 == 0, "chunk");
-    static_assert(ZI + TI <= NT9, "one staging item per thread");
+    static_assert(ZI + TI <= NTW, "one staging item per thread");
+    static_assert(NTW <= 1024 && (!ROWS || size_t(NTW / 64) * 6 * 256 * 4 <= LDS), "row-wave partials fit");
     static_assert((CS / 8) % 16 == 1 && (CK / 8) % 16 == 9, "bank slots");
     static_assert(LDS <= 160 * 1024, "LDS");
 };
@@ -1185,7 +1195,7 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
         const int h0 = th_i * K::TH, w0 = tw_i * K::TW;
 #pragma unroll
         for (int u = 0; u < K::NP; ++u) {
-            const int p = min(tid + u * NT9, K::NPC - 1), item = p / 9, j = p - item * 9;
+            const int p = min(tid + u * K::NTW, K::NPC - 1), item = p / 9, j = p - item * 9;
             const bool z = item < K::ZI;
             const int it = z ? item : item - K::ZI, il = it / K::GPL, ig = it - il * K::GPL;
             int hh, ww;
@@ -1208,6 +1218,11 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
     h16_t *dst = zitem ? zT + il * D + 8 * ig : tT + K::CK + il * D + 8 * ig;  // copy 1
     const int pitch = zitem ? ZP : K::CS;
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // ROWS: wave kk = rh * TH + rr (tap row rh, chunk row rr), taps (rh, 0..2)
+    const int rh = kk / K::TH, rr = kk - rh * K::TH;
+    f32x4 racc[K::ROWS ? 3 : 1][2];
+#pragma unroll
+    for (int t = 0; t < (K::ROWS ? 3 : 1); ++t) racc[t][0] = racc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int cend = min(c0 + npc, nchunk);
     if (c0 < cend) load(c0);
 #pragma unroll 1
@@ -1215,7 +1230,7 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
         if constexpr (K::ALIAS) __syncthreads();  // the previous chunk's readers of copy 2 (= raw) are done
 #pragma unroll
         for (int u = 0; u < K::NP; ++u) {  // raw pieces (non-aliased: the area's readers passed the last barrier)
-            const int p = tid + u * NT9;
+            const int p = tid + u * K::NTW;
             if (p < K::NPC) reinterpret_cast<u32x4 *>(raw)[p] = v[u];
         }
         __syncthreads();  // raw complete; the previous chunk's fragments are read
@@ -1236,7 +1251,7 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
         __syncthreads();  // copy 1 complete (and raw dead)
         // copies 0 and 2 of row group (channel, line, group) from copy 1: dwords 4g - 1 .. 4g + 4
         // of the line (circular), each output dword one v_alignbyte
-        for (int q = tid; q < K::NRG; q += NT9) {
+        for (int q = tid; q < K::NRG; q += K::NTW) {
             const int g = q % K::GPL, lr = q / K::GPL;  // lr = channel * HL + line
             const uint32_t *r1 = reinterpret_cast<const uint32_t *>(tT + K::CK + (lr / K::HL) * K::CS + (lr % K::HL) * D);
             const u32x4 m = reinterpret_cast<const u32x4 *>(r1)[g];
@@ -1251,27 +1266,77 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
         }
         __syncthreads();
         if (c + 1 < cend) load(c + 1);
-#pragma unroll 4
-        for (int ks = 0; ks < CHV / 32; ++ks) {
-            const int vv = 32 * ks + 8 * kb, l = vv / D, d0 = vv - l * D;
-            const int hl = (l / K::TW + kh) * K::LW + l % K::TW + kw;
-            const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + vv);
-            const int off = hl * D + d0;  // copy kd: position d0 - 1 + kd at index d0
+        if constexpr (K::ROWS) {
+            // wave (rh = tap row, rr = chunk row): line lw of the row takes halo columns lw .. lw + 2
+            // of halo row rr + rh; a line is one k-step (D = 32)
+            const h16_t *bt = tT + (rr + rh) * K::LW * D + 8 * kb;
+            hx8 bw[3][2];
 #pragma unroll
-            for (int n = 0; n < 2; ++n) acc[n] = mfma(af, *reinterpret_cast<const hx8 *>(tT + toff[n] + off), acc[n]);
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int n = 0; n < 2; ++n) bw[c][n] = *reinterpret_cast<const hx8 *>(bt + toff[n] + c * D);
+#pragma unroll
+            for (int lw = 0; lw < K::TW; ++lw) {
+#pragma unroll
+                for (int n = 0; n < 2; ++n) bw[(lw + 2) % 3][n] = *reinterpret_cast<const hx8 *>(bt + toff[n] + (lw + 2) * D);
+                const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + (rr * K::TW + lw) * D + 8 * kb);
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+#pragma unroll
+                    for (int n = 0; n < 2; ++n) racc[t][n] = mfma(af, bw[(lw + t) % 3][n], racc[t][n]);
+            }
+        } else {
+#pragma unroll 4
+            for (int ks = 0; ks < CHV / 32; ++ks) {
+                const int vv = 32 * ks + 8 * kb, l = vv / D, d0 = vv - l * D;
+                const int hl = (l / K::TW + kh) * K::LW + l % K::TW + kw;
+                const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + vv);
+                const int off = hl * D + d0;  // copy kd: position d0 - 1 + kd at index d0
+#pragma unroll
+                for (int n = 0; n < 2; ++n) acc[n] = mfma(af, *reinterpret_cast<const hx8 *>(tT + toff[n] + off), acc[n]);
+            }
         }
     }
-    float *dstp = p2a + (int64_t(bid) * 9 + kk) * NER;
+    if constexpr (K::ROWS) {
+        // the TH row waves of a tap row summed in row order through LDS (over the dead tiles)
+        float *red = reinterpret_cast<float *>(smem);  // [wave][tap t][n][lane][4]
+        __syncthreads();  // every wave's last MFMA reads are done
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+        for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int co = 4 * kb + j, col = 16 * n + row;
-            if (co < BR && col < 27) dstp[co * 27 + col] = acc[n][j];
+            for (int n = 0; n < 2; ++n)
+                *reinterpret_cast<f32x4 *>(red + (((kk * 3 + t) * 2 + n) * 64 + lane) * 4) = racc[t][n];
+        __syncthreads();
+        if (rr == 0) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                float *dstp = p2a + (int64_t(bid) * 9 + rh * 3 + t) * NER;
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    f32x4 v = racc[t][n];
+                    for (int q = 1; q < K::TH; ++q)
+                        v += *reinterpret_cast<const f32x4 *>(red + ((((kk + q) * 3 + t) * 2 + n) * 64 + lane) * 4);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int co = 4 * kb + j, col = 16 * n + row;
+                        if (co < BR && col < 27) dstp[co * 27 + col] = v[j];
+                    }
+                }
+            }
         }
+    } else {
+        float *dstp = p2a + (int64_t(bid) * 9 + kk) * NER;
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = 4 * kb + j, col = 16 * n + row;
+                if (co < BR && col < 27) dstp[co * 27 + col] = acc[n][j];
+            }
+    }
 }
 template <int D>
-__global__ __launch_bounds__(NT9) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const h16_t *__restrict__ gz3,
+__global__ __launch_bounds__(W2c<D>::NTW) void k_pm_w2grad(PmArgs a, int nchunk, int npc, const h16_t *__restrict__ gz3,
                                                    const h16_t *__restrict__ t2, float *__restrict__ p2a) {
     pm_w2grad<D>(a, nchunk, npc, gz3, t2, p2a);
 }
@@ -1290,7 +1355,7 @@ struct MidRunWs {
     int64_t ogz3, ogz1, op2a, op2b;  // byte offsets inside a block's workspace slice
 };
 template <int D>
-__global__ __launch_bounds__(NT9) void k_pm_w2grad_run(PmArgs a, int nchunk, int npc, MidRunWs w, MidRunPtrs r) {
+__global__ __launch_bounds__(W2c<D>::NTW) void k_pm_w2grad_run(PmArgs a, int nchunk, int npc, MidRunWs w, MidRunPtrs r) {
     const int i = blockIdx.y;
     const char *b = w.base + size_t(i) * w.stride;
     pm_w2grad<D>(a, nchunk, npc, reinterpret_cast<const h16_t *>(b + w.ogz3), r.t2[i],
@@ -1577,7 +1642,7 @@ void launch_w2(const PmArgs &a, int nwa, int npc, const h16_t *gz3, const h16_t 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, int(W2c<D>::LDS));
         init = true;
     }
-    k_pm_w2grad<D><<<nwa, NT9, W2c<D>::LDS, s>>>(a, int(int64_t(a.B) * a.H * a.W * a.D / CHV), npc, gz3, t2, p2a);
+    k_pm_w2grad<D><<<nwa, W2c<D>::NTW, W2c<D>::LDS, s>>>(a, int(int64_t(a.B) * a.H * a.W * a.D / CHV), npc, gz3, t2, p2a);
 }
 
 void launch_fwd(int batch, int h, int w, int dd, const void *x, const float *w2, const float *w3,
@@ -1831,11 +1896,11 @@ int vq3d_preact_mid_wgrad_run(int32_t dtype, int32_t nblocks, int32_t batch, int
         MidRunWs wr{b0 + size_t(i0) * workspace_stride, workspace_stride, off(m.gz3), off(m.gz1), off(m.p2a), off(m.p2b)};
         const dim3 ga(unsigned(m.nwa), unsigned(nb));
         switch (dd) {
-            case 8: k_pm_w2grad_run<8><<<ga, NT9, W2c<8>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
-            case 16: k_pm_w2grad_run<16><<<ga, NT9, W2c<16>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
-            case 32: k_pm_w2grad_run<32><<<ga, NT9, W2c<32>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
-            case 64: k_pm_w2grad_run<64><<<ga, NT9, W2c<64>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
-            default: k_pm_w2grad_run<128><<<ga, NT9, W2c<128>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 8: k_pm_w2grad_run<8><<<ga, W2c<8>::NTW, W2c<8>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 16: k_pm_w2grad_run<16><<<ga, W2c<16>::NTW, W2c<16>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 32: k_pm_w2grad_run<32><<<ga, W2c<32>::NTW, W2c<32>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            case 64: k_pm_w2grad_run<64><<<ga, W2c<64>::NTW, W2c<64>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
+            default: k_pm_w2grad_run<128><<<ga, W2c<128>::NTW, W2c<128>::LDS, s>>>(a, nchunk, m.npc, wr, r); break;
         }
         k_pm_w13grad_run<<<dim3(unsigned(m.nchb), unsigned(nb)), NT, w13_lds(), s>>>(m.npb, wr, r, params + size_t(i0) * 11);
     }
