@@ -1121,11 +1121,13 @@ constexpr int NT9 = 9 * 64;
 #endif
 template <int D>
 struct W2c {
-    // D = 32 (PM_W2ROWS): 12 waves, wave (kh, r) sums taps (kh, 0..2) over chunk row r -- its TW
+    // D = 32, 64 (PM_W2ROWS): 12 waves, wave (kh, r, s) sums taps (kh, 0..2) over chunk row r (line
+    // segment s of 32 voxels) -- its TW
     // lines' A fragments are read once for 3 taps and the B fragments of halo columns c, c + 1,
     // c + 2 are shared by neighbouring lines (TW + 2 column reads instead of 3 TW): 192 instead of
     // 432 16-byte LDS reads per chunk for the same 288 MFMAs.  Otherwise 9 waves, one per tap row.
-    static constexpr bool ROWS = PM_W2ROWS && D == 32;
+    static constexpr bool ROWS = PM_W2ROWS && (D == 32 || D == 64);
+    static constexpr int SEG = D >= 32 ? D / 32 : 1;        // ROWS: 32-voxel k-steps per line
     static constexpr int NL = CHV / D;  // lines per chunk
     static constexpr int TH = NL >= 64 ? 8 : NL >= 16 ? 4 : NL >= 4 ? 2 : 1, TW = NL / TH;
     static constexpr int LW = TW + 2, HL = (TH + 2) * LW;  // halo lines
@@ -1134,7 +1136,8 @@ struct W2c {
     static constexpr int CK = 9 * CS;                       // copy stride
     static constexpr int ZI = NL * GPL, TI = HL * GPL;      // staging items (gz3, t2)
     static constexpr int NPC = (ZI + TI) * 9;               // 16-B pieces per chunk
-    static constexpr int NTW = ROWS ? 3 * TH * 64 : NT9;    // threads
+    static constexpr int NPART = TH * SEG;                  // ROWS: waves per tap row (chunk row, segment)
+    static constexpr int NTW = ROWS ? 3 * NPART * 64 : NT9; // threads
     static constexpr int NP = (NPC + NTW - 1) / NTW;        // pieces per thread
     static constexpr int RAW = (ZI + TI) * 72;              // voxel-major staging area (elements)
     static constexpr int NRG = BR * HL * GPL;               // row groups of copies 0 / 2 to build
@@ -1218,8 +1221,8 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
     h16_t *dst = zitem ? zT + il * D + 8 * ig : tT + K::CK + il * D + 8 * ig;  // copy 1
     const int pitch = zitem ? ZP : K::CS;
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    // ROWS: wave kk = rh * TH + rr (tap row rh, chunk row rr), taps (rh, 0..2)
-    const int rh = kk / K::TH, rr = kk - rh * K::TH;
+    // ROWS: wave kk = (rh * TH + rr) * SEG + sg (tap row rh, chunk row rr, line segment sg), taps (rh, 0..2)
+    const int rh = kk / K::NPART, rr = (kk - rh * K::NPART) / K::SEG, sg = kk - rh * K::NPART - rr * K::SEG;
     f32x4 racc[K::ROWS ? 3 : 1][2];
 #pragma unroll
     for (int t = 0; t < (K::ROWS ? 3 : 1); ++t) racc[t][0] = racc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1267,9 +1270,9 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
         __syncthreads();
         if (c + 1 < cend) load(c + 1);
         if constexpr (K::ROWS) {
-            // wave (rh = tap row, rr = chunk row): line lw of the row takes halo columns lw .. lw + 2
-            // of halo row rr + rh; a line is one k-step (D = 32)
-            const h16_t *bt = tT + (rr + rh) * K::LW * D + 8 * kb;
+            // wave (rh = tap row, rr = chunk row, sg = segment): line lw of the row takes halo columns
+            // lw .. lw + 2 of halo row rr + rh; a line segment is one k-step
+            const h16_t *bt = tT + (rr + rh) * K::LW * D + 32 * sg + 8 * kb;
             hx8 bw[3][2];
 #pragma unroll
             for (int c = 0; c < 2; ++c)
@@ -1279,7 +1282,7 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
             for (int lw = 0; lw < K::TW; ++lw) {
 #pragma unroll
                 for (int n = 0; n < 2; ++n) bw[(lw + 2) % 3][n] = *reinterpret_cast<const hx8 *>(bt + toff[n] + (lw + 2) * D);
-                const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + (rr * K::TW + lw) * D + 8 * kb);
+                const hx8 af = *reinterpret_cast<const hx8 *>(zT + row * ZP + (rr * K::TW + lw) * D + 32 * sg + 8 * kb);
 #pragma unroll
                 for (int t = 0; t < 3; ++t)
 #pragma unroll
@@ -1298,7 +1301,7 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
         }
     }
     if constexpr (K::ROWS) {
-        // the TH row waves of a tap row summed in row order through LDS (over the dead tiles)
+        // the NPART waves of a tap row summed in wave order through LDS (over the dead tiles)
         float *red = reinterpret_cast<float *>(smem);  // [wave][tap t][n][lane][4]
         __syncthreads();  // every wave's last MFMA reads are done
 #pragma unroll
@@ -1307,14 +1310,14 @@ __device__ __forceinline__ void pm_w2grad(const PmArgs &a, int nchunk, int npc, 
             for (int n = 0; n < 2; ++n)
                 *reinterpret_cast<f32x4 *>(red + (((kk * 3 + t) * 2 + n) * 64 + lane) * 4) = racc[t][n];
         __syncthreads();
-        if (rr == 0) {
+        if (kk == rh * K::NPART) {
 #pragma unroll
             for (int t = 0; t < 3; ++t) {
                 float *dstp = p2a + (int64_t(bid) * 9 + rh * 3 + t) * NER;
 #pragma unroll
                 for (int n = 0; n < 2; ++n) {
                     f32x4 v = racc[t][n];
-                    for (int q = 1; q < K::TH; ++q)
+                    for (int q = 1; q < K::NPART; ++q)
                         v += *reinterpret_cast<const f32x4 *>(red + ((((kk + q) * 3 + t) * 2 + n) * 64 + lane) * 4);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {

@@ -19,7 +19,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last_3d
-SHAPES = [(1, 18, 8, 8, 16), (2, 18, 16, 8, 16), (1, 18, 32, 16, 16), (1, 18, 128, 128, 32)]
+SHAPES = [(1, 18, 8, 8, 16), (2, 18, 16, 8, 16), (1, 18, 32, 16, 16), (1, 18, 16, 16, 64), (1, 18, 128, 128, 32)]
 
 
 def _block(seed):
