@@ -291,6 +291,30 @@ __device__ __forceinline__ F block_sum(F v, F *scratch /* >= NT/64 */) {
     return t;
 }
 
+// N deterministic block sums at once, each bit-identical to block_sum over scratch + k * S (the
+// same wave trees and wave order), with one barrier pair for all N instead of one per value
+template <typename F, int NT, int N, int S>
+__device__ __forceinline__ void block_sums(F (&v)[N], F *scratch /* >= (N - 1) * S + NT / 64 */) {
+    static_assert(S >= NT / 64, "scratch stride");
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    F w[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) w[k] = wave_sum(v[k]);
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) scratch[k * S + wid] = w[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        F t = 0;
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) t += scratch[k * S + i];
+        v[k] = t;
+    }
+}
+
 // ---------------------------------------------------------------- in-grid partial sums
 // A grid's per-workgroup partials summed by its LAST workgroup to finish, in the order a separate
 // one-workgroup pass over them would use (deterministic, bit-identical to that pass) without the

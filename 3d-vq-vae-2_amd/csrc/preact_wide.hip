@@ -562,12 +562,14 @@ __global__ __launch_bounds__(NT) void k_wide_bwd_data(WArgs a, const float *__re
         }
     }
     // scalar partials: b4, b3b, b3a, scale, b2b, b2a, b1b, b1a
-    const float sums[NSC] = {s4, s3b, s3a, ssc, s2b, s2a, s1b, s1a};
+    // (all eight in one barrier pair: eight sequential block sums cost sixteen barriers on the
+    // run's critical path)
+    float sums[NSC] = {s4, s3b, s3a, ssc, s2b, s2a, s1b, s1a};
+    block_sums<float, NT, NSC, 8>(sums, red);
     float *dst = part + int64_t(blockIdx.x) * NSC;
+    if (tid == 0) {
 #pragma unroll
-    for (int k = 0; k < NSC; ++k) {
-        const float t = block_sum<float, NT>(sums[k], red + 8 * k);
-        if (tid == 0) dst[k] = t;
+        for (int k = 0; k < NSC; ++k) dst[k] = sums[k];
     }
 }
 
