@@ -211,8 +211,12 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(S2Args a, const T *__restrict_
         }
     }
     if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
@@ -408,8 +412,12 @@ __global__ __launch_bounds__(256) void k_dgrad_s2_cell(S2Args a, const h16_t *__
     }
 done:
     if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
@@ -538,8 +546,12 @@ __global__ __launch_bounds__(256) void k_dgrad_s2_mma(S2Args a, const h16_t *__r
         }
     }
     if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }

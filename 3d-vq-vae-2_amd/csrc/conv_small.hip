@@ -298,8 +298,12 @@ __global__ __launch_bounds__(256) void k_small_epi(SArgs s, const float *__restr
                                out2 ? out2 + int64_t(v) * a.Cin2 : nullptr, pre, post);
     }
     if (DG && (dpre || dpost)) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }

@@ -262,8 +262,12 @@ __global__ __launch_bounds__(NTC) void k_tc(TcArgs a, const T *__restrict__ in, 
         vstore<T, DV * CO>(out + vox0 * CO, r);
     }
     if (DG && (dpre || dpost)) {
-        pre = block_sum<float, NTC>(pre, red);
-        post = block_sum<float, NTC>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, NTC, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         if (tid == 0) {
             part[blockIdx.x] = pre;
             part[gridDim.x + blockIdx.x] = post;

@@ -231,8 +231,12 @@ __global__ __launch_bounds__(SEG) void k_pw2(PwArgs a, const T *__restrict__ in,
         if (a.N2) copy_out<T>(out2 + v0 * a.N2, sout2, nv * a.N2, a.vec);
     }
     if (DGRAD && (dpre || dpost)) {
-        pre = block_sum<float, SEG>(pre, red);
-        post = block_sum<float, SEG>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, SEG, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
             finish_partials<256>(part, int(gridDim.x), int(blockIdx.x), pre, post, dpre, dpost, slot, red);
         } else if (threadIdx.x == 0) {
@@ -415,8 +419,12 @@ __global__ __launch_bounds__(256) void k_pw_rows(int64_t nvox, const T *__restri
         }
     }
     if (DGRAD && (dpre || dpost)) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
             finish_partials<256>(part, int(gridDim.x), int(blockIdx.x), pre, post, dpre, dpost, slot, red);
         } else if (threadIdx.x == 0) {
@@ -549,8 +557,12 @@ __global__ __launch_bounds__(256) void k_pw_sg(SgArgs s, ConvArgs ca, const T *_
                                  out2 ? out2 + v * ca.Cin2 : nullptr, pre, post);
     }
     if (DG && (dpre || dpost)) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
             finish_partials<256>(part, int(gridDim.x * gridDim.y), int(blockIdx.y * gridDim.x + blockIdx.x), pre, post, dpre, dpost, slot, red);
         } else if (threadIdx.x == 0) {
@@ -799,8 +811,12 @@ __global__ __launch_bounds__(256) void k_pw_mma(MmArgs m, ConvArgs ca, const h16
         }
     }
     if (DG && (dpre || dpost)) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         if (part) {  // per-workgroup partials, summed in order by the grid's last workgroup
             finish_partials<256>(part, int(gridDim.x * gridDim.y), int(blockIdx.y * gridDim.x + blockIdx.x), pre, post, dpre, dpost, slot, red);
         } else if (threadIdx.x == 0) {

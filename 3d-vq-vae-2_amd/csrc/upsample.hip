@@ -184,8 +184,12 @@ __global__ __launch_bounds__(256) void k_up2_bwd(UArgs a, const T *__restrict__ 
         stv<T, CV>(gx + o, acc);
     }
     if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
@@ -283,8 +287,12 @@ __global__ __launch_bounds__(256) void k_up2_bwd_run4(UArgs a, const h16_t *__re
         *reinterpret_cast<u32x4 *>(gx + o + 8) = res[1];
     }
     if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
@@ -411,8 +419,12 @@ __global__ __launch_bounds__(256) void k_up2_bwd_quad(UArgs a, const h16_t *__re
             }
     }
     if (dpre || dpost) {
-        pre = block_sum<float, 256>(pre, red);
-        post = block_sum<float, 256>(post, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {pre, post};
+            block_sums<float, 256, 2, 4>(pp, red);
+            pre = pp[0];
+            post = pp[1];
+        }
         grid_sum2<256>(gsum, pre, post, dpre, dpost, red);
     }
 }
