@@ -379,8 +379,12 @@ __global__ __launch_bounds__(256) void k_lines_wgrad_reduce(WArgs a, int ntm, co
         }
     }
     if (dscale || dbias) {
-        wg = block_sum<float, 256>(wg, red);
-        bs = block_sum<float, 256>(bs, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {wg, bs};
+            block_sums<float, 256, 2, 4>(pp, red);
+            wg = pp[0];
+            bs = pp[1];
+        }
         grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }

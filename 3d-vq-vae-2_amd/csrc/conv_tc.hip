@@ -283,8 +283,12 @@ __global__ __launch_bounds__(256) void k_tc_sum(const float *__restrict__ part, 
         s0 += part[i];
         s1 += part[n + i];
     }
-    s0 = block_sum<float, 256>(s0, red);
-    s1 = block_sum<float, 256>(s1, red + 4);
+    {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+        float pp[2] = {s0, s1};
+        block_sums<float, 256, 2, 4>(pp, red);
+        s0 = pp[0];
+        s1 = pp[1];
+    }
     if (threadIdx.x == 0) {
         if (dpre) *dpre += s0;
         if (dpost) *dpost += s1;
@@ -391,8 +395,12 @@ __global__ __launch_bounds__(256) void k_tc_wgrad_reduce(const float *__restrict
         }
     }
     if (dscale || dbias) {
-        wg = block_sum<float, 256>(wg, red);
-        bs = block_sum<float, 256>(bs, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {wg, bs};
+            block_sums<float, 256, 2, 4>(pp, red);
+            wg = pp[0];
+            bs = pp[1];
+        }
         grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }

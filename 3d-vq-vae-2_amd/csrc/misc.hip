@@ -463,8 +463,12 @@ __global__ __launch_bounds__(256) void k_preact_act_bwd(int64_t n, const TG *__r
         sa += v;
         sb += gv;
     }
-    sa = block_sum<float, 256>(sa, red);
-    sb = block_sum<float, 256>(sb, red + 4);
+    {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+        float pp[2] = {sa, sb};
+        block_sums<float, 256, 2, 4>(pp, red);
+        sa = pp[0];
+        sb = pp[1];
+    }
     grid_sum2<256>(gsum, sa, sb, da, db, red);
 }
 // 4 consecutive elements (16-byte fp32 / 8-byte 16-bit accesses)
@@ -504,8 +508,12 @@ __global__ __launch_bounds__(256) void k_preact_act_bwd4(int64_t n4, const TG *_
         }
         if (gx) st4(gx + 4 * i, v);
     }
-    sa = block_sum<float, 256>(sa, red);
-    sb = block_sum<float, 256>(sb, red + 4);
+    {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+        float pp[2] = {sa, sb};
+        block_sums<float, 256, 2, 4>(pp, red);
+        sa = pp[0];
+        sb = pp[1];
+    }
     grid_sum2<256>(gsum, sa, sb, da, db, red);
 }
 template <typename TO>
@@ -528,8 +536,12 @@ __global__ __launch_bounds__(256) void k_scale_bias_res_bwd4(int64_t n4, const f
         }
         if (go) st4(go + 4 * i, v);
     }
-    ss = block_sum<float, 256>(ss, red);
-    sb = block_sum<float, 256>(sb, red + 4);
+    {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+        float pp[2] = {ss, sb};
+        block_sums<float, 256, 2, 4>(pp, red);
+        ss = pp[0];
+        sb = pp[1];
+    }
     grid_sum2<256>(gsum, ss, sb, dscale, dbias, red);
 }
 static unsigned grid4_for(int64_t n4) { return unsigned(std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 512))); }
@@ -557,8 +569,12 @@ __global__ __launch_bounds__(256) void k_scale_bias_res_bwd(int64_t n, const flo
         ss = fmaf(gv, ld(o + i), ss);
         sb += gv;
     }
-    ss = block_sum<float, 256>(ss, red);
-    sb = block_sum<float, 256>(sb, red + 4);
+    {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+        float pp[2] = {ss, sb};
+        block_sums<float, 256, 2, 4>(pp, red);
+        ss = pp[0];
+        sb = pp[1];
+    }
     grid_sum2<256>(gsum, ss, sb, dscale, dbias, red);
 }
 

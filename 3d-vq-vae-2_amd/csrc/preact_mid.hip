@@ -915,27 +915,23 @@ __global__ __launch_bounds__(QNT) __attribute__((amdgpu_waves_per_eu(PM_BWD_WPE)
     }
     if constexpr (CHAIN) {
         float *dp = part1p + int64_t(blockIdx.x) * NE1;
-        const float t4 = block_sum<float, QNT>(q4, red);
-        const float t3b = block_sum<float, QNT>(q3b, red + 8);
-        const float t3a = block_sum<float, QNT>(q3a, red + 16);
-        const float tsc = block_sum<float, QNT>(qsc, red + 24);
+        float q[4] = {q4, q3b, q3a, qsc};  // one barrier pair for the four (bit-identical)
+        block_sums<float, QNT, 4, 8>(q, red);
         if (tid == 0) {
-            dp[0] = t4;
-            dp[1] = t3b;
-            dp[2] = t3a;
-            dp[3] = tsc;
+            dp[0] = q[0];
+            dp[1] = q[1];
+            dp[2] = q[2];
+            dp[3] = q[3];
         }
     }
     float *dst = part + int64_t(blockIdx.x) * NE2;
-    const float t2b = block_sum<float, QNT>(s2b, red);
-    const float t2a = block_sum<float, QNT>(s2a, red + 8);
-    const float t1b = block_sum<float, QNT>(s1b, red + 16);
-    const float t1a = block_sum<float, QNT>(s1a, red + 24);
+    float q2[4] = {s2b, s2a, s1b, s1a};
+    block_sums<float, QNT, 4, 8>(q2, red);
     if (tid == 0) {
-        dst[0] = t2b;
-        dst[1] = t2a;
-        dst[2] = t1b;
-        dst[3] = t1a;
+        dst[0] = q2[0];
+        dst[1] = q2[1];
+        dst[2] = q2[2];
+        dst[3] = q2[3];
     }
 }
 

@@ -101,8 +101,12 @@ __device__ __forceinline__ void finish_entry(const WgOut &o, int e, int Ct, floa
 
 __device__ __forceinline__ void finish_block(const WgOut &o, float wg, float bs, float *red) {
     if (!o.dscale && !o.dbias) return;
-    wg = block_sum<float, 256>(wg, red);
-    bs = block_sum<float, 256>(bs, red + 4);
+    {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+        float pp[2] = {wg, bs};
+        block_sums<float, 256, 2, 4>(pp, red);
+        wg = pp[0];
+        bs = pp[1];
+    }
     grid_sum2<256>(o.gsum, wg, bs, o.dscale, o.dbias, red);
 }
 
@@ -338,8 +342,12 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce(const float *__restrict
         }
     }
     if (dscale || dbias) {
-        wg = block_sum<float, 256>(wg, red);
-        bs = block_sum<float, 256>(bs, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {wg, bs};
+            block_sums<float, 256, 2, 4>(pp, red);
+            wg = pp[0];
+            bs = pp[1];
+        }
         grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }
@@ -623,8 +631,12 @@ __global__ __launch_bounds__(256) void k_pw_wgrad_reduce_t(const float *__restri
         }
     }
     if (dscale || dbias) {
-        wg = block_sum<float, 256>(wg, red);
-        bs = block_sum<float, 256>(bs, red + 4);
+        {  // both sums in one barrier pair (bit-identical to two block_sum calls)
+            float pp[2] = {wg, bs};
+            block_sums<float, 256, 2, 4>(pp, red);
+            wg = pp[0];
+            bs = pp[1];
+        }
         grid_sum2<256>(gsum, wg, bs, dscale, dbias, red);
     }
 }
