@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void k_pin_fwd(const float *__restrict__ x, in
 template <int C>
 __global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, const h16_t *__restrict__ g, int64_t n4,
                                                   float *__restrict__ part) {
-    __shared__ float red[4];
+    __shared__ float red[4 * 2 * C];
     float sw[C], sb[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) sw[c] = sb[c] = 0.f;
@@ -124,14 +124,16 @@ __global__ __launch_bounds__(256) void k_pin_wgrad(const float *__restrict__ x, 
                 sb[c] += gv[v * C + c];
             }
     }
+    float v[2 * C];  // all 2 C sums in one barrier pair (bit-identical to 2 C block_sum calls)
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        const float a = block_sum<float, 256>(sw[c], red);
-        const float bb = block_sum<float, 256>(sb[c], red);
-        if (threadIdx.x == 0) {
-            part[int64_t(blockIdx.x) * 2 * C + c] = a;
-            part[int64_t(blockIdx.x) * 2 * C + C + c] = bb;
-        }
+        v[c] = sw[c];
+        v[C + c] = sb[c];
+    }
+    block_sums<float, 256, 2 * C, 4>(v, red);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int e = 0; e < 2 * C; ++e) part[int64_t(blockIdx.x) * 2 * C + e] = v[e];
     }
 }
 // fixed-order sum of the partials (one workgroup per entry, a block tree), added into dw / db
