@@ -386,8 +386,10 @@ __device__ __forceinline__ void finish_partials(float *part, int nb, int bid, fl
                 s1 += __uint_as_float(uint32_t(v[u] >> 32));
             }
     }
-    s0 = block_sum<float, NT>(s0, red);
-    s1 = block_sum<float, NT>(s1, red + 4);
+    float ss[2] = {s0, s1};  // one barrier pair (bit-identical to two block_sum calls)
+    block_sums<float, NT, 2, 4>(ss, red);
+    s0 = ss[0];
+    s1 = ss[1];
     if (threadIdx.x == 0) {
         if (dpre) *dpre += s0;
         if (dpost) *dpost += s1;

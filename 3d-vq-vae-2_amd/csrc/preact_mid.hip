@@ -434,15 +434,13 @@ __global__ __launch_bounds__(NT) void k_pm_bwd1(int64_t nvox, const h16_t *__res
             reinterpret_cast<uint4 *>(gz3o + v0 * BR)[i] = reinterpret_cast<const uint4 *>(zs)[i];
     }
     float *dst = part + int64_t(blockIdx.x) * NE1;
-    const float t4 = block_sum<float, NT>(s4, red);
-    const float t3b = block_sum<float, NT>(s3b, red + 8);
-    const float t3a = block_sum<float, NT>(s3a, red + 16);
-    const float tsc = block_sum<float, NT>(ssc, red + 24);
+    float q[4] = {s4, s3b, s3a, ssc};  // one barrier pair for the four (bit-identical)
+    block_sums<float, NT, 4, 8>(q, red);
     if (tid == 0) {
-        dst[0] = t4;
-        dst[1] = t3b;
-        dst[2] = t3a;
-        dst[3] = tsc;
+        dst[0] = q[0];
+        dst[1] = q[1];
+        dst[2] = q[2];
+        dst[3] = q[3];
     }
 }
 
