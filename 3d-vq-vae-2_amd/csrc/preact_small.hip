@@ -76,6 +76,17 @@ constexpr int s2_of(int BR) { return BR >= 4 ? SMALL_S2 : 28; }  // W2-gradient 
 
 __device__ __forceinline__ int wrapm(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 __device__ __forceinline__ float rbf(float v) { return h2f_lo(uint32_t(f2h(v))); }
+#ifndef SMALL_FASTEXP
+#define SMALL_FASTEXP 1  // the brick kernels' elu on the hardware exp (v_exp_f32), as the column kernels' elu_f
+#endif
+__device__ __forceinline__ float belu(float z) {
+    if constexpr (SMALL_FASTEXP) return z > 0.f ? z : __expf(z) - 1.f;
+    else return elu(z);
+}
+__device__ __forceinline__ float belu_grad(float z) {
+    if constexpr (SMALL_FASTEXP) return z > 0.f ? 1.f : __expf(z);
+    else return elu_grad(z);
+}
 __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
@@ -249,14 +260,14 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
                 float xv[C];
                 unraw<TX, C>(xr[u], xv);
 #pragma unroll
-                for (int c = 0; c < C; ++c) xv[c] = elu(xv[c] + s.b1a) + s.b1b;
+                for (int c = 0; c < C; ++c) xv[c] = belu(xv[c] + s.b1a) + s.b1b;
                 float t[BR];
 #pragma unroll
                 for (int o = 0; o < BR; ++o) {
                     float acc = 0.f;
 #pragma unroll
                     for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], xv[c], acc);
-                    t[o] = rbf(elu(acc + s.b2a) + s.b2b);
+                    t[o] = rbf(belu(acc + s.b2a) + s.b2b);
                     t2h[q * BR + o] = t[o];
                 }
                 if (vi[u] >= 0 && t2o) stv<BR>(t2o + vox[u] * BR, t);
@@ -270,7 +281,7 @@ __global__ __launch_bounds__(NT) void k_small_fwd(SArgs a, const TX *__restrict_
             const int64_t vox = brick_vox(a, k, v);
             float t3v[BR], ov[C];
 #pragma unroll
-            for (int o = 0; o < BR; ++o) t3v[o] = rbf(elu(acc[o] + s.b3a) + s.b3b);
+            for (int o = 0; o < BR; ++o) t3v[o] = rbf(belu(acc[o] + s.b3a) + s.b3b);
             if (t3o) stv<BR>(t3o + vox * BR, t3v);
 #pragma unroll
             for (int co = 0; co < C; ++co) {
@@ -454,11 +465,11 @@ __global__ __launch_bounds__(NT) void k_small_bwd(SArgs a, const TO *__restrict_
 #pragma unroll
             for (int o = 0; o < BR; ++o) r = fmaf(w1s[o * C + ci], z1[o], r);
             sp[6] += r;
-            const float e = r * elu_grad(xv[ci] + s.b1a);
+            const float e = r * belu_grad(xv[ci] + s.b1a);
             sp[7] += e;
             const float gv = gs[v * C + ci];
             gxv[ci] = gv + e;
-            const float u = elu(xv[ci] + s.b1a) + s.b1b;
+            const float u = belu(xv[ci] + s.b1a) + s.b1b;
 #pragma unroll
             for (int o = 0; o < BR; ++o) {
                 acc1[ci][o] = fmaf(gv, t3v[o], acc1[ci][o]);
