@@ -107,6 +107,14 @@ __device__ __forceinline__ float bf(uint32_t u16) { return h2f_lo(u16); }
 // ELU on the hardware exp (v_exp_f32 of z log2 e: ~1e-7 relative, far inside the bf16 rounding that
 // follows every use in the tile kernels; the libm expf is ~10 instructions)
 __device__ __forceinline__ float elu_fast(float z) { return z > 0.f ? z : __expf(z) - 1.f; }
+#ifndef PM_FAST_ELU
+#define PM_FAST_ELU 1  // the first block's t2 stage and the W1-gradient staging's u1 on elu_fast too (as k_pm_fwd's u1)
+#endif
+#if PM_FAST_ELU
+#define PM_ELU elu_fast
+#else
+#define PM_ELU elu
+#endif
 __device__ __forceinline__ float elu_d_act(float t, float b) {  // elu'(z) from t = elu(z) + b
     const float z1 = t - b;
     return z1 > 0.f ? 1.f : z1 + 1.f;
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const h16_t *__restr
                 const int e = h * C + c;  // element of the 36 bf16 of the pair
                 const uint2 w = v[e / 4];
                 const uint32_t d = (e & 2) ? w.y : w.x;
-                uu[c] = bf(f2h(elu(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b));
+                uu[c] = bf(f2h(PM_ELU(bf((e & 1) ? (d >> 16) : (d & 0xffffu)) + s.b1a) + s.b1b));
             }
             float t2v[BR];
 #pragma unroll
@@ -347,7 +355,7 @@ __global__ __launch_bounds__(NT) void k_pm_t2(int64_t nvox, const h16_t *__restr
                 float acc = 0.f;
 #pragma unroll
                 for (int c = 0; c < C; ++c) acc = fmaf(w1s[o * C + c], uu[c], acc);
-                t2v[o] = elu(acc + s.b2a) + s.b2b;
+                t2v[o] = PM_ELU(acc + s.b2a) + s.b2b;
             }
 #pragma unroll
             for (int o = 0; o < BR; ++o) {
@@ -1420,8 +1428,8 @@ __device__ __forceinline__ void pm_w13grad(int npb, const h16_t *__restrict__ gz
                     uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        w[j] = uint32_t(f2h(elu(h2f_lo(w[j]) + s.b1a) + s.b1b)) |
-                               (uint32_t(f2h(elu(h2f_hi(w[j]) + s.b1a) + s.b1b)) << 16);
+                        w[j] = uint32_t(f2h(PM_ELU(h2f_lo(w[j]) + s.b1a) + s.b1b)) |
+                               (uint32_t(f2h(PM_ELU(h2f_hi(w[j]) + s.b1a) + s.b1b)) << 16);
                     q = u32x4{w[0], w[1], w[2], w[3]};
                 }
                 reinterpret_cast<u32x4 *>(raw)[i] = q;
